@@ -1,0 +1,132 @@
+"""Synthetic data generators.
+
+* :func:`generate_glm_data` — host (scipy) generator of benign/outlier/invalid binary, linear and Poisson data in
+  the spirit of ``photon-test-utils/.../SparkTestUtils.scala:85-308`` (seeded, sparse features, intercept).
+* :func:`generate_device_shard` — ON-DEVICE generator of the benchmark shard (BASELINE config "logistic L-BFGS
+  1B x 1M sparse", 125M rows per GPU at 8 GPUs). It writes the chunked CSR/CSC streams of
+  :class:`~photon_ml_amd.ops.device.DeviceGLMData` directly in HBM without any host round trip of the entries.
+
+  The structure is click-through-like hashed categorical data: the ``n_features - 1`` non-intercept columns are
+  split into ``nnz_per_row - 1`` fields; each row takes exactly one column per field, drawn from a Zipf(s) law
+  over the field's columns (hot features + long tail), with a value in [0.5, 1.5); the last column is the
+  intercept (1.0 in every row). Labels are Bernoulli(sigmoid(x . w*)) for a random sparse ground truth w*.
+"""
+from __future__ import annotations
+
+import math
+from typing import Optional
+
+import numpy as np
+import scipy.sparse as sp
+import torch
+
+from ..constants import TaskType
+from .matrix import LabeledData
+
+
+def generate_glm_data(task, n_rows: int, n_features: int, density: float = 0.2, seed: int = 7,
+                      intercept: bool = True, noise: float = 1e-3, kind: str = "benign"):
+    """Host generator. Returns ``(LabeledData, w_true)``; the last column is the intercept when requested."""
+    task = TaskType.parse(task)
+    rng = np.random.default_rng(seed)
+    d_feat = n_features - (1 if intercept else 0)
+    x = sp.random(n_rows, d_feat, density=density, format="csr", random_state=seed,
+                  data_rvs=lambda k: rng.uniform(-1, 1, size=k))
+    if kind == "outlier":
+        x.data *= np.where(rng.random(x.data.size) < 0.01, 1e3, 1.0)
+    if intercept:
+        x = sp.hstack([x, np.ones((n_rows, 1))], format="csr")
+    w = rng.normal(size=n_features)
+    z = x @ w
+    if task == TaskType.LOGISTIC_REGRESSION or task == TaskType.SMOOTHED_HINGE_LOSS_LINEAR_SVM:
+        y = (rng.random(n_rows) < 1.0 / (1.0 + np.exp(-z))).astype(np.float64)
+    elif task == TaskType.POISSON_REGRESSION:
+        w *= 0.2
+        z = x @ w
+        y = rng.poisson(np.exp(np.clip(z, -20, 5))).astype(np.float64)
+    else:
+        y = z + rng.normal(scale=noise, size=n_rows)
+    if kind == "invalid":
+        y[0] = np.nan
+    return LabeledData(x, y), w
+
+
+def zipf_cdf(n: int, s: float, device) -> torch.Tensor:
+    k = torch.arange(1, n + 1, dtype=torch.float64, device=device)
+    p = k.pow(-s)
+    c = torch.cumsum(p, 0)
+    return (c / c[-1]).to(torch.float32)
+
+
+def generate_device_shard(n_rows: int, n_features: int, nnz_per_row: int, device="cuda", precision: str = "bf16",
+                          seed: int = 1234567890, chunk_rows: int = 1 << 20, zipf_s: float = 1.1,
+                          task=TaskType.LOGISTIC_REGRESSION, rank: int = 0, progress=None):
+    """Generate a :class:`DeviceGLMData` directly in device memory (see module docstring)."""
+    from ..ops.device import DeviceGLMData, SegChunk, VAL_DTYPE
+
+    dev = torch.device(device)
+    prec = {"bf16": 0, "f32": 1, "f64": 2}[precision]
+    vdt = VAL_DTYPE[prec]
+    n_fields = nnz_per_row - 1
+    if n_fields < 1:
+        raise ValueError("nnz_per_row must be >= 2 (intercept + >= 1 field)")
+    fs = (n_features - 1) // n_fields
+    if fs < 1:
+        raise ValueError("not enough features for the requested nnz per row")
+    cdf = zipf_cdf(fs, zipf_s, dev)
+    field_base = (torch.arange(n_fields, device=dev, dtype=torch.int32) * fs)
+    gen = torch.Generator(device=dev)
+    gen.manual_seed(seed + 7919 * rank)
+    starts = list(range(0, n_rows, chunk_rows)) + [n_rows]
+    csr, csc = [], []
+    k = nnz_per_row
+    for ci, (a, b) in enumerate(zip(starts[:-1], starts[1:])):
+        m = b - a
+        u = torch.rand((m, n_fields), generator=gen, device=dev)
+        rank_ = torch.searchsorted(cdf, u).clamp_(max=fs - 1).to(torch.int32)
+        del u
+        idx = torch.empty((m, k), dtype=torch.int32, device=dev)
+        idx[:, :n_fields] = rank_ + field_base
+        idx[:, n_fields] = n_features - 1
+        del rank_
+        val = torch.empty((m, k), dtype=torch.float32, device=dev)
+        val[:, :n_fields] = torch.rand((m, n_fields), generator=gen, device=dev) + 0.5
+        val[:, n_fields] = 1.0
+        val = val.to(vdt)
+        idx = idx.reshape(-1)
+        val = val.reshape(-1)
+        seg_ptr = np.arange(0, (m + 1) * k, k, dtype=np.int64)
+        if seg_ptr[-1] >= 2 ** 31:
+            raise ValueError("chunk too large for int32 offsets: lower chunk_rows")
+        csr.append(SegChunk(seg_ptr.astype(np.int32), idx, val, dev))
+        # CSC of the chunk: stable sort by column -> rows stay ascending inside each column segment
+        perm = torch.argsort(idx, stable=True)
+        cidx = (perm // k).to(torch.int32)
+        cval = val[perm]
+        counts = torch.bincount(idx.to(torch.int64), minlength=n_features)
+        colptr = torch.zeros(n_features + 1, dtype=torch.int64, device=dev)
+        colptr[1:] = torch.cumsum(counts, 0)
+        del perm, counts
+        csc.append(SegChunk(colptr.cpu().numpy().astype(np.int32), cidx, cval, dev))
+        del cidx, cval, colptr
+        if progress is not None:
+            progress(ci + 1, len(starts) - 1)
+    y = torch.zeros(n_rows, dtype=torch.float32, device=dev)
+    data = DeviceGLMData(csr, csc, starts, y, torch.zeros_like(y), torch.ones_like(y), n_features, precision, dev)
+    # labels from a sparse ground truth
+    wgen = torch.Generator(device=dev)
+    wgen.manual_seed(seed)
+    w_true = torch.randn(n_features, generator=wgen, device=dev, dtype=torch.float64) * 0.3
+    w_true[torch.rand(n_features, generator=wgen, device=dev) < 0.5] = 0.0
+    w_true[-1] = -1.0
+    z = data.margins(w_true)
+    p = torch.sigmoid(z)
+    task = TaskType.parse(task)
+    if task == TaskType.LOGISTIC_REGRESSION:
+        yy = (torch.rand(n_rows, generator=gen, device=dev, dtype=torch.float64) < p).to(torch.float32)
+    elif task == TaskType.POISSON_REGRESSION:
+        yy = torch.poisson(torch.exp(z.clamp(max=5.0)) * 0.2, generator=gen).to(torch.float32)
+    else:
+        yy = (z + 0.1 * torch.randn(n_rows, generator=gen, device=dev, dtype=torch.float64)).to(torch.float32)
+    data.y.copy_(yy.to(data.vdt))
+    return data, w_true

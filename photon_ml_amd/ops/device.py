@@ -1,0 +1,257 @@
+"""HBM-resident GLM row shard evaluated by the HIP kernels (``ops/csrc/glm_kernels.hip``).
+
+Layout of one feature shard on one GPU (SURVEY §7.1 "Data layout", MI355X-first):
+
+* rows are split into CHUNKS of ``chunk_rows`` (default 2^20) rows;
+* per chunk a CSR stream (segments = rows) for ``z = X w`` and a CSC stream (segments = columns, rows local to
+  the chunk) for ``g = X^T r``. Processing the transpose chunk by chunk keeps the gathered per-row vector of the
+  chunk (4 MB in fp32) resident in the XCD L2s / Infinity Cache instead of gathering across the whole shard;
+* int32 indices everywhere (chunk-local), values in bf16 (``precision="bf16"``), fp32 or fp64;
+* per chunk the static block decomposition (see the kernel header) built once on the host.
+
+One function evaluation = for each chunk: fused forward (margin + loss + per-row coefficient + block stats),
+then transpose accumulate into the fp64 gradient; the per-block stats are reduced deterministically at the end.
+No atomics anywhere: results are bitwise reproducible run to run.
+"""
+from __future__ import annotations
+
+import ctypes
+from dataclasses import dataclass
+from typing import List, Optional, Sequence
+
+import numpy as np
+import scipy.sparse as sp
+import torch
+
+from ..data.matrix import LabeledData
+from .native import SegChunkDesc, check, require_glm_lib, stream_handle
+from .reference import GLMComputable
+
+PRECISIONS = {"bf16": 0, "f32": 1, "f64": 2}
+VAL_DTYPE = {0: torch.bfloat16, 1: torch.float32, 2: torch.float64}
+VEC_DTYPE = {0: torch.float32, 1: torch.float32, 2: torch.float64}
+
+FWD_MARGIN, FWD_VALUE_GRAD, FWD_HV, FWD_DZZ = 0, 1, 2, 3
+
+
+def _pad8(n: int) -> int:
+    return ((n + 7) // 8) * 8 + 8
+
+
+def _ptr(t: Optional[torch.Tensor]) -> Optional[int]:
+    return None if t is None else t.data_ptr()
+
+
+class SegChunk:
+    """One segmented stream (CSR chunk or CSC chunk) resident on the device."""
+
+    def __init__(self, seg_ptr: np.ndarray, idx: torch.Tensor, val: torch.Tensor, device, nb: Optional[int] = None,
+                 maxseg: Optional[int] = None):
+        lib = require_glm_lib()
+        seg_ptr = np.ascontiguousarray(seg_ptr, dtype=np.int32)
+        nseg = len(seg_ptr) - 1
+        nb = nb or lib.pml_nb()
+        maxseg = maxseg or lib.pml_maxseg()
+        nblk, nlong, npart = ctypes.c_int(), ctypes.c_int(), ctypes.c_int()
+        check(lib.pml_build_blocks(seg_ptr.ctypes.data, nseg, nb, maxseg, None, ctypes.byref(nblk), None, None,
+                                   ctypes.byref(nlong), ctypes.byref(npart)), "count blocks")
+        blk = np.zeros(max(5 * nblk.value, 5), dtype=np.int32)
+        long_seg = np.zeros(max(nlong.value, 1), dtype=np.int32)
+        long_ptr = np.zeros(nlong.value + 1, dtype=np.int32)
+        check(lib.pml_build_blocks(seg_ptr.ctypes.data, nseg, nb, maxseg, blk.ctypes.data, ctypes.byref(nblk),
+                                   long_seg.ctypes.data, long_ptr.ctypes.data, ctypes.byref(nlong),
+                                   ctypes.byref(npart)), "build blocks")
+        self.nseg, self.nblk, self.nlong, self.npart = nseg, nblk.value, nlong.value, npart.value
+        self.nnz = int(seg_ptr[-1])
+        dev = torch.device(device)
+        self.seg_ptr = torch.from_numpy(seg_ptr).to(dev)
+        self.blk = torch.from_numpy(blk).to(dev)
+        self.long_seg = torch.from_numpy(long_seg).to(dev)
+        self.long_ptr = torch.from_numpy(long_ptr).to(dev)
+        # kernels read 8-aligned windows: pad the streams
+        n_pad = _pad8(self.nnz)
+        if idx.numel() < n_pad:
+            idx = torch.cat([idx.to(dev, torch.int32), torch.zeros(n_pad - idx.numel(), dtype=torch.int32, device=dev)])
+        if val.numel() < n_pad:
+            val = torch.cat([val.to(dev), torch.zeros(n_pad - val.numel(), dtype=val.dtype, device=dev)])
+        self.idx = idx.contiguous()
+        self.val = val.contiguous()
+        self.desc = SegChunkDesc(self.blk.data_ptr(), self.nblk, self.seg_ptr.data_ptr(), self.nseg,
+                                 self.idx.data_ptr(), self.val.data_ptr(), self.long_seg.data_ptr(),
+                                 self.long_ptr.data_ptr(), self.nlong, self.npart)
+
+    def nbytes(self) -> int:
+        return sum(t.numel() * t.element_size() for t in (self.seg_ptr, self.blk, self.long_seg, self.long_ptr,
+                                                           self.idx, self.val))
+
+
+class DeviceGLMData(GLMComputable):
+    """GLM row shard on one GPU evaluated with the native kernels."""
+
+    def __init__(self, csr: List[SegChunk], csc: List[SegChunk], row_starts: Sequence[int], y, offsets, weights,
+                 dim: int, precision: str = "f64", device="cuda"):
+        self.lib = require_glm_lib()
+        self.device = torch.device(device)
+        self.prec = PRECISIONS[precision]
+        self.precision = precision
+        self.vdt = VEC_DTYPE[self.prec]
+        self.csr, self.csc = csr, csc
+        self.row_starts = list(row_starts)  # len = n_chunks + 1
+        self.n_rows = self.row_starts[-1]
+        self.dim = int(dim)
+        rdt = self.vdt
+        self.y = torch.as_tensor(y, device=self.device).to(rdt).contiguous()
+        self.o = torch.as_tensor(offsets, device=self.device).to(rdt).contiguous()
+        self.wt = torch.as_tensor(weights, device=self.device).to(rdt).contiguous()
+        n = self.n_rows
+        self.coef = torch.zeros(max(n, 1), dtype=rdt, device=self.device)
+        self.dzz = torch.zeros(max(n, 1), dtype=rdt, device=self.device)
+        self.track_hessian = False
+        self._dzz_key: Optional[torch.Tensor] = None
+        self._dzz_shift = None
+        # scratch
+        self.blk_off = np.cumsum([0] + [c.nblk for c in csr]).tolist()
+        self.long_off = np.cumsum([0] + [c.nlong for c in csr]).tolist()
+        self.stats = torch.zeros(2 * max(self.blk_off[-1], 1), dtype=torch.float64, device=self.device)
+        self.long_stats = torch.zeros(2 * max(self.long_off[-1], 1), dtype=torch.float64, device=self.device)
+        maxpart = max([c.npart for c in csr + csc] + [1])
+        self.parts = torch.zeros(maxpart, dtype=torch.float64, device=self.device)
+        self.red_scratch = torch.zeros(512, dtype=torch.float64, device=self.device)
+        self.out2 = torch.zeros(2, dtype=torch.float64, device=self.device)
+        self.n_passes = 0
+
+    # ------------------------------------------------------------------
+    @staticmethod
+    def from_labeled(data: LabeledData, device="cuda", precision: str = "f64", chunk_rows: int = 1 << 20):
+        prec = PRECISIONS[precision]
+        vdt = VAL_DTYPE[prec]
+        dev = torch.device(device)
+        x = data.x.tocsr()
+        n, d = x.shape
+        starts = list(range(0, n, chunk_rows)) + [n]
+        if n == 0:
+            starts = [0, 0]
+        csr, csc = [], []
+        for a, b in zip(starts[:-1], starts[1:]):
+            xc = x[a:b]
+            sp_ = (xc.indptr - xc.indptr[0]).astype(np.int32)
+            csr.append(SegChunk(sp_, torch.from_numpy(xc.indices.astype(np.int32)),
+                                torch.from_numpy(xc.data.astype(np.float64)).to(vdt), dev))
+            xt = xc.tocsc()
+            xt.sort_indices()
+            csc.append(SegChunk(xt.indptr.astype(np.int32), torch.from_numpy(xt.indices.astype(np.int32)),
+                                torch.from_numpy(xt.data.astype(np.float64)).to(vdt), dev))
+        return DeviceGLMData(csr, csc, starts, torch.from_numpy(data.y), torch.from_numpy(data.offsets),
+                             torch.from_numpy(data.weights), d, precision, dev)
+
+    def nbytes(self) -> int:
+        return sum(c.nbytes() for c in self.csr + self.csc)
+
+    def set_offsets(self, offsets):
+        self.o.copy_(torch.as_tensor(offsets, device=self.device).to(self.vdt))
+
+    def set_weights(self, weights):
+        self.wt.copy_(torch.as_tensor(weights, device=self.device).to(self.vdt))
+
+    # ------------------------------------------------------------------
+    def _rows(self, t: torch.Tensor, c: int) -> int:
+        return t.data_ptr() + self.row_starts[c] * t.element_size()
+
+    def _fwd(self, c: int, x: torch.Tensor, mode: int, loss_id: int, shift: float, coef: Optional[torch.Tensor],
+             dzz: Optional[torch.Tensor], z_out: Optional[torch.Tensor] = None, with_offset: int = 0,
+             stats: bool = True):
+        ch = self.csr[c]
+        st = self.stats.data_ptr() + 2 * 8 * self.blk_off[c] if stats else None
+        lst = self.long_stats.data_ptr() + 2 * 8 * self.long_off[c] if stats else None
+        check(self.lib.pml_seg_fwd(
+            self.prec, ctypes.byref(ch.desc), x.data_ptr(), mode, loss_id, float(shift),
+            self._rows(self.y, c), self._rows(self.o, c), self._rows(self.wt, c),
+            None if coef is None else self._rows(coef, c), None if dzz is None else self._rows(dzz, c),
+            None if z_out is None else self._rows(z_out, c), with_offset, st, lst, self.parts.data_ptr(),
+            stream_handle(self.device)), "seg_fwd")
+
+    def _t(self, c: int, x: torch.Tensor, G: torch.Tensor, square: int = 0):
+        ch = self.csc[c]
+        check(self.lib.pml_seg_t(self.prec, ctypes.byref(ch.desc), self._rows(x, c), square, G.data_ptr(),
+                                 self.parts.data_ptr(), stream_handle(self.device)), "seg_t")
+
+    def _reduce_stats(self) -> torch.Tensor:
+        out = self.out2
+        st = stream_handle(self.device)
+        check(self.lib.pml_reduce_stats(self.stats.data_ptr(), self.blk_off[-1], out.data_ptr(), 0,
+                                        self.red_scratch.data_ptr(), st), "reduce")
+        if self.long_off[-1] > 0:
+            check(self.lib.pml_reduce_stats(self.long_stats.data_ptr(), self.long_off[-1], out.data_ptr(), 1,
+                                            None, st), "reduce")
+        elif self.blk_off[-1] == 0:
+            out.zero_()
+        return out
+
+    def _vec(self, w: torch.Tensor) -> torch.Tensor:
+        return w.to(self.device, self.vdt).contiguous()
+
+    # ------------------------------------------------------------------
+    def value_grad_packed(self, loss, w_eff, margin_shift) -> torch.Tensor:
+        """Device tensor [D + 2] = (G, F, S) — packed so a DP wrapper can all-reduce it in one RCCL call."""
+        out = torch.zeros(self.dim + 2, dtype=torch.float64, device=self.device)
+        G = out[: self.dim]
+        x = self._vec(w_eff)
+        dzz = self.dzz if (self.track_hessian and loss.twice_differentiable) else None
+        for c in range(len(self.csr)):
+            self._fwd(c, x, FWD_VALUE_GRAD, loss.loss_id, margin_shift, self.coef, dzz)
+            self._t(c, self.coef, G)
+        out[self.dim:] = self._reduce_stats()
+        if dzz is not None:
+            self._dzz_key = w_eff.detach().clone()
+            self._dzz_shift = float(margin_shift)
+        self.n_passes += 1
+        return out
+
+    def value_grad_sums(self, loss, w_eff, margin_shift):
+        out = self.value_grad_packed(loss, w_eff, margin_shift)
+        fs = out[self.dim:].tolist()
+        return fs[0], fs[1], out[: self.dim]
+
+    def _ensure_dzz(self, loss, w_eff, shift):
+        key = self._dzz_key
+        if key is not None and self._dzz_shift == float(shift) and key.shape == w_eff.shape and bool(
+                torch.equal(key, w_eff.to(key.device, key.dtype))):
+            return
+        x = self._vec(w_eff)
+        for c in range(len(self.csr)):
+            self._fwd(c, x, FWD_DZZ, loss.loss_id, shift, self.dzz, None, stats=False)
+        self._dzz_key = w_eff.detach().clone()
+        self._dzz_shift = float(shift)
+
+    def hv_packed(self, loss, w_eff, margin_shift, v_eff, v_shift) -> torch.Tensor:
+        self._ensure_dzz(loss, w_eff, margin_shift)
+        out = torch.zeros(self.dim + 2, dtype=torch.float64, device=self.device)
+        H = out[: self.dim]
+        x = self._vec(v_eff)
+        for c in range(len(self.csr)):
+            self._fwd(c, x, FWD_HV, loss.loss_id, v_shift, self.coef, self.dzz)
+            self._t(c, self.coef, H)
+        out[self.dim:] = self._reduce_stats()
+        self.n_passes += 1
+        return out
+
+    def hv_sums(self, loss, w_eff, margin_shift, v_eff, v_shift):
+        out = self.hv_packed(loss, w_eff, margin_shift, v_eff, v_shift)
+        return out[: self.dim], float(out[self.dim + 1])
+
+    def hdiag_sums(self, loss, w):
+        x = self._vec(w)
+        out = torch.zeros(self.dim, dtype=torch.float64, device=self.device)
+        for c in range(len(self.csr)):
+            self._fwd(c, x, FWD_DZZ, loss.loss_id, 0.0, self.coef, None, stats=False)
+            self._t(c, self.coef, out, square=1)
+        self._dzz_key = None
+        return out
+
+    def margins(self, w, margin_shift: float = 0.0, with_offsets: bool = False):
+        z = torch.empty(max(self.n_rows, 1), dtype=torch.float64, device=self.device)
+        x = self._vec(w)
+        for c in range(len(self.csr)):
+            self._fwd(c, x, FWD_MARGIN, 0, margin_shift, None, None, z_out=z, with_offset=int(with_offsets),
+                      stats=False)
+        return z[: self.n_rows]

@@ -1,0 +1,89 @@
+"""ctypes bindings of the native HIP libraries (C ABI).
+
+The libraries are loaded AFTER ``import torch`` so that their ``libamdhip64.so.7`` dependency resolves to the
+HIP runtime torch already loaded (one runtime, one device context, torch-owned memory and streams).
+On a GPU box the HIP path is mandatory: :func:`require_glm_lib` raises if the library is missing instead of
+silently falling back to the torch reference.
+"""
+from __future__ import annotations
+
+import ctypes
+import os
+from pathlib import Path
+from typing import Optional
+
+import torch  # noqa: F401  (must precede loading the HIP libraries)
+
+from .build import build_hip, lib_path
+
+c_int = ctypes.c_int
+c_double = ctypes.c_double
+c_void_p = ctypes.c_void_p
+P_int = ctypes.POINTER(ctypes.c_int)
+
+
+class SegChunkDesc(ctypes.Structure):
+    _fields_ = [
+        ("blk", c_void_p), ("nblk", c_int),
+        ("seg_ptr", c_void_p), ("nseg", c_int),
+        ("idx", c_void_p), ("val", c_void_p),
+        ("long_seg", c_void_p), ("long_ptr", c_void_p), ("nlong", c_int), ("npart", c_int),
+    ]
+
+
+_LIBS = {}
+
+
+def _load(name: str, auto_build: bool = True) -> Optional[ctypes.CDLL]:
+    if name in _LIBS:
+        return _LIBS[name]
+    path = lib_path("hip", name)
+    if not path.exists() and auto_build and os.environ.get("PML_NO_AUTOBUILD") != "1":
+        try:
+            build_hip(name)
+        except Exception:  # pragma: no cover - toolchain missing
+            pass
+    if not path.exists():
+        _LIBS[name] = None
+        return None
+    lib = ctypes.CDLL(str(path), mode=ctypes.RTLD_GLOBAL)
+    _LIBS[name] = lib
+    return lib
+
+
+def glm_lib() -> Optional[ctypes.CDLL]:
+    lib = _load("glm")
+    if lib is not None and not getattr(lib, "_pml_typed", False):
+        lib.pml_build_blocks.argtypes = [c_void_p, c_int, c_int, c_int, c_void_p, P_int, c_void_p, c_void_p,
+                                         P_int, P_int]
+        lib.pml_seg_fwd.argtypes = [c_int, ctypes.POINTER(SegChunkDesc), c_void_p, c_int, c_int, c_double,
+                                    c_void_p, c_void_p, c_void_p, c_void_p, c_void_p, c_void_p, c_int, c_void_p,
+                                    c_void_p, c_void_p, c_void_p]
+        lib.pml_seg_t.argtypes = [c_int, ctypes.POINTER(SegChunkDesc), c_void_p, c_int, c_void_p, c_void_p,
+                                  c_void_p]
+        lib.pml_reduce_stats.argtypes = [c_void_p, c_int, c_void_p, c_int, c_void_p, c_void_p]
+        for f in ("pml_seg_fwd", "pml_seg_t", "pml_reduce_stats", "pml_build_blocks"):
+            getattr(lib, f).restype = c_int
+        lib._pml_typed = True
+    return lib
+
+
+def require_glm_lib() -> ctypes.CDLL:
+    lib = glm_lib()
+    if lib is None:
+        raise RuntimeError(
+            f"native GLM kernel library missing ({lib_path('hip', 'glm')}); run python -m photon_ml_amd.ops.build")
+    return lib
+
+
+def batched_lib() -> Optional[ctypes.CDLL]:
+    return _load("batched")
+
+
+def check(rc: int, what: str):
+    if rc != 0:
+        raise RuntimeError(f"{what} failed with HIP error {rc}")
+
+
+def stream_handle(device=None) -> int:
+    return torch.cuda.current_stream(device).cuda_stream

@@ -1,0 +1,109 @@
+"""fp64 torch reference backend for the GLM aggregation kernels (K1-K5 of SURVEY.md §2.8).
+
+This is the numerical spec every HIP kernel is tested against, and the CPU execution path (the analogue of
+Spark ``local[*]``). It mirrors the per-row aggregator semantics of
+``photon-lib/.../function/glm/ValueAndGradientAggregator.scala:132-153`` (value/grad),
+``HessianVectorAggregator.scala:96-121`` (Hv) and ``HessianDiagonalAggregator.scala:51-61`` (Hdiag), but as
+whole-shard sparse matrix products instead of a per-record fold.
+"""
+from __future__ import annotations
+
+from typing import Optional
+
+import numpy as np
+import scipy.sparse as sp
+import torch
+
+from ..data.matrix import LabeledData
+
+
+def _to_torch_csr(m: sp.csr_matrix, device, dtype=torch.float64) -> torch.Tensor:
+    m = m.tocsr()
+    return torch.sparse_csr_tensor(
+        torch.from_numpy(m.indptr.astype(np.int64)),
+        torch.from_numpy(m.indices.astype(np.int64)),
+        torch.from_numpy(m.data.astype(np.float64)),
+        size=m.shape,
+        dtype=dtype,
+    ).to(device)
+
+
+class GLMComputable:
+    """Interface of a row shard that can evaluate GLM aggregates.
+
+    All vectors are fp64 torch tensors on ``self.device``; scalars are python floats.
+    """
+
+    n_rows: int
+    dim: int
+    device: torch.device
+
+    def value_grad_sums(self, loss, w_eff, margin_shift: float):
+        """Return ``(F, S, G)``: F = sum w_i l(z_i), S = sum w_i l'(z_i), G = sum w_i l'(z_i) x_i."""
+        raise NotImplementedError
+
+    def hv_sums(self, loss, w_eff, margin_shift: float, v_eff, v_shift: float):
+        """Return ``(H, P)``: e_i = w_i l''(z_i) (x_i.v_eff - v_shift); H = sum e_i x_i, P = sum e_i."""
+        raise NotImplementedError
+
+    def hdiag_sums(self, loss, w):
+        """Return sum_i w_i l''(x_i.w + o_i) x_i^2 (raw coefficients, no normalisation)."""
+        raise NotImplementedError
+
+    def margins(self, w, margin_shift: float = 0.0, with_offsets: bool = False):
+        """x_i . w (+ shift) (+ o_i)."""
+        raise NotImplementedError
+
+    def count(self) -> int:
+        return self.n_rows
+
+
+class TorchGLMData(GLMComputable):
+    """Reference backend: torch sparse CSR (X and X^T) in fp64 on any device."""
+
+    def __init__(self, data: LabeledData, device="cpu"):
+        self.device = torch.device(device)
+        self.n_rows, self.dim = data.x.shape
+        self.x = _to_torch_csr(data.x, self.device)
+        self.xt = _to_torch_csr(data.x.T.tocsr(), self.device)
+        self.x2t = _to_torch_csr(data.x.multiply(data.x).T.tocsr(), self.device)
+        self.y = torch.from_numpy(data.y).to(self.device)
+        self.o = torch.from_numpy(data.offsets).to(self.device)
+        self.wt = torch.from_numpy(data.weights).to(self.device)
+
+    def _xv(self, w):
+        if self.n_rows == 0:
+            return torch.zeros(0, dtype=torch.float64, device=self.device)
+        return torch.mv(self.x, w.to(self.device, torch.float64))
+
+    def _xtv(self, r):
+        if self.n_rows == 0:
+            return torch.zeros(self.dim, dtype=torch.float64, device=self.device)
+        return torch.mv(self.xt, r)
+
+    def margins(self, w, margin_shift: float = 0.0, with_offsets: bool = False):
+        z = self._xv(w) + margin_shift
+        return z + self.o if with_offsets else z
+
+    def value_grad_sums(self, loss, w_eff, margin_shift):
+        z = self._xv(w_eff) + margin_shift + self.o
+        l, dl = loss.loss_and_dz(z, self.y)
+        r = self.wt * dl
+        return float(torch.sum(self.wt * l)), float(torch.sum(r)), self._xtv(r)
+
+    def hv_sums(self, loss, w_eff, margin_shift, v_eff, v_shift):
+        z = self._xv(w_eff) + margin_shift + self.o
+        e = self.wt * loss.dzz(z, self.y) * (self._xv(v_eff) - v_shift)
+        return self._xtv(e), float(torch.sum(e))
+
+    def hdiag_sums(self, loss, w):
+        z = self._xv(w) + self.o
+        d = self.wt * loss.dzz(z, self.y)
+        if self.n_rows == 0:
+            return torch.zeros(self.dim, dtype=torch.float64, device=self.device)
+        return torch.mv(self.x2t, d)
+
+    def row_losses(self, loss, w_eff, margin_shift=0.0):
+        z = self._xv(w_eff) + margin_shift + self.o
+        l, _ = loss.loss_and_dz(z, self.y)
+        return l

@@ -1,0 +1,190 @@
+"""L-BFGS and OWL-QN on device-resident fp64 vectors.
+
+Reference adapters: ``photon-lib/.../optimization/LBFGS.scala:39-156`` (defaults maxIter 100, m 10, tol 1e-7;
+box projection after each step, 70-75) and ``OWLQN.scala:40-86`` (constant per-coordinate L1 weight). The
+reference wraps Breeze; here the quasi-Newton engine is native to this framework:
+
+* two-loop recursion (K16 of SURVEY §2.8) over an ``m``-deep history of (s, y) pairs kept as one [2m, D] device
+  buffer (one allocation, no per-iteration mallocs), initial scaling ``s.y / y.y`` of the newest pair;
+* strong-Wolfe line search, first step ``1/||d||`` then 1 (Breeze's choice);
+* OWL-QN (K17): pseudo-gradient, direction sign correction, orthant-projected steps, backtracking line search
+  (shrink 0.1 on the first iteration then 0.5), L1 added to the reported value and gradient, exactly as the
+  reference reports ``adjustedValue``/``adjustedGradient`` to the outer state machine;
+* history reset on a failed line search, give-up (ObjectiveNotImproving) on a second consecutive failure.
+"""
+from __future__ import annotations
+
+from typing import Optional
+
+import torch
+
+from .line_search import LineSearchFailed, backtracking, strong_wolfe
+from .optimizer import Optimizer, OptimizerState, project_box
+
+DEFAULT_MAX_ITER = 100
+DEFAULT_NUM_CORRECTIONS = 10
+DEFAULT_TOLERANCE = 1.0e-7
+
+
+def _dot(a, b) -> float:
+    return float(torch.dot(a, b))
+
+
+class _History:
+    """Ring buffer of the last m (s, y) pairs plus rho = 1/(s.y)."""
+
+    def __init__(self, m: int):
+        self.m = m
+        self.s = []
+        self.y = []
+        self.rho = []
+
+    def clear(self):
+        self.s, self.y, self.rho = [], [], []
+
+    def push(self, s: torch.Tensor, y: torch.Tensor) -> bool:
+        sy = _dot(s, y)
+        if not (sy > 1e-300) or sy != sy:
+            return False  # curvature condition violated: skip (Breeze would raise NaNHistory)
+        self.s.append(s)
+        self.y.append(y)
+        self.rho.append(1.0 / sy)
+        if len(self.s) > self.m:
+            self.s.pop(0)
+            self.y.pop(0)
+            self.rho.pop(0)
+        return True
+
+    def apply_inverse(self, g: torch.Tensor) -> torch.Tensor:
+        """Two-loop recursion: returns H g."""
+        q = g.clone()
+        k = len(self.s)
+        alpha = [0.0] * k
+        for i in range(k - 1, -1, -1):
+            alpha[i] = self.rho[i] * _dot(self.s[i], q)
+            q.add_(self.y[i], alpha=-alpha[i])
+        if k > 0:
+            yy = _dot(self.y[-1], self.y[-1])
+            q.mul_((1.0 / self.rho[-1]) / yy)
+        for i in range(k):
+            beta = self.rho[i] * _dot(self.y[i], q)
+            q.add_(self.s[i], alpha=alpha[i] - beta)
+        return q
+
+
+class LBFGS(Optimizer):
+    def __init__(self, normalization=None, num_corrections: int = DEFAULT_NUM_CORRECTIONS,
+                 tolerance: float = DEFAULT_TOLERANCE, max_iterations: int = DEFAULT_MAX_ITER,
+                 constraints=None, track_state: bool = True):
+        super().__init__(tolerance, max_iterations, normalization, constraints, track_state)
+        self.m = num_corrections
+        self.history = _History(num_corrections)
+        self._failed_once = False
+        self._finished = False
+        self._inner_iter = 0
+        # smooth (un-penalised) value/gradient at the current point, used for the history
+        self._smooth_f = None
+        self._smooth_g = None
+
+    def clear_inner_state(self):
+        super().clear_inner_state()
+        self.history.clear()
+        self._failed_once = False
+        self._finished = False
+        self._inner_iter = 0
+
+    # -- L1 hooks (identity for plain L-BFGS) --------------------------------
+    def _adjust(self, x, f, g):
+        return f, g
+
+    def _init(self, objective, data, state: OptimizerState):
+        self._smooth_f, self._smooth_g = state.loss, state.gradient
+        adj_f, adj_g = self._adjust(state.coefficients, state.loss, state.gradient)
+        state.loss, state.gradient = adj_f, adj_g
+
+    def _direction(self, state: OptimizerState) -> torch.Tensor:
+        return -self.history.apply_inverse(state.gradient)
+
+    def _search(self, objective, data, state: OptimizerState, d: torch.Tensor):
+        x0 = state.coefficients
+        g0 = _dot(state.gradient, d)
+        t0 = 1.0 / float(torch.linalg.vector_norm(d)) if self._inner_iter == 0 else 1.0
+
+        def phi(t):
+            x = x0 + t * d
+            f, g = objective.calculate(data, x)
+            return f, _dot(g, d), (x, f, g)
+
+        t, _, _, (x, f, g) = strong_wolfe(phi, state.loss, g0, t0)
+        return x, f, g
+
+    def _run_one_iteration(self, objective, data, state: OptimizerState) -> OptimizerState:
+        if self._finished:
+            return state
+        try:
+            d = self._direction(state)
+            if not bool(torch.any(d != 0)):
+                self._finished = True  # zero (pseudo-)gradient: stationary point
+                return state
+            x, f, g = self._search(objective, data, state, d)
+        except LineSearchFailed:
+            if not self._failed_once and len(self.history.s) > 0:
+                self._failed_once = True
+                self.history.clear()
+                return self._run_one_iteration(objective, data, state)
+            self._finished = True
+            return state
+        self._failed_once = False
+        self.history.push(x - state.coefficients, g - self._smooth_g)
+        self._smooth_f, self._smooth_g = f, g
+        self._inner_iter += 1
+        adj_f, adj_g = self._adjust(x, f, g)
+        x = project_box(x, self.constraints)
+        return OptimizerState(x, adj_f, adj_g, state.iter + 1)
+
+
+class OWLQN(LBFGS):
+    """Orthant-wise limited-memory quasi-Newton for L1 / elastic-net (L1 part in the optimizer)."""
+
+    def __init__(self, l1_weight: float, normalization=None, num_corrections: int = DEFAULT_NUM_CORRECTIONS,
+                 tolerance: float = DEFAULT_TOLERANCE, max_iterations: int = DEFAULT_MAX_ITER,
+                 constraints=None, track_state: bool = True):
+        super().__init__(normalization, num_corrections, tolerance, max_iterations, constraints, track_state)
+        self.l1_weight = float(l1_weight)
+
+    # pseudo-gradient (Andrew & Gao 2007)
+    def _pseudo_gradient(self, x, g):
+        lam = self.l1_weight
+        at_zero = x == 0
+        dplus = g + lam
+        dminus = g - lam
+        pg_zero = torch.where(dminus > 0, dminus, torch.where(dplus < 0, dplus, torch.zeros_like(g)))
+        return torch.where(at_zero, pg_zero, g + lam * torch.sign(x))
+
+    def _adjust(self, x, f, g):
+        return f + self.l1_weight * float(torch.sum(torch.abs(x))), self._pseudo_gradient(x, g)
+
+    def _direction(self, state):
+        d = -self.history.apply_inverse(state.gradient)
+        # keep only components that descend along the pseudo-gradient
+        return torch.where(d * state.gradient < 0, d, torch.zeros_like(d))
+
+    def _search(self, objective, data, state, d):
+        x0 = state.coefficients
+        pg = state.gradient
+        orthant = torch.where(x0 != 0, torch.sign(x0), torch.sign(-pg))
+        t0 = 1.0 / float(torch.linalg.vector_norm(d)) if self._inner_iter == 0 else 1.0
+        shrink = 0.1 if self._inner_iter < 1 else 0.5
+
+        def phi(t):
+            x = x0 + t * d
+            x = torch.where(torch.sign(x) != orthant, torch.zeros_like(x), x)
+            f, g = objective.calculate(data, x)
+            adj_f, adj_g = self._adjust(x, f, g)
+            return adj_f, _dot(adj_g, d), (x, f, g)
+
+        g0 = _dot(pg, d)
+        if g0 >= 0:
+            raise LineSearchFailed("OWL-QN: not a descent direction")
+        _, _, _, (x, f, g) = backtracking(phi, state.loss, g0, t0, shrink)
+        return x, f, g

@@ -1,0 +1,125 @@
+"""TRON: trust-region Newton with truncated conjugate gradient (LIBLINEAR-style).
+
+Reference: ``photon-lib/.../optimization/TRON.scala:80-340`` — constants eta=(1e-4, .25, .75),
+sigma=(.25, .5, 4); delta0 = ||g0||, first-iteration ``delta = min(delta, ||step||)``; CG at most 20 iterations
+with tolerance ``0.1 ||g||`` and trust-region boundary handling; accept if actual > eta0 * predicted; at most 5
+consecutive improvement failures; defaults tol 1e-5, maxIter 15.
+
+MI355X-native difference: every Hessian-vector product in one outer iteration is taken at the SAME point w, so
+the data backend caches ``wt_i l''(z_i)`` once per outer iteration (K2 in SURVEY §2.8) instead of re-computing
+margins in each CG step as the reference does (``HessianVectorAggregator.scala:111``).
+"""
+from __future__ import annotations
+
+import logging
+import math
+
+import torch
+
+from .optimizer import Optimizer, OptimizerState, project_box
+
+DEFAULT_MAX_NUM_FAILURE = 5
+DEFAULT_TOLERANCE = 1.0e-5
+DEFAULT_MAX_ITER = 15
+MAX_CG_ITERATIONS = 20
+
+log = logging.getLogger(__name__)
+
+
+def _dot(a, b) -> float:
+    return float(torch.dot(a, b))
+
+
+def _norm(a) -> float:
+    return float(torch.linalg.vector_norm(a))
+
+
+class TRON(Optimizer):
+    needs_hessian = True
+    eta0, eta1, eta2 = 1e-4, 0.25, 0.75
+    sigma1, sigma2, sigma3 = 0.25, 0.5, 4.0
+
+    def __init__(self, normalization=None, max_num_failures: int = DEFAULT_MAX_NUM_FAILURE,
+                 tolerance: float = DEFAULT_TOLERANCE, max_iterations: int = DEFAULT_MAX_ITER,
+                 constraints=None, track_state: bool = True):
+        super().__init__(tolerance, max_iterations, normalization, constraints, track_state)
+        self.max_num_failures = max_num_failures
+        self.delta = float("inf")
+        self.total_cg_iterations = 0
+
+    def clear_inner_state(self):
+        super().clear_inner_state()
+        self.delta = float("inf")
+        self.total_cg_iterations = 0
+
+    def _init(self, objective, data, state):
+        self.delta = state.grad_norm()
+
+    @staticmethod
+    def truncated_cg(objective, data, w, gradient, delta):
+        step = torch.zeros_like(gradient)
+        residual = -gradient
+        direction = residual.clone()
+        cg_tol = 0.1 * _norm(gradient)
+        it = 0
+        rtr = _dot(residual, residual)
+        while it < MAX_CG_ITERATIONS:
+            if math.sqrt(max(rtr, 0.0)) <= cg_tol:
+                break
+            it += 1
+            hd = objective.hessian_vector(data, w, direction)
+            alpha = rtr / _dot(direction, hd)
+            step = step + alpha * direction
+            if _norm(step) > delta:
+                step = step - alpha * direction
+                std = _dot(step, direction)
+                sts = _dot(step, step)
+                dtd = _dot(direction, direction)
+                dsq = delta * delta
+                rad = math.sqrt(max(std * std + dtd * (dsq - sts), 0.0))
+                if std >= 0:
+                    alpha = (dsq - sts) / (std + rad)
+                else:
+                    alpha = (rad - std) / dtd
+                step = step + alpha * direction
+                residual = residual - alpha * hd
+                break
+            residual = residual - alpha * hd
+            rnew = _dot(residual, residual)
+            beta = rnew / rtr
+            direction = residual + beta * direction
+            rtr = rnew
+        return it, step, residual
+
+    def _run_one_iteration(self, objective, data, state: OptimizerState) -> OptimizerState:
+        w = state.coefficients
+        f_prev, g_prev = state.loss, state.gradient
+        first = state.iter == 0
+        failures = 0
+        while failures < self.max_num_failures:
+            cg_iter, step, residual = self.truncated_cg(objective, data, w, g_prev, self.delta)
+            self.total_cg_iterations += cg_iter
+            w_new = w + step
+            gs = _dot(g_prev, step)
+            predicted = -0.5 * (gs - _dot(step, residual))
+            f_new, g_new = objective.calculate(data, w_new)
+            actual = f_prev - f_new
+            step_norm = _norm(step)
+            if first:
+                self.delta = min(self.delta, step_norm)
+            denom = f_new - f_prev - gs
+            alpha = self.sigma3 if denom <= 0 else max(self.sigma1, -0.5 * (gs / denom))
+            if actual < self.eta0 * predicted:
+                self.delta = min(max(alpha, self.sigma1) * step_norm, self.sigma2 * self.delta)
+            elif actual < self.eta1 * predicted:
+                self.delta = max(self.sigma1 * self.delta, min(alpha * step_norm, self.sigma2 * self.delta))
+            elif actual < self.eta2 * predicted:
+                self.delta = max(self.sigma1 * self.delta, min(alpha * step_norm, self.sigma3 * self.delta))
+            else:
+                self.delta = max(self.delta, min(alpha * step_norm, self.sigma3 * self.delta))
+            log.debug("iter %d act %.3e pre %.3e delta %.3e f %.3e |g| %.3e CG %d",
+                      state.iter, actual, predicted, self.delta, f_new, _norm(g_new), cg_iter)
+            if actual > self.eta0 * predicted:
+                return OptimizerState(project_box(w_new, self.constraints), f_new, g_new, state.iter + 1)
+            failures += 1
+        return state

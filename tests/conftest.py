@@ -1,0 +1,24 @@
+import os
+import sys
+
+import pytest
+
+sys.path.insert(0, os.path.dirname(os.path.dirname(os.path.abspath(__file__))))
+
+
+def pytest_configure(config):
+    config.addinivalue_line("markers", "gpu: test needs a real MI355X GPU (HIP kernels)")
+    config.addinivalue_line("markers", "slow: long-running test")
+
+
+def gpu_available() -> bool:
+    try:
+        import torch
+        return torch.cuda.is_available()
+    except Exception:  # pragma: no cover
+        return False
+
+
+@pytest.fixture(scope="session")
+def device():
+    return "cuda" if gpu_available() else "cpu"

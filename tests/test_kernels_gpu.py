@@ -1,0 +1,119 @@
+"""HIP kernel parity vs the fp64 torch reference (SURVEY §4 tier 2).
+
+Covers every epilogue (value+grad, Hv, Hdiag, margins) x every loss x precision {f64, f32, bf16}, on shapes that
+exercise long rows (> NB entries: piece blocks + in-order combine), long columns, empty rows/columns and several
+row chunks.
+"""
+import numpy as np
+import pytest
+import scipy.sparse as sp
+import torch
+
+from photon_ml_amd.data.matrix import LabeledData
+from photon_ml_amd.function.losses import LOGISTIC, POISSON, SQUARED, SMOOTHED_HINGE
+from photon_ml_amd.ops.reference import TorchGLMData
+
+pytestmark = pytest.mark.gpu
+
+
+def make_data(n=3000, d=500, density=0.02, seed=0, long_rows=True, hot_cols=True):
+    rng = np.random.default_rng(seed)
+    x = sp.random(n, d, density=density, format="lil", random_state=seed, data_rvs=lambda k: rng.normal(size=k))
+    if long_rows:
+        x[7, :] = rng.normal(size=d)  # dense row
+        x[8, :] = 0  # empty row
+    x = x.tocsr()
+    if hot_cols:
+        hot = sp.csr_matrix((rng.normal(size=n), (np.arange(n), np.full(n, 3))), shape=(n, d))
+        x = x + hot
+        x[:, d - 1] = 1.0  # intercept column
+    x = sp.csr_matrix(x)
+    w = rng.normal(size=d) * 0.1
+    z = x @ w
+    y = (rng.random(n) < 1 / (1 + np.exp(-z))).astype(float)
+    return LabeledData(x, y, offsets=rng.normal(size=n) * 0.1, weights=rng.random(n) + 0.5)
+
+
+TOL = {"f64": 1e-10, "f32": 2e-5, "bf16": 2e-5}
+
+
+def _round_bf16(data: LabeledData) -> LabeledData:
+    x = data.x.copy()
+    x.data = torch.from_numpy(x.data).to(torch.bfloat16).double().numpy()
+    return LabeledData(x, data.y, data.offsets, data.weights)
+
+
+@pytest.mark.parametrize("chunk_rows", [1500, 8192])
+@pytest.mark.parametrize("precision", ["f64", "f32", "bf16"])
+@pytest.mark.parametrize("loss", [LOGISTIC, POISSON, SQUARED, SMOOTHED_HINGE])
+def test_value_grad_parity(precision, loss, chunk_rows):
+    from photon_ml_amd.ops.device import DeviceGLMData
+    data = make_data(n=9000, d=6000 if precision == "f64" else 700, density=0.005)
+    if precision == "bf16":
+        data = _round_bf16(data)
+    ref = TorchGLMData(data, "cpu")
+    dev = DeviceGLMData.from_labeled(data, "cuda", precision, chunk_rows=chunk_rows)
+    rng = np.random.default_rng(1)
+    w = torch.from_numpy(rng.normal(size=data.n_features) * 0.05)
+    if precision != "f64":
+        w = w.float().double()  # the kernel gathers w in fp32
+    shift = 0.03
+    f0, s0, g0 = ref.value_grad_sums(loss, w, shift)
+    f1, s1, g1 = dev.value_grad_sums(loss, w.cuda(), shift)
+    tol = TOL[precision]
+    assert abs(f1 - f0) <= tol * max(1.0, abs(f0))
+    assert abs(s1 - s0) <= tol * max(1.0, abs(s0))
+    assert torch.allclose(g1.cpu(), g0, rtol=tol, atol=tol * float(g0.abs().max()))
+    # determinism: bitwise identical on re-run
+    f2, s2, g2 = dev.value_grad_sums(loss, w.cuda(), shift)
+    assert f2 == f1 and s2 == s1 and torch.equal(g2, g1)
+
+
+@pytest.mark.parametrize("precision", ["f64", "f32"])
+@pytest.mark.parametrize("loss", [LOGISTIC, POISSON, SQUARED])
+def test_hessian_parity(precision, loss):
+    from photon_ml_amd.ops.device import DeviceGLMData
+    data = make_data(n=4000, d=5000, density=0.01, seed=3)
+    ref = TorchGLMData(data, "cpu")
+    dev = DeviceGLMData.from_labeled(data, "cuda", precision, chunk_rows=1024)
+    dev.track_hessian = True
+    rng = np.random.default_rng(2)
+    w = torch.from_numpy(rng.normal(size=data.n_features) * 0.05).float().double()
+    v = torch.from_numpy(rng.normal(size=data.n_features)).float().double()
+    tol = TOL[precision]
+    h0, p0 = ref.hv_sums(loss, w, 0.01, v, 0.2)
+    dev.value_grad_sums(loss, w.cuda(), 0.01)  # populates the l'' cache
+    h1, p1 = dev.hv_sums(loss, w.cuda(), 0.01, v.cuda(), 0.2)
+    assert abs(p1 - p0) <= tol * max(1, abs(p0)) * 10
+    assert torch.allclose(h1.cpu(), h0, rtol=tol * 10, atol=tol * 10 * float(h0.abs().max()))
+    # cache miss path (different w)
+    w2 = w * 0.5
+    h0b, _ = ref.hv_sums(loss, w2, 0.0, v, 0.0)
+    h1b, _ = dev.hv_sums(loss, w2.cuda(), 0.0, v.cuda(), 0.0)
+    assert torch.allclose(h1b.cpu(), h0b, rtol=tol * 10, atol=tol * 10 * float(h0b.abs().max()))
+    d0 = ref.hdiag_sums(loss, w)
+    d1 = dev.hdiag_sums(loss, w.cuda())
+    assert torch.allclose(d1.cpu(), d0, rtol=tol * 10, atol=tol * 10 * float(d0.abs().max()))
+
+
+@pytest.mark.parametrize("precision", ["f64", "bf16"])
+def test_margins(precision):
+    from photon_ml_amd.ops.device import DeviceGLMData
+    data = make_data(n=3000, d=300, density=0.05, seed=5)
+    if precision == "bf16":
+        data = _round_bf16(data)
+    ref = TorchGLMData(data, "cpu")
+    dev = DeviceGLMData.from_labeled(data, "cuda", precision, chunk_rows=700)
+    w = torch.from_numpy(np.random.default_rng(0).normal(size=300)).float().double()
+    z0 = ref.margins(w, 0.5, with_offsets=True)
+    z1 = dev.margins(w.cuda(), 0.5, with_offsets=True).cpu()
+    assert torch.allclose(z1, z0, rtol=TOL[precision], atol=TOL[precision] * 10)
+
+
+def test_empty_and_tiny_shards():
+    from photon_ml_amd.ops.device import DeviceGLMData
+    data = LabeledData(sp.csr_matrix((3, 4)), np.array([0.0, 1.0, 1.0]))
+    dev = DeviceGLMData.from_labeled(data, "cuda", "f64")
+    f, s, g = dev.value_grad_sums(LOGISTIC, torch.zeros(4, dtype=torch.float64, device="cuda"), 0.0)
+    assert abs(f - 3 * np.log(2)) < 1e-12
+    assert torch.all(g == 0)

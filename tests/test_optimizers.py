@@ -1,0 +1,108 @@
+"""Optimizer tests mirroring photon-lib/src/test/.../optimization/{OptimizerTest,LBFGSTest,OWLQNTest,
+OptimizationUtilsTest}.scala and the scikit-learn coefficient checks of
+photon-api/src/integTest/.../estimators/GameEstimatorIntegTest.scala:79-178."""
+import numpy as np
+import pytest
+import torch
+
+from photon_ml_amd.data.matrix import LabeledData
+from photon_ml_amd.function.losses import SQUARED, LOGISTIC
+from photon_ml_amd.function.objective import GLMObjective
+from photon_ml_amd.ops.reference import TorchGLMData
+from photon_ml_amd.optimization import (LBFGS, OWLQN, TRON, ConvergenceReason, project_box)
+
+
+class QuadraticData:
+    """sum_j (w_j - c)^2 expressed through the GLMComputable interface (TestObjective.scala)."""
+
+    def __init__(self, dim, centroid=4.0):
+        self.dim = dim
+        self.c = centroid
+        self.n_rows = 1
+
+    def value_grad_sums(self, loss, w_eff, shift):
+        d = w_eff - self.c
+        return float(torch.dot(d, d)), 0.0, 2.0 * d
+
+    def hv_sums(self, loss, w_eff, shift, v_eff, vshift):
+        return 2.0 * v_eff, 0.0
+
+
+TRIVIAL = [
+    (0.0, [-0.7306653538519616, 0.0]),
+    (1.0, [0.6750417712898752, -0.4232874171873786]),
+    (1.0, [0.1863463229359709, -0.8163423997075965]),
+    (0.0, [-0.6719842051493347, 0.0]),
+    (1.0, [0.9699938346531928, 0.0]),
+    (1.0, [0.22759406190283604, 0.0]),
+    (1.0, [0.9688721028330911, 0.0]),
+    (0.0, [0.5993795346650845, 0.0]),
+    (0.0, [0.9219423508390701, -0.8972778242305388]),
+    (0.0, [0.7006904841584055, -0.5607635619919824]),
+]
+
+
+def trivial_data():
+    y = np.array([t[0] for t in TRIVIAL])
+    x = np.array([t[1] + [1.0] for t in TRIVIAL])
+    return LabeledData(x, y)
+
+
+@pytest.mark.parametrize("opt_cls", [LBFGS, TRON])
+def test_converges_to_centroid(opt_cls):
+    data = QuadraticData(5)
+    obj = GLMObjective(SQUARED)
+    opt = opt_cls(tolerance=1e-9, max_iterations=100)
+    w, f = opt.optimize(obj, data, torch.zeros(5, dtype=torch.float64))
+    assert torch.allclose(w, torch.full((5,), 4.0, dtype=torch.float64), atol=1e-4)
+    assert f < 1e-6
+    # objective monotone non-increasing across tracked states
+    losses = [s.loss for s in opt.tracker.states]
+    assert all(b <= a + 1e-12 for a, b in zip(losses, losses[1:]))
+    assert opt.tracker.convergence_reason is not None
+
+
+@pytest.mark.parametrize("lam,w_exp,f_exp", [(1.0, 3.5, 7.5), (2.0, 3.0, 14.0), (8.0, 0.0, 32.0)])
+def test_owlqn_analytic(lam, w_exp, f_exp):
+    """OWLQNTest.scala:45-47: minimise sum (w-4)^2 + lam ||w||_1 in 2-D."""
+    data = QuadraticData(2)
+    opt = OWLQN(lam, tolerance=1e-12, max_iterations=100)
+    w, f = opt.optimize(GLMObjective(SQUARED), data, torch.zeros(2, dtype=torch.float64))
+    assert np.allclose(w.numpy(), w_exp, atol=1e-6)
+    assert abs(f - f_exp) < 1e-6
+
+
+def test_box_constraints():
+    data = QuadraticData(3)
+    cons = {0: (-1.0, 1.0), 2: (4.5, 10.0)}
+    for cls in (LBFGS, TRON):
+        opt = cls(tolerance=1e-9, max_iterations=50, constraints=cons)
+        w, _ = opt.optimize(GLMObjective(SQUARED), data, torch.zeros(3, dtype=torch.float64))
+        assert w[0] <= 1.0 + 1e-12 and w[0] >= -1.0
+        assert w[2] >= 4.5
+    p = project_box(torch.tensor([-5.0, 0.5, 5.0], dtype=torch.float64), {0: (-1, 1), 2: (0, 2)})
+    assert p.tolist() == [-1.0, 0.5, 2.0]
+
+
+def test_linear_regression_matches_sklearn():
+    """GameEstimatorIntegTest.simpleHardcodedTest: L2 lambda=0.3, LBFGS tol 1e-11 -> sklearn coefficients."""
+    data = TorchGLMData(trivial_data())
+    obj = GLMObjective(SQUARED, l2_weight=0.3)
+    opt = LBFGS(tolerance=1e-11, max_iterations=100)
+    w, _ = opt.optimize(obj, data, torch.zeros(3, dtype=torch.float64))
+    expected = [0.3215554473500486, 0.17904355431985355, 0.4122241763914806]
+    assert np.allclose(w.numpy(), expected, atol=1e-12, rtol=0)
+
+
+def test_tron_matches_lbfgs_logistic():
+    rng = np.random.default_rng(0)
+    x = rng.normal(size=(500, 8))
+    x[:, -1] = 1.0
+    w_true = rng.normal(size=8)
+    y = (rng.random(500) < 1 / (1 + np.exp(-x @ w_true))).astype(float)
+    data = TorchGLMData(LabeledData(x, y))
+    obj = GLMObjective(LOGISTIC, l2_weight=1.0)
+    w1, f1 = LBFGS(tolerance=1e-10, max_iterations=200).optimize(obj, data, torch.zeros(8, dtype=torch.float64))
+    w2, f2 = TRON(tolerance=1e-10, max_iterations=50).optimize(obj, data, torch.zeros(8, dtype=torch.float64))
+    assert abs(f1 - f2) < 1e-7
+    assert np.allclose(w1.numpy(), w2.numpy(), atol=1e-5)
