@@ -78,8 +78,9 @@ def generate_device_shard(n_rows: int, n_features: int, nnz_per_row: int, device
     gen = torch.Generator(device=dev)
     gen.manual_seed(seed + 7919 * rank)
     starts = list(range(0, n_rows, chunk_rows)) + [n_rows]
-    csr, csc = [], []
     k = nnz_per_row
+    raw = []
+    counts = torch.zeros(n_features, dtype=torch.int64, device=dev)
     for ci, (a, b) in enumerate(zip(starts[:-1], starts[1:])):
         m = b - a
         u = torch.rand((m, n_fields), generator=gen, device=dev)
@@ -92,27 +93,38 @@ def generate_device_shard(n_rows: int, n_features: int, nnz_per_row: int, device
         val = torch.empty((m, k), dtype=torch.float32, device=dev)
         val[:, :n_fields] = torch.rand((m, n_fields), generator=gen, device=dev) + 0.5
         val[:, n_fields] = 1.0
-        val = val.to(vdt)
         idx = idx.reshape(-1)
-        val = val.reshape(-1)
-        seg_ptr = np.arange(0, (m + 1) * k, k, dtype=np.int64)
-        if seg_ptr[-1] >= 2 ** 31:
+        counts += torch.bincount(idx.to(torch.int64), minlength=n_features)
+        raw.append((idx, val.to(vdt).reshape(-1)))
+        if (m + 1) * k >= 2 ** 31:
             raise ValueError("chunk too large for int32 offsets: lower chunk_rows")
-        csr.append(SegChunk(seg_ptr.astype(np.int32), idx, val, dev))
+    # relabel features hottest-first (the forward kernel keeps the head of w in an LDS hot table)
+    old_of_new = torch.argsort(counts, descending=True, stable=True)
+    new_of_old = torch.empty_like(old_of_new)
+    new_of_old[old_of_new] = torch.arange(n_features, device=dev)
+    new_of_old32 = new_of_old.to(torch.int32)
+    del counts
+    csr, csc = [], []
+    for ci, ((a, b), (idx, val)) in enumerate(zip(zip(starts[:-1], starts[1:]), raw)):
+        m = b - a
+        idx = new_of_old32[idx.to(torch.int64)]
+        seg_ptr = np.arange(0, (m + 1) * k, k, dtype=np.int64).astype(np.int32)
+        csr.append(SegChunk(seg_ptr, idx, val, dev, forward=True))
         # CSC of the chunk: stable sort by column -> rows stay ascending inside each column segment
         perm = torch.argsort(idx, stable=True)
         cidx = (perm // k).to(torch.int32)
         cval = val[perm]
-        counts = torch.bincount(idx.to(torch.int64), minlength=n_features)
         colptr = torch.zeros(n_features + 1, dtype=torch.int64, device=dev)
-        colptr[1:] = torch.cumsum(counts, 0)
-        del perm, counts
+        colptr[1:] = torch.cumsum(torch.bincount(idx.to(torch.int64), minlength=n_features), 0)
+        del perm
         csc.append(SegChunk(colptr.cpu().numpy().astype(np.int32), cidx, cval, dev))
-        del cidx, cval, colptr
+        raw[ci] = None
+        del cidx, cval, colptr, idx, val
         if progress is not None:
             progress(ci + 1, len(starts) - 1)
     y = torch.zeros(n_rows, dtype=torch.float32, device=dev)
-    data = DeviceGLMData(csr, csc, starts, y, torch.zeros_like(y), torch.ones_like(y), n_features, precision, dev)
+    data = DeviceGLMData(csr, csc, starts, y, torch.zeros_like(y), torch.ones_like(y), n_features, precision, dev,
+                         old_of_new)
     # labels from a sparse ground truth
     wgen = torch.Generator(device=dev)
     wgen.manual_seed(seed)

@@ -27,7 +27,7 @@
 #define NB 4096          // max entries per block
 #define NTHREADS 256     // 4 wave64 per block
 #define VEC 8            // entries per lane per load round
-#define MAXSEG 2048      // max segments per normal block
+#define MAXSEG 1024      // max segments per normal block
 
 enum LossId { LOSS_LOGISTIC = 0, LOSS_POISSON = 1, LOSS_SQUARED = 2, LOSS_HINGE = 3 };
 enum FwdMode { FWD_MARGIN = 0, FWD_VALUE_GRAD = 1, FWD_HV = 2, FWD_DZZ = 3 };
@@ -121,40 +121,163 @@ __device__ __forceinline__ BlockDesc load_desc(const int* __restrict__ blk, int 
   return d;
 }
 
-// Stream [lo8, hi8) (8-aligned window around [nz_lo, nz_hi)), computing products val*x[idx] (SQ: val^2*x[idx]).
-// Normal blocks stage products into LDS; piece blocks return the thread's partial sum.
-template <typename VT, typename XT, typename AT, bool SQ>
+// ------------------------------------------------------------------------------------------------------------
+// Streaming a block's window [lo8, hi8) (8-aligned around [nz_lo, nz_hi)) and forming products val * x[idx]
+// (SQ: val^2 * x[idx]). Two lane layouts:
+//   VECTOR  : lane owns 8 consecutive entries per round (16-B index/value loads).
+//   STRIDED : entry = round*256 + lane, i.e. one wave-instruction touches 64 CONSECUTIVE entries. Index loads are
+//             4 B/lane but still fully coalesced (256 B per wave-instruction); the gain is on the GATHERS: in a hot
+//             CSC column consecutive entries are nearby rows, so one gather instruction hits a handful of cache
+//             lines instead of 64 (the vector layout spreads an instruction's lanes over 512 entries).
+// All of a block's stream loads are issued first (non-temporal: read once per pass, keep L1/L2 for the gathered
+// vector), then all gathers, then the products. HOT: indices < hot_n are served from an LDS copy of the head of
+// x (features relabelled by frequency, so the head is the hottest features).
+typedef int v4i __attribute__((ext_vector_type(4)));
+typedef unsigned int v4u __attribute__((ext_vector_type(4)));
+typedef float v4f __attribute__((ext_vector_type(4)));
+typedef double v2d __attribute__((ext_vector_type(2)));
+#define ROUNDS (NB / (NTHREADS * VEC))   // vector layout rounds (2)
+#define SROUNDS (NB / NTHREADS)          // strided layout rounds (16)
+
+template <typename VT> struct RawVals;
+template <> struct RawVals<uint16_t> {
+  v4u r;
+  __device__ __forceinline__ void load(const uint16_t* p) { r = __builtin_nontemporal_load((const v4u*)p); }
+  __device__ __forceinline__ void get(float* v) const {
+#pragma unroll
+    for (int k = 0; k < 4; ++k) {
+      v[2 * k] = __uint_as_float(r[k] << 16);
+      v[2 * k + 1] = __uint_as_float(r[k] & 0xffff0000u);
+    }
+  }
+};
+template <> struct RawVals<float> {
+  v4f a, b;
+  __device__ __forceinline__ void load(const float* p) {
+    a = __builtin_nontemporal_load((const v4f*)p);
+    b = __builtin_nontemporal_load((const v4f*)(p + 4));
+  }
+  __device__ __forceinline__ void get(float* v) const {
+#pragma unroll
+    for (int k = 0; k < 4; ++k) { v[k] = a[k]; v[4 + k] = b[k]; }
+  }
+};
+template <> struct RawVals<double> {
+  v2d a[4];
+  __device__ __forceinline__ void load(const double* p) {
+#pragma unroll
+    for (int k = 0; k < 4; ++k) a[k] = __builtin_nontemporal_load((const v2d*)(p + 2 * k));
+  }
+  __device__ __forceinline__ void get(double* v) const {
+#pragma unroll
+    for (int k = 0; k < 4; ++k) { v[2 * k] = a[k][0]; v[2 * k + 1] = a[k][1]; }
+  }
+};
+
+__device__ __forceinline__ float val1(const uint16_t* p) {
+  return __uint_as_float(((unsigned)__builtin_nontemporal_load(p)) << 16);
+}
+__device__ __forceinline__ float val1(const float* p) { return __builtin_nontemporal_load(p); }
+__device__ __forceinline__ double val1(const double* p) { return __builtin_nontemporal_load(p); }
+
+template <typename XT, bool HOT>
+__device__ __forceinline__ XT gather(const XT* __restrict__ x, const XT* hot, int hot_n, int j) {
+  if (HOT) return j < hot_n ? hot[j] : x[j];
+  return x[j];
+}
+
+template <typename VT, typename XT, typename AT, bool SQ, bool STRIDED, bool HOT>
 __device__ __forceinline__ double stream_products(const BlockDesc& d, const int* __restrict__ idx,
                                                   const VT* __restrict__ val, const XT* __restrict__ x,
-                                                  AT* prod, bool to_lds) {
+                                                  const XT* hot, int hot_n, AT* prod, bool to_lds, int abl) {
   const int lo = d.nz_lo & ~(VEC - 1);
   const int hi = (d.nz_hi + VEC - 1) & ~(VEC - 1);
+  const int amask = (abl & 1) ? 255 : 0x7fffffff;
   double acc = 0.0;
-  for (int e = lo + threadIdx.x * VEC; e < hi; e += NTHREADS * VEC) {
-    int4 i0 = *reinterpret_cast<const int4*>(idx + e);
-    int4 i1 = *reinterpret_cast<const int4*>(idx + e + 4);
-    int ii[8] = {i0.x, i0.y, i0.z, i0.w, i1.x, i1.y, i1.z, i1.w};
-    AT v[8];
-    Loader<VT, AT>::load8(val + e, v);
-    AT p[8];
+  for (int base = lo; base < hi; base += NB) {
+    if (STRIDED) {
+      int ii[SROUNDS];
+      AT v[SROUNDS];
 #pragma unroll
-    for (int k = 0; k < 8; ++k) {
-      const bool in = (e + k >= d.nz_lo) && (e + k < d.nz_hi);
-      const int j = in ? ii[k] : 0;
-      AT xv = static_cast<AT>(x[j]);
-      AT vv = SQ ? v[k] * v[k] : v[k];
-      p[k] = in ? vv * xv : AT(0);
-    }
-    if (to_lds) {
+      for (int r = 0; r < SROUNDS; ++r) {
+        const int e = base + r * NTHREADS + threadIdx.x;
+        ii[r] = e < hi ? __builtin_nontemporal_load(idx + e) : 0;
+      }
 #pragma unroll
-      for (int k = 0; k < 8; ++k) prod[e - lo + k] = p[k];
+      for (int r = 0; r < SROUNDS; ++r) {
+        const int e = base + r * NTHREADS + threadIdx.x;
+        v[r] = e < hi ? static_cast<AT>(val1(val + e)) : AT(0);
+      }
+      XT xv[SROUNDS];
+#pragma unroll
+      for (int r = 0; r < SROUNDS; ++r) {
+        const int e = base + r * NTHREADS + threadIdx.x;
+        const bool in = (e >= d.nz_lo) && (e < d.nz_hi);
+        xv[r] = gather<XT, HOT>(x, hot, hot_n, (in ? ii[r] : 0) & amask);
+      }
+      AT s = AT(0);
+#pragma unroll
+      for (int r = 0; r < SROUNDS; ++r) {
+        const int e = base + r * NTHREADS + threadIdx.x;
+        const bool in = (e >= d.nz_lo) && (e < d.nz_hi);
+        const AT vv = SQ ? v[r] * v[r] : v[r];
+        const AT p = in ? vv * static_cast<AT>(xv[r]) : AT(0);
+        if (to_lds) {
+          if (e < hi) prod[e - lo] = p;
+        } else {
+          s += p;
+        }
+      }
+      if (!to_lds) acc += static_cast<double>(s);
     } else {
-      float s4 = 0.f;
-      double s = 0.0;
+      v4i i0[ROUNDS], i1[ROUNDS];
+      RawVals<VT> rv[ROUNDS];
 #pragma unroll
-      for (int k = 0; k < 8; ++k) s += static_cast<double>(p[k]);
-      (void)s4;
-      acc += s;
+      for (int r = 0; r < ROUNDS; ++r) {
+        const int e = base + (r * NTHREADS + threadIdx.x) * VEC;
+        if (e < hi) {
+          i0[r] = __builtin_nontemporal_load((const v4i*)(idx + e));
+          i1[r] = __builtin_nontemporal_load((const v4i*)(idx + e + 4));
+          rv[r].load(val + e);
+        }
+      }
+      XT xv[ROUNDS][8];
+#pragma unroll
+      for (int r = 0; r < ROUNDS; ++r) {
+        const int e = base + (r * NTHREADS + threadIdx.x) * VEC;
+        if (e < hi) {
+#pragma unroll
+          for (int k = 0; k < 8; ++k) {
+            const int ik = k < 4 ? i0[r][k] : i1[r][k - 4];
+            const bool in = (e + k >= d.nz_lo) && (e + k < d.nz_hi);
+            xv[r][k] = gather<XT, HOT>(x, hot, hot_n, (in ? ik : 0) & amask);
+          }
+        }
+      }
+#pragma unroll
+      for (int r = 0; r < ROUNDS; ++r) {
+        const int e = base + (r * NTHREADS + threadIdx.x) * VEC;
+        if (e < hi) {
+          AT v[8], p[8];
+          rv[r].get(v);
+#pragma unroll
+          for (int k = 0; k < 8; ++k) {
+            const bool in = (e + k >= d.nz_lo) && (e + k < d.nz_hi);
+            const AT vv = SQ ? v[k] * v[k] : v[k];
+            p[k] = in ? vv * static_cast<AT>(xv[r][k]) : AT(0);
+          }
+          if (to_lds) {
+            AT* q = prod + (e - lo);
+#pragma unroll
+            for (int k = 0; k < 8; ++k) q[k] = p[k];
+          } else {
+            AT s = AT(0);
+#pragma unroll
+            for (int k = 0; k < 8; ++k) s += p[k];
+            acc += static_cast<double>(s);
+          }
+        }
+      }
     }
   }
   return acc;
@@ -173,7 +296,6 @@ __device__ __forceinline__ int group_size(int nseg) {
   return 1;
 }
 
-template <typename AT>
 __device__ __forceinline__ double group_reduce(double v, int G) {
   for (int o = G >> 1; o > 0; o >>= 1) v += __shfl_xor(v, o, 64);
   return v;
@@ -190,27 +312,41 @@ struct FwdArgs {
   XT* dzz;            // VALUE_GRAD with cache: wt*l''; HV: input D_i
   double* z_out;      // MARGIN: z (double)
   int with_offset;    // MARGIN: add offset
+  int abl;            // ablation bits (profiling only): 1 = gather from a 1 KB window, 2 = skip segmented reduce
+  int hot_n;          // entries of x staged in LDS (features relabelled hottest-first), 0 = none
 };
 
+// Per-row epilogue inputs, prefetched at block start (coalesced, latency hidden behind the stream phase)
 template <typename XT, typename RT>
-__device__ __forceinline__ void fwd_epilogue(const FwdArgs<XT, RT>& a, int s, double sum, double& F, double& S) {
+struct RowIn { RT y, off, wt; XT d; };
+
+template <typename XT, typename RT>
+__device__ __forceinline__ RowIn<XT, RT> fwd_prefetch(const FwdArgs<XT, RT>& a, int s) {
+  RowIn<XT, RT> r;
+  r.y = RT(0); r.off = RT(0); r.wt = RT(0); r.d = XT(0);
+  if (a.mode == FWD_MARGIN) { if (a.with_offset) r.off = a.off[s]; }
+  else if (a.mode == FWD_HV) { r.d = a.dzz[s]; }
+  else { r.y = a.y[s]; r.off = a.off[s]; r.wt = a.wt[s]; }
+  return r;
+}
+
+template <typename XT, typename RT>
+__device__ __forceinline__ void fwd_finish(const FwdArgs<XT, RT>& a, int s, double sum, const RowIn<XT, RT>& r,
+                                           double& F, double& S) {
   if (a.mode == FWD_MARGIN) {
-    double z = sum + a.shift;
-    if (a.with_offset) z += static_cast<double>(a.off[s]);
-    a.z_out[s] = z;
+    a.z_out[s] = sum + a.shift + static_cast<double>(r.off);
     return;
   }
   if (a.mode == FWD_HV) {
-    double e = static_cast<double>(a.dzz[s]) * (sum - a.shift);
+    const double e = static_cast<double>(r.d) * (sum - a.shift);
     a.coef[s] = static_cast<XT>(e);
     S += e;
     return;
   }
-  const double z = sum + a.shift + static_cast<double>(a.off[s]);
-  const double y = static_cast<double>(a.y[s]);
-  const double w = static_cast<double>(a.wt[s]);
+  const double z = sum + a.shift + static_cast<double>(r.off);
+  const double w = static_cast<double>(r.wt);
   double l, dl, d2;
-  pointwise_loss(a.loss, z, y, l, dl, d2);
+  pointwise_loss(a.loss, z, static_cast<double>(r.y), l, dl, d2);
   if (a.mode == FWD_VALUE_GRAD) {
     a.coef[s] = static_cast<XT>(w * dl);
     if (a.dzz) a.dzz[s] = static_cast<XT>(w * d2);
@@ -221,44 +357,91 @@ __device__ __forceinline__ void fwd_epilogue(const FwdArgs<XT, RT>& a, int s, do
   }
 }
 
-template <typename VT, typename XT, typename RT, typename AT>
-__global__ __launch_bounds__(NTHREADS) void seg_fwd_kernel(
-    const int* __restrict__ blk, const int* __restrict__ seg_ptr, const int* __restrict__ idx,
-    const VT* __restrict__ val, const XT* __restrict__ x, FwdArgs<XT, RT> a, double* __restrict__ stats,
-    double* __restrict__ parts) {
-  __shared__ AT prod[NB + 2 * VEC];
-  __shared__ double sh[2 * NTHREADS / 64];
-  const BlockDesc d = load_desc(blk, blockIdx.x);
-  if (d.part >= 0) {
-    double acc = stream_products<VT, XT, AT, false>(d, idx, val, x, prod, false);
-    double dummy = 0.0;
-    block_sum2(acc, dummy, sh);
-    if (threadIdx.x == 0) parts[d.part] = acc;
-    if (threadIdx.x == 0 && stats) { stats[2 * blockIdx.x] = 0.0; stats[2 * blockIdx.x + 1] = 0.0; }
-    return;
-  }
-  stream_products<VT, XT, AT, false>(d, idx, val, x, prod, true);
-  __syncthreads();
-  const int lo = d.nz_lo & ~(VEC - 1);
-  const int nseg = d.seg_hi - d.seg_lo;
+#define HOT_BYTES 32768
+#define MAXSEG_FWD 256            // forward (CSR) blocks hold <= 256 rows: one row per thread in the epilogue
+#define SPT_FWD (MAXSEG_FWD / NTHREADS)
+#define SPT_T (MAXSEG / NTHREADS)
+
+// Shared-memory image of one block (kept in ONE struct so the kernels declare a single __shared__ object)
+template <typename AT, typename XT, bool HOT, int MS>
+struct BlockSmem {
+  AT prod[NB + 2 * VEC];
+  int segoff[MS + 1];
+  double segsum[MS];
+  double red[2 * NTHREADS / 64];
+  XT hot[HOT ? HOT_BYTES / sizeof(XT) : 1];
+};
+
+// Phase A: segment sums from the LDS products into segsum[] (group size from the segment count).
+template <typename AT, typename XT, bool HOT, int MS>
+__device__ __forceinline__ void segment_sums(BlockSmem<AT, XT, HOT, MS>& sm, int nseg) {
   const int G = group_size(nseg);
   const int gid = threadIdx.x / G, gl = threadIdx.x % G, ngroups = NTHREADS / G;
-  double F = 0.0, S = 0.0;
   for (int base = 0; base < nseg; base += ngroups) {
     const int si = base + gid;
     double sum = 0.0;
-    int s = -1;
     if (si < nseg) {
-      s = d.seg_lo + si;
-      const int b0 = seg_ptr[s] - lo, b1 = seg_ptr[s + 1] - lo;
-      for (int j = b0 + gl; j < b1; j += G) sum += static_cast<double>(prod[j]);
+      const int b0 = sm.segoff[si], b1 = sm.segoff[si + 1];
+      AT part = AT(0);
+      for (int j = b0 + gl; j < b1; j += G) part += sm.prod[j];
+      sum = static_cast<double>(part);
     }
-    sum = group_reduce<AT>(sum, G);
-    if (si < nseg && gl == 0) fwd_epilogue(a, s, sum, F, S);
+    sum = group_reduce(sum, G);
+    if (si < nseg && gl == 0) sm.segsum[si] = sum;
   }
-  if (stats) {
-    block_sum2(F, S, sh);
-    if (threadIdx.x == 0) { stats[2 * blockIdx.x] = F; stats[2 * blockIdx.x + 1] = S; }
+}
+
+// Persistent forward kernel: grid <= resident capacity; each workgroup (optionally) loads the LDS hot table once,
+// then walks blocks b = blockIdx.x, +gridDim.x, ...  Per block: prefetch segment offsets (LDS) and per-row
+// epilogue inputs (registers), stream + gather + products (LDS), segment sums, thread-per-row epilogue with
+// coalesced row I/O, block (F, S) partials.
+template <typename VT, typename XT, typename RT, typename AT, bool STRIDED, bool HOT>
+__global__ __launch_bounds__(NTHREADS) void seg_fwd_kernel(
+    const int* __restrict__ blk, int nblk, const int* __restrict__ seg_ptr, const int* __restrict__ idx,
+    const VT* __restrict__ val, const XT* __restrict__ x, FwdArgs<XT, RT> a, double* __restrict__ stats,
+    double* __restrict__ parts) {
+  __shared__ __attribute__((aligned(16))) BlockSmem<AT, XT, HOT, MAXSEG_FWD> sm;
+  const int hot_n = HOT ? a.hot_n : 0;
+  if (HOT) {
+    for (int i = threadIdx.x; i < hot_n; i += NTHREADS) sm.hot[i] = x[i];
+    __syncthreads();
+  }
+  for (int b = blockIdx.x; b < nblk; b += gridDim.x) {
+    const BlockDesc d = load_desc(blk, b);
+    if (d.part >= 0 || (a.abl & 2)) {
+      double acc = stream_products<VT, XT, AT, false, STRIDED, HOT>(d, idx, val, x, sm.hot, hot_n, sm.prod, false,
+                                                                    a.abl);
+      double dummy = 0.0;
+      block_sum2(acc, dummy, sm.red);
+      if (threadIdx.x == 0 && d.part >= 0) parts[d.part] = acc;
+      if (threadIdx.x == 0 && stats) { stats[2 * b] = (a.abl & 2) ? acc : 0.0; stats[2 * b + 1] = 0.0; }
+      __syncthreads();
+      continue;
+    }
+    const int lo = d.nz_lo & ~(VEC - 1);
+    const int nseg = d.seg_hi - d.seg_lo;
+    for (int i = threadIdx.x; i <= nseg; i += NTHREADS) sm.segoff[i] = seg_ptr[d.seg_lo + i] - lo;
+    RowIn<XT, RT> pre[SPT_FWD];
+#pragma unroll
+    for (int k = 0; k < SPT_FWD; ++k) {
+      const int si = threadIdx.x + k * NTHREADS;
+      if (si < nseg) pre[k] = fwd_prefetch(a, d.seg_lo + si);
+    }
+    stream_products<VT, XT, AT, false, STRIDED, HOT>(d, idx, val, x, sm.hot, hot_n, sm.prod, true, a.abl);
+    __syncthreads();
+    segment_sums(sm, nseg);
+    __syncthreads();
+    double F = 0.0, S = 0.0;
+#pragma unroll
+    for (int k = 0; k < SPT_FWD; ++k) {
+      const int si = threadIdx.x + k * NTHREADS;
+      if (si < nseg) fwd_finish(a, d.seg_lo + si, sm.segsum[si], pre[k], F, S);
+    }
+    if (stats) {
+      block_sum2(F, S, sm.red);
+      if (threadIdx.x == 0) { stats[2 * b] = F; stats[2 * b + 1] = S; }
+    }
+    __syncthreads();  // LDS is rewritten by the next block
   }
 }
 
@@ -275,46 +458,47 @@ __global__ __launch_bounds__(64) void seg_fwd_long_kernel(const int* __restrict_
   sum = wave_sum(sum);
   if (threadIdx.x == 0) {
     double F = 0.0, S = 0.0;
-    fwd_epilogue(a, long_seg[L], sum, F, S);
+    const int s = long_seg[L];
+    fwd_finish(a, s, sum, fwd_prefetch(a, s), F, S);
     if (long_stats) { long_stats[2 * L] = F; long_stats[2 * L + 1] = S; }
   }
 }
 
 // ------------------------------------------------------------------------------------------------------------
-// Transpose (row-chunked CSC): G[col] += sum_i val * x[row]   (SQ: val^2)
-template <typename VT, typename XT, typename AT, bool SQ>
+// Transpose (row-chunked CSC): G[col] += sum_i val * x[row]   (SQ: val^2). The block's columns are a contiguous
+// range, so the fp64 read-modify-write of G is prefetched at block start and written back coalesced.
+template <typename VT, typename XT, typename AT, bool SQ, bool STRIDED>
 __global__ __launch_bounds__(NTHREADS) void seg_t_kernel(const int* __restrict__ blk,
                                                          const int* __restrict__ seg_ptr,
                                                          const int* __restrict__ idx, const VT* __restrict__ val,
                                                          const XT* __restrict__ x, double* __restrict__ G,
-                                                         double* __restrict__ parts) {
-  __shared__ AT prod[NB + 2 * VEC];
-  __shared__ double sh[2 * NTHREADS / 64];
+                                                         double* __restrict__ parts, int abl) {
+  __shared__ __attribute__((aligned(16))) BlockSmem<AT, XT, false, MAXSEG> sm;
   const BlockDesc d = load_desc(blk, blockIdx.x);
   if (d.part >= 0) {
-    double acc = stream_products<VT, XT, AT, SQ>(d, idx, val, x, prod, false);
+    double acc = stream_products<VT, XT, AT, SQ, STRIDED, false>(d, idx, val, x, nullptr, 0, sm.prod, false, abl);
     double dummy = 0.0;
-    block_sum2(acc, dummy, sh);
+    block_sum2(acc, dummy, sm.red);
     if (threadIdx.x == 0) parts[d.part] = acc;
     return;
   }
-  stream_products<VT, XT, AT, SQ>(d, idx, val, x, prod, true);
-  __syncthreads();
   const int lo = d.nz_lo & ~(VEC - 1);
   const int nseg = d.seg_hi - d.seg_lo;
-  const int G_ = group_size(nseg);
-  const int gid = threadIdx.x / G_, gl = threadIdx.x % G_, ngroups = NTHREADS / G_;
-  for (int base = 0; base < nseg; base += ngroups) {
-    const int si = base + gid;
-    double sum = 0.0;
-    int s = -1, b0 = 0, b1 = 0;
-    if (si < nseg) {
-      s = d.seg_lo + si;
-      b0 = seg_ptr[s] - lo; b1 = seg_ptr[s + 1] - lo;
-      for (int j = b0 + gl; j < b1; j += G_) sum += static_cast<double>(prod[j]);
-    }
-    sum = group_reduce<AT>(sum, G_);
-    if (si < nseg && gl == 0 && b1 > b0) G[s] += sum;
+  for (int i = threadIdx.x; i <= nseg; i += NTHREADS) sm.segoff[i] = seg_ptr[d.seg_lo + i] - lo;
+  double g0[SPT_T];
+#pragma unroll
+  for (int k = 0; k < SPT_T; ++k) {
+    const int si = threadIdx.x + k * NTHREADS;
+    g0[k] = si < nseg ? G[d.seg_lo + si] : 0.0;
+  }
+  stream_products<VT, XT, AT, SQ, STRIDED, false>(d, idx, val, x, nullptr, 0, sm.prod, true, abl);
+  __syncthreads();
+  segment_sums(sm, nseg);
+  __syncthreads();
+#pragma unroll
+  for (int k = 0; k < SPT_T; ++k) {
+    const int si = threadIdx.x + k * NTHREADS;
+    if (si < nseg) G[d.seg_lo + si] = g0[k] + sm.segsum[si];
   }
 }
 
@@ -371,12 +555,35 @@ struct SegChunkDesc {
     if (e_ != hipSuccess) return (int)e_;                      \
   } while (0)
 
+static int g_ablate = 0;
+// Runtime kernel configuration (set from Python): lane layout per direction, hot-table size, persistent grid.
+static int g_fwd_strided = 0;
+static int g_t_strided = 1;
+static int g_hot_n = 0;          // requested LDS hot-table entries (clamped to HOT_BYTES / sizeof(XT))
+static int g_fwd_grid = 256 * 4; // persistent forward grid (workgroups)
+
+template <typename VT, typename XT, typename RT, typename AT, bool STRIDED, bool HOT>
+static void launch_fwd(const SegChunkDesc* c, const void* x, FwdArgs<XT, RT> a, double* stats, double* parts,
+                       hipStream_t st) {
+  const int grid = c->nblk < g_fwd_grid ? c->nblk : g_fwd_grid;
+  hipLaunchKernelGGL((seg_fwd_kernel<VT, XT, RT, AT, STRIDED, HOT>), dim3(grid), dim3(NTHREADS), 0, st, c->blk,
+                     c->nblk, c->seg_ptr, c->idx, (const VT*)c->val, (const XT*)x, a, stats, parts);
+}
+
 template <typename VT, typename XT, typename RT, typename AT>
 static int fwd_impl(const SegChunkDesc* c, const void* x, FwdArgs<XT, RT> a, double* stats, double* long_stats,
                     double* parts, hipStream_t st) {
+  const int max_hot = HOT_BYTES / (int)sizeof(XT);
+  a.hot_n = g_hot_n < max_hot ? g_hot_n : max_hot;
   if (c->nblk > 0) {
-    hipLaunchKernelGGL((seg_fwd_kernel<VT, XT, RT, AT>), dim3(c->nblk), dim3(NTHREADS), 0, st, c->blk,
-                       c->seg_ptr, c->idx, (const VT*)c->val, (const XT*)x, a, stats, parts);
+    const bool hot = a.hot_n > 0;
+    if (g_fwd_strided) {
+      if (hot) launch_fwd<VT, XT, RT, AT, true, true>(c, x, a, stats, parts, st);
+      else launch_fwd<VT, XT, RT, AT, true, false>(c, x, a, stats, parts, st);
+    } else {
+      if (hot) launch_fwd<VT, XT, RT, AT, false, true>(c, x, a, stats, parts, st);
+      else launch_fwd<VT, XT, RT, AT, false, false>(c, x, a, stats, parts, st);
+    }
     LAUNCH_CHECK();
   }
   if (c->nlong > 0) {
@@ -390,8 +597,12 @@ static int fwd_impl(const SegChunkDesc* c, const void* x, FwdArgs<XT, RT> a, dou
 template <typename VT, typename XT, typename AT, bool SQ>
 static int t_impl(const SegChunkDesc* c, const void* x, double* G, double* parts, hipStream_t st) {
   if (c->nblk > 0) {
-    hipLaunchKernelGGL((seg_t_kernel<VT, XT, AT, SQ>), dim3(c->nblk), dim3(NTHREADS), 0, st, c->blk, c->seg_ptr,
-                       c->idx, (const VT*)c->val, (const XT*)x, G, parts);
+    if (g_t_strided)
+      hipLaunchKernelGGL((seg_t_kernel<VT, XT, AT, SQ, true>), dim3(c->nblk), dim3(NTHREADS), 0, st, c->blk,
+                         c->seg_ptr, c->idx, (const VT*)c->val, (const XT*)x, G, parts, g_ablate);
+    else
+      hipLaunchKernelGGL((seg_t_kernel<VT, XT, AT, SQ, false>), dim3(c->nblk), dim3(NTHREADS), 0, st, c->blk,
+                         c->seg_ptr, c->idx, (const VT*)c->val, (const XT*)x, G, parts, g_ablate);
     LAUNCH_CHECK();
   }
   if (c->nlong > 0) {
@@ -404,8 +615,15 @@ static int t_impl(const SegChunkDesc* c, const void* x, double* G, double* parts
 extern "C" {
 
 int pml_version() { return 1; }
+void pml_set_ablate(int a) { g_ablate = a; }
+// layout: 0 = vector, 1 = strided; grid: persistent forward grid size (workgroups)
+void pml_set_config(int fwd_strided, int t_strided, int hot_n, int fwd_grid) {
+  g_fwd_strided = fwd_strided; g_t_strided = t_strided; g_hot_n = hot_n;
+  if (fwd_grid > 0) g_fwd_grid = fwd_grid;
+}
 int pml_nb() { return NB; }
 int pml_maxseg() { return MAXSEG; }
+int pml_maxseg_fwd() { return MAXSEG_FWD; }
 
 // ---- host-side block construction (greedy, sequential; the pattern is static so this runs once) ----------
 // seg_ptr: int32[nseg+1] (host). Outputs sized by a first call with blk == NULL.
@@ -465,11 +683,11 @@ int pml_seg_fwd(int prec, const SegChunkDesc* c, const void* x, int mode, int lo
   hipStream_t st = (hipStream_t)stream;
   if (prec == 2) {
     FwdArgs<double, double> a{mode, loss, shift, (const double*)y, (const double*)off, (const double*)wt,
-                              (double*)coef, (double*)dzz, z_out, with_offset};
+                              (double*)coef, (double*)dzz, z_out, with_offset, g_ablate, 0};
     return fwd_impl<double, double, double, double>(c, x, a, stats, long_stats, parts, st);
   }
   FwdArgs<float, float> a{mode, loss, shift, (const float*)y, (const float*)off, (const float*)wt,
-                          (float*)coef, (float*)dzz, z_out, with_offset};
+                          (float*)coef, (float*)dzz, z_out, with_offset, g_ablate, 0};
   if (prec == 1) return fwd_impl<float, float, float, float>(c, x, a, stats, long_stats, parts, st);
   return fwd_impl<uint16_t, float, float, float>(c, x, a, stats, long_stats, parts, st);
 }

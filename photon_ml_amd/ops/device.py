@@ -46,12 +46,13 @@ class SegChunk:
     """One segmented stream (CSR chunk or CSC chunk) resident on the device."""
 
     def __init__(self, seg_ptr: np.ndarray, idx: torch.Tensor, val: torch.Tensor, device, nb: Optional[int] = None,
-                 maxseg: Optional[int] = None):
+                 maxseg: Optional[int] = None, forward: bool = False):
+        """``forward=True`` for CSR (row) streams: their blocks hold at most ``pml_maxseg_fwd()`` rows."""
         lib = require_glm_lib()
         seg_ptr = np.ascontiguousarray(seg_ptr, dtype=np.int32)
         nseg = len(seg_ptr) - 1
         nb = nb or lib.pml_nb()
-        maxseg = maxseg or lib.pml_maxseg()
+        maxseg = maxseg or (lib.pml_maxseg_fwd() if forward else lib.pml_maxseg())
         nblk, nlong, npart = ctypes.c_int(), ctypes.c_int(), ctypes.c_int()
         check(lib.pml_build_blocks(seg_ptr.ctypes.data, nseg, nb, maxseg, None, ctypes.byref(nblk), None, None,
                                    ctypes.byref(nlong), ctypes.byref(npart)), "count blocks")
@@ -89,7 +90,7 @@ class DeviceGLMData(GLMComputable):
     """GLM row shard on one GPU evaluated with the native kernels."""
 
     def __init__(self, csr: List[SegChunk], csc: List[SegChunk], row_starts: Sequence[int], y, offsets, weights,
-                 dim: int, precision: str = "f64", device="cuda"):
+                 dim: int, precision: str = "f64", device="cuda", old_of_new: Optional[torch.Tensor] = None):
         self.lib = require_glm_lib()
         self.device = torch.device(device)
         self.prec = PRECISIONS[precision]
@@ -119,15 +120,30 @@ class DeviceGLMData(GLMComputable):
         self.red_scratch = torch.zeros(512, dtype=torch.float64, device=self.device)
         self.out2 = torch.zeros(2, dtype=torch.float64, device=self.device)
         self.n_passes = 0
+        # Features are relabelled hottest-first on device (so the forward kernel's LDS hot table holds the most
+        # frequent features); the permutation is applied to the D-vectors at the boundary, invisible to callers.
+        self.old_of_new = None if old_of_new is None else old_of_new.to(self.device, torch.int64)
+        if self.old_of_new is not None:
+            self.new_of_old = torch.empty_like(self.old_of_new)
+            self.new_of_old[self.old_of_new] = torch.arange(self.dim, device=self.device)
 
     # ------------------------------------------------------------------
     @staticmethod
-    def from_labeled(data: LabeledData, device="cuda", precision: str = "f64", chunk_rows: int = 1 << 20):
+    def from_labeled(data: LabeledData, device="cuda", precision: str = "f64", chunk_rows: int = 1 << 20,
+                     relabel: bool = True):
         prec = PRECISIONS[precision]
         vdt = VAL_DTYPE[prec]
         dev = torch.device(device)
         x = data.x.tocsr()
         n, d = x.shape
+        old_of_new = None
+        if relabel and x.nnz > 0:
+            counts = np.bincount(x.indices, minlength=d)
+            old_of_new_np = np.argsort(-counts, kind="stable")
+            new_of_old_np = np.empty(d, dtype=np.int64)
+            new_of_old_np[old_of_new_np] = np.arange(d)
+            x = sp.csr_matrix((x.data, new_of_old_np[x.indices], x.indptr), shape=x.shape)
+            old_of_new = torch.from_numpy(old_of_new_np)
         starts = list(range(0, n, chunk_rows)) + [n]
         if n == 0:
             starts = [0, 0]
@@ -136,13 +152,14 @@ class DeviceGLMData(GLMComputable):
             xc = x[a:b]
             sp_ = (xc.indptr - xc.indptr[0]).astype(np.int32)
             csr.append(SegChunk(sp_, torch.from_numpy(xc.indices.astype(np.int32)),
-                                torch.from_numpy(xc.data.astype(np.float64)).to(vdt), dev))
+                                torch.from_numpy(xc.data.astype(np.float64)).to(vdt), dev, forward=True))
             xt = xc.tocsc()
             xt.sort_indices()
+            xc = xc.copy()
             csc.append(SegChunk(xt.indptr.astype(np.int32), torch.from_numpy(xt.indices.astype(np.int32)),
                                 torch.from_numpy(xt.data.astype(np.float64)).to(vdt), dev))
         return DeviceGLMData(csr, csc, starts, torch.from_numpy(data.y), torch.from_numpy(data.offsets),
-                             torch.from_numpy(data.weights), d, precision, dev)
+                             torch.from_numpy(data.weights), d, precision, dev, old_of_new)
 
     def nbytes(self) -> int:
         return sum(c.nbytes() for c in self.csr + self.csc)
@@ -188,7 +205,13 @@ class DeviceGLMData(GLMComputable):
         return out
 
     def _vec(self, w: torch.Tensor) -> torch.Tensor:
-        return w.to(self.device, self.vdt).contiguous()
+        w = w.to(self.device)
+        if self.old_of_new is not None:
+            w = w[self.old_of_new]
+        return w.to(self.vdt).contiguous()
+
+    def _unperm(self, g: torch.Tensor) -> torch.Tensor:
+        return g if self.old_of_new is None else g[self.new_of_old]
 
     # ------------------------------------------------------------------
     def value_grad_packed(self, loss, w_eff, margin_shift) -> torch.Tensor:
@@ -201,6 +224,8 @@ class DeviceGLMData(GLMComputable):
             self._fwd(c, x, FWD_VALUE_GRAD, loss.loss_id, margin_shift, self.coef, dzz)
             self._t(c, self.coef, G)
         out[self.dim:] = self._reduce_stats()
+        if self.old_of_new is not None:
+            out[: self.dim] = self._unperm(G.clone())
         if dzz is not None:
             self._dzz_key = w_eff.detach().clone()
             self._dzz_shift = float(margin_shift)
@@ -232,6 +257,8 @@ class DeviceGLMData(GLMComputable):
             self._fwd(c, x, FWD_HV, loss.loss_id, v_shift, self.coef, self.dzz)
             self._t(c, self.coef, H)
         out[self.dim:] = self._reduce_stats()
+        if self.old_of_new is not None:
+            out[: self.dim] = self._unperm(H.clone())
         self.n_passes += 1
         return out
 
@@ -246,7 +273,7 @@ class DeviceGLMData(GLMComputable):
             self._fwd(c, x, FWD_DZZ, loss.loss_id, 0.0, self.coef, None, stats=False)
             self._t(c, self.coef, out, square=1)
         self._dzz_key = None
-        return out
+        return self._unperm(out)
 
     def margins(self, w, margin_shift: float = 0.0, with_offsets: bool = False):
         z = torch.empty(max(self.n_rows, 1), dtype=torch.float64, device=self.device)

@@ -64,8 +64,29 @@ def glm_lib() -> Optional[ctypes.CDLL]:
         lib.pml_reduce_stats.argtypes = [c_void_p, c_int, c_void_p, c_int, c_void_p, c_void_p]
         for f in ("pml_seg_fwd", "pml_seg_t", "pml_reduce_stats", "pml_build_blocks"):
             getattr(lib, f).restype = c_int
+        lib.pml_set_config.argtypes = [c_int, c_int, c_int, c_int]
         lib._pml_typed = True
+        configure()
     return lib
+
+
+# Kernel configuration defaults (tuned on MI355X, see profiles/): forward = vector layout + 8192-entry LDS hot
+# table of the most frequent features; transpose = strided layout. Env overrides for experiments:
+# PML_FWD_STRIDED, PML_T_STRIDED, PML_HOT_N, PML_FWD_GRID.
+KERNEL_CONFIG = {"fwd_strided": 0, "t_strided": 0, "hot_n": 0, "fwd_grid": 1024}
+
+
+def configure(**kw):
+    KERNEL_CONFIG.update({k: v for k, v in kw.items() if v is not None})
+    for k in list(KERNEL_CONFIG):
+        env = os.environ.get("PML_" + k.upper())
+        if env is not None and k not in kw:
+            KERNEL_CONFIG[k] = int(env)
+    lib = _LIBS.get("glm")
+    if lib is not None:
+        lib.pml_set_config(KERNEL_CONFIG["fwd_strided"], KERNEL_CONFIG["t_strided"], KERNEL_CONFIG["hot_n"],
+                           KERNEL_CONFIG["fwd_grid"])
+    return dict(KERNEL_CONFIG)
 
 
 def require_glm_lib() -> ctypes.CDLL:
