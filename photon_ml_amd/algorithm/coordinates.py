@@ -1,0 +1,248 @@
+"""GAME coordinates: fixed effect (one GLM over a row-sharded feature shard) and random effect (one GLM per
+entity, batched).
+
+Reference: ``photon-lib/.../algorithm/Coordinate.scala:27-80`` (score / initializeModel / updateModel(model,
+partialScore) = add the partial score to the offsets, then optimise), ``photon-api/.../algorithm/
+FixedEffectCoordinate.scala:35-166``, ``RandomEffectCoordinate.scala:39-222`` and
+``RandomEffectCoordinateInProjectedSpace.scala``.
+
+Scores are N-length fp64 tensors aligned with the samples of the training ``GameData`` (no joins). The fixed
+effect coordinate keeps ONE device-resident shard for its whole life and only rewrites its offset / weight
+vectors per update; the random-effect coordinate keeps its buckets resident and gathers the per-slot offsets
+from the partial-score vector (C11 routing) before each batched solve.
+"""
+from __future__ import annotations
+
+from typing import Optional
+
+import numpy as np
+import torch
+
+from ..constants import EPSILON, TaskType
+from ..data.game_data import GameData
+from ..data.random_effect import FixedEffectDataConfiguration, RandomEffectDataConfiguration, RandomEffectDataset
+from ..function.losses import loss_for_task
+from ..models.game import FixedEffectModel, RandomEffectModel
+from ..models.glm import Coefficients, model_for_task
+from ..normalization.context import NormalizationContext
+from ..ops.backend import default_device, make_glm_data
+from ..optimization.batched import BatchedGLMData, batched_lbfgs, batched_tron
+from ..optimization.config import GLMOptimizationConfiguration, OptimizerType, RegularizationType
+from ..optimization.problem import GLMOptimizationProblem
+from ..parallel.dist import DistributedGLMData, is_dist
+from ..sampling.samplers import down_sampler_for_task
+
+
+class Coordinate:
+    coordinate_id: str
+
+    def initialize_model(self):
+        raise NotImplementedError
+
+    def update_model(self, model, partial_score: Optional[torch.Tensor] = None):
+        raise NotImplementedError
+
+    def score(self, model) -> torch.Tensor:
+        raise NotImplementedError
+
+    def regularization_term_value(self, model) -> float:
+        raise NotImplementedError
+
+
+class FixedEffectCoordinate(Coordinate):
+    def __init__(self, coordinate_id: str, data: GameData, data_config: FixedEffectDataConfiguration,
+                 opt_config: GLMOptimizationConfiguration, task, normalization: Optional[NormalizationContext] = None,
+                 compute_variance: bool = False, device=None, precision: str = "f64", local_rows=None):
+        self.coordinate_id = coordinate_id
+        self.data = data
+        self.shard_id = data_config.feature_shard_id
+        self.task = TaskType.parse(task)
+        self.device = torch.device(device) if device is not None else default_device()
+        labeled = data.labeled(self.shard_id)
+        if local_rows is not None:  # row sharding for multi-GPU data parallelism
+            labeled = labeled.subset(local_rows)
+        self.local_rows = local_rows
+        self.base_offsets = labeled.offsets.copy()
+        self.base_weights = labeled.weights.copy()
+        self.labels = labeled.y
+        self.glm_data = make_glm_data(labeled, self.device, precision)
+        self.compute_variance = compute_variance
+        self.normalization = normalization
+        self.set_config(opt_config)
+        self.last_tracker = None
+
+    def set_config(self, opt_config: GLMOptimizationConfiguration):
+        self.opt_config = opt_config
+        self.problem = GLMOptimizationProblem(opt_config, self.task, self.normalization, self.compute_variance)
+        rate = opt_config.down_sampling_rate
+        self.sampler = down_sampler_for_task(self.task, rate) if rate < 1.0 else None
+
+    @property
+    def dim(self) -> int:
+        return self.glm_data.dim
+
+    def _data_view(self):
+        return DistributedGLMData(self.glm_data) if is_dist() else self.glm_data
+
+    def initialize_model(self):
+        return FixedEffectModel(model_for_task(self.task, Coefficients.zeros(self.dim)), self.shard_id)
+
+    def update_model(self, model: FixedEffectModel, partial_score: Optional[torch.Tensor] = None):
+        off = self.base_offsets
+        if partial_score is not None:
+            ps = partial_score.detach().cpu().numpy()
+            if self.local_rows is not None:
+                ps = ps[self.local_rows]
+            off = off + ps
+        self.glm_data.set_offsets(torch.from_numpy(off))
+        wts = self.base_weights if self.sampler is None else self.sampler.sample_weights(self.labels,
+                                                                                            self.base_weights)
+        self.glm_data.set_weights(torch.from_numpy(np.asarray(wts, dtype=np.float64)))
+        glm = self.problem.run(self._data_view(), model.glm if model is not None else None, dim=self.dim)
+        self.last_tracker = self.problem.tracker
+        # restore full weights for scoring/evaluation
+        if self.sampler is not None:
+            self.glm_data.set_weights(torch.from_numpy(self.base_weights))
+        return FixedEffectModel(glm.update_coefficients(
+            Coefficients(glm.coefficients.means.cpu(), None if glm.coefficients.variances is None
+                         else glm.coefficients.variances.cpu())), self.shard_id)
+
+    def score(self, model: FixedEffectModel) -> torch.Tensor:
+        if self.local_rows is None:
+            w = model.glm.coefficients.means.to(self.glm_data.device, torch.float64)
+            return self.glm_data.margins(w).to(self.device, torch.float64)
+        return model.score(self.data, self.device)
+
+    def regularization_term_value(self, model: FixedEffectModel) -> float:
+        return self.problem.regularization_term_value(model.glm)
+
+
+class RandomEffectCoordinate(Coordinate):
+    """Per-entity GLMs solved in size buckets on the device (K7)."""
+
+    def __init__(self, coordinate_id: str, data: GameData, data_config: RandomEffectDataConfiguration,
+                 opt_config: GLMOptimizationConfiguration, task, compute_variance: bool = False, device=None,
+                 dtype=torch.float64, entity_subset=None):
+        self.coordinate_id = coordinate_id
+        self.data = data
+        self.data_config = data_config
+        self.task = TaskType.parse(task)
+        self.loss = loss_for_task(self.task)
+        self.device = torch.device(device) if device is not None else default_device()
+        self.dataset = RandomEffectDataset(data, data_config, self.device, dtype, entity_subset=entity_subset)
+        self.compute_variance = compute_variance
+        self.base_offsets = torch.from_numpy(data.offsets).to(self.device)
+        self.set_config(opt_config)
+        self._W = {}  # projected-space warm-start state per bucket
+        self.last_stats = {}
+
+    def set_config(self, opt_config: GLMOptimizationConfiguration):
+        rt = opt_config.regularization_context.regularization_type
+        if opt_config.optimizer_config.optimizer_type == OptimizerType.TRON and rt in (
+                RegularizationType.L1, RegularizationType.ELASTIC_NET):
+            raise ValueError("TRON optimizer incompatible with L1 regularization")
+        self.opt_config = opt_config
+
+    def initialize_model(self):
+        ds = self.dataset
+        return RandomEffectModel(self.data_config.random_effect_type, self.data_config.feature_shard_id, self.task,
+                                 ds.entity_ids, ds.dim, np.zeros(0, np.int64), np.zeros(0))
+
+    def _warm_start(self, b, bucket, model: Optional[RandomEffectModel]):
+        key = b
+        dev, dt = self.device, self.dataset.dtype
+        B, _, d = bucket.X.shape
+        if key in self._W and self._W[key].shape == (B, d):
+            return self._W[key]
+        W = torch.zeros(B, d, dtype=dt, device=dev)
+        ds = self.dataset
+        if model is not None and len(model.keys) and ds.projector_type.kind.value == "INDEX_MAP":
+            # map original-space coefficients into each entity's local index space
+            ptr, feat = ds.projection.ptr, ds.projection.feat
+            ents = bucket.entities
+            b_idx = np.concatenate([np.full(ds.d_local[e], i) for i, e in enumerate(ents)]) if len(ents) else []
+            c_idx = np.concatenate([np.arange(ds.d_local[e]) for e in ents]) if len(ents) else []
+            gf = np.concatenate([feat[ptr[e]:ptr[e + 1]] for e in ents]) if len(ents) else []
+            mi = model.entity_index(ds.entity_ids[np.repeat(ents, ds.d_local[ents])])
+            k = mi.astype(np.int64) * model.dim + np.asarray(gf, dtype=np.int64)
+            pos = np.searchsorted(model.keys, k)
+            pos_c = np.minimum(pos, len(model.keys) - 1)
+            hit = (pos < len(model.keys)) & (model.keys[pos_c] == k) & (mi >= 0)
+            vals = np.where(hit, model.values[pos_c], 0.0)
+            Wn = np.zeros((B, d))
+            Wn[np.asarray(b_idx, dtype=np.int64), np.asarray(c_idx, dtype=np.int64)] = vals
+            W = torch.from_numpy(Wn).to(dev, dt)
+        return W
+
+    def update_model(self, model: Optional[RandomEffectModel], partial_score: Optional[torch.Tensor] = None):
+        ds = self.dataset
+        cfg = self.opt_config
+        reg, lam = cfg.regularization_context, cfg.regularization_weight
+        l1, l2 = reg.l1_weight(lam), reg.l2_weight(lam)
+        offs = self.base_offsets if partial_score is None else self.base_offsets + partial_score.to(self.device)
+        keys, vals, vars_ = [], [], []
+        iters, n_conv = [], 0
+        for b, bucket in enumerate(ds.buckets):
+            O = ds.bucket_offsets(bucket, offs)
+            bd = BatchedGLMData(bucket.X, bucket.y, O, bucket.w)
+            W0 = self._warm_start(b, bucket, model)
+            oc = cfg.optimizer_config
+            if oc.optimizer_type == OptimizerType.TRON:
+                res = batched_tron(bd, self.loss, l2, W0, oc.tolerance, oc.maximum_iterations)
+            else:
+                res = batched_lbfgs(bd, self.loss, l2, W0, oc.tolerance, oc.maximum_iterations, l1=l1)
+            self._W[b] = res.W
+            iters.append(res.iters)
+            W = res.W
+            var = None
+            if self.compute_variance and self.loss.twice_differentiable:
+                var = 1.0 / (bd.hdiag(self.loss, W, l2) + EPSILON)
+            k, v, vv = self._to_original(bucket, W, var)
+            keys.append(k)
+            vals.append(v)
+            if vv is not None:
+                vars_.append(vv)
+        it = torch.cat(iters) if iters else torch.zeros(0)
+        self.last_stats = {"entities": int(it.numel()), "mean_iterations": float(it.double().mean()) if it.numel()
+                           else 0.0, "max_iterations": int(it.max()) if it.numel() else 0}
+        keys = np.concatenate(keys) if keys else np.zeros(0, np.int64)
+        vals = np.concatenate(vals) if vals else np.zeros(0)
+        variances = np.concatenate(vars_) if vars_ else None
+        return RandomEffectModel(self.data_config.random_effect_type, self.data_config.feature_shard_id, self.task,
+                                 ds.entity_ids, ds.dim, keys, vals, variances)
+
+    def _to_original(self, bucket, W: torch.Tensor, var: Optional[torch.Tensor]):
+        ds = self.dataset
+        kind = ds.projector_type.kind.value
+        Wn = W.detach().cpu().numpy()
+        Vn = None if var is None else var.detach().cpu().numpy()
+        ents = bucket.entities
+        if kind == "INDEX_MAP":
+            ptr, feat = ds.projection.ptr, ds.projection.feat
+            dl = ds.d_local[ents]
+            b_idx = np.repeat(np.arange(len(ents)), dl)
+            c_idx = np.concatenate([np.arange(x) for x in dl]) if len(ents) else np.zeros(0, np.int64)
+            gf = np.concatenate([feat[ptr[e]:ptr[e + 1]] for e in ents]) if len(ents) else np.zeros(0, np.int64)
+            vals = Wn[b_idx, c_idx]
+            keys = np.repeat(ents, dl).astype(np.int64) * ds.dim + gf
+            vv = None if Vn is None else Vn[b_idx, c_idx]
+        else:
+            if kind == "RANDOM":
+                orig = Wn @ ds.matrix  # [B, D]
+                vorig = None if Vn is None else Vn @ (ds.matrix ** 2)
+            else:
+                orig, vorig = Wn, Vn
+            b_idx, f_idx = np.nonzero(orig)
+            keys = ents[b_idx].astype(np.int64) * ds.dim + f_idx
+            vals = orig[b_idx, f_idx]
+            vv = None if vorig is None else vorig[b_idx, f_idx]
+        nz = vals != 0
+        return keys[nz], vals[nz], (None if vv is None else vv[nz])
+
+    def score(self, model: RandomEffectModel) -> torch.Tensor:
+        return model.score(self.data, self.device, mask=self.dataset.score_mask).to(torch.float64)
+
+    def regularization_term_value(self, model: RandomEffectModel) -> float:
+        reg, lam = self.opt_config.regularization_context, self.opt_config.regularization_weight
+        v = model.values
+        return reg.l1_weight(lam) * float(np.abs(v).sum()) + 0.5 * reg.l2_weight(lam) * float((v * v).sum())

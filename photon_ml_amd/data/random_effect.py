@@ -1,0 +1,307 @@
+"""Random-effect datasets: entity grouping, active/passive split, reservoir cap, Pearson feature selection,
+projection, and the bucketed dense layout consumed by the batched solvers.
+
+Reference: ``photon-api/.../data/RandomEffectDataSet.scala`` (active data via groupByKey or the reservoir cap
+``326-389``; passive data ``402-447``; feature selection ``458-476``), ``LocalDataSet.scala`` (Pearson scores
+``221-280``), ``RandomEffectDataSetPartitioner.scala`` (entity -> partition bin packing) and
+``data/CoordinateDataConfiguration.scala`` (``RandomEffectDataConfiguration``).
+
+MI355X-first layout: entities are sorted by (active rows, projected dim) and packed into BUCKETS of similar
+shape; each bucket is one dense zero-padded tensor ``X [B, n_max, d_max]`` resident on the device plus the
+sample index of every slot, so the per-update residual routing (C11) is a single gather of the N-length offset
+vector and the per-entity solves are batched (``optimization/batched.py``). Multi-GPU entity sharding uses the
+same greedy least-loaded bin packing as the reference partitioner (``parallel/sharding.py``).
+"""
+from __future__ import annotations
+
+import math
+from dataclasses import dataclass, field
+from typing import List, Optional
+
+import numpy as np
+import scipy.sparse as sp
+import torch
+
+from ..constants import EPSILON
+from ..projector.projectors import (IndexMapProjection, ProjectorKind, ProjectorType, gaussian_projection_matrix)
+from .game_data import GameData
+
+
+@dataclass
+class RandomEffectDataConfiguration:
+    random_effect_type: str
+    feature_shard_id: str
+    min_partitions: int = 1
+    active_data_upper_bound: Optional[int] = None
+    passive_data_lower_bound: Optional[int] = None
+    features_to_samples_ratio: Optional[float] = None
+    projector_type: ProjectorType = field(default_factory=lambda: ProjectorType())
+
+    def __post_init__(self):
+        self.projector_type = ProjectorType.parse(self.projector_type)
+        if self.active_data_upper_bound is not None and self.active_data_upper_bound <= 0:
+            raise ValueError("active data upper bound must be positive")
+        if self.passive_data_lower_bound is not None and self.passive_data_lower_bound < 0:
+            raise ValueError("passive data lower bound must be non-negative")
+        if self.features_to_samples_ratio is not None and self.features_to_samples_ratio <= 0:
+            raise ValueError("features to samples ratio must be positive")
+
+
+@dataclass
+class FixedEffectDataConfiguration:
+    feature_shard_id: str
+    min_partitions: int = 1
+
+
+# ----------------------------------------------------------------------------------------------------------------
+# Reservoir key (RandomEffectDataSet.scala:361-367): (byteswap64(reType.hashCode) ^ byteswap64(uid)).hashCode()
+def java_string_hash(s: str) -> int:
+    h = 0
+    for ch in s:
+        h = (31 * h + ord(ch)) & 0xFFFFFFFF
+    return h - (1 << 32) if h >= (1 << 31) else h
+
+
+def _byteswap64(v: np.ndarray) -> np.ndarray:
+    return v.astype(np.uint64).byteswap()
+
+
+def reservoir_keys(re_type: str, uids: np.ndarray) -> np.ndarray:
+    t = np.array([java_string_hash(re_type)], dtype=np.int64).astype(np.uint64)
+    x = _byteswap64(t) ^ _byteswap64(uids.astype(np.int64).astype(np.uint64))
+    h = (x ^ (x >> np.uint64(32))) & np.uint64(0xFFFFFFFF)
+    return h.astype(np.int64) - ((h >= (1 << 31)).astype(np.int64) << 32)
+
+
+def pearson_scores(xe: sp.csr_matrix, y: np.ndarray) -> dict:
+    """LocalDataSet.computePearsonCorrelationScore for one entity's rows (first near-constant feature -> 1)."""
+    n = xe.shape[0]
+    coo = xe.tocoo()
+    feats = np.unique(coo.col)
+    s1 = np.bincount(coo.col, weights=coo.data, minlength=xe.shape[1])
+    s2 = np.bincount(coo.col, weights=coo.data ** 2, minlength=xe.shape[1])
+    sxy = np.bincount(coo.col, weights=coo.data * y[coo.row], minlength=xe.shape[1])
+    ly, ly2 = y.sum(), (y * y).sum()
+    out = {}
+    intercept_added = False
+    for j in feats:
+        num = n * sxy[j] - s1[j] * ly
+        std = math.sqrt(abs(n * s2[j] - s1[j] * s1[j]))
+        den = std * math.sqrt(max(n * ly2 - ly * ly, 0.0))
+        if std < EPSILON:
+            score = 0.0 if intercept_added else 1.0
+            intercept_added = True
+        else:
+            score = num / (den + EPSILON)
+        out[int(j)] = score
+    return out
+
+
+@dataclass
+class Bucket:
+    entities: np.ndarray      # entity indices in this bucket [B]
+    rows: torch.Tensor        # [B, n] global sample index of each slot, -1 for padding
+    X: torch.Tensor           # [B, n, d] projected features
+    y: torch.Tensor           # [B, n]
+    w: torch.Tensor           # [B, n] (0 on padding, x reservoir multiplier)
+    d_local: np.ndarray       # projected dim per entity
+
+
+class RandomEffectDataset:
+    """Active/passive data of one random-effect coordinate, projected and bucketed."""
+
+    def __init__(self, data: GameData, config: RandomEffectDataConfiguration, device="cpu",
+                 dtype=torch.float64, bucket_elems: int = 1 << 24, entity_subset: Optional[np.ndarray] = None):
+        self.config = config
+        self.device = torch.device(device)
+        self.dtype = dtype
+        re_type, shard_id = config.random_effect_type, config.feature_shard_id
+        x = data.shard(shard_id)
+        self.dim = x.shape[1]
+        ids = data.id_tags[re_type]
+        ids_s = ids.astype(str) if ids.dtype == object else ids
+        self.entity_ids, ent = np.unique(ids_s, return_inverse=True)
+        n_ent = len(self.entity_ids)
+        n = data.n_rows
+        self.n_rows = n
+        self.sample_entity = ent.astype(np.int64)
+        rows = np.arange(n, dtype=np.int64)
+        if entity_subset is not None:  # entity sharding across ranks: keep only owned entities
+            own = np.zeros(n_ent, dtype=bool)
+            own[entity_subset] = True
+            rows = rows[own[ent]]
+        # ---- active data (optionally reservoir-capped)
+        weight_mult = np.ones(n)
+        counts = np.bincount(ent[rows], minlength=n_ent)
+        cap = config.active_data_upper_bound
+        if cap is not None:
+            key = reservoir_keys(re_type, data.uids[rows])
+            order = np.lexsort((-key, ent[rows]))  # by entity, key descending
+            r_sorted = rows[order]
+            e_sorted = ent[r_sorted]
+            start = np.searchsorted(e_sorted, e_sorted, side="left")
+            rank = np.arange(len(r_sorted)) - start
+            keep = rank < cap
+            active_rows = np.sort(r_sorted[keep])
+            kept = np.minimum(counts, cap)
+            mult = np.where(kept > 0, counts / np.maximum(kept, 1), 1.0)
+            weight_mult[active_rows] = mult[ent[active_rows]]
+        else:
+            active_rows = rows
+        self.active_rows = active_rows
+        self.weight_mult = weight_mult
+        # ---- passive data
+        passive_rows = np.zeros(0, dtype=np.int64)
+        if config.passive_data_lower_bound is not None:
+            is_active = np.zeros(n, dtype=bool)
+            is_active[active_rows] = True
+            cand = rows[~is_active[rows]]
+            pcount = np.bincount(ent[cand], minlength=n_ent)
+            passive_rows = cand[pcount[ent[cand]] > config.passive_data_lower_bound]
+        self.passive_rows = passive_rows
+        self.score_mask = np.zeros(n, dtype=bool)
+        self.score_mask[active_rows] = True
+        self.score_mask[passive_rows] = True
+        # ---- feature selection (Pearson) on active rows
+        xa = x[active_rows]
+        ea = ent[active_rows]
+        self.feature_keep = None
+        if config.features_to_samples_ratio is not None:
+            xa = self._pearson_filter(xa, ea, data.response[active_rows], config.features_to_samples_ratio)
+        self.x_active = xa
+        # ---- projection
+        pt = config.projector_type
+        self.projector_type = pt
+        if pt.kind == ProjectorKind.INDEX_MAP:
+            coo = xa.tocoo()
+            e_all = ea[coo.row]
+            f_all = coo.col
+            if len(passive_rows):
+                cp = x[passive_rows].tocoo()
+                e_all = np.concatenate([e_all, ent[passive_rows][cp.row]])
+                f_all = np.concatenate([f_all, cp.col])
+            self.projection = IndexMapProjection.build(e_all, f_all, n_ent, self.dim)
+            d_local = self.projection.local_dims()
+        elif pt.kind == ProjectorKind.RANDOM:
+            self.matrix = gaussian_projection_matrix(pt.projected_dim, self.dim, keep_intercept=True)
+            d_local = np.full(n_ent, self.matrix.shape[0], dtype=np.int64)
+        else:
+            d_local = np.full(n_ent, self.dim, dtype=np.int64)
+        self.d_local = d_local
+        # ---- buckets
+        n_act = np.bincount(ea, minlength=n_ent)
+        self.n_active = n_act
+        self.buckets = self._make_buckets(xa, ea, active_rows, data.response, weight_mult * data.weights,
+                                          n_act, d_local, bucket_elems)
+
+    # ------------------------------------------------------------------
+    def _pearson_filter(self, xa: sp.csr_matrix, ea: np.ndarray, y: np.ndarray, ratio: float) -> sp.csr_matrix:
+        xa = xa.tocsr()
+        order = np.argsort(ea, kind="stable")
+        keep_mask_rows = []
+        out_rows, out_cols, out_vals = [], [], []
+        starts = np.searchsorted(ea[order], np.arange(ea.max() + 2 if len(ea) else 1))
+        xa_coo = xa.tocoo()
+        keep_entry = np.ones(xa.nnz, dtype=bool)
+        row_ent = ea
+        # per entity: compute scores over its rows, keep top-k features
+        by_ent = {}
+        for e in np.unique(ea):
+            r = order[starts[e]:starts[e + 1]]
+            xe = xa[r]
+            k = int(math.ceil(ratio * len(r)))
+            n_feat = len(np.unique(xe.indices))
+            if k >= n_feat:
+                continue
+            scores = pearson_scores(xe, y[r])
+            ranked = sorted(scores.items(), key=lambda kv: abs(kv[1]))
+            keep = {f for f, _ in ranked[-k:]}
+            by_ent[e] = keep
+        if not by_ent:
+            return xa
+        ent_of_entry = row_ent[xa_coo.row]
+        for e, keep in by_ent.items():
+            m = ent_of_entry == e
+            keep_entry[m] = np.isin(xa_coo.col[m], np.fromiter(keep, dtype=np.int64))
+        return sp.csr_matrix((xa_coo.data[keep_entry], (xa_coo.row[keep_entry], xa_coo.col[keep_entry])),
+                             shape=xa.shape)
+
+    def _project_rows(self, xr: sp.csr_matrix, er: np.ndarray):
+        """Return (row_idx, local_col, value) triplets of rows ``xr`` of entities ``er`` in projected space."""
+        pt = self.projector_type
+        if pt.kind == ProjectorKind.INDEX_MAP:
+            coo = xr.tocoo()
+            lc = self.projection.local_index(er[coo.row], coo.col)
+            ok = lc >= 0
+            return coo.row[ok], lc[ok], coo.data[ok]
+        if pt.kind == ProjectorKind.RANDOM:
+            dense = np.asarray(xr @ self.matrix.T)
+            r, c = np.nonzero(dense)
+            return r, c, dense[r, c]
+        coo = xr.tocoo()
+        return coo.row, coo.col, coo.data
+
+    def _make_buckets(self, xa, ea, active_rows, y, wts, n_act, d_local, budget) -> List[Bucket]:
+        n_ent = len(n_act)
+        ents = np.nonzero(n_act > 0)[0]
+        order = ents[np.lexsort((d_local[ents], n_act[ents]))]
+        buckets_e: List[List[int]] = []
+        cur: List[int] = []
+        n0 = d0 = nm = dm = 0
+        for e in order:
+            ne, de = int(n_act[e]), max(int(d_local[e]), 1)
+            if cur:
+                nm2, dm2 = max(nm, ne), max(dm, de)
+                if ((len(cur) + 1) * nm2 * dm2 > budget) or nm2 > 2 * n0 + 8 or dm2 > 2 * d0 + 8:
+                    buckets_e.append(cur)
+                    cur = []
+            if not cur:
+                n0, d0, nm, dm = ne, de, ne, de
+            nm, dm = max(nm, ne), max(dm, de)
+            cur.append(e)
+        if cur:
+            buckets_e.append(cur)
+        # rows of each entity (active), in sample order
+        ord_rows = np.argsort(ea, kind="stable")
+        starts = np.zeros(n_ent + 1, dtype=np.int64)
+        starts[1:] = np.cumsum(n_act)
+        out = []
+        for be in buckets_e:
+            be = np.asarray(be, dtype=np.int64)
+            B = len(be)
+            nmax = int(n_act[be].max())
+            dmax = max(int(d_local[be].max()), 1)
+            loc_rows = np.concatenate([ord_rows[starts[e]:starts[e + 1]] for e in be])  # into active arrays
+            slot_b = np.repeat(np.arange(B), n_act[be])
+            slot_r = np.concatenate([np.arange(n_act[e]) for e in be])
+            xr = xa[loc_rows]
+            rr, cc, vv = self._project_rows(xr, ea[loc_rows])
+            X = np.zeros((B, nmax, dmax))
+            X[slot_b[rr], slot_r[rr], cc] = vv
+            rows = np.full((B, nmax), -1, dtype=np.int64)
+            rows[slot_b, slot_r] = active_rows[loc_rows]
+            Y = np.zeros((B, nmax))
+            Y[slot_b, slot_r] = y[active_rows[loc_rows]]
+            W = np.zeros((B, nmax))
+            W[slot_b, slot_r] = wts[active_rows[loc_rows]]
+            dev, dt = self.device, self.dtype
+            out.append(Bucket(be, torch.from_numpy(rows).to(dev), torch.from_numpy(X).to(dev, dt),
+                              torch.from_numpy(Y).to(dev, dt), torch.from_numpy(W).to(dev, dt), d_local[be]))
+        return out
+
+    @property
+    def n_entities(self) -> int:
+        return len(self.entity_ids)
+
+    def bucket_offsets(self, bucket: Bucket, offsets: torch.Tensor) -> torch.Tensor:
+        """Gather per-slot offsets (C11 residual routing): offsets is the N-length vector on the device."""
+        r = bucket.rows.clamp(min=0)
+        o = offsets.to(self.device, self.dtype)[r]
+        return torch.where(bucket.rows >= 0, o, torch.zeros_like(o))
+
+    def summary(self) -> str:
+        d = self.d_local[self.n_active > 0]
+        return (f"RandomEffectDataset(type={self.config.random_effect_type}, shard={self.config.feature_shard_id},"
+                f" entities={self.n_entities}, active rows={len(self.active_rows)}, passive rows="
+                f"{len(self.passive_rows)}, buckets={len(self.buckets)}, mean projected dim="
+                f"{float(d.mean()) if len(d) else 0:.1f})")

@@ -1,0 +1,156 @@
+"""GAME models: fixed-effect model, random-effect model, GameModel.
+
+Reference: ``photon-api/.../model/FixedEffectModel.scala:31-145`` (broadcast GLM + shard id, scoring = dot
+product), ``RandomEffectModel.scala:38-298`` (RDD of per-entity GLMs; scoring is a partitioned hash join),
+``photon-lib/.../model/GameModel.scala:32-170`` (coordinate -> model map, a single task type enforced) and
+``DatumScoringModel.scala``.
+
+Random-effect models are stored entity-major in the ORIGINAL feature space as one sorted key array
+``key = entity_index * D + feature`` with values (and optional variances) — a CSR over entities. Scoring any
+dataset (K6) is then one vectorised ``searchsorted`` of the sample non-zeros' keys, executed on the device; no
+per-entity Python objects, no joins.
+"""
+from __future__ import annotations
+
+from collections import OrderedDict
+from typing import Dict, Iterable, Optional
+
+import numpy as np
+import scipy.sparse as sp
+import torch
+
+from ..constants import TaskType
+from .glm import Coefficients, GeneralizedLinearModel, model_for_task
+
+
+def _csr_to_torch(x: sp.csr_matrix, device):
+    coo = x.tocoo()
+    return (torch.from_numpy(coo.row.astype(np.int64)).to(device), torch.from_numpy(coo.col.astype(np.int64)).to(device),
+            torch.from_numpy(coo.data.astype(np.float64)).to(device))
+
+
+class FixedEffectModel:
+    def __init__(self, glm: GeneralizedLinearModel, feature_shard_id: str):
+        self.glm = glm
+        self.feature_shard_id = feature_shard_id
+
+    @property
+    def task(self) -> TaskType:
+        return self.glm.task
+
+    def score(self, data, device="cpu") -> torch.Tensor:
+        x = data.shard(self.feature_shard_id)
+        w = self.glm.coefficients.means.cpu().numpy()
+        if x.shape[1] != len(w):
+            raise ValueError(f"shard {self.feature_shard_id} dim {x.shape[1]} != model dim {len(w)}")
+        return torch.from_numpy(np.asarray(x @ w).reshape(-1)).to(device)
+
+    def __repr__(self):
+        return f"FixedEffectModel(shard={self.feature_shard_id}, dim={self.glm.coefficients.dim})"
+
+
+class RandomEffectModel:
+    def __init__(self, random_effect_type: str, feature_shard_id: str, task: TaskType, entity_ids: np.ndarray,
+                 dim: int, keys: np.ndarray, values: np.ndarray, variances: Optional[np.ndarray] = None):
+        self.random_effect_type = random_effect_type
+        self.feature_shard_id = feature_shard_id
+        self._task = TaskType.parse(task)
+        self.entity_ids = np.asarray(entity_ids)
+        self.dim = int(dim)
+        order = np.argsort(keys, kind="stable")
+        self.keys = np.asarray(keys, dtype=np.int64)[order]
+        self.values = np.asarray(values, dtype=np.float64)[order]
+        self.variances = None if variances is None else np.asarray(variances, dtype=np.float64)[order]
+
+    @property
+    def task(self) -> TaskType:
+        return self._task
+
+    @property
+    def n_entities(self) -> int:
+        return len(self.entity_ids)
+
+    def entity_index(self, ids: np.ndarray) -> np.ndarray:
+        ids = np.asarray(ids)
+        ids_s = ids.astype(str) if ids.dtype == object else ids
+        ent = self.entity_ids
+        pos = np.searchsorted(ent, ids_s)
+        pos_c = np.minimum(pos, max(len(ent) - 1, 0))
+        ok = (pos < len(ent)) & (ent[pos_c] == ids_s) if len(ent) else np.zeros(len(ids_s), bool)
+        return np.where(ok, pos, -1)
+
+    def coefficients_of(self, entity_id) -> Coefficients:
+        e = int(self.entity_index(np.array([entity_id]))[0])
+        if e < 0:
+            raise KeyError(entity_id)
+        lo, hi = np.searchsorted(self.keys, [e * self.dim, (e + 1) * self.dim])
+        means = np.zeros(self.dim)
+        means[self.keys[lo:hi] - e * self.dim] = self.values[lo:hi]
+        var = None
+        if self.variances is not None:
+            var = np.zeros(self.dim)
+            var[self.keys[lo:hi] - e * self.dim] = self.variances[lo:hi]
+        return Coefficients(torch.from_numpy(means), None if var is None else torch.from_numpy(var))
+
+    def models(self) -> Iterable:
+        """Yield (entity_id, GLM) pairs (for IO / inspection)."""
+        for i, eid in enumerate(self.entity_ids):
+            yield eid, model_for_task(self._task, self.coefficients_of(eid))
+
+    def score(self, data, device="cpu", mask: Optional[np.ndarray] = None) -> torch.Tensor:
+        """Score every sample whose entity has a model (K6): sum_j x_ij * w_{e(i), j}."""
+        x = data.shard(self.feature_shard_id)
+        n = x.shape[0]
+        ent = self.entity_index(data.id_tags[self.random_effect_type])
+        if mask is not None:
+            ent = np.where(mask, ent, -1)
+        dev = torch.device(device)
+        row, col, val = _csr_to_torch(x, dev)
+        ent_t = torch.from_numpy(ent).to(dev)
+        e = ent_t[row]
+        keys = torch.from_numpy(self.keys).to(dev)
+        vals = torch.from_numpy(self.values).to(dev)
+        out = torch.zeros(n, dtype=torch.float64, device=dev)
+        if keys.numel() == 0 or row.numel() == 0:
+            return out
+        k = e * self.dim + col
+        pos = torch.searchsorted(keys, k).clamp(max=keys.numel() - 1)
+        hit = (keys[pos] == k) & (e >= 0)
+        contrib = torch.where(hit, val * vals[pos], torch.zeros_like(val))
+        return out.index_add_(0, row, contrib)
+
+    def __repr__(self):
+        return (f"RandomEffectModel(type={self.random_effect_type}, shard={self.feature_shard_id}, "
+                f"entities={self.n_entities}, nnz={len(self.keys)})")
+
+
+class GameModel:
+    """Ordered map coordinate id -> model; all sub-models must share one task type."""
+
+    def __init__(self, models: "OrderedDict[str, object]"):
+        self.models = OrderedDict(models)
+        tasks = {m.task for m in self.models.values()}
+        if len(tasks) > 1:
+            raise ValueError(f"GameModel sub-models have different task types: {tasks}")
+        self.task = tasks.pop() if tasks else TaskType.NONE
+
+    def get(self, coordinate_id: str):
+        return self.models.get(coordinate_id)
+
+    def updated(self, coordinate_id: str, model) -> "GameModel":
+        m = OrderedDict(self.models)
+        m[coordinate_id] = model
+        return GameModel(m)
+
+    def score(self, data, device="cpu") -> torch.Tensor:
+        """Sum of every coordinate's scores (no offsets)."""
+        total = torch.zeros(data.n_rows, dtype=torch.float64, device=device)
+        for m in self.models.values():
+            total = total + m.score(data, device)
+        return total
+
+    def __iter__(self):
+        return iter(self.models.items())
+
+    def __repr__(self):
+        return "GameModel(" + ", ".join(f"{k}: {v}" for k, v in self.models.items()) + ")"

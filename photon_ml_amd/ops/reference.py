@@ -107,3 +107,9 @@ class TorchGLMData(GLMComputable):
         z = self._xv(w_eff) + margin_shift + self.o
         l, _ = loss.loss_and_dz(z, self.y)
         return l
+
+    def set_offsets(self, offsets):
+        self.o = torch.as_tensor(offsets, dtype=torch.float64).to(self.device)
+
+    def set_weights(self, weights):
+        self.wt = torch.as_tensor(weights, dtype=torch.float64).to(self.device)

@@ -1,0 +1,121 @@
+"""GAME (fixed + random effects, coordinate descent) tests on CPU.
+
+Mirrors photon-api/src/integTest/.../algorithm/*, model/*, data/RandomEffectDataSet tests and the CoordinateDescent
+unit tests (photon-lib/src/test/.../algorithm/CoordinateDescentTest.scala)."""
+from collections import OrderedDict
+
+import numpy as np
+import pytest
+import torch
+
+from photon_ml_amd.algorithm.coordinate_descent import CoordinateDescent
+from photon_ml_amd.algorithm.coordinates import FixedEffectCoordinate, RandomEffectCoordinate
+from photon_ml_amd.data.game_data import generate_game_data
+from photon_ml_amd.data.random_effect import (FixedEffectDataConfiguration, RandomEffectDataConfiguration,
+                                              RandomEffectDataset, reservoir_keys, java_string_hash)
+from photon_ml_amd.evaluation.evaluators import build_evaluator
+from photon_ml_amd.optimization.config import (GLMOptimizationConfiguration, OptimizerConfig, RegularizationContext)
+from photon_ml_amd.projector import RandomProjection
+
+
+def _cfg(opt="TRON", lam=1.0, it=30, tol=1e-8, reg="L2"):
+    return GLMOptimizationConfiguration(OptimizerConfig(opt, it, tol), RegularizationContext(reg), lam)
+
+
+def _coords(data, task="LINEAR_REGRESSION", re_opt="TRON"):
+    return OrderedDict([
+        ("global", FixedEffectCoordinate("global", data, FixedEffectDataConfiguration("global"), _cfg(), task,
+                                         device="cpu")),
+        ("per-user", RandomEffectCoordinate("per-user", data, RandomEffectDataConfiguration("userId", "user"),
+                                            _cfg(re_opt), task, device="cpu")),
+        ("per-item", RandomEffectCoordinate("per-item", data, RandomEffectDataConfiguration("itemId", "item"),
+                                            _cfg(re_opt), task, device="cpu")),
+    ])
+
+
+def test_java_hash_and_reservoir_keys():
+    assert java_string_hash("userId") == -836030906
+    assert java_string_hash("") == 0
+    k = reservoir_keys("userId", np.array([0, 1, 2, 12345678901]))
+    assert k.dtype == np.int64 and len(set(k.tolist())) == 4
+
+
+def test_game_linear_mixed_effects_improves_rmse():
+    data, _ = generate_game_data(n_rows=3000, seed=3)
+    val, _ = generate_game_data(n_rows=3000, seed=3)
+    coords = _coords(data)
+    rmse = build_evaluator("RMSE", val.response, val.offsets, val.weights)
+    cd = CoordinateDescent(coords, build_evaluator("SQUARED_LOSS", data.response), val, [rmse])
+    model, evals = cd.run(2)
+    fe_only = CoordinateDescent(OrderedDict([("global", coords["global"])]), None, val, [rmse])
+    _, evals_fe = fe_only.run(1)
+    assert evals[0][1] < 0.8 * evals_fe[0][1], (evals, evals_fe)
+    # training loss monotone over coordinate updates
+    losses = [h["training_loss"] for h in cd.history]
+    assert all(b <= a * (1 + 1e-9) for a, b in zip(losses, losses[1:]))
+
+
+def test_single_coordinate_matches_glm():
+    data, _ = generate_game_data(n_rows=1500, seed=4, task="LOGISTIC_REGRESSION")
+    coord = FixedEffectCoordinate("g", data, FixedEffectDataConfiguration("global"), _cfg("LBFGS", 1.0, 100, 1e-10),
+                                  "LOGISTIC_REGRESSION", device="cpu")
+    model, _ = CoordinateDescent(OrderedDict(g=coord)).run(1)
+    from photon_ml_amd.function.losses import LOGISTIC
+    from photon_ml_amd.function.objective import GLMObjective
+    from photon_ml_amd.ops.reference import TorchGLMData
+    from photon_ml_amd.optimization import LBFGS
+    w, _ = LBFGS(tolerance=1e-10).optimize(GLMObjective(LOGISTIC, 1.0), TorchGLMData(data.labeled("global")),
+                                           torch.zeros(data.shards["global"].shape[1], dtype=torch.float64))
+    assert torch.allclose(model.get("g").glm.coefficients.means, w, atol=1e-6)
+
+
+@pytest.mark.parametrize("re_opt,reg", [("LBFGS", "L2"), ("LBFGS", "L1"), ("TRON", "L2")])
+def test_random_effect_matches_per_entity_solves(re_opt, reg):
+    data, _ = generate_game_data(n_rows=800, n_users=12, seed=5, task="LOGISTIC_REGRESSION")
+    cfg = _cfg(re_opt, 0.5, 200, 1e-12, reg)
+    coord = RandomEffectCoordinate("u", data, RandomEffectDataConfiguration("userId", "user"), cfg,
+                                   "LOGISTIC_REGRESSION", device="cpu")
+    m = coord.update_model(coord.initialize_model())
+    from photon_ml_amd.data.matrix import LabeledData
+    from photon_ml_amd.function.losses import LOGISTIC
+    from photon_ml_amd.function.objective import GLMObjective
+    from photon_ml_amd.ops.reference import TorchGLMData
+    from photon_ml_amd.optimization import LBFGS, OWLQN
+    x = data.shards["user"]
+    for eid in m.entity_ids[:5]:
+        rows = np.nonzero(data.id_tags["userId"] == eid)[0]
+        ld = LabeledData(x[rows], data.response[rows])
+        if reg == "L1":
+            opt, obj = OWLQN(0.5, tolerance=1e-12, max_iterations=300), GLMObjective(LOGISTIC, 0.0)
+        else:
+            opt, obj = LBFGS(tolerance=1e-12, max_iterations=300), GLMObjective(LOGISTIC, 0.5)
+        w, _ = opt.optimize(obj, TorchGLMData(ld), torch.zeros(x.shape[1], dtype=torch.float64))
+        got = m.coefficients_of(eid).means
+        assert torch.allclose(got, w, atol=2e-4), (eid, got, w)
+
+
+def test_reservoir_cap_and_passive_data():
+    data, _ = generate_game_data(n_rows=2000, n_users=10, seed=6)
+    cfg = RandomEffectDataConfiguration("userId", "user", active_data_upper_bound=20, passive_data_lower_bound=5)
+    ds = RandomEffectDataset(data, cfg)
+    assert ds.n_active.max() <= 20
+    counts = np.bincount(ds.sample_entity, minlength=ds.n_entities)
+    capped = counts > 20
+    # weights of capped entities multiplied by count/cap
+    for b in ds.buckets:
+        for i, e in enumerate(b.entities):
+            if capped[e]:
+                w = b.w[i][b.rows[i] >= 0]
+                assert torch.allclose(w, torch.full_like(w, counts[e] / 20))
+    assert len(ds.passive_rows) > 0
+    assert not np.intersect1d(ds.passive_rows, ds.active_rows).size
+
+
+def test_random_projection_and_feature_selection_run():
+    data, _ = generate_game_data(n_rows=1000, n_users=8, d_user=12, seed=7)
+    for cfg in (RandomEffectDataConfiguration("userId", "user", projector_type=RandomProjection(4)),
+                RandomEffectDataConfiguration("userId", "user", features_to_samples_ratio=0.05)):
+        coord = RandomEffectCoordinate("u", data, cfg, _cfg("TRON"), "LINEAR_REGRESSION", device="cpu")
+        m = coord.update_model(coord.initialize_model())
+        s = coord.score(m)
+        assert torch.isfinite(s).all() and float(s.abs().sum()) > 0
