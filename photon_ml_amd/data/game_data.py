@@ -25,6 +25,7 @@ class GameData:
     offsets: Optional[np.ndarray] = None
     weights: Optional[np.ndarray] = None
     uids: Optional[np.ndarray] = None
+    raw_uids: Optional[np.ndarray] = None  # original (string) uids from the input records, for score output
 
     def __post_init__(self):
         n = len(self.response)
@@ -55,7 +56,7 @@ class GameData:
         rows = np.asarray(rows)
         return GameData(self.response[rows], {k: v[rows] for k, v in self.shards.items()},
                         {k: v[rows] for k, v in self.id_tags.items()}, self.offsets[rows], self.weights[rows],
-                        self.uids[rows])
+                        self.uids[rows], None if self.raw_uids is None else self.raw_uids[rows])
 
 
 def generate_game_data(n_rows: int = 2000, n_users: int = 50, n_items: int = 30, d_global: int = 20,

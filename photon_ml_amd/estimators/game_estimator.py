@@ -1,0 +1,216 @@
+"""Estimator API: GameEstimator (fit), GameTransformer (score), and the legacy GLM lambda-path trainer.
+
+Reference:
+  * ``photon-api/.../estimators/GameEstimator.scala:56-753`` — params (training task, input column names,
+    coordinate data configurations, update sequence, CD iterations (default 1), normalization contexts,
+    compute variance (false), tree aggregate depth (1), validation evaluators, warm start (true)); ``fit`` trains
+    one GAME model per optimisation configuration in sequence, warm-starting from the previous one.
+  * ``photon-api/.../transformers/GameTransformer.scala:38-308`` — score a dataset with a GameModel, optionally
+    evaluate.
+  * ``photon-api/.../ModelTraining.scala:35-234`` — legacy GLM training over a lambda grid sorted DESCENDING,
+    each lambda warm-started from the previous model.
+
+Datasets are built ONCE per ``fit`` (device-resident shards / buckets) and reused across configurations; a new
+configuration only swaps the optimisation problem of each coordinate.
+"""
+from __future__ import annotations
+
+import logging
+from collections import OrderedDict
+from dataclasses import dataclass
+from typing import Dict, List, Optional, Sequence, Tuple
+
+import numpy as np
+import torch
+
+from ..algorithm.coordinate_descent import CoordinateDescent
+from ..algorithm.coordinates import FixedEffectCoordinate, RandomEffectCoordinate
+from ..constants import TaskType
+from ..data.game_data import GameData
+from ..data.matrix import LabeledData
+from ..data.random_effect import FixedEffectDataConfiguration, RandomEffectDataConfiguration
+from ..evaluation.evaluators import (build_evaluator, default_validation_evaluator, parse_evaluator_type,
+                                     training_loss_evaluator_type)
+from ..models.game import GameModel
+from ..normalization.context import NormalizationContext, NormalizationType
+from ..ops.backend import default_device, make_glm_data
+from ..optimization.config import (GLMOptimizationConfiguration, OptimizerConfig, OptimizerType,
+                                   RegularizationContext)
+from ..optimization.problem import GLMOptimizationProblem
+from ..parallel.dist import DistributedGLMData, is_dist
+from ..stat.summary import BasicStatisticalSummary
+
+log = logging.getLogger(__name__)
+
+DEFAULT_TREE_AGGREGATE_DEPTH = 1
+
+
+@dataclass
+class GameResult:
+    model: GameModel
+    evaluations: Optional[list]
+    config: Dict[str, GLMOptimizationConfiguration]
+
+
+class GameEstimator:
+    def __init__(self, device=None, precision: str = "f64"):
+        self.training_task: Optional[TaskType] = None
+        self.coordinate_data_configurations: "OrderedDict[str, object]" = OrderedDict()
+        self.coordinate_update_sequence: Optional[List[str]] = None
+        self.coordinate_descent_iterations = 1
+        self.coordinate_normalization_contexts: Dict[str, NormalizationContext] = {}
+        self.compute_variance = False
+        self.tree_aggregate_depth = DEFAULT_TREE_AGGREGATE_DEPTH
+        self.validation_evaluators: Optional[List[str]] = None
+        self.use_warm_start = True
+        self.device = torch.device(device) if device is not None else default_device()
+        self.precision = precision
+        self.event_callback = None
+        self.coordinates = None
+        self.history: List[list] = []
+
+    # fluent setters mirroring Spark ML Params ------------------------------------------------------------
+    def set_training_task(self, t):
+        self.training_task = TaskType.parse(t)
+        return self
+
+    def set_coordinate_data_configurations(self, cfgs):
+        self.coordinate_data_configurations = OrderedDict(cfgs)
+        return self
+
+    def set_coordinate_update_sequence(self, seq):
+        self.coordinate_update_sequence = list(seq)
+        return self
+
+    def set_coordinate_descent_iterations(self, n: int):
+        if n <= 0:
+            raise ValueError("coordinate descent iterations must be > 0")
+        self.coordinate_descent_iterations = n
+        return self
+
+    def set_coordinate_normalization_contexts(self, ctxs):
+        self.coordinate_normalization_contexts = dict(ctxs)
+        return self
+
+    def set_compute_variance(self, b: bool):
+        self.compute_variance = bool(b)
+        return self
+
+    def set_tree_aggregate_depth(self, d: int):
+        if d <= 0:
+            raise ValueError("tree aggregate depth must be > 0")
+        self.tree_aggregate_depth = d  # RCCL chooses ring/tree itself; kept for API parity
+        return self
+
+    def set_validation_evaluators(self, evs):
+        self.validation_evaluators = [e if isinstance(e, str) else e.name for e in evs]
+        return self
+
+    def set_warm_start(self, b: bool):
+        self.use_warm_start = bool(b)
+        return self
+
+    # ----------------------------------------------------------------------------------------------------
+    def validate_params(self):
+        if self.training_task is None:
+            raise ValueError("training task is required")
+        if not self.coordinate_data_configurations:
+            raise ValueError("coordinate data configurations are required")
+        seq = self.coordinate_update_sequence or list(self.coordinate_data_configurations)
+        missing = [c for c in seq if c not in self.coordinate_data_configurations]
+        if missing:
+            raise ValueError(f"coordinates {missing} in the update sequence have no data configuration")
+        return seq
+
+    def _build_coordinates(self, data: GameData, first_cfg: Dict[str, GLMOptimizationConfiguration], seq):
+        coords = OrderedDict()
+        for cid in seq:
+            dc = self.coordinate_data_configurations[cid]
+            oc = first_cfg[cid]
+            if isinstance(dc, RandomEffectDataConfiguration):
+                coords[cid] = RandomEffectCoordinate(cid, data, dc, oc, self.training_task, self.compute_variance,
+                                                     self.device)
+            else:
+                coords[cid] = FixedEffectCoordinate(cid, data, dc, oc, self.training_task,
+                                                    self.coordinate_normalization_contexts.get(cid),
+                                                    self.compute_variance, self.device, self.precision)
+        return coords
+
+    def _validation_evaluators(self, validation: GameData):
+        names = self.validation_evaluators or [default_validation_evaluator(self.training_task)]
+        return [build_evaluator(parse_evaluator_type(n), validation.response, validation.offsets, validation.weights,
+                                validation.id_tags) for n in names]
+
+    def fit(self, data: GameData, validation: Optional[GameData],
+            configurations: Sequence[Dict[str, GLMOptimizationConfiguration]]) -> List[GameResult]:
+        seq = self.validate_params()
+        if not configurations:
+            raise ValueError("at least one optimization configuration is required")
+        for cfg in configurations:
+            missing = [c for c in seq if c not in cfg]
+            if missing:
+                raise ValueError(f"optimization configuration missing coordinates {missing}")
+        self.coordinates = self._build_coordinates(data, configurations[0], seq)
+        train_eval = build_evaluator(training_loss_evaluator_type(self.training_task), data.response, data.offsets,
+                                     data.weights)
+        val_evals = self._validation_evaluators(validation) if validation is not None else []
+        results, prev = [], None
+        for cfg in configurations:
+            for cid, c in self.coordinates.items():
+                c.set_config(cfg[cid])
+            cd = CoordinateDescent(self.coordinates, train_eval, validation, val_evals,
+                                   event_callback=self.event_callback)
+            model, evals = cd.run(self.coordinate_descent_iterations, prev if self.use_warm_start else None)
+            self.history.append(cd.history)
+            results.append(GameResult(model, evals, cfg))
+            if self.use_warm_start:
+                prev = model
+        return results
+
+
+class GameTransformer:
+    def __init__(self, model: GameModel, validation_evaluators: Optional[Sequence[str]] = None, device="cpu"):
+        self.model = model
+        self.validation_evaluators = list(validation_evaluators or [])
+        self.device = device
+
+    def transform(self, data: GameData):
+        """Return (scores WITHOUT offsets, evaluations or None)."""
+        scores = self.model.score(data, self.device)
+        evals = None
+        if self.validation_evaluators:
+            evals = []
+            for n in self.validation_evaluators:
+                e = build_evaluator(parse_evaluator_type(n), data.response, data.offsets, data.weights, data.id_tags)
+                evals.append((e, e.evaluate(scores)))
+        return scores, evals
+
+
+# --------------------------------------------------------------------------------------------------------------
+def train_generalized_linear_model(data: LabeledData, task, optimizer_type="LBFGS",
+                                   regularization: RegularizationContext = RegularizationContext("L2"),
+                                   regularization_weights: Sequence[float] = (10.0,),
+                                   normalization: Optional[NormalizationContext] = None, max_iterations: int = 80,
+                                   tolerance: float = 1e-6, constraint_map=None, warm_start_models=None,
+                                   use_warm_start: bool = True, compute_variance: bool = False, device=None,
+                                   precision: str = "f64", glm_data=None):
+    """ModelTraining.trainGeneralizedLinearModel -> list of (lambda, model, tracker), lambdas DESCENDING."""
+    device = torch.device(device) if device is not None else default_device()
+    gdata = glm_data if glm_data is not None else make_glm_data(data, device, precision)
+    view = DistributedGLMData(gdata) if is_dist() else gdata
+    lams = sorted(regularization_weights, reverse=True)
+    out = []
+    prev = None
+    for lam in lams:
+        cfg = GLMOptimizationConfiguration(OptimizerConfig(optimizer_type, max_iterations, tolerance, constraint_map),
+                                           regularization, lam)
+        prob = GLMOptimizationProblem(cfg, task, normalization, compute_variance)
+        init = None
+        if warm_start_models and lam in warm_start_models:
+            init = warm_start_models[lam]
+        elif use_warm_start and prev is not None:
+            init = prev
+        model = prob.run(view, init, dim=gdata.dim)
+        out.append((lam, model, prob.tracker))
+        prev = model
+    return out

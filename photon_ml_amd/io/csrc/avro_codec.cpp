@@ -1,0 +1,844 @@
+// photon_ml_amd native Avro Object Container File codec (C++17, pybind11).
+//
+// Replaces the JVM Avro 1.7.7 stack the reference uses (photon-client/.../data/avro/{AvroUtils,AvroDataReader,
+// ModelProcessingUtils,ScoreProcessingUtils}.scala). Supports the full Avro binary encoding (null, boolean, int,
+// long, float, double, bytes, string, record, enum, array, map, union, fixed, named-type references with
+// namespaces), OCF containers with the "null", "deflate" (zlib raw) and "snappy" (own implementation + CRC32C
+// trailer) codecs, generic decode to Python objects, generic encode from Python objects, and a columnar fast path
+// for training data: records are decoded straight into numpy arrays (labels, weights, offsets, uids, id tags) and
+// one CSR triplet per feature bag with interned "name\u0001term" keys — no per-record Python objects.
+#include <pybind11/numpy.h>
+#include <pybind11/pybind11.h>
+#include <pybind11/stl.h>
+#include <zlib.h>
+
+#include <cmath>
+#include <cstdint>
+#include <cstring>
+#include <fstream>
+#include <map>
+#include <memory>
+#include <random>
+#include <sstream>
+#include <stdexcept>
+#include <string>
+#include <unordered_map>
+#include <vector>
+
+namespace py = pybind11;
+
+// ============================================================================================================
+// Minimal JSON (schemas / metadata only)
+// ============================================================================================================
+struct JVal {
+  enum T { NUL, BOOL, NUM, STR, ARR, OBJ } t = NUL;
+  bool b = false;
+  double num = 0;
+  std::string s;
+  std::vector<JVal> arr;
+  std::vector<std::pair<std::string, JVal>> obj;
+  const JVal* get(const std::string& k) const {
+    for (auto& kv : obj)
+      if (kv.first == k) return &kv.second;
+    return nullptr;
+  }
+};
+
+struct JParser {
+  const std::string& s;
+  size_t i = 0;
+  explicit JParser(const std::string& str) : s(str) {}
+  void ws() {
+    while (i < s.size() && isspace((unsigned char)s[i])) ++i;
+  }
+  [[noreturn]] void fail(const char* m) { throw std::runtime_error(std::string("JSON parse error: ") + m); }
+  std::string str() {
+    if (s[i] != '"') fail("expected string");
+    ++i;
+    std::string out;
+    while (i < s.size() && s[i] != '"') {
+      char c = s[i++];
+      if (c == '\\') {
+        char e = s[i++];
+        switch (e) {
+          case 'n': out += '\n'; break;
+          case 't': out += '\t'; break;
+          case 'r': out += '\r'; break;
+          case 'b': out += '\b'; break;
+          case 'f': out += '\f'; break;
+          case 'u': {
+            unsigned cp = std::stoul(s.substr(i, 4), nullptr, 16);
+            i += 4;
+            if (cp < 0x80) out += (char)cp;
+            else if (cp < 0x800) { out += (char)(0xC0 | (cp >> 6)); out += (char)(0x80 | (cp & 0x3F)); }
+            else { out += (char)(0xE0 | (cp >> 12)); out += (char)(0x80 | ((cp >> 6) & 0x3F)); out += (char)(0x80 | (cp & 0x3F)); }
+            break;
+          }
+          default: out += e;
+        }
+      } else {
+        out += c;
+      }
+    }
+    ++i;
+    return out;
+  }
+  JVal val() {
+    ws();
+    JVal v;
+    if (i >= s.size()) fail("eof");
+    char c = s[i];
+    if (c == '{') {
+      v.t = JVal::OBJ; ++i; ws();
+      if (s[i] == '}') { ++i; return v; }
+      while (true) {
+        ws(); std::string k = str(); ws();
+        if (s[i] != ':') fail("expected :");
+        ++i;
+        v.obj.emplace_back(k, val()); ws();
+        if (s[i] == ',') { ++i; continue; }
+        if (s[i] == '}') { ++i; break; }
+        fail("expected , or }");
+      }
+    } else if (c == '[') {
+      v.t = JVal::ARR; ++i; ws();
+      if (s[i] == ']') { ++i; return v; }
+      while (true) {
+        v.arr.push_back(val()); ws();
+        if (s[i] == ',') { ++i; continue; }
+        if (s[i] == ']') { ++i; break; }
+        fail("expected , or ]");
+      }
+    } else if (c == '"') {
+      v.t = JVal::STR; v.s = str();
+    } else if (s.compare(i, 4, "true") == 0) { v.t = JVal::BOOL; v.b = true; i += 4; }
+    else if (s.compare(i, 5, "false") == 0) { v.t = JVal::BOOL; i += 5; }
+    else if (s.compare(i, 4, "null") == 0) { v.t = JVal::NUL; i += 4; }
+    else {
+      size_t j = i;
+      while (j < s.size() && (isdigit((unsigned char)s[j]) || s[j] == '-' || s[j] == '+' || s[j] == '.' ||
+                              s[j] == 'e' || s[j] == 'E')) ++j;
+      v.t = JVal::NUM; v.num = std::stod(s.substr(i, j - i)); i = j;
+    }
+    return v;
+  }
+};
+
+// ============================================================================================================
+// Schema
+// ============================================================================================================
+enum class AT { NUL, BOOL, INT, LONG, FLOAT, DOUBLE, BYTES, STRING, RECORD, ENUM, ARRAY, MAP, UNION, FIXED };
+
+struct Node {
+  AT t = AT::NUL;
+  std::string name;  // full name for named types
+  std::vector<std::pair<std::string, Node*>> fields;
+  Node* items = nullptr;  // array items / map values
+  std::vector<Node*> branches;
+  std::vector<std::string> symbols;
+  int fixed_size = 0;
+};
+
+struct Schema {
+  std::vector<std::unique_ptr<Node>> pool;
+  std::map<std::string, Node*> named;
+  Node* root = nullptr;
+  std::string json;
+
+  Node* mk() { pool.emplace_back(new Node()); return pool.back().get(); }
+
+  static std::string full(const std::string& n, const std::string& ns) {
+    if (n.find('.') != std::string::npos || ns.empty()) return n;
+    return ns + "." + n;
+  }
+
+  Node* lookup(const std::string& n, const std::string& ns) {
+    auto it = named.find(full(n, ns));
+    if (it != named.end()) return it->second;
+    it = named.find(n);
+    if (it != named.end()) return it->second;
+    // match by short name
+    for (auto& kv : named) {
+      auto p = kv.first.rfind('.');
+      if ((p == std::string::npos ? kv.first : kv.first.substr(p + 1)) == n) return kv.second;
+    }
+    return nullptr;
+  }
+
+  Node* parse(const JVal& v, const std::string& ns) {
+    if (v.t == JVal::STR) {
+      const std::string& s = v.s;
+      Node* n;
+      if (s == "null") { n = mk(); n->t = AT::NUL; return n; }
+      if (s == "boolean") { n = mk(); n->t = AT::BOOL; return n; }
+      if (s == "int") { n = mk(); n->t = AT::INT; return n; }
+      if (s == "long") { n = mk(); n->t = AT::LONG; return n; }
+      if (s == "float") { n = mk(); n->t = AT::FLOAT; return n; }
+      if (s == "double") { n = mk(); n->t = AT::DOUBLE; return n; }
+      if (s == "bytes") { n = mk(); n->t = AT::BYTES; return n; }
+      if (s == "string") { n = mk(); n->t = AT::STRING; return n; }
+      Node* r = lookup(s, ns);
+      if (!r) throw std::runtime_error("unknown Avro type reference: " + s);
+      return r;
+    }
+    if (v.t == JVal::ARR) {
+      Node* n = mk(); n->t = AT::UNION;
+      for (auto& b : v.arr) n->branches.push_back(parse(b, ns));
+      return n;
+    }
+    if (v.t != JVal::OBJ) throw std::runtime_error("bad schema node");
+    const JVal* tp = v.get("type");
+    if (!tp) throw std::runtime_error("schema object without type");
+    if (tp->t != JVal::STR) return parse(*tp, ns);
+    const std::string& t = tp->s;
+    if (t == "record" || t == "error" || t == "enum" || t == "fixed") {
+      const JVal* nm = v.get("name");
+      const JVal* nsv = v.get("namespace");
+      std::string nns = nsv && nsv->t == JVal::STR ? nsv->s : ns;
+      std::string fname = full(nm ? nm->s : "anon", nns);
+      auto dot = fname.rfind('.');
+      std::string child_ns = dot == std::string::npos ? "" : fname.substr(0, dot);
+      Node* n = mk();
+      n->name = fname;
+      named[fname] = n;
+      if (t == "enum") {
+        n->t = AT::ENUM;
+        for (auto& sym : v.get("symbols")->arr) n->symbols.push_back(sym.s);
+      } else if (t == "fixed") {
+        n->t = AT::FIXED; n->fixed_size = (int)v.get("size")->num;
+      } else {
+        n->t = AT::RECORD;
+        for (auto& f : v.get("fields")->arr) n->fields.emplace_back(f.get("name")->s, parse(*f.get("type"), child_ns));
+      }
+      return n;
+    }
+    if (t == "array") { Node* n = mk(); n->t = AT::ARRAY; n->items = parse(*v.get("items"), ns); return n; }
+    if (t == "map") { Node* n = mk(); n->t = AT::MAP; n->items = parse(*v.get("values"), ns); return n; }
+    JVal s; s.t = JVal::STR; s.s = t;
+    return parse(s, ns);
+  }
+
+  explicit Schema(const std::string& j) : json(j) {
+    JParser p(j);
+    JVal v = p.val();
+    root = parse(v, "");
+  }
+};
+
+// ============================================================================================================
+// Binary reader / writer
+// ============================================================================================================
+struct Reader {
+  const uint8_t* p;
+  const uint8_t* end;
+  Reader(const uint8_t* b, size_t n) : p(b), end(b + n) {}
+  [[noreturn]] void fail() { throw std::runtime_error("Avro decode: unexpected end of data"); }
+  int64_t varlong() {
+    uint64_t v = 0; int shift = 0;
+    while (true) {
+      if (p >= end) fail();
+      uint8_t b = *p++;
+      v |= (uint64_t)(b & 0x7F) << shift;
+      if (!(b & 0x80)) break;
+      shift += 7;
+      if (shift > 63) throw std::runtime_error("varint too long");
+    }
+    return (int64_t)((v >> 1) ^ (~(v & 1) + 1));
+  }
+  double dbl() { if (end - p < 8) fail(); double d; memcpy(&d, p, 8); p += 8; return d; }
+  float flt() { if (end - p < 4) fail(); float f; memcpy(&f, p, 4); p += 4; return f; }
+  std::string str() {
+    int64_t n = varlong();
+    if (n < 0 || end - p < n) fail();
+    std::string s((const char*)p, (size_t)n); p += n; return s;
+  }
+  void skip(int64_t n) { if (n < 0 || end - p < n) fail(); p += n; }
+};
+
+struct Writer {
+  std::string buf;
+  void varlong(int64_t v) {
+    uint64_t z = ((uint64_t)v << 1) ^ (uint64_t)(v >> 63);
+    while (z & ~0x7FULL) { buf.push_back((char)((z & 0x7F) | 0x80)); z >>= 7; }
+    buf.push_back((char)z);
+  }
+  void dbl(double d) { char b[8]; memcpy(b, &d, 8); buf.append(b, 8); }
+  void flt(float f) { char b[4]; memcpy(b, &f, 4); buf.append(b, 4); }
+  void str(const std::string& s) { varlong((int64_t)s.size()); buf.append(s); }
+};
+
+// generic skip
+static void skip_value(Reader& r, const Node* n) {
+  switch (n->t) {
+    case AT::NUL: return;
+    case AT::BOOL: r.skip(1); return;
+    case AT::INT: case AT::LONG: case AT::ENUM: r.varlong(); return;
+    case AT::FLOAT: r.skip(4); return;
+    case AT::DOUBLE: r.skip(8); return;
+    case AT::BYTES: case AT::STRING: r.skip(r.varlong()); return;
+    case AT::FIXED: r.skip(n->fixed_size); return;
+    case AT::RECORD: for (auto& f : n->fields) skip_value(r, f.second); return;
+    case AT::UNION: { int64_t k = r.varlong(); skip_value(r, n->branches.at((size_t)k)); return; }
+    case AT::ARRAY: case AT::MAP: {
+      while (true) {
+        int64_t c = r.varlong();
+        if (c == 0) break;
+        if (c < 0) { int64_t sz = r.varlong(); r.skip(sz); continue; }
+        for (int64_t i = 0; i < c; ++i) {
+          if (n->t == AT::MAP) r.skip(r.varlong());
+          skip_value(r, n->items);
+        }
+      }
+      return;
+    }
+  }
+}
+
+static py::object decode_generic(Reader& r, const Node* n) {
+  switch (n->t) {
+    case AT::NUL: return py::none();
+    case AT::BOOL: { if (r.p >= r.end) r.fail(); bool b = *r.p++ != 0; return py::bool_(b); }
+    case AT::INT: case AT::LONG: return py::int_(r.varlong());
+    case AT::FLOAT: return py::float_(r.flt());
+    case AT::DOUBLE: return py::float_(r.dbl());
+    case AT::STRING: return py::str(r.str());
+    case AT::BYTES: { std::string s = r.str(); return py::bytes(s); }
+    case AT::FIXED: { std::string s((const char*)r.p, (size_t)n->fixed_size); r.skip(n->fixed_size); return py::bytes(s); }
+    case AT::ENUM: return py::str(n->symbols.at((size_t)r.varlong()));
+    case AT::UNION: { int64_t k = r.varlong(); return decode_generic(r, n->branches.at((size_t)k)); }
+    case AT::RECORD: {
+      py::dict d;
+      for (auto& f : n->fields) d[py::str(f.first)] = decode_generic(r, f.second);
+      return d;
+    }
+    case AT::ARRAY: {
+      py::list l;
+      while (true) {
+        int64_t c = r.varlong();
+        if (c == 0) break;
+        if (c < 0) { c = -c; r.varlong(); }
+        for (int64_t i = 0; i < c; ++i) l.append(decode_generic(r, n->items));
+      }
+      return l;
+    }
+    case AT::MAP: {
+      py::dict d;
+      while (true) {
+        int64_t c = r.varlong();
+        if (c == 0) break;
+        if (c < 0) { c = -c; r.varlong(); }
+        for (int64_t i = 0; i < c; ++i) { std::string k = r.str(); d[py::str(k)] = decode_generic(r, n->items); }
+      }
+      return d;
+    }
+  }
+  return py::none();
+}
+
+// union branch choice for a Python value
+static int pick_branch(const Node* n, const py::handle& v) {
+  auto& br = n->branches;
+  for (size_t i = 0; i < br.size(); ++i) {
+    AT t = br[i]->t;
+    if (v.is_none()) { if (t == AT::NUL) return (int)i; continue; }
+    if (py::isinstance<py::bool_>(v)) { if (t == AT::BOOL) return (int)i; continue; }
+    if (py::isinstance<py::int_>(v)) { if (t == AT::LONG || t == AT::INT) return (int)i; continue; }
+    if (py::isinstance<py::float_>(v)) { if (t == AT::DOUBLE || t == AT::FLOAT) return (int)i; continue; }
+    if (py::isinstance<py::str>(v)) { if (t == AT::STRING || t == AT::ENUM) return (int)i; continue; }
+    if (py::isinstance<py::bytes>(v)) { if (t == AT::BYTES || t == AT::FIXED) return (int)i; continue; }
+    if (py::isinstance<py::dict>(v)) { if (t == AT::RECORD || t == AT::MAP) return (int)i; continue; }
+    if (py::isinstance<py::list>(v) || py::isinstance<py::tuple>(v)) { if (t == AT::ARRAY) return (int)i; continue; }
+  }
+  // numeric promotion: int value into a double branch
+  if (py::isinstance<py::int_>(v))
+    for (size_t i = 0; i < br.size(); ++i)
+      if (br[i]->t == AT::DOUBLE || br[i]->t == AT::FLOAT) return (int)i;
+  throw std::runtime_error("no union branch matches value");
+}
+
+static void encode_generic(Writer& w, const Node* n, const py::handle& v) {
+  switch (n->t) {
+    case AT::NUL: return;
+    case AT::BOOL: w.buf.push_back(v.cast<bool>() ? 1 : 0); return;
+    case AT::INT: case AT::LONG: w.varlong(v.cast<int64_t>()); return;
+    case AT::FLOAT: w.flt(v.cast<float>()); return;
+    case AT::DOUBLE: w.dbl(v.cast<double>()); return;
+    case AT::STRING: w.str(py::str(v).cast<std::string>()); return;
+    case AT::BYTES: w.str(v.cast<std::string>()); return;
+    case AT::FIXED: w.buf.append(v.cast<std::string>()); return;
+    case AT::ENUM: {
+      std::string s = v.cast<std::string>();
+      for (size_t i = 0; i < n->symbols.size(); ++i)
+        if (n->symbols[i] == s) { w.varlong((int64_t)i); return; }
+      throw std::runtime_error("bad enum symbol " + s);
+    }
+    case AT::UNION: { int k = pick_branch(n, v); w.varlong(k); encode_generic(w, n->branches[(size_t)k], v); return; }
+    case AT::RECORD: {
+      py::dict d = py::reinterpret_borrow<py::dict>(v);
+      for (auto& f : n->fields) {
+        py::str key(f.first);
+        if (d.contains(key)) encode_generic(w, f.second, d[key]);
+        else encode_generic(w, f.second, py::none());
+      }
+      return;
+    }
+    case AT::ARRAY: {
+      py::sequence seq = py::reinterpret_borrow<py::sequence>(v);
+      if (py::len(seq) > 0) {
+        w.varlong((int64_t)py::len(seq));
+        for (auto item : seq) encode_generic(w, n->items, item);
+      }
+      w.varlong(0);
+      return;
+    }
+    case AT::MAP: {
+      py::dict d = py::reinterpret_borrow<py::dict>(v);
+      if (py::len(d) > 0) {
+        w.varlong((int64_t)py::len(d));
+        for (auto kv : d) { w.str(py::str(kv.first).cast<std::string>()); encode_generic(w, n->items, kv.second); }
+      }
+      w.varlong(0);
+      return;
+    }
+  }
+}
+
+// ============================================================================================================
+// Codecs
+// ============================================================================================================
+static uint32_t crc32c_table[256];
+static void init_crc32c() {
+  static bool done = false;
+  if (done) return;
+  for (uint32_t i = 0; i < 256; ++i) {
+    uint32_t c = i;
+    for (int k = 0; k < 8; ++k) c = (c & 1) ? (c >> 1) ^ 0x82F63B78u : (c >> 1);
+    crc32c_table[i] = c;
+  }
+  done = true;
+}
+// Avro's snappy codec appends the big-endian CRC32 (ISO-HDLC, the zlib crc32) of the uncompressed data
+static uint32_t crc32_iso(const std::string& s) {
+  return (uint32_t)crc32(0L, (const Bytef*)s.data(), (uInt)s.size());
+}
+
+static std::string snappy_decompress(const uint8_t* p, size_t n) {
+  const uint8_t* end = p + n;
+  uint64_t len = 0; int shift = 0;
+  while (true) {
+    if (p >= end) throw std::runtime_error("snappy: truncated header");
+    uint8_t b = *p++;
+    len |= (uint64_t)(b & 0x7F) << shift;
+    if (!(b & 0x80)) break;
+    shift += 7;
+  }
+  std::string out;
+  out.reserve(len);
+  while (p < end) {
+    uint8_t tag = *p++;
+    int type = tag & 3;
+    if (type == 0) {
+      uint32_t l = tag >> 2;
+      if (l >= 60) {
+        int nb = (int)l - 59; l = 0;
+        for (int i = 0; i < nb; ++i) l |= (uint32_t)p[i] << (8 * i);
+        p += nb;
+      }
+      l += 1;
+      if ((size_t)(end - p) < l) throw std::runtime_error("snappy: bad literal");
+      out.append((const char*)p, l); p += l;
+    } else {
+      uint32_t l, off;
+      if (type == 1) { l = ((tag >> 2) & 7) + 4; off = ((uint32_t)(tag >> 5) << 8) | *p++; }
+      else if (type == 2) { l = (tag >> 2) + 1; off = p[0] | (p[1] << 8); p += 2; }
+      else { l = (tag >> 2) + 1; off = p[0] | (p[1] << 8) | (p[2] << 16) | ((uint32_t)p[3] << 24); p += 4; }
+      if (off == 0 || off > out.size()) throw std::runtime_error("snappy: bad copy offset");
+      size_t start = out.size() - off;
+      for (uint32_t i = 0; i < l; ++i) out.push_back(out[start + i]);
+    }
+  }
+  if (out.size() != len) throw std::runtime_error("snappy: length mismatch");
+  return out;
+}
+
+// valid snappy stream made of literal chunks (no back-references): simple and exact
+static std::string snappy_compress_literal(const std::string& in) {
+  std::string out;
+  uint64_t n = in.size();
+  while (true) { uint8_t b = n & 0x7F; n >>= 7; if (n) { out.push_back((char)(b | 0x80)); } else { out.push_back((char)b); break; } }
+  size_t i = 0;
+  while (i < in.size()) {
+    size_t l = std::min<size_t>(in.size() - i, 65536);
+    uint32_t lm1 = (uint32_t)(l - 1);
+    if (lm1 < 60) out.push_back((char)(lm1 << 2));
+    else if (lm1 < 256) { out.push_back((char)(60 << 2)); out.push_back((char)lm1); }
+    else { out.push_back((char)(61 << 2)); out.push_back((char)(lm1 & 0xFF)); out.push_back((char)(lm1 >> 8)); }
+    out.append(in, i, l);
+    i += l;
+  }
+  return out;
+}
+
+static std::string inflate_raw(const uint8_t* p, size_t n) {
+  z_stream zs; memset(&zs, 0, sizeof(zs));
+  if (inflateInit2(&zs, -15) != Z_OK) throw std::runtime_error("inflateInit2 failed");
+  zs.next_in = (Bytef*)p; zs.avail_in = (uInt)n;
+  std::string out;
+  char buf[1 << 16];
+  int ret;
+  do {
+    zs.next_out = (Bytef*)buf; zs.avail_out = sizeof(buf);
+    ret = inflate(&zs, Z_NO_FLUSH);
+    if (ret != Z_OK && ret != Z_STREAM_END) { inflateEnd(&zs); throw std::runtime_error("inflate failed"); }
+    out.append(buf, sizeof(buf) - zs.avail_out);
+  } while (ret != Z_STREAM_END);
+  inflateEnd(&zs);
+  return out;
+}
+
+static std::string deflate_raw(const std::string& in, int level) {
+  z_stream zs; memset(&zs, 0, sizeof(zs));
+  if (deflateInit2(&zs, level, Z_DEFLATED, -15, 8, Z_DEFAULT_STRATEGY) != Z_OK) throw std::runtime_error("deflateInit2");
+  zs.next_in = (Bytef*)in.data(); zs.avail_in = (uInt)in.size();
+  std::string out;
+  char buf[1 << 16];
+  int ret;
+  do {
+    zs.next_out = (Bytef*)buf; zs.avail_out = sizeof(buf);
+    ret = deflate(&zs, Z_FINISH);
+    out.append(buf, sizeof(buf) - zs.avail_out);
+  } while (ret != Z_STREAM_END);
+  deflateEnd(&zs);
+  return out;
+}
+
+// ============================================================================================================
+// OCF container
+// ============================================================================================================
+struct OCF {
+  std::string data;  // whole file
+  std::string schema_json, codec;
+  std::unique_ptr<Schema> schema;
+  std::vector<std::pair<int64_t, std::string>> blocks;  // (count, decompressed bytes)
+
+  explicit OCF(const std::string& path) {
+    std::ifstream f(path, std::ios::binary);
+    if (!f) throw std::runtime_error("cannot open " + path);
+    std::stringstream ss; ss << f.rdbuf(); data = ss.str();
+    if (data.size() < 4 || data.compare(0, 4, std::string("Obj\x01", 4)) != 0)
+      throw std::runtime_error("not an Avro object container file: " + path);
+    Reader r((const uint8_t*)data.data() + 4, data.size() - 4);
+    // metadata map
+    while (true) {
+      int64_t c = r.varlong();
+      if (c == 0) break;
+      if (c < 0) { c = -c; r.varlong(); }
+      for (int64_t i = 0; i < c; ++i) {
+        std::string k = r.str(), v = r.str();
+        if (k == "avro.schema") schema_json = v;
+        else if (k == "avro.codec") codec = v;
+      }
+    }
+    if (codec.empty()) codec = "null";
+    std::string sync((const char*)r.p, 16); r.skip(16);
+    schema.reset(new Schema(schema_json));
+    while (r.p < r.end) {
+      int64_t cnt = r.varlong();
+      int64_t sz = r.varlong();
+      if (sz < 0 || r.end - r.p < sz) throw std::runtime_error("truncated block");
+      const uint8_t* b = r.p; r.skip(sz);
+      std::string blk;
+      if (codec == "null") blk.assign((const char*)b, (size_t)sz);
+      else if (codec == "deflate") blk = inflate_raw(b, (size_t)sz);
+      else if (codec == "snappy") {
+        if (sz < 4) throw std::runtime_error("snappy block too small");
+        blk = snappy_decompress(b, (size_t)sz - 4);
+        uint32_t want = ((uint32_t)b[sz - 4] << 24) | ((uint32_t)b[sz - 3] << 16) | ((uint32_t)b[sz - 2] << 8) | b[sz - 1];
+        if (crc32_iso(blk) != want) throw std::runtime_error("snappy block CRC mismatch");
+      } else throw std::runtime_error("unsupported Avro codec: " + codec);
+      blocks.emplace_back(cnt, std::move(blk));
+      if (r.end - r.p < 16) throw std::runtime_error("missing sync marker");
+      if (memcmp(r.p, sync.data(), 16) != 0) throw std::runtime_error("sync marker mismatch");
+      r.skip(16);
+    }
+  }
+};
+
+static py::tuple read_ocf(const std::string& path) {
+  OCF o(path);
+  py::list recs;
+  for (auto& b : o.blocks) {
+    Reader r((const uint8_t*)b.second.data(), b.second.size());
+    for (int64_t i = 0; i < b.first; ++i) recs.append(decode_generic(r, o.schema->root));
+  }
+  return py::make_tuple(o.schema_json, recs, o.codec);
+}
+
+static std::string read_schema(const std::string& path) {
+  OCF o(path);
+  return o.schema_json;
+}
+
+static void write_ocf(const std::string& path, const std::string& schema_json, py::list records,
+                      const std::string& codec, int block_records) {
+  Schema sch(schema_json);
+  std::string out("Obj\x01", 4);
+  Writer hdr;
+  hdr.varlong(2);
+  hdr.str("avro.schema"); hdr.str(schema_json);
+  hdr.str("avro.codec"); hdr.str(codec);
+  hdr.varlong(0);
+  out += hdr.buf;
+  std::string sync(16, '\0');
+  std::mt19937_64 rng(0x5eed1234abcdULL ^ (uint64_t)records.size());
+  for (int i = 0; i < 16; ++i) sync[i] = (char)(rng() & 0xFF);
+  out += sync;
+  size_t n = py::len(records);
+  size_t i = 0;
+  while (i < n) {
+    size_t m = std::min<size_t>(n - i, (size_t)std::max(block_records, 1));
+    Writer body;
+    for (size_t k = 0; k < m; ++k) encode_generic(body, sch.root, records[i + k]);
+    std::string payload;
+    if (codec == "null") payload = body.buf;
+    else if (codec == "deflate") payload = deflate_raw(body.buf, 6);
+    else if (codec == "snappy") {
+      payload = snappy_compress_literal(body.buf);
+      uint32_t c = crc32_iso(body.buf);
+      payload.push_back((char)(c >> 24)); payload.push_back((char)(c >> 16));
+      payload.push_back((char)(c >> 8)); payload.push_back((char)c);
+    } else throw std::runtime_error("unsupported codec " + codec);
+    Writer bh; bh.varlong((int64_t)m); bh.varlong((int64_t)payload.size());
+    out += bh.buf; out += payload; out += sync;
+    i += m;
+  }
+  std::ofstream f(path, std::ios::binary);
+  if (!f) throw std::runtime_error("cannot write " + path);
+  f.write(out.data(), (std::streamsize)out.size());
+}
+
+// ============================================================================================================
+// Columnar training-data fast path
+// ============================================================================================================
+static bool is_numeric(AT t) { return t == AT::INT || t == AT::LONG || t == AT::FLOAT || t == AT::DOUBLE || t == AT::BOOL; }
+
+static double read_number(Reader& r, const Node* n, bool& ok) {
+  switch (n->t) {
+    case AT::INT: case AT::LONG: ok = true; return (double)r.varlong();
+    case AT::FLOAT: ok = true; return r.flt();
+    case AT::DOUBLE: ok = true; return r.dbl();
+    case AT::BOOL: { ok = true; bool b = *r.p++ != 0; return b ? 1.0 : 0.0; }
+    case AT::STRING: { std::string s = r.str(); try { ok = true; return std::stod(s); } catch (...) { ok = false; return NAN; } }
+    case AT::NUL: ok = false; return NAN;
+    case AT::UNION: { int64_t k = r.varlong(); return read_number(r, n->branches.at((size_t)k), ok); }
+    default: skip_value(r, n); ok = false; return NAN;
+  }
+}
+
+static bool read_string_like(Reader& r, const Node* n, std::string& out) {
+  switch (n->t) {
+    case AT::STRING: case AT::BYTES: out = r.str(); return true;
+    case AT::INT: case AT::LONG: out = std::to_string(r.varlong()); return true;
+    case AT::DOUBLE: { std::ostringstream o; o << r.dbl(); out = o.str(); return true; }
+    case AT::FLOAT: { std::ostringstream o; o << r.flt(); out = o.str(); return true; }
+    case AT::BOOL: { bool b = *r.p++ != 0; out = b ? "true" : "false"; return true; }
+    case AT::ENUM: out = n->symbols.at((size_t)r.varlong()); return true;
+    case AT::NUL: return false;
+    case AT::UNION: { int64_t k = r.varlong(); return read_string_like(r, n->branches.at((size_t)k), out); }
+    default: skip_value(r, n); return false;
+  }
+}
+
+static const Node* strip_null_union(const Node* n) {
+  if (n->t != AT::UNION) return n;
+  const Node* keep = nullptr;
+  for (auto* b : n->branches)
+    if (b->t != AT::NUL) { if (keep) return n; keep = b; }
+  return keep ? keep : n;
+}
+
+// Is this node a feature bag (array of records with name + value fields)?
+static bool is_bag(const Node* n) {
+  n = strip_null_union(n);
+  if (n->t != AT::ARRAY) return false;
+  const Node* it = strip_null_union(n->items);
+  if (it->t != AT::RECORD) return false;
+  bool has_name = false, has_value = false;
+  for (auto& f : it->fields) { if (f.first == "name") has_name = true; if (f.first == "value") has_value = true; }
+  return has_name && has_value;
+}
+
+struct Interner {
+  std::unordered_map<std::string, int32_t> ids;
+  std::vector<std::string> keys;
+  int32_t get(const std::string& k) {
+    auto it = ids.find(k);
+    if (it != ids.end()) return it->second;
+    int32_t id = (int32_t)keys.size();
+    ids.emplace(k, id); keys.push_back(k);
+    return id;
+  }
+};
+
+struct BagOut {
+  std::vector<int64_t> rowptr{0};
+  std::vector<int32_t> keys;
+  std::vector<double> vals;
+};
+
+// Decode TrainingExample-like files into columns.
+static py::dict read_columnar(const std::vector<std::string>& paths, const std::vector<std::string>& label_fields,
+                              const std::string& weight_field, const std::string& offset_field,
+                              const std::string& uid_field, const std::string& metadata_field,
+                              const std::vector<std::string>& bags_wanted, const std::vector<std::string>& id_tags,
+                              const std::string& delimiter) {
+  std::vector<double> label, weight, offset;
+  std::vector<std::string> uid;
+  std::vector<uint8_t> has_uid;
+  std::map<std::string, std::vector<std::string>> tags;
+  for (auto& t : id_tags) tags[t];
+  std::map<std::string, BagOut> bags;
+  Interner intern;
+  std::string label_used;
+  int64_t n = 0;
+  for (auto& path : paths) {
+    OCF o(path);
+    const Node* root = o.schema->root;
+    if (root->t != AT::RECORD) throw std::runtime_error("top-level Avro schema must be a record: " + path);
+    // field roles
+    std::vector<int> role(root->fields.size(), 0);  // 0 skip, 1 label, 2 weight, 3 offset, 4 uid, 5 meta, 6 bag, 7 tag
+    std::vector<std::string> rname(root->fields.size());
+    int label_idx = -1;
+    for (auto& lf : label_fields) {
+      for (size_t i = 0; i < root->fields.size(); ++i)
+        if (root->fields[i].first == lf) { label_idx = (int)i; break; }
+      if (label_idx >= 0) { label_used = lf; break; }
+    }
+    for (size_t i = 0; i < root->fields.size(); ++i) {
+      const std::string& fn = root->fields[i].first;
+      const Node* fnode = root->fields[i].second;
+      if ((int)i == label_idx) role[i] = 1;
+      else if (fn == weight_field) role[i] = 2;
+      else if (fn == offset_field) role[i] = 3;
+      else if (fn == uid_field) role[i] = 4;
+      else if (fn == metadata_field) role[i] = 5;
+      else if (tags.count(fn)) { role[i] = 7; rname[i] = fn; }
+      else if (is_bag(fnode)) {
+        bool want = bags_wanted.empty();
+        for (auto& b : bags_wanted) if (b == fn) want = true;
+        if (want) { role[i] = 6; rname[i] = fn; bags[fn]; }
+      }
+    }
+    for (auto& blk : o.blocks) {
+      Reader r((const uint8_t*)blk.second.data(), blk.second.size());
+      for (int64_t rec = 0; rec < blk.first; ++rec) {
+        double lab = NAN, wt = NAN, off = NAN;
+        std::string u; bool hu = false;
+        std::map<std::string, std::string> rec_tags;
+        std::map<std::string, bool> bag_seen;
+        for (size_t i = 0; i < root->fields.size(); ++i) {
+          const Node* fnode = root->fields[i].second;
+          bool ok;
+          switch (role[i]) {
+            case 1: lab = read_number(r, fnode, ok); break;
+            case 2: wt = read_number(r, fnode, ok); break;
+            case 3: off = read_number(r, fnode, ok); break;
+            case 4: hu = read_string_like(r, fnode, u); break;
+            case 7: { std::string s; if (read_string_like(r, fnode, s)) rec_tags[rname[i]] = s; break; }
+            case 5: {
+              const Node* m = fnode;
+              if (m->t == AT::UNION) { int64_t k = r.varlong(); m = m->branches.at((size_t)k); }
+              if (m->t != AT::MAP) { skip_value(r, m); break; }
+              while (true) {
+                int64_t c = r.varlong();
+                if (c == 0) break;
+                if (c < 0) { c = -c; r.varlong(); }
+                for (int64_t k = 0; k < c; ++k) {
+                  std::string key = r.str();
+                  std::string sval;
+                  bool has = read_string_like(r, m->items, sval);
+                  if (has && tags.count(key) && !rec_tags.count(key)) rec_tags[key] = sval;
+                }
+              }
+              break;
+            }
+            case 6: {
+              BagOut& bo = bags[rname[i]];
+              const Node* arr = fnode;
+              if (arr->t == AT::UNION) { int64_t k = r.varlong(); arr = arr->branches.at((size_t)k); }
+              if (arr->t != AT::ARRAY) { skip_value(r, arr); break; }
+              const Node* item = arr->items;
+              while (true) {
+                int64_t c = r.varlong();
+                if (c == 0) break;
+                if (c < 0) { c = -c; r.varlong(); }
+                for (int64_t k = 0; k < c; ++k) {
+                  const Node* it = item;
+                  if (it->t == AT::UNION) { int64_t b = r.varlong(); it = it->branches.at((size_t)b); }
+                  std::string name, term;
+                  double val = NAN;
+                  for (auto& f : it->fields) {
+                    if (f.first == "name") read_string_like(r, f.second, name);
+                    else if (f.first == "term") { if (!read_string_like(r, f.second, term)) term.clear(); }
+                    else if (f.first == "value") { bool okv; val = read_number(r, f.second, okv); }
+                    else skip_value(r, f.second);
+                  }
+                  bo.keys.push_back(intern.get(name + delimiter + term));
+                  bo.vals.push_back(val);
+                }
+              }
+              bag_seen[rname[i]] = true;
+              break;
+            }
+            default: skip_value(r, fnode);
+          }
+        }
+        label.push_back(lab); weight.push_back(wt); offset.push_back(off);
+        uid.push_back(u); has_uid.push_back(hu ? 1 : 0);
+        for (auto& t : tags) {
+          auto it = rec_tags.find(t.first);
+          t.second.push_back(it == rec_tags.end() ? std::string() : it->second);
+        }
+        for (auto& b : bags) b.second.rowptr.push_back((int64_t)b.second.keys.size());
+        ++n;
+      }
+    }
+  }
+  auto arr_d = [](std::vector<double>& v) { return py::array_t<double>((py::ssize_t)v.size(), v.data()); };
+  py::dict out;
+  out["n"] = n;
+  out["label_field"] = label_used;
+  out["label"] = arr_d(label);
+  out["weight"] = arr_d(weight);
+  out["offset"] = arr_d(offset);
+  out["uid"] = py::cast(uid);
+  out["has_uid"] = py::array_t<uint8_t>((py::ssize_t)has_uid.size(), has_uid.data());
+  py::dict tg;
+  for (auto& t : tags) tg[py::str(t.first)] = py::cast(t.second);
+  out["id_tags"] = tg;
+  py::dict bg;
+  for (auto& b : bags) {
+    bg[py::str(b.first)] = py::make_tuple(py::array_t<int64_t>((py::ssize_t)b.second.rowptr.size(), b.second.rowptr.data()),
+                                          py::array_t<int32_t>((py::ssize_t)b.second.keys.size(), b.second.keys.data()),
+                                          py::array_t<double>((py::ssize_t)b.second.vals.size(), b.second.vals.data()));
+  }
+  out["bags"] = bg;
+  out["vocab"] = py::cast(intern.keys);
+  return out;
+}
+
+PYBIND11_MODULE(libpml_avro, m) {
+  m.doc() = "photon_ml_amd native Avro OCF codec";
+  m.def("read_ocf", &read_ocf, "Decode an OCF file -> (schema_json, [records], codec)");
+  m.def("read_schema", &read_schema);
+  m.def("write_ocf", &write_ocf, py::arg("path"), py::arg("schema_json"), py::arg("records"),
+        py::arg("codec") = "deflate", py::arg("block_records") = 4096);
+  m.def("read_columnar", &read_columnar, py::arg("paths"), py::arg("label_fields"), py::arg("weight_field"),
+        py::arg("offset_field"), py::arg("uid_field"), py::arg("metadata_field"), py::arg("bags"),
+        py::arg("id_tags"), py::arg("delimiter") = std::string("\x01"));
+  m.def("snappy_roundtrip", [](const std::string& s) {
+    std::string c = snappy_compress_literal(s);
+    return snappy_decompress((const uint8_t*)c.data(), c.size()) == s;
+  });
+  init_crc32c();
+}

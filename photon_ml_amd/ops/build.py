@@ -68,7 +68,12 @@ def build_cpp(name: str, force: bool = False, verbose: bool = False) -> Path:
         return out
     out.parent.mkdir(parents=True, exist_ok=True)
     if force or _needs_build(src, out):
-        cmd = ["g++", "-O3", "-std=c++17", "-fPIC", "-shared", str(src), "-o", str(out) + ".tmp", "-lz"]
+        import sysconfig
+        import pybind11
+        inc = ["-I" + sysconfig.get_paths()["include"], "-I" + pybind11.get_include()]
+        vis = ["-fvisibility=hidden"] if name == "avro" else []  # pybind11 module vs plain C ABI
+        cmd = ["g++", "-O3", "-std=c++17", "-fPIC", "-shared", *vis, *inc, str(src), "-o", str(out) + ".tmp",
+               "-lz"]
         if verbose:
             print(" ".join(cmd), flush=True)
         subprocess.run(cmd, check=True)

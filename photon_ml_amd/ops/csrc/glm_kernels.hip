@@ -180,10 +180,24 @@ __device__ __forceinline__ float val1(const uint16_t* p) {
 __device__ __forceinline__ float val1(const float* p) { return __builtin_nontemporal_load(p); }
 __device__ __forceinline__ double val1(const double* p) { return __builtin_nontemporal_load(p); }
 
+// Hot-table gather: lanes whose feature is in the LDS head read LDS; their global address collapses onto x[0]
+// so that, whatever the compiler does with the predicated global load, they add no distinct cache lines.
 template <typename XT, bool HOT>
 __device__ __forceinline__ XT gather(const XT* __restrict__ x, const XT* hot, int hot_n, int j) {
-  if (HOT) return j < hot_n ? hot[j] : x[j];
+  if (HOT) {
+    const bool h = j < hot_n;
+    const XT g = x[h ? 0 : j];
+    return h ? hot[j] : g;
+  }
   return x[j];
+}
+
+// ablation index transform (profiling builds only; abl == 0 in production)
+__device__ __forceinline__ int abl_index(int abl, int j, int e) {
+  if (abl & 1) return j & 255;            // 1 KB window: L1-resident gathers
+  if (abl & 4) return j & 0xFFFF;         // 256 KB window: L2-resident random gathers
+  if (abl & 8) return e & 0x3FFFF;        // perfectly coalesced gathers (consecutive entries)
+  return j;
 }
 
 template <typename VT, typename XT, typename AT, bool SQ, bool STRIDED, bool HOT>
@@ -192,7 +206,6 @@ __device__ __forceinline__ double stream_products(const BlockDesc& d, const int*
                                                   const XT* hot, int hot_n, AT* prod, bool to_lds, int abl) {
   const int lo = d.nz_lo & ~(VEC - 1);
   const int hi = (d.nz_hi + VEC - 1) & ~(VEC - 1);
-  const int amask = (abl & 1) ? 255 : 0x7fffffff;
   double acc = 0.0;
   for (int base = lo; base < hi; base += NB) {
     if (STRIDED) {
@@ -213,7 +226,7 @@ __device__ __forceinline__ double stream_products(const BlockDesc& d, const int*
       for (int r = 0; r < SROUNDS; ++r) {
         const int e = base + r * NTHREADS + threadIdx.x;
         const bool in = (e >= d.nz_lo) && (e < d.nz_hi);
-        xv[r] = gather<XT, HOT>(x, hot, hot_n, (in ? ii[r] : 0) & amask);
+        xv[r] = gather<XT, HOT>(x, hot, hot_n, abl_index(abl, in ? ii[r] : 0, e));
       }
       AT s = AT(0);
 #pragma unroll
@@ -250,7 +263,7 @@ __device__ __forceinline__ double stream_products(const BlockDesc& d, const int*
           for (int k = 0; k < 8; ++k) {
             const int ik = k < 4 ? i0[r][k] : i1[r][k - 4];
             const bool in = (e + k >= d.nz_lo) && (e + k < d.nz_hi);
-            xv[r][k] = gather<XT, HOT>(x, hot, hot_n, (in ? ik : 0) & amask);
+            xv[r][k] = gather<XT, HOT>(x, hot, hot_n, abl_index(abl, in ? ik : 0, e + k));
           }
         }
       }

@@ -10,9 +10,13 @@ from __future__ import annotations
 
 from typing import Optional
 
+import warnings
+
 import numpy as np
 import scipy.sparse as sp
 import torch
+
+warnings.filterwarnings("ignore", message="Sparse CSR tensor support is in beta state")
 
 from ..data.matrix import LabeledData
 

@@ -1,1 +1,1 @@
-
+from .summary import BasicStatisticalSummary

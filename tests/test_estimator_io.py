@@ -1,0 +1,127 @@
+"""Estimator, normalization and IO tests.
+
+* GameEstimatorIntegTest.testNormalization (photon-api/src/integTest/.../estimators/GameEstimatorIntegTest.scala
+  :129-178): every normalization type, no regularization -> scikit-learn coefficients to 1e-8.
+* ModelProcessingUtilsTest save/load round trip; Avro codec round trips incl. reference files.
+"""
+import json
+import os
+
+import numpy as np
+import pytest
+import torch
+
+from photon_ml_amd.data.game_data import GameData, generate_game_data
+from photon_ml_amd.data.random_effect import FixedEffectDataConfiguration, RandomEffectDataConfiguration
+from photon_ml_amd.estimators.game_estimator import GameEstimator, GameTransformer, train_generalized_linear_model
+from photon_ml_amd.io import avro
+from photon_ml_amd.io.index_map import DefaultIndexMap
+from photon_ml_amd.io.model_io import load_game_model, save_game_model, load_model_task
+from photon_ml_amd.normalization.context import NormalizationContext, NormalizationType
+from photon_ml_amd.optimization.config import GLMOptimizationConfiguration, OptimizerConfig, RegularizationContext
+from photon_ml_amd.stat.summary import BasicStatisticalSummary
+
+from test_optimizers import trivial_data
+
+REF = "/root/reference/photon-client/src/integTest/resources"
+
+
+@pytest.mark.parametrize("ntype", list(NormalizationType))
+def test_normalization_matches_sklearn(ntype):
+    ld = trivial_data()
+    summary = BasicStatisticalSummary.compute(ld.x)
+    norm = NormalizationContext.build(ntype, summary, intercept_id=2)
+    res = train_generalized_linear_model(ld, "LINEAR_REGRESSION", "LBFGS", RegularizationContext("NONE"), [0.0],
+                                         norm, max_iterations=100, tolerance=1e-11, device="cpu")
+    w = res[0][1].coefficients.means.numpy()
+    np.testing.assert_allclose(w, [0.34945501725815586, 0.26339479490270173, 0.4366125400310442], atol=1e-8)
+
+
+def test_standardized_summary_known_values():
+    ld = trivial_data()
+    s = BasicStatisticalSummary.compute(ld.x)
+    assert s.count == 10
+    assert abs(float(s.mean[2]) - 1.0) < 1e-12 and float(s.variance[2]) == 0.0
+    assert float(s.max[1]) == 0.0 and float(s.min[1]) < -0.89
+    assert int(s.num_nonzeros[1]) == 4
+
+
+def test_lambda_path_descending_warm_start():
+    ld = trivial_data()
+    res = train_generalized_linear_model(ld, "LOGISTIC_REGRESSION", "TRON", RegularizationContext("L2"),
+                                         [0.1, 10.0, 1.0], device="cpu")
+    assert [r[0] for r in res] == [10.0, 1.0, 0.1]
+    norms = [float(r[1].coefficients.means.norm()) for r in res]
+    assert norms[0] < norms[1] < norms[2]
+
+
+def test_l1_sparsity_monotone_in_lambda():
+    """DriverTest: number of non-zero coefficients non-increasing in the L1 weight."""
+    from photon_ml_amd.data.synthetic import generate_glm_data
+    ld, _ = generate_glm_data("LOGISTIC_REGRESSION", 800, 30, density=0.3, seed=1)
+    res = train_generalized_linear_model(ld, "LOGISTIC_REGRESSION", "LBFGS", RegularizationContext("L1"),
+                                         [0.1, 1, 10, 100], max_iterations=200, tolerance=1e-9, device="cpu")
+    nnz = [int((r[1].coefficients.means.abs() > 0).sum()) for r in res]
+    assert all(a <= b for a, b in zip(nnz, nnz[1:])), nnz  # lambdas descending -> nnz ascending
+
+
+def test_avro_reference_model_file_and_roundtrip(tmp_path):
+    p = f"{REF}/GameIntegTest/fixedEffectOnlyGAMEModel/fixed-effect/globalShard/coefficients/part-00000.avro"
+    schema, recs = avro.read_records(p)
+    assert schema["name"] == "BayesianLinearModelAvro" and len(recs) == 1
+    assert recs[0]["modelClass"].endswith("LinearRegressionModel")
+    means = recs[0]["means"]
+    assert means[0]["name"] == "(INTERCEPT)"
+    # sorted by |value| descending, all above threshold
+    vals = [abs(m["value"]) for m in means]
+    assert vals == sorted(vals, reverse=True) and min(vals) > 1e-4
+    for codec in ("null", "deflate", "snappy"):
+        out = tmp_path / f"m-{codec}.avro"
+        avro.write_records(str(out), schema, recs, codec=codec)
+        assert avro.read_records(str(out))[1] == recs
+
+
+def test_load_reference_fixed_effect_model():
+    d = f"{REF}/GameIntegTest/fixedEffectOnlyGAMEModel"
+    recs = avro.read_records(f"{d}/fixed-effect/globalShard/coefficients/part-00000.avro")[1]
+    keys = [f"{m['name']}\u0001{m['term']}" for m in recs[0]["means"]]
+    im = DefaultIndexMap.from_keys(sorted(keys))
+    model = load_game_model(d, {"globalShard": im})
+    assert load_model_task(d).value == "LINEAR_REGRESSION"
+    glm = model.get("globalShard").glm
+    assert glm.task.value == "LINEAR_REGRESSION"
+    assert abs(float(glm.coefficients.means[im.get_index("(INTERCEPT)\u0001")]) - 3.5525033712866567) < 1e-12
+
+
+def test_game_model_save_load_roundtrip(tmp_path):
+    data, _ = generate_game_data(n_rows=600, n_users=15, seed=8, task="LOGISTIC_REGRESSION")
+    cfg = GLMOptimizationConfiguration(OptimizerConfig("TRON", 20, 1e-7), RegularizationContext("L2"), 1.0)
+    est = (GameEstimator(device="cpu").set_training_task("LOGISTIC_REGRESSION")
+           .set_coordinate_data_configurations({"global": FixedEffectDataConfiguration("global"),
+                                                "per-user": RandomEffectDataConfiguration("userId", "user")})
+           .set_coordinate_update_sequence(["global", "per-user"]).set_compute_variance(True))
+    res = est.fit(data, data, [{"global": cfg, "per-user": cfg}])
+    model = res[0].model
+    maps = {s: DefaultIndexMap.from_keys([f"f{j}\u0001t" for j in range(data.shards[s].shape[1])])
+            for s in data.shards}
+    save_game_model(model, str(tmp_path / "m"), maps, opt_configs=res[0].config)
+    meta = json.load(open(tmp_path / "m" / "model-metadata.json"))
+    assert meta["modelType"] == "LOGISTIC_REGRESSION"
+    assert open(tmp_path / "m" / "random-effect" / "per-user" / "id-info").read().split() == ["userId", "user"]
+    loaded = load_game_model(str(tmp_path / "m"), maps)
+    s0, _ = GameTransformer(model).transform(data)
+    s1, ev = GameTransformer(loaded, ["AUC", "LOGISTIC_LOSS"]).transform(data)
+    # coefficients below 1e-4 are dropped on save -> tiny score differences only
+    assert torch.allclose(s0, s1, atol=5e-3)
+    assert ev[0][1] > 0.7
+    fe = loaded.get("global").glm.coefficients
+    assert fe.variances is not None and bool((fe.variances > 0).all())
+
+
+def test_avro_data_reader_heart():
+    from photon_ml_amd.io.data_reader import AvroDataReader, FeatureShardConfiguration
+    data, maps = AvroDataReader().read(f"{REF}/DriverIntegTest/input/heart.avro",
+                                       {"s": FeatureShardConfiguration(["features"], True)})
+    assert data.n_rows == 250 and data.shards["s"].shape == (250, 14)
+    assert maps["s"].intercept_index == 13
+    assert set(np.unique(data.response)) == {0.0, 1.0}
