@@ -1,0 +1,116 @@
+"""CLI driver tests (GameTrainingDriverIntegTest / GameScoringDriverIntegTest analogues, on CPU).
+
+Reference: ``photon-client/src/integTest/.../cli/game/training/GameTrainingDriverIntegTest.scala`` (fixed-effect,
+random-effect and mixed runs; output layout best/ + models/<i>/ with model-spec; hyper-parameter tuning adds
+models; output modes) and ``GameScoringDriverIntegTest.scala`` (scores written as ScoringResultAvro and equal to
+in-memory scoring). Data: synthetic GAME data written as Avro by :mod:`photon_ml_amd.io.data_writer`.
+"""
+import os
+
+import numpy as np
+import pytest
+
+from photon_ml_amd.cli import game_scoring, game_training
+from photon_ml_amd.cli.params import (expand_game_configurations, parse_coordinate_configuration,
+                                      parse_feature_shard_configuration)
+from photon_ml_amd.data.game_data import generate_game_data
+from photon_ml_amd.io.data_writer import write_game_avro
+from photon_ml_amd.io.score_io import load_scores
+
+SHARDS = ["--feature-shard-configurations", "name=global,feature.bags=features",
+          "--feature-shard-configurations", "name=user,feature.bags=userFeatures,intercept=true"]
+FIXED = "name=fixed,feature.shard=global,optimizer=LBFGS,max.iter=50,tolerance=1e-8,regularization=L2,reg.weights=10|0.1"
+RANDOM = ("name=per-user,feature.shard=user,random.effect.type=userId,optimizer=TRON,max.iter=20,tolerance=1e-8,"
+          "regularization=L2,reg.weights=1")
+
+
+@pytest.fixture(scope="module")
+def game_avro(tmp_path_factory):
+    root = tmp_path_factory.mktemp("game")
+    data, _ = generate_game_data(n_rows=1500, n_users=20, seed=3, task="LOGISTIC_REGRESSION")
+    tr, va = data.subset(np.arange(1200)), data.subset(np.arange(1200, 1500))
+    bags = {"global": "features", "user": "userFeatures"}
+    write_game_avro(str(root / "train"), tr, bags, n_files=2)
+    write_game_avro(str(root / "val"), va, bags)
+    return root
+
+
+def test_dsl_parsing_and_grid():
+    cc = parse_coordinate_configuration(FIXED + ",down.sampling.rate=0.5")
+    cc.update(parse_coordinate_configuration(RANDOM.replace("reg.weights=1", "reg.weights=1|3")))
+    fixed = cc["fixed"]
+    assert not fixed.is_random_effect and fixed.optimization_configuration.down_sampling_rate == 0.5
+    lams = [c.regularization_weight for c in fixed.expand_optimization_configurations()]
+    assert lams == [10.0, 0.1]
+    grid = expand_game_configurations(cc)
+    assert len(grid) == 4 and {tuple(sorted(g)) for g in grid} == {("fixed", "per-user")}
+    fs = parse_feature_shard_configuration("name=s,feature.bags=a|b,intercept=false")
+    assert fs["s"].feature_bags == ["a", "b"] and not fs["s"].has_intercept
+    with pytest.raises(ValueError):
+        parse_coordinate_configuration("name=x,feature.shard=s")
+
+
+def test_training_then_scoring(game_avro, tmp_path):
+    out = tmp_path / "train-out"
+    args = ["--input-data-directories", str(game_avro / "train"),
+            "--validation-data-directories", str(game_avro / "val"),
+            "--root-output-directory", str(out), "--training-task", "LOGISTIC_REGRESSION", *SHARDS,
+            "--coordinate-configurations", FIXED, "--coordinate-configurations", RANDOM,
+            "--coordinate-update-sequence", "fixed,per-user", "--coordinate-descent-iterations", "2",
+            "--evaluators", "AUC,LOGISTIC_LOSS", "--output-mode", "ALL", "--device", "cpu",
+            "--data-summary-directory", str(tmp_path / "summary"), "--data-validation", "VALIDATE_FULL"]
+    res = game_training.GameTrainingDriver(game_training.build_parser().parse_args(args)).run()
+    assert len(res["explicit"]) == 2 and res["best"] is not None
+    aucs = [r.evaluations[0][1] for r in res["explicit"]]
+    assert max(aucs) > 0.75
+    assert res["best"].evaluations[0][1] == max(aucs)
+    for d in ["best", "models/0", "models/1"]:
+        assert os.path.exists(out / d / "model-metadata.json")
+        assert os.path.exists(out / d / "model-spec")
+        assert os.path.exists(out / d / "fixed-effect" / "fixed" / "coefficients" / "part-00000.avro")
+        assert os.path.exists(out / d / "random-effect" / "per-user" / "id-info")
+    assert os.path.exists(out / "logs" / "log-message.txt")
+    assert os.path.exists(tmp_path / "summary" / "global" / "part-00000.avro")
+
+    sout = tmp_path / "score-out"
+    sargs = ["--input-data-directories", str(game_avro / "val"), "--root-output-directory", str(sout), *SHARDS,
+             "--model-input-directory", str(out / "best"), "--model-id", "m1", "--evaluators", "AUC",
+             "--device", "cpu"]
+    sres = game_scoring.GameScoringDriver(game_scoring.build_parser().parse_args(sargs)).run()
+    recs = load_scores(str(sout / "scores"))
+    assert len(recs) == 300 and all(r["modelId"] == "m1" for r in recs)
+    # scores of the saved model (coefficients < 1e-4 dropped) vs the in-memory best model
+    best_val_auc = res["best"].evaluations[0][1]
+    assert abs(sres["evaluations"][0][1] - best_val_auc) < 5e-3
+    pred = np.array([r["predictionScore"] for r in recs])
+    assert np.allclose(pred, sres["scores"].numpy() + sres["data"].offsets)
+
+
+def test_output_dir_exists_fails(game_avro, tmp_path):
+    out = tmp_path / "o"
+    out.mkdir()
+    args = ["--input-data-directories", str(game_avro / "train"), "--root-output-directory", str(out),
+            "--training-task", "LOGISTIC_REGRESSION", *SHARDS, "--coordinate-configurations", FIXED,
+            "--coordinate-update-sequence", "fixed", "--coordinate-descent-iterations", "1", "--device", "cpu"]
+    with pytest.raises(FileExistsError):
+        game_training.GameTrainingDriver(game_training.build_parser().parse_args(args)).run()
+    args += ["--override-output-directory", "true", "--output-mode", "EXPLICIT"]
+    res = game_training.GameTrainingDriver(game_training.build_parser().parse_args(args)).run()
+    # no validation data -> no evaluations; best falls back to the last explicit model
+    assert len(res["explicit"]) == 2 and os.path.exists(out / "models" / "1" / "model-spec")
+
+
+def test_hyperparameter_tuning_adds_models(game_avro, tmp_path):
+    out = tmp_path / "tuned"
+    args = ["--input-data-directories", str(game_avro / "train"),
+            "--validation-data-directories", str(game_avro / "val"),
+            "--root-output-directory", str(out), "--training-task", "LOGISTIC_REGRESSION", *SHARDS,
+            "--coordinate-configurations", FIXED.replace("10|0.1", "1"),
+            "--coordinate-update-sequence", "fixed", "--coordinate-descent-iterations", "1",
+            "--hyper-parameter-tuning", "RANDOM", "--hyper-parameter-tuning-iterations", "3",
+            "--output-mode", "TUNED", "--device", "cpu"]
+    res = game_training.GameTrainingDriver(game_training.build_parser().parse_args(args)).run()
+    assert len(res["tuned"]) == 3
+    lams = {r.config["fixed"].regularization_weight for r in res["tuned"]}
+    assert len(lams) == 3 and all(1e-4 <= l <= 1e4 for l in lams)
+    assert sorted(os.listdir(out / "models")) == ["0", "1", "2"]
