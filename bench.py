@@ -9,7 +9,8 @@ device (no datasets are available offline) — see ``photon_ml_amd/data/syntheti
 
 One STEP = one full L-BFGS iteration of the production optimizer (``photon_ml_amd.optimization.LBFGS``):
 two-loop direction + strong-Wolfe line search, where every trial point is a full pass over the local shard
-(fused CSR forward + loss, chunked CSC transpose: ``ops/csrc/glm_kernels.hip``) followed by ONE RCCL all-reduce
+(fused forward + loss over row blocks, transpose over column tiles — the gather-coalesced "tiled" layout of
+``ops/csrc/glm_kernels.hip``) followed by ONE RCCL all-reduce
 of the packed fp64 [gradient | loss | sum l'] buffer. Nothing is skipped inside the timed region.
 
 value = (total rows over all ranks) x (L-BFGS iterations) / seconds  [examples/sec/node].
@@ -42,6 +43,8 @@ def main():
     ap.add_argument("--chunk-rows", type=int, default=1 << 20)
     ap.add_argument("--l2", type=float, default=1.0)
     ap.add_argument("--seed", type=int, default=1234567890)
+    ap.add_argument("--layout", default="auto", choices=["auto", "tiled", "segmented"],
+                    help="sparse layout: tiled (gather-coalesced, default when representable) or segmented")
     args = ap.parse_args()
 
     import torch
@@ -66,9 +69,11 @@ def main():
             log(f"generated chunk {i}/{n}")
 
     data, _ = generate_device_shard(args.rows_per_gpu, args.features, args.nnz, dev, args.precision,
-                                    seed=args.seed, chunk_rows=args.chunk_rows, rank=rank, progress=progress)
+                                    seed=args.seed, chunk_rows=args.chunk_rows, rank=rank, progress=progress,
+                                    layout=args.layout)
     torch.cuda.synchronize()
-    log(f"data ready in {time.time() - t_gen:.1f}s: {data.n_rows} rows/GPU, {data.nbytes() / 2**30:.1f} GiB/GPU")
+    log(f"data ready in {time.time() - t_gen:.1f}s: {data.n_rows} rows/GPU, {data.nbytes() / 2**30:.1f} GiB/GPU, "
+        f"layout={data.layout}")
     gdata = DistributedGLMData(data) if world > 1 else data
 
     obj = GLMObjective(LOGISTIC, l2_weight=args.l2)
@@ -116,6 +121,7 @@ def main():
                 "features": args.features,
                 "nnz_per_row": args.nnz,
                 "parallelism": f"dp{world}",
+                "layout": data.layout,
             },
             "evals_per_step": passes / args.steps,
             "optimizer_stalled": stalled,

@@ -60,9 +60,10 @@ def zipf_cdf(n: int, s: float, device) -> torch.Tensor:
 
 def generate_device_shard(n_rows: int, n_features: int, nnz_per_row: int, device="cuda", precision: str = "bf16",
                           seed: int = 1234567890, chunk_rows: int = 1 << 20, zipf_s: float = 1.1,
-                          task=TaskType.LOGISTIC_REGRESSION, rank: int = 0, progress=None):
+                          task=TaskType.LOGISTIC_REGRESSION, rank: int = 0, progress=None, layout: str = "auto"):
     """Generate a :class:`DeviceGLMData` directly in device memory (see module docstring)."""
-    from ..ops.device import DeviceGLMData, SegChunk, VAL_DTYPE
+    from ..ops.device import DeviceGLMData, SegChunk, VAL_DTYPE, resolve_layout
+    from ..ops.tiled import TLFwdChunk, TLTChunk
 
     dev = torch.device(device)
     prec = {"bf16": 0, "f32": 1, "f64": 2}[precision]
@@ -73,6 +74,7 @@ def generate_device_shard(n_rows: int, n_features: int, nnz_per_row: int, device
     fs = (n_features - 1) // n_fields
     if fs < 1:
         raise ValueError("not enough features for the requested nnz per row")
+    layout = resolve_layout(layout, n_features, chunk_rows)
     cdf = zipf_cdf(fs, zipf_s, dev)
     field_base = (torch.arange(n_fields, device=dev, dtype=torch.int32) * fs)
     gen = torch.Generator(device=dev)
@@ -108,6 +110,17 @@ def generate_device_shard(n_rows: int, n_features: int, nnz_per_row: int, device
     for ci, ((a, b), (idx, val)) in enumerate(zip(zip(starts[:-1], starts[1:]), raw)):
         m = b - a
         idx = new_of_old32[idx.to(torch.int64)]
+        if layout == "tiled":
+            rp = torch.arange(0, (m + 1) * k, k, dtype=torch.int64, device=dev)
+            col = idx.to(torch.int64)
+            del idx
+            csr.append(TLFwdChunk(rp, col, val, n_features))
+            csc.append(TLTChunk(rp, col, val, n_features, chunk_rows))
+            raw[ci] = None
+            del col, val, rp
+            if progress is not None:
+                progress(ci + 1, len(starts) - 1)
+            continue
         seg_ptr = np.arange(0, (m + 1) * k, k, dtype=np.int64).astype(np.int32)
         csr.append(SegChunk(seg_ptr, idx, val, dev, forward=True))
         # CSC of the chunk: stable sort by column -> rows stay ascending inside each column segment

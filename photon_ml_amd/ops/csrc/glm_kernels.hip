@@ -29,6 +29,12 @@
 #define VEC 8            // entries per lane per load round
 #define MAXSEG 1024      // max segments per normal block
 
+#define LAUNCH_CHECK()                                         \
+  do {                                                         \
+    hipError_t e_ = hipGetLastError();                         \
+    if (e_ != hipSuccess) return (int)e_;                      \
+  } while (0)
+
 enum LossId { LOSS_LOGISTIC = 0, LOSS_POISSON = 1, LOSS_SQUARED = 2, LOSS_HINGE = 3 };
 enum FwdMode { FWD_MARGIN = 0, FWD_VALUE_GRAD = 1, FWD_HV = 2, FWD_DZZ = 3 };
 
@@ -134,6 +140,7 @@ __device__ __forceinline__ BlockDesc load_desc(const int* __restrict__ blk, int 
 // x (features relabelled by frequency, so the head is the hottest features).
 typedef int v4i __attribute__((ext_vector_type(4)));
 typedef unsigned int v4u __attribute__((ext_vector_type(4)));
+typedef unsigned int v2u __attribute__((ext_vector_type(2)));
 typedef float v4f __attribute__((ext_vector_type(4)));
 typedef double v2d __attribute__((ext_vector_type(2)));
 #define ROUNDS (NB / (NTHREADS * VEC))   // vector layout rounds (2)
@@ -551,6 +558,198 @@ __global__ __launch_bounds__(NTHREADS) void reduce_stats_l1_kernel(const double*
   if (threadIdx.x == 0) { partial[2 * blockIdx.x] = a; partial[2 * blockIdx.x + 1] = b; }
 }
 
+
+// ============================================================================================================
+// TILED LAYOUT ("TL") — gather-coalesced kernels.
+//
+// Profiling the segmented-stream kernels showed them bound by the number of DISTINCT cache lines per gather
+// instruction (~53 of 64 lanes hit different lines), not by HBM bytes. The tiled layout sorts each unit of work
+// so that the lanes of one gather instruction hit neighbouring addresses, and accumulates through wave-private
+// LDS (ds_add_f64) instead of segmented reductions:
+//   forward  : ROW BLOCKS of <= 2^rbits rows; inside a block entries are sorted by (column, row) and packed as
+//              (col << rbits) | local_row. Gathers x[col] walk the coefficient vector in order (hot columns, which
+//              are relabelled to the lowest indices, collapse onto one or two lines per instruction).
+//   transpose: COLUMN TILES of 2^cbits columns; inside a tile entries are sorted by (row, column) and packed as
+//              (local_row << cbits) | (col & (2^cbits-1)). Gathers x[row] walk the per-row vector in order.
+// Determinism: each wave owns a private LDS accumulator row and walks its entries in a fixed order, and the 4
+// wave rows are summed in a fixed order; items of a column tile that is split across work-groups write fp64
+// partial rows that a combine kernel adds IN ORDER. Results are bitwise reproducible run to run.
+// ============================================================================================================
+#define TL_VEC 4                              // entries per lane per round (16-B pack loads)
+#define TL_ROUND (64 * TL_VEC)                // entries per wave-round
+#define TL_U 2                                // wave-rounds in flight per iteration
+#define TL_WAVES (NTHREADS / 64)
+#define TL_MAXR 1024                          // max rows per forward block / columns per transpose tile
+
+template <typename VT> struct TLVals;
+template <> struct TLVals<uint16_t> {
+  static __device__ __forceinline__ void load(const uint16_t* p, double* v) {
+    const v2u u = __builtin_nontemporal_load((const v2u*)p);
+    v[0] = (double)__uint_as_float(u.x << 16); v[1] = (double)__uint_as_float(u.x & 0xffff0000u);
+    v[2] = (double)__uint_as_float(u.y << 16); v[3] = (double)__uint_as_float(u.y & 0xffff0000u);
+  }
+};
+template <> struct TLVals<float> {
+  static __device__ __forceinline__ void load(const float* p, double* v) {
+    const v4f a = __builtin_nontemporal_load((const v4f*)p);
+    v[0] = a[0]; v[1] = a[1]; v[2] = a[2]; v[3] = a[3];
+  }
+};
+template <> struct TLVals<double> {
+  static __device__ __forceinline__ void load(const double* p, double* v) {
+    const v2d a = __builtin_nontemporal_load((const v2d*)p);
+    const v2d b = __builtin_nontemporal_load((const v2d*)(p + 2));
+    v[0] = a[0]; v[1] = a[1]; v[2] = b[0]; v[3] = b[1];
+  }
+};
+
+// Stream entries [e_lo, e_hi) of one work unit: wave w walks a contiguous share of the 4-aligned window.
+// For each entry: key = pack >> sbits (gather index), slot = pack & smask (LDS accumulator slot);
+// acc[slot] += val (or val^2) * x[key + xoff].
+template <typename VT, typename XT, bool SQ>
+__device__ __forceinline__ void tl_stream(const uint32_t* __restrict__ pack, const VT* __restrict__ val,
+                                          const XT* __restrict__ x, int e_lo, int e_hi, int sbits, double* acc) {
+  const int lane = threadIdx.x & 63, w = threadIdx.x >> 6;
+  const uint32_t smask = (1u << sbits) - 1u;
+  const int lo = e_lo & ~(TL_VEC - 1);
+  const int nr = (e_hi - lo + TL_ROUND - 1) / TL_ROUND;
+  const int r0 = (nr * w) / TL_WAVES, r1 = (nr * (w + 1)) / TL_WAVES;
+  // TL_U rounds per iteration: all stream loads first, then all gathers, then the LDS accumulation
+  for (int r = r0; r < r1; r += TL_U) {
+    v4u pk[TL_U];
+    double v[TL_U][TL_VEC];
+    bool in[TL_U][TL_VEC];
+#pragma unroll
+    for (int u = 0; u < TL_U; ++u) {
+      const int e = lo + (r + u) * TL_ROUND + lane * TL_VEC;
+      const bool ok = (r + u < r1) && (e < e_hi);
+      const int es = ok ? e : lo;  // out-of-range lanes re-read the first (valid) quad; results are masked
+      pk[u] = __builtin_nontemporal_load((const v4u*)(pack + es));
+      TLVals<VT>::load(val + es, v[u]);
+#pragma unroll
+      for (int k = 0; k < TL_VEC; ++k) in[u][k] = ok && (e + k >= e_lo) && (e + k < e_hi);
+    }
+    // unconditional gathers (masked lanes read x[0]) so that all of them are in flight together
+    XT xv[TL_U][TL_VEC];
+#pragma unroll
+    for (int u = 0; u < TL_U; ++u)
+#pragma unroll
+      for (int k = 0; k < TL_VEC; ++k) xv[u][k] = x[in[u][k] ? (pk[u][k] >> sbits) : 0u];
+#pragma unroll
+    for (int u = 0; u < TL_U; ++u)
+#pragma unroll
+      for (int k = 0; k < TL_VEC; ++k) {
+        if (in[u][k]) {
+          const double vv = SQ ? v[u][k] * v[u][k] : v[u][k];
+          atomicAdd(&acc[pk[u][k] & smask], vv * static_cast<double>(xv[u][k]));
+        }
+      }
+  }
+}
+
+// Forward over row blocks. blk: 4 ints per block {row_lo, nrows, e_lo, e_hi} (chunk-local).
+template <typename VT, typename XT, typename RT>
+__global__ __launch_bounds__(NTHREADS) void tl_fwd_kernel(const int* __restrict__ blk, int rbits,
+                                                          const uint32_t* __restrict__ pack,
+                                                          const VT* __restrict__ val, const XT* __restrict__ x,
+                                                          FwdArgs<XT, RT> a, double* __restrict__ stats) {
+  __shared__ double acc[TL_WAVES][TL_MAXR];
+  __shared__ double red[2 * NTHREADS / 64];
+  const int b = blockIdx.x;
+  const int row_lo = blk[4 * b], nrows = blk[4 * b + 1], e_lo = blk[4 * b + 2], e_hi = blk[4 * b + 3];
+  for (int i = threadIdx.x; i < TL_WAVES * TL_MAXR; i += NTHREADS) (&acc[0][0])[i] = 0.0;
+  __syncthreads();
+  tl_stream<VT, XT, false>(pack, val, x, e_lo, e_hi, rbits, acc[threadIdx.x >> 6]);
+  __syncthreads();
+  double F = 0.0, S = 0.0;
+  for (int r = threadIdx.x; r < nrows; r += NTHREADS) {
+    double z = acc[0][r];
+#pragma unroll
+    for (int w = 1; w < TL_WAVES; ++w) z += acc[w][r];
+    const int s = row_lo + r;
+    fwd_finish(a, s, z, fwd_prefetch(a, s), F, S);
+  }
+  if (stats) {
+    block_sum2(F, S, red);
+    if (threadIdx.x == 0) { stats[2 * b] = F; stats[2 * b + 1] = S; }
+  }
+}
+
+// Transpose over column-tile items. items: 4 ints {tile, e_lo, e_hi, part}; part < 0: the item is its tile's
+// only one -> G[tile cols] += sums directly; else the item's row of partial sums goes to parts[part * C ...].
+template <typename VT, typename XT, bool SQ>
+__global__ __launch_bounds__(NTHREADS) void tl_t_kernel(const int* __restrict__ items, int cbits,
+                                                        const uint32_t* __restrict__ pack,
+                                                        const VT* __restrict__ val, const XT* __restrict__ x,
+                                                        double* __restrict__ G, int dim, double* __restrict__ parts) {
+  __shared__ double acc[TL_WAVES][TL_MAXR];
+  const int it = blockIdx.x;
+  const int tile = items[4 * it], e_lo = items[4 * it + 1], e_hi = items[4 * it + 2], part = items[4 * it + 3];
+  const int C = 1 << cbits;
+  for (int i = threadIdx.x; i < TL_WAVES * TL_MAXR; i += NTHREADS) (&acc[0][0])[i] = 0.0;
+  __syncthreads();
+  tl_stream<VT, XT, SQ>(pack, val, x, e_lo, e_hi, cbits, acc[threadIdx.x >> 6]);
+  __syncthreads();
+  const int c0 = tile << cbits;
+  for (int c = threadIdx.x; c < C; c += NTHREADS) {
+    double s = acc[0][c];
+#pragma unroll
+    for (int w = 1; w < TL_WAVES; ++w) s += acc[w][c];
+    if (part < 0) {
+      if (c0 + c < dim) G[c0 + c] += s;
+    } else {
+      parts[(size_t)part * C + c] = s;
+    }
+  }
+}
+
+// Combine the partial rows of split tiles in item order: mt_tiles[t], parts mt_ptr[t]..mt_ptr[t+1]-1.
+__global__ __launch_bounds__(NTHREADS) void tl_t_combine_kernel(const int* __restrict__ mt_tiles,
+                                                                const int* __restrict__ mt_ptr, int cbits,
+                                                                const double* __restrict__ parts,
+                                                                double* __restrict__ G, int dim) {
+  const int t = blockIdx.x;
+  const int C = 1 << cbits;
+  const int p0 = mt_ptr[t], p1 = mt_ptr[t + 1];
+  const int c0 = mt_tiles[t] << cbits;
+  for (int c = threadIdx.x; c < C; c += NTHREADS) {
+    double s = 0.0;
+    for (int p = p0; p < p1; ++p) s += parts[(size_t)p * C + c];
+    if (c0 + c < dim) G[c0 + c] += s;
+  }
+}
+
+struct TLFwdDesc { const int* blk; int nblk; int rbits; const uint32_t* pack; const void* val; };
+struct TLTDesc {
+  const int* items; int nitems; int cbits; const uint32_t* pack; const void* val;
+  const int* mt_tiles; const int* mt_ptr; int nmt; int dim;
+};
+
+template <typename VT, typename XT, typename RT>
+static int tl_fwd_impl(const TLFwdDesc* c, const void* x, FwdArgs<XT, RT> a, double* stats, hipStream_t st) {
+  if (c->nblk <= 0) return 0;
+  if (c->rbits < 1 || (1 << c->rbits) > TL_MAXR) return -22;
+  hipLaunchKernelGGL((tl_fwd_kernel<VT, XT, RT>), dim3(c->nblk), dim3(NTHREADS), 0, st, c->blk, c->rbits,
+                     c->pack, (const VT*)c->val, (const XT*)x, a, stats);
+  LAUNCH_CHECK();
+  return 0;
+}
+
+template <typename VT, typename XT, bool SQ>
+static int tl_t_impl(const TLTDesc* c, const void* x, double* G, double* parts, hipStream_t st) {
+  if (c->nitems <= 0) return 0;
+  if (c->cbits < 1 || (1 << c->cbits) > TL_MAXR) return -22;
+  hipLaunchKernelGGL((tl_t_kernel<VT, XT, SQ>), dim3(c->nitems), dim3(NTHREADS), 0, st, c->items, c->cbits,
+                     c->pack, (const VT*)c->val, (const XT*)x, G, c->dim, parts);
+  LAUNCH_CHECK();
+  if (c->nmt > 0) {
+    hipLaunchKernelGGL(tl_t_combine_kernel, dim3(c->nmt), dim3(NTHREADS), 0, st, c->mt_tiles, c->mt_ptr, c->cbits,
+                       parts, G, c->dim);
+    LAUNCH_CHECK();
+  }
+  return 0;
+}
+
 // ============================================================================================================
 // C ABI
 // ============================================================================================================
@@ -562,11 +761,6 @@ struct SegChunkDesc {
   const int* long_seg; const int* long_ptr; int nlong; int npart;
 };
 
-#define LAUNCH_CHECK()                                         \
-  do {                                                         \
-    hipError_t e_ = hipGetLastError();                         \
-    if (e_ != hipSuccess) return (int)e_;                      \
-  } while (0)
 
 static int g_ablate = 0;
 // Runtime kernel configuration (set from Python): lane layout per direction, hot-table size, persistent grid.
@@ -738,6 +932,34 @@ int pml_reduce_stats(const double* stats, int n, double* out, int accumulate, do
   hipLaunchKernelGGL(reduce_stats_kernel, dim3(1), dim3(NTHREADS), 0, st, scratch, nwg, out, accumulate);
   LAUNCH_CHECK();
   return 0;
+}
+
+// ---- tiled layout entry points ------------------------------------------------------------------------------
+int pml_tl_maxr() { return TL_MAXR; }
+
+int pml_tl_fwd(int prec, const TLFwdDesc* c, const void* x, int mode, int loss, double shift, const void* y,
+               const void* off, const void* wt, void* coef, void* dzz, double* z_out, int with_offset,
+               double* stats, void* stream) {
+  hipStream_t st = (hipStream_t)stream;
+  if (prec == 2) {
+    FwdArgs<double, double> a{mode, loss, shift, (const double*)y, (const double*)off, (const double*)wt,
+                              (double*)coef, (double*)dzz, z_out, with_offset, 0, 0};
+    return tl_fwd_impl<double, double, double>(c, x, a, stats, st);
+  }
+  FwdArgs<float, float> a{mode, loss, shift, (const float*)y, (const float*)off, (const float*)wt,
+                          (float*)coef, (float*)dzz, z_out, with_offset, 0, 0};
+  if (prec == 1) return tl_fwd_impl<float, float, float>(c, x, a, stats, st);
+  return tl_fwd_impl<uint16_t, float, float>(c, x, a, stats, st);
+}
+
+int pml_tl_t(int prec, const TLTDesc* c, const void* x, int square, double* G, double* parts, void* stream) {
+  hipStream_t st = (hipStream_t)stream;
+  if (prec == 2) return square ? tl_t_impl<double, double, true>(c, x, G, parts, st)
+                               : tl_t_impl<double, double, false>(c, x, G, parts, st);
+  if (prec == 1) return square ? tl_t_impl<float, float, true>(c, x, G, parts, st)
+                               : tl_t_impl<float, float, false>(c, x, G, parts, st);
+  return square ? tl_t_impl<uint16_t, float, true>(c, x, G, parts, st)
+                : tl_t_impl<uint16_t, float, false>(c, x, G, parts, st);
 }
 
 }  // extern "C"

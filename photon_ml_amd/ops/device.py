@@ -26,6 +26,23 @@ import torch
 from ..data.matrix import LabeledData
 from .native import SegChunkDesc, check, require_glm_lib, stream_handle
 from .reference import GLMComputable
+from .tiled import DEFAULT_ITEM_ENTRIES, TLFwdChunk, TLTChunk, tl_supported
+
+LAYOUTS = ("auto", "tiled", "segmented")
+
+
+def resolve_layout(layout: str, dim: int, chunk_rows: int) -> str:
+    """``auto`` -> tiled when the packing can represent the shape (PML_LAYOUT env overrides ``auto``)."""
+    import os
+    if layout == "auto":
+        layout = os.environ.get("PML_LAYOUT", "auto")
+    if layout not in LAYOUTS:
+        raise ValueError(f"unknown layout {layout}")
+    if layout == "auto":
+        layout = "tiled" if tl_supported(dim, chunk_rows) else "segmented"
+    if layout == "tiled" and not tl_supported(dim, chunk_rows):
+        raise ValueError(f"tiled layout cannot pack dim={dim} with chunk_rows={chunk_rows}")
+    return layout
 
 PRECISIONS = {"bf16": 0, "f32": 1, "f64": 2}
 VAL_DTYPE = {0: torch.bfloat16, 1: torch.float32, 2: torch.float64}
@@ -81,6 +98,16 @@ class SegChunk:
                                  self.idx.data_ptr(), self.val.data_ptr(), self.long_seg.data_ptr(),
                                  self.long_ptr.data_ptr(), self.nlong, self.npart)
 
+    kind = "seg"
+
+    @property
+    def nstats(self) -> int:
+        return self.nblk
+
+    @property
+    def parts_needed(self) -> int:
+        return self.npart
+
     def nbytes(self) -> int:
         return sum(t.numel() * t.element_size() for t in (self.seg_ptr, self.blk, self.long_seg, self.long_ptr,
                                                            self.idx, self.val))
@@ -111,11 +138,12 @@ class DeviceGLMData(GLMComputable):
         self._dzz_key: Optional[torch.Tensor] = None
         self._dzz_shift = None
         # scratch
-        self.blk_off = np.cumsum([0] + [c.nblk for c in csr]).tolist()
-        self.long_off = np.cumsum([0] + [c.nlong for c in csr]).tolist()
+        self.layout = "tiled" if csr and csr[0].kind == "tl" else "segmented"
+        self.blk_off = np.cumsum([0] + [c.nstats for c in csr]).tolist()
+        self.long_off = np.cumsum([0] + [getattr(c, "nlong", 0) for c in csr]).tolist()
         self.stats = torch.zeros(2 * max(self.blk_off[-1], 1), dtype=torch.float64, device=self.device)
         self.long_stats = torch.zeros(2 * max(self.long_off[-1], 1), dtype=torch.float64, device=self.device)
-        maxpart = max([c.npart for c in csr + csc] + [1])
+        maxpart = max([c.parts_needed for c in csr + csc] + [1])
         self.parts = torch.zeros(maxpart, dtype=torch.float64, device=self.device)
         self.red_scratch = torch.zeros(512, dtype=torch.float64, device=self.device)
         self.out2 = torch.zeros(2, dtype=torch.float64, device=self.device)
@@ -130,7 +158,7 @@ class DeviceGLMData(GLMComputable):
     # ------------------------------------------------------------------
     @staticmethod
     def from_labeled(data: LabeledData, device="cuda", precision: str = "f64", chunk_rows: int = 1 << 20,
-                     relabel: bool = True):
+                     relabel: bool = True, layout: str = "auto", item_entries: int = DEFAULT_ITEM_ENTRIES):
         prec = PRECISIONS[precision]
         vdt = VAL_DTYPE[prec]
         dev = torch.device(device)
@@ -148,8 +176,16 @@ class DeviceGLMData(GLMComputable):
         if n == 0:
             starts = [0, 0]
         csr, csc = [], []
+        layout = resolve_layout(layout, d, chunk_rows)
         for a, b in zip(starts[:-1], starts[1:]):
             xc = x[a:b]
+            if layout == "tiled":
+                rp = torch.from_numpy((xc.indptr - xc.indptr[0]).astype(np.int64)).to(dev)
+                col = torch.from_numpy(xc.indices.astype(np.int64)).to(dev)
+                val = torch.from_numpy(xc.data.astype(np.float64)).to(dev).to(vdt)
+                csr.append(TLFwdChunk(rp, col, val, d))
+                csc.append(TLTChunk(rp, col, val, d, chunk_rows, item_entries=item_entries))
+                continue
             sp_ = (xc.indptr - xc.indptr[0]).astype(np.int32)
             csr.append(SegChunk(sp_, torch.from_numpy(xc.indices.astype(np.int32)),
                                 torch.from_numpy(xc.data.astype(np.float64)).to(vdt), dev, forward=True))
@@ -179,6 +215,14 @@ class DeviceGLMData(GLMComputable):
              stats: bool = True):
         ch = self.csr[c]
         st = self.stats.data_ptr() + 2 * 8 * self.blk_off[c] if stats else None
+        if ch.kind == "tl":
+            check(self.lib.pml_tl_fwd(
+                self.prec, ctypes.byref(ch.desc), x.data_ptr(), mode, loss_id, float(shift),
+                self._rows(self.y, c), self._rows(self.o, c), self._rows(self.wt, c),
+                None if coef is None else self._rows(coef, c), None if dzz is None else self._rows(dzz, c),
+                None if z_out is None else self._rows(z_out, c), with_offset, st, stream_handle(self.device)),
+                "tl_fwd")
+            return
         lst = self.long_stats.data_ptr() + 2 * 8 * self.long_off[c] if stats else None
         check(self.lib.pml_seg_fwd(
             self.prec, ctypes.byref(ch.desc), x.data_ptr(), mode, loss_id, float(shift),
@@ -189,6 +233,10 @@ class DeviceGLMData(GLMComputable):
 
     def _t(self, c: int, x: torch.Tensor, G: torch.Tensor, square: int = 0):
         ch = self.csc[c]
+        if ch.kind == "tl":
+            check(self.lib.pml_tl_t(self.prec, ctypes.byref(ch.desc), self._rows(x, c), square, G.data_ptr(),
+                                    self.parts.data_ptr(), stream_handle(self.device)), "tl_t")
+            return
         check(self.lib.pml_seg_t(self.prec, ctypes.byref(ch.desc), self._rows(x, c), square, G.data_ptr(),
                                  self.parts.data_ptr(), stream_handle(self.device)), "seg_t")
 

@@ -31,6 +31,17 @@ class SegChunkDesc(ctypes.Structure):
     ]
 
 
+class TLFwdDesc(ctypes.Structure):
+    _fields_ = [("blk", c_void_p), ("nblk", c_int), ("rbits", c_int), ("pack", c_void_p), ("val", c_void_p)]
+
+
+class TLTDesc(ctypes.Structure):
+    _fields_ = [
+        ("items", c_void_p), ("nitems", c_int), ("cbits", c_int), ("pack", c_void_p), ("val", c_void_p),
+        ("mt_tiles", c_void_p), ("mt_ptr", c_void_p), ("nmt", c_int), ("dim", c_int),
+    ]
+
+
 _LIBS = {}
 
 
@@ -62,7 +73,11 @@ def glm_lib() -> Optional[ctypes.CDLL]:
         lib.pml_seg_t.argtypes = [c_int, ctypes.POINTER(SegChunkDesc), c_void_p, c_int, c_void_p, c_void_p,
                                   c_void_p]
         lib.pml_reduce_stats.argtypes = [c_void_p, c_int, c_void_p, c_int, c_void_p, c_void_p]
-        for f in ("pml_seg_fwd", "pml_seg_t", "pml_reduce_stats", "pml_build_blocks"):
+        lib.pml_tl_fwd.argtypes = [c_int, ctypes.POINTER(TLFwdDesc), c_void_p, c_int, c_int, c_double, c_void_p,
+                                   c_void_p, c_void_p, c_void_p, c_void_p, c_void_p, c_int, c_void_p, c_void_p]
+        lib.pml_tl_t.argtypes = [c_int, ctypes.POINTER(TLTDesc), c_void_p, c_int, c_void_p, c_void_p, c_void_p]
+        for f in ("pml_seg_fwd", "pml_seg_t", "pml_reduce_stats", "pml_build_blocks", "pml_tl_fwd", "pml_tl_t",
+                  "pml_tl_maxr"):
             getattr(lib, f).restype = c_int
         lib.pml_set_config.argtypes = [c_int, c_int, c_int, c_int]
         lib._pml_typed = True

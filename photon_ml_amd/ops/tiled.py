@@ -1,0 +1,180 @@
+"""Tiled ("TL") sparse layout for the gather-coalesced HIP kernels (``glm_kernels.hip``, section TILED LAYOUT).
+
+One row chunk of a feature shard is stored twice:
+
+* forward copy — ROW BLOCKS of ``2^rbits`` consecutive rows; inside a block the entries are sorted by
+  (column, row) and packed into one uint32 ``(col << rbits) | local_row``. Block table: ``{row_lo, nrows, e_lo,
+  e_hi}``. ``rbits = min(10, 32 - bits(D))``.
+* transpose copy — COLUMN TILES of ``2^cbits`` columns; inside a tile entries are sorted by (row, column) and
+  packed as ``(local_row << cbits) | (col & (2^cbits - 1))``; a tile is cut into work items of at most
+  ``item_entries`` entries. Item table: ``{tile, e_lo, e_hi, part}`` with ``part = -1`` for single-item tiles
+  and a partial-row index otherwise; split tiles are combined in item order (deterministic).
+  ``cbits = min(10, 32 - bits(chunk_rows))``.
+
+The builders run with torch ops on the data's device (GPU sort for the 100M-entry bench chunks, CPU in tests).
+Values keep the shard precision (bf16 / fp32 / fp64). Both copies cost 4 B + sizeof(value) per entry, the same
+as the segmented-stream CSR/CSC pair they replace. Shapes the packing cannot represent (``D > 2^27`` or chunks
+of more than 2^27 rows) fall back to the segmented-stream layout (:mod:`photon_ml_amd.ops.device`).
+"""
+from __future__ import annotations
+
+from typing import Optional
+
+import numpy as np
+import torch
+
+from .native import TLFwdDesc, TLTDesc
+
+TL_MAXBITS = 10          # 2^10 = TL_MAXR rows per block / columns per tile (LDS: 4 waves x 1024 fp64)
+TL_MINBITS = 5
+DEFAULT_ITEM_ENTRIES = 1 << 16
+_PAD = 8                 # kernels read 4-entry quads; pad so that the last quad stays in bounds
+
+
+def _bits(n: int) -> int:
+    return max(1, int(n - 1).bit_length())
+
+
+def fwd_bits(dim: int) -> Optional[int]:
+    r = min(TL_MAXBITS, 32 - _bits(dim))
+    return r if r >= TL_MINBITS else None
+
+
+def t_bits(chunk_rows: int) -> Optional[int]:
+    c = min(TL_MAXBITS, 32 - _bits(chunk_rows))
+    return c if c >= TL_MINBITS else None
+
+
+def tl_supported(dim: int, chunk_rows: int) -> bool:
+    return fwd_bits(dim) is not None and t_bits(chunk_rows) is not None
+
+
+def _to_u32_bits(x64: torch.Tensor) -> torch.Tensor:
+    """int64 values in [0, 2^32) -> int32 tensor with the same low 32 bits (the kernels read uint32)."""
+    return torch.where(x64 >= (1 << 31), x64 - (1 << 32), x64).to(torch.int32)
+
+
+def _pad(t: torch.Tensor) -> torch.Tensor:
+    return torch.cat([t, torch.zeros(_PAD, dtype=t.dtype, device=t.device)]).contiguous()
+
+
+class TLFwdChunk:
+    """Forward copy of one row chunk (``m`` rows)."""
+
+    kind = "tl"
+
+    def __init__(self, rowptr: torch.Tensor, col: torch.Tensor, val: torch.Tensor, dim: int,
+                 rbits: Optional[int] = None):
+        dev = val.device
+        rowptr = rowptr.to(dev, torch.int64)
+        col = col.to(dev, torch.int64)
+        m = rowptr.numel() - 1
+        self.rbits = fwd_bits(dim) if rbits is None else rbits
+        if self.rbits is None:
+            raise ValueError(f"tiled forward layout cannot pack dim={dim}")
+        R = 1 << self.rbits
+        nnz = col.numel()
+        rows = torch.repeat_interleave(torch.arange(m, device=dev), rowptr[1:] - rowptr[:-1]) if nnz else \
+            torch.zeros(0, dtype=torch.int64, device=dev)
+        pack = (col << self.rbits) | (rows & (R - 1))
+        key = ((rows >> self.rbits) << 32) | pack
+        key, perm = torch.sort(key, stable=True)
+        self.pack = _pad(_to_u32_bits(key & 0xFFFFFFFF))
+        self.val = _pad(val[perm].contiguous())
+        del key, perm, rows
+        nblk = (m + R - 1) // R
+        b = torch.arange(nblk, device=dev)
+        lo = b * R
+        hi = torch.clamp(lo + R, max=m)
+        self.blk = torch.stack([lo, hi - lo, rowptr[lo], rowptr[hi]], 1).to(torch.int32).contiguous()
+        self.nblk, self.m, self.nnz = nblk, m, nnz
+        self.desc = TLFwdDesc(self.blk.data_ptr(), nblk, self.rbits, self.pack.data_ptr(), self.val.data_ptr())
+
+    @property
+    def nstats(self) -> int:
+        return self.nblk
+
+    def nbytes(self) -> int:
+        return sum(t.numel() * t.element_size() for t in (self.blk, self.pack, self.val))
+
+    # host emulation of the kernel arithmetic (tests / CPU fallback)
+    def emulate_matvec(self, x: torch.Tensor) -> torch.Tensor:
+        p = self.pack[: self.nnz].to(torch.int64) & 0xFFFFFFFF
+        col = p >> self.rbits
+        blk_of_entry = torch.repeat_interleave(torch.arange(self.nblk, device=p.device),
+                                               (self.blk[:, 3] - self.blk[:, 2]).to(torch.int64))
+        row = (blk_of_entry << self.rbits) + (p & ((1 << self.rbits) - 1))
+        z = torch.zeros(self.m, dtype=torch.float64, device=p.device)
+        return z.index_add_(0, row, self.val[: self.nnz].to(torch.float64) * x.to(torch.float64)[col])
+
+
+class TLTChunk:
+    """Transpose copy of one row chunk."""
+
+    kind = "tl"
+
+    def __init__(self, rowptr: torch.Tensor, col: torch.Tensor, val: torch.Tensor, dim: int, chunk_rows: int,
+                 cbits: Optional[int] = None, item_entries: int = DEFAULT_ITEM_ENTRIES):
+        dev = val.device
+        rowptr = rowptr.to(dev, torch.int64)
+        col = col.to(dev, torch.int64)
+        m = rowptr.numel() - 1
+        self.cbits = t_bits(max(chunk_rows, m)) if cbits is None else cbits
+        if self.cbits is None:
+            raise ValueError(f"tiled transpose layout cannot pack chunk_rows={chunk_rows}")
+        C = 1 << self.cbits
+        nnz = col.numel()
+        rows = torch.repeat_interleave(torch.arange(m, device=dev), rowptr[1:] - rowptr[:-1]) if nnz else \
+            torch.zeros(0, dtype=torch.int64, device=dev)
+        tile = col >> self.cbits
+        pack = (rows << self.cbits) | (col & (C - 1))
+        key = (tile << 32) | pack
+        del rows, pack
+        key, perm = torch.sort(key, stable=True)
+        self.pack = _pad(_to_u32_bits(key & 0xFFFFFFFF))
+        self.val = _pad(val[perm].contiguous())
+        del key, perm
+        ntiles = (dim + C - 1) // C
+        counts = torch.bincount(tile, minlength=ntiles).cpu().numpy().astype(np.int64)
+        del tile
+        tptr = np.concatenate([[0], np.cumsum(counts)])
+        nz = np.nonzero(counts)[0]
+        n_it = np.maximum(1, -(-counts[nz] // item_entries))
+        items, mt_tiles, mt_ptr = [], [], [0]
+        part = 0
+        for t, k in zip(nz.tolist(), n_it.tolist()):
+            a, b = int(tptr[t]), int(tptr[t + 1])
+            cuts = [a + (b - a) * i // k for i in range(k + 1)]
+            for i in range(k):
+                items.append((t, cuts[i], cuts[i + 1], -1 if k == 1 else part + i))
+            if k > 1:
+                part += k
+                mt_tiles.append(t)
+                mt_ptr.append(part)
+        self.nitems, self.nmt, self.nparts = len(items), len(mt_tiles), part
+        self.items = torch.tensor(np.asarray(items, dtype=np.int32).reshape(-1, 4), device=dev)
+        self.mt_tiles = torch.tensor(np.asarray(mt_tiles or [0], dtype=np.int32), device=dev)
+        self.mt_ptr = torch.tensor(np.asarray(mt_ptr, dtype=np.int32), device=dev)
+        self.m, self.nnz, self.dim = m, nnz, dim
+        self.desc = TLTDesc(self.items.data_ptr(), self.nitems, self.cbits, self.pack.data_ptr(),
+                            self.val.data_ptr(), self.mt_tiles.data_ptr(), self.mt_ptr.data_ptr(), self.nmt, dim)
+
+    @property
+    def parts_needed(self) -> int:
+        return self.nparts << self.cbits
+
+    def nbytes(self) -> int:
+        return sum(t.numel() * t.element_size() for t in (self.items, self.mt_tiles, self.mt_ptr, self.pack,
+                                                           self.val))
+
+    def emulate_rmatvec(self, r: torch.Tensor, square: bool = False) -> torch.Tensor:
+        p = self.pack[: self.nnz].to(torch.int64) & 0xFFFFFFFF
+        row = p >> self.cbits
+        tile_of_entry = torch.repeat_interleave(self.items[:, 0].to(torch.int64),
+                                                (self.items[:, 2] - self.items[:, 1]).to(torch.int64))
+        col = (tile_of_entry << self.cbits) + (p & ((1 << self.cbits) - 1))
+        v = self.val[: self.nnz].to(torch.float64)
+        if square:
+            v = v * v
+        g = torch.zeros(self.dim, dtype=torch.float64, device=p.device)
+        return g.index_add_(0, col, v * r.to(torch.float64)[row])

@@ -21,6 +21,7 @@ def main():
     ap.add_argument("--chunk-rows", type=int, nargs="+", default=[1 << 20])
     ap.add_argument("--precision", default="bf16")
     ap.add_argument("--reps", type=int, default=5)
+    ap.add_argument("--layout", default="auto")
     ap.add_argument("--ablate", type=int, nargs="+", default=[0])
     ap.add_argument("--configs", default="0,1,8192", help="semicolon list of fwd_strided,t_strided,hot_n")
     args = ap.parse_args()
@@ -35,7 +36,7 @@ def main():
             cache.clear()
             torch.cuda.empty_cache()
             cache[cr] = generate_device_shard(args.rows, args.features, args.nnz, "cuda", args.precision,
-                                              chunk_rows=cr)
+                                              chunk_rows=cr, layout=args.layout)
         data, w = cache[cr]
         lib.pml_set_ablate(abl)
         configure(fwd_strided=cfg[0], t_strided=cfg[1], hot_n=cfg[2])
@@ -69,7 +70,8 @@ def main():
         r = {"cfg": cfg, "ablate": abl, "chunk_rows": cr, "rows": args.rows, "fwd_ms": min(tf), "t_ms": min(tt), "pass_ms": tp,
              "fwd_GBps": bytes_per / min(tf) / 1e6, "t_GBps": bytes_per / min(tt) / 1e6,
              "stream_GB": bytes_per / 1e9, "nblk_fwd": sum(c.nblk for c in data.csr),
-             "nblk_t": sum(c.nblk for c in data.csc), "nlong_t": sum(c.nlong for c in data.csc)}
+             "nblk_t": sum(getattr(c, "nblk", getattr(c, "nitems", 0)) for c in data.csc),
+             "nlong_t": sum(getattr(c, "nlong", 0) for c in data.csc), "layout": data.layout}
         print(json.dumps(r), flush=True)
         res.append(r)
 

@@ -43,16 +43,22 @@ def _round_bf16(data: LabeledData) -> LabeledData:
     return LabeledData(x, data.y, data.offsets, data.weights)
 
 
+LAYOUTS = ["tiled", "segmented"]
+
+
+@pytest.mark.parametrize("layout", LAYOUTS)
 @pytest.mark.parametrize("chunk_rows", [1500, 8192])
 @pytest.mark.parametrize("precision", ["f64", "f32", "bf16"])
 @pytest.mark.parametrize("loss", [LOGISTIC, POISSON, SQUARED, SMOOTHED_HINGE])
-def test_value_grad_parity(precision, loss, chunk_rows):
+def test_value_grad_parity(precision, loss, chunk_rows, layout):
     from photon_ml_amd.ops.device import DeviceGLMData
     data = make_data(n=9000, d=6000 if precision == "f64" else 700, density=0.005)
     if precision == "bf16":
         data = _round_bf16(data)
     ref = TorchGLMData(data, "cpu")
-    dev = DeviceGLMData.from_labeled(data, "cuda", precision, chunk_rows=chunk_rows)
+    dev = DeviceGLMData.from_labeled(data, "cuda", precision, chunk_rows=chunk_rows, layout=layout,
+                                     item_entries=20000)
+    assert dev.layout == layout
     rng = np.random.default_rng(1)
     w = torch.from_numpy(rng.normal(size=data.n_features) * 0.05)
     if precision != "f64":
@@ -69,13 +75,14 @@ def test_value_grad_parity(precision, loss, chunk_rows):
     assert f2 == f1 and s2 == s1 and torch.equal(g2, g1)
 
 
+@pytest.mark.parametrize("layout", LAYOUTS)
 @pytest.mark.parametrize("precision", ["f64", "f32"])
 @pytest.mark.parametrize("loss", [LOGISTIC, POISSON, SQUARED])
-def test_hessian_parity(precision, loss):
+def test_hessian_parity(precision, loss, layout):
     from photon_ml_amd.ops.device import DeviceGLMData
     data = make_data(n=4000, d=5000, density=0.01, seed=3)
     ref = TorchGLMData(data, "cpu")
-    dev = DeviceGLMData.from_labeled(data, "cuda", precision, chunk_rows=1024)
+    dev = DeviceGLMData.from_labeled(data, "cuda", precision, chunk_rows=1024, layout=layout)
     dev.track_hessian = True
     rng = np.random.default_rng(2)
     w = torch.from_numpy(rng.normal(size=data.n_features) * 0.05).float().double()
@@ -96,24 +103,41 @@ def test_hessian_parity(precision, loss):
     assert torch.allclose(d1.cpu(), d0, rtol=tol * 10, atol=tol * 10 * float(d0.abs().max()))
 
 
+@pytest.mark.parametrize("layout", LAYOUTS)
 @pytest.mark.parametrize("precision", ["f64", "bf16"])
-def test_margins(precision):
+def test_margins(precision, layout):
     from photon_ml_amd.ops.device import DeviceGLMData
     data = make_data(n=3000, d=300, density=0.05, seed=5)
     if precision == "bf16":
         data = _round_bf16(data)
     ref = TorchGLMData(data, "cpu")
-    dev = DeviceGLMData.from_labeled(data, "cuda", precision, chunk_rows=700)
+    dev = DeviceGLMData.from_labeled(data, "cuda", precision, chunk_rows=700, layout=layout)
     w = torch.from_numpy(np.random.default_rng(0).normal(size=300)).float().double()
     z0 = ref.margins(w, 0.5, with_offsets=True)
     z1 = dev.margins(w.cuda(), 0.5, with_offsets=True).cpu()
     assert torch.allclose(z1, z0, rtol=TOL[precision], atol=TOL[precision] * 10)
 
 
-def test_empty_and_tiny_shards():
+@pytest.mark.parametrize("layout", LAYOUTS)
+def test_empty_and_tiny_shards(layout):
     from photon_ml_amd.ops.device import DeviceGLMData
     data = LabeledData(sp.csr_matrix((3, 4)), np.array([0.0, 1.0, 1.0]))
-    dev = DeviceGLMData.from_labeled(data, "cuda", "f64")
+    dev = DeviceGLMData.from_labeled(data, "cuda", "f64", layout=layout)
     f, s, g = dev.value_grad_sums(LOGISTIC, torch.zeros(4, dtype=torch.float64, device="cuda"), 0.0)
     assert abs(f - 3 * np.log(2)) < 1e-12
     assert torch.all(g == 0)
+
+
+def test_device_shard_layouts_agree():
+    """On-device synthetic shard (bench generator): tiled and segmented layouts give the same objective."""
+    from photon_ml_amd.data.synthetic import generate_device_shard
+    out = {}
+    for layout in LAYOUTS:
+        data, _ = generate_device_shard(300_000, 200_000, 40, "cuda", "bf16", seed=5, chunk_rows=1 << 17,
+                                        layout=layout)
+        assert data.layout == layout
+        w = torch.randn(200_000, generator=torch.Generator().manual_seed(0), dtype=torch.float64) * 0.05
+        out[layout] = data.value_grad_sums(LOGISTIC, w.float().double().cuda(), 0.0)
+    (f0, s0, g0), (f1, s1, g1) = out["segmented"], out["tiled"]
+    assert abs(f1 - f0) <= 1e-5 * abs(f0) and abs(s1 - s0) <= 1e-4 * max(1.0, abs(s0))
+    assert torch.allclose(g1, g0, rtol=1e-4, atol=1e-4 * float(g0.abs().max()))

@@ -1,0 +1,46 @@
+"""Tiled (TL) layout construction on the CPU: packing, block/item tables and a host emulation of the kernels'
+arithmetic against scipy (the GPU kernels are checked against the same reference in test_kernels_gpu.py)."""
+import numpy as np
+import pytest
+import scipy.sparse as sp
+import torch
+
+from photon_ml_amd.ops.tiled import TLFwdChunk, TLTChunk, fwd_bits, t_bits, tl_supported
+
+
+@pytest.mark.parametrize("m,d,dens,item", [(3000, 500, 0.05, 64), (5000, 70000, 0.0005, 1 << 16), (100, 7, 0.5, 8),
+                                           (2048, 4096, 0.01, 300), (10, 3, 0.0, 64)])
+def test_tl_emulation_matches_scipy(m, d, dens, item):
+    rng = np.random.default_rng(0)
+    x = sp.random(m, d, density=dens, format="csr", random_state=1)
+    x.data = rng.normal(size=x.nnz)
+    rp = torch.from_numpy(x.indptr.astype(np.int64))
+    col = torch.from_numpy(x.indices.astype(np.int64))
+    val = torch.from_numpy(x.data)
+    f = TLFwdChunk(rp, col, val, d)
+    t = TLTChunk(rp, col, val, d, m, item_entries=item)
+    w = rng.normal(size=d)
+    r = rng.normal(size=m)
+    np.testing.assert_allclose(f.emulate_matvec(torch.from_numpy(w)).numpy(), x @ w, atol=1e-12)
+    np.testing.assert_allclose(t.emulate_rmatvec(torch.from_numpy(r)).numpy(), x.T @ r, atol=1e-12)
+    np.testing.assert_allclose(t.emulate_rmatvec(torch.from_numpy(r), square=True).numpy(),
+                               x.multiply(x).T @ r, atol=1e-12)
+    # tables: blocks cover rows in order, items cover every entry exactly once, tile by tile
+    b = f.blk.numpy()
+    assert b[0, 0] == 0 and (b[1:, 0] == b[:-1, 0] + b[:-1, 1]).all() and b[-1, 0] + b[-1, 1] == m
+    it = t.items.numpy()
+    if len(it):
+        assert it[0, 1] == 0 and (it[1:, 1] == it[:-1, 2]).all() and it[-1, 2] == x.nnz
+        assert (it[:, 2] - it[:, 1] <= item).all()
+        assert t.nparts == int((it[:, 3] >= 0).sum())
+    # forward blocks: entries sorted by column inside a block; transpose tiles: sorted by row
+    p = f.pack[: x.nnz].to(torch.int64).numpy() & 0xFFFFFFFF
+    for lo, hi in b[:, 2:]:
+        cols = p[lo:hi] >> f.rbits
+        assert (np.diff(cols) >= 0).all()
+
+
+def test_bits():
+    assert fwd_bits(1_000_000) == 10 and t_bits(1 << 20) == 10
+    assert fwd_bits(1 << 26) == 6 and fwd_bits(1 << 28) is None
+    assert not tl_supported(1 << 28, 1 << 20) and tl_supported(1 << 24, 1 << 22)
