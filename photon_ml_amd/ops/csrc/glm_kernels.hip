@@ -703,26 +703,45 @@ __global__ __launch_bounds__(NTHREADS) void tl_t_kernel(const int* __restrict__ 
   }
 }
 
-// Combine the partial rows of split tiles in item order: mt_tiles[t], parts mt_ptr[t]..mt_ptr[t+1]-1.
-__global__ __launch_bounds__(NTHREADS) void tl_t_combine_kernel(const int* __restrict__ mt_tiles,
-                                                                const int* __restrict__ mt_ptr, int cbits,
-                                                                const double* __restrict__ parts,
-                                                                double* __restrict__ G, int dim) {
-  const int t = blockIdx.x;
+// Combine the partial rows of split tiles, deterministically, in two levels (a hot tile can have hundreds of
+// items: one work-group per tile would serialise its whole partial block):
+//   level 1: unit u sums parts [cu[3u+1], cu[3u+2]) (<= TL_SEG consecutive items of one tile) -> l1[u * C + c]
+//   level 2: tile t (blockIdx.x) sums its units [mt_ptr[t], mt_ptr[t+1]) in order, one column per thread
+//            (blockIdx.y = column group), and adds into G.
+__global__ __launch_bounds__(NTHREADS) void tl_t_combine1_kernel(const int* __restrict__ cu, int cbits,
+                                                                 const double* __restrict__ parts,
+                                                                 double* __restrict__ l1) {
+  const int u = blockIdx.x;
   const int C = 1 << cbits;
-  const int p0 = mt_ptr[t], p1 = mt_ptr[t + 1];
-  const int c0 = mt_tiles[t] << cbits;
+  const int p0 = cu[3 * u + 1], p1 = cu[3 * u + 2];
   for (int c = threadIdx.x; c < C; c += NTHREADS) {
     double s = 0.0;
     for (int p = p0; p < p1; ++p) s += parts[(size_t)p * C + c];
-    if (c0 + c < dim) G[c0 + c] += s;
+    l1[(size_t)u * C + c] = s;
   }
+}
+
+__global__ __launch_bounds__(NTHREADS) void tl_t_combine2_kernel(const int* __restrict__ mt_tiles,
+                                                                 const int* __restrict__ mt_ptr, int cbits,
+                                                                 const double* __restrict__ l1,
+                                                                 double* __restrict__ G, int dim) {
+  const int t = blockIdx.x;
+  const int C = 1 << cbits;
+  const int c = blockIdx.y * NTHREADS + threadIdx.x;
+  if (c >= C) return;
+  const int u0 = mt_ptr[t], u1 = mt_ptr[t + 1];
+  double s = 0.0;
+  for (int u = u0; u < u1; ++u) s += l1[(size_t)u * C + c];
+  const int col = (mt_tiles[t] << cbits) + c;
+  if (col < dim) G[col] += s;
 }
 
 struct TLFwdDesc { const int* blk; int nblk; int rbits; const uint32_t* pack; const void* val; };
 struct TLTDesc {
   const int* items; int nitems; int cbits; const uint32_t* pack; const void* val;
   const int* mt_tiles; const int* mt_ptr; int nmt; int dim;
+  const int* cu; int ncu;     // level-1 combine units {tile, part_lo, part_hi}; mt_ptr indexes units
+  int nparts_total;           // item partial rows (the level-1 rows follow them in the scratch buffer)
 };
 
 template <typename VT, typename XT, typename RT>
@@ -743,8 +762,12 @@ static int tl_t_impl(const TLTDesc* c, const void* x, double* G, double* parts, 
                      c->pack, (const VT*)c->val, (const XT*)x, G, c->dim, parts);
   LAUNCH_CHECK();
   if (c->nmt > 0) {
-    hipLaunchKernelGGL(tl_t_combine_kernel, dim3(c->nmt), dim3(NTHREADS), 0, st, c->mt_tiles, c->mt_ptr, c->cbits,
-                       parts, G, c->dim);
+    const int C = 1 << c->cbits;
+    double* l1 = parts + (size_t)c->nparts_total * C;
+    hipLaunchKernelGGL(tl_t_combine1_kernel, dim3(c->ncu), dim3(NTHREADS), 0, st, c->cu, c->cbits, parts, l1);
+    LAUNCH_CHECK();
+    hipLaunchKernelGGL(tl_t_combine2_kernel, dim3(c->nmt, (C + NTHREADS - 1) / NTHREADS), dim3(NTHREADS), 0, st,
+                       c->mt_tiles, c->mt_ptr, c->cbits, l1, G, c->dim);
     LAUNCH_CHECK();
   }
   return 0;

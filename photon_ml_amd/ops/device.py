@@ -158,7 +158,7 @@ class DeviceGLMData(GLMComputable):
     # ------------------------------------------------------------------
     @staticmethod
     def from_labeled(data: LabeledData, device="cuda", precision: str = "f64", chunk_rows: int = 1 << 20,
-                     relabel: bool = True, layout: str = "auto", item_entries: int = DEFAULT_ITEM_ENTRIES):
+                     relabel: bool = True, layout: str = "auto", item_entries: Optional[int] = None):
         prec = PRECISIONS[precision]
         vdt = VAL_DTYPE[prec]
         dev = torch.device(device)

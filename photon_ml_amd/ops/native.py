@@ -39,6 +39,7 @@ class TLTDesc(ctypes.Structure):
     _fields_ = [
         ("items", c_void_p), ("nitems", c_int), ("cbits", c_int), ("pack", c_void_p), ("val", c_void_p),
         ("mt_tiles", c_void_p), ("mt_ptr", c_void_p), ("nmt", c_int), ("dim", c_int),
+        ("cu", c_void_p), ("ncu", c_int), ("nparts_total", c_int),
     ]
 
 

@@ -8,7 +8,8 @@ One row chunk of a feature shard is stored twice:
 * transpose copy — COLUMN TILES of ``2^cbits`` columns; inside a tile entries are sorted by (row, column) and
   packed as ``(local_row << cbits) | (col & (2^cbits - 1))``; a tile is cut into work items of at most
   ``item_entries`` entries. Item table: ``{tile, e_lo, e_hi, part}`` with ``part = -1`` for single-item tiles
-  and a partial-row index otherwise; split tiles are combined in item order (deterministic).
+  and a partial-row index otherwise; split tiles are combined in item order by a two-level fixed-order
+  reduction (units of ``COMBINE_SEG`` partial rows, then the units of a tile) — deterministic.
   ``cbits = min(10, 32 - bits(chunk_rows))``.
 
 The builders run with torch ops on the data's device (GPU sort for the 100M-entry bench chunks, CPU in tests).
@@ -18,6 +19,7 @@ of more than 2^27 rows) fall back to the segmented-stream layout (:mod:`photon_m
 """
 from __future__ import annotations
 
+import os
 from typing import Optional
 
 import numpy as np
@@ -29,6 +31,7 @@ TL_MAXBITS = 10          # 2^10 = TL_MAXR rows per block / columns per tile (LDS
 TL_MINBITS = 5
 DEFAULT_ITEM_ENTRIES = 1 << 16
 _PAD = 8                 # kernels read 4-entry quads; pad so that the last quad stays in bounds
+COMBINE_SEG = 16         # partial rows summed per level-1 combine work-group
 
 
 def _bits(n: int) -> int:
@@ -94,6 +97,8 @@ class TLFwdChunk:
     def nstats(self) -> int:
         return self.nblk
 
+    parts_needed = 0
+
     def nbytes(self) -> int:
         return sum(t.numel() * t.element_size() for t in (self.blk, self.pack, self.val))
 
@@ -114,7 +119,9 @@ class TLTChunk:
     kind = "tl"
 
     def __init__(self, rowptr: torch.Tensor, col: torch.Tensor, val: torch.Tensor, dim: int, chunk_rows: int,
-                 cbits: Optional[int] = None, item_entries: int = DEFAULT_ITEM_ENTRIES):
+                 cbits: Optional[int] = None, item_entries: Optional[int] = None):
+        if item_entries is None:
+            item_entries = int(os.environ.get("PML_TL_ITEM_ENTRIES", DEFAULT_ITEM_ENTRIES))
         dev = val.device
         rowptr = rowptr.to(dev, torch.int64)
         col = col.to(dev, torch.int64)
@@ -140,7 +147,7 @@ class TLTChunk:
         tptr = np.concatenate([[0], np.cumsum(counts)])
         nz = np.nonzero(counts)[0]
         n_it = np.maximum(1, -(-counts[nz] // item_entries))
-        items, mt_tiles, mt_ptr = [], [], [0]
+        items, mt_tiles, mt_ptr, cu = [], [], [0], []
         part = 0
         for t, k in zip(nz.tolist(), n_it.tolist()):
             a, b = int(tptr[t]), int(tptr[t + 1])
@@ -148,23 +155,29 @@ class TLTChunk:
             for i in range(k):
                 items.append((t, cuts[i], cuts[i + 1], -1 if k == 1 else part + i))
             if k > 1:
+                # level-1 combine units of <= COMBINE_SEG consecutive partial rows of this tile
+                for s0 in range(part, part + k, COMBINE_SEG):
+                    cu.append((len(mt_tiles), s0, min(part + k, s0 + COMBINE_SEG)))
                 part += k
                 mt_tiles.append(t)
-                mt_ptr.append(part)
-        self.nitems, self.nmt, self.nparts = len(items), len(mt_tiles), part
+                mt_ptr.append(len(cu))
+        self.nitems, self.nmt, self.nparts, self.ncu = len(items), len(mt_tiles), part, len(cu)
         self.items = torch.tensor(np.asarray(items, dtype=np.int32).reshape(-1, 4), device=dev)
         self.mt_tiles = torch.tensor(np.asarray(mt_tiles or [0], dtype=np.int32), device=dev)
         self.mt_ptr = torch.tensor(np.asarray(mt_ptr, dtype=np.int32), device=dev)
+        self.cu = torch.tensor(np.asarray(cu or [(0, 0, 0)], dtype=np.int32).reshape(-1, 3), device=dev)
         self.m, self.nnz, self.dim = m, nnz, dim
         self.desc = TLTDesc(self.items.data_ptr(), self.nitems, self.cbits, self.pack.data_ptr(),
-                            self.val.data_ptr(), self.mt_tiles.data_ptr(), self.mt_ptr.data_ptr(), self.nmt, dim)
+                            self.val.data_ptr(), self.mt_tiles.data_ptr(), self.mt_ptr.data_ptr(), self.nmt, dim,
+                            self.cu.data_ptr(), self.ncu, self.nparts)
 
     @property
     def parts_needed(self) -> int:
-        return self.nparts << self.cbits
+        """fp64 scratch: item partial rows followed by the level-1 combine rows."""
+        return (self.nparts + self.ncu) << self.cbits
 
     def nbytes(self) -> int:
-        return sum(t.numel() * t.element_size() for t in (self.items, self.mt_tiles, self.mt_ptr, self.pack,
+        return sum(t.numel() * t.element_size() for t in (self.items, self.mt_tiles, self.mt_ptr, self.cu, self.pack,
                                                            self.val))
 
     def emulate_rmatvec(self, r: torch.Tensor, square: bool = False) -> torch.Tensor:

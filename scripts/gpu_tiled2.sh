@@ -1,0 +1,16 @@
+#!/bin/bash
+# Tiled layout: parity tests after the two-level combine, item-size sweep, kernel-trace profile, full bench.
+set -o pipefail
+mkdir -p gpurun_out
+export TMPDIR=/tmp
+python __graft_entry__.py build > gpurun_out/build.log 2>&1 || { echo "build failed"; tail -20 gpurun_out/build.log; exit 1; }
+timeout -k 10 900 python -m pytest tests/test_kernels_gpu.py -x -q > gpurun_out/pytest_kernels.log 2>&1 || { echo "pytest failed"; tail -60 gpurun_out/pytest_kernels.log; exit 1; }
+tail -2 gpurun_out/pytest_kernels.log
+for it in 32768 65536 262144; do
+  PML_TL_ITEM_ENTRIES=$it timeout -k 10 300 python scripts/kbench.py --rows 16000000 --layout tiled --configs "0,0,0" > gpurun_out/kbench_tiled_$it.log 2>&1 || { echo "kbench failed"; tail -30 gpurun_out/kbench_tiled_$it.log; exit 1; }
+  echo "item $it: $(tail -1 gpurun_out/kbench_tiled_$it.log)"
+done
+cd /tmp && timeout -k 10 400 rocprofv3 --kernel-trace --stats -d $GRAFT_REPO_ROOT/gpurun_out/prof_tl -o prof -- python3 $GRAFT_REPO_ROOT/scripts/kbench.py --rows 16000000 --layout tiled --configs "0,0,0" > $GRAFT_REPO_ROOT/gpurun_out/prof_tl.log 2>&1 || { echo "prof failed"; tail -30 $GRAFT_REPO_ROOT/gpurun_out/prof_tl.log; exit 1; }
+cd $GRAFT_REPO_ROOT
+timeout -k 10 900 python bench.py > gpurun_out/bench_tiled.json 2> gpurun_out/bench_tiled.log || { echo "bench failed"; tail -40 gpurun_out/bench_tiled.log; exit 1; }
+cat gpurun_out/bench_tiled.json

@@ -8,7 +8,7 @@ import time
 
 import torch
 
-sys.path.insert(0, ".")
+sys.path.insert(0, __import__("os").path.dirname(__import__("os").path.dirname(__import__("os").path.abspath(__file__))))
 from photon_ml_amd.data.synthetic import generate_device_shard  # noqa: E402
 from photon_ml_amd.function.losses import LOGISTIC  # noqa: E402
 

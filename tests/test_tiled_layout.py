@@ -44,3 +44,15 @@ def test_bits():
     assert fwd_bits(1_000_000) == 10 and t_bits(1 << 20) == 10
     assert fwd_bits(1 << 26) == 6 and fwd_bits(1 << 28) is None
     assert not tl_supported(1 << 28, 1 << 20) and tl_supported(1 << 24, 1 << 22)
+
+
+@pytest.mark.parametrize("layout", ["tiled", "segmented"])
+def test_device_data_construction_cpu(layout):
+    """DeviceGLMData tables/scratch sizing for both layouts (construction only: kernels need a GPU)."""
+    from photon_ml_amd.data.synthetic import generate_glm_data
+    from photon_ml_amd.ops.device import DeviceGLMData
+    data, _ = generate_glm_data("LOGISTIC_REGRESSION", 3000, 300, density=0.05, seed=2)
+    dev = DeviceGLMData.from_labeled(data, "cpu", "bf16", chunk_rows=1000, layout=layout, item_entries=500)
+    assert dev.layout == layout and len(dev.csr) == 3 and len(dev.csc) == 3
+    assert dev.stats.numel() >= 2 * sum(c.nstats for c in dev.csr)
+    assert dev.parts.numel() >= max(c.parts_needed for c in dev.csc)
