@@ -577,20 +577,19 @@ __global__ __launch_bounds__(NTHREADS) void reduce_stats_l1_kernel(const double*
 // ============================================================================================================
 #define TL_VEC 4                              // entries per lane per round (16-B pack loads)
 #define TL_ROUND (64 * TL_VEC)                // entries per wave-round
-#define TL_U 2                                // wave-rounds in flight per iteration
 #define TL_WAVES (NTHREADS / 64)
-#define TL_MAXR 1024                          // max rows per forward block / columns per transpose tile
+#define TL_MAXBITS 12                         // up to 4096 rows per forward block / columns per transpose tile
 
 template <typename VT> struct TLVals;
 template <> struct TLVals<uint16_t> {
-  static __device__ __forceinline__ void load(const uint16_t* p, double* v) {
+  static __device__ __forceinline__ void load(const uint16_t* p, float* v) {
     const v2u u = __builtin_nontemporal_load((const v2u*)p);
-    v[0] = (double)__uint_as_float(u.x << 16); v[1] = (double)__uint_as_float(u.x & 0xffff0000u);
-    v[2] = (double)__uint_as_float(u.y << 16); v[3] = (double)__uint_as_float(u.y & 0xffff0000u);
+    v[0] = __uint_as_float(u.x << 16); v[1] = __uint_as_float(u.x & 0xffff0000u);
+    v[2] = __uint_as_float(u.y << 16); v[3] = __uint_as_float(u.y & 0xffff0000u);
   }
 };
 template <> struct TLVals<float> {
-  static __device__ __forceinline__ void load(const float* p, double* v) {
+  static __device__ __forceinline__ void load(const float* p, float* v) {
     const v4f a = __builtin_nontemporal_load((const v4f*)p);
     v[0] = a[0]; v[1] = a[1]; v[2] = a[2]; v[3] = a[3];
   }
@@ -602,25 +601,28 @@ template <> struct TLVals<double> {
     v[0] = a[0]; v[1] = a[1]; v[2] = b[0]; v[3] = b[1];
   }
 };
+template <typename VT> struct TLValT { typedef float T; };
+template <> struct TLValT<double> { typedef double T; };
 
 // Stream entries [e_lo, e_hi) of one work unit: wave w walks a contiguous share of the 4-aligned window.
 // For each entry: key = pack >> sbits (gather index), slot = pack & smask (LDS accumulator slot);
-// acc[slot] += val (or val^2) * x[key + xoff].
-template <typename VT, typename XT, bool SQ>
+// acc[slot] += val (or val^2) * x[key]. U wave-rounds per iteration: all stream loads first, then all gathers,
+// then the LDS accumulation (AT: float -> ds_add_f32, double -> ds_add_f64).
+template <typename VT, typename XT, typename AT, bool SQ, int U>
 __device__ __forceinline__ void tl_stream(const uint32_t* __restrict__ pack, const VT* __restrict__ val,
-                                          const XT* __restrict__ x, int e_lo, int e_hi, int sbits, double* acc) {
+                                          const XT* __restrict__ x, int e_lo, int e_hi, int sbits, AT* acc) {
+  typedef typename TLValT<VT>::T LT;
   const int lane = threadIdx.x & 63, w = threadIdx.x >> 6;
   const uint32_t smask = (1u << sbits) - 1u;
   const int lo = e_lo & ~(TL_VEC - 1);
   const int nr = (e_hi - lo + TL_ROUND - 1) / TL_ROUND;
   const int r0 = (nr * w) / TL_WAVES, r1 = (nr * (w + 1)) / TL_WAVES;
-  // TL_U rounds per iteration: all stream loads first, then all gathers, then the LDS accumulation
-  for (int r = r0; r < r1; r += TL_U) {
-    v4u pk[TL_U];
-    double v[TL_U][TL_VEC];
-    bool in[TL_U][TL_VEC];
+  for (int r = r0; r < r1; r += U) {
+    v4u pk[U];
+    LT v[U][TL_VEC];
+    bool in[U][TL_VEC];
 #pragma unroll
-    for (int u = 0; u < TL_U; ++u) {
+    for (int u = 0; u < U; ++u) {
       const int e = lo + (r + u) * TL_ROUND + lane * TL_VEC;
       const bool ok = (r + u < r1) && (e < e_hi);
       const int es = ok ? e : lo;  // out-of-range lanes re-read the first (valid) quad; results are masked
@@ -630,42 +632,45 @@ __device__ __forceinline__ void tl_stream(const uint32_t* __restrict__ pack, con
       for (int k = 0; k < TL_VEC; ++k) in[u][k] = ok && (e + k >= e_lo) && (e + k < e_hi);
     }
     // unconditional gathers (masked lanes read x[0]) so that all of them are in flight together
-    XT xv[TL_U][TL_VEC];
+    XT xv[U][TL_VEC];
 #pragma unroll
-    for (int u = 0; u < TL_U; ++u)
+    for (int u = 0; u < U; ++u)
 #pragma unroll
       for (int k = 0; k < TL_VEC; ++k) xv[u][k] = x[in[u][k] ? (pk[u][k] >> sbits) : 0u];
 #pragma unroll
-    for (int u = 0; u < TL_U; ++u)
+    for (int u = 0; u < U; ++u)
 #pragma unroll
       for (int k = 0; k < TL_VEC; ++k) {
         if (in[u][k]) {
-          const double vv = SQ ? v[u][k] * v[u][k] : v[u][k];
-          atomicAdd(&acc[pk[u][k] & smask], vv * static_cast<double>(xv[u][k]));
+          const AT vv = SQ ? static_cast<AT>(v[u][k]) * static_cast<AT>(v[u][k]) : static_cast<AT>(v[u][k]);
+          atomicAdd(&acc[pk[u][k] & smask], vv * static_cast<AT>(xv[u][k]));
         }
       }
   }
 }
 
 // Forward over row blocks. blk: 4 ints per block {row_lo, nrows, e_lo, e_hi} (chunk-local).
-template <typename VT, typename XT, typename RT>
+template <typename VT, typename XT, typename RT, typename AT, int MAXR, int U>
 __global__ __launch_bounds__(NTHREADS) void tl_fwd_kernel(const int* __restrict__ blk, int rbits,
                                                           const uint32_t* __restrict__ pack,
                                                           const VT* __restrict__ val, const XT* __restrict__ x,
                                                           FwdArgs<XT, RT> a, double* __restrict__ stats) {
-  __shared__ double acc[TL_WAVES][TL_MAXR];
+  __shared__ AT acc[TL_WAVES][MAXR];
   __shared__ double red[2 * NTHREADS / 64];
   const int b = blockIdx.x;
   const int row_lo = blk[4 * b], nrows = blk[4 * b + 1], e_lo = blk[4 * b + 2], e_hi = blk[4 * b + 3];
-  for (int i = threadIdx.x; i < TL_WAVES * TL_MAXR; i += NTHREADS) (&acc[0][0])[i] = 0.0;
+  const int R = 1 << rbits;
+  for (int i = threadIdx.x; i < R; i += NTHREADS)
+#pragma unroll
+    for (int w = 0; w < TL_WAVES; ++w) acc[w][i] = AT(0);
   __syncthreads();
-  tl_stream<VT, XT, false>(pack, val, x, e_lo, e_hi, rbits, acc[threadIdx.x >> 6]);
+  tl_stream<VT, XT, AT, false, U>(pack, val, x, e_lo, e_hi, rbits, acc[threadIdx.x >> 6]);
   __syncthreads();
   double F = 0.0, S = 0.0;
   for (int r = threadIdx.x; r < nrows; r += NTHREADS) {
-    double z = acc[0][r];
+    double z = static_cast<double>(acc[0][r]);
 #pragma unroll
-    for (int w = 1; w < TL_WAVES; ++w) z += acc[w][r];
+    for (int w = 1; w < TL_WAVES; ++w) z += static_cast<double>(acc[w][r]);
     const int s = row_lo + r;
     fwd_finish(a, s, z, fwd_prefetch(a, s), F, S);
   }
@@ -677,24 +682,26 @@ __global__ __launch_bounds__(NTHREADS) void tl_fwd_kernel(const int* __restrict_
 
 // Transpose over column-tile items. items: 4 ints {tile, e_lo, e_hi, part}; part < 0: the item is its tile's
 // only one -> G[tile cols] += sums directly; else the item's row of partial sums goes to parts[part * C ...].
-template <typename VT, typename XT, bool SQ>
+template <typename VT, typename XT, typename AT, bool SQ, int MAXR, int U>
 __global__ __launch_bounds__(NTHREADS) void tl_t_kernel(const int* __restrict__ items, int cbits,
                                                         const uint32_t* __restrict__ pack,
                                                         const VT* __restrict__ val, const XT* __restrict__ x,
                                                         double* __restrict__ G, int dim, double* __restrict__ parts) {
-  __shared__ double acc[TL_WAVES][TL_MAXR];
+  __shared__ AT acc[TL_WAVES][MAXR];
   const int it = blockIdx.x;
   const int tile = items[4 * it], e_lo = items[4 * it + 1], e_hi = items[4 * it + 2], part = items[4 * it + 3];
   const int C = 1 << cbits;
-  for (int i = threadIdx.x; i < TL_WAVES * TL_MAXR; i += NTHREADS) (&acc[0][0])[i] = 0.0;
+  for (int i = threadIdx.x; i < C; i += NTHREADS)
+#pragma unroll
+    for (int w = 0; w < TL_WAVES; ++w) acc[w][i] = AT(0);
   __syncthreads();
-  tl_stream<VT, XT, SQ>(pack, val, x, e_lo, e_hi, cbits, acc[threadIdx.x >> 6]);
+  tl_stream<VT, XT, AT, SQ, U>(pack, val, x, e_lo, e_hi, cbits, acc[threadIdx.x >> 6]);
   __syncthreads();
   const int c0 = tile << cbits;
   for (int c = threadIdx.x; c < C; c += NTHREADS) {
-    double s = acc[0][c];
+    double s = static_cast<double>(acc[0][c]);
 #pragma unroll
-    for (int w = 1; w < TL_WAVES; ++w) s += acc[w][c];
+    for (int w = 1; w < TL_WAVES; ++w) s += static_cast<double>(acc[w][c]);
     if (part < 0) {
       if (c0 + c < dim) G[c0 + c] += s;
     } else {
@@ -744,22 +751,65 @@ struct TLTDesc {
   int nparts_total;           // item partial rows (the level-1 rows follow them in the scratch buffer)
 };
 
+// Runtime TL configuration: accumulator precision for bf16/f32 data (0 = fp32 LDS, 1 = fp64 LDS) and the number
+// of wave-rounds in flight (2 or 4). fp64 data always accumulates in fp64.
+static int g_tl_acc64 = 0;
+static int g_tl_u = 2;
+
+template <typename VT, typename XT, typename RT, typename AT, int MAXR>
+static void tl_fwd_launch(const TLFwdDesc* c, const void* x, FwdArgs<XT, RT> a, double* stats, hipStream_t st) {
+  if (g_tl_u >= 4)
+    hipLaunchKernelGGL((tl_fwd_kernel<VT, XT, RT, AT, MAXR, 4>), dim3(c->nblk), dim3(NTHREADS), 0, st, c->blk,
+                       c->rbits, c->pack, (const VT*)c->val, (const XT*)x, a, stats);
+  else
+    hipLaunchKernelGGL((tl_fwd_kernel<VT, XT, RT, AT, MAXR, 2>), dim3(c->nblk), dim3(NTHREADS), 0, st, c->blk,
+                       c->rbits, c->pack, (const VT*)c->val, (const XT*)x, a, stats);
+}
+
 template <typename VT, typename XT, typename RT>
 static int tl_fwd_impl(const TLFwdDesc* c, const void* x, FwdArgs<XT, RT> a, double* stats, hipStream_t st) {
   if (c->nblk <= 0) return 0;
-  if (c->rbits < 1 || (1 << c->rbits) > TL_MAXR) return -22;
-  hipLaunchKernelGGL((tl_fwd_kernel<VT, XT, RT>), dim3(c->nblk), dim3(NTHREADS), 0, st, c->blk, c->rbits,
-                     c->pack, (const VT*)c->val, (const XT*)x, a, stats);
+  if (c->rbits < 1 || c->rbits > TL_MAXBITS) return -22;
+  const bool f64 = sizeof(XT) == 8 || g_tl_acc64;
+  if (f64) {
+    if (c->rbits > 10) return -22;  // fp64 LDS: 4 waves x 1024 rows = 32 KB
+    tl_fwd_launch<VT, XT, RT, double, 1024>(c, x, a, stats, st);
+  } else if (c->rbits <= 10) {
+    tl_fwd_launch<VT, XT, RT, float, 1024>(c, x, a, stats, st);
+  } else if (c->rbits == 11) {
+    tl_fwd_launch<VT, XT, RT, float, 2048>(c, x, a, stats, st);
+  } else {
+    tl_fwd_launch<VT, XT, RT, float, 4096>(c, x, a, stats, st);
+  }
   LAUNCH_CHECK();
   return 0;
+}
+
+template <typename VT, typename XT, typename AT, bool SQ, int MAXR>
+static void tl_t_launch(const TLTDesc* c, const void* x, double* G, double* parts, hipStream_t st) {
+  if (g_tl_u >= 4)
+    hipLaunchKernelGGL((tl_t_kernel<VT, XT, AT, SQ, MAXR, 4>), dim3(c->nitems), dim3(NTHREADS), 0, st, c->items,
+                       c->cbits, c->pack, (const VT*)c->val, (const XT*)x, G, c->dim, parts);
+  else
+    hipLaunchKernelGGL((tl_t_kernel<VT, XT, AT, SQ, MAXR, 2>), dim3(c->nitems), dim3(NTHREADS), 0, st, c->items,
+                       c->cbits, c->pack, (const VT*)c->val, (const XT*)x, G, c->dim, parts);
 }
 
 template <typename VT, typename XT, bool SQ>
 static int tl_t_impl(const TLTDesc* c, const void* x, double* G, double* parts, hipStream_t st) {
   if (c->nitems <= 0) return 0;
-  if (c->cbits < 1 || (1 << c->cbits) > TL_MAXR) return -22;
-  hipLaunchKernelGGL((tl_t_kernel<VT, XT, SQ>), dim3(c->nitems), dim3(NTHREADS), 0, st, c->items, c->cbits,
-                     c->pack, (const VT*)c->val, (const XT*)x, G, c->dim, parts);
+  if (c->cbits < 1 || c->cbits > TL_MAXBITS) return -22;
+  const bool f64 = sizeof(XT) == 8 || g_tl_acc64;
+  if (f64) {
+    if (c->cbits > 10) return -22;
+    tl_t_launch<VT, XT, double, SQ, 1024>(c, x, G, parts, st);
+  } else if (c->cbits <= 10) {
+    tl_t_launch<VT, XT, float, SQ, 1024>(c, x, G, parts, st);
+  } else if (c->cbits == 11) {
+    tl_t_launch<VT, XT, float, SQ, 2048>(c, x, G, parts, st);
+  } else {
+    tl_t_launch<VT, XT, float, SQ, 4096>(c, x, G, parts, st);
+  }
   LAUNCH_CHECK();
   if (c->nmt > 0) {
     const int C = 1 << c->cbits;
@@ -958,7 +1008,8 @@ int pml_reduce_stats(const double* stats, int n, double* out, int accumulate, do
 }
 
 // ---- tiled layout entry points ------------------------------------------------------------------------------
-int pml_tl_maxr() { return TL_MAXR; }
+int pml_tl_maxbits() { return TL_MAXBITS; }
+void pml_tl_config(int acc64, int u) { g_tl_acc64 = acc64; g_tl_u = u; }
 
 int pml_tl_fwd(int prec, const TLFwdDesc* c, const void* x, int mode, int loss, double shift, const void* y,
                const void* off, const void* wt, void* coef, void* dzz, double* z_out, int with_offset,

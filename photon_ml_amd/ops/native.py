@@ -77,8 +77,9 @@ def glm_lib() -> Optional[ctypes.CDLL]:
         lib.pml_tl_fwd.argtypes = [c_int, ctypes.POINTER(TLFwdDesc), c_void_p, c_int, c_int, c_double, c_void_p,
                                    c_void_p, c_void_p, c_void_p, c_void_p, c_void_p, c_int, c_void_p, c_void_p]
         lib.pml_tl_t.argtypes = [c_int, ctypes.POINTER(TLTDesc), c_void_p, c_int, c_void_p, c_void_p, c_void_p]
+        lib.pml_tl_config.argtypes = [c_int, c_int]
         for f in ("pml_seg_fwd", "pml_seg_t", "pml_reduce_stats", "pml_build_blocks", "pml_tl_fwd", "pml_tl_t",
-                  "pml_tl_maxr"):
+                  "pml_tl_maxbits"):
             getattr(lib, f).restype = c_int
         lib.pml_set_config.argtypes = [c_int, c_int, c_int, c_int]
         lib._pml_typed = True
@@ -89,7 +90,7 @@ def glm_lib() -> Optional[ctypes.CDLL]:
 # Kernel configuration defaults (tuned on MI355X, see profiles/): forward = vector layout + 8192-entry LDS hot
 # table of the most frequent features; transpose = strided layout. Env overrides for experiments:
 # PML_FWD_STRIDED, PML_T_STRIDED, PML_HOT_N, PML_FWD_GRID.
-KERNEL_CONFIG = {"fwd_strided": 0, "t_strided": 0, "hot_n": 0, "fwd_grid": 1024}
+KERNEL_CONFIG = {"fwd_strided": 0, "t_strided": 0, "hot_n": 0, "fwd_grid": 1024, "tl_acc64": 0, "tl_u": 2}
 
 
 def configure(**kw):
@@ -102,6 +103,7 @@ def configure(**kw):
     if lib is not None:
         lib.pml_set_config(KERNEL_CONFIG["fwd_strided"], KERNEL_CONFIG["t_strided"], KERNEL_CONFIG["hot_n"],
                            KERNEL_CONFIG["fwd_grid"])
+        lib.pml_tl_config(KERNEL_CONFIG["tl_acc64"], KERNEL_CONFIG["tl_u"])
     return dict(KERNEL_CONFIG)
 
 

@@ -27,8 +27,11 @@ import torch
 
 from .native import TLFwdDesc, TLTDesc
 
-TL_MAXBITS = 10          # 2^10 = TL_MAXR rows per block / columns per tile (LDS: 4 waves x 1024 fp64)
+TL_MAXBITS = 12          # kernel limit: 4096 rows per block / columns per tile (fp32 LDS: 4 waves x 16 KB)
+TL_MAXBITS_F64 = 10      # fp64 data accumulates in fp64 LDS: 4 waves x 1024 x 8 B
 TL_MINBITS = 5
+DEFAULT_RBITS = int(os.environ.get("PML_TL_RBITS", 10))
+DEFAULT_CBITS = int(os.environ.get("PML_TL_CBITS", 10))
 DEFAULT_ITEM_ENTRIES = 1 << 16
 _PAD = 8                 # kernels read 4-entry quads; pad so that the last quad stays in bounds
 COMBINE_SEG = 16         # partial rows summed per level-1 combine work-group
@@ -38,13 +41,17 @@ def _bits(n: int) -> int:
     return max(1, int(n - 1).bit_length())
 
 
-def fwd_bits(dim: int) -> Optional[int]:
-    r = min(TL_MAXBITS, 32 - _bits(dim))
+def _cap(want: int, f64: bool) -> int:
+    return min(want, TL_MAXBITS_F64 if f64 else TL_MAXBITS)
+
+
+def fwd_bits(dim: int, f64: bool = False, want: Optional[int] = None) -> Optional[int]:
+    r = min(_cap(DEFAULT_RBITS if want is None else want, f64), 32 - _bits(dim))
     return r if r >= TL_MINBITS else None
 
 
-def t_bits(chunk_rows: int) -> Optional[int]:
-    c = min(TL_MAXBITS, 32 - _bits(chunk_rows))
+def t_bits(chunk_rows: int, f64: bool = False, want: Optional[int] = None) -> Optional[int]:
+    c = min(_cap(DEFAULT_CBITS if want is None else want, f64), 32 - _bits(chunk_rows))
     return c if c >= TL_MINBITS else None
 
 
@@ -72,7 +79,7 @@ class TLFwdChunk:
         rowptr = rowptr.to(dev, torch.int64)
         col = col.to(dev, torch.int64)
         m = rowptr.numel() - 1
-        self.rbits = fwd_bits(dim) if rbits is None else rbits
+        self.rbits = fwd_bits(dim, val.dtype == torch.float64, rbits)
         if self.rbits is None:
             raise ValueError(f"tiled forward layout cannot pack dim={dim}")
         R = 1 << self.rbits
@@ -126,7 +133,7 @@ class TLTChunk:
         rowptr = rowptr.to(dev, torch.int64)
         col = col.to(dev, torch.int64)
         m = rowptr.numel() - 1
-        self.cbits = t_bits(max(chunk_rows, m)) if cbits is None else cbits
+        self.cbits = t_bits(max(chunk_rows, m), val.dtype == torch.float64, cbits)
         if self.cbits is None:
             raise ValueError(f"tiled transpose layout cannot pack chunk_rows={chunk_rows}")
         C = 1 << self.cbits

@@ -9,7 +9,7 @@ def short(name: str) -> str:
     m = re.match(r"void ([\w:]+)(<[^(]*?>)?", name)
     base = m.group(1) if m else name[:80]
     tmpl = (m.group(2) or "") if m else ""
-    if base.startswith("seg_") or base.startswith("reduce_") or base.startswith("re_"):
+    if base.startswith(("seg_", "reduce_", "re_", "tl_")):
         return base + tmpl
     return base + ("<…>" if tmpl else "")
 
