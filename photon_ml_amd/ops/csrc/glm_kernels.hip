@@ -753,7 +753,7 @@ struct TLTDesc {
 
 // Runtime TL configuration: accumulator precision for bf16/f32 data (0 = fp32 LDS, 1 = fp64 LDS) and the number
 // of wave-rounds in flight (2 or 4). fp64 data always accumulates in fp64.
-static int g_tl_acc64 = 0;
+static int g_tl_acc64 = 1;   // measured on MI355X: ds_add_f64 accumulation is ~3x faster than ds_add_f32 here
 static int g_tl_u = 2;
 
 template <typename VT, typename XT, typename RT, typename AT, int MAXR>
@@ -772,8 +772,9 @@ static int tl_fwd_impl(const TLFwdDesc* c, const void* x, FwdArgs<XT, RT> a, dou
   if (c->rbits < 1 || c->rbits > TL_MAXBITS) return -22;
   const bool f64 = sizeof(XT) == 8 || g_tl_acc64;
   if (f64) {
-    if (c->rbits > 10) return -22;  // fp64 LDS: 4 waves x 1024 rows = 32 KB
-    tl_fwd_launch<VT, XT, RT, double, 1024>(c, x, a, stats, st);
+    if (c->rbits > 11) return -22;  // fp64 LDS: 4 waves x 2048 rows = 64 KB
+    if (c->rbits <= 10) tl_fwd_launch<VT, XT, RT, double, 1024>(c, x, a, stats, st);
+    else tl_fwd_launch<VT, XT, RT, double, 2048>(c, x, a, stats, st);
   } else if (c->rbits <= 10) {
     tl_fwd_launch<VT, XT, RT, float, 1024>(c, x, a, stats, st);
   } else if (c->rbits == 11) {
@@ -801,8 +802,9 @@ static int tl_t_impl(const TLTDesc* c, const void* x, double* G, double* parts, 
   if (c->cbits < 1 || c->cbits > TL_MAXBITS) return -22;
   const bool f64 = sizeof(XT) == 8 || g_tl_acc64;
   if (f64) {
-    if (c->cbits > 10) return -22;
-    tl_t_launch<VT, XT, double, SQ, 1024>(c, x, G, parts, st);
+    if (c->cbits > 11) return -22;
+    if (c->cbits <= 10) tl_t_launch<VT, XT, double, SQ, 1024>(c, x, G, parts, st);
+    else tl_t_launch<VT, XT, double, SQ, 2048>(c, x, G, parts, st);
   } else if (c->cbits <= 10) {
     tl_t_launch<VT, XT, float, SQ, 1024>(c, x, G, parts, st);
   } else if (c->cbits == 11) {

@@ -90,7 +90,7 @@ def glm_lib() -> Optional[ctypes.CDLL]:
 # Kernel configuration defaults (tuned on MI355X, see profiles/): forward = vector layout + 8192-entry LDS hot
 # table of the most frequent features; transpose = strided layout. Env overrides for experiments:
 # PML_FWD_STRIDED, PML_T_STRIDED, PML_HOT_N, PML_FWD_GRID.
-KERNEL_CONFIG = {"fwd_strided": 0, "t_strided": 0, "hot_n": 0, "fwd_grid": 1024, "tl_acc64": 0, "tl_u": 2}
+KERNEL_CONFIG = {"fwd_strided": 0, "t_strided": 0, "hot_n": 0, "fwd_grid": 1024, "tl_acc64": 1, "tl_u": 2}
 
 
 def configure(**kw):

@@ -28,7 +28,7 @@ import torch
 from .native import TLFwdDesc, TLTDesc
 
 TL_MAXBITS = 12          # kernel limit: 4096 rows per block / columns per tile (fp32 LDS: 4 waves x 16 KB)
-TL_MAXBITS_F64 = 10      # fp64 data accumulates in fp64 LDS: 4 waves x 1024 x 8 B
+TL_MAXBITS_F64 = 11      # fp64 LDS accumulators: 4 waves x 2048 x 8 B = 64 KB
 TL_MINBITS = 5
 DEFAULT_RBITS = int(os.environ.get("PML_TL_RBITS", 10))
 DEFAULT_CBITS = int(os.environ.get("PML_TL_CBITS", 10))

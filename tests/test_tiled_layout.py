@@ -42,7 +42,7 @@ def test_tl_emulation_matches_scipy(m, d, dens, item):
 
 def test_bits():
     assert fwd_bits(1_000_000) == 10 and t_bits(1 << 20) == 10 and fwd_bits(1_000_000, want=12) == 12
-    assert fwd_bits(1 << 26) == 6 and fwd_bits(1 << 28) is None and t_bits(1 << 20, f64=True, want=12) == 10
+    assert fwd_bits(1 << 26) == 6 and fwd_bits(1 << 28) is None and t_bits(1 << 20, f64=True, want=12) == 11
     assert not tl_supported(1 << 28, 1 << 20) and tl_supported(1 << 24, 1 << 22)
 
 
