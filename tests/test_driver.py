@@ -1,0 +1,144 @@
+"""Legacy driver + diagnostics tests (DriverTest / DriverIntegTest / diagnostics unit tests analogues).
+
+Reference: ``photon-client/src/integTest/scala/com/linkedin/photon/ml/DriverTest.scala`` (stages, number of
+models, best model only with validation data, LibSVM input, invalid parameter combinations),
+``photon-diagnostics/src/test/.../{hl,independence,featureimportance}`` and the Evaluation metric definitions.
+Data: the reference's own heart.avro / heart.txt fixtures.
+"""
+import os
+
+import numpy as np
+import pytest
+import torch
+
+from photon_ml_amd.cli import driver as drv
+from photon_ml_amd.diagnostics import evaluation as ev
+from photon_ml_amd.diagnostics.diagnostics import hosmer_lemeshow, kendall_tau
+from photon_ml_amd.io.index_map import DefaultIndexMap
+
+REF = "/root/reference/photon-client/src/integTest/resources/DriverIntegTest/input"
+HEART_FEATURES = 14
+HEART_ROWS = 250
+
+
+def run(tmp_path, *extra, out="out"):
+    args = ["--training-data-directory", f"{REF}/heart.avro", "--output-directory", str(tmp_path / out),
+            "--task", "LOGISTIC_REGRESSION", "--num-iterations", "50", "--device", "cpu", *extra]
+    return drv.Driver(drv.build_parser().parse_args(args)).run()
+
+
+def test_minimal_run(tmp_path):
+    d = run(tmp_path)
+    assert d.stage_history == [drv.DriverStage.INIT, drv.DriverStage.PREPROCESSED] and \
+        d.stage == drv.DriverStage.TRAINED
+    assert d.train_data.n_features == HEART_FEATURES and d.train_data.n_rows == HEART_ROWS
+    models = drv.read_text_model(str(tmp_path / "out" / drv.LEARNED_MODELS_TEXT))
+    assert list(models) == [10.0] and len(models[10.0]) == HEART_FEATURES
+    assert not os.path.exists(tmp_path / "out" / drv.BEST_MODEL_TEXT)
+    assert os.path.exists(tmp_path / "out" / "log-message.txt")
+
+
+def test_validation_selects_best_and_diagnoses(tmp_path):
+    d = run(tmp_path, "--validating-data-directory", f"{REF}/heart_validation.avro",
+            "--regularization-weights", "0.1,1,10,100", "--diagnostic-mode", "VALIDATE",
+            "--summarization-output-dir", str(tmp_path / "summary"), "--normalization-type", "STANDARDIZATION")
+    assert d.stage == drv.DriverStage.DIAGNOSED
+    models = drv.read_text_model(str(tmp_path / "out" / drv.LEARNED_MODELS_TEXT))
+    assert sorted(models) == [0.1, 1.0, 10.0, 100.0]
+    best = drv.read_text_model(str(tmp_path / "out" / drv.BEST_MODEL_TEXT))
+    assert len(best) == 1
+    lam = list(best)[0]
+    aucs = {l: m[ev.AREA_UNDER_RECEIVER_OPERATOR_CHARACTERISTICS] for l, m in d.per_model_metrics.items()}
+    assert aucs[lam] == max(aucs.values()) and max(aucs.values()) > 0.8
+    html = open(tmp_path / "out" / "diagnostic.html").read()
+    assert "Hosmer-Lemeshow" in html and "<svg" in html and "Kendall" in html
+    assert os.path.exists(tmp_path / "summary" / "part-00000.avro")
+
+
+def test_libsvm_run_with_validation(tmp_path):
+    args = ["--training-data-directory", f"{REF}/heart.txt", "--validating-data-directory",
+            f"{REF}/heart_validation.txt", "--output-directory", str(tmp_path / "o"), "--task",
+            "LOGISTIC_REGRESSION", "--input-file-format", "LIBSVM", "--feature-dimension", "13",
+            "--num-iterations", "50", "--device", "cpu"]
+    d = drv.Driver(drv.build_parser().parse_args(args)).run()
+    assert d.train_data.n_features == HEART_FEATURES and d.stage == drv.DriverStage.VALIDATED
+    assert list(drv.read_text_model(str(tmp_path / "o" / drv.BEST_MODEL_TEXT))) == [10.0]
+
+
+@pytest.mark.parametrize("extra", [
+    ["--regularization-type", "L1", "--optimizer", "TRON"],
+    ["--regularization-type", "ELASTIC_NET", "--optimizer", "TRON"],
+    ["--normalization-type", "STANDARDIZATION", "--intercept", "false"],
+    ["--diagnostic-mode", "ALL"],
+    ["--normalization-type", "SCALE_WITH_MAX_MAGNITUDE", "--coefficient-box-constraints",
+     '[{"name": "1", "term": "", "lowerBound": 0, "upperBound": 1}]'],
+])
+def test_invalid_combinations(tmp_path, extra):
+    with pytest.raises(ValueError):
+        run(tmp_path, *extra)
+
+
+def test_box_constraints(tmp_path):
+    cons = '[{"name": "*", "term": "*", "lowerBound": -0.01, "upperBound": 0.01}]'
+    d = run(tmp_path, "--coefficient-box-constraints", cons, "--regularization-weights", "0.1")
+    w = d.lambda_models[0][1].coefficients.means.numpy()
+    icpt = d.index_map.intercept_index
+    mask = np.arange(len(w)) != icpt
+    assert np.all(np.abs(w[mask]) <= 0.01 + 1e-12) and np.any(np.abs(np.abs(w[mask]) - 0.01) < 1e-9)
+
+
+def test_constraint_map_wildcards():
+    im = DefaultIndexMap.from_keys(["a\u0001x", "a\u0001y", "b\u0001", "(INTERCEPT)\u0001"])
+    m = drv.constraint_map_from_json('[{"name": "a", "term": "*", "upperBound": 1}, {"name": "b", "term": "", '
+                                     '"lowerBound": -2}]', im)
+    assert m == {0: (-np.inf, 1.0), 1: (-np.inf, 1.0), 2: (-2.0, np.inf)}
+    with pytest.raises(ValueError):
+        drv.constraint_map_from_json('[{"name": "a", "term": "*", "upperBound": 1}, '
+                                     '{"name": "a", "term": "x", "upperBound": 2}]', im)
+    with pytest.raises(ValueError):
+        drv.constraint_map_from_json('[{"name": "*", "term": "x", "upperBound": 1}]', im)
+
+
+def test_binary_metrics_known_values():
+    s = np.array([0.9, 0.8, 0.7, 0.6, 0.55, 0.4, 0.3, 0.2])
+    y = np.array([1, 1, 0, 1, 0, 0, 1, 0.0])
+    m = ev.binary_metrics(s, y)
+    from sklearn.metrics import roc_auc_score
+    assert abs(m[ev.AREA_UNDER_RECEIVER_OPERATOR_CHARACTERISTICS] - roc_auc_score(y, s)) < 1e-12
+    # peak F1: threshold 0.6 -> tp=3, fp=1, fn=1 -> 0.75
+    assert abs(m[ev.PEAK_F1_SCORE] - 0.75) < 1e-12
+    assert 0 < m[ev.AREA_UNDER_PRECISION_RECALL] <= 1
+    r = ev.regression_metrics(np.array([1.0, 2.0, 3.0]), np.array([1.0, 1.0, 5.0]))
+    assert r[ev.MEAN_ABSOLUTE_ERROR] == 1.0 and abs(r[ev.MEAN_SQUARE_ERROR] - 5 / 3) < 1e-12
+
+
+def test_hosmer_lemeshow_and_kendall():
+    rng = np.random.default_rng(0)
+    p = rng.random(20000)
+    y = (rng.random(20000) < p).astype(float)
+    rep = hosmer_lemeshow(y, p, dim=8)
+    assert len(rep.histogram) == 10 and rep.degrees_of_freedom == 8
+    assert rep.chi_squared_prob < 0.999  # well-calibrated scores are not rejected at the extreme level
+    bad = hosmer_lemeshow(y, np.clip(p * 0.3, 0, 1), dim=8)
+    assert bad.chi_squared_score > 100 * rep.chi_squared_score
+    a = rng.normal(size=300)
+    kt = kendall_tau(a, a + 0.01 * rng.normal(size=300))
+    from scipy.stats import kendalltau
+    assert abs(kt.tau_alpha - kendalltau(a, a + 0.01 * rng.normal(size=300))[0]) < 0.05
+    ind = kendall_tau(a, rng.normal(size=300))
+    assert abs(ind.tau_alpha) < 0.1 and ind.concordant + ind.discordant == 300 * 299 // 2
+
+
+def test_training_diagnostics(tmp_path):
+    d = run(tmp_path, "--diagnostic-mode", "TRAIN", "--regularization-weights", "1,10")
+    rep = {r.lam: r for r in d.model_reports}
+    assert set(rep) == {1.0, 10.0}
+    fit = rep[10.0].fit_report
+    portions, train, test = fit.metrics[ev.AREA_UNDER_RECEIVER_OPERATOR_CHARACTERISTICS]
+    assert len(portions) == 9 and np.all(np.diff(portions) > 0) and portions[-1] < 100
+    boot = rep[10.0].bootstrap_report
+    lo, q1, med, q3, hi = boot.metric_distributions[ev.AREA_UNDER_RECEIVER_OPERATOR_CHARACTERISTICS]
+    assert lo <= q1 <= med <= q3 <= hi and med > 0.7
+    assert len(boot.important_features) == 14
+    txt = open(tmp_path / "out" / "diagnostic.txt").read()
+    assert "Learning curve" in txt and "Bootstrap" in txt
