@@ -114,3 +114,36 @@ def test_hyperparameter_tuning_adds_models(game_avro, tmp_path):
     lams = {r.config["fixed"].regularization_weight for r in res["tuned"]}
     assert len(lams) == 3 and all(1e-4 <= l <= 1e4 for l in lams)
     assert sorted(os.listdir(out / "models")) == ["0", "1", "2"]
+
+
+def test_feature_tools_index_and_bags(game_avro, tmp_path):
+    from photon_ml_amd.cli import feature_tools
+    from photon_ml_amd.io.index_map import OffHeapIndexMap, index_map_from_feature_bags
+    a = feature_tools.build_parser().parse_args(
+        ["index", "--input-data-directories", str(game_avro / "train"), "--root-output-directory",
+         str(tmp_path / "idx"), "--num-storage-partitions", "3", *SHARDS])
+    maps = feature_tools.run_indexing(a)
+    assert maps["global"].feature_dimension == 20 and maps["user"].feature_dimension == 6
+    b = feature_tools.build_parser().parse_args(
+        ["bags", "--input-data-directories", str(game_avro / "train"), "--root-output-directory",
+         str(tmp_path / "bags"), "--feature-bags-keys", "features,userFeatures"])
+    keys = feature_tools.run_bags(b)
+    assert len(keys["features"]) == 19 and open(tmp_path / "bags" / "features").read().count("\t") == 19
+    im = index_map_from_feature_bags(str(tmp_path / "bags"), ["features"], True)
+    assert im.feature_dimension == 20
+    # training against the off-heap maps and then the bags directory gives the same model
+    res = {}
+    for i, opt in enumerate([["--off-heap-index-map-directory", str(tmp_path / "idx"),
+                              "--off-heap-index-map-partitions", "3"],
+                ["--feature-bags-directory", str(tmp_path / "bags")]]):
+        out = tmp_path / f"o{i}"
+        args = ["--input-data-directories", str(game_avro / "train"), "--root-output-directory", str(out),
+                "--training-task", "LOGISTIC_REGRESSION", *SHARDS, "--coordinate-configurations",
+                FIXED.replace("10|0.1", "1"), "--coordinate-update-sequence", "fixed",
+                "--coordinate-descent-iterations", "1", "--device", "cpu", *opt]
+        r = game_training.GameTrainingDriver(game_training.build_parser().parse_args(args)).run()
+        m, maps_used = r["explicit"][0].model, r["index_maps"]["global"]
+        w = m.get("fixed").glm.coefficients.means.numpy()
+        res[opt[0]] = {maps_used.get_feature_name(j): w[j] for j in range(len(w))}
+    a_, b_ = res.values()
+    assert set(a_) == set(b_) and all(abs(a_[k] - b_[k]) < 1e-6 for k in a_)
