@@ -39,6 +39,12 @@ class CoordinateDescent:
     def _dev(self, t: torch.Tensor) -> torch.Tensor:
         return t if self.score_device is None else t.to(self.score_device)
 
+    def _score_validation(self, cid, model, device):
+        coord = self.coordinates[cid]
+        if hasattr(coord, "score_validation"):  # entity-sharded coordinates route validation rows to owners
+            return coord.score_validation(model, self.validation_data)
+        return model.score(self.validation_data, device)
+
     def run(self, iterations: int, initial_model: Optional[GameModel] = None) -> Tuple[GameModel, Optional[list]]:
         if iterations <= 0:
             raise ValueError(f"Number of coordinate descent iterations must be greater than 0: {iterations}")
@@ -53,7 +59,7 @@ class CoordinateDescent:
         reg_terms = {cid: c.regularization_term_value(model.get(cid)) for cid, c in self.coordinates.items()}
         val_scores, val_full = None, None
         if self.validation_data is not None:
-            val_scores = {cid: self._dev(model.get(cid).score(self.validation_data, full.device))
+            val_scores = {cid: self._dev(self._score_validation(cid, model.get(cid), full.device))
                           for cid in self.coordinates}
             val_full = sum(val_scores.values())
         best_model, best_evals = None, None
@@ -80,7 +86,7 @@ class CoordinateDescent:
                         rec["training_loss"] = loss
                         rec["objective"] = loss + sum(reg_terms.values())
                     if self.validation_data is not None:
-                        vs = self._dev(new.score(self.validation_data, full.device))
+                        vs = self._dev(self._score_validation(cid, new, full.device))
                         val_full = val_full - val_scores[cid] + vs
                         val_scores[cid] = vs
                         evaluations = [(e, e.evaluate(val_full)) for e in self.validation_evaluators]

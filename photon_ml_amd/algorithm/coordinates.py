@@ -246,3 +246,89 @@ class RandomEffectCoordinate(Coordinate):
         reg, lam = self.opt_config.regularization_context, self.opt_config.regularization_weight
         v = model.values
         return reg.l1_weight(lam) * float(np.abs(v).sum()) + 0.5 * reg.l2_weight(lam) * float((v * v).sum())
+
+
+class ShardedRandomEffectCoordinate(Coordinate):
+    """Random-effect coordinate under a process group: entities are OWNED by one rank each.
+
+    Construction routes every local sample row of this coordinate's feature shard to the owner of its entity
+    (:class:`photon_ml_amd.parallel.sharding.RowRouter`, one all-to-all — SURVEY C8) and builds an ordinary
+    :class:`RandomEffectCoordinate` over the received rows. Each update then moves only N-length vectors:
+    partial scores forward (C11), new scores backward (C12). The returned :class:`RandomEffectModel` holds the
+    owned entities only; save it per rank (``io.model_io.save_game_model`` writes per-rank part files).
+    Reference: ``RandomEffectDataSetPartitioner.scala:113-147``, ``RandomEffectCoordinate.scala:103-187``.
+    """
+
+    def __init__(self, coordinate_id: str, data: GameData, data_config: RandomEffectDataConfiguration,
+                 opt_config: GLMOptimizationConfiguration, task, compute_variance: bool = False, device=None,
+                 dtype=torch.float64):
+        from ..parallel.sharding import EntityPartitioner, RowRouter, stable_hash64
+        self.coordinate_id = coordinate_id
+        self.data_config = data_config
+        self.device = torch.device(device) if device is not None else default_device()
+        re_type, shard = data_config.random_effect_type, data_config.feature_shard_id
+        ids = np.asarray(data.id_tags[re_type])
+        keys = stable_hash64(ids)
+        self.partitioner = EntityPartitioner.build(keys)
+        self.router = RowRouter(self.partitioner.owner(keys))
+        self.recv_data = self._route(data, self.router, ids)
+        self.inner = RandomEffectCoordinate(coordinate_id, self.recv_data, data_config, opt_config, task,
+                                            compute_variance, device, dtype)
+        self._val_cache = {}
+
+    def _route(self, data: GameData, router, ids) -> GameData:
+        re_type, shard = self.data_config.random_effect_type, self.data_config.feature_shard_id
+        fwd = lambda a: router.forward(torch.from_numpy(np.ascontiguousarray(a))).numpy()
+        x = router.forward_csr(data.shard(shard))
+        # entity-id strings of the received rows: send the index into this rank's unique-id table with the row,
+        # and all-gather the (small) unique-id tables once
+        from torch import distributed as tdist
+        from ..parallel.dist import world_size
+        uniq, inv = np.unique(ids.astype(str), return_inverse=True)
+        tables = [None] * world_size()
+        tdist.all_gather_object(tables, list(uniq))
+        code = fwd(inv.astype(np.int64))
+        flat = np.array([s for t in tables for s in t], dtype=object)
+        base = np.concatenate([[0], np.cumsum([len(t) for t in tables])]).astype(np.int64)
+        recv_ids = flat[base[router.src_rank] + code] if len(code) else np.zeros(0, dtype=object)
+        tags = {re_type: recv_ids}
+        return GameData(fwd(data.response), {shard: x}, tags, fwd(data.offsets), fwd(data.weights),
+                        fwd(data.uids), None)
+
+    @property
+    def dataset(self):
+        return self.inner.dataset
+
+    @property
+    def last_stats(self):
+        return self.inner.last_stats
+
+    def set_config(self, opt_config):
+        self.inner.set_config(opt_config)
+
+    def initialize_model(self):
+        return self.inner.initialize_model()
+
+    def update_model(self, model, partial_score: Optional[torch.Tensor] = None):
+        p = None if partial_score is None else self.router.forward(partial_score.detach().to("cpu", torch.float64))
+        return self.inner.update_model(model, p)
+
+    def score(self, model) -> torch.Tensor:
+        s = self.inner.score(model).detach().to("cpu", torch.float64)
+        return self.router.backward(s).to(self.device)
+
+    def score_validation(self, model, vdata: GameData) -> torch.Tensor:
+        """Route validation rows to entity owners once (cached per dataset), score there, route back."""
+        from ..parallel.sharding import RowRouter, stable_hash64
+        key = id(vdata)
+        if key not in self._val_cache:
+            ids = np.asarray(vdata.id_tags[self.data_config.random_effect_type])
+            router = RowRouter(self.partitioner.owner(stable_hash64(ids)))
+            self._val_cache[key] = (router, self._route(vdata, router, ids))
+        router, recv = self._val_cache[key]
+        s = model.score(recv, "cpu").to(torch.float64)
+        return router.backward(s).to(self.device)
+
+    def regularization_term_value(self, model) -> float:
+        from ..parallel.dist import all_reduce_scalar
+        return all_reduce_scalar(self.inner.regularization_term_value(model))

@@ -24,7 +24,7 @@ import numpy as np
 import torch
 
 from ..algorithm.coordinate_descent import CoordinateDescent
-from ..algorithm.coordinates import FixedEffectCoordinate, RandomEffectCoordinate
+from ..algorithm.coordinates import FixedEffectCoordinate, RandomEffectCoordinate, ShardedRandomEffectCoordinate
 from ..constants import TaskType
 from ..data.game_data import GameData
 from ..data.matrix import LabeledData
@@ -128,8 +128,8 @@ class GameEstimator:
             dc = self.coordinate_data_configurations[cid]
             oc = first_cfg[cid]
             if isinstance(dc, RandomEffectDataConfiguration):
-                coords[cid] = RandomEffectCoordinate(cid, data, dc, oc, self.training_task, self.compute_variance,
-                                                     self.device)
+                cls = ShardedRandomEffectCoordinate if is_dist() else RandomEffectCoordinate
+                coords[cid] = cls(cid, data, dc, oc, self.training_task, self.compute_variance, self.device)
             else:
                 coords[cid] = FixedEffectCoordinate(cid, data, dc, oc, self.training_task,
                                                     self.coordinate_normalization_contexts.get(cid),

@@ -19,7 +19,7 @@ from __future__ import annotations
 import math
 import re
 from dataclasses import dataclass
-from typing import Optional, Sequence
+from typing import List, Optional, Sequence
 
 import numpy as np
 import torch
@@ -64,11 +64,35 @@ def precision_at_k(scores, labels, k: int) -> float:
     return hits / k
 
 
+def _dist():
+    from ..parallel.dist import is_dist
+    return is_dist()
+
+
+def _allsum(*vals: float) -> List[float]:
+    """Sum scalars over the process group (one collective)."""
+    from ..parallel.dist import all_reduce_
+    from ..parallel.sharding import comm_device
+    t = torch.tensor(vals, dtype=torch.float64, device=comm_device())
+    all_reduce_(t)
+    return t.tolist()
+
+
+def _gather(t: torch.Tensor) -> torch.Tensor:
+    from ..parallel.sharding import all_gather_varlen
+    return torch.cat([x.to(t.device) for x in all_gather_varlen(t.detach().cpu())])
+
+
 class Evaluator:
+    """Evaluates ``scores + offsets`` against the labels. Under a process group every rank holds a row shard:
+    additive metrics (losses, RMSE) all-reduce their sums, rank metrics (AUC, per-group metrics) all-gather the
+    (score, label[, weight, group]) columns first."""
+
     name = "EVALUATOR"
     higher_is_better = True
 
     def __init__(self, labels, offsets=None, weights=None, device=None):
+        self.distributed = _dist()
         self.labels = _t(labels, device)
         n = self.labels.numel()
         self.offsets = torch.zeros(n, dtype=torch.float64, device=self.labels.device) if offsets is None else _t(
@@ -94,6 +118,8 @@ class AUCEvaluator(Evaluator):
     name = "AUC"
 
     def _evaluate(self, s):
+        if self.distributed:
+            return auc_weighted(_gather(s), _gather(self.labels), None)
         return auc_weighted(s, self.labels, None)  # MLlib AUC ignores weights
 
 
@@ -103,7 +129,10 @@ class RMSEEvaluator(Evaluator):
 
     def _evaluate(self, s):
         d = s - self.labels
-        return math.sqrt(float(torch.sum(self.weights * 0.5 * d * d)) / max(self.labels.numel(), 1))
+        num, cnt = float(torch.sum(self.weights * 0.5 * d * d)), float(self.labels.numel())
+        if self.distributed:
+            num, cnt = _allsum(num, cnt)
+        return math.sqrt(num / max(cnt, 1.0))
 
 
 class _LossEvaluator(Evaluator):
@@ -112,7 +141,8 @@ class _LossEvaluator(Evaluator):
 
     def _evaluate(self, s):
         l, _ = self.loss.loss_and_dz(s, self.labels)
-        return float(torch.sum(self.weights * l))
+        v = float(torch.sum(self.weights * l))
+        return _allsum(v)[0] if self.distributed else v
 
 
 class LogisticLossEvaluator(_LossEvaluator):
@@ -141,7 +171,14 @@ class MultiEvaluator(Evaluator):
     def __init__(self, ids, labels, offsets=None, weights=None, device=None):
         super().__init__(labels, offsets, weights, device)
         ids = np.asarray(ids)
-        uniq, inv = np.unique(ids.astype(str) if ids.dtype == object else ids, return_inverse=True)
+        if self.distributed:  # groups can span ranks: gather group keys once, evaluate on the gathered columns
+            from ..parallel.sharding import stable_hash64
+            keys = _gather(torch.from_numpy(stable_hash64(ids))).numpy()
+            uniq, inv = np.unique(keys, return_inverse=True)
+            self.labels_all = _gather(self.labels)
+            self.weights_all = _gather(self.weights)
+        else:
+            uniq, inv = np.unique(ids.astype(str) if ids.dtype == object else ids, return_inverse=True)
         self.group = torch.as_tensor(inv, dtype=torch.int64, device=self.labels.device)
         self.n_groups = len(uniq)
 
@@ -151,7 +188,10 @@ class MultiEvaluator(Evaluator):
     def _evaluate(self, s):
         order = torch.argsort(self.group, stable=True)
         g = self.group[order]
-        s, y, w = s[order], self.labels[order], self.weights[order]
+        if self.distributed:
+            s, y, w = _gather(s)[order], self.labels_all[order], self.weights_all[order]
+        else:
+            s, y, w = s[order], self.labels[order], self.weights[order]
         counts = torch.bincount(g, minlength=self.n_groups).cpu().numpy()
         starts = np.concatenate([[0], np.cumsum(counts)])
         vals = []

@@ -89,12 +89,20 @@ def opt_configs_to_json(configs) -> dict:
 
 def save_game_model(model: GameModel, out_dir: str, index_maps: Dict[str, IndexMap], task=None,
                     opt_configs=None, re_file_limit: Optional[int] = None, entities_per_file: int = 100000):
+    from ..parallel.dist import is_dist, rank
     task = TaskType.parse(task) if task is not None else model.task
     os.makedirs(out_dir, exist_ok=True)
-    with open(os.path.join(out_dir, METADATA), "w") as f:
-        json.dump({"modelType": task.value, "optimizationConfigurations": opt_configs_to_json(opt_configs)}, f,
-                  indent=2)
+    # under a process group: rank 0 writes metadata + (replicated) fixed effects; every rank writes the random-effect
+    # entities it owns as its own part files (the reference saves RE RDD partitions in parallel the same way)
+    sharded, r = is_dist(), rank()
+    lead = r == 0
+    if lead:
+        with open(os.path.join(out_dir, METADATA), "w") as f:
+            json.dump({"modelType": task.value, "optimizationConfigurations": opt_configs_to_json(opt_configs)}, f,
+                      indent=2)
     for cid, m in model:
+        if isinstance(m, FixedEffectModel) and not lead:
+            continue
         if isinstance(m, FixedEffectModel):
             d = os.path.join(out_dir, FIXED_EFFECT, cid)
             os.makedirs(os.path.join(d, COEFFICIENTS), exist_ok=True)
@@ -108,8 +116,9 @@ def save_game_model(model: GameModel, out_dir: str, index_maps: Dict[str, IndexM
         elif isinstance(m, RandomEffectModel):
             d = os.path.join(out_dir, RANDOM_EFFECT, cid)
             os.makedirs(os.path.join(d, COEFFICIENTS), exist_ok=True)
-            with open(os.path.join(d, ID_INFO), "w") as f:
-                f.write(m.random_effect_type + "\n" + m.feature_shard_id + "\n")
+            if lead:
+                with open(os.path.join(d, ID_INFO), "w") as f:
+                    f.write(m.random_effect_type + "\n" + m.feature_shard_id + "\n")
             im = index_maps[m.feature_shard_id]
             ent = m.keys // m.dim
             feat = m.keys % m.dim
@@ -125,8 +134,9 @@ def save_game_model(model: GameModel, out_dir: str, index_maps: Dict[str, IndexM
             if re_file_limit is not None:
                 n_files = max(1, min(n_files, re_file_limit))
             per = (len(recs) + n_files - 1) // n_files if recs else 0
+            prefix = f"part-r{r:05d}-" if sharded else "part-"
             for i in range(n_files):
-                write_records(os.path.join(d, COEFFICIENTS, f"part-{i:05d}.avro"), BAYESIAN_LINEAR_MODEL,
+                write_records(os.path.join(d, COEFFICIENTS, f"{prefix}{i:05d}.avro"), BAYESIAN_LINEAR_MODEL,
                               recs[i * per:(i + 1) * per])
         else:
             raise TypeError(f"unknown model type {type(m)}")

@@ -1,0 +1,204 @@
+"""Entity sharding and residual routing for multi-GPU GAME (SURVEY §2.9 C8-C12, §2.10 entity parallelism).
+
+Reference: ``photon-api/.../data/RandomEffectDataSetPartitioner.scala:42-148`` (count rows per entity, take the
+10,000 largest, greedily bin-pack them onto the least-loaded partition with a min-heap, hash the rest),
+``RandomEffectDataSet.scala:68-88, 239-315`` (groupByKey of rows by entity, ``addScoresToOffsets`` = join +
+groupByKey every update) and ``RandomEffectCoordinate.scala:157-187`` (scores re-partitioned by uid).
+
+MI355X design: rows stay in their sample shard for the fixed effects; for each random-effect coordinate every row
+is ROUTED ONCE to the GPU that owns its entity (one variable-size all-to-all of the feature rows at build time,
+C8). The permutation is kept, so each coordinate update moves only N-length fp64 vectors: partial scores to the
+owners (C11) and new scores back (C12) — two ``all_to_all_single`` calls over xGMI per RE update instead of two
+shuffles. Entity ownership is computed identically on every rank from all-gathered (entity key, count) pairs
+(C9), so no broadcast is needed.
+"""
+from __future__ import annotations
+
+import heapq
+from typing import List, Optional, Sequence, Tuple
+
+import numpy as np
+import scipy.sparse as sp
+import torch
+import torch.distributed as dist
+
+from .dist import is_dist, rank as _rank, world_size as _world
+
+TOP_ENTITIES = 10_000
+
+
+def stable_hash64(ids: np.ndarray) -> np.ndarray:
+    """Deterministic 64-bit key of each entity id (same on every rank / run; pandas' SipHash with a fixed key)."""
+    import pandas as pd
+    ids = np.asarray(ids)
+    if ids.dtype.kind in "iu":
+        return pd.util.hash_array(ids.astype(np.int64)).view(np.int64)
+    return pd.util.hash_array(ids.astype(str).astype(object)).view(np.int64)
+
+
+def comm_device(group=None) -> torch.device:
+    if is_dist() and dist.get_backend(group) == "nccl":
+        return torch.device("cuda", torch.cuda.current_device())
+    return torch.device("cpu")
+
+
+def all_gather_varlen(t: torch.Tensor, group=None) -> List[torch.Tensor]:
+    """All-gather 1-D tensors of different lengths (pads to the max length)."""
+    if not is_dist():
+        return [t]
+    dev = comm_device(group)
+    n = torch.tensor([t.numel()], dtype=torch.int64, device=dev)
+    sizes = [torch.zeros_like(n) for _ in range(_world())]
+    dist.all_gather(sizes, n, group=group)
+    sizes = [int(s.item()) for s in sizes]
+    m = max(sizes) if sizes else 0
+    buf = torch.zeros(m, dtype=t.dtype, device=dev)
+    buf[: t.numel()] = t.to(dev)
+    outs = [torch.zeros_like(buf) for _ in range(_world())]
+    dist.all_gather(outs, buf, group=group)
+    return [o[:s].to(t.device) for o, s in zip(outs, sizes)]
+
+
+def all_to_all_varlen(send: torch.Tensor, send_counts: Sequence[int], group=None) -> Tuple[torch.Tensor, List[int]]:
+    """Variable-size all-to-all along dim 0 (rows already grouped by destination rank)."""
+    if not is_dist():
+        return send, list(send_counts)
+    dev = comm_device(group)
+    sc = torch.tensor(list(send_counts), dtype=torch.int64, device=dev)
+    rc = torch.empty_like(sc)
+    dist.all_to_all_single(rc, sc, group=group)
+    recv_counts = [int(x) for x in rc.tolist()]
+    tail = tuple(send.shape[1:])
+    out = torch.empty((sum(recv_counts),) + tail, dtype=send.dtype, device=dev)
+    dist.all_to_all_single(out, send.to(dev).contiguous(), recv_counts, list(send_counts), group=group)
+    return out.to(send.device), recv_counts
+
+
+class EntityPartitioner:
+    """Entity key -> owning rank: greedy least-loaded bin packing of the largest entities, hash for the rest."""
+
+    def __init__(self, keys: np.ndarray, counts: np.ndarray, n_parts: int, top_k: int = TOP_ENTITIES):
+        self.n_parts = n_parts
+        order = np.lexsort((keys, -counts))  # count desc, key asc: identical on every rank
+        top = order[:top_k]
+        heap = [(0, p) for p in range(n_parts)]
+        heapq.heapify(heap)
+        owner = {}
+        for i in top:
+            load, p = heapq.heappop(heap)
+            owner[int(keys[i])] = p
+            heapq.heappush(heap, (load + int(counts[i]), p))
+        self.top_keys = np.fromiter(owner.keys(), dtype=np.int64, count=len(owner))
+        self.top_owner = np.fromiter(owner.values(), dtype=np.int64, count=len(owner))
+        srt = np.argsort(self.top_keys)
+        self.top_keys, self.top_owner = self.top_keys[srt], self.top_owner[srt]
+
+    def owner(self, keys: np.ndarray) -> np.ndarray:
+        keys = np.asarray(keys, dtype=np.int64)
+        out = (keys.view(np.uint64) % np.uint64(self.n_parts)).astype(np.int64)
+        if len(self.top_keys):
+            pos = np.searchsorted(self.top_keys, keys)
+            pos_c = np.minimum(pos, len(self.top_keys) - 1)
+            hit = self.top_keys[pos_c] == keys
+            out[hit] = self.top_owner[pos_c[hit]]
+        return out
+
+    @staticmethod
+    def build(local_keys: np.ndarray, group=None, top_k: int = TOP_ENTITIES) -> "EntityPartitioner":
+        """All-gather per-rank (key, count) histograms (C9) and build the same partitioner everywhere."""
+        uk, cnt = np.unique(np.asarray(local_keys, dtype=np.int64), return_counts=True)
+        ks = all_gather_varlen(torch.from_numpy(uk), group)
+        cs = all_gather_varlen(torch.from_numpy(cnt.astype(np.int64)), group)
+        keys = torch.cat(ks).numpy()
+        counts = torch.cat(cs).numpy()
+        gk, inv = np.unique(keys, return_inverse=True)
+        gc = np.bincount(inv, weights=counts).astype(np.int64)
+        return EntityPartitioner(gk, gc, _world(), top_k)
+
+
+class RowRouter:
+    """Fixed permutation between this rank's sample rows and the rows it owns after routing by ``dest``.
+
+    ``forward(v)``: local sample order -> concatenation over source ranks of the rows sent here (owner order);
+    ``backward(u)``: the inverse (owner order -> local sample order). Both are one ``all_to_all_single``.
+    """
+
+    def __init__(self, dest: np.ndarray, group=None):
+        self.group = group
+        dest = np.asarray(dest, dtype=np.int64)
+        self.n_local = len(dest)
+        P = _world()
+        self.perm = np.argsort(dest, kind="stable")          # local rows grouped by destination
+        self.send_counts = np.bincount(dest, minlength=P).tolist()
+        # exchange counts
+        if is_dist():
+            dev = comm_device(group)
+            sc = torch.tensor(self.send_counts, dtype=torch.int64, device=dev)
+            rc = torch.empty_like(sc)
+            dist.all_to_all_single(rc, sc, group=group)
+            self.recv_counts = [int(x) for x in rc.tolist()]
+        else:
+            self.recv_counts = list(self.send_counts)
+        self.n_recv = int(sum(self.recv_counts))
+        self.src_rank = np.repeat(np.arange(P), self.recv_counts)
+
+    def forward(self, v) -> torch.Tensor:
+        t = torch.as_tensor(v)
+        send = t[torch.from_numpy(self.perm).to(t.device)]
+        if not is_dist():
+            return send
+        out, _ = self._a2a(send, self.send_counts, self.recv_counts)
+        return out
+
+    def backward(self, u) -> torch.Tensor:
+        t = torch.as_tensor(u)
+        if is_dist():
+            t, _ = self._a2a(t, self.recv_counts, self.send_counts)
+        out = torch.empty_like(t)
+        out[torch.from_numpy(self.perm).to(t.device)] = t
+        return out
+
+    def _a2a(self, send: torch.Tensor, sc: List[int], rc: List[int]):
+        dev = comm_device(self.group)
+        tail = tuple(send.shape[1:])
+        out = torch.empty((sum(rc),) + tail, dtype=send.dtype, device=dev)
+        dist.all_to_all_single(out, send.to(dev).contiguous(), rc, sc, group=self.group)
+        return out.to(send.device), rc
+
+    def forward_csr(self, x: sp.csr_matrix) -> sp.csr_matrix:
+        """Route sparse rows (one all-to-all each for row lengths, column indices and values)."""
+        x = x.tocsr()
+        lens = np.diff(x.indptr).astype(np.int64)
+        rl = self.forward(torch.from_numpy(lens)).numpy()
+        order = self.perm
+        ol = lens[order]
+        tot = int(ol.sum())
+        # entry positions of the permuted rows, vectorised: start of each row repeated + offset within the row
+        first = np.repeat(x.indptr[order].astype(np.int64) - np.concatenate([[0], np.cumsum(ol)[:-1]]), ol)
+        ent = first + np.arange(tot, dtype=np.int64)
+        idx, val = x.indices[ent], x.data[ent]
+        nnz_send = [int(lens[order[a:b]].sum()) for a, b in _ranges(self.send_counts)]
+        nnz_recv = [int(rl[a:b].sum()) for a, b in _ranges(self.recv_counts)]
+        ri = torch.from_numpy(idx.astype(np.int64))
+        rv = torch.from_numpy(val.astype(np.float64))
+        if is_dist():
+            ri, _ = self._a2a(ri, nnz_send, nnz_recv)
+            rv, _ = self._a2a(rv, nnz_send, nnz_recv)
+        indptr = np.concatenate([[0], np.cumsum(rl)]).astype(np.int64)
+        return sp.csr_matrix((rv.numpy(), ri.numpy(), indptr), shape=(self.n_recv, x.shape[1]))
+
+
+def _ranges(counts: Sequence[int]):
+    s = 0
+    for c in counts:
+        yield s, s + int(c)
+        s += int(c)
+
+
+def gather_strings(values: Sequence[str], group=None) -> List[str]:
+    """All-gather a list of strings (object collective; used once per coordinate for entity-id names)."""
+    if not is_dist():
+        return list(values)
+    out: List[Optional[list]] = [None] * _world()
+    dist.all_gather_object(out, list(values), group=group)
+    return [s for part in out for s in part]

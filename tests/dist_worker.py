@@ -1,0 +1,89 @@
+"""Worker bodies for the multi-process (gloo, CPU) tests in test_distributed.py — the analogue of the
+reference's Spark local[*] "fake cluster" tests (SURVEY §4 tier 4)."""
+import os
+import sys
+
+import numpy as np
+import torch
+
+sys.path.insert(0, os.path.dirname(os.path.dirname(os.path.abspath(__file__))))
+
+
+def _init(rank, world, port):
+    os.environ.update({"MASTER_ADDR": "127.0.0.1", "MASTER_PORT": str(port), "RANK": str(rank),
+                       "WORLD_SIZE": str(world), "LOCAL_RANK": str(rank), "PML_BACKEND": "torch"})
+    from photon_ml_amd.parallel.dist import init_distributed
+    init_distributed("gloo")
+
+
+def glm_worker(rank, world, port, out):
+    _init(rank, world, port)
+    from photon_ml_amd.data.synthetic import generate_glm_data
+    from photon_ml_amd.estimators.game_estimator import train_generalized_linear_model
+    from photon_ml_amd.optimization.config import RegularizationContext
+    data, _ = generate_glm_data("LOGISTIC_REGRESSION", 3000, 40, density=0.2, seed=7)
+    local = data.subset(np.arange(rank, data.n_rows, world))
+    for opt, reg in (("LBFGS", "L2"), ("TRON", "L2"), ("LBFGS", "L1")):
+        res = train_generalized_linear_model(local, "LOGISTIC_REGRESSION", opt, RegularizationContext(reg), [1.0],
+                                             max_iterations=200, tolerance=1e-10, device="cpu")
+        np.save(f"{out}/glm_{opt}_{reg}_r{rank}.npy", res[0][1].coefficients.means.numpy())
+    import torch.distributed as dist
+    dist.destroy_process_group()
+
+
+def game_worker(rank, world, port, out):
+    _init(rank, world, port)
+    from photon_ml_amd.data.game_data import generate_game_data
+    from photon_ml_amd.data.random_effect import FixedEffectDataConfiguration, RandomEffectDataConfiguration
+    from photon_ml_amd.estimators.game_estimator import GameEstimator
+    from photon_ml_amd.io.index_map import DefaultIndexMap
+    from photon_ml_amd.io.model_io import save_game_model
+    from photon_ml_amd.optimization.config import (GLMOptimizationConfiguration, OptimizerConfig,
+                                                   RegularizationContext)
+    data, _ = generate_game_data(n_rows=3000, n_users=40, n_items=25, seed=31, task="LOGISTIC_REGRESSION")
+    tr, va = data.subset(np.arange(2400)), data.subset(np.arange(2400, 3000))
+    tr_l = tr.subset(np.arange(rank, tr.n_rows, world))
+    va_l = va.subset(np.arange(rank, va.n_rows, world))
+    cfg = GLMOptimizationConfiguration(OptimizerConfig("TRON", 50, 1e-10), RegularizationContext("L2"), 1.0)
+    est = (GameEstimator(device="cpu").set_training_task("LOGISTIC_REGRESSION")
+           .set_coordinate_data_configurations({"global": FixedEffectDataConfiguration("global"),
+                                                "per-user": RandomEffectDataConfiguration("userId", "user"),
+                                                "per-item": RandomEffectDataConfiguration("itemId", "item")})
+           .set_coordinate_update_sequence(["global", "per-user", "per-item"])
+           .set_coordinate_descent_iterations(2)
+           .set_validation_evaluators(["AUC", "LOGISTIC_LOSS", "AUC:userId"]))
+    res = est.fit(tr_l, va_l, [{"global": cfg, "per-user": cfg, "per-item": cfg}])[0]
+    np.save(f"{out}/game_fe_r{rank}.npy", res.model.get("global").glm.coefficients.means.numpy())
+    np.save(f"{out}/game_eval_r{rank}.npy", np.array([v for _, v in res.evaluations]))
+    maps = {s: DefaultIndexMap.from_keys([f"f{j}\u0001t" for j in range(data.shards[s].shape[1])])
+            for s in data.shards}
+    save_game_model(res.model, f"{out}/model", maps, opt_configs=res.config)
+    import torch.distributed as dist
+    dist.barrier()
+    dist.destroy_process_group()
+
+
+def sharding_worker(rank, world, port, out):
+    _init(rank, world, port)
+    import scipy.sparse as sp
+    from photon_ml_amd.parallel.sharding import EntityPartitioner, RowRouter, stable_hash64
+    rng = np.random.default_rng(rank)
+    ids = np.array([f"u{i}" for i in rng.integers(0, 30, 80)], dtype=object)
+    keys = stable_hash64(ids)
+    part = EntityPartitioner.build(keys, top_k=5)
+    router = RowRouter(part.owner(keys))
+    v = torch.arange(80, dtype=torch.float64) + 1000 * rank
+    assert torch.equal(router.backward(router.forward(v)), v)
+    x = sp.random(80, 9, density=0.3, format="csr", random_state=rank)
+    assert np.allclose(router.forward_csr(x).toarray(), router.forward(torch.from_numpy(x.toarray())).numpy())
+    # every received row belongs to an entity this rank owns
+    recv_keys = router.forward(torch.from_numpy(keys)).numpy()
+    assert np.all(part.owner(recv_keys) == rank)
+    np.save(f"{out}/shard_r{rank}.npy", np.array([router.n_recv]))
+    import torch.distributed as dist
+    dist.destroy_process_group()
+
+
+if __name__ == "__main__":
+    fn = {"glm": glm_worker, "game": game_worker, "sharding": sharding_worker}[sys.argv[1]]
+    fn(int(sys.argv[2]), int(sys.argv[3]), int(sys.argv[4]), sys.argv[5])
