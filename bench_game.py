@@ -1,0 +1,128 @@
+#!/usr/bin/env python3
+"""GAME benchmark: fixed + random effect coordinate descent iterations per second (BASELINE.json's second
+metric, "GAME coord-descent iters/sec"; config 5 = fixed + per-entity random effects sharded across the GPUs).
+
+Weak scaling: every rank generates ``--entities-per-gpu`` entities x ``--rows-per-entity`` rows (synthetic,
+``photon_ml_amd.data.synthetic.generate_game_bench_data``): a ``global`` fixed-effect shard (``--fe-dim``
+Zipf features, ``--fe-nnz`` per row + intercept) and an ``entity`` random-effect shard (``--re-dim`` private
+features per entity, ``--re-nnz`` per row + intercept). Under torchrun the fixed effect is row-data-parallel (one
+packed RCCL all-reduce per evaluation) and the random effect is entity-sharded (all-to-all residual routing);
+random-effect solves run as ONE block-diagonal TRON over all owned entities on the GLM HIP kernels.
+
+One STEP = one full coordinate-descent sweep: fixed-effect L-BFGS (``--fe-iters`` iterations) on offsets =
+random-effect scores, then the batched per-entity TRON (``--re-iters`` iterations) on offsets = fixed-effect
+scores, both rescored, plus the training-loss evaluation. Nothing is skipped inside the timed region.
+
+Usage: python bench_game.py [--gpus N --steps K --warmup W]; for N > 1 launch with torch.distributed.run.
+"""
+from __future__ import annotations
+
+import argparse
+import json
+import os
+import sys
+import time
+
+
+def log(msg):
+    if int(os.environ.get("RANK", "0")) == 0:
+        print(f"[bench_game {time.strftime('%H:%M:%S')}] {msg}", file=sys.stderr, flush=True)
+
+
+def main():
+    ap = argparse.ArgumentParser()
+    ap.add_argument("--gpus", type=int, default=1)
+    ap.add_argument("--steps", type=int, default=3)
+    ap.add_argument("--warmup", type=int, default=1)
+    ap.add_argument("--entities-per-gpu", type=int, default=200_000)
+    ap.add_argument("--rows-per-entity", type=int, default=50)
+    ap.add_argument("--re-dim", type=int, default=100)
+    ap.add_argument("--re-nnz", type=int, default=10)
+    ap.add_argument("--fe-dim", type=int, default=1_000_000)
+    ap.add_argument("--fe-nnz", type=int, default=30)
+    ap.add_argument("--fe-iters", type=int, default=10)
+    ap.add_argument("--re-iters", type=int, default=10)
+    ap.add_argument("--precision", default="bf16", choices=["bf16", "f32", "f64"])
+    ap.add_argument("--seed", type=int, default=11)
+    args = ap.parse_args()
+
+    import numpy as np
+    import torch
+    from collections import OrderedDict
+    from photon_ml_amd.parallel.dist import init_distributed, all_reduce_scalar, barrier
+    rank, world, local = init_distributed()
+    if torch.cuda.is_available():
+        torch.cuda.set_device(local)
+        dev = torch.device("cuda", local)
+    else:
+        dev = torch.device("cpu")
+    from photon_ml_amd.algorithm.coordinate_descent import CoordinateDescent
+    from photon_ml_amd.algorithm.coordinates import (FixedEffectCoordinate, RandomEffectCoordinate,
+                                                     ShardedRandomEffectCoordinate)
+    from photon_ml_amd.data.random_effect import FixedEffectDataConfiguration, RandomEffectDataConfiguration
+    from photon_ml_amd.data.synthetic import generate_game_bench_data
+    from photon_ml_amd.evaluation.evaluators import build_evaluator
+    from photon_ml_amd.optimization.config import (GLMOptimizationConfiguration, OptimizerConfig,
+                                                   RegularizationContext)
+
+    t0 = time.time()
+    data = generate_game_bench_data(args.entities_per_gpu, args.rows_per_entity, args.re_dim, args.re_nnz,
+                                    args.fe_dim, args.fe_nnz, seed=args.seed + 1000 * rank,
+                                    entity_offset=rank * args.entities_per_gpu)
+    log(f"data generated in {time.time() - t0:.1f}s: {data.n_rows} rows/GPU")
+    t0 = time.time()
+    fe_cfg = GLMOptimizationConfiguration(OptimizerConfig("LBFGS", args.fe_iters, 1e-12),
+                                          RegularizationContext("L2"), 1.0)
+    re_cfg = GLMOptimizationConfiguration(OptimizerConfig("TRON", args.re_iters, 1e-12),
+                                          RegularizationContext("L2"), 1.0)
+    task = "LOGISTIC_REGRESSION"
+    re_cls = ShardedRandomEffectCoordinate if world > 1 else RandomEffectCoordinate
+    coords = OrderedDict([
+        ("global", FixedEffectCoordinate("global", data, FixedEffectDataConfiguration("global"), fe_cfg, task,
+                                         device=dev, precision=args.precision)),
+        ("per-entity", re_cls("per-entity", data, RandomEffectDataConfiguration("entityId", "entity"), re_cfg,
+                              task, device=dev)),
+    ])
+    if torch.cuda.is_available():
+        torch.cuda.synchronize()
+    log(f"coordinates built in {time.time() - t0:.1f}s; RE: {coords['per-entity'].dataset.summary()}")
+    train_eval = build_evaluator("LOGISTIC_LOSS", data.response, data.offsets, data.weights, device=dev)
+    cd = CoordinateDescent(coords, train_eval, score_device=dev)
+    model, _ = cd.run(args.warmup)
+    if torch.cuda.is_available():
+        torch.cuda.synchronize()
+    barrier()
+    t1 = time.perf_counter()
+    model, _ = cd.run(args.steps, model)
+    if torch.cuda.is_available():
+        torch.cuda.synchronize()
+    barrier()
+    elapsed = all_reduce_scalar(time.perf_counter() - t1, "max")
+    loss = cd.history[-1].get("training_loss")
+    re_stats = coords["per-entity"].last_stats
+    total_rows = int(all_reduce_scalar(float(data.n_rows)))
+    if rank == 0:
+        log(f"final training loss {loss:.6e}; RE stats {re_stats}")
+        print(json.dumps({
+            "metric": "GAME coord-descent iters/sec (fixed + per-entity random effect)",
+            "value": args.steps / elapsed,
+            "unit": "CD iterations/sec",
+            "n_gpus": world,
+            "steps": args.steps,
+            "warmup": args.warmup,
+            "ms_per_step": 1000.0 * elapsed / args.steps,
+            "higher_is_better": True,
+            "scaling": "weak",
+            "vs_baseline": None,
+            "dtype": args.precision,
+            "data": "synthetic (Zipf fixed-effect features, per-entity private random-effect features)",
+            "config": {"model": "game_logistic_fe_lbfgs_re_tron", "global_batch": total_rows, "seq_len": None,
+                       "entities": args.entities_per_gpu * world, "rows_per_entity": args.rows_per_entity,
+                       "re_dim": args.re_dim, "fe_dim": args.fe_dim, "fe_iters": args.fe_iters,
+                       "re_iters": args.re_iters, "parallelism": f"dp{world}+ep{world}"},
+            "examples_per_sec": total_rows * args.steps / elapsed,
+        }), flush=True)
+
+
+if __name__ == "__main__":
+    main()

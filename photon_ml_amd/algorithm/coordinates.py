@@ -122,14 +122,15 @@ class RandomEffectCoordinate(Coordinate):
 
     def __init__(self, coordinate_id: str, data: GameData, data_config: RandomEffectDataConfiguration,
                  opt_config: GLMOptimizationConfiguration, task, compute_variance: bool = False, device=None,
-                 dtype=torch.float64, entity_subset=None):
+                 dtype=torch.float64, entity_subset=None, layout: str = "auto"):
         self.coordinate_id = coordinate_id
         self.data = data
         self.data_config = data_config
         self.task = TaskType.parse(task)
         self.loss = loss_for_task(self.task)
         self.device = torch.device(device) if device is not None else default_device()
-        self.dataset = RandomEffectDataset(data, data_config, self.device, dtype, entity_subset=entity_subset)
+        self.dataset = RandomEffectDataset(data, data_config, self.device, dtype, entity_subset=entity_subset,
+                                           layout=layout)
         self.compute_variance = compute_variance
         self.base_offsets = torch.from_numpy(data.offsets).to(self.device)
         self.set_config(opt_config)
@@ -180,6 +181,8 @@ class RandomEffectCoordinate(Coordinate):
         reg, lam = cfg.regularization_context, cfg.regularization_weight
         l1, l2 = reg.l1_weight(lam), reg.l2_weight(lam)
         offs = self.base_offsets if partial_score is None else self.base_offsets + partial_score.to(self.device)
+        if ds.layout == "segmented":
+            return self._update_segmented(model, offs, l1, l2)
         keys, vals, vars_ = [], [], []
         iters, n_conv = [], 0
         for b, bucket in enumerate(ds.buckets):
@@ -210,6 +213,48 @@ class RandomEffectCoordinate(Coordinate):
         variances = np.concatenate(vars_) if vars_ else None
         return RandomEffectModel(self.data_config.random_effect_type, self.data_config.feature_shard_id, self.task,
                                  ds.entity_ids, ds.dim, keys, vals, variances)
+
+    def _update_segmented(self, model, offs, l1: float, l2: float):
+        """All entities as one block-diagonal problem (``SegmentedGLMData``): one TRON / L-BFGS over the
+        concatenated per-entity coefficient vector, per-entity convergence via segment reductions."""
+        ds, cfg = self.dataset, self.opt_config
+        seg = ds.seg
+        seg.o = offs.to(seg.y.device, torch.float64)[ds.seg_rows]
+        seg._dzz_key = None
+        W0 = self._warm_start_segmented(model)
+        oc = cfg.optimizer_config
+        if oc.optimizer_type == OptimizerType.TRON:
+            res = batched_tron(seg, self.loss, l2, W0, oc.tolerance, oc.maximum_iterations)
+        else:
+            res = batched_lbfgs(seg, self.loss, l2, W0, oc.tolerance, oc.maximum_iterations, l1=l1)
+        self._W["seg"] = res.W
+        it = res.iters[torch.from_numpy(ds.n_active > 0).to(res.iters.device)]
+        self.last_stats = {"entities": int(it.numel()), "mean_iterations": float(it.double().mean()) if it.numel()
+                           else 0.0, "max_iterations": int(it.max()) if it.numel() else 0}
+        W = res.W.detach().cpu().numpy()
+        var = None
+        if self.compute_variance and self.loss.twice_differentiable:
+            var = (1.0 / (seg.hdiag(self.loss, res.W, l2) + EPSILON)).detach().cpu().numpy()
+        keys = ds.projection.keys  # entity * dim + feature, sorted, aligned with W
+        nz = W != 0
+        return RandomEffectModel(self.data_config.random_effect_type, self.data_config.feature_shard_id, self.task,
+                                 ds.entity_ids, ds.dim, keys[nz], W[nz], None if var is None else var[nz])
+
+    def _warm_start_segmented(self, model):
+        ds = self.dataset
+        dev = ds.seg.y.device
+        prev = self._W.get("seg")
+        if prev is not None and prev.numel() == ds.d_total:
+            return prev
+        if model is None or not len(model.keys):
+            return torch.zeros(ds.d_total, dtype=torch.float64, device=dev)
+        ent = np.repeat(np.arange(ds.n_entities), np.diff(ds.projection.ptr))
+        mi = model.entity_index(ds.entity_ids)[ent]
+        k = mi.astype(np.int64) * model.dim + ds.projection.feat
+        pos = np.searchsorted(model.keys, k)
+        pos_c = np.minimum(pos, len(model.keys) - 1)
+        hit = (pos < len(model.keys)) & (model.keys[pos_c] == k) & (mi >= 0)
+        return torch.from_numpy(np.where(hit, model.values[pos_c], 0.0)).to(dev)
 
     def _to_original(self, bucket, W: torch.Tensor, var: Optional[torch.Tensor]):
         ds = self.dataset

@@ -25,6 +25,7 @@ import torch
 from ..constants import EPSILON
 from ..projector.projectors import (IndexMapProjection, ProjectorKind, ProjectorType, gaussian_projection_matrix)
 from .game_data import GameData
+from .matrix import LabeledData
 
 
 @dataclass
@@ -111,7 +112,11 @@ class RandomEffectDataset:
     """Active/passive data of one random-effect coordinate, projected and bucketed."""
 
     def __init__(self, data: GameData, config: RandomEffectDataConfiguration, device="cpu",
-                 dtype=torch.float64, bucket_elems: int = 1 << 24, entity_subset: Optional[np.ndarray] = None):
+                 dtype=torch.float64, bucket_elems: int = 1 << 24, entity_subset: Optional[np.ndarray] = None,
+                 layout: str = "auto"):
+        """``layout``: ``dense`` = size buckets of padded ``[B, n, d]`` problems (batched GEMMs); ``segmented`` =
+        one block-diagonal sparse GLM over all entities (INDEX_MAP projection only; the GLM kernels do the
+        products, no padding). ``auto`` = segmented for INDEX_MAP on a GPU, dense otherwise."""
         self.config = config
         self.device = torch.device(device)
         self.dtype = dtype
@@ -188,11 +193,21 @@ class RandomEffectDataset:
         else:
             d_local = np.full(n_ent, self.dim, dtype=np.int64)
         self.d_local = d_local
-        # ---- buckets
+        # ---- buckets (dense) or one block-diagonal problem (segmented)
         n_act = np.bincount(ea, minlength=n_ent)
         self.n_active = n_act
-        self.buckets = self._make_buckets(xa, ea, active_rows, data.response, weight_mult * data.weights,
-                                          n_act, d_local, bucket_elems)
+        if layout == "auto":
+            layout = "segmented" if (pt.kind == ProjectorKind.INDEX_MAP and self.device.type == "cuda") else "dense"
+        if layout == "segmented" and pt.kind != ProjectorKind.INDEX_MAP:
+            raise ValueError("the segmented random-effect layout needs the INDEX_MAP projector")
+        self.layout = layout
+        self.buckets = []
+        self.seg = None
+        if layout == "segmented":
+            self._make_segmented(xa, ea, active_rows, data.response, weight_mult * data.weights, n_ent)
+        else:
+            self.buckets = self._make_buckets(xa, ea, active_rows, data.response, weight_mult * data.weights,
+                                              n_act, d_local, bucket_elems)
 
     # ------------------------------------------------------------------
     def _pearson_filter(self, xa: sp.csr_matrix, ea: np.ndarray, y: np.ndarray, ratio: float) -> sp.csr_matrix:
@@ -288,6 +303,28 @@ class RandomEffectDataset:
             out.append(Bucket(be, torch.from_numpy(rows).to(dev), torch.from_numpy(X).to(dev, dt),
                               torch.from_numpy(Y).to(dev, dt), torch.from_numpy(W).to(dev, dt), d_local[be]))
         return out
+
+    def _make_segmented(self, xa, ea, active_rows, y, wts, n_ent):
+        from ..ops.backend import make_glm_data
+        from ..optimization.batched import SegmentedGLMData
+        order = np.argsort(ea, kind="stable")        # active rows grouped by entity (sample order inside)
+        xs = xa[order].tocoo()
+        e_row = ea[order]
+        pos = self.projection.local_index(e_row[xs.row], xs.col) + self.projection.ptr[e_row[xs.row]]
+        d_total = int(self.projection.ptr[-1])
+        x_seg = sp.csr_matrix((xs.data, (xs.row, pos)), shape=(len(order), max(d_total, 1)))
+        rows = active_rows[order]
+        yy = np.asarray(y, dtype=np.float64)[rows]
+        ww = np.asarray(wts, dtype=np.float64)[rows]
+        glm = make_glm_data(LabeledData(x_seg, yy, np.zeros(len(rows)), ww), self.device, "f64", col_windows=True)
+        dev = glm.device
+        col_entity = np.repeat(np.arange(n_ent, dtype=np.int64), np.diff(self.projection.ptr))
+        self.seg_rows = torch.from_numpy(rows).to(dev)
+        self.seg = SegmentedGLMData(glm, torch.from_numpy(e_row.astype(np.int64)).to(dev),
+                                    torch.from_numpy(col_entity).to(dev), n_ent,
+                                    torch.from_numpy(yy).to(dev), torch.from_numpy(ww).to(dev),
+                                    torch.zeros(len(rows), dtype=torch.float64, device=dev))
+        self.d_total = d_total
 
     @property
     def n_entities(self) -> int:

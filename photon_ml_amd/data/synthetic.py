@@ -155,3 +155,64 @@ def generate_device_shard(n_rows: int, n_features: int, nnz_per_row: int, device
         yy = (z + 0.1 * torch.randn(n_rows, generator=gen, device=dev, dtype=torch.float64)).to(torch.float32)
     data.y.copy_(yy.to(data.vdt))
     return data, w_true
+
+
+def generate_game_bench_data(n_entities: int, rows_per_entity: int, re_dim: int = 100, re_nnz: int = 10,
+                             fe_dim: int = 100_000, fe_nnz: int = 30, re_vocab: int = 1 << 20, seed: int = 7,
+                             entity_offset: int = 0, task: str = "LOGISTIC_REGRESSION"):
+    """Synthetic GAME data at benchmark scale (vectorised, no per-row Python):
+
+    * ``global`` shard: ``fe_nnz`` Zipf(1.1) features out of ``fe_dim`` + intercept (last column);
+    * ``entity`` shard: each entity draws its ``re_nnz`` features per row from a private pool of ``re_dim``
+      features of a ``re_vocab`` hashed vocabulary (+ intercept) -> after INDEX_MAP projection every entity has
+      ~``re_dim`` coefficients;
+    * id tag ``entityId`` = ``e<global entity index>`` (``entity_offset`` shifts the range, e.g. per rank);
+    * labels from a random ground truth (logistic / linear / Poisson).
+    """
+    from ..data.game_data import GameData
+    rng = np.random.default_rng(seed)
+    n = n_entities * rows_per_entity
+    ent = rng.permutation(np.repeat(np.arange(n_entities, dtype=np.int64), rows_per_entity))
+    # fixed effect shard
+    ranks = np.arange(1, fe_dim)
+    p = ranks ** -1.1
+    cdf = np.cumsum(p) / p.sum()
+    fcol = np.minimum(np.searchsorted(cdf, rng.random((n, fe_nnz))), fe_dim - 2)
+    fcol = np.sort(fcol, axis=1)
+    dup = np.zeros_like(fcol, dtype=bool)
+    dup[:, 1:] = fcol[:, 1:] == fcol[:, :-1]
+    fval = np.where(dup, 0.0, rng.random((n, fe_nnz)) + 0.5)
+    fcols = np.concatenate([fcol, np.full((n, 1), fe_dim - 1)], 1)
+    fvals = np.concatenate([fval, np.ones((n, 1))], 1)
+    xg = sp.csr_matrix((fvals.ravel(), fcols.ravel(), np.arange(0, n * (fe_nnz + 1) + 1, fe_nnz + 1)),
+                       shape=(n, fe_dim))
+    xg.eliminate_zeros()
+    # random effect shard: pool slot k of entity e -> feature (hash(e) + k * stride) % re_vocab
+    slot = rng.integers(0, re_dim, size=(n, re_nnz))
+    slot = np.sort(slot, axis=1)
+    rdup = np.zeros_like(slot, dtype=bool)
+    rdup[:, 1:] = slot[:, 1:] == slot[:, :-1]
+    gid = ent + entity_offset
+    base = (gid * 2654435761) % (re_vocab - 1)
+    rcol = (base[:, None] + slot * 40503) % (re_vocab - 1)
+    rval = np.where(rdup, 0.0, rng.normal(size=(n, re_nnz)))
+    xr = sp.csr_matrix((np.concatenate([rval, np.ones((n, 1))], 1).ravel(),
+                        np.concatenate([rcol, np.full((n, 1), re_vocab - 1)], 1).ravel(),
+                        np.arange(0, n * (re_nnz + 1) + 1, re_nnz + 1)), shape=(n, re_vocab))
+    xr.sum_duplicates()
+    xr.eliminate_zeros()
+    # ground truth
+    wg = rng.normal(size=fe_dim) * 0.2
+    wg[-1] = -0.5
+    w_slot = np.random.default_rng(seed + 1).normal(size=re_dim) * 0.5
+    zr = np.where(rdup, 0.0, rval * w_slot[slot]).sum(1) + 0.3 * np.sin(gid)
+    z = np.asarray(xg @ wg).ravel() + zr
+    task = TaskType.parse(task)
+    if task == TaskType.LOGISTIC_REGRESSION:
+        y = (rng.random(n) < 1.0 / (1.0 + np.exp(-z))).astype(np.float64)
+    elif task == TaskType.POISSON_REGRESSION:
+        y = rng.poisson(np.exp(np.clip(z * 0.3, -10, 3))).astype(np.float64)
+    else:
+        y = z + 0.1 * rng.normal(size=n)
+    ids = np.char.add("e", gid.astype(str)).astype(object)
+    return GameData(y, {"global": xg, "entity": xr}, {"entityId": ids})

@@ -21,9 +21,10 @@ def default_device() -> torch.device:
     return torch.device("cpu")
 
 
-def make_glm_data(data: LabeledData, device=None, precision: str = "f64", chunk_rows: int = 1 << 20):
+def make_glm_data(data: LabeledData, device=None, precision: str = "f64", chunk_rows: int = 1 << 20, **kw):
+    """``kw`` goes to :meth:`DeviceGLMData.from_labeled` (e.g. ``col_windows=True`` for block-diagonal data)."""
     device = torch.device(device) if device is not None else default_device()
     if device.type == "cuda" and os.environ.get("PML_BACKEND") != "torch":
         from .device import DeviceGLMData
-        return DeviceGLMData.from_labeled(data, device, precision, chunk_rows)
+        return DeviceGLMData.from_labeled(data, device, precision, chunk_rows, **kw)
     return TorchGLMData(data, device)

@@ -139,6 +139,7 @@ class DeviceGLMData(GLMComputable):
         self._dzz_shift = None
         # scratch
         self.layout = "tiled" if csr and csr[0].kind == "tl" else "segmented"
+        self.col_lo = [0] * len(csr)  # per-chunk column window base (see from_labeled(col_windows=True))
         self.blk_off = np.cumsum([0] + [c.nstats for c in csr]).tolist()
         self.long_off = np.cumsum([0] + [getattr(c, "nlong", 0) for c in csr]).tolist()
         self.stats = torch.zeros(2 * max(self.blk_off[-1], 1), dtype=torch.float64, device=self.device)
@@ -158,7 +159,13 @@ class DeviceGLMData(GLMComputable):
     # ------------------------------------------------------------------
     @staticmethod
     def from_labeled(data: LabeledData, device="cuda", precision: str = "f64", chunk_rows: int = 1 << 20,
-                     relabel: bool = True, layout: str = "auto", item_entries: Optional[int] = None):
+                     relabel: bool = True, layout: str = "auto", item_entries: Optional[int] = None,
+                     col_windows: bool = False):
+        """``col_windows``: store each chunk in its own column window ``[min col, max col]`` (local column ids,
+        pointer-offset vectors). Used by the block-diagonal random-effect problems, where a chunk of
+        entity-sorted rows touches a narrow contiguous column range of a huge ``dim`` (implies no relabel)."""
+        if col_windows:
+            relabel = False
         prec = PRECISIONS[precision]
         vdt = VAL_DTYPE[prec]
         dev = torch.device(device)
@@ -176,15 +183,29 @@ class DeviceGLMData(GLMComputable):
         if n == 0:
             starts = [0, 0]
         csr, csc = [], []
-        layout = resolve_layout(layout, d, chunk_rows)
+        col_lo = []
+        wins = []
         for a, b in zip(starts[:-1], starts[1:]):
             xc = x[a:b]
+            if col_windows and xc.nnz:
+                lo, hi = int(xc.indices.min()), int(xc.indices.max()) + 1
+            else:
+                lo, hi = 0, d
+            wins.append((lo, hi))
+        dmax = max([hi - lo for lo, hi in wins] + [1])
+        layout = resolve_layout(layout, dmax, chunk_rows)
+        for (a, b), (lo, hi) in zip(zip(starts[:-1], starts[1:]), wins):
+            xc = x[a:b]
+            col_lo.append(lo)
+            if lo != 0 or hi != d:
+                xc = sp.csr_matrix((xc.data, xc.indices - lo, xc.indptr), shape=(b - a, hi - lo))
+            dc = hi - lo
             if layout == "tiled":
                 rp = torch.from_numpy((xc.indptr - xc.indptr[0]).astype(np.int64)).to(dev)
                 col = torch.from_numpy(xc.indices.astype(np.int64)).to(dev)
                 val = torch.from_numpy(xc.data.astype(np.float64)).to(dev).to(vdt)
-                csr.append(TLFwdChunk(rp, col, val, d))
-                csc.append(TLTChunk(rp, col, val, d, chunk_rows, item_entries=item_entries))
+                csr.append(TLFwdChunk(rp, col, val, dc))
+                csc.append(TLTChunk(rp, col, val, dc, chunk_rows, item_entries=item_entries))
                 continue
             sp_ = (xc.indptr - xc.indptr[0]).astype(np.int32)
             csr.append(SegChunk(sp_, torch.from_numpy(xc.indices.astype(np.int32)),
@@ -194,8 +215,10 @@ class DeviceGLMData(GLMComputable):
             xc = xc.copy()
             csc.append(SegChunk(xt.indptr.astype(np.int32), torch.from_numpy(xt.indices.astype(np.int32)),
                                 torch.from_numpy(xt.data.astype(np.float64)).to(vdt), dev))
-        return DeviceGLMData(csr, csc, starts, torch.from_numpy(data.y), torch.from_numpy(data.offsets),
-                             torch.from_numpy(data.weights), d, precision, dev, old_of_new)
+        out = DeviceGLMData(csr, csc, starts, torch.from_numpy(data.y), torch.from_numpy(data.offsets),
+                            torch.from_numpy(data.weights), d, precision, dev, old_of_new)
+        out.col_lo = col_lo
+        return out
 
     def nbytes(self) -> int:
         return sum(c.nbytes() for c in self.csr + self.csc)
@@ -215,9 +238,10 @@ class DeviceGLMData(GLMComputable):
              stats: bool = True):
         ch = self.csr[c]
         st = self.stats.data_ptr() + 2 * 8 * self.blk_off[c] if stats else None
+        xp = x.data_ptr() + self.col_lo[c] * x.element_size()
         if ch.kind == "tl":
             check(self.lib.pml_tl_fwd(
-                self.prec, ctypes.byref(ch.desc), x.data_ptr(), mode, loss_id, float(shift),
+                self.prec, ctypes.byref(ch.desc), xp, mode, loss_id, float(shift),
                 self._rows(self.y, c), self._rows(self.o, c), self._rows(self.wt, c),
                 None if coef is None else self._rows(coef, c), None if dzz is None else self._rows(dzz, c),
                 None if z_out is None else self._rows(z_out, c), with_offset, st, stream_handle(self.device)),
@@ -225,7 +249,7 @@ class DeviceGLMData(GLMComputable):
             return
         lst = self.long_stats.data_ptr() + 2 * 8 * self.long_off[c] if stats else None
         check(self.lib.pml_seg_fwd(
-            self.prec, ctypes.byref(ch.desc), x.data_ptr(), mode, loss_id, float(shift),
+            self.prec, ctypes.byref(ch.desc), xp, mode, loss_id, float(shift),
             self._rows(self.y, c), self._rows(self.o, c), self._rows(self.wt, c),
             None if coef is None else self._rows(coef, c), None if dzz is None else self._rows(dzz, c),
             None if z_out is None else self._rows(z_out, c), with_offset, st, lst, self.parts.data_ptr(),
@@ -233,11 +257,12 @@ class DeviceGLMData(GLMComputable):
 
     def _t(self, c: int, x: torch.Tensor, G: torch.Tensor, square: int = 0):
         ch = self.csc[c]
+        gp = G.data_ptr() + self.col_lo[c] * G.element_size()
         if ch.kind == "tl":
-            check(self.lib.pml_tl_t(self.prec, ctypes.byref(ch.desc), self._rows(x, c), square, G.data_ptr(),
+            check(self.lib.pml_tl_t(self.prec, ctypes.byref(ch.desc), self._rows(x, c), square, gp,
                                     self.parts.data_ptr(), stream_handle(self.device)), "tl_t")
             return
-        check(self.lib.pml_seg_t(self.prec, ctypes.byref(ch.desc), self._rows(x, c), square, G.data_ptr(),
+        check(self.lib.pml_seg_t(self.prec, ctypes.byref(ch.desc), self._rows(x, c), square, gp,
                                  self.parts.data_ptr(), stream_handle(self.device)), "seg_t")
 
     def _reduce_stats(self) -> torch.Tensor:
@@ -321,6 +346,20 @@ class DeviceGLMData(GLMComputable):
             self._fwd(c, x, FWD_DZZ, loss.loss_id, 0.0, self.coef, None, stats=False)
             self._t(c, self.coef, out, square=1)
         self._dzz_key = None
+        return self._unperm(out)
+
+    def matvec(self, w) -> torch.Tensor:
+        """z = X w (fp64, no offsets)."""
+        return self.margins(w, 0.0, False)
+
+    def rmatvec(self, r, square: bool = False) -> torch.Tensor:
+        """g = X^T r (``square``: (X.X)^T r) for a per-row vector r (fp64 result, original column order)."""
+        rr = torch.as_tensor(r, device=self.device).to(self.vdt).contiguous()
+        if rr.numel() < max(self.n_rows, 1):
+            rr = torch.cat([rr, torch.zeros(max(self.n_rows, 1) - rr.numel(), dtype=self.vdt, device=self.device)])
+        out = torch.zeros(self.dim, dtype=torch.float64, device=self.device)
+        for c in range(len(self.csc)):
+            self._t(c, rr, out, square=int(square))
         return self._unperm(out)
 
     def margins(self, w, margin_shift: float = 0.0, with_offsets: bool = False):

@@ -58,6 +58,14 @@ class GLMComputable:
         """x_i . w (+ shift) (+ o_i)."""
         raise NotImplementedError
 
+    def matvec(self, w):
+        """X w."""
+        raise NotImplementedError
+
+    def rmatvec(self, r, square: bool = False):
+        """X^T r (``square``: (X.X)^T r)."""
+        raise NotImplementedError
+
     def count(self) -> int:
         return self.n_rows
 
@@ -88,6 +96,16 @@ class TorchGLMData(GLMComputable):
     def margins(self, w, margin_shift: float = 0.0, with_offsets: bool = False):
         z = self._xv(w) + margin_shift
         return z + self.o if with_offsets else z
+
+    def matvec(self, w):
+        return self._xv(w)
+
+    def rmatvec(self, r, square: bool = False):
+        r = torch.as_tensor(r, dtype=torch.float64, device=self.device)
+        if self.n_rows == 0:
+            return torch.zeros(self.dim, dtype=torch.float64, device=self.device)
+        m = self.x2t if square else self.xt
+        return (m @ r.unsqueeze(1)).squeeze(1)
 
     def value_grad_sums(self, loss, w_eff, margin_shift):
         z = self._xv(w_eff) + margin_shift + self.o

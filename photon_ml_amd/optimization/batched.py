@@ -28,7 +28,7 @@ REASON_CODES = {0: None, 1: ConvergenceReason.MAX_ITERATIONS, 2: ConvergenceReas
 
 
 class BatchedGLMData:
-    """Dense padded batch of per-entity GLM problems."""
+    """Dense padded batch of per-entity GLM problems. Vectors are ``[B, d]``."""
 
     def __init__(self, X: torch.Tensor, y: torch.Tensor, offsets: torch.Tensor, weights: torch.Tensor):
         self.X = X  # [B, n, d]
@@ -37,6 +37,20 @@ class BatchedGLMData:
         self.w = weights  # 0 on padding rows
         self._dzz_key = None
         self._dzz = None
+
+    # ---- batch vector space: per-entity dot products / broadcasting of per-entity scalars
+    @property
+    def n_batch(self) -> int:
+        return self.X.shape[0]
+
+    def bdot(self, a, b):
+        return (a * b).sum(-1)
+
+    def bexp(self, s):
+        return s.unsqueeze(-1)
+
+    def babs_sum(self, a):
+        return a.abs().sum(-1)
 
     @property
     def shape(self):
@@ -74,17 +88,81 @@ class BatchedGLMData:
         return h + l2 if l2 > 0 else h
 
 
-def _bdot(a, b):
-    return (a * b).sum(-1)
+class SegmentedGLMData:
+    """All entities of a random-effect coordinate as ONE block-diagonal sparse GLM.
+
+    Rows are the active rows sorted by entity; entity ``e`` owns the contiguous coefficient range
+    ``[col_ptr[e], col_ptr[e+1])`` (its INDEX_MAP-projected features), so the design matrix is block diagonal and
+    a "batched" solve is a single vector of length ``D_total = sum d_e`` with per-entity scalars obtained by
+    segment sums. The matrix products run on the GLM HIP kernels (``matvec`` = forward pass, ``rmatvec`` =
+    transpose pass over column tiles / windows) — no padding, any mix of entity sizes, one launch sequence for all
+    entities (reference ``SingleNodeOptimizationProblem`` per entity).
+    """
+
+    def __init__(self, glm, row_entity: torch.Tensor, col_entity: torch.Tensor, n_entities: int, y: torch.Tensor,
+                 weights: torch.Tensor, offsets: torch.Tensor):
+        self.glm = glm
+        self.row_entity = row_entity
+        self.col_entity = col_entity
+        self.B = int(n_entities)
+        self.y, self.w, self.o = y, weights, offsets
+        self._dzz_key = None
+        self._dzz = None
+
+    @property
+    def n_batch(self) -> int:
+        return self.B
+
+    def _seg(self, v, idx):
+        return torch.zeros(self.B, dtype=v.dtype, device=v.device).index_add_(0, idx, v)
+
+    def bdot(self, a, b):
+        return self._seg(a * b, self.col_entity)
+
+    def bexp(self, s):
+        return s[self.col_entity]
+
+    def babs_sum(self, a):
+        return self._seg(a.abs(), self.col_entity)
+
+    def margins(self, W):
+        return self.glm.matvec(W) + self.o
+
+    def value_grad(self, loss, W, l2: float):
+        z = self.margins(W)
+        l, dl = loss.loss_and_dz(z, self.y)
+        f = self._seg(self.w * l, self.row_entity)
+        g = self.glm.rmatvec(self.w * dl)
+        if l2 > 0:
+            f = f + 0.5 * l2 * self.bdot(W, W)
+            g = g + l2 * W
+        return f, g
+
+    def _dzz_at(self, loss, W):
+        if self._dzz_key is not None and self._dzz_key.shape == W.shape and torch.equal(self._dzz_key, W):
+            return self._dzz
+        self._dzz = self.w * loss.dzz(self.margins(W), self.y)
+        self._dzz_key = W.clone()
+        return self._dzz
+
+    def hv(self, loss, W, V, l2: float):
+        D = self._dzz_at(loss, W)
+        h = self.glm.rmatvec(D * self.glm.matvec(V))
+        return h + l2 * V if l2 > 0 else h
+
+    def hdiag(self, loss, W, l2: float):
+        D = self.w * loss.dzz(self.margins(W), self.y)
+        h = self.glm.rmatvec(D, square=True)
+        return h + l2 if l2 > 0 else h
 
 
-def _bnorm(a):
-    return torch.linalg.vector_norm(a, dim=-1)
+def _bn(data, a):
+    return torch.sqrt(data.bdot(a, a).clamp(min=0))
 
 
 @dataclass
 class BatchedResult:
-    W: torch.Tensor          # [B, d] coefficients
+    W: torch.Tensor          # [B, d] (dense batch) or [D_total] (segmented) coefficients
     f: torch.Tensor          # [B] final objective (incl. regularisation)
     iters: torch.Tensor      # [B] iterations
     reason: torch.Tensor     # [B] int convergence codes (see REASON_CODES)
@@ -93,9 +171,10 @@ class BatchedResult:
 class _Convergence:
     """Vectorised Photon convergence bookkeeping."""
 
-    def __init__(self, f0z, g0z, tol, max_iter, device):
+    def __init__(self, data, f0z, g0z, tol, max_iter, device):
+        self.data = data
         self.loss_tol = f0z * tol
-        self.grad_tol = _bnorm(g0z) * tol
+        self.grad_tol = _bn(data, g0z) * tol
         self.max_iter = max_iter
 
     def check(self, it, f_new, f_prev, g_new, completed, not_improving):
@@ -103,7 +182,7 @@ class _Convergence:
         reason = torch.zeros_like(it)
         r_max = it >= self.max_iter
         r_fv = (f_new - f_prev).abs() <= self.loss_tol
-        r_gc = _bnorm(g_new) <= self.grad_tol
+        r_gc = _bn(self.data, g_new) <= self.grad_tol
         reason = torch.where(completed & r_gc, torch.full_like(reason, 4), reason)
         reason = torch.where(completed & r_fv, torch.full_like(reason, 3), reason)
         reason = torch.where(not_improving, torch.full_like(reason, 2), reason)
@@ -111,27 +190,28 @@ class _Convergence:
         return reason
 
 
-def batched_tron(data: BatchedGLMData, loss, l2: float, W0: torch.Tensor, tol: float = 1e-5, max_iter: int = 15,
+def batched_tron(data, loss, l2: float, W0: torch.Tensor, tol: float = 1e-5, max_iter: int = 15,
                  max_fail: int = 5, max_cg: int = 20) -> BatchedResult:
     """Vectorised TRON (``photon-lib/.../optimization/TRON.scala:80-340``) over a batch of entities."""
     eta0, eta1, eta2 = 1e-4, 0.25, 0.75
     s1, s2, s3 = 0.25, 0.5, 4.0
     W = W0.clone()
-    B = W.shape[0]
+    B = data.n_batch
+    E = data.bexp
     dev = W.device
     f, g = data.value_grad(loss, W, l2)
     if bool((W0 == 0).all()):
         f0z, g0z = f, g
     else:
         f0z, g0z = data.value_grad(loss, torch.zeros_like(W), l2)
-    conv = _Convergence(f0z, g0z, tol, max_iter, dev)
-    delta = _bnorm(g)
+    conv = _Convergence(data, f0z, g0z, tol, max_iter, dev)
+    delta = _bn(data, g)
     it = torch.zeros(B, dtype=torch.long, device=dev)
     fails = torch.zeros(B, dtype=torch.long, device=dev)
     reason = torch.zeros(B, dtype=torch.long, device=dev)
     # entities with an all-zero problem (no data) converge immediately
     active = torch.ones(B, dtype=torch.bool, device=dev)
-    zero_g = _bnorm(g) == 0
+    zero_g = _bn(data, g) == 0
     reason = torch.where(zero_g, torch.full_like(reason, 4), reason)
     active &= ~zero_g
     guard = 0
@@ -143,46 +223,46 @@ def batched_tron(data: BatchedGLMData, loss, l2: float, W0: torch.Tensor, tol: f
         step = torch.zeros_like(W)
         r = -g.clone()
         d = r.clone()
-        rtr = _bdot(r, r)
-        cg_tol = 0.1 * _bnorm(g)
+        rtr = data.bdot(r, r)
+        cg_tol = 0.1 * _bn(data, g)
         cg_on = active.clone()
         for _ in range(max_cg):
             cg_on &= torch.sqrt(rtr.clamp(min=0)) > cg_tol
             if not bool(cg_on.any()):
                 break
             Hd = data.hv(loss, W, d, l2)
-            dHd = _bdot(d, Hd)
+            dHd = data.bdot(d, Hd)
             alpha = torch.where(cg_on, rtr / torch.where(dHd == 0, torch.ones_like(dHd), dHd),
                                 torch.zeros_like(rtr))
-            trial = step + alpha.unsqueeze(1) * d
-            hit = cg_on & (_bnorm(trial) > delta)
+            trial = step + E(alpha) * d
+            hit = cg_on & (_bn(data, trial) > delta)
             # boundary solution for entities that leave the trust region
-            std = _bdot(step, d)
-            sts = _bdot(step, step)
-            dtd = _bdot(d, d)
+            std = data.bdot(step, d)
+            sts = data.bdot(step, step)
+            dtd = data.bdot(d, d)
             dsq = delta * delta
             rad = torch.sqrt((std * std + dtd * (dsq - sts)).clamp(min=0))
             tau = torch.where(std >= 0, (dsq - sts) / (std + rad).clamp(min=1e-300),
                               (rad - std) / dtd.clamp(min=1e-300))
             move = cg_on & ~hit
-            step = torch.where(move.unsqueeze(1), trial, step)
-            step = torch.where(hit.unsqueeze(1), step + tau.unsqueeze(1) * d, step)
-            r_new = torch.where(move.unsqueeze(1), r - alpha.unsqueeze(1) * Hd, r)
-            r_new = torch.where(hit.unsqueeze(1), r - tau.unsqueeze(1) * Hd, r_new)
-            rnew_tr = _bdot(r_new, r_new)
+            step = torch.where(E(move), trial, step)
+            step = torch.where(E(hit), step + E(tau) * d, step)
+            r_new = torch.where(E(move), r - E(alpha) * Hd, r)
+            r_new = torch.where(E(hit), r - E(tau) * Hd, r_new)
+            rnew_tr = data.bdot(r_new, r_new)
             beta = torch.where(move, rnew_tr / torch.where(rtr == 0, torch.ones_like(rtr), rtr),
                                torch.zeros_like(rtr))
-            d = torch.where(move.unsqueeze(1), r_new + beta.unsqueeze(1) * d, d)
+            d = torch.where(E(move), r_new + E(beta) * d, d)
             r = r_new
             rtr = torch.where(move, rnew_tr, rtr)
             cg_on &= ~hit
         # ---- trial step
         W_new = W + step
-        gs = _bdot(g, step)
-        pred = -0.5 * (gs - _bdot(step, r))
+        gs = data.bdot(g, step)
+        pred = -0.5 * (gs - data.bdot(step, r))
         f_new, g_new = data.value_grad(loss, W_new, l2)
         actual = f - f_new
-        snorm = _bnorm(step)
+        snorm = _bn(data, step)
         first = active & (it == 0)
         delta = torch.where(first, torch.minimum(delta, snorm), delta)
         den = f_new - f - gs
@@ -199,9 +279,9 @@ def batched_tron(data: BatchedGLMData, loss, l2: float, W0: torch.Tensor, tol: f
         delta = torch.where(active, nd, delta)
         accept = active & (actual > eta0 * pred)
         f_prev = f
-        W = torch.where(accept.unsqueeze(1), W_new, W)
+        W = torch.where(E(accept), W_new, W)
         f = torch.where(accept, f_new, f)
-        g = torch.where(accept.unsqueeze(1), g_new, g)
+        g = torch.where(E(accept), g_new, g)
         it = it + accept.long()
         fails = torch.where(accept, torch.zeros_like(fails), fails + active.long())
         not_improving = active & ~accept & (fails >= max_fail)
@@ -213,18 +293,19 @@ def batched_tron(data: BatchedGLMData, loss, l2: float, W0: torch.Tensor, tol: f
     return BatchedResult(W, f, it, reason)
 
 
-def batched_lbfgs(data: BatchedGLMData, loss, l2: float, W0: torch.Tensor, tol: float = 1e-7,
+def batched_lbfgs(data, loss, l2: float, W0: torch.Tensor, tol: float = 1e-7,
                   max_iter: int = 100, m: int = 10, l1: float = 0.0, max_ls: int = 30) -> BatchedResult:
     """Vectorised L-BFGS (OWL-QN when ``l1 > 0``) with backtracking Armijo line search per entity."""
     W = W0.clone()
-    B, dim = W.shape
+    B = data.n_batch
+    E = data.bexp
     dev, dt = W.device, W.dtype
     owl = l1 > 0
 
     def adjust(Wc, fc, gc):
         if not owl:
             return fc, gc
-        f_adj = fc + l1 * Wc.abs().sum(1)
+        f_adj = fc + l1 * data.babs_sum(Wc)
         dplus, dminus = gc + l1, gc - l1
         pg0 = torch.where(dminus > 0, dminus, torch.where(dplus < 0, dplus, torch.zeros_like(gc)))
         pg = torch.where(Wc == 0, pg0, gc + l1 * torch.sign(Wc))
@@ -235,15 +316,15 @@ def batched_lbfgs(data: BatchedGLMData, loss, l2: float, W0: torch.Tensor, tol: 
         f0z, g0z = f_s, g_s
     else:
         f0z, g0z = data.value_grad(loss, torch.zeros_like(W), l2)
-    conv = _Convergence(f0z, g0z, tol, max_iter, dev)
+    conv = _Convergence(data, f0z, g0z, tol, max_iter, dev)
     f, g = adjust(W, f_s, g_s)
-    S = torch.zeros(B, m, dim, dtype=dt, device=dev)
-    Y = torch.zeros_like(S)
+    S = [torch.zeros_like(W) for _ in range(m)]  # history slot k: k-th most recent pair (slot 0 newest)
+    Y = [torch.zeros_like(W) for _ in range(m)]
     rho = torch.zeros(B, m, dtype=dt, device=dev)
     hist = torch.zeros(B, dtype=torch.long, device=dev)  # number of valid pairs
     it = torch.zeros(B, dtype=torch.long, device=dev)
     reason = torch.zeros(B, dtype=torch.long, device=dev)
-    active = _bnorm(g) > 0
+    active = _bn(data, g) > 0
     reason = torch.where(~active, torch.full_like(reason, 4), reason)
     for _ in range(max_iter + 2):
         if not bool(active.any()):
@@ -253,27 +334,27 @@ def batched_lbfgs(data: BatchedGLMData, loss, l2: float, W0: torch.Tensor, tol: 
         alphas = []
         for k in range(m):
             valid = (hist > k).to(dt)
-            a = valid * rho[:, k] * _bdot(S[:, k], q)
-            q = q - a.unsqueeze(1) * Y[:, k]
+            a = valid * rho[:, k] * data.bdot(S[k], q)
+            q = q - E(a) * Y[k]
             alphas.append(a)
-        yy = _bdot(Y[:, 0], Y[:, 0])
+        yy = data.bdot(Y[0], Y[0])
         scale = torch.where(hist > 0, 1.0 / (rho[:, 0] * yy).clamp(min=1e-300), torch.ones_like(yy))
-        q = q * scale.unsqueeze(1)
+        q = q * E(scale)
         for k in range(m - 1, -1, -1):
             valid = (hist > k).to(dt)
-            b = valid * rho[:, k] * _bdot(Y[:, k], q)
-            q = q + (alphas[k] - b).unsqueeze(1) * S[:, k]
+            b = valid * rho[:, k] * data.bdot(Y[k], q)
+            q = q + E(alphas[k] - b) * S[k]
         dvec = -q
         if owl:
             dvec = torch.where(dvec * g < 0, dvec, torch.zeros_like(dvec))
-        gd = _bdot(g, dvec)
+        gd = data.bdot(g, dvec)
         bad = active & (gd >= 0)
         # reset history and use steepest descent where the direction is not a descent direction
-        dvec = torch.where(bad.unsqueeze(1), -g, dvec)
+        dvec = torch.where(E(bad), -g, dvec)
         hist = torch.where(bad, torch.zeros_like(hist), hist)
-        gd = _bdot(g, dvec)
+        gd = data.bdot(g, dvec)
         orthant = torch.where(W != 0, torch.sign(W), torch.sign(-g))
-        t = torch.where(it == 0, 1.0 / _bnorm(dvec).clamp(min=1e-300), torch.ones_like(gd))
+        t = torch.where(it == 0, 1.0 / _bn(data, dvec).clamp(min=1e-300), torch.ones_like(gd))
         shrink = torch.where(it == 0, torch.full_like(gd, 0.1 if owl else 0.5), torch.full_like(gd, 0.5))
         searching = active.clone()
         W_acc, f_acc, g_acc, fs_acc, gs_acc = W.clone(), f.clone(), g.clone(), f_s.clone(), g_s.clone()
@@ -281,36 +362,37 @@ def batched_lbfgs(data: BatchedGLMData, loss, l2: float, W0: torch.Tensor, tol: 
         for _ls in range(max_ls):
             if not bool(searching.any()):
                 break
-            Wt = W + t.unsqueeze(1) * dvec
+            Wt = W + E(t) * dvec
             if owl:
                 Wt = torch.where(torch.sign(Wt) != orthant, torch.zeros_like(Wt), Wt)
             ft_s, gt_s = data.value_grad(loss, Wt, l2)
             ft, gt = adjust(Wt, ft_s, gt_s)
             ok = searching & torch.isfinite(ft) & (ft <= f + 1e-4 * t * gd)
-            W_acc = torch.where(ok.unsqueeze(1), Wt, W_acc)
+            W_acc = torch.where(E(ok), Wt, W_acc)
             f_acc = torch.where(ok, ft, f_acc)
-            g_acc = torch.where(ok.unsqueeze(1), gt, g_acc)
+            g_acc = torch.where(E(ok), gt, g_acc)
             fs_acc = torch.where(ok, ft_s, fs_acc)
-            gs_acc = torch.where(ok.unsqueeze(1), gt_s, gs_acc)
+            gs_acc = torch.where(E(ok), gt_s, gs_acc)
             found |= ok
             searching &= ~ok
             t = torch.where(searching, t * shrink, t)
         moved = active & found
         s_new = W_acc - W
         y_new = gs_acc - g_s
-        sy = _bdot(s_new, y_new)
+        sy = data.bdot(s_new, y_new)
         upd = moved & (sy > 1e-300)
         # shift history (newest in slot 0)
-        S = torch.where(upd[:, None, None], torch.cat([s_new.unsqueeze(1), S[:, :-1]], 1), S)
-        Y = torch.where(upd[:, None, None], torch.cat([y_new.unsqueeze(1), Y[:, :-1]], 1), Y)
+        ue = E(upd)
+        S = [torch.where(ue, s_new if k == 0 else S[k - 1], S[k]) for k in range(m)]
+        Y = [torch.where(ue, y_new if k == 0 else Y[k - 1], Y[k]) for k in range(m)]
         rho = torch.where(upd[:, None], torch.cat([(1.0 / sy.clamp(min=1e-300)).unsqueeze(1), rho[:, :-1]], 1), rho)
         hist = torch.where(upd, (hist + 1).clamp(max=m), hist)
         f_prev = f
-        W = torch.where(moved.unsqueeze(1), W_acc, W)
+        W = torch.where(E(moved), W_acc, W)
         f = torch.where(moved, f_acc, f)
-        g = torch.where(moved.unsqueeze(1), g_acc, g)
+        g = torch.where(E(moved), g_acc, g)
         f_s = torch.where(moved, fs_acc, f_s)
-        g_s = torch.where(moved.unsqueeze(1), gs_acc, g_s)
+        g_s = torch.where(E(moved), gs_acc, g_s)
         it = it + moved.long()
         not_improving = active & ~found
         rc = conv.check(it, f, f_prev, g, moved, not_improving)

@@ -119,3 +119,24 @@ def test_random_projection_and_feature_selection_run():
         m = coord.update_model(coord.initialize_model())
         s = coord.score(m)
         assert torch.isfinite(s).all() and float(s.abs().sum()) > 0
+
+
+@pytest.mark.parametrize("task,opt", [("LOGISTIC_REGRESSION", "TRON"), ("LINEAR_REGRESSION", "LBFGS"),
+                                      ("POISSON_REGRESSION", "TRON")])
+def test_segmented_re_layout_matches_dense(task, opt):
+    """Block-diagonal (segmented) random-effect solve == dense bucketed batch solve, entity by entity."""
+    data, _ = generate_game_data(n_rows=2500, n_users=30, seed=12, task=task)
+    cfg = _cfg(opt, 1.0, 100, 1e-10)
+    out = {}
+    for layout in ("dense", "segmented"):
+        c = RandomEffectCoordinate("u", data, RandomEffectDataConfiguration("userId", "user"), cfg, task,
+                                   compute_variance=True, device="cpu", layout=layout)
+        assert c.dataset.layout == layout
+        out[layout] = c.update_model(c.initialize_model())
+    a, b = out["dense"], out["segmented"]
+    assert list(a.entity_ids) == list(b.entity_ids)
+    for e in a.entity_ids:
+        np.testing.assert_allclose(a.coefficients_of(e).means.numpy(), b.coefficients_of(e).means.numpy(),
+                                   rtol=1e-6, atol=1e-7)
+        np.testing.assert_allclose(a.coefficients_of(e).variances.numpy(), b.coefficients_of(e).variances.numpy(),
+                                   rtol=1e-6, atol=1e-7)

@@ -48,3 +48,21 @@ def test_game_fit_gpu_bf16_features_close():
     r64 = _fit("cuda", "LOGISTIC_REGRESSION", data)
     r16 = _fit("cuda", "LOGISTIC_REGRESSION", data, precision="bf16")
     assert abs(r64.evaluations[0][1] - r16.evaluations[0][1]) < 5e-3
+
+
+@pytest.mark.parametrize("opt", ["TRON", "LBFGS"])
+def test_segmented_random_effect_on_gpu_matches_cpu_dense(opt):
+    """The block-diagonal random-effect solve on the HIP kernels == the dense CPU batch solve."""
+    from photon_ml_amd.algorithm.coordinates import RandomEffectCoordinate
+    data, _ = generate_game_data(n_rows=5000, n_users=60, seed=23, task="LOGISTIC_REGRESSION")
+    cfg = GLMOptimizationConfiguration(OptimizerConfig(opt, 100, 1e-10), RegularizationContext("L2"), 1.0)
+    cpu = RandomEffectCoordinate("u", data, RandomEffectDataConfiguration("userId", "user"), cfg,
+                                 "LOGISTIC_REGRESSION", device="cpu", layout="dense")
+    gpu = RandomEffectCoordinate("u", data, RandomEffectDataConfiguration("userId", "user"), cfg,
+                                 "LOGISTIC_REGRESSION", device="cuda", layout="segmented")
+    a, b = cpu.update_model(cpu.initialize_model()), gpu.update_model(gpu.initialize_model())
+    for e in a.entity_ids[:20]:
+        np.testing.assert_allclose(a.coefficients_of(e).means.numpy(), b.coefficients_of(e).means.numpy(),
+                                   rtol=1e-5, atol=1e-6)
+    sa, sb = cpu.score(a).cpu(), gpu.score(b).cpu()
+    assert torch.allclose(sa, sb, atol=1e-5)

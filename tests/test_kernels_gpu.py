@@ -141,3 +141,26 @@ def test_device_shard_layouts_agree():
     (f0, s0, g0), (f1, s1, g1) = out["segmented"], out["tiled"]
     assert abs(f1 - f0) <= 1e-5 * abs(f0) and abs(s1 - s0) <= 1e-4 * max(1.0, abs(s0))
     assert torch.allclose(g1, g0, rtol=1e-4, atol=1e-4 * float(g0.abs().max()))
+
+
+@pytest.mark.parametrize("layout", LAYOUTS)
+def test_column_windows_block_diagonal(layout):
+    """Block-diagonal data (random-effect layout): per-chunk column windows give the same products."""
+    from photon_ml_amd.ops.device import DeviceGLMData
+    rng = np.random.default_rng(4)
+    n_ent, rows_per, d_e = 300, 40, 25
+    blocks = [sp.random(rows_per, d_e, density=0.3, format="csr", random_state=int(rng.integers(1 << 30)),
+                        data_rvs=lambda k: rng.normal(size=k)) for _ in range(n_ent)]
+    x = sp.block_diag(blocks, format="csr")
+    data = LabeledData(x, (rng.random(x.shape[0]) < 0.5).astype(float))
+    ref = TorchGLMData(data, "cpu")
+    dev = DeviceGLMData.from_labeled(data, "cuda", "f64", chunk_rows=1000, layout=layout, col_windows=True)
+    assert max(dev.col_lo) > 0
+    w = torch.from_numpy(rng.normal(size=x.shape[1]))
+    r = torch.from_numpy(rng.normal(size=x.shape[0]))
+    assert torch.allclose(dev.matvec(w.cuda()).cpu(), ref.matvec(w), atol=1e-10)
+    assert torch.allclose(dev.rmatvec(r.cuda()).cpu(), ref.rmatvec(r), atol=1e-10)
+    assert torch.allclose(dev.rmatvec(r.cuda(), square=True).cpu(), ref.rmatvec(r, square=True), atol=1e-10)
+    f0, s0, g0 = ref.value_grad_sums(LOGISTIC, w * 0.1, 0.0)
+    f1, s1, g1 = dev.value_grad_sums(LOGISTIC, (w * 0.1).cuda(), 0.0)
+    assert abs(f1 - f0) < 1e-9 * abs(f0) and torch.allclose(g1.cpu(), g0, atol=1e-9)
