@@ -237,8 +237,10 @@ class RandomEffectCoordinate(Coordinate):
             var = (1.0 / (seg.hdiag(self.loss, res.W, l2) + EPSILON)).detach().cpu().numpy()
         keys = ds.projection.keys  # entity * dim + feature, sorted, aligned with W
         nz = W != 0
-        return RandomEffectModel(self.data_config.random_effect_type, self.data_config.feature_shard_id, self.task,
-                                 ds.entity_ids, ds.dim, keys[nz], W[nz], None if var is None else var[nz])
+        out = RandomEffectModel(self.data_config.random_effect_type, self.data_config.feature_shard_id, self.task,
+                                ds.entity_ids, ds.dim, keys[nz], W[nz], None if var is None else var[nz])
+        self._last = (out, res.W)
+        return out
 
     def _warm_start_segmented(self, model):
         ds = self.dataset
@@ -285,7 +287,19 @@ class RandomEffectCoordinate(Coordinate):
         return keys[nz], vals[nz], (None if vv is None else vv[nz])
 
     def score(self, model: RandomEffectModel) -> torch.Tensor:
-        return model.score(self.data, self.device, mask=self.dataset.score_mask).to(torch.float64)
+        ds = self.dataset
+        last = getattr(self, "_last", None)
+        if ds.layout == "segmented" and last is not None and last[0] is model:
+            # the model just solved: its active-row scores are one forward pass over the block-diagonal data
+            z = ds.seg.glm.matvec(last[1])
+            out = torch.zeros(self.data.n_rows, dtype=torch.float64, device=z.device)
+            out[ds.seg_rows] = z
+            if len(ds.passive_rows):
+                pm = np.zeros(self.data.n_rows, dtype=bool)
+                pm[ds.passive_rows] = True
+                out = out + model.score(self.data, z.device, mask=pm).to(torch.float64)
+            return out.to(self.device)
+        return model.score(self.data, self.device, mask=ds.score_mask).to(torch.float64)
 
     def regularization_term_value(self, model: RandomEffectModel) -> float:
         reg, lam = self.opt_config.regularization_context, self.opt_config.regularization_weight

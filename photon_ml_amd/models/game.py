@@ -57,10 +57,16 @@ class RandomEffectModel:
         self._task = TaskType.parse(task)
         self.entity_ids = np.asarray(entity_ids)
         self.dim = int(dim)
-        order = np.argsort(keys, kind="stable")
-        self.keys = np.asarray(keys, dtype=np.int64)[order]
-        self.values = np.asarray(values, dtype=np.float64)[order]
-        self.variances = None if variances is None else np.asarray(variances, dtype=np.float64)[order]
+        keys = np.asarray(keys, dtype=np.int64)
+        values = np.asarray(values, dtype=np.float64)
+        if len(keys) > 1 and not bool(np.all(keys[1:] >= keys[:-1])):  # solvers emit sorted keys: skip the sort
+            order = np.argsort(keys, kind="stable")
+            keys, values = keys[order], values[order]
+            if variances is not None:
+                variances = np.asarray(variances)[order]
+        self.keys = keys
+        self.values = values
+        self.variances = None if variances is None else np.asarray(variances, dtype=np.float64)
 
     @property
     def task(self) -> TaskType:
@@ -101,6 +107,8 @@ class RandomEffectModel:
         """Score every sample whose entity has a model (K6): sum_j x_ij * w_{e(i), j}."""
         x = data.shard(self.feature_shard_id)
         n = x.shape[0]
+        if len(self.keys) == 0:
+            return torch.zeros(n, dtype=torch.float64, device=device)
         ent = self.entity_index(data.id_tags[self.random_effect_type])
         if mask is not None:
             ent = np.where(mask, ent, -1)

@@ -78,8 +78,9 @@ def glm_lib() -> Optional[ctypes.CDLL]:
                                    c_void_p, c_void_p, c_void_p, c_void_p, c_void_p, c_int, c_void_p, c_void_p]
         lib.pml_tl_t.argtypes = [c_int, ctypes.POINTER(TLTDesc), c_void_p, c_int, c_void_p, c_void_p, c_void_p]
         lib.pml_tl_config.argtypes = [c_int, c_int]
+        lib.pml_segdot.argtypes = [c_void_p, c_void_p, c_int, c_void_p, c_int, c_void_p, c_void_p]
         for f in ("pml_seg_fwd", "pml_seg_t", "pml_reduce_stats", "pml_build_blocks", "pml_tl_fwd", "pml_tl_t",
-                  "pml_tl_maxbits"):
+                  "pml_tl_maxbits", "pml_segdot"):
             getattr(lib, f).restype = c_int
         lib.pml_set_config.argtypes = [c_int, c_int, c_int, c_int]
         lib._pml_typed = True
@@ -113,6 +114,28 @@ def require_glm_lib() -> ctypes.CDLL:
         raise RuntimeError(
             f"native GLM kernel library missing ({lib_path('hip', 'glm')}); run python -m photon_ml_amd.ops.build")
     return lib
+
+
+def segdot(a: torch.Tensor, b: Optional[torch.Tensor], ptr: torch.Tensor, mode: int = 0) -> torch.Tensor:
+    """Per-segment sum of a*b (mode 0) / a (1) / |a| (2) over contiguous segments ``ptr`` (int64, device).
+    fp64, deterministic; CUDA tensors use the HIP kernel, CPU tensors a cumsum-free reduceat."""
+    nseg = ptr.numel() - 1
+    if a.device.type != "cuda":
+        import numpy as np
+        v = (a * b if mode == 0 else (a if mode == 1 else a.abs())).detach().cpu().numpy()
+        p = ptr.cpu().numpy()
+        out = np.zeros(nseg)
+        nz = p[1:] > p[:-1]
+        if v.size and nz.any():
+            out[nz] = np.add.reduceat(v, p[:-1][nz])
+        return torch.from_numpy(out).to(a.device)
+    lib = require_glm_lib()
+    a = a.contiguous()
+    b = a if b is None else b.contiguous()
+    out = torch.empty(nseg, dtype=torch.float64, device=a.device)
+    check(lib.pml_segdot(a.data_ptr(), b.data_ptr(), mode, ptr.data_ptr(), nseg, out.data_ptr(),
+                         stream_handle(a.device)), "segdot")
+    return out
 
 
 def batched_lib() -> Optional[ctypes.CDLL]:

@@ -102,10 +102,14 @@ class SegmentedGLMData:
     def __init__(self, glm, row_entity: torch.Tensor, col_entity: torch.Tensor, n_entities: int, y: torch.Tensor,
                  weights: torch.Tensor, offsets: torch.Tensor):
         self.glm = glm
-        self.row_entity = row_entity
-        self.col_entity = col_entity
+        self.row_entity = row_entity  # sorted: rows grouped by entity
+        self.col_entity = col_entity  # sorted: each entity's coefficients are contiguous
         self.B = int(n_entities)
         self.y, self.w, self.o = y, weights, offsets
+        dev = y.device
+        ar = torch.arange(self.B + 1, device=dev)
+        self.row_ptr = torch.searchsorted(row_entity, ar).to(torch.int64)
+        self.col_ptr = torch.searchsorted(col_entity, ar).to(torch.int64)
         self._dzz_key = None
         self._dzz = None
 
@@ -113,17 +117,21 @@ class SegmentedGLMData:
     def n_batch(self) -> int:
         return self.B
 
-    def _seg(self, v, idx):
-        return torch.zeros(self.B, dtype=v.dtype, device=v.device).index_add_(0, idx, v)
-
+    # per-entity reductions over contiguous segments: deterministic segmented kernel (no scatter atomics)
     def bdot(self, a, b):
-        return self._seg(a * b, self.col_entity)
+        from ..ops.native import segdot
+        return segdot(a, b, self.col_ptr, 0)
 
     def bexp(self, s):
         return s[self.col_entity]
 
     def babs_sum(self, a):
-        return self._seg(a.abs(), self.col_entity)
+        from ..ops.native import segdot
+        return segdot(a, None, self.col_ptr, 2)
+
+    def _rowsum(self, v):
+        from ..ops.native import segdot
+        return segdot(v, None, self.row_ptr, 1)
 
     def margins(self, W):
         return self.glm.matvec(W) + self.o
@@ -131,7 +139,7 @@ class SegmentedGLMData:
     def value_grad(self, loss, W, l2: float):
         z = self.margins(W)
         l, dl = loss.loss_and_dz(z, self.y)
-        f = self._seg(self.w * l, self.row_entity)
+        f = self._rowsum(self.w * l)
         g = self.glm.rmatvec(self.w * dl)
         if l2 > 0:
             f = f + 0.5 * l2 * self.bdot(W, W)

@@ -127,13 +127,17 @@ def test_segmented_re_layout_matches_dense(task, opt):
     """Block-diagonal (segmented) random-effect solve == dense bucketed batch solve, entity by entity."""
     data, _ = generate_game_data(n_rows=2500, n_users=30, seed=12, task=task)
     cfg = _cfg(opt, 1.0, 100, 1e-10)
-    out = {}
+    out, coords = {}, {}
     for layout in ("dense", "segmented"):
         c = RandomEffectCoordinate("u", data, RandomEffectDataConfiguration("userId", "user"), cfg, task,
                                    compute_variance=True, device="cpu", layout=layout)
         assert c.dataset.layout == layout
         out[layout] = c.update_model(c.initialize_model())
+        coords[layout] = c
     a, b = out["dense"], out["segmented"]
+    # fast device scoring of the just-solved model == generic model scoring
+    assert torch.allclose(coords["segmented"].score(b), coords["dense"].score(a), atol=1e-6)
+    assert torch.allclose(coords["segmented"].score(b), b.score(data, "cpu"), atol=1e-10)
     assert list(a.entity_ids) == list(b.entity_ids)
     for e in a.entity_ids:
         np.testing.assert_allclose(a.coefficients_of(e).means.numpy(), b.coefficients_of(e).means.numpy(),

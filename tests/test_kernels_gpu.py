@@ -164,3 +164,19 @@ def test_column_windows_block_diagonal(layout):
     f0, s0, g0 = ref.value_grad_sums(LOGISTIC, w * 0.1, 0.0)
     f1, s1, g1 = dev.value_grad_sums(LOGISTIC, (w * 0.1).cuda(), 0.0)
     assert abs(f1 - f0) < 1e-9 * abs(f0) and torch.allclose(g1.cpu(), g0, atol=1e-9)
+
+
+def test_segdot_kernel():
+    from photon_ml_amd.ops.native import segdot
+    rng = np.random.default_rng(9)
+    lens = rng.integers(0, 300, size=2000)
+    lens[5] = 5000  # long segment
+    ptr = torch.from_numpy(np.concatenate([[0], np.cumsum(lens)]).astype(np.int64))
+    a = torch.from_numpy(rng.normal(size=int(ptr[-1])))
+    b = torch.from_numpy(rng.normal(size=int(ptr[-1])))
+    for mode in (0, 1, 2):
+        ref = segdot(a, b, ptr, mode)  # CPU reduceat path
+        got = segdot(a.cuda(), b.cuda(), ptr.cuda(), mode).cpu()
+        assert torch.allclose(got, ref, rtol=1e-12, atol=1e-12)
+        again = segdot(a.cuda(), b.cuda(), ptr.cuda(), mode).cpu()
+        assert torch.equal(got, again)
