@@ -45,9 +45,23 @@ class CoordinateDescent:
             return coord.score_validation(model, self.validation_data)
         return model.score(self.validation_data, device)
 
-    def run(self, iterations: int, initial_model: Optional[GameModel] = None) -> Tuple[GameModel, Optional[list]]:
+    def run(self, iterations: int, initial_model: Optional[GameModel] = None, checkpointer=None,
+            tag: str = "") -> Tuple[GameModel, Optional[list]]:
+        """``checkpointer`` (:class:`photon_ml_amd.utils.checkpoint.Checkpointer`): save the state after every
+        coordinate update and, when a state with the same ``tag`` exists, resume from the coordinate after the
+        last one saved (scores are recomputed from the restored model)."""
         if iterations <= 0:
             raise ValueError(f"Number of coordinate descent iterations must be greater than 0: {iterations}")
+        start_it, start_c = 0, 0
+        resumed = None
+        if checkpointer is not None:
+            st = checkpointer.load_cd()
+            if st is not None and st.get("tag", "") == tag:
+                resumed = st
+                initial_model = st["model"]
+                start_it, start_c = st["iteration"], st["next"]
+                self.history = list(st["history"])
+                log.info("resuming coordinate descent at iteration %d, coordinate %d", start_it, start_c)
         if initial_model is None:
             initial_model = GameModel(OrderedDict((cid, c.initialize_model()) for cid, c in self.coordinates.items()))
         for cid in self.coordinates:
@@ -63,10 +77,19 @@ class CoordinateDescent:
                           for cid in self.coordinates}
             val_full = sum(val_scores.values())
         best_model, best_evals = None, None
-        for it in range(iterations):
+        if resumed is not None and resumed["best_model"] is not None and resumed["best_evals"]:
+            by_name = {e.name: e for e in self.validation_evaluators}
+            best_model = resumed["best_model"]
+            best_evals = [(by_name[n], v) for n, v in resumed["best_evals"] if n in by_name] or None
+        cids = list(self.coordinates)
+        evaluations = None
+        for it in range(start_it, iterations):
             with Timed(f"Coordinate descent iteration {it}", log):
-                evaluations = None
-                for cid, coord in self.coordinates.items():
+                if it > start_it or start_c == 0:
+                    evaluations = None
+                for ci, (cid, coord) in enumerate(self.coordinates.items()):
+                    if it == start_it and ci < start_c:
+                        continue
                     t0 = time.time()
                     old = model.get(cid)
                     with Timed(f"Update coordinate {cid}", log):
@@ -97,8 +120,18 @@ class CoordinateDescent:
                     self.history.append(rec)
                     if self.event_callback is not None:
                         self.event_callback(rec)
-                if evaluations:
-                    e0, v0 = evaluations[0]
-                    if best_evals is None or e0.better_than(v0, best_evals[0][1]):
-                        best_model, best_evals = model, evaluations
+                    last = ci == len(cids) - 1
+                    if last and evaluations:
+                        e0, v0 = evaluations[0]
+                        if best_evals is None or e0.better_than(v0, best_evals[0][1]):
+                            best_model, best_evals = model, evaluations
+                    if checkpointer is not None:
+                        nxt_it, nxt_c = (it + 1, 0) if last else (it, ci + 1)
+                        checkpointer.save_cd(model, nxt_it, nxt_c, best_model,
+                                             None if best_evals is None else [(e.name, v) for e, v in best_evals],
+                                             self.history, tag)
+        if self.validation_data is not None and evaluations is None and best_evals is None:
+            # resumed exactly at the end of the last sweep: re-evaluate the restored model
+            evaluations = [(e, e.evaluate(val_full)) for e in self.validation_evaluators]
+            best_model, best_evals = model, evaluations
         return (best_model if best_model is not None else model), best_evals

@@ -107,6 +107,9 @@ def build_parser() -> argparse.ArgumentParser:
     p.add_argument("--hyper-parameter-tuning-scale", default="LOG", choices=["LOG", "LINEAR"])
     p.add_argument("--compute-variance", type=parse_bool, default=False)
     p.add_argument("--use-warm-start", type=parse_bool, default=True)
+    p.add_argument("--checkpoint-directory", help="save coordinate-descent state after every coordinate update")
+    p.add_argument("--resume", type=parse_bool, default=False,
+                   help="continue an interrupted run from --checkpoint-directory (the output directory is kept)")
     return p
 
 
@@ -216,8 +219,9 @@ class GameTrainingDriver(GameDriverBase):
     def run(self) -> Dict[str, object]:
         a = self.args
         with Timed("Clean output directories"):
-            process_output_dir(a.root_output_directory, a.override_output_directory)
-            if a.data_summary_directory:
+            if not (a.resume and os.path.exists(a.root_output_directory)):
+                process_output_dir(a.root_output_directory, a.override_output_directory)
+            if a.data_summary_directory and not a.resume:
                 process_output_dir(a.data_summary_directory, a.override_output_directory)
         self.logger = PhotonLogger(os.path.join(a.root_output_directory, LOGS), a.logging_level, rank=rank())
         try:
@@ -274,6 +278,8 @@ class GameTrainingDriver(GameDriverBase):
                .set_coordinate_normalization_contexts(norm_ctx))
         if a.evaluators:
             est.set_validation_evaluators(split_list(a.evaluators))
+        if a.checkpoint_directory:
+            est.set_checkpoint_directory(a.checkpoint_directory, a.resume)
         with Timed("Fit models"):
             explicit = est.fit(train, validation, configs)
         for i, r in enumerate(explicit):

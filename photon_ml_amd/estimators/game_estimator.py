@@ -16,6 +16,7 @@ configuration only swaps the optimisation problem of each coordinate.
 from __future__ import annotations
 
 import logging
+import os
 from collections import OrderedDict
 from dataclasses import dataclass
 from typing import Dict, List, Optional, Sequence, Tuple
@@ -68,6 +69,8 @@ class GameEstimator:
         self.event_callback = None
         self.coordinates = None
         self.history: List[list] = []
+        self.checkpoint_directory: Optional[str] = None
+        self.resume = False
 
     # fluent setters mirroring Spark ML Params ------------------------------------------------------------
     def set_training_task(self, t):
@@ -108,6 +111,13 @@ class GameEstimator:
 
     def set_warm_start(self, b: bool):
         self.use_warm_start = bool(b)
+        return self
+
+    def set_checkpoint_directory(self, directory: Optional[str], resume: bool = False):
+        """Checkpoint coordinate descent after every coordinate update (one state file per configuration and
+        rank); with ``resume`` an interrupted fit continues where it stopped (see utils/checkpoint.py)."""
+        self.checkpoint_directory = directory
+        self.resume = bool(resume)
         return self
 
     # ----------------------------------------------------------------------------------------------------
@@ -155,12 +165,21 @@ class GameEstimator:
                                      data.weights)
         val_evals = self._validation_evaluators(validation) if validation is not None else []
         results, prev = [], None
-        for cfg in configurations:
+        for i, cfg in enumerate(configurations):
             for cid, c in self.coordinates.items():
                 c.set_config(cfg[cid])
             cd = CoordinateDescent(self.coordinates, train_eval, validation, val_evals,
                                    event_callback=self.event_callback)
-            model, evals = cd.run(self.coordinate_descent_iterations, prev if self.use_warm_start else None)
+            ck, tag = None, ""
+            if self.checkpoint_directory:
+                from ..utils.checkpoint import Checkpointer
+                import json as _json
+                ck = Checkpointer(self.checkpoint_directory, f"cd-state-{i}")
+                tag = _json.dumps({c: cfg[c].to_json() for c in sorted(cfg)}, sort_keys=True)
+                if not self.resume and ck.exists():
+                    os.remove(ck.path)
+            model, evals = cd.run(self.coordinate_descent_iterations, prev if self.use_warm_start else None, ck,
+                                  tag)
             self.history.append(cd.history)
             results.append(GameResult(model, evals, cfg))
             if self.use_warm_start:

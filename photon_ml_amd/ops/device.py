@@ -27,6 +27,7 @@ from ..data.matrix import LabeledData
 from .native import SegChunkDesc, check, require_glm_lib, stream_handle
 from .reference import GLMComputable
 from .tiled import DEFAULT_ITEM_ENTRIES, TLFwdChunk, TLTChunk, tl_supported
+from ..utils.timing import trace_range
 
 LAYOUTS = ("auto", "tiled", "segmented")
 
@@ -289,6 +290,10 @@ class DeviceGLMData(GLMComputable):
     # ------------------------------------------------------------------
     def value_grad_packed(self, loss, w_eff, margin_shift) -> torch.Tensor:
         """Device tensor [D + 2] = (G, F, S) — packed so a DP wrapper can all-reduce it in one RCCL call."""
+        with trace_range("K1 value+grad pass"):
+            return self._value_grad_packed(loss, w_eff, margin_shift)
+
+    def _value_grad_packed(self, loss, w_eff, margin_shift) -> torch.Tensor:
         out = torch.zeros(self.dim + 2, dtype=torch.float64, device=self.device)
         G = out[: self.dim]
         x = self._vec(w_eff)
@@ -322,6 +327,10 @@ class DeviceGLMData(GLMComputable):
         self._dzz_shift = float(shift)
 
     def hv_packed(self, loss, w_eff, margin_shift, v_eff, v_shift) -> torch.Tensor:
+        with trace_range("K2 Hessian-vector pass"):
+            return self._hv_packed(loss, w_eff, margin_shift, v_eff, v_shift)
+
+    def _hv_packed(self, loss, w_eff, margin_shift, v_eff, v_shift) -> torch.Tensor:
         self._ensure_dzz(loss, w_eff, margin_shift)
         out = torch.zeros(self.dim + 2, dtype=torch.float64, device=self.device)
         H = out[: self.dim]

@@ -174,7 +174,9 @@ class Optimizer:
 
     def step(self, objective, data) -> OptimizerState:
         """Run one optimizer iteration from the current state."""
-        self._update_current(self._run_one_iteration(objective, data, self.current))
+        from ..utils.timing import trace_range
+        with trace_range(f"{type(self).__name__} iteration {self.current.iter + 1}"):
+            self._update_current(self._run_one_iteration(objective, data, self.current))
         return self.current
 
     def optimize(self, objective, data, initial: torch.Tensor, skip_zero_tolerance_pass: bool = False):

@@ -19,6 +19,8 @@ from typing import Optional
 import torch
 import torch.distributed as dist
 
+from ..utils.timing import trace_range
+
 
 def env_world() -> tuple[int, int, int]:
     return (int(os.environ.get("RANK", 0)), int(os.environ.get("WORLD_SIZE", 1)),
@@ -120,12 +122,13 @@ class DistributedGLMData:
                 h, p = a, b
                 buf = torch.cat([h.to(torch.float64), torch.tensor([0.0, p], dtype=torch.float64, device=h.device)])
         dev = self._comm_device()
-        if buf.device != dev:
-            tmp = buf.to(dev)
-            all_reduce_(tmp, group=self.group)
-            buf = tmp.to(buf.device)
-        else:
-            all_reduce_(buf, group=self.group)
+        with trace_range(f"C1 all-reduce {fn} [{buf.numel()} fp64]"):
+            if buf.device != dev:
+                tmp = buf.to(dev)
+                all_reduce_(tmp, group=self.group)
+                buf = tmp.to(buf.device)
+            else:
+                all_reduce_(buf, group=self.group)
         if self.nan_guard:
             check_finite_(buf, fn)
         return buf

@@ -1,0 +1,145 @@
+"""Mid-training checkpoint / resume (SURVEY §5 "Checkpoint / resume" — absent in the reference, which only
+persists final models; Spark lineage recomputation was its only recovery).
+
+* GAME coordinate descent: after every coordinate update the current GAME model, the sweep position
+  (iteration, next coordinate), the best model so far with its evaluations and the history are written to
+  ``<dir>/cd-state[-rank<r>].safetensors`` (atomic rename). ``CoordinateDescent.run(..., checkpointer=...)``
+  resumes from the next coordinate: scores are recomputed from the restored model (one scoring pass), so no
+  N-length arrays are stored.
+* Legacy λ path: every finished (λ, model) is stored; a resumed run skips the λ values already trained and
+  warm-starts from the last one.
+
+Format: safetensors (tensors / numpy arrays only, nothing executable) + a JSON metadata string. Every rank of a
+process group writes its own file (entity-sharded random effects differ per rank).
+"""
+from __future__ import annotations
+
+import json
+import os
+from collections import OrderedDict
+from typing import Dict, List, Optional, Tuple
+
+import numpy as np
+import torch
+
+from ..constants import TaskType
+
+
+def _rank() -> int:
+    from ..parallel.dist import rank
+    return rank()
+
+
+def _strings_to_array(values) -> np.ndarray:
+    return np.frombuffer("\n".join(str(v) for v in values).encode("utf-8"), dtype=np.uint8).copy()
+
+
+def _array_to_strings(a: np.ndarray, n: int) -> np.ndarray:
+    if n == 0:
+        return np.zeros(0, dtype=object)
+    return np.array(bytes(a.tobytes()).decode("utf-8").split("\n"), dtype=object)
+
+
+def game_model_to_arrays(model, prefix: str) -> Tuple[Dict[str, np.ndarray], dict]:
+    from ..models.game import FixedEffectModel, RandomEffectModel
+    arrays, meta = {}, {"coordinates": []}
+    for cid, m in model:
+        key = f"{prefix}{cid}"
+        if isinstance(m, FixedEffectModel):
+            c = m.glm.coefficients
+            arrays[key + ".means"] = c.means.detach().cpu().numpy().astype(np.float64)
+            if c.variances is not None:
+                arrays[key + ".variances"] = c.variances.detach().cpu().numpy().astype(np.float64)
+            meta["coordinates"].append({"id": cid, "kind": "fixed", "shard": m.feature_shard_id,
+                                        "task": m.task.value})
+        elif isinstance(m, RandomEffectModel):
+            arrays[key + ".keys"] = m.keys
+            arrays[key + ".values"] = m.values
+            if m.variances is not None:
+                arrays[key + ".variances"] = m.variances
+            arrays[key + ".entities"] = _strings_to_array(m.entity_ids)
+            meta["coordinates"].append({"id": cid, "kind": "random", "shard": m.feature_shard_id,
+                                        "re_type": m.random_effect_type, "task": m.task.value, "dim": m.dim,
+                                        "n_entities": int(m.n_entities)})
+        else:
+            raise TypeError(type(m))
+    return arrays, meta
+
+
+def game_model_from_arrays(arrays: Dict[str, np.ndarray], meta: dict, prefix: str):
+    from ..models.game import FixedEffectModel, GameModel, RandomEffectModel
+    from ..models.glm import Coefficients, model_for_task
+    models = OrderedDict()
+    for c in meta["coordinates"]:
+        key = f"{prefix}{c['id']}"
+        task = TaskType.parse(c["task"])
+        if c["kind"] == "fixed":
+            var = arrays.get(key + ".variances")
+            coef = Coefficients(torch.from_numpy(arrays[key + ".means"].copy()),
+                                None if var is None else torch.from_numpy(var.copy()))
+            models[c["id"]] = FixedEffectModel(model_for_task(task, coef), c["shard"])
+        else:
+            ents = _array_to_strings(arrays[key + ".entities"], c["n_entities"])
+            models[c["id"]] = RandomEffectModel(c["re_type"], c["shard"], task, ents, c["dim"],
+                                                arrays[key + ".keys"], arrays[key + ".values"],
+                                                arrays.get(key + ".variances"))
+    return GameModel(models)
+
+
+class Checkpointer:
+    """Writes / reads one state file per rank under ``directory``."""
+
+    def __init__(self, directory: str, name: str = "cd-state"):
+        self.directory = directory
+        self.name = name
+        os.makedirs(directory, exist_ok=True)
+
+    @property
+    def path(self) -> str:
+        r = _rank()
+        return os.path.join(self.directory, f"{self.name}{'' if r == 0 else f'-rank{r}'}.safetensors")
+
+    def save(self, arrays: Dict[str, np.ndarray], meta: dict):
+        from safetensors.numpy import save_file
+        tmp = self.path + ".tmp"
+        arrays = {k: np.ascontiguousarray(v) for k, v in arrays.items()}
+        if not arrays:
+            arrays = {"_empty": np.zeros(1)}
+        save_file(arrays, tmp, metadata={"meta": json.dumps(meta)})
+        os.replace(tmp, self.path)
+
+    def load(self) -> Optional[Tuple[Dict[str, np.ndarray], dict]]:
+        if not os.path.exists(self.path):
+            return None
+        from safetensors import safe_open
+        arrays = {}
+        with safe_open(self.path, framework="numpy") as f:
+            meta = json.loads(f.metadata()["meta"])
+            for k in f.keys():
+                arrays[k] = f.get_tensor(k)
+        return arrays, meta
+
+    def exists(self) -> bool:
+        return os.path.exists(self.path)
+
+    # ---- coordinate descent state
+    def save_cd(self, model, iteration: int, next_coordinate: int, best_model, best_evals, history: List[dict],
+                tag: str = ""):
+        arrays, meta = game_model_to_arrays(model, "model/")
+        meta = {"model": meta, "iteration": iteration, "next": next_coordinate, "tag": tag,
+                "history": history, "best_evals": best_evals}
+        if best_model is not None:
+            ba, bm = game_model_to_arrays(best_model, "best/")
+            arrays.update(ba)
+            meta["best"] = bm
+        self.save(arrays, meta)
+
+    def load_cd(self):
+        got = self.load()
+        if got is None:
+            return None
+        arrays, meta = got
+        model = game_model_from_arrays(arrays, meta["model"], "model/")
+        best = game_model_from_arrays(arrays, meta["best"], "best/") if "best" in meta else None
+        return {"model": model, "iteration": meta["iteration"], "next": meta["next"], "best_model": best,
+                "best_evals": meta.get("best_evals"), "history": meta.get("history", []), "tag": meta.get("tag")}
