@@ -604,11 +604,26 @@ template <> struct TLVals<double> {
 template <typename VT> struct TLValT { typedef float T; };
 template <> struct TLValT<double> { typedef double T; };
 
+// block-wide sum of two doubles over NW waves; result valid in thread 0
+template <int NW>
+__device__ __forceinline__ void block_sum2_nw(double& a, double& b, double* sh /*[2*NW]*/) {
+  a = wave_sum(a);
+  b = wave_sum(b);
+  const int lane = threadIdx.x & 63, w = threadIdx.x >> 6;
+  __syncthreads();
+  if (lane == 0) { sh[2 * w] = a; sh[2 * w + 1] = b; }
+  __syncthreads();
+  if (threadIdx.x == 0) {
+    a = 0.0; b = 0.0;
+    for (int i = 0; i < NW; ++i) { a += sh[2 * i]; b += sh[2 * i + 1]; }
+  }
+}
+
 // Stream entries [e_lo, e_hi) of one work unit: wave w walks a contiguous share of the 4-aligned window.
 // For each entry: key = pack >> sbits (gather index), slot = pack & smask (LDS accumulator slot);
 // acc[slot] += val (or val^2) * x[key]. U wave-rounds per iteration: all stream loads first, then all gathers,
 // then the LDS accumulation (AT: float -> ds_add_f32, double -> ds_add_f64).
-template <typename VT, typename XT, typename AT, bool SQ, int U>
+template <typename VT, typename XT, typename AT, bool SQ, int U, int NW>
 __device__ __forceinline__ void tl_stream(const uint32_t* __restrict__ pack, const VT* __restrict__ val,
                                           const XT* __restrict__ x, int e_lo, int e_hi, int sbits, AT* acc) {
   typedef typename TLValT<VT>::T LT;
@@ -616,7 +631,7 @@ __device__ __forceinline__ void tl_stream(const uint32_t* __restrict__ pack, con
   const uint32_t smask = (1u << sbits) - 1u;
   const int lo = e_lo & ~(TL_VEC - 1);
   const int nr = (e_hi - lo + TL_ROUND - 1) / TL_ROUND;
-  const int r0 = (nr * w) / TL_WAVES, r1 = (nr * (w + 1)) / TL_WAVES;
+  const int r0 = (nr * w) / NW, r1 = (nr * (w + 1)) / NW;
   for (int r = r0; r < r1; r += U) {
     v4u pk[U];
     LT v[U][TL_VEC];
@@ -650,58 +665,58 @@ __device__ __forceinline__ void tl_stream(const uint32_t* __restrict__ pack, con
 }
 
 // Forward over row blocks. blk: 4 ints per block {row_lo, nrows, e_lo, e_hi} (chunk-local).
-template <typename VT, typename XT, typename RT, typename AT, int MAXR, int U>
-__global__ __launch_bounds__(NTHREADS) void tl_fwd_kernel(const int* __restrict__ blk, int rbits,
+template <typename VT, typename XT, typename RT, typename AT, int MAXR, int U, int NW>
+__global__ __launch_bounds__(NW * 64) void tl_fwd_kernel(const int* __restrict__ blk, int rbits,
                                                           const uint32_t* __restrict__ pack,
                                                           const VT* __restrict__ val, const XT* __restrict__ x,
                                                           FwdArgs<XT, RT> a, double* __restrict__ stats) {
-  __shared__ AT acc[TL_WAVES][MAXR];
-  __shared__ double red[2 * NTHREADS / 64];
+  __shared__ AT acc[NW][MAXR];
+  __shared__ double red[2 * NW];
   const int b = blockIdx.x;
   const int row_lo = blk[4 * b], nrows = blk[4 * b + 1], e_lo = blk[4 * b + 2], e_hi = blk[4 * b + 3];
   const int R = 1 << rbits;
-  for (int i = threadIdx.x; i < R; i += NTHREADS)
+  for (int i = threadIdx.x; i < R; i += NW * 64)
 #pragma unroll
-    for (int w = 0; w < TL_WAVES; ++w) acc[w][i] = AT(0);
+    for (int w = 0; w < NW; ++w) acc[w][i] = AT(0);
   __syncthreads();
-  tl_stream<VT, XT, AT, false, U>(pack, val, x, e_lo, e_hi, rbits, acc[threadIdx.x >> 6]);
+  tl_stream<VT, XT, AT, false, U, NW>(pack, val, x, e_lo, e_hi, rbits, acc[threadIdx.x >> 6]);
   __syncthreads();
   double F = 0.0, S = 0.0;
-  for (int r = threadIdx.x; r < nrows; r += NTHREADS) {
+  for (int r = threadIdx.x; r < nrows; r += NW * 64) {
     double z = static_cast<double>(acc[0][r]);
 #pragma unroll
-    for (int w = 1; w < TL_WAVES; ++w) z += static_cast<double>(acc[w][r]);
+    for (int w = 1; w < NW; ++w) z += static_cast<double>(acc[w][r]);
     const int s = row_lo + r;
     fwd_finish(a, s, z, fwd_prefetch(a, s), F, S);
   }
   if (stats) {
-    block_sum2(F, S, red);
+    block_sum2_nw<NW>(F, S, red);
     if (threadIdx.x == 0) { stats[2 * b] = F; stats[2 * b + 1] = S; }
   }
 }
 
 // Transpose over column-tile items. items: 4 ints {tile, e_lo, e_hi, part}; part < 0: the item is its tile's
 // only one -> G[tile cols] += sums directly; else the item's row of partial sums goes to parts[part * C ...].
-template <typename VT, typename XT, typename AT, bool SQ, int MAXR, int U>
-__global__ __launch_bounds__(NTHREADS) void tl_t_kernel(const int* __restrict__ items, int cbits,
+template <typename VT, typename XT, typename AT, bool SQ, int MAXR, int U, int NW>
+__global__ __launch_bounds__(NW * 64) void tl_t_kernel(const int* __restrict__ items, int cbits,
                                                         const uint32_t* __restrict__ pack,
                                                         const VT* __restrict__ val, const XT* __restrict__ x,
                                                         double* __restrict__ G, int dim, double* __restrict__ parts) {
-  __shared__ AT acc[TL_WAVES][MAXR];
+  __shared__ AT acc[NW][MAXR];
   const int it = blockIdx.x;
   const int tile = items[4 * it], e_lo = items[4 * it + 1], e_hi = items[4 * it + 2], part = items[4 * it + 3];
   const int C = 1 << cbits;
-  for (int i = threadIdx.x; i < C; i += NTHREADS)
+  for (int i = threadIdx.x; i < C; i += NW * 64)
 #pragma unroll
-    for (int w = 0; w < TL_WAVES; ++w) acc[w][i] = AT(0);
+    for (int w = 0; w < NW; ++w) acc[w][i] = AT(0);
   __syncthreads();
-  tl_stream<VT, XT, AT, SQ, U>(pack, val, x, e_lo, e_hi, cbits, acc[threadIdx.x >> 6]);
+  tl_stream<VT, XT, AT, SQ, U, NW>(pack, val, x, e_lo, e_hi, cbits, acc[threadIdx.x >> 6]);
   __syncthreads();
   const int c0 = tile << cbits;
-  for (int c = threadIdx.x; c < C; c += NTHREADS) {
+  for (int c = threadIdx.x; c < C; c += NW * 64) {
     double s = static_cast<double>(acc[0][c]);
 #pragma unroll
-    for (int w = 1; w < TL_WAVES; ++w) s += static_cast<double>(acc[w][c]);
+    for (int w = 1; w < NW; ++w) s += static_cast<double>(acc[w][c]);
     if (part < 0) {
       if (c0 + c < dim) G[c0 + c] += s;
     } else {
@@ -752,17 +767,18 @@ struct TLTDesc {
 };
 
 // Runtime TL configuration: accumulator precision for bf16/f32 data (0 = fp32 LDS, 1 = fp64 LDS) and the number
-// of wave-rounds in flight (2 or 4). fp64 data always accumulates in fp64.
+// of waves per work-group (2 or 4: each wave owns an LDS accumulator row, so fewer waves = less LDS per WG = more
+// resident WGs per CU). fp64 data always accumulates in fp64.
 static int g_tl_acc64 = 1;   // measured on MI355X: ds_add_f64 accumulation is ~3x faster than ds_add_f32 here
-static int g_tl_u = 2;
+static int g_tl_waves = 4;
 
 template <typename VT, typename XT, typename RT, typename AT, int MAXR>
 static void tl_fwd_launch(const TLFwdDesc* c, const void* x, FwdArgs<XT, RT> a, double* stats, hipStream_t st) {
-  if (g_tl_u >= 4)
-    hipLaunchKernelGGL((tl_fwd_kernel<VT, XT, RT, AT, MAXR, 4>), dim3(c->nblk), dim3(NTHREADS), 0, st, c->blk,
+  if (g_tl_waves == 2)
+    hipLaunchKernelGGL((tl_fwd_kernel<VT, XT, RT, AT, MAXR, 2, 2>), dim3(c->nblk), dim3(128), 0, st, c->blk,
                        c->rbits, c->pack, (const VT*)c->val, (const XT*)x, a, stats);
   else
-    hipLaunchKernelGGL((tl_fwd_kernel<VT, XT, RT, AT, MAXR, 2>), dim3(c->nblk), dim3(NTHREADS), 0, st, c->blk,
+    hipLaunchKernelGGL((tl_fwd_kernel<VT, XT, RT, AT, MAXR, 2, 4>), dim3(c->nblk), dim3(256), 0, st, c->blk,
                        c->rbits, c->pack, (const VT*)c->val, (const XT*)x, a, stats);
 }
 
@@ -788,11 +804,11 @@ static int tl_fwd_impl(const TLFwdDesc* c, const void* x, FwdArgs<XT, RT> a, dou
 
 template <typename VT, typename XT, typename AT, bool SQ, int MAXR>
 static void tl_t_launch(const TLTDesc* c, const void* x, double* G, double* parts, hipStream_t st) {
-  if (g_tl_u >= 4)
-    hipLaunchKernelGGL((tl_t_kernel<VT, XT, AT, SQ, MAXR, 4>), dim3(c->nitems), dim3(NTHREADS), 0, st, c->items,
+  if (g_tl_waves == 2)
+    hipLaunchKernelGGL((tl_t_kernel<VT, XT, AT, SQ, MAXR, 2, 2>), dim3(c->nitems), dim3(128), 0, st, c->items,
                        c->cbits, c->pack, (const VT*)c->val, (const XT*)x, G, c->dim, parts);
   else
-    hipLaunchKernelGGL((tl_t_kernel<VT, XT, AT, SQ, MAXR, 2>), dim3(c->nitems), dim3(NTHREADS), 0, st, c->items,
+    hipLaunchKernelGGL((tl_t_kernel<VT, XT, AT, SQ, MAXR, 2, 4>), dim3(c->nitems), dim3(256), 0, st, c->items,
                        c->cbits, c->pack, (const VT*)c->val, (const XT*)x, G, c->dim, parts);
 }
 
@@ -824,7 +840,6 @@ static int tl_t_impl(const TLTDesc* c, const void* x, double* G, double* parts, 
   }
   return 0;
 }
-
 
 // ============================================================================================================
 // Segmented dot products for the block-diagonal random-effect solver: out[s] = sum_{i in [ptr[s], ptr[s+1])} f(a_i,
@@ -1033,7 +1048,7 @@ int pml_reduce_stats(const double* stats, int n, double* out, int accumulate, do
 
 // ---- tiled layout entry points ------------------------------------------------------------------------------
 int pml_tl_maxbits() { return TL_MAXBITS; }
-void pml_tl_config(int acc64, int u) { g_tl_acc64 = acc64; g_tl_u = u; }
+void pml_tl_config(int acc64, int waves) { g_tl_acc64 = acc64; g_tl_waves = waves == 2 ? 2 : 4; }
 
 int pml_tl_fwd(int prec, const TLFwdDesc* c, const void* x, int mode, int loss, double shift, const void* y,
                const void* off, const void* wt, void* coef, void* dzz, double* z_out, int with_offset,

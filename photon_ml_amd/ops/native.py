@@ -91,7 +91,7 @@ def glm_lib() -> Optional[ctypes.CDLL]:
 # Kernel configuration defaults (tuned on MI355X, see profiles/): forward = vector layout + 8192-entry LDS hot
 # table of the most frequent features; transpose = strided layout. Env overrides for experiments:
 # PML_FWD_STRIDED, PML_T_STRIDED, PML_HOT_N, PML_FWD_GRID.
-KERNEL_CONFIG = {"fwd_strided": 0, "t_strided": 0, "hot_n": 0, "fwd_grid": 1024, "tl_acc64": 1, "tl_u": 2}
+KERNEL_CONFIG = {"fwd_strided": 0, "t_strided": 0, "hot_n": 0, "fwd_grid": 1024, "tl_acc64": 1, "tl_waves": 4}
 
 
 def configure(**kw):
@@ -104,7 +104,7 @@ def configure(**kw):
     if lib is not None:
         lib.pml_set_config(KERNEL_CONFIG["fwd_strided"], KERNEL_CONFIG["t_strided"], KERNEL_CONFIG["hot_n"],
                            KERNEL_CONFIG["fwd_grid"])
-        lib.pml_tl_config(KERNEL_CONFIG["tl_acc64"], KERNEL_CONFIG["tl_u"])
+        lib.pml_tl_config(KERNEL_CONFIG["tl_acc64"], KERNEL_CONFIG["tl_waves"])
     return dict(KERNEL_CONFIG)
 
 
