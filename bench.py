@@ -52,6 +52,7 @@ def main():
     rank, world, local = init_distributed()
     if world != args.gpus:
         log(f"warning: --gpus {args.gpus} but WORLD_SIZE={world}; using WORLD_SIZE")
+    local = local % max(torch.cuda.device_count(), 1)  # several ranks may share a GPU in rehearsal runs
     torch.cuda.set_device(local)
     dev = torch.device("cuda", local)
 

@@ -52,6 +52,7 @@ def main():
     from photon_ml_amd.parallel.dist import init_distributed, all_reduce_scalar, barrier
     rank, world, local = init_distributed()
     if torch.cuda.is_available():
+        local = local % torch.cuda.device_count()  # several ranks may share a GPU in rehearsal runs
         torch.cuda.set_device(local)
         dev = torch.device("cuda", local)
     else:

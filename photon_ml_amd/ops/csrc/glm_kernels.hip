@@ -580,26 +580,32 @@ __global__ __launch_bounds__(NTHREADS) void reduce_stats_l1_kernel(const double*
 #define TL_WAVES (NTHREADS / 64)
 #define TL_MAXBITS 12                         // up to 4096 rows per forward block / columns per transpose tile
 
+// Value quads: ``Raw`` is what one 4-entry load returns (kept as loaded so a prefetch does not force a wait),
+// ``get`` converts to the arithmetic type at use.
 template <typename VT> struct TLVals;
 template <> struct TLVals<uint16_t> {
-  static __device__ __forceinline__ void load(const uint16_t* p, float* v) {
-    const v2u u = __builtin_nontemporal_load((const v2u*)p);
+  typedef v2u Raw;
+  static __device__ __forceinline__ Raw load(const uint16_t* p) { return __builtin_nontemporal_load((const v2u*)p); }
+  static __device__ __forceinline__ void get(const Raw& u, float* v) {
     v[0] = __uint_as_float(u.x << 16); v[1] = __uint_as_float(u.x & 0xffff0000u);
     v[2] = __uint_as_float(u.y << 16); v[3] = __uint_as_float(u.y & 0xffff0000u);
   }
 };
 template <> struct TLVals<float> {
-  static __device__ __forceinline__ void load(const float* p, float* v) {
-    const v4f a = __builtin_nontemporal_load((const v4f*)p);
-    v[0] = a[0]; v[1] = a[1]; v[2] = a[2]; v[3] = a[3];
-  }
+  typedef v4f Raw;
+  static __device__ __forceinline__ Raw load(const float* p) { return __builtin_nontemporal_load((const v4f*)p); }
+  static __device__ __forceinline__ void get(const Raw& a, float* v) { v[0] = a[0]; v[1] = a[1]; v[2] = a[2]; v[3] = a[3]; }
 };
+struct d4 { v2d a, b; };
 template <> struct TLVals<double> {
-  static __device__ __forceinline__ void load(const double* p, double* v) {
-    const v2d a = __builtin_nontemporal_load((const v2d*)p);
-    const v2d b = __builtin_nontemporal_load((const v2d*)(p + 2));
-    v[0] = a[0]; v[1] = a[1]; v[2] = b[0]; v[3] = b[1];
+  typedef d4 Raw;
+  static __device__ __forceinline__ Raw load(const double* p) {
+    d4 r;
+    r.a = __builtin_nontemporal_load((const v2d*)p);
+    r.b = __builtin_nontemporal_load((const v2d*)(p + 2));
+    return r;
   }
+  static __device__ __forceinline__ void get(const Raw& r, double* v) { v[0] = r.a[0]; v[1] = r.a[1]; v[2] = r.b[0]; v[3] = r.b[1]; }
 };
 template <typename VT> struct TLValT { typedef float T; };
 template <> struct TLValT<double> { typedef double T; };
@@ -626,41 +632,54 @@ __device__ __forceinline__ void block_sum2_nw(double& a, double& b, double* sh /
 template <typename VT, typename XT, typename AT, bool SQ, int U, int NW>
 __device__ __forceinline__ void tl_stream(const uint32_t* __restrict__ pack, const VT* __restrict__ val,
                                           const XT* __restrict__ x, int e_lo, int e_hi, int sbits, AT* acc) {
+  // Software-pipelined: the stream loads (pack + value quads) of round r + 1 are issued before the gathers and
+  // LDS accumulation of round r, so the HBM latency of the stream overlaps with the gather latency.
   typedef typename TLValT<VT>::T LT;
   const int lane = threadIdx.x & 63, w = threadIdx.x >> 6;
   const uint32_t smask = (1u << sbits) - 1u;
   const int lo = e_lo & ~(TL_VEC - 1);
   const int nr = (e_hi - lo + TL_ROUND - 1) / TL_ROUND;
   const int r0 = (nr * w) / NW, r1 = (nr * (w + 1)) / NW;
-  for (int r = r0; r < r1; r += U) {
-    v4u pk[U];
-    LT v[U][TL_VEC];
-    bool in[U][TL_VEC];
+  if (r0 >= r1) return;
+  typedef typename TLVals<VT>::Raw Raw;
+  // two prefetch slots (A: even rounds, B: odd rounds); the loop is unrolled by two so the slots stay in
+  // registers (no dynamic indexing -> no scratch)
+  v4u pkA, pkB;
+  Raw vA, vB;
+  auto load_round = [&](int r, v4u& pk, Raw& v) {
+    const int e = lo + r * TL_ROUND + lane * TL_VEC;
+    const int es = (r < r1 && e < e_hi) ? e : lo;  // out-of-range lanes re-read a valid quad; masked below
+    pk = __builtin_nontemporal_load((const v4u*)(pack + es));
+    v = TLVals<VT>::load(val + es);
+  };
+  auto process = [&](int r, v4u& pk_slot, Raw& v_slot) {
+    const v4u pk = pk_slot;
+    const Raw v_raw = v_slot;
+    const int e = lo + r * TL_ROUND + lane * TL_VEC;
+    bool in[TL_VEC];
+    XT xv[TL_VEC];
 #pragma unroll
-    for (int u = 0; u < U; ++u) {
-      const int e = lo + (r + u) * TL_ROUND + lane * TL_VEC;
-      const bool ok = (r + u < r1) && (e < e_hi);
-      const int es = ok ? e : lo;  // out-of-range lanes re-read the first (valid) quad; results are masked
-      pk[u] = __builtin_nontemporal_load((const v4u*)(pack + es));
-      TLVals<VT>::load(val + es, v[u]);
-#pragma unroll
-      for (int k = 0; k < TL_VEC; ++k) in[u][k] = ok && (e + k >= e_lo) && (e + k < e_hi);
+    for (int k = 0; k < TL_VEC; ++k) {
+      in[k] = (e + k >= e_lo) && (e + k < e_hi);
+      xv[k] = x[in[k] ? (pk[k] >> sbits) : 0u];  // unconditional: all four gathers in flight together
     }
-    // unconditional gathers (masked lanes read x[0]) so that all of them are in flight together
-    XT xv[U][TL_VEC];
+    // refill this slot with round r + 2 AFTER issuing the gathers (vmcnt retires in issue order)
+    if (r + 2 < r1) load_round(r + 2, pk_slot, v_slot);
+    LT v[TL_VEC];
+    TLVals<VT>::get(v_raw, v);
 #pragma unroll
-    for (int u = 0; u < U; ++u)
-#pragma unroll
-      for (int k = 0; k < TL_VEC; ++k) xv[u][k] = x[in[u][k] ? (pk[u][k] >> sbits) : 0u];
-#pragma unroll
-    for (int u = 0; u < U; ++u)
-#pragma unroll
-      for (int k = 0; k < TL_VEC; ++k) {
-        if (in[u][k]) {
-          const AT vv = SQ ? static_cast<AT>(v[u][k]) * static_cast<AT>(v[u][k]) : static_cast<AT>(v[u][k]);
-          atomicAdd(&acc[pk[u][k] & smask], vv * static_cast<AT>(xv[u][k]));
-        }
+    for (int k = 0; k < TL_VEC; ++k) {
+      if (in[k]) {
+        const AT vv = SQ ? static_cast<AT>(v[k]) * static_cast<AT>(v[k]) : static_cast<AT>(v[k]);
+        atomicAdd(&acc[pk[k] & smask], vv * static_cast<AT>(xv[k]));
       }
+    }
+  };
+  load_round(r0, pkA, vA);
+  if (r0 + 1 < r1) load_round(r0 + 1, pkB, vB);
+  for (int r = r0; r < r1; r += 2) {
+    process(r, pkA, vA);
+    if (r + 1 < r1) process(r + 1, pkB, vB);
   }
 }
 
@@ -770,7 +789,8 @@ struct TLTDesc {
 // of waves per work-group (2 or 4: each wave owns an LDS accumulator row, so fewer waves = less LDS per WG = more
 // resident WGs per CU). fp64 data always accumulates in fp64.
 static int g_tl_acc64 = 1;   // measured on MI355X: ds_add_f64 accumulation is ~3x faster than ds_add_f32 here
-static int g_tl_waves = 4;
+static int g_tl_waves = 4;     // forward
+static int g_tl_waves_t = 4;   // transpose
 
 template <typename VT, typename XT, typename RT, typename AT, int MAXR>
 static void tl_fwd_launch(const TLFwdDesc* c, const void* x, FwdArgs<XT, RT> a, double* stats, hipStream_t st) {
@@ -804,7 +824,7 @@ static int tl_fwd_impl(const TLFwdDesc* c, const void* x, FwdArgs<XT, RT> a, dou
 
 template <typename VT, typename XT, typename AT, bool SQ, int MAXR>
 static void tl_t_launch(const TLTDesc* c, const void* x, double* G, double* parts, hipStream_t st) {
-  if (g_tl_waves == 2)
+  if (g_tl_waves_t == 2)
     hipLaunchKernelGGL((tl_t_kernel<VT, XT, AT, SQ, MAXR, 2, 2>), dim3(c->nitems), dim3(128), 0, st, c->items,
                        c->cbits, c->pack, (const VT*)c->val, (const XT*)x, G, c->dim, parts);
   else
@@ -1048,7 +1068,9 @@ int pml_reduce_stats(const double* stats, int n, double* out, int accumulate, do
 
 // ---- tiled layout entry points ------------------------------------------------------------------------------
 int pml_tl_maxbits() { return TL_MAXBITS; }
-void pml_tl_config(int acc64, int waves) { g_tl_acc64 = acc64; g_tl_waves = waves == 2 ? 2 : 4; }
+void pml_tl_config(int acc64, int waves, int waves_t) {
+  g_tl_acc64 = acc64; g_tl_waves = waves == 2 ? 2 : 4; g_tl_waves_t = waves_t == 4 ? 4 : 2;
+}
 
 int pml_tl_fwd(int prec, const TLFwdDesc* c, const void* x, int mode, int loss, double shift, const void* y,
                const void* off, const void* wt, void* coef, void* dzz, double* z_out, int with_offset,

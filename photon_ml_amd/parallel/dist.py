@@ -34,9 +34,9 @@ def init_distributed(backend: Optional[str] = None, timeout_s: int = 1800) -> tu
         os.environ.setdefault("MASTER_ADDR", "127.0.0.1")
         os.environ.setdefault("MASTER_PORT", "29500")
         if backend is None:
-            backend = "nccl" if torch.cuda.is_available() else "gloo"
+            backend = os.environ.get("PML_DIST_BACKEND") or ("nccl" if torch.cuda.is_available() else "gloo")
         if backend == "nccl":
-            torch.cuda.set_device(local)
+            torch.cuda.set_device(local % torch.cuda.device_count())
         dist.init_process_group(backend=backend, timeout=datetime.timedelta(seconds=timeout_s))
     return rank, world, local
 
