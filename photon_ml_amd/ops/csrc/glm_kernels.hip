@@ -631,7 +631,10 @@ __device__ __forceinline__ void block_sum2_nw(double& a, double& b, double* sh /
 // then the LDS accumulation (AT: float -> ds_add_f32, double -> ds_add_f64).
 template <typename VT, typename XT, typename AT, bool SQ, int U, int NW>
 __device__ __forceinline__ void tl_stream(const uint32_t* __restrict__ pack, const VT* __restrict__ val,
-                                          const XT* __restrict__ x, int e_lo, int e_hi, int sbits, AT* acc) {
+                                          const XT* __restrict__ x, int e_lo, int e_hi, int sbits, AT* acc,
+                                          int abl = 0) {
+  // abl (profiling builds only, 0 in production): 1 = gathers from a 1 KB window (L1-resident),
+  // 2 = no LDS accumulation (products summed in a register), 4 = gathers skipped (x = 1)
   // Software-pipelined: the stream loads (pack + value quads) of round r + 1 are issued before the gathers and
   // LDS accumulation of round r, so the HBM latency of the stream overlaps with the gather latency.
   typedef typename TLValT<VT>::T LT;
@@ -642,6 +645,7 @@ __device__ __forceinline__ void tl_stream(const uint32_t* __restrict__ pack, con
   const int r0 = (nr * w) / NW, r1 = (nr * (w + 1)) / NW;
   if (r0 >= r1) return;
   typedef typename TLVals<VT>::Raw Raw;
+  AT regacc = AT(0);
   // two prefetch slots (A: even rounds, B: odd rounds); the loop is unrolled by two so the slots stay in
   // registers (no dynamic indexing -> no scratch)
   v4u pkA, pkB;
@@ -661,7 +665,9 @@ __device__ __forceinline__ void tl_stream(const uint32_t* __restrict__ pack, con
 #pragma unroll
     for (int k = 0; k < TL_VEC; ++k) {
       in[k] = (e + k >= e_lo) && (e + k < e_hi);
-      xv[k] = x[in[k] ? (pk[k] >> sbits) : 0u];  // unconditional: all four gathers in flight together
+      uint32_t gi = in[k] ? (pk[k] >> sbits) : 0u;
+      if (abl & 1) gi &= 255u;
+      xv[k] = (abl & 4) ? XT(1) : x[gi];  // unconditional: all four gathers in flight together
     }
     // refill this slot with round r + 2 AFTER issuing the gathers (vmcnt retires in issue order)
     if (r + 2 < r1) load_round(r + 2, pk_slot, v_slot);
@@ -671,7 +677,8 @@ __device__ __forceinline__ void tl_stream(const uint32_t* __restrict__ pack, con
     for (int k = 0; k < TL_VEC; ++k) {
       if (in[k]) {
         const AT vv = SQ ? static_cast<AT>(v[k]) * static_cast<AT>(v[k]) : static_cast<AT>(v[k]);
-        atomicAdd(&acc[pk[k] & smask], vv * static_cast<AT>(xv[k]));
+        if (abl & 2) regacc += vv * static_cast<AT>(xv[k]);
+        else atomicAdd(&acc[pk[k] & smask], vv * static_cast<AT>(xv[k]));
       }
     }
   };
@@ -681,6 +688,7 @@ __device__ __forceinline__ void tl_stream(const uint32_t* __restrict__ pack, con
     process(r, pkA, vA);
     if (r + 1 < r1) process(r + 1, pkB, vB);
   }
+  if (abl & 2) atomicAdd(&acc[lane], regacc);  // keep the ablated work observable
 }
 
 // Forward over row blocks. blk: 4 ints per block {row_lo, nrows, e_lo, e_hi} (chunk-local).
@@ -698,7 +706,7 @@ __global__ __launch_bounds__(NW * 64) void tl_fwd_kernel(const int* __restrict__
 #pragma unroll
     for (int w = 0; w < NW; ++w) acc[w][i] = AT(0);
   __syncthreads();
-  tl_stream<VT, XT, AT, false, U, NW>(pack, val, x, e_lo, e_hi, rbits, acc[threadIdx.x >> 6]);
+  tl_stream<VT, XT, AT, false, U, NW>(pack, val, x, e_lo, e_hi, rbits, acc[threadIdx.x >> 6], a.abl);
   __syncthreads();
   double F = 0.0, S = 0.0;
   for (int r = threadIdx.x; r < nrows; r += NW * 64) {
@@ -720,7 +728,8 @@ template <typename VT, typename XT, typename AT, bool SQ, int MAXR, int U, int N
 __global__ __launch_bounds__(NW * 64) void tl_t_kernel(const int* __restrict__ items, int cbits,
                                                         const uint32_t* __restrict__ pack,
                                                         const VT* __restrict__ val, const XT* __restrict__ x,
-                                                        double* __restrict__ G, int dim, double* __restrict__ parts) {
+                                                        double* __restrict__ G, int dim, double* __restrict__ parts,
+                                                        int abl) {
   __shared__ AT acc[NW][MAXR];
   const int it = blockIdx.x;
   const int tile = items[4 * it], e_lo = items[4 * it + 1], e_hi = items[4 * it + 2], part = items[4 * it + 3];
@@ -729,7 +738,7 @@ __global__ __launch_bounds__(NW * 64) void tl_t_kernel(const int* __restrict__ i
 #pragma unroll
     for (int w = 0; w < NW; ++w) acc[w][i] = AT(0);
   __syncthreads();
-  tl_stream<VT, XT, AT, SQ, U, NW>(pack, val, x, e_lo, e_hi, cbits, acc[threadIdx.x >> 6]);
+  tl_stream<VT, XT, AT, SQ, U, NW>(pack, val, x, e_lo, e_hi, cbits, acc[threadIdx.x >> 6], abl);
   __syncthreads();
   const int c0 = tile << cbits;
   for (int c = threadIdx.x; c < C; c += NW * 64) {
@@ -788,6 +797,7 @@ struct TLTDesc {
 // Runtime TL configuration: accumulator precision for bf16/f32 data (0 = fp32 LDS, 1 = fp64 LDS) and the number
 // of waves per work-group (2 or 4: each wave owns an LDS accumulator row, so fewer waves = less LDS per WG = more
 // resident WGs per CU). fp64 data always accumulates in fp64.
+static int g_ablate = 0;      // profiling ablation bits (0 in production)
 static int g_tl_acc64 = 1;   // measured on MI355X: ds_add_f64 accumulation is ~3x faster than ds_add_f32 here
 static int g_tl_waves = 4;     // forward
 static int g_tl_waves_t = 4;   // transpose
@@ -826,10 +836,10 @@ template <typename VT, typename XT, typename AT, bool SQ, int MAXR>
 static void tl_t_launch(const TLTDesc* c, const void* x, double* G, double* parts, hipStream_t st) {
   if (g_tl_waves_t == 2)
     hipLaunchKernelGGL((tl_t_kernel<VT, XT, AT, SQ, MAXR, 2, 2>), dim3(c->nitems), dim3(128), 0, st, c->items,
-                       c->cbits, c->pack, (const VT*)c->val, (const XT*)x, G, c->dim, parts);
+                       c->cbits, c->pack, (const VT*)c->val, (const XT*)x, G, c->dim, parts, g_ablate);
   else
     hipLaunchKernelGGL((tl_t_kernel<VT, XT, AT, SQ, MAXR, 2, 4>), dim3(c->nitems), dim3(256), 0, st, c->items,
-                       c->cbits, c->pack, (const VT*)c->val, (const XT*)x, G, c->dim, parts);
+                       c->cbits, c->pack, (const VT*)c->val, (const XT*)x, G, c->dim, parts, g_ablate);
 }
 
 template <typename VT, typename XT, bool SQ>
@@ -894,7 +904,6 @@ struct SegChunkDesc {
 };
 
 
-static int g_ablate = 0;
 // Runtime kernel configuration (set from Python): lane layout per direction, hot-table size, persistent grid.
 static int g_fwd_strided = 0;
 static int g_t_strided = 1;
@@ -1078,11 +1087,11 @@ int pml_tl_fwd(int prec, const TLFwdDesc* c, const void* x, int mode, int loss, 
   hipStream_t st = (hipStream_t)stream;
   if (prec == 2) {
     FwdArgs<double, double> a{mode, loss, shift, (const double*)y, (const double*)off, (const double*)wt,
-                              (double*)coef, (double*)dzz, z_out, with_offset, 0, 0};
+                              (double*)coef, (double*)dzz, z_out, with_offset, g_ablate, 0};
     return tl_fwd_impl<double, double, double>(c, x, a, stats, st);
   }
   FwdArgs<float, float> a{mode, loss, shift, (const float*)y, (const float*)off, (const float*)wt,
-                          (float*)coef, (float*)dzz, z_out, with_offset, 0, 0};
+                          (float*)coef, (float*)dzz, z_out, with_offset, g_ablate, 0};
   if (prec == 1) return tl_fwd_impl<float, float, float>(c, x, a, stats, st);
   return tl_fwd_impl<uint16_t, float, float>(c, x, a, stats, st);
 }
