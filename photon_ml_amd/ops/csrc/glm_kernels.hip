@@ -630,11 +630,8 @@ __device__ __forceinline__ void block_sum2_nw(double& a, double& b, double* sh /
 // acc[slot] += val (or val^2) * x[key]. U wave-rounds per iteration: all stream loads first, then all gathers,
 // then the LDS accumulation (AT: float -> ds_add_f32, double -> ds_add_f64).
 template <typename VT, typename XT, typename AT, bool SQ, int U, int NW>
-__device__ __forceinline__ void tl_stream(const uint32_t* __restrict__ pack, const VT* __restrict__ val,
-                                          const XT* __restrict__ x, int e_lo, int e_hi, int sbits, AT* acc,
-                                          int abl = 0) {
-  // abl (profiling builds only, 0 in production): 1 = gathers from a 1 KB window (L1-resident),
-  // 2 = no LDS accumulation (products summed in a register), 4 = gathers skipped (x = 1)
+__device__ __forceinline__ void tl_stream_p0(const uint32_t* __restrict__ pack, const VT* __restrict__ val,
+                                          const XT* __restrict__ x, int e_lo, int e_hi, int sbits, AT* acc) {
   // Software-pipelined: the stream loads (pack + value quads) of round r + 1 are issued before the gathers and
   // LDS accumulation of round r, so the HBM latency of the stream overlaps with the gather latency.
   typedef typename TLValT<VT>::T LT;
@@ -645,7 +642,6 @@ __device__ __forceinline__ void tl_stream(const uint32_t* __restrict__ pack, con
   const int r0 = (nr * w) / NW, r1 = (nr * (w + 1)) / NW;
   if (r0 >= r1) return;
   typedef typename TLVals<VT>::Raw Raw;
-  AT regacc = AT(0);
   // two prefetch slots (A: even rounds, B: odd rounds); the loop is unrolled by two so the slots stay in
   // registers (no dynamic indexing -> no scratch)
   v4u pkA, pkB;
@@ -665,9 +661,7 @@ __device__ __forceinline__ void tl_stream(const uint32_t* __restrict__ pack, con
 #pragma unroll
     for (int k = 0; k < TL_VEC; ++k) {
       in[k] = (e + k >= e_lo) && (e + k < e_hi);
-      uint32_t gi = in[k] ? (pk[k] >> sbits) : 0u;
-      if (abl & 1) gi &= 255u;
-      xv[k] = (abl & 4) ? XT(1) : x[gi];  // unconditional: all four gathers in flight together
+      xv[k] = x[in[k] ? (pk[k] >> sbits) : 0u];  // unconditional: all four gathers in flight together
     }
     // refill this slot with round r + 2 AFTER issuing the gathers (vmcnt retires in issue order)
     if (r + 2 < r1) load_round(r + 2, pk_slot, v_slot);
@@ -677,8 +671,7 @@ __device__ __forceinline__ void tl_stream(const uint32_t* __restrict__ pack, con
     for (int k = 0; k < TL_VEC; ++k) {
       if (in[k]) {
         const AT vv = SQ ? static_cast<AT>(v[k]) * static_cast<AT>(v[k]) : static_cast<AT>(v[k]);
-        if (abl & 2) regacc += vv * static_cast<AT>(xv[k]);
-        else atomicAdd(&acc[pk[k] & smask], vv * static_cast<AT>(xv[k]));
+        atomicAdd(&acc[pk[k] & smask], vv * static_cast<AT>(xv[k]));
       }
     }
   };
@@ -688,11 +681,96 @@ __device__ __forceinline__ void tl_stream(const uint32_t* __restrict__ pack, con
     process(r, pkA, vA);
     if (r + 1 < r1) process(r + 1, pkB, vB);
   }
-  if (abl & 2) atomicAdd(&acc[lane], regacc);  // keep the ablated work observable
+}
+
+template <typename VT, typename XT, typename AT, bool SQ, int U, int NW>
+__device__ __forceinline__ void tl_stream_p1(const uint32_t* __restrict__ pack, const VT* __restrict__ val,
+                                          const XT* __restrict__ x, int e_lo, int e_hi, int sbits, AT* acc) {
+  // Three-stage software pipeline per wave (measured: removing the gathers halves the kernel time while
+  // removing the LDS accumulation changes nothing, so the dependent stream-load -> gather -> accumulate chain
+  // is latency bound):
+  //   iteration r: issue gathers for round r+1 (its pack quad arrived one iteration ago), issue the stream loads
+  //   of round r+2, then accumulate round r (its gathers were issued one iteration ago).
+  // vmcnt retires in issue order, so the accumulation waits only for the gathers of round r while the six newer
+  // loads stay in flight. Unrolled by two so the rotating slots stay in registers.
+  typedef typename TLValT<VT>::T LT;
+  typedef typename TLVals<VT>::Raw Raw;
+  const int lane = threadIdx.x & 63, w = threadIdx.x >> 6;
+  const uint32_t smask = (1u << sbits) - 1u;
+  const int lo = e_lo & ~(TL_VEC - 1);
+  const int nr = (e_hi - lo + TL_ROUND - 1) / TL_ROUND;
+  const int r0 = (nr * w) / NW, r1 = (nr * (w + 1)) / NW;
+  if (r0 >= r1) return;
+  auto load_round = [&](int r, v4u& pk, Raw& v) {
+    const int e = lo + r * TL_ROUND + lane * TL_VEC;
+    const int es = (r < r1 && e < e_hi) ? e : lo;  // out-of-range lanes re-read a valid quad; masked below
+    pk = __builtin_nontemporal_load((const v4u*)(pack + es));
+    v = TLVals<VT>::load(val + es);
+  };
+  auto gather = [&](int r, const v4u& pk, XT* xv) {
+    const int e = lo + r * TL_ROUND + lane * TL_VEC;
+#pragma unroll
+    for (int k = 0; k < TL_VEC; ++k) {
+      const bool in = (r < r1) && (e + k >= e_lo) && (e + k < e_hi);
+      xv[k] = x[in ? (pk[k] >> sbits) : 0u];
+    }
+  };
+  auto accumulate = [&](int r, const v4u& pk, const Raw& v_raw, const XT* xv) {
+    const int e = lo + r * TL_ROUND + lane * TL_VEC;
+    LT v[TL_VEC];
+    TLVals<VT>::get(v_raw, v);
+#pragma unroll
+    for (int k = 0; k < TL_VEC; ++k) {
+      if ((e + k >= e_lo) && (e + k < e_hi)) {
+        const AT vv = SQ ? static_cast<AT>(v[k]) * static_cast<AT>(v[k]) : static_cast<AT>(v[k]);
+        atomicAdd(&acc[pk[k] & smask], vv * static_cast<AT>(xv[k]));
+      }
+    }
+  };
+  // slots: A holds even rounds, B odd rounds
+  v4u pkA, pkB;
+  Raw vA, vB;
+  XT xA[TL_VEC], xB[TL_VEC];
+  load_round(r0, pkA, vA);
+  load_round(r0 + 1, pkB, vB);
+  gather(r0, pkA, xA);
+  for (int r = r0; r < r1; r += 2) {
+    // round r (slot A) accumulates; round r+1 (slot B) gathers; round r+2 streams into slot A
+    gather(r + 1, pkB, xB);
+    {
+      const v4u pk = pkA;
+      const Raw vv = vA;
+      XT xc[TL_VEC];
+#pragma unroll
+      for (int k = 0; k < TL_VEC; ++k) xc[k] = xA[k];
+      load_round(r + 2, pkA, vA);
+      accumulate(r, pk, vv, xc);
+    }
+    if (r + 1 >= r1) break;
+    // round r+1 (slot B) accumulates; round r+2 (slot A) gathers; round r+3 streams into slot B
+    gather(r + 2, pkA, xA);
+    {
+      const v4u pk = pkB;
+      const Raw vv = vB;
+      XT xc[TL_VEC];
+#pragma unroll
+      for (int k = 0; k < TL_VEC; ++k) xc[k] = xB[k];
+      load_round(r + 3, pkB, vB);
+      accumulate(r + 1, pk, vv, xc);
+    }
+  }
+}
+
+// pipeline variant: P = 0 two-slot stream prefetch; P = 1 three-stage (stream r+2 / gather r+1 / accumulate r)
+template <typename VT, typename XT, typename AT, bool SQ, int U, int NW, int P>
+__device__ __forceinline__ void tl_stream(const uint32_t* __restrict__ pack, const VT* __restrict__ val,
+                                          const XT* __restrict__ x, int e_lo, int e_hi, int sbits, AT* acc) {
+  if (P == 1) tl_stream_p1<VT, XT, AT, SQ, U, NW>(pack, val, x, e_lo, e_hi, sbits, acc);
+  else tl_stream_p0<VT, XT, AT, SQ, U, NW>(pack, val, x, e_lo, e_hi, sbits, acc);
 }
 
 // Forward over row blocks. blk: 4 ints per block {row_lo, nrows, e_lo, e_hi} (chunk-local).
-template <typename VT, typename XT, typename RT, typename AT, int MAXR, int U, int NW>
+template <typename VT, typename XT, typename RT, typename AT, int MAXR, int U, int NW, int P>
 __global__ __launch_bounds__(NW * 64) void tl_fwd_kernel(const int* __restrict__ blk, int rbits,
                                                           const uint32_t* __restrict__ pack,
                                                           const VT* __restrict__ val, const XT* __restrict__ x,
@@ -706,7 +784,7 @@ __global__ __launch_bounds__(NW * 64) void tl_fwd_kernel(const int* __restrict__
 #pragma unroll
     for (int w = 0; w < NW; ++w) acc[w][i] = AT(0);
   __syncthreads();
-  tl_stream<VT, XT, AT, false, U, NW>(pack, val, x, e_lo, e_hi, rbits, acc[threadIdx.x >> 6], a.abl);
+  tl_stream<VT, XT, AT, false, U, NW, P>(pack, val, x, e_lo, e_hi, rbits, acc[threadIdx.x >> 6]);
   __syncthreads();
   double F = 0.0, S = 0.0;
   for (int r = threadIdx.x; r < nrows; r += NW * 64) {
@@ -724,12 +802,11 @@ __global__ __launch_bounds__(NW * 64) void tl_fwd_kernel(const int* __restrict__
 
 // Transpose over column-tile items. items: 4 ints {tile, e_lo, e_hi, part}; part < 0: the item is its tile's
 // only one -> G[tile cols] += sums directly; else the item's row of partial sums goes to parts[part * C ...].
-template <typename VT, typename XT, typename AT, bool SQ, int MAXR, int U, int NW>
+template <typename VT, typename XT, typename AT, bool SQ, int MAXR, int U, int NW, int P>
 __global__ __launch_bounds__(NW * 64) void tl_t_kernel(const int* __restrict__ items, int cbits,
                                                         const uint32_t* __restrict__ pack,
                                                         const VT* __restrict__ val, const XT* __restrict__ x,
-                                                        double* __restrict__ G, int dim, double* __restrict__ parts,
-                                                        int abl) {
+                                                        double* __restrict__ G, int dim, double* __restrict__ parts) {
   __shared__ AT acc[NW][MAXR];
   const int it = blockIdx.x;
   const int tile = items[4 * it], e_lo = items[4 * it + 1], e_hi = items[4 * it + 2], part = items[4 * it + 3];
@@ -738,7 +815,7 @@ __global__ __launch_bounds__(NW * 64) void tl_t_kernel(const int* __restrict__ i
 #pragma unroll
     for (int w = 0; w < NW; ++w) acc[w][i] = AT(0);
   __syncthreads();
-  tl_stream<VT, XT, AT, SQ, U, NW>(pack, val, x, e_lo, e_hi, cbits, acc[threadIdx.x >> 6], abl);
+  tl_stream<VT, XT, AT, SQ, U, NW, P>(pack, val, x, e_lo, e_hi, cbits, acc[threadIdx.x >> 6]);
   __syncthreads();
   const int c0 = tile << cbits;
   for (int c = threadIdx.x; c < C; c += NW * 64) {
@@ -801,15 +878,15 @@ static int g_ablate = 0;      // profiling ablation bits (0 in production)
 static int g_tl_acc64 = 1;   // measured on MI355X: ds_add_f64 accumulation is ~3x faster than ds_add_f32 here
 static int g_tl_waves = 4;     // forward
 static int g_tl_waves_t = 4;   // transpose
+static int g_tl_pipe = 0;      // stream pipeline variant (see tl_stream)
 
 template <typename VT, typename XT, typename RT, typename AT, int MAXR>
 static void tl_fwd_launch(const TLFwdDesc* c, const void* x, FwdArgs<XT, RT> a, double* stats, hipStream_t st) {
-  if (g_tl_waves == 2)
-    hipLaunchKernelGGL((tl_fwd_kernel<VT, XT, RT, AT, MAXR, 2, 2>), dim3(c->nblk), dim3(128), 0, st, c->blk,
-                       c->rbits, c->pack, (const VT*)c->val, (const XT*)x, a, stats);
-  else
-    hipLaunchKernelGGL((tl_fwd_kernel<VT, XT, RT, AT, MAXR, 2, 4>), dim3(c->nblk), dim3(256), 0, st, c->blk,
-                       c->rbits, c->pack, (const VT*)c->val, (const XT*)x, a, stats);
+#define TLF(NW, P) hipLaunchKernelGGL((tl_fwd_kernel<VT, XT, RT, AT, MAXR, 2, NW, P>), dim3(c->nblk), dim3(NW * 64), 0, \
+                                    st, c->blk, c->rbits, c->pack, (const VT*)c->val, (const XT*)x, a, stats)
+  if (g_tl_waves == 2) { if (g_tl_pipe) TLF(2, 1); else TLF(2, 0); }
+  else { if (g_tl_pipe) TLF(4, 1); else TLF(4, 0); }
+#undef TLF
 }
 
 template <typename VT, typename XT, typename RT>
@@ -834,12 +911,11 @@ static int tl_fwd_impl(const TLFwdDesc* c, const void* x, FwdArgs<XT, RT> a, dou
 
 template <typename VT, typename XT, typename AT, bool SQ, int MAXR>
 static void tl_t_launch(const TLTDesc* c, const void* x, double* G, double* parts, hipStream_t st) {
-  if (g_tl_waves_t == 2)
-    hipLaunchKernelGGL((tl_t_kernel<VT, XT, AT, SQ, MAXR, 2, 2>), dim3(c->nitems), dim3(128), 0, st, c->items,
-                       c->cbits, c->pack, (const VT*)c->val, (const XT*)x, G, c->dim, parts, g_ablate);
-  else
-    hipLaunchKernelGGL((tl_t_kernel<VT, XT, AT, SQ, MAXR, 2, 4>), dim3(c->nitems), dim3(256), 0, st, c->items,
-                       c->cbits, c->pack, (const VT*)c->val, (const XT*)x, G, c->dim, parts, g_ablate);
+#define TLT(NW, P) hipLaunchKernelGGL((tl_t_kernel<VT, XT, AT, SQ, MAXR, 2, NW, P>), dim3(c->nitems), dim3(NW * 64), 0, \
+                                    st, c->items, c->cbits, c->pack, (const VT*)c->val, (const XT*)x, G, c->dim, parts)
+  if (g_tl_waves_t == 2) { if (g_tl_pipe) TLT(2, 1); else TLT(2, 0); }
+  else { if (g_tl_pipe) TLT(4, 1); else TLT(4, 0); }
+#undef TLT
 }
 
 template <typename VT, typename XT, bool SQ>
@@ -1077,8 +1153,8 @@ int pml_reduce_stats(const double* stats, int n, double* out, int accumulate, do
 
 // ---- tiled layout entry points ------------------------------------------------------------------------------
 int pml_tl_maxbits() { return TL_MAXBITS; }
-void pml_tl_config(int acc64, int waves, int waves_t) {
-  g_tl_acc64 = acc64; g_tl_waves = waves == 2 ? 2 : 4; g_tl_waves_t = waves_t == 4 ? 4 : 2;
+void pml_tl_config(int acc64, int waves, int waves_t, int pipe) {
+  g_tl_acc64 = acc64; g_tl_waves = waves == 2 ? 2 : 4; g_tl_waves_t = waves_t == 2 ? 2 : 4; g_tl_pipe = pipe ? 1 : 0;
 }
 
 int pml_tl_fwd(int prec, const TLFwdDesc* c, const void* x, int mode, int loss, double shift, const void* y,

@@ -77,7 +77,7 @@ def glm_lib() -> Optional[ctypes.CDLL]:
         lib.pml_tl_fwd.argtypes = [c_int, ctypes.POINTER(TLFwdDesc), c_void_p, c_int, c_int, c_double, c_void_p,
                                    c_void_p, c_void_p, c_void_p, c_void_p, c_void_p, c_int, c_void_p, c_void_p]
         lib.pml_tl_t.argtypes = [c_int, ctypes.POINTER(TLTDesc), c_void_p, c_int, c_void_p, c_void_p, c_void_p]
-        lib.pml_tl_config.argtypes = [c_int, c_int, c_int]
+        lib.pml_tl_config.argtypes = [c_int, c_int, c_int, c_int]
         lib.pml_segdot.argtypes = [c_void_p, c_void_p, c_int, c_void_p, c_int, c_void_p, c_void_p]
         for f in ("pml_seg_fwd", "pml_seg_t", "pml_reduce_stats", "pml_build_blocks", "pml_tl_fwd", "pml_tl_t",
                   "pml_tl_maxbits", "pml_segdot"):
@@ -91,7 +91,7 @@ def glm_lib() -> Optional[ctypes.CDLL]:
 # Kernel configuration defaults (tuned on MI355X, see profiles/): forward = vector layout + 8192-entry LDS hot
 # table of the most frequent features; transpose = strided layout. Env overrides for experiments:
 # PML_FWD_STRIDED, PML_T_STRIDED, PML_HOT_N, PML_FWD_GRID.
-KERNEL_CONFIG = {"fwd_strided": 0, "t_strided": 0, "hot_n": 0, "fwd_grid": 1024, "tl_acc64": 1, "tl_waves": 4, "tl_waves_t": 4}
+KERNEL_CONFIG = {"fwd_strided": 0, "t_strided": 0, "hot_n": 0, "fwd_grid": 1024, "tl_acc64": 1, "tl_waves": 4, "tl_waves_t": 4, "tl_pipe": 0}
 
 
 def configure(**kw):
@@ -104,7 +104,8 @@ def configure(**kw):
     if lib is not None:
         lib.pml_set_config(KERNEL_CONFIG["fwd_strided"], KERNEL_CONFIG["t_strided"], KERNEL_CONFIG["hot_n"],
                            KERNEL_CONFIG["fwd_grid"])
-        lib.pml_tl_config(KERNEL_CONFIG["tl_acc64"], KERNEL_CONFIG["tl_waves"], KERNEL_CONFIG["tl_waves_t"])
+        lib.pml_tl_config(KERNEL_CONFIG["tl_acc64"], KERNEL_CONFIG["tl_waves"], KERNEL_CONFIG["tl_waves_t"],
+                          KERNEL_CONFIG["tl_pipe"])
     return dict(KERNEL_CONFIG)
 
 

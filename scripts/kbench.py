@@ -22,6 +22,7 @@ def main():
     ap.add_argument("--precision", default="bf16")
     ap.add_argument("--reps", type=int, default=5)
     ap.add_argument("--layout", default="auto")
+    ap.add_argument("--tl-configs", default="", help="semicolon list of tl_waves,tl_waves_t,tl_pipe (in-process A/B)")
     ap.add_argument("--ablate", type=int, nargs="+", default=[0])
     ap.add_argument("--configs", default="0,1,8192", help="semicolon list of fwd_strided,t_strided,hot_n")
     args = ap.parse_args()
@@ -29,6 +30,8 @@ def main():
     from photon_ml_amd.ops.native import glm_lib, configure
     lib = glm_lib()
     configs = [tuple(int(v) for v in c.split(",")) for c in args.configs.split(";")]
+    if args.tl_configs:
+        configs = [("tl",) + tuple(int(v) for v in c.split(",")) for c in args.tl_configs.split(";")]
     cache = {}
     for cr, abl, cfg in [(c, a, g) for c in args.chunk_rows for a in args.ablate for g in configs]:
         lib.pml_set_ablate(0)
@@ -39,7 +42,10 @@ def main():
                                               chunk_rows=cr, layout=args.layout)
         data, w = cache[cr]
         lib.pml_set_ablate(abl)
-        configure(fwd_strided=cfg[0], t_strided=cfg[1], hot_n=cfg[2])
+        if cfg[0] == "tl":
+            configure(tl_waves=cfg[1], tl_waves_t=cfg[2], tl_pipe=cfg[3])
+        else:
+            configure(fwd_strided=cfg[0], t_strided=cfg[1], hot_n=cfg[2])
         x = (w * 0.1).float()
         bytes_per = sum(c.nnz for c in data.csr) * (4 + data.csr[0].val.element_size())
         G = torch.zeros(args.features, dtype=torch.float64, device="cuda")
