@@ -13,6 +13,7 @@ from the partial-score vector (C11 routing) before each batched solve.
 """
 from __future__ import annotations
 
+import time
 from typing import Optional
 
 import numpy as np
@@ -31,6 +32,24 @@ from ..optimization.config import GLMOptimizationConfiguration, OptimizerType, R
 from ..optimization.problem import GLMOptimizationProblem
 from ..parallel.dist import DistributedGLMData, is_dist
 from ..sampling.samplers import down_sampler_for_task
+
+
+def random_effect_tracker_stats(iters: torch.Tensor, reasons: torch.Tensor, seconds: float) -> dict:
+    """RandomEffectOptimizationTracker (photon-api/.../RandomEffectOptimizationTracker.scala:100-150): counts of
+    convergence reasons and iteration statistics over the entities of one update."""
+    from ..optimization.batched import REASON_CODES
+    it = iters.detach().double().cpu()
+    rc = reasons.detach().cpu()
+    counts = {}
+    for code, reason in REASON_CODES.items():
+        n = int((rc == code).sum())
+        if n:
+            counts["not converged" if reason is None else reason.value] = n
+    return {"entities": int(it.numel()), "mean_iterations": float(it.mean()) if it.numel() else 0.0,
+            "std_iterations": float(it.std()) if it.numel() > 1 else 0.0,
+            "max_iterations": int(it.max()) if it.numel() else 0,
+            "min_iterations": int(it.min()) if it.numel() else 0,
+            "convergence_reasons": counts, "seconds": seconds}
 
 
 class Coordinate:
@@ -184,7 +203,8 @@ class RandomEffectCoordinate(Coordinate):
         if ds.layout == "segmented":
             return self._update_segmented(model, offs, l1, l2)
         keys, vals, vars_ = [], [], []
-        iters, n_conv = [], 0
+        iters, reasons = [], []
+        t_start = time.time()
         for b, bucket in enumerate(ds.buckets):
             O = ds.bucket_offsets(bucket, offs)
             bd = BatchedGLMData(bucket.X, bucket.y, O, bucket.w)
@@ -196,6 +216,7 @@ class RandomEffectCoordinate(Coordinate):
                 res = batched_lbfgs(bd, self.loss, l2, W0, oc.tolerance, oc.maximum_iterations, l1=l1)
             self._W[b] = res.W
             iters.append(res.iters)
+            reasons.append(res.reason)
             W = res.W
             var = None
             if self.compute_variance and self.loss.twice_differentiable:
@@ -205,9 +226,9 @@ class RandomEffectCoordinate(Coordinate):
             vals.append(v)
             if vv is not None:
                 vars_.append(vv)
-        it = torch.cat(iters) if iters else torch.zeros(0)
-        self.last_stats = {"entities": int(it.numel()), "mean_iterations": float(it.double().mean()) if it.numel()
-                           else 0.0, "max_iterations": int(it.max()) if it.numel() else 0}
+        it = torch.cat([i.cpu() for i in iters]) if iters else torch.zeros(0)
+        rs = torch.cat([r.cpu() for r in reasons]) if reasons else torch.zeros(0, dtype=torch.long)
+        self.last_stats = random_effect_tracker_stats(it, rs, time.time() - t_start)
         keys = np.concatenate(keys) if keys else np.zeros(0, np.int64)
         vals = np.concatenate(vals) if vals else np.zeros(0)
         variances = np.concatenate(vars_) if vars_ else None
@@ -222,15 +243,15 @@ class RandomEffectCoordinate(Coordinate):
         seg.o = offs.to(seg.y.device, torch.float64)[ds.seg_rows]
         seg._dzz_key = None
         W0 = self._warm_start_segmented(model)
+        t_start = time.time()
         oc = cfg.optimizer_config
         if oc.optimizer_type == OptimizerType.TRON:
             res = batched_tron(seg, self.loss, l2, W0, oc.tolerance, oc.maximum_iterations)
         else:
             res = batched_lbfgs(seg, self.loss, l2, W0, oc.tolerance, oc.maximum_iterations, l1=l1)
         self._W["seg"] = res.W
-        it = res.iters[torch.from_numpy(ds.n_active > 0).to(res.iters.device)]
-        self.last_stats = {"entities": int(it.numel()), "mean_iterations": float(it.double().mean()) if it.numel()
-                           else 0.0, "max_iterations": int(it.max()) if it.numel() else 0}
+        act = torch.from_numpy(ds.n_active > 0).to(res.iters.device)
+        self.last_stats = random_effect_tracker_stats(res.iters[act], res.reason[act], time.time() - t_start)
         W = res.W.detach().cpu().numpy()
         var = None
         if self.compute_variance and self.loss.twice_differentiable:

@@ -76,6 +76,13 @@ SCORING_RESULT = {
     ],
 }
 
+LATENT_FACTOR = {
+    "type": "record", "name": "LatentFactorAvro", "namespace": "com.linkedin.photon.avro.generated",
+    "doc": "latent factor of a matrix-factorization model (schema parity only: the reference has no MF training)",
+    "fields": [{"name": "effectId", "type": "string"},
+               {"name": "latentFactor", "type": {"type": "array", "items": "double"}}],
+}
+
 FEATURE_SUMMARY = {
     "type": "record", "name": "FeatureSummarizationResultAvro", "namespace": "com.linkedin.photon.avro.generated",
     "fields": [{"name": "featureName", "type": "string"}, {"name": "featureTerm", "type": "string"},

@@ -147,3 +147,19 @@ def test_feature_tools_index_and_bags(game_avro, tmp_path):
         res[opt[0]] = {maps_used.get_feature_name(j): w[j] for j in range(len(w))}
     a_, b_ = res.values()
     assert set(a_) == set(b_) and all(abs(a_[k] - b_[k]) < 1e-6 for k in a_)
+
+
+def test_libsvm_to_avro_roundtrip(tmp_path):
+    """dev-scripts/libsvm_text_to_trainingexample_avro.py analogue: LibSVM heart -> Avro -> same matrix."""
+    from photon_ml_amd.io.data_reader import AvroDataReader, read_libsvm
+    from photon_ml_amd.tools.libsvm_to_avro import convert
+    src = "/root/reference/photon-client/src/integTest/resources/DriverIntegTest/input/heart.txt"
+    n = convert(src, str(tmp_path / "heart"), records_per_file=100, binarize=True)
+    assert n == 250 and len(os.listdir(tmp_path / "heart")) == 3
+    ld_avro, im = AvroDataReader().read_labeled(str(tmp_path / "heart"))
+    ld_txt, _ = read_libsvm(src, 13, binarize_labels=True)
+    assert np.array_equal(ld_avro.y, ld_txt.y)
+    # column j of the LibSVM matrix is feature name str(j + 1)
+    for j in range(13):
+        col = im.get_index(f"{j + 1}\u0001")
+        np.testing.assert_allclose(ld_avro.x[:, col].toarray(), ld_txt.x[:, j].toarray())
