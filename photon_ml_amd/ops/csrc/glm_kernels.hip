@@ -771,14 +771,10 @@ __device__ __forceinline__ void tl_stream(const uint32_t* __restrict__ pack, con
 
 // Forward over row blocks. blk: 4 ints per block {row_lo, nrows, e_lo, e_hi} (chunk-local).
 template <typename VT, typename XT, typename RT, typename AT, int MAXR, int U, int NW, int P>
-__global__ __launch_bounds__(NW * 64) void tl_fwd_kernel(const int* __restrict__ blk, int rbits,
-                                                          const uint32_t* __restrict__ pack,
-                                                          const VT* __restrict__ val, const XT* __restrict__ x,
-                                                          FwdArgs<XT, RT> a, double* __restrict__ stats) {
-  __shared__ AT acc[NW][MAXR];
-  __shared__ double red[2 * NW];
-  const int b = blockIdx.x;
-  const int row_lo = blk[4 * b], nrows = blk[4 * b + 1], e_lo = blk[4 * b + 2], e_hi = blk[4 * b + 3];
+__device__ __forceinline__ void tl_fwd_block(int b, int row_lo, int nrows, int e_lo, int e_hi, int rbits,
+                                             const uint32_t* __restrict__ pack, const VT* __restrict__ val,
+                                             const XT* __restrict__ x, const FwdArgs<XT, RT>& a,
+                                             double* __restrict__ stats, AT (*acc)[MAXR], double* red) {
   const int R = 1 << rbits;
   for (int i = threadIdx.x; i < R; i += NW * 64)
 #pragma unroll
@@ -798,6 +794,36 @@ __global__ __launch_bounds__(NW * 64) void tl_fwd_kernel(const int* __restrict__
     block_sum2_nw<NW>(F, S, red);
     if (threadIdx.x == 0) { stats[2 * b] = F; stats[2 * b + 1] = S; }
   }
+}
+
+template <typename VT, typename XT, typename RT, typename AT, int MAXR, int U, int NW, int P>
+__global__ __launch_bounds__(NW * 64) void tl_fwd_kernel(const int* __restrict__ blk, int rbits,
+                                                          const uint32_t* __restrict__ pack,
+                                                          const VT* __restrict__ val, const XT* __restrict__ x,
+                                                          FwdArgs<XT, RT> a, double* __restrict__ stats) {
+  __shared__ AT acc[NW][MAXR];
+  __shared__ double red[2 * NW];
+  const int b = blockIdx.x;
+  tl_fwd_block<VT, XT, RT, AT, MAXR, U, NW, P>(b, blk[4 * b], blk[4 * b + 1], blk[4 * b + 2], blk[4 * b + 3],
+                                              rbits, pack, val, x, a, stats, acc, red);
+}
+
+// All chunks of a shard in ONE launch (no per-chunk tails / launch gaps): block table of 6 ints
+// {chunk, global row_lo, nrows, e_lo, e_hi, col_lo}; per-chunk stream pointers in device arrays; row-data
+// pointers in ``a`` are shard-global; stats index = global block index.
+template <typename VT, typename XT, typename RT, typename AT, int MAXR, int U, int NW, int P>
+__global__ __launch_bounds__(NW * 64) void tl_fwd_multi_kernel(const int* __restrict__ blk, int rbits,
+                                                                const unsigned long long* __restrict__ packs,
+                                                                const unsigned long long* __restrict__ vals,
+                                                                const XT* __restrict__ x, FwdArgs<XT, RT> a,
+                                                                double* __restrict__ stats) {
+  __shared__ AT acc[NW][MAXR];
+  __shared__ double red[2 * NW];
+  const int b = blockIdx.x;
+  const int* q = blk + 6 * b;
+  const int c = q[0];
+  tl_fwd_block<VT, XT, RT, AT, MAXR, U, NW, P>(b, q[1], q[2], q[3], q[4], rbits, (const uint32_t*)packs[c],
+                                              (const VT*)vals[c], x + q[5], a, stats, acc, red);
 }
 
 // Transpose over column-tile items. items: 4 ints {tile, e_lo, e_hi, part}; part < 0: the item is its tile's
@@ -864,6 +890,7 @@ __global__ __launch_bounds__(NTHREADS) void tl_t_combine2_kernel(const int* __re
 }
 
 struct TLFwdDesc { const int* blk; int nblk; int rbits; const uint32_t* pack; const void* val; };
+struct TLFwdMultiDesc { const int* blk; int nblk; int rbits; const unsigned long long* packs; const unsigned long long* vals; };
 struct TLTDesc {
   const int* items; int nitems; int cbits; const uint32_t* pack; const void* val;
   const int* mt_tiles; const int* mt_ptr; int nmt; int dim;
@@ -887,6 +914,32 @@ static void tl_fwd_launch(const TLFwdDesc* c, const void* x, FwdArgs<XT, RT> a, 
   if (g_tl_waves == 2) { if (g_tl_pipe) TLF(2, 1); else TLF(2, 0); }
   else { if (g_tl_pipe) TLF(4, 1); else TLF(4, 0); }
 #undef TLF
+}
+
+template <typename VT, typename XT, typename RT, typename AT, int MAXR>
+static void tl_fwd_multi_launch(const TLFwdMultiDesc* c, const void* x, FwdArgs<XT, RT> a, double* stats,
+                                hipStream_t st) {
+#define TLM(NW) hipLaunchKernelGGL((tl_fwd_multi_kernel<VT, XT, RT, AT, MAXR, 2, NW, 0>), dim3(c->nblk), dim3(NW * 64), \
+                                   0, st, c->blk, c->rbits, c->packs, c->vals, (const XT*)x, a, stats)
+  if (g_tl_waves == 2) TLM(2); else TLM(4);
+#undef TLM
+}
+
+template <typename VT, typename XT, typename RT>
+static int tl_fwd_multi_impl(const TLFwdMultiDesc* c, const void* x, FwdArgs<XT, RT> a, double* stats,
+                             hipStream_t st) {
+  if (c->nblk <= 0) return 0;
+  if (c->rbits < 1 || c->rbits > 11) return -22;
+  const bool f64 = sizeof(XT) == 8 || g_tl_acc64;
+  if (f64) {
+    if (c->rbits <= 10) tl_fwd_multi_launch<VT, XT, RT, double, 1024>(c, x, a, stats, st);
+    else tl_fwd_multi_launch<VT, XT, RT, double, 2048>(c, x, a, stats, st);
+  } else {
+    if (c->rbits <= 10) tl_fwd_multi_launch<VT, XT, RT, float, 1024>(c, x, a, stats, st);
+    else tl_fwd_multi_launch<VT, XT, RT, float, 2048>(c, x, a, stats, st);
+  }
+  LAUNCH_CHECK();
+  return 0;
 }
 
 template <typename VT, typename XT, typename RT>
@@ -1190,6 +1243,21 @@ int pml_segdot(const double* a, const double* b, int mode, const long long* ptr,
                      mode, ptr, nseg, out);
   LAUNCH_CHECK();
   return 0;
+}
+
+int pml_tl_fwd_multi(int prec, const TLFwdMultiDesc* c, const void* x, int mode, int loss, double shift,
+                     const void* y, const void* off, const void* wt, void* coef, void* dzz, double* z_out,
+                     int with_offset, double* stats, void* stream) {
+  hipStream_t st = (hipStream_t)stream;
+  if (prec == 2) {
+    FwdArgs<double, double> a{mode, loss, shift, (const double*)y, (const double*)off, (const double*)wt,
+                              (double*)coef, (double*)dzz, z_out, with_offset, 0, 0};
+    return tl_fwd_multi_impl<double, double, double>(c, x, a, stats, st);
+  }
+  FwdArgs<float, float> a{mode, loss, shift, (const float*)y, (const float*)off, (const float*)wt,
+                          (float*)coef, (float*)dzz, z_out, with_offset, 0, 0};
+  if (prec == 1) return tl_fwd_multi_impl<float, float, float>(c, x, a, stats, st);
+  return tl_fwd_multi_impl<uint16_t, float, float>(c, x, a, stats, st);
 }
 
 }  // extern "C"

@@ -266,6 +266,49 @@ class DeviceGLMData(GLMComputable):
         check(self.lib.pml_seg_t(self.prec, ctypes.byref(ch.desc), self._rows(x, c), square, gp,
                                  self.parts.data_ptr(), stream_handle(self.device)), "seg_t")
 
+    def _build_multi(self):
+        """One-launch forward over all TL chunks (block table {chunk, row_lo, nrows, e_lo, e_hi, col_lo})."""
+        self._multi = None
+        if not self.csr or any(ch.kind != "tl" for ch in self.csr) or len({ch.rbits for ch in self.csr}) != 1:
+            return
+        tabs = []
+        for c, ch in enumerate(self.csr):
+            b = ch.blk.to(torch.int64)
+            t = torch.empty((b.shape[0], 6), dtype=torch.int64, device=b.device)
+            t[:, 0] = c
+            t[:, 1] = b[:, 0] + self.row_starts[c]
+            t[:, 2:5] = b[:, 1:4]
+            t[:, 5] = self.col_lo[c]
+            tabs.append(t)
+        self._multi_blk = torch.cat(tabs).to(torch.int32).contiguous()
+        self._multi_packs = torch.tensor([ch.pack.data_ptr() for ch in self.csr], dtype=torch.int64,
+                                         device=self.device)
+        self._multi_vals = torch.tensor([ch.val.data_ptr() for ch in self.csr], dtype=torch.int64,
+                                        device=self.device)
+        from .native import TLFwdMultiDesc
+        self._multi = TLFwdMultiDesc(self._multi_blk.data_ptr(), self._multi_blk.shape[0], self.csr[0].rbits,
+                                     self._multi_packs.data_ptr(), self._multi_vals.data_ptr())
+
+    def fwd_all(self, x, mode, loss_id, shift, coef, dzz, z_out=None, with_offset=0, stats=True):
+        """Forward pass over every chunk: one launch in the tiled layout (``KERNEL_CONFIG['tl_multi']``),
+        else one launch per chunk."""
+        from .native import KERNEL_CONFIG
+        if getattr(self, "_multi", "unset") == "unset":
+            self._build_multi()
+        if self._multi is not None and KERNEL_CONFIG.get("tl_multi", 1):
+            p = lambda t: None if t is None else t.data_ptr()
+            check(self.lib.pml_tl_fwd_multi(
+                self.prec, ctypes.byref(self._multi), x.data_ptr(), mode, loss_id, float(shift), self.y.data_ptr(),
+                self.o.data_ptr(), self.wt.data_ptr(), p(coef), p(dzz), p(z_out), with_offset,
+                self.stats.data_ptr() if stats else None, stream_handle(self.device)), "tl_fwd_multi")
+            return
+        for c in range(len(self.csr)):
+            self._fwd(c, x, mode, loss_id, shift, coef, dzz, z_out, with_offset, stats)
+
+    def t_all(self, x, G, square: int = 0):
+        for c in range(len(self.csc)):
+            self._t(c, x, G, square)
+
     def _reduce_stats(self) -> torch.Tensor:
         out = self.out2
         st = stream_handle(self.device)
@@ -298,9 +341,8 @@ class DeviceGLMData(GLMComputable):
         G = out[: self.dim]
         x = self._vec(w_eff)
         dzz = self.dzz if (self.track_hessian and loss.twice_differentiable) else None
-        for c in range(len(self.csr)):
-            self._fwd(c, x, FWD_VALUE_GRAD, loss.loss_id, margin_shift, self.coef, dzz)
-            self._t(c, self.coef, G)
+        self.fwd_all(x, FWD_VALUE_GRAD, loss.loss_id, margin_shift, self.coef, dzz)
+        self.t_all(self.coef, G)
         out[self.dim:] = self._reduce_stats()
         if self.old_of_new is not None:
             out[: self.dim] = self._unperm(G.clone())
@@ -321,8 +363,7 @@ class DeviceGLMData(GLMComputable):
                 torch.equal(key, w_eff.to(key.device, key.dtype))):
             return
         x = self._vec(w_eff)
-        for c in range(len(self.csr)):
-            self._fwd(c, x, FWD_DZZ, loss.loss_id, shift, self.dzz, None, stats=False)
+        self.fwd_all(x, FWD_DZZ, loss.loss_id, shift, self.dzz, None, stats=False)
         self._dzz_key = w_eff.detach().clone()
         self._dzz_shift = float(shift)
 
@@ -335,9 +376,8 @@ class DeviceGLMData(GLMComputable):
         out = torch.zeros(self.dim + 2, dtype=torch.float64, device=self.device)
         H = out[: self.dim]
         x = self._vec(v_eff)
-        for c in range(len(self.csr)):
-            self._fwd(c, x, FWD_HV, loss.loss_id, v_shift, self.coef, self.dzz)
-            self._t(c, self.coef, H)
+        self.fwd_all(x, FWD_HV, loss.loss_id, v_shift, self.coef, self.dzz)
+        self.t_all(self.coef, H)
         out[self.dim:] = self._reduce_stats()
         if self.old_of_new is not None:
             out[: self.dim] = self._unperm(H.clone())
@@ -351,9 +391,8 @@ class DeviceGLMData(GLMComputable):
     def hdiag_sums(self, loss, w):
         x = self._vec(w)
         out = torch.zeros(self.dim, dtype=torch.float64, device=self.device)
-        for c in range(len(self.csr)):
-            self._fwd(c, x, FWD_DZZ, loss.loss_id, 0.0, self.coef, None, stats=False)
-            self._t(c, self.coef, out, square=1)
+        self.fwd_all(x, FWD_DZZ, loss.loss_id, 0.0, self.coef, None, stats=False)
+        self.t_all(self.coef, out, square=1)
         self._dzz_key = None
         return self._unperm(out)
 
@@ -374,7 +413,6 @@ class DeviceGLMData(GLMComputable):
     def margins(self, w, margin_shift: float = 0.0, with_offsets: bool = False):
         z = torch.empty(max(self.n_rows, 1), dtype=torch.float64, device=self.device)
         x = self._vec(w)
-        for c in range(len(self.csr)):
-            self._fwd(c, x, FWD_MARGIN, 0, margin_shift, None, None, z_out=z, with_offset=int(with_offsets),
-                      stats=False)
+        self.fwd_all(x, FWD_MARGIN, 0, margin_shift, None, None, z_out=z, with_offset=int(with_offsets),
+                     stats=False)
         return z[: self.n_rows]

@@ -35,6 +35,10 @@ class TLFwdDesc(ctypes.Structure):
     _fields_ = [("blk", c_void_p), ("nblk", c_int), ("rbits", c_int), ("pack", c_void_p), ("val", c_void_p)]
 
 
+class TLFwdMultiDesc(ctypes.Structure):
+    _fields_ = [("blk", c_void_p), ("nblk", c_int), ("rbits", c_int), ("packs", c_void_p), ("vals", c_void_p)]
+
+
 class TLTDesc(ctypes.Structure):
     _fields_ = [
         ("items", c_void_p), ("nitems", c_int), ("cbits", c_int), ("pack", c_void_p), ("val", c_void_p),
@@ -78,9 +82,12 @@ def glm_lib() -> Optional[ctypes.CDLL]:
                                    c_void_p, c_void_p, c_void_p, c_void_p, c_void_p, c_int, c_void_p, c_void_p]
         lib.pml_tl_t.argtypes = [c_int, ctypes.POINTER(TLTDesc), c_void_p, c_int, c_void_p, c_void_p, c_void_p]
         lib.pml_tl_config.argtypes = [c_int, c_int, c_int, c_int]
+        lib.pml_tl_fwd_multi.argtypes = [c_int, ctypes.POINTER(TLFwdMultiDesc), c_void_p, c_int, c_int, c_double,
+                                         c_void_p, c_void_p, c_void_p, c_void_p, c_void_p, c_void_p, c_int, c_void_p,
+                                         c_void_p]
         lib.pml_segdot.argtypes = [c_void_p, c_void_p, c_int, c_void_p, c_int, c_void_p, c_void_p]
         for f in ("pml_seg_fwd", "pml_seg_t", "pml_reduce_stats", "pml_build_blocks", "pml_tl_fwd", "pml_tl_t",
-                  "pml_tl_maxbits", "pml_segdot"):
+                  "pml_tl_maxbits", "pml_segdot", "pml_tl_fwd_multi"):
             getattr(lib, f).restype = c_int
         lib.pml_set_config.argtypes = [c_int, c_int, c_int, c_int]
         lib._pml_typed = True
@@ -91,7 +98,7 @@ def glm_lib() -> Optional[ctypes.CDLL]:
 # Kernel configuration defaults (tuned on MI355X, see profiles/): forward = vector layout + 8192-entry LDS hot
 # table of the most frequent features; transpose = strided layout. Env overrides for experiments:
 # PML_FWD_STRIDED, PML_T_STRIDED, PML_HOT_N, PML_FWD_GRID.
-KERNEL_CONFIG = {"fwd_strided": 0, "t_strided": 0, "hot_n": 0, "fwd_grid": 1024, "tl_acc64": 1, "tl_waves": 4, "tl_waves_t": 4, "tl_pipe": 0}
+KERNEL_CONFIG = {"fwd_strided": 0, "t_strided": 0, "hot_n": 0, "fwd_grid": 1024, "tl_acc64": 1, "tl_waves": 2, "tl_waves_t": 4, "tl_pipe": 0, "tl_multi": 1}
 
 
 def configure(**kw):

@@ -43,7 +43,8 @@ def main():
         data, w = cache[cr]
         lib.pml_set_ablate(abl)
         if cfg[0] == "tl":
-            configure(tl_waves=cfg[1], tl_waves_t=cfg[2], tl_pipe=cfg[3])
+            configure(tl_waves=cfg[1], tl_waves_t=cfg[2], tl_pipe=cfg[3],
+                      tl_multi=cfg[4] if len(cfg) > 4 else 1)
         else:
             configure(fwd_strided=cfg[0], t_strided=cfg[1], hot_n=cfg[2])
         x = (w * 0.1).float()
@@ -51,16 +52,14 @@ def main():
         G = torch.zeros(args.features, dtype=torch.float64, device="cuda")
         nch = len(data.csr)
         # warmup
-        for c in range(nch):
-            data._fwd(c, x, 1, LOGISTIC.loss_id, 0.0, data.coef, None)
-            data._t(c, data.coef, G)
+        data.fwd_all(x, 1, LOGISTIC.loss_id, 0.0, data.coef, None)
+        data.t_all(data.coef, G)
         torch.cuda.synchronize()
         ev = [torch.cuda.Event(enable_timing=True) for _ in range(3)]
         tf, tt = [], []
         for _ in range(args.reps):
             ev[0].record()
-            for c in range(nch):
-                data._fwd(c, x, 1, LOGISTIC.loss_id, 0.0, data.coef, None)
+            data.fwd_all(x, 1, LOGISTIC.loss_id, 0.0, data.coef, None)
             ev[1].record()
             for c in range(nch):
                 data._t(c, data.coef, G)
