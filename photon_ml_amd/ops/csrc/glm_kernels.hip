@@ -829,13 +829,10 @@ __global__ __launch_bounds__(NW * 64) void tl_fwd_multi_kernel(const int* __rest
 // Transpose over column-tile items. items: 4 ints {tile, e_lo, e_hi, part}; part < 0: the item is its tile's
 // only one -> G[tile cols] += sums directly; else the item's row of partial sums goes to parts[part * C ...].
 template <typename VT, typename XT, typename AT, bool SQ, int MAXR, int U, int NW, int P>
-__global__ __launch_bounds__(NW * 64) void tl_t_kernel(const int* __restrict__ items, int cbits,
-                                                        const uint32_t* __restrict__ pack,
-                                                        const VT* __restrict__ val, const XT* __restrict__ x,
-                                                        double* __restrict__ G, int dim, double* __restrict__ parts) {
-  __shared__ AT acc[NW][MAXR];
-  const int it = blockIdx.x;
-  const int tile = items[4 * it], e_lo = items[4 * it + 1], e_hi = items[4 * it + 2], part = items[4 * it + 3];
+__device__ __forceinline__ void tl_t_item(int tile, int e_lo, int e_hi, int part, int cbits,
+                                          const uint32_t* __restrict__ pack, const VT* __restrict__ val,
+                                          const XT* __restrict__ x, double* __restrict__ G, int dim,
+                                          double* __restrict__ parts, AT (*acc)[MAXR]) {
   const int C = 1 << cbits;
   for (int i = threadIdx.x; i < C; i += NW * 64)
 #pragma unroll
@@ -854,6 +851,32 @@ __global__ __launch_bounds__(NW * 64) void tl_t_kernel(const int* __restrict__ i
       parts[(size_t)part * C + c] = s;
     }
   }
+}
+
+template <typename VT, typename XT, typename AT, bool SQ, int MAXR, int U, int NW, int P>
+__global__ __launch_bounds__(NW * 64) void tl_t_kernel(const int* __restrict__ items, int cbits,
+                                                        const uint32_t* __restrict__ pack,
+                                                        const VT* __restrict__ val, const XT* __restrict__ x,
+                                                        double* __restrict__ G, int dim, double* __restrict__ parts) {
+  __shared__ AT acc[NW][MAXR];
+  const int* q = items + 4 * blockIdx.x;
+  tl_t_item<VT, XT, AT, SQ, MAXR, U, NW, P>(q[0], q[1], q[2], q[3], cbits, pack, val, x, G, dim, parts, acc);
+}
+
+// All row chunks of a shard in one launch. items: 6 ints {chunk, tile, e_lo, e_hi, part, row_base}; a tile with a
+// single item in the whole shard writes G directly, every other item writes a partial row that the shard-wide
+// combine sums in (chunk, item) order — deterministic and race-free across chunks.
+template <typename VT, typename XT, typename AT, bool SQ, int MAXR, int U, int NW, int P>
+__global__ __launch_bounds__(NW * 64) void tl_t_multi_kernel(const int* __restrict__ items, int cbits,
+                                                              const unsigned long long* __restrict__ packs,
+                                                              const unsigned long long* __restrict__ vals,
+                                                              const XT* __restrict__ x, double* __restrict__ G,
+                                                              int dim, double* __restrict__ parts) {
+  __shared__ AT acc[NW][MAXR];
+  const int* q = items + 6 * blockIdx.x;
+  const int c = q[0];
+  tl_t_item<VT, XT, AT, SQ, MAXR, U, NW, P>(q[1], q[2], q[3], q[4], cbits, (const uint32_t*)packs[c],
+                                            (const VT*)vals[c], x + q[5], G, dim, parts, acc);
 }
 
 // Combine the partial rows of split tiles, deterministically, in two levels (a hot tile can have hundreds of
@@ -896,6 +919,12 @@ struct TLTDesc {
   const int* mt_tiles; const int* mt_ptr; int nmt; int dim;
   const int* cu; int ncu;     // level-1 combine units {tile, part_lo, part_hi}; mt_ptr indexes units
   int nparts_total;           // item partial rows (the level-1 rows follow them in the scratch buffer)
+};
+// Shard-wide transpose: items of every chunk (6 ints, see tl_t_multi_kernel) with per-chunk stream pointers.
+struct TLTMultiDesc {
+  const int* items; int nitems; int cbits; const unsigned long long* packs; const unsigned long long* vals;
+  const int* mt_tiles; const int* mt_ptr; int nmt; int dim;
+  const int* cu; int ncu; int nparts_total;
 };
 
 // Runtime TL configuration: accumulator precision for bf16/f32 data (0 = fp32 LDS, 1 = fp64 LDS) and the number
@@ -986,6 +1015,40 @@ static int tl_t_impl(const TLTDesc* c, const void* x, double* G, double* parts, 
     tl_t_launch<VT, XT, float, SQ, 2048>(c, x, G, parts, st);
   } else {
     tl_t_launch<VT, XT, float, SQ, 4096>(c, x, G, parts, st);
+  }
+  LAUNCH_CHECK();
+  if (c->nmt > 0) {
+    const int C = 1 << c->cbits;
+    double* l1 = parts + (size_t)c->nparts_total * C;
+    hipLaunchKernelGGL(tl_t_combine1_kernel, dim3(c->ncu), dim3(NTHREADS), 0, st, c->cu, c->cbits, parts, l1);
+    LAUNCH_CHECK();
+    hipLaunchKernelGGL(tl_t_combine2_kernel, dim3(c->nmt, (C + NTHREADS - 1) / NTHREADS), dim3(NTHREADS), 0, st,
+                       c->mt_tiles, c->mt_ptr, c->cbits, l1, G, c->dim);
+    LAUNCH_CHECK();
+  }
+  return 0;
+}
+
+template <typename VT, typename XT, typename AT, bool SQ, int MAXR>
+static void tl_t_multi_launch(const TLTMultiDesc* c, const void* x, double* G, double* parts, hipStream_t st) {
+#define TLTM(NW) hipLaunchKernelGGL((tl_t_multi_kernel<VT, XT, AT, SQ, MAXR, 2, NW, 0>), dim3(c->nitems), dim3(NW * 64), \
+                                    0, st, c->items, c->cbits, c->packs, c->vals, (const XT*)x, G, c->dim, parts)
+  if (g_tl_waves_t == 2) TLTM(2); else TLTM(4);
+#undef TLTM
+}
+
+template <typename VT, typename XT, bool SQ>
+static int tl_t_multi_impl(const TLTMultiDesc* c, const void* x, double* G, double* parts, hipStream_t st) {
+  if (c->nitems <= 0) return 0;
+  if (c->cbits < 1 || c->cbits > 11) return -22;
+  const bool f64 = sizeof(XT) == 8 || g_tl_acc64;
+  if (f64) {
+    if (c->cbits <= 10) tl_t_multi_launch<VT, XT, double, SQ, 1024>(c, x, G, parts, st);
+    else tl_t_multi_launch<VT, XT, double, SQ, 2048>(c, x, G, parts, st);
+  } else if (c->cbits <= 10) {
+    tl_t_multi_launch<VT, XT, float, SQ, 1024>(c, x, G, parts, st);
+  } else {
+    tl_t_multi_launch<VT, XT, float, SQ, 2048>(c, x, G, parts, st);
   }
   LAUNCH_CHECK();
   if (c->nmt > 0) {
@@ -1233,6 +1296,17 @@ int pml_tl_t(int prec, const TLTDesc* c, const void* x, int square, double* G, d
                                : tl_t_impl<float, float, false>(c, x, G, parts, st);
   return square ? tl_t_impl<uint16_t, float, true>(c, x, G, parts, st)
                 : tl_t_impl<uint16_t, float, false>(c, x, G, parts, st);
+}
+
+int pml_tl_t_multi(int prec, const TLTMultiDesc* c, const void* x, int square, double* G, double* parts,
+                   void* stream) {
+  hipStream_t st = (hipStream_t)stream;
+  if (prec == 2) return square ? tl_t_multi_impl<double, double, true>(c, x, G, parts, st)
+                               : tl_t_multi_impl<double, double, false>(c, x, G, parts, st);
+  if (prec == 1) return square ? tl_t_multi_impl<float, float, true>(c, x, G, parts, st)
+                               : tl_t_multi_impl<float, float, false>(c, x, G, parts, st);
+  return square ? tl_t_multi_impl<uint16_t, float, true>(c, x, G, parts, st)
+                : tl_t_multi_impl<uint16_t, float, false>(c, x, G, parts, st);
 }
 
 int pml_segdot(const double* a, const double* b, int mode, const long long* ptr, int nseg, double* out,

@@ -289,6 +289,17 @@ class DeviceGLMData(GLMComputable):
         self._multi = TLFwdMultiDesc(self._multi_blk.data_ptr(), self._multi_blk.shape[0], self.csr[0].rbits,
                                      self._multi_packs.data_ptr(), self._multi_vals.data_ptr())
 
+    def _build_multi_t(self):
+        self._multi_t = None
+        if (not self.csc or any(ch.kind != "tl" for ch in self.csc) or len({ch.cbits for ch in self.csc}) != 1
+                or any(self.col_lo)):
+            return
+        from .tiled import TLTMulti
+        self._multi_t = TLTMulti(self.csc, self.row_starts, self.dim)
+        need = self._multi_t.parts_needed
+        if need > self.parts.numel():
+            self.parts = torch.zeros(need, dtype=torch.float64, device=self.device)
+
     def fwd_all(self, x, mode, loss_id, shift, coef, dzz, z_out=None, with_offset=0, stats=True):
         """Forward pass over every chunk: one launch in the tiled layout (``KERNEL_CONFIG['tl_multi']``),
         else one launch per chunk."""
@@ -306,6 +317,16 @@ class DeviceGLMData(GLMComputable):
             self._fwd(c, x, mode, loss_id, shift, coef, dzz, z_out, with_offset, stats)
 
     def t_all(self, x, G, square: int = 0):
+        """Transpose pass over every chunk: one launch + one shard-wide combine in the tiled layout
+        (``KERNEL_CONFIG['tl_multi']``), else per chunk."""
+        from .native import KERNEL_CONFIG
+        if getattr(self, "_multi_t", "unset") == "unset":
+            self._build_multi_t()
+        if self._multi_t is not None and KERNEL_CONFIG.get("tl_multi", 1):
+            check(self.lib.pml_tl_t_multi(self.prec, ctypes.byref(self._multi_t.desc), x.data_ptr(), square,
+                                          G.data_ptr(), self.parts.data_ptr(), stream_handle(self.device)),
+                  "tl_t_multi")
+            return
         for c in range(len(self.csc)):
             self._t(c, x, G, square)
 

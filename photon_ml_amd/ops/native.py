@@ -39,6 +39,12 @@ class TLFwdMultiDesc(ctypes.Structure):
     _fields_ = [("blk", c_void_p), ("nblk", c_int), ("rbits", c_int), ("packs", c_void_p), ("vals", c_void_p)]
 
 
+class TLTMultiDesc(ctypes.Structure):
+    _fields_ = [("items", c_void_p), ("nitems", c_int), ("cbits", c_int), ("packs", c_void_p), ("vals", c_void_p),
+                ("mt_tiles", c_void_p), ("mt_ptr", c_void_p), ("nmt", c_int), ("dim", c_int), ("cu", c_void_p),
+                ("ncu", c_int), ("nparts_total", c_int)]
+
+
 class TLTDesc(ctypes.Structure):
     _fields_ = [
         ("items", c_void_p), ("nitems", c_int), ("cbits", c_int), ("pack", c_void_p), ("val", c_void_p),
@@ -82,12 +88,14 @@ def glm_lib() -> Optional[ctypes.CDLL]:
                                    c_void_p, c_void_p, c_void_p, c_void_p, c_void_p, c_int, c_void_p, c_void_p]
         lib.pml_tl_t.argtypes = [c_int, ctypes.POINTER(TLTDesc), c_void_p, c_int, c_void_p, c_void_p, c_void_p]
         lib.pml_tl_config.argtypes = [c_int, c_int, c_int, c_int]
+        lib.pml_tl_t_multi.argtypes = [c_int, ctypes.POINTER(TLTMultiDesc), c_void_p, c_int, c_void_p, c_void_p,
+                                       c_void_p]
         lib.pml_tl_fwd_multi.argtypes = [c_int, ctypes.POINTER(TLFwdMultiDesc), c_void_p, c_int, c_int, c_double,
                                          c_void_p, c_void_p, c_void_p, c_void_p, c_void_p, c_void_p, c_int, c_void_p,
                                          c_void_p]
         lib.pml_segdot.argtypes = [c_void_p, c_void_p, c_int, c_void_p, c_int, c_void_p, c_void_p]
         for f in ("pml_seg_fwd", "pml_seg_t", "pml_reduce_stats", "pml_build_blocks", "pml_tl_fwd", "pml_tl_t",
-                  "pml_tl_maxbits", "pml_segdot", "pml_tl_fwd_multi"):
+                  "pml_tl_maxbits", "pml_segdot", "pml_tl_fwd_multi", "pml_tl_t_multi"):
             getattr(lib, f).restype = c_int
         lib.pml_set_config.argtypes = [c_int, c_int, c_int, c_int]
         lib._pml_typed = True

@@ -20,7 +20,7 @@ of more than 2^27 rows) fall back to the segmented-stream layout (:mod:`photon_m
 from __future__ import annotations
 
 import os
-from typing import Optional
+from typing import Optional, Sequence
 
 import numpy as np
 import torch
@@ -198,3 +198,87 @@ class TLTChunk:
             v = v * v
         g = torch.zeros(self.dim, dtype=torch.float64, device=p.device)
         return g.index_add_(0, col, v * r.to(torch.float64)[row])
+
+
+class TLTMulti:
+    """Shard-wide transpose over every row chunk in one launch (``tl_t_multi_kernel``).
+
+    Items of all chunks keep their launch order (chunk, item); each carries its chunk (stream pointers), its row
+    base (offset into the shard-length row vector) and a partial-row slot. Tiles hit by more than one item in the
+    whole shard are combined by the same two-level fixed-order combine as a single chunk's split tiles, so the
+    result is deterministic and independent of chunk scheduling. Requires chunk-independent column tiles (no
+    per-chunk column windows) and one ``cbits`` for all chunks.
+    """
+
+    def __init__(self, chunks: Sequence["TLTChunk"], row_starts: Sequence[int], dim: int):
+        from .native import TLTMultiDesc
+        dev = chunks[0].pack.device
+        self.cbits = chunks[0].cbits
+        its = []
+        for c, ch in enumerate(chunks):
+            it = ch.items[: ch.nitems].cpu().numpy().astype(np.int64).reshape(-1, 4)
+            its.append(np.column_stack([np.full(len(it), c), it[:, 0], it[:, 1], it[:, 2],
+                                        np.full(len(it), row_starts[c])]))
+        it = np.concatenate(its) if its else np.zeros((0, 5), np.int64)
+        n = len(it)
+        tile = it[:, 1]
+        order = np.lexsort((np.arange(n), tile))          # grouped by tile, (chunk, item) order inside
+        ts = tile[order]
+        starts = np.flatnonzero(np.r_[True, ts[1:] != ts[:-1]]) if n else np.zeros(0, np.int64)
+        k = np.diff(np.r_[starts, n])                    # items per tile (shard-wide)
+        multi_tile = np.repeat(k > 1, k)
+        part = np.full(n, -1, np.int64)
+        part[order[multi_tile]] = np.arange(int(multi_tile.sum()))
+        # level-1 units of <= COMBINE_SEG consecutive partial rows per split tile
+        km = k[k > 1]
+        plo = np.cumsum(km) - km
+        nu = -(-km // COMBINE_SEG)
+        u_tile = np.repeat(np.arange(len(km)), nu)
+        u_first = np.repeat(plo, nu) + COMBINE_SEG * (np.arange(int(nu.sum())) - np.repeat(np.cumsum(nu) - nu, nu))
+        u_last = np.minimum(u_first + COMBINE_SEG, np.repeat(plo + km, nu))
+        self.nitems, self.nparts, self.ncu, self.nmt = n, int(km.sum()), int(nu.sum()), len(km)
+        rows = np.column_stack([it[:, 0], it[:, 1], it[:, 2], it[:, 3], part, it[:, 4]]).astype(np.int32)
+        self.items = torch.tensor(rows.reshape(-1, 6), device=dev)
+        self.mt_tiles = torch.tensor(np.r_[ts[starts][k > 1], 0].astype(np.int32)[: max(self.nmt, 1)], device=dev)
+        self.mt_ptr = torch.tensor(np.r_[0, np.cumsum(nu)].astype(np.int32), device=dev)
+        self.cu = torch.tensor(np.column_stack([u_tile, u_first, u_last]).astype(np.int32).reshape(-1, 3)
+                               if self.ncu else np.zeros((1, 3), np.int32), device=dev)
+        self.packs = torch.tensor([ch.pack.data_ptr() for ch in chunks], dtype=torch.int64, device=dev)
+        self.vals = torch.tensor([ch.val.data_ptr() for ch in chunks], dtype=torch.int64, device=dev)
+        self._chunks = list(chunks)  # keep the streams alive
+        self.desc = TLTMultiDesc(self.items.data_ptr(), n, self.cbits, self.packs.data_ptr(), self.vals.data_ptr(),
+                                 self.mt_tiles.data_ptr(), self.mt_ptr.data_ptr(), self.nmt, dim,
+                                 self.cu.data_ptr(), self.ncu, self.nparts)
+
+    @property
+    def parts_needed(self) -> int:
+        return (self.nparts + self.ncu) << self.cbits
+
+    def emulate_rmatvec(self, r: torch.Tensor, square: bool = False) -> torch.Tensor:
+        """Host emulation of the launch + combine (item partial rows, direct tiles, two-level combine)."""
+        C = 1 << self.cbits
+        dim = self.desc.dim
+        ntiles = (dim + C - 1) // C
+        G = torch.zeros(ntiles * C, dtype=torch.float64)
+        parts = torch.zeros((max(self.nparts, 1), C), dtype=torch.float64)
+        r = r.to(torch.float64).cpu()
+        for c, tile, e_lo, e_hi, part, rb in self.items.cpu().tolist():
+            ch = self._chunks[c]
+            p = ch.pack[e_lo:e_hi].to(torch.int64).cpu() & 0xFFFFFFFF
+            v = ch.val[e_lo:e_hi].to(torch.float64).cpu()
+            if square:
+                v = v * v
+            acc = torch.zeros(C, dtype=torch.float64).index_add_(0, p & (C - 1), v * r[rb + (p >> self.cbits)])
+            if part < 0:
+                G[tile * C:(tile + 1) * C] += acc
+            else:
+                parts[part] = acc
+        cu = self.cu.cpu().tolist()
+        l1 = [parts[a:b].sum(0) for _, a, b in cu[: self.ncu]]
+        mp = self.mt_ptr.cpu().tolist()
+        for t, tile in enumerate(self.mt_tiles.cpu().tolist()[: self.nmt]):
+            s = torch.zeros(C, dtype=torch.float64)
+            for u in range(mp[t], mp[t + 1]):
+                s += l1[u]
+            G[tile * C:(tile + 1) * C] += s
+        return G[:dim]

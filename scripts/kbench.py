@@ -61,8 +61,7 @@ def main():
             ev[0].record()
             data.fwd_all(x, 1, LOGISTIC.loss_id, 0.0, data.coef, None)
             ev[1].record()
-            for c in range(nch):
-                data._t(c, data.coef, G)
+            data.t_all(data.coef, G)
             ev[2].record()
             torch.cuda.synchronize()
             tf.append(ev[0].elapsed_time(ev[1]))

@@ -184,26 +184,31 @@ def test_segdot_kernel():
 
 @pytest.mark.parametrize("col_windows", [False, True])
 def test_tl_multi_launch_matches_per_chunk(col_windows):
-    """One-launch forward over all tiled chunks == one launch per chunk, bit for bit (same blocks, same order)."""
+    """Shard-wide launches (forward: all chunks' blocks; transpose: all chunks' items + one combine) vs one launch
+    per chunk: forward outputs bit for bit (same blocks), gradients to rounding (different fixed summation
+    order), and the shard-wide path is itself bitwise deterministic."""
     from photon_ml_amd.ops.device import DeviceGLMData
     from photon_ml_amd.ops.native import configure
     data = make_data(n=9000, d=700, density=0.01, seed=3)
-    dev = DeviceGLMData.from_labeled(data, "cuda", "f32", chunk_rows=2000, layout="tiled", col_windows=col_windows)
+    dev = DeviceGLMData.from_labeled(data, "cuda", "f32", chunk_rows=2000, layout="tiled", col_windows=col_windows,
+                                     item_entries=500)
     assert len(dev.csr) > 1
     w = torch.from_numpy(np.random.default_rng(1).normal(size=700) * 0.1).cuda()
     v = torch.from_numpy(np.random.default_rng(2).normal(size=700)).cuda()
     res = {}
     try:
-        for multi in (0, 1):
+        for multi in (0, 1, 1):
             configure(tl_multi=multi)
             dev._dzz_key = None
             f, s, g = dev.value_grad_sums(LOGISTIC, w, 0.0)
             hv = dev.hv_packed(LOGISTIC, w, 0.0, v, 0.0).clone()
             hd = dev.hdiag_sums(LOGISTIC, w).clone()
-            res[multi] = (f, s, g.clone(), dev.margins(w).clone(), hv, hd)
+            r = (f, s, g.clone(), dev.margins(w).clone(), hv, hd)
+            if multi in res:
+                assert r[:2] == res[multi][:2] and all(torch.equal(a, b) for a, b in zip(r[2:], res[multi][2:]))
+            res[multi] = r
     finally:
         configure(tl_multi=1)
-    assert res[0][0] == res[1][0] and res[0][1] == res[1][1]
-    assert torch.equal(res[0][2], res[1][2]) and torch.equal(res[0][3], res[1][3])
-    assert torch.equal(res[0][4], res[1][4])
-    assert torch.equal(res[0][5], res[1][5])
+    assert res[0][0] == res[1][0] and res[0][1] == res[1][1] and torch.equal(res[0][3], res[1][3])
+    for a, b in zip(res[0][2:], res[1][2:]):
+        assert torch.allclose(a, b, rtol=1e-12, atol=1e-12 * float(a.abs().max()))

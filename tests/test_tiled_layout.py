@@ -56,3 +56,38 @@ def test_device_data_construction_cpu(layout):
     assert dev.layout == layout and len(dev.csr) == 3 and len(dev.csc) == 3
     assert dev.stats.numel() >= 2 * sum(c.nstats for c in dev.csr)
     assert dev.parts.numel() >= max(c.parts_needed for c in dev.csc)
+
+
+@pytest.mark.parametrize("chunk,item,hot", [(700, 64, False), (1000, 300, True), (5000, 1 << 16, False)])
+def test_tl_shard_wide_transpose_emulation(chunk, item, hot):
+    """Shard-wide transpose tables (all chunks in one launch): every entry once, split tiles combined in
+    (chunk, item) order, single-item tiles direct; result == X^T r."""
+    from photon_ml_amd.ops.tiled import COMBINE_SEG, TLTMulti
+    rng = np.random.default_rng(3)
+    m, d = 5000, 3000
+    x = sp.random(m, d, density=0.01, format="lil", random_state=2)
+    if hot:
+        x[:, 5] = 1.0  # a column in every row -> tiles with many items across chunks
+    x = x.tocsr()
+    x.data = rng.normal(size=x.nnz)
+    starts = list(range(0, m, chunk)) + [m]
+    chunks = []
+    for a, b in zip(starts[:-1], starts[1:]):
+        xc = x[a:b]
+        chunks.append(TLTChunk(torch.from_numpy(xc.indptr.astype(np.int64)),
+                               torch.from_numpy(xc.indices.astype(np.int64)), torch.from_numpy(xc.data), d, chunk,
+                               item_entries=item))
+    mt = TLTMulti(chunks, starts, d)
+    r = rng.normal(size=m)
+    np.testing.assert_allclose(mt.emulate_rmatvec(torch.from_numpy(r)).numpy(), x.T @ r, atol=1e-11)
+    np.testing.assert_allclose(mt.emulate_rmatvec(torch.from_numpy(r), square=True).numpy(),
+                               x.multiply(x).T @ r, atol=1e-11)
+    it = mt.items.numpy()
+    assert it.shape == (sum(c.nitems for c in chunks), 6)
+    assert mt.nparts == int((it[:, 4] >= 0).sum()) and sorted(it[it[:, 4] >= 0, 4]) == list(range(mt.nparts))
+    # a tile is direct iff it has exactly one item in the shard
+    tiles, cnt = np.unique(it[:, 1], return_counts=True)
+    single = set(tiles[cnt == 1].tolist())
+    assert all((row[4] < 0) == (row[1] in single) for row in it)
+    cu = mt.cu.numpy()[: mt.ncu]
+    assert (cu[:, 2] - cu[:, 1] <= COMBINE_SEG).all() and mt.mt_ptr.numpy()[-1] == mt.ncu
