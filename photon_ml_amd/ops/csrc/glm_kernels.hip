@@ -761,11 +761,77 @@ __device__ __forceinline__ void tl_stream_p1(const uint32_t* __restrict__ pack, 
   }
 }
 
-// pipeline variant: P = 0 two-slot stream prefetch; P = 1 three-stage (stream r+2 / gather r+1 / accumulate r)
+// Two-slot prefetch like tl_stream_p0 with Q quads (4 * Q entries) per lane per round: Q = 2 doubles the
+// loads and gathers each wave keeps in flight (memory-level parallelism per wave) at the cost of VGPRs.
+template <typename VT, typename XT, typename AT, bool SQ, int NW, int Q>
+__device__ __forceinline__ void tl_stream_wide(const uint32_t* __restrict__ pack, const VT* __restrict__ val,
+                                            const XT* __restrict__ x, int e_lo, int e_hi, int sbits, AT* acc) {
+  typedef typename TLValT<VT>::T LT;
+  typedef typename TLVals<VT>::Raw Raw;
+  constexpr int V = 4 * Q, ROUND = 64 * V;
+  const int lane = threadIdx.x & 63, w = threadIdx.x >> 6;
+  const uint32_t smask = (1u << sbits) - 1u;
+  const int lo = e_lo & ~(TL_VEC - 1);
+  const int nr = (e_hi - lo + ROUND - 1) / ROUND;
+  const int r0 = (nr * w) / NW, r1 = (nr * (w + 1)) / NW;
+  if (r0 >= r1) return;
+  struct Slot { v4u pk[Q]; Raw v[Q]; };
+  Slot A, B;
+  auto load_round = [&](int r, Slot& sl) {
+    const int e = lo + r * ROUND + lane * V;
+#pragma unroll
+    for (int q = 0; q < Q; ++q) {
+      const int eq = e + 4 * q;
+      const int es = (r < r1 && eq < e_hi) ? eq : lo;  // out-of-range quads re-read a valid one; masked below
+      sl.pk[q] = __builtin_nontemporal_load((const v4u*)(pack + es));
+      sl.v[q] = TLVals<VT>::load(val + es);
+    }
+  };
+  auto process = [&](int r, Slot& sl) {
+    v4u pk[Q];
+    Raw vr[Q];
+#pragma unroll
+    for (int q = 0; q < Q; ++q) { pk[q] = sl.pk[q]; vr[q] = sl.v[q]; }
+    const int e = lo + r * ROUND + lane * V;
+    bool in[V];
+    XT xv[V];
+#pragma unroll
+    for (int q = 0; q < Q; ++q)
+#pragma unroll
+      for (int k = 0; k < 4; ++k) {
+        const int i = 4 * q + k;
+        in[i] = (e + i >= e_lo) && (e + i < e_hi);
+        xv[i] = x[in[i] ? (pk[q][k] >> sbits) : 0u];
+      }
+    if (r + 2 < r1) load_round(r + 2, sl);
+#pragma unroll
+    for (int q = 0; q < Q; ++q) {
+      LT v[4];
+      TLVals<VT>::get(vr[q], v);
+#pragma unroll
+      for (int k = 0; k < 4; ++k) {
+        const int i = 4 * q + k;
+        if (in[i]) {
+          const AT vv = SQ ? static_cast<AT>(v[k]) * static_cast<AT>(v[k]) : static_cast<AT>(v[k]);
+          atomicAdd(&acc[pk[q][k] & smask], vv * static_cast<AT>(xv[i]));
+        }
+      }
+    }
+  };
+  load_round(r0, A);
+  if (r0 + 1 < r1) load_round(r0 + 1, B);
+  for (int r = r0; r < r1; r += 2) {
+    process(r, A);
+    if (r + 1 < r1) process(r + 1, B);
+  }
+}
+
+// pipeline variant: P = 0 two-slot stream prefetch; P = 1 three-stage (stream r+2 / gather r+1 / accumulate r); P = 2 two-slot, 8 entries per lane
 template <typename VT, typename XT, typename AT, bool SQ, int U, int NW, int P>
 __device__ __forceinline__ void tl_stream(const uint32_t* __restrict__ pack, const VT* __restrict__ val,
                                           const XT* __restrict__ x, int e_lo, int e_hi, int sbits, AT* acc) {
   if (P == 1) tl_stream_p1<VT, XT, AT, SQ, U, NW>(pack, val, x, e_lo, e_hi, sbits, acc);
+  else if (P == 2) tl_stream_wide<VT, XT, AT, SQ, NW, 2>(pack, val, x, e_lo, e_hi, sbits, acc);
   else tl_stream_p0<VT, XT, AT, SQ, U, NW>(pack, val, x, e_lo, e_hi, sbits, acc);
 }
 
@@ -934,23 +1000,25 @@ static int g_ablate = 0;      // profiling ablation bits (0 in production)
 static int g_tl_acc64 = 1;   // measured on MI355X: ds_add_f64 accumulation is ~3x faster than ds_add_f32 here
 static int g_tl_waves = 4;     // forward
 static int g_tl_waves_t = 4;   // transpose
-static int g_tl_pipe = 0;      // stream pipeline variant (see tl_stream)
+static int g_tl_pipe = 0;      // forward stream pipeline variant (see tl_stream)
+static int g_tl_pipe_t = 0;    // transpose stream pipeline variant
 
 template <typename VT, typename XT, typename RT, typename AT, int MAXR>
 static void tl_fwd_launch(const TLFwdDesc* c, const void* x, FwdArgs<XT, RT> a, double* stats, hipStream_t st) {
 #define TLF(NW, P) hipLaunchKernelGGL((tl_fwd_kernel<VT, XT, RT, AT, MAXR, 2, NW, P>), dim3(c->nblk), dim3(NW * 64), 0, \
                                     st, c->blk, c->rbits, c->pack, (const VT*)c->val, (const XT*)x, a, stats)
-  if (g_tl_waves == 2) { if (g_tl_pipe) TLF(2, 1); else TLF(2, 0); }
-  else { if (g_tl_pipe) TLF(4, 1); else TLF(4, 0); }
+  if (g_tl_waves == 2) { if (g_tl_pipe == 1) TLF(2, 1); else TLF(2, 0); }
+  else { if (g_tl_pipe == 1) TLF(4, 1); else TLF(4, 0); }
 #undef TLF
 }
 
 template <typename VT, typename XT, typename RT, typename AT, int MAXR>
 static void tl_fwd_multi_launch(const TLFwdMultiDesc* c, const void* x, FwdArgs<XT, RT> a, double* stats,
                                 hipStream_t st) {
-#define TLM(NW) hipLaunchKernelGGL((tl_fwd_multi_kernel<VT, XT, RT, AT, MAXR, 2, NW, 0>), dim3(c->nblk), dim3(NW * 64), \
-                                   0, st, c->blk, c->rbits, c->packs, c->vals, (const XT*)x, a, stats)
-  if (g_tl_waves == 2) TLM(2); else TLM(4);
+#define TLM(NW, P) hipLaunchKernelGGL((tl_fwd_multi_kernel<VT, XT, RT, AT, MAXR, 2, NW, P>), dim3(c->nblk), \
+                                      dim3(NW * 64), 0, st, c->blk, c->rbits, c->packs, c->vals, (const XT*)x, a, stats)
+  if (g_tl_waves == 2) { if (g_tl_pipe == 2) TLM(2, 2); else TLM(2, 0); }
+  else { if (g_tl_pipe == 2) TLM(4, 2); else TLM(4, 0); }
 #undef TLM
 }
 
@@ -995,8 +1063,8 @@ template <typename VT, typename XT, typename AT, bool SQ, int MAXR>
 static void tl_t_launch(const TLTDesc* c, const void* x, double* G, double* parts, hipStream_t st) {
 #define TLT(NW, P) hipLaunchKernelGGL((tl_t_kernel<VT, XT, AT, SQ, MAXR, 2, NW, P>), dim3(c->nitems), dim3(NW * 64), 0, \
                                     st, c->items, c->cbits, c->pack, (const VT*)c->val, (const XT*)x, G, c->dim, parts)
-  if (g_tl_waves_t == 2) { if (g_tl_pipe) TLT(2, 1); else TLT(2, 0); }
-  else { if (g_tl_pipe) TLT(4, 1); else TLT(4, 0); }
+  if (g_tl_waves_t == 2) { if (g_tl_pipe_t == 1) TLT(2, 1); else TLT(2, 0); }
+  else { if (g_tl_pipe_t == 1) TLT(4, 1); else TLT(4, 0); }
 #undef TLT
 }
 
@@ -1031,9 +1099,11 @@ static int tl_t_impl(const TLTDesc* c, const void* x, double* G, double* parts, 
 
 template <typename VT, typename XT, typename AT, bool SQ, int MAXR>
 static void tl_t_multi_launch(const TLTMultiDesc* c, const void* x, double* G, double* parts, hipStream_t st) {
-#define TLTM(NW) hipLaunchKernelGGL((tl_t_multi_kernel<VT, XT, AT, SQ, MAXR, 2, NW, 0>), dim3(c->nitems), dim3(NW * 64), \
-                                    0, st, c->items, c->cbits, c->packs, c->vals, (const XT*)x, G, c->dim, parts)
-  if (g_tl_waves_t == 2) TLTM(2); else TLTM(4);
+#define TLTM(NW, P) hipLaunchKernelGGL((tl_t_multi_kernel<VT, XT, AT, SQ, MAXR, 2, NW, P>), dim3(c->nitems), \
+                                       dim3(NW * 64), 0, st, c->items, c->cbits, c->packs, c->vals, (const XT*)x, G, \
+                                       c->dim, parts)
+  if (g_tl_waves_t == 2) { if (g_tl_pipe_t == 2) TLTM(2, 2); else TLTM(2, 0); }
+  else { if (g_tl_pipe_t == 2) TLTM(4, 2); else TLTM(4, 0); }
 #undef TLTM
 }
 
@@ -1270,7 +1340,7 @@ int pml_reduce_stats(const double* stats, int n, double* out, int accumulate, do
 // ---- tiled layout entry points ------------------------------------------------------------------------------
 int pml_tl_maxbits() { return TL_MAXBITS; }
 void pml_tl_config(int acc64, int waves, int waves_t, int pipe) {
-  g_tl_acc64 = acc64; g_tl_waves = waves == 2 ? 2 : 4; g_tl_waves_t = waves_t == 2 ? 2 : 4; g_tl_pipe = pipe ? 1 : 0;
+  g_tl_acc64 = acc64; g_tl_waves = waves == 2 ? 2 : 4; g_tl_waves_t = waves_t == 2 ? 2 : 4; g_tl_pipe = pipe & 3; g_tl_pipe_t = (pipe >> 2) & 3;
 }
 
 int pml_tl_fwd(int prec, const TLFwdDesc* c, const void* x, int mode, int loss, double shift, const void* y,

@@ -106,7 +106,7 @@ def glm_lib() -> Optional[ctypes.CDLL]:
 # Kernel configuration defaults (tuned on MI355X, see profiles/): forward = vector layout + 8192-entry LDS hot
 # table of the most frequent features; transpose = strided layout. Env overrides for experiments:
 # PML_FWD_STRIDED, PML_T_STRIDED, PML_HOT_N, PML_FWD_GRID.
-KERNEL_CONFIG = {"fwd_strided": 0, "t_strided": 0, "hot_n": 0, "fwd_grid": 1024, "tl_acc64": 1, "tl_waves": 2, "tl_waves_t": 4, "tl_pipe": 0, "tl_multi": 1}
+KERNEL_CONFIG = {"fwd_strided": 0, "t_strided": 0, "hot_n": 0, "fwd_grid": 1024, "tl_acc64": 1, "tl_waves": 2, "tl_waves_t": 4, "tl_pipe": 0, "tl_pipe_t": 0, "tl_multi": 1}
 
 
 def configure(**kw):
@@ -120,7 +120,7 @@ def configure(**kw):
         lib.pml_set_config(KERNEL_CONFIG["fwd_strided"], KERNEL_CONFIG["t_strided"], KERNEL_CONFIG["hot_n"],
                            KERNEL_CONFIG["fwd_grid"])
         lib.pml_tl_config(KERNEL_CONFIG["tl_acc64"], KERNEL_CONFIG["tl_waves"], KERNEL_CONFIG["tl_waves_t"],
-                          KERNEL_CONFIG["tl_pipe"])
+                          (KERNEL_CONFIG["tl_pipe"] & 3) | ((KERNEL_CONFIG["tl_pipe_t"] & 3) << 2))
     return dict(KERNEL_CONFIG)
 
 

@@ -212,3 +212,29 @@ def test_tl_multi_launch_matches_per_chunk(col_windows):
     assert res[0][0] == res[1][0] and res[0][1] == res[1][1] and torch.equal(res[0][3], res[1][3])
     for a, b in zip(res[0][2:], res[1][2:]):
         assert torch.allclose(a, b, rtol=1e-12, atol=1e-12 * float(a.abs().max()))
+
+
+@pytest.mark.parametrize("pipe", [0, 1, 2])
+@pytest.mark.parametrize("precision", ["f64", "bf16"])
+def test_tl_stream_variants(pipe, precision):
+    """Every stream pipeline variant (two-slot, three-stage, two-slot 8 entries/lane) x per-chunk / shard-wide
+    launches against the fp64 reference."""
+    from photon_ml_amd.ops.device import DeviceGLMData
+    from photon_ml_amd.ops.native import configure
+    data = make_data(n=7000, d=900, density=0.01, seed=6)
+    if precision == "bf16":
+        data = _round_bf16(data)
+    ref = TorchGLMData(data, "cpu")
+    dev = DeviceGLMData.from_labeled(data, "cuda", precision, chunk_rows=2500, layout="tiled", item_entries=700)
+    w = torch.from_numpy(np.random.default_rng(1).normal(size=900) * 0.1)
+    wd = w.float().double() if precision == "bf16" else w
+    f0, _, g0 = ref.value_grad_sums(LOGISTIC, wd, 0.0)
+    try:
+        for multi in (0, 1):
+            configure(tl_pipe=pipe, tl_pipe_t=pipe, tl_multi=multi)
+            f1, _, g1 = dev.value_grad_sums(LOGISTIC, wd.cuda(), 0.0)
+            tol = TOL[precision]
+            assert abs(f1 - f0) <= tol * abs(f0), (multi, f1, f0)
+            assert torch.allclose(g1.cpu(), g0, rtol=tol, atol=tol * float(g0.abs().max())), multi
+    finally:
+        configure(tl_pipe=0, tl_pipe_t=0, tl_multi=1)
