@@ -15,7 +15,15 @@ of the packed fp64 [gradient | loss | sum l'] buffer. Nothing is skipped inside 
 
 value = (total rows over all ranks) x (L-BFGS iterations) / seconds  [examples/sec/node].
 
-Usage: python bench.py [--gpus N --steps K --warmup W]; for N > 1 launch with torch.distributed.run.
+Other BASELINE.json configs (``--config``; per-GPU shapes are the 8-GPU configs divided by 8):
+
+* ``lbfgs``  (default, headline): logistic + L2, L-BFGS, 125M rows/GPU x 1M features;
+* ``owlqn``: logistic + L1 (OWL-QN), 125M rows/GPU x 10M features (config "1B rows x 10M sparse feats, 8 GPUs");
+* ``tron``:  Poisson + L2, TRON (one STEP = one outer trust-region iteration incl. its Hessian-vector CG passes),
+  62.5M rows/GPU x 1M features (config "Poisson regression TRON, 500M rows, 8 GPUs").
+
+Usage: python bench.py [--gpus N --steps K --warmup W] [--config lbfgs|owlqn|tron]; for N > 1 launch with
+torch.distributed.run.
 """
 from __future__ import annotations
 
@@ -31,21 +39,39 @@ def log(msg):
         print(f"[bench {time.strftime('%H:%M:%S')}] {msg}", file=sys.stderr, flush=True)
 
 
+CONFIGS = {
+    "lbfgs": {"rows_per_gpu": 125_000_000, "features": 1_000_000, "task": "LOGISTIC_REGRESSION",
+              "model": "logistic_regression_l2_lbfgs", "metric": "examples/sec/node, logistic L-BFGS 1B×1M-sparse"},
+    "owlqn": {"rows_per_gpu": 125_000_000, "features": 10_000_000, "task": "LOGISTIC_REGRESSION",
+              "model": "logistic_regression_l1_owlqn",
+              "metric": "examples/sec/node, logistic OWL-QN (L1) 1B×10M-sparse"},
+    "tron": {"rows_per_gpu": 62_500_000, "features": 1_000_000, "task": "POISSON_REGRESSION",
+             "model": "poisson_regression_l2_tron", "metric": "examples/sec/node, Poisson TRON 500M×1M-sparse"},
+}
+
+
 def main():
     ap = argparse.ArgumentParser()
     ap.add_argument("--gpus", type=int, default=1)
     ap.add_argument("--steps", type=int, default=10)
     ap.add_argument("--warmup", type=int, default=3)
-    ap.add_argument("--rows-per-gpu", type=int, default=125_000_000)
-    ap.add_argument("--features", type=int, default=1_000_000)
+    ap.add_argument("--config", default="lbfgs", choices=list(CONFIGS))
+    ap.add_argument("--rows-per-gpu", type=int, default=None)
+    ap.add_argument("--features", type=int, default=None)
     ap.add_argument("--nnz", type=int, default=100)
     ap.add_argument("--precision", default="bf16", choices=["bf16", "f32", "f64"])
     ap.add_argument("--chunk-rows", type=int, default=1 << 20)
     ap.add_argument("--l2", type=float, default=1.0)
+    ap.add_argument("--l1", type=float, default=10.0, help="L1 weight of the owlqn config")
     ap.add_argument("--seed", type=int, default=1234567890)
     ap.add_argument("--layout", default="auto", choices=["auto", "tiled", "segmented"],
                     help="sparse layout: tiled (gather-coalesced, default when representable) or segmented")
     args = ap.parse_args()
+    cfg = CONFIGS[args.config]
+    if args.rows_per_gpu is None:
+        args.rows_per_gpu = cfg["rows_per_gpu"]
+    if args.features is None:
+        args.features = cfg["features"]
 
     import torch
     from photon_ml_amd.parallel.dist import init_distributed, DistributedGLMData, all_reduce_scalar, barrier
@@ -57,9 +83,10 @@ def main():
     dev = torch.device("cuda", local)
 
     from photon_ml_amd.data.synthetic import generate_device_shard
-    from photon_ml_amd.function.losses import LOGISTIC
+    from photon_ml_amd.function.losses import LOGISTIC, POISSON
     from photon_ml_amd.function.objective import GLMObjective
-    from photon_ml_amd.optimization.lbfgs import LBFGS
+    from photon_ml_amd.optimization.lbfgs import LBFGS, OWLQN
+    from photon_ml_amd.optimization.tron import TRON
 
     t_gen = time.time()
     last = [time.time()]
@@ -71,14 +98,21 @@ def main():
 
     data, _ = generate_device_shard(args.rows_per_gpu, args.features, args.nnz, dev, args.precision,
                                     seed=args.seed, chunk_rows=args.chunk_rows, rank=rank, progress=progress,
-                                    layout=args.layout)
+                                    layout=args.layout, task=cfg["task"])
     torch.cuda.synchronize()
     log(f"data ready in {time.time() - t_gen:.1f}s: {data.n_rows} rows/GPU, {data.nbytes() / 2**30:.1f} GiB/GPU, "
         f"layout={data.layout}")
     gdata = DistributedGLMData(data) if world > 1 else data
 
-    obj = GLMObjective(LOGISTIC, l2_weight=args.l2)
-    opt = LBFGS(tolerance=0.0, max_iterations=10 ** 9, track_state=False)
+    if args.config == "owlqn":
+        obj = GLMObjective(LOGISTIC, l2_weight=0.0)
+        opt = OWLQN(args.l1, tolerance=0.0, max_iterations=10 ** 9, track_state=False)
+    elif args.config == "tron":
+        obj = GLMObjective(POISSON, l2_weight=args.l2)
+        opt = TRON(tolerance=0.0, max_iterations=10 ** 9, track_state=False)
+    else:
+        obj = GLMObjective(LOGISTIC, l2_weight=args.l2)
+        opt = LBFGS(tolerance=0.0, max_iterations=10 ** 9, track_state=False)
     w0 = torch.zeros(args.features, dtype=torch.float64, device=dev)
     opt.start(obj, gdata, w0, skip_zero_tolerance_pass=True)
     for i in range(args.warmup):
@@ -102,7 +136,7 @@ def main():
         log(f"final f={st.loss:.6e} |g|={st.grad_norm():.3e} evals/step={passes / args.steps:.2f} "
             f"optimizer_stalled={stalled}")
         out = {
-            "metric": "examples/sec/node, logistic L-BFGS 1B×1M-sparse",
+            "metric": cfg["metric"],
             "value": value,
             "unit": "examples/sec",
             "n_gpus": world,
@@ -115,7 +149,7 @@ def main():
             "dtype": args.precision,
             "data": "synthetic (on-device Zipf hashed-categorical sparse rows, random ground-truth labels)",
             "config": {
-                "model": "logistic_regression_l2_lbfgs",
+                "model": cfg["model"],
                 "global_batch": total_rows,
                 "seq_len": None,
                 "rows_per_gpu": args.rows_per_gpu,
