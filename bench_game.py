@@ -13,7 +13,12 @@ One STEP = one full coordinate-descent sweep: fixed-effect L-BFGS (``--fe-iters`
 random-effect scores, then the batched per-entity TRON (``--re-iters`` iterations) on offsets = fixed-effect
 scores, both rescored, plus the training-loss evaluation. Nothing is skipped inside the timed region.
 
-Usage: python bench_game.py [--gpus N --steps K --warmup W]; for N > 1 launch with torch.distributed.run.
+``--config game5`` = BASELINE.json config 5 at its per-GPU shape: 10M entities x 1k coefficients each over 8
+GPUs -> 1.25M entities per GPU, 20 rows x 50 features per entity covering each entity's 1000-feature pool exactly
+(+ intercept: 1001 coefficients per entity), integer entity ids, 1M-feature fixed effect.
+
+Usage: python bench_game.py [--gpus N --steps K --warmup W] [--config small|game5]; for N > 1 launch with
+torch.distributed.run.
 """
 from __future__ import annotations
 
@@ -29,22 +34,36 @@ def log(msg):
         print(f"[bench_game {time.strftime('%H:%M:%S')}] {msg}", file=sys.stderr, flush=True)
 
 
+PRESETS = {
+    "small": dict(entities_per_gpu=200_000, rows_per_entity=50, re_dim=100, re_nnz=10, fe_dim=1_000_000, fe_nnz=30,
+                  pool="random", int_ids=0),
+    "game5": dict(entities_per_gpu=1_250_000, rows_per_entity=20, re_dim=1000, re_nnz=50, fe_dim=1_000_000,
+                  fe_nnz=30, pool="exact", int_ids=1),
+}
+
+
 def main():
     ap = argparse.ArgumentParser()
     ap.add_argument("--gpus", type=int, default=1)
     ap.add_argument("--steps", type=int, default=3)
     ap.add_argument("--warmup", type=int, default=1)
-    ap.add_argument("--entities-per-gpu", type=int, default=200_000)
-    ap.add_argument("--rows-per-entity", type=int, default=50)
-    ap.add_argument("--re-dim", type=int, default=100)
-    ap.add_argument("--re-nnz", type=int, default=10)
-    ap.add_argument("--fe-dim", type=int, default=1_000_000)
-    ap.add_argument("--fe-nnz", type=int, default=30)
+    ap.add_argument("--config", default="small", choices=list(PRESETS))
+    ap.add_argument("--entities-per-gpu", type=int)
+    ap.add_argument("--rows-per-entity", type=int)
+    ap.add_argument("--re-dim", type=int)
+    ap.add_argument("--re-nnz", type=int)
+    ap.add_argument("--fe-dim", type=int)
+    ap.add_argument("--fe-nnz", type=int)
+    ap.add_argument("--pool", choices=["random", "exact"])
+    ap.add_argument("--int-ids", type=int)
     ap.add_argument("--fe-iters", type=int, default=10)
     ap.add_argument("--re-iters", type=int, default=10)
     ap.add_argument("--precision", default="bf16", choices=["bf16", "f32", "f64"])
     ap.add_argument("--seed", type=int, default=11)
     args = ap.parse_args()
+    for k, v in PRESETS[args.config].items():
+        if getattr(args, k) is None:
+            setattr(args, k, v)
 
     import numpy as np
     import torch
@@ -69,7 +88,8 @@ def main():
     t0 = time.time()
     data = generate_game_bench_data(args.entities_per_gpu, args.rows_per_entity, args.re_dim, args.re_nnz,
                                     args.fe_dim, args.fe_nnz, seed=args.seed + 1000 * rank,
-                                    entity_offset=rank * args.entities_per_gpu)
+                                    entity_offset=rank * args.entities_per_gpu, pool=args.pool,
+                                    int_ids=bool(args.int_ids))
     log(f"data generated in {time.time() - t0:.1f}s: {data.n_rows} rows/GPU")
     t0 = time.time()
     fe_cfg = GLMOptimizationConfiguration(OptimizerConfig("LBFGS", args.fe_iters, 1e-12),
@@ -119,7 +139,7 @@ def main():
             "vs_baseline": None,
             "dtype": args.precision,
             "data": "synthetic (Zipf fixed-effect features, per-entity private random-effect features)",
-            "config": {"model": "game_logistic_fe_lbfgs_re_tron", "global_batch": total_rows, "seq_len": None,
+            "config": {"model": "game_logistic_fe_lbfgs_re_tron", "preset": args.config, "global_batch": total_rows, "seq_len": None,
                        "entities": args.entities_per_gpu * world, "rows_per_entity": args.rows_per_entity,
                        "re_dim": args.re_dim, "fe_dim": args.fe_dim, "fe_iters": args.fe_iters,
                        "re_iters": args.re_iters, "parallelism": f"dp{world}+ep{world}"},

@@ -176,7 +176,7 @@ class RandomEffectCoordinate(Coordinate):
             return self._W[key]
         W = torch.zeros(B, d, dtype=dt, device=dev)
         ds = self.dataset
-        if model is not None and len(model.keys) and ds.projector_type.kind.value == "INDEX_MAP":
+        if model is not None and model.nnz and ds.projector_type.kind.value == "INDEX_MAP":
             # map original-space coefficients into each entity's local index space
             ptr, feat = ds.projection.ptr, ds.projection.feat
             ents = bucket.entities
@@ -252,12 +252,12 @@ class RandomEffectCoordinate(Coordinate):
         self._W["seg"] = res.W
         act = torch.from_numpy(ds.n_active > 0).to(res.iters.device)
         self.last_stats = random_effect_tracker_stats(res.iters[act], res.reason[act], time.time() - t_start)
-        W = res.W.detach().cpu().numpy()
+        W = res.W.detach()
         var = None
         if self.compute_variance and self.loss.twice_differentiable:
-            var = (1.0 / (seg.hdiag(self.loss, res.W, l2) + EPSILON)).detach().cpu().numpy()
-        keys = ds.projection.keys  # entity * dim + feature, sorted, aligned with W
-        nz = W != 0
+            var = 1.0 / (seg.hdiag(self.loss, res.W, l2) + EPSILON)
+        keys = ds.projection_keys_t  # entity * dim + feature, sorted, aligned with W (device)
+        nz = torch.nonzero(W != 0).squeeze(1)  # device compaction; the model stays resident (host copy lazily)
         out = RandomEffectModel(self.data_config.random_effect_type, self.data_config.feature_shard_id, self.task,
                                 ds.entity_ids, ds.dim, keys[nz], W[nz], None if var is None else var[nz])
         self._last = (out, res.W)
@@ -269,15 +269,15 @@ class RandomEffectCoordinate(Coordinate):
         prev = self._W.get("seg")
         if prev is not None and prev.numel() == ds.d_total:
             return prev
-        if model is None or not len(model.keys):
+        if model is None or model.nnz == 0:
             return torch.zeros(ds.d_total, dtype=torch.float64, device=dev)
-        ent = np.repeat(np.arange(ds.n_entities), np.diff(ds.projection.ptr))
-        mi = model.entity_index(ds.entity_ids)[ent]
-        k = mi.astype(np.int64) * model.dim + ds.projection.feat
-        pos = np.searchsorted(model.keys, k)
-        pos_c = np.minimum(pos, len(model.keys) - 1)
-        hit = (pos < len(model.keys)) & (model.keys[pos_c] == k) & (mi >= 0)
-        return torch.from_numpy(np.where(hit, model.values[pos_c], 0.0)).to(dev)
+        # map (entity, feature) of every projected coefficient to the model's entity numbering, look up on device
+        mi = torch.from_numpy(model.entity_index(ds.entity_ids).astype(np.int64)).to(dev)[ds.col_entity_t]
+        k = mi * model.dim + ds.projection_keys_t % ds.dim
+        mk, mv = model.tensors(dev)
+        pos = torch.searchsorted(mk, k).clamp(max=mk.numel() - 1)
+        hit = (mk[pos] == k) & (mi >= 0)
+        return torch.where(hit, mv[pos], torch.zeros_like(mv[pos]))
 
     def _to_original(self, bucket, W: torch.Tensor, var: Optional[torch.Tensor]):
         ds = self.dataset
@@ -324,8 +324,8 @@ class RandomEffectCoordinate(Coordinate):
 
     def regularization_term_value(self, model: RandomEffectModel) -> float:
         reg, lam = self.opt_config.regularization_context, self.opt_config.regularization_weight
-        v = model.values
-        return reg.l1_weight(lam) * float(np.abs(v).sum()) + 0.5 * reg.l2_weight(lam) * float((v * v).sum())
+        a, q = model.sum_abs_and_sq()
+        return reg.l1_weight(lam) * a + 0.5 * reg.l2_weight(lam) * q
 
 
 class ShardedRandomEffectCoordinate(Coordinate):

@@ -168,15 +168,30 @@ class RandomEffectDataset:
         self.score_mask[active_rows] = True
         self.score_mask[passive_rows] = True
         # ---- feature selection (Pearson) on active rows
-        xa = x[active_rows]
+        xa = x if len(active_rows) == n else x[active_rows]  # no copy when every row is active
         ea = ent[active_rows]
         self.feature_keep = None
         if config.features_to_samples_ratio is not None:
             xa = self._pearson_filter(xa, ea, data.response[active_rows], config.features_to_samples_ratio)
         self.x_active = xa
-        # ---- projection
         pt = config.projector_type
         self.projector_type = pt
+        n_act = np.bincount(ea, minlength=n_ent)
+        self.n_active = n_act
+        if layout == "auto":
+            layout = "segmented" if (pt.kind == ProjectorKind.INDEX_MAP and self.device.type == "cuda") else "dense"
+        if layout == "segmented" and pt.kind != ProjectorKind.INDEX_MAP:
+            raise ValueError("the segmented random-effect layout needs the INDEX_MAP projector")
+        self.layout = layout
+        self.buckets = []
+        self.seg = None
+        wts = weight_mult * data.weights
+        if layout == "segmented" and self.device.type == "cuda":
+            # GPU build: projection + entity-sorted block-diagonal layout computed on the device
+            self._make_segmented_device(x, xa, ea, ent, active_rows, passive_rows, data.response, wts, n_ent)
+            self.d_local = self.projection.local_dims()
+            return
+        # ---- projection
         if pt.kind == ProjectorKind.INDEX_MAP:
             coo = xa.tocoo()
             e_all = ea[coo.row]
@@ -194,20 +209,11 @@ class RandomEffectDataset:
             d_local = np.full(n_ent, self.dim, dtype=np.int64)
         self.d_local = d_local
         # ---- buckets (dense) or one block-diagonal problem (segmented)
-        n_act = np.bincount(ea, minlength=n_ent)
-        self.n_active = n_act
-        if layout == "auto":
-            layout = "segmented" if (pt.kind == ProjectorKind.INDEX_MAP and self.device.type == "cuda") else "dense"
-        if layout == "segmented" and pt.kind != ProjectorKind.INDEX_MAP:
-            raise ValueError("the segmented random-effect layout needs the INDEX_MAP projector")
-        self.layout = layout
-        self.buckets = []
-        self.seg = None
         if layout == "segmented":
-            self._make_segmented(xa, ea, active_rows, data.response, weight_mult * data.weights, n_ent)
+            self._make_segmented(xa, ea, active_rows, data.response, wts, n_ent)
         else:
-            self.buckets = self._make_buckets(xa, ea, active_rows, data.response, weight_mult * data.weights,
-                                              n_act, d_local, bucket_elems)
+            self.buckets = self._make_buckets(xa, ea, active_rows, data.response, wts, n_act, d_local,
+                                              bucket_elems)
 
     # ------------------------------------------------------------------
     def _pearson_filter(self, xa: sp.csr_matrix, ea: np.ndarray, y: np.ndarray, ratio: float) -> sp.csr_matrix:
@@ -320,10 +326,60 @@ class RandomEffectDataset:
         dev = glm.device
         col_entity = np.repeat(np.arange(n_ent, dtype=np.int64), np.diff(self.projection.ptr))
         self.seg_rows = torch.from_numpy(rows).to(dev)
+        self.projection_keys_t = torch.from_numpy(self.projection.keys).to(dev)
+        self.col_entity_t = torch.from_numpy(col_entity).to(dev)
         self.seg = SegmentedGLMData(glm, torch.from_numpy(e_row.astype(np.int64)).to(dev),
-                                    torch.from_numpy(col_entity).to(dev), n_ent,
+                                    self.col_entity_t, n_ent,
                                     torch.from_numpy(yy).to(dev), torch.from_numpy(ww).to(dev),
                                     torch.zeros(len(rows), dtype=torch.float64, device=dev))
+        self.d_total = d_total
+
+    def _make_segmented_device(self, x, xa, ea, ent, active_rows, passive_rows, y, wts, n_ent):
+        """Device build of the block-diagonal problem (K14 on the GPU): rows sorted by entity (stable), the
+        INDEX_MAP projection = sorted unique ``entity * D + feature`` keys of the active (+ passive) non-zeros,
+        each non-zero's block column = its key's rank; then the tiled layout is built from the device CSR."""
+        from ..ops.device import DeviceGLMData
+        from ..optimization.batched import SegmentedGLMData
+        dev, D = self.device, self.dim
+        xa = xa.tocsr()
+        ip = torch.from_numpy(xa.indptr.astype(np.int64)).to(dev)
+        ea_t = torch.from_numpy(ea.astype(np.int64)).to(dev)
+        order = torch.argsort(ea_t, stable=True)
+        lens = (ip[1:] - ip[:-1])[order]
+        nip = torch.zeros(len(ea) + 1, dtype=torch.int64, device=dev)
+        torch.cumsum(lens, 0, out=nip[1:])
+        nnz = int(nip[-1])
+        src = torch.repeat_interleave(ip[:-1][order] - nip[:-1], lens, output_size=nnz)
+        src += torch.arange(nnz, device=dev)
+        del ip
+        col = torch.from_numpy(xa.indices).to(dev)[src].to(torch.int64)
+        val = torch.from_numpy(xa.data).to(dev, torch.float64)[src]
+        del src
+        e_row = ea_t[order]
+        key = torch.repeat_interleave(e_row, lens, output_size=nnz) * D + col
+        del col, lens
+        allk = key
+        if len(passive_rows):
+            cp = x[passive_rows].tocoo()
+            pk = torch.from_numpy(ent[passive_rows][cp.row].astype(np.int64) * D + cp.col.astype(np.int64))
+            allk = torch.cat([key, pk.to(dev)])
+        ukeys = torch.unique(allk, sorted=True)
+        del allk
+        self.projection = IndexMapProjection.from_sorted_keys(ukeys, n_ent, D)
+        pos = torch.searchsorted(ukeys, key)
+        del key
+        d_total = int(ukeys.numel())
+        rows_t = torch.from_numpy(active_rows.astype(np.int64)).to(dev)[order]
+        yy = torch.from_numpy(np.asarray(y, dtype=np.float64)).to(dev)[rows_t]
+        ww = torch.from_numpy(np.asarray(wts, dtype=np.float64)).to(dev)[rows_t]
+        glm = DeviceGLMData.from_device_csr(nip, pos, val, yy, torch.zeros_like(yy), ww, max(d_total, 1), dev,
+                                            "f64", col_windows=True)
+        del pos, val
+        self.projection_keys_t = ukeys
+        self.col_entity_t = ukeys // D
+        self.seg_rows = rows_t
+        self.seg = SegmentedGLMData(glm, e_row, self.col_entity_t, n_ent, yy, ww,
+                                    torch.zeros_like(yy))
         self.d_total = d_total
 
     @property

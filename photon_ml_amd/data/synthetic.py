@@ -159,14 +159,19 @@ def generate_device_shard(n_rows: int, n_features: int, nnz_per_row: int, device
 
 def generate_game_bench_data(n_entities: int, rows_per_entity: int, re_dim: int = 100, re_nnz: int = 10,
                              fe_dim: int = 100_000, fe_nnz: int = 30, re_vocab: int = 1 << 20, seed: int = 7,
-                             entity_offset: int = 0, task: str = "LOGISTIC_REGRESSION"):
+                             entity_offset: int = 0, task: str = "LOGISTIC_REGRESSION", pool: str = "random",
+                             int_ids: bool = False):
     """Synthetic GAME data at benchmark scale (vectorised, no per-row Python):
 
     * ``global`` shard: ``fe_nnz`` Zipf(1.1) features out of ``fe_dim`` + intercept (last column);
     * ``entity`` shard: each entity draws its ``re_nnz`` features per row from a private pool of ``re_dim``
       features of a ``re_vocab`` hashed vocabulary (+ intercept) -> after INDEX_MAP projection every entity has
       ~``re_dim`` coefficients;
-    * id tag ``entityId`` = ``e<global entity index>`` (``entity_offset`` shifts the range, e.g. per rank);
+    * ``pool="exact"``: instead of random draws, row j of an entity takes pool slots ``[j * re_nnz, (j + 1) *
+      re_nnz) mod re_dim`` — every entity then has exactly ``min(re_dim, rows * re_nnz)`` coefficients (e.g. the
+      "1k coefficients per entity" GAME config with 20 rows x 50 features);
+    * id tag ``entityId`` = ``e<global entity index>`` (or the integer index with ``int_ids``; ``entity_offset``
+      shifts the range, e.g. per rank);
     * labels from a random ground truth (logistic / linear / Poisson).
     """
     from ..data.game_data import GameData
@@ -188,24 +193,44 @@ def generate_game_bench_data(n_entities: int, rows_per_entity: int, re_dim: int 
                        shape=(n, fe_dim))
     xg.eliminate_zeros()
     # random effect shard: pool slot k of entity e -> feature (hash(e) + k * stride) % re_vocab
-    slot = rng.integers(0, re_dim, size=(n, re_nnz))
-    slot = np.sort(slot, axis=1)
-    rdup = np.zeros_like(slot, dtype=bool)
-    rdup[:, 1:] = slot[:, 1:] == slot[:, :-1]
+    if pool == "exact":
+        if re_nnz > re_dim:
+            raise ValueError("pool='exact' needs re_nnz <= re_dim")
+        srt = np.argsort(ent, kind="stable")
+        within = np.empty(n, dtype=np.int64)
+        within[srt] = np.arange(n) - np.repeat(np.arange(n_entities) * rows_per_entity, rows_per_entity)
+        slot = (within[:, None] * re_nnz + np.arange(re_nnz)[None, :]) % re_dim
+        del srt, within
+        slot.sort(axis=1)
+        rdup = None
+    else:
+        slot = rng.integers(0, re_dim, size=(n, re_nnz))
+        slot = np.sort(slot, axis=1)
+        rdup = np.zeros_like(slot, dtype=bool)
+        rdup[:, 1:] = slot[:, 1:] == slot[:, :-1]
     gid = ent + entity_offset
     base = (gid * 2654435761) % (re_vocab - 1)
     rcol = (base[:, None] + slot * 40503) % (re_vocab - 1)
-    rval = np.where(rdup, 0.0, rng.normal(size=(n, re_nnz)))
-    xr = sp.csr_matrix((np.concatenate([rval, np.ones((n, 1))], 1).ravel(),
-                        np.concatenate([rcol, np.full((n, 1), re_vocab - 1)], 1).ravel(),
-                        np.arange(0, n * (re_nnz + 1) + 1, re_nnz + 1)), shape=(n, re_vocab))
-    xr.sum_duplicates()
-    xr.eliminate_zeros()
+    rval = rng.normal(size=(n, re_nnz)) if rdup is None else np.where(rdup, 0.0, rng.normal(size=(n, re_nnz)))
+    rc = np.empty((n, re_nnz + 1), dtype=np.int32)
+    rc[:, :re_nnz] = rcol
+    rc[:, re_nnz] = re_vocab - 1
+    del rcol
+    rv = np.empty((n, re_nnz + 1))
+    rv[:, :re_nnz] = rval
+    rv[:, re_nnz] = 1.0
+    xr = sp.csr_matrix((rv.ravel(), rc.ravel(), np.arange(0, n * (re_nnz + 1) + 1, re_nnz + 1, dtype=np.int64)),
+                       shape=(n, re_vocab))
+    del rc, rv
+    if rdup is not None:
+        xr.sum_duplicates()
+        xr.eliminate_zeros()
     # ground truth
     wg = rng.normal(size=fe_dim) * 0.2
     wg[-1] = -0.5
     w_slot = np.random.default_rng(seed + 1).normal(size=re_dim) * 0.5
-    zr = np.where(rdup, 0.0, rval * w_slot[slot]).sum(1) + 0.3 * np.sin(gid)
+    zr = (rval * w_slot[slot] if rdup is None else np.where(rdup, 0.0, rval * w_slot[slot])).sum(1) + 0.3 * np.sin(gid)
+    del rval, slot
     z = np.asarray(xg @ wg).ravel() + zr
     task = TaskType.parse(task)
     if task == TaskType.LOGISTIC_REGRESSION:
@@ -214,5 +239,5 @@ def generate_game_bench_data(n_entities: int, rows_per_entity: int, re_dim: int 
         y = rng.poisson(np.exp(np.clip(z * 0.3, -10, 3))).astype(np.float64)
     else:
         y = z + 0.1 * rng.normal(size=n)
-    ids = np.char.add("e", gid.astype(str)).astype(object)
+    ids = gid.copy() if int_ids else np.char.add("e", gid.astype(str)).astype(object)
     return GameData(y, {"global": xg, "entity": xr}, {"entityId": ids})

@@ -50,13 +50,28 @@ class FixedEffectModel:
 
 
 class RandomEffectModel:
+    """Per-entity GLMs of one random-effect coordinate, stored entity-major as sorted ``key = entity * dim +
+    feature`` with values (and optional variances) — the whole coordinate's models as three flat arrays.
+
+    The arrays may be numpy (host) or torch tensors (e.g. device-resident, straight out of the block-diagonal
+    solver): ``keys`` / ``values`` / ``variances`` give host numpy views (copied from the device once, lazily),
+    ``tensors(device)`` gives torch tensors without a host round trip (scoring, regularization term, warm start).
+    """
+
     def __init__(self, random_effect_type: str, feature_shard_id: str, task: TaskType, entity_ids: np.ndarray,
-                 dim: int, keys: np.ndarray, values: np.ndarray, variances: Optional[np.ndarray] = None):
+                 dim: int, keys, values, variances=None):
         self.random_effect_type = random_effect_type
         self.feature_shard_id = feature_shard_id
         self._task = TaskType.parse(task)
         self.entity_ids = np.asarray(entity_ids)
         self.dim = int(dim)
+        self._host = None
+        self._dev = None
+        if isinstance(keys, torch.Tensor):
+            # solver output: keys already sorted (entity-major projection order)
+            self._dev = (keys.to(torch.int64), values.to(torch.float64),
+                         None if variances is None else variances.to(torch.float64))
+            return
         keys = np.asarray(keys, dtype=np.int64)
         values = np.asarray(values, dtype=np.float64)
         if len(keys) > 1 and not bool(np.all(keys[1:] >= keys[:-1])):  # solvers emit sorted keys: skip the sort
@@ -64,9 +79,46 @@ class RandomEffectModel:
             keys, values = keys[order], values[order]
             if variances is not None:
                 variances = np.asarray(variances)[order]
-        self.keys = keys
-        self.values = values
-        self.variances = None if variances is None else np.asarray(variances, dtype=np.float64)
+        self._host = (keys, values, None if variances is None else np.asarray(variances, dtype=np.float64))
+
+    def _h(self):
+        if self._host is None:
+            k, v, var = self._dev
+            self._host = (k.cpu().numpy(), v.cpu().numpy(), None if var is None else var.cpu().numpy())
+        return self._host
+
+    @property
+    def keys(self) -> np.ndarray:
+        return self._h()[0]
+
+    @property
+    def values(self) -> np.ndarray:
+        return self._h()[1]
+
+    @property
+    def variances(self) -> Optional[np.ndarray]:
+        if self._host is None and self._dev is not None and self._dev[2] is None:
+            return None
+        return self._h()[2]
+
+    @property
+    def nnz(self) -> int:
+        return int(self._dev[0].numel()) if self._dev is not None else len(self._host[0])
+
+    def tensors(self, device):
+        """(keys, values) as torch tensors on ``device`` (no host copy when already resident there)."""
+        dev = torch.device(device)
+        if self._dev is not None:
+            return self._dev[0].to(dev), self._dev[1].to(dev)
+        return torch.from_numpy(self._host[0]).to(dev), torch.from_numpy(self._host[1]).to(dev)
+
+    def sum_abs_and_sq(self):
+        """(sum |w|, sum w^2) over all coefficients (regularization term value), computed where they live."""
+        if self._dev is not None:
+            v = self._dev[1]
+            return float(v.abs().sum()), float((v * v).sum())
+        v = self._host[1]
+        return float(np.abs(v).sum()), float((v * v).sum())
 
     @property
     def task(self) -> TaskType:
@@ -107,7 +159,7 @@ class RandomEffectModel:
         """Score every sample whose entity has a model (K6): sum_j x_ij * w_{e(i), j}."""
         x = data.shard(self.feature_shard_id)
         n = x.shape[0]
-        if len(self.keys) == 0:
+        if self.nnz == 0:
             return torch.zeros(n, dtype=torch.float64, device=device)
         ent = self.entity_index(data.id_tags[self.random_effect_type])
         if mask is not None:
@@ -116,8 +168,7 @@ class RandomEffectModel:
         row, col, val = _csr_to_torch(x, dev)
         ent_t = torch.from_numpy(ent).to(dev)
         e = ent_t[row]
-        keys = torch.from_numpy(self.keys).to(dev)
-        vals = torch.from_numpy(self.values).to(dev)
+        keys, vals = self.tensors(dev)
         out = torch.zeros(n, dtype=torch.float64, device=dev)
         if keys.numel() == 0 or row.numel() == 0:
             return out
@@ -129,7 +180,7 @@ class RandomEffectModel:
 
     def __repr__(self):
         return (f"RandomEffectModel(type={self.random_effect_type}, shard={self.feature_shard_id}, "
-                f"entities={self.n_entities}, nnz={len(self.keys)})")
+                f"entities={self.n_entities}, nnz={self.nnz})")
 
 
 class GameModel:

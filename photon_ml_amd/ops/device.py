@@ -221,6 +221,45 @@ class DeviceGLMData(GLMComputable):
         out.col_lo = col_lo
         return out
 
+    @staticmethod
+    def from_device_csr(indptr: torch.Tensor, col: torch.Tensor, val: torch.Tensor, y, offsets, weights, dim: int,
+                        device="cuda", precision: str = "f64", chunk_rows: int = 1 << 20,
+                        item_entries: Optional[int] = None, col_windows: bool = False):
+        """Tiled-layout shard built from device-resident CSR arrays: chunking, column windows, the forward
+        block sort and the transpose tile sort all run on the device (no host round trip of the non-zeros)."""
+        dev = torch.device(device)
+        vdt = VAL_DTYPE[PRECISIONS[precision]]
+        indptr = indptr.to(dev, torch.int64)
+        col = col.to(dev, torch.int64)
+        n = indptr.numel() - 1
+        starts = list(range(0, n, chunk_rows)) + [n] if n else [0, 0]
+        ip = indptr[torch.tensor(starts, device=dev)].tolist()
+        wins = []
+        for i in range(len(starts) - 1):
+            ea, eb = ip[i], ip[i + 1]
+            if col_windows and eb > ea:
+                lo, hi = torch.aminmax(col[ea:eb])
+                wins.append((int(lo), int(hi) + 1))
+            else:
+                wins.append((0, dim))
+        dmax = max([hi - lo for lo, hi in wins] + [1])
+        if resolve_layout("auto", dmax, chunk_rows) != "tiled":
+            raise ValueError(f"from_device_csr needs the tiled layout (window {dmax} columns)")
+        csr, csc, col_lo = [], [], []
+        for i, (lo, hi) in enumerate(wins):
+            a, b = starts[i], starts[i + 1]
+            ea, eb = ip[i], ip[i + 1]
+            rp = indptr[a:b + 1] - ea
+            c = col[ea:eb] - lo if lo else col[ea:eb]
+            v = val[ea:eb].to(dev).to(vdt)
+            csr.append(TLFwdChunk(rp, c, v, hi - lo))
+            csc.append(TLTChunk(rp, c, v, hi - lo, chunk_rows, item_entries=item_entries))
+            col_lo.append(lo)
+            del c, v
+        out = DeviceGLMData(csr, csc, starts, y, offsets, weights, dim, precision, dev, None)
+        out.col_lo = col_lo
+        return out
+
     def nbytes(self) -> int:
         return sum(c.nbytes() for c in self.csr + self.csc)
 

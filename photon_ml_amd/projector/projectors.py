@@ -56,15 +56,41 @@ def RandomProjection(k: int) -> ProjectorType:  # noqa: N802 (reference name)
 
 
 class IndexMapProjection:
-    """Entity-major compaction of active feature ids: ``ptr[E+1]``, ``feat[sum d_e]`` (sorted per entity)."""
+    """Entity-major compaction of active feature ids: ``ptr[E+1]``, ``feat[sum d_e]`` (sorted per entity).
 
-    def __init__(self, ptr: np.ndarray, feat: np.ndarray, dim: int):
+    Built on the host (:meth:`build`) or from device-resident sorted keys (:meth:`from_sorted_keys`, the
+    GPU dataset build); in the latter case ``keys`` / ``feat`` are copied to the host only when asked for."""
+
+    def __init__(self, ptr: np.ndarray, feat: Optional[np.ndarray], dim: int, keys_t=None):
         self.ptr = ptr.astype(np.int64)
-        self.feat = feat.astype(np.int64)
         self.dim = int(dim)
-        n_ent = len(ptr) - 1
-        ent = np.repeat(np.arange(n_ent, dtype=np.int64), np.diff(self.ptr))
-        self.keys = ent * self.dim + self.feat  # sorted ascending
+        self._keys_t = keys_t
+        self._feat = None if feat is None else feat.astype(np.int64)
+        self._keys = None
+        if feat is not None:
+            n_ent = len(ptr) - 1
+            ent = np.repeat(np.arange(n_ent, dtype=np.int64), np.diff(self.ptr))
+            self._keys = ent * self.dim + self._feat  # sorted ascending
+
+    @staticmethod
+    def from_sorted_keys(keys_t, n_entities: int, dim: int) -> "IndexMapProjection":
+        import torch
+        cnt = torch.bincount(keys_t // dim, minlength=n_entities)
+        ptr = np.zeros(n_entities + 1, dtype=np.int64)
+        ptr[1:] = np.cumsum(cnt.cpu().numpy())
+        return IndexMapProjection(ptr, None, dim, keys_t=keys_t)
+
+    @property
+    def keys(self) -> np.ndarray:
+        if self._keys is None:
+            self._keys = self._keys_t.cpu().numpy()
+        return self._keys
+
+    @property
+    def feat(self) -> np.ndarray:
+        if self._feat is None:
+            self._feat = self.keys % self.dim
+        return self._feat
 
     @staticmethod
     def build(entity_of_entry: np.ndarray, feature_of_entry: np.ndarray, n_entities: int, dim: int):
