@@ -94,8 +94,10 @@ def glm_lib() -> Optional[ctypes.CDLL]:
                                          c_void_p, c_void_p, c_void_p, c_void_p, c_void_p, c_void_p, c_int, c_void_p,
                                          c_void_p]
         lib.pml_segdot.argtypes = [c_void_p, c_void_p, c_int, c_void_p, c_int, c_void_p, c_void_p]
+        lib.pml_seg_expand.argtypes = [c_void_p, c_int, c_void_p, c_void_p, c_int, c_void_p]
+        lib.pml_seg_cg_step.argtypes = [c_void_p, c_int] + [c_void_p] * 7 + [c_double, c_void_p]
         for f in ("pml_seg_fwd", "pml_seg_t", "pml_reduce_stats", "pml_build_blocks", "pml_tl_fwd", "pml_tl_t",
-                  "pml_tl_maxbits", "pml_segdot", "pml_tl_fwd_multi", "pml_tl_t_multi"):
+                  "pml_tl_maxbits", "pml_segdot", "pml_tl_fwd_multi", "pml_tl_t_multi", "pml_seg_cg_step", "pml_seg_expand"):
             getattr(lib, f).restype = c_int
         lib.pml_set_config.argtypes = [c_int, c_int, c_int, c_int]
         lib._pml_typed = True
@@ -152,6 +154,57 @@ def segdot(a: torch.Tensor, b: Optional[torch.Tensor], ptr: torch.Tensor, mode: 
     check(lib.pml_segdot(a.data_ptr(), b.data_ptr(), mode, ptr.data_ptr(), nseg, out.data_ptr(),
                          stream_handle(a.device)), "segdot")
     return out
+
+
+def seg_expand(s: torch.Tensor, ptr: torch.Tensor, n: int) -> torch.Tensor:
+    """``out[i] = s[e]`` over contiguous segments ``ptr`` (length ``n`` = ptr[-1]); 8-byte or 1-byte dtypes."""
+    if s.device.type != "cuda" or s.element_size() not in (1, 8):
+        return torch.repeat_interleave(s, ptr[1:] - ptr[:-1], output_size=n)
+    lib = require_glm_lib()
+    s = s.contiguous()
+    out = torch.empty(n, dtype=s.dtype, device=s.device)
+    check(lib.pml_seg_expand(ptr.data_ptr(), ptr.numel() - 1, s.data_ptr(), out.data_ptr(), s.element_size(),
+                             stream_handle(s.device)), "seg_expand")
+    return out
+
+
+def seg_cg_step(ptr: torch.Tensor, step: torch.Tensor, r: torch.Tensor, d: torch.Tensor, Hd: torch.Tensor,
+                rtr: torch.Tensor, on: torch.Tensor, delta: torch.Tensor, l2: float = 0.0) -> None:
+    """One truncated-CG iteration for every entity segment, in place (``seg_cg_step_kernel``): updates
+    ``step``, ``r``, ``d`` (fp64, concatenated segments), ``rtr`` (fp64 per entity) and ``on`` (uint8 per entity,
+    cleared when the step hits the trust-region boundary ``delta``). ``Hd`` is the data term of the
+    Hessian-vector product; ``l2 * d`` is added on the fly. CPU tensors: same arithmetic in torch."""
+    nseg = ptr.numel() - 1
+    if step.device.type == "cuda":
+        lib = require_glm_lib()
+        for t in (step, r, d, Hd, rtr, on, delta):
+            assert t.is_contiguous()
+        assert on.dtype == torch.uint8 and rtr.dtype == torch.float64 and step.dtype == torch.float64
+        check(lib.pml_seg_cg_step(ptr.data_ptr(), nseg, step.data_ptr(), r.data_ptr(), d.data_ptr(), Hd.data_ptr(),
+                                  rtr.data_ptr(), on.data_ptr(), delta.data_ptr(), float(l2),
+                                  stream_handle(step.device)),
+              "seg_cg_step")
+        return
+    ent = torch.repeat_interleave(torch.arange(nseg), ptr[1:] - ptr[:-1])
+    sd = lambda a, b: segdot(a, b, ptr, 0)
+    Hd = Hd + l2 * d if l2 else Hd
+    act = on.bool()
+    dhd, std_, sts, dtd = sd(d, Hd), sd(step, d), sd(step, step), sd(d, d)
+    alpha = rtr / torch.where(dhd == 0, torch.ones_like(dhd), dhd)
+    trial = step + alpha[ent] * d
+    hit = torch.sqrt(sd(trial, trial).clamp(min=0)) > delta
+    dsq = delta * delta
+    rad = torch.sqrt((std_ * std_ + dtd * (dsq - sts)).clamp(min=0))
+    tau = torch.where(std_ >= 0, (dsq - sts) / (std_ + rad).clamp(min=1e-300), (rad - std_) / dtd.clamp(min=1e-300))
+    a = torch.where(act, torch.where(hit, tau, alpha), torch.zeros_like(alpha))
+    step.add_(a[ent] * d)
+    r.sub_(a[ent] * Hd)
+    rn = sd(r, r)
+    move = act & ~hit
+    beta = rn / torch.where(rtr == 0, torch.ones_like(rtr), rtr)
+    d.copy_(torch.where(move[ent], r + beta[ent] * d, d))
+    rtr.copy_(torch.where(move, rn, rtr))
+    on.copy_((act & ~hit).to(torch.uint8))
 
 
 def batched_lib() -> Optional[ctypes.CDLL]:

@@ -16,6 +16,7 @@ projection. Entities converge independently (masked); the batch loop ends when e
 from __future__ import annotations
 
 import math
+import os
 from dataclasses import dataclass
 from typing import Optional
 
@@ -70,10 +71,13 @@ class BatchedGLMData:
         return f, g
 
     def _dzz_at(self, loss, W):
-        if self._dzz_key is not None and self._dzz_key.shape == W.shape and torch.equal(self._dzz_key, W):
+        # cache keyed by tensor identity + in-place version (holding the reference keeps W alive, so its
+        # storage cannot be recycled under the key); no O(D) comparison / copy per Hessian-vector product
+        key = self._dzz_key
+        if key is not None and key[0] is W and key[1] == W._version and key[2] is loss:
             return self._dzz
         self._dzz = self.w * loss.dzz(self.margins(W), self.y)
-        self._dzz_key = W.clone()
+        self._dzz_key = (W, W._version, loss)
         return self._dzz
 
     def hv(self, loss, W, V, l2: float):
@@ -123,7 +127,8 @@ class SegmentedGLMData:
         return segdot(a, b, self.col_ptr, 0)
 
     def bexp(self, s):
-        return s[self.col_entity]
+        from ..ops.native import seg_expand
+        return seg_expand(s, self.col_ptr, self.col_entity.numel())
 
     def babs_sum(self, a):
         from ..ops.native import segdot
@@ -132,6 +137,12 @@ class SegmentedGLMData:
     def _rowsum(self, v):
         from ..ops.native import segdot
         return segdot(v, None, self.row_ptr, 1)
+
+    def cg_step(self, step, r, d, Hd, rtr, on, delta, l2: float = 0.0):
+        """Fused truncated-CG iteration over all entity segments (see ``ops.native.seg_cg_step``); ``Hd``
+        without the L2 term (added in the kernel)."""
+        from ..ops.native import seg_cg_step
+        seg_cg_step(self.col_ptr, step, r, d, Hd, rtr, on, delta, l2)
 
     def margins(self, W):
         return self.glm.matvec(W) + self.o
@@ -147,10 +158,13 @@ class SegmentedGLMData:
         return f, g
 
     def _dzz_at(self, loss, W):
-        if self._dzz_key is not None and self._dzz_key.shape == W.shape and torch.equal(self._dzz_key, W):
+        # cache keyed by tensor identity + in-place version (holding the reference keeps W alive, so its
+        # storage cannot be recycled under the key); no O(D) comparison / copy per Hessian-vector product
+        key = self._dzz_key
+        if key is not None and key[0] is W and key[1] == W._version and key[2] is loss:
             return self._dzz
         self._dzz = self.w * loss.dzz(self.margins(W), self.y)
-        self._dzz_key = W.clone()
+        self._dzz_key = (W, W._version, loss)
         return self._dzz
 
     def hv(self, loss, W, V, l2: float):
@@ -199,8 +213,13 @@ class _Convergence:
 
 
 def batched_tron(data, loss, l2: float, W0: torch.Tensor, tol: float = 1e-5, max_iter: int = 15,
-                 max_fail: int = 5, max_cg: int = 20) -> BatchedResult:
-    """Vectorised TRON (``photon-lib/.../optimization/TRON.scala:80-340``) over a batch of entities."""
+                 max_fail: int = 5, max_cg: int = 20, fused: Optional[bool] = None) -> BatchedResult:
+    """Vectorised TRON (``photon-lib/.../optimization/TRON.scala:80-340``) over a batch of entities.
+
+    ``fused``: run each CG iteration's vector algebra as one segmented kernel (``data.cg_step``; default when the
+    data provides it, i.e. the block-diagonal layout) instead of ~30 elementwise / reduction ops."""
+    if fused is None:
+        fused = hasattr(data, "cg_step") and os.environ.get("PML_FUSED_CG", "1") != "0"
     eta0, eta1, eta2 = 1e-4, 0.25, 0.75
     s1, s2, s3 = 0.25, 0.5, 4.0
     W = W0.clone()
@@ -234,10 +253,18 @@ def batched_tron(data, loss, l2: float, W0: torch.Tensor, tol: float = 1e-5, max
         rtr = data.bdot(r, r)
         cg_tol = 0.1 * _bn(data, g)
         cg_on = active.clone()
+        if fused:
+            rtr, delta = rtr.contiguous(), delta.to(torch.float64).contiguous()
         for _ in range(max_cg):
             cg_on &= torch.sqrt(rtr.clamp(min=0)) > cg_tol
             if not bool(cg_on.any()):
                 break
+            if fused:
+                Hd = data.hv(loss, W, d, 0.0)
+                on8 = cg_on.to(torch.uint8)
+                data.cg_step(step, r, d, Hd, rtr, on8, delta, l2)
+                cg_on = on8.bool()
+                continue
             Hd = data.hv(loss, W, d, l2)
             dHd = data.bdot(d, Hd)
             alpha = torch.where(cg_on, rtr / torch.where(dHd == 0, torch.ones_like(dHd), dHd),

@@ -32,4 +32,5 @@ def main(db, out, title, top=20):
 
 
 if __name__ == "__main__":
-    main(sys.argv[1], sys.argv[2], sys.argv[3] if len(sys.argv) > 3 else "rocprofv3 kernel summary")
+    main(sys.argv[1], sys.argv[2], sys.argv[3] if len(sys.argv) > 3 else "rocprofv3 kernel summary",
+         int(sys.argv[4]) if len(sys.argv) > 4 else 20)

@@ -144,3 +144,21 @@ def test_segmented_re_layout_matches_dense(task, opt):
                                    rtol=1e-6, atol=1e-7)
         np.testing.assert_allclose(a.coefficients_of(e).variances.numpy(), b.coefficients_of(e).variances.numpy(),
                                    rtol=1e-6, atol=1e-7)
+
+
+@pytest.mark.parametrize("task", ["LOGISTIC_REGRESSION", "POISSON_REGRESSION", "LINEAR_REGRESSION"])
+def test_fused_cg_step_matches_unfused_tron(task):
+    """The fused per-entity CG iteration (one segmented kernel; CPU: same arithmetic in torch) gives the same
+    block-diagonal TRON solution as the op-by-op vectorised CG."""
+    from photon_ml_amd.function.losses import loss_for_task
+    from photon_ml_amd.optimization.batched import batched_tron
+    data, _ = generate_game_data(n_rows=2000, n_users=25, seed=5, task=task)
+    c = RandomEffectCoordinate("u", data, RandomEffectDataConfiguration("userId", "user"), _cfg("TRON"), task,
+                               device="cpu", layout="segmented")
+    seg = c.dataset.seg
+    loss = loss_for_task(task)
+    W0 = torch.zeros(c.dataset.d_total, dtype=torch.float64)
+    res = {f: batched_tron(seg, loss, 1.0, W0, 1e-9, 30, fused=f) for f in (False, True)}
+    assert torch.equal(res[False].iters, res[True].iters)
+    assert torch.allclose(res[False].W, res[True].W, rtol=1e-9, atol=1e-11)
+    assert torch.allclose(res[False].f, res[True].f, rtol=1e-12)

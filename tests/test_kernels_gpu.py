@@ -238,3 +238,41 @@ def test_tl_stream_variants(pipe, precision):
             assert torch.allclose(g1.cpu(), g0, rtol=tol, atol=tol * float(g0.abs().max())), multi
     finally:
         configure(tl_pipe=0, tl_pipe_t=0, tl_multi=1)
+
+
+def test_seg_cg_step_kernel_matches_torch():
+    """seg_cg_step_kernel (one wave per entity segment) vs the torch arithmetic of the same CG iteration, with a
+    mix of inactive entities, boundary hits and interior steps, empty and long segments."""
+    from photon_ml_amd.ops.native import seg_cg_step
+    g = torch.Generator().manual_seed(3)
+    lens = torch.randint(0, 300, (500,), generator=g)
+    lens[:3] = torch.tensor([0, 1, 5000])
+    ptr = torch.zeros(501, dtype=torch.int64)
+    ptr[1:] = torch.cumsum(lens, 0)
+    n = int(ptr[-1])
+    vec = lambda: torch.randn(n, generator=g, dtype=torch.float64)
+    step, r, d, Hd = vec() * 0.1, vec(), vec(), vec().abs() + 0.5
+    rtr = torch.rand(500, generator=g, dtype=torch.float64) + 0.1
+    on = (torch.rand(500, generator=g) < 0.8).to(torch.uint8)
+    delta = torch.rand(500, generator=g, dtype=torch.float64) * 3
+    cpu = [t.clone() for t in (step, r, d, Hd, rtr, on, delta)]
+    seg_cg_step(ptr, *cpu, l2=0.7)
+    gpu = [t.clone().cuda() for t in (step, r, d, Hd, rtr, on, delta)]
+    seg_cg_step(ptr.cuda(), *gpu, l2=0.7)
+    assert torch.equal(gpu[5].cpu(), cpu[5])
+    assert 0 < int(cpu[5].sum()) < int(on.sum())  # some entities hit the boundary, some kept going
+    for a, b in zip(gpu[:5], cpu[:5]):
+        assert torch.allclose(a.cpu(), b, rtol=1e-12, atol=1e-12)
+
+
+def test_seg_expand_kernel():
+    from photon_ml_amd.ops.native import seg_expand
+    lens = torch.tensor([0, 3, 1, 700, 0, 65, 2])
+    ptr = torch.zeros(8, dtype=torch.int64)
+    ptr[1:] = torch.cumsum(lens, 0)
+    n = int(ptr[-1])
+    for s in (torch.randn(7, dtype=torch.float64), torch.tensor([1, 0, 1, 1, 0, 0, 1], dtype=torch.bool),
+              torch.arange(7, dtype=torch.int64)):
+        ref = torch.repeat_interleave(s, lens)
+        out = seg_expand(s.cuda(), ptr.cuda(), n)
+        assert out.dtype == s.dtype and torch.equal(out.cpu(), ref)
