@@ -826,12 +826,67 @@ __device__ __forceinline__ void tl_stream_wide(const uint32_t* __restrict__ pack
   }
 }
 
-// pipeline variant: P = 0 two-slot stream prefetch; P = 1 three-stage (stream r+2 / gather r+1 / accumulate r); P = 2 two-slot, 8 entries per lane
+// Lane-interleaved stream (the "il" layout, ops/tiled.py): every work unit starts on a TL_ROUND boundary and is
+// padded to whole rounds; inside a round of 256 sorted entries the quad of lane L holds the logical entries
+// L, L+64, L+128, L+192. The 16-B stream loads stay fully coalesced, and gather k of a wave now reads 64
+// CONSECUTIVE sorted entries (neighbouring columns in the forward, neighbouring rows in the transpose) instead of
+// 64 entries spaced 4 apart, so each gather instruction touches ~4x fewer distinct cache lines in the sparse tail.
+// Two-slot stream prefetch as tl_stream_p0; no lower-bound masks (windows are round-aligned).
+template <typename VT, typename XT, typename AT, bool SQ, int NW>
+__device__ __forceinline__ void tl_stream_il(const uint32_t* __restrict__ pack, const VT* __restrict__ val,
+                                             const XT* __restrict__ x, int e_lo, int e_hi, int sbits, AT* acc) {
+  typedef typename TLValT<VT>::T LT;
+  typedef typename TLVals<VT>::Raw Raw;
+  const int lane = threadIdx.x & 63, w = threadIdx.x >> 6;
+  const uint32_t smask = (1u << sbits) - 1u;
+  const int nr = (e_hi - e_lo + TL_ROUND - 1) / TL_ROUND;
+  const int r0 = (nr * w) / NW, r1 = (nr * (w + 1)) / NW;
+  if (r0 >= r1) return;
+  v4u pkA, pkB;
+  Raw vA, vB;
+  auto load_round = [&](int r, v4u& pk, Raw& v) {
+    const int e = e_lo + r * TL_ROUND + lane * TL_VEC;  // physical quad: always inside the padded unit
+    pk = __builtin_nontemporal_load((const v4u*)(pack + e));
+    v = TLVals<VT>::load(val + e);
+  };
+  auto process = [&](int r, v4u& pk_slot, Raw& v_slot) {
+    const v4u pk = pk_slot;
+    const Raw v_raw = v_slot;
+    const int e = e_lo + r * TL_ROUND + lane;  // logical index of quad element 0; element k is e + 64k
+    bool in[TL_VEC];
+    XT xv[TL_VEC];
+#pragma unroll
+    for (int k = 0; k < TL_VEC; ++k) {
+      in[k] = e + 64 * k < e_hi;
+      xv[k] = x[in[k] ? (pk[k] >> sbits) : 0u];
+    }
+    if (r + 2 < r1) load_round(r + 2, pk_slot, v_slot);
+    LT v[TL_VEC];
+    TLVals<VT>::get(v_raw, v);
+#pragma unroll
+    for (int k = 0; k < TL_VEC; ++k) {
+      if (in[k]) {
+        const AT vv = SQ ? static_cast<AT>(v[k]) * static_cast<AT>(v[k]) : static_cast<AT>(v[k]);
+        atomicAdd(&acc[pk[k] & smask], vv * static_cast<AT>(xv[k]));
+      }
+    }
+  };
+  load_round(r0, pkA, vA);
+  if (r0 + 1 < r1) load_round(r0 + 1, pkB, vB);
+  for (int r = r0; r < r1; r += 2) {
+    process(r, pkA, vA);
+    if (r + 1 < r1) process(r + 1, pkB, vB);
+  }
+}
+
+// pipeline variant: P = 0 two-slot stream prefetch; P = 1 three-stage (stream r+2 / gather r+1 / accumulate r);
+// P = 2 two-slot, 8 entries per lane; P = 3 lane-interleaved layout (tl_stream_il)
 template <typename VT, typename XT, typename AT, bool SQ, int U, int NW, int P>
 __device__ __forceinline__ void tl_stream(const uint32_t* __restrict__ pack, const VT* __restrict__ val,
                                           const XT* __restrict__ x, int e_lo, int e_hi, int sbits, AT* acc) {
   if (P == 1) tl_stream_p1<VT, XT, AT, SQ, U, NW>(pack, val, x, e_lo, e_hi, sbits, acc);
   else if (P == 2) tl_stream_wide<VT, XT, AT, SQ, NW, 2>(pack, val, x, e_lo, e_hi, sbits, acc);
+  else if (P == 3) tl_stream_il<VT, XT, AT, SQ, NW>(pack, val, x, e_lo, e_hi, sbits, acc);
   else tl_stream_p0<VT, XT, AT, SQ, U, NW>(pack, val, x, e_lo, e_hi, sbits, acc);
 }
 
@@ -978,19 +1033,21 @@ __global__ __launch_bounds__(NTHREADS) void tl_t_combine2_kernel(const int* __re
   if (col < dim) G[col] += s;
 }
 
-struct TLFwdDesc { const int* blk; int nblk; int rbits; const uint32_t* pack; const void* val; };
-struct TLFwdMultiDesc { const int* blk; int nblk; int rbits; const unsigned long long* packs; const unsigned long long* vals; };
+// ``il``: 1 = the streams are stored in the lane-interleaved layout (see tl_stream_il) -> pipeline P = 3.
+struct TLFwdDesc { const int* blk; int nblk; int rbits; const uint32_t* pack; const void* val; int il; };
+struct TLFwdMultiDesc { const int* blk; int nblk; int rbits; const unsigned long long* packs; const unsigned long long* vals; int il; };
 struct TLTDesc {
   const int* items; int nitems; int cbits; const uint32_t* pack; const void* val;
   const int* mt_tiles; const int* mt_ptr; int nmt; int dim;
   const int* cu; int ncu;     // level-1 combine units {tile, part_lo, part_hi}; mt_ptr indexes units
   int nparts_total;           // item partial rows (the level-1 rows follow them in the scratch buffer)
+  int il;
 };
 // Shard-wide transpose: items of every chunk (6 ints, see tl_t_multi_kernel) with per-chunk stream pointers.
 struct TLTMultiDesc {
   const int* items; int nitems; int cbits; const unsigned long long* packs; const unsigned long long* vals;
   const int* mt_tiles; const int* mt_ptr; int nmt; int dim;
-  const int* cu; int ncu; int nparts_total;
+  const int* cu; int ncu; int nparts_total; int il;
 };
 
 // Runtime TL configuration: accumulator precision for bf16/f32 data (0 = fp32 LDS, 1 = fp64 LDS) and the number
@@ -1007,7 +1064,8 @@ template <typename VT, typename XT, typename RT, typename AT, int MAXR>
 static void tl_fwd_launch(const TLFwdDesc* c, const void* x, FwdArgs<XT, RT> a, double* stats, hipStream_t st) {
 #define TLF(NW, P) hipLaunchKernelGGL((tl_fwd_kernel<VT, XT, RT, AT, MAXR, 2, NW, P>), dim3(c->nblk), dim3(NW * 64), 0, \
                                     st, c->blk, c->rbits, c->pack, (const VT*)c->val, (const XT*)x, a, stats)
-  if (g_tl_waves == 2) { if (g_tl_pipe == 1) TLF(2, 1); else TLF(2, 0); }
+  if (c->il) { if (g_tl_waves == 2) TLF(2, 3); else TLF(4, 3); }
+  else if (g_tl_waves == 2) { if (g_tl_pipe == 1) TLF(2, 1); else TLF(2, 0); }
   else { if (g_tl_pipe == 1) TLF(4, 1); else TLF(4, 0); }
 #undef TLF
 }
@@ -1017,7 +1075,8 @@ static void tl_fwd_multi_launch(const TLFwdMultiDesc* c, const void* x, FwdArgs<
                                 hipStream_t st) {
 #define TLM(NW, P) hipLaunchKernelGGL((tl_fwd_multi_kernel<VT, XT, RT, AT, MAXR, 2, NW, P>), dim3(c->nblk), \
                                       dim3(NW * 64), 0, st, c->blk, c->rbits, c->packs, c->vals, (const XT*)x, a, stats)
-  if (g_tl_waves == 2) { if (g_tl_pipe == 2) TLM(2, 2); else TLM(2, 0); }
+  if (c->il) { if (g_tl_waves == 2) TLM(2, 3); else TLM(4, 3); }
+  else if (g_tl_waves == 2) { if (g_tl_pipe == 2) TLM(2, 2); else TLM(2, 0); }
   else { if (g_tl_pipe == 2) TLM(4, 2); else TLM(4, 0); }
 #undef TLM
 }
@@ -1063,7 +1122,8 @@ template <typename VT, typename XT, typename AT, bool SQ, int MAXR>
 static void tl_t_launch(const TLTDesc* c, const void* x, double* G, double* parts, hipStream_t st) {
 #define TLT(NW, P) hipLaunchKernelGGL((tl_t_kernel<VT, XT, AT, SQ, MAXR, 2, NW, P>), dim3(c->nitems), dim3(NW * 64), 0, \
                                     st, c->items, c->cbits, c->pack, (const VT*)c->val, (const XT*)x, G, c->dim, parts)
-  if (g_tl_waves_t == 2) { if (g_tl_pipe_t == 1) TLT(2, 1); else TLT(2, 0); }
+  if (c->il) { if (g_tl_waves_t == 2) TLT(2, 3); else TLT(4, 3); }
+  else if (g_tl_waves_t == 2) { if (g_tl_pipe_t == 1) TLT(2, 1); else TLT(2, 0); }
   else { if (g_tl_pipe_t == 1) TLT(4, 1); else TLT(4, 0); }
 #undef TLT
 }
@@ -1102,7 +1162,8 @@ static void tl_t_multi_launch(const TLTMultiDesc* c, const void* x, double* G, d
 #define TLTM(NW, P) hipLaunchKernelGGL((tl_t_multi_kernel<VT, XT, AT, SQ, MAXR, 2, NW, P>), dim3(c->nitems), \
                                        dim3(NW * 64), 0, st, c->items, c->cbits, c->packs, c->vals, (const XT*)x, G, \
                                        c->dim, parts)
-  if (g_tl_waves_t == 2) { if (g_tl_pipe_t == 2) TLTM(2, 2); else TLTM(2, 0); }
+  if (c->il) { if (g_tl_waves_t == 2) TLTM(2, 3); else TLTM(4, 3); }
+  else if (g_tl_waves_t == 2) { if (g_tl_pipe_t == 2) TLTM(2, 2); else TLTM(2, 0); }
   else { if (g_tl_pipe_t == 2) TLTM(4, 2); else TLTM(4, 0); }
 #undef TLTM
 }

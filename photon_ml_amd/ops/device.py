@@ -325,8 +325,10 @@ class DeviceGLMData(GLMComputable):
         self._multi_vals = torch.tensor([ch.val.data_ptr() for ch in self.csr], dtype=torch.int64,
                                         device=self.device)
         from .native import TLFwdMultiDesc
+        if len({ch.il for ch in self.csr}) != 1:
+            return
         self._multi = TLFwdMultiDesc(self._multi_blk.data_ptr(), self._multi_blk.shape[0], self.csr[0].rbits,
-                                     self._multi_packs.data_ptr(), self._multi_vals.data_ptr())
+                                     self._multi_packs.data_ptr(), self._multi_vals.data_ptr(), self.csr[0].il)
 
     def _build_multi_t(self):
         self._multi_t = None

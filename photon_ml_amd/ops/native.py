@@ -32,24 +32,26 @@ class SegChunkDesc(ctypes.Structure):
 
 
 class TLFwdDesc(ctypes.Structure):
-    _fields_ = [("blk", c_void_p), ("nblk", c_int), ("rbits", c_int), ("pack", c_void_p), ("val", c_void_p)]
+    _fields_ = [("blk", c_void_p), ("nblk", c_int), ("rbits", c_int), ("pack", c_void_p), ("val", c_void_p),
+                ("il", c_int)]
 
 
 class TLFwdMultiDesc(ctypes.Structure):
-    _fields_ = [("blk", c_void_p), ("nblk", c_int), ("rbits", c_int), ("packs", c_void_p), ("vals", c_void_p)]
+    _fields_ = [("blk", c_void_p), ("nblk", c_int), ("rbits", c_int), ("packs", c_void_p), ("vals", c_void_p),
+                ("il", c_int)]
 
 
 class TLTMultiDesc(ctypes.Structure):
     _fields_ = [("items", c_void_p), ("nitems", c_int), ("cbits", c_int), ("packs", c_void_p), ("vals", c_void_p),
                 ("mt_tiles", c_void_p), ("mt_ptr", c_void_p), ("nmt", c_int), ("dim", c_int), ("cu", c_void_p),
-                ("ncu", c_int), ("nparts_total", c_int)]
+                ("ncu", c_int), ("nparts_total", c_int), ("il", c_int)]
 
 
 class TLTDesc(ctypes.Structure):
     _fields_ = [
         ("items", c_void_p), ("nitems", c_int), ("cbits", c_int), ("pack", c_void_p), ("val", c_void_p),
         ("mt_tiles", c_void_p), ("mt_ptr", c_void_p), ("nmt", c_int), ("dim", c_int),
-        ("cu", c_void_p), ("ncu", c_int), ("nparts_total", c_int),
+        ("cu", c_void_p), ("ncu", c_int), ("nparts_total", c_int), ("il", c_int),
     ]
 
 

@@ -12,6 +12,12 @@ One row chunk of a feature shard is stored twice:
   reduction (units of ``COMBINE_SEG`` partial rows, then the units of a tile) — deterministic.
   ``cbits = min(10, 32 - bits(chunk_rows))``.
 
+Both copies are stored LANE-INTERLEAVED by default (``il``; ``PML_TL_IL=0`` keeps the plain order): every work
+unit (forward block / transpose item) starts on a 256-entry round boundary and is zero-padded to whole rounds,
+and inside a round the 16-B quad of lane L holds the unit's sorted entries L, L+64, L+128, L+192, so each gather
+instruction of the kernels reads 64 consecutive sorted entries (``tl_stream_il`` in ``glm_kernels.hip``). Padding
+costs < 0.5 % of the stream at the bench shapes.
+
 The builders run with torch ops on the data's device (GPU sort for the 100M-entry bench chunks, CPU in tests).
 Values keep the shard precision (bf16 / fp32 / fp64). Both copies cost 4 B + sizeof(value) per entry, the same
 as the segmented-stream CSR/CSC pair they replace. Shapes the packing cannot represent (``D > 2^27`` or chunks
@@ -35,6 +41,8 @@ DEFAULT_CBITS = int(os.environ.get("PML_TL_CBITS", 10))
 DEFAULT_ITEM_ENTRIES = 1 << 16
 _PAD = 8                 # kernels read 4-entry quads; pad so that the last quad stays in bounds
 COMBINE_SEG = 16         # partial rows summed per level-1 combine work-group
+IL_ROUND = 256           # entries per wave-round of the kernels (64 lanes x 4-entry quads)
+INTERLEAVE = int(os.environ.get("PML_TL_IL", "1"))
 
 
 def _bits(n: int) -> int:
@@ -68,14 +76,42 @@ def _pad(t: torch.Tensor) -> torch.Tensor:
     return torch.cat([t, torch.zeros(_PAD, dtype=t.dtype, device=t.device)]).contiguous()
 
 
+def il_phys(e_lo: torch.Tensor, n: torch.Tensor) -> torch.Tensor:
+    """Physical positions of the logical entries of units starting at ``e_lo`` (round-aligned) with ``n``
+    entries each, in unit order: logical j of a unit lives at e_lo + 256*(j//256) + 4*(j%64) + (j%256)//64."""
+    e_lo = e_lo.to(torch.int64)
+    n = n.to(torch.int64)
+    tot = int(n.sum())
+    unit = torch.repeat_interleave(torch.arange(n.numel(), device=n.device), n)
+    j = torch.arange(tot, device=n.device) - (torch.cumsum(n, 0) - n)[unit]
+    t = j & (IL_ROUND - 1)
+    return e_lo[unit] + (j - t) + ((t & 63) << 2) + (t >> 6)
+
+
+def _interleave(pack: torch.Tensor, val: torch.Tensor, n: torch.Tensor):
+    """Lane-interleave sorted streams whose units are consecutive runs of ``n`` entries. Returns the padded
+    streams and the new (round-aligned) unit starts."""
+    n = n.to(torch.int64)
+    padded = (n + IL_ROUND - 1) // IL_ROUND * IL_ROUND
+    new_lo = torch.cumsum(padded, 0) - padded
+    total = int(padded.sum()) + _PAD
+    phys = il_phys(new_lo, n)
+    p = torch.zeros(total, dtype=pack.dtype, device=pack.device)
+    v = torch.zeros(total, dtype=val.dtype, device=val.device)
+    p[phys] = pack
+    v[phys] = val
+    return p, v, new_lo
+
+
 class TLFwdChunk:
     """Forward copy of one row chunk (``m`` rows)."""
 
     kind = "tl"
 
     def __init__(self, rowptr: torch.Tensor, col: torch.Tensor, val: torch.Tensor, dim: int,
-                 rbits: Optional[int] = None):
+                 rbits: Optional[int] = None, il: Optional[int] = None):
         dev = val.device
+        self.il = INTERLEAVE if il is None else int(il)
         rowptr = rowptr.to(dev, torch.int64)
         col = col.to(dev, torch.int64)
         m = rowptr.numel() - 1
@@ -89,16 +125,22 @@ class TLFwdChunk:
         pack = (col << self.rbits) | (rows & (R - 1))
         key = ((rows >> self.rbits) << 32) | pack
         key, perm = torch.sort(key, stable=True)
-        self.pack = _pad(_to_u32_bits(key & 0xFFFFFFFF))
-        self.val = _pad(val[perm].contiguous())
-        del key, perm, rows
         nblk = (m + R - 1) // R
         b = torch.arange(nblk, device=dev)
         lo = b * R
         hi = torch.clamp(lo + R, max=m)
-        self.blk = torch.stack([lo, hi - lo, rowptr[lo], rowptr[hi]], 1).to(torch.int32).contiguous()
+        e_lo, e_hi = rowptr[lo], rowptr[hi]
+        if self.il:
+            self.pack, self.val, e_lo = _interleave(_to_u32_bits(key & 0xFFFFFFFF), val[perm], e_hi - rowptr[lo])
+            e_hi = e_lo + (rowptr[hi] - rowptr[lo])
+        else:
+            self.pack = _pad(_to_u32_bits(key & 0xFFFFFFFF))
+            self.val = _pad(val[perm].contiguous())
+        del key, perm, rows
+        self.blk = torch.stack([lo, hi - lo, e_lo, e_hi], 1).to(torch.int32).contiguous()
         self.nblk, self.m, self.nnz = nblk, m, nnz
-        self.desc = TLFwdDesc(self.blk.data_ptr(), nblk, self.rbits, self.pack.data_ptr(), self.val.data_ptr())
+        self.desc = TLFwdDesc(self.blk.data_ptr(), nblk, self.rbits, self.pack.data_ptr(), self.val.data_ptr(),
+                              self.il)
 
     @property
     def nstats(self) -> int:
@@ -109,15 +151,23 @@ class TLFwdChunk:
     def nbytes(self) -> int:
         return sum(t.numel() * t.element_size() for t in (self.blk, self.pack, self.val))
 
+    def logical(self):
+        """(pack, val) of the non-zeros in sorted (unit) order, whatever the storage order."""
+        if not self.il:
+            return self.pack[: self.nnz], self.val[: self.nnz]
+        ph = il_phys(self.blk[:, 2], self.blk[:, 3] - self.blk[:, 2])
+        return self.pack[ph], self.val[ph]
+
     # host emulation of the kernel arithmetic (tests / CPU fallback)
     def emulate_matvec(self, x: torch.Tensor) -> torch.Tensor:
-        p = self.pack[: self.nnz].to(torch.int64) & 0xFFFFFFFF
+        pk, vl = self.logical()
+        p = pk.to(torch.int64) & 0xFFFFFFFF
         col = p >> self.rbits
         blk_of_entry = torch.repeat_interleave(torch.arange(self.nblk, device=p.device),
                                                (self.blk[:, 3] - self.blk[:, 2]).to(torch.int64))
         row = (blk_of_entry << self.rbits) + (p & ((1 << self.rbits) - 1))
         z = torch.zeros(self.m, dtype=torch.float64, device=p.device)
-        return z.index_add_(0, row, self.val[: self.nnz].to(torch.float64) * x.to(torch.float64)[col])
+        return z.index_add_(0, row, vl.to(torch.float64) * x.to(torch.float64)[col])
 
 
 class TLTChunk:
@@ -126,7 +176,8 @@ class TLTChunk:
     kind = "tl"
 
     def __init__(self, rowptr: torch.Tensor, col: torch.Tensor, val: torch.Tensor, dim: int, chunk_rows: int,
-                 cbits: Optional[int] = None, item_entries: Optional[int] = None):
+                 cbits: Optional[int] = None, item_entries: Optional[int] = None, il: Optional[int] = None):
+        self.il = INTERLEAVE if il is None else int(il)
         if item_entries is None:
             item_entries = int(os.environ.get("PML_TL_ITEM_ENTRIES", DEFAULT_ITEM_ENTRIES))
         dev = val.device
@@ -145,8 +196,8 @@ class TLTChunk:
         key = (tile << 32) | pack
         del rows, pack
         key, perm = torch.sort(key, stable=True)
-        self.pack = _pad(_to_u32_bits(key & 0xFFFFFFFF))
-        self.val = _pad(val[perm].contiguous())
+        pack = _to_u32_bits(key & 0xFFFFFFFF)
+        val = val[perm]
         del key, perm
         ntiles = (dim + C - 1) // C
         counts = torch.bincount(tile, minlength=ntiles).cpu().numpy().astype(np.int64)
@@ -169,14 +220,23 @@ class TLTChunk:
                 mt_tiles.append(t)
                 mt_ptr.append(len(cu))
         self.nitems, self.nmt, self.nparts, self.ncu = len(items), len(mt_tiles), part, len(cu)
-        self.items = torch.tensor(np.asarray(items, dtype=np.int32).reshape(-1, 4), device=dev)
+        items = np.asarray(items, dtype=np.int64).reshape(-1, 4)
+        if self.il:
+            cnt = torch.from_numpy(items[:, 2] - items[:, 1]).to(dev)
+            self.pack, self.val, new_lo = _interleave(pack, val, cnt)
+            items[:, 1] = new_lo.cpu().numpy()
+            items[:, 2] = items[:, 1] + cnt.cpu().numpy()
+        else:
+            self.pack, self.val = _pad(pack), _pad(val.contiguous())
+        del pack, val
+        self.items = torch.tensor(items.astype(np.int32), device=dev)
         self.mt_tiles = torch.tensor(np.asarray(mt_tiles or [0], dtype=np.int32), device=dev)
         self.mt_ptr = torch.tensor(np.asarray(mt_ptr, dtype=np.int32), device=dev)
         self.cu = torch.tensor(np.asarray(cu or [(0, 0, 0)], dtype=np.int32).reshape(-1, 3), device=dev)
         self.m, self.nnz, self.dim = m, nnz, dim
         self.desc = TLTDesc(self.items.data_ptr(), self.nitems, self.cbits, self.pack.data_ptr(),
                             self.val.data_ptr(), self.mt_tiles.data_ptr(), self.mt_ptr.data_ptr(), self.nmt, dim,
-                            self.cu.data_ptr(), self.ncu, self.nparts)
+                            self.cu.data_ptr(), self.ncu, self.nparts, self.il)
 
     @property
     def parts_needed(self) -> int:
@@ -187,13 +247,27 @@ class TLTChunk:
         return sum(t.numel() * t.element_size() for t in (self.items, self.mt_tiles, self.mt_ptr, self.cu, self.pack,
                                                            self.val))
 
+    def window(self, e_lo: int, e_hi: int):
+        """(pack, val) of one item window in sorted order."""
+        if not self.il:
+            return self.pack[e_lo:e_hi], self.val[e_lo:e_hi]
+        ph = il_phys(torch.tensor([e_lo]), torch.tensor([e_hi - e_lo])).to(self.pack.device)
+        return self.pack[ph], self.val[ph]
+
+    def logical(self):
+        if not self.il:
+            return self.pack[: self.nnz], self.val[: self.nnz]
+        ph = il_phys(self.items[:, 1], self.items[:, 2] - self.items[:, 1])
+        return self.pack[ph], self.val[ph]
+
     def emulate_rmatvec(self, r: torch.Tensor, square: bool = False) -> torch.Tensor:
-        p = self.pack[: self.nnz].to(torch.int64) & 0xFFFFFFFF
+        pk, vl = self.logical()
+        p = pk.to(torch.int64) & 0xFFFFFFFF
         row = p >> self.cbits
         tile_of_entry = torch.repeat_interleave(self.items[:, 0].to(torch.int64),
                                                 (self.items[:, 2] - self.items[:, 1]).to(torch.int64))
         col = (tile_of_entry << self.cbits) + (p & ((1 << self.cbits) - 1))
-        v = self.val[: self.nnz].to(torch.float64)
+        v = vl.to(torch.float64)
         if square:
             v = v * v
         g = torch.zeros(self.dim, dtype=torch.float64, device=p.device)
@@ -214,6 +288,9 @@ class TLTMulti:
         from .native import TLTMultiDesc
         dev = chunks[0].pack.device
         self.cbits = chunks[0].cbits
+        self.il = chunks[0].il
+        if any(ch.il != self.il for ch in chunks):
+            raise ValueError("TLTMulti: chunks mix interleaved and plain streams")
         its = []
         for c, ch in enumerate(chunks):
             it = ch.items[: ch.nitems].cpu().numpy().astype(np.int64).reshape(-1, 4)
@@ -248,7 +325,7 @@ class TLTMulti:
         self._chunks = list(chunks)  # keep the streams alive
         self.desc = TLTMultiDesc(self.items.data_ptr(), n, self.cbits, self.packs.data_ptr(), self.vals.data_ptr(),
                                  self.mt_tiles.data_ptr(), self.mt_ptr.data_ptr(), self.nmt, dim,
-                                 self.cu.data_ptr(), self.ncu, self.nparts)
+                                 self.cu.data_ptr(), self.ncu, self.nparts, self.il)
 
     @property
     def parts_needed(self) -> int:
@@ -264,8 +341,9 @@ class TLTMulti:
         r = r.to(torch.float64).cpu()
         for c, tile, e_lo, e_hi, part, rb in self.items.cpu().tolist():
             ch = self._chunks[c]
-            p = ch.pack[e_lo:e_hi].to(torch.int64).cpu() & 0xFFFFFFFF
-            v = ch.val[e_lo:e_hi].to(torch.float64).cpu()
+            pk, vl = ch.window(e_lo, e_hi)
+            p = pk.to(torch.int64).cpu() & 0xFFFFFFFF
+            v = vl.to(torch.float64).cpu()
             if square:
                 v = v * v
             acc = torch.zeros(C, dtype=torch.float64).index_add_(0, p & (C - 1), v * r[rb + (p >> self.cbits)])

@@ -25,6 +25,7 @@ def main():
     ap.add_argument("--tl-configs", default="", help="semicolon list of tl_waves,tl_waves_t,tl_pipe (in-process A/B)")
     ap.add_argument("--ablate", type=int, nargs="+", default=[0])
     ap.add_argument("--configs", default="0,1,8192", help="semicolon list of fwd_strided,t_strided,hot_n")
+    ap.add_argument("--il", type=int, nargs="+", default=[1], help="tiled stream order(s): 1 lane-interleaved, 0 plain")
     args = ap.parse_args()
     res = []
     from photon_ml_amd.ops.native import glm_lib, configure
@@ -33,14 +34,17 @@ def main():
     if args.tl_configs:
         configs = [("tl",) + tuple(int(v) for v in c.split(",")) for c in args.tl_configs.split(";")]
     cache = {}
-    for cr, abl, cfg in [(c, a, g) for c in args.chunk_rows for a in args.ablate for g in configs]:
+    from photon_ml_amd.ops import tiled
+    for cr, il, abl, cfg in [(c, i, a, g) for c in args.chunk_rows for i in args.il for a in args.ablate
+                             for g in configs]:
         lib.pml_set_ablate(0)
-        if cr not in cache:
+        if (cr, il) not in cache:
             cache.clear()
             torch.cuda.empty_cache()
-            cache[cr] = generate_device_shard(args.rows, args.features, args.nnz, "cuda", args.precision,
-                                              chunk_rows=cr, layout=args.layout)
-        data, w = cache[cr]
+            tiled.INTERLEAVE = il
+            cache[(cr, il)] = generate_device_shard(args.rows, args.features, args.nnz, "cuda", args.precision,
+                                                    chunk_rows=cr, layout=args.layout)
+        data, w = cache[(cr, il)]
         lib.pml_set_ablate(abl)
         if cfg[0] == "tl":
             configure(tl_waves=cfg[1], tl_waves_t=cfg[2], tl_pipe=cfg[3],
@@ -71,7 +75,7 @@ def main():
             data.value_grad_packed(LOGISTIC, w * 0.1, 0.0)
         torch.cuda.synchronize()
         tp = (time.perf_counter() - t0) / args.reps * 1e3
-        r = {"cfg": cfg, "ablate": abl, "chunk_rows": cr, "rows": args.rows, "fwd_ms": min(tf), "t_ms": min(tt), "pass_ms": tp,
+        r = {"cfg": cfg, "il": il, "ablate": abl, "chunk_rows": cr, "rows": args.rows, "fwd_ms": min(tf), "t_ms": min(tt), "pass_ms": tp,
              "fwd_GBps": bytes_per / min(tf) / 1e6, "t_GBps": bytes_per / min(tt) / 1e6,
              "stream_GB": bytes_per / 1e9, "nblk_fwd": sum(c.nblk for c in data.csr),
              "nblk_t": sum(getattr(c, "nblk", getattr(c, "nitems", 0)) for c in data.csc),

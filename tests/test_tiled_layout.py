@@ -8,17 +8,18 @@ import torch
 from photon_ml_amd.ops.tiled import TLFwdChunk, TLTChunk, fwd_bits, t_bits, tl_supported
 
 
+@pytest.mark.parametrize("il", [0, 1])
 @pytest.mark.parametrize("m,d,dens,item", [(3000, 500, 0.05, 64), (5000, 70000, 0.0005, 1 << 16), (100, 7, 0.5, 8),
                                            (2048, 4096, 0.01, 300), (10, 3, 0.0, 64)])
-def test_tl_emulation_matches_scipy(m, d, dens, item):
+def test_tl_emulation_matches_scipy(m, d, dens, item, il):
     rng = np.random.default_rng(0)
     x = sp.random(m, d, density=dens, format="csr", random_state=1)
     x.data = rng.normal(size=x.nnz)
     rp = torch.from_numpy(x.indptr.astype(np.int64))
     col = torch.from_numpy(x.indices.astype(np.int64))
     val = torch.from_numpy(x.data)
-    f = TLFwdChunk(rp, col, val, d)
-    t = TLTChunk(rp, col, val, d, m, item_entries=item)
+    f = TLFwdChunk(rp, col, val, d, il=il)
+    t = TLTChunk(rp, col, val, d, m, item_entries=item, il=il)
     w = rng.normal(size=d)
     r = rng.normal(size=m)
     np.testing.assert_allclose(f.emulate_matvec(torch.from_numpy(w)).numpy(), x @ w, atol=1e-12)
@@ -30,14 +31,29 @@ def test_tl_emulation_matches_scipy(m, d, dens, item):
     assert b[0, 0] == 0 and (b[1:, 0] == b[:-1, 0] + b[:-1, 1]).all() and b[-1, 0] + b[-1, 1] == m
     it = t.items.numpy()
     if len(it):
-        assert it[0, 1] == 0 and (it[1:, 1] == it[:-1, 2]).all() and it[-1, 2] == x.nnz
-        assert (it[:, 2] - it[:, 1] <= item).all()
+        assert it[0, 1] == 0 and (it[:, 2] - it[:, 1] <= item).all() and (it[:, 2] - it[:, 1]).sum() == x.nnz
+        if il:  # round-aligned, zero-padded windows
+            assert (it[:, 1] % 256 == 0).all() and (it[1:, 1] >= it[:-1, 2]).all()
+            assert (b[:, 2] % 256 == 0).all()
+        else:
+            assert (it[1:, 1] == it[:-1, 2]).all() and it[-1, 2] == x.nnz
         assert t.nparts == int((it[:, 3] >= 0).sum())
-    # forward blocks: entries sorted by column inside a block; transpose tiles: sorted by row
-    p = f.pack[: x.nnz].to(torch.int64).numpy() & 0xFFFFFFFF
-    for lo, hi in b[:, 2:]:
+    # forward blocks: entries sorted by column inside a block (in logical order)
+    pk, _ = f.logical()
+    p = pk.to(torch.int64).numpy() & 0xFFFFFFFF
+    starts = np.r_[0, np.cumsum(b[:, 3] - b[:, 2])]
+    for lo, hi in zip(starts[:-1], starts[1:]):
         cols = p[lo:hi] >> f.rbits
         assert (np.diff(cols) >= 0).all()
+    if il and x.nnz:
+        # lane L's quad of a round holds logical entries L, L+64, L+128, L+192 of that round
+        lo = int(b[0, 2])
+        n0 = int(b[0, 3] - b[0, 2])
+        if n0 >= 256:
+            phys = f.pack[lo:lo + 256].to(torch.int64).numpy()
+            logi = p[:256].astype(np.int64)
+            phys_u = phys & 0xFFFFFFFF
+            assert (phys_u.reshape(64, 4).T.reshape(-1) == logi).all()
 
 
 def test_bits():
