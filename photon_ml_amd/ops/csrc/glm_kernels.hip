@@ -143,13 +143,24 @@ typedef unsigned int v4u __attribute__((ext_vector_type(4)));
 typedef unsigned int v2u __attribute__((ext_vector_type(2)));
 typedef float v4f __attribute__((ext_vector_type(4)));
 typedef double v2d __attribute__((ext_vector_type(2)));
+
+// Streaming loads through an explicit GLOBAL address-space pointer. Stream pointers that are themselves loaded
+// from memory (per-chunk pointer tables of the shard-wide kernels) would otherwise compile to FLAT loads, which
+// count in both vmcnt and lgkmcnt and may return out of order: every later wait then degenerates to
+// vmcnt(0) lgkmcnt(0) and the software-pipelined prefetch of the next rounds is drained at every LDS add.
+template <typename T> __device__ __forceinline__ T ldg_nt(const T* p) {
+  return __builtin_nontemporal_load((const __attribute__((address_space(1))) T*)p);
+}
+template <typename T> __device__ __forceinline__ T ldg(const T* p) {
+  return *((const __attribute__((address_space(1))) T*)p);
+}
 #define ROUNDS (NB / (NTHREADS * VEC))   // vector layout rounds (2)
 #define SROUNDS (NB / NTHREADS)          // strided layout rounds (16)
 
 template <typename VT> struct RawVals;
 template <> struct RawVals<uint16_t> {
   v4u r;
-  __device__ __forceinline__ void load(const uint16_t* p) { r = __builtin_nontemporal_load((const v4u*)p); }
+  __device__ __forceinline__ void load(const uint16_t* p) { r = ldg_nt((const v4u*)p); }
   __device__ __forceinline__ void get(float* v) const {
 #pragma unroll
     for (int k = 0; k < 4; ++k) {
@@ -161,8 +172,8 @@ template <> struct RawVals<uint16_t> {
 template <> struct RawVals<float> {
   v4f a, b;
   __device__ __forceinline__ void load(const float* p) {
-    a = __builtin_nontemporal_load((const v4f*)p);
-    b = __builtin_nontemporal_load((const v4f*)(p + 4));
+    a = ldg_nt((const v4f*)p);
+    b = ldg_nt((const v4f*)(p + 4));
   }
   __device__ __forceinline__ void get(float* v) const {
 #pragma unroll
@@ -173,7 +184,7 @@ template <> struct RawVals<double> {
   v2d a[4];
   __device__ __forceinline__ void load(const double* p) {
 #pragma unroll
-    for (int k = 0; k < 4; ++k) a[k] = __builtin_nontemporal_load((const v2d*)(p + 2 * k));
+    for (int k = 0; k < 4; ++k) a[k] = ldg_nt((const v2d*)(p + 2 * k));
   }
   __device__ __forceinline__ void get(double* v) const {
 #pragma unroll
@@ -182,10 +193,10 @@ template <> struct RawVals<double> {
 };
 
 __device__ __forceinline__ float val1(const uint16_t* p) {
-  return __uint_as_float(((unsigned)__builtin_nontemporal_load(p)) << 16);
+  return __uint_as_float(((unsigned)ldg_nt(p)) << 16);
 }
-__device__ __forceinline__ float val1(const float* p) { return __builtin_nontemporal_load(p); }
-__device__ __forceinline__ double val1(const double* p) { return __builtin_nontemporal_load(p); }
+__device__ __forceinline__ float val1(const float* p) { return ldg_nt(p); }
+__device__ __forceinline__ double val1(const double* p) { return ldg_nt(p); }
 
 // Hot-table gather: lanes whose feature is in the LDS head read LDS; their global address collapses onto x[0]
 // so that, whatever the compiler does with the predicated global load, they add no distinct cache lines.
@@ -221,7 +232,7 @@ __device__ __forceinline__ double stream_products(const BlockDesc& d, const int*
 #pragma unroll
       for (int r = 0; r < SROUNDS; ++r) {
         const int e = base + r * NTHREADS + threadIdx.x;
-        ii[r] = e < hi ? __builtin_nontemporal_load(idx + e) : 0;
+        ii[r] = e < hi ? ldg_nt(idx + e) : 0;
       }
 #pragma unroll
       for (int r = 0; r < SROUNDS; ++r) {
@@ -256,8 +267,8 @@ __device__ __forceinline__ double stream_products(const BlockDesc& d, const int*
       for (int r = 0; r < ROUNDS; ++r) {
         const int e = base + (r * NTHREADS + threadIdx.x) * VEC;
         if (e < hi) {
-          i0[r] = __builtin_nontemporal_load((const v4i*)(idx + e));
-          i1[r] = __builtin_nontemporal_load((const v4i*)(idx + e + 4));
+          i0[r] = ldg_nt((const v4i*)(idx + e));
+          i1[r] = ldg_nt((const v4i*)(idx + e + 4));
           rv[r].load(val + e);
         }
       }
@@ -585,7 +596,7 @@ __global__ __launch_bounds__(NTHREADS) void reduce_stats_l1_kernel(const double*
 template <typename VT> struct TLVals;
 template <> struct TLVals<uint16_t> {
   typedef v2u Raw;
-  static __device__ __forceinline__ Raw load(const uint16_t* p) { return __builtin_nontemporal_load((const v2u*)p); }
+  static __device__ __forceinline__ Raw load(const uint16_t* p) { return ldg_nt((const v2u*)p); }
   static __device__ __forceinline__ void get(const Raw& u, float* v) {
     v[0] = __uint_as_float(u.x << 16); v[1] = __uint_as_float(u.x & 0xffff0000u);
     v[2] = __uint_as_float(u.y << 16); v[3] = __uint_as_float(u.y & 0xffff0000u);
@@ -593,7 +604,7 @@ template <> struct TLVals<uint16_t> {
 };
 template <> struct TLVals<float> {
   typedef v4f Raw;
-  static __device__ __forceinline__ Raw load(const float* p) { return __builtin_nontemporal_load((const v4f*)p); }
+  static __device__ __forceinline__ Raw load(const float* p) { return ldg_nt((const v4f*)p); }
   static __device__ __forceinline__ void get(const Raw& a, float* v) { v[0] = a[0]; v[1] = a[1]; v[2] = a[2]; v[3] = a[3]; }
 };
 struct d4 { v2d a, b; };
@@ -601,8 +612,8 @@ template <> struct TLVals<double> {
   typedef d4 Raw;
   static __device__ __forceinline__ Raw load(const double* p) {
     d4 r;
-    r.a = __builtin_nontemporal_load((const v2d*)p);
-    r.b = __builtin_nontemporal_load((const v2d*)(p + 2));
+    r.a = ldg_nt((const v2d*)p);
+    r.b = ldg_nt((const v2d*)(p + 2));
     return r;
   }
   static __device__ __forceinline__ void get(const Raw& r, double* v) { v[0] = r.a[0]; v[1] = r.a[1]; v[2] = r.b[0]; v[3] = r.b[1]; }
@@ -649,7 +660,7 @@ __device__ __forceinline__ void tl_stream_p0(const uint32_t* __restrict__ pack, 
   auto load_round = [&](int r, v4u& pk, Raw& v) {
     const int e = lo + r * TL_ROUND + lane * TL_VEC;
     const int es = (r < r1 && e < e_hi) ? e : lo;  // out-of-range lanes re-read a valid quad; masked below
-    pk = __builtin_nontemporal_load((const v4u*)(pack + es));
+    pk = ldg_nt((const v4u*)(pack + es));
     v = TLVals<VT>::load(val + es);
   };
   auto process = [&](int r, v4u& pk_slot, Raw& v_slot) {
@@ -661,7 +672,7 @@ __device__ __forceinline__ void tl_stream_p0(const uint32_t* __restrict__ pack, 
 #pragma unroll
     for (int k = 0; k < TL_VEC; ++k) {
       in[k] = (e + k >= e_lo) && (e + k < e_hi);
-      xv[k] = x[in[k] ? (pk[k] >> sbits) : 0u];  // unconditional: all four gathers in flight together
+      xv[k] = ldg(x + (in[k] ? (pk[k] >> sbits) : 0u));  // unconditional: all four gathers in flight together
     }
     // refill this slot with round r + 2 AFTER issuing the gathers (vmcnt retires in issue order)
     if (r + 2 < r1) load_round(r + 2, pk_slot, v_slot);
@@ -704,7 +715,7 @@ __device__ __forceinline__ void tl_stream_p1(const uint32_t* __restrict__ pack, 
   auto load_round = [&](int r, v4u& pk, Raw& v) {
     const int e = lo + r * TL_ROUND + lane * TL_VEC;
     const int es = (r < r1 && e < e_hi) ? e : lo;  // out-of-range lanes re-read a valid quad; masked below
-    pk = __builtin_nontemporal_load((const v4u*)(pack + es));
+    pk = ldg_nt((const v4u*)(pack + es));
     v = TLVals<VT>::load(val + es);
   };
   auto gather = [&](int r, const v4u& pk, XT* xv) {
@@ -712,7 +723,7 @@ __device__ __forceinline__ void tl_stream_p1(const uint32_t* __restrict__ pack, 
 #pragma unroll
     for (int k = 0; k < TL_VEC; ++k) {
       const bool in = (r < r1) && (e + k >= e_lo) && (e + k < e_hi);
-      xv[k] = x[in ? (pk[k] >> sbits) : 0u];
+      xv[k] = ldg(x + (in ? (pk[k] >> sbits) : 0u));
     }
   };
   auto accumulate = [&](int r, const v4u& pk, const Raw& v_raw, const XT* xv) {
@@ -783,7 +794,7 @@ __device__ __forceinline__ void tl_stream_wide(const uint32_t* __restrict__ pack
     for (int q = 0; q < Q; ++q) {
       const int eq = e + 4 * q;
       const int es = (r < r1 && eq < e_hi) ? eq : lo;  // out-of-range quads re-read a valid one; masked below
-      sl.pk[q] = __builtin_nontemporal_load((const v4u*)(pack + es));
+      sl.pk[q] = ldg_nt((const v4u*)(pack + es));
       sl.v[q] = TLVals<VT>::load(val + es);
     }
   };
@@ -801,7 +812,7 @@ __device__ __forceinline__ void tl_stream_wide(const uint32_t* __restrict__ pack
       for (int k = 0; k < 4; ++k) {
         const int i = 4 * q + k;
         in[i] = (e + i >= e_lo) && (e + i < e_hi);
-        xv[i] = x[in[i] ? (pk[q][k] >> sbits) : 0u];
+        xv[i] = ldg(x + (in[i] ? (pk[q][k] >> sbits) : 0u));
       }
     if (r + 2 < r1) load_round(r + 2, sl);
 #pragma unroll
@@ -832,6 +843,18 @@ __device__ __forceinline__ void tl_stream_wide(const uint32_t* __restrict__ pack
 // CONSECUTIVE sorted entries (neighbouring columns in the forward, neighbouring rows in the transpose) instead of
 // 64 entries spaced 4 apart, so each gather instruction touches ~4x fewer distinct cache lines in the sparse tail.
 // Two-slot stream prefetch as tl_stream_p0; no lower-bound masks (windows are round-aligned).
+// Profiling ablation of the interleaved stream, compiled only with -DPML_TL_ABLATE (a runtime check in the
+// production loop cost ~30 %): set through pml_set_ablate, bit 8 -> no coefficient gathers (x = 1), bit 16 -> no
+// LDS adds (register sum, one add per lane at the end). Measured (16M rows, bf16): the gathers are the whole
+// difference between the stream rate (fwd 5.9 TB/s, transpose 4.6 TB/s without them) and the full kernels;
+// removing the LDS adds changes nothing.
+#ifdef PML_TL_ABLATE
+__constant__ int c_tl_ablate = 0;
+#define TL_ABL c_tl_ablate
+#else
+#define TL_ABL 0
+#endif
+
 template <typename VT, typename XT, typename AT, bool SQ, int NW>
 __device__ __forceinline__ void tl_stream_il(const uint32_t* __restrict__ pack, const VT* __restrict__ val,
                                              const XT* __restrict__ x, int e_lo, int e_hi, int sbits, AT* acc) {
@@ -842,11 +865,13 @@ __device__ __forceinline__ void tl_stream_il(const uint32_t* __restrict__ pack, 
   const int nr = (e_hi - e_lo + TL_ROUND - 1) / TL_ROUND;
   const int r0 = (nr * w) / NW, r1 = (nr * (w + 1)) / NW;
   if (r0 >= r1) return;
+  const int abl = TL_ABL;
+  AT regsum = AT(0);
   v4u pkA, pkB;
   Raw vA, vB;
   auto load_round = [&](int r, v4u& pk, Raw& v) {
     const int e = e_lo + r * TL_ROUND + lane * TL_VEC;  // physical quad: always inside the padded unit
-    pk = __builtin_nontemporal_load((const v4u*)(pack + e));
+    pk = ldg_nt((const v4u*)(pack + e));
     v = TLVals<VT>::load(val + e);
   };
   auto process = [&](int r, v4u& pk_slot, Raw& v_slot) {
@@ -858,25 +883,29 @@ __device__ __forceinline__ void tl_stream_il(const uint32_t* __restrict__ pack, 
 #pragma unroll
     for (int k = 0; k < TL_VEC; ++k) {
       in[k] = e + 64 * k < e_hi;
-      xv[k] = x[in[k] ? (pk[k] >> sbits) : 0u];
+      xv[k] = (abl & 8) ? XT(1) : ldg(x + (in[k] ? (pk[k] >> sbits) : 0u));
     }
-    if (r + 2 < r1) load_round(r + 2, pk_slot, v_slot);
+    // unconditional refill (past the end: re-read round r, L2-hot, never used) so the wave's outstanding-load
+    // count is static and each LDS add waits only for its own gather (vmcnt(5..2)), not for the prefetch
+    load_round(r + 2 < r1 ? r + 2 : r, pk_slot, v_slot);
     LT v[TL_VEC];
     TLVals<VT>::get(v_raw, v);
+    // branchless: padding / past-the-end entries add an exact 0 (select, not multiply: no NaN from x)
 #pragma unroll
     for (int k = 0; k < TL_VEC; ++k) {
-      if (in[k]) {
-        const AT vv = SQ ? static_cast<AT>(v[k]) * static_cast<AT>(v[k]) : static_cast<AT>(v[k]);
-        atomicAdd(&acc[pk[k] & smask], vv * static_cast<AT>(xv[k]));
-      }
+      const AT vv = SQ ? static_cast<AT>(v[k]) * static_cast<AT>(v[k]) : static_cast<AT>(v[k]);
+      const AT add = in[k] ? vv * static_cast<AT>(xv[k]) : AT(0);
+      if (abl & 16) regsum += add + AT(pk[k] & smask);
+      else atomicAdd(&acc[in[k] ? (pk[k] & smask) : 0u], add);
     }
   };
   load_round(r0, pkA, vA);
-  if (r0 + 1 < r1) load_round(r0 + 1, pkB, vB);
+  load_round(r0 + 1 < r1 ? r0 + 1 : r0, pkB, vB);
   for (int r = r0; r < r1; r += 2) {
     process(r, pkA, vA);
     if (r + 1 < r1) process(r + 1, pkB, vB);
   }
+  if (abl & 16) atomicAdd(&acc[lane], regsum);
 }
 
 // pipeline variant: P = 0 two-slot stream prefetch; P = 1 three-stage (stream r+2 / gather r+1 / accumulate r);
@@ -1366,7 +1395,12 @@ static int t_impl(const SegChunkDesc* c, const void* x, double* G, double* parts
 extern "C" {
 
 int pml_version() { return 1; }
-void pml_set_ablate(int a) { g_ablate = a; }
+void pml_set_ablate(int a) {
+  g_ablate = a;
+#ifdef PML_TL_ABLATE
+  (void)hipMemcpyToSymbol(HIP_SYMBOL(c_tl_ablate), &a, sizeof(int));
+#endif
+}
 // layout: 0 = vector, 1 = strided; grid: persistent forward grid size (workgroups)
 void pml_set_config(int fwd_strided, int t_strided, int hot_n, int fwd_grid) {
   g_fwd_strided = fwd_strided; g_t_strided = t_strided; g_hot_n = hot_n;
