@@ -64,6 +64,9 @@ def main():
     ap.add_argument("--l2", type=float, default=1.0)
     ap.add_argument("--l1", type=float, default=10.0, help="L1 weight of the owlqn config")
     ap.add_argument("--seed", type=int, default=1234567890)
+    ap.add_argument("--optimizer-state", default="replicated", choices=["replicated", "feature-sharded"],
+                    help="replicated: one all-reduce of [g|F|S] per evaluation (default); feature-sharded: w, g and "
+                         "the L-BFGS history sharded over features (all-gather w + reduce-scatter g per evaluation)")
     ap.add_argument("--layout", default="auto", choices=["auto", "tiled", "segmented"],
                     help="sparse layout: tiled (gather-coalesced, default when representable) or segmented")
     args = ap.parse_args()
@@ -102,7 +105,8 @@ def main():
     torch.cuda.synchronize()
     log(f"data ready in {time.time() - t_gen:.1f}s: {data.n_rows} rows/GPU, {data.nbytes() / 2**30:.1f} GiB/GPU, "
         f"layout={data.layout}")
-    gdata = DistributedGLMData(data) if world > 1 else data
+    sharded = args.optimizer_state == "feature-sharded"
+    gdata = DistributedGLMData(data) if world > 1 and not sharded else data
 
     if args.config == "owlqn":
         obj = GLMObjective(LOGISTIC, l2_weight=0.0)
@@ -113,27 +117,38 @@ def main():
     else:
         obj = GLMObjective(LOGISTIC, l2_weight=args.l2)
         opt = LBFGS(tolerance=0.0, max_iterations=10 ** 9, track_state=False)
+    import contextlib
+    space = contextlib.nullcontext()
     w0 = torch.zeros(args.features, dtype=torch.float64, device=dev)
-    opt.start(obj, gdata, w0, skip_zero_tolerance_pass=True)
-    for i in range(args.warmup):
-        st = opt.step(obj, gdata)
-        log(f"warmup {i + 1}/{args.warmup}: f={st.loss:.6e}")
-    torch.cuda.synchronize()
-    barrier()
-    passes0 = data.n_passes
-    t0 = time.perf_counter()
-    for i in range(args.steps):
-        st = opt.step(obj, gdata)
-    torch.cuda.synchronize()
-    barrier()
-    elapsed = time.perf_counter() - t0
+    if sharded:
+        from photon_ml_amd.optimization.vector_space import ShardedSpace, active_space
+        from photon_ml_amd.parallel.feature_sharding import FeatureShardLayout, FeatureShardedObjective
+        layout = FeatureShardLayout.current(args.features)
+        obj = FeatureShardedObjective(obj, layout)
+        w0 = layout.slice(w0).clone()
+        space = active_space(ShardedSpace())
+    with space:
+        opt.start(obj, gdata, w0, skip_zero_tolerance_pass=True)
+        for i in range(args.warmup):
+            st = opt.step(obj, gdata)
+            log(f"warmup {i + 1}/{args.warmup}: f={st.loss:.6e}")
+        torch.cuda.synchronize()
+        barrier()
+        passes0 = data.n_passes
+        t0 = time.perf_counter()
+        for i in range(args.steps):
+            st = opt.step(obj, gdata)
+        torch.cuda.synchronize()
+        barrier()
+        elapsed = time.perf_counter() - t0
+        gnorm = st.grad_norm()
     elapsed = all_reduce_scalar(elapsed, "max", device=dev)
     passes = data.n_passes - passes0
     stalled = bool(getattr(opt, "_finished", False))
-    total_rows = gdata.n_rows if world > 1 else data.n_rows
+    total_rows = int(all_reduce_scalar(data.n_rows, "sum", device=dev)) if world > 1 else data.n_rows
     value = total_rows * args.steps / elapsed
     if rank == 0:
-        log(f"final f={st.loss:.6e} |g|={st.grad_norm():.3e} evals/step={passes / args.steps:.2f} "
+        log(f"final f={st.loss:.6e} |g|={gnorm:.3e} evals/step={passes / args.steps:.2f} "
             f"optimizer_stalled={stalled}")
         out = {
             "metric": cfg["metric"],
@@ -155,7 +170,8 @@ def main():
                 "rows_per_gpu": args.rows_per_gpu,
                 "features": args.features,
                 "nnz_per_row": args.nnz,
-                "parallelism": f"dp{world}",
+                "parallelism": f"dp{world}" + ("+fs" if sharded else ""),
+                "optimizer_state": args.optimizer_state,
                 "layout": data.layout,
             },
             "evals_per_step": passes / args.steps,

@@ -212,18 +212,21 @@ def train_generalized_linear_model(data: LabeledData, task, optimizer_type="LBFG
                                    normalization: Optional[NormalizationContext] = None, max_iterations: int = 80,
                                    tolerance: float = 1e-6, constraint_map=None, warm_start_models=None,
                                    use_warm_start: bool = True, compute_variance: bool = False, device=None,
-                                   precision: str = "f64", glm_data=None):
-    """ModelTraining.trainGeneralizedLinearModel -> list of (lambda, model, tracker), lambdas DESCENDING."""
+                                   precision: str = "f64", glm_data=None, feature_sharded: bool = False):
+    """ModelTraining.trainGeneralizedLinearModel -> list of (lambda, model, tracker), lambdas DESCENDING.
+
+    ``feature_sharded``: under a process group, shard the optimizer state over features instead of replicating
+    it (``parallel/feature_sharding.py``; for models too large to replicate)."""
     device = torch.device(device) if device is not None else default_device()
     gdata = glm_data if glm_data is not None else make_glm_data(data, device, precision)
-    view = DistributedGLMData(gdata) if is_dist() else gdata
+    view = DistributedGLMData(gdata) if is_dist() and not feature_sharded else gdata
     lams = sorted(regularization_weights, reverse=True)
     out = []
     prev = None
     for lam in lams:
         cfg = GLMOptimizationConfiguration(OptimizerConfig(optimizer_type, max_iterations, tolerance, constraint_map),
                                            regularization, lam)
-        prob = GLMOptimizationProblem(cfg, task, normalization, compute_variance)
+        prob = GLMOptimizationProblem(cfg, task, normalization, compute_variance, feature_sharded=feature_sharded)
         init = None
         if warm_start_models and lam in warm_start_models:
             init = warm_start_models[lam]

@@ -19,15 +19,13 @@ from typing import Optional
 import torch
 
 from .line_search import LineSearchFailed, backtracking, strong_wolfe
+from . import vector_space
 from .optimizer import Optimizer, OptimizerState, project_box
+from .vector_space import vdot as _dot, vnorm as _norm
 
 DEFAULT_MAX_ITER = 100
 DEFAULT_NUM_CORRECTIONS = 10
 DEFAULT_TOLERANCE = 1.0e-7
-
-
-def _dot(a, b) -> float:
-    return float(torch.dot(a, b))
 
 
 class _History:
@@ -57,6 +55,8 @@ class _History:
 
     def apply_inverse(self, g: torch.Tensor) -> torch.Tensor:
         """Two-loop recursion: returns H g."""
+        if vector_space.current().sharded and self.s:
+            return self._apply_inverse_gram(g)
         q = g.clone()
         k = len(self.s)
         alpha = [0.0] * k
@@ -70,6 +70,28 @@ class _History:
             beta = self.rho[i] * _dot(self.y[i], q)
             q.add_(self.s[i], alpha=alpha[i] - beta)
         return q
+
+    def _apply_inverse_gram(self, g: torch.Tensor) -> torch.Tensor:
+        """Vector-free two-loop (Chen, Wang & Zhou 2014, "Large-scale L-BFGS using MapReduce"): H g is a linear
+        combination of the basis b = [s_0..s_{k-1}, y_0..y_{k-1}, g]; the recursion runs on the (2k+1) coefficient
+        vector delta using the Gram matrix B = b b^T, which costs ONE batched all-reduce of (2k+1)^2 scalars per
+        iteration over feature shards instead of 4k+1 sequential scalar all-reduces. Exact in exact arithmetic."""
+        k = len(self.s)
+        basis = self.s + self.y + [g]
+        B = vector_space.current().gram(basis)
+        delta = torch.zeros(2 * k + 1, dtype=torch.float64)
+        delta[2 * k] = 1.0
+        alpha = [0.0] * k
+        for i in range(k - 1, -1, -1):
+            alpha[i] = self.rho[i] * float(delta @ B[:, i])          # rho_i s_i . q
+            delta[k + i] -= alpha[i]                                 # q -= alpha_i y_i
+        yy = float(B[2 * k - 1, 2 * k - 1])
+        delta *= (1.0 / self.rho[-1]) / yy
+        for i in range(k):
+            beta = self.rho[i] * float(delta @ B[:, k + i])           # rho_i y_i . r
+            delta[i] += alpha[i] - beta                              # r += (alpha_i - beta) s_i
+        V = torch.stack(basis)
+        return delta.to(V.device, V.dtype) @ V
 
 
 class LBFGS(Optimizer):
@@ -108,7 +130,7 @@ class LBFGS(Optimizer):
     def _search(self, objective, data, state: OptimizerState, d: torch.Tensor):
         x0 = state.coefficients
         g0 = _dot(state.gradient, d)
-        t0 = 1.0 / float(torch.linalg.vector_norm(d)) if self._inner_iter == 0 else 1.0
+        t0 = 1.0 / _norm(d) if self._inner_iter == 0 else 1.0
 
         def phi(t):
             x = x0 + t * d
@@ -123,7 +145,7 @@ class LBFGS(Optimizer):
             return state
         try:
             d = self._direction(state)
-            if not bool(torch.any(d != 0)):
+            if not vector_space.current().any_nonzero(d):
                 self._finished = True  # zero (pseudo-)gradient: stationary point
                 return state
             x, f, g = self._search(objective, data, state, d)
@@ -162,7 +184,7 @@ class OWLQN(LBFGS):
         return torch.where(at_zero, pg_zero, g + lam * torch.sign(x))
 
     def _adjust(self, x, f, g):
-        return f + self.l1_weight * float(torch.sum(torch.abs(x))), self._pseudo_gradient(x, g)
+        return f + self.l1_weight * vector_space.current().abs_sum(x), self._pseudo_gradient(x, g)
 
     def _direction(self, state):
         d = -self.history.apply_inverse(state.gradient)
@@ -173,7 +195,7 @@ class OWLQN(LBFGS):
         x0 = state.coefficients
         pg = state.gradient
         orthant = torch.where(x0 != 0, torch.sign(x0), torch.sign(-pg))
-        t0 = 1.0 / float(torch.linalg.vector_norm(d)) if self._inner_iter == 0 else 1.0
+        t0 = 1.0 / _norm(d) if self._inner_iter == 0 else 1.0
         shrink = 0.1 if self._inner_iter < 1 else 0.5
 
         def phi(t):

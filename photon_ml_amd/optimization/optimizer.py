@@ -19,6 +19,7 @@ from typing import Dict, List, Optional, Tuple
 import torch
 
 from ..normalization.context import NormalizationContext, no_normalization
+from . import vector_space
 
 
 class ConvergenceReason(str, enum.Enum):
@@ -36,7 +37,7 @@ class OptimizerState:
     iter: int
 
     def grad_norm(self) -> float:
-        return float(torch.linalg.vector_norm(self.gradient))
+        return vector_space.vnorm(self.gradient)
 
 
 class OptimizationStatesTracker:
@@ -164,7 +165,7 @@ class Optimizer:
         w0 = self.normalization.model_to_transformed_space(initial.to(torch.float64))
         self.clear_inner_state()
         init_state = self._calculate_state(objective, data, w0)
-        if skip_zero_tolerance_pass and bool(torch.all(w0 == 0)):
+        if skip_zero_tolerance_pass and vector_space.current().all_zero(w0):
             self._set_abs_tolerances(init_state)
         else:
             self._set_abs_tolerances(self._calculate_state(objective, data, torch.zeros_like(w0)))

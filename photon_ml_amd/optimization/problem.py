@@ -24,8 +24,11 @@ from .lbfgs import OWLQN
 
 class GLMOptimizationProblem:
     def __init__(self, config: GLMOptimizationConfiguration, task, normalization: Optional[NormalizationContext] = None,
-                 compute_variance: bool = False, track_state: bool = True):
+                 compute_variance: bool = False, track_state: bool = True, feature_sharded: bool = False):
         self.config = config
+        # optimizer state sharded over features across the process group (parallel/feature_sharding.py); the
+        # data passed to run() is then this rank's row shard, not a DistributedGLMData wrapper
+        self.feature_sharded = feature_sharded
         self.task = TaskType.parse(task)
         self.loss = loss_for_task(self.task)
         self.normalization = normalization or no_normalization()
@@ -56,6 +59,8 @@ class GLMOptimizationProblem:
         d = dim if dim is not None else data.dim
         w0 = (initial.coefficients.means.to(dev, torch.float64) if initial is not None
               else torch.zeros(d, dtype=torch.float64, device=dev))
+        if self.feature_sharded:
+            return self._run_feature_sharded(data, w0)
         if self.optimizer.needs_hessian and hasattr(data, "track_hessian"):
             data.track_hessian = True
         w_t, _ = self.optimizer.optimize(self.objective, data, w0)
@@ -65,6 +70,24 @@ class GLMOptimizationProblem:
             variances = self.normalization.model_to_original_space(1.0 / (hd + EPSILON))
         means = self.normalization.model_to_original_space(w_t)
         model = model_for_task(self.task, Coefficients(means.detach(), None if variances is None else variances))
+        model.validate_coefficients()
+        return model
+
+    def _run_feature_sharded(self, data, w0: torch.Tensor) -> GeneralizedLinearModel:
+        from ..parallel.feature_sharding import optimize_feature_sharded
+        local = getattr(data, "local", data)
+        reg = self.config.regularization_context
+        opt = build_optimizer(self.config.optimizer_config, None, reg, self.config.regularization_weight,
+                              self.track_state)
+        self.optimizer = opt
+        means, _, sobj = optimize_feature_sharded(opt, self.objective, local, w0, self.normalization)
+        variances = None
+        if self.compute_variance and self.loss.twice_differentiable:
+            from ..parallel.feature_sharding import all_gather_shards
+            w_t = self.normalization.model_to_transformed_space(means.clone())
+            hd = all_gather_shards(sobj.hessian_diagonal(local, sobj.layout.slice(w_t)), sobj.layout, sobj.group)
+            variances = self.normalization.model_to_original_space(1.0 / (hd + EPSILON))
+        model = model_for_task(self.task, Coefficients(means.detach(), variances))
         model.validate_coefficients()
         return model
 

@@ -17,6 +17,7 @@ import math
 import torch
 
 from .optimizer import Optimizer, OptimizerState, project_box
+from .vector_space import vdot as _dot, vnorm as _norm
 
 DEFAULT_MAX_NUM_FAILURE = 5
 DEFAULT_TOLERANCE = 1.0e-5
@@ -24,14 +25,6 @@ DEFAULT_MAX_ITER = 15
 MAX_CG_ITERATIONS = 20
 
 log = logging.getLogger(__name__)
-
-
-def _dot(a, b) -> float:
-    return float(torch.dot(a, b))
-
-
-def _norm(a) -> float:
-    return float(torch.linalg.vector_norm(a))
 
 
 class TRON(Optimizer):

@@ -84,6 +84,39 @@ def sharding_worker(rank, world, port, out):
     dist.destroy_process_group()
 
 
+def fsdp_worker(rank, world, port, out):
+    """Feature-sharded optimizer state (each rank: half the rows, a 1/world slice of w, g and the history)."""
+    _init(rank, world, port)
+    from photon_ml_amd.data.synthetic import generate_glm_data
+    from photon_ml_amd.function.losses import loss_for_task
+    from photon_ml_amd.function.objective import GLMObjective
+    from photon_ml_amd.normalization.context import NormalizationContext
+    from photon_ml_amd.ops.backend import make_glm_data
+    from photon_ml_amd.optimization.config import OptimizerConfig, RegularizationContext, build_optimizer
+    from photon_ml_amd.parallel.feature_sharding import optimize_feature_sharded
+    from photon_ml_amd.stat.summary import BasicStatisticalSummary
+    data, _ = generate_glm_data("LOGISTIC_REGRESSION", 3000, 41, density=0.2, seed=7)
+    local = data.subset(np.arange(rank, data.n_rows, world))
+    gd = make_glm_data(local, "cpu", "f64")
+    for opt, reg, norm in (("LBFGS", "L2", None), ("TRON", "L2", None), ("LBFGS", "L1", None),
+                           ("LBFGS", "L2", "STANDARDIZATION")):
+        rc = RegularizationContext(reg)
+        nc = None
+        if norm:
+            nc = NormalizationContext.build(norm, BasicStatisticalSummary.compute(data.x), data.n_features - 1)
+        obj = GLMObjective(loss_for_task("LOGISTIC_REGRESSION"), rc.l2_weight(1.0), nc)
+        o = build_optimizer(OptimizerConfig(opt, 200, 1e-10), None, rc, 1.0, track_state=False)
+        w, f, _ = optimize_feature_sharded(o, obj, gd, normalization=nc)
+        np.save(f"{out}/fsdp_{opt}_{reg}_{norm}_r{rank}.npy", w.numpy())
+    from photon_ml_amd.estimators.game_estimator import train_generalized_linear_model
+    m = train_generalized_linear_model(local, "LOGISTIC_REGRESSION", "TRON", RegularizationContext("L2"), [1.0],
+                                       max_iterations=100, tolerance=1e-10, compute_variance=True, device="cpu",
+                                       feature_sharded=True)[0][1]
+    np.save(f"{out}/fsdp_api_r{rank}.npy", np.stack([m.coefficients.means.numpy(), m.coefficients.variances.numpy()]))
+    import torch.distributed as dist
+    dist.destroy_process_group()
+
+
 if __name__ == "__main__":
-    fn = {"glm": glm_worker, "game": game_worker, "sharding": sharding_worker}[sys.argv[1]]
+    fn = {"glm": glm_worker, "game": game_worker, "sharding": sharding_worker, "fsdp": fsdp_worker}[sys.argv[1]]
     fn(int(sys.argv[2]), int(sys.argv[3]), int(sys.argv[4]), sys.argv[5])
