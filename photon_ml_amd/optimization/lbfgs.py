@@ -115,6 +115,17 @@ class LBFGS(Optimizer):
         self._finished = False
         self._inner_iter = 0
 
+    def _inner_state(self) -> dict:
+        h = self.history
+        return {"s": list(h.s), "y": list(h.y), "rho": list(h.rho), "failed_once": self._failed_once,
+                "finished": self._finished, "inner_iter": self._inner_iter, "smooth_f": self._smooth_f,
+                "smooth_g": self._smooth_g}
+
+    def _load_inner_state(self, d: dict):
+        self.history.s, self.history.y, self.history.rho = list(d["s"]), list(d["y"]), list(d["rho"])
+        self._failed_once, self._finished, self._inner_iter = d["failed_once"], d["finished"], d["inner_iter"]
+        self._smooth_f, self._smooth_g = d["smooth_f"], d["smooth_g"]
+
     # -- L1 hooks (identity for plain L-BFGS) --------------------------------
     def _adjust(self, x, f, g):
         return f, g

@@ -196,6 +196,32 @@ class Optimizer:
             self.tracker.convergence_reason = self.convergence_reason()
         return self.current.coefficients, self.current.loss
 
+    # checkpoint / resume ---------------------------------------------
+    def state_dict(self) -> dict:
+        """Everything needed to continue the run bitwise-identically (SURVEY §5 checkpoint: coefficients,
+        L-BFGS history, TRON trust radius, tolerances). Tensors stay on their device; ``utils.checkpoint``
+        serialises with safetensors."""
+        def st(s: Optional[OptimizerState]):
+            return None if s is None else {"coefficients": s.coefficients, "loss": s.loss, "gradient": s.gradient,
+                                           "iter": s.iter}
+        return {"kind": type(self).__name__, "loss_abs_tol": self.loss_abs_tol, "grad_abs_tol": self.grad_abs_tol,
+                "current": st(self.current), "previous": st(self.previous), "inner": self._inner_state()}
+
+    def load_state_dict(self, sd: dict):
+        if sd["kind"] != type(self).__name__:
+            raise ValueError(f"checkpoint of a {sd['kind']} cannot resume a {type(self).__name__}")
+        self.clear_inner_state()
+        self.loss_abs_tol, self.grad_abs_tol = sd["loss_abs_tol"], sd["grad_abs_tol"]
+        mk = lambda d: None if d is None else OptimizerState(d["coefficients"], d["loss"], d["gradient"], d["iter"])
+        self.previous, self.current = mk(sd["previous"]), mk(sd["current"])
+        self._load_inner_state(sd["inner"])
+
+    def _inner_state(self) -> dict:
+        return {}
+
+    def _load_inner_state(self, d: dict):
+        pass
+
     # hooks -----------------------------------------------------------
     def _init(self, objective, data, state: OptimizerState):
         raise NotImplementedError

@@ -29,6 +29,7 @@ class GLMOptimizationProblem:
         # optimizer state sharded over features across the process group (parallel/feature_sharding.py); the
         # data passed to run() is then this rank's row shard, not a DistributedGLMData wrapper
         self.feature_sharded = feature_sharded
+        self.checkpointer, self.checkpoint_every = None, 1
         self.task = TaskType.parse(task)
         self.loss = loss_for_task(self.task)
         self.normalization = normalization or no_normalization()
@@ -63,7 +64,10 @@ class GLMOptimizationProblem:
             return self._run_feature_sharded(data, w0)
         if self.optimizer.needs_hessian and hasattr(data, "track_hessian"):
             data.track_hessian = True
-        w_t, _ = self.optimizer.optimize(self.objective, data, w0)
+        if self.checkpointer is not None:
+            w_t = self._optimize_checkpointed(data, w0)
+        else:
+            w_t, _ = self.optimizer.optimize(self.objective, data, w0)
         variances = None
         if self.compute_variance and self.loss.twice_differentiable:
             hd = self.objective.hessian_diagonal(data, w_t)
@@ -72,6 +76,23 @@ class GLMOptimizationProblem:
         model = model_for_task(self.task, Coefficients(means.detach(), None if variances is None else variances))
         model.validate_coefficients()
         return model
+
+    def enable_checkpointing(self, checkpointer, every: int = 1):
+        """Save the optimizer state every ``every`` iterations (and resume from an existing checkpoint)."""
+        self.checkpointer, self.checkpoint_every = checkpointer, max(1, int(every))
+        return self
+
+    def _optimize_checkpointed(self, data, w0):
+        opt = self.optimizer
+        if not self.checkpointer.load_optimizer(opt, device=w0.device):
+            opt.start(self.objective, data, w0)
+        while not opt.is_done():
+            opt.step(self.objective, data)
+            if opt.current.iter % self.checkpoint_every == 0:
+                self.checkpointer.save_optimizer(opt)
+        if opt.tracker is not None:
+            opt.tracker.convergence_reason = opt.convergence_reason()
+        return opt.current.coefficients
 
     def _run_feature_sharded(self, data, w0: torch.Tensor) -> GeneralizedLinearModel:
         from ..parallel.feature_sharding import optimize_feature_sharded

@@ -48,6 +48,12 @@ class TRON(Optimizer):
     def _init(self, objective, data, state):
         self.delta = state.grad_norm()
 
+    def _inner_state(self) -> dict:
+        return {"delta": self.delta, "total_cg_iterations": self.total_cg_iterations}
+
+    def _load_inner_state(self, d: dict):
+        self.delta, self.total_cg_iterations = d["delta"], d["total_cg_iterations"]
+
     @staticmethod
     def truncated_cg(objective, data, w, gradient, delta):
         step = torch.zeros_like(gradient)

@@ -30,7 +30,12 @@ def env_world() -> tuple[int, int, int]:
 def init_distributed(backend: Optional[str] = None, timeout_s: int = 1800) -> tuple[int, int, int]:
     """Initialise the default process group from torchrun env vars (no-op for world size 1)."""
     rank, world, local = env_world()
+    from ..utils.watchdog import start_watchdog
+    start_watchdog()  # PML_WATCHDOG_S: abort this rank (-> torchrun aborts the group) when progress stops
     if world > 1 and not dist.is_initialized():
+        # a collective that exceeds ``timeout_s`` raises instead of hanging (RCCL async error handling)
+        os.environ.setdefault("TORCH_NCCL_ASYNC_ERROR_HANDLING", "1")
+        timeout_s = int(os.environ.get("PML_COLLECTIVE_TIMEOUT_S", timeout_s))
         os.environ.setdefault("MASTER_ADDR", "127.0.0.1")
         os.environ.setdefault("MASTER_PORT", "29500")
         if backend is None:

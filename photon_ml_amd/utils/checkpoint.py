@@ -143,3 +143,44 @@ class Checkpointer:
         best = game_model_from_arrays(arrays, meta["best"], "best/") if "best" in meta else None
         return {"model": model, "iteration": meta["iteration"], "next": meta["next"], "best_model": best,
                 "best_evals": meta.get("best_evals"), "history": meta.get("history", []), "tag": meta.get("tag")}
+
+    # ---- optimizer state (mid-solve checkpoint of one GLM / fixed-effect optimisation)
+    def save_optimizer(self, optimizer, tag: str = ""):
+        """Serialise ``optimizer.state_dict()``: tensors -> safetensors arrays (fp64, host copies), scalars and
+        structure -> JSON metadata. Resuming with :meth:`load_optimizer` continues bitwise-identically."""
+        arrays: Dict[str, np.ndarray] = {}
+
+        def enc(v, key):
+            import torch
+            if isinstance(v, torch.Tensor):
+                arrays[key] = v.detach().cpu().numpy()
+                return {"__t": key, "device": str(v.device)}
+            if isinstance(v, dict):
+                return {k: enc(x, f"{key}/{k}") for k, x in v.items()}
+            if isinstance(v, (list, tuple)):
+                return {"__l": [enc(x, f"{key}/{i}") for i, x in enumerate(v)]}
+            return v
+
+        meta = {"optimizer": enc(optimizer.state_dict(), "opt"), "tag": tag}
+        self.save(arrays, meta)
+
+    def load_optimizer(self, optimizer, device=None) -> bool:
+        """Restore into ``optimizer``; returns False when there is no checkpoint."""
+        got = self.load()
+        if got is None:
+            return False
+        arrays, meta = got
+        import torch
+
+        def dec(v):
+            if isinstance(v, dict) and "__t" in v:
+                return torch.from_numpy(arrays[v["__t"]].copy()).to(device or v["device"])
+            if isinstance(v, dict) and "__l" in v:
+                return [dec(x) for x in v["__l"]]
+            if isinstance(v, dict):
+                return {k: dec(x) for k, x in v.items()}
+            return v
+
+        optimizer.load_state_dict(dec(meta["optimizer"]))
+        return True
+

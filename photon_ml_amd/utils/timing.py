@@ -17,6 +17,8 @@ import time
 from collections import defaultdict
 from contextlib import contextmanager
 
+from .watchdog import heartbeat
+
 TIMELINE = defaultdict(list)
 _TRACE = os.environ.get("PML_TRACE", "0") == "1"
 _TIMELINE_PATH = os.environ.get("PML_TIMELINE")
@@ -63,6 +65,7 @@ class Timed:
         return self
 
     def __exit__(self, *exc):
+        heartbeat()
         self.elapsed = time.perf_counter() - self.t0
         if self._pushed:
             _roctx_pop()
@@ -78,6 +81,7 @@ def trace_range(name: str):
     try:
         yield
     finally:
+        heartbeat()
         if pushed:
             _roctx_pop()
 
