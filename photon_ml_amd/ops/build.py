@@ -27,9 +27,18 @@ CPP_SOURCES = {
 ARCH = os.environ.get("PYTORCH_ROCM_ARCH", "gfx950").split(";")[0]
 
 
-def lib_path(kind: str, name: str) -> Path:
+def sanitize_enabled() -> bool:
+    """``PML_NATIVE_SANITIZE=1``: load the AddressSanitizer + UBSan builds of the HOST C++ libraries (Avro codec,
+    index map). GPU sanitizers are unavailable on the target pool, so device code is checked by host-side shape
+    validation and the kernel parity tests instead (SURVEY §5 race detection / sanitizers)."""
+    return os.environ.get("PML_NATIVE_SANITIZE", "0") == "1"
+
+
+def lib_path(kind: str, name: str, sanitize: bool = None) -> Path:
     base = PKG / ("ops" if kind == "hip" else "io") / "_lib"
-    return base / f"libpml_{name}.so"
+    if sanitize is None:
+        sanitize = kind != "hip" and sanitize_enabled()
+    return base / f"libpml_{name}{'_asan' if sanitize else ''}.so"
 
 
 def _needs_build(src: Path, out: Path) -> bool:
@@ -61,9 +70,10 @@ def build_hip(name: str, force: bool = False, verbose: bool = False) -> Path:
     return out
 
 
-def build_cpp(name: str, force: bool = False, verbose: bool = False) -> Path:
+def build_cpp(name: str, force: bool = False, verbose: bool = False, sanitize: bool = None) -> Path:
     src = CPP_SOURCES[name]
-    out = lib_path("cpp", name)
+    sanitize = sanitize_enabled() if sanitize is None else sanitize
+    out = lib_path("cpp", name, sanitize)
     if not src.exists():
         return out
     out.parent.mkdir(parents=True, exist_ok=True)
@@ -72,7 +82,9 @@ def build_cpp(name: str, force: bool = False, verbose: bool = False) -> Path:
         import pybind11
         inc = ["-I" + sysconfig.get_paths()["include"], "-I" + pybind11.get_include()]
         vis = ["-fvisibility=hidden"] if name == "avro" else []  # pybind11 module vs plain C ABI
-        cmd = ["g++", "-O3", "-std=c++17", "-fPIC", "-shared", *vis, *inc, str(src), "-o", str(out) + ".tmp",
+        opt = ["-O1", "-g", "-fno-omit-frame-pointer", "-fsanitize=address,undefined",
+               "-fno-sanitize-recover=undefined"] if sanitize else ["-O3"]
+        cmd = ["g++", *opt, "-std=c++17", "-fPIC", "-shared", *vis, *inc, str(src), "-o", str(out) + ".tmp",
                "-lz"]
         if verbose:
             print(" ".join(cmd), flush=True)

@@ -16,6 +16,7 @@ No atomics anywhere: results are bitwise reproducible run to run.
 from __future__ import annotations
 
 import ctypes
+import os
 from dataclasses import dataclass
 from typing import List, Optional, Sequence
 
@@ -156,6 +157,54 @@ class DeviceGLMData(GLMComputable):
         if self.old_of_new is not None:
             self.new_of_old = torch.empty_like(self.old_of_new)
             self.new_of_old[self.old_of_new] = torch.arange(self.dim, device=self.device)
+        if os.environ.get("PML_CHECK_KERNEL_INPUTS", "0") == "1":
+            self.validate()
+
+    def validate(self):
+        """Host-side check of every invariant the HIP kernels index by (no GPU sanitizer on the target pool):
+        block/item windows inside their streams, round-aligned interleaved windows, gather indices < the column
+        window / chunk rows, LDS slots < 2^bits, row ranges inside the shard. Raises ValueError on violation.
+        Enabled at construction with ``PML_CHECK_KERNEL_INPUTS=1`` (costs one host pass over the streams)."""
+        from .tiled import il_phys
+        for c, (f, t) in enumerate(zip(self.csr, self.csc)):
+            if f.kind != "tl":
+                continue
+            m = self.row_starts[c + 1] - self.row_starts[c]
+            b = f.blk.cpu().to(torch.int64)
+            if f.nblk and (int(b[:, 0].min()) < 0 or int((b[:, 0] + b[:, 1]).max()) > m
+                           or int(b[:, 1].max()) > (1 << f.rbits)):
+                raise ValueError(f"chunk {c}: forward block rows out of range")
+            q = 256 if f.il else 4   # the kernels read whole rounds (il) / whole quads
+            end = b[:, 2] + (b[:, 3] - b[:, 2] + q - 1) // q * q if f.il else (b[:, 3] + 3) // 4 * 4
+            if f.nblk and (int(b[:, 2].min()) < 0 or int(end.max()) > f.pack.numel()):
+                raise ValueError(f"chunk {c}: forward block window outside the stream")
+            if f.il and f.nblk and bool((b[:, 2] % 256 != 0).any()):
+                raise ValueError(f"chunk {c}: interleaved forward windows not round-aligned")
+            pk, _ = f.logical()
+            p = pk.cpu().to(torch.int64) & 0xFFFFFFFF
+            ncols = int(self.dim) - self.col_lo[c]
+            if p.numel() and int((p >> f.rbits).max()) >= ncols:
+                raise ValueError(f"chunk {c}: forward gather index >= column window")
+            counts = (b[:, 3] - b[:, 2])
+            blk_rows = torch.repeat_interleave(b[:, 1], counts)
+            if p.numel() and bool(((p & ((1 << f.rbits) - 1)) >= blk_rows).any()):
+                raise ValueError(f"chunk {c}: forward LDS slot >= block rows")
+            it = t.items.cpu().to(torch.int64)
+            if t.nitems:
+                if int(it[:, 1].min()) < 0 or int(it[:, 2].max()) > t.pack.numel():
+                    raise ValueError(f"chunk {c}: transpose item window outside the stream")
+                if int(it[:, 3].max()) >= max(t.nparts, 1) and t.nparts:
+                    raise ValueError(f"chunk {c}: transpose partial-row slot out of range")
+                tp, _ = t.logical()
+                q = tp.cpu().to(torch.int64) & 0xFFFFFFFF
+                if q.numel() and int((q >> t.cbits).max()) >= m:
+                    raise ValueError(f"chunk {c}: transpose gather row >= chunk rows")
+                cols = (torch.repeat_interleave(it[:, 0], it[:, 2] - it[:, 1]) << t.cbits) + (q & ((1 << t.cbits) - 1))
+                if q.numel() and int(cols.max()) >= t.dim:
+                    raise ValueError(f"chunk {c}: transpose column >= dim")
+        if self.parts.numel() < max([c.parts_needed for c in self.csr + self.csc] + [1]):
+            raise ValueError("partial-row scratch too small")
+        return True
 
     # ------------------------------------------------------------------
     @staticmethod

@@ -4,6 +4,8 @@ import sys
 import pytest
 
 sys.path.insert(0, os.path.dirname(os.path.dirname(os.path.abspath(__file__))))
+# every device shard built in a test is validated on the host before a kernel can index it
+os.environ.setdefault("PML_CHECK_KERNEL_INPUTS", "1")
 
 
 def pytest_configure(config):

@@ -72,6 +72,14 @@ def test_device_data_construction_cpu(layout):
     assert dev.layout == layout and len(dev.csr) == 3 and len(dev.csc) == 3
     assert dev.stats.numel() >= 2 * sum(c.nstats for c in dev.csr)
     assert dev.parts.numel() >= max(c.parts_needed for c in dev.csc)
+    if layout == "tiled":
+        assert dev.validate()
+        # a corrupted gather index is caught on the host before any kernel could read out of bounds
+        f = dev.csr[1]
+        lo = int(f.blk[0, 2])
+        f.pack[lo] = (300 + 5) << f.rbits
+        with pytest.raises(ValueError, match="gather index"):
+            dev.validate()
 
 
 @pytest.mark.parametrize("chunk,item,hot", [(700, 64, False), (1000, 300, True), (5000, 1 << 16, False)])
