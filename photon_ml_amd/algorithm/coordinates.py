@@ -13,6 +13,7 @@ from the partial-score vector (C11 routing) before each batched solve.
 """
 from __future__ import annotations
 
+import os
 import time
 from typing import Optional
 
@@ -27,7 +28,7 @@ from ..models.game import FixedEffectModel, RandomEffectModel
 from ..models.glm import Coefficients, model_for_task
 from ..normalization.context import NormalizationContext
 from ..ops.backend import default_device, make_glm_data
-from ..optimization.batched import BatchedGLMData, batched_lbfgs, batched_tron
+from ..optimization.batched import BatchedGLMData, BatchedResult, batched_lbfgs, batched_tron
 from ..optimization.config import GLMOptimizationConfiguration, OptimizerType, RegularizationType
 from ..optimization.problem import GLMOptimizationProblem
 from ..parallel.dist import DistributedGLMData, is_dist
@@ -245,10 +246,31 @@ class RandomEffectCoordinate(Coordinate):
         W0 = self._warm_start_segmented(model)
         t_start = time.time()
         oc = cfg.optimizer_config
-        if oc.optimizer_type == OptimizerType.TRON:
-            res = batched_tron(seg, self.loss, l2, W0, oc.tolerance, oc.maximum_iterations)
+        rs = self._row_space(l1, oc)
+        frozen = None
+        if rs is not None and rs.B:
+            # wide entities (n_e <= d_e) solved exactly in their row space (optimization/row_space.py)
+            opt = "TRON" if oc.optimizer_type == OptimizerType.TRON else "LBFGS"
+            rres = rs.solve(self.loss, l2, opt, W0, oc.tolerance, oc.maximum_iterations,
+                            reuse_beta=self._W.get("seg") is not None)
+            frozen = rs.mask
+            W0 = torch.where(seg.bexp(frozen), torch.zeros_like(W0), W0)
+        if frozen is None or not bool(frozen.all()):
+            if oc.optimizer_type == OptimizerType.TRON:
+                res = batched_tron(seg, self.loss, l2, W0, oc.tolerance, oc.maximum_iterations, frozen=frozen)
+            else:
+                res = batched_lbfgs(seg, self.loss, l2, W0, oc.tolerance, oc.maximum_iterations, l1=l1,
+                                    frozen=frozen)
+            W_all, iters, reasons = res.W, res.iters, res.reason
         else:
-            res = batched_lbfgs(seg, self.loss, l2, W0, oc.tolerance, oc.maximum_iterations, l1=l1)
+            W_all = torch.zeros_like(W0)
+            iters = torch.zeros(seg.B, dtype=torch.long, device=W0.device)
+            reasons = torch.zeros(seg.B, dtype=torch.long, device=W0.device)
+        if frozen is not None:
+            W_all = W_all + rs.to_primal(rres.W)
+            iters = iters.index_copy(0, rs.ents, rres.iters)
+            reasons = reasons.index_copy(0, rs.ents, rres.reason)
+        res = BatchedResult(W_all, None, iters, reasons)
         self._W["seg"] = res.W
         act = torch.from_numpy(ds.n_active > 0).to(res.iters.device)
         self.last_stats = random_effect_tracker_stats(res.iters[act], res.reason[act], time.time() - t_start)
@@ -262,6 +284,15 @@ class RandomEffectCoordinate(Coordinate):
                                 ds.entity_ids, ds.dim, keys[nz], W[nz], None if var is None else var[nz])
         self._last = (out, res.W)
         return out
+
+    def _row_space(self, l1: float, oc):
+        """Row-space batch for the wide entities (built once per dataset), or None when not applicable."""
+        from ..optimization.row_space import RowSpaceBatch, row_space_eligible
+        if os.environ.get("PML_RE_ROW_SPACE", "1") == "0" or not row_space_eligible(l1, oc.constraint_map):
+            return None
+        if getattr(self, "_rs", None) is None:
+            self._rs = RowSpaceBatch(self.dataset.seg)
+        return self._rs
 
     def _warm_start_segmented(self, model):
         ds = self.dataset

@@ -98,8 +98,11 @@ def glm_lib() -> Optional[ctypes.CDLL]:
         lib.pml_segdot.argtypes = [c_void_p, c_void_p, c_int, c_void_p, c_int, c_void_p, c_void_p]
         lib.pml_seg_expand.argtypes = [c_void_p, c_int, c_void_p, c_void_p, c_int, c_void_p]
         lib.pml_seg_cg_step.argtypes = [c_void_p, c_int] + [c_void_p] * 7 + [c_double, c_void_p]
+        lib.pml_bgemv.argtypes = [c_int, c_int, c_void_p, c_void_p, c_void_p, c_int, c_void_p]
+        lib.pml_bhv.argtypes = [c_int, c_int, c_void_p, c_void_p, c_void_p, c_double, c_void_p, c_void_p]
         for f in ("pml_seg_fwd", "pml_seg_t", "pml_reduce_stats", "pml_build_blocks", "pml_tl_fwd", "pml_tl_t",
-                  "pml_tl_maxbits", "pml_segdot", "pml_tl_fwd_multi", "pml_tl_t_multi", "pml_seg_cg_step", "pml_seg_expand"):
+                  "pml_tl_maxbits", "pml_segdot", "pml_tl_fwd_multi", "pml_tl_t_multi", "pml_seg_cg_step",
+                  "pml_seg_expand", "pml_bgemv", "pml_bhv"):
             getattr(lib, f).restype = c_int
         lib.pml_set_config.argtypes = [c_int, c_int, c_int, c_int]
         lib._pml_typed = True
@@ -155,6 +158,38 @@ def segdot(a: torch.Tensor, b: Optional[torch.Tensor], ptr: torch.Tensor, mode: 
     out = torch.empty(nseg, dtype=torch.float64, device=a.device)
     check(lib.pml_segdot(a.data_ptr(), b.data_ptr(), mode, ptr.data_ptr(), nseg, out.data_ptr(),
                          stream_handle(a.device)), "segdot")
+    return out
+
+
+def batched_gemv(A: torch.Tensor, x: torch.Tensor, trans: bool = False) -> torch.Tensor:
+    """``y[b] = A[b] x[b]`` (or ``A[b]^T x[b]``) for a batch of small square fp64 matrices (n <= 64):
+    ``bgemv_kernel`` on the device, ``bmm`` on the host."""
+    if A.device.type != "cuda" or A.shape[-1] > 64 or A.shape[-1] != A.shape[-2]:
+        M = A.transpose(1, 2) if trans else A
+        return torch.bmm(M, x.unsqueeze(-1)).squeeze(-1)
+    lib = require_glm_lib()
+    A, x = A.contiguous(), x.contiguous()
+    B, n, _ = A.shape
+    assert A.dtype == torch.float64 and x.dtype == torch.float64 and x.shape == (B, n)
+    y = torch.empty_like(x)
+    check(lib.pml_bgemv(B, n, A.data_ptr(), x.data_ptr(), y.data_ptr(), int(trans), stream_handle(A.device)),
+          "bgemv")
+    return y
+
+
+def batched_hv(A: torch.Tensor, dw: torch.Tensor, v: torch.Tensor, l2: float = 0.0) -> torch.Tensor:
+    """``A^T (dw * (A v)) + l2 v`` per problem (fp64, n <= 64): one read of each block (``bhv_kernel``)."""
+    if A.device.type != "cuda" or A.shape[-1] > 64 or A.shape[-1] != A.shape[-2]:
+        xv = torch.bmm(A, v.unsqueeze(-1)).squeeze(-1)
+        h = torch.bmm(A.transpose(1, 2), (dw * xv).unsqueeze(-1)).squeeze(-1)
+        return h + l2 * v if l2 > 0 else h
+    lib = require_glm_lib()
+    A, dw, v = A.contiguous(), dw.contiguous(), v.contiguous()
+    B, n, _ = A.shape
+    assert A.dtype == dw.dtype == v.dtype == torch.float64 and v.shape == (B, n) and dw.shape == (B, n)
+    out = torch.empty_like(v)
+    check(lib.pml_bhv(B, n, A.data_ptr(), dw.data_ptr(), v.data_ptr(), float(l2), out.data_ptr(),
+                      stream_handle(A.device)), "bhv")
     return out
 
 

@@ -57,14 +57,21 @@ class BatchedGLMData:
     def shape(self):
         return tuple(self.X.shape)
 
+    def _mv(self, v, trans: bool = False):
+        from ..ops.native import batched_gemv
+        if self.X.shape[1] == self.X.shape[2] and self.X.dtype == torch.float64:
+            return batched_gemv(self.X, v, trans)   # small square blocks (row-space problems): HIP kernel
+        M = self.X.transpose(1, 2) if trans else self.X
+        return torch.bmm(M, v.unsqueeze(-1)).squeeze(-1)
+
     def margins(self, W: torch.Tensor) -> torch.Tensor:
-        return torch.bmm(self.X, W.unsqueeze(-1)).squeeze(-1) + self.o
+        return self._mv(W) + self.o
 
     def value_grad(self, loss, W, l2: float):
         z = self.margins(W)
         l, dl = loss.loss_and_dz(z, self.y)
         f = (self.w * l).sum(1)
-        g = torch.bmm(self.X.transpose(1, 2), (self.w * dl).unsqueeze(-1)).squeeze(-1)
+        g = self._mv(self.w * dl, trans=True)
         if l2 > 0:
             f = f + 0.5 * l2 * (W * W).sum(1)
             g = g + l2 * W
@@ -82,6 +89,9 @@ class BatchedGLMData:
 
     def hv(self, loss, W, V, l2: float):
         D = self._dzz_at(loss, W)
+        if self.X.shape[1] == self.X.shape[2] and self.X.dtype == torch.float64:
+            from ..ops.native import batched_hv
+            return batched_hv(self.X, D, V, l2)
         xv = torch.bmm(self.X, V.unsqueeze(-1)).squeeze(-1)
         h = torch.bmm(self.X.transpose(1, 2), (D * xv).unsqueeze(-1)).squeeze(-1)
         return h + l2 * V if l2 > 0 else h
@@ -213,8 +223,12 @@ class _Convergence:
 
 
 def batched_tron(data, loss, l2: float, W0: torch.Tensor, tol: float = 1e-5, max_iter: int = 15,
-                 max_fail: int = 5, max_cg: int = 20, fused: Optional[bool] = None) -> BatchedResult:
+                 max_fail: int = 5, max_cg: int = 20, fused: Optional[bool] = None,
+                 frozen: Optional[torch.Tensor] = None) -> BatchedResult:
     """Vectorised TRON (``photon-lib/.../optimization/TRON.scala:80-340``) over a batch of entities.
+
+    ``frozen`` [B] bool: entities solved elsewhere (e.g. in their row space, ``row_space.py``) — kept at W0, not
+    iterated, reason code 0.
 
     ``fused``: run each CG iteration's vector algebra as one segmented kernel (``data.cg_step``; default when the
     data provides it, i.e. the block-diagonal layout) instead of ~30 elementwise / reduction ops."""
@@ -241,6 +255,9 @@ def batched_tron(data, loss, l2: float, W0: torch.Tensor, tol: float = 1e-5, max
     zero_g = _bn(data, g) == 0
     reason = torch.where(zero_g, torch.full_like(reason, 4), reason)
     active &= ~zero_g
+    if frozen is not None:
+        active &= ~frozen
+        reason = torch.where(frozen, torch.zeros_like(reason), reason)
     guard = 0
     while bool(active.any()):
         guard += 1
@@ -329,7 +346,8 @@ def batched_tron(data, loss, l2: float, W0: torch.Tensor, tol: float = 1e-5, max
 
 
 def batched_lbfgs(data, loss, l2: float, W0: torch.Tensor, tol: float = 1e-7,
-                  max_iter: int = 100, m: int = 10, l1: float = 0.0, max_ls: int = 30) -> BatchedResult:
+                  max_iter: int = 100, m: int = 10, l1: float = 0.0, max_ls: int = 30,
+                  frozen: Optional[torch.Tensor] = None) -> BatchedResult:
     """Vectorised L-BFGS (OWL-QN when ``l1 > 0``) with backtracking Armijo line search per entity."""
     W = W0.clone()
     B = data.n_batch
@@ -361,6 +379,9 @@ def batched_lbfgs(data, loss, l2: float, W0: torch.Tensor, tol: float = 1e-7,
     reason = torch.zeros(B, dtype=torch.long, device=dev)
     active = _bn(data, g) > 0
     reason = torch.where(~active, torch.full_like(reason, 4), reason)
+    if frozen is not None:
+        active &= ~frozen
+        reason = torch.where(frozen, torch.zeros_like(reason), reason)
     for _ in range(max_iter + 2):
         if not bool(active.any()):
             break

@@ -162,3 +162,35 @@ def test_fused_cg_step_matches_unfused_tron(task):
     assert torch.equal(res[False].iters, res[True].iters)
     assert torch.allclose(res[False].W, res[True].W, rtol=1e-9, atol=1e-11)
     assert torch.allclose(res[False].f, res[True].f, rtol=1e-12)
+
+
+@pytest.mark.parametrize("task,opt", [("LOGISTIC_REGRESSION", "TRON"), ("LINEAR_REGRESSION", "LBFGS"),
+                                      ("POISSON_REGRESSION", "TRON"), ("LOGISTIC_REGRESSION", "LBFGS")])
+def test_row_space_random_effect_solve_matches_primal(task, opt, monkeypatch):
+    """Wide entities (n_e rows < d_e coefficients) solved in their row space (w = X^T L^-T beta, exact
+    re-parametrisation) give the primal block-diagonal solution, the same per-entity iteration counts, and the
+    same warm-started second coordinate-descent update; entities with more rows than coefficients, or beyond
+    the row cap, stay on the primal path in the same solve."""
+    # Zipf users: most have a few rows (wide -> row space), a few have many (-> primal path in the same solve)
+    data, _ = generate_game_data(n_rows=2500, n_users=300, d_user=30, seed=21, task=task)
+    cfg = _cfg(opt, 1.0, 60, 1e-10)
+    out = {}
+    for mode in ("0", "1"):
+        monkeypatch.setenv("PML_RE_ROW_SPACE", mode)
+        c = RandomEffectCoordinate("u", data, RandomEffectDataConfiguration("userId", "user"), cfg, task,
+                                   device="cpu", layout="segmented")
+        m1 = c.update_model(c.initialize_model())
+        it1 = c.last_stats
+        m2 = c.update_model(m1, partial_score=torch.from_numpy(np.sin(np.arange(data.n_rows)) * 0.3))
+        out[mode] = (c, m1, m2, it1)
+        if mode == "1":
+            assert c._rs is not None and 0 < c._rs.B < int((c.dataset.n_active > 0).sum())
+    (c0, a1, a2, s0), (c1, b1, b2, s1) = out["0"], out["1"]
+    # same iterates in exact arithmetic; at tol 1e-10 rounding can move a convergence test by one iteration
+    assert s0["mean_iterations"] == pytest.approx(s1["mean_iterations"], rel=0.02)
+    # entities that stop on "objective not improving" may stop one rounding-level step apart
+    for (a, b), tol in (((a1, b1), 2e-7), ((a2, b2), 5e-6)):
+        for e in a.entity_ids:
+            np.testing.assert_allclose(a.coefficients_of(e).means.numpy(), b.coefficients_of(e).means.numpy(),
+                                       rtol=1e-4, atol=tol)
+    assert torch.allclose(c0.score(a2), c1.score(b2), atol=1e-5)

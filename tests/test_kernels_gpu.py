@@ -276,3 +276,21 @@ def test_seg_expand_kernel():
         ref = torch.repeat_interleave(s, lens)
         out = seg_expand(s.cuda(), ptr.cuda(), n)
         assert out.dtype == s.dtype and torch.equal(out.cpu(), ref)
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("n", [1, 5, 20, 32, 64])
+def test_batched_small_gemv_and_hv_match_torch(n):
+    """bgemv_kernel / bhv_kernel (row-space random-effect solve) vs fp64 torch bmm references."""
+    from photon_ml_amd.ops.native import batched_gemv, batched_hv
+    g = torch.Generator(device="cuda").manual_seed(n)
+    B = 1003
+    A = torch.randn(B, n, n, dtype=torch.float64, device="cuda", generator=g)
+    x = torch.randn(B, n, dtype=torch.float64, device="cuda", generator=g)
+    dw = torch.rand(B, n, dtype=torch.float64, device="cuda", generator=g)
+    ref = torch.bmm(A, x.unsqueeze(-1)).squeeze(-1)
+    reft = torch.bmm(A.transpose(1, 2), x.unsqueeze(-1)).squeeze(-1)
+    torch.testing.assert_close(batched_gemv(A, x), ref, rtol=1e-12, atol=1e-12)
+    torch.testing.assert_close(batched_gemv(A, x, trans=True), reft, rtol=1e-12, atol=1e-12)
+    hv = torch.bmm(A.transpose(1, 2), (dw * ref).unsqueeze(-1)).squeeze(-1) + 0.7 * x
+    torch.testing.assert_close(batched_hv(A, dw, x, 0.7), hv, rtol=1e-12, atol=1e-11)
