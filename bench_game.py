@@ -124,8 +124,8 @@ def main():
     total_rows = int(all_reduce_scalar(float(data.n_rows)))
     if rank == 0:
         log(f"final training loss {loss:.6e}; RE stats {re_stats}")
-        for rec in cd.history[-2:]:
-            log(f"  coordinate {rec['coordinate']}: {rec['seconds']:.3f}s")
+        for rec in cd.history[-2 * args.steps:]:
+            log(f"  iteration {rec.get('iteration')} coordinate {rec['coordinate']}: {rec['seconds']:.3f}s")
         print(json.dumps({
             "metric": "GAME coord-descent iters/sec (fixed + per-entity random effect)",
             "value": args.steps / elapsed,

@@ -13,6 +13,7 @@ from the partial-score vector (C11 routing) before each batched solve.
 """
 from __future__ import annotations
 
+import logging
 import os
 import time
 from typing import Optional
@@ -21,6 +22,7 @@ import numpy as np
 import torch
 
 from ..constants import EPSILON, TaskType
+from ..utils.timing import Timed
 from ..data.game_data import GameData
 from ..data.random_effect import FixedEffectDataConfiguration, RandomEffectDataConfiguration, RandomEffectDataset
 from ..function.losses import loss_for_task
@@ -33,6 +35,15 @@ from ..optimization.config import GLMOptimizationConfiguration, OptimizerType, R
 from ..optimization.problem import GLMOptimizationProblem
 from ..parallel.dist import DistributedGLMData, is_dist
 from ..sampling.samplers import down_sampler_for_task
+
+
+log = logging.getLogger(__name__)
+
+
+def _sync(t):
+    """Device sync for phase timing (``PML_SYNC_TIMING=1`` only; asynchronous otherwise)."""
+    if os.environ.get("PML_SYNC_TIMING") == "1" and t is not None and t.is_cuda:
+        torch.cuda.synchronize(t.device)
 
 
 def random_effect_tracker_stats(iters: torch.Tensor, reasons: torch.Tensor, seconds: float) -> dict:
@@ -107,17 +118,26 @@ class FixedEffectCoordinate(Coordinate):
     def initialize_model(self):
         return FixedEffectModel(model_for_task(self.task, Coefficients.zeros(self.dim)), self.shard_id)
 
+    def _device_row_data(self):
+        """Base offsets / weights (and the DP row subset) kept on the data's device: the per-update residual
+        offsets are formed there (C15: no N-length host round trip per coordinate update)."""
+        if getattr(self, "_base_off_t", None) is None:
+            dev = getattr(self.glm_data, "device", torch.device("cpu"))
+            self._base_off_t = torch.from_numpy(self.base_offsets).to(dev)
+            self._rows_t = None if self.local_rows is None else torch.from_numpy(
+                np.asarray(self.local_rows, dtype=np.int64)).to(dev)
+        return self._base_off_t, self._rows_t
+
     def update_model(self, model: FixedEffectModel, partial_score: Optional[torch.Tensor] = None):
-        off = self.base_offsets
+        base, rows = self._device_row_data()
+        off = base
         if partial_score is not None:
-            ps = partial_score.detach().cpu().numpy()
-            if self.local_rows is not None:
-                ps = ps[self.local_rows]
-            off = off + ps
-        self.glm_data.set_offsets(torch.from_numpy(off))
-        wts = self.base_weights if self.sampler is None else self.sampler.sample_weights(self.labels,
-                                                                                            self.base_weights)
-        self.glm_data.set_weights(torch.from_numpy(np.asarray(wts, dtype=np.float64)))
+            ps = partial_score.detach().to(base.device, torch.float64)
+            off = base + (ps if rows is None else ps[rows])
+        self.glm_data.set_offsets(off)
+        if self.sampler is not None:
+            wts = self.sampler.sample_weights(self.labels, self.base_weights)
+            self.glm_data.set_weights(torch.from_numpy(np.asarray(wts, dtype=np.float64)))
         glm = self.problem.run(self._data_view(), model.glm if model is not None else None, dim=self.dim)
         self.last_tracker = self.problem.tracker
         # restore full weights for scoring/evaluation
@@ -246,28 +266,34 @@ class RandomEffectCoordinate(Coordinate):
         W0 = self._warm_start_segmented(model)
         t_start = time.time()
         oc = cfg.optimizer_config
-        rs = self._row_space(l1, oc)
+        with Timed(f"RE {self.coordinate_id}: row-space setup", log, logging.DEBUG):
+            rs = self._row_space(l1, oc)
         frozen = None
         if rs is not None and rs.B:
             # wide entities (n_e <= d_e) solved exactly in their row space (optimization/row_space.py)
             opt = "TRON" if oc.optimizer_type == OptimizerType.TRON else "LBFGS"
-            rres = rs.solve(self.loss, l2, opt, W0, oc.tolerance, oc.maximum_iterations,
-                            reuse_beta=self._W.get("seg") is not None)
+            with Timed(f"RE {self.coordinate_id}: row-space solve", log, logging.DEBUG):
+                rres = rs.solve(self.loss, l2, opt, W0, oc.tolerance, oc.maximum_iterations,
+                                reuse_beta=self._W.get("seg") is not None)
+                _sync(W0)
             frozen = rs.mask
             W0 = torch.where(seg.bexp(frozen), torch.zeros_like(W0), W0)
         if frozen is None or not bool(frozen.all()):
-            if oc.optimizer_type == OptimizerType.TRON:
-                res = batched_tron(seg, self.loss, l2, W0, oc.tolerance, oc.maximum_iterations, frozen=frozen)
-            else:
-                res = batched_lbfgs(seg, self.loss, l2, W0, oc.tolerance, oc.maximum_iterations, l1=l1,
-                                    frozen=frozen)
-            W_all, iters, reasons = res.W, res.iters, res.reason
+            with Timed(f"RE {self.coordinate_id}: primal block-diagonal solve", log, logging.DEBUG):
+                if oc.optimizer_type == OptimizerType.TRON:
+                    res = batched_tron(seg, self.loss, l2, W0, oc.tolerance, oc.maximum_iterations, frozen=frozen)
+                else:
+                    res = batched_lbfgs(seg, self.loss, l2, W0, oc.tolerance, oc.maximum_iterations, l1=l1,
+                                        frozen=frozen)
+                W_all, iters, reasons = res.W, res.iters, res.reason
         else:
             W_all = torch.zeros_like(W0)
             iters = torch.zeros(seg.B, dtype=torch.long, device=W0.device)
             reasons = torch.zeros(seg.B, dtype=torch.long, device=W0.device)
         if frozen is not None:
-            W_all = W_all + rs.to_primal(rres.W)
+            with Timed(f"RE {self.coordinate_id}: row-space -> primal", log, logging.DEBUG):
+                W_all = W_all + rs.to_primal(rres.W)
+                _sync(W_all)
             iters = iters.index_copy(0, rs.ents, rres.iters)
             reasons = reasons.index_copy(0, rs.ents, rres.reason)
         res = BatchedResult(W_all, None, iters, reasons)

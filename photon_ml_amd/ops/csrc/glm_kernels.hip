@@ -23,6 +23,7 @@
 #include <hip/hip_runtime.h>
 #include <stdint.h>
 #include <math.h>
+#include <algorithm>
 
 #define NB 4096          // max entries per block
 #define NTHREADS 256     // 4 wave64 per block
@@ -1394,57 +1395,79 @@ static int t_impl(const SegChunkDesc* c, const void* x, double* G, double* parts
 
 // ============================================================================================================
 // Batched SMALL dense products for the row-space random-effect solve (optimization/row_space.py): a batch of
-// B problems with n x n (n <= 64) fp64 design matrices L_b. A wave holds floor(64 / n) problems, lane
-// (g, i) = problem g's row i; each problem's n^2 block is read once per product (rows stay L1-resident across
-// the column loop), fp64 accumulation in a fixed order (deterministic). rocBLAS batched GEMM/GEMV pick a
-// 32x64 tile per problem for these shapes (0.63 ms per product at 250K problems of 20 x 20, measured).
+// B problems with n x n (n <= 64) fp64 design matrices. A wave owns per = floor(64 / n) CONSECUTIVE problems,
+// i.e. one contiguous run of per * n^2 doubles: it is staged through LDS with coalesced loads (rows padded to
+// n + 1 doubles: conflict-free row reads), then lane (g, i) = problem g's row / column i computes its dot
+// product from LDS with x_j broadcast by shuffles. fp64 accumulation in a fixed order (deterministic).
+// Measured on MI355X at 250K problems of 20 x 20: rocBLAS batched GEMM 0.63 ms, an L1-strided version of this
+// kernel 1.0 ms (uncoalesced row reads thrash L1) — the staged form streams the blocks once.
 // ============================================================================================================
+__device__ __forceinline__ void stage_blocks(const double* __restrict__ A, long long b0, int count, int n,
+                                             double* sA) {
+  const int lane = threadIdx.x & 63;
+  const int nn = n * n, np = n * (n + 1);
+  const double* src = A + b0 * nn;
+  const int tot = count * nn;
+  for (int k = lane; k < tot; k += 64) {
+    const int p = k / nn, rem = k - p * nn;
+    const int i = rem / n, j = rem - i * n;
+    sA[p * np + i * (n + 1) + j] = ldg_nt(src + k);
+  }
+}
+
 __global__ __launch_bounds__(NTHREADS) void bgemv_kernel(int B, int n, const double* __restrict__ A,
                                                           const double* __restrict__ x, double* __restrict__ y,
                                                           int trans) {
-  const int lane = threadIdx.x & 63;
-  const int per = 64 / n;
+  extern __shared__ double smem[];
+  const int lane = threadIdx.x & 63, w = threadIdx.x >> 6;
+  const int per = 64 / n, np = n * (n + 1);
+  double* sA = smem + w * per * np;
+  const long long b0 = ((long long)blockIdx.x * (blockDim.x >> 6) + w) * per;
+  if (b0 >= B) return;
+  const int count = (int)min((long long)per, B - b0);
+  stage_blocks(A, b0, count, n, sA);
   const int g = lane / n, i = lane - g * n;
-  const long long b = ((long long)blockIdx.x * (NTHREADS / 64) + (threadIdx.x >> 6)) * per + g;
-  const bool on = g < per && b < B;
-  const long long bb = on ? b : 0;
-  const double* Ab = A + bb * n * n;
-  const int base = lane - i;                     // first lane of this problem's group
-  const double xi = on ? x[bb * n + i] : 0.0;
+  const bool on = g < count;
+  const int base = lane - i;
+  const double xi = on ? x[(b0 + g) * n + i] : 0.0;
+  __builtin_amdgcn_s_waitcnt(0);
+  __builtin_amdgcn_wave_barrier();
+  const double* Ab = sA + (on ? g : 0) * np;
   double acc = 0.0;
   for (int j = 0; j < n; ++j) {
     const double xj = __shfl(xi, base + j, 64);
-    const double a = on ? (trans ? Ab[(long long)j * n + i] : Ab[(long long)i * n + j]) : 0.0;
-    acc = fma(a, xj, acc);
+    acc = fma(trans ? Ab[j * (n + 1) + i] : Ab[i * (n + 1) + j], xj, acc);
   }
-  if (on) y[bb * n + i] = acc;
+  if (on) y[(b0 + g) * n + i] = acc;
 }
 
 // out = A^T (dw .* (A v)) + l2 v  (Hessian-vector product of the batched dense GLM, one read of each block)
 __global__ __launch_bounds__(NTHREADS) void bhv_kernel(int B, int n, const double* __restrict__ A,
                                                         const double* __restrict__ dw, const double* __restrict__ v,
                                                         double l2, double* __restrict__ out) {
-  const int lane = threadIdx.x & 63;
-  const int per = 64 / n;
+  extern __shared__ double smem[];
+  const int lane = threadIdx.x & 63, w = threadIdx.x >> 6;
+  const int per = 64 / n, np = n * (n + 1);
+  double* sA = smem + w * per * np;
+  const long long b0 = ((long long)blockIdx.x * (blockDim.x >> 6) + w) * per;
+  if (b0 >= B) return;
+  const int count = (int)min((long long)per, B - b0);
+  stage_blocks(A, b0, count, n, sA);
   const int g = lane / n, i = lane - g * n;
-  const long long b = ((long long)blockIdx.x * (NTHREADS / 64) + (threadIdx.x >> 6)) * per + g;
-  const bool on = g < per && b < B;
-  const long long bb = on ? b : 0;
-  const double* Ab = A + bb * n * n;
+  const bool on = g < count;
   const int base = lane - i;
-  const double vi = on ? v[bb * n + i] : 0.0;
+  const long long o = (b0 + (on ? g : 0)) * n + i;
+  const double vi = on ? v[o] : 0.0;
+  const double dwi = on ? dw[o] : 0.0;
+  __builtin_amdgcn_s_waitcnt(0);
+  __builtin_amdgcn_wave_barrier();
+  const double* Ab = sA + (on ? g : 0) * np;
   double t = 0.0;
-  for (int j = 0; j < n; ++j) {
-    const double vj = __shfl(vi, base + j, 64);
-    t = fma(on ? Ab[(long long)i * n + j] : 0.0, vj, t);
-  }
-  t *= on ? dw[bb * n + i] : 0.0;
+  for (int j = 0; j < n; ++j) t = fma(Ab[i * (n + 1) + j], __shfl(vi, base + j, 64), t);
+  t *= dwi;
   double acc = 0.0;
-  for (int r = 0; r < n; ++r) {
-    const double tr = __shfl(t, base + r, 64);
-    acc = fma(on ? Ab[(long long)r * n + i] : 0.0, tr, acc);
-  }
-  if (on) out[bb * n + i] = acc + l2 * vi;
+  for (int r = 0; r < n; ++r) acc = fma(Ab[r * (n + 1) + i], __shfl(t, base + r, 64), acc);
+  if (on) out[o] = acc + l2 * vi;
 }
 
 extern "C" {
@@ -1639,8 +1662,12 @@ int pml_bgemv(int B, int n, const double* A, const double* x, double* y, int tra
   if (B <= 0) return 0;
   if (n < 1 || n > 64) return -22;
   const long long waves = (B + (64 / n) - 1) / (64 / n);
-  const long long grid = (waves + NTHREADS / 64 - 1) / (NTHREADS / 64);
-  hipLaunchKernelGGL(bgemv_kernel, dim3((unsigned)grid), dim3(NTHREADS), 0, (hipStream_t)stream, B, n, A, x, y, trans);
+  const size_t wave_lds = (size_t)(64 / n) * n * (n + 1) * sizeof(double);
+  const int nw = (int)std::max<size_t>(1, std::min<size_t>(4, 65536 / wave_lds));  // <= 64 KB LDS per workgroup
+  const long long grid = (waves + nw - 1) / nw;
+  const size_t lds = nw * wave_lds;
+  hipLaunchKernelGGL(bgemv_kernel, dim3((unsigned)grid), dim3(nw * 64), lds, (hipStream_t)stream, B, n, A, x, y,
+                     trans);
   LAUNCH_CHECK();
   return 0;
 }
@@ -1649,8 +1676,12 @@ int pml_bhv(int B, int n, const double* A, const double* dw, const double* v, do
   if (B <= 0) return 0;
   if (n < 1 || n > 64) return -22;
   const long long waves = (B + (64 / n) - 1) / (64 / n);
-  const long long grid = (waves + NTHREADS / 64 - 1) / (NTHREADS / 64);
-  hipLaunchKernelGGL(bhv_kernel, dim3((unsigned)grid), dim3(NTHREADS), 0, (hipStream_t)stream, B, n, A, dw, v, l2, out);
+  const size_t wave_lds = (size_t)(64 / n) * n * (n + 1) * sizeof(double);
+  const int nw = (int)std::max<size_t>(1, std::min<size_t>(4, 65536 / wave_lds));  // <= 64 KB LDS per workgroup
+  const long long grid = (waves + nw - 1) / nw;
+  const size_t lds = nw * wave_lds;
+  hipLaunchKernelGGL(bhv_kernel, dim3((unsigned)grid), dim3(nw * 64), lds, (hipStream_t)stream, B, n, A, dw, v, l2,
+                     out);
   LAUNCH_CHECK();
   return 0;
 }

@@ -44,11 +44,27 @@ class BatchedGLMData:
     def n_batch(self) -> int:
         return self.X.shape[0]
 
+    def _regular_ptr(self):
+        p = getattr(self, "_ptr", None)
+        if p is None:
+            B, _, d = self.X.shape
+            p = self._ptr = torch.arange(B + 1, dtype=torch.int64, device=self.X.device) * d
+        return p
+
     def bdot(self, a, b):
+        if a.is_cuda and a.dtype == torch.float64 and a.is_contiguous() and b.is_contiguous():
+            from ..ops.native import segdot   # one deterministic kernel instead of multiply + reduce
+            return segdot(a.view(-1), b.view(-1), self._regular_ptr(), 0)
         return (a * b).sum(-1)
 
     def bexp(self, s):
         return s.unsqueeze(-1)
+
+    def cg_step(self, step, r, d, Hd, rtr, on, delta, l2: float = 0.0):
+        """Fused truncated-CG iteration for every problem (``seg_cg_step`` over the regular [B, d] layout)."""
+        from ..ops.native import seg_cg_step
+        seg_cg_step(self._regular_ptr(), step.view(-1), r.view(-1), d.view(-1), Hd.contiguous().view(-1), rtr, on,
+                    delta, l2)
 
     def babs_sum(self, a):
         return a.abs().sum(-1)
