@@ -1470,6 +1470,155 @@ __global__ __launch_bounds__(NTHREADS) void bhv_kernel(int B, int n, const doubl
   if (on) out[o] = acc + l2 * vi;
 }
 
+// ============================================================================================================
+// Fused per-entity TRON for the row-space random-effect problems ("one workgroup per entity,
+// dense tiles in LDS"). Each problem is a dense GLM with an n x n design matrix L (n <= 64, fp64): a lane group
+// of G = pow2 >= n lanes owns one problem (lane i: data row i AND coefficient i), the block sits in LDS for the
+// whole solve, and the complete trust-region Newton iteration — truncated CG with Hessian-vector products
+// L^T (D (L d)), trust-region radius updates, accept / reject, Photon convergence tests — runs in registers.
+// One HBM read of L per SOLVE instead of one per Hessian-vector product. Semantics follow batched_tron in
+// optimization/batched.py (which follows TRON.scala:80-340): eta = (1e-4, .25, .75), sigma = (.25, .5, 4),
+// delta0 = ||g0||, first-iteration delta = min(delta, ||step||), CG tolerance 0.1 ||g||, <= max_cg CG steps,
+// <= max_fail consecutive rejections; reason codes 1 max-iter, 2 not-improving, 3 f-converged, 4 g-converged.
+// Per-problem reductions are fixed-order butterflies inside the lane group: deterministic.
+// ============================================================================================================
+__global__ __launch_bounds__(NTHREADS) void rs_tron_kernel(
+    int B, int n, int G, const double* __restrict__ Lm, const double* __restrict__ Y, const double* __restrict__ O,
+    const double* __restrict__ WT, double* __restrict__ Beta, double* __restrict__ Fout, int* __restrict__ Iters,
+    int* __restrict__ Reason, int loss, double l2, double tol, int max_iter, int max_fail, int max_cg) {
+  extern __shared__ double smem[];
+  const int lane = threadIdx.x & 63, w = threadIdx.x >> 6;
+  const int per = 64 / G, np = n * (n + 1);
+  double* sA = smem + w * per * np;
+  const long long b0 = ((long long)blockIdx.x * (blockDim.x >> 6) + w) * per;
+  if (b0 >= B) return;
+  const int count = (int)min((long long)per, B - b0);
+  stage_blocks(Lm, b0, count, n, sA);
+  const int g = lane / G, i = lane - g * G;
+  const bool prob_on = g < count;
+  const bool on = prob_on && i < n;
+  const long long b = b0 + (prob_on ? g : 0);
+  const long long o = b * n + (i < n ? i : 0);
+  const double y = on ? Y[o] : 0.0, off = on ? O[o] : 0.0, wt = on ? WT[o] : 0.0;
+  double W = on ? Beta[o] : 0.0;
+  const int base = lane - i;
+  const int ii = on ? i : 0;
+  __builtin_amdgcn_s_waitcnt(0);
+  __builtin_amdgcn_wave_barrier();
+  const double* Lb = sA + (prob_on ? g : 0) * np;
+
+  auto gsum = [&](double v) {
+    for (int s = G >> 1; s > 0; s >>= 1) v += __shfl_xor(v, s, 64);
+    return v;
+  };
+  auto mv = [&](double v) {  // (L v)_i
+    double acc = 0.0;
+    for (int j = 0; j < n; ++j) acc = fma(Lb[ii * (n + 1) + j], __shfl(v, base + j, 64), acc);
+    return on ? acc : 0.0;
+  };
+  auto mvt = [&](double u) {  // (L^T u)_i
+    double acc = 0.0;
+    for (int r = 0; r < n; ++r) acc = fma(Lb[r * (n + 1) + ii], __shfl(u, base + r, 64), acc);
+    return on ? acc : 0.0;
+  };
+  auto vg = [&](double v, double& f, double& gr, double& Dw) {
+    const double z = mv(v) + off;
+    double l, dl, d2;
+    pointwise_loss(loss, z, y, l, dl, d2);
+    if (!on) { l = 0.0; dl = 0.0; d2 = 0.0; }
+    f = gsum(wt * l + 0.5 * l2 * v * v);
+    gr = mvt(wt * dl) + l2 * v;
+    Dw = wt * d2;
+  };
+  const double eta0 = 1e-4, eta1 = 0.25, eta2 = 0.75, s1 = 0.25, s2 = 0.5, s3 = 4.0;
+  double f, gr, Dw;
+  vg(W, f, gr, Dw);
+  double f0z, g0n;
+  if (gsum(W != 0.0 ? 1.0 : 0.0) == 0.0) {
+    f0z = f;
+    g0n = sqrt(gsum(gr * gr));
+  } else {
+    double f0, g0, D0;
+    vg(0.0, f0, g0, D0);
+    f0z = f0;
+    g0n = sqrt(gsum(g0 * g0));
+  }
+  const double loss_tol = f0z * tol, grad_tol = g0n * tol;
+  double delta = sqrt(gsum(gr * gr));
+  int it = 0, fails = 0, reason = 0;
+  bool active = prob_on;
+  if (delta == 0.0) { reason = 4; active = false; }
+  const int guard_max = max_iter * (max_fail + 1) + 5;
+  for (int guard = 0; guard < guard_max; ++guard) {
+    if (!__any(active)) break;
+    // ---- truncated CG at W (Hessian weights Dw of the current iterate)
+    double step = 0.0, r = -gr, d = r;
+    double rtr = gsum(r * r);
+    const double cg_tol = 0.1 * sqrt(gsum(gr * gr));
+    bool cg_on = active;
+    for (int k = 0; k < max_cg; ++k) {
+      cg_on = cg_on && sqrt(rtr > 0.0 ? rtr : 0.0) > cg_tol;
+      if (!__any(cg_on)) break;
+      const double Hd = mvt(Dw * mv(d));
+      const double Hl = Hd + l2 * d;
+      const double dhd = gsum(d * Hl), std_ = gsum(step * d), sts = gsum(step * step), dtd = gsum(d * d);
+      const double alpha = rtr / (dhd == 0.0 ? 1.0 : dhd);
+      const double tr = step + alpha * d;
+      const double tn = gsum(tr * tr);
+      const bool hit = sqrt(tn > 0.0 ? tn : 0.0) > delta;
+      double a = alpha;
+      if (hit) {
+        const double dsq = delta * delta;
+        const double q = std_ * std_ + dtd * (dsq - sts);
+        const double rad = sqrt(q > 0.0 ? q : 0.0);
+        const double den1 = std_ + rad;
+        a = std_ >= 0.0 ? (dsq - sts) / (den1 > 1e-300 ? den1 : 1e-300) : (rad - std_) / (dtd > 1e-300 ? dtd : 1e-300);
+      }
+      const double step_n = step + a * d;
+      const double r_n = r - a * Hl;
+      const double rn = gsum(r_n * r_n);
+      const double beta = rn / (rtr == 0.0 ? 1.0 : rtr);
+      if (cg_on) {
+        step = step_n;
+        r = r_n;
+        if (!hit) { d = r_n + beta * d; rtr = rn; }
+      }
+      cg_on = cg_on && !hit;
+    }
+    // ---- trial point, trust-region update, acceptance
+    const double Wn = W + step;
+    const double gs = gsum(gr * step);
+    const double pred = -0.5 * (gs - gsum(step * r));
+    double fn, gn, Dn;
+    vg(Wn, fn, gn, Dn);
+    const double actual = f - fn;
+    const double snorm = sqrt(gsum(step * step));
+    if (active && it == 0) delta = fmin(delta, snorm);
+    const double den = fn - f - gs;
+    const double al = den <= 0.0 ? s3 : fmax(s1, -0.5 * gs / (den == 0.0 ? 1.0 : den));
+    double nd;
+    if (actual < eta0 * pred) nd = fmin(fmax(al, s1) * snorm, s2 * delta);
+    else if (actual < eta1 * pred) nd = fmax(s1 * delta, fmin(al * snorm, s2 * delta));
+    else if (actual < eta2 * pred) nd = fmax(s1 * delta, fmin(al * snorm, s3 * delta));
+    else nd = fmax(delta, fmin(al * snorm, s3 * delta));
+    if (active) delta = nd;
+    const bool accept = active && actual > eta0 * pred;
+    const double f_prev = f;
+    if (accept) { W = Wn; f = fn; gr = gn; Dw = Dn; ++it; fails = 0; }
+    else if (active) ++fails;
+    const bool not_impr = active && !accept && fails >= max_fail;
+    const double gnorm = sqrt(gsum(gr * gr));
+    int rc = 0;
+    if (accept && gnorm <= grad_tol) rc = 4;
+    if (accept && fabs(f - f_prev) <= loss_tol) rc = 3;
+    if (not_impr) rc = 2;
+    if ((accept || not_impr) && it >= max_iter) rc = 1;
+    if (active && rc > 0) { reason = rc; active = false; }
+  }
+  if (on) Beta[o] = W;
+  if (prob_on && i == 0) { Fout[b] = f; Iters[b] = it; Reason[b] = reason; }
+}
+
 extern "C" {
 
 int pml_version() { return 1; }
@@ -1682,6 +1831,24 @@ int pml_bhv(int B, int n, const double* A, const double* dw, const double* v, do
   const size_t lds = nw * wave_lds;
   hipLaunchKernelGGL(bhv_kernel, dim3((unsigned)grid), dim3(nw * 64), lds, (hipStream_t)stream, B, n, A, dw, v, l2,
                      out);
+  LAUNCH_CHECK();
+  return 0;
+}
+
+int pml_rs_tron(int B, int n, const double* L, const double* y, const double* off, const double* wt, double* beta,
+                double* f, int* iters, int* reason, int loss, double l2, double tol, int max_iter, int max_fail,
+                int max_cg, void* stream) {
+  if (B <= 0) return 0;
+  if (n < 1 || n > 64 || loss < 0 || loss > 2) return -22;
+  int G = 1;
+  while (G < n) G <<= 1;
+  const int per = 64 / G;
+  const long long waves = (B + per - 1) / per;
+  const size_t wave_lds = (size_t)per * n * (n + 1) * sizeof(double);
+  const int nw = (int)std::max<size_t>(1, std::min<size_t>(4, 65536 / wave_lds));
+  const long long grid = (waves + nw - 1) / nw;
+  hipLaunchKernelGGL(rs_tron_kernel, dim3((unsigned)grid), dim3(nw * 64), nw * wave_lds, (hipStream_t)stream, B, n, G,
+                     L, y, off, wt, beta, f, iters, reason, loss, l2, tol, max_iter, max_fail, max_cg);
   LAUNCH_CHECK();
   return 0;
 }

@@ -100,9 +100,11 @@ def glm_lib() -> Optional[ctypes.CDLL]:
         lib.pml_seg_cg_step.argtypes = [c_void_p, c_int] + [c_void_p] * 7 + [c_double, c_void_p]
         lib.pml_bgemv.argtypes = [c_int, c_int, c_void_p, c_void_p, c_void_p, c_int, c_void_p]
         lib.pml_bhv.argtypes = [c_int, c_int, c_void_p, c_void_p, c_void_p, c_double, c_void_p, c_void_p]
+        lib.pml_rs_tron.argtypes = [c_int, c_int] + [c_void_p] * 8 + [c_int, c_double, c_double, c_int, c_int, c_int,
+                                                                      c_void_p]
         for f in ("pml_seg_fwd", "pml_seg_t", "pml_reduce_stats", "pml_build_blocks", "pml_tl_fwd", "pml_tl_t",
                   "pml_tl_maxbits", "pml_segdot", "pml_tl_fwd_multi", "pml_tl_t_multi", "pml_seg_cg_step",
-                  "pml_seg_expand", "pml_bgemv", "pml_bhv"):
+                  "pml_seg_expand", "pml_bgemv", "pml_bhv", "pml_rs_tron"):
             getattr(lib, f).restype = c_int
         lib.pml_set_config.argtypes = [c_int, c_int, c_int, c_int]
         lib._pml_typed = True
@@ -191,6 +193,26 @@ def batched_hv(A: torch.Tensor, dw: torch.Tensor, v: torch.Tensor, l2: float = 0
     check(lib.pml_bhv(B, n, A.data_ptr(), dw.data_ptr(), v.data_ptr(), float(l2), out.data_ptr(),
                       stream_handle(A.device)), "bhv")
     return out
+
+
+def rs_tron(L: torch.Tensor, y: torch.Tensor, o: torch.Tensor, w: torch.Tensor, beta0: torch.Tensor, loss_id: int,
+            l2: float, tol: float, max_iter: int, max_fail: int = 5, max_cg: int = 20):
+    """Fused per-problem TRON over a batch of small dense GLMs (``rs_tron_kernel``): returns
+    (beta, f, iters, reason). Device only; n <= 64; losses logistic / Poisson / squared."""
+    lib = require_glm_lib()
+    B, n, _ = L.shape
+    ts = [t.contiguous() for t in (L, y, o, w)]
+    for t in ts:
+        assert t.dtype == torch.float64 and t.is_cuda
+    assert y.shape == (B, n) and o.shape == (B, n) and w.shape == (B, n) and beta0.shape == (B, n)
+    beta = beta0.to(torch.float64).contiguous().clone()
+    f = torch.empty(B, dtype=torch.float64, device=L.device)
+    iters = torch.empty(B, dtype=torch.int32, device=L.device)
+    reason = torch.empty(B, dtype=torch.int32, device=L.device)
+    check(lib.pml_rs_tron(B, n, ts[0].data_ptr(), ts[1].data_ptr(), ts[2].data_ptr(), ts[3].data_ptr(),
+                          beta.data_ptr(), f.data_ptr(), iters.data_ptr(), reason.data_ptr(), int(loss_id), float(l2),
+                          float(tol), int(max_iter), int(max_fail), int(max_cg), stream_handle(L.device)), "rs_tron")
+    return beta, f, iters.to(torch.long), reason.to(torch.long)
 
 
 def seg_expand(s: torch.Tensor, ptr: torch.Tensor, n: int) -> torch.Tensor:

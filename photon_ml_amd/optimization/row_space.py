@@ -27,6 +27,7 @@ D_total = 1.25e9-coefficient vectors, and the model returns to the primal space 
 """
 from __future__ import annotations
 
+import os
 from typing import Optional
 
 import torch
@@ -137,7 +138,16 @@ class RowSpaceBatch:
             beta0 = self.beta_from_primal(W0)
         else:
             beta0 = torch.zeros(self.B, self.n, dtype=torch.float64, device=self.L.device)
-        data = BatchedGLMData(self.L, self.y, self._slots(self.seg.o), self.w)
+        o = self._slots(self.seg.o)
+        if (optimizer == "TRON" and self.L.is_cuda and self.n <= 64 and getattr(loss, "loss_id", -1) in (0, 1, 2)
+                and os.environ.get("PML_RS_FUSED_TRON", "1") != "0"):
+            # whole per-entity TRON in one kernel, L resident in LDS (ops/csrc/glm_kernels.hip rs_tron_kernel)
+            from ..ops.native import rs_tron
+            beta, f, iters, reason = rs_tron(self.L, self.y, o, self.w, beta0, loss.loss_id, l2, tol, max_iter)
+            res = BatchedResult(beta, f, iters, reason)
+            self.beta = res.W
+            return res
+        data = BatchedGLMData(self.L, self.y, o, self.w)
         if optimizer == "TRON":
             res = batched_tron(data, loss, l2, beta0, tol, max_iter)
         else:

@@ -294,3 +294,35 @@ def test_batched_small_gemv_and_hv_match_torch(n):
     torch.testing.assert_close(batched_gemv(A, x, trans=True), reft, rtol=1e-12, atol=1e-12)
     hv = torch.bmm(A.transpose(1, 2), (dw * ref).unsqueeze(-1)).squeeze(-1) + 0.7 * x
     torch.testing.assert_close(batched_hv(A, dw, x, 0.7), hv, rtol=1e-12, atol=1e-11)
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("loss_name,n", [("LOGISTIC", 20), ("POISSON", 7), ("SQUARED", 33), ("LOGISTIC", 64),
+                                         ("LOGISTIC", 1)])
+@pytest.mark.parametrize("warm", [False, True])
+def test_fused_row_space_tron_matches_batched_tron(loss_name, n, warm):
+    """rs_tron_kernel (whole per-problem TRON in one kernel) vs the vectorised batched TRON of
+    optimization/batched.py on the same dense problems (fp64): same solutions, objective and iteration counts."""
+    from photon_ml_amd.function import losses
+    from photon_ml_amd.ops.native import rs_tron
+    from photon_ml_amd.optimization.batched import BatchedGLMData, batched_tron
+    loss = {"LOGISTIC": losses.LOGISTIC, "POISSON": losses.POISSON, "SQUARED": losses.SQUARED}[loss_name]
+    g = torch.Generator(device="cuda").manual_seed(7 * n + int(warm))
+    B = 777
+    L = torch.tril(torch.randn(B, n, n, dtype=torch.float64, device="cuda", generator=g)) * 0.5
+    L.diagonal(dim1=1, dim2=2).copy_(torch.rand(B, n, dtype=torch.float64, device="cuda", generator=g) + 0.5)
+    nvalid = torch.randint(1, n + 1, (B,), device="cuda", generator=g)
+    valid = torch.arange(n, device="cuda").unsqueeze(0) < nvalid.unsqueeze(1)
+    w = torch.where(valid, torch.rand(B, n, dtype=torch.float64, device="cuda", generator=g) + 0.5, 0.0)
+    z = torch.randn(B, n, dtype=torch.float64, device="cuda", generator=g)
+    y = (z > 0).double() if loss_name == "LOGISTIC" else (z.abs().round() if loss_name == "POISSON" else z)
+    o = 0.1 * torch.randn(B, n, dtype=torch.float64, device="cuda", generator=g)
+    b0 = 0.3 * torch.randn(B, n, dtype=torch.float64, device="cuda", generator=g) if warm else torch.zeros(
+        B, n, dtype=torch.float64, device="cuda")
+    ref = batched_tron(BatchedGLMData(L, y, o, w), loss, 0.7, b0, 1e-9, 30)
+    beta, f, it, reason = rs_tron(L, y, o, w, b0, loss.loss_id, 0.7, 1e-9, 30)
+    torch.testing.assert_close(beta, ref.W, rtol=1e-6, atol=1e-7)
+    torch.testing.assert_close(f, ref.f, rtol=1e-10, atol=1e-10)
+    # reduction order differs (butterfly vs torch sum): at tol 1e-9 a convergence test can flip by one iteration
+    assert float((it != ref.iters).double().mean()) < 0.05
+    assert float((reason != ref.reason).double().mean()) < 0.05
