@@ -1094,7 +1094,7 @@ template <typename VT, typename XT, typename RT, typename AT, int MAXR>
 static void tl_fwd_launch(const TLFwdDesc* c, const void* x, FwdArgs<XT, RT> a, double* stats, hipStream_t st) {
 #define TLF(NW, P) hipLaunchKernelGGL((tl_fwd_kernel<VT, XT, RT, AT, MAXR, 2, NW, P>), dim3(c->nblk), dim3(NW * 64), 0, \
                                     st, c->blk, c->rbits, c->pack, (const VT*)c->val, (const XT*)x, a, stats)
-  if (c->il) { if (g_tl_waves == 2) TLF(2, 3); else TLF(4, 3); }
+  if (c->il) { if (g_tl_waves <= 2) TLF(2, 3); else TLF(4, 3); }
   else if (g_tl_waves == 2) { if (g_tl_pipe == 1) TLF(2, 1); else TLF(2, 0); }
   else { if (g_tl_pipe == 1) TLF(4, 1); else TLF(4, 0); }
 #undef TLF
@@ -1105,7 +1105,7 @@ static void tl_fwd_multi_launch(const TLFwdMultiDesc* c, const void* x, FwdArgs<
                                 hipStream_t st) {
 #define TLM(NW, P) hipLaunchKernelGGL((tl_fwd_multi_kernel<VT, XT, RT, AT, MAXR, 2, NW, P>), dim3(c->nblk), \
                                       dim3(NW * 64), 0, st, c->blk, c->rbits, c->packs, c->vals, (const XT*)x, a, stats)
-  if (c->il) { if (g_tl_waves == 2) TLM(2, 3); else TLM(4, 3); }
+  if (c->il) { if (g_tl_waves == 1) TLM(1, 3); else if (g_tl_waves == 2) TLM(2, 3); else TLM(4, 3); }
   else if (g_tl_waves == 2) { if (g_tl_pipe == 2) TLM(2, 2); else TLM(2, 0); }
   else { if (g_tl_pipe == 2) TLM(4, 2); else TLM(4, 0); }
 #undef TLM
@@ -1742,7 +1742,7 @@ int pml_reduce_stats(const double* stats, int n, double* out, int accumulate, do
 // ---- tiled layout entry points ------------------------------------------------------------------------------
 int pml_tl_maxbits() { return TL_MAXBITS; }
 void pml_tl_config(int acc64, int waves, int waves_t, int pipe) {
-  g_tl_acc64 = acc64; g_tl_waves = waves == 2 ? 2 : 4; g_tl_waves_t = waves_t == 2 ? 2 : 4; g_tl_pipe = pipe & 3; g_tl_pipe_t = (pipe >> 2) & 3;
+  g_tl_acc64 = acc64; g_tl_waves = (waves == 1 || waves == 2) ? waves : 4; g_tl_waves_t = waves_t == 2 ? 2 : 4; g_tl_pipe = pipe & 3; g_tl_pipe_t = (pipe >> 2) & 3;
 }
 
 int pml_tl_fwd(int prec, const TLFwdDesc* c, const void* x, int mode, int loss, double shift, const void* y,
