@@ -107,6 +107,8 @@ def main():
         f"layout={data.layout}")
     sharded = args.optimizer_state == "feature-sharded"
     gdata = DistributedGLMData(data) if world > 1 and not sharded else data
+    if world > 1 and not sharded:
+        log(f"gradient all-reduce: {'overlapped, %d buckets' % gdata.buckets if gdata.overlap else 'one-shot'}")
 
     if args.config == "owlqn":
         obj = GLMObjective(LOGISTIC, l2_weight=0.0)

@@ -100,7 +100,14 @@ def generate_device_shard(n_rows: int, n_features: int, nnz_per_row: int, device
         raw.append((idx, val.to(vdt).reshape(-1)))
         if (m + 1) * k >= 2 ** 31:
             raise ValueError("chunk too large for int32 offsets: lower chunk_rows")
-    # relabel features hottest-first (the forward kernel keeps the head of w in an LDS hot table)
+    # relabel features hottest-first (the forward kernel keeps the head of w in an LDS hot table); under a process
+    # group the counts are summed first so every rank shares ONE feature order (gradient all-reduce buckets then
+    # cover the same columns on every rank, see DistributedGLMData)
+    import torch.distributed as dist
+    if dist.is_available() and dist.is_initialized() and dist.get_world_size() > 1:
+        cc = counts if dist.get_backend() == "nccl" else counts.cpu()
+        dist.all_reduce(cc)
+        counts = cc.to(dev)
     old_of_new = torch.argsort(counts, descending=True, stable=True)
     new_of_old = torch.empty_like(old_of_new)
     new_of_old[old_of_new] = torch.arange(n_features, device=dev)

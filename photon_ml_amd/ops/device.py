@@ -420,6 +420,84 @@ class DeviceGLMData(GLMComputable):
         for c in range(len(self.csc)):
             self._t(c, x, G, square)
 
+    # ---- gradient buckets: the transpose split into column-tile ranges so each range's all-reduce can start as
+    # soon as that range is final (overlap of the C1 collective with the rest of the transpose pass)
+    def grad_buckets(self, nb: int):
+        """``nb`` shard-wide transpose launches over contiguous column-tile ranges of ~equal entry counts:
+        list of (TLTMulti, col_lo, col_hi) in PERMUTED column order; None if the layout does not allow it."""
+        cache = getattr(self, "_gbuckets", None)
+        if cache is not None and cache[0] == nb:
+            return cache[1]
+        if getattr(self, "_multi_t", "unset") == "unset":
+            self._build_multi_t()
+        if self._multi_t is None or nb < 2:
+            self._gbuckets = (nb, None)
+            return None
+        from .tiled import TLTMulti
+        C = 1 << self._multi_t.cbits
+        ntiles = (self.dim + C - 1) // C
+        work = np.zeros(ntiles, np.int64)
+        for ch in self.csc:
+            it = ch.items[: ch.nitems].cpu().numpy().astype(np.int64)
+            np.add.at(work, it[:, 0], it[:, 2] - it[:, 1])
+        cum = np.cumsum(work)
+        cuts = [0] + [int(np.searchsorted(cum, cum[-1] * k / nb, side="right")) for k in range(1, nb)] + [ntiles]
+        cuts = sorted(set(min(max(c, 0), ntiles) for c in cuts))
+        out = []
+        for t0, t1 in zip(cuts[:-1], cuts[1:]):
+            if t1 > t0:
+                mt = TLTMulti(self.csc, self.row_starts, self.dim, tile_range=(t0, t1))
+                out.append((mt, t0 * C, min(t1 * C, self.dim)))
+                if mt.parts_needed > self.parts.numel():
+                    self.parts = torch.zeros(mt.parts_needed, dtype=torch.float64, device=self.device)
+        self._gbuckets = (nb, out)
+        return out
+
+    def _packed_bucketed(self, x, G, start_reduce, nb: int, square: int = 0):
+        for mt, c0, c1 in self.grad_buckets(nb):
+            check(self.lib.pml_tl_t_multi(self.prec, ctypes.byref(mt.desc), x.data_ptr(), square, G.data_ptr(),
+                                          self.parts.data_ptr(), stream_handle(self.device)), "tl_t_multi")
+            start_reduce(G[c0:c1])
+
+    def value_grad_packed_overlap(self, loss, w_eff, margin_shift, start_reduce, nb: int = 4) -> torch.Tensor:
+        """As :meth:`value_grad_packed` but the gradient is produced in ``nb`` column buckets and
+        ``start_reduce(slice)`` is called on each final slice (and on [F, S]) while the rest of the pass is still
+        running. The result stays in the PERMUTED (hot-first) feature order: the caller reduces across ranks —
+        which must share the permutation — then applies :meth:`_unperm`. Bitwise equal to the one-launch pass."""
+        with trace_range("K1 value+grad pass (bucketed)"):
+            out = torch.zeros(self.dim + 2, dtype=torch.float64, device=self.device)
+            x = self._vec(w_eff)
+            dzz = self.dzz if (self.track_hessian and loss.twice_differentiable) else None
+            self.fwd_all(x, FWD_VALUE_GRAD, loss.loss_id, margin_shift, self.coef, dzz)
+            out[self.dim:] = self._reduce_stats()
+            start_reduce(out[self.dim:])
+            self._packed_bucketed(self.coef, out[: self.dim], start_reduce, nb)
+            if dzz is not None:
+                self._dzz_key = w_eff.detach().clone()
+                self._dzz_shift = float(margin_shift)
+            self.n_passes += 1
+            return out
+
+    def hv_packed_overlap(self, loss, w_eff, margin_shift, v_eff, v_shift, start_reduce, nb: int = 4):
+        with trace_range("K2 Hessian-vector pass (bucketed)"):
+            self._ensure_dzz(loss, w_eff, margin_shift)
+            out = torch.zeros(self.dim + 2, dtype=torch.float64, device=self.device)
+            x = self._vec(v_eff)
+            self.fwd_all(x, FWD_HV, loss.loss_id, v_shift, self.coef, self.dzz)
+            out[self.dim:] = self._reduce_stats()
+            start_reduce(out[self.dim:])
+            self._packed_bucketed(self.coef, out[: self.dim], start_reduce, nb)
+            self.n_passes += 1
+            return out
+
+    def perm_fingerprint(self) -> float:
+        """Order-sensitive fingerprint of the feature relabelling (0 for none): ranks must agree before they
+        reduce gradients in the permuted order."""
+        if self.old_of_new is None:
+            return 0.0
+        k = torch.arange(self.dim, device=self.device, dtype=torch.float64)
+        return float((self.old_of_new.to(torch.float64) * torch.sin(k * 0.618 + 0.1)).sum()) + 1.0
+
     def _reduce_stats(self) -> torch.Tensor:
         out = self.out2
         st = stream_handle(self.device)

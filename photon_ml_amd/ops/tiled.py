@@ -26,7 +26,7 @@ of more than 2^27 rows) fall back to the segmented-stream layout (:mod:`photon_m
 from __future__ import annotations
 
 import os
-from typing import Optional, Sequence
+from typing import Optional, Sequence, Tuple
 
 import numpy as np
 import torch
@@ -284,7 +284,10 @@ class TLTMulti:
     per-chunk column windows) and one ``cbits`` for all chunks.
     """
 
-    def __init__(self, chunks: Sequence["TLTChunk"], row_starts: Sequence[int], dim: int):
+    def __init__(self, chunks: Sequence["TLTChunk"], row_starts: Sequence[int], dim: int,
+                 tile_range: Optional[Tuple[int, int]] = None):
+        """``tile_range`` = [t0, t1): only the items of those column tiles (a gradient BUCKET: columns
+        [t0 * C, t1 * C) are final after this launch + its combine, so their all-reduce can start)."""
         from .native import TLTMultiDesc
         dev = chunks[0].pack.device
         self.cbits = chunks[0].cbits
@@ -297,6 +300,8 @@ class TLTMulti:
             its.append(np.column_stack([np.full(len(it), c), it[:, 0], it[:, 1], it[:, 2],
                                         np.full(len(it), row_starts[c])]))
         it = np.concatenate(its) if its else np.zeros((0, 5), np.int64)
+        if tile_range is not None:
+            it = it[(it[:, 1] >= tile_range[0]) & (it[:, 1] < tile_range[1])]
         n = len(it)
         tile = it[:, 1]
         order = np.lexsort((np.arange(n), tile))          # grouped by tile, (chunk, item) order inside

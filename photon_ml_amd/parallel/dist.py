@@ -99,6 +99,15 @@ class DistributedGLMData:
         all_reduce_(n, group=group)
         self.n_rows = int(n.item())
         self.local_rows = local.n_rows
+        # Overlapped C1: gradient buckets reduced while the transpose pass still runs (needs the bucketed device
+        # path and ONE feature order on every rank — the reduction happens in the device's permuted order).
+        self.buckets = int(os.environ.get("PML_GRAD_BUCKETS", "4"))
+        self.overlap = False
+        if is_dist() and self.buckets > 1 and hasattr(local, "value_grad_packed_overlap"):
+            fp = local.perm_fingerprint()
+            lo = all_reduce_scalar(fp, "min", group=group)
+            hi = all_reduce_scalar(fp, "max", group=group)
+            self.overlap = lo == hi and local.grad_buckets(self.buckets) is not None
 
     def _comm_device(self):
         if is_dist() and dist.get_backend(self.group) == "nccl":
@@ -114,8 +123,29 @@ class DistributedGLMData:
         if hasattr(self.local, "track_hessian"):
             self.local.track_hessian = v
 
+    def _packed_overlap(self, fn, *args) -> torch.Tensor:
+        """Bucketed pass: each final gradient slice (and [F, S]) is all-reduced asynchronously while the
+        transpose kernels of the next buckets run; RCCL's stream waits on the compute stream at each call, so
+        ordering is by construction. Same bits as the one-shot path (tiles are independent)."""
+        works = []
+
+        def start(t):
+            works.append(dist.all_reduce(t, group=self.group, async_op=True))
+
+        with trace_range(f"C1 overlapped all-reduce {fn} [{self.dim + 2} fp64, {self.buckets} buckets]"):
+            buf = getattr(self.local, fn + "_packed_overlap")(*args, start, nb=self.buckets)
+            for w in works:
+                w.wait()
+        if self.local.old_of_new is not None:
+            buf[: self.dim] = self.local._unperm(buf[: self.dim].clone())
+        if self.nan_guard:
+            check_finite_(buf, fn)
+        return buf
+
     def _packed(self, fn, *args) -> torch.Tensor:
         local = self.local
+        if self.overlap and fn in ("value_grad", "hv"):
+            return self._packed_overlap(fn, *args)
         if hasattr(local, fn + "_packed"):
             buf = getattr(local, fn + "_packed")(*args)
         else:

@@ -326,3 +326,31 @@ def test_fused_row_space_tron_matches_batched_tron(loss_name, n, warm):
     # reduction order differs (butterfly vs torch sum): at tol 1e-9 a convergence test can flip by one iteration
     assert float((it != ref.iters).double().mean()) < 0.05
     assert float((reason != ref.reason).double().mean()) < 0.05
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("nb", [2, 3, 7])
+def test_bucketed_gradient_pass_is_bitwise_equal(nb):
+    """Gradient produced in column-tile buckets (for the overlapped all-reduce) == the one-launch pass, bit for
+    bit, for value+gradient and Hessian-vector passes; every slice handed to the reducer is final when handed."""
+    from photon_ml_amd.data.synthetic import generate_device_shard
+    from photon_ml_amd.function.losses import LOGISTIC
+    data, w = generate_device_shard(300_000, 50_000, 30, "cuda", "bf16", chunk_rows=1 << 17, layout="tiled")
+    w = (w * 0.05).to(torch.float64)
+    ref = data.value_grad_packed(LOGISTIC, w, 0.1)
+    seen = []
+    out = data.value_grad_packed_overlap(LOGISTIC, w, 0.1, lambda t: seen.append(t.clone()), nb=nb)
+    g = out.clone()
+    if data.old_of_new is not None:
+        g[: data.dim] = data._unperm(out[: data.dim].clone())
+    assert torch.equal(g, ref)
+    assert len(seen) == len(data.grad_buckets(nb)) + 1 and sum(t.numel() for t in seen) == data.dim + 2
+    assert torch.equal(torch.cat(seen[1:]), out[: data.dim]) and torch.equal(seen[0], out[data.dim:])
+    data.track_hessian = True
+    data.value_grad_packed(LOGISTIC, w, 0.1)
+    v = torch.randn(data.dim, dtype=torch.float64, device="cuda")
+    href = data.hv_packed(LOGISTIC, w, 0.1, v, 0.0)
+    hb = data.hv_packed_overlap(LOGISTIC, w, 0.1, v, 0.0, lambda t: None, nb=nb)
+    if data.old_of_new is not None:
+        hb[: data.dim] = data._unperm(hb[: data.dim].clone())
+    assert torch.equal(hb, href)
