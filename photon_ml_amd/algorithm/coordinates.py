@@ -277,8 +277,11 @@ class RandomEffectCoordinate(Coordinate):
                                 reuse_beta=self._W.get("seg") is not None)
                 _sync(W0)
             frozen = rs.mask
-            W0 = torch.where(seg.bexp(frozen), torch.zeros_like(W0), W0)
-        if frozen is None or not bool(frozen.all()):
+            n_e = seg.row_ptr[1:] - seg.row_ptr[:-1]
+            all_rs = bool((frozen | (n_e == 0)).all())   # nothing left for the primal path
+            if not all_rs:
+                W0 = torch.where(seg.bexp(frozen), torch.zeros_like(W0), W0)
+        if frozen is None or not all_rs:
             with Timed(f"RE {self.coordinate_id}: primal block-diagonal solve", log, logging.DEBUG):
                 if oc.optimizer_type == OptimizerType.TRON:
                     res = batched_tron(seg, self.loss, l2, W0, oc.tolerance, oc.maximum_iterations, frozen=frozen)
@@ -287,13 +290,17 @@ class RandomEffectCoordinate(Coordinate):
                                         frozen=frozen)
                 W_all, iters, reasons = res.W, res.iters, res.reason
         else:
-            W_all = torch.zeros_like(W0)
+            W_all = None
             iters = torch.zeros(seg.B, dtype=torch.long, device=W0.device)
             reasons = torch.zeros(seg.B, dtype=torch.long, device=W0.device)
+        self._rs_scores = None
         if frozen is not None:
             with Timed(f"RE {self.coordinate_id}: row-space -> primal", log, logging.DEBUG):
-                W_all = W_all + rs.to_primal(rres.W)
+                Wp = rs.to_primal(rres.W)
+                W_all = Wp if W_all is None else W_all + Wp
                 _sync(W_all)
+            if all_rs:  # active-row scores X w = L beta without a pass over the sparse data
+                self._rs_scores = rs.margins(rres.W)
             iters = iters.index_copy(0, rs.ents, rres.iters)
             reasons = reasons.index_copy(0, rs.ents, rres.reason)
         res = BatchedResult(W_all, None, iters, reasons)
@@ -304,10 +311,11 @@ class RandomEffectCoordinate(Coordinate):
         var = None
         if self.compute_variance and self.loss.twice_differentiable:
             var = 1.0 / (seg.hdiag(self.loss, res.W, l2) + EPSILON)
-        keys = ds.projection_keys_t  # entity * dim + feature, sorted, aligned with W (device)
-        nz = torch.nonzero(W != 0).squeeze(1)  # device compaction; the model stays resident (host copy lazily)
+        # the model keeps the projected keys (entity * dim + feature, sorted, aligned with W) without compaction:
+        # W is dense in the projected space, and zeros are harmless (dropped at save, <1e-4 as in the reference);
+        # compacting 1.25e9 coefficients per update was ~40 GB of traffic at config 5
         out = RandomEffectModel(self.data_config.random_effect_type, self.data_config.feature_shard_id, self.task,
-                                ds.entity_ids, ds.dim, keys[nz], W[nz], None if var is None else var[nz])
+                                ds.entity_ids, ds.dim, ds.projection_keys_t, W, var)
         self._last = (out, res.W)
         return out
 
@@ -369,7 +377,9 @@ class RandomEffectCoordinate(Coordinate):
         last = getattr(self, "_last", None)
         if ds.layout == "segmented" and last is not None and last[0] is model:
             # the model just solved: its active-row scores are one forward pass over the block-diagonal data
-            z = ds.seg.glm.matvec(last[1])
+            # (or, when every entity was solved in its row space, L beta)
+            rz = getattr(self, "_rs_scores", None)
+            z = rz if rz is not None else ds.seg.glm.matvec(last[1])
             out = torch.zeros(self.data.n_rows, dtype=torch.float64, device=z.device)
             out[ds.seg_rows] = z
             if len(ds.passive_rows):

@@ -129,6 +129,12 @@ class RowSpaceBatch:
         r[self.rows[self.valid]] = alpha[self.valid]
         return self.seg.glm.rmatvec(r)
 
+    def margins(self, beta: torch.Tensor) -> torch.Tensor:
+        """Per-row X w (no offsets) of the handled entities = L beta, in the segmented row order."""
+        z = torch.zeros(self.seg.y.numel(), dtype=torch.float64, device=beta.device)
+        z[self.rows[self.valid]] = _bmv(self.L, beta)[self.valid]
+        return z
+
     def solve(self, loss, l2: float, optimizer: str, W0: Optional[torch.Tensor], tol: float, max_iter: int,
               reuse_beta: bool = True) -> BatchedResult:
         """Solve the handled entities; returns the batched result over the ``B`` row-space problems."""
