@@ -63,6 +63,20 @@ class GLMObjective:
             grad = grad + self.l2_weight * w
         return f, grad
 
+    def margin_line_search(self, data, x0: torch.Tensor, d: torch.Tensor,
+                           t0: float = 1.0) -> Optional["MarginLineSearch"]:
+        """Line search along x0 + t d in MARGIN space (GLM margins are affine in t), or None when the data
+        backend cannot cache margins. See :class:`MarginLineSearch`."""
+        if not hasattr(data, "ls_begin"):
+            return None
+        norm = self.normalization
+        w0_eff, shift0 = norm.effective(x0)
+        d_eff = d * norm.factors.to(d) if norm.factors is not None else d
+        d_shift = -float(torch.dot(d_eff, norm.shifts.to(d_eff))) if norm.shifts is not None else 0.0
+        if not data.ls_begin(w0_eff, shift0, d_eff, d_shift, t0, self.loss):
+            return None
+        return MarginLineSearch(self, data, x0, d)
+
     def value(self, data, w: torch.Tensor) -> float:
         return self.calculate(data, w)[0]
 
@@ -91,3 +105,44 @@ class GLMObjective:
         if self.l2_weight > 0:
             d = d + self.l2_weight
         return d
+
+
+class MarginLineSearch:
+    """phi(t) = F(x0 + t d) for a GLM objective, evaluated from cached margins.
+
+    z(t) = z0 + t zd with z0 the margins at x0 (kept by the last full evaluation) and zd = X d_eff + d_shift (one
+    forward pass), so each trial costs one elementwise pass over the rows (``ls_eval_kernel``) instead of a
+    forward + transpose pass over every non-zero; phi'(t) = sum w l'(z(t)) zd + l2 x(t).d (the normalization
+    shift terms cancel: d_eff . G - S d_eff . s = sum w l' (zd - d_shift) + S d_shift). Only the ACCEPTED step
+    pays the transpose pass for the full gradient. The reference evaluates the full objective (broadcast +
+    treeAggregate) at every trial point (Breeze StrongWolfeLineSearch through ``DiffFunction.calculate``).
+    """
+
+    def __init__(self, obj: GLMObjective, data, x0: torch.Tensor, d: torch.Tensor):
+        from ..optimization.vector_space import vdot
+        self.obj, self.data, self.x0, self.d = obj, data, x0, d
+        l2 = obj.l2_weight
+        self.l2 = l2
+        if l2 > 0:
+            self.a, self.b, self.c = vdot(x0, x0), vdot(x0, d), vdot(d, d)
+
+    def eval(self, t: float):
+        f, dd = self.data.ls_eval(self.obj.loss, t)
+        if self.l2 > 0:
+            f += 0.5 * self.l2 * (self.a + 2.0 * t * self.b + t * t * self.c)
+            dd += self.l2 * (self.b + t * self.c)
+        return f, dd
+
+    def finish(self, t: float):
+        """(x(t), f(x(t)), gradient at x(t)) — one transpose pass."""
+        x = self.x0 + t * self.d
+        norm = self.obj.normalization
+        w_eff, shift = norm.effective(x)
+        f, s, g = self.data.ls_finish_sums(self.obj.loss, t, w_eff, shift, norm.shifts is not None)
+        self.obj.n_value_grad += 1
+        grad = norm.finalize_vector(g, s)
+        if self.obj.l2_weight > 0:
+            f += self.obj.l2_value(x)
+            grad = grad + self.obj.l2_weight * x
+        return x, f, grad
+

@@ -37,7 +37,7 @@
   } while (0)
 
 enum LossId { LOSS_LOGISTIC = 0, LOSS_POISSON = 1, LOSS_SQUARED = 2, LOSS_HINGE = 3 };
-enum FwdMode { FWD_MARGIN = 0, FWD_VALUE_GRAD = 1, FWD_HV = 2, FWD_DZZ = 3 };
+enum FwdMode { FWD_MARGIN = 0, FWD_VALUE_GRAD = 1, FWD_HV = 2, FWD_DZZ = 3, FWD_LS = 4 };
 
 // ------------------------------------------------------------------------------------------------------------
 // value loads: 8 consecutive entries -> AT[8]
@@ -346,17 +346,21 @@ struct FwdArgs {
   int with_offset;    // MARGIN: add offset
   int abl;            // ablation bits (profiling only): 1 = gather from a 1 KB window, 2 = skip segmented reduce
   int hot_n;          // entries of x staged in LDS (features relabelled hottest-first), 0 = none
+  // FWD_LS (margin-space line search, direction pass): z_out = zd (in: previous direction, out: new one),
+  // z0 = cached margins (materialised here: z0 += tpend * zd_prev), first trial t0 -> (F, D) stats + coef
+  double* z0; double t0; double tpend;
 };
 
 // Per-row epilogue inputs, prefetched at block start (coalesced, latency hidden behind the stream phase)
 template <typename XT, typename RT>
-struct RowIn { RT y, off, wt; XT d; };
+struct RowIn { RT y, off, wt; XT d; double z0, zd; };
 
 template <typename XT, typename RT>
 __device__ __forceinline__ RowIn<XT, RT> fwd_prefetch(const FwdArgs<XT, RT>& a, int s) {
   RowIn<XT, RT> r;
-  r.y = RT(0); r.off = RT(0); r.wt = RT(0); r.d = XT(0);
+  r.y = RT(0); r.off = RT(0); r.wt = RT(0); r.d = XT(0); r.z0 = 0.0; r.zd = 0.0;
   if (a.mode == FWD_MARGIN) { if (a.with_offset) r.off = a.off[s]; }
+  else if (a.mode == FWD_LS) { r.y = a.y[s]; r.wt = a.wt[s]; r.z0 = a.z0[s]; r.zd = a.z_out[s]; }
   else if (a.mode == FWD_HV) { r.d = a.dzz[s]; }
   else { r.y = a.y[s]; r.off = a.off[s]; r.wt = a.wt[s]; }
   return r;
@@ -367,6 +371,19 @@ __device__ __forceinline__ void fwd_finish(const FwdArgs<XT, RT>& a, int s, doub
                                            double& F, double& S) {
   if (a.mode == FWD_MARGIN) {
     a.z_out[s] = sum + a.shift + static_cast<double>(r.off);
+    return;
+  }
+  if (a.mode == FWD_LS) {
+    const double zdn = sum + a.shift;                 // direction margin X d_eff + d_shift
+    const double z0v = r.z0 + a.tpend * r.zd;         // accepted step of the previous line search
+    a.z0[s] = z0v;
+    a.z_out[s] = zdn;
+    const double w = static_cast<double>(r.wt);
+    double l, dl, d2;
+    pointwise_loss(a.loss, z0v + a.t0 * zdn, static_cast<double>(r.y), l, dl, d2);
+    a.coef[s] = static_cast<XT>(w * dl);              // speculative: the transpose input if t0 is accepted
+    F += w * l;
+    S += w * dl * zdn;
     return;
   }
   if (a.mode == FWD_HV) {
@@ -382,6 +399,7 @@ __device__ __forceinline__ void fwd_finish(const FwdArgs<XT, RT>& a, int s, doub
   if (a.mode == FWD_VALUE_GRAD) {
     a.coef[s] = static_cast<XT>(w * dl);
     if (a.dzz) a.dzz[s] = static_cast<XT>(w * d2);
+    if (a.z_out) a.z_out[s] = z;  // margin cache for the margin-space line search (ls_eval_kernel)
     F += w * l;
     S += w * dl;
   } else {  // FWD_DZZ
@@ -1084,6 +1102,9 @@ struct TLTMultiDesc {
 // of waves per work-group (2 or 4: each wave owns an LDS accumulator row, so fewer waves = less LDS per WG = more
 // resident WGs per CU). fp64 data always accumulates in fp64.
 static int g_ablate = 0;      // profiling ablation bits (0 in production)
+// FWD_LS arguments (set by pml_set_ls_args right before a direction pass; host-side, single stream)
+static double* g_ls_z0 = nullptr;
+static double g_ls_t0 = 0.0, g_ls_tpend = 0.0;
 static int g_tl_acc64 = 1;   // measured on MI355X: ds_add_f64 accumulation is ~3x faster than ds_add_f32 here
 static int g_tl_waves = 4;     // forward
 static int g_tl_waves_t = 4;   // transpose
@@ -1619,9 +1640,47 @@ __global__ __launch_bounds__(NTHREADS) void rs_tron_kernel(
   if (prob_on && i == 0) { Fout[b] = f; Iters[b] = it; Reason[b] = reason; }
 }
 
+// ============================================================================================================
+// Margin-space line search (GLM L-BFGS): along x(t) = x0 + t d the margins are affine, z(t) = z0 + t zd with
+// z0 = X x0_eff + shift0 + offset (cached by the accepted evaluation) and zd = X d_eff + d_shift (one forward
+// pass per iteration). Each trial step then costs one elementwise pass over the rows instead of a full
+// forward + transpose pass over the non-zeros:
+//   F(t) = sum w l(z(t), y),   D(t) = sum w l'(z(t), y) zd     (phi'(t) = D(t) + l2 x(t).d)
+// final = 1 (the accepted t): coef = w l'(z), optional dzz = w l'' and S = sum w l' for the gradient's
+// transpose pass; z0 <- z0 + t zd is deferred into the next direction pass (FWD_LS epilogue). Per-block (F, D|S) partials, reduced in a fixed order (deterministic).
+// ============================================================================================================
+template <typename XT, typename RT>
+__global__ __launch_bounds__(NTHREADS) void ls_eval_kernel(int n, double t, int loss, double* __restrict__ z0,
+                                                            const double* __restrict__ zd, const RT* __restrict__ y,
+                                                            const RT* __restrict__ wt, int final_, XT* __restrict__ coef,
+                                                            XT* __restrict__ dzz, double* __restrict__ stats) {
+  __shared__ double sh[2 * NTHREADS / 64];
+  double F = 0.0, D = 0.0;
+  const long long stride = (long long)gridDim.x * NTHREADS;
+  for (long long i = (long long)blockIdx.x * NTHREADS + threadIdx.x; i < n; i += stride) {
+    const double zdi = zd[i];
+    const double z = z0[i] + t * zdi;
+    const double w = static_cast<double>(wt[i]);
+    double l, dl, d2;
+    pointwise_loss(loss, z, static_cast<double>(y[i]), l, dl, d2);
+    F += w * l;
+    if (final_) {
+      coef[i] = static_cast<XT>(w * dl);
+      if (dzz) dzz[i] = static_cast<XT>(w * d2);
+      D += w * dl;
+    } else {
+      D += w * dl * zdi;
+    }
+  }
+  block_sum2(F, D, sh);
+  if (threadIdx.x == 0) { stats[2 * blockIdx.x] = F; stats[2 * blockIdx.x + 1] = D; }
+}
+
 extern "C" {
 
 int pml_version() { return 1; }
+void pml_set_ls_args(double* z0, double t0, double tpend) { g_ls_z0 = z0; g_ls_t0 = t0; g_ls_tpend = tpend; }
+
 void pml_set_ablate(int a) {
   g_ablate = a;
 #ifdef PML_TL_ABLATE
@@ -1695,11 +1754,11 @@ int pml_seg_fwd(int prec, const SegChunkDesc* c, const void* x, int mode, int lo
   hipStream_t st = (hipStream_t)stream;
   if (prec == 2) {
     FwdArgs<double, double> a{mode, loss, shift, (const double*)y, (const double*)off, (const double*)wt,
-                              (double*)coef, (double*)dzz, z_out, with_offset, g_ablate, 0};
+                              (double*)coef, (double*)dzz, z_out, with_offset, g_ablate, 0, g_ls_z0, g_ls_t0, g_ls_tpend};
     return fwd_impl<double, double, double, double>(c, x, a, stats, long_stats, parts, st);
   }
   FwdArgs<float, float> a{mode, loss, shift, (const float*)y, (const float*)off, (const float*)wt,
-                          (float*)coef, (float*)dzz, z_out, with_offset, g_ablate, 0};
+                          (float*)coef, (float*)dzz, z_out, with_offset, g_ablate, 0, g_ls_z0, g_ls_t0, g_ls_tpend};
   if (prec == 1) return fwd_impl<float, float, float, float>(c, x, a, stats, long_stats, parts, st);
   return fwd_impl<uint16_t, float, float, float>(c, x, a, stats, long_stats, parts, st);
 }
@@ -1751,11 +1810,11 @@ int pml_tl_fwd(int prec, const TLFwdDesc* c, const void* x, int mode, int loss, 
   hipStream_t st = (hipStream_t)stream;
   if (prec == 2) {
     FwdArgs<double, double> a{mode, loss, shift, (const double*)y, (const double*)off, (const double*)wt,
-                              (double*)coef, (double*)dzz, z_out, with_offset, g_ablate, 0};
+                              (double*)coef, (double*)dzz, z_out, with_offset, g_ablate, 0, g_ls_z0, g_ls_t0, g_ls_tpend};
     return tl_fwd_impl<double, double, double>(c, x, a, stats, st);
   }
   FwdArgs<float, float> a{mode, loss, shift, (const float*)y, (const float*)off, (const float*)wt,
-                          (float*)coef, (float*)dzz, z_out, with_offset, g_ablate, 0};
+                          (float*)coef, (float*)dzz, z_out, with_offset, g_ablate, 0, g_ls_z0, g_ls_t0, g_ls_tpend};
   if (prec == 1) return tl_fwd_impl<float, float, float>(c, x, a, stats, st);
   return tl_fwd_impl<uint16_t, float, float>(c, x, a, stats, st);
 }
@@ -1853,6 +1912,24 @@ int pml_rs_tron(int B, int n, const double* L, const double* y, const double* of
   return 0;
 }
 
+// Margin-space line-search evaluation; out[0..1] = (F, D) or (F, S) when final. stats: >= 2 * 1024 doubles.
+int pml_ls_eval(int prec, int n, double t, int loss, double* z0, const double* zd, const void* y, const void* wt,
+                int final_, void* coef, void* dzz, double* stats, double* out, void* stream) {
+  if (n <= 0) return 0;
+  hipStream_t st = (hipStream_t)stream;
+  const int nb = (int)std::min<long long>(1024, ((long long)n + NTHREADS - 1) / NTHREADS);
+  if (prec == 2)
+    hipLaunchKernelGGL((ls_eval_kernel<double, double>), dim3(nb), dim3(NTHREADS), 0, st, n, t, loss, z0, zd,
+                       (const double*)y, (const double*)wt, final_, (double*)coef, (double*)dzz, stats);
+  else
+    hipLaunchKernelGGL((ls_eval_kernel<float, float>), dim3(nb), dim3(NTHREADS), 0, st, n, t, loss, z0, zd,
+                       (const float*)y, (const float*)wt, final_, (float*)coef, (float*)dzz, stats);
+  LAUNCH_CHECK();
+  hipLaunchKernelGGL(reduce_stats_kernel, dim3(1), dim3(NTHREADS), 0, st, stats, nb, out, 0);
+  LAUNCH_CHECK();
+  return 0;
+}
+
 int pml_segdot(const double* a, const double* b, int mode, const long long* ptr, int nseg, double* out,
                void* stream) {
   if (nseg <= 0) return 0;
@@ -1869,11 +1946,11 @@ int pml_tl_fwd_multi(int prec, const TLFwdMultiDesc* c, const void* x, int mode,
   hipStream_t st = (hipStream_t)stream;
   if (prec == 2) {
     FwdArgs<double, double> a{mode, loss, shift, (const double*)y, (const double*)off, (const double*)wt,
-                              (double*)coef, (double*)dzz, z_out, with_offset, 0, 0};
+                              (double*)coef, (double*)dzz, z_out, with_offset, 0, 0, g_ls_z0, g_ls_t0, g_ls_tpend};
     return tl_fwd_multi_impl<double, double, double>(c, x, a, stats, st);
   }
   FwdArgs<float, float> a{mode, loss, shift, (const float*)y, (const float*)off, (const float*)wt,
-                          (float*)coef, (float*)dzz, z_out, with_offset, 0, 0};
+                          (float*)coef, (float*)dzz, z_out, with_offset, 0, 0, g_ls_z0, g_ls_t0, g_ls_tpend};
   if (prec == 1) return tl_fwd_multi_impl<float, float, float>(c, x, a, stats, st);
   return tl_fwd_multi_impl<uint16_t, float, float>(c, x, a, stats, st);
 }

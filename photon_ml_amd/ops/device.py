@@ -50,7 +50,7 @@ PRECISIONS = {"bf16": 0, "f32": 1, "f64": 2}
 VAL_DTYPE = {0: torch.bfloat16, 1: torch.float32, 2: torch.float64}
 VEC_DTYPE = {0: torch.float32, 1: torch.float32, 2: torch.float64}
 
-FWD_MARGIN, FWD_VALUE_GRAD, FWD_HV, FWD_DZZ = 0, 1, 2, 3
+FWD_MARGIN, FWD_VALUE_GRAD, FWD_HV, FWD_DZZ, FWD_LS = 0, 1, 2, 3, 4
 
 
 def _pad8(n: int) -> int:
@@ -314,6 +314,97 @@ class DeviceGLMData(GLMComputable):
 
     def set_offsets(self, offsets):
         self.o.copy_(torch.as_tensor(offsets, device=self.device).to(self.vdt))
+        self._z_key = None
+
+    # ---- margin-space line search (GLMObjective.margin_line_search / LBFGS): z(t) = z0 + t zd ----------------
+    # State: the margins of the last accepted point are z0 + tpend * zd (the accepted step is materialised
+    # lazily in the next direction pass); _z_key identifies that point.
+    LS_REFRESH = 50  # recompute z0 with a forward pass after this many chained updates (bounds rounding drift)
+
+    def enable_margin_cache(self):
+        """Keep the margins of the last full evaluation (8 B/row) so a line search needs one forward pass for
+        the direction (which also evaluates the first trial step) and one elementwise pass per further trial."""
+        if getattr(self, "z_cache", None) is None:
+            n = max(self.n_rows, 1)
+            self.z_cache = torch.zeros(n, dtype=torch.float64, device=self.device)
+            self.zd = torch.zeros(n, dtype=torch.float64, device=self.device)
+            self.ls_stats = torch.zeros(2 * 1024, dtype=torch.float64, device=self.device)
+            self.ls_out = torch.zeros(2, dtype=torch.float64, device=self.device)
+            self._z_key, self._z_chain, self._tpend, self._ls_t0 = None, 0, 0.0, None
+        return True
+
+    def _z_valid_for(self, w_eff, shift) -> bool:
+        key = getattr(self, "_z_key", None)
+        return (key is not None and key[1] == float(shift) and key[0].shape == w_eff.shape
+                and self._z_chain < self.LS_REFRESH and bool(torch.equal(key[0], w_eff.to(key[0].device, key[0].dtype))))
+
+    def ls_begin(self, w0_eff, shift0, d_eff, d_shift, t0: float = 1.0, loss=None) -> bool:
+        """Direction pass (FWD_LS): zd = X d_eff + d_shift, materialises the pending step into z0, and evaluates
+        the first trial t0 (F, D and the speculative gradient input coef = w l'(z(t0)))."""
+        if loss is None:
+            return False
+        if getattr(self, "z_cache", None) is None:
+            self.enable_margin_cache()   # from now on every value+gradient pass also stores its margins
+        if not self._z_valid_for(w0_eff, shift0):
+            self.fwd_all(self._vec(w0_eff), FWD_MARGIN, 0, shift0, None, None, z_out=self.z_cache, with_offset=1,
+                         stats=False)
+            self._z_key, self._z_chain, self._tpend = (w0_eff.detach().clone(), float(shift0)), 0, 0.0
+        with trace_range("K1' direction pass (margins of d + first trial)"):
+            self.lib.pml_set_ls_args(self.z_cache.data_ptr(), float(t0), float(self._tpend))
+            self.fwd_all(self._vec(d_eff), FWD_LS, loss.loss_id, d_shift, self.coef, None, z_out=self.zd)
+            self.lib.pml_set_ls_args(None, 0.0, 0.0)
+            self._tpend = 0.0
+            self._ls_t0 = float(t0)
+            self._ls_t0_vals = tuple(self._reduce_stats().tolist())   # local (F, D) at t0
+        return True
+
+    def _ls(self, loss, t, final, out):
+        dzz = self.dzz if (final and self.track_hessian and loss.twice_differentiable) else None
+        check(self.lib.pml_ls_eval(self.prec, self.n_rows, float(t), loss.loss_id, self.z_cache.data_ptr(),
+                                   self.zd.data_ptr(), self.y.data_ptr(), self.wt.data_ptr(), int(final),
+                                   self.coef.data_ptr() if final else None, None if dzz is None else dzz.data_ptr(),
+                                   self.ls_stats.data_ptr(), out.data_ptr(), stream_handle(self.device)), "ls_eval")
+
+    def ls_eval(self, loss, t: float):
+        if self._ls_t0 is not None and float(t) == self._ls_t0:
+            return self._ls_t0_vals       # evaluated by the direction pass
+        with trace_range("line-search trial (margin space)"):
+            self._ls(loss, t, 0, self.ls_out)
+            f, d = self.ls_out.tolist()
+        return f, d
+
+    def ls_finish_packed(self, loss, t: float, w_eff, shift, need_s: bool = True, start_reduce=None,
+                         nb: int = 0) -> torch.Tensor:
+        """Accepted step: gradient input coef = w l'(z(t)) (already there when t is the first trial), then ONLY
+        the transpose pass: packed local [G | F | S]. z0 <- z(t) is deferred to the next direction pass."""
+        with trace_range("K1 gradient at the accepted step (transpose pass)"):
+            out = torch.zeros(self.dim + 2, dtype=torch.float64, device=self.device)
+            if self._ls_t0 is not None and float(t) == self._ls_t0 and not (
+                    self.track_hessian and loss.twice_differentiable):
+                out[self.dim] = self._ls_t0_vals[0]
+                if need_s:
+                    out[self.dim + 1] = self.coef[: self.n_rows].to(torch.float64).sum()
+            else:
+                self._ls(loss, t, 1, out[self.dim:])
+            self._tpend = float(t)
+            self._ls_t0 = None
+            self._z_key, self._z_chain = (w_eff.detach().clone(), float(shift)), self._z_chain + 1
+            if self.track_hessian and loss.twice_differentiable:
+                self._dzz_key, self._dzz_shift = w_eff.detach().clone(), float(shift)
+            if start_reduce is not None:
+                start_reduce(out[self.dim:])
+                self._packed_bucketed(self.coef, out[: self.dim], start_reduce, nb)
+            else:
+                self.t_all(self.coef, out[: self.dim])
+                if self.old_of_new is not None:
+                    out[: self.dim] = self._unperm(out[: self.dim].clone())
+            self.n_passes += 1
+            return out
+
+    def ls_finish_sums(self, loss, t: float, w_eff, shift, need_s: bool = True):
+        out = self.ls_finish_packed(loss, t, w_eff, shift, need_s)
+        f, s_ = out[self.dim:].tolist()
+        return f, s_, out[: self.dim]
 
     def set_weights(self, weights):
         self.wt.copy_(torch.as_tensor(weights, device=self.device).to(self.vdt))
@@ -468,7 +559,11 @@ class DeviceGLMData(GLMComputable):
             out = torch.zeros(self.dim + 2, dtype=torch.float64, device=self.device)
             x = self._vec(w_eff)
             dzz = self.dzz if (self.track_hessian and loss.twice_differentiable) else None
-            self.fwd_all(x, FWD_VALUE_GRAD, loss.loss_id, margin_shift, self.coef, dzz)
+            zc = getattr(self, "z_cache", None)
+            self.fwd_all(x, FWD_VALUE_GRAD, loss.loss_id, margin_shift, self.coef, dzz, z_out=zc)
+            if zc is not None:
+                self._z_key, self._z_chain, self._tpend, self._ls_t0 = (w_eff.detach().clone(),
+                                                                         float(margin_shift)), 0, 0.0, None
             out[self.dim:] = self._reduce_stats()
             start_reduce(out[self.dim:])
             self._packed_bucketed(self.coef, out[: self.dim], start_reduce, nb)
@@ -530,7 +625,11 @@ class DeviceGLMData(GLMComputable):
         G = out[: self.dim]
         x = self._vec(w_eff)
         dzz = self.dzz if (self.track_hessian and loss.twice_differentiable) else None
-        self.fwd_all(x, FWD_VALUE_GRAD, loss.loss_id, margin_shift, self.coef, dzz)
+        zc = getattr(self, "z_cache", None)
+        self.fwd_all(x, FWD_VALUE_GRAD, loss.loss_id, margin_shift, self.coef, dzz, z_out=zc)
+        if zc is not None:
+            self._z_key, self._z_chain, self._tpend, self._ls_t0 = (w_eff.detach().clone(), float(margin_shift)), \
+                0, 0.0, None
         self.t_all(self.coef, G)
         out[self.dim:] = self._reduce_stats()
         if self.old_of_new is not None:

@@ -100,11 +100,14 @@ def glm_lib() -> Optional[ctypes.CDLL]:
         lib.pml_seg_cg_step.argtypes = [c_void_p, c_int] + [c_void_p] * 7 + [c_double, c_void_p]
         lib.pml_bgemv.argtypes = [c_int, c_int, c_void_p, c_void_p, c_void_p, c_int, c_void_p]
         lib.pml_bhv.argtypes = [c_int, c_int, c_void_p, c_void_p, c_void_p, c_double, c_void_p, c_void_p]
+        lib.pml_set_ls_args.argtypes = [c_void_p, c_double, c_double]
+        lib.pml_ls_eval.argtypes = [c_int, c_int, c_double, c_int, c_void_p, c_void_p, c_void_p, c_void_p, c_int,
+                                    c_void_p, c_void_p, c_void_p, c_void_p, c_void_p]
         lib.pml_rs_tron.argtypes = [c_int, c_int] + [c_void_p] * 8 + [c_int, c_double, c_double, c_int, c_int, c_int,
                                                                       c_void_p]
         for f in ("pml_seg_fwd", "pml_seg_t", "pml_reduce_stats", "pml_build_blocks", "pml_tl_fwd", "pml_tl_t",
                   "pml_tl_maxbits", "pml_segdot", "pml_tl_fwd_multi", "pml_tl_t_multi", "pml_seg_cg_step",
-                  "pml_seg_expand", "pml_bgemv", "pml_bhv", "pml_rs_tron"):
+                  "pml_seg_expand", "pml_bgemv", "pml_bhv", "pml_rs_tron", "pml_ls_eval"):
             getattr(lib, f).restype = c_int
         lib.pml_set_config.argtypes = [c_int, c_int, c_int, c_int]
         lib._pml_typed = True

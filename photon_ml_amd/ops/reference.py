@@ -130,6 +130,22 @@ class TorchGLMData(GLMComputable):
         l, _ = loss.loss_and_dz(z, self.y)
         return l
 
+    # margin-space line search (see GLMObjective.margin_line_search); fp64 reference of ls_eval_kernel
+    def ls_begin(self, w0_eff, shift0, d_eff, d_shift, t0: float = 1.0, loss=None) -> bool:
+        self._z0 = self.margins(w0_eff, shift0, True)
+        self._zd = self.margins(d_eff, d_shift, False)
+        return True
+
+    def ls_eval(self, loss, t: float):
+        l, dl = loss.loss_and_dz(self._z0 + t * self._zd, self.y)
+        return float(torch.sum(self.wt * l)), float(torch.sum(self.wt * dl * self._zd))
+
+    def ls_finish_sums(self, loss, t: float, w_eff, shift, need_s: bool = True):
+        z = self._z0 + t * self._zd
+        l, dl = loss.loss_and_dz(z, self.y)
+        r = self.wt * dl
+        return float(torch.sum(self.wt * l)), float(torch.sum(r)), self._xtv(r)
+
     def set_offsets(self, offsets):
         self.o = torch.as_tensor(offsets, dtype=torch.float64).to(self.device)
 

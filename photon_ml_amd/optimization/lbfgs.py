@@ -14,6 +14,7 @@ reference wraps Breeze; here the quasi-Newton engine is native to this framework
 """
 from __future__ import annotations
 
+import os
 from typing import Optional
 
 import torch
@@ -24,6 +25,8 @@ from .optimizer import Optimizer, OptimizerState, project_box
 from .vector_space import vdot as _dot, vnorm as _norm
 
 DEFAULT_MAX_ITER = 100
+# L-BFGS line searches in margin space when the data backend caches margins (GLMObjective.margin_line_search)
+MARGIN_LINE_SEARCH = os.environ.get("PML_MARGIN_LINE_SEARCH", "1") != "0"
 DEFAULT_NUM_CORRECTIONS = 10
 DEFAULT_TOLERANCE = 1.0e-7
 
@@ -142,6 +145,13 @@ class LBFGS(Optimizer):
         x0 = state.coefficients
         g0 = _dot(state.gradient, d)
         t0 = 1.0 / _norm(d) if self._inner_iter == 0 else 1.0
+        mls = None
+        if MARGIN_LINE_SEARCH and not self.constraints and hasattr(objective, "margin_line_search"):
+            mls = objective.margin_line_search(data, x0, d, t0)
+        if mls is not None:
+            # trials in margin space (one elementwise pass each), full gradient only at the accepted step
+            _, _, _, t = strong_wolfe(lambda tt: (*mls.eval(tt), tt), state.loss, g0, t0)  # payload = the step
+            return mls.finish(t)
 
         def phi(t):
             x = x0 + t * d

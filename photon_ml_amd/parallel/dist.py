@@ -168,6 +168,49 @@ class DistributedGLMData:
             check_finite_(buf, fn)
         return buf
 
+    # margin-space line search: trials need two scalars per rank; the accepted step one (overlapped) reduction
+    def ls_begin(self, w0_eff, shift0, d_eff, d_shift, t0: float = 1.0, loss=None) -> bool:
+        ok = bool(getattr(self.local, "ls_begin", lambda *a, **k: False)(w0_eff, shift0, d_eff, d_shift, t0, loss))
+        return all_reduce_scalar(1.0 if ok else 0.0, "min", device=self._scalar_device(), group=self.group) > 0
+
+    def _scalar_device(self):
+        return self.local.device if dist.get_backend(self.group) == "nccl" else None
+
+    def ls_eval(self, loss, t: float):
+        f, d = self.local.ls_eval(loss, t)
+        dev = self._comm_device()
+        v = torch.tensor([f, d], dtype=torch.float64, device=dev)
+        all_reduce_(v, group=self.group)
+        if self.nan_guard:
+            check_finite_(v, "line search")
+        f, d = v.tolist()
+        return f, d
+
+    def ls_finish_sums(self, loss, t: float, w_eff, shift, need_s: bool = True):
+        if self.overlap and hasattr(self.local, "ls_finish_packed"):
+            works = []
+
+            def start(x):
+                works.append(dist.all_reduce(x, group=self.group, async_op=True))
+
+            with trace_range(f"C1 overlapped all-reduce (accepted step) [{self.dim + 2} fp64]"):
+                buf = self.local.ls_finish_packed(loss, t, w_eff, shift, need_s, start_reduce=start, nb=self.buckets)
+                for w in works:
+                    w.wait()
+            if self.local.old_of_new is not None:
+                buf[: self.dim] = self.local._unperm(buf[: self.dim].clone())
+        else:
+            f, s_, g = self.local.ls_finish_sums(loss, t, w_eff, shift, need_s)
+            buf = torch.cat([g.to(torch.float64), torch.tensor([f, s_], dtype=torch.float64, device=g.device)])
+            dev = self._comm_device()
+            tmp = buf.to(dev)
+            all_reduce_(tmp, group=self.group)
+            buf = tmp.to(buf.device)
+        if self.nan_guard:
+            check_finite_(buf, "ls_finish")
+        fs = buf[self.dim:].tolist()
+        return fs[0], fs[1], buf[: self.dim]
+
     def value_grad_sums(self, loss, w_eff, margin_shift):
         buf = self._packed("value_grad", loss, w_eff, margin_shift)
         fs = buf[self.dim:].tolist()

@@ -354,3 +354,29 @@ def test_bucketed_gradient_pass_is_bitwise_equal(nb):
     if data.old_of_new is not None:
         hb[: data.dim] = data._unperm(hb[: data.dim].clone())
     assert torch.equal(hb, href)
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("precision", ["f64", "bf16"])
+def test_margin_space_line_search_on_device(precision, monkeypatch):
+    """ls_eval_kernel path (cached margins, elementwise trials, transpose-only accepted step) vs full
+    evaluations at every trial on the HIP data backend: same L-BFGS iterates (f64: tight; bf16 data: the fp32
+    coefficient rounding differs between z0 + t zd and X fp32(x0 + t d), so only to ~1e-5)."""
+    import photon_ml_amd.optimization.lbfgs as lb
+    from photon_ml_amd.data.synthetic import generate_glm_data
+    from photon_ml_amd.function.losses import LOGISTIC
+    from photon_ml_amd.function.objective import GLMObjective
+    from photon_ml_amd.ops.device import DeviceGLMData
+    data, _ = generate_glm_data("LOGISTIC_REGRESSION", 20000, 300, density=0.05, seed=9)
+    out = {}
+    for mode in (False, True):
+        monkeypatch.setattr(lb, "MARGIN_LINE_SEARCH", mode)
+        dev = DeviceGLMData.from_labeled(data, "cuda", precision, chunk_rows=8192, layout="tiled")
+        obj = GLMObjective(LOGISTIC, 1.0)
+        opt = lb.LBFGS(tolerance=1e-12, max_iterations=15)
+        w, f = opt.optimize(obj, dev, torch.zeros(300, dtype=torch.float64, device="cuda"))
+        out[mode] = (w, f, dev.n_passes)
+    (w0, f0, p0), (w1, f1, p1) = out[False], out[True]
+    tol = 1e-9 if precision == "f64" else 1e-5
+    assert torch.allclose(w0, w1, rtol=tol, atol=tol) and abs(f0 - f1) <= tol * abs(f0)
+    assert p1 <= p0

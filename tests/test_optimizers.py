@@ -106,3 +106,32 @@ def test_tron_matches_lbfgs_logistic():
     w2, f2 = TRON(tolerance=1e-10, max_iterations=50).optimize(obj, data, torch.zeros(8, dtype=torch.float64))
     assert abs(f1 - f2) < 1e-7
     assert np.allclose(w1.numpy(), w2.numpy(), atol=1e-5)
+
+
+@pytest.mark.parametrize("norm", [None, "STANDARDIZATION"])
+@pytest.mark.parametrize("task", ["LOGISTIC_REGRESSION", "POISSON_REGRESSION", "LINEAR_REGRESSION"])
+def test_margin_space_line_search_matches_full_evaluations(task, norm, monkeypatch):
+    """L-BFGS with trial steps evaluated from cached margins (z0 + t zd; full gradient only at the accepted step)
+    follows the same iterates as the line search that evaluates the full objective at every trial."""
+    import photon_ml_amd.optimization.lbfgs as lb
+    from photon_ml_amd.data.synthetic import generate_glm_data
+    from photon_ml_amd.function.losses import loss_for_task
+    from photon_ml_amd.function.objective import GLMObjective
+    from photon_ml_amd.normalization.context import NormalizationContext
+    from photon_ml_amd.ops.reference import TorchGLMData
+    from photon_ml_amd.stat.summary import BasicStatisticalSummary
+    data, _ = generate_glm_data(task, 2000, 25, density=0.3, seed=4)
+    nc = NormalizationContext.build(norm, BasicStatisticalSummary.compute(data.x), data.n_features - 1) if norm \
+        else None
+    gd = TorchGLMData(data, "cpu")
+    out = {}
+    for mode in (False, True):
+        monkeypatch.setattr(lb, "MARGIN_LINE_SEARCH", mode)
+        obj = GLMObjective(loss_for_task(task), 0.5, nc)
+        opt = lb.LBFGS(tolerance=1e-12, max_iterations=25)
+        w, f = opt.optimize(obj, gd, torch.zeros(25, dtype=torch.float64))
+        out[mode] = (w, f, obj.n_value_grad, opt.current.iter)
+    (w0, f0, n0, i0), (w1, f1, n1, i1) = out[False], out[True]
+    assert i0 == i1
+    assert torch.allclose(w0, w1, rtol=1e-8, atol=1e-10) and abs(f0 - f1) <= 1e-10 * abs(f0)
+    assert n1 <= n0  # full (forward + transpose) evaluations: only initial state + one per accepted step
