@@ -75,3 +75,57 @@ class BasicStatisticalSummary:
                 dist.all_reduce(tmn, op=dist.ReduceOp.MIN)
                 mx, mn = tmx.numpy(), tmn.numpy()
         return BasicStatisticalSummary.from_sufficient(count, s1, s2, sabs, nnz, mx, mn)
+
+    @staticmethod
+    def from_device(data, all_reduce: bool = False) -> "BasicStatisticalSummary":
+        """Same statistics straight from a device-resident shard (``ops.device.DeviceGLMData``, tiled layout):
+        column reductions over the forward streams with device scatter-reductions, no host copy of the
+        non-zeros (K9 on the GPU); with ``all_reduce`` the sufficient statistics are reduced over the process
+        group (C24). Feature order: original (the device relabelling is undone)."""
+        dev = data.device
+        d = data.dim
+        f64 = torch.float64
+        s1 = torch.zeros(d, dtype=f64, device=dev)
+        s2 = torch.zeros(d, dtype=f64, device=dev)
+        sabs = torch.zeros(d, dtype=f64, device=dev)
+        nnz = torch.zeros(d, dtype=f64, device=dev)
+        mx = torch.full((d,), float("-inf"), dtype=f64, device=dev)
+        mn = torch.full((d,), float("inf"), dtype=f64, device=dev)
+        for c, ch in enumerate(data.csr):
+            if getattr(ch, "kind", None) != "tl":
+                raise ValueError("from_device needs the tiled layout")
+            pk, vl = ch.logical()
+            col = ((pk.to(torch.int64) & 0xFFFFFFFF) >> ch.rbits) + data.col_lo[c]
+            v = vl.to(f64)
+            s1.index_add_(0, col, v)
+            s2.index_add_(0, col, v * v)
+            sabs.index_add_(0, col, v.abs())
+            nnz.index_add_(0, col, torch.ones_like(v))
+            mx.scatter_reduce_(0, col, v, "amax")
+            mn.scatter_reduce_(0, col, v, "amin")
+            del pk, vl, col, v
+        if data.old_of_new is not None:   # device column j is original feature old_of_new[j]
+            def unperm(t):
+                out = torch.empty_like(t)
+                out[data.old_of_new] = t
+                return out
+            s1, s2, sabs, nnz, mx, mn = (unperm(t) for t in (s1, s2, sabs, nnz, mx, mn))
+        count = float(data.n_rows)
+        if all_reduce:
+            from ..parallel.dist import is_dist
+            import torch.distributed as dist
+            if is_dist():
+                cdev = dev if dist.get_backend() == "nccl" else torch.device("cpu")
+                buf = torch.cat([torch.tensor([count], dtype=f64, device=dev), s1, s2, sabs, nnz]).to(cdev)
+                dist.all_reduce(buf)
+                count = float(buf[0])
+                s1, s2, sabs, nnz = (t.to(dev) for t in buf[1:].split(d))
+                tmx, tmn = mx.to(cdev), mn.to(cdev)
+                dist.all_reduce(tmx, op=dist.ReduceOp.MAX)
+                dist.all_reduce(tmn, op=dist.ReduceOp.MIN)
+                mx, mn = tmx.to(dev), tmn.to(dev)
+        mx = torch.where(torch.isinf(mx), torch.zeros_like(mx), mx)
+        mn = torch.where(torch.isinf(mn), torch.zeros_like(mn), mn)
+        h = lambda t: t.cpu().numpy()
+        return BasicStatisticalSummary.from_sufficient(int(count), h(s1), h(s2), h(sabs), h(nnz), h(mx), h(mn))
+

@@ -115,3 +115,21 @@ def test_tl_shard_wide_transpose_emulation(chunk, item, hot):
     assert all((row[4] < 0) == (row[1] in single) for row in it)
     cu = mt.cu.numpy()[: mt.ncu]
     assert (cu[:, 2] - cu[:, 1] <= COMBINE_SEG).all() and mt.mt_ptr.numpy()[-1] == mt.ncu
+
+
+@pytest.mark.parametrize("il", [0, 1])
+def test_feature_statistics_from_device_shard_match_host(il, monkeypatch):
+    """BasicStatisticalSummary.from_device (column reductions over the tiled streams, relabelling undone) ==
+    the host scipy computation (MLlib colStats semantics, implicit zeros in max/min)."""
+    from photon_ml_amd.data.synthetic import generate_glm_data
+    from photon_ml_amd.ops import tiled
+    from photon_ml_amd.ops.device import DeviceGLMData
+    from photon_ml_amd.stat.summary import BasicStatisticalSummary
+    monkeypatch.setattr(tiled, "INTERLEAVE", il)
+    data, _ = generate_glm_data("LOGISTIC_REGRESSION", 3000, 200, density=0.05, seed=4)
+    dev = DeviceGLMData.from_labeled(data, "cpu", "f64", chunk_rows=1000, layout="tiled", relabel=True)
+    a = BasicStatisticalSummary.from_device(dev)
+    b = BasicStatisticalSummary.compute(data.x)
+    for f in ("mean", "variance", "num_nonzeros", "max", "min", "norm_l1", "norm_l2", "mean_abs"):
+        np.testing.assert_allclose(getattr(a, f).numpy(), getattr(b, f).numpy(), rtol=1e-12, atol=1e-12, err_msg=f)
+    assert a.count == b.count
