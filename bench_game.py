@@ -46,7 +46,8 @@ def main():
     ap = argparse.ArgumentParser()
     ap.add_argument("--gpus", type=int, default=1)
     ap.add_argument("--steps", type=int, default=3)
-    ap.add_argument("--warmup", type=int, default=1)
+    ap.add_argument("--warmup", type=int, default=3,
+                    help="untimed sweeps (the first sweeps also grow the caching allocator's pool of model-sized blocks)")
     ap.add_argument("--config", default="small", choices=list(PRESETS))
     ap.add_argument("--entities-per-gpu", type=int)
     ap.add_argument("--rows-per-entity", type=int)
@@ -124,6 +125,10 @@ def main():
     total_rows = int(all_reduce_scalar(float(data.n_rows)))
     if rank == 0:
         log(f"final training loss {loss:.6e}; RE stats {re_stats}")
+        if torch.cuda.is_available():
+            ms = torch.cuda.memory_stats()
+            log(f"allocator: peak reserved {ms.get('reserved_bytes.all.peak', 0) / 2**30:.1f} GiB, "
+                f"alloc retries {ms.get('num_alloc_retries', 0)}, device mallocs {ms.get('segment.all.allocated', 0)}")
         for rec in cd.history[-2 * args.steps:]:
             log(f"  iteration {rec.get('iteration')} coordinate {rec['coordinate']}: {rec['seconds']:.3f}s")
         print(json.dumps({
