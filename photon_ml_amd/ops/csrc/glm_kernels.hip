@@ -874,7 +874,7 @@ __constant__ int c_tl_ablate = 0;
 #define TL_ABL 0
 #endif
 
-template <typename VT, typename XT, typename AT, bool SQ, int NW>
+template <typename VT, typename XT, typename AT, bool SQ, int NW, bool DD = false>
 __device__ __forceinline__ void tl_stream_il(const uint32_t* __restrict__ pack, const VT* __restrict__ val,
                                              const XT* __restrict__ x, int e_lo, int e_hi, int sbits, AT* acc) {
   typedef typename TLValT<VT>::T LT;
@@ -899,14 +899,35 @@ __device__ __forceinline__ void tl_stream_il(const uint32_t* __restrict__ pack, 
     const int e = e_lo + r * TL_ROUND + lane;  // logical index of quad element 0; element k is e + 64k
     bool in[TL_VEC];
     XT xv[TL_VEC];
+    int hd[TL_VEC];
 #pragma unroll
     for (int k = 0; k < TL_VEC; ++k) {
       in[k] = e + 64 * k < e_hi;
-      xv[k] = (abl & 8) ? XT(1) : ldg(x + (in[k] ? (pk[k] >> sbits) : 0u));
+      const uint32_t key = in[k] ? (pk[k] >> sbits) : 0u;
+      if (DD) {
+        // gather dedup: lanes hold consecutive sorted entries, so equal gather keys form runs of lanes; only
+        // each run's head lane issues the load (fewer active lanes for the texture address/data units) and the
+        // value is broadcast from the head (prefix-max of head lane ids, 6 shuffle steps). Measured on MI355X
+        // (16M rows, profiles/tl_dedup_ab_16M.txt): forward 2.50 -> 3.42 ms, transpose 2.70 -> 3.65 ms — the
+        // TA/TD cost of a gather does not shrink with masked lanes, the shuffles are pure overhead. Off.
+        const uint32_t prev = __shfl_up(key, 1, 64);
+        const bool head = lane == 0 || prev != key;
+        int h = head ? lane : 0;
+#pragma unroll
+        for (int o = 1; o < 64; o <<= 1) h = max(h, __shfl_up(h, o, 64));
+        hd[k] = h;
+        xv[k] = head ? ldg(x + key) : XT(0);
+      } else {
+        xv[k] = (abl & 8) ? XT(1) : ldg(x + key);
+      }
     }
     // unconditional refill (past the end: re-read round r, L2-hot, never used) so the wave's outstanding-load
     // count is static and each LDS add waits only for its own gather (vmcnt(5..2)), not for the prefetch
     load_round(r + 2 < r1 ? r + 2 : r, pk_slot, v_slot);
+    if (DD) {
+#pragma unroll
+      for (int k = 0; k < TL_VEC; ++k) xv[k] = __shfl(xv[k], hd[k], 64);
+    }
     LT v[TL_VEC];
     TLVals<VT>::get(v_raw, v);
     // branchless: padding / past-the-end entries add an exact 0 (select, not multiply: no NaN from x)
@@ -935,6 +956,7 @@ __device__ __forceinline__ void tl_stream(const uint32_t* __restrict__ pack, con
   if (P == 1) tl_stream_p1<VT, XT, AT, SQ, U, NW>(pack, val, x, e_lo, e_hi, sbits, acc);
   else if (P == 2) tl_stream_wide<VT, XT, AT, SQ, NW, 2>(pack, val, x, e_lo, e_hi, sbits, acc);
   else if (P == 3) tl_stream_il<VT, XT, AT, SQ, NW>(pack, val, x, e_lo, e_hi, sbits, acc);
+  else if (P == 4) tl_stream_il<VT, XT, AT, SQ, NW, true>(pack, val, x, e_lo, e_hi, sbits, acc);
   else tl_stream_p0<VT, XT, AT, SQ, U, NW>(pack, val, x, e_lo, e_hi, sbits, acc);
 }
 
@@ -1110,12 +1132,14 @@ static int g_tl_waves = 4;     // forward
 static int g_tl_waves_t = 4;   // transpose
 static int g_tl_pipe = 0;      // forward stream pipeline variant (see tl_stream)
 static int g_tl_pipe_t = 0;    // transpose stream pipeline variant
+static int g_tl_dedup = 0;     // interleaved forward: gather dedup across lanes (P = 4)
+static int g_tl_dedup_t = 0;   // interleaved transpose: gather dedup
 
 template <typename VT, typename XT, typename RT, typename AT, int MAXR>
 static void tl_fwd_launch(const TLFwdDesc* c, const void* x, FwdArgs<XT, RT> a, double* stats, hipStream_t st) {
 #define TLF(NW, P) hipLaunchKernelGGL((tl_fwd_kernel<VT, XT, RT, AT, MAXR, 2, NW, P>), dim3(c->nblk), dim3(NW * 64), 0, \
                                     st, c->blk, c->rbits, c->pack, (const VT*)c->val, (const XT*)x, a, stats)
-  if (c->il) { if (g_tl_waves <= 2) TLF(2, 3); else TLF(4, 3); }
+  if (c->il) { if (g_tl_waves <= 2) { if (g_tl_dedup) TLF(2, 4); else TLF(2, 3); } else { if (g_tl_dedup) TLF(4, 4); else TLF(4, 3); } }
   else if (g_tl_waves == 2) { if (g_tl_pipe == 1) TLF(2, 1); else TLF(2, 0); }
   else { if (g_tl_pipe == 1) TLF(4, 1); else TLF(4, 0); }
 #undef TLF
@@ -1126,7 +1150,10 @@ static void tl_fwd_multi_launch(const TLFwdMultiDesc* c, const void* x, FwdArgs<
                                 hipStream_t st) {
 #define TLM(NW, P) hipLaunchKernelGGL((tl_fwd_multi_kernel<VT, XT, RT, AT, MAXR, 2, NW, P>), dim3(c->nblk), \
                                       dim3(NW * 64), 0, st, c->blk, c->rbits, c->packs, c->vals, (const XT*)x, a, stats)
-  if (c->il) { if (g_tl_waves == 1) TLM(1, 3); else if (g_tl_waves == 2) TLM(2, 3); else TLM(4, 3); }
+  if (c->il) {
+    if (g_tl_dedup) { if (g_tl_waves == 1) TLM(1, 4); else if (g_tl_waves == 2) TLM(2, 4); else TLM(4, 4); }
+    else { if (g_tl_waves == 1) TLM(1, 3); else if (g_tl_waves == 2) TLM(2, 3); else TLM(4, 3); }
+  }
   else if (g_tl_waves == 2) { if (g_tl_pipe == 2) TLM(2, 2); else TLM(2, 0); }
   else { if (g_tl_pipe == 2) TLM(4, 2); else TLM(4, 0); }
 #undef TLM
@@ -1173,7 +1200,7 @@ template <typename VT, typename XT, typename AT, bool SQ, int MAXR>
 static void tl_t_launch(const TLTDesc* c, const void* x, double* G, double* parts, hipStream_t st) {
 #define TLT(NW, P) hipLaunchKernelGGL((tl_t_kernel<VT, XT, AT, SQ, MAXR, 2, NW, P>), dim3(c->nitems), dim3(NW * 64), 0, \
                                     st, c->items, c->cbits, c->pack, (const VT*)c->val, (const XT*)x, G, c->dim, parts)
-  if (c->il) { if (g_tl_waves_t == 2) TLT(2, 3); else TLT(4, 3); }
+  if (c->il) { if (g_tl_waves_t == 2) { if (g_tl_dedup_t) TLT(2, 4); else TLT(2, 3); } else { if (g_tl_dedup_t) TLT(4, 4); else TLT(4, 3); } }
   else if (g_tl_waves_t == 2) { if (g_tl_pipe_t == 1) TLT(2, 1); else TLT(2, 0); }
   else { if (g_tl_pipe_t == 1) TLT(4, 1); else TLT(4, 0); }
 #undef TLT
@@ -1213,7 +1240,7 @@ static void tl_t_multi_launch(const TLTMultiDesc* c, const void* x, double* G, d
 #define TLTM(NW, P) hipLaunchKernelGGL((tl_t_multi_kernel<VT, XT, AT, SQ, MAXR, 2, NW, P>), dim3(c->nitems), \
                                        dim3(NW * 64), 0, st, c->items, c->cbits, c->packs, c->vals, (const XT*)x, G, \
                                        c->dim, parts)
-  if (c->il) { if (g_tl_waves_t == 2) TLTM(2, 3); else TLTM(4, 3); }
+  if (c->il) { if (g_tl_waves_t == 2) { if (g_tl_dedup_t) TLTM(2, 4); else TLTM(2, 3); } else { if (g_tl_dedup_t) TLTM(4, 4); else TLTM(4, 3); } }
   else if (g_tl_waves_t == 2) { if (g_tl_pipe_t == 2) TLTM(2, 2); else TLTM(2, 0); }
   else { if (g_tl_pipe_t == 2) TLTM(4, 2); else TLTM(4, 0); }
 #undef TLTM
@@ -1679,6 +1706,8 @@ __global__ __launch_bounds__(NTHREADS) void ls_eval_kernel(int n, double t, int 
 extern "C" {
 
 int pml_version() { return 1; }
+void pml_tl_set_dedup(int fwd, int t) { g_tl_dedup = fwd; g_tl_dedup_t = t; }
+
 void pml_set_ls_args(double* z0, double t0, double tpend) { g_ls_z0 = z0; g_ls_t0 = t0; g_ls_tpend = tpend; }
 
 void pml_set_ablate(int a) {

@@ -101,6 +101,7 @@ def glm_lib() -> Optional[ctypes.CDLL]:
         lib.pml_bgemv.argtypes = [c_int, c_int, c_void_p, c_void_p, c_void_p, c_int, c_void_p]
         lib.pml_bhv.argtypes = [c_int, c_int, c_void_p, c_void_p, c_void_p, c_double, c_void_p, c_void_p]
         lib.pml_set_ls_args.argtypes = [c_void_p, c_double, c_double]
+        lib.pml_tl_set_dedup.argtypes = [c_int, c_int]
         lib.pml_ls_eval.argtypes = [c_int, c_int, c_double, c_int, c_void_p, c_void_p, c_void_p, c_void_p, c_int,
                                     c_void_p, c_void_p, c_void_p, c_void_p, c_void_p]
         lib.pml_rs_tron.argtypes = [c_int, c_int] + [c_void_p] * 8 + [c_int, c_double, c_double, c_int, c_int, c_int,
@@ -118,7 +119,8 @@ def glm_lib() -> Optional[ctypes.CDLL]:
 # Kernel configuration defaults (tuned on MI355X, see profiles/): forward = vector layout + 8192-entry LDS hot
 # table of the most frequent features; transpose = strided layout. Env overrides for experiments:
 # PML_FWD_STRIDED, PML_T_STRIDED, PML_HOT_N, PML_FWD_GRID.
-KERNEL_CONFIG = {"fwd_strided": 0, "t_strided": 0, "hot_n": 0, "fwd_grid": 1024, "tl_acc64": 1, "tl_waves": 2, "tl_waves_t": 4, "tl_pipe": 0, "tl_pipe_t": 0, "tl_multi": 1}
+KERNEL_CONFIG = {"fwd_strided": 0, "t_strided": 0, "hot_n": 0, "fwd_grid": 1024, "tl_acc64": 1, "tl_waves": 2,
+                 "tl_waves_t": 4, "tl_pipe": 0, "tl_pipe_t": 0, "tl_multi": 1, "tl_dedup": 0, "tl_dedup_t": 0}
 
 
 def configure(**kw):
@@ -133,6 +135,7 @@ def configure(**kw):
                            KERNEL_CONFIG["fwd_grid"])
         lib.pml_tl_config(KERNEL_CONFIG["tl_acc64"], KERNEL_CONFIG["tl_waves"], KERNEL_CONFIG["tl_waves_t"],
                           (KERNEL_CONFIG["tl_pipe"] & 3) | ((KERNEL_CONFIG["tl_pipe_t"] & 3) << 2))
+        lib.pml_tl_set_dedup(KERNEL_CONFIG["tl_dedup"], KERNEL_CONFIG["tl_dedup_t"])
     return dict(KERNEL_CONFIG)
 
 

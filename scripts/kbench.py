@@ -48,7 +48,8 @@ def main():
         lib.pml_set_ablate(abl)
         if cfg[0] == "tl":
             configure(tl_waves=cfg[1], tl_waves_t=cfg[2], tl_pipe=cfg[3],
-                      tl_multi=cfg[4] if len(cfg) > 4 else 1, tl_pipe_t=cfg[5] if len(cfg) > 5 else cfg[3])
+                      tl_multi=cfg[4] if len(cfg) > 4 else 1, tl_pipe_t=cfg[5] if len(cfg) > 5 else cfg[3],
+                      tl_dedup=cfg[6] if len(cfg) > 6 else 0, tl_dedup_t=cfg[7] if len(cfg) > 7 else 0)
         else:
             configure(fwd_strided=cfg[0], t_strided=cfg[1], hot_n=cfg[2])
         x = (w * 0.1).float()

@@ -380,3 +380,20 @@ def test_margin_space_line_search_on_device(precision, monkeypatch):
     tol = 1e-9 if precision == "f64" else 1e-5
     assert torch.allclose(w0, w1, rtol=tol, atol=tol) and abs(f0 - f1) <= tol * abs(f0)
     assert p1 <= p0
+
+
+@pytest.mark.gpu
+def test_gather_dedup_variant_is_bitwise_equal():
+    """Lane-run gather dedup (only run heads load, value broadcast by shuffles) changes no bits."""
+    from photon_ml_amd.data.synthetic import generate_device_shard
+    from photon_ml_amd.function.losses import LOGISTIC
+    from photon_ml_amd.ops.native import configure
+    data, w = generate_device_shard(300_000, 50_000, 30, "cuda", "bf16", chunk_rows=1 << 17, layout="tiled")
+    w = (w * 0.05).to(torch.float64)
+    try:
+        ref = data.value_grad_packed(LOGISTIC, w, 0.1)
+        configure(tl_dedup=1, tl_dedup_t=1)
+        got = data.value_grad_packed(LOGISTIC, w, 0.1)
+    finally:
+        configure(tl_dedup=0, tl_dedup_t=0)
+    assert torch.equal(got, ref)
