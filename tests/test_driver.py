@@ -142,3 +142,39 @@ def test_training_diagnostics(tmp_path):
     assert len(boot.important_features) == 14
     txt = open(tmp_path / "out" / "diagnostic.txt").read()
     assert "Learning curve" in txt and "Bootstrap" in txt
+
+
+@pytest.mark.parametrize("reg,opt,lams", [("NONE", "TRON", "0"), ("L2", "TRON", "0,1000"), ("L1", "LBFGS", "0,1000"),
+                                          ("ELASTIC_NET", "LBFGS", "0,1000")])
+def test_driver_linear_regression_diagnostic_matrix(tmp_path, reg, opt, lams):
+    """DriverTest.testDiagnosticGeneration analogue on the reference's linear_regression_train/val.avro fixtures:
+    7 features (with intercept), 1000 rows, standardization, full diagnostics, one model per lambda."""
+    args = ["--training-data-directory", f"{REF}/linear_regression_train.avro", "--validating-data-directory",
+            f"{REF}/linear_regression_val.avro", "--output-directory", str(tmp_path / "o"), "--task",
+            "LINEAR_REGRESSION", "--format", "TRAINING_EXAMPLE", "--optimizer", opt, "--regularization-type", reg,
+            "--regularization-weights", lams, "--normalization-type", "STANDARDIZATION", "--convergence-tolerance",
+            "1e-6", "--num-iterations", "20", "--diagnostic-mode", "ALL", "--summarization-output-dir",
+            str(tmp_path / "summary"), "--device", "cpu"]
+    if reg == "ELASTIC_NET":
+        args += ["--elastic-net-alpha", "0.5"]
+    d = drv.Driver(drv.build_parser().parse_args(args)).run()
+    assert d.train_data.n_features == 7 and d.train_data.n_rows == 1000
+    assert d.stage == drv.DriverStage.DIAGNOSED
+    models = drv.read_text_model(str(tmp_path / "o" / drv.LEARNED_MODELS_TEXT))
+    assert sorted(models) == sorted(float(x) for x in lams.split(","))
+
+
+def test_a9a_logistic_libsvm_quality(tmp_path):
+    """a9a (the reference's LOGISTIC fixture: 32,561 rows, 123 features + intercept = 124) as LibSVM: L2
+    logistic regression validated on a9a.t reaches the usual a9a quality (AUC ~0.90)."""
+    args = ["--training-data-directory", f"{REF}/a9a", "--validating-data-directory", f"{REF}/a9a.t",
+            "--output-directory", str(tmp_path / "o"), "--task", "LOGISTIC_REGRESSION", "--input-file-format",
+            "LIBSVM", "--feature-dimension", "123", "--regularization-weights", "1", "--num-iterations", "100",
+            "--device", "cpu"]
+    d = drv.Driver(drv.build_parser().parse_args(args)).run()
+    assert d.train_data.n_features == 124 and d.train_data.n_rows == 32561
+    model = drv.read_text_model(str(tmp_path / "o" / drv.BEST_MODEL_TEXT))[1.0]
+    assert len(model) >= 100
+    met = d.per_model_metrics[1.0]
+    auc = [v for k, v in met.items() if "ROC" in str(k).upper()][0]
+    assert auc > 0.89, met
