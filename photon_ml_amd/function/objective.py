@@ -77,6 +77,30 @@ class GLMObjective:
             return None
         return MarginLineSearch(self, data, x0, d)
 
+    # ---- TRON trial point from margins (see DeviceGLMData.step_begin) ----------------------------------------
+    def step_begin(self, data, w: torch.Tensor) -> bool:
+        """Start tracking the margins of a step from ``w``; False when the backend cannot."""
+        if not hasattr(data, "step_begin"):
+            return False
+        w_eff, shift = self.normalization.effective(w)
+        return bool(data.step_begin(w_eff, shift))
+
+    def step_add(self, data, alpha: float):
+        """The step grew by ``alpha`` times the direction of the last :meth:`hessian_vector` call."""
+        data.step_add(alpha)
+
+    def calculate_step(self, data, w_new: torch.Tensor) -> Tuple[float, torch.Tensor]:
+        """:meth:`calculate` at ``w_new`` = w + (tracked step), from margins: no forward pass."""
+        self.n_value_grad += 1
+        norm = self.normalization
+        w_eff, shift = norm.effective(w_new)
+        f, s, g = data.ls_finish_sums(self.loss, 1.0, w_eff, shift, norm.shifts is not None)
+        grad = norm.finalize_vector(g, s)
+        if self.l2_weight > 0:
+            f += self.l2_value(w_new)
+            grad = grad + self.l2_weight * w_new
+        return f, grad
+
     def value(self, data, w: torch.Tensor) -> float:
         return self.calculate(data, w)[0]
 

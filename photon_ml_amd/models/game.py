@@ -24,9 +24,33 @@ from .glm import Coefficients, GeneralizedLinearModel, model_for_task
 
 
 def _csr_to_torch(x: sp.csr_matrix, device):
-    coo = x.tocoo()
-    return (torch.from_numpy(coo.row.astype(np.int64)).to(device), torch.from_numpy(coo.col.astype(np.int64)).to(device),
-            torch.from_numpy(coo.data.astype(np.float64)).to(device))
+    """(row, col, val, indptr) device tensors of a CSR shard, cached ON the matrix object per device: validation
+    data is scored after every coordinate update (``CoordinateDescent._score_validation``), and re-uploading
+    24 B/nnz each time would dominate scoring a large validation set."""
+    dev = torch.device(device)
+    cache = getattr(x, "_pml_dev_cache", None)
+    if cache is None:
+        cache = {}
+        try:
+            x._pml_dev_cache = cache
+        except AttributeError:  # pragma: no cover - exotic sparse subclasses
+            pass
+    key = str(dev)
+    if key not in cache:
+        x = x.tocsr()
+        indptr = np.asarray(x.indptr, dtype=np.int64)
+        row = np.repeat(np.arange(x.shape[0], dtype=np.int64), np.diff(indptr))
+        cache[key] = (torch.from_numpy(row).to(dev), torch.from_numpy(x.indices.astype(np.int64)).to(dev),
+                      torch.from_numpy(x.data.astype(np.float64)).to(dev), torch.from_numpy(indptr).to(dev))
+    return cache[key]
+
+
+def _row_sums(contrib: torch.Tensor, row: torch.Tensor, indptr: torch.Tensor, n: int) -> torch.Tensor:
+    """Per-row sums of CSR-ordered per-entry values, fp64. On the GPU a segmented reduction over the CSR row
+    pointer (deterministic: no atomics, unlike ``index_add_``)."""
+    if contrib.is_cuda and contrib.numel() > 0:
+        return torch.segment_reduce(contrib, "sum", offsets=indptr, unsafe=True)
+    return torch.zeros(n, dtype=torch.float64, device=contrib.device).index_add_(0, row, contrib)
 
 
 class FixedEffectModel:
@@ -40,10 +64,15 @@ class FixedEffectModel:
 
     def score(self, data, device="cpu") -> torch.Tensor:
         x = data.shard(self.feature_shard_id)
-        w = self.glm.coefficients.means.cpu().numpy()
-        if x.shape[1] != len(w):
-            raise ValueError(f"shard {self.feature_shard_id} dim {x.shape[1]} != model dim {len(w)}")
-        return torch.from_numpy(np.asarray(x @ w).reshape(-1)).to(device)
+        means = self.glm.coefficients.means
+        if x.shape[1] != means.numel():
+            raise ValueError(f"shard {self.feature_shard_id} dim {x.shape[1]} != model dim {means.numel()}")
+        dev = torch.device(device)
+        if dev.type == "cpu":
+            w = means.cpu().numpy()
+            return torch.from_numpy(np.asarray(x @ w).reshape(-1))
+        row, col, val, indptr = _csr_to_torch(x, dev)
+        return _row_sums(val * means.to(dev, torch.float64)[col], row, indptr, x.shape[0])
 
     def __repr__(self):
         return f"FixedEffectModel(shard={self.feature_shard_id}, dim={self.glm.coefficients.dim})"
@@ -165,7 +194,7 @@ class RandomEffectModel:
         if mask is not None:
             ent = np.where(mask, ent, -1)
         dev = torch.device(device)
-        row, col, val = _csr_to_torch(x, dev)
+        row, col, val, indptr = _csr_to_torch(x, dev)
         ent_t = torch.from_numpy(ent).to(dev)
         e = ent_t[row]
         keys, vals = self.tensors(dev)
@@ -176,7 +205,9 @@ class RandomEffectModel:
         pos = torch.searchsorted(keys, k).clamp(max=keys.numel() - 1)
         hit = (keys[pos] == k) & (e >= 0)
         contrib = torch.where(hit, val * vals[pos], torch.zeros_like(val))
-        return out.index_add_(0, row, contrib)
+        if dev.type == "cpu":
+            return out.index_add_(0, row, contrib)
+        return _row_sums(contrib, row, indptr, n)
 
     def __repr__(self):
         return (f"RandomEffectModel(type={self.random_effect_type}, shard={self.feature_shard_id}, "

@@ -342,7 +342,7 @@ struct FwdArgs {
   const RT* y; const RT* off; const RT* wt;
   XT* coef;           // VALUE_GRAD: wt*l'; HV: e_i; DZZ: wt*l''
   XT* dzz;            // VALUE_GRAD with cache: wt*l''; HV: input D_i
-  double* z_out;      // MARGIN: z (double)
+  double* z_out;      // MARGIN: z (double); VALUE_GRAD: margin cache; HV: direction margins (optional)
   int with_offset;    // MARGIN: add offset
   int abl;            // ablation bits (profiling only): 1 = gather from a 1 KB window, 2 = skip segmented reduce
   int hot_n;          // entries of x staged in LDS (features relabelled hottest-first), 0 = none
@@ -387,8 +387,10 @@ __device__ __forceinline__ void fwd_finish(const FwdArgs<XT, RT>& a, int s, doub
     return;
   }
   if (a.mode == FWD_HV) {
-    const double e = static_cast<double>(r.d) * (sum - a.shift);
+    const double u = sum - a.shift;                   // margin change along the direction (X v_eff - v_eff.s)
+    const double e = static_cast<double>(r.d) * u;
     a.coef[s] = static_cast<XT>(e);
+    if (a.z_out) a.z_out[s] = u;                      // TRON: step margins accumulate sum_i alpha_i u_i
     S += e;
     return;
   }

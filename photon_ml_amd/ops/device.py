@@ -315,6 +315,7 @@ class DeviceGLMData(GLMComputable):
     def set_offsets(self, offsets):
         self.o.copy_(torch.as_tensor(offsets, device=self.device).to(self.vdt))
         self._z_key = None
+        self._step_base = None
 
     # ---- margin-space line search (GLMObjective.margin_line_search / LBFGS): z(t) = z0 + t zd ----------------
     # State: the margins of the last accepted point are z0 + tpend * zd (the accepted step is materialised
@@ -388,6 +389,7 @@ class DeviceGLMData(GLMComputable):
                 self._ls(loss, t, 1, out[self.dim:])
             self._tpend = float(t)
             self._ls_t0 = None
+            self._track_u = False
             self._z_key, self._z_chain = (w_eff.detach().clone(), float(shift)), self._z_chain + 1
             if self.track_hessian and loss.twice_differentiable:
                 self._dzz_key, self._dzz_shift = w_eff.detach().clone(), float(shift)
@@ -405,6 +407,45 @@ class DeviceGLMData(GLMComputable):
         out = self.ls_finish_packed(loss, t, w_eff, shift, need_s)
         f, s_ = out[self.dim:].tolist()
         return f, s_, out[: self.dim]
+
+    # ---- TRON trial point in margin space: margins(w + s) = z0 + sum_i alpha_i u_i ------------------------------
+    def step_begin(self, w_eff, shift) -> bool:
+        """Start a TRON step at ``w``: z0 <- margins at w (normally already cached by the last evaluation; after a
+        rejected trial the base margins are still in z0), zd <- 0, and from now on every Hessian-vector pass also
+        stores its direction margins u = X d_eff - d_eff.s (8 B/row, ``FwdArgs.z_out`` in FWD_HV mode) so that
+        :meth:`step_add` can accumulate the step's margins. The trial point is then evaluated by
+        ``ls_finish_packed(t=1)``: one elementwise pass + the transpose pass, no forward pass."""
+        if getattr(self, "z_cache", None) is None:
+            self.enable_margin_cache()
+        n = max(self.n_rows, 1)
+        if not self._z_valid_for(w_eff, shift):
+            base = getattr(self, "_step_base", None)
+            if (base is not None and base[0] is not None and base[0][1] == float(shift)
+                    and base[0][0].shape == w_eff.shape and base[1] < self.LS_REFRESH
+                    and bool(torch.equal(base[0][0], w_eff.to(base[0][0].device, base[0][0].dtype)))):
+                self._z_key, self._z_chain = base     # rejected trial: z0 still holds the margins at w
+            else:
+                self.fwd_all(self._vec(w_eff), FWD_MARGIN, 0, shift, None, None, z_out=self.z_cache, with_offset=1,
+                             stats=False)
+                self._z_key, self._z_chain = (w_eff.detach().clone(), float(shift)), 0
+            self._tpend = 0.0
+        if self._tpend:
+            self.z_cache.add_(self.zd, alpha=self._tpend)   # materialise the accepted step
+            self._tpend = 0.0
+        self.zd.zero_()
+        self._ls_t0 = None
+        if getattr(self, "u_dir", None) is None:
+            self.u_dir = torch.zeros(n, dtype=torch.float64, device=self.device)
+        self._track_u = True
+        self._step_base = (self._z_key, self._z_chain)
+        return True
+
+    def step_add(self, alpha: float):
+        """zd += alpha * (direction margins of the last Hessian-vector pass)."""
+        self.zd.add_(self.u_dir, alpha=float(alpha))
+
+    def _u_out(self):
+        return self.u_dir if getattr(self, "_track_u", False) else None
 
     def set_weights(self, weights):
         self.wt.copy_(torch.as_tensor(weights, device=self.device).to(self.vdt))
@@ -578,7 +619,7 @@ class DeviceGLMData(GLMComputable):
             self._ensure_dzz(loss, w_eff, margin_shift)
             out = torch.zeros(self.dim + 2, dtype=torch.float64, device=self.device)
             x = self._vec(v_eff)
-            self.fwd_all(x, FWD_HV, loss.loss_id, v_shift, self.coef, self.dzz)
+            self.fwd_all(x, FWD_HV, loss.loss_id, v_shift, self.coef, self.dzz, z_out=self._u_out())
             out[self.dim:] = self._reduce_stats()
             start_reduce(out[self.dim:])
             self._packed_bucketed(self.coef, out[: self.dim], start_reduce, nb)
@@ -664,7 +705,7 @@ class DeviceGLMData(GLMComputable):
         out = torch.zeros(self.dim + 2, dtype=torch.float64, device=self.device)
         H = out[: self.dim]
         x = self._vec(v_eff)
-        self.fwd_all(x, FWD_HV, loss.loss_id, v_shift, self.coef, self.dzz)
+        self.fwd_all(x, FWD_HV, loss.loss_id, v_shift, self.coef, self.dzz, z_out=self._u_out())
         self.t_all(self.coef, H)
         out[self.dim:] = self._reduce_stats()
         if self.old_of_new is not None:

@@ -115,7 +115,10 @@ class TorchGLMData(GLMComputable):
 
     def hv_sums(self, loss, w_eff, margin_shift, v_eff, v_shift):
         z = self._xv(w_eff) + margin_shift + self.o
-        e = self.wt * loss.dzz(z, self.y) * (self._xv(v_eff) - v_shift)
+        u = self._xv(v_eff) - v_shift
+        if getattr(self, "_track_u", False):
+            self._u = u
+        e = self.wt * loss.dzz(z, self.y) * u
         return self._xtv(e), float(torch.sum(e))
 
     def hdiag_sums(self, loss, w):
@@ -141,10 +144,21 @@ class TorchGLMData(GLMComputable):
         return float(torch.sum(self.wt * l)), float(torch.sum(self.wt * dl * self._zd))
 
     def ls_finish_sums(self, loss, t: float, w_eff, shift, need_s: bool = True):
+        self._track_u = False
         z = self._z0 + t * self._zd
         l, dl = loss.loss_and_dz(z, self.y)
         r = self.wt * dl
         return float(torch.sum(self.wt * l)), float(torch.sum(r)), self._xtv(r)
+
+    # TRON trial in margin space (see DeviceGLMData.step_begin): fp64 reference
+    def step_begin(self, w_eff, shift) -> bool:
+        self._z0 = self.margins(w_eff, shift, True)
+        self._zd = torch.zeros_like(self._z0)
+        self._track_u = True
+        return True
+
+    def step_add(self, alpha: float):
+        self._zd = self._zd + float(alpha) * self._u
 
     def set_offsets(self, offsets):
         self.o = torch.as_tensor(offsets, dtype=torch.float64).to(self.device)

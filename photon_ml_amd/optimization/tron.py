@@ -13,6 +13,7 @@ from __future__ import annotations
 
 import logging
 import math
+import os
 
 import torch
 
@@ -23,6 +24,9 @@ DEFAULT_MAX_NUM_FAILURE = 5
 DEFAULT_TOLERANCE = 1.0e-5
 DEFAULT_MAX_ITER = 15
 MAX_CG_ITERATIONS = 20
+# Evaluate each trial point w + s from margins accumulated during CG (GLMObjective.step_begin) instead of a full
+# forward pass; the data backend must support it (device / torch reference backends), otherwise ignored.
+MARGIN_TRIAL = os.environ.get("PML_TRON_MARGIN_TRIAL", "1") != "0"
 
 log = logging.getLogger(__name__)
 
@@ -37,6 +41,7 @@ class TRON(Optimizer):
                  constraints=None, track_state: bool = True):
         super().__init__(tolerance, max_iterations, normalization, constraints, track_state)
         self.max_num_failures = max_num_failures
+        self.margin_trial = MARGIN_TRIAL
         self.delta = float("inf")
         self.total_cg_iterations = 0
 
@@ -55,7 +60,9 @@ class TRON(Optimizer):
         self.delta, self.total_cg_iterations = d["delta"], d["total_cg_iterations"]
 
     @staticmethod
-    def truncated_cg(objective, data, w, gradient, delta):
+    def truncated_cg(objective, data, w, gradient, delta, track=None):
+        """``track(alpha)``: called after each step update ``step += alpha * direction`` (net alpha on the trust
+        region boundary) right after the Hessian-vector product of that direction (margin-space trial)."""
         step = torch.zeros_like(gradient)
         residual = -gradient
         direction = residual.clone()
@@ -81,8 +88,12 @@ class TRON(Optimizer):
                 else:
                     alpha = (rad - std) / dtd
                 step = step + alpha * direction
+                if track is not None:
+                    track(alpha)          # step = previous step + alpha * direction
                 residual = residual - alpha * hd
                 break
+            if track is not None:
+                track(alpha)
             residual = residual - alpha * hd
             rnew = _dot(residual, residual)
             beta = rnew / rtr
@@ -96,12 +107,17 @@ class TRON(Optimizer):
         first = state.iter == 0
         failures = 0
         while failures < self.max_num_failures:
-            cg_iter, step, residual = self.truncated_cg(objective, data, w, g_prev, self.delta)
+            margins = self.margin_trial and hasattr(objective, "step_begin") and objective.step_begin(data, w)
+            track = (lambda a: objective.step_add(data, a)) if margins else None
+            cg_iter, step, residual = self.truncated_cg(objective, data, w, g_prev, self.delta, track)
             self.total_cg_iterations += cg_iter
             w_new = w + step
             gs = _dot(g_prev, step)
             predicted = -0.5 * (gs - _dot(step, residual))
-            f_new, g_new = objective.calculate(data, w_new)
+            if margins:   # margins(w + step) = z(w) + sum alpha_i X d_i: elementwise loss + transpose pass only
+                f_new, g_new = objective.calculate_step(data, w_new)
+            else:
+                f_new, g_new = objective.calculate(data, w_new)
             actual = f_prev - f_new
             step_norm = _norm(step)
             if first:

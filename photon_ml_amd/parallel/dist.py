@@ -173,6 +173,14 @@ class DistributedGLMData:
         ok = bool(getattr(self.local, "ls_begin", lambda *a, **k: False)(w0_eff, shift0, d_eff, d_shift, t0, loss))
         return all_reduce_scalar(1.0 if ok else 0.0, "min", device=self._scalar_device(), group=self.group) > 0
 
+    def step_begin(self, w_eff, shift) -> bool:
+        """TRON margin-space trial (DeviceGLMData.step_begin) on every rank, or on none."""
+        ok = bool(getattr(self.local, "step_begin", lambda *a: False)(w_eff, shift))
+        return all_reduce_scalar(1.0 if ok else 0.0, "min", device=self._scalar_device(), group=self.group) > 0
+
+    def step_add(self, alpha: float):
+        self.local.step_add(alpha)
+
     def _scalar_device(self):
         return self.local.device if dist.get_backend(self.group) == "nccl" else None
 

@@ -66,3 +66,19 @@ def test_segmented_random_effect_on_gpu_matches_cpu_dense(opt):
                                    rtol=1e-5, atol=1e-6)
     sa, sb = cpu.score(a).cpu(), gpu.score(b).cpu()
     assert torch.allclose(sa, sb, atol=1e-5)
+
+
+def test_game_model_scoring_on_device_matches_host():
+    """FE / RE scoring on the device (cached CSR upload + segmented row reduction) == host scipy / torch, and
+    repeated scoring of the same dataset reuses the device copy."""
+    data, _ = generate_game_data(n_rows=3000, n_users=30, n_items=20, seed=24, task="LOGISTIC_REGRESSION")
+    res = _fit("cpu", "LOGISTIC_REGRESSION", data, opt="TRON")
+    model = res.model
+    host = model.score(data, "cpu")
+    dev1 = model.score(data, "cuda")
+    dev2 = model.score(data, "cuda")
+    assert dev1.is_cuda
+    torch.testing.assert_close(dev1.cpu(), host, rtol=1e-12, atol=1e-12)
+    assert torch.equal(dev1, dev2)
+    x = data.shard(model.get("global").feature_shard_id)
+    assert "cuda:0" in x._pml_dev_cache or "cuda" in x._pml_dev_cache

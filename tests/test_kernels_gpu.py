@@ -383,6 +383,38 @@ def test_margin_space_line_search_on_device(precision, monkeypatch):
 
 
 @pytest.mark.gpu
+@pytest.mark.parametrize("precision,layout,norm", [("f64", "tiled", None), ("bf16", "tiled", None),
+                                                   ("f64", "segmented", None), ("f64", "tiled", "STANDARDIZATION")])
+def test_tron_margin_space_trial_on_device(precision, layout, norm):
+    """TRON trial points from margins accumulated in the FWD_HV epilogue (z_out = direction margins) + ls_eval
+    final mode + transpose only, vs a forward+transpose evaluation of every trial: same iterates, fewer passes."""
+    from photon_ml_amd.data.synthetic import generate_glm_data
+    from photon_ml_amd.function.losses import LOGISTIC
+    from photon_ml_amd.function.objective import GLMObjective
+    from photon_ml_amd.normalization.context import NormalizationContext
+    from photon_ml_amd.ops.device import DeviceGLMData
+    from photon_ml_amd.optimization import TRON
+    from photon_ml_amd.stat.summary import BasicStatisticalSummary
+    data, _ = generate_glm_data("LOGISTIC_REGRESSION", 20000, 300, density=0.05, seed=10)
+    nc = (NormalizationContext.build(norm, BasicStatisticalSummary.compute(data.x), data.n_features - 1).to("cuda")
+          if norm else None)
+    out = {}
+    for mode in (False, True):
+        dev = DeviceGLMData.from_labeled(data, "cuda", precision, chunk_rows=8192, layout=layout)
+        dev.track_hessian = True
+        obj = GLMObjective(LOGISTIC, 1.0, nc)
+        opt = TRON(tolerance=1e-12, max_iterations=10)
+        opt.margin_trial = mode
+        w, f = opt.optimize(obj, dev, torch.zeros(300, dtype=torch.float64, device="cuda"))
+        out[mode] = (w, f, dev.n_passes, opt.current.iter, opt.total_cg_iterations)
+    (w0, f0, p0, i0, c0), (w1, f1, p1, i1, c1) = out[False], out[True]
+    tol = 1e-9 if precision == "f64" else 1e-5
+    assert torch.allclose(w0, w1, rtol=tol, atol=tol) and abs(f0 - f1) <= tol * abs(f0)
+    if precision == "f64":   # bf16 data: fp32 coefficient rounding differs (X fp32(w + s) vs z + sum alpha X fp32(d)),
+        assert (i0, c0) == (i1, c1)  # which can flip the stopping iteration at tolerance 1e-12
+
+
+@pytest.mark.gpu
 def test_gather_dedup_variant_is_bitwise_equal():
     """Lane-run gather dedup (only run heads load, value broadcast by shuffles) changes no bits."""
     from photon_ml_amd.data.synthetic import generate_device_shard

@@ -135,3 +135,28 @@ def test_margin_space_line_search_matches_full_evaluations(task, norm, monkeypat
     assert i0 == i1
     assert torch.allclose(w0, w1, rtol=1e-8, atol=1e-10) and abs(f0 - f1) <= 1e-10 * abs(f0)
     assert n1 <= n0  # full (forward + transpose) evaluations: only initial state + one per accepted step
+
+
+@pytest.mark.parametrize("norm", [None, "STANDARDIZATION"])
+@pytest.mark.parametrize("task", ["LOGISTIC_REGRESSION", "POISSON_REGRESSION", "LINEAR_REGRESSION"])
+def test_tron_margin_space_trial_matches_full_evaluations(task, norm):
+    """TRON with each trial point w + s evaluated from margins accumulated during CG (z(w) + sum alpha_i X d_i,
+    normalization shifts included) follows the same iterates as evaluating the full objective at w + s."""
+    from photon_ml_amd.data.synthetic import generate_glm_data
+    from photon_ml_amd.function.losses import loss_for_task
+    from photon_ml_amd.normalization.context import NormalizationContext
+    from photon_ml_amd.stat.summary import BasicStatisticalSummary
+    data, _ = generate_glm_data(task, 2000, 25, density=0.3, seed=5)
+    nc = NormalizationContext.build(norm, BasicStatisticalSummary.compute(data.x), data.n_features - 1) if norm \
+        else None
+    gd = TorchGLMData(data, "cpu")
+    out = {}
+    for mode in (False, True):
+        obj = GLMObjective(loss_for_task(task), 0.5, nc)
+        opt = TRON(tolerance=1e-12, max_iterations=15)
+        opt.margin_trial = mode
+        w, f = opt.optimize(obj, gd, torch.zeros(25, dtype=torch.float64))
+        out[mode] = (w, f, opt.current.iter, opt.total_cg_iterations)
+    (w0, f0, i0, c0), (w1, f1, i1, c1) = out[False], out[True]
+    assert (i0, c0) == (i1, c1)
+    assert torch.allclose(w0, w1, rtol=1e-8, atol=1e-10) and abs(f0 - f1) <= 1e-10 * abs(f0)
