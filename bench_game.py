@@ -116,6 +116,9 @@ def main():
     barrier()
     t1 = time.perf_counter()
     model, _ = cd.run(args.steps, model)
+    for _, m in model:       # the trained model's coefficients are part of the timed work (row-space RE: lazy)
+        if hasattr(m, "materialize"):
+            m.materialize()
     if torch.cuda.is_available():
         torch.cuda.synchronize()
     barrier()

@@ -157,6 +157,9 @@ class FixedEffectCoordinate(Coordinate):
         return self.problem.regularization_term_value(model.glm)
 
 
+_RS_WARM = object()   # warm-start marker: the last segmented solve kept only row-space coordinates
+
+
 class RandomEffectCoordinate(Coordinate):
     """Per-entity GLMs solved in size buckets on the device (K7)."""
 
@@ -263,7 +266,9 @@ class RandomEffectCoordinate(Coordinate):
         seg = ds.seg
         seg.o = offs.to(seg.y.device, torch.float64)[ds.seg_rows]
         seg._dzz_key = None
-        W0 = self._warm_start_segmented(model)
+        # previous update kept only beta (lazy primal model): the row-space solve warm-starts from it directly
+        prev_lazy = self._W.get("seg") is _RS_WARM
+        W0 = None if prev_lazy else self._warm_start_segmented(model)
         t_start = time.time()
         oc = cfg.optimizer_config
         with Timed(f"RE {self.coordinate_id}: row-space setup", log, logging.DEBUG):
@@ -275,13 +280,17 @@ class RandomEffectCoordinate(Coordinate):
             with Timed(f"RE {self.coordinate_id}: row-space solve", log, logging.DEBUG):
                 rres = rs.solve(self.loss, l2, opt, W0, oc.tolerance, oc.maximum_iterations,
                                 reuse_beta=self._W.get("seg") is not None)
-                _sync(W0)
+                _sync(rres.W)
             frozen = rs.mask
             n_e = seg.row_ptr[1:] - seg.row_ptr[:-1]
             all_rs = bool((frozen | (n_e == 0)).all())   # nothing left for the primal path
             if not all_rs:
+                if W0 is None:
+                    W0 = self._lazy_W()
                 W0 = torch.where(seg.bexp(frozen), torch.zeros_like(W0), W0)
         if frozen is None or not all_rs:
+            if W0 is None:
+                W0 = self._lazy_W()
             with Timed(f"RE {self.coordinate_id}: primal block-diagonal solve", log, logging.DEBUG):
                 if oc.optimizer_type == OptimizerType.TRON:
                     res = batched_tron(seg, self.loss, l2, W0, oc.tolerance, oc.maximum_iterations, frozen=frozen)
@@ -291,9 +300,28 @@ class RandomEffectCoordinate(Coordinate):
                 W_all, iters, reasons = res.W, res.iters, res.reason
         else:
             W_all = None
-            iters = torch.zeros(seg.B, dtype=torch.long, device=W0.device)
-            reasons = torch.zeros(seg.B, dtype=torch.long, device=W0.device)
+            iters = torch.zeros(seg.B, dtype=torch.long, device=seg.y.device)
+            reasons = torch.zeros(seg.B, dtype=torch.long, device=seg.y.device)
         self._rs_scores = None
+        need_var = self.compute_variance and self.loss.twice_differentiable
+        if (frozen is not None and all_rs and not need_var and not len(self.dataset.passive_rows)
+                and os.environ.get("PML_RE_LAZY_PRIMAL", "1") != "0"):
+            # every entity solved in its row space: scores are L beta, ||w||^2 = ||beta||^2, and the primal
+            # coefficients w = X^T L^-T beta (one transpose pass over the block-diagonal data) are produced only
+            # when the model is read
+            beta = rres.W
+            self._rs_scores = rs.margins(beta)
+            self._lazy_W = lambda: rs.to_primal(beta)
+            self._W["seg"] = _RS_WARM
+            n_iter = torch.zeros(seg.B, dtype=torch.long, device=beta.device).index_copy(0, rs.ents, rres.iters)
+            n_reason = torch.zeros(seg.B, dtype=torch.long, device=beta.device).index_copy(0, rs.ents, rres.reason)
+            act = torch.from_numpy(ds.n_active > 0).to(n_iter.device)
+            self.last_stats = random_effect_tracker_stats(n_iter[act], n_reason[act], time.time() - t_start)
+            sum_sq = float(torch.linalg.vector_norm(torch.where(rs.valid, beta, torch.zeros_like(beta)))) ** 2
+            out = RandomEffectModel(self.data_config.random_effect_type, self.data_config.feature_shard_id, self.task,
+                                    ds.entity_ids, ds.dim, ds.projection_keys_t, self._lazy_W, None, sum_sq=sum_sq)
+            self._last = (out, None)
+            return out
         if frozen is not None:
             with Timed(f"RE {self.coordinate_id}: row-space -> primal", log, logging.DEBUG):
                 Wp = rs.to_primal(rres.W)
@@ -391,8 +419,9 @@ class RandomEffectCoordinate(Coordinate):
 
     def regularization_term_value(self, model: RandomEffectModel) -> float:
         reg, lam = self.opt_config.regularization_context, self.opt_config.regularization_weight
-        a, q = model.sum_abs_and_sq()
-        return reg.l1_weight(lam) * a + 0.5 * reg.l2_weight(lam) * q
+        l1w = reg.l1_weight(lam)
+        a, q = model.sum_abs_and_sq(need_abs=l1w != 0)
+        return (l1w * a if l1w != 0 else 0.0) + 0.5 * reg.l2_weight(lam) * q
 
 
 class ShardedRandomEffectCoordinate(Coordinate):

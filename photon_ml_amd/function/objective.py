@@ -143,12 +143,12 @@ class MarginLineSearch:
     """
 
     def __init__(self, obj: GLMObjective, data, x0: torch.Tensor, d: torch.Tensor):
-        from ..optimization.vector_space import vdot
+        from ..optimization.vector_space import vdots
         self.obj, self.data, self.x0, self.d = obj, data, x0, d
         l2 = obj.l2_weight
         self.l2 = l2
         if l2 > 0:
-            self.a, self.b, self.c = vdot(x0, x0), vdot(x0, d), vdot(d, d)
+            self.a, self.b, self.c = vdots([(x0, x0), (x0, d), (d, d)])
 
     def eval(self, t: float):
         f, dd = self.data.ls_eval(self.obj.loss, t)

@@ -88,7 +88,12 @@ class RandomEffectModel:
     """
 
     def __init__(self, random_effect_type: str, feature_shard_id: str, task: TaskType, entity_ids: np.ndarray,
-                 dim: int, keys, values, variances=None):
+                 dim: int, keys, values, variances=None, sum_sq: Optional[float] = None):
+        """``values`` may be a zero-argument callable producing the device values on first use (with device
+        ``keys``): the row-space random-effect solve returns its primal coefficients lazily, because inside
+        coordinate descent only the scores (L beta) and ||w||^2 = ||beta||^2 (``sum_sq``) are needed — the
+        transpose pass that builds w runs only when the model itself is read (validation scoring, save, warm
+        start of another coordinate)."""
         self.random_effect_type = random_effect_type
         self.feature_shard_id = feature_shard_id
         self._task = TaskType.parse(task)
@@ -96,9 +101,14 @@ class RandomEffectModel:
         self.dim = int(dim)
         self._host = None
         self._dev = None
+        self._lazy = None
+        self._sum_sq = sum_sq
         if isinstance(keys, torch.Tensor):
             # solver output: keys already sorted (entity-major projection order)
-            self._dev = (keys.to(torch.int64), values.to(torch.float64),
+            if callable(values):
+                self._lazy = values
+                values = None
+            self._dev = (keys.to(torch.int64), None if values is None else values.to(torch.float64),
                          None if variances is None else variances.to(torch.float64))
             return
         keys = np.asarray(keys, dtype=np.int64)
@@ -110,9 +120,25 @@ class RandomEffectModel:
                 variances = np.asarray(variances)[order]
         self._host = (keys, values, None if variances is None else np.asarray(variances, dtype=np.float64))
 
+    def _d(self):
+        if self._lazy is not None:
+            k, _, var = self._dev
+            self._dev = (k, self._lazy().to(torch.float64), var)
+            self._lazy = None
+        return self._dev
+
+    def materialize(self) -> "RandomEffectModel":
+        """Produce lazily deferred coefficients now (on the device)."""
+        self._d()
+        return self
+
+    @property
+    def materialized(self) -> bool:
+        return self._lazy is None
+
     def _h(self):
         if self._host is None:
-            k, v, var = self._dev
+            k, v, var = self._d()
             self._host = (k.cpu().numpy(), v.cpu().numpy(), None if var is None else var.cpu().numpy())
         return self._host
 
@@ -138,13 +164,17 @@ class RandomEffectModel:
         """(keys, values) as torch tensors on ``device`` (no host copy when already resident there)."""
         dev = torch.device(device)
         if self._dev is not None:
-            return self._dev[0].to(dev), self._dev[1].to(dev)
+            k, v, _ = self._d()
+            return k.to(dev), v.to(dev)
         return torch.from_numpy(self._host[0]).to(dev), torch.from_numpy(self._host[1]).to(dev)
 
-    def sum_abs_and_sq(self):
-        """(sum |w|, sum w^2) over all coefficients (regularization term value), computed where they live."""
+    def sum_abs_and_sq(self, need_abs: bool = True):
+        """(sum |w|, sum w^2) over all coefficients (regularization term value), computed where they live.
+        ``need_abs=False`` on a lazy model returns (nan, ||beta||^2) without materialising it."""
+        if self._lazy is not None and not need_abs and self._sum_sq is not None:
+            return float("nan"), float(self._sum_sq)
         if self._dev is not None:
-            v = self._dev[1]   # reductions without model-sized temporaries (1.25e9 coefficients at config 5)
+            v = self._d()[1]   # reductions without model-sized temporaries (1.25e9 coefficients at config 5)
             return float(torch.linalg.vector_norm(v, 1)), float(torch.linalg.vector_norm(v, 2)) ** 2
         v = self._host[1]
         return float(np.abs(v).sum()), float((v * v).sum())

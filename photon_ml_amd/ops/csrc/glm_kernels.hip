@@ -1705,6 +1705,56 @@ __global__ __launch_bounds__(NTHREADS) void ls_eval_kernel(int n, double t, int 
   if (threadIdx.x == 0) { stats[2 * blockIdx.x] = F; stats[2 * blockIdx.x + 1] = D; }
 }
 
+
+// ------------------------------------------------------------------------------------------------------------
+// Gram matrix of a few (k <= 22) long fp64 vectors and their linear combination: the vector-free L-BFGS two-loop
+// (optimization/lbfgs.py _History._apply_inverse_gram). One pass over the k vectors each: a tile of 256 elements
+// of every vector is staged in LDS (rows padded to 257 doubles: distinct rows land in distinct banks), then
+// thread p < k(k+1)/2 owns pair (a, b) and accumulates sum_e tile[a][e] tile[b][e] in fp64; per-workgroup
+// partials [grid, npairs] are summed on the host side (deterministic). The pointers travel by value in the
+// kernel arguments (no pointer-table upload).
+#define GRAM_MAXK 22
+#define GRAM_TILE 256
+struct VecSet { const double* p[GRAM_MAXK]; double c[GRAM_MAXK]; };
+
+__global__ __launch_bounds__(GRAM_TILE) void gram_kernel(VecSet vs, int k, long long n, double* __restrict__ partial) {
+  __shared__ double sm[GRAM_MAXK][GRAM_TILE + 1];
+  const int tid = threadIdx.x;
+  const int np = k * (k + 1) / 2;
+  int pa = 0, pb = 0;
+  if (tid < np) {
+    int p = tid, a = 0;
+    while (p >= k - a) { p -= k - a; ++a; }
+    pa = a; pb = a + p;
+  }
+  double acc = 0.0;
+  const long long ntiles = (n + GRAM_TILE - 1) / GRAM_TILE;
+  for (long long t = blockIdx.x; t < ntiles; t += gridDim.x) {
+    const long long i = t * GRAM_TILE + tid;
+    for (int j = 0; j < k; ++j) sm[j][tid] = i < n ? __builtin_nontemporal_load(vs.p[j] + i) : 0.0;
+    __syncthreads();
+    if (tid < np) {
+      double s0 = 0.0, s1 = 0.0;
+#pragma unroll 8
+      for (int e = 0; e < GRAM_TILE; e += 2) {
+        s0 = fma(sm[pa][e], sm[pb][e], s0);
+        s1 = fma(sm[pa][e + 1], sm[pb][e + 1], s1);
+      }
+      acc += s0 + s1;
+    }
+    __syncthreads();
+  }
+  if (tid < np) partial[(long long)blockIdx.x * np + tid] = acc;
+}
+
+__global__ __launch_bounds__(256) void lincomb_kernel(VecSet vs, int k, long long n, double* __restrict__ out) {
+  for (long long i = (long long)blockIdx.x * 256 + threadIdx.x; i < n; i += (long long)gridDim.x * 256) {
+    double s = 0.0;
+    for (int j = 0; j < k; ++j) s = fma(vs.c[j], vs.p[j][i], s);
+    out[i] = s;
+  }
+}
+
 extern "C" {
 
 int pml_version() { return 1; }
@@ -1893,6 +1943,33 @@ int pml_seg_expand(const long long* ptr, int nseg, const void* src, void* out, i
                        (const unsigned char*)src, (unsigned char*)out);
   else
     return -22;
+  LAUNCH_CHECK();
+  return 0;
+}
+
+// Gram: partial [grid, k(k+1)/2] (grid = pml_gram_grid(n)); the caller sums over the grid.
+int pml_gram_grid(long long n) {
+  const long long t = (n + GRAM_TILE - 1) / GRAM_TILE;
+  return (int)std::max<long long>(1, std::min<long long>(t, 2048));
+}
+
+int pml_gram(const double* const* ptrs, int k, long long n, double* partial, void* stream) {
+  if (k < 1 || k > GRAM_MAXK || n < 0) return -22;
+  VecSet vs{};
+  for (int j = 0; j < k; ++j) vs.p[j] = ptrs[j];
+  hipLaunchKernelGGL(gram_kernel, dim3(pml_gram_grid(n)), dim3(GRAM_TILE), 0, (hipStream_t)stream, vs, k, n,
+                     partial);
+  LAUNCH_CHECK();
+  return 0;
+}
+
+int pml_lincomb(const double* const* ptrs, const double* coefs, int k, long long n, double* out, void* stream) {
+  if (k < 1 || k > GRAM_MAXK || n < 0) return -22;
+  if (n == 0) return 0;
+  VecSet vs{};
+  for (int j = 0; j < k; ++j) { vs.p[j] = ptrs[j]; vs.c[j] = coefs[j]; }
+  const long long blocks = std::min<long long>((n + 255) / 256, 4096);
+  hipLaunchKernelGGL(lincomb_kernel, dim3((unsigned)blocks), dim3(256), 0, (hipStream_t)stream, vs, k, n, out);
   LAUNCH_CHECK();
   return 0;
 }

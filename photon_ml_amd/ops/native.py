@@ -101,6 +101,9 @@ def glm_lib() -> Optional[ctypes.CDLL]:
         lib.pml_bgemv.argtypes = [c_int, c_int, c_void_p, c_void_p, c_void_p, c_int, c_void_p]
         lib.pml_bhv.argtypes = [c_int, c_int, c_void_p, c_void_p, c_void_p, c_double, c_void_p, c_void_p]
         lib.pml_set_ls_args.argtypes = [c_void_p, c_double, c_double]
+        lib.pml_gram_grid.argtypes = [ctypes.c_longlong]
+        lib.pml_gram.argtypes = [c_void_p, c_int, ctypes.c_longlong, c_void_p, c_void_p]
+        lib.pml_lincomb.argtypes = [c_void_p, c_void_p, c_int, ctypes.c_longlong, c_void_p, c_void_p]
         lib.pml_tl_set_dedup.argtypes = [c_int, c_int]
         lib.pml_ls_eval.argtypes = [c_int, c_int, c_double, c_int, c_void_p, c_void_p, c_void_p, c_void_p, c_int,
                                     c_void_p, c_void_p, c_void_p, c_void_p, c_void_p]
@@ -108,7 +111,8 @@ def glm_lib() -> Optional[ctypes.CDLL]:
                                                                       c_void_p]
         for f in ("pml_seg_fwd", "pml_seg_t", "pml_reduce_stats", "pml_build_blocks", "pml_tl_fwd", "pml_tl_t",
                   "pml_tl_maxbits", "pml_segdot", "pml_tl_fwd_multi", "pml_tl_t_multi", "pml_seg_cg_step",
-                  "pml_seg_expand", "pml_bgemv", "pml_bhv", "pml_rs_tron", "pml_ls_eval"):
+                  "pml_seg_expand", "pml_bgemv", "pml_bhv", "pml_rs_tron", "pml_ls_eval", "pml_gram_grid", "pml_gram",
+                  "pml_lincomb"):
             getattr(lib, f).restype = c_int
         lib.pml_set_config.argtypes = [c_int, c_int, c_int, c_int]
         lib._pml_typed = True
@@ -166,6 +170,46 @@ def segdot(a: torch.Tensor, b: Optional[torch.Tensor], ptr: torch.Tensor, mode: 
     out = torch.empty(nseg, dtype=torch.float64, device=a.device)
     check(lib.pml_segdot(a.data_ptr(), b.data_ptr(), mode, ptr.data_ptr(), nseg, out.data_ptr(),
                          stream_handle(a.device)), "segdot")
+    return out
+
+
+GRAM_MAXK = 22
+
+
+def _fast_vecs(vs) -> bool:
+    return (0 < len(vs) <= GRAM_MAXK and all(v.device.type == "cuda" and v.dtype == torch.float64
+                                             and v.dim() == 1 and v.is_contiguous() for v in vs)
+            and len({v.numel() for v in vs}) == 1 and len({v.device for v in vs}) == 1)
+
+
+def gram(vs) -> torch.Tensor:
+    """Device fp64 [k, k] matrix of all inner products of k <= 22 equal-length device vectors, ONE pass over
+    them (``gram_kernel``), or None when the inputs do not qualify."""
+    if not _fast_vecs(vs):
+        return None
+    lib = require_glm_lib()
+    k, n = len(vs), vs[0].numel()
+    ptrs = (ctypes.c_void_p * k)(*[v.data_ptr() for v in vs])
+    npairs = k * (k + 1) // 2
+    partial = torch.empty(lib.pml_gram_grid(n), npairs, dtype=torch.float64, device=vs[0].device)
+    check(lib.pml_gram(ptrs, k, n, partial.data_ptr(), stream_handle(vs[0].device)), "gram")
+    tri = partial.sum(0)
+    iu = torch.triu_indices(k, k, device=tri.device)
+    G = torch.zeros(k, k, dtype=torch.float64, device=tri.device)
+    G[iu[0], iu[1]] = tri
+    return G + G.triu(1).T
+
+
+def lincomb(coefs, vs):
+    """sum_j coefs[j] vs[j] in one pass (``lincomb_kernel``; host coefficients), or None when not applicable."""
+    if not _fast_vecs(vs):
+        return None
+    lib = require_glm_lib()
+    k, n = len(vs), vs[0].numel()
+    ptrs = (ctypes.c_void_p * k)(*[v.data_ptr() for v in vs])
+    cs = (ctypes.c_double * k)(*[float(c) for c in coefs])
+    out = torch.empty(n, dtype=torch.float64, device=vs[0].device)
+    check(lib.pml_lincomb(ptrs, cs, k, n, out.data_ptr(), stream_handle(vs[0].device)), "lincomb")
     return out
 
 

@@ -40,6 +40,10 @@ class LocalSpace:
     def abs_sum(self, a: torch.Tensor) -> float:
         return float(torch.sum(torch.abs(a)))
 
+    def dots(self, pairs) -> list:
+        """Several inner products with ONE host synchronisation."""
+        return torch.stack([torch.dot(a, b) for a, b in pairs]).to(torch.float64).tolist()
+
     def gram(self, vs: Sequence[torch.Tensor]) -> torch.Tensor:
         """Host fp64 matrix of all inner products ``vs[i] . vs[j]``."""
         return _gram_local(vs).to("cpu", torch.float64)
@@ -78,6 +82,9 @@ class ShardedSpace(LocalSpace):
     def abs_sum(self, a) -> float:
         return float(self._sum(torch.sum(torch.abs(a)).reshape(1).to(torch.float64))[0])
 
+    def dots(self, pairs) -> list:
+        return self._sum(torch.stack([torch.dot(a, b) for a, b in pairs]).to(torch.float64)).tolist()
+
     def gram(self, vs):
         return self._sum(_gram_local(vs).to(torch.float64))
 
@@ -89,6 +96,11 @@ def _gram_local(vs: Sequence[torch.Tensor]) -> torch.Tensor:
     """V V^T for a few (k ~ 21) very long vectors. A plain GEMM with K = D ~ 1e6-1e8 and a 21 x 21 output gives the
     BLAS one tile and no split-K (measured on MI355X: 160 ms per call at D = 1M, 281 ms at 10M); cut K into 16K blocks and
     batch them (one bmm of D / 16K independent 21 x 16K x 21 products; 2.8-2.9 ms at both sizes), then sum."""
+    if vs and vs[0].is_cuda:
+        from ..ops.native import gram
+        G = gram(list(vs))          # one-pass LDS-tiled HIP kernel (ops/csrc/glm_kernels.hip gram_kernel)
+        if G is not None:
+            return G
     V = torch.stack(list(vs))
     k, n = V.shape
     if n <= 4 * _GRAM_BLOCK:
@@ -120,6 +132,10 @@ def active_space(space: LocalSpace) -> Iterator[LocalSpace]:
 
 def vdot(a, b) -> float:
     return current().dot(a, b)
+
+
+def vdots(pairs) -> list:
+    return current().dots(pairs)
 
 
 def vnorm(a) -> float:

@@ -194,3 +194,28 @@ def test_row_space_random_effect_solve_matches_primal(task, opt, monkeypatch):
             np.testing.assert_allclose(a.coefficients_of(e).means.numpy(), b.coefficients_of(e).means.numpy(),
                                        rtol=1e-4, atol=tol)
     assert torch.allclose(c0.score(a2), c1.score(b2), atol=1e-5)
+
+
+def test_row_space_lazy_primal_model(monkeypatch):
+    """When every entity is solved in its row space, the returned model defers w = X^T L^-T beta until it is
+    read: scores (L beta), the regularization term (||beta||^2) and the warm-started next update need no
+    transpose pass, and the materialised coefficients equal the eager ones."""
+    data, _ = generate_game_data(n_rows=600, n_items=200, d_item=40, seed=31, task="LOGISTIC_REGRESSION")
+    cfg = _cfg("TRON", 1.0, 60, 1e-10)
+    out = {}
+    for mode in ("0", "1"):
+        monkeypatch.setenv("PML_RE_LAZY_PRIMAL", mode)
+        c = RandomEffectCoordinate("i", data, RandomEffectDataConfiguration("itemId", "item"), cfg,
+                                   "LOGISTIC_REGRESSION", device="cpu", layout="segmented")
+        m1 = c.update_model(c.initialize_model())
+        s1, r1 = c.score(m1), c.regularization_term_value(m1)
+        m2 = c.update_model(m1, partial_score=torch.from_numpy(np.cos(np.arange(data.n_rows)) * 0.3))
+        s2, r2 = c.score(m2), c.regularization_term_value(m2)
+        out[mode] = (m1, m2, s1, s2, r1, r2, m2.materialized)
+    (a1, a2, as1, as2, ar1, ar2, amat), (b1, b2, bs1, bs2, br1, br2, bmat) = out["0"], out["1"]
+    assert amat and not bmat            # lazy path taken (all entities in row space), eager path materialised
+    torch.testing.assert_close(as1, bs1, rtol=1e-9, atol=1e-10)
+    torch.testing.assert_close(as2, bs2, rtol=1e-9, atol=1e-10)
+    assert ar1 == pytest.approx(br1, rel=1e-9) and ar2 == pytest.approx(br2, rel=1e-9)
+    np.testing.assert_allclose(b2.values, a2.values, rtol=1e-8, atol=1e-10)
+    assert b2.materialized

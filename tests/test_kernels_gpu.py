@@ -429,3 +429,38 @@ def test_gather_dedup_variant_is_bitwise_equal():
     finally:
         configure(tl_dedup=0, tl_dedup_t=0)
     assert torch.equal(got, ref)
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("k,n", [(1, 1), (3, 1000), (21, 1_000_003), (22, 300_000)])
+def test_gram_and_lincomb_kernels(k, n):
+    """gram_kernel / lincomb_kernel (vector-free L-BFGS two-loop) vs fp64 torch."""
+    from photon_ml_amd.ops.native import gram, lincomb
+    g = torch.Generator(device="cuda").manual_seed(k)
+    vs = [torch.randn(n, dtype=torch.float64, device="cuda", generator=g) for _ in range(k)]
+    G = gram(vs)
+    V = torch.stack(vs)
+    torch.testing.assert_close(G, V @ V.T, rtol=1e-12, atol=1e-9)
+    c = [0.5 * j - 1.0 for j in range(k)]
+    q = lincomb(c, vs)
+    torch.testing.assert_close(q, torch.tensor(c, dtype=torch.float64, device="cuda") @ V, rtol=1e-12, atol=1e-12)
+
+
+@pytest.mark.gpu
+def test_lbfgs_vector_free_two_loop_on_device(monkeypatch):
+    """L-BFGS with the Gram-kernel two-loop on long device vectors == the dot-product recursion."""
+    import photon_ml_amd.optimization.lbfgs as lb
+    from photon_ml_amd.data.synthetic import generate_glm_data
+    from photon_ml_amd.function.losses import LOGISTIC
+    from photon_ml_amd.function.objective import GLMObjective
+    from photon_ml_amd.ops.device import DeviceGLMData
+    data, _ = generate_glm_data("LOGISTIC_REGRESSION", 20000, 300, density=0.05, seed=11)
+    out = {}
+    for gmin in (1 << 40, 1):
+        monkeypatch.setattr(lb, "GRAM_MIN_DIM", gmin)
+        dev = DeviceGLMData.from_labeled(data, "cuda", "f64", chunk_rows=8192, layout="tiled")
+        opt = lb.LBFGS(tolerance=1e-9, max_iterations=30)
+        w, f = opt.optimize(GLMObjective(LOGISTIC, 1.0), dev, torch.zeros(300, dtype=torch.float64, device="cuda"))
+        out[gmin] = (w, f)
+    (w0, f0), (w1, f1) = out[1 << 40], out[1]
+    assert torch.allclose(w0, w1, rtol=1e-6, atol=1e-7) and abs(f0 - f1) <= 1e-10 * abs(f0)

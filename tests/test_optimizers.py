@@ -160,3 +160,18 @@ def test_tron_margin_space_trial_matches_full_evaluations(task, norm):
     (w0, f0, i0, c0), (w1, f1, i1, c1) = out[False], out[True]
     assert (i0, c0) == (i1, c1)
     assert torch.allclose(w0, w1, rtol=1e-8, atol=1e-10) and abs(f0 - f1) <= 1e-10 * abs(f0)
+
+
+def test_vector_free_two_loop_matches_recursion():
+    """The Gram-matrix (vector-free) two-loop used for long device vectors and feature shards == the classic
+    two-loop recursion."""
+    from photon_ml_amd.optimization.lbfgs import _History
+    rng = np.random.default_rng(3)
+    h = _History(5)
+    A = rng.normal(size=(40, 40))
+    A = A @ A.T + 40 * np.eye(40)
+    for _ in range(7):
+        s = torch.from_numpy(rng.normal(size=40))
+        h.push(s, torch.from_numpy(A) @ s)
+    g = torch.from_numpy(rng.normal(size=40))
+    torch.testing.assert_close(h._apply_inverse_gram(g), h.apply_inverse(g), rtol=1e-10, atol=1e-12)
