@@ -1134,6 +1134,7 @@ static int g_tl_waves = 4;     // forward
 static int g_tl_waves_t = 4;   // transpose
 static int g_tl_pipe = 0;      // forward stream pipeline variant (see tl_stream)
 static int g_tl_pipe_t = 0;    // transpose stream pipeline variant
+static int g_rs_variant = 2;   // rs_tron_kernel variant (see the kernel); 2 measured fastest (scripts/rs_tron_bench.py)
 static int g_tl_dedup = 0;     // interleaved forward: gather dedup across lanes (P = 4)
 static int g_tl_dedup_t = 0;   // interleaved transpose: gather dedup
 
@@ -1532,6 +1533,28 @@ __global__ __launch_bounds__(NTHREADS) void bhv_kernel(int B, int n, const doubl
 // <= max_fail consecutive rejections; reason codes 1 max-iter, 2 not-improving, 3 f-converged, 4 g-converged.
 // Per-problem reductions are fixed-order butterflies inside the lane group: deterministic.
 // ============================================================================================================
+// Cross-lane moves of a double within a lane group, without the LDS crossbar where possible: DPP (quad
+// permutations, row half-mirror / mirror: all inside 16 lanes) and ds_swizzle (xor 16 inside 32 lanes).
+template <int CTRL>
+__device__ __forceinline__ double dpp_f64(double v) {
+  const long long b = __builtin_bit_cast(long long, v);
+  const int lo = __builtin_amdgcn_update_dpp(0, (int)b, CTRL, 0xF, 0xF, true);
+  const int hi = __builtin_amdgcn_update_dpp(0, (int)(b >> 32), CTRL, 0xF, 0xF, true);
+  return __builtin_bit_cast(double, ((long long)hi << 32) | (long long)(unsigned int)lo);
+}
+template <int PAT>
+__device__ __forceinline__ double swz_f64(double v) {
+  const long long b = __builtin_bit_cast(long long, v);
+  const int lo = __builtin_amdgcn_ds_swizzle((int)b, PAT);
+  const int hi = __builtin_amdgcn_ds_swizzle((int)(b >> 32), PAT);
+  return __builtin_bit_cast(double, ((long long)hi << 32) | (long long)(unsigned int)lo);
+}
+
+// V >= 1: the matrix-vector products read the vector from a per-problem LDS slot (one ds_write per product,
+// then broadcast ds_reads) instead of two ds_bpermute shuffles per element, with two accumulators.
+// V >= 2: group sums by DPP / swizzle steps instead of ds_bpermute butterflies (every step is symmetric, so all
+// lanes of a group hold bitwise the same sum).
+template <int V>
 __global__ __launch_bounds__(NTHREADS) void rs_tron_kernel(
     int B, int n, int G, const double* __restrict__ Lm, const double* __restrict__ Y, const double* __restrict__ O,
     const double* __restrict__ WT, double* __restrict__ Beta, double* __restrict__ Fout, int* __restrict__ Iters,
@@ -1539,7 +1562,8 @@ __global__ __launch_bounds__(NTHREADS) void rs_tron_kernel(
   extern __shared__ double smem[];
   const int lane = threadIdx.x & 63, w = threadIdx.x >> 6;
   const int per = 64 / G, np = n * (n + 1);
-  double* sA = smem + w * per * np;
+  double* sA = smem + w * per * (np + (V >= 1 ? G : 0));
+  double* sv = sA + per * np + (lane / G) * G;   // V = 1: this problem's vector slot
   const long long b0 = ((long long)blockIdx.x * (blockDim.x >> 6) + w) * per;
   if (b0 >= B) return;
   const int count = (int)min((long long)per, B - b0);
@@ -1558,18 +1582,55 @@ __global__ __launch_bounds__(NTHREADS) void rs_tron_kernel(
   const double* Lb = sA + (prob_on ? g : 0) * np;
 
   auto gsum = [&](double v) {
-    for (int s = G >> 1; s > 0; s >>= 1) v += __shfl_xor(v, s, 64);
-    return v;
+    if constexpr (V >= 2) {
+      if (G >= 2) v += dpp_f64<0xB1>(v);      // quad_perm [1,0,3,2]
+      if (G >= 4) v += dpp_f64<0x4E>(v);      // quad_perm [2,3,0,1]
+      if (G >= 8) v += dpp_f64<0x141>(v);     // row_half_mirror
+      if (G >= 16) v += dpp_f64<0x140>(v);    // row_mirror
+      if (G >= 32) v += swz_f64<0x401F>(v);   // xor 16 within 32 lanes
+      if (G >= 64) v += __shfl_xor(v, 32, 64);
+      return v;
+    } else {
+      for (int s = G >> 1; s > 0; s >>= 1) v += __shfl_xor(v, s, 64);
+      return v;
+    }
+  };
+  auto put = [&](double v) {
+    sv[i] = on ? v : 0.0;
+    __builtin_amdgcn_s_waitcnt(0);
+    __builtin_amdgcn_wave_barrier();
   };
   auto mv = [&](double v) {  // (L v)_i
-    double acc = 0.0;
-    for (int j = 0; j < n; ++j) acc = fma(Lb[ii * (n + 1) + j], __shfl(v, base + j, 64), acc);
-    return on ? acc : 0.0;
+    if constexpr (V >= 1) {
+      put(v);
+      const double* Lr = Lb + ii * (n + 1);
+      double a0 = 0.0, a1 = 0.0;
+      int j = 0;
+      for (; j + 1 < n; j += 2) { a0 = fma(Lr[j], sv[j], a0); a1 = fma(Lr[j + 1], sv[j + 1], a1); }
+      if (j < n) a0 = fma(Lr[j], sv[j], a0);
+      return on ? a0 + a1 : 0.0;
+    } else {
+      double acc = 0.0;
+      for (int j = 0; j < n; ++j) acc = fma(Lb[ii * (n + 1) + j], __shfl(v, base + j, 64), acc);
+      return on ? acc : 0.0;
+    }
   };
   auto mvt = [&](double u) {  // (L^T u)_i
-    double acc = 0.0;
-    for (int r = 0; r < n; ++r) acc = fma(Lb[r * (n + 1) + ii], __shfl(u, base + r, 64), acc);
-    return on ? acc : 0.0;
+    if constexpr (V >= 1) {
+      put(u);
+      double a0 = 0.0, a1 = 0.0;
+      int r = 0;
+      for (; r + 1 < n; r += 2) {
+        a0 = fma(Lb[r * (n + 1) + ii], sv[r], a0);
+        a1 = fma(Lb[(r + 1) * (n + 1) + ii], sv[r + 1], a1);
+      }
+      if (r < n) a0 = fma(Lb[r * (n + 1) + ii], sv[r], a0);
+      return on ? a0 + a1 : 0.0;
+    } else {
+      double acc = 0.0;
+      for (int r = 0; r < n; ++r) acc = fma(Lb[r * (n + 1) + ii], __shfl(u, base + r, 64), acc);
+      return on ? acc : 0.0;
+    }
   };
   auto vg = [&](double v, double& f, double& gr, double& Dw) {
     const double z = mv(v) + off;
@@ -2002,6 +2063,8 @@ int pml_bhv(int B, int n, const double* A, const double* dw, const double* v, do
   return 0;
 }
 
+void pml_rs_set_variant(int v) { g_rs_variant = v; }
+
 int pml_rs_tron(int B, int n, const double* L, const double* y, const double* off, const double* wt, double* beta,
                 double* f, int* iters, int* reason, int loss, double l2, double tol, int max_iter, int max_fail,
                 int max_cg, void* stream) {
@@ -2011,11 +2074,19 @@ int pml_rs_tron(int B, int n, const double* L, const double* y, const double* of
   while (G < n) G <<= 1;
   const int per = 64 / G;
   const long long waves = (B + per - 1) / per;
-  const size_t wave_lds = (size_t)per * n * (n + 1) * sizeof(double);
+  const int V = g_rs_variant;
+  const size_t wave_lds = (size_t)per * (n * (n + 1) + (V >= 1 ? G : 0)) * sizeof(double);
   const int nw = (int)std::max<size_t>(1, std::min<size_t>(4, 65536 / wave_lds));
   const long long grid = (waves + nw - 1) / nw;
-  hipLaunchKernelGGL(rs_tron_kernel, dim3((unsigned)grid), dim3(nw * 64), nw * wave_lds, (hipStream_t)stream, B, n, G,
-                     L, y, off, wt, beta, f, iters, reason, loss, l2, tol, max_iter, max_fail, max_cg);
+  if (V == 2)
+    hipLaunchKernelGGL(rs_tron_kernel<2>, dim3((unsigned)grid), dim3(nw * 64), nw * wave_lds, (hipStream_t)stream, B,
+                       n, G, L, y, off, wt, beta, f, iters, reason, loss, l2, tol, max_iter, max_fail, max_cg);
+  else if (V == 1)
+    hipLaunchKernelGGL(rs_tron_kernel<1>, dim3((unsigned)grid), dim3(nw * 64), nw * wave_lds, (hipStream_t)stream, B,
+                       n, G, L, y, off, wt, beta, f, iters, reason, loss, l2, tol, max_iter, max_fail, max_cg);
+  else
+    hipLaunchKernelGGL(rs_tron_kernel<0>, dim3((unsigned)grid), dim3(nw * 64), nw * wave_lds, (hipStream_t)stream, B,
+                       n, G, L, y, off, wt, beta, f, iters, reason, loss, l2, tol, max_iter, max_fail, max_cg);
   LAUNCH_CHECK();
   return 0;
 }

@@ -105,6 +105,8 @@ def glm_lib() -> Optional[ctypes.CDLL]:
         lib.pml_gram.argtypes = [c_void_p, c_int, ctypes.c_longlong, c_void_p, c_void_p]
         lib.pml_lincomb.argtypes = [c_void_p, c_void_p, c_int, ctypes.c_longlong, c_void_p, c_void_p]
         lib.pml_tl_set_dedup.argtypes = [c_int, c_int]
+        lib.pml_rs_set_variant.argtypes = [c_int]
+        lib.pml_rs_set_variant(int(os.environ.get("PML_RS_VARIANT", "2")))
         lib.pml_ls_eval.argtypes = [c_int, c_int, c_double, c_int, c_void_p, c_void_p, c_void_p, c_void_p, c_int,
                                     c_void_p, c_void_p, c_void_p, c_void_p, c_void_p]
         lib.pml_rs_tron.argtypes = [c_int, c_int] + [c_void_p] * 8 + [c_int, c_double, c_double, c_int, c_int, c_int,

@@ -300,11 +300,23 @@ def test_batched_small_gemv_and_hv_match_torch(n):
 @pytest.mark.parametrize("loss_name,n", [("LOGISTIC", 20), ("POISSON", 7), ("SQUARED", 33), ("LOGISTIC", 64),
                                          ("LOGISTIC", 1)])
 @pytest.mark.parametrize("warm", [False, True])
-def test_fused_row_space_tron_matches_batched_tron(loss_name, n, warm):
+@pytest.mark.parametrize("variant", [0, 1, 2])
+def test_fused_row_space_tron_matches_batched_tron(loss_name, n, warm, variant):
     """rs_tron_kernel (whole per-problem TRON in one kernel) vs the vectorised batched TRON of
-    optimization/batched.py on the same dense problems (fp64): same solutions, objective and iteration counts."""
+    optimization/batched.py on the same dense problems (fp64): same solutions, objective and iteration counts.
+    Every matrix-vector / group-sum variant of the kernel (bpermute shuffles, LDS vector slot, DPP sums)."""
+    import os
     from photon_ml_amd.function import losses
-    from photon_ml_amd.ops.native import rs_tron
+    from photon_ml_amd.ops.native import require_glm_lib, rs_tron
+    lib = require_glm_lib()
+    lib.pml_rs_set_variant(variant)
+    try:
+        _check_rs_tron(loss_name, n, warm, losses, rs_tron)
+    finally:
+        lib.pml_rs_set_variant(int(os.environ.get("PML_RS_VARIANT", "2")))
+
+
+def _check_rs_tron(loss_name, n, warm, losses, rs_tron):
     from photon_ml_amd.optimization.batched import BatchedGLMData, batched_tron
     loss = {"LOGISTIC": losses.LOGISTIC, "POISSON": losses.POISSON, "SQUARED": losses.SQUARED}[loss_name]
     g = torch.Generator(device="cuda").manual_seed(7 * n + int(warm))
