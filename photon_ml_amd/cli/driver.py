@@ -45,7 +45,7 @@ from ..normalization.context import NormalizationContext, NormalizationType
 from ..optimization.config import OptimizerType, RegularizationContext, RegularizationType
 from ..stat.summary import BasicStatisticalSummary
 from ..utils.logging_utils import EventEmitter, PhotonLogger
-from .params import parse_bool, split_list
+from .params import add_config_arguments, parse_args_with_config, parse_bool, split_list
 
 LEARNED_MODELS_TEXT = "learned-models-text"
 BEST_MODEL_TEXT = "best-model-text"
@@ -105,6 +105,7 @@ def build_parser() -> argparse.ArgumentParser:
     p.add_argument("--device", default=None)
     p.add_argument("--precision", default="f64", choices=["bf16", "f32", "f64"])
     p.add_argument("--seed", type=int, default=0)
+    add_config_arguments(p)
     return p
 
 
@@ -378,7 +379,7 @@ def read_text_model(path: str) -> Dict[float, Dict[Tuple[str, str], float]]:
 
 
 def main(argv=None) -> int:
-    Driver(build_parser().parse_args(argv)).run()
+    Driver(parse_args_with_config(build_parser(), argv)).run()
     return 0
 
 

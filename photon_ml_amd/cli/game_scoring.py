@@ -25,7 +25,7 @@ from ..parallel.dist import rank
 from ..utils.logging_utils import PhotonLogger
 from ..utils.timing import Timed
 from .game_training import GameDriverBase, add_common_arguments, process_output_dir, resolve_paths
-from .params import parse_bool, split_list
+from .params import parse_args_with_config, parse_bool, split_list
 
 SCORES_DIR = "scores"
 DEFAULT_APPLICATION_NAME = "GAME-Scoring"
@@ -105,7 +105,7 @@ class GameScoringDriver(GameDriverBase):
 
 
 def main(argv=None) -> int:
-    args = build_parser().parse_args(argv)
+    args = parse_args_with_config(build_parser(), argv)
     if "LOCAL_RANK" in os.environ or "RANK" in os.environ:
         from ..parallel.dist import init_distributed
         init_distributed()

@@ -53,9 +53,10 @@ from ..parallel.dist import is_dist, rank, world_size
 from ..stat.summary import BasicStatisticalSummary
 from ..utils.logging_utils import PhotonLogger
 from ..utils.timing import Timed
-from .params import (HyperparameterTuningMode, ModelOutputMode, coordinate_configuration_to_string,
+from .params import (HyperparameterTuningMode, ModelOutputMode, add_config_arguments, coordinate_configuration_to_string,
                      expand_daily_dirs, expand_game_configurations, parse_bool, parse_coordinate_configuration,
-                     parse_date_range, parse_days_range, parse_feature_shard_configuration, parse_kv, split_list)
+                     parse_args_with_config, parse_date_range, parse_days_range, parse_feature_shard_configuration, parse_kv,
+                     split_list)
 
 MODELS_DIR = "models"
 MODEL_SPEC_DIR = "model-spec"
@@ -84,6 +85,7 @@ def add_common_arguments(p: argparse.ArgumentParser):
     p.add_argument("--device", default=None, help="torch device (default: cuda if available)")
     p.add_argument("--precision", default="f64", choices=["bf16", "f32", "f64"],
                    help="fixed-effect feature storage precision on the GPU (accumulation is always fp64)")
+    add_config_arguments(p)
 
 
 def build_parser() -> argparse.ArgumentParser:
@@ -368,7 +370,7 @@ def optimization_config_to_string(config, coord_configs=None) -> str:
 
 
 def main(argv=None) -> int:
-    args = build_parser().parse_args(argv)
+    args = parse_args_with_config(build_parser(), argv)
     if "LOCAL_RANK" in os.environ or "RANK" in os.environ:
         from ..parallel.dist import init_distributed
         init_distributed()

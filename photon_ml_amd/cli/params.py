@@ -185,3 +185,130 @@ def split_list(values: Optional[Sequence[str]]) -> List[str]:
     for v in values or []:
         out.extend(x.strip() for x in str(v).split(",") if x.strip())
     return out
+
+
+# --------------------------------------------------------------------------------------------------------------
+# Config files: every driver flag can also come from a JSON / YAML mapping {flag-name: value}, and the parsed
+# command line can be written back out (the round-trip the reference's ScoptParameter printer gives,
+# ``CLI/io/scopt/ScoptParameter.scala:58-90``, as a file instead of a log line).
+
+CONFIG_FILE_FLAG = "--config-file"
+WRITE_CONFIG_FLAG = "--write-config"
+
+
+def _long_option(action) -> Optional[str]:
+    longs = [s for s in action.option_strings if s.startswith("--")]
+    return longs[0] if longs else None
+
+
+def _is_append(action) -> bool:
+    import argparse
+    return isinstance(action, argparse._AppendAction)
+
+
+def load_config_file(path: str) -> Dict[str, object]:
+    """A ``{flag-name: value}`` mapping from ``.json`` or ``.yaml``/``.yml`` (safe loader only)."""
+    with open(path) as f:
+        if path.endswith((".yaml", ".yml")):
+            import yaml
+            cfg = yaml.safe_load(f) or {}
+        else:
+            import json
+            cfg = json.load(f)
+    if not isinstance(cfg, dict):
+        raise ValueError(f"{path}: a config file must hold a mapping of flag names to values")
+    return cfg
+
+
+def _scalar(v) -> str:
+    if isinstance(v, bool):
+        return "true" if v else "false"
+    return str(v)
+
+
+def config_to_argv(parser, cfg: Dict[str, object]) -> List[str]:
+    """Command-line tokens for a config mapping; keys are flag names with or without the leading ``--``."""
+    known = {}
+    for a in parser._actions:
+        for s in a.option_strings:
+            known[s] = a
+    argv: List[str] = []
+    for key, value in cfg.items():
+        flag = key if key.startswith("--") else "--" + key.replace("_", "-")
+        action = known.get(flag)
+        if action is None:
+            raise ValueError(f"unknown option {flag!r} in config file")
+        if value is None:
+            continue
+        values = value if isinstance(value, (list, tuple)) else [value]
+        if not _is_append(action) and isinstance(value, (list, tuple)):
+            raise ValueError(f"option {flag!r} takes one value, got a list")
+        for v in values:
+            argv += [flag, _scalar(v)]
+    return argv
+
+
+def args_to_config(parser, args) -> Dict[str, object]:
+    """The parsed options as a ``{flag-name: value}`` mapping that :func:`config_to_argv` turns back into ``args``."""
+    out: Dict[str, object] = {}
+    for a in parser._actions:
+        flag = _long_option(a)
+        if flag is None or flag in (CONFIG_FILE_FLAG, WRITE_CONFIG_FLAG) or not hasattr(args, a.dest):
+            continue
+        v = getattr(args, a.dest)
+        if v is None or v == a.default:
+            continue
+        if isinstance(v, enum.Enum):
+            v = v.value
+        out[flag[2:]] = list(v) if isinstance(v, (list, tuple)) else v
+    return out
+
+
+def parse_args_with_config(parser, argv: Optional[Sequence[str]] = None):
+    """``parser.parse_args`` that also accepts ``--config-file PATH`` (values from the file; a flag given on the
+    command line replaces the file's value, for repeatable flags the whole list) and ``--write-config PATH`` (writes
+    the effective options as JSON or YAML by extension)."""
+    import sys
+    argv = list(sys.argv[1:] if argv is None else argv)
+    pre = _preparser()
+    known, rest = pre.parse_known_args(argv)
+    file_argv: List[str] = []
+    if known.config_file:
+        cfg = load_config_file(known.config_file)
+        on_cli = {tok.split("=", 1)[0] for tok in rest if tok.startswith("--")}
+        aliases = {}
+        for a in parser._actions:
+            for s in a.option_strings:
+                aliases[s] = set(a.option_strings)
+        cfg = {k: v for k, v in cfg.items()
+               if not (aliases.get(k if k.startswith("--") else "--" + k.replace("_", "-"), set()) & on_cli)}
+        file_argv = config_to_argv(parser, cfg)
+    args = parser.parse_args(file_argv + rest)
+    if known.write_config:
+        write_config_file(known.write_config, args_to_config(parser, args))
+    return args
+
+
+def write_config_file(path: str, cfg: Dict[str, object]) -> None:
+    os.makedirs(os.path.dirname(os.path.abspath(path)), exist_ok=True)
+    with open(path, "w") as f:
+        if path.endswith((".yaml", ".yml")):
+            import yaml
+            yaml.safe_dump(cfg, f, sort_keys=True, default_flow_style=False)
+        else:
+            import json
+            json.dump(cfg, f, indent=2, sort_keys=True)
+
+
+def _preparser():
+    import argparse
+    pre = argparse.ArgumentParser(add_help=False, allow_abbrev=False)
+    pre.add_argument(CONFIG_FILE_FLAG)
+    pre.add_argument(WRITE_CONFIG_FLAG)
+    return pre
+
+
+def add_config_arguments(p) -> None:
+    """Registers the config-file flags on a driver parser (so ``--help`` lists them)."""
+    p.add_argument(CONFIG_FILE_FLAG, help="JSON/YAML mapping of flag names to values; command-line flags win")
+    p.add_argument(WRITE_CONFIG_FLAG, help="write the effective options to this JSON/YAML file")

@@ -163,3 +163,37 @@ def test_libsvm_to_avro_roundtrip(tmp_path):
     for j in range(13):
         col = im.get_index(f"{j + 1}\u0001")
         np.testing.assert_allclose(ld_avro.x[:, col].toarray(), ld_txt.x[:, j].toarray())
+
+
+@pytest.mark.parametrize("ext", ["json", "yaml"])
+def test_config_file_round_trip(game_avro, tmp_path, ext):
+    """``--config-file`` / ``--write-config``: the written options parse back to the same namespace, command-line
+    flags replace the file's values (repeatable flags as a whole), and a run driven by a config file trains."""
+    from photon_ml_amd.cli.params import load_config_file, parse_args_with_config
+    out = tmp_path / "cfg-out"
+    args = ["--input-data-directories", str(game_avro / "train"),
+            "--root-output-directory", str(out), "--training-task", "LOGISTIC_REGRESSION", *SHARDS,
+            "--coordinate-configurations", FIXED, "--coordinate-update-sequence", "fixed",
+            "--coordinate-descent-iterations", "1", "--device", "cpu", "--compute-variance", "true"]
+    cfg_path = str(tmp_path / f"train.{ext}")
+    parser = game_training.build_parser()
+    direct = parser.parse_args(args)
+    written = parse_args_with_config(parser, args + ["--write-config", cfg_path])
+    cfg = load_config_file(cfg_path)
+    assert cfg["training-task"] == "LOGISTIC_REGRESSION" and len(cfg["feature-shard-configurations"]) == 2
+    assert cfg["compute-variance"] is True
+    from_file = parse_args_with_config(game_training.build_parser(), ["--config-file", cfg_path])
+    for ns in (written, from_file):
+        d, f = vars(direct), vars(ns)
+        assert {k: v for k, v in f.items() if k not in ("config_file", "write_config")} == \
+               {k: v for k, v in d.items() if k not in ("config_file", "write_config")}
+    over = parse_args_with_config(game_training.build_parser(),
+                                  ["--config-file", cfg_path, "--coordinate-descent-iterations", "3",
+                                   "--feature-shard-configurations", "name=global,feature.bags=features"])
+    assert over.coordinate_descent_iterations == 3 and len(over.feature_shard_configurations) == 1
+    assert over.training_task == "LOGISTIC_REGRESSION"
+    res = game_training.GameTrainingDriver(from_file).run()
+    assert res["best"] is not None and os.path.exists(out / "best" / "model-metadata.json")
+    with pytest.raises(ValueError):
+        from photon_ml_amd.cli.params import config_to_argv
+        config_to_argv(game_training.build_parser(), {"no-such-flag": 1})
