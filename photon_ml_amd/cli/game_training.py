@@ -110,6 +110,8 @@ def build_parser() -> argparse.ArgumentParser:
     p.add_argument("--compute-variance", type=parse_bool, default=False)
     p.add_argument("--use-warm-start", type=parse_bool, default=True)
     p.add_argument("--checkpoint-directory", help="save coordinate-descent state after every coordinate update")
+    p.add_argument("--model-input-directory",
+                   help="initialise training from a saved GAME model directory (e.g. a previous run's best/)")
     p.add_argument("--resume", type=parse_bool, default=False,
                    help="continue an interrupted run from --checkpoint-directory (the output directory is kept)")
     return p
@@ -278,6 +280,9 @@ class GameTrainingDriver(GameDriverBase):
                .set_warm_start(a.use_warm_start)
                .set_tree_aggregate_depth(a.tree_aggregate_depth)
                .set_coordinate_normalization_contexts(norm_ctx))
+        if a.model_input_directory:
+            from ..io.model_io import load_game_model
+            est.set_initial_model(load_game_model(a.model_input_directory, maps))
         if a.evaluators:
             est.set_validation_evaluators(split_list(a.evaluators))
         if a.checkpoint_directory:

@@ -113,6 +113,12 @@ class GameEstimator:
         self.use_warm_start = bool(b)
         return self
 
+    def set_initial_model(self, model: Optional[GameModel]):
+        """Start the first configuration from a saved model (e.g. ``load_game_model``) instead of zeros; the
+        reference has no such option (warm start only in-process)."""
+        self.initial_model = model
+        return self
+
     def set_checkpoint_directory(self, directory: Optional[str], resume: bool = False):
         """Checkpoint coordinate descent after every coordinate update (one state file per configuration and
         rank); with ``resume`` an interrupted fit continues where it stopped (see utils/checkpoint.py)."""
@@ -164,7 +170,7 @@ class GameEstimator:
         train_eval = build_evaluator(training_loss_evaluator_type(self.training_task), data.response, data.offsets,
                                      data.weights)
         val_evals = self._validation_evaluators(validation) if validation is not None else []
-        results, prev = [], None
+        results, prev = [], getattr(self, "initial_model", None)
         for i, cfg in enumerate(configurations):
             for cid, c in self.coordinates.items():
                 c.set_config(cfg[cid])
@@ -178,7 +184,7 @@ class GameEstimator:
                 tag = _json.dumps({c: cfg[c].to_json() for c in sorted(cfg)}, sort_keys=True)
                 if not self.resume and ck.exists():
                     os.remove(ck.path)
-            model, evals = cd.run(self.coordinate_descent_iterations, prev if self.use_warm_start else None, ck,
+            model, evals = cd.run(self.coordinate_descent_iterations, prev if (self.use_warm_start or i == 0) else None, ck,
                                   tag)
             self.history.append(cd.history)
             results.append(GameResult(model, evals, cfg))

@@ -197,3 +197,25 @@ def test_config_file_round_trip(game_avro, tmp_path, ext):
     with pytest.raises(ValueError):
         from photon_ml_amd.cli.params import config_to_argv
         config_to_argv(game_training.build_parser(), {"no-such-flag": 1})
+
+
+def test_training_from_saved_model(game_avro, tmp_path):
+    """``--model-input-directory`` on the training driver: a run initialised from a previous run's best model
+    starts at (and stays near) that model's training loss instead of the zero model's."""
+    base = ["--input-data-directories", str(game_avro / "train"), "--training-task", "LOGISTIC_REGRESSION", *SHARDS,
+            "--coordinate-configurations", FIXED.replace("reg.weights=10|0.1", "reg.weights=1"),
+            "--coordinate-configurations", RANDOM, "--coordinate-update-sequence", "fixed,per-user",
+            "--device", "cpu"]
+    first = game_training.GameTrainingDriver(game_training.build_parser().parse_args(
+        base + ["--root-output-directory", str(tmp_path / "a"), "--coordinate-descent-iterations", "2"])).run()
+    est_cold = game_training.GameTrainingDriver(game_training.build_parser().parse_args(
+        base + ["--root-output-directory", str(tmp_path / "b"), "--coordinate-descent-iterations", "1"]))
+    cold = est_cold.run()
+    warm = game_training.GameTrainingDriver(game_training.build_parser().parse_args(
+        base + ["--root-output-directory", str(tmp_path / "c"), "--coordinate-descent-iterations", "1",
+                "--model-input-directory", str(tmp_path / "a" / "best")])).run()
+    fw = first["best"].model.get("fixed").glm.coefficients.means
+    ww = warm["best"].model.get("fixed").glm.coefficients.means
+    cw = cold["best"].model.get("fixed").glm.coefficients.means
+    # warm start from the converged 2-sweep model moves it far less than a cold 1-sweep run differs from it
+    assert float(np.abs(np.asarray(ww) - np.asarray(fw)).max()) < 0.5 * float(np.abs(np.asarray(cw) - np.asarray(fw)).max())

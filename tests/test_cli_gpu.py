@@ -84,3 +84,21 @@ def test_legacy_driver_on_gpu_matches_cpu(tmp_path, norm, rtol):
         assert set(c) == set(g)
         for k in c:
             assert abs(c[k] - g[k]) <= rtol * max(1.0, abs(c[k])), (lam, k, c[k], g[k])
+
+
+def test_game_training_from_saved_model_on_gpu(game_avro, tmp_path):
+    """``--model-input-directory`` on the training driver with the device path: a saved (host) model initialises
+    the cuda coordinates, and one more sweep from it matches the same warm start on the CPU backend."""
+    first = _train(game_avro, tmp_path / "first", "cpu")
+    assert first["best"] is not None
+    outs = {}
+    for dev in ("cpu", "cuda"):
+        args = ["--input-data-directories", str(game_avro / "train"),
+                "--validation-data-directories", str(game_avro / "val"),
+                "--root-output-directory", str(tmp_path / f"warm-{dev}"), "--training-task", "LOGISTIC_REGRESSION",
+                *SHARDS, "--coordinate-configurations", FIXED, "--coordinate-configurations", RANDOM,
+                "--coordinate-update-sequence", "fixed,per-user", "--coordinate-descent-iterations", "1",
+                "--evaluators", "AUC", "--device", dev, "--model-input-directory", str(tmp_path / "first" / "best")]
+        outs[dev] = game_training.GameTrainingDriver(game_training.build_parser().parse_args(args)).run()
+    a_c, a_g = outs["cpu"]["best"].evaluations[0][1], outs["cuda"]["best"].evaluations[0][1]
+    assert a_g > 0.7 and abs(a_g - a_c) < 1e-6
