@@ -86,6 +86,7 @@ def main():
     dev = torch.device("cuda", local)
 
     from photon_ml_amd.data.synthetic import generate_device_shard
+    from photon_ml_amd.utils.timing import trace_range
     from photon_ml_amd.function.losses import LOGISTIC, POISSON
     from photon_ml_amd.function.objective import GLMObjective
     from photon_ml_amd.optimization.lbfgs import LBFGS, OWLQN
@@ -138,9 +139,10 @@ def main():
         barrier()
         passes0 = data.n_passes
         t0 = time.perf_counter()
-        for i in range(args.steps):
-            st = opt.step(obj, gdata)
-        torch.cuda.synchronize()
+        with trace_range("bench timed steps"):  # roctx region (PML_TRACE=1) for timed-window profiles
+            for i in range(args.steps):
+                st = opt.step(obj, gdata)
+            torch.cuda.synchronize()
         barrier()
         elapsed = time.perf_counter() - t0
         gnorm = st.grad_norm()
