@@ -178,6 +178,7 @@ class RandomEffectCoordinate(Coordinate):
         self.base_offsets = torch.from_numpy(data.offsets).to(self.device)
         self.set_config(opt_config)
         self._W = {}  # projected-space warm-start state per bucket
+        self._returned = None  # the model object the last update returned (its solver state is in _W / _rs)
         self.last_stats = {}
 
     def set_config(self, opt_config: GLMOptimizationConfiguration):
@@ -186,6 +187,14 @@ class RandomEffectCoordinate(Coordinate):
                 RegularizationType.L1, RegularizationType.ELASTIC_NET):
             raise ValueError("TRON optimizer incompatible with L1 regularization")
         self.opt_config = opt_config
+        self._reset_warm_state()
+
+    def _reset_warm_state(self):
+        """Forget cached solver state (bucket W, segmented W, row-space beta, lazy primal model)."""
+        self._W = {}
+        self._returned = None
+        if getattr(self, "_rs", None) is not None:
+            self._rs.beta = None
 
     def initialize_model(self):
         ds = self.dataset
@@ -224,8 +233,17 @@ class RandomEffectCoordinate(Coordinate):
         reg, lam = cfg.regularization_context, cfg.regularization_weight
         l1, l2 = reg.l1_weight(lam), reg.l2_weight(lam)
         offs = self.base_offsets if partial_score is None else self.base_offsets + partial_score.to(self.device)
-        if ds.layout == "segmented":
-            return self._update_segmented(model, offs, l1, l2)
+        if model is None or model is not self._returned:
+            # the cached solver state belongs to the model this coordinate returned last; any other starting model
+            # (a fresh start, another configuration's best model) is mapped from its coefficients instead
+            self._reset_warm_state()
+        out = (self._update_segmented(model, offs, l1, l2) if ds.layout == "segmented"
+               else self._update_buckets(model, offs, l1, l2))
+        self._returned = out
+        return out
+
+    def _update_buckets(self, model, offs, l1: float, l2: float):
+        ds, cfg = self.dataset, self.opt_config
         keys, vals, vars_ = [], [], []
         iters, reasons = [], []
         t_start = time.time()

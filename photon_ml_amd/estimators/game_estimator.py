@@ -26,7 +26,7 @@ import torch
 
 from ..algorithm.coordinate_descent import CoordinateDescent
 from ..algorithm.coordinates import FixedEffectCoordinate, RandomEffectCoordinate, ShardedRandomEffectCoordinate
-from ..constants import TaskType
+from ..constants import RANDOM_SEED, TaskType
 from ..data.game_data import GameData
 from ..data.matrix import LabeledData
 from ..data.random_effect import FixedEffectDataConfiguration, RandomEffectDataConfiguration
@@ -170,6 +170,13 @@ class GameEstimator:
         train_eval = build_evaluator(training_loss_evaluator_type(self.training_task), data.response, data.offsets,
                                      data.weights)
         val_evals = self._validation_evaluators(validation) if validation is not None else []
+        if val_evals:
+            # random-guess baseline of every validation metric (GameEstimator.scala:496-500)
+            gen = torch.Generator().manual_seed(RANDOM_SEED)
+            rnd = torch.rand(validation.n_rows, generator=gen, dtype=torch.float64)
+            for e in val_evals:
+                log.info("Random guessing based baseline evaluation metric for %s: %s", e.name,
+                         e.evaluate(rnd))
         results, prev = [], getattr(self, "initial_model", None)
         for i, cfg in enumerate(configurations):
             for cid, c in self.coordinates.items():

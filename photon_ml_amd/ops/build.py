@@ -18,7 +18,6 @@ from pathlib import Path
 PKG = Path(__file__).resolve().parents[1]
 HIP_SOURCES = {
     "glm": PKG / "ops" / "csrc" / "glm_kernels.hip",
-    "batched": PKG / "ops" / "csrc" / "batched_glm.hip",
 }
 CPP_SOURCES = {
     "avro": PKG / "io" / "csrc" / "avro_codec.cpp",

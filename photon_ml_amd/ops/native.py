@@ -318,10 +318,6 @@ def seg_cg_step(ptr: torch.Tensor, step: torch.Tensor, r: torch.Tensor, d: torch
     on.copy_((act & ~hit).to(torch.uint8))
 
 
-def batched_lib() -> Optional[ctypes.CDLL]:
-    return _load("batched")
-
-
 def check(rc: int, what: str):
     if rc != 0:
         raise RuntimeError(f"{what} failed with HIP error {rc}")

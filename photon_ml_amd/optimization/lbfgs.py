@@ -226,7 +226,9 @@ class OWLQN(LBFGS):
         x0 = state.coefficients
         pg = state.gradient
         orthant = torch.where(x0 != 0, torch.sign(x0), torch.sign(-pg))
-        t0 = 1.0 / _norm(d) if self._inner_iter == 0 else 1.0
+        # first trial as Breeze OWLQN.determineStepSize: 0.5 / ||adjusted gradient|| on iteration 0, else 1
+        # first trial as Breeze OWLQN.determineStepSize: 0.5 / ||adjusted gradient|| on iteration 0, else 1
+        t0 = 0.5 / _norm(pg) if self._inner_iter == 0 else 1.0
         shrink = 0.1 if self._inner_iter < 1 else 0.5
 
         def phi(t):

@@ -30,14 +30,30 @@ def _rank() -> int:
     return rank()
 
 
+def _world() -> int:
+    from ..parallel.dist import world_size
+    return world_size()
+
+
 def _strings_to_array(values) -> np.ndarray:
-    return np.frombuffer("\n".join(str(v) for v in values).encode("utf-8"), dtype=np.uint8).copy()
+    """Length-prefixed UTF-8 strings: ``[n, len_0 .. len_{n-1}]`` as little-endian int64 bytes, then the data
+    (ids may contain any character, including newlines)."""
+    enc = [str(v).encode("utf-8") for v in values]
+    head = np.array([len(enc)] + [len(b) for b in enc], dtype="<i8").tobytes()
+    return np.frombuffer(head + b"".join(enc), dtype=np.uint8).copy()
 
 
 def _array_to_strings(a: np.ndarray, n: int) -> np.ndarray:
-    if n == 0:
-        return np.zeros(0, dtype=object)
-    return np.array(bytes(a.tobytes()).decode("utf-8").split("\n"), dtype=object)
+    raw = bytes(np.ascontiguousarray(a).tobytes())
+    count = int(np.frombuffer(raw[:8], dtype="<i8")[0]) if len(raw) >= 8 else -1
+    if count != n:
+        raise ValueError(f"checkpoint entity table holds {count} ids, metadata says {n}")
+    lens = np.frombuffer(raw[8:8 + 8 * n], dtype="<i8")
+    ends = 8 + 8 * n + np.cumsum(lens)
+    if n and ends[-1] != len(raw):
+        raise ValueError("checkpoint entity table is truncated or corrupt")
+    starts = ends - lens
+    return np.array([raw[s:e].decode("utf-8") for s, e in zip(starts, ends)], dtype=object)
 
 
 def game_model_to_arrays(model, prefix: str) -> Tuple[Dict[str, np.ndarray], dict]:
@@ -127,7 +143,7 @@ class Checkpointer:
                 tag: str = ""):
         arrays, meta = game_model_to_arrays(model, "model/")
         meta = {"model": meta, "iteration": iteration, "next": next_coordinate, "tag": tag,
-                "history": history, "best_evals": best_evals}
+                "history": history, "best_evals": best_evals, "world_size": _world()}
         if best_model is not None:
             ba, bm = game_model_to_arrays(best_model, "best/")
             arrays.update(ba)
@@ -139,6 +155,10 @@ class Checkpointer:
         if got is None:
             return None
         arrays, meta = got
+        if meta.get("world_size", 1) != _world():
+            # entity-sharded random effects: each rank's file holds the entities that rank owned
+            raise RuntimeError(f"checkpoint {self.path} was written by {meta.get('world_size', 1)} ranks, "
+                               f"this run has {_world()}: resume with the same world size")
         model = game_model_from_arrays(arrays, meta["model"], "model/")
         best = game_model_from_arrays(arrays, meta["best"], "best/") if "best" in meta else None
         return {"model": model, "iteration": meta["iteration"], "next": meta["next"], "best_model": best,

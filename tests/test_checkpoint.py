@@ -128,3 +128,16 @@ def test_glm_problem_checkpointed_run_resumes(tmp_path):
     GLMOptimizationProblem(short, "LOGISTIC_REGRESSION").enable_checkpointing(ck, 2).run(gd)
     resumed = GLMOptimizationProblem(cfg, "LOGISTIC_REGRESSION").enable_checkpointing(ck, 2).run(gd)
     assert torch.equal(full.coefficients.means, resumed.coefficients.means)
+
+
+def test_entity_ids_round_trip_any_characters_and_world_size_guard(tmp_path, monkeypatch):
+    from photon_ml_amd.utils import checkpoint as ck
+    ids = ["a", "", "line\nbreak", "ünïcode", "x" * 300]
+    arr = ck._strings_to_array(ids)
+    assert list(ck._array_to_strings(arr, len(ids))) == ids
+    with pytest.raises(ValueError):
+        ck._array_to_strings(arr, len(ids) - 1)
+    c = ck.Checkpointer(str(tmp_path))
+    c.save({"x": np.zeros(1)}, {"model": {"coordinates": []}, "iteration": 0, "next": 0, "world_size": 2})
+    with pytest.raises(RuntimeError, match="world size"):
+        c.load_cd()

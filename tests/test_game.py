@@ -219,3 +219,48 @@ def test_row_space_lazy_primal_model(monkeypatch):
     assert ar1 == pytest.approx(br1, rel=1e-9) and ar2 == pytest.approx(br2, rel=1e-9)
     np.testing.assert_allclose(b2.values, a2.values, rtol=1e-8, atol=1e-10)
     assert b2.materialized
+
+
+@pytest.mark.parametrize("layout", ["dense", "segmented"])
+def test_random_effect_reused_coordinate_starts_from_given_model(layout):
+    """A coordinate reused across configurations (GameEstimator.fit) must start from the model it is GIVEN, not
+    from the solver state of its previous solve: a zero initial model after a solve == a fresh coordinate."""
+    data, _ = generate_game_data(n_rows=1200, n_users=40, d_user=8, seed=41, task="LOGISTIC_REGRESSION")
+    cfg1, cfg2 = _cfg("TRON", 0.3, 2, 1e-12), _cfg("TRON", 3.0, 2, 1e-12)
+    dc = RandomEffectDataConfiguration("userId", "user")
+    reused = RandomEffectCoordinate("u", data, dc, cfg1, "LOGISTIC_REGRESSION", device="cpu", layout=layout)
+    reused.update_model(reused.initialize_model())
+    reused.set_config(cfg2)
+    got = reused.update_model(reused.initialize_model())
+    fresh = RandomEffectCoordinate("u", data, dc, cfg2, "LOGISTIC_REGRESSION", device="cpu", layout=layout)
+    want = fresh.update_model(fresh.initialize_model())
+    for e in want.entity_ids:
+        np.testing.assert_allclose(got.coefficients_of(e).means.numpy(), want.coefficients_of(e).means.numpy(),
+                                   rtol=1e-10, atol=1e-12)
+    # the coordinate's own last model still warm-starts from the cached state (same result as mapping it)
+    again = reused.update_model(got)
+    mapped = fresh.update_model(want)
+    for e in want.entity_ids:
+        np.testing.assert_allclose(again.coefficients_of(e).means.numpy(), mapped.coefficients_of(e).means.numpy(),
+                                   rtol=1e-6, atol=1e-8)
+
+
+def test_estimator_without_warm_start_matches_fresh_fit():
+    from photon_ml_amd.estimators.game_estimator import GameEstimator
+    data, _ = generate_game_data(n_rows=1500, n_users=30, seed=42, task="LOGISTIC_REGRESSION")
+    dcs = OrderedDict([("global", FixedEffectDataConfiguration("global")),
+                       ("per-user", RandomEffectDataConfiguration("userId", "user"))])
+    cfgs = [{"global": _cfg("LBFGS", lam, 5, 1e-12), "per-user": _cfg("TRON", lam, 3, 1e-12)} for lam in (0.1, 5.0)]
+
+    def fit(cs):
+        est = (GameEstimator(device="cpu").set_training_task("LOGISTIC_REGRESSION")
+               .set_coordinate_data_configurations(dcs).set_coordinate_descent_iterations(2).set_warm_start(False))
+        return est.fit(data, None, cs)
+
+    both, alone = fit(cfgs), fit(cfgs[1:])
+    a, b = both[1].model, alone[0].model
+    torch.testing.assert_close(a.get("global").glm.coefficients.means, b.get("global").glm.coefficients.means,
+                               rtol=1e-9, atol=1e-11)
+    for e in b.get("per-user").entity_ids:
+        np.testing.assert_allclose(a.get("per-user").coefficients_of(e).means.numpy(),
+                                   b.get("per-user").coefficients_of(e).means.numpy(), rtol=1e-9, atol=1e-11)
