@@ -504,12 +504,14 @@ class ShardedRandomEffectCoordinate(Coordinate):
         return self.inner.initialize_model()
 
     def update_model(self, model, partial_score: Optional[torch.Tensor] = None):
-        p = None if partial_score is None else self.router.forward(partial_score.detach().to("cpu", torch.float64))
+        # partial scores go to the entity owners on the device (no host staging under RCCL, see RowRouter)
+        p = None if partial_score is None else self.router.forward(
+            partial_score.detach().to(self.device, torch.float64))
         return self.inner.update_model(model, p)
 
     def score(self, model) -> torch.Tensor:
-        s = self.inner.score(model).detach().to("cpu", torch.float64)
-        return self.router.backward(s).to(self.device)
+        s = self.inner.score(model).detach().to(self.device, torch.float64)
+        return self.router.backward(s)
 
     def score_validation(self, model, vdata: GameData) -> torch.Tensor:
         """Route validation rows to entity owners once (cached per dataset), score there, route back."""
@@ -520,8 +522,8 @@ class ShardedRandomEffectCoordinate(Coordinate):
             router = RowRouter(self.partitioner.owner(stable_hash64(ids)))
             self._val_cache[key] = (router, self._route(vdata, router, ids))
         router, recv = self._val_cache[key]
-        s = model.score(recv, "cpu").to(torch.float64)
-        return router.backward(s).to(self.device)
+        s = model.score(recv, self.device).to(torch.float64)
+        return router.backward(s)
 
     def regularization_term_value(self, model) -> float:
         from ..parallel.dist import all_reduce_scalar

@@ -1,7 +1,9 @@
 """Synthetic data generators.
 
-* :func:`generate_glm_data` — host (scipy) generator of benign/outlier/invalid binary, linear and Poisson data in
-  the spirit of ``photon-test-utils/.../SparkTestUtils.scala:85-308`` (seeded, sparse features, intercept).
+* :func:`generate_glm_data` — host (scipy) generator of binary, linear and Poisson data from a random ground
+  truth (seeded, sparse features, intercept).
+* :func:`draw_samples` — the reference's benign / outlier / invalid-feature / invalid-label test families
+  (``photon-test-utils/.../SparkTestUtils.scala:85-308``).
 * :func:`generate_device_shard` — ON-DEVICE generator of the benchmark shard (BASELINE config "logistic L-BFGS
   1B x 1M sparse", 125M rows per GPU at 8 GPUs). It writes the chunked CSR/CSC streams of
   :class:`~photon_ml_amd.ops.device.DeviceGLMData` directly in HBM without any host round trip of the entries.
@@ -22,6 +24,78 @@ import torch
 
 from ..constants import TaskType
 from .matrix import LabeledData
+
+
+# SparkTestUtils constants (photon-test-utils/.../SparkTestUtils.scala:310-316)
+INLIER_PROBABILITY = 0.90
+INLIER_STANDARD_DEVIATION = 1e-3
+OUTLIER_STANDARD_DEVIATION = 1.0
+SAMPLE_KINDS = ("benign", "outlier", "invalid_features", "invalid_labels")
+
+
+def draw_samples(task, kind: str, seed: int, size: int, dimensionality: int,
+                 desired_sparsity: float = 0.1) -> LabeledData:
+    """Reference test-data families (``SparkTestUtils.scala:85-308, 320-873``): one row per sample, column 0 the
+    label-correlated attribute, every other column present with probability ``desired_sparsity`` (the
+    reference's negative-binomial skip-ahead coin toss).
+
+    * ``benign``: dummy columns uniform in [-1, 1);
+    * ``outlier``: dummy columns ``N(0, 1e-3)`` with probability 0.9, else +-1 (and, for linear regression, the
+      attribute carries unit-variance noise);
+    * ``invalid_features``: as outlier but the 10 % are NaN / +inf / -inf, plus NaN, +inf, -inf in the last three
+      columns of every row;
+    * ``invalid_labels``: benign features, labels drawn from {+inf, -inf, NaN}.
+
+    Labels: binary classification 1/0 with probability 0.5 and a strictly separable attribute +-[0.1, 1);
+    Poisson ``1 + 10 u`` with attribute ``log(label) / log(11)``; linear ``2u - 1`` (benign) or ``1 + u``.
+    The RNG is numpy's (the reference's Well19937a streams are not reproduced), the families are."""
+    task = TaskType.parse(task)
+    if kind not in SAMPLE_KINDS:
+        raise ValueError(f"unknown sample kind {kind!r}, expected one of {SAMPLE_KINDS}")
+    rng = np.random.default_rng(5000 * seed)
+    n, d = int(size), int(dimensionality)
+    u = rng.random(n)
+    binary = task in (TaskType.LOGISTIC_REGRESSION, TaskType.SMOOTHED_HINGE_LOSS_LINEAR_SVM)
+    if kind == "invalid_labels":
+        y = np.array([np.inf, -np.inf, np.nan])[rng.integers(0, 3, n)]
+        x0 = 0.1 + 0.9 * u
+    elif binary:
+        y = (rng.random(n) <= 0.5).astype(np.float64)
+        x0 = np.where(y == 1.0, 1.0, -1.0) * (0.1 + 0.9 * u)
+    elif task == TaskType.POISSON_REGRESSION:
+        y = 1.0 + 10.0 * u
+        x0 = (np.log(y) + rng.normal(size=n) * INLIER_STANDARD_DEVIATION) / np.log(11.0)
+    elif kind == "benign":
+        y = 2.0 * u - 1.0
+        x0 = y + rng.normal(size=n) * INLIER_STANDARD_DEVIATION
+    else:
+        y = 1.0 + u
+        x0 = y - 1.0 + rng.normal(size=n) * OUTLIER_STANDARD_DEVIATION
+    tail_end = d - 3 if kind == "invalid_features" else d
+    mask = rng.random((n, max(tail_end - 1, 0))) < desired_sparsity
+    rows, cols = np.nonzero(mask)
+    cols = cols + 1
+    k = rows.size
+    if kind in ("benign", "invalid_labels"):
+        vals = 2.0 * (rng.random(k) - 0.5)
+    else:
+        inlier = rng.random(k) < INLIER_PROBABILITY
+        if kind == "outlier":
+            bad = np.where(rng.random(k) < 0.5, 1.0, -1.0)
+        else:
+            bad = np.array([np.nan, np.inf, -np.inf])[rng.integers(0, 3, k)]
+        vals = np.where(inlier, rng.normal(size=k) * INLIER_STANDARD_DEVIATION, bad)
+    r_all = [np.arange(n), rows]
+    c_all = [np.zeros(n, np.int64), cols]
+    v_all = [x0, vals]
+    if kind == "invalid_features":
+        for j, v in zip((d - 3, d - 2, d - 1), (np.nan, np.inf, -np.inf)):
+            r_all.append(np.arange(n))
+            c_all.append(np.full(n, j))
+            v_all.append(np.full(n, v))
+    x = sp.csr_matrix((np.concatenate(v_all), (np.concatenate(r_all), np.concatenate(c_all))), shape=(n, d))
+    x.sort_indices()
+    return LabeledData(x, y)
 
 
 def generate_glm_data(task, n_rows: int, n_features: int, density: float = 0.2, seed: int = 7,

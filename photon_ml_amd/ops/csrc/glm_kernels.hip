@@ -950,6 +950,125 @@ __device__ __forceinline__ void tl_stream_il(const uint32_t* __restrict__ pack, 
   if (abl & 16) atomicAdd(&acc[lane], regsum);
 }
 
+// Deep-pipelined interleaved stream (P = 5): S stream slots in flight per wave and the gathers of round r + D
+// issued before round r is accumulated, so each wave keeps S rounds of stream and D + 1 rounds of gathers
+// outstanding instead of exposing one gather latency per round (tl_stream_il waits for the gathers it has just
+// issued). Slots are a compile-time ring (fully unrolled -> registers). Same entry order per wave as
+// tl_stream_il, so the result is bitwise identical.
+template <typename VT, typename XT, typename AT, bool SQ, int NW, int S, int D>
+__device__ __forceinline__ void tl_stream_il_deep(const uint32_t* __restrict__ pack, const VT* __restrict__ val,
+                                                  const XT* __restrict__ x, int e_lo, int e_hi, int sbits,
+                                                  AT* acc) {
+  static_assert(D < S && S % (D + 1) == 0, "gathers run ahead of loaded slots; the gather ring divides the slots");
+  typedef typename TLValT<VT>::T LT;
+  typedef typename TLVals<VT>::Raw Raw;
+  const int lane = threadIdx.x & 63, w = threadIdx.x >> 6;
+  const uint32_t smask = (1u << sbits) - 1u;
+  const int nr = (e_hi - e_lo + TL_ROUND - 1) / TL_ROUND;
+  const int r0 = (nr * w) / NW, r1 = (nr * (w + 1)) / NW;
+  if (r0 >= r1) return;
+  v4u pk[S];
+  Raw vr[S];
+  XT xg[D + 1][TL_VEC];
+  auto load_round = [&](int r, v4u& p, Raw& v) {
+    const int rr = r < r1 ? r : r1 - 1;  // past the end: re-read the last round (L2-hot, never used)
+    const int e = e_lo + rr * TL_ROUND + lane * TL_VEC;
+    p = ldg_nt((const v4u*)(pack + e));
+    v = TLVals<VT>::load(val + e);
+  };
+  auto gather = [&](int r, const v4u& p, XT* xv) {
+    const int e = e_lo + r * TL_ROUND + lane;
+#pragma unroll
+    for (int k = 0; k < TL_VEC; ++k) xv[k] = ldg(x + ((e + 64 * k < e_hi && r < r1) ? (p[k] >> sbits) : 0u));
+  };
+#pragma unroll
+  for (int i = 0; i < S; ++i) load_round(r0 + i, pk[i], vr[i]);
+#pragma unroll
+  for (int i = 0; i < D; ++i) gather(r0 + i, pk[i], xg[i]);
+  for (int r = r0; r < r1; r += S) {
+#pragma unroll
+    for (int i = 0; i < S; ++i) {
+      const int rc = r + i;
+      if (rc >= r1) break;
+      // gathers of round rc + D (its stream slot arrived S - D rounds ago)
+      gather(rc + D, pk[(i + D) % S], xg[(i + D) % (D + 1)]);
+      const v4u p = pk[i];
+      const Raw v_raw = vr[i];
+      load_round(rc + S, pk[i], vr[i]);
+      LT v[TL_VEC];
+      TLVals<VT>::get(v_raw, v);
+      const int e = e_lo + rc * TL_ROUND + lane;
+#pragma unroll
+      for (int k = 0; k < TL_VEC; ++k) {
+        const bool in = e + 64 * k < e_hi;
+        const AT vv = SQ ? static_cast<AT>(v[k]) * static_cast<AT>(v[k]) : static_cast<AT>(v[k]);
+        const AT add = in ? vv * static_cast<AT>(xg[i % (D + 1)][k]) : AT(0);
+        atomicAdd(&acc[in ? (p[k] & smask) : 0u], add);
+      }
+    }
+  }
+}
+
+// NARROW rounds (ops/tiled.py, "narrow section" of a work unit): a round of 256 sorted entries whose gather keys
+// span fewer than 64 values is stored with 16-bit packs ((key - base) << sbits | slot) plus one int32 base per
+// round. Instead of four 64-lane gathers (the texture-address-bound part of the wide rounds: TA 80-94 % busy in
+// profiles/pmc_tl_interleaved_4M.txt), the wave loads the round's whole key window x[base .. base+63] with ONE
+// coalesced dword load and every lane picks its values with ds_bpermute (__shfl) from the window's lanes:
+// 3 vector-memory instructions per round instead of 6, and 4 B/entry of stream instead of 6 (bf16).
+// The layout builder guarantees base + 63 < len(x), so the window load is always in bounds. Bases are fetched 64
+// rounds at a time (one coalesced load) and broadcast with readlane. Accumulation order per wave is fixed, as in
+// the wide stream (deterministic).
+template <typename T> __device__ __forceinline__ T lane_bcast(T v, int src) { return __shfl(v, src, 64); }
+
+template <typename VT, typename XT, typename AT, bool SQ, int NW, int S = 2>
+__device__ __forceinline__ void tl_stream_narrow(const uint16_t* __restrict__ npk, const VT* __restrict__ nvl,
+                                                 const int* __restrict__ nbs, int n_lo, int n_hi, int sbits,
+                                                 const XT* __restrict__ x, AT* acc) {
+  typedef typename TLValT<VT>::T LT;
+  typedef typename TLVals<VT>::Raw Raw;
+  const int lane = threadIdx.x & 63, w = threadIdx.x >> 6;
+  const int nr = n_hi - n_lo;
+  const int r0 = n_lo + (nr * w) / NW, r1 = n_lo + (nr * (w + 1)) / NW;
+  const uint32_t smask = (1u << sbits) - 1u;
+  for (int rb = r0; rb < r1; rb += 64) {
+    const int re = min(rb + 64, r1);
+    const int bases = ldg(nbs + min(rb + lane, re - 1));
+    v2u pks[S];
+    Raw vs[S];
+    XT xs[S];
+    auto load_round = [&](int r, v2u& pk, Raw& v, XT& xw) {
+      const size_t e = (size_t)r * TL_ROUND + lane * TL_VEC;
+      pk = ldg_nt((const v2u*)(npk + e));
+      v = TLVals<VT>::load(nvl + e);
+      const int base = __builtin_amdgcn_readlane(bases, r - rb);
+      xw = ldg(x + base + lane);
+    };
+    auto process = [&](int r, v2u& pk_slot, Raw& v_slot, XT& x_slot) {
+      const v2u pk = pk_slot;
+      const Raw v_raw = v_slot;
+      const XT xw = x_slot;
+      if (r + S < re) load_round(r + S, pk_slot, v_slot, x_slot);
+      LT v[TL_VEC];
+      TLVals<VT>::get(v_raw, v);
+      const uint32_t p[TL_VEC] = {pk.x & 0xffffu, pk.x >> 16, pk.y & 0xffffu, pk.y >> 16};
+#pragma unroll
+      for (int k = 0; k < TL_VEC; ++k) {
+        const XT xv = lane_bcast(xw, (int)(p[k] >> sbits));
+        const AT vv = SQ ? static_cast<AT>(v[k]) * static_cast<AT>(v[k]) : static_cast<AT>(v[k]);
+        atomicAdd(&acc[p[k] & smask], vv * static_cast<AT>(xv));
+      }
+    };
+#pragma unroll
+    for (int i = 0; i < S; ++i)
+      if (rb + i < re) load_round(rb + i, pks[i], vs[i], xs[i]);
+    for (int r = rb; r < re; r += S) {
+#pragma unroll
+      for (int i = 0; i < S; ++i)
+        if (r + i < re) process(r + i, pks[i], vs[i], xs[i]);
+    }
+  }
+}
+
 // pipeline variant: P = 0 two-slot stream prefetch; P = 1 three-stage (stream r+2 / gather r+1 / accumulate r);
 // P = 2 two-slot, 8 entries per lane; P = 3 lane-interleaved layout (tl_stream_il)
 template <typename VT, typename XT, typename AT, bool SQ, int U, int NW, int P>
@@ -959,13 +1078,19 @@ __device__ __forceinline__ void tl_stream(const uint32_t* __restrict__ pack, con
   else if (P == 2) tl_stream_wide<VT, XT, AT, SQ, NW, 2>(pack, val, x, e_lo, e_hi, sbits, acc);
   else if (P == 3) tl_stream_il<VT, XT, AT, SQ, NW>(pack, val, x, e_lo, e_hi, sbits, acc);
   else if (P == 4) tl_stream_il<VT, XT, AT, SQ, NW, true>(pack, val, x, e_lo, e_hi, sbits, acc);
+  else if (P == 5) tl_stream_il_deep<VT, XT, AT, SQ, NW, 4, 1>(pack, val, x, e_lo, e_hi, sbits, acc);
+  else if (P == 6) tl_stream_il_deep<VT, XT, AT, SQ, NW, 6, 2>(pack, val, x, e_lo, e_hi, sbits, acc);
   else tl_stream_p0<VT, XT, AT, SQ, U, NW>(pack, val, x, e_lo, e_hi, sbits, acc);
 }
 
-// Forward over row blocks. blk: 4 ints per block {row_lo, nrows, e_lo, e_hi} (chunk-local).
+// Narrow-section streams of one chunk (see tl_stream_narrow); n_lo == n_hi: the unit has no narrow rounds.
+struct TLNarrow { const uint16_t* pack; const void* val; const int* base; };
+
+// Forward over row blocks. blk: 6 ints per block {row_lo, nrows, e_lo, e_hi, n_lo, n_hi} (chunk-local).
 template <typename VT, typename XT, typename RT, typename AT, int MAXR, int U, int NW, int P>
-__device__ __forceinline__ void tl_fwd_block(int b, int row_lo, int nrows, int e_lo, int e_hi, int rbits,
-                                             const uint32_t* __restrict__ pack, const VT* __restrict__ val,
+__device__ __forceinline__ void tl_fwd_block(int b, int row_lo, int nrows, int e_lo, int e_hi, int n_lo, int n_hi,
+                                             int rbits, const uint32_t* __restrict__ pack,
+                                             const VT* __restrict__ val, const TLNarrow& nar,
                                              const XT* __restrict__ x, const FwdArgs<XT, RT>& a,
                                              double* __restrict__ stats, AT (*acc)[MAXR], double* red) {
   const int R = 1 << rbits;
@@ -973,6 +1098,10 @@ __device__ __forceinline__ void tl_fwd_block(int b, int row_lo, int nrows, int e
 #pragma unroll
     for (int w = 0; w < NW; ++w) acc[w][i] = AT(0);
   __syncthreads();
+  if (n_hi > n_lo)
+    tl_stream_narrow<VT, XT, AT, false, NW, (P >= 5 ? 4 : 2)>(nar.pack, (const VT*)nar.val, nar.base, n_lo, n_hi,
+                                                              rbits, x,
+                                            acc[threadIdx.x >> 6]);
   tl_stream<VT, XT, AT, false, U, NW, P>(pack, val, x, e_lo, e_hi, rbits, acc[threadIdx.x >> 6]);
   __syncthreads();
   double F = 0.0, S = 0.0;
@@ -992,45 +1121,52 @@ __device__ __forceinline__ void tl_fwd_block(int b, int row_lo, int nrows, int e
 template <typename VT, typename XT, typename RT, typename AT, int MAXR, int U, int NW, int P>
 __global__ __launch_bounds__(NW * 64) void tl_fwd_kernel(const int* __restrict__ blk, int rbits,
                                                           const uint32_t* __restrict__ pack,
-                                                          const VT* __restrict__ val, const XT* __restrict__ x,
-                                                          FwdArgs<XT, RT> a, double* __restrict__ stats) {
+                                                          const VT* __restrict__ val, TLNarrow nar,
+                                                          const XT* __restrict__ x, FwdArgs<XT, RT> a,
+                                                          double* __restrict__ stats) {
   __shared__ AT acc[NW][MAXR];
   __shared__ double red[2 * NW];
   const int b = blockIdx.x;
-  tl_fwd_block<VT, XT, RT, AT, MAXR, U, NW, P>(b, blk[4 * b], blk[4 * b + 1], blk[4 * b + 2], blk[4 * b + 3],
-                                              rbits, pack, val, x, a, stats, acc, red);
+  const int* q = blk + 6 * b;
+  tl_fwd_block<VT, XT, RT, AT, MAXR, U, NW, P>(b, q[0], q[1], q[2], q[3], q[4], q[5], rbits, pack, val, nar, x, a,
+                                              stats, acc, red);
 }
 
-// All chunks of a shard in ONE launch (no per-chunk tails / launch gaps): block table of 6 ints
-// {chunk, global row_lo, nrows, e_lo, e_hi, col_lo}; per-chunk stream pointers in device arrays; row-data
-// pointers in ``a`` are shard-global; stats index = global block index.
+// All chunks of a shard in ONE launch (no per-chunk tails / launch gaps): block table of 8 ints
+// {chunk, global row_lo, nrows, e_lo, e_hi, col_lo, n_lo, n_hi}; per-chunk stream pointers in device arrays
+// (ptrs[5 * chunk + {0: pack, 1: val, 2: narrow pack, 3: narrow val, 4: narrow base}]); row-data pointers in ``a``
+// are shard-global; stats index = global block index.
 template <typename VT, typename XT, typename RT, typename AT, int MAXR, int U, int NW, int P>
 __global__ __launch_bounds__(NW * 64) void tl_fwd_multi_kernel(const int* __restrict__ blk, int rbits,
-                                                                const unsigned long long* __restrict__ packs,
-                                                                const unsigned long long* __restrict__ vals,
+                                                                const unsigned long long* __restrict__ ptrs,
                                                                 const XT* __restrict__ x, FwdArgs<XT, RT> a,
                                                                 double* __restrict__ stats) {
   __shared__ AT acc[NW][MAXR];
   __shared__ double red[2 * NW];
   const int b = blockIdx.x;
-  const int* q = blk + 6 * b;
-  const int c = q[0];
-  tl_fwd_block<VT, XT, RT, AT, MAXR, U, NW, P>(b, q[1], q[2], q[3], q[4], rbits, (const uint32_t*)packs[c],
-                                              (const VT*)vals[c], x + q[5], a, stats, acc, red);
+  const int* q = blk + 8 * b;
+  const unsigned long long* pc = ptrs + 5 * q[0];
+  const TLNarrow nar = {(const uint16_t*)pc[2], (const void*)pc[3], (const int*)pc[4]};
+  tl_fwd_block<VT, XT, RT, AT, MAXR, U, NW, P>(b, q[1], q[2], q[3], q[4], q[6], q[7], rbits, (const uint32_t*)pc[0],
+                                              (const VT*)pc[1], nar, x + q[5], a, stats, acc, red);
 }
 
 // Transpose over column-tile items. items: 4 ints {tile, e_lo, e_hi, part}; part < 0: the item is its tile's
 // only one -> G[tile cols] += sums directly; else the item's row of partial sums goes to parts[part * C ...].
 template <typename VT, typename XT, typename AT, bool SQ, int MAXR, int U, int NW, int P>
-__device__ __forceinline__ void tl_t_item(int tile, int e_lo, int e_hi, int part, int cbits,
+__device__ __forceinline__ void tl_t_item(int tile, int e_lo, int e_hi, int part, int n_lo, int n_hi, int cbits,
                                           const uint32_t* __restrict__ pack, const VT* __restrict__ val,
-                                          const XT* __restrict__ x, double* __restrict__ G, int dim,
-                                          double* __restrict__ parts, AT (*acc)[MAXR]) {
+                                          const TLNarrow& nar, const XT* __restrict__ x, double* __restrict__ G,
+                                          int dim, double* __restrict__ parts, AT (*acc)[MAXR]) {
   const int C = 1 << cbits;
   for (int i = threadIdx.x; i < C; i += NW * 64)
 #pragma unroll
     for (int w = 0; w < NW; ++w) acc[w][i] = AT(0);
   __syncthreads();
+  if (n_hi > n_lo)
+    tl_stream_narrow<VT, XT, AT, SQ, NW, (P >= 5 ? 4 : 2)>(nar.pack, (const VT*)nar.val, nar.base, n_lo, n_hi,
+                                                           cbits, x,
+                                         acc[threadIdx.x >> 6]);
   tl_stream<VT, XT, AT, SQ, U, NW, P>(pack, val, x, e_lo, e_hi, cbits, acc[threadIdx.x >> 6]);
   __syncthreads();
   const int c0 = tile << cbits;
@@ -1049,27 +1185,30 @@ __device__ __forceinline__ void tl_t_item(int tile, int e_lo, int e_hi, int part
 template <typename VT, typename XT, typename AT, bool SQ, int MAXR, int U, int NW, int P>
 __global__ __launch_bounds__(NW * 64) void tl_t_kernel(const int* __restrict__ items, int cbits,
                                                         const uint32_t* __restrict__ pack,
-                                                        const VT* __restrict__ val, const XT* __restrict__ x,
-                                                        double* __restrict__ G, int dim, double* __restrict__ parts) {
+                                                        const VT* __restrict__ val, TLNarrow nar,
+                                                        const XT* __restrict__ x, double* __restrict__ G, int dim,
+                                                        double* __restrict__ parts) {
   __shared__ AT acc[NW][MAXR];
-  const int* q = items + 4 * blockIdx.x;
-  tl_t_item<VT, XT, AT, SQ, MAXR, U, NW, P>(q[0], q[1], q[2], q[3], cbits, pack, val, x, G, dim, parts, acc);
+  const int* q = items + 6 * blockIdx.x;
+  tl_t_item<VT, XT, AT, SQ, MAXR, U, NW, P>(q[0], q[1], q[2], q[3], q[4], q[5], cbits, pack, val, nar, x, G, dim,
+                                            parts, acc);
 }
 
-// All row chunks of a shard in one launch. items: 6 ints {chunk, tile, e_lo, e_hi, part, row_base}; a tile with a
-// single item in the whole shard writes G directly, every other item writes a partial row that the shard-wide
-// combine sums in (chunk, item) order — deterministic and race-free across chunks.
+// All row chunks of a shard in one launch. items: 8 ints {chunk, tile, e_lo, e_hi, part, row_base, n_lo, n_hi};
+// a tile with a single item in the whole shard writes G directly, every other item writes a partial row that the
+// shard-wide combine sums in (chunk, item) order — deterministic and race-free across chunks. Stream pointers as
+// in tl_fwd_multi_kernel (5 per chunk).
 template <typename VT, typename XT, typename AT, bool SQ, int MAXR, int U, int NW, int P>
 __global__ __launch_bounds__(NW * 64) void tl_t_multi_kernel(const int* __restrict__ items, int cbits,
-                                                              const unsigned long long* __restrict__ packs,
-                                                              const unsigned long long* __restrict__ vals,
+                                                              const unsigned long long* __restrict__ ptrs,
                                                               const XT* __restrict__ x, double* __restrict__ G,
                                                               int dim, double* __restrict__ parts) {
   __shared__ AT acc[NW][MAXR];
-  const int* q = items + 6 * blockIdx.x;
-  const int c = q[0];
-  tl_t_item<VT, XT, AT, SQ, MAXR, U, NW, P>(q[1], q[2], q[3], q[4], cbits, (const uint32_t*)packs[c],
-                                            (const VT*)vals[c], x + q[5], G, dim, parts, acc);
+  const int* q = items + 8 * blockIdx.x;
+  const unsigned long long* pc = ptrs + 5 * q[0];
+  const TLNarrow nar = {(const uint16_t*)pc[2], (const void*)pc[3], (const int*)pc[4]};
+  tl_t_item<VT, XT, AT, SQ, MAXR, U, NW, P>(q[1], q[2], q[3], q[4], q[6], q[7], cbits, (const uint32_t*)pc[0],
+                                            (const VT*)pc[1], nar, x + q[5], G, dim, parts, acc);
 }
 
 // Combine the partial rows of split tiles, deterministically, in two levels (a hot tile can have hundreds of
@@ -1106,18 +1245,20 @@ __global__ __launch_bounds__(NTHREADS) void tl_t_combine2_kernel(const int* __re
 }
 
 // ``il``: 1 = the streams are stored in the lane-interleaved layout (see tl_stream_il) -> pipeline P = 3.
-struct TLFwdDesc { const int* blk; int nblk; int rbits; const uint32_t* pack; const void* val; int il; };
-struct TLFwdMultiDesc { const int* blk; int nblk; int rbits; const unsigned long long* packs; const unsigned long long* vals; int il; };
+struct TLFwdDesc { const int* blk; int nblk; int rbits; const uint32_t* pack; const void* val; int il; TLNarrow nar; };
+// ptrs: 5 stream pointers per chunk (see tl_fwd_multi_kernel)
+struct TLFwdMultiDesc { const int* blk; int nblk; int rbits; const unsigned long long* ptrs; int il; };
 struct TLTDesc {
   const int* items; int nitems; int cbits; const uint32_t* pack; const void* val;
   const int* mt_tiles; const int* mt_ptr; int nmt; int dim;
   const int* cu; int ncu;     // level-1 combine units {tile, part_lo, part_hi}; mt_ptr indexes units
   int nparts_total;           // item partial rows (the level-1 rows follow them in the scratch buffer)
   int il;
+  TLNarrow nar;
 };
-// Shard-wide transpose: items of every chunk (6 ints, see tl_t_multi_kernel) with per-chunk stream pointers.
+// Shard-wide transpose: items of every chunk (8 ints, see tl_t_multi_kernel) with per-chunk stream pointers.
 struct TLTMultiDesc {
-  const int* items; int nitems; int cbits; const unsigned long long* packs; const unsigned long long* vals;
+  const int* items; int nitems; int cbits; const unsigned long long* ptrs;
   const int* mt_tiles; const int* mt_ptr; int nmt; int dim;
   const int* cu; int ncu; int nparts_total; int il;
 };
@@ -1135,14 +1276,17 @@ static int g_tl_waves_t = 4;   // transpose
 static int g_tl_pipe = 0;      // forward stream pipeline variant (see tl_stream)
 static int g_tl_pipe_t = 0;    // transpose stream pipeline variant
 static int g_rs_variant = 2;   // rs_tron_kernel variant (see the kernel); 2 measured fastest (scripts/rs_tron_bench.py)
-static int g_tl_dedup = 0;     // interleaved forward: gather dedup across lanes (P = 4)
-static int g_tl_dedup_t = 0;   // interleaved transpose: gather dedup
+static int g_tl_deep = 0;      // interleaved forward: 0 two-slot pipeline (P = 3), 1 deep S4/D1 (P = 5), 2 S6/D2 (P = 6)
+static int g_tl_deep_t = 0;    // interleaved transpose: same
 
 template <typename VT, typename XT, typename RT, typename AT, int MAXR>
 static void tl_fwd_launch(const TLFwdDesc* c, const void* x, FwdArgs<XT, RT> a, double* stats, hipStream_t st) {
 #define TLF(NW, P) hipLaunchKernelGGL((tl_fwd_kernel<VT, XT, RT, AT, MAXR, 2, NW, P>), dim3(c->nblk), dim3(NW * 64), 0, \
-                                    st, c->blk, c->rbits, c->pack, (const VT*)c->val, (const XT*)x, a, stats)
-  if (c->il) { if (g_tl_waves <= 2) { if (g_tl_dedup) TLF(2, 4); else TLF(2, 3); } else { if (g_tl_dedup) TLF(4, 4); else TLF(4, 3); } }
+                                    st, c->blk, c->rbits, c->pack, (const VT*)c->val, c->nar, (const XT*)x, a, stats)
+  if (c->il) {
+    if (g_tl_waves <= 2) { if (g_tl_deep == 2) TLF(2, 6); else if (g_tl_deep) TLF(2, 5); else TLF(2, 3); }
+    else { if (g_tl_deep == 2) TLF(4, 6); else if (g_tl_deep) TLF(4, 5); else TLF(4, 3); }
+  }
   else if (g_tl_waves == 2) { if (g_tl_pipe == 1) TLF(2, 1); else TLF(2, 0); }
   else { if (g_tl_pipe == 1) TLF(4, 1); else TLF(4, 0); }
 #undef TLF
@@ -1152,10 +1296,11 @@ template <typename VT, typename XT, typename RT, typename AT, int MAXR>
 static void tl_fwd_multi_launch(const TLFwdMultiDesc* c, const void* x, FwdArgs<XT, RT> a, double* stats,
                                 hipStream_t st) {
 #define TLM(NW, P) hipLaunchKernelGGL((tl_fwd_multi_kernel<VT, XT, RT, AT, MAXR, 2, NW, P>), dim3(c->nblk), \
-                                      dim3(NW * 64), 0, st, c->blk, c->rbits, c->packs, c->vals, (const XT*)x, a, stats)
+                                      dim3(NW * 64), 0, st, c->blk, c->rbits, c->ptrs, (const XT*)x, a, stats)
   if (c->il) {
-    if (g_tl_dedup) { if (g_tl_waves == 1) TLM(1, 4); else if (g_tl_waves == 2) TLM(2, 4); else TLM(4, 4); }
-    else { if (g_tl_waves == 1) TLM(1, 3); else if (g_tl_waves == 2) TLM(2, 3); else TLM(4, 3); }
+    if (g_tl_deep == 2) { if (g_tl_waves == 2) TLM(2, 6); else TLM(4, 6); }
+    else if (g_tl_deep) { if (g_tl_waves == 2) TLM(2, 5); else TLM(4, 5); }
+    else { if (g_tl_waves == 2) TLM(2, 3); else TLM(4, 3); }
   }
   else if (g_tl_waves == 2) { if (g_tl_pipe == 2) TLM(2, 2); else TLM(2, 0); }
   else { if (g_tl_pipe == 2) TLM(4, 2); else TLM(4, 0); }
@@ -1202,8 +1347,12 @@ static int tl_fwd_impl(const TLFwdDesc* c, const void* x, FwdArgs<XT, RT> a, dou
 template <typename VT, typename XT, typename AT, bool SQ, int MAXR>
 static void tl_t_launch(const TLTDesc* c, const void* x, double* G, double* parts, hipStream_t st) {
 #define TLT(NW, P) hipLaunchKernelGGL((tl_t_kernel<VT, XT, AT, SQ, MAXR, 2, NW, P>), dim3(c->nitems), dim3(NW * 64), 0, \
-                                    st, c->items, c->cbits, c->pack, (const VT*)c->val, (const XT*)x, G, c->dim, parts)
-  if (c->il) { if (g_tl_waves_t == 2) { if (g_tl_dedup_t) TLT(2, 4); else TLT(2, 3); } else { if (g_tl_dedup_t) TLT(4, 4); else TLT(4, 3); } }
+                                    st, c->items, c->cbits, c->pack, (const VT*)c->val, c->nar, (const XT*)x, G, c->dim, \
+                                    parts)
+  if (c->il) {
+    if (g_tl_waves_t == 2) { if (g_tl_deep_t == 2) TLT(2, 6); else if (g_tl_deep_t) TLT(2, 5); else TLT(2, 3); }
+    else { if (g_tl_deep_t == 2) TLT(4, 6); else if (g_tl_deep_t) TLT(4, 5); else TLT(4, 3); }
+  }
   else if (g_tl_waves_t == 2) { if (g_tl_pipe_t == 1) TLT(2, 1); else TLT(2, 0); }
   else { if (g_tl_pipe_t == 1) TLT(4, 1); else TLT(4, 0); }
 #undef TLT
@@ -1241,9 +1390,12 @@ static int tl_t_impl(const TLTDesc* c, const void* x, double* G, double* parts, 
 template <typename VT, typename XT, typename AT, bool SQ, int MAXR>
 static void tl_t_multi_launch(const TLTMultiDesc* c, const void* x, double* G, double* parts, hipStream_t st) {
 #define TLTM(NW, P) hipLaunchKernelGGL((tl_t_multi_kernel<VT, XT, AT, SQ, MAXR, 2, NW, P>), dim3(c->nitems), \
-                                       dim3(NW * 64), 0, st, c->items, c->cbits, c->packs, c->vals, (const XT*)x, G, \
+                                       dim3(NW * 64), 0, st, c->items, c->cbits, c->ptrs, (const XT*)x, G, \
                                        c->dim, parts)
-  if (c->il) { if (g_tl_waves_t == 2) { if (g_tl_dedup_t) TLTM(2, 4); else TLTM(2, 3); } else { if (g_tl_dedup_t) TLTM(4, 4); else TLTM(4, 3); } }
+  if (c->il) {
+    if (g_tl_waves_t == 2) { if (g_tl_deep_t == 2) TLTM(2, 6); else if (g_tl_deep_t) TLTM(2, 5); else TLTM(2, 3); }
+    else { if (g_tl_deep_t == 2) TLTM(4, 6); else if (g_tl_deep_t) TLTM(4, 5); else TLTM(4, 3); }
+  }
   else if (g_tl_waves_t == 2) { if (g_tl_pipe_t == 2) TLTM(2, 2); else TLTM(2, 0); }
   else { if (g_tl_pipe_t == 2) TLTM(4, 2); else TLTM(4, 0); }
 #undef TLTM
@@ -1819,7 +1971,7 @@ __global__ __launch_bounds__(256) void lincomb_kernel(VecSet vs, int k, long lon
 extern "C" {
 
 int pml_version() { return 1; }
-void pml_tl_set_dedup(int fwd, int t) { g_tl_dedup = fwd; g_tl_dedup_t = t; }
+void pml_tl_set_deep(int fwd, int t) { g_tl_deep = fwd; g_tl_deep_t = t; }
 
 void pml_set_ls_args(double* z0, double t0, double tpend) { g_ls_z0 = z0; g_ls_t0 = t0; g_ls_tpend = tpend; }
 

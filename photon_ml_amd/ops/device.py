@@ -180,12 +180,13 @@ class DeviceGLMData(GLMComputable):
                 raise ValueError(f"chunk {c}: forward block window outside the stream")
             if f.il and f.nblk and bool((b[:, 2] % 256 != 0).any()):
                 raise ValueError(f"chunk {c}: interleaved forward windows not round-aligned")
+            ncols = int(self.dim) - self.col_lo[c]
+            self._validate_narrow(c, f, b, ncols, "forward")
             pk, _ = f.logical()
             p = pk.cpu().to(torch.int64) & 0xFFFFFFFF
-            ncols = int(self.dim) - self.col_lo[c]
             if p.numel() and int((p >> f.rbits).max()) >= ncols:
                 raise ValueError(f"chunk {c}: forward gather index >= column window")
-            counts = (b[:, 3] - b[:, 2])
+            counts = f.unit_counts().cpu()
             blk_rows = torch.repeat_interleave(b[:, 1], counts)
             if p.numel() and bool(((p & ((1 << f.rbits) - 1)) >= blk_rows).any()):
                 raise ValueError(f"chunk {c}: forward LDS slot >= block rows")
@@ -195,16 +196,34 @@ class DeviceGLMData(GLMComputable):
                     raise ValueError(f"chunk {c}: transpose item window outside the stream")
                 if int(it[:, 3].max()) >= max(t.nparts, 1) and t.nparts:
                     raise ValueError(f"chunk {c}: transpose partial-row slot out of range")
+                self._validate_narrow(c, t, it, m, "transpose")
                 tp, _ = t.logical()
                 q = tp.cpu().to(torch.int64) & 0xFFFFFFFF
                 if q.numel() and int((q >> t.cbits).max()) >= m:
                     raise ValueError(f"chunk {c}: transpose gather row >= chunk rows")
-                cols = (torch.repeat_interleave(it[:, 0], it[:, 2] - it[:, 1]) << t.cbits) + (q & ((1 << t.cbits) - 1))
+                cols = (torch.repeat_interleave(it[:, 0], t.unit_counts().cpu()) << t.cbits) + (q & ((1 << t.cbits) - 1))
                 if q.numel() and int(cols.max()) >= t.dim:
                     raise ValueError(f"chunk {c}: transpose column >= dim")
         if self.parts.numel() < max([c.parts_needed for c in self.csr + self.csc] + [1]):
             raise ValueError("partial-row scratch too small")
         return True
+
+    @staticmethod
+    def _validate_narrow(c: int, ch, table: torch.Tensor, xlen: int, what: str):
+        """Narrow rounds: per-unit ranges consecutive inside the narrow stream, every key window
+        [base, base + 64) inside the gathered vector."""
+        if table.shape[0] == 0:
+            return
+        n_lo, n_hi = table[:, 4], table[:, 5]
+        nrounds = ch.nbase.numel() if ch.n_narrow_rounds else 0
+        if bool((n_hi < n_lo).any()) or int(n_hi.max()) > nrounds or bool((n_lo[1:] != n_hi[:-1]).any()):
+            raise ValueError(f"chunk {c}: {what} narrow round ranges inconsistent")
+        if nrounds:
+            base = ch.nbase.cpu().to(torch.int64)
+            if ch.npack.numel() < 256 * nrounds or ch.nval.numel() < 256 * nrounds:
+                raise ValueError(f"chunk {c}: {what} narrow stream shorter than its rounds")
+            if int(base.min()) < 0 or int(base.max()) + 64 > xlen:
+                raise ValueError(f"chunk {c}: {what} narrow key window outside the gathered vector")
 
     # ------------------------------------------------------------------
     @staticmethod
@@ -222,8 +241,18 @@ class DeviceGLMData(GLMComputable):
         x = data.x.tocsr()
         n, d = x.shape
         old_of_new = None
-        if relabel and x.nnz > 0:
-            counts = np.bincount(x.indices, minlength=d)
+        from ..parallel.dist import is_dist
+        shared = relabel and is_dist() and not col_windows
+        if shared or (relabel and x.nnz > 0):
+            counts = np.bincount(x.indices, minlength=d).astype(np.int64)
+            if shared:
+                # one feature order on every rank (summed counts): the data-parallel gradient all-reduce can then
+                # be bucketed and overlapped with the transpose pass (DistributedGLMData.overlap)
+                import torch.distributed as tdist
+                from ..parallel.sharding import comm_device
+                ct = torch.from_numpy(counts).to(comm_device())
+                tdist.all_reduce(ct)
+                counts = ct.cpu().numpy()
             old_of_new_np = np.argsort(-counts, kind="stable")
             new_of_old_np = np.empty(d, dtype=np.int64)
             new_of_old_np[old_of_new_np] = np.arange(d)
@@ -487,29 +516,29 @@ class DeviceGLMData(GLMComputable):
                                  self.parts.data_ptr(), stream_handle(self.device)), "seg_t")
 
     def _build_multi(self):
-        """One-launch forward over all TL chunks (block table {chunk, row_lo, nrows, e_lo, e_hi, col_lo})."""
+        """One-launch forward over all TL chunks (block table {chunk, row_lo, nrows, e_lo, e_hi, col_lo, n_lo,
+        n_hi})."""
         self._multi = None
         if not self.csr or any(ch.kind != "tl" for ch in self.csr) or len({ch.rbits for ch in self.csr}) != 1:
             return
         tabs = []
         for c, ch in enumerate(self.csr):
             b = ch.blk.to(torch.int64)
-            t = torch.empty((b.shape[0], 6), dtype=torch.int64, device=b.device)
+            t = torch.empty((b.shape[0], 8), dtype=torch.int64, device=b.device)
             t[:, 0] = c
             t[:, 1] = b[:, 0] + self.row_starts[c]
             t[:, 2:5] = b[:, 1:4]
             t[:, 5] = self.col_lo[c]
+            t[:, 6:8] = b[:, 4:6]
             tabs.append(t)
         self._multi_blk = torch.cat(tabs).to(torch.int32).contiguous()
-        self._multi_packs = torch.tensor([ch.pack.data_ptr() for ch in self.csr], dtype=torch.int64,
-                                         device=self.device)
-        self._multi_vals = torch.tensor([ch.val.data_ptr() for ch in self.csr], dtype=torch.int64,
-                                        device=self.device)
+        from .tiled import stream_ptr_table
+        self._multi_ptrs = stream_ptr_table(self.csr, self.device)
         from .native import TLFwdMultiDesc
         if len({ch.il for ch in self.csr}) != 1:
             return
         self._multi = TLFwdMultiDesc(self._multi_blk.data_ptr(), self._multi_blk.shape[0], self.csr[0].rbits,
-                                     self._multi_packs.data_ptr(), self._multi_vals.data_ptr(), self.csr[0].il)
+                                     self._multi_ptrs.data_ptr(), self.csr[0].il)
 
     def _build_multi_t(self):
         self._multi_t = None

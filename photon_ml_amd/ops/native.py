@@ -31,18 +31,23 @@ class SegChunkDesc(ctypes.Structure):
     ]
 
 
+class TLNarrow(ctypes.Structure):
+    """Narrow-section streams of one chunk (16-bit packs, values, one int32 base per round)."""
+    _fields_ = [("pack", c_void_p), ("val", c_void_p), ("base", c_void_p)]
+
+
 class TLFwdDesc(ctypes.Structure):
     _fields_ = [("blk", c_void_p), ("nblk", c_int), ("rbits", c_int), ("pack", c_void_p), ("val", c_void_p),
-                ("il", c_int)]
+                ("il", c_int), ("nar", TLNarrow)]
 
 
 class TLFwdMultiDesc(ctypes.Structure):
-    _fields_ = [("blk", c_void_p), ("nblk", c_int), ("rbits", c_int), ("packs", c_void_p), ("vals", c_void_p),
-                ("il", c_int)]
+    """``ptrs``: 5 stream pointers per chunk {pack, val, narrow pack, narrow val, narrow base}."""
+    _fields_ = [("blk", c_void_p), ("nblk", c_int), ("rbits", c_int), ("ptrs", c_void_p), ("il", c_int)]
 
 
 class TLTMultiDesc(ctypes.Structure):
-    _fields_ = [("items", c_void_p), ("nitems", c_int), ("cbits", c_int), ("packs", c_void_p), ("vals", c_void_p),
+    _fields_ = [("items", c_void_p), ("nitems", c_int), ("cbits", c_int), ("ptrs", c_void_p),
                 ("mt_tiles", c_void_p), ("mt_ptr", c_void_p), ("nmt", c_int), ("dim", c_int), ("cu", c_void_p),
                 ("ncu", c_int), ("nparts_total", c_int), ("il", c_int)]
 
@@ -51,7 +56,7 @@ class TLTDesc(ctypes.Structure):
     _fields_ = [
         ("items", c_void_p), ("nitems", c_int), ("cbits", c_int), ("pack", c_void_p), ("val", c_void_p),
         ("mt_tiles", c_void_p), ("mt_ptr", c_void_p), ("nmt", c_int), ("dim", c_int),
-        ("cu", c_void_p), ("ncu", c_int), ("nparts_total", c_int), ("il", c_int),
+        ("cu", c_void_p), ("ncu", c_int), ("nparts_total", c_int), ("il", c_int), ("nar", TLNarrow),
     ]
 
 
@@ -104,7 +109,7 @@ def glm_lib() -> Optional[ctypes.CDLL]:
         lib.pml_gram_grid.argtypes = [ctypes.c_longlong]
         lib.pml_gram.argtypes = [c_void_p, c_int, ctypes.c_longlong, c_void_p, c_void_p]
         lib.pml_lincomb.argtypes = [c_void_p, c_void_p, c_int, ctypes.c_longlong, c_void_p, c_void_p]
-        lib.pml_tl_set_dedup.argtypes = [c_int, c_int]
+        lib.pml_tl_set_deep.argtypes = [c_int, c_int]
         lib.pml_rs_set_variant.argtypes = [c_int]
         lib.pml_rs_set_variant(int(os.environ.get("PML_RS_VARIANT", "2")))
         lib.pml_ls_eval.argtypes = [c_int, c_int, c_double, c_int, c_void_p, c_void_p, c_void_p, c_void_p, c_int,
@@ -126,7 +131,7 @@ def glm_lib() -> Optional[ctypes.CDLL]:
 # table of the most frequent features; transpose = strided layout. Env overrides for experiments:
 # PML_FWD_STRIDED, PML_T_STRIDED, PML_HOT_N, PML_FWD_GRID.
 KERNEL_CONFIG = {"fwd_strided": 0, "t_strided": 0, "hot_n": 0, "fwd_grid": 1024, "tl_acc64": 1, "tl_waves": 2,
-                 "tl_waves_t": 4, "tl_pipe": 0, "tl_pipe_t": 0, "tl_multi": 1, "tl_dedup": 0, "tl_dedup_t": 0}
+                 "tl_waves_t": 4, "tl_pipe": 0, "tl_pipe_t": 0, "tl_multi": 1, "tl_deep": 0, "tl_deep_t": 0}
 
 
 def configure(**kw):
@@ -141,7 +146,7 @@ def configure(**kw):
                            KERNEL_CONFIG["fwd_grid"])
         lib.pml_tl_config(KERNEL_CONFIG["tl_acc64"], KERNEL_CONFIG["tl_waves"], KERNEL_CONFIG["tl_waves_t"],
                           (KERNEL_CONFIG["tl_pipe"] & 3) | ((KERNEL_CONFIG["tl_pipe_t"] & 3) << 2))
-        lib.pml_tl_set_dedup(KERNEL_CONFIG["tl_dedup"], KERNEL_CONFIG["tl_dedup_t"])
+        lib.pml_tl_set_deep(KERNEL_CONFIG["tl_deep"], KERNEL_CONFIG["tl_deep_t"])
     return dict(KERNEL_CONFIG)
 
 

@@ -12,6 +12,15 @@ One row chunk of a feature shard is stored twice:
   reduction (units of ``COMBINE_SEG`` partial rows, then the units of a tile) — deterministic.
   ``cbits = min(10, 32 - bits(chunk_rows))``.
 
+NARROW SECTION (``PML_TL_NARROW``, default on with the interleaved layout): a unit's sorted entries are cut into
+groups of 256 (one kernel round); a full group whose gather keys span fewer than 64 values (hot columns in the
+forward copy, dense rows in the transpose copy: about half of the entries at the bench shape) is moved to the
+unit's narrow section and stored with a 16-bit pack ``((key - base) << bits) | slot`` and one int32 ``base`` per
+round (``base + 63 < len(x)``). The kernel reads such a round's key window with one coalesced load and picks the
+values with cross-lane permutes (``tl_stream_narrow``): 4 B/entry of stream instead of 6 (bf16) and a third of the
+gather instructions. Unit tables gain ``{n_lo, n_hi}`` (the unit's narrow rounds); a unit's narrow rounds are
+processed before its remaining (wide) entries, both in sorted order.
+
 Both copies are stored LANE-INTERLEAVED by default (``il``; ``PML_TL_IL=0`` keeps the plain order): every work
 unit (forward block / transpose item) starts on a 256-entry round boundary and is zero-padded to whole rounds,
 and inside a round the 16-B quad of lane L holds the unit's sorted entries L, L+64, L+128, L+192, so each gather
@@ -42,7 +51,10 @@ DEFAULT_ITEM_ENTRIES = 1 << 17  # measured (16M rows, interleaved): 64K 2.87 ms,
 _PAD = 8                 # kernels read 4-entry quads; pad so that the last quad stays in bounds
 COMBINE_SEG = 16         # partial rows summed per level-1 combine work-group
 IL_ROUND = 256           # entries per wave-round of the kernels (64 lanes x 4-entry quads)
+TL_VEC = 4               # entries per lane per round
 INTERLEAVE = int(os.environ.get("PML_TL_IL", "1"))
+NARROW = int(os.environ.get("PML_TL_NARROW", "1"))
+NARROW_W = 64            # key window of a narrow round (one wave64 load); needs bits + 6 <= 16
 
 
 def _bits(n: int) -> int:
@@ -103,7 +115,109 @@ def _interleave(pack: torch.Tensor, val: torch.Tensor, n: torch.Tensor):
     return p, v, new_lo
 
 
-class TLFwdChunk:
+def _empty_narrow(val: torch.Tensor):
+    dev = val.device
+    return (torch.zeros(IL_ROUND, dtype=torch.int16, device=dev), torch.zeros(IL_ROUND, dtype=val.dtype, device=dev),
+            torch.zeros(1, dtype=torch.int32, device=dev))
+
+
+def split_narrow(pack: torch.Tensor, val: torch.Tensor, n: torch.Tensor, sbits: int, xlen: int, enable: bool = True):
+    """Move the narrow rounds of every unit out of sorted, unit-contiguous streams.
+
+    ``pack`` (int64, low 32 bits = the packed entry ``key << sbits | slot``) and ``val`` hold units of ``n[u]``
+    consecutive entries, each unit sorted by key. Returns ``(wide_pack, wide_val, wide_n, npack, nval, nbase,
+    nrounds)``: the remaining entries per unit (same order), the interleaved 16-bit narrow stream (int16 bit
+    patterns), its values, one base per narrow round and the number of narrow rounds per unit."""
+    dev = pack.device
+    n = n.to(torch.int64)
+    U = n.numel()
+    gcount = n // IL_ROUND
+    ok = enable and NARROW and sbits + 6 <= 16 and xlen >= NARROW_W and int(gcount.sum()) > 0
+    if not ok:
+        z = torch.zeros(U, dtype=torch.int64, device=dev)
+        return (pack, val, n, *_empty_narrow(val), z)
+    starts = torch.cumsum(n, 0) - n
+    gu = torch.repeat_interleave(torch.arange(U, device=dev), gcount)
+    gi = torch.arange(gu.numel(), device=dev) - (torch.cumsum(gcount, 0) - gcount)[gu]
+    gs = starts[gu] + IL_ROUND * gi
+    key = pack >> sbits
+    first, last = key[gs], key[gs + IL_ROUND - 1]
+    nar = (last - first) < NARROW_W
+    gs_n, first_n = gs[nar], first[nar]
+    base = torch.clamp(first_n, max=xlen - NARROW_W)
+    idx = gs_n[:, None] + torch.arange(IL_ROUND, device=dev)[None, :]
+    p16 = ((key[idx] - base[:, None]) << sbits) | (pack[idx] & ((1 << sbits) - 1))
+    # interleave: logical t = 64 k + L of a round lives at 4 L + k
+    il = lambda t: t.reshape(-1, TL_VEC, 64).transpose(1, 2).reshape(-1)
+    npack = il(torch.where(p16 >= 32768, p16 - 65536, p16).to(torch.int16)).contiguous()
+    nval = il(val[idx]).contiguous()
+    nbase = base.to(torch.int32).contiguous()
+    nrounds = torch.bincount(gu[nar], minlength=U).to(torch.int64)
+    keep = torch.ones(pack.numel(), dtype=torch.bool, device=dev)
+    keep[idx.reshape(-1)] = False
+    del idx, p16
+    return pack[keep], val[keep], n - IL_ROUND * nrounds, npack, nval, nbase, nrounds
+
+
+
+def narrow_logical(npack: torch.Tensor, nval: torch.Tensor, nbase: torch.Tensor, r_lo, r_hi, sbits: int):
+    """(pack32 as int64, val) of narrow rounds [r_lo, r_hi) in logical order."""
+    r = torch.arange(int(r_lo), int(r_hi), device=npack.device)
+    if not r.numel():
+        return torch.zeros(0, dtype=torch.int64, device=npack.device), nval[:0]
+    ph = (r[:, None] * IL_ROUND + torch.arange(IL_ROUND, device=npack.device)[None, :]).reshape(-1, 64, TL_VEC)
+    ph = ph.transpose(1, 2).reshape(-1)          # physical position of logical entry t of each round
+    p16 = npack[ph].to(torch.int64) & 0xFFFF
+    base = nbase[r].to(torch.int64).repeat_interleave(IL_ROUND)
+    return (((p16 >> sbits) + base) << sbits) | (p16 & ((1 << sbits) - 1)), nval[ph]
+
+
+class _NarrowMixin:
+    """Narrow-section bookkeeping shared by the forward and transpose chunks (``table`` columns 4, 5 hold the
+    per-unit narrow round range [n_lo, n_hi); the wide window is columns ``_ew``)."""
+
+    def _set_narrow(self, npack, nval, nbase):
+        from .native import TLNarrow
+        self.npack, self.nval, self.nbase = npack, nval, nbase
+        self.nar = TLNarrow(npack.data_ptr(), nval.data_ptr(), nbase.data_ptr())
+
+    @property
+    def n_narrow_rounds(self) -> int:
+        t = self._table()
+        return int((t[:, 5] - t[:, 4]).sum()) if t.shape[0] else 0
+
+    def unit_counts(self) -> torch.Tensor:
+        t = self._table().to(torch.int64)
+        lo, hi = self._ew
+        return (t[:, hi] - t[:, lo]) + IL_ROUND * (t[:, 5] - t[:, 4])
+
+    def narrow_window(self, r_lo: int, r_hi: int):
+        return narrow_logical(self.npack, self.nval, self.nbase, r_lo, r_hi, self._sbits)
+
+    def _logical_all(self, wide_pack, wide_val):
+        """Units in table order; inside a unit its narrow entries, then its wide entries."""
+        t = self._table().to(torch.int64)
+        dev = wide_pack.device
+        lo, hi = self._ew
+        nn = IL_ROUND * (t[:, 5] - t[:, 4])
+        nw = t[:, hi] - t[:, lo]
+        if int(nn.sum()) == 0:
+            return wide_pack, wide_val
+        npk, nvl = narrow_logical(self.npack, self.nval, self.nbase, 0, int(t[:, 5].max()), self._sbits)
+        # narrow rounds of a unit are consecutive and in unit order -> gather them unit by unit
+        U = t.shape[0]
+        nu = torch.repeat_interleave(torch.arange(U, device=dev), nn.to(dev))
+        nj = torch.arange(int(nn.sum()), device=dev) - (torch.cumsum(nn, 0) - nn).to(dev)[nu]
+        npos = t[:, 4].to(dev)[nu] * IL_ROUND + nj
+        wu = torch.repeat_interleave(torch.arange(U, device=dev), nw.to(dev))
+        unit = torch.cat([nu, wu])
+        order = torch.sort(unit, stable=True).indices
+        pk = torch.cat([npk[npos], wide_pack.to(torch.int64) & 0xFFFFFFFF])[order]
+        vl = torch.cat([nvl[npos], wide_val])[order]
+        return pk, vl
+
+
+class TLFwdChunk(_NarrowMixin):
     """Forward copy of one row chunk (``m`` rows)."""
 
     kind = "tl"
@@ -130,17 +244,27 @@ class TLFwdChunk:
         lo = b * R
         hi = torch.clamp(lo + R, max=m)
         e_lo, e_hi = rowptr[lo], rowptr[hi]
+        self._sbits, self._ew = self.rbits, (2, 3)
+        n_lo = n_hi = torch.zeros(nblk, dtype=torch.int64, device=dev)
         if self.il:
-            self.pack, self.val, e_lo = _interleave(_to_u32_bits(key & 0xFFFFFFFF), val[perm], e_hi - rowptr[lo])
-            e_hi = e_lo + (rowptr[hi] - rowptr[lo])
+            wp, wv, wn, npk, nvl, nbs, nr = split_narrow(key & 0xFFFFFFFF, val[perm], e_hi - e_lo, self.rbits, dim)
+            del key, perm
+            self.pack, self.val, e_lo = _interleave(_to_u32_bits(wp), wv, wn)
+            e_hi = e_lo + wn
+            n_hi = torch.cumsum(nr, 0)
+            n_lo = n_hi - nr
+            del wp, wv
         else:
             self.pack = _pad(_to_u32_bits(key & 0xFFFFFFFF))
             self.val = _pad(val[perm].contiguous())
-        del key, perm, rows
-        self.blk = torch.stack([lo, hi - lo, e_lo, e_hi], 1).to(torch.int32).contiguous()
+            npk, nvl, nbs = _empty_narrow(val)
+            del key, perm
+        del rows
+        self._set_narrow(npk, nvl, nbs)
+        self.blk = torch.stack([lo, hi - lo, e_lo, e_hi, n_lo, n_hi], 1).to(torch.int32).contiguous()
         self.nblk, self.m, self.nnz = nblk, m, nnz
         self.desc = TLFwdDesc(self.blk.data_ptr(), nblk, self.rbits, self.pack.data_ptr(), self.val.data_ptr(),
-                              self.il)
+                              self.il, self.nar)
 
     @property
     def nstats(self) -> int:
@@ -148,29 +272,33 @@ class TLFwdChunk:
 
     parts_needed = 0
 
+    def _table(self):
+        return self.blk
+
     def nbytes(self) -> int:
-        return sum(t.numel() * t.element_size() for t in (self.blk, self.pack, self.val))
+        return sum(t.numel() * t.element_size() for t in (self.blk, self.pack, self.val, self.npack, self.nval,
+                                                           self.nbase))
 
     def logical(self):
-        """(pack, val) of the non-zeros in sorted (unit) order, whatever the storage order."""
+        """(pack, val) of the non-zeros in unit order (per block: its narrow entries, then its wide entries, each
+        sorted by column), whatever the storage order."""
         if not self.il:
             return self.pack[: self.nnz], self.val[: self.nnz]
         ph = il_phys(self.blk[:, 2], self.blk[:, 3] - self.blk[:, 2])
-        return self.pack[ph], self.val[ph]
+        return self._logical_all(self.pack[ph], self.val[ph])
 
     # host emulation of the kernel arithmetic (tests / CPU fallback)
     def emulate_matvec(self, x: torch.Tensor) -> torch.Tensor:
         pk, vl = self.logical()
         p = pk.to(torch.int64) & 0xFFFFFFFF
         col = p >> self.rbits
-        blk_of_entry = torch.repeat_interleave(torch.arange(self.nblk, device=p.device),
-                                               (self.blk[:, 3] - self.blk[:, 2]).to(torch.int64))
+        blk_of_entry = torch.repeat_interleave(torch.arange(self.nblk, device=p.device), self.unit_counts())
         row = (blk_of_entry << self.rbits) + (p & ((1 << self.rbits) - 1))
         z = torch.zeros(self.m, dtype=torch.float64, device=p.device)
         return z.index_add_(0, row, vl.to(torch.float64) * x.to(torch.float64)[col])
 
 
-class TLTChunk:
+class TLTChunk(_NarrowMixin):
     """Transpose copy of one row chunk."""
 
     kind = "tl"
@@ -221,14 +349,24 @@ class TLTChunk:
                 mt_ptr.append(len(cu))
         self.nitems, self.nmt, self.nparts, self.ncu = len(items), len(mt_tiles), part, len(cu)
         items = np.asarray(items, dtype=np.int64).reshape(-1, 4)
+        items = np.column_stack([items, np.zeros((len(items), 2), np.int64)])
+        self._sbits, self._ew = self.cbits, (1, 2)
         if self.il:
             cnt = torch.from_numpy(items[:, 2] - items[:, 1]).to(dev)
-            self.pack, self.val, new_lo = _interleave(pack, val, cnt)
+            wp, wv, wn, npk, nvl, nbs, nr = split_narrow(pack.to(torch.int64) & 0xFFFFFFFF, val, cnt, self.cbits, m)
+            del pack, val
+            self.pack, self.val, new_lo = _interleave(_to_u32_bits(wp), wv, wn)
+            del wp, wv
             items[:, 1] = new_lo.cpu().numpy()
-            items[:, 2] = items[:, 1] + cnt.cpu().numpy()
+            items[:, 2] = items[:, 1] + wn.cpu().numpy()
+            nr = nr.cpu().numpy()
+            items[:, 5] = np.cumsum(nr)
+            items[:, 4] = items[:, 5] - nr
         else:
             self.pack, self.val = _pad(pack), _pad(val.contiguous())
-        del pack, val
+            npk, nvl, nbs = _empty_narrow(val)
+            del pack, val
+        self._set_narrow(npk, nvl, nbs)
         self.items = torch.tensor(items.astype(np.int32), device=dev)
         self.mt_tiles = torch.tensor(np.asarray(mt_tiles or [0], dtype=np.int32), device=dev)
         self.mt_ptr = torch.tensor(np.asarray(mt_ptr, dtype=np.int32), device=dev)
@@ -236,19 +374,22 @@ class TLTChunk:
         self.m, self.nnz, self.dim = m, nnz, dim
         self.desc = TLTDesc(self.items.data_ptr(), self.nitems, self.cbits, self.pack.data_ptr(),
                             self.val.data_ptr(), self.mt_tiles.data_ptr(), self.mt_ptr.data_ptr(), self.nmt, dim,
-                            self.cu.data_ptr(), self.ncu, self.nparts, self.il)
+                            self.cu.data_ptr(), self.ncu, self.nparts, self.il, self.nar)
 
     @property
     def parts_needed(self) -> int:
         """fp64 scratch: item partial rows followed by the level-1 combine rows."""
         return (self.nparts + self.ncu) << self.cbits
 
+    def _table(self):
+        return self.items
+
     def nbytes(self) -> int:
         return sum(t.numel() * t.element_size() for t in (self.items, self.mt_tiles, self.mt_ptr, self.cu, self.pack,
-                                                           self.val))
+                                                           self.val, self.npack, self.nval, self.nbase))
 
     def window(self, e_lo: int, e_hi: int):
-        """(pack, val) of one item window in sorted order."""
+        """(pack, val) of one item's wide window in sorted order."""
         if not self.il:
             return self.pack[e_lo:e_hi], self.val[e_lo:e_hi]
         ph = il_phys(torch.tensor([e_lo]), torch.tensor([e_hi - e_lo])).to(self.pack.device)
@@ -258,14 +399,13 @@ class TLTChunk:
         if not self.il:
             return self.pack[: self.nnz], self.val[: self.nnz]
         ph = il_phys(self.items[:, 1], self.items[:, 2] - self.items[:, 1])
-        return self.pack[ph], self.val[ph]
+        return self._logical_all(self.pack[ph], self.val[ph])
 
     def emulate_rmatvec(self, r: torch.Tensor, square: bool = False) -> torch.Tensor:
         pk, vl = self.logical()
         p = pk.to(torch.int64) & 0xFFFFFFFF
         row = p >> self.cbits
-        tile_of_entry = torch.repeat_interleave(self.items[:, 0].to(torch.int64),
-                                                (self.items[:, 2] - self.items[:, 1]).to(torch.int64))
+        tile_of_entry = torch.repeat_interleave(self.items[:, 0].to(torch.int64), self.unit_counts())
         col = (tile_of_entry << self.cbits) + (p & ((1 << self.cbits) - 1))
         v = vl.to(torch.float64)
         if square:
@@ -296,10 +436,10 @@ class TLTMulti:
             raise ValueError("TLTMulti: chunks mix interleaved and plain streams")
         its = []
         for c, ch in enumerate(chunks):
-            it = ch.items[: ch.nitems].cpu().numpy().astype(np.int64).reshape(-1, 4)
+            it = ch.items[: ch.nitems].cpu().numpy().astype(np.int64).reshape(-1, 6)
             its.append(np.column_stack([np.full(len(it), c), it[:, 0], it[:, 1], it[:, 2],
-                                        np.full(len(it), row_starts[c])]))
-        it = np.concatenate(its) if its else np.zeros((0, 5), np.int64)
+                                        np.full(len(it), row_starts[c]), it[:, 4], it[:, 5]]))
+        it = np.concatenate(its) if its else np.zeros((0, 7), np.int64)
         if tile_range is not None:
             it = it[(it[:, 1] >= tile_range[0]) & (it[:, 1] < tile_range[1])]
         n = len(it)
@@ -319,16 +459,16 @@ class TLTMulti:
         u_first = np.repeat(plo, nu) + COMBINE_SEG * (np.arange(int(nu.sum())) - np.repeat(np.cumsum(nu) - nu, nu))
         u_last = np.minimum(u_first + COMBINE_SEG, np.repeat(plo + km, nu))
         self.nitems, self.nparts, self.ncu, self.nmt = n, int(km.sum()), int(nu.sum()), len(km)
-        rows = np.column_stack([it[:, 0], it[:, 1], it[:, 2], it[:, 3], part, it[:, 4]]).astype(np.int32)
-        self.items = torch.tensor(rows.reshape(-1, 6), device=dev)
+        rows = np.column_stack([it[:, 0], it[:, 1], it[:, 2], it[:, 3], part, it[:, 4], it[:, 5],
+                                it[:, 6]]).astype(np.int32)
+        self.items = torch.tensor(rows.reshape(-1, 8), device=dev)
         self.mt_tiles = torch.tensor(np.r_[ts[starts][k > 1], 0].astype(np.int32)[: max(self.nmt, 1)], device=dev)
         self.mt_ptr = torch.tensor(np.r_[0, np.cumsum(nu)].astype(np.int32), device=dev)
         self.cu = torch.tensor(np.column_stack([u_tile, u_first, u_last]).astype(np.int32).reshape(-1, 3)
                                if self.ncu else np.zeros((1, 3), np.int32), device=dev)
-        self.packs = torch.tensor([ch.pack.data_ptr() for ch in chunks], dtype=torch.int64, device=dev)
-        self.vals = torch.tensor([ch.val.data_ptr() for ch in chunks], dtype=torch.int64, device=dev)
+        self.ptrs = stream_ptr_table(chunks, dev)
         self._chunks = list(chunks)  # keep the streams alive
-        self.desc = TLTMultiDesc(self.items.data_ptr(), n, self.cbits, self.packs.data_ptr(), self.vals.data_ptr(),
+        self.desc = TLTMultiDesc(self.items.data_ptr(), n, self.cbits, self.ptrs.data_ptr(),
                                  self.mt_tiles.data_ptr(), self.mt_ptr.data_ptr(), self.nmt, dim,
                                  self.cu.data_ptr(), self.ncu, self.nparts, self.il)
 
@@ -344,11 +484,12 @@ class TLTMulti:
         G = torch.zeros(ntiles * C, dtype=torch.float64)
         parts = torch.zeros((max(self.nparts, 1), C), dtype=torch.float64)
         r = r.to(torch.float64).cpu()
-        for c, tile, e_lo, e_hi, part, rb in self.items.cpu().tolist():
+        for c, tile, e_lo, e_hi, part, rb, n_lo, n_hi in self.items.cpu().tolist():
             ch = self._chunks[c]
             pk, vl = ch.window(e_lo, e_hi)
-            p = pk.to(torch.int64).cpu() & 0xFFFFFFFF
-            v = vl.to(torch.float64).cpu()
+            npk, nvl = ch.narrow_window(n_lo, n_hi)
+            p = torch.cat([npk.cpu(), pk.to(torch.int64).cpu() & 0xFFFFFFFF])
+            v = torch.cat([nvl.cpu(), vl.cpu()]).to(torch.float64)
             if square:
                 v = v * v
             acc = torch.zeros(C, dtype=torch.float64).index_add_(0, p & (C - 1), v * r[rb + (p >> self.cbits)])
@@ -365,3 +506,9 @@ class TLTMulti:
                 s += l1[u]
             G[tile * C:(tile + 1) * C] += s
         return G[:dim]
+
+
+def stream_ptr_table(chunks, device) -> torch.Tensor:
+    """Per-chunk stream pointers of the shard-wide kernels: {pack, val, narrow pack, narrow val, narrow base}."""
+    return torch.tensor([[ch.pack.data_ptr(), ch.val.data_ptr(), ch.npack.data_ptr(), ch.nval.data_ptr(),
+                          ch.nbase.data_ptr()] for ch in chunks], dtype=torch.int64, device=device).reshape(-1)

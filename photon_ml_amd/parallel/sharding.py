@@ -121,6 +121,11 @@ class RowRouter:
 
     ``forward(v)``: local sample order -> concatenation over source ranks of the rows sent here (owner order);
     ``backward(u)``: the inverse (owner order -> local sample order). Both are one ``all_to_all_single``.
+
+    Vectors stay where they are: the permutation is cached on each device it is used on, and under RCCL (``nccl``
+    backend) the all-to-all runs directly on device tensors — an RE update moves its N-length score vectors
+    GPU to GPU over xGMI with no host staging (C11/C12). Only the gloo backend (CPU rehearsals) stages through host
+    memory, because gloo collectives take CPU tensors.
     """
 
     def __init__(self, dest: np.ndarray, group=None):
@@ -141,10 +146,18 @@ class RowRouter:
             self.recv_counts = list(self.send_counts)
         self.n_recv = int(sum(self.recv_counts))
         self.src_rank = np.repeat(np.arange(P), self.recv_counts)
+        self._perm_on = {}
+
+    def perm_on(self, device) -> torch.Tensor:
+        """The routing permutation as an int64 tensor on ``device`` (uploaded once per device)."""
+        key = str(torch.device(device))
+        if key not in self._perm_on:
+            self._perm_on[key] = torch.from_numpy(self.perm).to(device)
+        return self._perm_on[key]
 
     def forward(self, v) -> torch.Tensor:
         t = torch.as_tensor(v)
-        send = t[torch.from_numpy(self.perm).to(t.device)]
+        send = t[self.perm_on(t.device)]
         if not is_dist():
             return send
         out, _ = self._a2a(send, self.send_counts, self.recv_counts)
@@ -155,7 +168,7 @@ class RowRouter:
         if is_dist():
             t, _ = self._a2a(t, self.recv_counts, self.send_counts)
         out = torch.empty_like(t)
-        out[torch.from_numpy(self.perm).to(t.device)] = t
+        out[self.perm_on(t.device)] = t
         return out
 
     def _a2a(self, send: torch.Tensor, sc: List[int], rc: List[int]):

@@ -26,6 +26,7 @@ def main():
     ap.add_argument("--ablate", type=int, nargs="+", default=[0])
     ap.add_argument("--configs", default="0,1,8192", help="semicolon list of fwd_strided,t_strided,hot_n")
     ap.add_argument("--il", type=int, nargs="+", default=[1], help="tiled stream order(s): 1 lane-interleaved, 0 plain")
+    ap.add_argument("--narrow", type=int, nargs="+", default=[1], help="narrow rounds (16-bit packs) off/on")
     args = ap.parse_args()
     res = []
     from photon_ml_amd.ops.native import glm_lib, configure
@@ -35,21 +36,22 @@ def main():
         configs = [("tl",) + tuple(int(v) for v in c.split(",")) for c in args.tl_configs.split(";")]
     cache = {}
     from photon_ml_amd.ops import tiled
-    for cr, il, abl, cfg in [(c, i, a, g) for c in args.chunk_rows for i in args.il for a in args.ablate
-                             for g in configs]:
+    for cr, il, nar, abl, cfg in [(c, i, n, a, g) for c in args.chunk_rows for i in args.il for n in args.narrow
+                                  for a in args.ablate for g in configs]:
         lib.pml_set_ablate(0)
-        if (cr, il) not in cache:
+        if (cr, il, nar) not in cache:
             cache.clear()
             torch.cuda.empty_cache()
             tiled.INTERLEAVE = il
-            cache[(cr, il)] = generate_device_shard(args.rows, args.features, args.nnz, "cuda", args.precision,
-                                                    chunk_rows=cr, layout=args.layout)
-        data, w = cache[(cr, il)]
+            tiled.NARROW = nar
+            cache[(cr, il, nar)] = generate_device_shard(args.rows, args.features, args.nnz, "cuda", args.precision,
+                                                         chunk_rows=cr, layout=args.layout)
+        data, w = cache[(cr, il, nar)]
         lib.pml_set_ablate(abl)
         if cfg[0] == "tl":
             configure(tl_waves=cfg[1], tl_waves_t=cfg[2], tl_pipe=cfg[3],
                       tl_multi=cfg[4] if len(cfg) > 4 else 1, tl_pipe_t=cfg[5] if len(cfg) > 5 else cfg[3],
-                      tl_dedup=cfg[6] if len(cfg) > 6 else 0, tl_dedup_t=cfg[7] if len(cfg) > 7 else 0)
+                      tl_deep=cfg[6] if len(cfg) > 6 else 0, tl_deep_t=cfg[7] if len(cfg) > 7 else 0)
         else:
             configure(fwd_strided=cfg[0], t_strided=cfg[1], hot_n=cfg[2])
         x = (w * 0.1).float()
@@ -76,7 +78,11 @@ def main():
             data.value_grad_packed(LOGISTIC, w * 0.1, 0.0)
         torch.cuda.synchronize()
         tp = (time.perf_counter() - t0) / args.reps * 1e3
-        r = {"cfg": cfg, "il": il, "ablate": abl, "chunk_rows": cr, "rows": args.rows, "fwd_ms": min(tf), "t_ms": min(tt), "pass_ms": tp,
+        r = {"cfg": cfg, "il": il, "narrow": nar, "ablate": abl,
+             "fwd_stream_GB": sum(c.nbytes() for c in data.csr) / 1e9,
+             "t_stream_GB": sum(c.nbytes() for c in data.csc) / 1e9,
+             "narrow_frac_fwd": 256 * sum(getattr(c, "n_narrow_rounds", 0) for c in data.csr) / max(1, sum(c.nnz for c in data.csr)),
+             "narrow_frac_t": 256 * sum(getattr(c, "n_narrow_rounds", 0) for c in data.csc) / max(1, sum(c.nnz for c in data.csc)), "chunk_rows": cr, "rows": args.rows, "fwd_ms": min(tf), "t_ms": min(tt), "pass_ms": tp,
              "fwd_GBps": bytes_per / min(tf) / 1e6, "t_GBps": bytes_per / min(tt) / 1e6,
              "stream_GB": bytes_per / 1e9, "nblk_fwd": sum(c.nblk for c in data.csr),
              "nblk_t": sum(getattr(c, "nblk", getattr(c, "nitems", 0)) for c in data.csc),

@@ -80,6 +80,16 @@ def sharding_worker(rank, world, port, out):
     recv_keys = router.forward(torch.from_numpy(keys)).numpy()
     assert np.all(part.owner(recv_keys) == rank)
     np.save(f"{out}/shard_r{rank}.npy", np.array([router.n_recv]))
+    # device data built from DIFFERENT row shards shares one feature order (all-reduced counts), so the bucketed,
+    # overlapped gradient all-reduce is enabled for real (CLI / GAME) data, not only for the synthetic bench
+    from photon_ml_amd.data.synthetic import generate_glm_data
+    from photon_ml_amd.ops.device import DeviceGLMData
+    from photon_ml_amd.parallel.dist import DistributedGLMData
+    data, _ = generate_glm_data("LOGISTIC_REGRESSION", 2000, 300, density=0.05, seed=3)
+    local = data.subset(np.arange(rank * 700, 1300 + rank * 700))
+    dev = DeviceGLMData.from_labeled(local, "cpu", "f64", chunk_rows=512, layout="tiled")
+    assert DistributedGLMData(dev).overlap
+    np.save(f"{out}/perm_r{rank}.npy", dev.old_of_new.numpy())
     import torch.distributed as dist
     dist.destroy_process_group()
 

@@ -44,6 +44,8 @@ def test_sharding_primitives(tmp_path):
     _launch("sharding", tmp_path)
     n = [int(np.load(tmp_path / f"shard_r{r}.npy")[0]) for r in range(2)]
     assert sum(n) == 160
+    p0, p1 = np.load(tmp_path / "perm_r0.npy"), np.load(tmp_path / "perm_r1.npy")
+    assert np.array_equal(p0, p1)
 
 
 def test_data_parallel_glm_matches_single_process(tmp_path):

@@ -91,3 +91,25 @@ def test_validators():
                     "VALIDATE_DISABLED") == []
     with pytest.raises(DataValidationError):
         sanity_check("LOGISTIC_REGRESSION", np.array([0.0, 2.0, 1.0]), None, None, {"s": x})
+
+
+@pytest.mark.parametrize("task", ["LOGISTIC_REGRESSION", "POISSON_REGRESSION", "LINEAR_REGRESSION"])
+def test_validators_on_reference_sample_families(task):
+    """DataValidatorsTest: the reference's benign / outlier families pass FULL and SAMPLE validation; the
+    invalid-feature and invalid-label families are rejected (SparkTestUtils.scala:85-308 generators)."""
+    from photon_ml_amd.data.synthetic import draw_samples
+    for kind in ("benign", "outlier"):
+        ld = draw_samples(task, kind, seed=3, size=500, dimensionality=20)
+        for mode in ("VALIDATE_FULL", "VALIDATE_SAMPLE"):
+            assert validate(task, ld.y, ld.offsets, ld.weights, {"s": ld.x}, mode) == [], (kind, mode)
+    bad_x = draw_samples(task, "invalid_features", seed=3, size=500, dimensionality=20)
+    msgs = validate(task, bad_x.y, bad_x.offsets, bad_x.weights, {"s": bad_x.x})
+    assert any("non-finite feature" in m for m in msgs)
+    bad_y = draw_samples(task, "invalid_labels", seed=3, size=500, dimensionality=20)
+    msgs = validate(task, bad_y.y, bad_y.offsets, bad_y.weights, {"s": bad_y.x})
+    assert any("non-finite label" in m for m in msgs)
+    with pytest.raises(DataValidationError):
+        sanity_check(task, bad_y.y, None, None, {"s": bad_y.x})
+    # scoring data may carry any label, but never non-finite features
+    assert validate(task, bad_y.y, None, None, {"s": bad_y.x}, for_training=False) == []
+    assert validate(task, bad_x.y, None, None, {"s": bad_x.x}, for_training=False)

@@ -427,20 +427,27 @@ def test_tron_margin_space_trial_on_device(precision, layout, norm):
 
 
 @pytest.mark.gpu
-def test_gather_dedup_variant_is_bitwise_equal():
-    """Lane-run gather dedup (only run heads load, value broadcast by shuffles) changes no bits."""
+@pytest.mark.parametrize("deep", [1, 2])
+@pytest.mark.parametrize("precision", ["bf16", "f64"])
+def test_deep_pipeline_variants_are_bitwise_equal(deep, precision):
+    """Deeper software pipelines of the interleaved / narrow streams (more rounds of stream and gathers in flight
+    per wave) keep each wave's accumulation order: bitwise identical value, gradient and Hessian products."""
     from photon_ml_amd.data.synthetic import generate_device_shard
     from photon_ml_amd.function.losses import LOGISTIC
     from photon_ml_amd.ops.native import configure
-    data, w = generate_device_shard(300_000, 50_000, 30, "cuda", "bf16", chunk_rows=1 << 17, layout="tiled")
+    data, w = generate_device_shard(300_000, 50_000, 30, "cuda", precision, chunk_rows=1 << 17, layout="tiled")
     w = (w * 0.05).to(torch.float64)
+    data.track_hessian = True
+    v = torch.randn(50_000, generator=torch.Generator().manual_seed(3), dtype=torch.float64).cuda()
     try:
-        ref = data.value_grad_packed(LOGISTIC, w, 0.1)
-        configure(tl_dedup=1, tl_dedup_t=1)
+        ref = data.value_grad_packed(LOGISTIC, w, 0.1).clone()
+        ref_h = data.hv_sums(LOGISTIC, w, 0.1, v, 0.0)[0].clone()
+        configure(tl_deep=deep, tl_deep_t=deep)
         got = data.value_grad_packed(LOGISTIC, w, 0.1)
+        got_h = data.hv_sums(LOGISTIC, w, 0.1, v, 0.0)[0]
     finally:
-        configure(tl_dedup=0, tl_dedup_t=0)
-    assert torch.equal(got, ref)
+        configure(tl_deep=0, tl_deep_t=0)
+    assert torch.equal(got, ref) and torch.equal(got_h, ref_h)
 
 
 @pytest.mark.gpu
@@ -476,3 +483,37 @@ def test_lbfgs_vector_free_two_loop_on_device(monkeypatch):
         out[gmin] = (w, f)
     (w0, f0), (w1, f1) = out[1 << 40], out[1]
     assert torch.allclose(w0, w1, rtol=1e-6, atol=1e-7) and abs(f0 - f1) <= 1e-10 * abs(f0)
+
+
+@pytest.mark.parametrize("precision", ["f64", "bf16"])
+def test_narrow_rounds_match_wide_only_layout(precision, monkeypatch):
+    """Narrow rounds (16-bit packs + one coalesced key-window load + cross-lane permutes, tl_stream_narrow) give
+    the same value / gradient / Hessian products as the all-wide layout, and the fp64 reference."""
+    from photon_ml_amd.data.synthetic import generate_device_shard
+    from photon_ml_amd.ops import tiled
+    out = {}
+    for nar in (0, 1):
+        monkeypatch.setattr(tiled, "NARROW", nar)
+        data, _ = generate_device_shard(200_000, 50_000, 30, "cuda", precision, seed=6, chunk_rows=1 << 16,
+                                        layout="tiled")
+        nr_f = sum(c.n_narrow_rounds for c in data.csr)
+        nr_t = sum(c.n_narrow_rounds for c in data.csc)
+        assert (nr_f > 0 and nr_t > 0) == bool(nar), (nr_f, nr_t)
+        assert data.validate()
+        data.track_hessian = True
+        w = (torch.randn(50_000, generator=torch.Generator().manual_seed(1), dtype=torch.float64) * 0.05).float()
+        w = w.double().cuda()
+        f, s, g = data.value_grad_sums(LOGISTIC, w, 0.01)
+        v = torch.randn(50_000, generator=torch.Generator().manual_seed(2), dtype=torch.float64).float().double()
+        h, _ = data.hv_sums(LOGISTIC, w, 0.01, v.cuda(), 0.0)
+        d = data.hdiag_sums(LOGISTIC, w)
+        out[nar] = (f, s, g, h, d)
+        # bitwise reproducible run to run
+        f2, s2, g2 = data.value_grad_sums(LOGISTIC, w, 0.01)
+        assert f2 == f and s2 == s and torch.equal(g2, g)
+        del data
+    (f0, s0, g0, h0, d0), (f1, s1, g1, h1, d1) = out[0], out[1]
+    tol = 1e-12 if precision == "f64" else 1e-6
+    assert abs(f1 - f0) <= tol * abs(f0) and abs(s1 - s0) <= tol * max(1.0, abs(s0))
+    for a, b in ((g1, g0), (h1, h0), (d1, d0)):
+        assert torch.allclose(a, b, rtol=tol, atol=tol * float(b.abs().max()))

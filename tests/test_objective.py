@@ -90,3 +90,29 @@ def test_linear_regression_max_error():
                                        max_iterations=200, tolerance=1e-12, device="cpu")[0][1]
     pred = ld.x @ m.coefficients.means.numpy()
     assert np.max(np.abs(pred - ld.y)) <= 1e-2
+
+
+@pytest.mark.parametrize("task", TASKS)
+@pytest.mark.parametrize("kind", ["benign", "outlier"])
+@pytest.mark.parametrize("l2", [0.0, 1.0])
+def test_finite_differences_on_reference_sample_families(task, kind, l2):
+    """DistributedObjectiveFunctionTest.scala:406-437: gradient / Hessian-vector vs finite differences on the
+    reference's benign AND outlier data families (SparkTestUtils generators, data/synthetic.draw_samples)."""
+    from photon_ml_amd.data.synthetic import draw_samples
+    ld = draw_samples(task, kind, seed=7, size=300, dimensionality=15)
+    obj = GLMObjective(loss_for_task(task), l2)
+    data = TorchGLMData(ld)
+    rng = np.random.default_rng(1)
+    w = torch.from_numpy(rng.normal(scale=0.2, size=ld.n_features))
+    _, g = obj.calculate(data, w)
+    for j in range(ld.n_features):
+        e = torch.zeros_like(w)
+        e[j] = DELTA
+        fd = (obj.value(data, w + e) - obj.value(data, w - e)) / (2 * DELTA)
+        assert _close(float(g[j]), fd), (j, float(g[j]), fd)
+    if obj.twice_differentiable:
+        v = torch.from_numpy(rng.normal(size=ld.n_features))
+        hv = obj.hessian_vector(data, w, v)
+        fd_hv = (obj.gradient(data, w + DELTA * v) - obj.gradient(data, w - DELTA * v)) / (2 * DELTA)
+        for j in range(ld.n_features):
+            assert _close(float(hv[j]), float(fd_hv[j])), (j, float(hv[j]), float(fd_hv[j]))

@@ -31,7 +31,8 @@ def test_tl_emulation_matches_scipy(m, d, dens, item, il):
     assert b[0, 0] == 0 and (b[1:, 0] == b[:-1, 0] + b[:-1, 1]).all() and b[-1, 0] + b[-1, 1] == m
     it = t.items.numpy()
     if len(it):
-        assert it[0, 1] == 0 and (it[:, 2] - it[:, 1] <= item).all() and (it[:, 2] - it[:, 1]).sum() == x.nnz
+        cnt = t.unit_counts().numpy()
+        assert it[0, 1] == 0 and (cnt <= item).all() and cnt.sum() == x.nnz
         if il:  # round-aligned, zero-padded windows
             assert (it[:, 1] % 256 == 0).all() and (it[1:, 1] >= it[:-1, 2]).all()
             assert (b[:, 2] % 256 == 0).all()
@@ -41,15 +42,17 @@ def test_tl_emulation_matches_scipy(m, d, dens, item, il):
     # forward blocks: entries sorted by column inside a block (in logical order)
     pk, _ = f.logical()
     p = pk.to(torch.int64).numpy() & 0xFFFFFFFF
-    starts = np.r_[0, np.cumsum(b[:, 3] - b[:, 2])]
-    for lo, hi in zip(starts[:-1], starts[1:]):
-        cols = p[lo:hi] >> f.rbits
-        assert (np.diff(cols) >= 0).all()
+    # forward blocks: narrow section then wide section, each sorted by column (in logical order)
+    nn = 256 * (b[:, 5] - b[:, 4])
+    starts = np.r_[0, np.cumsum(f.unit_counts().numpy())]
+    for lo, hi, k in zip(starts[:-1], starts[1:], nn):
+        for a, z in ((lo, lo + k), (lo + k, hi)):
+            assert (np.diff(p[a:z] >> f.rbits) >= 0).all()
     if il and x.nnz:
         # lane L's quad of a round holds logical entries L, L+64, L+128, L+192 of that round
         lo = int(b[0, 2])
         n0 = int(b[0, 3] - b[0, 2])
-        if n0 >= 256:
+        if n0 >= 256 and b[0, 5] == b[0, 4]:
             phys = f.pack[lo:lo + 256].to(torch.int64).numpy()
             logi = p[:256].astype(np.int64)
             phys_u = phys & 0xFFFFFFFF
@@ -107,7 +110,7 @@ def test_tl_shard_wide_transpose_emulation(chunk, item, hot):
     np.testing.assert_allclose(mt.emulate_rmatvec(torch.from_numpy(r), square=True).numpy(),
                                x.multiply(x).T @ r, atol=1e-11)
     it = mt.items.numpy()
-    assert it.shape == (sum(c.nitems for c in chunks), 6)
+    assert it.shape == (sum(c.nitems for c in chunks), 8)
     assert mt.nparts == int((it[:, 4] >= 0).sum()) and sorted(it[it[:, 4] >= 0, 4]) == list(range(mt.nparts))
     # a tile is direct iff it has exactly one item in the shard
     tiles, cnt = np.unique(it[:, 1], return_counts=True)
@@ -133,3 +136,27 @@ def test_feature_statistics_from_device_shard_match_host(il, monkeypatch):
     for f in ("mean", "variance", "num_nonzeros", "max", "min", "norm_l1", "norm_l2", "mean_abs"):
         np.testing.assert_allclose(getattr(a, f).numpy(), getattr(b, f).numpy(), rtol=1e-12, atol=1e-12, err_msg=f)
     assert a.count == b.count
+
+
+def test_narrow_rounds_on_zipf_data_cpu():
+    """Zipf columns (bench-like): a large share of entries lands in narrow rounds in both copies; the emulated
+    products still equal scipy and every narrow key window lies inside the gathered vector."""
+    from photon_ml_amd.ops.tiled import NARROW_W
+    rng = np.random.default_rng(5)
+    m, d, k = 6000, 5000, 12
+    ranks = np.minimum(rng.zipf(1.3, size=(m, k)) - 1, d - 1)
+    rows = np.repeat(np.arange(m), k)
+    x = sp.csr_matrix((rng.normal(size=m * k), (rows, ranks.ravel())), shape=(m, d))
+    x.sum_duplicates()
+    rp = torch.from_numpy(x.indptr.astype(np.int64))
+    col = torch.from_numpy(x.indices.astype(np.int64))
+    val = torch.from_numpy(x.data)
+    f = TLFwdChunk(rp, col, val, d, il=1)
+    t = TLTChunk(rp, col, val, d, m, item_entries=1 << 14, il=1)
+    for ch, n in ((f, x.nnz), (t, x.nnz)):
+        assert ch.n_narrow_rounds * 256 > 0.2 * n
+        assert int(ch.nbase.min()) >= 0
+    assert int(f.nbase.max()) + NARROW_W <= d and int(t.nbase.max()) + NARROW_W <= m
+    w, r = rng.normal(size=d), rng.normal(size=m)
+    np.testing.assert_allclose(f.emulate_matvec(torch.from_numpy(w)).numpy(), x @ w, atol=1e-11)
+    np.testing.assert_allclose(t.emulate_rmatvec(torch.from_numpy(r)).numpy(), x.T @ r, atol=1e-11)
