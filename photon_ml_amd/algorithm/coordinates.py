@@ -406,7 +406,14 @@ class RandomEffectCoordinate(Coordinate):
             keys = np.repeat(ents, dl).astype(np.int64) * ds.dim + gf
             vv = None if Vn is None else Vn[b_idx, c_idx]
         else:
-            if kind == "RANDOM":
+            if kind == "RANDOM" and W.is_cuda:
+                # back-projection W P (and V P^2) on the matrix cores: gemm_nt_mfma_kernel, fp64 MFMA
+                from ..ops.native import gemm_nt
+                PT = ds._matrix_t(W.device)
+                orig = gemm_nt(W.detach().to(torch.float64).contiguous(), PT).cpu().numpy()
+                vorig = None if var is None else gemm_nt(var.detach().to(torch.float64).contiguous(),
+                                                         (PT * PT).contiguous()).cpu().numpy()
+            elif kind == "RANDOM":
                 orig = Wn @ ds.matrix  # [B, D]
                 vorig = None if Vn is None else Vn @ (ds.matrix ** 2)
             else:

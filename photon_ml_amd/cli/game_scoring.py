@@ -89,7 +89,9 @@ class GameScoringDriver(GameDriverBase):
             self.log(f"data: {data.n_rows} rows")
         with Timed("Score data"):
             tr = GameTransformer(self.model, split_list(a.evaluators) if a.evaluators else None,
-                                 device=a.device or "cpu")
+                                 device=a.device or None)
+            self.scoring_device = tr.device
+            self.log(f"scoring on {tr.device}")
             scores, evals = tr.transform(data)
         if evals:
             for e, v in evals:

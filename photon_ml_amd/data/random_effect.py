@@ -247,6 +247,13 @@ class RandomEffectDataset:
         return sp.csr_matrix((xa_coo.data[keep_entry], (xa_coo.row[keep_entry], xa_coo.col[keep_entry])),
                              shape=xa.shape)
 
+    def _matrix_t(self, device) -> torch.Tensor:
+        """P^T [D x k] of the random projection as a device fp64 tensor (uploaded once)."""
+        cache = self.__dict__.setdefault("_mt_cache", {})
+        if str(device) not in cache:
+            cache[str(device)] = torch.from_numpy(np.ascontiguousarray(self.matrix.T, dtype=np.float64)).to(device)
+        return cache[str(device)]
+
     def _project_rows(self, xr: sp.csr_matrix, er: np.ndarray):
         """Return (row_idx, local_col, value) triplets of rows ``xr`` of entities ``er`` in projected space."""
         pt = self.projector_type
@@ -256,7 +263,12 @@ class RandomEffectDataset:
             ok = lc >= 0
             return coo.row[ok], lc[ok], coo.data[ok]
         if pt.kind == ProjectorKind.RANDOM:
-            dense = np.asarray(xr @ self.matrix.T)
+            if self.device.type == "cuda":
+                # K15 forward map on the device (spmm_rows_kernel): one wave per row over the k projected dims
+                from ..ops.native import spmm_rows
+                dense = spmm_rows(xr, self._matrix_t(self.device)).cpu().numpy()
+            else:
+                dense = np.asarray(xr @ self.matrix.T)
             r, c = np.nonzero(dense)
             return r, c, dense[r, c]
         coo = xr.tocoo()

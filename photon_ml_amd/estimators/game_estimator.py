@@ -201,10 +201,11 @@ class GameEstimator:
 
 
 class GameTransformer:
-    def __init__(self, model: GameModel, validation_evaluators: Optional[Sequence[str]] = None, device="cpu"):
+    def __init__(self, model: GameModel, validation_evaluators: Optional[Sequence[str]] = None, device=None):
+        """``device`` defaults to the current GPU (the HIP scoring kernels, K5/K6) and to the CPU without one."""
         self.model = model
         self.validation_evaluators = list(validation_evaluators or [])
-        self.device = device
+        self.device = torch.device(device) if device is not None else default_device()
 
     def transform(self, data: GameData):
         """Return (scores WITHOUT offsets, evaluations or None)."""

@@ -6,9 +6,10 @@ product), ``RandomEffectModel.scala:38-298`` (RDD of per-entity GLMs; scoring is
 ``DatumScoringModel.scala``.
 
 Random-effect models are stored entity-major in the ORIGINAL feature space as one sorted key array
-``key = entity_index * D + feature`` with values (and optional variances) — a CSR over entities. Scoring any
-dataset (K6) is then one vectorised ``searchsorted`` of the sample non-zeros' keys, executed on the device; no
-per-entity Python objects, no joins.
+``key = entity_index * D + feature`` with values (and optional variances) — a CSR over entities. On the GPU,
+scoring (K5 fixed effect, K6 random effect) is the ``score_rows_kernel`` HIP kernel (``ops/csrc/game_kernels.hip``:
+16 lanes per sample row, per-lane binary search in the row's entity segment, fixed-order reduction); on the host
+it is one vectorised ``searchsorted`` of the sample non-zeros' keys. No per-entity Python objects, no joins.
 """
 from __future__ import annotations
 
@@ -45,6 +46,23 @@ def _csr_to_torch(x: sp.csr_matrix, device):
     return cache[key]
 
 
+def _csr_col32(x: sp.csr_matrix, device) -> torch.Tensor:
+    """int32 column ids of a cached device CSR (the scoring kernel's index type), cached beside it."""
+    dev = torch.device(device)
+    col = _csr_to_torch(x, dev)[1]
+    cache = getattr(x, "_pml_dev_cache", None)
+    key = "col32:" + str(dev)
+    if cache is None:
+        return col.to(torch.int32)
+    if key not in cache:
+        cache[key] = col.to(torch.int32)
+    return cache[key]
+
+
+def _use_kernel(dev: torch.device) -> bool:
+    return dev.type == "cuda"
+
+
 def _row_sums(contrib: torch.Tensor, row: torch.Tensor, indptr: torch.Tensor, n: int) -> torch.Tensor:
     """Per-row sums of CSR-ordered per-entry values, fp64. On the GPU a segmented reduction over the CSR row
     pointer (deterministic: no atomics, unlike ``index_add_``)."""
@@ -72,6 +90,9 @@ class FixedEffectModel:
             w = means.cpu().numpy()
             return torch.from_numpy(np.asarray(x @ w).reshape(-1))
         row, col, val, indptr = _csr_to_torch(x, dev)
+        if _use_kernel(dev):
+            from ..ops.native import score_rows
+            return score_rows(indptr, _csr_col32(x, dev), val, means.to(dev, torch.float64).contiguous())
         return _row_sums(val * means.to(dev, torch.float64)[col], row, indptr, x.shape[0])
 
     def __repr__(self):
@@ -214,16 +235,51 @@ class RandomEffectModel:
         for i, eid in enumerate(self.entity_ids):
             yield eid, model_for_task(self._task, self.coefficients_of(eid))
 
+    def entity_csr(self, device):
+        """Entity-major CSR of the model on ``device``: (eptr [E + 1] int64, sorted feature ids int32, values f64),
+        cached per device (models are immutable once built)."""
+        dev = torch.device(device)
+        cache = self.__dict__.setdefault("_ecsr", {})
+        if str(dev) not in cache:
+            keys, vals = self.tensors(dev)
+            ent = torch.div(keys, self.dim, rounding_mode="floor")
+            bounds = torch.arange(self.n_entities + 1, device=dev, dtype=torch.int64) * self.dim
+            eptr = torch.searchsorted(keys, bounds)
+            cache[str(dev)] = (eptr, (keys - ent * self.dim).to(torch.int32), vals.contiguous())
+        return cache[str(dev)]
+
+    def _row_entities(self, data, dev) -> torch.Tensor:
+        """Model entity index of every sample row (-1: no model), int32 on ``dev``; cached on the data object for
+        this entity table (validation data is scored after every coordinate update)."""
+        cache = data.__dict__.setdefault("_pml_ent_cache", {})
+        ids = self.entity_ids
+        key = (self.random_effect_type, id(ids), len(ids), str(dev))
+        hit = cache.get(key)
+        if hit is None or hit[0] is not ids:
+            ent = self.entity_index(data.id_tags[self.random_effect_type]).astype(np.int32)
+            hit = (ids, torch.from_numpy(ent).to(dev))
+            cache[key] = hit
+        return hit[1]
+
     def score(self, data, device="cpu", mask: Optional[np.ndarray] = None) -> torch.Tensor:
         """Score every sample whose entity has a model (K6): sum_j x_ij * w_{e(i), j}."""
         x = data.shard(self.feature_shard_id)
         n = x.shape[0]
         if self.nnz == 0:
             return torch.zeros(n, dtype=torch.float64, device=device)
+        dev = torch.device(device)
+        if _use_kernel(dev):
+            from ..ops.native import score_rows
+            row, col, val, indptr = _csr_to_torch(x, dev)
+            ent_t = self._row_entities(data, dev)
+            if mask is not None:
+                ent_t = torch.where(torch.from_numpy(np.asarray(mask, dtype=bool)).to(dev), ent_t,
+                                    torch.full_like(ent_t, -1))
+            eptr, efeat, vals = self.entity_csr(dev)
+            return score_rows(indptr, _csr_col32(x, dev), val, vals, ent_t.contiguous(), eptr, efeat)
         ent = self.entity_index(data.id_tags[self.random_effect_type])
         if mask is not None:
             ent = np.where(mask, ent, -1)
-        dev = torch.device(device)
         row, col, val, indptr = _csr_to_torch(x, dev)
         ent_t = torch.from_numpy(ent).to(dev)
         e = ent_t[row]

@@ -18,6 +18,7 @@ from pathlib import Path
 PKG = Path(__file__).resolve().parents[1]
 HIP_SOURCES = {
     "glm": PKG / "ops" / "csrc" / "glm_kernels.hip",
+    "game": PKG / "ops" / "csrc" / "game_kernels.hip",
 }
 CPP_SOURCES = {
     "avro": PKG / "io" / "csrc" / "avro_codec.cpp",
@@ -61,6 +62,22 @@ def build_hip(name: str, force: bool = False, verbose: bool = False) -> Path:
     out.parent.mkdir(parents=True, exist_ok=True)
     if force or _needs_build(src, out):
         cmd = [_hipcc(), f"--offload-arch={ARCH}", "-O3", "-std=c++17", "-fPIC", "-shared",
+               "-Wno-unused-result", str(src), "-o", str(out) + ".tmp"]
+        if verbose:
+            print(" ".join(cmd), flush=True)
+        subprocess.run(cmd, check=True)
+        os.replace(str(out) + ".tmp", out)
+    return out
+
+
+def build_experiment(force: bool = False, verbose: bool = False) -> Path:
+    """Profiling build of the GLM kernels with the runtime ablation switches compiled in (``-DPML_TL_EXPERIMENT``,
+    ``libpml_glm_abl.so``; load it with ``PML_GLM_LIB=<path>``). Never used in production."""
+    src = HIP_SOURCES["glm"]
+    out = lib_path("hip", "glm_abl")
+    out.parent.mkdir(parents=True, exist_ok=True)
+    if force or _needs_build(src, out):
+        cmd = [_hipcc(), f"--offload-arch={ARCH}", "-O3", "-std=c++17", "-fPIC", "-shared", "-DPML_TL_EXPERIMENT",
                "-Wno-unused-result", str(src), "-o", str(out) + ".tmp"]
         if verbose:
             print(" ".join(cmd), flush=True)

@@ -1,0 +1,255 @@
+// photon_ml_amd — CDNA4 (gfx950 / MI355X) kernels for GAME scoring and the dense random-effect paths
+// (row-space Gram of K7).
+//
+// * score_rows_kernel  — K5 fixed-effect scoring s_i = x_i . w and K6 random-effect scoring s_i = x_i . w_{e(i)}
+//   over a CSR shard. 16 lanes per row (4 rows per wave64): lane-strided fp64 partial sums combined by a fixed
+//   shuffle tree, so scores are bitwise reproducible. Random-effect models are entity-major CSR (eptr / sorted
+//   feature ids / values, models/game.py): each lane binary-searches its feature in the row's entity segment.
+//   Reference: photon-api/.../model/FixedEffectModel.scala:132-144, RandomEffectModel.scala:256-297.
+// * MFMA kernels (dense GEMM-shaped work on the matrix cores, fp64 v_mfma_f64_16x16x4f64):
+//   - bgram_mfma_kernel  — batched Gram K_b = A_b A_b^T of small dense blocks (row-space random-effect
+//     re-parametrisation, optimization/row_space.py);
+//   - gemm_nt_mfma_kernel — C = A B^T: back-projection of projected coefficients W P (and variances) of the
+//     random projection (projector/ProjectionMatrix.scala:95-124);
+// * spmm_rows_kernel — K15 forward random projection X P^T of sparse rows (ProjectionMatrix.scala:48-63).
+//
+// Built with: hipcc --offload-arch=gfx950 -O3 -shared -fPIC (photon_ml_amd/ops/build.py). C ABI, ctypes.
+
+#include <hip/hip_runtime.h>
+#include <stdint.h>
+
+#define LAUNCH_CHECK()                                         \
+  do {                                                         \
+    hipError_t e_ = hipGetLastError();                         \
+    if (e_ != hipSuccess) return (int)e_;                      \
+  } while (0)
+
+// ------------------------------------------------------------------------------------------------------------
+// K5 / K6 scoring
+// ------------------------------------------------------------------------------------------------------------
+#define SCORE_GROUP 16                       // lanes per row
+#define SCORE_THREADS 256
+#define SCORE_ROWS_PER_BLOCK (SCORE_THREADS / SCORE_GROUP)
+
+template <bool RE>
+__global__ __launch_bounds__(SCORE_THREADS) void score_rows_kernel(
+    const long long* __restrict__ indptr, const int* __restrict__ col, const double* __restrict__ val,
+    long long n_rows, const double* __restrict__ w, const int* __restrict__ ent,
+    const long long* __restrict__ eptr, const int* __restrict__ efeat, double* __restrict__ out) {
+  const long long row = (long long)blockIdx.x * SCORE_ROWS_PER_BLOCK + (threadIdx.x / SCORE_GROUP);
+  const int g = threadIdx.x % SCORE_GROUP;
+  double s = 0.0;
+  if (row < n_rows) {
+    const long long lo = indptr[row], hi = indptr[row + 1];
+    long long e_lo = 0, e_hi = 0;
+    bool ok = true;
+    if (RE) {
+      const int e = ent[row];
+      if (e < 0) ok = false;
+      else { e_lo = eptr[e]; e_hi = eptr[e + 1]; }
+    }
+    if (ok) {
+      for (long long p = lo + g; p < hi; p += SCORE_GROUP) {
+        const int c = col[p];
+        double wv;
+        if (RE) {
+          long long a = e_lo, b = e_hi;         // lower bound of c in the entity's sorted feature ids
+          while (a < b) {
+            const long long m = (a + b) >> 1;
+            if (efeat[m] < c) a = m + 1; else b = m;
+          }
+          wv = (a < e_hi && efeat[a] == c) ? w[a] : 0.0;
+        } else {
+          wv = w[c];
+        }
+        s += val[p] * wv;
+      }
+    }
+  }
+#pragma unroll
+  for (int o = SCORE_GROUP / 2; o > 0; o >>= 1) s += __shfl_xor(s, o, SCORE_GROUP);
+  if (g == 0 && row < n_rows) out[row] = s;
+}
+
+// ------------------------------------------------------------------------------------------------------------
+// MFMA: fp64 16x16x4 tiles. One wave computes a 16x16 fp64 output tile. v_mfma_f64_16x16x4_f64 fragments on
+// gfx950: lane l holds A[row = l & 15][k = l >> 4] and B[k = l >> 4][col = l & 15]; accumulator i (of 4) of lane l
+// holds C[row = (l >> 4) + 4 i][col = l & 15] (the f64 C/D map differs from the f32 / bf16 ones).
+// ------------------------------------------------------------------------------------------------------------
+typedef double v4d __attribute__((ext_vector_type(4)));
+
+__device__ __forceinline__ v4d mfma_f64_16x16x4(double a, double b, v4d c) {
+  return __builtin_amdgcn_mfma_f64_16x16x4f64(a, b, c, 0, 0, 0);
+}
+
+// Batched Gram: for every block b, K_b[i][j] = sum_k A_b[i][k] A_b[j][k], A_b row-major [n x m] (stride lda
+// between rows, sa between blocks), K_b row-major [n x n] (stride sk between blocks). One work-group (4 waves)
+// per block; the block's rows are staged through LDS in K-slices of 64 columns; each wave owns output tiles
+// (ti, tj) with tj >= ti (the Gram is symmetric: the lower triangle is mirrored on store).
+#define GR_TK 64
+#define GR_MAXN 64
+__global__ __launch_bounds__(256) void bgram_mfma_kernel(int B, int n, int m, const double* __restrict__ A,
+                                                          long long sa, int lda, double* __restrict__ K,
+                                                          long long sk) {
+  __shared__ double tile[GR_MAXN][GR_TK + 1];
+  const int b = blockIdx.x;
+  if (b >= B) return;
+  const double* Ab = A + (long long)b * sa;
+  const int lane = threadIdx.x & 63, wv = threadIdx.x >> 6;
+  const int nt = (n + 15) / 16;
+  const int ntiles = nt * (nt + 1) / 2;
+  v4d acc[4];                                            // up to 4 tiles per wave (n <= 64 -> <= 10 tiles / 4 waves)
+#pragma unroll
+  for (int t = 0; t < 4; ++t) acc[t] = v4d{0.0, 0.0, 0.0, 0.0};
+  for (int k0 = 0; k0 < m; k0 += GR_TK) {
+    const int kw = min(GR_TK, m - k0);
+    __syncthreads();
+    for (int idx = threadIdx.x; idx < GR_MAXN * GR_TK; idx += 256) {
+      const int r = idx / GR_TK, c = idx % GR_TK;
+      tile[r][c] = (r < n && c < kw) ? Ab[(long long)r * lda + k0 + c] : 0.0;
+    }
+    __syncthreads();
+#pragma unroll
+    for (int t = 0; t < 4; ++t) {
+      const int id = wv + 4 * t;
+      if (id >= ntiles) break;
+      int ti = 0, rem = id;
+      while (rem >= nt - ti) { rem -= nt - ti; ++ti; }
+      const int tj = ti + rem;
+      for (int kk = 0; kk < kw; kk += 4) {
+        const double a = tile[16 * ti + (lane & 15)][kk + (lane >> 4)];
+        const double bb = tile[16 * tj + (lane & 15)][kk + (lane >> 4)];
+        acc[t] = mfma_f64_16x16x4(a, bb, acc[t]);
+      }
+    }
+  }
+  double* Kb = K + (long long)b * sk;
+#pragma unroll
+  for (int t = 0; t < 4; ++t) {
+    const int id = wv + 4 * t;
+    if (id >= ntiles) break;
+    int ti = 0, rem = id;
+    while (rem >= nt - ti) { rem -= nt - ti; ++ti; }
+    const int tj = ti + rem;
+    const int cj = 16 * tj + (lane & 15);
+#pragma unroll
+    for (int i = 0; i < 4; ++i) {
+      const int ri = 16 * ti + (lane >> 4) + 4 * i;
+      if (ri < n && cj < n) {
+        Kb[(long long)ri * n + cj] = acc[t][i];
+        Kb[(long long)cj * n + ri] = acc[t][i];
+      }
+    }
+  }
+}
+
+// C[M x N] = A[M x K] * B[N x K]^T (all row-major fp64, leading dimensions lda / ldb / ldc). Work-group = 4 waves
+// = a 32 x 32 output tile (2 x 2 wave tiles of 16 x 16); K staged through LDS in slices of 32. Grid over output
+// tiles; blockIdx.x runs over N tiles fastest so neighbouring work-groups share the A panel in L2.
+#define GN_T 32
+#define GN_K 32
+__global__ __launch_bounds__(256) void gemm_nt_mfma_kernel(int M, int N, int K, const double* __restrict__ A, int lda,
+                                                            const double* __restrict__ Bm, int ldb,
+                                                            double* __restrict__ C, int ldc) {
+  __shared__ double sa[GN_T][GN_K + 1];
+  __shared__ double sb[GN_T][GN_K + 1];
+  const int tn = blockIdx.x, tm = blockIdx.y;
+  const int lane = threadIdx.x & 63, wv = threadIdx.x >> 6;
+  const int wm = wv >> 1, wn = wv & 1;
+  v4d acc = {0.0, 0.0, 0.0, 0.0};
+  for (int k0 = 0; k0 < K; k0 += GN_K) {
+    __syncthreads();
+    for (int idx = threadIdx.x; idx < GN_T * GN_K; idx += 256) {
+      const int r = idx / GN_K, c = idx % GN_K;
+      const int gr = tm * GN_T + r, gc = k0 + c;
+      sa[r][c] = (gr < M && gc < K) ? A[(long long)gr * lda + gc] : 0.0;
+      const int hr = tn * GN_T + r;
+      sb[r][c] = (hr < N && gc < K) ? Bm[(long long)hr * ldb + gc] : 0.0;
+    }
+    __syncthreads();
+#pragma unroll
+    for (int kk = 0; kk < GN_K; kk += 4) {
+      const double a = sa[16 * wm + (lane & 15)][kk + (lane >> 4)];
+      const double b = sb[16 * wn + (lane & 15)][kk + (lane >> 4)];
+      acc = mfma_f64_16x16x4(a, b, acc);
+    }
+  }
+  const int cj = tn * GN_T + 16 * wn + (lane & 15);
+#pragma unroll
+  for (int i = 0; i < 4; ++i) {
+    const int ri = tm * GN_T + 16 * wm + (lane >> 4) + 4 * i;
+    if (ri < M && cj < N) C[(long long)ri * ldc + cj] = acc[i];
+  }
+}
+
+// K15 forward projection: Y[row][j] = sum_p val[p] * PT[col[p]][j] for a CSR X (rows) and a dense row-major
+// PT [D x k] (the transposed projection matrix): one wave per row, lanes over the k outputs (strided by 64),
+// non-zeros in CSR order -> deterministic. Each non-zero reads one contiguous k-row of PT (coalesced).
+__global__ __launch_bounds__(256) void spmm_rows_kernel(const long long* __restrict__ indptr,
+                                                         const int* __restrict__ col, const double* __restrict__ val,
+                                                         long long n_rows, const double* __restrict__ PT, int k,
+                                                         double* __restrict__ Y) {
+  const long long row = (long long)blockIdx.x * 4 + (threadIdx.x >> 6);
+  const int lane = threadIdx.x & 63;
+  if (row >= n_rows) return;
+  const long long lo = indptr[row], hi = indptr[row + 1];
+  for (int j0 = 0; j0 < k; j0 += 64) {
+    const int j = j0 + lane;
+    double acc = 0.0;
+    for (long long p = lo; p < hi; ++p) {
+      const double v = val[p];
+      const long long c = col[p];
+      if (j < k) acc += v * PT[c * k + j];
+    }
+    if (j < k) Y[row * k + j] = acc;
+  }
+}
+
+extern "C" {
+
+int pml_spmm_rows(const long long* indptr, const int* col, const double* val, long long n_rows, const double* PT,
+                  int k, double* Y, void* stream) {
+  if (n_rows <= 0 || k <= 0) return 0;
+  const long long blocks = (n_rows + 3) / 4;
+  if (blocks > 0x7fffffffLL) return -22;
+  hipLaunchKernelGGL(spmm_rows_kernel, dim3((unsigned)blocks), dim3(256), 0, (hipStream_t)stream, indptr, col, val,
+                     n_rows, PT, k, Y);
+  LAUNCH_CHECK();
+  return 0;
+}
+
+int pml_score_rows(const long long* indptr, const int* col, const double* val, long long n_rows, const double* w,
+                   const int* ent, const long long* eptr, const int* efeat, double* out, void* stream) {
+  if (n_rows <= 0) return 0;
+  const long long blocks = (n_rows + SCORE_ROWS_PER_BLOCK - 1) / SCORE_ROWS_PER_BLOCK;
+  if (blocks > 0x7fffffffLL) return -22;
+  if (ent) {
+    hipLaunchKernelGGL(score_rows_kernel<true>, dim3((unsigned)blocks), dim3(SCORE_THREADS), 0, (hipStream_t)stream,
+                       indptr, col, val, n_rows, w, ent, eptr, efeat, out);
+  } else {
+    hipLaunchKernelGGL(score_rows_kernel<false>, dim3((unsigned)blocks), dim3(SCORE_THREADS), 0,
+                       (hipStream_t)stream, indptr, col, val, n_rows, w, ent, eptr, efeat, out);
+  }
+  LAUNCH_CHECK();
+  return 0;
+}
+
+int pml_bgram(int B, int n, int m, const double* A, long long sa, int lda, double* K, long long sk, void* stream) {
+  if (B <= 0) return 0;
+  if (n < 1 || n > GR_MAXN || m < 0) return -22;
+  hipLaunchKernelGGL(bgram_mfma_kernel, dim3(B), dim3(256), 0, (hipStream_t)stream, B, n, m, A, sa, lda, K, sk);
+  LAUNCH_CHECK();
+  return 0;
+}
+
+int pml_gemm_nt(int M, int N, int K, const double* A, int lda, const double* Bm, int ldb, double* C, int ldc,
+                void* stream) {
+  if (M <= 0 || N <= 0) return 0;
+  if (K < 0) return -22;
+  dim3 grid((N + GN_T - 1) / GN_T, (M + GN_T - 1) / GN_T);
+  hipLaunchKernelGGL(gemm_nt_mfma_kernel, grid, dim3(256), 0, (hipStream_t)stream, M, N, K, A, lda, Bm, ldb, C, ldc);
+  LAUNCH_CHECK();
+  return 0;
+}
+
+}  // extern "C"

@@ -863,150 +863,102 @@ __device__ __forceinline__ void tl_stream_wide(const uint32_t* __restrict__ pack
 // L, L+64, L+128, L+192. The 16-B stream loads stay fully coalesced, and gather k of a wave now reads 64
 // CONSECUTIVE sorted entries (neighbouring columns in the forward, neighbouring rows in the transpose) instead of
 // 64 entries spaced 4 apart, so each gather instruction touches ~4x fewer distinct cache lines in the sparse tail.
-// Two-slot stream prefetch as tl_stream_p0; no lower-bound masks (windows are round-aligned).
-// Profiling ablation of the interleaved stream, compiled only with -DPML_TL_ABLATE (a runtime check in the
-// production loop cost ~30 %): set through pml_set_ablate, bit 8 -> no coefficient gathers (x = 1), bit 16 -> no
-// LDS adds (register sum, one add per lane at the end). Measured (16M rows, bf16): the gathers are the whole
-// difference between the stream rate (fwd 5.9 TB/s, transpose 4.6 TB/s without them) and the full kernels;
-// removing the LDS adds changes nothing.
-#ifdef PML_TL_ABLATE
+// No lower-bound masks (windows are round-aligned). Round-1 ablation (16M rows, bf16; profiles/
+// kbench_il_ablation_16M.jsonl): without the coefficient gathers the streams ran at fwd 5.9 TB/s, transpose
+// 4.6 TB/s; without the LDS adds nothing changed. A lane-run gather dedup (only run heads load, shuffle
+// broadcast) measured 37 % slower (profiles/tl_dedup_ab_16M.txt) and was removed.
+
+// Profiling ablations (experiment build only: -DPML_TL_EXPERIMENT, libpml_glm_abl.so, scripts/kbench.py
+// --ablate): bit 1 -> register sums instead of the LDS atomics, bit 2 -> no coefficient gathers / key-window loads
+// (x = 1), bit 4 -> fp32 products, bit 8 -> no wide-round gathers only, bit 16 -> no narrow key windows or
+// permutes only. The production build compiles TL_ABL to 0 (no runtime checks).
+#ifdef PML_TL_EXPERIMENT
 __constant__ int c_tl_ablate = 0;
 #define TL_ABL c_tl_ablate
 #else
 #define TL_ABL 0
 #endif
 
-template <typename VT, typename XT, typename AT, bool SQ, int NW, bool DD = false>
-__device__ __forceinline__ void tl_stream_il(const uint32_t* __restrict__ pack, const VT* __restrict__ val,
-                                             const XT* __restrict__ x, int e_lo, int e_hi, int sbits, AT* acc) {
-  typedef typename TLValT<VT>::T LT;
-  typedef typename TLVals<VT>::Raw Raw;
-  const int lane = threadIdx.x & 63, w = threadIdx.x >> 6;
-  const uint32_t smask = (1u << sbits) - 1u;
-  const int nr = (e_hi - e_lo + TL_ROUND - 1) / TL_ROUND;
-  const int r0 = (nr * w) / NW, r1 = (nr * (w + 1)) / NW;
-  if (r0 >= r1) return;
-  const int abl = TL_ABL;
-  AT regsum = AT(0);
-  v4u pkA, pkB;
-  Raw vA, vB;
-  auto load_round = [&](int r, v4u& pk, Raw& v) {
-    const int e = e_lo + r * TL_ROUND + lane * TL_VEC;  // physical quad: always inside the padded unit
-    pk = ldg_nt((const v4u*)(pack + e));
-    v = TLVals<VT>::load(val + e);
-  };
-  auto process = [&](int r, v4u& pk_slot, Raw& v_slot) {
-    const v4u pk = pk_slot;
-    const Raw v_raw = v_slot;
-    const int e = e_lo + r * TL_ROUND + lane;  // logical index of quad element 0; element k is e + 64k
-    bool in[TL_VEC];
-    XT xv[TL_VEC];
-    int hd[TL_VEC];
-#pragma unroll
-    for (int k = 0; k < TL_VEC; ++k) {
-      in[k] = e + 64 * k < e_hi;
-      const uint32_t key = in[k] ? (pk[k] >> sbits) : 0u;
-      if (DD) {
-        // gather dedup: lanes hold consecutive sorted entries, so equal gather keys form runs of lanes; only
-        // each run's head lane issues the load (fewer active lanes for the texture address/data units) and the
-        // value is broadcast from the head (prefix-max of head lane ids, 6 shuffle steps). Measured on MI355X
-        // (16M rows, profiles/tl_dedup_ab_16M.txt): forward 2.50 -> 3.42 ms, transpose 2.70 -> 3.65 ms — the
-        // TA/TD cost of a gather does not shrink with masked lanes, the shuffles are pure overhead. Off.
-        const uint32_t prev = __shfl_up(key, 1, 64);
-        const bool head = lane == 0 || prev != key;
-        int h = head ? lane : 0;
-#pragma unroll
-        for (int o = 1; o < 64; o <<= 1) h = max(h, __shfl_up(h, o, 64));
-        hd[k] = h;
-        xv[k] = head ? ldg(x + key) : XT(0);
-      } else {
-        xv[k] = (abl & 8) ? XT(1) : ldg(x + key);
-      }
-    }
-    // unconditional refill (past the end: re-read round r, L2-hot, never used) so the wave's outstanding-load
-    // count is static and each LDS add waits only for its own gather (vmcnt(5..2)), not for the prefetch
-    load_round(r + 2 < r1 ? r + 2 : r, pk_slot, v_slot);
-    if (DD) {
-#pragma unroll
-      for (int k = 0; k < TL_VEC; ++k) xv[k] = __shfl(xv[k], hd[k], 64);
-    }
-    LT v[TL_VEC];
-    TLVals<VT>::get(v_raw, v);
-    // branchless: padding / past-the-end entries add an exact 0 (select, not multiply: no NaN from x)
-#pragma unroll
-    for (int k = 0; k < TL_VEC; ++k) {
-      const AT vv = SQ ? static_cast<AT>(v[k]) * static_cast<AT>(v[k]) : static_cast<AT>(v[k]);
-      const AT add = in[k] ? vv * static_cast<AT>(xv[k]) : AT(0);
-      if (abl & 16) regsum += add + AT(pk[k] & smask);
-      else atomicAdd(&acc[in[k] ? (pk[k] & smask) : 0u], add);
-    }
-  };
-  load_round(r0, pkA, vA);
-  load_round(r0 + 1 < r1 ? r0 + 1 : r0, pkB, vB);
-  for (int r = r0; r < r1; r += 2) {
-    process(r, pkA, vA);
-    if (r + 1 < r1) process(r + 1, pkB, vB);
-  }
-  if (abl & 16) atomicAdd(&acc[lane], regsum);
-}
-
-// Deep-pipelined interleaved stream (P = 5): S stream slots in flight per wave and the gathers of round r + D
-// issued before round r is accumulated, so each wave keeps S rounds of stream and D + 1 rounds of gathers
-// outstanding instead of exposing one gather latency per round (tl_stream_il waits for the gathers it has just
-// issued). Slots are a compile-time ring (fully unrolled -> registers). Same entry order per wave as
-// tl_stream_il, so the result is bitwise identical.
+// Ring-pipelined interleaved stream (P = 3: S = 2, D = 0; P = 5: S = 3, D = 1; P = 6: S = 5, D = 2): S rounds of
+// stream in flight per wave and the gathers of round r + D issued before round r is accumulated.
+// Code-generation rules that matter here (violating them serialised the loops: the waitcnt pass drained the
+// whole queue, vmcnt(0), once per round — see README "Kernel pipelining"):
+//  * the wave index is made wave-uniform (readfirstlane), so every loop bound and branch is scalar;
+//  * every load is UNCONDITIONAL (past the end: a clamped re-read of the last round, never used), so the
+//    outstanding-load sequence is the same on every path and every iteration;
+//  * a ring of S + 1 register slots, refilled BEFORE the round in the oldest slot is processed, so a load never
+//    targets a register that is still live (no loop-carried register copies, which force a wait on the load);
+//  * no branch in the loop body: tail rounds (past r1) are processed with a select that adds an exact +0.0 (an
+//    accumulator starting at +0.0 never holds -0.0, so the added zeros change no bits);
+//  * a scheduling barrier keeps each step's loads ahead of its accumulation.
+// Same entry order per wave for every (S, D): the result is bitwise identical across variants.
 template <typename VT, typename XT, typename AT, bool SQ, int NW, int S, int D>
-__device__ __forceinline__ void tl_stream_il_deep(const uint32_t* __restrict__ pack, const VT* __restrict__ val,
-                                                  const XT* __restrict__ x, int e_lo, int e_hi, int sbits,
-                                                  AT* acc) {
-  static_assert(D < S && S % (D + 1) == 0, "gathers run ahead of loaded slots; the gather ring divides the slots");
+__device__ __forceinline__ void tl_stream_ring(const uint32_t* __restrict__ pack, const VT* __restrict__ val,
+                                               const XT* __restrict__ x, int e_lo, int e_hi, int sbits, AT* acc) {
+  constexpr int R = S + 1;
+  static_assert(D < S && R % (D + 1) == 0, "gathers run ahead of loaded slots; the gather ring divides the slots");
   typedef typename TLValT<VT>::T LT;
   typedef typename TLVals<VT>::Raw Raw;
-  const int lane = threadIdx.x & 63, w = threadIdx.x >> 6;
+  const int lane = threadIdx.x & 63;
+  const int w = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
   const uint32_t smask = (1u << sbits) - 1u;
   const int nr = (e_hi - e_lo + TL_ROUND - 1) / TL_ROUND;
   const int r0 = (nr * w) / NW, r1 = (nr * (w + 1)) / NW;
   if (r0 >= r1) return;
-  v4u pk[S];
-  Raw vr[S];
+  v4u pk[R];
+  Raw vr[R];
   XT xg[D + 1][TL_VEC];
   auto load_round = [&](int r, v4u& p, Raw& v) {
-    const int rr = r < r1 ? r : r1 - 1;  // past the end: re-read the last round (L2-hot, never used)
-    const int e = e_lo + rr * TL_ROUND + lane * TL_VEC;
+    const int e = e_lo + min(r, r1 - 1) * TL_ROUND + lane * TL_VEC;
     p = ldg_nt((const v4u*)(pack + e));
     v = TLVals<VT>::load(val + e);
   };
+  const int abl = TL_ABL;
+  AT regsum = AT(0);
   auto gather = [&](int r, const v4u& p, XT* xv) {
     const int e = e_lo + r * TL_ROUND + lane;
 #pragma unroll
-    for (int k = 0; k < TL_VEC; ++k) xv[k] = ldg(x + ((e + 64 * k < e_hi && r < r1) ? (p[k] >> sbits) : 0u));
+    for (int k = 0; k < TL_VEC; ++k)
+      xv[k] = (abl & 10) ? XT(1) : ldg(x + ((e + 64 * k < e_hi) ? (p[k] >> sbits) : 0u));
   };
+  // prologue in the steady state's issue order (loads of rounds r0 .. r0+S-1, then gathers of r0 .. r0+D-1), so
+  // the outstanding-load sequence at the loop head is the same from the prologue and from the back edge
 #pragma unroll
-  for (int i = 0; i < S; ++i) load_round(r0 + i, pk[i], vr[i]);
+  for (int i = 0; i < S; ++i) {
+    load_round(r0 + i, pk[i], vr[i]);
+    __builtin_amdgcn_sched_barrier(0);
+  }
 #pragma unroll
-  for (int i = 0; i < D; ++i) gather(r0 + i, pk[i], xg[i]);
-  for (int r = r0; r < r1; r += S) {
+  for (int i = 0; i < D; ++i) {
+    gather(r0 + i, pk[i], xg[i]);
+    __builtin_amdgcn_sched_barrier(0);
+  }
+  for (int r = r0; r < r1; r += R) {
 #pragma unroll
-    for (int i = 0; i < S; ++i) {
+    for (int i = 0; i < R; ++i) {
       const int rc = r + i;
-      if (rc >= r1) break;
-      // gathers of round rc + D (its stream slot arrived S - D rounds ago)
-      gather(rc + D, pk[(i + D) % S], xg[(i + D) % (D + 1)]);
-      const v4u p = pk[i];
-      const Raw v_raw = vr[i];
-      load_round(rc + S, pk[i], vr[i]);
+      load_round(rc + S, pk[(i + S) % R], vr[(i + S) % R]);          // slot of round rc - 1 (consumed)
+      __builtin_amdgcn_sched_barrier(0);
+      gather(rc + D, pk[(i + D) % R], xg[(i + D) % (D + 1)]);        // gathers of round rc + D
+      __builtin_amdgcn_sched_barrier(0);
       LT v[TL_VEC];
-      TLVals<VT>::get(v_raw, v);
+      TLVals<VT>::get(vr[i], v);
       const int e = e_lo + rc * TL_ROUND + lane;
 #pragma unroll
       for (int k = 0; k < TL_VEC; ++k) {
-        const bool in = e + 64 * k < e_hi;
+        const bool in = (e + 64 * k < e_hi) && (rc < r1);
         const AT vv = SQ ? static_cast<AT>(v[k]) * static_cast<AT>(v[k]) : static_cast<AT>(v[k]);
-        const AT add = in ? vv * static_cast<AT>(xg[i % (D + 1)][k]) : AT(0);
-        atomicAdd(&acc[in ? (p[k] & smask) : 0u], add);
+        AT add;
+        if (abl & 4) add = in ? static_cast<AT>(static_cast<float>(v[k]) * static_cast<float>(xg[i % (D + 1)][k]))
+                              : AT(0);
+        else add = in ? vv * static_cast<AT>(xg[i % (D + 1)][k]) : AT(0);  // select: no NaN from x
+        if (abl & 1) regsum += add;
+        else atomicAdd(&acc[in ? (pk[i][k] & smask) : 0u], add);
       }
+      __builtin_amdgcn_sched_barrier(0);
     }
   }
+  if (abl & 1) atomicAdd(&acc[lane], regsum);
 }
 
 // NARROW rounds (ops/tiled.py, "narrow section" of a work unit): a round of 256 sorted entries whose gather keys
@@ -1015,58 +967,70 @@ __device__ __forceinline__ void tl_stream_il_deep(const uint32_t* __restrict__ p
 // profiles/pmc_tl_interleaved_4M.txt), the wave loads the round's whole key window x[base .. base+63] with ONE
 // coalesced dword load and every lane picks its values with ds_bpermute (__shfl) from the window's lanes:
 // 3 vector-memory instructions per round instead of 6, and 4 B/entry of stream instead of 6 (bf16).
-// The layout builder guarantees base + 63 < len(x), so the window load is always in bounds. Bases are fetched 64
-// rounds at a time (one coalesced load) and broadcast with readlane. Accumulation order per wave is fixed, as in
-// the wide stream (deterministic).
+// The layout builder guarantees base + 63 < len(x), so the window load is always in bounds. The bases are read
+// with SCALAR loads (read-only data through the constant address space: s_load into SGPRs, counted in lgkmcnt,
+// not in the vector-memory queue) one round ahead of the window load that needs them. Ring pipeline with S + 1
+// slots under the code-generation rules of tl_stream_ring. Accumulation order per wave is fixed (deterministic).
 template <typename T> __device__ __forceinline__ T lane_bcast(T v, int src) { return __shfl(v, src, 64); }
+typedef const __attribute__((address_space(4))) int* const_int_p;
 
 template <typename VT, typename XT, typename AT, bool SQ, int NW, int S = 2>
 __device__ __forceinline__ void tl_stream_narrow(const uint16_t* __restrict__ npk, const VT* __restrict__ nvl,
                                                  const int* __restrict__ nbs, int n_lo, int n_hi, int sbits,
                                                  const XT* __restrict__ x, AT* acc) {
+  constexpr int R = S + 1;
   typedef typename TLValT<VT>::T LT;
   typedef typename TLVals<VT>::Raw Raw;
-  const int lane = threadIdx.x & 63, w = threadIdx.x >> 6;
+  const int lane = threadIdx.x & 63;
+  const int w = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
   const int nr = n_hi - n_lo;
   const int r0 = n_lo + (nr * w) / NW, r1 = n_lo + (nr * (w + 1)) / NW;
+  if (r0 >= r1) return;
   const uint32_t smask = (1u << sbits) - 1u;
-  for (int rb = r0; rb < r1; rb += 64) {
-    const int re = min(rb + 64, r1);
-    const int bases = ldg(nbs + min(rb + lane, re - 1));
-    v2u pks[S];
-    Raw vs[S];
-    XT xs[S];
-    auto load_round = [&](int r, v2u& pk, Raw& v, XT& xw) {
-      const size_t e = (size_t)r * TL_ROUND + lane * TL_VEC;
-      pk = ldg_nt((const v2u*)(npk + e));
-      v = TLVals<VT>::load(nvl + e);
-      const int base = __builtin_amdgcn_readlane(bases, r - rb);
-      xw = ldg(x + base + lane);
-    };
-    auto process = [&](int r, v2u& pk_slot, Raw& v_slot, XT& x_slot) {
-      const v2u pk = pk_slot;
-      const Raw v_raw = v_slot;
-      const XT xw = x_slot;
-      if (r + S < re) load_round(r + S, pk_slot, v_slot, x_slot);
+  const const_int_p bp = (const_int_p)nbs;
+  v2u pks[R];
+  Raw vs[R];
+  XT xs[R];
+  const int abl = TL_ABL;
+  AT regsum = AT(0);
+  auto issue = [&](int r, int base, v2u& pk, Raw& v, XT& xw) {
+    const size_t e = (size_t)min(r, r1 - 1) * TL_ROUND + lane * TL_VEC;   // clamped re-read past the end
+    pk = ldg_nt((const v2u*)(npk + e));
+    v = TLVals<VT>::load(nvl + e);
+    xw = (abl & 18) ? XT(1) : ldg(x + base + lane);
+  };
+#pragma unroll
+  for (int i = 0; i < S; ++i) {
+    issue(r0 + i, bp[min(r0 + i, r1 - 1)], pks[i], vs[i], xs[i]);
+    __builtin_amdgcn_sched_barrier(0);
+  }
+  int nb = bp[min(r0 + S, r1 - 1)];
+  for (int r = r0; r < r1; r += R) {
+#pragma unroll
+    for (int i = 0; i < R; ++i) {
+      const int rc = r + i;
+      issue(rc + S, nb, pks[(i + S) % R], vs[(i + S) % R], xs[(i + S) % R]);   // slot of round rc - 1
+      nb = bp[min(rc + S + 1, r1 - 1)];
+      __builtin_amdgcn_sched_barrier(0);
+      const bool live = rc < r1;          // tail rounds add an exact +0.0 (see tl_stream_ring)
       LT v[TL_VEC];
-      TLVals<VT>::get(v_raw, v);
+      TLVals<VT>::get(vs[i], v);
+      const v2u pk = pks[i];
       const uint32_t p[TL_VEC] = {pk.x & 0xffffu, pk.x >> 16, pk.y & 0xffffu, pk.y >> 16};
 #pragma unroll
       for (int k = 0; k < TL_VEC; ++k) {
-        const XT xv = lane_bcast(xw, (int)(p[k] >> sbits));
+        const XT xv = (abl & 16) ? xs[i] : lane_bcast(xs[i], (int)(p[k] >> sbits));
         const AT vv = SQ ? static_cast<AT>(v[k]) * static_cast<AT>(v[k]) : static_cast<AT>(v[k]);
-        atomicAdd(&acc[p[k] & smask], vv * static_cast<AT>(xv));
+        AT add;
+        if (abl & 4) add = live ? static_cast<AT>(static_cast<float>(v[k]) * static_cast<float>(xv)) : AT(0);
+        else add = live ? vv * static_cast<AT>(xv) : AT(0);
+        if (abl & 1) regsum += add + AT(p[k] & smask);
+        else atomicAdd(&acc[live ? (p[k] & smask) : 0u], add);
       }
-    };
-#pragma unroll
-    for (int i = 0; i < S; ++i)
-      if (rb + i < re) load_round(rb + i, pks[i], vs[i], xs[i]);
-    for (int r = rb; r < re; r += S) {
-#pragma unroll
-      for (int i = 0; i < S; ++i)
-        if (r + i < re) process(r + i, pks[i], vs[i], xs[i]);
+      __builtin_amdgcn_sched_barrier(0);
     }
   }
+  if (abl & 1) atomicAdd(&acc[lane], regsum);
 }
 
 // pipeline variant: P = 0 two-slot stream prefetch; P = 1 three-stage (stream r+2 / gather r+1 / accumulate r);
@@ -1076,10 +1040,9 @@ __device__ __forceinline__ void tl_stream(const uint32_t* __restrict__ pack, con
                                           const XT* __restrict__ x, int e_lo, int e_hi, int sbits, AT* acc) {
   if (P == 1) tl_stream_p1<VT, XT, AT, SQ, U, NW>(pack, val, x, e_lo, e_hi, sbits, acc);
   else if (P == 2) tl_stream_wide<VT, XT, AT, SQ, NW, 2>(pack, val, x, e_lo, e_hi, sbits, acc);
-  else if (P == 3) tl_stream_il<VT, XT, AT, SQ, NW>(pack, val, x, e_lo, e_hi, sbits, acc);
-  else if (P == 4) tl_stream_il<VT, XT, AT, SQ, NW, true>(pack, val, x, e_lo, e_hi, sbits, acc);
-  else if (P == 5) tl_stream_il_deep<VT, XT, AT, SQ, NW, 4, 1>(pack, val, x, e_lo, e_hi, sbits, acc);
-  else if (P == 6) tl_stream_il_deep<VT, XT, AT, SQ, NW, 6, 2>(pack, val, x, e_lo, e_hi, sbits, acc);
+  else if (P == 3) tl_stream_ring<VT, XT, AT, SQ, NW, 2, 0>(pack, val, x, e_lo, e_hi, sbits, acc);
+  else if (P == 5) tl_stream_ring<VT, XT, AT, SQ, NW, 3, 1>(pack, val, x, e_lo, e_hi, sbits, acc);
+  else if (P == 6) tl_stream_ring<VT, XT, AT, SQ, NW, 5, 2>(pack, val, x, e_lo, e_hi, sbits, acc);
   else tl_stream_p0<VT, XT, AT, SQ, U, NW>(pack, val, x, e_lo, e_hi, sbits, acc);
 }
 
@@ -1977,7 +1940,7 @@ void pml_set_ls_args(double* z0, double t0, double tpend) { g_ls_z0 = z0; g_ls_t
 
 void pml_set_ablate(int a) {
   g_ablate = a;
-#ifdef PML_TL_ABLATE
+#ifdef PML_TL_EXPERIMENT
   (void)hipMemcpyToSymbol(HIP_SYMBOL(c_tl_ablate), &a, sizeof(int));
 #endif
 }

@@ -67,6 +67,8 @@ def _load(name: str, auto_build: bool = True) -> Optional[ctypes.CDLL]:
     if name in _LIBS:
         return _LIBS[name]
     path = lib_path("hip", name)
+    if name == "glm" and os.environ.get("PML_GLM_LIB"):   # experiment builds (ops/build.py build_experiment)
+        path = Path(os.environ["PML_GLM_LIB"])
     if not path.exists() and auto_build and os.environ.get("PML_NO_AUTOBUILD") != "1":
         try:
             build_hip(name)
@@ -321,6 +323,99 @@ def seg_cg_step(ptr: torch.Tensor, step: torch.Tensor, r: torch.Tensor, d: torch
     d.copy_(torch.where(move[ent], r + beta[ent] * d, d))
     rtr.copy_(torch.where(move, rn, rtr))
     on.copy_((act & ~hit).to(torch.uint8))
+
+
+def game_lib() -> Optional[ctypes.CDLL]:
+    """Scoring (K5/K6) and MFMA dense kernels (``ops/csrc/game_kernels.hip``)."""
+    lib = _load("game")
+    if lib is not None and not getattr(lib, "_pml_typed", False):
+        lib.pml_score_rows.argtypes = [c_void_p, c_void_p, c_void_p, ctypes.c_longlong, c_void_p, c_void_p,
+                                       c_void_p, c_void_p, c_void_p, c_void_p]
+        lib.pml_bgram.argtypes = [c_int, c_int, c_int, c_void_p, ctypes.c_longlong, c_int, c_void_p,
+                                  ctypes.c_longlong, c_void_p]
+        lib.pml_gemm_nt.argtypes = [c_int, c_int, c_int, c_void_p, c_int, c_void_p, c_int, c_void_p, c_int,
+                                    c_void_p]
+        lib.pml_spmm_rows.argtypes = [c_void_p, c_void_p, c_void_p, ctypes.c_longlong, c_void_p, c_int, c_void_p,
+                                      c_void_p]
+        for f in ("pml_score_rows", "pml_bgram", "pml_gemm_nt", "pml_spmm_rows"):
+            getattr(lib, f).restype = c_int
+        lib._pml_typed = True
+    return lib
+
+
+def require_game_lib() -> ctypes.CDLL:
+    lib = game_lib()
+    if lib is None:
+        raise RuntimeError(
+            f"native GAME kernel library missing ({lib_path('hip', 'game')}); run python -m photon_ml_amd.ops.build")
+    return lib
+
+
+def score_rows(indptr: torch.Tensor, col32: torch.Tensor, val: torch.Tensor, w: torch.Tensor,
+               ent: Optional[torch.Tensor] = None, eptr: Optional[torch.Tensor] = None,
+               efeat: Optional[torch.Tensor] = None) -> torch.Tensor:
+    """K5 / K6 scoring of a device CSR shard (``score_rows_kernel``): ``x_i . w`` (fixed effect) or, with the
+    entity-major model CSR (``ent`` row -> entity index or -1, ``eptr``, sorted ``efeat``, values ``w``),
+    ``x_i . w_{e(i)}``. fp64, deterministic."""
+    lib = require_game_lib()
+    n = indptr.numel() - 1
+    assert indptr.dtype == torch.int64 and col32.dtype == torch.int32 and val.dtype == torch.float64
+    assert w.dtype == torch.float64 and indptr.is_cuda and col32.is_cuda and val.is_cuda and w.is_cuda
+    if ent is not None:
+        assert ent.dtype == torch.int32 and ent.numel() == n and eptr.dtype == torch.int64
+        assert efeat.dtype == torch.int32 and efeat.numel() == w.numel()
+    out = torch.empty(n, dtype=torch.float64, device=val.device)
+    p = lambda t: None if t is None else t.data_ptr()
+    check(lib.pml_score_rows(indptr.data_ptr(), col32.data_ptr(), val.data_ptr(), n, w.data_ptr(), p(ent), p(eptr),
+                             p(efeat), out.data_ptr(), stream_handle(val.device)), "score_rows")
+    return out
+
+
+def batched_gram(A: torch.Tensor) -> torch.Tensor:
+    """``K[b] = A[b] A[b]^T`` for a batch of dense fp64 blocks [B, n, m] with n <= 64 (``bgram_mfma_kernel``,
+    fp64 MFMA on the matrix cores); ``bmm`` off the GPU or for larger n."""
+    if A.device.type != "cuda" or A.shape[1] > 64 or A.dtype != torch.float64:
+        return torch.bmm(A, A.transpose(1, 2))
+    lib = require_game_lib()
+    A = A.contiguous()
+    B, n, m = A.shape
+    K = torch.empty(B, n, n, dtype=torch.float64, device=A.device)
+    check(lib.pml_bgram(B, n, m, A.data_ptr(), n * m, m, K.data_ptr(), n * n, stream_handle(A.device)), "bgram")
+    return K
+
+
+def gemm_nt(A: torch.Tensor, Bm: torch.Tensor) -> torch.Tensor:
+    """``A @ Bm.T`` for fp64 matrices (``gemm_nt_mfma_kernel``: fp64 MFMA, LDS-staged 32 x 32 tiles); torch
+    off the GPU."""
+    if A.device.type != "cuda" or A.dtype != torch.float64 or Bm.dtype != torch.float64:
+        return A @ Bm.T
+    lib = require_game_lib()
+    A, Bm = A.contiguous(), Bm.contiguous()
+    M, K = A.shape
+    N, K2 = Bm.shape
+    assert K == K2 and M < 2 ** 31 and N < 2 ** 31
+    C = torch.empty(M, N, dtype=torch.float64, device=A.device)
+    check(lib.pml_gemm_nt(M, N, K, A.data_ptr(), K, Bm.data_ptr(), K, C.data_ptr(), N, stream_handle(A.device)),
+          "gemm_nt")
+    return C
+
+
+def spmm_rows(x, PT: torch.Tensor) -> torch.Tensor:
+    """``X @ PT`` for a scipy CSR ``x`` [rows x D] and a dense fp64 device ``PT`` [D x k] (``spmm_rows_kernel``;
+    the random projection's forward map)."""
+    lib = require_game_lib()
+    dev = PT.device
+    x = x.tocsr()
+    indptr = torch.from_numpy(x.indptr.astype("int64")).to(dev)
+    col = torch.from_numpy(x.indices.astype("int32")).to(dev)
+    val = torch.from_numpy(x.data.astype("float64")).to(dev)
+    PT = PT.to(torch.float64).contiguous()
+    n, k = x.shape[0], PT.shape[1]
+    assert PT.shape[0] == x.shape[1]
+    Y = torch.empty(n, k, dtype=torch.float64, device=dev)
+    check(lib.pml_spmm_rows(indptr.data_ptr(), col.data_ptr(), val.data_ptr(), n, PT.data_ptr(), k, Y.data_ptr(),
+                            stream_handle(dev)), "spmm_rows")
+    return Y
 
 
 def check(rc: int, what: str):

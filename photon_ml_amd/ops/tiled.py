@@ -54,7 +54,12 @@ IL_ROUND = 256           # entries per wave-round of the kernels (64 lanes x 4-e
 TL_VEC = 4               # entries per lane per round
 INTERLEAVE = int(os.environ.get("PML_TL_IL", "1"))
 NARROW = int(os.environ.get("PML_TL_NARROW", "1"))
-NARROW_W = 64            # key window of a narrow round (one wave64 load); needs bits + 6 <= 16
+NARROW_W = 64            # key window loaded per narrow round (one wave64 load)
+
+
+def narrow_width(sbits: int) -> int:
+    """Largest key span of a narrow round: the 16-bit pack holds (key - base) in 16 - sbits bits."""
+    return min(NARROW_W, 1 << max(16 - sbits, 0))
 
 
 def _bits(n: int) -> int:
@@ -132,7 +137,8 @@ def split_narrow(pack: torch.Tensor, val: torch.Tensor, n: torch.Tensor, sbits: 
     n = n.to(torch.int64)
     U = n.numel()
     gcount = n // IL_ROUND
-    ok = enable and NARROW and sbits + 6 <= 16 and xlen >= NARROW_W and int(gcount.sum()) > 0
+    W = narrow_width(sbits)
+    ok = enable and NARROW and W >= 16 and xlen >= NARROW_W and int(gcount.sum()) > 0
     if not ok:
         z = torch.zeros(U, dtype=torch.int64, device=dev)
         return (pack, val, n, *_empty_narrow(val), z)
@@ -142,9 +148,9 @@ def split_narrow(pack: torch.Tensor, val: torch.Tensor, n: torch.Tensor, sbits: 
     gs = starts[gu] + IL_ROUND * gi
     key = pack >> sbits
     first, last = key[gs], key[gs + IL_ROUND - 1]
-    nar = (last - first) < NARROW_W
-    gs_n, first_n = gs[nar], first[nar]
-    base = torch.clamp(first_n, max=xlen - NARROW_W)
+    base = torch.clamp(first, max=xlen - NARROW_W)        # the 64-wide window load stays inside x
+    nar = (last - base) < W
+    gs_n, base = gs[nar], base[nar]
     idx = gs_n[:, None] + torch.arange(IL_ROUND, device=dev)[None, :]
     p16 = ((key[idx] - base[:, None]) << sbits) | (pack[idx] & ((1 << sbits) - 1))
     # interleave: logical t = 64 k + L of a round lives at 4 L + k

@@ -59,6 +59,18 @@ def test_game_training_and_scoring_cli_on_gpu_match_cpu(game_avro, tmp_path):
     sres = game_scoring.GameScoringDriver(game_scoring.build_parser().parse_args(sargs)).run()
     assert abs(sres["evaluations"][0][1] - a_gpu) < 5e-3
     assert os.path.exists(sout / "scores")
+    # no --device: the scoring driver uses the GPU by default, and matches the CPU scores to fp64 rounding
+    from photon_ml_amd.io.score_io import load_scores
+    outs = {}
+    for dev in (None, "cpu"):
+        o = tmp_path / f"score-{dev}"
+        args = sargs[:-2] + ([] if dev is None else ["--device", dev])
+        args[args.index("--root-output-directory") + 1] = str(o)
+        drv = game_scoring.GameScoringDriver(game_scoring.build_parser().parse_args(args))
+        drv.run()
+        outs[dev] = np.array([r["predictionScore"] for r in load_scores(str(o / "scores"))])
+        assert drv.scoring_device.type == ("cuda" if dev is None else "cpu")
+    np.testing.assert_allclose(outs[None], outs["cpu"], rtol=1e-10, atol=1e-10)
 
 
 @pytest.mark.parametrize("norm,rtol", [("NONE", 5e-4), ("STANDARDIZATION", 1e-5)])

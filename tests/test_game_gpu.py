@@ -82,3 +82,76 @@ def test_game_model_scoring_on_device_matches_host():
     assert torch.equal(dev1, dev2)
     x = data.shard(model.get("global").feature_shard_id)
     assert "cuda:0" in x._pml_dev_cache or "cuda" in x._pml_dev_cache
+
+
+def test_scoring_kernel_paths_and_masks():
+    """K5 / K6 HIP scoring kernel (score_rows_kernel): fixed and random effect, with a passive-row mask and
+    entities without a model, == host scoring to fp64 rounding; deterministic."""
+    from photon_ml_amd.ops.native import game_lib
+    assert game_lib() is not None
+    data, _ = generate_game_data(n_rows=4000, n_users=50, n_items=30, seed=25, task="LINEAR_REGRESSION")
+    res = _fit("cpu", "LINEAR_REGRESSION", data, opt="TRON")
+    rng = np.random.default_rng(0)
+    mask = rng.random(data.n_rows) < 0.7
+    for cid in ("global", "per-user", "per-item"):
+        m = res.model.get(cid)
+        kw = {} if cid == "global" else {"mask": mask}
+        h = m.score(data, "cpu", **kw)
+        d = m.score(data, "cuda", **kw)
+        torch.testing.assert_close(d.cpu(), h, rtol=1e-12, atol=1e-12)
+        assert torch.equal(d, m.score(data, "cuda", **kw))
+    # rows whose entity has no model score 0
+    sub = data.subset(np.arange(1000))
+    re = res.model.get("per-user")
+    from photon_ml_amd.models.game import RandomEffectModel
+    keep = re.entity_ids[::2]
+    idx = re.entity_index(keep)
+    k, v = re.keys, re.values
+    sel = np.isin(k // re.dim, idx)
+    remap = {int(e): i for i, e in enumerate(idx)}
+    nk = np.array([remap[int(a // re.dim)] * re.dim + int(a % re.dim) for a in k[sel]], dtype=np.int64)
+    half = RandomEffectModel(re.random_effect_type, re.feature_shard_id, re.task, keep, re.dim, nk, v[sel])
+    torch.testing.assert_close(half.score(sub, "cuda").cpu(), half.score(sub, "cpu"), rtol=1e-12, atol=1e-12)
+
+
+@pytest.mark.parametrize("n,m", [(1, 1), (7, 5), (16, 64), (20, 100), (33, 7), (64, 130)])
+def test_batched_gram_mfma_matches_fp64(n, m):
+    """bgram_mfma_kernel (fp64 MFMA 16x16x4 on the matrix cores) == torch fp64 bmm."""
+    from photon_ml_amd.ops.native import batched_gram
+    g = torch.Generator(device="cuda").manual_seed(n * 1000 + m)
+    A = torch.randn(37, n, m, generator=g, device="cuda", dtype=torch.float64)
+    K = batched_gram(A)
+    ref = torch.bmm(A, A.transpose(1, 2))
+    torch.testing.assert_close(K, ref, rtol=1e-12, atol=1e-11 * max(1, m))
+    assert torch.equal(K, K.transpose(1, 2))
+
+
+@pytest.mark.parametrize("M,N,K", [(1, 1, 1), (5, 40, 3), (100, 33, 64), (257, 129, 1000), (64, 2000, 17)])
+def test_gemm_nt_mfma_matches_fp64(M, N, K):
+    from photon_ml_amd.ops.native import gemm_nt
+    g = torch.Generator(device="cuda").manual_seed(M + N + K)
+    A = torch.randn(M, K, generator=g, device="cuda", dtype=torch.float64)
+    B = torch.randn(N, K, generator=g, device="cuda", dtype=torch.float64)
+    torch.testing.assert_close(gemm_nt(A, B), A @ B.T, rtol=1e-12, atol=1e-11 * max(1, K))
+
+
+def test_random_projection_coordinate_on_gpu_matches_cpu():
+    """RANDOM projector on the device: forward map X P^T (spmm_rows_kernel) and back-projection W P / V P^2
+    (gemm_nt_mfma_kernel) give the CPU coordinate's coefficients, variances and scores."""
+    from photon_ml_amd.algorithm.coordinates import RandomEffectCoordinate
+    from photon_ml_amd.projector import RandomProjection
+    data, _ = generate_game_data(n_rows=2000, n_users=12, d_user=30, seed=26, task="LINEAR_REGRESSION")
+    cfg = GLMOptimizationConfiguration(OptimizerConfig("TRON", 50, 1e-10), RegularizationContext("L2"), 1.0)
+    dc = RandomEffectDataConfiguration("userId", "user", projector_type=RandomProjection(6))
+    out = {}
+    for dev in ("cpu", "cuda"):
+        c = RandomEffectCoordinate("u", data, dc, cfg, "LINEAR_REGRESSION", compute_variance=True, device=dev)
+        m = c.update_model(c.initialize_model())
+        out[dev] = (m, c.score(m).cpu())
+    (a, sa), (b, sb) = out["cpu"], out["cuda"]
+    for e in a.entity_ids:
+        np.testing.assert_allclose(b.coefficients_of(e).means.numpy(), a.coefficients_of(e).means.numpy(),
+                                   rtol=1e-7, atol=1e-9)
+        np.testing.assert_allclose(b.coefficients_of(e).variances.numpy(), a.coefficients_of(e).variances.numpy(),
+                                   rtol=1e-7, atol=1e-9)
+    torch.testing.assert_close(sb, sa, rtol=1e-7, atol=1e-8)
