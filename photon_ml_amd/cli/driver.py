@@ -38,7 +38,7 @@ from ..diagnostics.evaluation import evaluate, select_best_model
 from ..diagnostics.reporting import build_document
 from ..estimators.game_estimator import train_generalized_linear_model
 from ..io.data_reader import AvroDataReader, read_libsvm
-from ..io.index_map import OffHeapIndexMap
+from ..io.index_map import open_index_map
 from ..io.model_io import write_text_models
 from ..io.score_io import save_feature_summary
 from ..normalization.context import NormalizationContext, NormalizationType
@@ -266,7 +266,7 @@ class Driver:
         if a.format.upper() == "TRAINING_EXAMPLE":
             reader.columns.response = "label"
         if index_map is None and a.offheap_indexmap_dir:
-            index_map = OffHeapIndexMap(a.offheap_indexmap_dir, "global", a.offheap_indexmap_num_partitions or 1)
+            index_map = open_index_map(a.offheap_indexmap_dir, "global", a.offheap_indexmap_num_partitions or 1)
         if index_map is None and a.selected_features_file:
             from ..io.avro import avro_files, read_records
             keys = set()

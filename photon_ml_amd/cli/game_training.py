@@ -45,7 +45,7 @@ from ..hyperparameter.game_tuning import GameEstimatorEvaluationFunction
 from ..hyperparameter.search import DoubleRange, GaussianProcessSearch, RandomSearch
 from ..io.avro import avro_files
 from ..io.data_reader import AvroDataReader, InputColumnNames
-from ..io.index_map import OffHeapIndexMap, index_map_from_feature_bags
+from ..io.index_map import index_map_from_feature_bags, open_index_map
 from ..io.model_io import save_game_model
 from ..io.score_io import save_feature_summary
 from ..normalization.context import NormalizationContext, NormalizationType
@@ -174,7 +174,7 @@ class GameDriverBase:
     def prepare_feature_maps(self):
         a = self.args
         if a.off_heap_index_map_directory:
-            return {sid: OffHeapIndexMap(a.off_heap_index_map_directory, sid, a.off_heap_index_map_partitions)
+            return {sid: open_index_map(a.off_heap_index_map_directory, sid, a.off_heap_index_map_partitions)
                     for sid in self.shard_configs}
         if a.feature_bags_directory:
             return {sid: index_map_from_feature_bags(a.feature_bags_directory, cfg.feature_bags, cfg.has_intercept)

@@ -271,3 +271,13 @@ def index_map_from_feature_bags(bags_dir: str, bags: Sequence[str], add_intercep
     for b in bags:
         keys.update(read_feature_bag_file(os.path.join(bags_dir, b)))
     return DefaultIndexMap.from_keys(sorted(keys), add_intercept)
+
+
+def open_index_map(directory: str, namespace: str, n_partitions: int = 1) -> IndexMap:
+    """Off-heap index map of one namespace (feature shard): the reference's PalDB stores
+    (``paldb-partition-<ns>-<i>.dat``, read by :mod:`photon_ml_amd.io.paldb`) when present, else the native mmap
+    stores written by the feature-indexing driver."""
+    from .paldb import PalDBIndexMap, has_paldb_stores
+    if has_paldb_stores(directory, namespace):
+        return PalDBIndexMap(directory, namespace, n_partitions)
+    return OffHeapIndexMap(directory, namespace, n_partitions)

@@ -1,0 +1,110 @@
+"""PalDB V1 index-store reader (io/paldb.py) on the reference's own stores.
+
+Reference expectations: ``photon-api/src/test/scala/com/linkedin/photon/ml/index/PalDBIndexMapTest.scala``
+(exact name -> index values of the heart stores, 2 partitions, with and without intercept); the GAME
+integration-test stores ``GameIntegTest/input/feature-indexes/paldb-partition-shard{1,2,3}-0.dat`` and the
+duplicate-feature Avro input of ``AvroDataReaderIntegTest.scala:85``. The heart stores and the duplicate-feature
+Avro file are copied into ``tests/fixtures``; the (larger) GAME stores are read from the reference tree.
+"""
+import os
+
+import numpy as np
+import pytest
+
+from photon_ml_amd.constants import INTERCEPT_KEY
+from photon_ml_amd.io.index_map import open_index_map
+from photon_ml_amd.io.paldb import PalDBIndexMap, partition_of, read_store
+
+FIX = os.path.join(os.path.dirname(__file__), "fixtures")
+GAME = "/root/reference/photon-client/src/integTest/resources/GameIntegTest/input"
+DELIM = "\u0001"
+
+
+def key(name, term=""):
+    return name + DELIM + term
+
+
+# PalDBIndexMapTest.testNoInterceptMap / testWithInterceptMap
+NO_ICPT = {"1": 0, "2": 7, "3": 5, "4": 11, "5": 6, "6": 9, "7": 3, "8": 8, "9": 1, "10": 4, "11": 12, "12": 2,
+           "13": 10}
+WITH_ICPT = {"1": 0, "2": 8, "3": 5, "4": 12, "5": 6, "6": 10, "7": 2, "8": 9, "9": 1, "10": 4, "11": 13, "12": 3,
+             "13": 11}
+
+
+def test_heart_store_without_intercept():
+    m = PalDBIndexMap(os.path.join(FIX, "paldb_heart"), "global", 2)
+    assert len(m) == 13 and m.feature_dimension == 13
+    assert m.get_index(INTERCEPT_KEY) == -1
+    for name, idx in NO_ICPT.items():
+        assert m.get_index(key(name)) == idx
+        assert m.get_feature_name(idx) == key(name)
+    assert m.get_feature_name(13) is None
+
+
+def test_heart_store_with_intercept_and_opener():
+    m = open_index_map(os.path.join(FIX, "paldb_heart_icpt"), "global", 2)
+    assert isinstance(m, PalDBIndexMap) and len(m) == 14
+    assert m.get_index(INTERCEPT_KEY) == 7
+    for name, idx in WITH_ICPT.items():
+        assert m.get_index(key(name)) == idx and m.get_feature_name(idx) == key(name)
+    np.testing.assert_array_equal(m.get_indices([key("2"), "nope", INTERCEPT_KEY]), [8, -1, 7])
+
+
+def test_partitioning_is_spark_hash_partitioner():
+    """Every feature key sits in partition nonNegativeMod(key.hashCode, n) (Spark HashPartitioner)."""
+    for d in ("paldb_heart", "paldb_heart_icpt"):
+        for p in range(2):
+            kv = read_store(os.path.join(FIX, d, f"paldb-partition-global-{p}.dat"))
+            names = [k for k in kv if isinstance(k, str)]
+            assert names and all(partition_of(k, 2) == p for k in names)
+
+
+@pytest.mark.skipif(not os.path.isdir(GAME), reason="reference GAME integration-test inputs not present")
+def test_game_integration_stores():
+    maps = {s: PalDBIndexMap(os.path.join(GAME, "feature-indexes"), s, 1) for s in ("shard1", "shard2", "shard3")}
+    for m in maps.values():
+        n = len(m)
+        names = m.keys_in_order()
+        assert len(set(names)) == n and all(m.get_index(k) == i for i, k in enumerate(names))
+        assert m.get_index(INTERCEPT_KEY) >= 0
+    k1, k2, k3 = (set(maps[s].keys_in_order()) for s in ("shard1", "shard2", "shard3"))
+    song = {key("s", str(i)) for i in range(30)}
+    user = {key("u", str(i)) for i in range(30)}
+    # shard3: song features + intercept; shard2: global + user features; shard1: global + user + song features
+    assert k3 == song | {INTERCEPT_KEY}
+    assert k2 == k1 - song and user <= k2 and not (song & k2)
+    # every name of the feature-bag lists that the indexing run saw in the data is indexed
+    lists = os.path.join(GAME, "feature-lists")
+
+    def bag(name):
+        return {line.rstrip("\n").replace("\t", DELIM) for line in open(os.path.join(lists, name), encoding="utf-8")
+                if line.strip()}
+    assert bag("songFeatures") <= k3 and bag("userFeatures") <= k2
+    assert len(bag("features") & k1) > 0.99 * len(k1 - song - user - {INTERCEPT_KEY})
+
+
+def test_duplicate_feature_records_are_rejected():
+    """AvroDataReaderIntegTest.testReadDuplicateFeatures: a record listing one feature twice fails the read."""
+    from photon_ml_amd.io.data_reader import AvroDataReader, DuplicateFeatureError, FeatureShardConfiguration
+    path = os.path.join(FIX, "duplicate-features-yahoo-music-train.avro")
+    with pytest.raises(DuplicateFeatureError):
+        AvroDataReader().read(path, {"global": FeatureShardConfiguration(["features"], True)})
+    # the other bags of the same file are clean
+    data, _ = AvroDataReader().read(path, {"user": FeatureShardConfiguration(["userFeatures"], True)})
+    assert data.n_rows == 6
+
+
+def test_legacy_driver_trains_with_reference_paldb_index(tmp_path):
+    """DriverIntegTest with an off-heap index map: the heart PalDB stores (with intercept) drive the feature
+    indexing of the heart Avro input; the learned model is laid out in the store's index order."""
+    from photon_ml_amd.cli import driver as drv
+    ref = "/root/reference/photon-client/src/integTest/resources/DriverIntegTest/input/heart.avro"
+    train = ref if os.path.exists(ref) else os.path.join(FIX, "heart.avro")
+    args = ["--training-data-directory", train, "--output-directory", str(tmp_path / "o"), "--task",
+            "LOGISTIC_REGRESSION", "--num-iterations", "30", "--device", "cpu", "--offheap-indexmap-dir",
+            os.path.join(FIX, "paldb_heart_icpt"), "--offheap-indexmap-num-partitions", "2"]
+    d = drv.Driver(drv.build_parser().parse_args(args)).run()
+    assert d.train_data.n_features == 14
+    models = drv.read_text_model(str(tmp_path / "o" / drv.LEARNED_MODELS_TEXT))
+    (lam, coefs), = models.items()
+    assert len(coefs) == 14
