@@ -136,16 +136,42 @@ class FixedEffectCoordinate(Coordinate):
             off = base + (ps if rows is None else ps[rows])
         self.glm_data.set_offsets(off)
         if self.sampler is not None:
-            wts = self.sampler.sample_weights(self.labels, self.base_weights)
-            self.glm_data.set_weights(torch.from_numpy(np.asarray(wts, dtype=np.float64)))
+            self._apply_down_sampling()
         glm = self.problem.run(self._data_view(), model.glm if model is not None else None, dim=self.dim)
         self.last_tracker = self.problem.tracker
         # restore full weights for scoring/evaluation
         if self.sampler is not None:
-            self.glm_data.set_weights(torch.from_numpy(self.base_weights))
+            self._restore_weights()
         return FixedEffectModel(glm.update_coefficients(
             Coefficients(glm.coefficients.means.cpu(), None if glm.coefficients.variances is None
                          else glm.coefficients.variances.cpu())), self.shard_id)
+
+    def _row_ids(self) -> np.ndarray:
+        """Global row ids of this coordinate's rows (the down-sampling hash input: rank-independent samples)."""
+        return np.arange(len(self.labels)) if self.local_rows is None else np.asarray(self.local_rows)
+
+    def _apply_down_sampling(self):
+        """K20: rewrite the device weight vector in place (downsample_kernel) — no host arrays, no upload per
+        update; host data backends get the same weights from the host twin of the hash."""
+        gd = self.glm_data
+        wt = getattr(gd, "wt", None)
+        if isinstance(wt, torch.Tensor) and wt.is_cuda:
+            if getattr(self, "_w_base_dev", None) is None:
+                self._w_base_dev = wt.clone()
+                self._rowid_dev = torch.from_numpy(self._row_ids().astype(np.int64)).to(wt.device)
+            self.sampler.sample_weights_device(gd.y, self._w_base_dev, self._rowid_dev, out=wt)
+            gd.mark_weights_changed()
+            return
+        wts = self.sampler.sample_weights(self.labels, self.base_weights, self._row_ids())
+        gd.set_weights(torch.from_numpy(np.asarray(wts, dtype=np.float64)))
+
+    def _restore_weights(self):
+        wt = getattr(self.glm_data, "wt", None)
+        if isinstance(wt, torch.Tensor) and wt.is_cuda and getattr(self, "_w_base_dev", None) is not None:
+            wt.copy_(self._w_base_dev)
+            self.glm_data.mark_weights_changed()
+        else:
+            self.glm_data.set_weights(torch.from_numpy(self.base_weights))
 
     def score(self, model: FixedEffectModel) -> torch.Tensor:
         if self.local_rows is None:

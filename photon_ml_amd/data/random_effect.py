@@ -15,6 +15,7 @@ same greedy least-loaded bin packing as the reference partitioner (``parallel/sh
 from __future__ import annotations
 
 import math
+import os
 from dataclasses import dataclass, field
 from typing import List, Optional
 
@@ -139,7 +140,21 @@ class RandomEffectDataset:
         weight_mult = np.ones(n)
         counts = np.bincount(ent[rows], minlength=n_ent)
         cap = config.active_data_upper_bound
-        if cap is not None:
+        # K21 / K13 on the device (data/re_build.py: whole-coordinate sorts + segment reductions)
+        mode = os.environ.get("PML_RE_DEVICE_BUILD", "1")   # "0" host numpy, "force" torch ops even on the CPU
+        self.device_build = (self.device.type == "cuda" and mode != "0") or mode == "force"
+        if self.device_build:
+            from . import re_build
+            dev = self.device
+            ent_t = torch.from_numpy(ent.astype(np.int64)).to(dev)
+            rows_t = torch.from_numpy(rows).to(dev)
+        if cap is not None and self.device_build:
+            keys_t = re_build.reservoir_keys_t(java_string_hash(re_type),
+                                               torch.from_numpy(np.asarray(data.uids[rows], dtype=np.int64)).to(dev))
+            act_t, mult_t = re_build.reservoir_active_rows(ent_t, rows_t, keys_t, cap, n_ent)
+            active_rows = act_t.cpu().numpy()
+            weight_mult[active_rows] = mult_t.cpu().numpy()[ent[active_rows]]
+        elif cap is not None:
             key = reservoir_keys(re_type, data.uids[rows])
             order = np.lexsort((-key, ent[rows]))  # by entity, key descending
             r_sorted = rows[order]
@@ -157,7 +172,10 @@ class RandomEffectDataset:
         self.weight_mult = weight_mult
         # ---- passive data
         passive_rows = np.zeros(0, dtype=np.int64)
-        if config.passive_data_lower_bound is not None:
+        if config.passive_data_lower_bound is not None and self.device_build:
+            passive_rows = re_build.passive_rows(ent_t, rows_t, torch.from_numpy(active_rows).to(dev), n, n_ent,
+                                                 config.passive_data_lower_bound).cpu().numpy()
+        elif config.passive_data_lower_bound is not None:
             is_active = np.zeros(n, dtype=bool)
             is_active[active_rows] = True
             cand = rows[~is_active[rows]]
@@ -217,6 +235,8 @@ class RandomEffectDataset:
 
     # ------------------------------------------------------------------
     def _pearson_filter(self, xa: sp.csr_matrix, ea: np.ndarray, y: np.ndarray, ratio: float) -> sp.csr_matrix:
+        if getattr(self, "device_build", False):
+            return self._pearson_filter_device(xa, ea, y, ratio)
         xa = xa.tocsr()
         order = np.argsort(ea, kind="stable")
         keep_mask_rows = []
@@ -246,6 +266,21 @@ class RandomEffectDataset:
             keep_entry[m] = np.isin(xa_coo.col[m], np.fromiter(keep, dtype=np.int64))
         return sp.csr_matrix((xa_coo.data[keep_entry], (xa_coo.row[keep_entry], xa_coo.col[keep_entry])),
                              shape=xa.shape)
+
+    def _pearson_filter_device(self, xa: sp.csr_matrix, ea: np.ndarray, y: np.ndarray, ratio: float):
+        """K13 for every entity at once on the device (data/re_build.pearson_keep_entries)."""
+        from .re_build import pearson_keep_entries
+        dev = self.device
+        coo = xa.tocoo()
+        n_ent = int(ea.max()) + 1 if len(ea) else 0
+        keep = pearson_keep_entries(torch.from_numpy(coo.row.astype(np.int64)).to(dev),
+                                    torch.from_numpy(coo.col.astype(np.int64)).to(dev),
+                                    torch.from_numpy(coo.data.astype(np.float64)).to(dev),
+                                    torch.from_numpy(ea.astype(np.int64)).to(dev),
+                                    torch.from_numpy(np.asarray(y, dtype=np.float64)).to(dev),
+                                    torch.bincount(torch.from_numpy(ea.astype(np.int64)).to(dev), minlength=n_ent),
+                                    ratio).cpu().numpy()
+        return sp.csr_matrix((coo.data[keep], (coo.row[keep], coo.col[keep])), shape=xa.shape)
 
     def _matrix_t(self, device) -> torch.Tensor:
         """P^T [D x k] of the random projection as a device fp64 tensor (uploaded once)."""

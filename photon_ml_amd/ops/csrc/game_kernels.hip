@@ -12,6 +12,7 @@
 //   - gemm_nt_mfma_kernel — C = A B^T: back-projection of projected coefficients W P (and variances) of the
 //     random projection (projector/ProjectionMatrix.scala:95-124);
 // * spmm_rows_kernel — K15 forward random projection X P^T of sparse rows (ProjectionMatrix.scala:48-63).
+// * downsample_kernel — K20 fixed-effect down-sampling as an on-device weight rewrite.
 //
 // Built with: hipcc --offload-arch=gfx950 -O3 -shared -fPIC (photon_ml_amd/ops/build.py). C ABI, ctypes.
 
@@ -205,7 +206,55 @@ __global__ __launch_bounds__(256) void spmm_rows_kernel(const long long* __restr
   }
 }
 
+// K20 down-sampling (BinaryClassificationDownSampler.scala:47-68, DefaultDownSampler.scala:27-41) as a weight
+// rewrite on the device: row r is kept with probability `rate` (binary tasks: every positive is kept and kept
+// negatives get weight / rate), dropped rows get weight 0 — the HBM streams never change. The uniform of row r is a
+// counter-based hash of (seed, global row id) (splitmix64 finaliser, top 53 bits), reproduced bit for bit by the
+// host sampler (sampling/samplers.py), so CPU and GPU runs and every rank of a data-parallel job draw the same
+// sample for the same row.
+__device__ __forceinline__ unsigned long long splitmix64(unsigned long long x) {
+  x += 0x9E3779B97F4A7C15ull;
+  x = (x ^ (x >> 30)) * 0xBF58476D1CE4E5B9ull;
+  x = (x ^ (x >> 27)) * 0x94D049BB133111EBull;
+  return x ^ (x >> 31);
+}
+
+template <typename T>
+__global__ __launch_bounds__(256) void downsample_kernel(const T* __restrict__ y, const T* __restrict__ w0,
+                                                          const long long* __restrict__ rowid, long long n,
+                                                          unsigned long long seed, double rate, int binary,
+                                                          T* __restrict__ w) {
+  const long long i = (long long)blockIdx.x * 256 + threadIdx.x;
+  if (i >= n) return;
+  const unsigned long long id = rowid ? (unsigned long long)rowid[i] : (unsigned long long)i;
+  const double u = (double)(splitmix64(seed ^ splitmix64(id)) >> 11) * 0x1.0p-53;
+  const double wi = (double)w0[i];
+  double out;
+  if (binary) {
+    const bool pos = (double)y[i] >= 0.5;
+    out = pos ? wi : (u < rate ? wi / rate : 0.0);
+  } else {
+    out = u < rate ? wi : 0.0;
+  }
+  w[i] = (T)out;
+}
+
 extern "C" {
+
+int pml_downsample(int f64, const void* y, const void* w0, const long long* rowid, long long n,
+                   unsigned long long seed, double rate, int binary, void* w, void* stream) {
+  if (n <= 0) return 0;
+  const long long blocks = (n + 255) / 256;
+  if (blocks > 0x7fffffffLL) return -22;
+  if (f64)
+    hipLaunchKernelGGL(downsample_kernel<double>, dim3((unsigned)blocks), dim3(256), 0, (hipStream_t)stream,
+                       (const double*)y, (const double*)w0, rowid, n, seed, rate, binary, (double*)w);
+  else
+    hipLaunchKernelGGL(downsample_kernel<float>, dim3((unsigned)blocks), dim3(256), 0, (hipStream_t)stream,
+                       (const float*)y, (const float*)w0, rowid, n, seed, rate, binary, (float*)w);
+  LAUNCH_CHECK();
+  return 0;
+}
 
 int pml_spmm_rows(const long long* indptr, const int* col, const double* val, long long n_rows, const double* PT,
                   int k, double* Y, void* stream) {

@@ -345,6 +345,13 @@ class DeviceGLMData(GLMComputable):
         self.o.copy_(torch.as_tensor(offsets, device=self.device).to(self.vdt))
         self._z_key = None
         self._step_base = None
+        self._dzz_key = None          # cached w l''(z) depends on the margins, hence on the offsets
+
+    def mark_weights_changed(self):
+        """The row weights were rewritten in place (down-sampling): drop every cache that folds them in."""
+        self._dzz_key = None
+        self._z_key = None
+        self._step_base = None
 
     # ---- margin-space line search (GLMObjective.margin_line_search / LBFGS): z(t) = z0 + t zd ----------------
     # State: the margins of the last accepted point are z0 + tpend * zd (the accepted step is materialised
@@ -478,6 +485,7 @@ class DeviceGLMData(GLMComputable):
 
     def set_weights(self, weights):
         self.wt.copy_(torch.as_tensor(weights, device=self.device).to(self.vdt))
+        self.mark_weights_changed()
 
     # ------------------------------------------------------------------
     def _rows(self, t: torch.Tensor, c: int) -> int:

@@ -337,7 +337,9 @@ def game_lib() -> Optional[ctypes.CDLL]:
                                     c_void_p]
         lib.pml_spmm_rows.argtypes = [c_void_p, c_void_p, c_void_p, ctypes.c_longlong, c_void_p, c_int, c_void_p,
                                       c_void_p]
-        for f in ("pml_score_rows", "pml_bgram", "pml_gemm_nt", "pml_spmm_rows"):
+        lib.pml_downsample.argtypes = [c_int, c_void_p, c_void_p, c_void_p, ctypes.c_longlong, ctypes.c_ulonglong,
+                                       c_double, c_int, c_void_p, c_void_p]
+        for f in ("pml_score_rows", "pml_bgram", "pml_gemm_nt", "pml_spmm_rows", "pml_downsample"):
             getattr(lib, f).restype = c_int
         lib._pml_typed = True
     return lib
@@ -416,6 +418,20 @@ def spmm_rows(x, PT: torch.Tensor) -> torch.Tensor:
     check(lib.pml_spmm_rows(indptr.data_ptr(), col.data_ptr(), val.data_ptr(), n, PT.data_ptr(), k, Y.data_ptr(),
                             stream_handle(dev)), "spmm_rows")
     return Y
+
+
+def downsample_weights(y: torch.Tensor, w0: torch.Tensor, rate: float, binary: bool, seed: int,
+                       rowid: Optional[torch.Tensor] = None, out: Optional[torch.Tensor] = None) -> torch.Tensor:
+    """K20 weight rewrite on the device (``downsample_kernel``); ``rowid`` = global row ids (int64) of the rows."""
+    lib = require_game_lib()
+    assert y.dtype == w0.dtype and y.dtype in (torch.float32, torch.float64) and y.numel() == w0.numel()
+    out = torch.empty_like(w0) if out is None else out
+    if rowid is not None:
+        assert rowid.dtype == torch.int64 and rowid.numel() == y.numel() and rowid.device == y.device
+    check(lib.pml_downsample(int(y.dtype == torch.float64), y.data_ptr(), w0.data_ptr(),
+                             None if rowid is None else rowid.data_ptr(), y.numel(), seed & 0xFFFFFFFFFFFFFFFF,
+                             float(rate), int(binary), out.data_ptr(), stream_handle(y.device)), "downsample")
+    return out
 
 
 def check(rc: int, what: str):

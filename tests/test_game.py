@@ -264,3 +264,35 @@ def test_estimator_without_warm_start_matches_fresh_fit():
     for e in b.get("per-user").entity_ids:
         np.testing.assert_allclose(a.get("per-user").coefficients_of(e).means.numpy(),
                                    b.get("per-user").coefficients_of(e).means.numpy(), rtol=1e-9, atol=1e-11)
+
+
+def test_device_build_keys_match_host():
+    from photon_ml_amd.data.re_build import reservoir_keys_t
+    uids = np.array([0, 1, 2, 12345678901, -5, 2 ** 62 + 17, -(2 ** 62)], dtype=np.int64)
+    for t in ("userId", "songId", ""):
+        host = reservoir_keys(t, uids)
+        dev = reservoir_keys_t(java_string_hash(t), torch.from_numpy(uids)).numpy()
+        assert np.array_equal(host, dev), (t, host, dev)
+
+
+@pytest.mark.parametrize("cap,passive,ratio", [(20, 5, None), (7, 0, 0.05), (None, None, 0.3), (3, 2, 0.5)])
+def test_random_effect_device_build_matches_host(cap, passive, ratio, monkeypatch):
+    """K21 reservoir, passive set and K13 Pearson selection as whole-coordinate sorts / segment sums
+    (data/re_build.py) == the host implementation: same active / passive rows, weights and selected features."""
+    data, _ = generate_game_data(n_rows=3000, n_users=25, d_user=20, seed=44, task="LOGISTIC_REGRESSION")
+    cfg = RandomEffectDataConfiguration("userId", "user", active_data_upper_bound=cap,
+                                        passive_data_lower_bound=passive, features_to_samples_ratio=ratio)
+    out = {}
+    for mode in ("0", "force"):
+        monkeypatch.setenv("PML_RE_DEVICE_BUILD", mode)
+        ds = RandomEffectDataset(data, cfg, "cpu", layout="dense")
+        assert ds.device_build == (mode == "force")
+        out[mode] = ds
+    a, b = out["0"], out["force"]
+    assert np.array_equal(a.active_rows, b.active_rows) and np.array_equal(a.passive_rows, b.passive_rows)
+    np.testing.assert_array_equal(a.weight_mult, b.weight_mult)
+    xa, xb = a.x_active.tocsr(), b.x_active.tocsr()
+    xa.sort_indices()
+    xb.sort_indices()
+    assert np.array_equal(xa.indptr, xb.indptr) and np.array_equal(xa.indices, xb.indices)
+    np.testing.assert_array_equal(xa.data, xb.data)

@@ -155,3 +155,23 @@ def test_random_projection_coordinate_on_gpu_matches_cpu():
         np.testing.assert_allclose(b.coefficients_of(e).variances.numpy(), a.coefficients_of(e).variances.numpy(),
                                    rtol=1e-7, atol=1e-9)
     torch.testing.assert_close(sb, sa, rtol=1e-7, atol=1e-8)
+
+
+@pytest.mark.parametrize("cap,passive,ratio", [(20, 5, None), (7, 0, 0.05), (3, 2, 0.5)])
+def test_random_effect_build_on_gpu_matches_host(cap, passive, ratio, monkeypatch):
+    """Reservoir (K21), passive set and Pearson selection (K13) on the GPU (radix sorts, segment sums) == host."""
+    from photon_ml_amd.data.random_effect import RandomEffectDataset
+    data, _ = generate_game_data(n_rows=6000, n_users=40, d_user=24, seed=45, task="LOGISTIC_REGRESSION")
+    cfg = RandomEffectDataConfiguration("userId", "user", active_data_upper_bound=cap,
+                                        passive_data_lower_bound=passive, features_to_samples_ratio=ratio)
+    monkeypatch.setenv("PML_RE_DEVICE_BUILD", "0")
+    a = RandomEffectDataset(data, cfg, "cuda", layout="dense")
+    monkeypatch.setenv("PML_RE_DEVICE_BUILD", "1")
+    b = RandomEffectDataset(data, cfg, "cuda", layout="dense")
+    assert b.device_build and not a.device_build
+    assert np.array_equal(a.active_rows, b.active_rows) and np.array_equal(a.passive_rows, b.passive_rows)
+    np.testing.assert_array_equal(a.weight_mult, b.weight_mult)
+    xa, xb = a.x_active.tocsr(), b.x_active.tocsr()
+    xa.sort_indices()
+    xb.sort_indices()
+    assert np.array_equal(xa.indptr, xb.indptr) and np.array_equal(xa.indices, xb.indices)
