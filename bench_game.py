@@ -17,7 +17,9 @@ scores, both rescored, plus the training-loss evaluation. Nothing is skipped ins
 GPUs -> 1.25M entities per GPU, 20 rows x 50 features per entity covering each entity's 1000-feature pool exactly
 (+ intercept: 1001 coefficients per entity), integer entity ids, 1M-feature fixed effect.
 
-Usage: python bench_game.py [--gpus N --steps K --warmup W] [--config small|game5]; for N > 1 launch with
+``--config game5pl`` = the same with power-law entity sizes (see ``generate_game_bench_data(sizes="powerlaw")``).
+
+Usage: python bench_game.py [--gpus N --steps K --warmup W] [--config small|game5|game5pl]; for N > 1 launch with
 torch.distributed.run.
 """
 from __future__ import annotations
@@ -39,6 +41,10 @@ PRESETS = {
                   pool="random", int_ids=0),
     "game5": dict(entities_per_gpu=1_250_000, rows_per_entity=20, re_dim=1000, re_nnz=50, fe_dim=1_000_000,
                   fe_nnz=30, pool="exact", int_ids=1),
+    # config 5 with power-law entity sizes (mean 20 rows, Pareto 1.3 tail up to 20k rows): row-space solves for
+    # the small entities, the primal block-diagonal solve for the large ones (n_e > 64 or n_e > d_e)
+    "game5pl": dict(entities_per_gpu=1_250_000, rows_per_entity=20, re_dim=1000, re_nnz=50, fe_dim=1_000_000,
+                    fe_nnz=30, pool="random", int_ids=1, sizes="powerlaw"),
 }
 
 
@@ -57,6 +63,7 @@ def main():
     ap.add_argument("--fe-nnz", type=int)
     ap.add_argument("--pool", choices=["random", "exact"])
     ap.add_argument("--int-ids", type=int)
+    ap.add_argument("--sizes", choices=["uniform", "powerlaw"])
     ap.add_argument("--fe-iters", type=int, default=10)
     ap.add_argument("--re-iters", type=int, default=10)
     ap.add_argument("--precision", default="bf16", choices=["bf16", "f32", "f64"])
@@ -90,7 +97,7 @@ def main():
     data = generate_game_bench_data(args.entities_per_gpu, args.rows_per_entity, args.re_dim, args.re_nnz,
                                     args.fe_dim, args.fe_nnz, seed=args.seed + 1000 * rank,
                                     entity_offset=rank * args.entities_per_gpu, pool=args.pool,
-                                    int_ids=bool(args.int_ids))
+                                    int_ids=bool(args.int_ids), sizes=args.sizes or "uniform")
     log(f"data generated in {time.time() - t0:.1f}s: {data.n_rows} rows/GPU")
     t0 = time.time()
     fe_cfg = GLMOptimizationConfiguration(OptimizerConfig("LBFGS", args.fe_iters, 1e-12),
@@ -147,7 +154,8 @@ def main():
             "vs_baseline": None,
             "dtype": args.precision,
             "data": "synthetic (Zipf fixed-effect features, per-entity private random-effect features)",
-            "config": {"model": "game_logistic_fe_lbfgs_re_tron", "preset": args.config, "global_batch": total_rows, "seq_len": None,
+            "config": {"model": "game_logistic_fe_lbfgs_re_tron", "preset": args.config, "global_batch": total_rows,
+                       "seq_len": None, "entity_sizes": args.sizes or "uniform",
                        "entities": args.entities_per_gpu * world, "rows_per_entity": args.rows_per_entity,
                        "re_dim": args.re_dim, "fe_dim": args.fe_dim, "fe_iters": args.fe_iters,
                        "re_iters": args.re_iters, "parallelism": f"dp{world}+ep{world}"},

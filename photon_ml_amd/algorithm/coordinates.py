@@ -336,12 +336,28 @@ class RandomEffectCoordinate(Coordinate):
             if W0 is None:
                 W0 = self._lazy_W()
             with Timed(f"RE {self.coordinate_id}: primal block-diagonal solve", log, logging.DEBUG):
-                if oc.optimizer_type == OptimizerType.TRON:
-                    res = batched_tron(seg, self.loss, l2, W0, oc.tolerance, oc.maximum_iterations, frozen=frozen)
+                sub = self._primal_subset(frozen) if frozen is not None else None
+                if sub is not None:
+                    # only the entities NOT solved in their row space, on their own rows / coefficients
+                    sub.seg.o = seg.o[sub.rows]
+                    sub.seg._dzz_key = None
+                    prob, W0p = sub.seg, W0[sub.cols].contiguous()
+                    fz = None
                 else:
-                    res = batched_lbfgs(seg, self.loss, l2, W0, oc.tolerance, oc.maximum_iterations, l1=l1,
-                                        frozen=frozen)
-                W_all, iters, reasons = res.W, res.iters, res.reason
+                    prob, W0p, fz = seg, W0, frozen
+                if oc.optimizer_type == OptimizerType.TRON:
+                    res = batched_tron(prob, self.loss, l2, W0p, oc.tolerance, oc.maximum_iterations, frozen=fz)
+                else:
+                    res = batched_lbfgs(prob, self.loss, l2, W0p, oc.tolerance, oc.maximum_iterations, l1=l1,
+                                        frozen=fz)
+                if sub is not None:
+                    W_all = torch.zeros_like(W0).index_copy_(0, sub.cols, res.W)
+                    iters = torch.zeros(seg.B, dtype=torch.long, device=W0.device).index_copy_(0, sub.entities,
+                                                                                             res.iters)
+                    reasons = torch.zeros(seg.B, dtype=torch.long, device=W0.device).index_copy_(0, sub.entities,
+                                                                                               res.reason)
+                else:
+                    W_all, iters, reasons = res.W, res.iters, res.reason
         else:
             W_all = None
             iters = torch.zeros(seg.B, dtype=torch.long, device=seg.y.device)
@@ -390,6 +406,28 @@ class RandomEffectCoordinate(Coordinate):
                                 ds.entity_ids, ds.dim, ds.projection_keys_t, W, var)
         self._last = (out, res.W)
         return out
+
+    def _primal_subset(self, frozen: torch.Tensor):
+        """Sub-problem of the entities outside the row-space batch (built once per row-space batch; the kept
+        segmented CSR is released afterwards). None when every entity with data is frozen or the data keeps no
+        CSR (then the frozen mask is used on the whole problem)."""
+        if os.environ.get("PML_RE_PRIMAL_SUBSET", "1") == "0":
+            return None
+        cached = getattr(self, "_sub", None)
+        if cached is not None and cached[0] is frozen:
+            return cached[1]
+        ds = self.dataset
+        if getattr(ds, "_seg_csr", None) is None:
+            return None
+        seg = ds.seg
+        n_e = seg.row_ptr[1:] - seg.row_ptr[:-1]
+        mask = (~frozen) & (n_e > 0)
+        if not bool(mask.any()):
+            return None
+        sub = ds.entity_subset(mask)
+        ds.release_csr()
+        self._sub = (frozen, sub)
+        return sub
 
     def _row_space(self, l1: float, oc):
         """Row-space batch for the wide entities (built once per dataset), or None when not applicable."""

@@ -100,6 +100,15 @@ def pearson_scores(xe: sp.csr_matrix, y: np.ndarray) -> dict:
 
 
 @dataclass
+class SegmentSubset:
+    """Block-diagonal sub-problem over some entities of a segmented coordinate (``entity_subset``)."""
+    seg: object               # SegmentedGLMData over the subset
+    rows: torch.Tensor        # positions of its rows in the parent's (entity-sorted) row order
+    cols: torch.Tensor        # positions of its coefficients in the parent's coefficient vector
+    entities: torch.Tensor    # parent entity index of each subset entity
+
+
+@dataclass
 class Bucket:
     entities: np.ndarray      # entity indices in this bucket [B]
     rows: torch.Tensor        # [B, n] global sample index of each slot, -1 for padding
@@ -371,6 +380,8 @@ class RandomEffectDataset:
         ww = np.asarray(wts, dtype=np.float64)[rows]
         glm = make_glm_data(LabeledData(x_seg, yy, np.zeros(len(rows)), ww), self.device, "f64", col_windows=True)
         dev = glm.device
+        self._seg_csr = (torch.from_numpy(x_seg.indptr.astype(np.int64)), torch.from_numpy(
+            x_seg.indices.astype(np.int64)), torch.from_numpy(x_seg.data.astype(np.float64)))
         col_entity = np.repeat(np.arange(n_ent, dtype=np.int64), np.diff(self.projection.ptr))
         self.seg_rows = torch.from_numpy(rows).to(dev)
         self.projection_keys_t = torch.from_numpy(self.projection.keys).to(dev)
@@ -421,13 +432,59 @@ class RandomEffectDataset:
         ww = torch.from_numpy(np.asarray(wts, dtype=np.float64)).to(dev)[rows_t]
         glm = DeviceGLMData.from_device_csr(nip, pos, val, yy, torch.zeros_like(yy), ww, max(d_total, 1), dev,
                                             "f64", col_windows=True)
-        del pos, val
+        self._seg_csr = (nip, pos, val)   # kept until the primal sub-problem is built (entity_subset), then freed
         self.projection_keys_t = ukeys
         self.col_entity_t = ukeys // D
         self.seg_rows = rows_t
         self.seg = SegmentedGLMData(glm, e_row, self.col_entity_t, n_ent, yy, ww,
                                     torch.zeros_like(yy))
         self.d_total = d_total
+
+    def entity_subset(self, mask: torch.Tensor) -> "SegmentSubset":
+        """The block-diagonal sub-problem of the entities in ``mask`` (their rows and coefficient ranges only),
+        built on the data's device from the kept CSR. Used for the primal solve of the entities NOT handled in
+        their row space: its Hessian-vector passes then stream only those entities' non-zeros (with power-law
+        entity sizes, ~40 % of them) instead of the whole coordinate."""
+        from ..ops.backend import make_glm_data
+        from ..ops.device import DeviceGLMData
+        from ..optimization.batched import SegmentedGLMData
+        if getattr(self, "_seg_csr", None) is None:
+            raise RuntimeError("entity_subset needs the segmented CSR (built once per dataset)")
+        seg = self.seg
+        nip, pos, val = self._seg_csr
+        dev = seg.y.device
+        mask = mask.to(dev)
+        row_sel = torch.nonzero(mask[seg.row_entity]).squeeze(1)
+        col_mask = mask[seg.col_entity]
+        col_sel = torch.nonzero(col_mask).squeeze(1)
+        newcol = torch.cumsum(col_mask.to(torch.int64), 0) - 1
+        nip_d, pos_d, val_d = nip.to(dev), pos.to(dev), val.to(dev)
+        lens = (nip_d[1:] - nip_d[:-1])[row_sel]
+        sip = torch.zeros(row_sel.numel() + 1, dtype=torch.int64, device=dev)
+        torch.cumsum(lens, 0, out=sip[1:])
+        nnz = int(sip[-1])
+        src = torch.repeat_interleave(nip_d[:-1][row_sel] - sip[:-1], lens, output_size=nnz) + torch.arange(
+            nnz, device=dev)
+        spos = newcol[pos_d[src]]
+        sval = val_d[src]
+        ent_new = torch.cumsum(mask.to(torch.int64), 0) - 1
+        B = int(mask.sum())
+        d_sub = int(col_sel.numel())
+        yy, ww = seg.y[row_sel], seg.w[row_sel]
+        if dev.type == "cuda":
+            glm = DeviceGLMData.from_device_csr(sip, spos, sval, yy, torch.zeros_like(yy), ww, max(d_sub, 1), dev,
+                                                "f64", col_windows=True)
+        else:
+            from .matrix import LabeledData as _LD
+            xs = sp.csr_matrix((sval.numpy(), spos.numpy(), sip.numpy()), shape=(row_sel.numel(), max(d_sub, 1)))
+            glm = make_glm_data(_LD(xs, yy.numpy(), np.zeros(row_sel.numel()), ww.numpy()), dev, "f64",
+                                col_windows=True)
+        sub = SegmentedGLMData(glm, ent_new[seg.row_entity[row_sel]], ent_new[seg.col_entity[col_sel]], B, yy, ww,
+                               torch.zeros_like(yy))
+        return SegmentSubset(sub, row_sel, col_sel, torch.nonzero(mask).squeeze(1))
+
+    def release_csr(self):
+        self._seg_csr = None
 
     @property
     def n_entities(self) -> int:

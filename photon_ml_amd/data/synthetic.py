@@ -241,7 +241,8 @@ def generate_device_shard(n_rows: int, n_features: int, nnz_per_row: int, device
 def generate_game_bench_data(n_entities: int, rows_per_entity: int, re_dim: int = 100, re_nnz: int = 10,
                              fe_dim: int = 100_000, fe_nnz: int = 30, re_vocab: int = 1 << 20, seed: int = 7,
                              entity_offset: int = 0, task: str = "LOGISTIC_REGRESSION", pool: str = "random",
-                             int_ids: bool = False):
+                             int_ids: bool = False, sizes: str = "uniform", size_alpha: float = 1.3,
+                             max_rows: int = 20000):
     """Synthetic GAME data at benchmark scale (vectorised, no per-row Python):
 
     * ``global`` shard: ``fe_nnz`` Zipf(1.1) features out of ``fe_dim`` + intercept (last column);
@@ -251,14 +252,33 @@ def generate_game_bench_data(n_entities: int, rows_per_entity: int, re_dim: int 
     * ``pool="exact"``: instead of random draws, row j of an entity takes pool slots ``[j * re_nnz, (j + 1) *
       re_nnz) mod re_dim`` — every entity then has exactly ``min(re_dim, rows * re_nnz)`` coefficients (e.g. the
       "1k coefficients per entity" GAME config with 20 rows x 50 features);
+    * ``sizes="powerlaw"``: rows per entity Pareto(``size_alpha``) distributed (1 .. ``max_rows``, mean
+      ``rows_per_entity``) instead of all equal — real GLMix entity sizes: most entities have a few rows (row-space
+      solves), a tail has hundreds to thousands (the primal block-diagonal solve, entities with n_e > d_e);
     * id tag ``entityId`` = ``e<global entity index>`` (or the integer index with ``int_ids``; ``entity_offset``
       shifts the range, e.g. per rank);
     * labels from a random ground truth (logistic / linear / Poisson).
     """
     from ..data.game_data import GameData
     rng = np.random.default_rng(seed)
-    n = n_entities * rows_per_entity
-    ent = rng.permutation(np.repeat(np.arange(n_entities, dtype=np.int64), rows_per_entity))
+    if sizes == "powerlaw":
+        if pool == "exact":
+            raise ValueError("pool='exact' needs equal entity sizes")
+        u = rng.random(n_entities)
+        target = n_entities * rows_per_entity
+        xm = float(rows_per_entity) * (size_alpha - 1) / size_alpha
+        for _ in range(30):          # scale so that the capped Pareto sizes have the requested mean
+            cnt = np.minimum(np.ceil(xm * u ** (-1.0 / size_alpha)), max_rows).astype(np.int64)
+            tot = int(cnt.sum())
+            if abs(tot - target) <= 0.001 * target:
+                break
+            xm *= target / tot
+        ent = rng.permutation(np.repeat(np.arange(n_entities, dtype=np.int64), cnt))
+    elif sizes == "uniform":
+        ent = rng.permutation(np.repeat(np.arange(n_entities, dtype=np.int64), rows_per_entity))
+    else:
+        raise ValueError(f"unknown entity size law {sizes!r}")
+    n = len(ent)
     # fixed effect shard
     ranks = np.arange(1, fe_dim)
     p = ranks ** -1.1

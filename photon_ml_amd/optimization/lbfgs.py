@@ -32,37 +32,76 @@ MARGIN_LINE_SEARCH = os.environ.get("PML_MARGIN_LINE_SEARCH", "1") != "0"
 # dot-product recursion is ~2 % of an iteration), so off by default for replicated vectors; feature-sharded
 # vectors always use it (one all-reduce instead of 4k + 1).
 GRAM_MIN_DIM = int(os.environ.get("PML_LBFGS_GRAM_MIN_DIM", str(1 << 62)))
+# Replicated device vectors run the two-loop with 0-d device scalars (PML_LBFGS_DEVICE_TWO_LOOP=0: host scalars,
+# one synchronisation per dot product).
+DEVICE_TWO_LOOP = os.environ.get("PML_LBFGS_DEVICE_TWO_LOOP", "1") != "0"
 DEFAULT_NUM_CORRECTIONS = 10
 DEFAULT_TOLERANCE = 1.0e-7
 
 
+def _device_loop(g: torch.Tensor) -> bool:
+    """Replicated device vectors: the two-loop keeps its scalars on the device (no host synchronisation)."""
+    return g.is_cuda and not vector_space.current().sharded and DEVICE_TWO_LOOP
+
+
 class _History:
-    """Ring buffer of the last m (s, y) pairs plus rho = 1/(s.y)."""
+    """Ring buffer of the last m (s, y) pairs plus rho = 1/(s.y) (host floats; for device vectors also 0-d
+    device tensors rho_t and the newest pair's scaling s.y / y.y, so the two-loop never synchronises)."""
 
     def __init__(self, m: int):
         self.m = m
         self.s = []
         self.y = []
         self.rho = []
+        self.rho_t = []
+        self.gamma_t = None
 
     def clear(self):
-        self.s, self.y, self.rho = [], [], []
+        self.s, self.y, self.rho, self.rho_t, self.gamma_t = [], [], [], [], None
 
     def push(self, s: torch.Tensor, y: torch.Tensor) -> bool:
-        sy = _dot(s, y)
+        if _device_loop(s):
+            # s.y and y.y in ONE host synchronisation (the curvature test is a host decision)
+            sy_t, yy_t = torch.dot(s, y), torch.dot(y, y)
+            sy, yy = torch.stack([sy_t, yy_t]).tolist()
+        else:
+            sy_t = yy_t = None
+            sy = _dot(s, y)
         if not (sy > 1e-300) or sy != sy:
             return False  # curvature condition violated: skip (Breeze would raise NaNHistory)
         self.s.append(s)
         self.y.append(y)
         self.rho.append(1.0 / sy)
+        if sy_t is not None:
+            self.rho_t.append(1.0 / sy_t)
+            self.gamma_t = sy_t / yy_t
         if len(self.s) > self.m:
             self.s.pop(0)
             self.y.pop(0)
             self.rho.pop(0)
+            if self.rho_t:
+                self.rho_t.pop(0)
         return True
+
+    def _apply_inverse_device(self, g: torch.Tensor) -> torch.Tensor:
+        """Two-loop with 0-d device scalars (dot products stay on the GPU, fused scaled adds via addcmul):
+        the same recursion and arithmetic order as the host-scalar loop below, no synchronisation."""
+        q = g.clone()
+        k = len(self.s)
+        alpha = [None] * k
+        for i in range(k - 1, -1, -1):
+            alpha[i] = self.rho_t[i] * torch.dot(self.s[i], q)
+            q.addcmul_(self.y[i], alpha[i], value=-1.0)
+        q.mul_(self.gamma_t)
+        for i in range(k):
+            beta = self.rho_t[i] * torch.dot(self.y[i], q)
+            q.addcmul_(self.s[i], alpha[i] - beta)
+        return q
 
     def apply_inverse(self, g: torch.Tensor) -> torch.Tensor:
         """Two-loop recursion: returns H g."""
+        if self.s and _device_loop(g) and len(self.rho_t) == len(self.s) and g.numel() < GRAM_MIN_DIM:
+            return self._apply_inverse_device(g)
         if self.s and (vector_space.current().sharded or (g.is_cuda and g.numel() >= GRAM_MIN_DIM)):
             return self._apply_inverse_gram(g)
         q = g.clone()
@@ -130,12 +169,19 @@ class LBFGS(Optimizer):
 
     def _inner_state(self) -> dict:
         h = self.history
-        return {"s": list(h.s), "y": list(h.y), "rho": list(h.rho), "failed_once": self._failed_once,
+        return {"s": list(h.s), "y": list(h.y), "rho": list(h.rho),
+                "gamma": None if h.gamma_t is None else float(h.gamma_t), "failed_once": self._failed_once,
                 "finished": self._finished, "inner_iter": self._inner_iter, "smooth_f": self._smooth_f,
                 "smooth_g": self._smooth_g}
 
     def _load_inner_state(self, d: dict):
         self.history.s, self.history.y, self.history.rho = list(d["s"]), list(d["y"]), list(d["rho"])
+        h = self.history
+        h.rho_t, h.gamma_t = [], None
+        if h.s and _device_loop(h.s[0]) and d.get("gamma") is not None:
+            dev = h.s[0].device      # device scalars of the sync-free two-loop (1/sy is exact-rounded either way)
+            h.rho_t = [torch.tensor(r, dtype=torch.float64, device=dev) for r in h.rho]
+            h.gamma_t = torch.tensor(d["gamma"], dtype=torch.float64, device=dev)
         self._failed_once, self._finished, self._inner_iter = d["failed_once"], d["finished"], d["inner_iter"]
         self._smooth_f, self._smooth_g = d["smooth_f"], d["smooth_g"]
 

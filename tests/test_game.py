@@ -296,3 +296,27 @@ def test_random_effect_device_build_matches_host(cap, passive, ratio, monkeypatc
     xb.sort_indices()
     assert np.array_equal(xa.indptr, xb.indptr) and np.array_equal(xa.indices, xb.indices)
     np.testing.assert_array_equal(xa.data, xb.data)
+
+
+@pytest.mark.parametrize("opt", ["TRON", "LBFGS"])
+def test_primal_entity_subset_matches_frozen_full_problem(opt, monkeypatch):
+    """Entities outside the row-space batch are solved on their own rows / coefficients (entity_subset) — same
+    coefficients, scores and iteration counts as the frozen-mask solve over the whole block-diagonal problem."""
+    data, _ = generate_game_data(n_rows=3000, n_users=300, d_user=30, seed=46, task="LOGISTIC_REGRESSION")
+    cfg = _cfg(opt, 1.0, 40, 1e-10)
+    out = {}
+    for mode in ("0", "1"):
+        monkeypatch.setenv("PML_RE_PRIMAL_SUBSET", mode)
+        c = RandomEffectCoordinate("u", data, RandomEffectDataConfiguration("userId", "user"), cfg,
+                                   "LOGISTIC_REGRESSION", device="cpu", layout="segmented")
+        m1 = c.update_model(c.initialize_model())
+        m2 = c.update_model(m1, partial_score=torch.from_numpy(np.cos(np.arange(data.n_rows)) * 0.2))
+        out[mode] = (c, m2, c.last_stats)
+        assert (getattr(c, "_sub", None) is not None) == (mode == "1")
+    (c0, a, s0), (c1, b, s1) = out["0"], out["1"]
+    assert 0 < c1._rs.B < int((c1.dataset.n_active > 0).sum())
+    assert s0["mean_iterations"] == pytest.approx(s1["mean_iterations"], rel=1e-6)
+    for e in a.entity_ids:
+        np.testing.assert_allclose(b.coefficients_of(e).means.numpy(), a.coefficients_of(e).means.numpy(),
+                                   rtol=1e-8, atol=1e-10)
+    torch.testing.assert_close(c1.score(b), c0.score(a), rtol=1e-8, atol=1e-10)

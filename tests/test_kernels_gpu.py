@@ -517,3 +517,21 @@ def test_narrow_rounds_match_wide_only_layout(precision, monkeypatch):
     assert abs(f1 - f0) <= tol * abs(f0) and abs(s1 - s0) <= tol * max(1.0, abs(s0))
     for a, b in ((g1, g0), (h1, h0), (d1, d0)):
         assert torch.allclose(a, b, rtol=tol, atol=tol * float(b.abs().max()))
+
+
+@pytest.mark.gpu
+def test_device_two_loop_matches_host_scalar_two_loop(monkeypatch):
+    """L-BFGS two-loop with 0-d device scalars (no per-dot synchronisation) == the host-scalar recursion."""
+    from photon_ml_amd.data.synthetic import generate_glm_data
+    from photon_ml_amd.function.objective import GLMObjective
+    from photon_ml_amd.ops.device import DeviceGLMData
+    from photon_ml_amd.optimization import lbfgs
+    data, _ = generate_glm_data("LOGISTIC_REGRESSION", 20000, 300, density=0.05, seed=12)
+    dev = DeviceGLMData.from_labeled(data, "cuda", "f64")
+    out = {}
+    for flag in (False, True):
+        monkeypatch.setattr(lbfgs, "DEVICE_TWO_LOOP", flag)
+        opt = lbfgs.LBFGS(tolerance=1e-10, max_iterations=40)
+        w, _ = opt.optimize(GLMObjective(LOGISTIC, 1.0), dev, torch.zeros(300, dtype=torch.float64, device="cuda"))
+        out[flag] = (w.cpu(), None)
+    torch.testing.assert_close(out[True][0], out[False][0], rtol=1e-9, atol=1e-11)
