@@ -68,7 +68,12 @@ def main():
     ap.add_argument("--re-iters", type=int, default=10)
     ap.add_argument("--precision", default="bf16", choices=["bf16", "f32", "f64"])
     ap.add_argument("--seed", type=int, default=11)
+    ap.add_argument("--log-level", default="WARNING",
+                    help="framework log level (DEBUG shows the per-phase timings of the random-effect update)")
     args = ap.parse_args()
+    import logging
+    logging.basicConfig(stream=sys.stderr, format="[%(asctime)s %(name)s] %(message)s")
+    logging.getLogger("photon_ml_amd").setLevel(args.log_level.upper())
     for k, v in PRESETS[args.config].items():
         if getattr(args, k) is None:
             setattr(args, k, v)

@@ -435,7 +435,7 @@ class RandomEffectCoordinate(Coordinate):
         if os.environ.get("PML_RE_ROW_SPACE", "1") == "0" or not row_space_eligible(l1, oc.constraint_map):
             return None
         if getattr(self, "_rs", None) is None:
-            self._rs = RowSpaceBatch(self.dataset.seg)
+            self._rs = RowSpaceBatch(self.dataset.seg, csr=getattr(self.dataset, "_seg_csr", None))
         return self._rs
 
     def _warm_start_segmented(self, model):

@@ -42,9 +42,11 @@ def lib_path(kind: str, name: str, sanitize: bool = None) -> Path:
 
 
 def _needs_build(src: Path, out: Path) -> bool:
+    """Out of date when the source or any header next to it (e.g. generated asm blocks) is newer."""
     if not out.exists():
         return True
-    return src.stat().st_mtime > out.stat().st_mtime
+    deps = [src] + sorted(src.parent.glob("*.h"))
+    return max(d.stat().st_mtime for d in deps) > out.stat().st_mtime
 
 
 def _hipcc() -> str:

@@ -1238,7 +1238,8 @@ static int g_tl_waves = 4;     // forward
 static int g_tl_waves_t = 4;   // transpose
 static int g_tl_pipe = 0;      // forward stream pipeline variant (see tl_stream)
 static int g_tl_pipe_t = 0;    // transpose stream pipeline variant
-static int g_rs_variant = 2;   // rs_tron_kernel variant (see the kernel); 2 measured fastest (scripts/rs_tron_bench.py)
+static int g_rs_variant = 3;   // rs_tron variant: 0-2 rs_tron_kernel<V>; for n <= 32: 3 rs_tron_dpp_kernel (L in registers
+                                // for n <= 16), 4 the same with L in LDS for every size (scripts/rs_tron_bench.py)
 static int g_tl_deep = 0;      // interleaved forward: 0 two-slot pipeline (P = 3), 1 deep S4/D1 (P = 5), 2 S6/D2 (P = 6)
 static int g_tl_deep_t = 0;    // interleaved transpose: same
 
@@ -1846,6 +1847,368 @@ __global__ __launch_bounds__(NTHREADS) void rs_tron_kernel(
 }
 
 // ============================================================================================================
+// Variant 3 of the fused row-space TRON (n <= 32): problems of GL = 4 / 8 / 16 lanes (K <= 4 / 8 / else), K =
+// the padded size (4, 8, 12, 16, 20, 24, 32), lane i holds vector entries i and (K > 16) i + 16.
+// Measured on variant 2 (profiles/rs_tron_roofline.md): 7.4K VALU instructions per wave of 2 problems, only
+// 20 % of them FMAs — the per-problem scalar work of truncated CG (divisions, square roots, trust-region
+// selects, butterfly sums) runs once per WAVE, so it is paid per problem in proportion to 64 / lanes-per-problem.
+// Here a wave holds 4 (K > 8), 8 or 16 problems, and every matrix-vector term is ONE instruction:
+// v_fmac_f64_dpp with row_newbcast (DPP64) broadcasts the vector entry from lane k of the 16-lane row straight
+// into the FMA (rs_dpp_blocks.h), with no LDS vector slot and no shuffles. L lives in registers for K <= 16 (row
+// i and column i of L: 2K doubles per lane) and in LDS for K > 16 (zero-padded K x (K+1) rows per problem);
+// triangular blocks of L above the diagonal are skipped. CG keeps ||step||^2 from the previous trial (the
+// same sum), forms the boundary terms (step.d, d.d) only when some problem hits the trust region, and takes
+// ||g||^2 = ||r0||^2: 3 group sums per CG step instead of 6. Same TRON semantics as rs_tron_kernel.
+// ============================================================================================================
+#include "rs_dpp_blocks.h"
+
+// two independent group sums, stage by stage (ILP 2 on the DPP / add latency chain)
+template <int GL>
+__device__ __forceinline__ void group_sum2(double& a, double& b) {
+  a += dpp_f64<0xB1>(a); b += dpp_f64<0xB1>(b);
+  a += dpp_f64<0x4E>(a); b += dpp_f64<0x4E>(b);
+  if constexpr (GL >= 8) { a += dpp_f64<0x141>(a); b += dpp_f64<0x141>(b); }
+  if constexpr (GL >= 16) { a += dpp_f64<0x140>(a); b += dpp_f64<0x140>(b); }
+}
+
+template <int GL>
+__device__ __forceinline__ double group_sum(double v) {
+  v += dpp_f64<0xB1>(v);                       // quad_perm [1,0,3,2]
+  v += dpp_f64<0x4E>(v);                       // quad_perm [2,3,0,1]
+  if constexpr (GL >= 8) v += dpp_f64<0x141>(v);   // row_half_mirror
+  if constexpr (GL >= 16) v += dpp_f64<0x140>(v);  // row_mirror
+  return v;
+}
+
+template <int K, bool LREG>
+struct RsGeom {
+  static constexpr int GL = K <= 4 ? 4 : (K <= 8 ? 8 : 16);
+  static constexpr int P = 64 / GL;                 // problems per wave
+  static constexpr int R = (K + 15) / 16;           // vector entries per lane
+  static constexpr bool REG = LREG && R == 1;       // L in registers (else LDS)
+  static constexpr int K1 = K > 16 ? K - 16 : 1;    // terms of the second column block
+  static constexpr int SP = K + 1;                  // LDS row stride (doubles)
+  static constexpr int PS0 = K * SP;
+  static constexpr int PS = PS0 + (((16 - PS0 % 32) % 32) + 32) % 32;   // problem stride = 16 mod 32 doubles
+  static constexpr int WPB = REG ? 4 : 2;           // waves per workgroup
+};
+
+template <int K, bool LREG>
+__global__ __launch_bounds__(256) void rs_tron_dpp_kernel(
+    int B, int n, const double* __restrict__ Lm, const double* __restrict__ Y, const double* __restrict__ O,
+    const double* __restrict__ WT, double* __restrict__ Beta, double* __restrict__ Fout, int* __restrict__ Iters,
+    int* __restrict__ Reason, int loss, double l2, double tol, int max_iter, int max_fail, int max_cg) {
+  using Gm = RsGeom<K, LREG>;
+  constexpr int GL = Gm::GL, P = Gm::P, R = Gm::R, K1 = Gm::K1, SP = Gm::SP, PS = Gm::PS;
+  extern __shared__ double smem[];
+  const int lane = threadIdx.x & 63, w = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
+  const int q = lane / GL, i = lane % GL;
+  const long long b0 = ((long long)blockIdx.x * Gm::WPB + w) * P;
+  if (b0 >= B) return;
+  const bool prob_on = b0 + q < B;
+  const long long b = prob_on ? b0 + q : b0;
+  const long long nn = (long long)n * n;
+  bool on[R];
+  long long o[R];
+  double y[R], off[R], wt[R], W[R];
+#pragma unroll
+  for (int s = 0; s < R; ++s) {
+    const int e = i + 16 * s;
+    on[s] = prob_on && e < n;
+    o[s] = b * n + (e < n ? e : 0);
+    y[s] = on[s] ? Y[o[s]] : 0.0;
+    off[s] = on[s] ? O[o[s]] : 0.0;
+    wt[s] = on[s] ? WT[o[s]] : 0.0;
+    W[s] = on[s] ? Beta[o[s]] : 0.0;
+  }
+  // ---- L: registers (row i and column i) or LDS (zero-padded, this wave's P problems)
+  double Lr[Gm::REG ? K : 1], Lc[Gm::REG ? K : 1];
+  int lq = 0;                                   // this problem's LDS base (doubles)
+  if constexpr (Gm::REG) {
+    const double* Lb = Lm + b * nn;
+#pragma unroll
+    for (int k = 0; k < K; ++k) {
+      const bool ok = prob_on && i < n && k < n;
+      Lr[k] = ok ? Lb[(long long)i * n + k] : 0.0;
+      Lc[k] = ok ? Lb[(long long)k * n + i] : 0.0;
+    }
+  } else {
+    const int wb = w * P * PS;
+    for (int idx = lane; idx < P * PS; idx += 64) {
+      const int qq = idx / PS, rem = idx - qq * PS, r = rem / SP, c = rem - r * SP;
+      double v = 0.0;
+      if (b0 + qq < B && r < n && c < n) v = Lm[(b0 + qq) * nn + (long long)r * n + c];
+      smem[wb + idx] = v;
+    }
+    __builtin_amdgcn_s_waitcnt(0);
+    __builtin_amdgcn_wave_barrier();
+    lq = wb + q * PS;
+  }
+  // sum_k m[k] * (entry k of the lane's problem vector), L in registers
+  auto reg_mv = [&](double v, const double (&m)[R == 1 ? K : 1]) {
+    if constexpr (R != 1) {
+      return 0.0;
+    } else if constexpr (GL == 16) {
+      double a0 = 0.0, a1 = 0.0;
+      bcf<16, K>(a0, a1, v, m);
+      return a0 + a1;
+    } else {
+      double acc[16 / GL];
+#pragma unroll
+      for (int g = 0; g < 16 / GL; ++g) acc[g] = 0.0;
+      bcg<GL, K>(acc, v, m);
+      const int mine = (lane & 15) / GL;
+      double r = acc[0];
+#pragma unroll
+      for (int g = 1; g < 16 / GL; ++g) r = mine == g ? acc[g] : r;
+      return r;
+    }
+  };
+  // (L v) and (L^T u) for the lane's entries; entries >= n are 0 on input and on output
+  auto mv = [&](const double (&v)[R], double (&out)[R]) {
+    if constexpr (Gm::REG) {
+      out[0] = on[0] ? reg_mv(v[0], Lr) : 0.0;
+    } else if constexpr (R == 1) {
+      double m[K];
+      int base = lq + i * SP;
+      asm volatile("" : "+v"(base));   // re-read L from LDS in every product (no hoisting into registers)
+#pragma unroll
+      for (int k = 0; k < K; ++k) m[k] = smem[base + k];
+      out[0] = on[0] ? reg_mv(v[0], m) : 0.0;
+    } else {
+      double m[16], m1[K1];
+      // re-read L from LDS in every product: laundering the (integer) base keeps the compiler from hoisting
+      // all 2K^2/16 values per lane out of the CG loop into (spilled) registers
+      int b0i = lq + i * SP, b1i = lq + min(i + 16, K - 1) * SP;
+      asm volatile("" : "+v"(b0i), "+v"(b1i));
+#pragma unroll
+      for (int k = 0; k < 16; ++k) m[k] = smem[b0i + k];
+      double a0 = 0.0, a1 = 0.0;
+      bcf<16, 16>(a0, a1, v[0], m);
+#pragma unroll
+      for (int k = 0; k < 16; ++k) m[k] = smem[b1i + k];
+#pragma unroll
+      for (int k = 0; k < K1; ++k) m1[k] = smem[b1i + 16 + k];
+      double c0 = 0.0, c1 = 0.0;
+      bcf<16, 16>(c0, c1, v[0], m);
+      bcf<16, K1>(c0, c1, v[1], m1);
+      out[0] = on[0] ? a0 + a1 : 0.0;
+      out[1] = on[1] ? c0 + c1 : 0.0;
+    }
+  };
+  auto mvt = [&](const double (&u)[R], double (&out)[R]) {
+    if constexpr (Gm::REG) {
+      out[0] = on[0] ? reg_mv(u[0], Lc) : 0.0;
+    } else if constexpr (R == 1) {
+      double m[K];
+      int base = lq + i;
+      asm volatile("" : "+v"(base));
+#pragma unroll
+      for (int k = 0; k < K; ++k) m[k] = smem[base + k * SP];
+      out[0] = on[0] ? reg_mv(u[0], m) : 0.0;
+    } else {
+      double m[16], m1[K1], m2[K1];
+      int c0i = lq + i, c1i = lq + min(i + 16, K - 1);
+      asm volatile("" : "+v"(c0i), "+v"(c1i));
+#pragma unroll
+      for (int k = 0; k < 16; ++k) m[k] = smem[c0i + k * SP];
+#pragma unroll
+      for (int k = 0; k < K1; ++k) { m1[k] = smem[c0i + (16 + k) * SP]; m2[k] = smem[c1i + (16 + k) * SP]; }
+      double a0 = 0.0, a1 = 0.0, c0 = 0.0, c1 = 0.0;
+      bcf<16, 16>(a0, a1, u[0], m);
+      bcf<16, K1>(a0, a1, u[1], m1);
+      bcf<16, K1>(c0, c1, u[1], m2);
+      out[0] = on[0] ? a0 + a1 : 0.0;
+      out[1] = on[1] ? c0 + c1 : 0.0;
+    }
+  };
+  auto gsum = [&](const double (&x)[R]) {
+    double v = x[0];
+    if constexpr (R == 2) v += x[1];
+    return group_sum<GL>(v);
+  };
+  auto vg = [&](const double (&v)[R], double& f, double (&gr)[R], double (&Dw)[R]) {
+    double z[R], lt[R], cf[R];
+    mv(v, z);
+#pragma unroll
+    for (int s = 0; s < R; ++s) {
+      double l, dl, d2;
+      pointwise_loss(loss, z[s] + off[s], y[s], l, dl, d2);
+      if (!on[s]) { l = 0.0; dl = 0.0; d2 = 0.0; }
+      lt[s] = wt[s] * l + 0.5 * l2 * v[s] * v[s];
+      cf[s] = wt[s] * dl;
+      Dw[s] = wt[s] * d2;
+    }
+    f = gsum(lt);
+    mvt(cf, gr);
+#pragma unroll
+    for (int s = 0; s < R; ++s) gr[s] += l2 * v[s];
+  };
+  const double eta0 = 1e-4, eta1 = 0.25, eta2 = 0.75, s1 = 0.25, s2 = 0.5, s3 = 4.0;
+  double f, gr[R], Dw[R];
+  vg(W, f, gr, Dw);
+  double nzw[R];
+#pragma unroll
+  for (int s = 0; s < R; ++s) nzw[s] = W[s] != 0.0 ? 1.0 : 0.0;
+  double f0z, g0n;
+  if (gsum(nzw) == 0.0) {
+    f0z = f;
+    double t[R];
+#pragma unroll
+    for (int s = 0; s < R; ++s) t[s] = gr[s] * gr[s];
+    g0n = sqrt(gsum(t));
+  } else {
+    double zero[R], f0, g0[R], D0[R], t[R];
+#pragma unroll
+    for (int s = 0; s < R; ++s) zero[s] = 0.0;
+    vg(zero, f0, g0, D0);
+    f0z = f0;
+#pragma unroll
+    for (int s = 0; s < R; ++s) t[s] = g0[s] * g0[s];
+    g0n = sqrt(gsum(t));
+  }
+  const double loss_tol = f0z * tol, grad_tol = g0n * tol;
+  double gg[R];
+#pragma unroll
+  for (int s = 0; s < R; ++s) gg[s] = gr[s] * gr[s];
+  double delta = sqrt(gsum(gg));
+  int it = 0, fails = 0, reason = 0;
+  bool active = prob_on;
+  if (delta == 0.0) { reason = 4; active = false; }
+  const int guard_max = max_iter * (max_fail + 1) + 5;
+  for (int guard = 0; guard < guard_max; ++guard) {
+    if (!__any(active)) break;
+    // ---- truncated CG at W (Hessian weights Dw of the current iterate)
+    double step[R], r[R], d[R], t[R];
+#pragma unroll
+    for (int s = 0; s < R; ++s) { step[s] = 0.0; r[s] = -gr[s]; d[s] = r[s]; t[s] = r[s] * r[s]; }
+    double rtr = gsum(t);
+    const double cg_tol = 0.1 * sqrt(rtr);      // ||g|| = ||r0||
+    const double cg_tol2 = cg_tol * cg_tol;     // squared tests: no square root per CG step
+    double sts = 0.0;                           // ||step||^2
+    bool cg_on = active;
+    for (int k = 0; k < max_cg; ++k) {
+      cg_on = cg_on && rtr > cg_tol2;
+      if (!__any(cg_on)) break;
+      double u[R], Hl[R];
+      mv(d, u);
+#pragma unroll
+      for (int s = 0; s < R; ++s) u[s] *= Dw[s];
+      mvt(u, Hl);
+#pragma unroll
+      for (int s = 0; s < R; ++s) { Hl[s] += l2 * d[s]; t[s] = d[s] * Hl[s]; }
+      const double dhd = gsum(t);
+      const double alpha = rtr / (dhd == 0.0 ? 1.0 : dhd);
+      // full step and its residual together (one pair of interleaved sums); a problem that leaves the trust
+      // region recomputes its residual at the boundary step (rare: uniform branch)
+      double tr[R], rn_[R], t2[R];
+#pragma unroll
+      for (int s = 0; s < R; ++s) {
+        tr[s] = step[s] + alpha * d[s];
+        rn_[s] = r[s] - alpha * Hl[s];
+        t[s] = tr[s] * tr[s];
+        t2[s] = rn_[s] * rn_[s];
+      }
+      double tn = t[0], rn = t2[0];
+      if constexpr (R == 2) { tn += t[1]; rn += t2[1]; }
+      group_sum2<GL>(tn, rn);
+      const bool hit = tn > delta * delta;
+      double a = alpha;
+      if (__any(hit && cg_on)) {
+#pragma unroll
+        for (int s = 0; s < R; ++s) { t[s] = step[s] * d[s]; t2[s] = d[s] * d[s]; }
+        double std_ = t[0], dtd = t2[0];
+        if constexpr (R == 2) { std_ += t[1]; dtd += t2[1]; }
+        group_sum2<GL>(std_, dtd);
+        if (hit) {
+          const double dsq = delta * delta;
+          const double qd = std_ * std_ + dtd * (dsq - sts);
+          const double rad = sqrt(qd > 0.0 ? qd : 0.0);
+          const double den1 = std_ + rad;
+          a = std_ >= 0.0 ? (dsq - sts) / (den1 > 1e-300 ? den1 : 1e-300)
+                          : (rad - std_) / (dtd > 1e-300 ? dtd : 1e-300);
+        }
+#pragma unroll
+        for (int s = 0; s < R; ++s) {
+          const double rh = r[s] - a * Hl[s];
+          rn_[s] = hit ? rh : rn_[s];
+          t[s] = rh * rh;
+        }
+        const double rnh = gsum(t);
+        rn = hit ? rnh : rn;
+      }
+      const double beta = rn / (rtr == 0.0 ? 1.0 : rtr);
+      if (cg_on) {
+#pragma unroll
+        for (int s = 0; s < R; ++s) {
+          step[s] = hit ? step[s] + a * d[s] : tr[s];
+          r[s] = rn_[s];
+          if (!hit) d[s] = rn_[s] + beta * d[s];
+        }
+        if (!hit) { rtr = rn; sts = tn; }
+      }
+      cg_on = cg_on && !hit;
+    }
+    // ---- trial point, trust-region update, acceptance
+    double Wn[R], t2[R];
+#pragma unroll
+    for (int s = 0; s < R; ++s) { Wn[s] = W[s] + step[s]; t[s] = gr[s] * step[s]; t2[s] = step[s] * r[s]; }
+    const double gs = gsum(t);
+    const double pred = -0.5 * (gs - gsum(t2));
+    double fn, gn[R], Dn[R];
+    vg(Wn, fn, gn, Dn);
+    const double actual = f - fn;
+#pragma unroll
+    for (int s = 0; s < R; ++s) t[s] = step[s] * step[s];
+    const double snorm = sqrt(gsum(t));
+    if (active && it == 0) delta = fmin(delta, snorm);
+    const double den = fn - f - gs;
+    const double al = den <= 0.0 ? s3 : fmax(s1, -0.5 * gs / (den == 0.0 ? 1.0 : den));
+    double nd;
+    if (actual < eta0 * pred) nd = fmin(fmax(al, s1) * snorm, s2 * delta);
+    else if (actual < eta1 * pred) nd = fmax(s1 * delta, fmin(al * snorm, s2 * delta));
+    else if (actual < eta2 * pred) nd = fmax(s1 * delta, fmin(al * snorm, s3 * delta));
+    else nd = fmax(delta, fmin(al * snorm, s3 * delta));
+    if (active) delta = nd;
+    const bool accept = active && actual > eta0 * pred;
+    const double f_prev = f;
+    if (accept) {
+#pragma unroll
+      for (int s = 0; s < R; ++s) { W[s] = Wn[s]; gr[s] = gn[s]; Dw[s] = Dn[s]; }
+      f = fn; ++it; fails = 0;
+    } else if (active) {
+      ++fails;
+    }
+    const bool not_impr = active && !accept && fails >= max_fail;
+#pragma unroll
+    for (int s = 0; s < R; ++s) t[s] = gr[s] * gr[s];
+    const double gnorm = sqrt(gsum(t));
+    int rc = 0;
+    if (accept && gnorm <= grad_tol) rc = 4;
+    if (accept && fabs(f - f_prev) <= loss_tol) rc = 3;
+    if (not_impr) rc = 2;
+    if ((accept || not_impr) && it >= max_iter) rc = 1;
+    if (active && rc > 0) { reason = rc; active = false; }
+  }
+#pragma unroll
+  for (int s = 0; s < R; ++s)
+    if (on[s]) Beta[o[s]] = W[s];
+  if (prob_on && i == 0) { Fout[b] = f; Iters[b] = it; Reason[b] = reason; }
+}
+
+template <int K, bool LREG>
+static void launch_rs_tron_dpp(int B, int n, const double* L, const double* y, const double* off, const double* wt,
+                               double* beta, double* f, int* iters, int* reason, int loss, double l2, double tol,
+                               int max_iter, int max_fail, int max_cg, hipStream_t st) {
+  using Gm = RsGeom<K, LREG>;
+  const long long waves = (B + Gm::P - 1) / Gm::P;
+  const long long grid = (waves + Gm::WPB - 1) / Gm::WPB;
+  const size_t lds = Gm::REG ? 0 : (size_t)Gm::WPB * Gm::P * Gm::PS * sizeof(double);
+  hipLaunchKernelGGL((rs_tron_dpp_kernel<K, LREG>), dim3((unsigned)grid), dim3(Gm::WPB * 64), lds, st, B, n, L, y, off, wt,
+                     beta, f, iters, reason, loss, l2, tol, max_iter, max_fail, max_cg);
+}
+
+// ============================================================================================================
 // Margin-space line search (GLM L-BFGS): along x(t) = x0 + t d the margins are affine, z(t) = z0 + t zd with
 // z0 = X x0_eff + shift0 + offset (cached by the accepted evaluation) and zd = X d_eff + d_shift (one forward
 // pass per iteration). Each trial step then costs one elementwise pass over the rows instead of a full
@@ -2185,15 +2548,33 @@ int pml_rs_tron(int B, int n, const double* L, const double* y, const double* of
                 int max_cg, void* stream) {
   if (B <= 0) return 0;
   if (n < 1 || n > 64 || loss < 0 || loss > 2) return -22;
+  const int V = g_rs_variant;
+  hipStream_t st = (hipStream_t)stream;
+  if (V >= 3 && n <= 32) {
+#define RS_DPP(KK)                                                                                              \
+  (V == 3 ? launch_rs_tron_dpp<KK, true>(B, n, L, y, off, wt, beta, f, iters, reason, loss, l2, tol, max_iter,    \
+                                         max_fail, max_cg, st)                                                     \
+          : launch_rs_tron_dpp<KK, false>(B, n, L, y, off, wt, beta, f, iters, reason, loss, l2, tol, max_iter,   \
+                                          max_fail, max_cg, st))
+    if (n <= 4) RS_DPP(4);
+    else if (n <= 8) RS_DPP(8);
+    else if (n <= 12) RS_DPP(12);
+    else if (n <= 16) RS_DPP(16);
+    else if (n <= 20) RS_DPP(20);
+    else if (n <= 24) RS_DPP(24);
+    else RS_DPP(32);
+#undef RS_DPP
+    LAUNCH_CHECK();
+    return 0;
+  }
   int G = 1;
   while (G < n) G <<= 1;
   const int per = 64 / G;
   const long long waves = (B + per - 1) / per;
-  const int V = g_rs_variant;
   const size_t wave_lds = (size_t)per * (n * (n + 1) + (V >= 1 ? G : 0)) * sizeof(double);
   const int nw = (int)std::max<size_t>(1, std::min<size_t>(4, 65536 / wave_lds));
   const long long grid = (waves + nw - 1) / nw;
-  if (V == 2)
+  if (V >= 2)
     hipLaunchKernelGGL(rs_tron_kernel<2>, dim3((unsigned)grid), dim3(nw * 64), nw * wave_lds, (hipStream_t)stream, B,
                        n, G, L, y, off, wt, beta, f, iters, reason, loss, l2, tol, max_iter, max_fail, max_cg);
   else if (V == 1)

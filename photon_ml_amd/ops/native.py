@@ -113,7 +113,7 @@ def glm_lib() -> Optional[ctypes.CDLL]:
         lib.pml_lincomb.argtypes = [c_void_p, c_void_p, c_int, ctypes.c_longlong, c_void_p, c_void_p]
         lib.pml_tl_set_deep.argtypes = [c_int, c_int]
         lib.pml_rs_set_variant.argtypes = [c_int]
-        lib.pml_rs_set_variant(int(os.environ.get("PML_RS_VARIANT", "2")))
+        lib.pml_rs_set_variant(int(os.environ.get("PML_RS_VARIANT", "3")))
         lib.pml_ls_eval.argtypes = [c_int, c_int, c_double, c_int, c_void_p, c_void_p, c_void_p, c_void_p, c_int,
                                     c_void_p, c_void_p, c_void_p, c_void_p, c_void_p]
         lib.pml_rs_tron.argtypes = [c_int, c_int] + [c_void_p] * 8 + [c_int, c_double, c_double, c_int, c_int, c_int,
@@ -255,16 +255,24 @@ def batched_hv(A: torch.Tensor, dw: torch.Tensor, v: torch.Tensor, l2: float = 0
 
 
 def rs_tron(L: torch.Tensor, y: torch.Tensor, o: torch.Tensor, w: torch.Tensor, beta0: torch.Tensor, loss_id: int,
-            l2: float, tol: float, max_iter: int, max_fail: int = 5, max_cg: int = 20):
+            l2: float, tol: float, max_iter: int, max_fail: int = 5, max_cg: int = 20,
+            out: Optional[torch.Tensor] = None):
     """Fused per-problem TRON over a batch of small dense GLMs (``rs_tron_kernel``): returns
-    (beta, f, iters, reason). Device only; n <= 64; losses logistic / Poisson / squared."""
+    (beta, f, iters, reason). Device only; n <= 64; losses logistic / Poisson / squared. ``out`` (contiguous
+    fp64 [B, n]) receives the solution in place (it starts from ``beta0``; ``out`` may be ``beta0``)."""
     lib = require_glm_lib()
     B, n, _ = L.shape
     ts = [t.contiguous() for t in (L, y, o, w)]
     for t in ts:
         assert t.dtype == torch.float64 and t.is_cuda
     assert y.shape == (B, n) and o.shape == (B, n) and w.shape == (B, n) and beta0.shape == (B, n)
-    beta = beta0.to(torch.float64).contiguous().clone()
+    if out is None:
+        beta = beta0.to(torch.float64).contiguous().clone()
+    else:
+        assert out.shape == (B, n) and out.dtype == torch.float64 and out.is_contiguous()
+        if out.data_ptr() != beta0.data_ptr():
+            out.copy_(beta0)
+        beta = out
     f = torch.empty(B, dtype=torch.float64, device=L.device)
     iters = torch.empty(B, dtype=torch.int32, device=L.device)
     reason = torch.empty(B, dtype=torch.int32, device=L.device)
@@ -339,6 +347,7 @@ def game_lib() -> Optional[ctypes.CDLL]:
                                       c_void_p]
         lib.pml_downsample.argtypes = [c_int, c_void_p, c_void_p, c_void_p, ctypes.c_longlong, ctypes.c_ulonglong,
                                        c_double, c_int, c_void_p, c_void_p]
+        lib.pml_seg_gram.argtypes = [c_int, c_int, c_int] + [c_void_p] * 8
         for f in ("pml_score_rows", "pml_bgram", "pml_gemm_nt", "pml_spmm_rows", "pml_downsample"):
             getattr(lib, f).restype = c_int
         lib._pml_typed = True
@@ -418,6 +427,28 @@ def spmm_rows(x, PT: torch.Tensor) -> torch.Tensor:
     check(lib.pml_spmm_rows(indptr.data_ptr(), col.data_ptr(), val.data_ptr(), n, PT.data_ptr(), k, Y.data_ptr(),
                             stream_handle(dev)), "spmm_rows")
     return Y
+
+
+def seg_gram(ents: torch.Tensor, n: int, row_ptr: torch.Tensor, col_ptr: torch.Tensor, nip: torch.Tensor,
+             pos: torch.Tensor, val: torch.Tensor) -> torch.Tensor:
+    """Per-entity Gram matrices ``K [B, n, n]`` (``seg_gram_kernel``) of the entities ``ents`` of a block-diagonal
+    CSR (rows grouped by entity: ``row_ptr``; entity column ranges: ``col_ptr``; ``nip/pos/val`` = int64 indptr,
+    int64 global columns, fp64 values, distinct columns per row). Entities with fewer than ``n`` rows are zero
+    padded. Device only."""
+    lib = require_game_lib()
+    dev = ents.device
+    B = int(ents.numel())
+    K = torch.empty(B, n, n, dtype=torch.float64, device=dev)
+    if B == 0:
+        return K
+    t = [x.to(dev).contiguous() for x in (ents, row_ptr, col_ptr, nip, pos)]
+    for x in t:
+        assert x.dtype == torch.int64
+    v = val.to(dev, torch.float64).contiguous()
+    dmax = int((col_ptr[ents + 1] - col_ptr[ents]).max())
+    check(lib.pml_seg_gram(B, n, dmax, t[0].data_ptr(), t[1].data_ptr(), t[2].data_ptr(), t[3].data_ptr(),
+                           t[4].data_ptr(), v.data_ptr(), K.data_ptr(), stream_handle(dev)), "seg_gram")
+    return K
 
 
 def downsample_weights(y: torch.Tensor, w0: torch.Tensor, rate: float, binary: bool, seed: int,

@@ -21,7 +21,8 @@ changes only the iterates, not the optimum).
 
 Cost: K_e for all entities takes 2 x n_max passes of the block-diagonal GLM kernels (column j of every K_e is
 X (X^T e_j): an indicator per-row vector through the transpose then the forward kernel — deterministic, fp64,
-no new kernels), once per dataset; each solve then touches B x n^2 doubles (4 GB at config 5) instead of the
+no new kernels), once per dataset; each solve then touches sum_e n_c(e)^2 doubles (4 GB at config 5, entities
+grouped in size classes so a power-law size mix does not pad every problem to the largest) instead of the
 D_total = 1.25e9-coefficient vectors, and the model returns to the primal space with one transpose pass
 (w = X^T L^{-T} beta).
 """
@@ -56,15 +57,56 @@ def _tri_inverse_lower(L: torch.Tensor) -> torch.Tensor:
     return X
 
 
+def _canonical_csr(csr, dev):
+    """The (indptr, columns, values) block-diagonal CSR on ``dev`` when every row's columns are strictly
+    increasing (what the per-entity Gram kernel needs), else None."""
+    if csr is None:
+        return None
+    nip, pos, val = (t.to(dev) for t in csr)
+    if pos.numel() > 1:
+        inc = pos[1:] > pos[:-1]
+        starts = nip[1:-1]
+        inc[starts[(starts > 0) & (starts < pos.numel())] - 1] = True   # a row's first entry may start lower
+        if not bool(inc.all()):
+            return None
+    return nip.to(torch.int64), pos.to(torch.int64), val.to(torch.float64)
+
+
 def row_space_eligible(l1: float, constraints=None) -> bool:
     return l1 == 0 and not constraints
 
 
+# Size classes of the row-space batch: an entity with n_e rows joins the smallest class bound >= n_e and a class
+# is padded to the largest n_e among its members (not to the bound). One padded batch over power-law entity
+# sizes (most entities have a handful of rows, a few have 64) would cost every problem the largest n^2 in
+# memory and in the fused kernel's lane group; per class the kernel uses G = pow2 >= n lanes per problem.
+SIZE_CLASSES = (1, 2, 4, 8, 12, 16, 24, 32, 48, 64)
+
+
+class _SizeClass:
+    """One padded dense batch of row-space problems: L [B, n, n] (padding rows: weight 0, unit diagonal)."""
+
+    def __init__(self, ents, n, L, rows, valid, w, y, off):
+        self.ents, self.n, self.L, self.rows, self.valid, self.w, self.y = ents, n, L, rows, valid, w, y
+        self.B = int(ents.numel())
+        self.off = off                                                   # offset in the packed beta vector
+        self.Linv = _tri_inverse_lower(L)                                # [B, n, n], lower
+
+    def view(self, flat: torch.Tensor) -> torch.Tensor:
+        return flat[self.off:self.off + self.B * self.n].view(self.B, self.n)
+
+    def slots(self, per_row: torch.Tensor) -> torch.Tensor:
+        return torch.where(self.valid, per_row[self.rows.clamp(min=0)],
+                           torch.zeros((), dtype=per_row.dtype, device=per_row.device))
+
+
 class RowSpaceBatch:
     """Entities of a :class:`SegmentedGLMData` with 0 < n_e <= min(nmax, d_e) and a positive-definite Gram
-    matrix, as one dense padded batch ``L [B, n, n]`` (padding rows: weight 0, unit diagonal)."""
+    matrix, as dense padded batches per size class (:data:`SIZE_CLASSES`). Row-space coefficients of all
+    classes are packed into one flat vector (class after class, ``[B_c, n_c]`` row-major each); ``ents``,
+    ``valid`` and the solver results follow the same order."""
 
-    def __init__(self, seg, nmax: int = 64):
+    def __init__(self, seg, nmax: int = 64, csr=None):
         self.seg = seg
         dev = seg.y.device
         n_e = seg.row_ptr[1:] - seg.row_ptr[:-1]
@@ -72,91 +114,136 @@ class RowSpaceBatch:
         cand = (n_e > 0) & (n_e <= nmax) & (n_e <= d_e)
         ents = torch.nonzero(cand).squeeze(1)
         self.n_entities = seg.B
+        self.classes = []
+        self.beta: Optional[torch.Tensor] = None                        # last solution (packed)
+        self.mask = torch.zeros(seg.B, dtype=torch.bool, device=dev)   # entities handled here
         if ents.numel() == 0:
             self.ents = ents
             self.B = 0
+            self.n = 0
             return
-        n = int(n_e[ents].max())
-        ar = torch.arange(n, device=dev)
-        ne = n_e[ents]
-        valid = ar.unsqueeze(0) < ne.unsqueeze(1)                               # [B, n]
-        rows = torch.where(valid, seg.row_ptr[ents].unsqueeze(1) + ar, torch.full_like(valid, -1, dtype=torch.long))
+        ne_all = n_e[ents]
+        bounds = torch.tensor([b for b in SIZE_CLASSES if b < nmax] + [nmax], device=dev)
+        cls_of = torch.searchsorted(bounds, ne_all)                    # smallest bound >= n_e
+        members = [(ents[cls_of == c], ne_all[cls_of == c]) for c in range(bounds.numel())]
+        members = [(e, ne) for e, ne in members if e.numel()]
+        n_max = int(ne_all.max())
         N = seg.y.numel()
-        K = torch.zeros(ents.numel(), n, n, dtype=torch.float64, device=dev)
-        ind = torch.zeros(N, dtype=torch.float64, device=dev)
-        for j in range(n):
-            vj = valid[:, j]
-            rj = rows[vj, j]
+        geo = []
+        for e, ne in members:
+            n = int(ne.max())
+            ar = torch.arange(n, device=dev)
+            valid = ar.unsqueeze(0) < ne.unsqueeze(1)                  # [B_c, n]
+            rows = torch.where(valid, seg.row_ptr[e].unsqueeze(1) + ar,
+                               torch.full_like(valid, -1, dtype=torch.long))
+            geo.append((e, n, valid, rows, torch.zeros(e.numel(), n, n, dtype=torch.float64, device=dev)))
+        csr = _canonical_csr(csr, dev) if dev.type == "cuda" else None
+        if csr is not None:
+            # K_e straight from the block-diagonal CSR, one wave per entity (seg_gram_kernel)
+            from ..ops.native import seg_gram
+            for gi, (e, n, valid, rows, _K) in enumerate(geo):
+                geo[gi] = (e, n, valid, rows, seg_gram(e, n, seg.row_ptr, seg.col_ptr, *csr))
+            n_max = 0
+        ind = torch.zeros(N, dtype=torch.float64, device=dev) if n_max else None
+        for j in range(n_max):
+            # column j of every K_e at once: indicator on row j of every handled entity with n_e > j
             ind.zero_()
-            ind[rj] = 1.0
-            u = seg.glm.rmatvec(ind)                  # every eligible entity's row j, at its own columns
+            for _, n, valid, rows, _K in geo:
+                if j < n:
+                    ind[rows[valid[:, j], j]] = 1.0
+            u = seg.glm.rmatvec(ind)                  # every entity's row j, at its own columns
             z = seg.glm.matvec(u)                      # (X_e X_e^T)[:, j] on the entity's rows
-            K[:, :, j] = torch.where(valid, z[rows.clamp(min=0)], torch.zeros((), dtype=torch.float64, device=dev))
+            for _, n, valid, rows, K in geo:
+                if j < n:
+                    K[:, :, j] = torch.where(valid, z[rows.clamp(min=0)],
+                                             torch.zeros((), dtype=torch.float64, device=dev))
+            del u, z
         del ind
-        # non-eligible entities also received u components (rows of OTHER entities never mix: block diagonal)
-        pad = (~valid).to(torch.float64)
-        K = K + torch.diag_embed(pad)
-        L, info = torch.linalg.cholesky_ex(K)
-        ok = info == 0
-        self.ents = ents[ok]
+        off = 0
+        kept = []
+        for e, n, valid, rows, K in geo:
+            # entities of other classes / the primal path also received u components (rows never mix)
+            K += torch.diag_embed((~valid).to(torch.float64))
+            L, info = torch.linalg.cholesky_ex(K)
+            del K
+            ok = info == 0
+            if not bool(ok.any()):
+                continue
+            L, rows, valid, e = L[ok].contiguous(), rows[ok], valid[ok], e[ok]
+            zero = torch.zeros((), dtype=torch.float64, device=dev)
+            w = torch.where(valid, seg.w[rows.clamp(min=0)], zero)
+            y = torch.where(valid, seg.y[rows.clamp(min=0)], zero)
+            c = _SizeClass(e, n, L, rows, valid, w, y, off)
+            off += c.B * n
+            self.classes.append(c)
+            kept.append(e)
+        self.ents = torch.cat(kept) if kept else ents[:0]
         self.B = int(self.ents.numel())
-        self.n = n
-        self.L = L[ok].contiguous()
-        self.rows = rows[ok]
-        self.valid = valid[ok]
-        self.w = torch.where(self.valid, seg.w[self.rows.clamp(min=0)], torch.zeros((), dtype=torch.float64,
-                                                                                   device=dev))
-        self.y = torch.where(self.valid, seg.y[self.rows.clamp(min=0)], torch.zeros((), dtype=torch.float64,
-                                                                                   device=dev))
-        self.Linv = _tri_inverse_lower(self.L)                           # [B, n, n], lower
-        self.mask = torch.zeros(seg.B, dtype=torch.bool, device=dev)   # entities handled here
+        self.n = max((c.n for c in self.classes), default=0)
+        self.size = off
         self.mask[self.ents] = True
-        self.beta: Optional[torch.Tensor] = None                        # last solution (row-space coordinates)
+        self.valid = (torch.cat([c.valid.reshape(-1) for c in self.classes]) if self.classes
+                      else torch.zeros(0, dtype=torch.bool, device=dev))
+        self.rows = (torch.cat([c.rows.reshape(-1) for c in self.classes]) if self.classes
+                     else torch.zeros(0, dtype=torch.long, device=dev))
 
     def _slots(self, per_row: torch.Tensor) -> torch.Tensor:
+        """Packed per-slot values of a per-row vector (0 in padding slots)."""
         return torch.where(self.valid, per_row[self.rows.clamp(min=0)],
                            torch.zeros((), dtype=per_row.dtype, device=per_row.device))
 
     def beta_from_primal(self, W: torch.Tensor) -> torch.Tensor:
-        """Orthogonal projection of primal coefficients onto the row space: beta = L^{-1} X w."""
+        """Orthogonal projection of primal coefficients onto the row space: beta = L^{-1} X w (packed)."""
         z = self._slots(self.seg.glm.matvec(W))
-        return _bmv(self.Linv, z)
+        return torch.cat([_bmv(c.Linv, c.view(z)).reshape(-1) for c in self.classes])
 
     def to_primal(self, beta: torch.Tensor) -> torch.Tensor:
         """w = X^T L^{-T} beta for the handled entities (zeros elsewhere): one transpose pass."""
-        alpha = _bmv(self.Linv, beta, trans=True)                        # L^{-T} beta
         r = torch.zeros(self.seg.y.numel(), dtype=torch.float64, device=beta.device)
-        r[self.rows[self.valid]] = alpha[self.valid]
+        for c in self.classes:
+            alpha = _bmv(c.Linv, c.view(beta), trans=True)               # L^{-T} beta
+            r[c.rows[c.valid]] = alpha[c.valid]
         return self.seg.glm.rmatvec(r)
 
     def margins(self, beta: torch.Tensor) -> torch.Tensor:
         """Per-row X w (no offsets) of the handled entities = L beta, in the segmented row order."""
         z = torch.zeros(self.seg.y.numel(), dtype=torch.float64, device=beta.device)
-        z[self.rows[self.valid]] = _bmv(self.L, beta)[self.valid]
+        for c in self.classes:
+            z[c.rows[c.valid]] = _bmv(c.L, c.view(beta))[c.valid]
         return z
 
     def solve(self, loss, l2: float, optimizer: str, W0: Optional[torch.Tensor], tol: float, max_iter: int,
               reuse_beta: bool = True) -> BatchedResult:
-        """Solve the handled entities; returns the batched result over the ``B`` row-space problems."""
+        """Solve the handled entities; returns the batched result over the ``B`` row-space problems (``W`` is
+        the packed coefficient vector; ``iters`` / ``reason`` / ``f`` follow ``ents``)."""
+        dev = self.seg.y.device
         if reuse_beta and self.beta is not None:
             beta0 = self.beta
         elif W0 is not None and bool((W0 != 0).any()):
             beta0 = self.beta_from_primal(W0)
         else:
-            beta0 = torch.zeros(self.B, self.n, dtype=torch.float64, device=self.L.device)
+            beta0 = torch.zeros(self.size, dtype=torch.float64, device=dev)
         o = self._slots(self.seg.o)
-        if (optimizer == "TRON" and self.L.is_cuda and self.n <= 64 and getattr(loss, "loss_id", -1) in (0, 1, 2)
-                and os.environ.get("PML_RS_FUSED_TRON", "1") != "0"):
-            # whole per-entity TRON in one kernel, L resident in LDS (ops/csrc/glm_kernels.hip rs_tron_kernel)
-            from ..ops.native import rs_tron
-            beta, f, iters, reason = rs_tron(self.L, self.y, o, self.w, beta0, loss.loss_id, l2, tol, max_iter)
-            res = BatchedResult(beta, f, iters, reason)
-            self.beta = res.W
-            return res
-        data = BatchedGLMData(self.L, self.y, o, self.w)
-        if optimizer == "TRON":
-            res = batched_tron(data, loss, l2, beta0, tol, max_iter)
-        else:
-            res = batched_lbfgs(data, loss, l2, beta0, tol, max_iter)
+        fused = (optimizer == "TRON" and self.seg.y.is_cuda and getattr(loss, "loss_id", -1) in (0, 1, 2)
+                 and os.environ.get("PML_RS_FUSED_TRON", "1") != "0")
+        beta = torch.empty_like(beta0)
+        fs, its, rcs = [], [], []
+        for c in self.classes:
+            b0, oc = c.view(beta0), c.view(o)
+            if fused:
+                # whole per-entity TRON in one kernel, L resident in LDS (ops/csrc/glm_kernels.hip rs_tron_kernel)
+                from ..ops.native import rs_tron
+                _, f, it, rc = rs_tron(c.L, c.y, oc, c.w, b0, loss.loss_id, l2, tol, max_iter, out=c.view(beta))
+            else:
+                data = BatchedGLMData(c.L, c.y, oc, c.w)
+                solver = batched_tron if optimizer == "TRON" else batched_lbfgs
+                r = solver(data, loss, l2, b0, tol, max_iter)
+                c.view(beta).copy_(r.W)
+                f, it, rc = r.f, r.iters, r.reason
+            fs.append(f)
+            its.append(it)
+            rcs.append(rc)
+        res = BatchedResult(beta, torch.cat(fs) if fs and fs[0] is not None else None, torch.cat(its),
+                            torch.cat(rcs))
         self.beta = res.W
         return res

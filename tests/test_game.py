@@ -185,6 +185,9 @@ def test_row_space_random_effect_solve_matches_primal(task, opt, monkeypatch):
         out[mode] = (c, m1, m2, it1)
         if mode == "1":
             assert c._rs is not None and 0 < c._rs.B < int((c.dataset.n_active > 0).sum())
+            # Zipf sizes: several size classes, each padded to its own largest entity
+            ns = [k.n for k in c._rs.classes]
+            assert len(ns) > 1 and ns == sorted(ns) and c._rs.size == sum(k.B * k.n for k in c._rs.classes)
     (c0, a1, a2, s0), (c1, b1, b2, s1) = out["0"], out["1"]
     # same iterates in exact arithmetic; at tol 1e-10 rounding can move a convergence test by one iteration
     assert s0["mean_iterations"] == pytest.approx(s1["mean_iterations"], rel=0.02)
@@ -320,3 +323,14 @@ def test_primal_entity_subset_matches_frozen_full_problem(opt, monkeypatch):
         np.testing.assert_allclose(b.coefficients_of(e).means.numpy(), a.coefficients_of(e).means.numpy(),
                                    rtol=1e-8, atol=1e-10)
     torch.testing.assert_close(c1.score(b), c0.score(a), rtol=1e-8, atol=1e-10)
+
+
+def test_canonical_csr_check():
+    """The per-entity Gram kernel needs strictly increasing columns inside each row (row starts may drop)."""
+    from photon_ml_amd.optimization.row_space import _canonical_csr
+    nip = torch.tensor([0, 2, 2, 5, 6])
+    good = torch.tensor([3, 7, 1, 4, 9, 0])
+    assert _canonical_csr((nip, good, torch.ones(6)), torch.device("cpu")) is not None
+    dup = torch.tensor([3, 7, 1, 4, 4, 0])
+    assert _canonical_csr((nip, dup, torch.ones(6)), torch.device("cpu")) is None
+    assert _canonical_csr(None, torch.device("cpu")) is None

@@ -175,3 +175,28 @@ def test_random_effect_build_on_gpu_matches_host(cap, passive, ratio, monkeypatc
     xa.sort_indices()
     xb.sort_indices()
     assert np.array_equal(xa.indptr, xb.indptr) and np.array_equal(xa.indices, xb.indices)
+
+
+def test_row_space_gram_kernel_matches_indicator_passes():
+    """seg_gram_kernel (K_e from the block-diagonal CSR, one wave per entity) == the Gram columns formed by
+    indicator passes through the transpose and forward GLM kernels, per size class; the solve on either set of
+    factors gives the same model."""
+    from photon_ml_amd.algorithm.coordinates import RandomEffectCoordinate
+    from photon_ml_amd.optimization.row_space import RowSpaceBatch
+    data, _ = generate_game_data(n_rows=6000, n_users=400, d_user=40, seed=24, task="LOGISTIC_REGRESSION")
+    cfg = GLMOptimizationConfiguration(OptimizerConfig("TRON", 60, 1e-10), RegularizationContext("L2"), 1.0)
+    c = RandomEffectCoordinate("u", data, RandomEffectDataConfiguration("userId", "user"), cfg,
+                               "LOGISTIC_REGRESSION", device="cuda", layout="segmented")
+    ds = c.dataset
+    a = RowSpaceBatch(ds.seg, csr=ds._seg_csr)
+    b = RowSpaceBatch(ds.seg)
+    assert a.B == b.B > 0 and len(a.classes) > 1 and [k.n for k in a.classes] == [k.n for k in b.classes]
+    assert torch.equal(a.ents, b.ents)
+    for ka, kb in zip(a.classes, b.classes):
+        torch.testing.assert_close(ka.L, kb.L, rtol=1e-10, atol=1e-12)
+    o = torch.zeros_like(ds.seg.y)
+    ds.seg.o = o
+    from photon_ml_amd.function.losses import LOGISTIC
+    ra = a.solve(LOGISTIC, 1.0, "TRON", None, 1e-10, 60)
+    rb = b.solve(LOGISTIC, 1.0, "TRON", None, 1e-10, 60)
+    torch.testing.assert_close(a.to_primal(ra.W), b.to_primal(rb.W), rtol=1e-6, atol=1e-8)

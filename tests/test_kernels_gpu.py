@@ -298,13 +298,18 @@ def test_batched_small_gemv_and_hv_match_torch(n):
 
 @pytest.mark.gpu
 @pytest.mark.parametrize("loss_name,n", [("LOGISTIC", 20), ("POISSON", 7), ("SQUARED", 33), ("LOGISTIC", 64),
-                                         ("LOGISTIC", 1)])
+                                         ("LOGISTIC", 1), ("LOGISTIC", 4), ("POISSON", 8), ("SQUARED", 11),
+                                         ("LOGISTIC", 16), ("POISSON", 18), ("LOGISTIC", 24), ("SQUARED", 29),
+                                         ("LOGISTIC", 32)])
 @pytest.mark.parametrize("warm", [False, True])
-@pytest.mark.parametrize("variant", [0, 1, 2])
+@pytest.mark.parametrize("variant", [0, 1, 2, 3, 4])
 def test_fused_row_space_tron_matches_batched_tron(loss_name, n, warm, variant):
     """rs_tron_kernel (whole per-problem TRON in one kernel) vs the vectorised batched TRON of
     optimization/batched.py on the same dense problems (fp64): same solutions, objective and iteration counts.
-    Every matrix-vector / group-sum variant of the kernel (bpermute shuffles, LDS vector slot, DPP sums)."""
+    Every matrix-vector / group-sum variant of the kernel (bpermute shuffles, LDS vector slot, DPP sums) and
+    the DPP64-broadcast kernel of variant 3 at every padded size K (4 .. 32; n < K pads with zeros)."""
+    if variant < 3 and n not in (20, 7, 33, 64, 1):
+        pytest.skip("sizes of the variant-3 kernel classes")
     import os
     from photon_ml_amd.function import losses
     from photon_ml_amd.ops.native import require_glm_lib, rs_tron
@@ -313,7 +318,7 @@ def test_fused_row_space_tron_matches_batched_tron(loss_name, n, warm, variant):
     try:
         _check_rs_tron(loss_name, n, warm, losses, rs_tron)
     finally:
-        lib.pml_rs_set_variant(int(os.environ.get("PML_RS_VARIANT", "2")))
+        lib.pml_rs_set_variant(int(os.environ.get("PML_RS_VARIANT", "3")))
 
 
 def _check_rs_tron(loss_name, n, warm, losses, rs_tron):
