@@ -90,7 +90,9 @@ def build_parser() -> argparse.ArgumentParser:
     p.add_argument("--normalization-type", default="NONE")
     p.add_argument("--coefficient-box-constraints")
     p.add_argument("--data-validation-type", default="VALIDATE_FULL")
-    p.add_argument("--tree-aggregate-depth", type=int, default=1)
+    p.add_argument("--tree-aggregate-depth", type=int, default=1,
+                   help="accepted for compatibility, no effect: the Spark treeAggregate depth has no analogue; "
+                        "gradients are all-reduced by RCCL, which picks ring / tree itself")
     p.add_argument("--diagnostic-mode", default="NONE")
     p.add_argument("--training-diagnostics", type=parse_bool, default=None,
                    help="deprecated alias: true -> --diagnostic-mode ALL")

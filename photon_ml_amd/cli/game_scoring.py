@@ -37,7 +37,9 @@ def build_parser() -> argparse.ArgumentParser:
     p.add_argument("--model-input-directory", required=True)
     p.add_argument("--model-id", default="N/A")
     p.add_argument("--log-data-and-model-stats", type=parse_bool, default=False)
-    p.add_argument("--spill-scores-to-disk", type=parse_bool, default=False)
+    p.add_argument("--spill-scores-to-disk", type=parse_bool, default=False,
+                   help="accepted for compatibility, no effect: scores are device/host arrays aligned by row, "
+                        "there is no Spark RDD to persist (written once to the output directory)")
     return p
 
 

@@ -102,7 +102,9 @@ def build_parser() -> argparse.ArgumentParser:
     p.add_argument("--coordinate-descent-iterations", type=int, required=True)
     p.add_argument("--normalization", default="NONE")
     p.add_argument("--data-summary-directory")
-    p.add_argument("--tree-aggregate-depth", type=int, default=1)
+    p.add_argument("--tree-aggregate-depth", type=int, default=1,
+                   help="accepted for compatibility, no effect: the Spark treeAggregate depth has no analogue; "
+                        "gradients are all-reduced by RCCL, which picks ring / tree itself")
     p.add_argument("--hyper-parameter-tuning", default="NONE")
     p.add_argument("--hyper-parameter-tuning-iterations", type=int, default=0)
     p.add_argument("--hyper-parameter-tuning-range", default="1e-4-1e4")

@@ -12,6 +12,7 @@
 #include <pybind11/stl.h>
 #include <zlib.h>
 
+#include <algorithm>
 #include <cmath>
 #include <cstdint>
 #include <cstring>
@@ -461,20 +462,75 @@ static std::string snappy_decompress(const uint8_t* p, size_t n) {
   return out;
 }
 
-// valid snappy stream made of literal chunks (no back-references): simple and exact
-static std::string snappy_compress_literal(const std::string& in) {
-  std::string out;
-  uint64_t n = in.size();
-  while (true) { uint8_t b = n & 0x7F; n >>= 7; if (n) { out.push_back((char)(b | 0x80)); } else { out.push_back((char)b); break; } }
-  size_t i = 0;
-  while (i < in.size()) {
-    size_t l = std::min<size_t>(in.size() - i, 65536);
-    uint32_t lm1 = (uint32_t)(l - 1);
+// Snappy compressor (the format's greedy LZ77 scheme): the input is cut into 64 KiB fragments; in each, a
+// 4-byte hash table of earlier positions proposes match candidates, a verified match of >= 4 bytes is emitted as
+// copy elements (1-byte offset form for 4..11 bytes within 2 KiB, else 2-byte offsets, at most 64 bytes each),
+// everything else as literal runs. Unmatched stretches are skipped over progressively faster (one extra byte
+// per 32 misses), as in the reference implementation, so incompressible data costs little.
+static void snappy_emit_literal(std::string& out, const char* p, size_t l) {
+  while (l > 0) {
+    const size_t c = std::min<size_t>(l, 65536);
+    const uint32_t lm1 = (uint32_t)(c - 1);
     if (lm1 < 60) out.push_back((char)(lm1 << 2));
     else if (lm1 < 256) { out.push_back((char)(60 << 2)); out.push_back((char)lm1); }
     else { out.push_back((char)(61 << 2)); out.push_back((char)(lm1 & 0xFF)); out.push_back((char)(lm1 >> 8)); }
-    out.append(in, i, l);
-    i += l;
+    out.append(p, c);
+    p += c;
+    l -= c;
+  }
+}
+
+static void snappy_emit_copy(std::string& out, size_t off, size_t len) {
+  while (len > 0) {
+    // leave at least 4 bytes for the last element (copies are 4+ bytes in the 1-byte-offset form)
+    size_t c = std::min<size_t>(len, 64);
+    if (len > 64 && len - 64 < 4) c = len - 4;
+    if (c >= 4 && c <= 11 && off < 2048) {
+      out.push_back((char)(((c - 4) << 2) | 1 | ((off >> 8) << 5)));
+      out.push_back((char)(off & 0xFF));
+    } else {
+      out.push_back((char)(((c - 1) << 2) | 2));
+      out.push_back((char)(off & 0xFF));
+      out.push_back((char)((off >> 8) & 0xFF));
+    }
+    len -= c;
+  }
+}
+
+static inline uint32_t snappy_load32(const char* p) { uint32_t v; memcpy(&v, p, 4); return v; }
+
+static std::string snappy_compress(const std::string& in) {
+  std::string out;
+  out.reserve(in.size() / 2 + 16);
+  uint64_t n = in.size();
+  while (true) { uint8_t b = n & 0x7F; n >>= 7; if (n) { out.push_back((char)(b | 0x80)); } else { out.push_back((char)b); break; } }
+  const char* base = in.data();
+  const int HBITS = 14;
+  std::vector<int32_t> table(1u << HBITS);
+  for (size_t frag = 0; frag < in.size(); frag += 65536) {
+    const size_t flen = std::min<size_t>(in.size() - frag, 65536);
+    const char* fp = base + frag;
+    std::fill(table.begin(), table.end(), -1);
+    size_t lit = 0, i = 0;
+    uint32_t skip = 32;
+    while (i + 4 <= flen) {
+      const uint32_t cur = snappy_load32(fp + i);
+      const uint32_t h = (cur * 0x1E35A7BDu) >> (32 - HBITS);
+      const int32_t cand = table[h];
+      table[h] = (int32_t)i;
+      if (cand >= 0 && snappy_load32(fp + cand) == cur) {
+        size_t len = 4;
+        while (i + len < flen && fp[cand + len] == fp[i + len]) ++len;
+        snappy_emit_literal(out, fp + lit, i - lit);
+        snappy_emit_copy(out, i - (size_t)cand, len);
+        i += len;
+        lit = i;
+        skip = 32;
+        continue;
+      }
+      i += skip++ >> 5;
+    }
+    snappy_emit_literal(out, fp + lit, flen - lit);
   }
   return out;
 }
@@ -603,7 +659,7 @@ static void write_ocf(const std::string& path, const std::string& schema_json, p
     if (codec == "null") payload = body.buf;
     else if (codec == "deflate") payload = deflate_raw(body.buf, 6);
     else if (codec == "snappy") {
-      payload = snappy_compress_literal(body.buf);
+      payload = snappy_compress(body.buf);
       uint32_t c = crc32_iso(body.buf);
       payload.push_back((char)(c >> 24)); payload.push_back((char)(c >> 16));
       payload.push_back((char)(c >> 8)); payload.push_back((char)c);
@@ -836,8 +892,9 @@ PYBIND11_MODULE(libpml_avro, m) {
   m.def("read_columnar", &read_columnar, py::arg("paths"), py::arg("label_fields"), py::arg("weight_field"),
         py::arg("offset_field"), py::arg("uid_field"), py::arg("metadata_field"), py::arg("bags"),
         py::arg("id_tags"), py::arg("delimiter") = std::string("\x01"));
+  m.def("snappy_compress", [](const std::string& s) { return py::bytes(snappy_compress(s)); });
   m.def("snappy_roundtrip", [](const std::string& s) {
-    std::string c = snappy_compress_literal(s);
+    std::string c = snappy_compress(s);
     return snappy_decompress((const uint8_t*)c.data(), c.size()) == s;
   });
   init_crc32c();

@@ -605,7 +605,11 @@ __global__ __launch_bounds__(NTHREADS) void reduce_stats_l1_kernel(const double*
 //              (local_row << cbits) | (col & (2^cbits-1)). Gathers x[row] walk the per-row vector in order.
 // Determinism: each wave owns a private LDS accumulator row and walks its entries in a fixed order, and the 4
 // wave rows are summed in a fixed order; items of a column tile that is split across work-groups write fp64
-// partial rows that a combine kernel adds IN ORDER. Results are bitwise reproducible run to run.
+// partial rows that a combine kernel adds IN ORDER. One assumption is MEASURED, not guaranteed by the ISA: when
+// several lanes of ONE ds_add_f64 instruction hit the same LDS address, the LDS applies them in a fixed (lane)
+// order. Every cross-instruction order is fixed by the program. Run-to-run bitwise equality is tested on each GPU
+// run (tests/test_kernels_gpu.py: *bitwise* / determinism tests, torch.equal over repeated passes), and the
+// fp64 results agree with the reference to ~1e-12 relative whatever the intra-instruction order.
 // ============================================================================================================
 #define TL_VEC 4                              // entries per lane per round (16-B pack loads)
 #define TL_ROUND (64 * TL_VEC)                // entries per wave-round
