@@ -144,6 +144,17 @@ def main():
             ms = torch.cuda.memory_stats()
             log(f"allocator: peak reserved {ms.get('reserved_bytes.all.peak', 0) / 2**30:.1f} GiB, "
                 f"alloc retries {ms.get('num_alloc_retries', 0)}, device mallocs {ms.get('segment.all.allocated', 0)}")
+        from photon_ml_amd.optimization.batched import tron_stats
+        st = tron_stats()
+        if st:
+            log(f"block-diagonal TRON: {len(st)} CG steps (all sweeps), mean fraction of rows still iterating "
+                f"{sum(st) / len(st):.3f}, min {min(st):.3f}")
+        from photon_ml_amd.ops.device import MASK_STATS
+        if MASK_STATS:
+            fb = sum(a for a, _ in MASK_STATS) / len(MASK_STATS)
+            ft = sum(b for _, b in MASK_STATS) / len(MASK_STATS)
+            log(f"entity-masked passes: {len(MASK_STATS)} table rebuilds, mean kept fraction: forward blocks "
+                f"{fb:.3f}, transpose items {ft:.3f}")
         for rec in cd.history[-2 * args.steps:]:
             log(f"  iteration {rec.get('iteration')} coordinate {rec['coordinate']}: {rec['seconds']:.3f}s")
         print(json.dumps({

@@ -17,12 +17,14 @@
 #include <cstdint>
 #include <cstring>
 #include <fstream>
+#include <atomic>
 #include <map>
 #include <memory>
 #include <random>
 #include <sstream>
 #include <stdexcept>
 #include <string>
+#include <thread>
 #include <unordered_map>
 #include <vector>
 
@@ -578,9 +580,12 @@ struct OCF {
   std::vector<std::pair<int64_t, std::string>> blocks;  // (count, decompressed bytes)
 
   explicit OCF(const std::string& path) {
-    std::ifstream f(path, std::ios::binary);
+    std::ifstream f(path, std::ios::binary | std::ios::ate);
     if (!f) throw std::runtime_error("cannot open " + path);
-    std::stringstream ss; ss << f.rdbuf(); data = ss.str();
+    const std::streamsize fsz = f.tellg();
+    f.seekg(0);
+    data.resize((size_t)std::max<std::streamsize>(fsz, 0));
+    if (fsz > 0 && !f.read(&data[0], fsz)) throw std::runtime_error("cannot read " + path);
     if (data.size() < 4 || data.compare(0, 4, std::string("Obj\x01", 4)) != 0)
       throw std::runtime_error("not an Avro object container file: " + path);
     Reader r((const uint8_t*)data.data() + 4, data.size() - 4);
@@ -693,7 +698,13 @@ static double read_number(Reader& r, const Node* n, bool& ok) {
 
 static bool read_string_like(Reader& r, const Node* n, std::string& out) {
   switch (n->t) {
-    case AT::STRING: case AT::BYTES: out = r.str(); return true;
+    case AT::STRING: case AT::BYTES: {
+      const int64_t len = r.varlong();
+      if (len < 0 || r.end - r.p < len) r.fail();
+      out.assign((const char*)r.p, (size_t)len);
+      r.p += len;
+      return true;
+    }
     case AT::INT: case AT::LONG: out = std::to_string(r.varlong()); return true;
     case AT::DOUBLE: { std::ostringstream o; o << r.dbl(); out = o.str(); return true; }
     case AT::FLOAT: { std::ostringstream o; o << r.flt(); out = o.str(); return true; }
@@ -724,14 +735,47 @@ static bool is_bag(const Node* n) {
   return has_name && has_value;
 }
 
+// Feature-key interner: ids in first-appearance order; an open-addressing table of (hash, id) pairs (one probe
+// is usually one cache line, unlike a node-based map whose lookups chase two or three pointers).
 struct Interner {
-  std::unordered_map<std::string, int32_t> ids;
   std::vector<std::string> keys;
+  std::vector<uint32_t> slot_id;    // id + 1, 0 = empty
+  std::vector<uint32_t> slot_h;
+  size_t mask = 0;
+  static uint64_t hash(const std::string& k) {
+    uint64_t h = 1469598103934665603ull;               // FNV-1a, then a final mix
+    for (unsigned char c : k) { h ^= c; h *= 1099511628211ull; }
+    h ^= h >> 29; h *= 0xBF58476D1CE4E5B9ull; h ^= h >> 32;
+    return h;
+  }
+  void grow() {
+    const size_t cap = std::max<size_t>(1024, slot_id.size() * 2);
+    std::vector<uint32_t> id(cap, 0), hh(cap, 0);
+    const size_t m = cap - 1;
+    for (size_t i = 0; i < slot_id.size(); ++i) {
+      if (!slot_id[i]) continue;
+      size_t j = slot_h[i] & m;
+      while (id[j]) j = (j + 1) & m;
+      id[j] = slot_id[i];
+      hh[j] = slot_h[i];
+    }
+    slot_id.swap(id);
+    slot_h.swap(hh);
+    mask = m;
+  }
   int32_t get(const std::string& k) {
-    auto it = ids.find(k);
-    if (it != ids.end()) return it->second;
-    int32_t id = (int32_t)keys.size();
-    ids.emplace(k, id); keys.push_back(k);
+    if ((keys.size() + 1) * 2 > slot_id.size()) grow();
+    const uint64_t h64 = hash(k);
+    const uint32_t h = (uint32_t)h64;
+    size_t j = h64 & mask;
+    while (slot_id[j]) {
+      if (slot_h[j] == h && keys[slot_id[j] - 1] == k) return (int32_t)(slot_id[j] - 1);
+      j = (j + 1) & mask;
+    }
+    const int32_t id = (int32_t)keys.size();
+    keys.push_back(k);
+    slot_id[j] = (uint32_t)id + 1;
+    slot_h[j] = h;
     return id;
   }
 };
@@ -742,123 +786,230 @@ struct BagOut {
   std::vector<double> vals;
 };
 
-// Decode TrainingExample-like files into columns.
+// Decode TrainingExample-like files into columns. Files are decoded in parallel (one worker per file, up to the
+// hardware threads; PML_AVRO_THREADS overrides), each into its own columns and its own feature-key interner;
+// the merge walks the files in order, so feature ids (first-appearance order), rows and every column are exactly
+// what a sequential decode produces. Per-record work avoids allocations: field roles and the bag item layout
+// are resolved once per file schema, feature keys are assembled in one reused buffer.
+struct FileCols {
+  std::vector<double> label, weight, offset;
+  std::vector<std::string> uid;
+  std::vector<uint8_t> has_uid;
+  std::vector<std::vector<std::string>> tags;     // per requested id tag
+  std::map<std::string, BagOut> bags;
+  Interner intern;
+  std::string label_used;
+  int64_t n = 0;
+};
+
+struct ColumnarOpts {
+  std::vector<std::string> label_fields;
+  std::string weight_field, offset_field, uid_field, metadata_field, delimiter;
+  std::vector<std::string> bags_wanted, id_tags;
+};
+
+static void decode_columnar_file(const std::string& path, const ColumnarOpts& op, FileCols& fc) {
+  OCF o(path);
+  const Node* root = o.schema->root;
+  if (root->t != AT::RECORD) throw std::runtime_error("top-level Avro schema must be a record: " + path);
+  const size_t nf = root->fields.size();
+  std::map<std::string, int> tag_index;
+  for (size_t t = 0; t < op.id_tags.size(); ++t) tag_index.emplace(op.id_tags[t], (int)t);
+  fc.tags.assign(op.id_tags.size(), {});
+  // field roles: 0 skip, 1 label, 2 weight, 3 offset, 4 uid, 5 meta, 6 bag, 7 tag
+  std::vector<int> role(nf, 0), tag_of(nf, -1);
+  std::vector<BagOut*> bag_of(nf, nullptr);
+  int label_idx = -1;
+  for (auto& lf : op.label_fields) {
+    for (size_t i = 0; i < nf; ++i)
+      if (root->fields[i].first == lf) { label_idx = (int)i; break; }
+    if (label_idx >= 0) { fc.label_used = lf; break; }
+  }
+  for (size_t i = 0; i < nf; ++i) {
+    const std::string& fn = root->fields[i].first;
+    const Node* fnode = root->fields[i].second;
+    if ((int)i == label_idx) role[i] = 1;
+    else if (fn == op.weight_field) role[i] = 2;
+    else if (fn == op.offset_field) role[i] = 3;
+    else if (fn == op.uid_field) role[i] = 4;
+    else if (fn == op.metadata_field) role[i] = 5;
+    else if (tag_index.count(fn)) { role[i] = 7; tag_of[i] = tag_index[fn]; }
+    else if (is_bag(fnode)) {
+      bool want = op.bags_wanted.empty();
+      for (auto& b : op.bags_wanted) if (b == fn) want = true;
+      if (want) { role[i] = 6; bag_of[i] = &fc.bags[fn]; }
+    }
+  }
+  // bag item layout per (item record node): 0 skip, 1 name, 2 term, 3 value
+  std::map<const Node*, std::vector<int>> item_roles;
+  auto roles_of = [&](const Node* it) -> const std::vector<int>& {
+    auto f = item_roles.find(it);
+    if (f != item_roles.end()) return f->second;
+    std::vector<int> v(it->fields.size(), 0);
+    for (size_t j = 0; j < it->fields.size(); ++j) {
+      const std::string& nm = it->fields[j].first;
+      v[j] = nm == "name" ? 1 : nm == "term" ? 2 : nm == "value" ? 3 : 0;
+    }
+    return item_roles.emplace(it, std::move(v)).first->second;
+  };
+  std::vector<std::string> rec_tags(op.id_tags.size());
+  std::vector<uint8_t> rec_has(op.id_tags.size());
+  std::string key, name, term, u, sval;
+  const Node* last_item = nullptr;
+  const std::vector<int>* last_roles = nullptr;
+  for (auto& blk : o.blocks) {
+    Reader r((const uint8_t*)blk.second.data(), blk.second.size());
+    for (int64_t rec = 0; rec < blk.first; ++rec) {
+      double lab = NAN, wt = NAN, off = NAN;
+      bool hu = false;
+      u.clear();
+      std::fill(rec_has.begin(), rec_has.end(), 0);
+      for (size_t i = 0; i < nf; ++i) {
+        const Node* fnode = root->fields[i].second;
+        bool ok;
+        switch (role[i]) {
+          case 1: lab = read_number(r, fnode, ok); break;
+          case 2: wt = read_number(r, fnode, ok); break;
+          case 3: off = read_number(r, fnode, ok); break;
+          case 4: hu = read_string_like(r, fnode, u); break;
+          case 7: {
+            const int t = tag_of[i];
+            if (read_string_like(r, fnode, sval)) { rec_tags[t] = sval; rec_has[t] = 1; }
+            break;
+          }
+          case 5: {
+            const Node* m = fnode;
+            if (m->t == AT::UNION) { int64_t k = r.varlong(); m = m->branches.at((size_t)k); }
+            if (m->t != AT::MAP) { skip_value(r, m); break; }
+            while (true) {
+              int64_t c = r.varlong();
+              if (c == 0) break;
+              if (c < 0) { c = -c; r.varlong(); }
+              for (int64_t k = 0; k < c; ++k) {
+                std::string mk = r.str();
+                bool has = read_string_like(r, m->items, sval);
+                auto ti = tag_index.find(mk);
+                if (has && ti != tag_index.end() && !rec_has[ti->second]) {
+                  rec_tags[ti->second] = sval;
+                  rec_has[ti->second] = 1;
+                }
+              }
+            }
+            break;
+          }
+          case 6: {
+            BagOut& bo = *bag_of[i];
+            const Node* arr = fnode;
+            if (arr->t == AT::UNION) { int64_t k = r.varlong(); arr = arr->branches.at((size_t)k); }
+            if (arr->t != AT::ARRAY) { skip_value(r, arr); break; }
+            const Node* item = arr->items;
+            while (true) {
+              int64_t c = r.varlong();
+              if (c == 0) break;
+              if (c < 0) { c = -c; r.varlong(); }
+              for (int64_t k = 0; k < c; ++k) {
+                const Node* it = item;
+                if (it->t == AT::UNION) { int64_t b = r.varlong(); it = it->branches.at((size_t)b); }
+                if (it != last_item) { last_roles = &roles_of(it); last_item = it; }
+                const std::vector<int>& fr = *last_roles;
+                name.clear();
+                term.clear();
+                double val = NAN;
+                for (size_t j = 0; j < it->fields.size(); ++j) {
+                  const Node* fnd = it->fields[j].second;
+                  switch (fr[j]) {
+                    case 1: read_string_like(r, fnd, name); break;
+                    case 2: if (!read_string_like(r, fnd, term)) term.clear(); break;
+                    case 3: { bool okv; val = read_number(r, fnd, okv); break; }
+                    default: skip_value(r, fnd);
+                  }
+                }
+                key.assign(name);
+                key.append(op.delimiter);
+                key.append(term);
+                bo.keys.push_back(fc.intern.get(key));
+                bo.vals.push_back(val);
+              }
+            }
+            break;
+          }
+          default: skip_value(r, fnode);
+        }
+      }
+      fc.label.push_back(lab); fc.weight.push_back(wt); fc.offset.push_back(off);
+      fc.uid.push_back(hu ? u : std::string()); fc.has_uid.push_back(hu ? 1 : 0);
+      for (size_t t = 0; t < rec_tags.size(); ++t) fc.tags[t].push_back(rec_has[t] ? rec_tags[t] : std::string());
+      for (auto& b : fc.bags) b.second.rowptr.push_back((int64_t)b.second.keys.size());
+      ++fc.n;
+    }
+  }
+}
+
 static py::dict read_columnar(const std::vector<std::string>& paths, const std::vector<std::string>& label_fields,
                               const std::string& weight_field, const std::string& offset_field,
                               const std::string& uid_field, const std::string& metadata_field,
                               const std::vector<std::string>& bags_wanted, const std::vector<std::string>& id_tags,
                               const std::string& delimiter) {
+  ColumnarOpts op{label_fields, weight_field, offset_field, uid_field, metadata_field, delimiter, bags_wanted,
+                  id_tags};
+  const size_t nfile = paths.size();
+  std::vector<FileCols> files(nfile);
+  std::vector<std::string> errors(nfile);
+  {
+    py::gil_scoped_release nogil;
+    unsigned nt = std::max(1u, std::thread::hardware_concurrency());
+    if (const char* e = std::getenv("PML_AVRO_THREADS")) nt = (unsigned)std::max(1, atoi(e));
+    nt = (unsigned)std::min<size_t>(nt, std::max<size_t>(nfile, 1));
+    std::atomic<size_t> next{0};
+    auto work = [&]() {
+      for (size_t f = next++; f < nfile; f = next++) {
+        try { decode_columnar_file(paths[f], op, files[f]); }
+        catch (const std::exception& ex) { errors[f] = ex.what(); }
+      }
+    };
+    std::vector<std::thread> pool;
+    for (unsigned t = 1; t < nt; ++t) pool.emplace_back(work);
+    work();
+    for (auto& t : pool) t.join();
+  }
+  for (size_t f = 0; f < nfile; ++f)
+    if (!errors[f].empty()) throw std::runtime_error(errors[f]);
+  // deterministic merge in file order
+  Interner intern;
+  int64_t n = 0;
+  std::string label_used;
   std::vector<double> label, weight, offset;
   std::vector<std::string> uid;
   std::vector<uint8_t> has_uid;
-  std::map<std::string, std::vector<std::string>> tags;
-  for (auto& t : id_tags) tags[t];
+  std::vector<std::vector<std::string>> tags(id_tags.size());
   std::map<std::string, BagOut> bags;
-  Interner intern;
-  std::string label_used;
-  int64_t n = 0;
-  for (auto& path : paths) {
-    OCF o(path);
-    const Node* root = o.schema->root;
-    if (root->t != AT::RECORD) throw std::runtime_error("top-level Avro schema must be a record: " + path);
-    // field roles
-    std::vector<int> role(root->fields.size(), 0);  // 0 skip, 1 label, 2 weight, 3 offset, 4 uid, 5 meta, 6 bag, 7 tag
-    std::vector<std::string> rname(root->fields.size());
-    int label_idx = -1;
-    for (auto& lf : label_fields) {
-      for (size_t i = 0; i < root->fields.size(); ++i)
-        if (root->fields[i].first == lf) { label_idx = (int)i; break; }
-      if (label_idx >= 0) { label_used = lf; break; }
-    }
-    for (size_t i = 0; i < root->fields.size(); ++i) {
-      const std::string& fn = root->fields[i].first;
-      const Node* fnode = root->fields[i].second;
-      if ((int)i == label_idx) role[i] = 1;
-      else if (fn == weight_field) role[i] = 2;
-      else if (fn == offset_field) role[i] = 3;
-      else if (fn == uid_field) role[i] = 4;
-      else if (fn == metadata_field) role[i] = 5;
-      else if (tags.count(fn)) { role[i] = 7; rname[i] = fn; }
-      else if (is_bag(fnode)) {
-        bool want = bags_wanted.empty();
-        for (auto& b : bags_wanted) if (b == fn) want = true;
-        if (want) { role[i] = 6; rname[i] = fn; bags[fn]; }
+  for (auto& fc : files)
+    for (auto& b : fc.bags) bags[b.first];
+  for (auto& fc : files) {
+    if (label_used.empty()) label_used = fc.label_used;
+    std::vector<int32_t> remap(fc.intern.keys.size());
+    for (size_t k = 0; k < remap.size(); ++k) remap[k] = intern.get(fc.intern.keys[k]);
+    label.insert(label.end(), fc.label.begin(), fc.label.end());
+    weight.insert(weight.end(), fc.weight.begin(), fc.weight.end());
+    offset.insert(offset.end(), fc.offset.begin(), fc.offset.end());
+    for (auto& x : fc.uid) uid.push_back(std::move(x));
+    has_uid.insert(has_uid.end(), fc.has_uid.begin(), fc.has_uid.end());
+    for (size_t t = 0; t < tags.size(); ++t)
+      for (auto& x : fc.tags[t]) tags[t].push_back(std::move(x));
+    for (auto& b : bags) {
+      BagOut& dst = b.second;
+      auto src = fc.bags.find(b.first);
+      const int64_t base = (int64_t)dst.keys.size();
+      if (src == fc.bags.end()) {
+        dst.rowptr.insert(dst.rowptr.end(), (size_t)fc.n, base);
+        continue;
       }
+      for (int32_t k : src->second.keys) dst.keys.push_back(remap[(size_t)k]);
+      dst.vals.insert(dst.vals.end(), src->second.vals.begin(), src->second.vals.end());
+      for (size_t r = 1; r < src->second.rowptr.size(); ++r) dst.rowptr.push_back(base + src->second.rowptr[r]);
     }
-    for (auto& blk : o.blocks) {
-      Reader r((const uint8_t*)blk.second.data(), blk.second.size());
-      for (int64_t rec = 0; rec < blk.first; ++rec) {
-        double lab = NAN, wt = NAN, off = NAN;
-        std::string u; bool hu = false;
-        std::map<std::string, std::string> rec_tags;
-        std::map<std::string, bool> bag_seen;
-        for (size_t i = 0; i < root->fields.size(); ++i) {
-          const Node* fnode = root->fields[i].second;
-          bool ok;
-          switch (role[i]) {
-            case 1: lab = read_number(r, fnode, ok); break;
-            case 2: wt = read_number(r, fnode, ok); break;
-            case 3: off = read_number(r, fnode, ok); break;
-            case 4: hu = read_string_like(r, fnode, u); break;
-            case 7: { std::string s; if (read_string_like(r, fnode, s)) rec_tags[rname[i]] = s; break; }
-            case 5: {
-              const Node* m = fnode;
-              if (m->t == AT::UNION) { int64_t k = r.varlong(); m = m->branches.at((size_t)k); }
-              if (m->t != AT::MAP) { skip_value(r, m); break; }
-              while (true) {
-                int64_t c = r.varlong();
-                if (c == 0) break;
-                if (c < 0) { c = -c; r.varlong(); }
-                for (int64_t k = 0; k < c; ++k) {
-                  std::string key = r.str();
-                  std::string sval;
-                  bool has = read_string_like(r, m->items, sval);
-                  if (has && tags.count(key) && !rec_tags.count(key)) rec_tags[key] = sval;
-                }
-              }
-              break;
-            }
-            case 6: {
-              BagOut& bo = bags[rname[i]];
-              const Node* arr = fnode;
-              if (arr->t == AT::UNION) { int64_t k = r.varlong(); arr = arr->branches.at((size_t)k); }
-              if (arr->t != AT::ARRAY) { skip_value(r, arr); break; }
-              const Node* item = arr->items;
-              while (true) {
-                int64_t c = r.varlong();
-                if (c == 0) break;
-                if (c < 0) { c = -c; r.varlong(); }
-                for (int64_t k = 0; k < c; ++k) {
-                  const Node* it = item;
-                  if (it->t == AT::UNION) { int64_t b = r.varlong(); it = it->branches.at((size_t)b); }
-                  std::string name, term;
-                  double val = NAN;
-                  for (auto& f : it->fields) {
-                    if (f.first == "name") read_string_like(r, f.second, name);
-                    else if (f.first == "term") { if (!read_string_like(r, f.second, term)) term.clear(); }
-                    else if (f.first == "value") { bool okv; val = read_number(r, f.second, okv); }
-                    else skip_value(r, f.second);
-                  }
-                  bo.keys.push_back(intern.get(name + delimiter + term));
-                  bo.vals.push_back(val);
-                }
-              }
-              bag_seen[rname[i]] = true;
-              break;
-            }
-            default: skip_value(r, fnode);
-          }
-        }
-        label.push_back(lab); weight.push_back(wt); offset.push_back(off);
-        uid.push_back(u); has_uid.push_back(hu ? 1 : 0);
-        for (auto& t : tags) {
-          auto it = rec_tags.find(t.first);
-          t.second.push_back(it == rec_tags.end() ? std::string() : it->second);
-        }
-        for (auto& b : bags) b.second.rowptr.push_back((int64_t)b.second.keys.size());
-        ++n;
-      }
-    }
+    n += fc.n;
+    std::vector<std::string>().swap(fc.intern.keys);   // release per-file memory as the merge proceeds
   }
   auto arr_d = [](std::vector<double>& v) { return py::array_t<double>((py::ssize_t)v.size(), v.data()); };
   py::dict out;
@@ -870,7 +1021,7 @@ static py::dict read_columnar(const std::vector<std::string>& paths, const std::
   out["uid"] = py::cast(uid);
   out["has_uid"] = py::array_t<uint8_t>((py::ssize_t)has_uid.size(), has_uid.data());
   py::dict tg;
-  for (auto& t : tags) tg[py::str(t.first)] = py::cast(t.second);
+  for (size_t t = 0; t < id_tags.size(); ++t) tg[py::str(id_tags[t])] = py::cast(tags[t]);
   out["id_tags"] = tg;
   py::dict bg;
   for (auto& b : bags) {

@@ -102,8 +102,8 @@ def build_cpp(name: str, force: bool = False, verbose: bool = False, sanitize: b
         vis = ["-fvisibility=hidden"] if name == "avro" else []  # pybind11 module vs plain C ABI
         opt = ["-O1", "-g", "-fno-omit-frame-pointer", "-fsanitize=address,undefined",
                "-fno-sanitize-recover=undefined"] if sanitize else ["-O3"]
-        cmd = ["g++", *opt, "-std=c++17", "-fPIC", "-shared", *vis, *inc, str(src), "-o", str(out) + ".tmp",
-               "-lz"]
+        cmd = ["g++", *opt, "-std=c++17", "-fPIC", "-shared", "-pthread", *vis, *inc, str(src), "-o",
+               str(out) + ".tmp", "-lz"]
         if verbose:
             print(" ".join(cmd), flush=True)
         subprocess.run(cmd, check=True)

@@ -115,6 +115,9 @@ class SegChunk:
                                                            self.idx, self.val))
 
 
+# PML_TRON_STATS=1: (kept forward blocks, kept transpose items) fractions of every entity-masked table rebuild
+MASK_STATS = [] if os.environ.get("PML_TRON_STATS") == "1" else None
+
 class DeviceGLMData(GLMComputable):
     """GLM row shard on one GPU evaluated with the native kernels."""
 
@@ -498,8 +501,10 @@ class DeviceGLMData(GLMComputable):
         st = self.stats.data_ptr() + 2 * 8 * self.blk_off[c] if stats else None
         xp = x.data_ptr() + self.col_lo[c] * x.element_size()
         if ch.kind == "tl":
+            masked = getattr(self, "_masked", None)
+            desc = masked[0][c] if masked is not None and isinstance(masked[0], list) else ch.desc
             check(self.lib.pml_tl_fwd(
-                self.prec, ctypes.byref(ch.desc), xp, mode, loss_id, float(shift),
+                self.prec, ctypes.byref(desc), xp, mode, loss_id, float(shift),
                 self._rows(self.y, c), self._rows(self.o, c), self._rows(self.wt, c),
                 None if coef is None else self._rows(coef, c), None if dzz is None else self._rows(dzz, c),
                 None if z_out is None else self._rows(z_out, c), with_offset, st, stream_handle(self.device)),
@@ -517,7 +522,9 @@ class DeviceGLMData(GLMComputable):
         ch = self.csc[c]
         gp = G.data_ptr() + self.col_lo[c] * G.element_size()
         if ch.kind == "tl":
-            check(self.lib.pml_tl_t(self.prec, ctypes.byref(ch.desc), self._rows(x, c), square, gp,
+            masked = getattr(self, "_masked", None)
+            desc = ch.desc if masked is None else masked[1][c]
+            check(self.lib.pml_tl_t(self.prec, ctypes.byref(desc), self._rows(x, c), square, gp,
                                     self.parts.data_ptr(), stream_handle(self.device)), "tl_t")
             return
         check(self.lib.pml_seg_t(self.prec, ctypes.byref(ch.desc), self._rows(x, c), square, gp,
@@ -567,8 +574,10 @@ class DeviceGLMData(GLMComputable):
             self._build_multi()
         if self._multi is not None and KERNEL_CONFIG.get("tl_multi", 1):
             p = lambda t: None if t is None else t.data_ptr()
+            masked = getattr(self, "_masked", None)
+            desc = self._multi if masked is None or isinstance(masked[0], list) else masked[0]
             check(self.lib.pml_tl_fwd_multi(
-                self.prec, ctypes.byref(self._multi), x.data_ptr(), mode, loss_id, float(shift), self.y.data_ptr(),
+                self.prec, ctypes.byref(desc), x.data_ptr(), mode, loss_id, float(shift), self.y.data_ptr(),
                 self.o.data_ptr(), self.wt.data_ptr(), p(coef), p(dzz), p(z_out), with_offset,
                 self.stats.data_ptr() if stats else None, stream_handle(self.device)), "tl_fwd_multi")
             return
@@ -588,6 +597,98 @@ class DeviceGLMData(GLMComputable):
             return
         for c in range(len(self.csc)):
             self._t(c, x, G, square)
+
+    # ---- entity-masked passes (block-diagonal random-effect problems, optimization/batched.py): the forward
+    # skips row blocks and the transpose skips column tiles whose rows / columns all belong to entities that are
+    # no longer iterating. Rows and columns are grouped by entity, so a skipped block or tile touches no live
+    # entity's margins or gradient; outputs of skipped rows / columns are left at zero.
+    def entity_mask_geometry(self, row_entity: torch.Tensor, col_entity: torch.Tensor):
+        """(first, last) entity of every forward block and of every transpose item of every chunk; False when
+        the layout does not support masked passes."""
+        cached = getattr(self, "_mgeo", None)
+        if cached is not None:
+            return cached
+        self._mgeo = False
+        if getattr(self, "_multi", "unset") == "unset":
+            self._build_multi()
+        if (self.old_of_new is not None or not self.csc or any(ch.kind != "tl" for ch in self.csc + self.csr)
+                or not self.n_rows):
+            return False
+        nr, nc = row_entity.numel(), col_entity.numel()
+        span = lambda lo, cnt: (row_entity[lo.clamp(0, nr - 1)], row_entity[(lo + cnt - 1).clamp(0, nr - 1)])
+        if self._multi is not None:
+            blk = self._multi_blk.to(torch.int64)
+            fwd = span(blk[:, 1], blk[:, 2])
+        else:                         # per-chunk forward tables {row_lo (chunk-local), nrows, ...}
+            fwd = [span(ch.blk[: ch.nblk, 0].to(torch.int64) + self.row_starts[c], ch.blk[: ch.nblk, 1].to(torch.int64))
+                   for c, ch in enumerate(self.csr)]
+        items = []
+        for c, ch in enumerate(self.csc):
+            C = 1 << ch.cbits
+            hi = self.col_lo[c] + ch.dim - 1
+            first = lambda t: (self.col_lo[c] + t.to(torch.int64) * C).clamp(0, nc - 1)
+            last = lambda t: torch.clamp(self.col_lo[c] + (t.to(torch.int64) + 1) * C - 1, max=hi).clamp(0, nc - 1)
+            it = ch.items[: ch.nitems, 0]
+            mt = ch.mt_tiles[: ch.nmt]
+            items.append(((col_entity[first(it)], col_entity[last(it)]), (col_entity[first(mt)], col_entity[last(mt)])))
+        self._mgeo = (fwd, items)
+        return self._mgeo
+
+    def set_entity_mask(self, active: Optional[torch.Tensor], geometry=None):
+        """Restrict matvec / rmatvec to the blocks and tiles of the ``active`` entities (bool [n_entities]);
+        None restores full passes."""
+        self._masked = None
+        if active is None or not geometry:
+            return
+        from .native import TLFwdMultiDesc, TLTDesc
+        fwd, items = geometry
+        cs = torch.zeros(active.numel() + 1, dtype=torch.int64, device=active.device)
+        torch.cumsum(active.to(torch.int64), 0, out=cs[1:])
+        live = lambda rng: (cs[rng[1] + 1] - cs[rng[0]]) > 0
+        if isinstance(fwd, tuple):
+            tab = self._multi_blk[live(fwd)].contiguous()
+            keep = [tab]
+            fdesc = TLFwdMultiDesc(tab.data_ptr(), tab.shape[0], self.csr[0].rbits, self._multi_ptrs.data_ptr(),
+                                   self.csr[0].il)
+            n_blk_kept, n_blk = tab.shape[0], self._multi_blk.shape[0]
+        else:
+            from .native import TLFwdDesc
+            fdesc, keep, n_blk_kept, n_blk = [], [], 0, 0
+            for ch, rng in zip(self.csr, fwd):
+                tab = ch.blk[: ch.nblk][live(rng)].contiguous()
+                keep.append(tab)
+                fdesc.append(TLFwdDesc(tab.data_ptr(), tab.shape[0], ch.rbits, ch.pack.data_ptr(), ch.val.data_ptr(),
+                                       ch.il, ch.nar))
+                n_blk_kept += tab.shape[0]
+                n_blk += ch.nblk
+        tdescs = []
+        for ch, (irng, mrng) in zip(self.csc, items):
+            it = ch.items[: ch.nitems][live(irng)].contiguous()
+            mkeep = live(mrng)
+            cu = ch.cu[: ch.ncu].to(torch.int64)
+            if ch.nmt:
+                newmt = torch.cumsum(mkeep.to(torch.int64), 0) - 1
+                ck = mkeep[cu[:, 0]]
+                cu_new = cu[ck]
+                cu_new[:, 0] = newmt[cu_new[:, 0]]
+                per = (ch.mt_ptr[1: ch.nmt + 1] - ch.mt_ptr[: ch.nmt]).to(torch.int64)[mkeep]
+                mt_ptr = torch.zeros(per.numel() + 1, dtype=torch.int64, device=per.device)
+                torch.cumsum(per, 0, out=mt_ptr[1:])
+                mt_tiles = ch.mt_tiles[: ch.nmt][mkeep].contiguous()
+            else:
+                cu_new, mt_ptr, mt_tiles = cu[:0], torch.zeros(1, dtype=torch.int64, device=cu.device), ch.mt_tiles
+            cu_new = cu_new.to(torch.int32).contiguous()
+            mt_ptr = mt_ptr.to(torch.int32).contiguous()
+            nmt = int(mt_tiles.numel()) if ch.nmt else 0
+            d = TLTDesc(it.data_ptr(), it.shape[0], ch.cbits, ch.pack.data_ptr(), ch.val.data_ptr(),
+                        mt_tiles.data_ptr(), mt_ptr.data_ptr(), nmt, ch.dim, cu_new.data_ptr(), cu_new.shape[0],
+                        ch.nparts, ch.il, ch.nar)
+            keep += [it, cu_new, mt_ptr, mt_tiles]
+            tdescs.append(d)
+        self._masked = (fdesc, tdescs, keep)
+        if MASK_STATS is not None:
+            n_it = sum(int(ch.nitems) for ch in self.csc)
+            MASK_STATS.append((n_blk_kept / max(1, n_blk), sum(int(d.nitems) for d in tdescs) / max(1, n_it)))
 
     # ---- gradient buckets: the transpose split into column-tile ranges so each range's all-reduce can start as
     # soon as that range is final (overlap of the C1 collective with the rest of the transpose pass)
@@ -777,7 +878,8 @@ class DeviceGLMData(GLMComputable):
         return self._unperm(out)
 
     def margins(self, w, margin_shift: float = 0.0, with_offsets: bool = False):
-        z = torch.empty(max(self.n_rows, 1), dtype=torch.float64, device=self.device)
+        alloc = torch.empty if getattr(self, "_masked", None) is None else torch.zeros   # skipped rows stay 0
+        z = alloc(max(self.n_rows, 1), dtype=torch.float64, device=self.device)
         x = self._vec(w)
         self.fwd_all(x, FWD_MARGIN, 0, margin_shift, None, None, z_out=z, with_offset=int(with_offsets),
                      stats=False)

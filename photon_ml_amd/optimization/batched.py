@@ -170,11 +170,35 @@ class SegmentedGLMData:
         from ..ops.native import seg_cg_step
         seg_cg_step(self.col_ptr, step, r, d, Hd, rtr, on, delta, l2)
 
-    def margins(self, W):
+    supports_active = True
+
+    def _set_active(self, active):
+        """Entity-masked GLM passes (``DeviceGLMData.set_entity_mask``): blocks / tiles of entities outside
+        ``active`` are skipped; their margins and gradient entries come back as zero (the callers only read the
+        active entities). The filtered tables are rebuilt only when the active set changed."""
+        glm = self.glm
+        if not MASKED_PASSES or not hasattr(glm, "entity_mask_geometry"):
+            return
+        if active is None:
+            if getattr(self, "_active_key", None) is not None:
+                glm.set_entity_mask(None)
+                self._active_key = None
+            return
+        geo = glm.entity_mask_geometry(self.row_entity, self.col_entity)
+        if not geo:
+            return
+        key = getattr(self, "_active_key", None)
+        if key is not None and key.shape == active.shape and bool(torch.equal(key, active)):
+            return
+        glm.set_entity_mask(active, geo)
+        self._active_key = active.clone()
+
+    def margins(self, W, active=None):
+        self._set_active(active)
         return self.glm.matvec(W) + self.o
 
-    def value_grad(self, loss, W, l2: float):
-        z = self.margins(W)
+    def value_grad(self, loss, W, l2: float, active=None):
+        z = self.margins(W, active)
         l, dl = loss.loss_and_dz(z, self.y)
         f = self._rowsum(self.w * l)
         g = self.glm.rmatvec(self.w * dl)
@@ -187,13 +211,16 @@ class SegmentedGLMData:
         # cache keyed by tensor identity + in-place version (holding the reference keeps W alive, so its
         # storage cannot be recycled under the key); no O(D) comparison / copy per Hessian-vector product
         key = self._dzz_key
-        if key is not None and key[0] is W and key[1] == W._version and key[2] is loss:
+        mk = getattr(self, "_active_key", None)
+        if (key is not None and key[0] is W and key[1] == W._version and key[2] is loss
+                and (key[3] is None or (mk is not None and bool((mk <= key[3]).all())))):
             return self._dzz
-        self._dzz = self.w * loss.dzz(self.margins(W), self.y)
-        self._dzz_key = (W, W._version, loss)
+        self._dzz = self.w * loss.dzz(self.glm.matvec(W) + self.o, self.y)
+        self._dzz_key = (W, W._version, loss, None if mk is None else mk.clone())
         return self._dzz
 
-    def hv(self, loss, W, V, l2: float):
+    def hv(self, loss, W, V, l2: float, active=None):
+        self._set_active(active)
         D = self._dzz_at(loss, W)
         h = self.glm.rmatvec(D * self.glm.matvec(V))
         return h + l2 * V if l2 > 0 else h
@@ -238,6 +265,18 @@ class _Convergence:
         return reason
 
 
+# block-diagonal passes skip the row blocks / column tiles of entities that stopped iterating (PML_RE_MASKED=0: off)
+MASKED_PASSES = os.environ.get("PML_RE_MASKED", "1") != "0"
+
+# PML_TRON_STATS=1: record, per CG step of the block-diagonal TRON, the fraction of rows whose entity is still
+# iterating (how much of each Hessian-vector pass is wasted on converged entities); read by bench_game.py
+_TRON_STATS = [] if os.environ.get("PML_TRON_STATS") == "1" else None
+
+
+def tron_stats():
+    return _TRON_STATS
+
+
 def batched_tron(data, loss, l2: float, W0: torch.Tensor, tol: float = 1e-5, max_iter: int = 15,
                  max_fail: int = 5, max_cg: int = 20, fused: Optional[bool] = None,
                  frozen: Optional[torch.Tensor] = None) -> BatchedResult:
@@ -248,6 +287,14 @@ def batched_tron(data, loss, l2: float, W0: torch.Tensor, tol: float = 1e-5, max
 
     ``fused``: run each CG iteration's vector algebra as one segmented kernel (``data.cg_step``; default when the
     data provides it, i.e. the block-diagonal layout) instead of ~30 elementwise / reduction ops."""
+    try:
+        return _batched_tron(data, loss, l2, W0, tol, max_iter, max_fail, max_cg, fused, frozen)
+    finally:
+        if getattr(data, "supports_active", False):
+            data._set_active(None)          # later users of the GLM data get full passes
+
+
+def _batched_tron(data, loss, l2, W0, tol, max_iter, max_fail, max_cg, fused, frozen) -> BatchedResult:
     if fused is None:
         fused = hasattr(data, "cg_step") and os.environ.get("PML_FUSED_CG", "1") != "0"
     eta0, eta1, eta2 = 1e-4, 0.25, 0.75
@@ -292,13 +339,17 @@ def batched_tron(data, loss, l2: float, W0: torch.Tensor, tol: float = 1e-5, max
             cg_on &= torch.sqrt(rtr.clamp(min=0)) > cg_tol
             if not bool(cg_on.any()):
                 break
+            if _TRON_STATS is not None and hasattr(data, "row_ptr"):
+                n_rows = (data.row_ptr[1:] - data.row_ptr[:-1]).to(torch.float64)
+                _TRON_STATS.append(float((n_rows * cg_on).sum() / n_rows.sum().clamp(min=1)))
+            act_kw = {"active": cg_on} if getattr(data, "supports_active", False) else {}
             if fused:
-                Hd = data.hv(loss, W, d, 0.0)
+                Hd = data.hv(loss, W, d, 0.0, **act_kw)
                 on8 = cg_on.to(torch.uint8)
                 data.cg_step(step, r, d, Hd, rtr, on8, delta, l2)
                 cg_on = on8.bool()
                 continue
-            Hd = data.hv(loss, W, d, l2)
+            Hd = data.hv(loss, W, d, l2, **act_kw)
             dHd = data.bdot(d, Hd)
             alpha = torch.where(cg_on, rtr / torch.where(dHd == 0, torch.ones_like(dHd), dHd),
                                 torch.zeros_like(rtr))
@@ -328,7 +379,8 @@ def batched_tron(data, loss, l2: float, W0: torch.Tensor, tol: float = 1e-5, max
         W_new = W + step
         gs = data.bdot(g, step)
         pred = -0.5 * (gs - data.bdot(step, r))
-        f_new, g_new = data.value_grad(loss, W_new, l2)
+        f_new, g_new = data.value_grad(loss, W_new, l2, **({"active": active} if getattr(
+            data, "supports_active", False) else {}))
         actual = f - f_new
         snorm = _bn(data, step)
         first = active & (it == 0)

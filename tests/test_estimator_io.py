@@ -143,3 +143,59 @@ def test_snappy_codec_compresses_and_round_trips():
     assert len(nat.snappy_compress(text)) < len(text) // 4
     noise = cases[4]
     assert len(nat.snappy_compress(noise)) <= len(noise) + len(noise) // 1000 + 16
+
+
+def test_parallel_columnar_decode_is_deterministic(tmp_path, monkeypatch):
+    """Files decoded on several threads merge in file order: same rows, same feature ids (first appearance),
+    same bags as a single-threaded decode."""
+    from photon_ml_amd.io import avro
+    from photon_ml_amd.io.data_writer import game_example_schema
+    rng = np.random.default_rng(5)
+    schema = game_example_schema(["features", "other"])
+    for part in range(5):
+        recs = []
+        for i in range(200 + 37 * part):
+            cols = rng.choice(300, 7, replace=False)
+            recs.append({"uid": f"{part}-{i}", "response": float(i % 2), "weight": 1.0, "offset": 0.0,
+                         "features": [{"name": f"f{c}", "term": "t", "value": float(c)} for c in cols],
+                         "other": [{"name": f"o{part}", "term": "", "value": 1.0}], "metadataMap": {}})
+        avro.write_records(str(tmp_path / f"part-{part}.avro"), schema, recs, codec="snappy" if part % 2 else "deflate")
+    files = sorted(str(p) for p in tmp_path.iterdir())
+    outs = []
+    for th in ("1", "4"):
+        monkeypatch.setenv("PML_AVRO_THREADS", th)
+        outs.append(avro.native().read_columnar(files, ["response"], "weight", "offset", "uid", "metadataMap",
+                                                ["features", "other"], [], "\x01"))
+    a, b = outs
+    assert a["n"] == b["n"] == sum(200 + 37 * p for p in range(5))
+    assert list(a["vocab"]) == list(b["vocab"]) and list(a["uid"]) == list(b["uid"])
+    for bag in ("features", "other"):
+        for x, y in zip(a["bags"][bag], b["bags"][bag]):
+            np.testing.assert_array_equal(x, y)
+
+
+def test_bags_to_csr_matches_coo_reference():
+    """Direct CSR placement of bag entries (+ intercept, unmapped keys dropped) == the COO construction."""
+    import scipy.sparse as sp
+    from photon_ml_amd.io.data_reader import _bags_to_csr
+    rng = np.random.default_rng(6)
+    n, dim = 50, 40
+    parts = []
+    for pool in (np.r_[0:15, 30:40], np.r_[15:30, 40:50]):        # disjoint bags; keys >= 30 are unmapped
+        cnt = rng.integers(0, 6, n)
+        rowptr = np.r_[0, np.cumsum(cnt)]
+        keys = np.concatenate([rng.choice(pool, c, replace=False) for c in cnt]).astype(np.int32)
+        parts.append((rowptr, keys, rng.random(len(keys))))
+    vocab_to_col = np.where(np.arange(60) < 30, np.arange(60), -1)
+    m = _bags_to_csr(n, parts, vocab_to_col, dim, 39, True)
+    rows, cols, vals = [], [], []
+    for rowptr, keys, v in parts:
+        rows.append(np.repeat(np.arange(n), np.diff(rowptr)))
+        cols.append(vocab_to_col[keys])
+        vals.append(v)
+    rows.append(np.arange(n)); cols.append(np.full(n, 39)); vals.append(np.ones(n))
+    r, c, v = map(np.concatenate, (rows, cols, vals))
+    ok = c >= 0
+    ref = sp.csr_matrix((v[ok], (r[ok], c[ok])), shape=(n, dim))
+    ref.sort_indices()
+    assert (m != ref).nnz == 0 and m.has_sorted_indices

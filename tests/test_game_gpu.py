@@ -200,3 +200,26 @@ def test_row_space_gram_kernel_matches_indicator_passes():
     ra = a.solve(LOGISTIC, 1.0, "TRON", None, 1e-10, 60)
     rb = b.solve(LOGISTIC, 1.0, "TRON", None, 1e-10, 60)
     torch.testing.assert_close(a.to_primal(ra.W), b.to_primal(rb.W), rtol=1e-6, atol=1e-8)
+
+
+@pytest.mark.parametrize("row_space", ["0", "1"])
+def test_entity_masked_passes_give_identical_solve(row_space, monkeypatch):
+    """The block-diagonal TRON skipping the row blocks / column tiles of entities that stopped iterating
+    (DeviceGLMData.set_entity_mask) reproduces the full-pass solve bit for bit: active entities see the same
+    entries in the same order; skipped outputs are never read."""
+    import photon_ml_amd.optimization.batched as bt
+    from photon_ml_amd.algorithm.coordinates import RandomEffectCoordinate
+    monkeypatch.setenv("PML_RE_ROW_SPACE", row_space)
+    data, _ = generate_game_data(n_rows=30000, n_users=500, d_user=8, seed=25, task="LOGISTIC_REGRESSION")
+    cfg = GLMOptimizationConfiguration(OptimizerConfig("TRON", 30, 1e-10), RegularizationContext("L2"), 1.0)
+    out = {}
+    for masked in (False, True):
+        monkeypatch.setattr(bt, "MASKED_PASSES", masked)
+        c = RandomEffectCoordinate("u", data, RandomEffectDataConfiguration("userId", "user"), cfg,
+                                   "LOGISTIC_REGRESSION", device="cuda", layout="segmented")
+        m1 = c.update_model(c.initialize_model())
+        m2 = c.update_model(m1, partial_score=torch.from_numpy(np.sin(np.arange(data.n_rows)) * 0.2))
+        out[masked] = (m2.values.copy(), c.last_stats["mean_iterations"], c.score(m2).cpu())
+    assert np.array_equal(out[False][0], out[True][0])
+    assert out[False][1] == out[True][1]
+    assert torch.equal(out[False][2], out[True][2])
