@@ -878,6 +878,17 @@ class DeviceGLMData(GLMComputable):
         return self._unperm(out)
 
     def margins(self, w, margin_shift: float = 0.0, with_offsets: bool = False):
+        if (getattr(self, "_masked", None) is None and getattr(self, "z_cache", None) is not None
+                and isinstance(w, torch.Tensor) and self._z_valid_for(w, margin_shift)):
+            # the margins of the optimizer's last accepted point are cached (z0 + t_pending zd, offsets included):
+            # scoring the returned model needs no forward pass
+            n = self.n_rows
+            z = self.z_cache[:n].clone()
+            if self._tpend:
+                z.add_(self.zd[:n], alpha=self._tpend)
+            if not with_offsets:
+                z.sub_(self.o[:n].to(torch.float64))
+            return z
         alloc = torch.empty if getattr(self, "_masked", None) is None else torch.zeros   # skipped rows stay 0
         z = alloc(max(self.n_rows, 1), dtype=torch.float64, device=self.device)
         x = self._vec(w)

@@ -540,3 +540,27 @@ def test_device_two_loop_matches_host_scalar_two_loop(monkeypatch):
         w, _ = opt.optimize(GLMObjective(LOGISTIC, 1.0), dev, torch.zeros(300, dtype=torch.float64, device="cuda"))
         out[flag] = (w.cpu(), None)
     torch.testing.assert_close(out[True][0], out[False][0], rtol=1e-9, atol=1e-11)
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("precision", ["f64", "bf16"])
+def test_scoring_reuses_cached_margins(precision):
+    """margins(w) at the optimizer's last accepted point comes from the margin cache (z0 + t zd - offsets, no
+    forward pass) and equals a fresh forward pass to rounding."""
+    from photon_ml_amd.data.synthetic import generate_device_shard
+    from photon_ml_amd.function.losses import LOGISTIC
+    data, w = generate_device_shard(200_000, 40_000, 20, "cuda", precision, chunk_rows=1 << 16, layout="tiled")
+    w = (w * 0.05).to(torch.float64)
+    data.set_offsets(0.1 * torch.randn(data.n_rows, dtype=torch.float64, device="cuda"))
+    data.enable_margin_cache()
+    data.value_grad_packed(LOGISTIC, w, 0.0)          # caches z at w
+    d = 0.01 * torch.randn_like(w)
+    assert data.ls_begin(w, 0.0, d, 0.0, 1.0, LOGISTIC)
+    w1 = w + 0.5 * d
+    data.ls_finish_packed(LOGISTIC, 0.5, w1, 0.0)      # accepted t = 0.5: pending step in the cache
+    n0 = data.n_passes
+    cached = data.margins(w1)
+    data._z_key = None
+    fresh = data.margins(w1)
+    torch.testing.assert_close(cached, fresh, rtol=1e-12, atol=1e-12)
+    assert data.n_passes == n0
