@@ -1090,10 +1090,12 @@ __global__ __launch_bounds__(NW * 64) void tl_fwd_kernel(const int* __restrict__
                                                           const uint32_t* __restrict__ pack,
                                                           const VT* __restrict__ val, TLNarrow nar,
                                                           const XT* __restrict__ x, FwdArgs<XT, RT> a,
-                                                          double* __restrict__ stats) {
+                                                          double* __restrict__ stats,
+                                                          const unsigned char* __restrict__ live) {
   __shared__ AT acc[NW][MAXR];
   __shared__ double red[2 * NW];
   const int b = blockIdx.x;
+  if (live && !live[b]) return;
   const int* q = blk + 6 * b;
   tl_fwd_block<VT, XT, RT, AT, MAXR, U, NW, P>(b, q[0], q[1], q[2], q[3], q[4], q[5], rbits, pack, val, nar, x, a,
                                               stats, acc, red);
@@ -1107,10 +1109,12 @@ template <typename VT, typename XT, typename RT, typename AT, int MAXR, int U, i
 __global__ __launch_bounds__(NW * 64) void tl_fwd_multi_kernel(const int* __restrict__ blk, int rbits,
                                                                 const unsigned long long* __restrict__ ptrs,
                                                                 const XT* __restrict__ x, FwdArgs<XT, RT> a,
-                                                                double* __restrict__ stats) {
+                                                                double* __restrict__ stats,
+                                                                const unsigned char* __restrict__ live) {
   __shared__ AT acc[NW][MAXR];
   __shared__ double red[2 * NW];
   const int b = blockIdx.x;
+  if (live && !live[b]) return;
   const int* q = blk + 8 * b;
   const unsigned long long* pc = ptrs + 5 * q[0];
   const TLNarrow nar = {(const uint16_t*)pc[2], (const void*)pc[3], (const int*)pc[4]};
@@ -1154,8 +1158,10 @@ __global__ __launch_bounds__(NW * 64) void tl_t_kernel(const int* __restrict__ i
                                                         const uint32_t* __restrict__ pack,
                                                         const VT* __restrict__ val, TLNarrow nar,
                                                         const XT* __restrict__ x, double* __restrict__ G, int dim,
-                                                        double* __restrict__ parts) {
+                                                        double* __restrict__ parts,
+                                                        const unsigned char* __restrict__ live) {
   __shared__ AT acc[NW][MAXR];
+  if (live && !live[blockIdx.x]) return;
   const int* q = items + 6 * blockIdx.x;
   tl_t_item<VT, XT, AT, SQ, MAXR, U, NW, P>(q[0], q[1], q[2], q[3], q[4], q[5], cbits, pack, val, nar, x, G, dim,
                                             parts, acc);
@@ -1169,8 +1175,10 @@ template <typename VT, typename XT, typename AT, bool SQ, int MAXR, int U, int N
 __global__ __launch_bounds__(NW * 64) void tl_t_multi_kernel(const int* __restrict__ items, int cbits,
                                                               const unsigned long long* __restrict__ ptrs,
                                                               const XT* __restrict__ x, double* __restrict__ G,
-                                                              int dim, double* __restrict__ parts) {
+                                                              int dim, double* __restrict__ parts,
+                                                              const unsigned char* __restrict__ live) {
   __shared__ AT acc[NW][MAXR];
+  if (live && !live[blockIdx.x]) return;
   const int* q = items + 8 * blockIdx.x;
   const unsigned long long* pc = ptrs + 5 * q[0];
   const TLNarrow nar = {(const uint16_t*)pc[2], (const void*)pc[3], (const int*)pc[4]};
@@ -1185,8 +1193,10 @@ __global__ __launch_bounds__(NW * 64) void tl_t_multi_kernel(const int* __restri
 //            (blockIdx.y = column group), and adds into G.
 __global__ __launch_bounds__(NTHREADS) void tl_t_combine1_kernel(const int* __restrict__ cu, int cbits,
                                                                  const double* __restrict__ parts,
-                                                                 double* __restrict__ l1) {
+                                                                 double* __restrict__ l1,
+                                                                 const unsigned char* __restrict__ live_mt) {
   const int u = blockIdx.x;
+  if (live_mt && !live_mt[cu[3 * u]]) return;
   const int C = 1 << cbits;
   const int p0 = cu[3 * u + 1], p1 = cu[3 * u + 2];
   for (int c = threadIdx.x; c < C; c += NTHREADS) {
@@ -1199,8 +1209,10 @@ __global__ __launch_bounds__(NTHREADS) void tl_t_combine1_kernel(const int* __re
 __global__ __launch_bounds__(NTHREADS) void tl_t_combine2_kernel(const int* __restrict__ mt_tiles,
                                                                  const int* __restrict__ mt_ptr, int cbits,
                                                                  const double* __restrict__ l1,
-                                                                 double* __restrict__ G, int dim) {
+                                                                 double* __restrict__ G, int dim,
+                                                                 const unsigned char* __restrict__ live_mt) {
   const int t = blockIdx.x;
+  if (live_mt && !live_mt[t]) return;
   const int C = 1 << cbits;
   const int c = blockIdx.y * NTHREADS + threadIdx.x;
   if (c >= C) return;
@@ -1212,9 +1224,12 @@ __global__ __launch_bounds__(NTHREADS) void tl_t_combine2_kernel(const int* __re
 }
 
 // ``il``: 1 = the streams are stored in the lane-interleaved layout (see tl_stream_il) -> pipeline P = 3.
-struct TLFwdDesc { const int* blk; int nblk; int rbits; const uint32_t* pack; const void* val; int il; TLNarrow nar; };
+// live: optional per-block flags (0 = skip the block: rows of converged entities in a block-diagonal problem)
+struct TLFwdDesc { const int* blk; int nblk; int rbits; const uint32_t* pack; const void* val; int il; TLNarrow nar;
+                  const unsigned char* live; };
 // ptrs: 5 stream pointers per chunk (see tl_fwd_multi_kernel)
-struct TLFwdMultiDesc { const int* blk; int nblk; int rbits; const unsigned long long* ptrs; int il; };
+struct TLFwdMultiDesc { const int* blk; int nblk; int rbits; const unsigned long long* ptrs; int il;
+                       const unsigned char* live; };
 struct TLTDesc {
   const int* items; int nitems; int cbits; const uint32_t* pack; const void* val;
   const int* mt_tiles; const int* mt_ptr; int nmt; int dim;
@@ -1222,12 +1237,16 @@ struct TLTDesc {
   int nparts_total;           // item partial rows (the level-1 rows follow them in the scratch buffer)
   int il;
   TLNarrow nar;
+  const unsigned char* live;      // optional per-item flags (0 = skip) and per-split-tile flags for the combine
+  const unsigned char* live_mt;
 };
 // Shard-wide transpose: items of every chunk (8 ints, see tl_t_multi_kernel) with per-chunk stream pointers.
 struct TLTMultiDesc {
   const int* items; int nitems; int cbits; const unsigned long long* ptrs;
   const int* mt_tiles; const int* mt_ptr; int nmt; int dim;
   const int* cu; int ncu; int nparts_total; int il;
+  const unsigned char* live;
+  const unsigned char* live_mt;
 };
 
 // Runtime TL configuration: accumulator precision for bf16/f32 data (0 = fp32 LDS, 1 = fp64 LDS) and the number
@@ -1250,7 +1269,8 @@ static int g_tl_deep_t = 0;    // interleaved transpose: same
 template <typename VT, typename XT, typename RT, typename AT, int MAXR>
 static void tl_fwd_launch(const TLFwdDesc* c, const void* x, FwdArgs<XT, RT> a, double* stats, hipStream_t st) {
 #define TLF(NW, P) hipLaunchKernelGGL((tl_fwd_kernel<VT, XT, RT, AT, MAXR, 2, NW, P>), dim3(c->nblk), dim3(NW * 64), 0, \
-                                    st, c->blk, c->rbits, c->pack, (const VT*)c->val, c->nar, (const XT*)x, a, stats)
+                                    st, c->blk, c->rbits, c->pack, (const VT*)c->val, c->nar, (const XT*)x, a, stats, \
+                                    c->live)
   if (c->il) {
     if (g_tl_waves <= 2) { if (g_tl_deep == 2) TLF(2, 6); else if (g_tl_deep) TLF(2, 5); else TLF(2, 3); }
     else { if (g_tl_deep == 2) TLF(4, 6); else if (g_tl_deep) TLF(4, 5); else TLF(4, 3); }
@@ -1264,7 +1284,8 @@ template <typename VT, typename XT, typename RT, typename AT, int MAXR>
 static void tl_fwd_multi_launch(const TLFwdMultiDesc* c, const void* x, FwdArgs<XT, RT> a, double* stats,
                                 hipStream_t st) {
 #define TLM(NW, P) hipLaunchKernelGGL((tl_fwd_multi_kernel<VT, XT, RT, AT, MAXR, 2, NW, P>), dim3(c->nblk), \
-                                      dim3(NW * 64), 0, st, c->blk, c->rbits, c->ptrs, (const XT*)x, a, stats)
+                                      dim3(NW * 64), 0, st, c->blk, c->rbits, c->ptrs, (const XT*)x, a, stats, \
+                                      c->live)
   if (c->il) {
     if (g_tl_deep == 2) { if (g_tl_waves == 2) TLM(2, 6); else TLM(4, 6); }
     else if (g_tl_deep) { if (g_tl_waves == 2) TLM(2, 5); else TLM(4, 5); }
@@ -1316,7 +1337,7 @@ template <typename VT, typename XT, typename AT, bool SQ, int MAXR>
 static void tl_t_launch(const TLTDesc* c, const void* x, double* G, double* parts, hipStream_t st) {
 #define TLT(NW, P) hipLaunchKernelGGL((tl_t_kernel<VT, XT, AT, SQ, MAXR, 2, NW, P>), dim3(c->nitems), dim3(NW * 64), 0, \
                                     st, c->items, c->cbits, c->pack, (const VT*)c->val, c->nar, (const XT*)x, G, c->dim, \
-                                    parts)
+                                    parts, c->live)
   if (c->il) {
     if (g_tl_waves_t == 2) { if (g_tl_deep_t == 2) TLT(2, 6); else if (g_tl_deep_t) TLT(2, 5); else TLT(2, 3); }
     else { if (g_tl_deep_t == 2) TLT(4, 6); else if (g_tl_deep_t) TLT(4, 5); else TLT(4, 3); }
@@ -1346,10 +1367,11 @@ static int tl_t_impl(const TLTDesc* c, const void* x, double* G, double* parts, 
   if (c->nmt > 0) {
     const int C = 1 << c->cbits;
     double* l1 = parts + (size_t)c->nparts_total * C;
-    hipLaunchKernelGGL(tl_t_combine1_kernel, dim3(c->ncu), dim3(NTHREADS), 0, st, c->cu, c->cbits, parts, l1);
+    hipLaunchKernelGGL(tl_t_combine1_kernel, dim3(c->ncu), dim3(NTHREADS), 0, st, c->cu, c->cbits, parts, l1,
+                       c->live_mt);
     LAUNCH_CHECK();
     hipLaunchKernelGGL(tl_t_combine2_kernel, dim3(c->nmt, (C + NTHREADS - 1) / NTHREADS), dim3(NTHREADS), 0, st,
-                       c->mt_tiles, c->mt_ptr, c->cbits, l1, G, c->dim);
+                       c->mt_tiles, c->mt_ptr, c->cbits, l1, G, c->dim, c->live_mt);
     LAUNCH_CHECK();
   }
   return 0;
@@ -1359,7 +1381,7 @@ template <typename VT, typename XT, typename AT, bool SQ, int MAXR>
 static void tl_t_multi_launch(const TLTMultiDesc* c, const void* x, double* G, double* parts, hipStream_t st) {
 #define TLTM(NW, P) hipLaunchKernelGGL((tl_t_multi_kernel<VT, XT, AT, SQ, MAXR, 2, NW, P>), dim3(c->nitems), \
                                        dim3(NW * 64), 0, st, c->items, c->cbits, c->ptrs, (const XT*)x, G, \
-                                       c->dim, parts)
+                                       c->dim, parts, c->live)
   if (c->il) {
     if (g_tl_waves_t == 2) { if (g_tl_deep_t == 2) TLTM(2, 6); else if (g_tl_deep_t) TLTM(2, 5); else TLTM(2, 3); }
     else { if (g_tl_deep_t == 2) TLTM(4, 6); else if (g_tl_deep_t) TLTM(4, 5); else TLTM(4, 3); }
@@ -1386,10 +1408,11 @@ static int tl_t_multi_impl(const TLTMultiDesc* c, const void* x, double* G, doub
   if (c->nmt > 0) {
     const int C = 1 << c->cbits;
     double* l1 = parts + (size_t)c->nparts_total * C;
-    hipLaunchKernelGGL(tl_t_combine1_kernel, dim3(c->ncu), dim3(NTHREADS), 0, st, c->cu, c->cbits, parts, l1);
+    hipLaunchKernelGGL(tl_t_combine1_kernel, dim3(c->ncu), dim3(NTHREADS), 0, st, c->cu, c->cbits, parts, l1,
+                       c->live_mt);
     LAUNCH_CHECK();
     hipLaunchKernelGGL(tl_t_combine2_kernel, dim3(c->nmt, (C + NTHREADS - 1) / NTHREADS), dim3(NTHREADS), 0, st,
-                       c->mt_tiles, c->mt_ptr, c->cbits, l1, G, c->dim);
+                       c->mt_tiles, c->mt_ptr, c->cbits, l1, G, c->dim, c->live_mt);
     LAUNCH_CHECK();
   }
   return 0;
@@ -1914,15 +1937,12 @@ __global__ __launch_bounds__(256) void rs_tron_dpp_kernel(
   const long long nn = (long long)n * n;
   bool on[R];
   long long o[R];
-  double y[R], off[R], wt[R], W[R];
+  double W[R];
 #pragma unroll
   for (int s = 0; s < R; ++s) {
     const int e = i + 16 * s;
     on[s] = prob_on && e < n;
     o[s] = b * n + (e < n ? e : 0);
-    y[s] = on[s] ? Y[o[s]] : 0.0;
-    off[s] = on[s] ? O[o[s]] : 0.0;
-    wt[s] = on[s] ? WT[o[s]] : 0.0;
     W[s] = on[s] ? Beta[o[s]] : 0.0;
   }
   // ---- L: registers (row i and column i) or LDS (zero-padded, this wave's P problems)
@@ -2036,12 +2056,15 @@ __global__ __launch_bounds__(256) void rs_tron_dpp_kernel(
     mv(v, z);
 #pragma unroll
     for (int s = 0; s < R; ++s) {
+      // response, offset and weight re-read per evaluation (L2 hits; a few evaluations per solve) instead of
+      // holding 3 R doubles per lane through the CG loop (VGPRs -> occupancy)
+      const double y = on[s] ? Y[o[s]] : 0.0, off = on[s] ? O[o[s]] : 0.0, wt = on[s] ? WT[o[s]] : 0.0;
       double l, dl, d2;
-      pointwise_loss(loss, z[s] + off[s], y[s], l, dl, d2);
+      pointwise_loss(loss, z[s] + off, y, l, dl, d2);
       if (!on[s]) { l = 0.0; dl = 0.0; d2 = 0.0; }
-      lt[s] = wt[s] * l + 0.5 * l2 * v[s] * v[s];
-      cf[s] = wt[s] * dl;
-      Dw[s] = wt[s] * d2;
+      lt[s] = wt * l + 0.5 * l2 * v[s] * v[s];
+      cf[s] = wt * dl;
+      Dw[s] = wt * d2;
     }
     f = gsum(lt);
     mvt(cf, gr);

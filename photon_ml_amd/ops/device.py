@@ -601,10 +601,13 @@ class DeviceGLMData(GLMComputable):
     # ---- entity-masked passes (block-diagonal random-effect problems, optimization/batched.py): the forward
     # skips row blocks and the transpose skips column tiles whose rows / columns all belong to entities that are
     # no longer iterating. Rows and columns are grouped by entity, so a skipped block or tile touches no live
-    # entity's margins or gradient; outputs of skipped rows / columns are left at zero.
+    # entity's margins or gradient; skipped margins come back as zero and skipped gradient columns as zero (or as
+    # whatever the caller's output held: callers read active entities only). The kernels take per-unit live
+    # flags (a workgroup of a dead unit exits at once): one device pass computes every flag, no host sync, no
+    # table rebuild.
     def entity_mask_geometry(self, row_entity: torch.Tensor, col_entity: torch.Tensor):
-        """(first, last) entity of every forward block and of every transpose item of every chunk; False when
-        the layout does not support masked passes."""
+        """(first, last) entity of every forward block and of every transpose item / split tile, concatenated
+        over the chunks (with host-side offsets); False when the layout does not support masked passes."""
         cached = getattr(self, "_mgeo", None)
         if cached is not None:
             return cached
@@ -615,23 +618,28 @@ class DeviceGLMData(GLMComputable):
                 or not self.n_rows):
             return False
         nr, nc = row_entity.numel(), col_entity.numel()
-        span = lambda lo, cnt: (row_entity[lo.clamp(0, nr - 1)], row_entity[(lo + cnt - 1).clamp(0, nr - 1)])
+        rspan = lambda lo, cnt: (row_entity[lo.clamp(0, nr - 1)], row_entity[(lo + cnt - 1).clamp(0, nr - 1)])
         if self._multi is not None:
             blk = self._multi_blk.to(torch.int64)
-            fwd = span(blk[:, 1], blk[:, 2])
+            f0, f1 = rspan(blk[:, 1], blk[:, 2])
+            f_off = [0, int(blk.shape[0])]
         else:                         # per-chunk forward tables {row_lo (chunk-local), nrows, ...}
-            fwd = [span(ch.blk[: ch.nblk, 0].to(torch.int64) + self.row_starts[c], ch.blk[: ch.nblk, 1].to(torch.int64))
-                   for c, ch in enumerate(self.csr)]
-        items = []
+            parts = [rspan(ch.blk[: ch.nblk, 0].to(torch.int64) + self.row_starts[c], ch.blk[: ch.nblk, 1].to(torch.int64))
+                     for c, ch in enumerate(self.csr)]
+            f0 = torch.cat([p[0] for p in parts])
+            f1 = torch.cat([p[1] for p in parts])
+            f_off = np.cumsum([0] + [int(ch.nblk) for ch in self.csr]).tolist()
+        firsts, lasts, i_off, m_off = [], [], [0], [0]
         for c, ch in enumerate(self.csc):
             C = 1 << ch.cbits
             hi = self.col_lo[c] + ch.dim - 1
-            first = lambda t: (self.col_lo[c] + t.to(torch.int64) * C).clamp(0, nc - 1)
-            last = lambda t: torch.clamp(self.col_lo[c] + (t.to(torch.int64) + 1) * C - 1, max=hi).clamp(0, nc - 1)
-            it = ch.items[: ch.nitems, 0]
-            mt = ch.mt_tiles[: ch.nmt]
-            items.append(((col_entity[first(it)], col_entity[last(it)]), (col_entity[first(mt)], col_entity[last(mt)])))
-        self._mgeo = (fwd, items)
+            for t in (ch.items[: ch.nitems, 0].to(torch.int64), ch.mt_tiles[: ch.nmt].to(torch.int64)):
+                firsts.append(col_entity[(self.col_lo[c] + t * C).clamp(0, nc - 1)])
+                lasts.append(col_entity[torch.clamp(self.col_lo[c] + (t + 1) * C - 1, max=hi).clamp(0, nc - 1)])
+            i_off.append(i_off[-1] + int(ch.nitems) + int(ch.nmt))
+            m_off.append(i_off[-2] + int(ch.nitems))          # start of this chunk's split tiles
+        t0, t1 = torch.cat(firsts), torch.cat(lasts)
+        self._mgeo = (f0, f1, f_off, t0, t1, i_off, m_off)
         return self._mgeo
 
     def set_entity_mask(self, active: Optional[torch.Tensor], geometry=None):
@@ -640,55 +648,31 @@ class DeviceGLMData(GLMComputable):
         self._masked = None
         if active is None or not geometry:
             return
-        from .native import TLFwdMultiDesc, TLTDesc
-        fwd, items = geometry
-        cs = torch.zeros(active.numel() + 1, dtype=torch.int64, device=active.device)
-        torch.cumsum(active.to(torch.int64), 0, out=cs[1:])
-        live = lambda rng: (cs[rng[1] + 1] - cs[rng[0]]) > 0
-        if isinstance(fwd, tuple):
-            tab = self._multi_blk[live(fwd)].contiguous()
-            keep = [tab]
-            fdesc = TLFwdMultiDesc(tab.data_ptr(), tab.shape[0], self.csr[0].rbits, self._multi_ptrs.data_ptr(),
-                                   self.csr[0].il)
-            n_blk_kept, n_blk = tab.shape[0], self._multi_blk.shape[0]
+        f0, f1, f_off, t0, t1, i_off, m_off = geometry
+        dup = lambda d: type(d).from_buffer_copy(d)
+        cs = torch.zeros(active.numel() + 1, dtype=torch.int32, device=active.device)
+        torch.cumsum(active.to(torch.int32), 0, out=cs[1:])
+        live_f = ((cs[f1 + 1] - cs[f0]) > 0).to(torch.uint8)
+        live_t = ((cs[t1 + 1] - cs[t0]) > 0).to(torch.uint8)
+        keep = [live_f, live_t]
+        if self._multi is not None:
+            fdesc = dup(self._multi)
+            fdesc.live = live_f.data_ptr()
         else:
-            from .native import TLFwdDesc
-            fdesc, keep, n_blk_kept, n_blk = [], [], 0, 0
-            for ch, rng in zip(self.csr, fwd):
-                tab = ch.blk[: ch.nblk][live(rng)].contiguous()
-                keep.append(tab)
-                fdesc.append(TLFwdDesc(tab.data_ptr(), tab.shape[0], ch.rbits, ch.pack.data_ptr(), ch.val.data_ptr(),
-                                       ch.il, ch.nar))
-                n_blk_kept += tab.shape[0]
-                n_blk += ch.nblk
+            fdesc = []
+            for c, ch in enumerate(self.csr):
+                d = dup(ch.desc)
+                d.live = live_f.data_ptr() + f_off[c]
+                fdesc.append(d)
         tdescs = []
-        for ch, (irng, mrng) in zip(self.csc, items):
-            it = ch.items[: ch.nitems][live(irng)].contiguous()
-            mkeep = live(mrng)
-            cu = ch.cu[: ch.ncu].to(torch.int64)
-            if ch.nmt:
-                newmt = torch.cumsum(mkeep.to(torch.int64), 0) - 1
-                ck = mkeep[cu[:, 0]]
-                cu_new = cu[ck]
-                cu_new[:, 0] = newmt[cu_new[:, 0]]
-                per = (ch.mt_ptr[1: ch.nmt + 1] - ch.mt_ptr[: ch.nmt]).to(torch.int64)[mkeep]
-                mt_ptr = torch.zeros(per.numel() + 1, dtype=torch.int64, device=per.device)
-                torch.cumsum(per, 0, out=mt_ptr[1:])
-                mt_tiles = ch.mt_tiles[: ch.nmt][mkeep].contiguous()
-            else:
-                cu_new, mt_ptr, mt_tiles = cu[:0], torch.zeros(1, dtype=torch.int64, device=cu.device), ch.mt_tiles
-            cu_new = cu_new.to(torch.int32).contiguous()
-            mt_ptr = mt_ptr.to(torch.int32).contiguous()
-            nmt = int(mt_tiles.numel()) if ch.nmt else 0
-            d = TLTDesc(it.data_ptr(), it.shape[0], ch.cbits, ch.pack.data_ptr(), ch.val.data_ptr(),
-                        mt_tiles.data_ptr(), mt_ptr.data_ptr(), nmt, ch.dim, cu_new.data_ptr(), cu_new.shape[0],
-                        ch.nparts, ch.il, ch.nar)
-            keep += [it, cu_new, mt_ptr, mt_tiles]
+        for c, ch in enumerate(self.csc):
+            d = dup(ch.desc)
+            d.live = live_t.data_ptr() + i_off[c]
+            d.live_mt = live_t.data_ptr() + m_off[c + 1]
             tdescs.append(d)
         self._masked = (fdesc, tdescs, keep)
         if MASK_STATS is not None:
-            n_it = sum(int(ch.nitems) for ch in self.csc)
-            MASK_STATS.append((n_blk_kept / max(1, n_blk), sum(int(d.nitems) for d in tdescs) / max(1, n_it)))
+            MASK_STATS.append((float(live_f.float().mean()), float(live_t.float().mean())))
 
     # ---- gradient buckets: the transpose split into column-tile ranges so each range's all-reduce can start as
     # soon as that range is final (overlap of the C1 collective with the rest of the transpose pass)

@@ -38,18 +38,19 @@ class TLNarrow(ctypes.Structure):
 
 class TLFwdDesc(ctypes.Structure):
     _fields_ = [("blk", c_void_p), ("nblk", c_int), ("rbits", c_int), ("pack", c_void_p), ("val", c_void_p),
-                ("il", c_int), ("nar", TLNarrow)]
+                ("il", c_int), ("nar", TLNarrow), ("live", c_void_p)]
 
 
 class TLFwdMultiDesc(ctypes.Structure):
     """``ptrs``: 5 stream pointers per chunk {pack, val, narrow pack, narrow val, narrow base}."""
-    _fields_ = [("blk", c_void_p), ("nblk", c_int), ("rbits", c_int), ("ptrs", c_void_p), ("il", c_int)]
+    _fields_ = [("blk", c_void_p), ("nblk", c_int), ("rbits", c_int), ("ptrs", c_void_p), ("il", c_int),
+                ("live", c_void_p)]
 
 
 class TLTMultiDesc(ctypes.Structure):
     _fields_ = [("items", c_void_p), ("nitems", c_int), ("cbits", c_int), ("ptrs", c_void_p),
                 ("mt_tiles", c_void_p), ("mt_ptr", c_void_p), ("nmt", c_int), ("dim", c_int), ("cu", c_void_p),
-                ("ncu", c_int), ("nparts_total", c_int), ("il", c_int)]
+                ("ncu", c_int), ("nparts_total", c_int), ("il", c_int), ("live", c_void_p), ("live_mt", c_void_p)]
 
 
 class TLTDesc(ctypes.Structure):
@@ -57,6 +58,7 @@ class TLTDesc(ctypes.Structure):
         ("items", c_void_p), ("nitems", c_int), ("cbits", c_int), ("pack", c_void_p), ("val", c_void_p),
         ("mt_tiles", c_void_p), ("mt_ptr", c_void_p), ("nmt", c_int), ("dim", c_int),
         ("cu", c_void_p), ("ncu", c_int), ("nparts_total", c_int), ("il", c_int), ("nar", TLNarrow),
+        ("live", c_void_p), ("live_mt", c_void_p),
     ]
 
 

@@ -174,8 +174,8 @@ class SegmentedGLMData:
 
     def _set_active(self, active):
         """Entity-masked GLM passes (``DeviceGLMData.set_entity_mask``): blocks / tiles of entities outside
-        ``active`` are skipped; their margins and gradient entries come back as zero (the callers only read the
-        active entities). The filtered tables are rebuilt only when the active set changed."""
+        ``active`` are skipped; their margins and gradient entries are not computed (the callers only read the
+        active entities)."""
         glm = self.glm
         if not MASKED_PASSES or not hasattr(glm, "entity_mask_geometry"):
             return
@@ -187,11 +187,8 @@ class SegmentedGLMData:
         geo = glm.entity_mask_geometry(self.row_entity, self.col_entity)
         if not geo:
             return
-        key = getattr(self, "_active_key", None)
-        if key is not None and key.shape == active.shape and bool(torch.equal(key, active)):
-            return
-        glm.set_entity_mask(active, geo)
-        self._active_key = active.clone()
+        glm.set_entity_mask(active, geo)           # a few device ops, no host synchronisation
+        self._active_key = True
 
     def margins(self, W, active=None):
         self._set_active(active)
@@ -212,11 +209,13 @@ class SegmentedGLMData:
         # storage cannot be recycled under the key); no O(D) comparison / copy per Hessian-vector product
         key = self._dzz_key
         mk = getattr(self, "_active_key", None)
+        # a cache filled under an entity mask covers that mask's entities; inside batched_tron every later mask
+        # at the same W is a subset (CG masks shrink, rejected steps keep W, the active set only shrinks)
         if (key is not None and key[0] is W and key[1] == W._version and key[2] is loss
-                and (key[3] is None or (mk is not None and bool((mk <= key[3]).all())))):
+                and (key[3] is None or mk is not None)):
             return self._dzz
         self._dzz = self.w * loss.dzz(self.glm.matvec(W) + self.o, self.y)
-        self._dzz_key = (W, W._version, loss, None if mk is None else mk.clone())
+        self._dzz_key = (W, W._version, loss, None if mk is None else True)
         return self._dzz
 
     def hv(self, loss, W, V, l2: float, active=None):

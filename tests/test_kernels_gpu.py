@@ -562,5 +562,10 @@ def test_scoring_reuses_cached_margins(precision):
     cached = data.margins(w1)
     data._z_key = None
     fresh = data.margins(w1)
-    torch.testing.assert_close(cached, fresh, rtol=1e-12, atol=1e-12)
+    if precision == "f64":
+        torch.testing.assert_close(cached, fresh, rtol=1e-12, atol=1e-12)
+    else:
+        # fp32 coefficient vector: z(w) + t z(d) vs z(fp32(w + t d)) differ by the rounding of w (what the margin-space
+        # line search itself works with)
+        torch.testing.assert_close(cached, fresh, rtol=0, atol=1e-6 * float(fresh.abs().max()))
     assert data.n_passes == n0
