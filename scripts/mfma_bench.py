@@ -23,7 +23,7 @@ for M, N, K in ((20000, 4096, 128), (4096, 4096, 1024)):
         gemm_nt(A, B)
     torch.cuda.synchronize()
     ms = (time.perf_counter() - t) / 5 * 1e3
-    print(f"gemm_nt {M}x{N}x{K}: {ms:.3f} ms, {2 * M * N * K / ms / 1e9:.1f} GFLOP/s fp64, rel err {err:.1e}", flush=True)
+    print(f"gemm_nt {M}x{N}x{K}: {ms:.3f} ms, {2 * M * N * K / ms / 1e9:.1f} TFLOP/s fp64, rel err {err:.1e}", flush=True)
 for B_, n, m in ((100000, 20, 64), (20000, 64, 256)):
     A = torch.randn(B_, n, m, dtype=torch.float64, device="cuda", generator=g)
     K = batched_gram(A)
@@ -35,5 +35,5 @@ for B_, n, m in ((100000, 20, 64), (20000, 64, 256)):
         batched_gram(A)
     torch.cuda.synchronize()
     ms = (time.perf_counter() - t) / 5 * 1e3
-    print(f"bgram {B_}x{n}x{m}: {ms:.3f} ms, {2 * B_ * n * n * m / ms / 1e9:.1f} GFLOP/s fp64, rel err {err:.1e}",
+    print(f"bgram {B_}x{n}x{m}: {ms:.3f} ms, {2 * B_ * n * n * m / ms / 1e9:.1f} TFLOP/s fp64, rel err {err:.1e}",
           flush=True)
