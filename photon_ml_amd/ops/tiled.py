@@ -34,6 +34,7 @@ of more than 2^27 rows) fall back to the segmented-stream layout (:mod:`photon_m
 """
 from __future__ import annotations
 
+import math
 import os
 from typing import Optional, Sequence, Tuple
 
@@ -49,7 +50,14 @@ DEFAULT_RBITS = int(os.environ.get("PML_TL_RBITS", 10))
 DEFAULT_CBITS = int(os.environ.get("PML_TL_CBITS", 10))
 DEFAULT_ITEM_ENTRIES = 1 << 17  # measured (16M rows, interleaved): 64K 2.87 ms, 128K 2.73, 256K 2.70 transpose
 _PAD = 8                 # kernels read 4-entry quads; pad so that the last quad stays in bounds
-COMBINE_SEG = 16         # partial rows summed per level-1 combine work-group
+COMBINE_SEG = 16         # minimum partial rows summed per level-1 combine work-group
+
+
+def combine_seg(k: int) -> int:
+    """Partial rows per level-1 combine unit of a tile split into ``k`` items: ~sqrt(k) (at least COMBINE_SEG), so
+    neither level loops over more than ~sqrt(k) rows per thread. A hot tile of a 125M-row shard has ~47K items:
+    fixed 16-row units left its level-2 sum a 2.9K-long serial chain per thread (1 ms per pass, measured)."""
+    return max(COMBINE_SEG, int(math.ceil(math.sqrt(k))))
 IL_ROUND = 256           # entries per wave-round of the kernels (64 lanes x 4-entry quads)
 TL_VEC = 4               # entries per lane per round
 INTERLEAVE = int(os.environ.get("PML_TL_IL", "1"))
@@ -348,8 +356,9 @@ class TLTChunk(_NarrowMixin):
                 items.append((t, cuts[i], cuts[i + 1], -1 if k == 1 else part + i))
             if k > 1:
                 # level-1 combine units of <= COMBINE_SEG consecutive partial rows of this tile
-                for s0 in range(part, part + k, COMBINE_SEG):
-                    cu.append((len(mt_tiles), s0, min(part + k, s0 + COMBINE_SEG)))
+                sg = combine_seg(k)
+                for s0 in range(part, part + k, sg):
+                    cu.append((len(mt_tiles), s0, min(part + k, s0 + sg)))
                 part += k
                 mt_tiles.append(t)
                 mt_ptr.append(len(cu))
@@ -460,10 +469,11 @@ class TLTMulti:
         # level-1 units of <= COMBINE_SEG consecutive partial rows per split tile
         km = k[k > 1]
         plo = np.cumsum(km) - km
-        nu = -(-km // COMBINE_SEG)
+        sg = np.maximum(COMBINE_SEG, np.ceil(np.sqrt(km)).astype(np.int64)) if len(km) else km
+        nu = -(-km // sg)
         u_tile = np.repeat(np.arange(len(km)), nu)
-        u_first = np.repeat(plo, nu) + COMBINE_SEG * (np.arange(int(nu.sum())) - np.repeat(np.cumsum(nu) - nu, nu))
-        u_last = np.minimum(u_first + COMBINE_SEG, np.repeat(plo + km, nu))
+        u_first = np.repeat(plo, nu) + np.repeat(sg, nu) * (np.arange(int(nu.sum())) - np.repeat(np.cumsum(nu) - nu, nu))
+        u_last = np.minimum(u_first + np.repeat(sg, nu), np.repeat(plo + km, nu))
         self.nitems, self.nparts, self.ncu, self.nmt = n, int(km.sum()), int(nu.sum()), len(km)
         rows = np.column_stack([it[:, 0], it[:, 1], it[:, 2], it[:, 3], part, it[:, 4], it[:, 5],
                                 it[:, 6]]).astype(np.int32)

@@ -89,7 +89,7 @@ def test_device_data_construction_cpu(layout):
 def test_tl_shard_wide_transpose_emulation(chunk, item, hot):
     """Shard-wide transpose tables (all chunks in one launch): every entry once, split tiles combined in
     (chunk, item) order, single-item tiles direct; result == X^T r."""
-    from photon_ml_amd.ops.tiled import COMBINE_SEG, TLTMulti
+    from photon_ml_amd.ops.tiled import TLTMulti, combine_seg
     rng = np.random.default_rng(3)
     m, d = 5000, 3000
     x = sp.random(m, d, density=0.01, format="lil", random_state=2)
@@ -117,7 +117,9 @@ def test_tl_shard_wide_transpose_emulation(chunk, item, hot):
     single = set(tiles[cnt == 1].tolist())
     assert all((row[4] < 0) == (row[1] in single) for row in it)
     cu = mt.cu.numpy()[: mt.ncu]
-    assert (cu[:, 2] - cu[:, 1] <= COMBINE_SEG).all() and mt.mt_ptr.numpy()[-1] == mt.ncu
+    k_of_unit = np.bincount(it[it[:, 4] >= 0, 1])[mt.mt_tiles.numpy()[cu[:, 0]]]
+    assert (cu[:, 2] - cu[:, 1] <= np.array([combine_seg(int(k)) for k in k_of_unit])).all()
+    assert mt.mt_ptr.numpy()[-1] == mt.ncu
 
 
 @pytest.mark.parametrize("il", [0, 1])
