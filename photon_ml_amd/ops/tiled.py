@@ -53,6 +53,28 @@ _PAD = 8                 # kernels read 4-entry quads; pad so that the last quad
 COMBINE_SEG = 16         # minimum partial rows summed per level-1 combine work-group
 
 
+# XCD-aware item order of the shard-wide transpose (PML_TL_XCD=8 turns it on). Work-groups are dispatched
+# round-robin over the 8 XCDs by blockIdx, each XCD has its own 4 MB L2, and an item gathers the per-row vector of
+# ITS chunk (1M rows x 4 B): interleaving 8 streams (chunks c = k mod 8 in stream k) makes the blocks that share
+# an XCD walk one chunk at a time. Pure scheduling (bitwise-identical results) -- but MEASURED SLOWER on the
+# headline bench (40.0-40.1 vs 39.2 ms/step, profiles/bench_xcd_order_ab.md), so the default is the plain
+# chunk-major order, in which all XCDs share the few in-flight chunks.
+XCD_GROUPS = int(os.environ.get("PML_TL_XCD", "0"))
+
+
+def xcd_order(chunk_of_item: np.ndarray, groups: int) -> np.ndarray:
+    """Permutation of items (chunk-major input order kept inside each stream) such that position b holds an
+    item of stream b % groups while every stream has items left."""
+    stream = np.asarray(chunk_of_item) % groups
+    lists = [np.flatnonzero(stream == k) for k in range(groups)]
+    longest = max(len(l) for l in lists)
+    grid = np.full((longest, groups), -1, dtype=np.int64)
+    for k, l in enumerate(lists):
+        grid[: len(l), k] = l
+    order = grid.reshape(-1)
+    return order[order >= 0]
+
+
 def combine_seg(k: int) -> int:
     """Partial rows per level-1 combine unit of a tile split into ``k`` items: ~sqrt(k) (at least COMBINE_SEG), so
     neither level loops over more than ~sqrt(k) rows per thread. A hot tile of a 125M-row shard has ~47K items:
@@ -477,6 +499,8 @@ class TLTMulti:
         self.nitems, self.nparts, self.ncu, self.nmt = n, int(km.sum()), int(nu.sum()), len(km)
         rows = np.column_stack([it[:, 0], it[:, 1], it[:, 2], it[:, 3], part, it[:, 4], it[:, 5],
                                 it[:, 6]]).astype(np.int32)
+        if XCD_GROUPS > 1 and n > XCD_GROUPS:
+            rows = rows[xcd_order(it[:, 0], XCD_GROUPS)]
         self.items = torch.tensor(rows.reshape(-1, 8), device=dev)
         self.mt_tiles = torch.tensor(np.r_[ts[starts][k > 1], 0].astype(np.int32)[: max(self.nmt, 1)], device=dev)
         self.mt_ptr = torch.tensor(np.r_[0, np.cumsum(nu)].astype(np.int32), device=dev)
