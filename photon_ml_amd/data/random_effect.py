@@ -135,7 +135,13 @@ class RandomEffectDataset:
         self.dim = x.shape[1]
         ids = data.id_tags[re_type]
         ids_s = ids.astype(str) if ids.dtype == object else ids
-        self.entity_ids, ent = np.unique(ids_s, return_inverse=True)
+        if self.device.type == "cuda" and np.issubdtype(ids_s.dtype, np.integer) and len(ids_s):
+            # integer entity ids: sorted unique + inverse on the device (np.unique: 1.3 s at 25M rows)
+            u, inv = torch.unique(torch.from_numpy(np.ascontiguousarray(ids_s)).to(self.device), sorted=True,
+                                  return_inverse=True)
+            self.entity_ids, ent = u.cpu().numpy().astype(ids_s.dtype, copy=False), inv.cpu().numpy()
+        else:
+            self.entity_ids, ent = np.unique(ids_s, return_inverse=True)
         n_ent = len(self.entity_ids)
         n = data.n_rows
         self.n_rows = n

@@ -243,6 +243,9 @@ class DeviceGLMData(GLMComputable):
         dev = torch.device(device)
         x = data.x.tocsr()
         n, d = x.shape
+        if dev.type == "cuda" and n and resolve_layout(layout, d, chunk_rows) == "tiled":
+            return DeviceGLMData._from_labeled_device(x, data, dev, precision, chunk_rows, relabel, item_entries,
+                                                      col_windows)
         old_of_new = None
         from ..parallel.dist import is_dist
         shared = relabel and is_dist() and not col_windows
@@ -300,6 +303,40 @@ class DeviceGLMData(GLMComputable):
         out = DeviceGLMData(csr, csc, starts, torch.from_numpy(data.y), torch.from_numpy(data.offsets),
                             torch.from_numpy(data.weights), d, precision, dev, old_of_new)
         out.col_lo = col_lo
+        return out
+
+    @staticmethod
+    def _from_labeled_device(x, data: LabeledData, dev, precision: str, chunk_rows: int, relabel: bool,
+                             item_entries: Optional[int], col_windows: bool):
+        """Tiled shard from a host CSR: the arrays are uploaded once and the feature counts, the hottest-first
+        relabel, the chunking, the column windows and the layout sorts all run on the device (the host path sliced
+        the CSR per chunk with scipy: 6.7 of 14.6 s at GAME config 5)."""
+        n, d = x.shape
+        indptr = torch.from_numpy(np.ascontiguousarray(x.indptr, dtype=np.int64)).to(dev)
+        col = torch.from_numpy(np.ascontiguousarray(x.indices)).to(dev).to(torch.int64)
+        val = torch.from_numpy(np.ascontiguousarray(x.data)).to(dev)
+        old_of_new = None
+        from ..parallel.dist import is_dist
+        shared = relabel and is_dist() and not col_windows
+        if shared or (relabel and col.numel() > 0):
+            counts = torch.bincount(col, minlength=d)
+            if shared:
+                import torch.distributed as tdist
+                from ..parallel.sharding import comm_device
+                ct = counts.to(comm_device())
+                tdist.all_reduce(ct)
+                counts = ct.to(dev)
+            oon = torch.argsort(-counts, stable=True)
+            non = torch.empty_like(oon)
+            non[oon] = torch.arange(d, device=dev)
+            col = non[col]
+            old_of_new = (oon, non)
+            del counts
+        out = DeviceGLMData.from_device_csr(indptr, col, val, torch.from_numpy(data.y), torch.from_numpy(data.offsets),
+                                            torch.from_numpy(data.weights), d, dev, precision, chunk_rows,
+                                            item_entries=item_entries, col_windows=col_windows)
+        if old_of_new is not None:
+            out.old_of_new, out.new_of_old = old_of_new
         return out
 
     @staticmethod

@@ -369,23 +369,28 @@ class TLTChunk(_NarrowMixin):
         tptr = np.concatenate([[0], np.cumsum(counts)])
         nz = np.nonzero(counts)[0]
         n_it = np.maximum(1, -(-counts[nz] // item_entries))
-        items, mt_tiles, mt_ptr, cu = [], [], [0], []
-        part = 0
-        for t, k in zip(nz.tolist(), n_it.tolist()):
-            a, b = int(tptr[t]), int(tptr[t + 1])
-            cuts = [a + (b - a) * i // k for i in range(k + 1)]
-            for i in range(k):
-                items.append((t, cuts[i], cuts[i + 1], -1 if k == 1 else part + i))
-            if k > 1:
-                # level-1 combine units of <= COMBINE_SEG consecutive partial rows of this tile
-                sg = combine_seg(k)
-                for s0 in range(part, part + k, sg):
-                    cu.append((len(mt_tiles), s0, min(part + k, s0 + sg)))
-                part += k
-                mt_tiles.append(t)
-                mt_ptr.append(len(cu))
-        self.nitems, self.nmt, self.nparts, self.ncu = len(items), len(mt_tiles), part, len(cu)
-        items = np.asarray(items, dtype=np.int64).reshape(-1, 4)
+        # items of every non-empty tile, vectorised: item i of a tile of k items covers [a + (b-a) i / k, ...)
+        it_tile = np.repeat(nz, n_it)
+        it_i = np.arange(len(it_tile)) - np.repeat(np.cumsum(n_it) - n_it, n_it)
+        it_k = np.repeat(n_it, n_it)
+        a, b = tptr[it_tile], tptr[it_tile + 1]
+        lo, hi = a + (b - a) * it_i // it_k, a + (b - a) * (it_i + 1) // it_k
+        split = it_k > 1
+        part_of = np.full(len(it_tile), -1, np.int64)
+        part_of[split] = np.arange(int(split.sum()))
+        # level-1 combine units of ~sqrt(k) consecutive partial rows per split tile (combine_seg)
+        km = n_it[n_it > 1]
+        plo = np.cumsum(km) - km
+        sg = np.maximum(COMBINE_SEG, np.ceil(np.sqrt(km)).astype(np.int64)) if len(km) else km
+        nu = -(-km // sg)
+        u_mt = np.repeat(np.arange(len(km)), nu)
+        u_first = np.repeat(plo, nu) + np.repeat(sg, nu) * (np.arange(int(nu.sum())) - np.repeat(np.cumsum(nu) - nu, nu))
+        u_last = np.minimum(u_first + np.repeat(sg, nu), np.repeat(plo + km, nu))
+        cu = np.column_stack([u_mt, u_first, u_last]) if len(km) else np.zeros((0, 3), np.int64)
+        mt_tiles = nz[n_it > 1].tolist()
+        mt_ptr = np.r_[0, np.cumsum(nu)].tolist() if len(km) else [0]
+        self.nitems, self.nmt, self.nparts, self.ncu = len(it_tile), len(mt_tiles), int(km.sum()), len(cu)
+        items = np.column_stack([it_tile, lo, hi, part_of]).astype(np.int64).reshape(-1, 4)
         items = np.column_stack([items, np.zeros((len(items), 2), np.int64)])
         self._sbits, self._ew = self.cbits, (1, 2)
         if self.il:
@@ -407,7 +412,7 @@ class TLTChunk(_NarrowMixin):
         self.items = torch.tensor(items.astype(np.int32), device=dev)
         self.mt_tiles = torch.tensor(np.asarray(mt_tiles or [0], dtype=np.int32), device=dev)
         self.mt_ptr = torch.tensor(np.asarray(mt_ptr, dtype=np.int32), device=dev)
-        self.cu = torch.tensor(np.asarray(cu or [(0, 0, 0)], dtype=np.int32).reshape(-1, 3), device=dev)
+        self.cu = torch.tensor(np.asarray(cu if len(cu) else [(0, 0, 0)], dtype=np.int32).reshape(-1, 3), device=dev)
         self.m, self.nnz, self.dim = m, nnz, dim
         self.desc = TLTDesc(self.items.data_ptr(), self.nitems, self.cbits, self.pack.data_ptr(),
                             self.val.data_ptr(), self.mt_tiles.data_ptr(), self.mt_ptr.data_ptr(), self.nmt, dim,
