@@ -48,20 +48,28 @@ def _sync(t):
 
 def random_effect_tracker_stats(iters: torch.Tensor, reasons: torch.Tensor, seconds: float) -> dict:
     """RandomEffectOptimizationTracker (photon-api/.../RandomEffectOptimizationTracker.scala:100-150): counts of
-    convergence reasons and iteration statistics over the entities of one update."""
+    convergence reasons and iteration statistics over the entities of one update. Reduced where the tensors live
+    (the device): one small transfer of scalars instead of the per-entity arrays."""
     from ..optimization.batched import REASON_CODES
-    it = iters.detach().double().cpu()
-    rc = reasons.detach().cpu()
+    it = iters.detach().to(torch.float64)
+    rc = reasons.detach().to(torch.int64)
+    n = it.numel()
+    if n == 0:
+        return {"entities": 0, "mean_iterations": 0.0, "std_iterations": 0.0, "max_iterations": 0,
+                "min_iterations": 0, "convergence_reasons": {}, "seconds": seconds}
+    codes = sorted(REASON_CODES)
+    hist = torch.stack([(rc == c).sum() for c in codes]).to(torch.float64)
+    vals = torch.cat([torch.stack([it.mean(), it.std() if n > 1 else torch.zeros((), dtype=torch.float64,
+                                                                                 device=it.device),
+                                   it.max(), it.min()]), hist]).cpu().tolist()
     counts = {}
-    for code, reason in REASON_CODES.items():
-        n = int((rc == code).sum())
-        if n:
-            counts["not converged" if reason is None else reason.value] = n
-    return {"entities": int(it.numel()), "mean_iterations": float(it.mean()) if it.numel() else 0.0,
-            "std_iterations": float(it.std()) if it.numel() > 1 else 0.0,
-            "max_iterations": int(it.max()) if it.numel() else 0,
-            "min_iterations": int(it.min()) if it.numel() else 0,
-            "convergence_reasons": counts, "seconds": seconds}
+    for code, cnt in zip(codes, vals[4:]):
+        if cnt:
+            reason = REASON_CODES[code]
+            counts["not converged" if reason is None else reason.value] = int(cnt)
+    return {"entities": int(n), "mean_iterations": float(vals[0]), "std_iterations": float(vals[1]),
+            "max_iterations": int(vals[2]), "min_iterations": int(vals[3]), "convergence_reasons": counts,
+            "seconds": seconds}
 
 
 class Coordinate:
@@ -375,7 +383,7 @@ class RandomEffectCoordinate(Coordinate):
             self._W["seg"] = _RS_WARM
             n_iter = torch.zeros(seg.B, dtype=torch.long, device=beta.device).index_copy(0, rs.ents, rres.iters)
             n_reason = torch.zeros(seg.B, dtype=torch.long, device=beta.device).index_copy(0, rs.ents, rres.reason)
-            act = torch.from_numpy(ds.n_active > 0).to(n_iter.device)
+            act = self._active_mask(n_iter.device)
             self.last_stats = random_effect_tracker_stats(n_iter[act], n_reason[act], time.time() - t_start)
             sum_sq = float(torch.linalg.vector_norm(torch.where(rs.valid, beta, torch.zeros_like(beta)))) ** 2
             out = RandomEffectModel(self.data_config.random_effect_type, self.data_config.feature_shard_id, self.task,
@@ -393,7 +401,7 @@ class RandomEffectCoordinate(Coordinate):
             reasons = reasons.index_copy(0, rs.ents, rres.reason)
         res = BatchedResult(W_all, None, iters, reasons)
         self._W["seg"] = res.W
-        act = torch.from_numpy(ds.n_active > 0).to(res.iters.device)
+        act = self._active_mask(res.iters.device)
         self.last_stats = random_effect_tracker_stats(res.iters[act], res.reason[act], time.time() - t_start)
         W = res.W.detach()
         var = None
@@ -406,6 +414,14 @@ class RandomEffectCoordinate(Coordinate):
                                 ds.entity_ids, ds.dim, ds.projection_keys_t, W, var)
         self._last = (out, res.W)
         return out
+
+    def _active_mask(self, device) -> torch.Tensor:
+        """Entities with active data (bool, on ``device``; uploaded once)."""
+        m = getattr(self, "_act_mask", None)
+        if m is None or m.device != torch.device(device):
+            m = torch.from_numpy(self.dataset.n_active > 0).to(device)
+            self._act_mask = m
+        return m
 
     def _primal_subset(self, frozen: torch.Tensor):
         """Sub-problem of the entities outside the row-space batch (built once per row-space batch; the kept
