@@ -48,7 +48,7 @@ TL_MAXBITS_F64 = 11      # fp64 LDS accumulators: 4 waves x 2048 x 8 B = 64 KB
 TL_MINBITS = 5
 DEFAULT_RBITS = int(os.environ.get("PML_TL_RBITS", 10))
 DEFAULT_CBITS = int(os.environ.get("PML_TL_CBITS", 10))
-DEFAULT_ITEM_ENTRIES = 1 << 17  # measured (16M rows, interleaved): 64K 2.87 ms, 128K 2.73, 256K 2.70 transpose
+DEFAULT_ITEM_ENTRIES = 1 << 18  # 125M rows (profiles/bench_knob_sweep.md): 64K 40.41, 128K 38.71-39.10, 256K 38.43-38.51, 512K 38.58, 1M 38.63 ms/step
 _PAD = 8                 # kernels read 4-entry quads; pad so that the last quad stays in bounds
 COMBINE_SEG = 16         # minimum partial rows summed per level-1 combine work-group
 
