@@ -145,8 +145,14 @@ class FixedEffectCoordinate(Coordinate):
         self.glm_data.set_offsets(off)
         if self.sampler is not None:
             self._apply_down_sampling()
+        gd = self.glm_data
+        n0 = (getattr(gd, "n_fwd", 0), getattr(gd, "n_t", 0))
         glm = self.problem.run(self._data_view(), model.glm if model is not None else None, dim=self.dim)
         self.last_tracker = self.problem.tracker
+        if log.isEnabledFor(logging.DEBUG) and hasattr(gd, "n_passes"):
+            log.debug("FE %s: %d forward + %d transpose passes in the update (%s iterations)", self.coordinate_id,
+                      getattr(gd, "n_fwd", 0) - n0[0], getattr(gd, "n_t", 0) - n0[1],
+                      getattr(self.last_tracker, "iterations", "?"))
         # restore full weights for scoring/evaluation
         if self.sampler is not None:
             self._restore_weights()

@@ -607,6 +607,7 @@ class DeviceGLMData(GLMComputable):
         """Forward pass over every chunk: one launch in the tiled layout (``KERNEL_CONFIG['tl_multi']``),
         else one launch per chunk."""
         from .native import KERNEL_CONFIG
+        self.n_fwd = getattr(self, "n_fwd", 0) + 1
         if getattr(self, "_multi", "unset") == "unset":
             self._build_multi()
         if self._multi is not None and KERNEL_CONFIG.get("tl_multi", 1):
@@ -625,6 +626,7 @@ class DeviceGLMData(GLMComputable):
         """Transpose pass over every chunk: one launch + one shard-wide combine in the tiled layout
         (``KERNEL_CONFIG['tl_multi']``), else per chunk."""
         from .native import KERNEL_CONFIG
+        self.n_t = getattr(self, "n_t", 0) + 1
         if getattr(self, "_multi_t", "unset") == "unset":
             self._build_multi_t()
         if self._multi_t is not None and KERNEL_CONFIG.get("tl_multi", 1):
@@ -745,6 +747,7 @@ class DeviceGLMData(GLMComputable):
         return out
 
     def _packed_bucketed(self, x, G, start_reduce, nb: int, square: int = 0):
+        self.n_t = getattr(self, "n_t", 0) + 1
         for mt, c0, c1 in self.grad_buckets(nb):
             check(self.lib.pml_tl_t_multi(self.prec, ctypes.byref(mt.desc), x.data_ptr(), square, G.data_ptr(),
                                           self.parts.data_ptr(), stream_handle(self.device)), "tl_t_multi")
@@ -757,6 +760,12 @@ class DeviceGLMData(GLMComputable):
         which must share the permutation — then applies :meth:`_unperm`. Bitwise equal to the one-launch pass."""
         with trace_range("K1 value+grad pass (bucketed)"):
             out = torch.zeros(self.dim + 2, dtype=torch.float64, device=self.device)
+            if self._zero_point(loss, w_eff):
+                self._zero_coef(loss, margin_shift, out[self.dim:])
+                start_reduce(out[self.dim:])
+                self._packed_bucketed(self.coef, out[: self.dim], start_reduce, nb)
+                self.n_passes += 1
+                return out
             x = self._vec(w_eff)
             dzz = self.dzz if (self.track_hessian and loss.twice_differentiable) else None
             zc = getattr(self, "z_cache", None)
@@ -820,9 +829,36 @@ class DeviceGLMData(GLMComputable):
         with trace_range("K1 value+grad pass"):
             return self._value_grad_packed(loss, w_eff, margin_shift)
 
+    def _zero_point(self, loss, w_eff) -> bool:
+        """``w_eff`` is the optimizer's all-zero tolerance point (tagged by Optimizer.start): margins = offsets."""
+        return bool(getattr(w_eff, "_pml_zero", False)) and not (self.track_hessian and loss.twice_differentiable)
+
+    def _zero_coef(self, loss, margin_shift, stats_out: torch.Tensor):
+        """coef = w l'(o + shift) and (F, S) at w = 0 by one elementwise pass (``ls_eval_kernel`` at t = 0): the
+        forward pass over the non-zeros would only add zeros to the offsets. The reference evaluates this point to
+        set its tolerances (Optimizer.scala, Appendix C.7)."""
+        n = self.n_rows
+        z0 = self.o[:n].to(torch.float64) + float(margin_shift)
+        check(self.lib.pml_ls_eval(self.prec, n, 0.0, loss.loss_id, z0.data_ptr(), z0.data_ptr(), self.y.data_ptr(),
+                                   self.wt.data_ptr(), 1, self.coef.data_ptr(), None, self.ls_stats_buf().data_ptr(),
+                                   stats_out.data_ptr(), stream_handle(self.device)), "ls_eval(zero)")
+
+    def ls_stats_buf(self) -> torch.Tensor:
+        buf = getattr(self, "ls_stats", None)
+        if buf is None:
+            self.ls_stats = buf = torch.zeros(2 * 1024, dtype=torch.float64, device=self.device)
+        return buf
+
     def _value_grad_packed(self, loss, w_eff, margin_shift) -> torch.Tensor:
         out = torch.zeros(self.dim + 2, dtype=torch.float64, device=self.device)
         G = out[: self.dim]
+        if self._zero_point(loss, w_eff):
+            self._zero_coef(loss, margin_shift, out[self.dim:])
+            self.t_all(self.coef, G)
+            if self.old_of_new is not None:
+                out[: self.dim] = self._unperm(G.clone())
+            self.n_passes += 1
+            return out
         x = self._vec(w_eff)
         dzz = self.dzz if (self.track_hessian and loss.twice_differentiable) else None
         zc = getattr(self, "z_cache", None)

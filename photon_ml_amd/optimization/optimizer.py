@@ -164,11 +164,15 @@ class Optimizer:
         """Set tolerances and the initial state (first half of ``Optimizer.optimize``)."""
         w0 = self.normalization.model_to_transformed_space(initial.to(torch.float64))
         self.clear_inner_state()
+        zero_state = None
+        if not (skip_zero_tolerance_pass and vector_space.current().all_zero(w0)):
+            # the zero point first, so the data's margin cache ends at w0 (the first line search then needs no
+            # extra forward pass); tagged so a data backend can evaluate it without a pass over the non-zeros
+            z = torch.zeros_like(w0)
+            z._pml_zero = True
+            zero_state = self._calculate_state(objective, data, z)
         init_state = self._calculate_state(objective, data, w0)
-        if skip_zero_tolerance_pass and vector_space.current().all_zero(w0):
-            self._set_abs_tolerances(init_state)
-        else:
-            self._set_abs_tolerances(self._calculate_state(objective, data, torch.zeros_like(w0)))
+        self._set_abs_tolerances(init_state if zero_state is None else zero_state)
         self._init(objective, data, init_state)
         self._update_current(init_state)
         return init_state

@@ -569,3 +569,23 @@ def test_scoring_reuses_cached_margins(precision):
         # line search itself works with)
         torch.testing.assert_close(cached, fresh, rtol=0, atol=1e-6 * float(fresh.abs().max()))
     assert data.n_passes == n0
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("precision", ["f64", "bf16"])
+def test_zero_point_evaluation_without_forward_pass(precision):
+    """The optimizer's tolerance point w = 0 (tagged by Optimizer.start) is evaluated from the offsets by one
+    elementwise pass + the transpose pass: same gradient bit for bit, same (F, S) to rounding, no forward pass."""
+    from photon_ml_amd.data.synthetic import generate_device_shard
+    from photon_ml_amd.function.losses import LOGISTIC
+    data, w = generate_device_shard(150_000, 30_000, 20, "cuda", precision, chunk_rows=1 << 16, layout="tiled")
+    data.set_offsets(0.2 * torch.randn(data.n_rows, dtype=torch.float64, device="cuda"))
+    z = torch.zeros(data.dim, dtype=torch.float64, device="cuda")
+    ref = data.value_grad_packed(LOGISTIC, z, 0.0)
+    tagged = torch.zeros_like(z)
+    tagged._pml_zero = True
+    nf = getattr(data, "n_fwd", 0)
+    got = data.value_grad_packed(LOGISTIC, tagged, 0.0)
+    assert getattr(data, "n_fwd", 0) == nf
+    assert torch.equal(got[: data.dim], ref[: data.dim])
+    torch.testing.assert_close(got[data.dim:], ref[data.dim:], rtol=1e-13, atol=0)
