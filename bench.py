@@ -77,7 +77,7 @@ def main():
         args.features = cfg["features"]
 
     import torch
-    from photon_ml_amd.parallel.dist import init_distributed, DistributedGLMData, all_reduce_scalar, barrier
+    from photon_ml_amd.parallel.dist import init_distributed, DistributedGLMData, all_reduce_scalar, barrier, is_dist
     rank, world, local = init_distributed()
     if world != args.gpus:
         log(f"warning: --gpus {args.gpus} but WORLD_SIZE={world}; using WORLD_SIZE")
@@ -107,8 +107,8 @@ def main():
     log(f"data ready in {time.time() - t_gen:.1f}s: {data.n_rows} rows/GPU, {data.nbytes() / 2**30:.1f} GiB/GPU, "
         f"layout={data.layout}")
     sharded = args.optimizer_state == "feature-sharded"
-    gdata = DistributedGLMData(data) if world > 1 and not sharded else data
-    if world > 1 and not sharded:
+    gdata = DistributedGLMData(data) if is_dist() and not sharded else data
+    if is_dist() and not sharded:
         log(f"gradient all-reduce: {'overlapped, %d buckets' % gdata.buckets if gdata.overlap else 'one-shot'}")
 
     if args.config == "owlqn":
@@ -149,7 +149,7 @@ def main():
     elapsed = all_reduce_scalar(elapsed, "max", device=dev)
     passes = data.n_passes - passes0
     stalled = bool(getattr(opt, "_finished", False))
-    total_rows = int(all_reduce_scalar(data.n_rows, "sum", device=dev)) if world > 1 else data.n_rows
+    total_rows = int(all_reduce_scalar(data.n_rows, "sum", device=dev)) if is_dist() else data.n_rows
     value = total_rows * args.steps / elapsed
     if rank == 0:
         log(f"final f={st.loss:.6e} |g|={gnorm:.3e} evals/step={passes / args.steps:.2f} "

@@ -81,7 +81,7 @@ def main():
     import numpy as np
     import torch
     from collections import OrderedDict
-    from photon_ml_amd.parallel.dist import init_distributed, all_reduce_scalar, barrier
+    from photon_ml_amd.parallel.dist import init_distributed, all_reduce_scalar, barrier, is_dist
     rank, world, local = init_distributed()
     if torch.cuda.is_available():
         local = local % torch.cuda.device_count()  # several ranks may share a GPU in rehearsal runs
@@ -110,7 +110,7 @@ def main():
     re_cfg = GLMOptimizationConfiguration(OptimizerConfig("TRON", args.re_iters, 1e-12),
                                           RegularizationContext("L2"), 1.0)
     task = "LOGISTIC_REGRESSION"
-    re_cls = ShardedRandomEffectCoordinate if world > 1 else RandomEffectCoordinate
+    re_cls = ShardedRandomEffectCoordinate if is_dist() else RandomEffectCoordinate
     coords = OrderedDict([
         ("global", FixedEffectCoordinate("global", data, FixedEffectDataConfiguration("global"), fe_cfg, task,
                                          device=dev, precision=args.precision)),

@@ -178,7 +178,8 @@ def generate_device_shard(n_rows: int, n_features: int, nnz_per_row: int, device
     # group the counts are summed first so every rank shares ONE feature order (gradient all-reduce buckets then
     # cover the same columns on every rank, see DistributedGLMData)
     import torch.distributed as dist
-    if dist.is_available() and dist.is_initialized() and dist.get_world_size() > 1:
+    from ..parallel.dist import is_dist
+    if is_dist():
         cc = counts if dist.get_backend() == "nccl" else counts.cpu()
         dist.all_reduce(cc)
         counts = cc.to(dev)

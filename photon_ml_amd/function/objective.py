@@ -63,10 +63,11 @@ class GLMObjective:
             grad = grad + self.l2_weight * w
         return f, grad
 
-    def margin_line_search(self, data, x0: torch.Tensor, d: torch.Tensor,
-                           t0: float = 1.0) -> Optional["MarginLineSearch"]:
+    def margin_line_search(self, data, x0: torch.Tensor, d: torch.Tensor, t0: float = 1.0,
+                           dots=None) -> Optional["MarginLineSearch"]:
         """Line search along x0 + t d in MARGIN space (GLM margins are affine in t), or None when the data
-        backend cannot cache margins. See :class:`MarginLineSearch`."""
+        backend cannot cache margins. ``dots``: (x0.x0, x0.d, d.d) when the caller already has them. See
+        :class:`MarginLineSearch`."""
         if not hasattr(data, "ls_begin"):
             return None
         norm = self.normalization
@@ -75,7 +76,7 @@ class GLMObjective:
         d_shift = -float(torch.dot(d_eff, norm.shifts.to(d_eff))) if norm.shifts is not None else 0.0
         if not data.ls_begin(w0_eff, shift0, d_eff, d_shift, t0, self.loss):
             return None
-        return MarginLineSearch(self, data, x0, d)
+        return MarginLineSearch(self, data, x0, d, dots)
 
     # ---- TRON trial point from margins (see DeviceGLMData.step_begin) ----------------------------------------
     def step_begin(self, data, w: torch.Tensor) -> bool:
@@ -142,13 +143,13 @@ class MarginLineSearch:
     treeAggregate) at every trial point (Breeze StrongWolfeLineSearch through ``DiffFunction.calculate``).
     """
 
-    def __init__(self, obj: GLMObjective, data, x0: torch.Tensor, d: torch.Tensor):
+    def __init__(self, obj: GLMObjective, data, x0: torch.Tensor, d: torch.Tensor, dots=None):
         from ..optimization.vector_space import vdots
         self.obj, self.data, self.x0, self.d = obj, data, x0, d
         l2 = obj.l2_weight
         self.l2 = l2
         if l2 > 0:
-            self.a, self.b, self.c = vdots([(x0, x0), (x0, d), (d, d)])
+            self.a, self.b, self.c = dots if dots is not None else vdots([(x0, x0), (x0, d), (d, d)])
 
     def eval(self, t: float):
         f, dd = self.data.ls_eval(self.obj.loss, t)
@@ -166,7 +167,8 @@ class MarginLineSearch:
         self.obj.n_value_grad += 1
         grad = norm.finalize_vector(g, s)
         if self.obj.l2_weight > 0:
-            f += self.obj.l2_value(x)
+            # ||x0 + t d||^2 from the cached inner products (no host synchronisation)
+            f += 0.5 * self.l2 * (self.a + 2.0 * t * self.b + t * t * self.c)
             grad = grad + self.obj.l2_weight * x
         return x, f, grad
 

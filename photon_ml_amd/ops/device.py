@@ -118,6 +118,28 @@ class SegChunk:
 # PML_TRON_STATS=1: (kept forward blocks, kept transpose items) fractions of every entity-masked table rebuild
 MASK_STATS = [] if os.environ.get("PML_TRON_STATS") == "1" else None
 
+class VecKey:
+    """Identity of the coefficient vector a cached device quantity (margins, w l'') was computed at. The same
+    tensor object at the same version matches without touching the device (the optimizer hands the accepted point
+    back unchanged); anything else falls back to a device comparison with a saved copy (one host sync)."""
+
+    __slots__ = ("copy", "src", "ver")
+
+    def __init__(self, w: torch.Tensor):
+        self.copy = w.detach().clone()
+        self.src = w
+        self.ver = w._version
+
+    @property
+    def shape(self):
+        return self.copy.shape
+
+    def matches(self, w: torch.Tensor) -> bool:
+        if w is self.src and w._version == self.ver:
+            return True
+        return self.copy.shape == w.shape and bool(torch.equal(self.copy, w.to(self.copy.device, self.copy.dtype)))
+
+
 class DeviceGLMData(GLMComputable):
     """GLM row shard on one GPU evaluated with the native kernels."""
 
@@ -412,8 +434,8 @@ class DeviceGLMData(GLMComputable):
 
     def _z_valid_for(self, w_eff, shift) -> bool:
         key = getattr(self, "_z_key", None)
-        return (key is not None and key[1] == float(shift) and key[0].shape == w_eff.shape
-                and self._z_chain < self.LS_REFRESH and bool(torch.equal(key[0], w_eff.to(key[0].device, key[0].dtype))))
+        return (key is not None and key[1] == float(shift) and self._z_chain < self.LS_REFRESH
+                and key[0].matches(w_eff))
 
     def ls_begin(self, w0_eff, shift0, d_eff, d_shift, t0: float = 1.0, loss=None) -> bool:
         """Direction pass (FWD_LS): zd = X d_eff + d_shift, materialises the pending step into z0, and evaluates
@@ -425,15 +447,24 @@ class DeviceGLMData(GLMComputable):
         if not self._z_valid_for(w0_eff, shift0):
             self.fwd_all(self._vec(w0_eff), FWD_MARGIN, 0, shift0, None, None, z_out=self.z_cache, with_offset=1,
                          stats=False)
-            self._z_key, self._z_chain, self._tpend = (w0_eff.detach().clone(), float(shift0)), 0, 0.0
+            self._z_key, self._z_chain, self._tpend = (VecKey(w0_eff), float(shift0)), 0, 0.0
         with trace_range("K1' direction pass (margins of d + first trial)"):
             self.lib.pml_set_ls_args(self.z_cache.data_ptr(), float(t0), float(self._tpend))
             self.fwd_all(self._vec(d_eff), FWD_LS, loss.loss_id, d_shift, self.coef, None, z_out=self.zd)
             self.lib.pml_set_ls_args(None, 0.0, 0.0)
             self._tpend = 0.0
             self._ls_t0 = float(t0)
-            self._ls_t0_vals = tuple(self._reduce_stats().tolist())   # local (F, D) at t0
+            # local (F, D) at t0, on the device: read by the first ls_eval (the caller synchronises once, after
+            # everything this iteration needs has been queued), copied device-to-device by ls_finish_packed
+            self._ls_t0_dev = self._reduce_stats().clone()
+            self._ls_t0_host = None
         return True
+
+    @property
+    def _ls_t0_vals(self):
+        if self._ls_t0_host is None:
+            self._ls_t0_host = tuple(self._ls_t0_dev.tolist())
+        return self._ls_t0_host
 
     def _ls(self, loss, t, final, out):
         dzz = self.dzz if (final and self.track_hessian and loss.twice_differentiable) else None
@@ -458,7 +489,7 @@ class DeviceGLMData(GLMComputable):
             out = torch.zeros(self.dim + 2, dtype=torch.float64, device=self.device)
             if self._ls_t0 is not None and float(t) == self._ls_t0 and not (
                     self.track_hessian and loss.twice_differentiable):
-                out[self.dim] = self._ls_t0_vals[0]
+                out[self.dim] = self._ls_t0_dev[0]
                 if need_s:
                     out[self.dim + 1] = self.coef[: self.n_rows].to(torch.float64).sum()
             else:
@@ -466,9 +497,9 @@ class DeviceGLMData(GLMComputable):
             self._tpend = float(t)
             self._ls_t0 = None
             self._track_u = False
-            self._z_key, self._z_chain = (w_eff.detach().clone(), float(shift)), self._z_chain + 1
+            self._z_key, self._z_chain = (VecKey(w_eff), float(shift)), self._z_chain + 1
             if self.track_hessian and loss.twice_differentiable:
-                self._dzz_key, self._dzz_shift = w_eff.detach().clone(), float(shift)
+                self._dzz_key, self._dzz_shift = VecKey(w_eff), float(shift)
             if start_reduce is not None:
                 start_reduce(out[self.dim:])
                 self._packed_bucketed(self.coef, out[: self.dim], start_reduce, nb)
@@ -503,7 +534,7 @@ class DeviceGLMData(GLMComputable):
             else:
                 self.fwd_all(self._vec(w_eff), FWD_MARGIN, 0, shift, None, None, z_out=self.z_cache, with_offset=1,
                              stats=False)
-                self._z_key, self._z_chain = (w_eff.detach().clone(), float(shift)), 0
+                self._z_key, self._z_chain = (VecKey(w_eff), float(shift)), 0
             self._tpend = 0.0
         if self._tpend:
             self.z_cache.add_(self.zd, alpha=self._tpend)   # materialise the accepted step
@@ -771,13 +802,13 @@ class DeviceGLMData(GLMComputable):
             zc = getattr(self, "z_cache", None)
             self.fwd_all(x, FWD_VALUE_GRAD, loss.loss_id, margin_shift, self.coef, dzz, z_out=zc)
             if zc is not None:
-                self._z_key, self._z_chain, self._tpend, self._ls_t0 = (w_eff.detach().clone(),
+                self._z_key, self._z_chain, self._tpend, self._ls_t0 = (VecKey(w_eff),
                                                                          float(margin_shift)), 0, 0.0, None
             out[self.dim:] = self._reduce_stats()
             start_reduce(out[self.dim:])
             self._packed_bucketed(self.coef, out[: self.dim], start_reduce, nb)
             if dzz is not None:
-                self._dzz_key = w_eff.detach().clone()
+                self._dzz_key = VecKey(w_eff)
                 self._dzz_shift = float(margin_shift)
             self.n_passes += 1
             return out
@@ -864,14 +895,14 @@ class DeviceGLMData(GLMComputable):
         zc = getattr(self, "z_cache", None)
         self.fwd_all(x, FWD_VALUE_GRAD, loss.loss_id, margin_shift, self.coef, dzz, z_out=zc)
         if zc is not None:
-            self._z_key, self._z_chain, self._tpend, self._ls_t0 = (w_eff.detach().clone(), float(margin_shift)), \
+            self._z_key, self._z_chain, self._tpend, self._ls_t0 = (VecKey(w_eff), float(margin_shift)), \
                 0, 0.0, None
         self.t_all(self.coef, G)
         out[self.dim:] = self._reduce_stats()
         if self.old_of_new is not None:
             out[: self.dim] = self._unperm(G.clone())
         if dzz is not None:
-            self._dzz_key = w_eff.detach().clone()
+            self._dzz_key = VecKey(w_eff)
             self._dzz_shift = float(margin_shift)
         self.n_passes += 1
         return out
@@ -883,12 +914,11 @@ class DeviceGLMData(GLMComputable):
 
     def _ensure_dzz(self, loss, w_eff, shift):
         key = self._dzz_key
-        if key is not None and self._dzz_shift == float(shift) and key.shape == w_eff.shape and bool(
-                torch.equal(key, w_eff.to(key.device, key.dtype))):
+        if key is not None and self._dzz_shift == float(shift) and key.matches(w_eff):
             return
         x = self._vec(w_eff)
         self.fwd_all(x, FWD_DZZ, loss.loss_id, shift, self.dzz, None, stats=False)
-        self._dzz_key = w_eff.detach().clone()
+        self._dzz_key = VecKey(w_eff)
         self._dzz_shift = float(shift)
 
     def hv_packed(self, loss, w_eff, margin_shift, v_eff, v_shift) -> torch.Tensor:

@@ -113,6 +113,9 @@ def glm_lib() -> Optional[ctypes.CDLL]:
         lib.pml_gram_grid.argtypes = [ctypes.c_longlong]
         lib.pml_gram.argtypes = [c_void_p, c_int, ctypes.c_longlong, c_void_p, c_void_p]
         lib.pml_lincomb.argtypes = [c_void_p, c_void_p, c_int, ctypes.c_longlong, c_void_p, c_void_p]
+        lib.pml_lbfgs_pair.argtypes = [c_void_p] * 4 + [ctypes.c_longlong] + [c_void_p] * 6
+        lib.pml_two_loop.argtypes = [c_int, c_void_p, c_void_p, c_void_p, c_void_p, c_void_p, ctypes.c_longlong,
+                                     c_void_p, c_void_p, c_int, c_void_p]
         lib.pml_tl_set_deep.argtypes = [c_int, c_int]
         lib.pml_rs_set_variant.argtypes = [c_int]
         lib.pml_rs_set_variant(int(os.environ.get("PML_RS_VARIANT", "3")))
@@ -123,7 +126,7 @@ def glm_lib() -> Optional[ctypes.CDLL]:
         for f in ("pml_seg_fwd", "pml_seg_t", "pml_reduce_stats", "pml_build_blocks", "pml_tl_fwd", "pml_tl_t",
                   "pml_tl_maxbits", "pml_segdot", "pml_tl_fwd_multi", "pml_tl_t_multi", "pml_seg_cg_step",
                   "pml_seg_expand", "pml_bgemv", "pml_bhv", "pml_rs_tron", "pml_ls_eval", "pml_gram_grid", "pml_gram",
-                  "pml_lincomb"):
+                  "pml_lincomb", "pml_two_loop", "pml_lbfgs_pair"):
             getattr(lib, f).restype = c_int
         lib.pml_set_config.argtypes = [c_int, c_int, c_int, c_int]
         lib._pml_typed = True
@@ -222,6 +225,62 @@ def lincomb(coefs, vs):
     out = torch.empty(n, dtype=torch.float64, device=vs[0].device)
     check(lib.pml_lincomb(ptrs, cs, k, n, out.data_ptr(), stream_handle(vs[0].device)), "lincomb")
     return out
+
+
+_TWO_LOOP_SCRATCH = {}
+
+
+def two_loop(s, y, rho, gamma, g, negate: bool = False):
+    """L-BFGS two-loop ``H g`` (``-H g`` with ``negate``) in ONE cooperative HIP launch (``lbfgs_two_loop_kernel``):
+    history vectors ``s``, ``y`` (k <= 32 fp64 device vectors), ``rho`` (0-d device tensors 1/s.y) and ``gamma``
+    (0-d device tensor s.y/y.y of the newest pair) stay on the device. None when the inputs do not qualify or the
+    device refuses the cooperative launch (the caller then runs the torch recursion)."""
+    k = len(s)
+    if not (0 < k <= 32 and g.device.type == "cuda" and g.dtype == torch.float64 and g.is_contiguous()):
+        return None
+    vecs = list(s) + list(y)
+    if not all(v.device == g.device and v.dtype == torch.float64 and v.is_contiguous() and v.numel() == g.numel()
+               for v in vecs):
+        return None
+    if not all(r.device == g.device and r.dtype == torch.float64 for r in list(rho) + [gamma]):
+        return None
+    lib = require_glm_lib()
+    scratch = _TWO_LOOP_SCRATCH.get(g.device)
+    if scratch is None:
+        scratch = _TWO_LOOP_SCRATCH[g.device] = torch.empty(2 * 512, dtype=torch.float64, device=g.device)
+    P = ctypes.c_void_p * k
+    q = torch.empty_like(g)
+    rc = lib.pml_two_loop(k, P(*[v.data_ptr() for v in s]), P(*[v.data_ptr() for v in y]),
+                          P(*[r.data_ptr() for r in rho]), gamma.data_ptr(), g.data_ptr(), g.numel(), q.data_ptr(),
+                          scratch.data_ptr(), int(negate), stream_handle(g.device))
+    if rc == -2:
+        return None          # cooperative launch refused (e.g. co-residency): torch recursion instead
+    check(rc, "two_loop")
+    return q
+
+
+_PAIR_SCRATCH = {}
+
+
+def lbfgs_pair(x, x0, g, g0):
+    """New L-BFGS history pair in one launch (``lbfgs_pair_kernel``): returns ``(s, y, out)`` with s = x - x0,
+    y = g - g0 and the device vector out = [s.y, y.y, 1/s.y, s.y/y.y, g.g]; None when the inputs do not qualify."""
+    vs = (x, x0, g, g0)
+    if not (x.device.type == "cuda" and all(v.device == x.device and v.dtype == torch.float64 and v.dim() == 1
+                                            and v.is_contiguous() and v.numel() == x.numel() for v in vs)
+            and x.numel() > 0):
+        return None
+    lib = require_glm_lib()
+    sc = _PAIR_SCRATCH.get(x.device)
+    if sc is None:
+        sc = _PAIR_SCRATCH[x.device] = (torch.empty(3 * 1024, dtype=torch.float64, device=x.device),
+                                        torch.zeros(1, dtype=torch.int32, device=x.device))
+    s, y = torch.empty_like(x), torch.empty_like(x)
+    out = torch.empty(5, dtype=torch.float64, device=x.device)
+    check(lib.pml_lbfgs_pair(x.data_ptr(), x0.data_ptr(), g.data_ptr(), g0.data_ptr(), x.numel(), s.data_ptr(),
+                             y.data_ptr(), sc[0].data_ptr(), sc[1].data_ptr(), out.data_ptr(),
+                             stream_handle(x.device)), "lbfgs_pair")
+    return s, y, out
 
 
 def batched_gemv(A: torch.Tensor, x: torch.Tensor, trans: bool = False) -> torch.Tensor:

@@ -35,6 +35,8 @@ GRAM_MIN_DIM = int(os.environ.get("PML_LBFGS_GRAM_MIN_DIM", str(1 << 62)))
 # Replicated device vectors run the two-loop with 0-d device scalars (PML_LBFGS_DEVICE_TWO_LOOP=0: host scalars,
 # one synchronisation per dot product).
 DEVICE_TWO_LOOP = os.environ.get("PML_LBFGS_DEVICE_TWO_LOOP", "1") != "0"
+# ... in one cooperative HIP launch (lbfgs_two_loop_kernel) instead of ~4 torch launches per history pair
+NATIVE_TWO_LOOP = os.environ.get("PML_LBFGS_NATIVE_TWO_LOOP", "1") != "0"
 DEFAULT_NUM_CORRECTIONS = 10
 DEFAULT_TOLERANCE = 1.0e-7
 
@@ -83,9 +85,43 @@ class _History:
                 self.rho_t.pop(0)
         return True
 
-    def _apply_inverse_device(self, g: torch.Tensor) -> torch.Tensor:
-        """Two-loop with 0-d device scalars (dot products stay on the GPU, fused scaled adds via addcmul):
-        the same recursion and arithmetic order as the host-scalar loop below, no synchronisation."""
+    def push_pair(self, x, x0, g, g0):
+        """push(x - x0, g - g0); replicated device vectors: the pair and its scalars in ONE kernel
+        (``ops.native.lbfgs_pair``) and one host synchronisation for the curvature test, which also returns
+        ||g||^2. Returns (pushed, ||g||^2 or None)."""
+        if NATIVE_TWO_LOOP and _device_loop(g):
+            from ..ops.native import lbfgs_pair
+            r = lbfgs_pair(x, x0, g, g0)
+            if r is not None:
+                s, y, out = r
+                sy, yy, _, _, gg = out.tolist()
+                if not (sy > 1e-300) or sy != sy:
+                    return False, gg
+                self.s.append(s)
+                self.y.append(y)
+                self.rho.append(1.0 / sy)
+                self.rho_t.append(out[2])
+                self.gamma_t = out[3]
+                if len(self.s) > self.m:
+                    self.s.pop(0)
+                    self.y.pop(0)
+                    self.rho.pop(0)
+                    self.rho_t.pop(0)
+                return True, gg
+        return self.push(x - x0, g - g0), None
+
+    def _apply_inverse_device(self, g: torch.Tensor, negate: bool = False) -> torch.Tensor:
+        """Two-loop with 0-d device scalars, no synchronisation: one cooperative HIP launch
+        (``ops.native.two_loop``) or, when the device refuses it, torch dot products + fused scaled adds."""
+        if NATIVE_TWO_LOOP:
+            from ..ops.native import two_loop
+            q = two_loop(self.s, self.y, self.rho_t, self.gamma_t, g, negate)
+            if q is not None:
+                return q
+        q = self._apply_inverse_device_torch(g)
+        return -q if negate else q
+
+    def _apply_inverse_device_torch(self, g: torch.Tensor) -> torch.Tensor:
         q = g.clone()
         k = len(self.s)
         alpha = [None] * k
@@ -98,10 +134,14 @@ class _History:
             q.addcmul_(self.s[i], alpha[i] - beta)
         return q
 
-    def apply_inverse(self, g: torch.Tensor) -> torch.Tensor:
-        """Two-loop recursion: returns H g."""
+    def apply_inverse(self, g: torch.Tensor, negate: bool = False) -> torch.Tensor:
+        """Two-loop recursion: returns H g (-H g with ``negate``)."""
         if self.s and _device_loop(g) and len(self.rho_t) == len(self.s) and g.numel() < GRAM_MIN_DIM:
-            return self._apply_inverse_device(g)
+            return self._apply_inverse_device(g, negate)
+        q = self._apply_inverse_host(g)
+        return -q if negate else q
+
+    def _apply_inverse_host(self, g: torch.Tensor) -> torch.Tensor:
         if self.s and (vector_space.current().sharded or (g.is_cuda and g.numel() >= GRAM_MIN_DIM)):
             return self._apply_inverse_gram(g)
         q = g.clone()
@@ -195,15 +235,45 @@ class LBFGS(Optimizer):
         state.loss, state.gradient = adj_f, adj_g
 
     def _direction(self, state: OptimizerState) -> torch.Tensor:
-        return -self.history.apply_inverse(state.gradient)
+        return self.history.apply_inverse(state.gradient, negate=True)
 
-    def _search(self, objective, data, state: OptimizerState, d: torch.Tensor):
+    def _prefetch(self, state: OptimizerState, d: torch.Tensor):
+        """Replicated device vectors: the device vector (g.d, d.d, x0.x0, x0.d), fetched later in ONE host
+        synchronisation (the descent test, the first trial step 1/||d||, the zero-direction test and the L2 terms
+        of the margin line search would otherwise each synchronise); None elsewhere."""
+        if not _device_loop(d):
+            return None
+        x0, g = state.coefficients, state.gradient
+        return torch.stack([torch.dot(g, d), torch.dot(d, d), torch.dot(x0, x0), torch.dot(x0, d)])
+
+    def _search(self, objective, data, state: OptimizerState, d: torch.Tensor, pre=None):
+        """``pre``: host list or device vector from :meth:`_prefetch`. A device vector is read AFTER the margin
+        line search has queued its direction pass (iterations > 0: t0 = 1 is known), so the GPU runs that pass
+        while the host waits instead of idling through the synchronisation."""
         x0 = state.coefficients
-        g0 = _dot(state.gradient, d)
-        t0 = 1.0 / _norm(d) if self._inner_iter == 0 else 1.0
+        from ..utils.timing import trace_range
+        use_mls = MARGIN_LINE_SEARCH and not self.constraints and hasattr(objective, "margin_line_search")
+        if pre is not None and not isinstance(pre, list) and (self._inner_iter == 0 or not use_mls):
+            pre = pre.tolist()
         mls = None
-        if MARGIN_LINE_SEARCH and not self.constraints and hasattr(objective, "margin_line_search"):
-            mls = objective.margin_line_search(data, x0, d, t0)
+        if use_mls:
+            t0 = (1.0 / pre[1] ** 0.5 if pre is not None else 1.0 / _norm(d)) if self._inner_iter == 0 else 1.0
+            lazy = pre is not None and not isinstance(pre, list)
+            mls = objective.margin_line_search(data, x0, d, t0, dots=None if pre is None or lazy
+                                               else (pre[2], pre[3], pre[1]))
+            if lazy:
+                pre = pre.tolist()
+                if mls is not None and mls.l2 > 0:
+                    mls.a, mls.b, mls.c = pre[2], pre[3], pre[1]
+        with trace_range("line-search setup"):
+            if pre is not None:
+                g0 = pre[0]
+                t0 = 1.0 / pre[1] ** 0.5 if self._inner_iter == 0 else 1.0
+                if not pre[1] > 0 and not vector_space.current().any_nonzero(d):
+                    raise _ZeroDirection()
+            else:
+                g0 = _dot(state.gradient, d)
+                t0 = 1.0 / _norm(d) if self._inner_iter == 0 else 1.0
         if mls is not None:
             # trials in margin space (one elementwise pass each), full gradient only at the accepted step
             _, _, _, t = strong_wolfe(lambda tt: (*mls.eval(tt), tt), state.loss, g0, t0)  # payload = the step
@@ -220,12 +290,20 @@ class LBFGS(Optimizer):
     def _run_one_iteration(self, objective, data, state: OptimizerState) -> OptimizerState:
         if self._finished:
             return state
+        from ..utils.timing import trace_range
         try:
-            d = self._direction(state)
-            if not vector_space.current().any_nonzero(d):
+            with trace_range("two-loop direction"):
+                d = self._direction(state)
+                pre = self._prefetch(state, d)
+                # device: d.d > 0 decides later, in _search (d.d == 0 -- all zero or underflow -- checks exactly)
+                nonzero = pre is not None or vector_space.current().any_nonzero(d)
+            if not nonzero:
                 self._finished = True  # zero (pseudo-)gradient: stationary point
                 return state
-            x, f, g = self._search(objective, data, state, d)
+            x, f, g = self._search(objective, data, state, d, pre)
+        except _ZeroDirection:
+            self._finished = True
+            return state
         except LineSearchFailed:
             if not self._failed_once and len(self.history.s) > 0:
                 self._failed_once = True
@@ -234,12 +312,20 @@ class LBFGS(Optimizer):
             self._finished = True
             return state
         self._failed_once = False
-        self.history.push(x - state.coefficients, g - self._smooth_g)
+        with trace_range("history push"):
+            _, gg = self.history.push_pair(x, state.coefficients, g, self._smooth_g)
         self._smooth_f, self._smooth_g = f, g
         self._inner_iter += 1
         adj_f, adj_g = self._adjust(x, f, g)
         x = project_box(x, self.constraints)
-        return OptimizerState(x, adj_f, adj_g, state.iter + 1)
+        new = OptimizerState(x, adj_f, adj_g, state.iter + 1)
+        if gg is not None and adj_g is g:
+            new._grad_norm = gg ** 0.5      # the convergence test needs no further synchronisation
+        return new
+
+
+class _ZeroDirection(Exception):
+    """The search direction is exactly zero (stationary point)."""
 
 
 class OWLQN(LBFGS):
@@ -264,15 +350,17 @@ class OWLQN(LBFGS):
         return f + self.l1_weight * vector_space.current().abs_sum(x), self._pseudo_gradient(x, g)
 
     def _direction(self, state):
-        d = -self.history.apply_inverse(state.gradient)
+        d = self.history.apply_inverse(state.gradient, negate=True)
         # keep only components that descend along the pseudo-gradient
         return torch.where(d * state.gradient < 0, d, torch.zeros_like(d))
 
-    def _search(self, objective, data, state, d):
+    def _prefetch(self, state, d):
+        return None        # the orthant-masked direction is tested for zero before the search, as before
+
+    def _search(self, objective, data, state, d, pre=None):
         x0 = state.coefficients
         pg = state.gradient
         orthant = torch.where(x0 != 0, torch.sign(x0), torch.sign(-pg))
-        # first trial as Breeze OWLQN.determineStepSize: 0.5 / ||adjusted gradient|| on iteration 0, else 1
         # first trial as Breeze OWLQN.determineStepSize: 0.5 / ||adjusted gradient|| on iteration 0, else 1
         t0 = 0.5 / _norm(pg) if self._inner_iter == 0 else 1.0
         shrink = 0.1 if self._inner_iter < 1 else 0.5

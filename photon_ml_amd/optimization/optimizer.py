@@ -37,7 +37,8 @@ class OptimizerState:
     iter: int
 
     def grad_norm(self) -> float:
-        return vector_space.vnorm(self.gradient)
+        gn = getattr(self, "_grad_norm", None)        # set by an optimizer that already reduced ||g||^2
+        return vector_space.vnorm(self.gradient) if gn is None else gn
 
 
 class OptimizationStatesTracker:

@@ -27,12 +27,20 @@ def env_world() -> tuple[int, int, int]:
             int(os.environ.get("LOCAL_RANK", 0)))
 
 
+def force_collectives() -> bool:
+    """``PML_FORCE_DIST=1``: a world of ONE rank still initialises the process group and routes every aggregate
+    through the collectives (RCCL on a single GPU: the multi-rank code path — bucketed async all-reduce, device
+    all-to-all, all-gather / reduce-scatter — executed on hardware with the trivial group)."""
+    return os.environ.get("PML_FORCE_DIST", "0") == "1"
+
+
 def init_distributed(backend: Optional[str] = None, timeout_s: int = 1800) -> tuple[int, int, int]:
-    """Initialise the default process group from torchrun env vars (no-op for world size 1)."""
+    """Initialise the default process group from torchrun env vars (no-op for world size 1 unless
+    ``PML_FORCE_DIST=1``)."""
     rank, world, local = env_world()
     from ..utils.watchdog import start_watchdog
     start_watchdog()  # PML_WATCHDOG_S: abort this rank (-> torchrun aborts the group) when progress stops
-    if world > 1 and not dist.is_initialized():
+    if (world > 1 or force_collectives()) and not dist.is_initialized():
         # a collective that exceeds ``timeout_s`` raises instead of hanging (RCCL async error handling)
         os.environ.setdefault("TORCH_NCCL_ASYNC_ERROR_HANDLING", "1")
         timeout_s = int(os.environ.get("PML_COLLECTIVE_TIMEOUT_S", timeout_s))
@@ -47,7 +55,8 @@ def init_distributed(backend: Optional[str] = None, timeout_s: int = 1800) -> tu
 
 
 def is_dist() -> bool:
-    return dist.is_available() and dist.is_initialized() and dist.get_world_size() > 1
+    return (dist.is_available() and dist.is_initialized()
+            and (dist.get_world_size() > 1 or force_collectives()))
 
 
 def world_size() -> int:

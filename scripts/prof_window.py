@@ -71,6 +71,34 @@ def main(db, sub, out=None):
     lines += ["", "| nested region | count | total ms |", "|---|---:|---:|"]
     for k, (n, t) in sorted(inner.items(), key=lambda kv: -kv[1][1])[:25]:
         lines.append(f"| {k} | {n} | {t / 1e6:.3f} |")
+    # idle gaps between kernels (GPU waiting for the host): grouped by the kernel pair around the gap and by the
+    # innermost nested region containing the gap
+    gaps = defaultdict(lambda: [0, 0])
+    greg = defaultdict(lambda: [0, 0])
+    nested = sorted(((n, s, e) for n, s, e in regs if s >= t0 and e <= t1 and (s, e) != (t0, t1)),
+                    key=lambda r: r[2] - r[1])
+    end_prev, name_prev = t0, "<window start>"
+    short = lambda n: re.sub(r"<.*$", "", re.sub(r"\(.*$", "", n))[:48]
+    for n, s, e in ks_ + [("<window end>", t1, t1)]:
+        if s - end_prev > 5000:
+            g = s - end_prev
+            key = f"{short(name_prev)} -> {short(n)}"
+            gaps[key][0] += 1
+            gaps[key][1] += g
+            mid = (s + end_prev) // 2
+            r = next((rn_ for rn_, rs_, re2 in nested if rs_ <= mid <= re2), "(top level)")
+            greg[r][0] += 1
+            greg[r][1] += g
+        if e > end_prev:
+            end_prev, name_prev = e, n
+    idle = sum(t for _, t in gaps.values())
+    lines += ["", f"Idle gaps > 5 us: {sum(c for c, _ in gaps.values())}, {idle / 1e6:.3f} ms", "",
+              "| previous kernel -> next kernel | gaps | idle ms |", "|---|---:|---:|"]
+    for k, (n, t) in sorted(gaps.items(), key=lambda kv: -kv[1][1])[:20]:
+        lines.append(f"| `{k}` | {n} | {t / 1e6:.3f} |")
+    lines += ["", "| innermost region of the gap | gaps | idle ms |", "|---|---:|---:|"]
+    for k, (n, t) in sorted(greg.items(), key=lambda kv: -kv[1][1])[:15]:
+        lines.append(f"| {k} | {n} | {t / 1e6:.3f} |")
     text = "\n".join(lines)
     print(text)
     if out:

@@ -59,8 +59,9 @@ def game_worker(rank, world, port, out):
             for s in data.shards}
     save_game_model(res.model, f"{out}/model", maps, opt_configs=res.config)
     import torch.distributed as dist
-    dist.barrier()
-    dist.destroy_process_group()
+    if dist.is_initialized():      # (not for a plain WORLD_SIZE=1 run)
+        dist.barrier()
+        dist.destroy_process_group()
 
 
 def sharding_worker(rank, world, port, out):

@@ -21,9 +21,9 @@ def _free_port():
         return s.getsockname()[1]
 
 
-def _launch(kind, out, world=2, timeout=600):
+def _launch(kind, out, world=2, timeout=600, **env_extra):
     port = _free_port()
-    env = dict(os.environ, PML_BACKEND="torch", OMP_NUM_THREADS="2")
+    env = dict(os.environ, PML_BACKEND="torch", OMP_NUM_THREADS="2", **env_extra)
     procs = [subprocess.Popen([sys.executable, os.path.join(HERE, "dist_worker.py"), kind, str(r), str(world),
                                str(port), str(out)], env=env, stdout=subprocess.PIPE, stderr=subprocess.STDOUT)
              for r in range(world)]
@@ -133,3 +133,16 @@ def test_entity_sharded_game_matches_single_process(tmp_path):
             ca, cb = a.coefficients_of(e).means.numpy(), b.coefficients_of(e).means.numpy()
             keep = np.abs(cb) > 1e-4  # the Avro writer drops |w| <= 1e-4
             np.testing.assert_allclose(ca[keep], cb[keep], rtol=1e-5, atol=1e-6)
+
+
+def test_forced_one_rank_group_is_bitwise_single_process(tmp_path):
+    """PML_FORCE_DIST=1 with WORLD_SIZE=1: the entity-sharded GAME path (routing all-to-alls, distributed
+    evaluators, per-rank model parts) runs through a one-rank process group — the mode the GPU test
+    ``test_rccl_gpu.py`` uses to execute the RCCL code paths on a single MI355X. It must give the single-process
+    model exactly (the distributed evaluators reduce in another order: 1e-12)."""
+    for mode, flag in (("forced", "1"), ("plain", "0")):
+        (tmp_path / mode).mkdir()
+        _launch("game", tmp_path / mode, world=1, PML_FORCE_DIST=flag)
+    assert np.array_equal(np.load(tmp_path / "forced/game_fe_r0.npy"), np.load(tmp_path / "plain/game_fe_r0.npy"))
+    np.testing.assert_allclose(np.load(tmp_path / "forced/game_eval_r0.npy"),
+                               np.load(tmp_path / "plain/game_eval_r0.npy"), rtol=1e-12)
