@@ -21,7 +21,6 @@
 // with ctypes after torch (one HIP runtime per process; torch tensors provide the memory, the caller the stream).
 
 #include <hip/hip_runtime.h>
-#include <hip/hip_cooperative_groups.h>
 #include <stdint.h>
 #include <math.h>
 #include <algorithm>
@@ -2322,22 +2321,9 @@ __global__ __launch_bounds__(256) void lincomb_kernel(VecSet vs, int k, long lon
   }
 }
 
-// ------------------------------------------------------------------------------------------------------------
-// L-BFGS two-loop recursion in ONE cooperative launch (optimization/lbfgs.py _History.apply_inverse; K16 of
-// SURVEY §2.8). The torch form issues ~4 launches per history pair (dot, reduction, scale, fused add): 80+ tiny
-// kernels per direction at m = 10, and on the GAME fixed-effect coordinate the GPU idled between them (3.3 ms of
-// gaps per 10 iterations, profiles/game5_fe_window_gaps.md). Here every thread owns a fixed grid-stride slice of
-// q, each step fuses the update q -= a_i y_i with the next dot product s_{i-1}.q, and the 2k scalar reductions
-// are grid-wide: per-workgroup partials (double-buffered) -> grid barrier -> every workgroup sums the partials in
-// the same fixed order (deterministic, identical a_i in every workgroup). rho_i and gamma stay device scalars
-// (no host synchronisation). Grid = co-resident workgroups (cooperative launch guarantees residency).
-#define TL2_MAXK 32
-#define TL2_BLOCK 256
-#define TL2_MAXGRID 512
-struct TwoLoopVecs { const double* s[TL2_MAXK]; const double* y[TL2_MAXK]; const double* rho[TL2_MAXK]; };
-
+// fixed-order 256-thread block sum: xor butterfly inside each wave, then the 4 wave sums in order (every thread
+// gets the result)
 __device__ __forceinline__ double tl2_block_sum(double v, double* sh) {
-  // fixed-order tree: xor butterfly inside each wave, then the 4 wave sums in order
 #pragma unroll
   for (int o = 32; o >= 1; o >>= 1) v += __shfl_xor(v, o, 64);
   const int w = threadIdx.x >> 6;
@@ -2345,77 +2331,6 @@ __device__ __forceinline__ double tl2_block_sum(double v, double* sh) {
   if ((threadIdx.x & 63) == 0) sh[w] = v;
   __syncthreads();
   return (sh[0] + sh[1]) + (sh[2] + sh[3]);
-}
-
-__device__ __forceinline__ double tl2_grid_sum(double acc, double* partial, int buf, double* sh) {
-  namespace cg = cooperative_groups;
-  const double b = tl2_block_sum(acc, sh);
-  if (threadIdx.x == 0) partial[buf * TL2_MAXGRID + blockIdx.x] = b;
-  cg::this_grid().sync();
-  double p = 0.0;
-  for (int j = threadIdx.x; j < (int)gridDim.x; j += TL2_BLOCK) p += partial[buf * TL2_MAXGRID + j];
-  return tl2_block_sum(p, sh);
-}
-
-__global__ __launch_bounds__(TL2_BLOCK) void lbfgs_two_loop_kernel(TwoLoopVecs v, int k, const double* __restrict__ gamma,
-                                                                   const double* __restrict__ g, long long n,
-                                                                   double* __restrict__ q, double* __restrict__ partial,
-                                                                   int negate) {
-  __shared__ double sh[4];
-  __shared__ double alpha[TL2_MAXK];   // identical in every thread: written by thread 0, read after a barrier
-  const long long stride = (long long)gridDim.x * TL2_BLOCK;
-  const long long i0 = (long long)blockIdx.x * TL2_BLOCK + threadIdx.x;
-  int buf = 0;
-  // q = g, acc = s_{k-1} . q
-  double acc = 0.0;
-  for (long long i = i0; i < n; i += stride) {
-    const double x = g[i];
-    q[i] = x;
-    acc = fma(v.s[k - 1][i], x, acc);
-  }
-  const double gm = *gamma;
-  for (int j = k - 1; j >= 0; --j) {
-    const double a = *v.rho[j] * tl2_grid_sum(acc, partial, buf, sh);
-    buf ^= 1;
-    if (threadIdx.x == 0) alpha[j] = a;
-    acc = 0.0;
-    const double* yj = v.y[j];
-    if (j > 0) {
-      const double* sn = v.s[j - 1];
-      for (long long i = i0; i < n; i += stride) {
-        const double x = fma(-a, yj[i], q[i]);
-        q[i] = x;
-        acc = fma(sn[i], x, acc);
-      }
-    } else {      // end of the first loop: q *= gamma, then the first dot of the second loop (y_0 . q)
-      const double* y0 = v.y[0];
-      for (long long i = i0; i < n; i += stride) {
-        const double x = fma(-a, yj[i], q[i]) * gm;
-        q[i] = x;
-        acc = fma(y0[i], x, acc);
-      }
-    }
-  }
-  for (int j = 0; j < k; ++j) {
-    const double bta = *v.rho[j] * tl2_grid_sum(acc, partial, buf, sh);
-    buf ^= 1;
-    const double c = alpha[j] - bta;
-    const double* sj = v.s[j];
-    acc = 0.0;
-    if (j + 1 < k) {
-      const double* yn = v.y[j + 1];
-      for (long long i = i0; i < n; i += stride) {
-        const double x = fma(c, sj[i], q[i]);
-        q[i] = x;
-        acc = fma(yn[i], x, acc);
-      }
-    } else {
-      for (long long i = i0; i < n; i += stride) {
-        const double x = fma(c, sj[i], q[i]);
-        q[i] = negate ? -x : x;
-      }
-    }
-  }
 }
 
 // New L-BFGS history pair in one launch: s = x - x0, y = g - g0 and out = [s.y, y.y, 1/s.y, s.y/y.y, g.g] (g.g: the
@@ -2473,37 +2388,8 @@ __global__ __launch_bounds__(256) void lbfgs_pair_kernel(const double* __restric
   }
 }
 
-static int g_tl2_grid = 0;
 
 extern "C" {
-
-// H g (negate: -H g) for an m <= 32 deep history; partial: 2 * 512 doubles of device scratch.
-int pml_two_loop(int k, const double* const* s, const double* const* y, const double* const* rho,
-                 const double* gamma, const double* g, long long n, double* q, double* partial, int negate,
-                 void* stream) {
-  if (k < 1 || k > TL2_MAXK || n <= 0) return -22;
-  if (g_tl2_grid == 0) {
-    int dev = 0, cus = 0, per = 0;
-    if (hipGetDevice(&dev) != hipSuccess) return -1;
-    if (hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, dev) != hipSuccess) return -1;
-    if (hipOccupancyMaxActiveBlocksPerMultiprocessor(&per, lbfgs_two_loop_kernel, TL2_BLOCK, 0) != hipSuccess)
-      return -1;
-    if (per < 1) return -1;
-    g_tl2_grid = std::min(TL2_MAXGRID, cus * per);
-  }
-  TwoLoopVecs v{};
-  for (int j = 0; j < k; ++j) { v.s[j] = s[j]; v.y[j] = y[j]; v.rho[j] = rho[j]; }
-  const long long need = (n + TL2_BLOCK - 1) / TL2_BLOCK;
-  int grid = (int)std::min<long long>(g_tl2_grid, need);
-  void* args[] = {&v, &k, &gamma, &g, &n, &q, &partial, &negate};
-  hipError_t e = hipLaunchCooperativeKernel((const void*)lbfgs_two_loop_kernel, dim3(grid), dim3(TL2_BLOCK), args, 0,
-                                            (hipStream_t)stream);
-  if (e != hipSuccess) {
-    (void)hipGetLastError();
-    return -2;
-  }
-  return 0;
-}
 
 // s = x - x0, y = g - g0, out[5] = [s.y, y.y, 1/s.y, s.y/y.y, g.g]; partial: 3 * 1024 doubles; counter: one zeroed
 // unsigned (re-armed by the kernel).

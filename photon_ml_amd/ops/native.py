@@ -114,8 +114,6 @@ def glm_lib() -> Optional[ctypes.CDLL]:
         lib.pml_gram.argtypes = [c_void_p, c_int, ctypes.c_longlong, c_void_p, c_void_p]
         lib.pml_lincomb.argtypes = [c_void_p, c_void_p, c_int, ctypes.c_longlong, c_void_p, c_void_p]
         lib.pml_lbfgs_pair.argtypes = [c_void_p] * 4 + [ctypes.c_longlong] + [c_void_p] * 6
-        lib.pml_two_loop.argtypes = [c_int, c_void_p, c_void_p, c_void_p, c_void_p, c_void_p, ctypes.c_longlong,
-                                     c_void_p, c_void_p, c_int, c_void_p]
         lib.pml_tl_set_deep.argtypes = [c_int, c_int]
         lib.pml_rs_set_variant.argtypes = [c_int]
         lib.pml_rs_set_variant(int(os.environ.get("PML_RS_VARIANT", "3")))
@@ -126,7 +124,7 @@ def glm_lib() -> Optional[ctypes.CDLL]:
         for f in ("pml_seg_fwd", "pml_seg_t", "pml_reduce_stats", "pml_build_blocks", "pml_tl_fwd", "pml_tl_t",
                   "pml_tl_maxbits", "pml_segdot", "pml_tl_fwd_multi", "pml_tl_t_multi", "pml_seg_cg_step",
                   "pml_seg_expand", "pml_bgemv", "pml_bhv", "pml_rs_tron", "pml_ls_eval", "pml_gram_grid", "pml_gram",
-                  "pml_lincomb", "pml_two_loop", "pml_lbfgs_pair"):
+                  "pml_lincomb", "pml_lbfgs_pair"):
             getattr(lib, f).restype = c_int
         lib.pml_set_config.argtypes = [c_int, c_int, c_int, c_int]
         lib._pml_typed = True
@@ -225,38 +223,6 @@ def lincomb(coefs, vs):
     out = torch.empty(n, dtype=torch.float64, device=vs[0].device)
     check(lib.pml_lincomb(ptrs, cs, k, n, out.data_ptr(), stream_handle(vs[0].device)), "lincomb")
     return out
-
-
-_TWO_LOOP_SCRATCH = {}
-
-
-def two_loop(s, y, rho, gamma, g, negate: bool = False):
-    """L-BFGS two-loop ``H g`` (``-H g`` with ``negate``) in ONE cooperative HIP launch (``lbfgs_two_loop_kernel``):
-    history vectors ``s``, ``y`` (k <= 32 fp64 device vectors), ``rho`` (0-d device tensors 1/s.y) and ``gamma``
-    (0-d device tensor s.y/y.y of the newest pair) stay on the device. None when the inputs do not qualify or the
-    device refuses the cooperative launch (the caller then runs the torch recursion)."""
-    k = len(s)
-    if not (0 < k <= 32 and g.device.type == "cuda" and g.dtype == torch.float64 and g.is_contiguous()):
-        return None
-    vecs = list(s) + list(y)
-    if not all(v.device == g.device and v.dtype == torch.float64 and v.is_contiguous() and v.numel() == g.numel()
-               for v in vecs):
-        return None
-    if not all(r.device == g.device and r.dtype == torch.float64 for r in list(rho) + [gamma]):
-        return None
-    lib = require_glm_lib()
-    scratch = _TWO_LOOP_SCRATCH.get(g.device)
-    if scratch is None:
-        scratch = _TWO_LOOP_SCRATCH[g.device] = torch.empty(2 * 512, dtype=torch.float64, device=g.device)
-    P = ctypes.c_void_p * k
-    q = torch.empty_like(g)
-    rc = lib.pml_two_loop(k, P(*[v.data_ptr() for v in s]), P(*[v.data_ptr() for v in y]),
-                          P(*[r.data_ptr() for r in rho]), gamma.data_ptr(), g.data_ptr(), g.numel(), q.data_ptr(),
-                          scratch.data_ptr(), int(negate), stream_handle(g.device))
-    if rc == -2:
-        return None          # cooperative launch refused (e.g. co-residency): torch recursion instead
-    check(rc, "two_loop")
-    return q
 
 
 _PAIR_SCRATCH = {}

@@ -35,8 +35,10 @@ GRAM_MIN_DIM = int(os.environ.get("PML_LBFGS_GRAM_MIN_DIM", str(1 << 62)))
 # Replicated device vectors run the two-loop with 0-d device scalars (PML_LBFGS_DEVICE_TWO_LOOP=0: host scalars,
 # one synchronisation per dot product).
 DEVICE_TWO_LOOP = os.environ.get("PML_LBFGS_DEVICE_TWO_LOOP", "1") != "0"
-# ... in one cooperative HIP launch (lbfgs_two_loop_kernel) instead of ~4 torch launches per history pair
-NATIVE_TWO_LOOP = os.environ.get("PML_LBFGS_NATIVE_TWO_LOOP", "1") != "0"
+# New history pair (s, y, s.y, y.y, 1/s.y, s.y/y.y, g.g) in one HIP kernel + one synchronisation. (A cooperative
+# single-launch two-loop kernel was measured SLOWER than the torch recursion below: 20 grid barriers at ~25 us
+# each, 0.61 ms per direction vs ~0.2 ms; profiles/lbfgs_device_two_loop_ab.md.)
+NATIVE_PAIR = os.environ.get("PML_LBFGS_NATIVE_PAIR", "1") != "0"
 DEFAULT_NUM_CORRECTIONS = 10
 DEFAULT_TOLERANCE = 1.0e-7
 
@@ -89,7 +91,7 @@ class _History:
         """push(x - x0, g - g0); replicated device vectors: the pair and its scalars in ONE kernel
         (``ops.native.lbfgs_pair``) and one host synchronisation for the curvature test, which also returns
         ||g||^2. Returns (pushed, ||g||^2 or None)."""
-        if NATIVE_TWO_LOOP and _device_loop(g):
+        if NATIVE_PAIR and _device_loop(g):
             from ..ops.native import lbfgs_pair
             r = lbfgs_pair(x, x0, g, g0)
             if r is not None:
@@ -111,17 +113,8 @@ class _History:
         return self.push(x - x0, g - g0), None
 
     def _apply_inverse_device(self, g: torch.Tensor, negate: bool = False) -> torch.Tensor:
-        """Two-loop with 0-d device scalars, no synchronisation: one cooperative HIP launch
-        (``ops.native.two_loop``) or, when the device refuses it, torch dot products + fused scaled adds."""
-        if NATIVE_TWO_LOOP:
-            from ..ops.native import two_loop
-            q = two_loop(self.s, self.y, self.rho_t, self.gamma_t, g, negate)
-            if q is not None:
-                return q
-        q = self._apply_inverse_device_torch(g)
-        return -q if negate else q
-
-    def _apply_inverse_device_torch(self, g: torch.Tensor) -> torch.Tensor:
+        """Two-loop with 0-d device scalars (dot products stay on the GPU, fused scaled adds via addcmul):
+        the same recursion and arithmetic order as the host-scalar loop below, no synchronisation."""
         q = g.clone()
         k = len(self.s)
         alpha = [None] * k
@@ -132,7 +125,7 @@ class _History:
         for i in range(k):
             beta = self.rho_t[i] * torch.dot(self.y[i], q)
             q.addcmul_(self.s[i], alpha[i] - beta)
-        return q
+        return q.neg_() if negate else q
 
     def apply_inverse(self, g: torch.Tensor, negate: bool = False) -> torch.Tensor:
         """Two-loop recursion: returns H g (-H g with ``negate``)."""
