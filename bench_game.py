@@ -126,6 +126,8 @@ def main():
     if torch.cuda.is_available():
         torch.cuda.synchronize()
     barrier()
+    fe_gd = coords["global"].glm_data
+    fe_pass0 = (getattr(fe_gd, "n_fwd", 0), getattr(fe_gd, "n_t", 0))
     t1 = time.perf_counter()
     model, _ = cd.run(args.steps, model)
     for _, m in model:       # the trained model's coefficients are part of the timed work (row-space RE: lazy)
@@ -135,6 +137,8 @@ def main():
         torch.cuda.synchronize()
     barrier()
     elapsed = all_reduce_scalar(time.perf_counter() - t1, "max")
+    log(f"fixed effect per sweep: {(getattr(fe_gd, 'n_fwd', 0) - fe_pass0[0]) / args.steps:.1f} forward + "
+        f"{(getattr(fe_gd, 'n_t', 0) - fe_pass0[1]) / args.steps:.1f} transpose passes")
     loss = cd.history[-1].get("training_loss")
     re_stats = coords["per-entity"].last_stats
     total_rows = int(all_reduce_scalar(float(data.n_rows)))

@@ -118,6 +118,10 @@ class SegChunk:
 # PML_TRON_STATS=1: (kept forward blocks, kept transpose items) fractions of every entity-masked table rebuild
 MASK_STATS = [] if os.environ.get("PML_TRON_STATS") == "1" else None
 
+# keep the margin cache across offset changes (set_offsets shifts it); PML_OFFSET_SHIFT_CACHE=0 drops it instead
+OFFSET_SHIFT_CACHE = os.environ.get("PML_OFFSET_SHIFT_CACHE", "1") != "0"
+
+
 class VecKey:
     """Identity of the coefficient vector a cached device quantity (margins, w l'') was computed at. The same
     tensor object at the same version matches without touching the device (the optimizer hands the accepted point
@@ -404,8 +408,21 @@ class DeviceGLMData(GLMComputable):
         return sum(c.nbytes() for c in self.csr + self.csc)
 
     def set_offsets(self, offsets):
-        self.o.copy_(torch.as_tensor(offsets, device=self.device).to(self.vdt))
-        self._z_key = None
+        new = torch.as_tensor(offsets, device=self.device).to(self.vdt)
+        zc = getattr(self, "z_cache", None)
+        if (zc is not None and getattr(self, "_z_key", None) is not None and self._z_chain + 1 < self.LS_REFRESH
+                and getattr(self, "_masked", None) is None and OFFSET_SHIFT_CACHE):
+            # GAME: the residual offsets change between coordinate updates while the fixed-effect coefficients do
+            # not; the cached margins (offsets included) shift by the offset change (one elementwise pass) and
+            # the next update starts without a forward pass over the non-zeros (reference: every
+            # FixedEffectCoordinate update re-evaluates X w from scratch)
+            n = self.n_rows
+            zc[:n].add_(new[:n].to(torch.float64) - self.o[:n].to(torch.float64))
+            self._z_chain += 1
+            self._ls_t0 = None
+        else:
+            self._z_key = None
+        self.o.copy_(new)
         self._step_base = None
         self._dzz_key = None          # cached w l''(z) depends on the margins, hence on the offsets
 
@@ -797,6 +814,15 @@ class DeviceGLMData(GLMComputable):
                 self._packed_bucketed(self.coef, out[: self.dim], start_reduce, nb)
                 self.n_passes += 1
                 return out
+            if self._cached_point(w_eff, margin_shift):
+                self._ls(loss, self._tpend, 1, out[self.dim:])
+                self._ls_t0 = None
+                if self.track_hessian and loss.twice_differentiable:
+                    self._dzz_key, self._dzz_shift = VecKey(w_eff), float(margin_shift)
+                start_reduce(out[self.dim:])
+                self._packed_bucketed(self.coef, out[: self.dim], start_reduce, nb)
+                self.n_passes += 1
+                return out
             x = self._vec(w_eff)
             dzz = self.dzz if (self.track_hessian and loss.twice_differentiable) else None
             zc = getattr(self, "z_cache", None)
@@ -860,6 +886,11 @@ class DeviceGLMData(GLMComputable):
         with trace_range("K1 value+grad pass"):
             return self._value_grad_packed(loss, w_eff, margin_shift)
 
+    def _cached_point(self, w_eff, shift) -> bool:
+        """The margins at ``w_eff`` are cached (z0 + t_pending zd): value + gradient need no forward pass."""
+        return (getattr(self, "z_cache", None) is not None and getattr(self, "_masked", None) is None
+                and self._z_valid_for(w_eff, shift))
+
     def _zero_point(self, loss, w_eff) -> bool:
         """``w_eff`` is the optimizer's all-zero tolerance point (tagged by Optimizer.start): margins = offsets."""
         return bool(getattr(w_eff, "_pml_zero", False)) and not (self.track_hessian and loss.twice_differentiable)
@@ -885,6 +916,16 @@ class DeviceGLMData(GLMComputable):
         G = out[: self.dim]
         if self._zero_point(loss, w_eff):
             self._zero_coef(loss, margin_shift, out[self.dim:])
+            self.t_all(self.coef, G)
+            if self.old_of_new is not None:
+                out[: self.dim] = self._unperm(G.clone())
+            self.n_passes += 1
+            return out
+        if self._cached_point(w_eff, margin_shift):
+            self._ls(loss, self._tpend, 1, out[self.dim:])    # coef (+ w l'') and (F, S) from cached margins
+            self._ls_t0 = None
+            if self.track_hessian and loss.twice_differentiable:
+                self._dzz_key, self._dzz_shift = VecKey(w_eff), float(margin_shift)
             self.t_all(self.coef, G)
             if self.old_of_new is not None:
                 out[: self.dim] = self._unperm(G.clone())

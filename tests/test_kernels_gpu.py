@@ -606,3 +606,29 @@ def test_zero_point_evaluation_without_forward_pass(precision):
     assert getattr(data, "n_fwd", 0) == nf
     assert torch.equal(got[: data.dim], ref[: data.dim])
     torch.testing.assert_close(got[data.dim:], ref[data.dim:], rtol=1e-13, atol=0)
+
+
+@pytest.mark.parametrize("layout", LAYOUTS)
+def test_offset_change_reuses_cached_margins(layout):
+    """GAME residual offsets change between fixed-effect updates while w does not: set_offsets shifts the cached
+    margins, and value+gradient at the cached point needs no forward pass; same numbers as a fresh evaluation."""
+    from photon_ml_amd.ops.device import DeviceGLMData
+    data = make_data(n=6000, d=800, density=0.02, seed=9)
+    rng = np.random.default_rng(3)
+    dev = DeviceGLMData.from_labeled(data, "cuda", "f64", chunk_rows=2048, layout=layout)
+    dev.enable_margin_cache()
+    w = torch.from_numpy(rng.normal(size=data.n_features) * 0.05).cuda()
+    dev.value_grad_sums(LOGISTIC, w, 0.02)
+    new_off = rng.normal(size=data.n_rows) * 0.1
+    dev.set_offsets(torch.from_numpy(new_off))
+    nf = dev.n_fwd
+    f1, s1, g1 = dev.value_grad_sums(LOGISTIC, w.clone(), 0.02)
+    assert dev.n_fwd == nf, "the cached margins must be reused"
+    fresh = DeviceGLMData.from_labeled(LabeledData(data.x, data.y, new_off, data.weights), "cuda", "f64",
+                                       chunk_rows=2048, layout=layout)
+    f0, s0, g0 = fresh.value_grad_sums(LOGISTIC, w, 0.02)
+    assert abs(f1 - f0) <= 1e-12 * abs(f0) and abs(s1 - s0) <= 1e-10 * max(1.0, abs(s0))
+    torch.testing.assert_close(g1, g0, rtol=1e-11, atol=1e-11 * float(g0.abs().max()))
+    # a different point still takes the forward pass
+    dev.value_grad_sums(LOGISTIC, w * 0.5, 0.02)
+    assert dev.n_fwd == nf + 1
