@@ -2388,8 +2388,84 @@ __global__ __launch_bounds__(256) void lbfgs_pair_kernel(const double* __restric
   }
 }
 
+// L-BFGS two-loop recursion as a chain of 2k + 1 fused step kernels launched back to back from C++ (no host work
+// between them; a single cooperative launch with grid barriers was measured slower, profiles/
+// lbfgs_device_two_loop_ab.md). Step: x = src (g first, then q); x += sign * c * u; x *= gamma; store x (or -x);
+// and the next dot product v . x, reduced by the last workgroup in workgroup order (deterministic) into the next
+// coefficient: rho * dot, or a_sub - rho * dot in the second loop. All scalars stay on the device.
+struct TwoLoopStep {
+  const double* src;      // g (first step) or q
+  const double* u;        // update vector (y_j or s_j) or null
+  const double* c;        // its coefficient (device scalar) or null
+  double sign;            // -1 (first loop) or +1 (second loop)
+  const double* gamma;    // scale after the update or null
+  const double* v;        // next dot product vector or null
+  const double* rho;      // rho of the next coefficient
+  const double* a_sub;    // second loop: coefficient = a_sub - rho * dot
+  double* out;            // next coefficient
+  int negate;             // last step: store -x
+};
+
+__global__ __launch_bounds__(256) void lbfgs_step_kernel(TwoLoopStep st, long long n, double* __restrict__ q,
+                                                         double* __restrict__ partial, unsigned* __restrict__ counter) {
+  __shared__ double sh[4];
+  __shared__ int last;
+  const double c = st.u ? st.sign * *st.c : 0.0;
+  const double gm = st.gamma ? *st.gamma : 1.0;
+  double acc = 0.0;
+  for (long long i = (long long)blockIdx.x * 256 + threadIdx.x; i < n; i += (long long)gridDim.x * 256) {
+    double x = st.src[i];
+    if (st.u) x = fma(c, st.u[i], x);
+    if (st.gamma) x *= gm;
+    q[i] = st.negate ? -x : x;
+    if (st.v) acc = fma(st.v[i], x, acc);
+  }
+  if (!st.v) return;
+  acc = tl2_block_sum(acc, sh);
+  if (threadIdx.x == 0) {
+    partial[blockIdx.x] = acc;
+    __threadfence();
+    last = atomicAdd(counter, 1u) == gridDim.x - 1;
+  }
+  __syncthreads();
+  if (!last) return;
+  __threadfence();
+  double a = 0.0;
+  for (int j = threadIdx.x; j < (int)gridDim.x; j += 256) a += partial[j];
+  a = tl2_block_sum(a, sh);
+  if (threadIdx.x == 0) {
+    const double r = *st.rho * a;
+    *st.out = st.a_sub ? *st.a_sub - r : r;
+    *counter = 0u;
+  }
+}
 
 extern "C" {
+
+// H g (negate: -H g) for a k-deep history (newest last): rho[j] = 1/s_j.y_j and gamma = s.y/y.y of the newest
+// pair are device scalars; coef: 2k doubles of device scratch; partial: 1024 doubles; counter: one zeroed unsigned.
+int pml_two_loop_chain(int k, const double* const* s, const double* const* y, const double* const* rho,
+                       const double* gamma, const double* g, long long n, double* q, double* coef, double* partial,
+                       unsigned* counter, int negate, void* stream) {
+  if (k < 1 || n <= 0) return -22;
+  const int grid = (int)std::min<long long>(PAIR_GRID, (n + 255) / 256);
+  double* alpha = coef;           // alpha[j]
+  double* cc = coef + k;          // alpha[j] - beta[j]
+  auto launch = [&](const TwoLoopStep& st) {
+    hipLaunchKernelGGL(lbfgs_step_kernel, dim3(grid), dim3(256), 0, (hipStream_t)stream, st, n, q, partial, counter);
+  };
+  // q = g; alpha[k-1] = rho (s_{k-1} . q)
+  launch(TwoLoopStep{g, nullptr, nullptr, 0.0, nullptr, s[k - 1], rho[k - 1], nullptr, alpha + k - 1, 0});
+  for (int j = k - 1; j >= 1; --j)   // q -= alpha_j y_j; alpha[j-1] = rho (s_{j-1} . q)
+    launch(TwoLoopStep{q, y[j], alpha + j, -1.0, nullptr, s[j - 1], rho[j - 1], nullptr, alpha + j - 1, 0});
+  // q -= alpha_0 y_0; q *= gamma; c[0] = alpha_0 - rho_0 (y_0 . q)
+  launch(TwoLoopStep{q, y[0], alpha, -1.0, gamma, y[0], rho[0], alpha, cc, 0});
+  for (int j = 0; j + 1 < k; ++j)    // q += c_j s_j; c[j+1] = alpha_{j+1} - rho_{j+1} (y_{j+1} . q)
+    launch(TwoLoopStep{q, s[j], cc + j, 1.0, nullptr, y[j + 1], rho[j + 1], alpha + j + 1, cc + j + 1, 0});
+  launch(TwoLoopStep{q, s[k - 1], cc + k - 1, 1.0, nullptr, nullptr, nullptr, nullptr, nullptr, negate});
+  LAUNCH_CHECK();
+  return 0;
+}
 
 // s = x - x0, y = g - g0, out[5] = [s.y, y.y, 1/s.y, s.y/y.y, g.g]; partial: 3 * 1024 doubles; counter: one zeroed
 // unsigned (re-armed by the kernel).

@@ -114,6 +114,8 @@ def glm_lib() -> Optional[ctypes.CDLL]:
         lib.pml_gram.argtypes = [c_void_p, c_int, ctypes.c_longlong, c_void_p, c_void_p]
         lib.pml_lincomb.argtypes = [c_void_p, c_void_p, c_int, ctypes.c_longlong, c_void_p, c_void_p]
         lib.pml_lbfgs_pair.argtypes = [c_void_p] * 4 + [ctypes.c_longlong] + [c_void_p] * 6
+        lib.pml_two_loop_chain.argtypes = [c_int] + [c_void_p] * 5 + [ctypes.c_longlong] + [c_void_p] * 4 + \
+            [c_int, c_void_p]
         lib.pml_tl_set_deep.argtypes = [c_int, c_int]
         lib.pml_rs_set_variant.argtypes = [c_int]
         lib.pml_rs_set_variant(int(os.environ.get("PML_RS_VARIANT", "3")))
@@ -124,7 +126,7 @@ def glm_lib() -> Optional[ctypes.CDLL]:
         for f in ("pml_seg_fwd", "pml_seg_t", "pml_reduce_stats", "pml_build_blocks", "pml_tl_fwd", "pml_tl_t",
                   "pml_tl_maxbits", "pml_segdot", "pml_tl_fwd_multi", "pml_tl_t_multi", "pml_seg_cg_step",
                   "pml_seg_expand", "pml_bgemv", "pml_bhv", "pml_rs_tron", "pml_ls_eval", "pml_gram_grid", "pml_gram",
-                  "pml_lincomb", "pml_lbfgs_pair"):
+                  "pml_lincomb", "pml_lbfgs_pair", "pml_two_loop_chain"):
             getattr(lib, f).restype = c_int
         lib.pml_set_config.argtypes = [c_int, c_int, c_int, c_int]
         lib._pml_typed = True
@@ -247,6 +249,37 @@ def lbfgs_pair(x, x0, g, g0):
                              y.data_ptr(), sc[0].data_ptr(), sc[1].data_ptr(), out.data_ptr(),
                              stream_handle(x.device)), "lbfgs_pair")
     return s, y, out
+
+
+_CHAIN_SCRATCH = {}
+
+
+def two_loop(s, y, rho, gamma, g, negate: bool = False):
+    """L-BFGS two-loop ``H g`` (``-H g`` with ``negate``): 2k + 1 fused step kernels (``lbfgs_step_kernel``)
+    launched from C++ in one call; history vectors ``s``, ``y`` and the 0-d device scalars ``rho`` (1/s.y),
+    ``gamma`` (s.y/y.y of the newest pair) stay on the device. None when the inputs do not qualify."""
+    k = len(s)
+    if not (k > 0 and g.device.type == "cuda" and g.dtype == torch.float64 and g.dim() == 1 and g.is_contiguous()
+            and g.numel() > 0):
+        return None
+    if not all(v.device == g.device and v.dtype == torch.float64 and v.is_contiguous() and v.numel() == g.numel()
+               for v in list(s) + list(y)):
+        return None
+    if not all(r.device == g.device and r.dtype == torch.float64 and r.numel() == 1 for r in list(rho) + [gamma]):
+        return None
+    lib = require_glm_lib()
+    sc = _CHAIN_SCRATCH.get(g.device)
+    if sc is None or sc[0].numel() < 2 * k:
+        sc = _CHAIN_SCRATCH[g.device] = (torch.empty(max(64, 2 * k), dtype=torch.float64, device=g.device),
+                                         torch.empty(1024, dtype=torch.float64, device=g.device),
+                                         torch.zeros(1, dtype=torch.int32, device=g.device))
+    P = ctypes.c_void_p * k
+    q = torch.empty_like(g)
+    check(lib.pml_two_loop_chain(k, P(*[v.data_ptr() for v in s]), P(*[v.data_ptr() for v in y]),
+                                 P(*[r.data_ptr() for r in rho]), gamma.data_ptr(), g.data_ptr(), g.numel(),
+                                 q.data_ptr(), sc[0].data_ptr(), sc[1].data_ptr(), sc[2].data_ptr(), int(negate),
+                                 stream_handle(g.device)), "two_loop_chain")
+    return q
 
 
 def batched_gemv(A: torch.Tensor, x: torch.Tensor, trans: bool = False) -> torch.Tensor:

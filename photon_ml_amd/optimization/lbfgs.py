@@ -39,6 +39,8 @@ DEVICE_TWO_LOOP = os.environ.get("PML_LBFGS_DEVICE_TWO_LOOP", "1") != "0"
 # single-launch two-loop kernel was measured SLOWER than the torch recursion below: 20 grid barriers at ~25 us
 # each, 0.61 ms per direction vs ~0.2 ms; profiles/lbfgs_device_two_loop_ab.md.)
 NATIVE_PAIR = os.environ.get("PML_LBFGS_NATIVE_PAIR", "1") != "0"
+# Two-loop as 2k + 1 fused HIP step kernels launched from C++ (no Python between launches); 0: torch recursion
+NATIVE_TWO_LOOP = os.environ.get("PML_LBFGS_NATIVE_TWO_LOOP", "1") != "0"
 DEFAULT_NUM_CORRECTIONS = 10
 DEFAULT_TOLERANCE = 1.0e-7
 
@@ -113,8 +115,16 @@ class _History:
         return self.push(x - x0, g - g0), None
 
     def _apply_inverse_device(self, g: torch.Tensor, negate: bool = False) -> torch.Tensor:
-        """Two-loop with 0-d device scalars (dot products stay on the GPU, fused scaled adds via addcmul):
-        the same recursion and arithmetic order as the host-scalar loop below, no synchronisation."""
+        """Two-loop with 0-d device scalars, no synchronisation: the fused HIP step-kernel chain
+        (``ops.native.two_loop``), else torch dot products + fused scaled adds (same recursion and order)."""
+        if NATIVE_TWO_LOOP:
+            from ..ops.native import two_loop
+            q = two_loop(self.s, self.y, self.rho_t, self.gamma_t, g, negate)
+            if q is not None:
+                return q
+        return self._apply_inverse_device_torch(g, negate)
+
+    def _apply_inverse_device_torch(self, g: torch.Tensor, negate: bool = False) -> torch.Tensor:
         q = g.clone()
         k = len(self.s)
         alpha = [None] * k

@@ -471,6 +471,29 @@ def test_gram_and_lincomb_kernels(k, n):
 
 
 @pytest.mark.gpu
+@pytest.mark.parametrize("k,n", [(1, 1), (2, 777), (10, 1_000_003), (17, 300_000)])
+def test_two_loop_step_chain_matches_recursion(k, n):
+    """lbfgs_step_kernel chain (2k + 1 launches, last-workgroup fixed-order reductions) vs the fp64 torch two-loop
+    on the same history; bitwise run-to-run; negate gives exactly -H g."""
+    from photon_ml_amd.ops.native import two_loop
+    from photon_ml_amd.optimization.lbfgs import _History
+    gen = torch.Generator(device="cuda").manual_seed(100 + k)
+    h = _History(k)
+    for _ in range(k):
+        s = torch.randn(n, dtype=torch.float64, device="cuda", generator=gen)
+        y = s * (1.0 + torch.rand(n, dtype=torch.float64, device="cuda", generator=gen)) \
+            + 0.1 * torch.randn(n, dtype=torch.float64, device="cuda", generator=gen)
+        assert h.push(s, y)
+    g = torch.randn(n, dtype=torch.float64, device="cuda", generator=gen)
+    ref = h._apply_inverse_device_torch(g)
+    q = two_loop(h.s, h.y, h.rho_t, h.gamma_t, g)
+    torch.testing.assert_close(q, ref, rtol=1e-10, atol=1e-12 * float(ref.abs().max()))
+    assert torch.equal(two_loop(h.s, h.y, h.rho_t, h.gamma_t, g), q)
+    assert torch.equal(two_loop(h.s, h.y, h.rho_t, h.gamma_t, g, negate=True), -q)
+    assert torch.equal(h.apply_inverse(g, negate=True), -q)
+
+
+@pytest.mark.gpu
 @pytest.mark.parametrize("n", [1, 300, 1_000_003, 5_000_000])
 def test_lbfgs_pair_kernel(n):
     """lbfgs_pair_kernel: s, y bitwise = x - x0, g - g0; [s.y, y.y, 1/s.y, s.y/y.y, g.g] vs fp64 torch; the counter
