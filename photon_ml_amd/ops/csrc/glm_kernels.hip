@@ -1261,7 +1261,8 @@ static int g_tl_waves = 4;     // forward
 static int g_tl_waves_t = 4;   // transpose
 static int g_tl_pipe = 0;      // forward stream pipeline variant (see tl_stream)
 static int g_tl_pipe_t = 0;    // transpose stream pipeline variant
-static int g_rs_variant = 3;   // rs_tron variant: 0-2 rs_tron_kernel<V>; for n <= 32: 3 rs_tron_dpp_kernel (L in registers
+static int g_rs_variant = 5;   // rs_tron variant: 0-2 rs_tron_kernel<V>; for n <= 32: 3 (5: one wave per workgroup
+                                // for the LDS sizes, finer LDS occupancy granularity) rs_tron_dpp_kernel (L in registers
                                 // for n <= 16), 4 the same with L in LDS for every size (scripts/rs_tron_bench.py)
 static int g_tl_deep = 0;      // interleaved forward: 0 two-slot pipeline (P = 3), 1 deep S4/D1 (P = 5), 2 S6/D2 (P = 6)
 static int g_tl_deep_t = 0;    // interleaved transpose: same
@@ -1907,7 +1908,7 @@ __device__ __forceinline__ double group_sum(double v) {
   return v;
 }
 
-template <int K, bool LREG>
+template <int K, bool LREG, int WL = 2>
 struct RsGeom {
   static constexpr int GL = K <= 4 ? 4 : (K <= 8 ? 8 : 16);
   static constexpr int P = 64 / GL;                 // problems per wave
@@ -1916,16 +1917,18 @@ struct RsGeom {
   static constexpr int K1 = K > 16 ? K - 16 : 1;    // terms of the second column block
   static constexpr int SP = K + 1;                  // LDS row stride (doubles)
   static constexpr int PS0 = K * SP;
-  static constexpr int PS = PS0 + (((16 - PS0 % 32) % 32) + 32) % 32;   // problem stride = 16 mod 32 doubles
-  static constexpr int WPB = REG ? 4 : 2;           // waves per workgroup
+  // problem stride = 16 mod 32 doubles (measured: dropping the pad to fit 12 one-wave workgroups per CU at K = 20
+  // gains nothing over variant 5, 7.66 vs 7.69 ms, and loses 3 % at K = 24)
+  static constexpr int PS = PS0 + (((16 - PS0 % 32) % 32) + 32) % 32;
+  static constexpr int WPB = REG ? 4 : WL;          // waves per workgroup (LDS sizes: WL, see variant 5)
 };
 
-template <int K, bool LREG>
+template <int K, bool LREG, int WL>
 __global__ __launch_bounds__(256) void rs_tron_dpp_kernel(
     int B, int n, const double* __restrict__ Lm, const double* __restrict__ Y, const double* __restrict__ O,
     const double* __restrict__ WT, double* __restrict__ Beta, double* __restrict__ Fout, int* __restrict__ Iters,
     int* __restrict__ Reason, int loss, double l2, double tol, int max_iter, int max_fail, int max_cg) {
-  using Gm = RsGeom<K, LREG>;
+  using Gm = RsGeom<K, LREG, WL>;
   constexpr int GL = Gm::GL, P = Gm::P, R = Gm::R, K1 = Gm::K1, SP = Gm::SP, PS = Gm::PS;
   extern __shared__ double smem[];
   const int lane = threadIdx.x & 63, w = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
@@ -2223,15 +2226,15 @@ __global__ __launch_bounds__(256) void rs_tron_dpp_kernel(
   if (prob_on && i == 0) { Fout[b] = f; Iters[b] = it; Reason[b] = reason; }
 }
 
-template <int K, bool LREG>
+template <int K, bool LREG, int WL = 2>
 static void launch_rs_tron_dpp(int B, int n, const double* L, const double* y, const double* off, const double* wt,
                                double* beta, double* f, int* iters, int* reason, int loss, double l2, double tol,
                                int max_iter, int max_fail, int max_cg, hipStream_t st) {
-  using Gm = RsGeom<K, LREG>;
+  using Gm = RsGeom<K, LREG, WL>;
   const long long waves = (B + Gm::P - 1) / Gm::P;
   const long long grid = (waves + Gm::WPB - 1) / Gm::WPB;
   const size_t lds = Gm::REG ? 0 : (size_t)Gm::WPB * Gm::P * Gm::PS * sizeof(double);
-  hipLaunchKernelGGL((rs_tron_dpp_kernel<K, LREG>), dim3((unsigned)grid), dim3(Gm::WPB * 64), lds, st, B, n, L, y, off, wt,
+  hipLaunchKernelGGL((rs_tron_dpp_kernel<K, LREG, WL>), dim3((unsigned)grid), dim3(Gm::WPB * 64), lds, st, B, n, L, y, off, wt,
                      beta, f, iters, reason, loss, l2, tol, max_iter, max_fail, max_cg);
 }
 
@@ -2737,6 +2740,8 @@ int pml_rs_tron(int B, int n, const double* L, const double* y, const double* of
 #define RS_DPP(KK)                                                                                              \
   (V == 3 ? launch_rs_tron_dpp<KK, true>(B, n, L, y, off, wt, beta, f, iters, reason, loss, l2, tol, max_iter,    \
                                          max_fail, max_cg, st)                                                     \
+   : V == 5 ? launch_rs_tron_dpp<KK, true, 1>(B, n, L, y, off, wt, beta, f, iters, reason, loss, l2, tol, max_iter, \
+                                              max_fail, max_cg, st)                                                \
           : launch_rs_tron_dpp<KK, false>(B, n, L, y, off, wt, beta, f, iters, reason, loss, l2, tol, max_iter,   \
                                           max_fail, max_cg, st))
     if (n <= 4) RS_DPP(4);

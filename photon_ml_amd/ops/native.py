@@ -118,7 +118,7 @@ def glm_lib() -> Optional[ctypes.CDLL]:
             [c_int, c_void_p]
         lib.pml_tl_set_deep.argtypes = [c_int, c_int]
         lib.pml_rs_set_variant.argtypes = [c_int]
-        lib.pml_rs_set_variant(int(os.environ.get("PML_RS_VARIANT", "3")))
+        lib.pml_rs_set_variant(int(os.environ.get("PML_RS_VARIANT", "5")))
         lib.pml_ls_eval.argtypes = [c_int, c_int, c_double, c_int, c_void_p, c_void_p, c_void_p, c_void_p, c_int,
                                     c_void_p, c_void_p, c_void_p, c_void_p, c_void_p]
         lib.pml_rs_tron.argtypes = [c_int, c_int] + [c_void_p] * 8 + [c_int, c_double, c_double, c_int, c_int, c_int,
