@@ -1927,7 +1927,8 @@ template <int K, bool LREG, int WL>
 __global__ __launch_bounds__(256) void rs_tron_dpp_kernel(
     int B, int n, const double* __restrict__ Lm, const double* __restrict__ Y, const double* __restrict__ O,
     const double* __restrict__ WT, double* __restrict__ Beta, double* __restrict__ Fout, int* __restrict__ Iters,
-    int* __restrict__ Reason, int loss, double l2, double tol, int max_iter, int max_fail, int max_cg) {
+    int* __restrict__ Reason, int loss, double l2, double tol, int max_iter, int max_fail, int max_cg,
+    const int* __restrict__ order) {
   using Gm = RsGeom<K, LREG, WL>;
   constexpr int GL = Gm::GL, P = Gm::P, R = Gm::R, K1 = Gm::K1, SP = Gm::SP, PS = Gm::PS;
   extern __shared__ double smem[];
@@ -1936,7 +1937,10 @@ __global__ __launch_bounds__(256) void rs_tron_dpp_kernel(
   const long long b0 = ((long long)blockIdx.x * Gm::WPB + w) * P;
   if (b0 >= B) return;
   const bool prob_on = b0 + q < B;
-  const long long b = prob_on ? b0 + q : b0;
+  // order (optional): the wave's problems are order[b0 .. b0 + P) -- problems of similar difficulty share a wave
+  // (a wave runs until its slowest problem finishes); results go to the problems' own slots
+  auto prob = [&](long long j) -> long long { return order ? (long long)order[j] : j; };
+  const long long b = prob(prob_on ? b0 + q : b0);
   const long long nn = (long long)n * n;
   bool on[R];
   long long o[R];
@@ -1964,7 +1968,7 @@ __global__ __launch_bounds__(256) void rs_tron_dpp_kernel(
     for (int idx = lane; idx < P * PS; idx += 64) {
       const int qq = idx / PS, rem = idx - qq * PS, r = rem / SP, c = rem - r * SP;
       double v = 0.0;
-      if (b0 + qq < B && r < n && c < n) v = Lm[(b0 + qq) * nn + (long long)r * n + c];
+      if (b0 + qq < B && r < n && c < n) v = Lm[prob(b0 + qq) * nn + (long long)r * n + c];
       smem[wb + idx] = v;
     }
     __builtin_amdgcn_s_waitcnt(0);
@@ -2229,13 +2233,13 @@ __global__ __launch_bounds__(256) void rs_tron_dpp_kernel(
 template <int K, bool LREG, int WL = 2>
 static void launch_rs_tron_dpp(int B, int n, const double* L, const double* y, const double* off, const double* wt,
                                double* beta, double* f, int* iters, int* reason, int loss, double l2, double tol,
-                               int max_iter, int max_fail, int max_cg, hipStream_t st) {
+                               int max_iter, int max_fail, int max_cg, hipStream_t st, const int* order) {
   using Gm = RsGeom<K, LREG, WL>;
   const long long waves = (B + Gm::P - 1) / Gm::P;
   const long long grid = (waves + Gm::WPB - 1) / Gm::WPB;
   const size_t lds = Gm::REG ? 0 : (size_t)Gm::WPB * Gm::P * Gm::PS * sizeof(double);
   hipLaunchKernelGGL((rs_tron_dpp_kernel<K, LREG, WL>), dim3((unsigned)grid), dim3(Gm::WPB * 64), lds, st, B, n, L, y, off, wt,
-                     beta, f, iters, reason, loss, l2, tol, max_iter, max_fail, max_cg);
+                     beta, f, iters, reason, loss, l2, tol, max_iter, max_fail, max_cg, order);
 }
 
 // ============================================================================================================
@@ -2729,9 +2733,11 @@ int pml_bhv(int B, int n, const double* A, const double* dw, const double* v, do
 
 void pml_rs_set_variant(int v) { g_rs_variant = v; }
 
+// order (optional, n <= 32 kernels): a permutation of the B problems; waves take consecutive problems of it
+// (a scheduling hint only: results land in each problem's own slot whatever the order)
 int pml_rs_tron(int B, int n, const double* L, const double* y, const double* off, const double* wt, double* beta,
                 double* f, int* iters, int* reason, int loss, double l2, double tol, int max_iter, int max_fail,
-                int max_cg, void* stream) {
+                int max_cg, const int* order, void* stream) {
   if (B <= 0) return 0;
   if (n < 1 || n > 64 || loss < 0 || loss > 2) return -22;
   const int V = g_rs_variant;
@@ -2739,11 +2745,11 @@ int pml_rs_tron(int B, int n, const double* L, const double* y, const double* of
   if (V >= 3 && n <= 32) {
 #define RS_DPP(KK)                                                                                              \
   (V == 3 ? launch_rs_tron_dpp<KK, true>(B, n, L, y, off, wt, beta, f, iters, reason, loss, l2, tol, max_iter,    \
-                                         max_fail, max_cg, st)                                                     \
+                                         max_fail, max_cg, st, order)                                              \
    : V == 5 ? launch_rs_tron_dpp<KK, true, 1>(B, n, L, y, off, wt, beta, f, iters, reason, loss, l2, tol, max_iter, \
-                                              max_fail, max_cg, st)                                                \
+                                              max_fail, max_cg, st, order)                                         \
           : launch_rs_tron_dpp<KK, false>(B, n, L, y, off, wt, beta, f, iters, reason, loss, l2, tol, max_iter,   \
-                                          max_fail, max_cg, st))
+                                          max_fail, max_cg, st, order))
     if (n <= 4) RS_DPP(4);
     else if (n <= 8) RS_DPP(8);
     else if (n <= 12) RS_DPP(12);

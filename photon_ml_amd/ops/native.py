@@ -122,7 +122,7 @@ def glm_lib() -> Optional[ctypes.CDLL]:
         lib.pml_ls_eval.argtypes = [c_int, c_int, c_double, c_int, c_void_p, c_void_p, c_void_p, c_void_p, c_int,
                                     c_void_p, c_void_p, c_void_p, c_void_p, c_void_p]
         lib.pml_rs_tron.argtypes = [c_int, c_int] + [c_void_p] * 8 + [c_int, c_double, c_double, c_int, c_int, c_int,
-                                                                      c_void_p]
+                                                                      c_void_p, c_void_p]
         for f in ("pml_seg_fwd", "pml_seg_t", "pml_reduce_stats", "pml_build_blocks", "pml_tl_fwd", "pml_tl_t",
                   "pml_tl_maxbits", "pml_segdot", "pml_tl_fwd_multi", "pml_tl_t_multi", "pml_seg_cg_step",
                   "pml_seg_expand", "pml_bgemv", "pml_bhv", "pml_rs_tron", "pml_ls_eval", "pml_gram_grid", "pml_gram",
@@ -316,10 +316,12 @@ def batched_hv(A: torch.Tensor, dw: torch.Tensor, v: torch.Tensor, l2: float = 0
 
 def rs_tron(L: torch.Tensor, y: torch.Tensor, o: torch.Tensor, w: torch.Tensor, beta0: torch.Tensor, loss_id: int,
             l2: float, tol: float, max_iter: int, max_fail: int = 5, max_cg: int = 20,
-            out: Optional[torch.Tensor] = None):
+            out: Optional[torch.Tensor] = None, order: Optional[torch.Tensor] = None):
     """Fused per-problem TRON over a batch of small dense GLMs (``rs_tron_kernel``): returns
     (beta, f, iters, reason). Device only; n <= 64; losses logistic / Poisson / squared. ``out`` (contiguous
-    fp64 [B, n]) receives the solution in place (it starts from ``beta0``; ``out`` may be ``beta0``)."""
+    fp64 [B, n]) receives the solution in place (it starts from ``beta0``; ``out`` may be ``beta0``). ``order``
+    (int32 permutation of the B problems): waves take consecutive problems of it -- grouping problems of similar
+    iteration counts cuts the time a wave waits for its slowest problem; the results do not depend on it."""
     lib = require_glm_lib()
     B, n, _ = L.shape
     ts = [t.contiguous() for t in (L, y, o, w)]
@@ -336,9 +338,14 @@ def rs_tron(L: torch.Tensor, y: torch.Tensor, o: torch.Tensor, w: torch.Tensor, 
     f = torch.empty(B, dtype=torch.float64, device=L.device)
     iters = torch.empty(B, dtype=torch.int32, device=L.device)
     reason = torch.empty(B, dtype=torch.int32, device=L.device)
+    if order is not None:
+        assert order.dtype == torch.int32 and order.is_cuda and order.shape == (B,) and order.is_contiguous()
+        if os.environ.get("PML_CHECK_KERNEL_INPUTS", "0") == "1":   # the kernel indexes L / y / beta through it
+            assert B == 0 or (int(order.min()) >= 0 and int(order.max()) < B), "rs_tron order out of range"
     check(lib.pml_rs_tron(B, n, ts[0].data_ptr(), ts[1].data_ptr(), ts[2].data_ptr(), ts[3].data_ptr(),
                           beta.data_ptr(), f.data_ptr(), iters.data_ptr(), reason.data_ptr(), int(loss_id), float(l2),
-                          float(tol), int(max_iter), int(max_fail), int(max_cg), stream_handle(L.device)), "rs_tron")
+                          float(tol), int(max_iter), int(max_fail), int(max_cg),
+                          None if order is None else order.data_ptr(), stream_handle(L.device)), "rs_tron")
     return beta, f, iters.to(torch.long), reason.to(torch.long)
 
 

@@ -35,6 +35,9 @@ import torch
 
 from .batched import BatchedGLMData, BatchedResult, batched_lbfgs, batched_tron
 
+# rs_tron problem order from the previous solve's iteration counts (PML_RS_ORDER=0: entity order)
+RS_ORDER = os.environ.get("PML_RS_ORDER", "1") != "0"
+
 
 def _bmv(A: torch.Tensor, x: torch.Tensor, trans: bool = False) -> torch.Tensor:
     """Batched small dense mat-vec (A [B, n, n] or A^T) x [B, n] (HIP kernel on the device, torch on the host)."""
@@ -233,7 +236,13 @@ class RowSpaceBatch:
             if fused:
                 # whole per-entity TRON in one kernel, L resident in LDS (ops/csrc/glm_kernels.hip rs_tron_kernel)
                 from ..ops.native import rs_tron
-                _, f, it, rc = rs_tron(c.L, c.y, oc, c.w, b0, loss.loss_id, l2, tol, max_iter, out=c.view(beta))
+                # waves group problems by the iteration counts of this class's previous solve (a wave waits for its
+                # slowest problem); a scheduling hint only, the results do not depend on it
+                order = getattr(c, "order", None) if RS_ORDER else None
+                _, f, it, rc = rs_tron(c.L, c.y, oc, c.w, b0, loss.loss_id, l2, tol, max_iter, out=c.view(beta),
+                                       order=order)
+                if RS_ORDER:
+                    c.order = torch.argsort(it, stable=True).to(torch.int32)
             else:
                 data = BatchedGLMData(c.L, c.y, oc, c.w)
                 solver = batched_tron if optimizer == "TRON" else batched_lbfgs

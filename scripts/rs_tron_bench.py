@@ -39,3 +39,17 @@ for v in VARIANTS[1:]:
     d = (res[v0][0] - res[v][0]).abs().max().item()
     fr = (res[v0][2] != res[v][2]).double().mean().item()
     print(f"variant {v} vs {v0}: max |beta diff| = {d:.3e}; iteration counts differ on {fr:.4%} of problems")
+# problem order grouped by iteration count (what optimization/row_space.py passes from the previous solve)
+vlast = VARIANTS[-1]
+lib.pml_rs_set_variant(vlast)
+order = torch.argsort(res[vlast][2], stable=True).to(torch.int32)
+for _ in range(2):
+    out = rs_tron(L, y, o, w, b0, 0, 1.0, 1e-7, 10, order=order)
+    torch.cuda.synchronize()
+    t = time.perf_counter()
+    for _ in range(3):
+        out = rs_tron(L, y, o, w, b0, 0, 1.0, 1e-7, 10, order=order)
+    torch.cuda.synchronize()
+    print(f"variant {vlast} ordered by iterations: {(time.perf_counter() - t) / 3 * 1e3:.2f} ms; bitwise equal to "
+          f"entity order: {bool(torch.equal(out[0], res[vlast][0]) and torch.equal(out[2], res[vlast][2]))}",
+          flush=True)

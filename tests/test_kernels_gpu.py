@@ -655,3 +655,24 @@ def test_offset_change_reuses_cached_margins(layout):
     # a different point still takes the forward pass
     dev.value_grad_sums(LOGISTIC, w * 0.5, 0.02)
     assert dev.n_fwd == nf + 1
+
+
+
+def test_rs_tron_problem_order_is_a_scheduling_hint_only():
+    """rs_tron with a problem order (waves take consecutive problems of a permutation) gives bitwise the same
+    solutions, values and iteration counts as entity order."""
+    from photon_ml_amd.ops.native import rs_tron
+    g = torch.Generator(device="cuda").manual_seed(5)
+    for n in (4, 13, 20, 29):
+        B = 3001
+        X = torch.randn(B, n, 2 * n, dtype=torch.float64, device="cuda", generator=g) * 0.3
+        L = torch.linalg.cholesky(X @ X.transpose(1, 2) + 1e-3 * torch.eye(n, dtype=torch.float64, device="cuda"))
+        y = (torch.rand(B, n, device="cuda", generator=g) < 0.5).double()
+        o = torch.randn(B, n, dtype=torch.float64, device="cuda", generator=g) * 0.1
+        w = torch.rand(B, n, dtype=torch.float64, device="cuda", generator=g) + 0.5
+        b0 = torch.zeros(B, n, dtype=torch.float64, device="cuda")
+        ref = rs_tron(L, y, o, w, b0, 0, 1.0, 1e-7, 10)
+        perm = torch.randperm(B, generator=torch.Generator().manual_seed(n)).to(torch.int32).cuda()
+        got = rs_tron(L, y, o, w, b0, 0, 1.0, 1e-7, 10, order=perm)
+        for a, b in zip(ref, got):
+            assert torch.equal(a, b), n
