@@ -239,6 +239,8 @@ class RowSpaceBatch:
                 # waves group problems by the iteration counts of this class's previous solve (a wave waits for its
                 # slowest problem); a scheduling hint only, the results do not depend on it
                 order = getattr(c, "order", None) if RS_ORDER else None
+                if order is not None and order.numel() != c.L.shape[0]:
+                    order = None
                 _, f, it, rc = rs_tron(c.L, c.y, oc, c.w, b0, loss.loss_id, l2, tol, max_iter, out=c.view(beta),
                                        order=order)
                 if RS_ORDER:
