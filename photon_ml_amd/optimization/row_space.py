@@ -35,8 +35,10 @@ import torch
 
 from .batched import BatchedGLMData, BatchedResult, batched_lbfgs, batched_tron
 
-# rs_tron problem order from the previous solve's iteration counts (PML_RS_ORDER=0: entity order)
-RS_ORDER = os.environ.get("PML_RS_ORDER", "1") != "0"
+# rs_tron problem order from the previous solve's iteration counts (PML_RS_ORDER=1). Off by default: measured
+# slower at 1.25M x 20 (8.04-8.24 vs 7.73-8.00 ms in entity order; the scattered L loads cost more than the
+# shorter wave tails gain, profiles/rs_tron_variants_v5_1p25M.log)
+RS_ORDER = os.environ.get("PML_RS_ORDER", "0") == "1"
 
 
 def _bmv(A: torch.Tensor, x: torch.Tensor, trans: bool = False) -> torch.Tensor:
