@@ -22,8 +22,8 @@ Other BASELINE.json configs (``--config``; per-GPU shapes are the 8-GPU configs 
 * ``tron``:  Poisson + L2, TRON (one STEP = one outer trust-region iteration incl. its Hessian-vector CG passes),
   62.5M rows/GPU x 1M features (config "Poisson regression TRON, 500M rows, 8 GPUs").
 
-Usage: python bench.py [--gpus N --steps K --warmup W] [--config lbfgs|owlqn|tron]; for N > 1 launch with
-torch.distributed.run.
+Usage: python bench.py [--gpus N --steps K --warmup W] [--config lbfgs|owlqn|tron]; for N > 1 either launch with
+torch.distributed.run (one rank per GPU) or let bench.py start that launcher itself as a child process.
 """
 from __future__ import annotations
 
@@ -75,12 +75,16 @@ def main():
         args.rows_per_gpu = cfg["rows_per_gpu"]
     if args.features is None:
         args.features = cfg["features"]
+    # --gpus N without a launcher: run N ranks under torch.distributed.run as a child (before any GPU call)
+    from photon_ml_amd.parallel.launch import relaunch_if_needed
+    rc = relaunch_if_needed(args.gpus, __file__, sys.argv[1:])
+    if rc is not None:
+        sys.exit(rc)
 
     import torch
     from photon_ml_amd.parallel.dist import init_distributed, DistributedGLMData, all_reduce_scalar, barrier, is_dist
     rank, world, local = init_distributed()
-    if world != args.gpus:
-        log(f"warning: --gpus {args.gpus} but WORLD_SIZE={world}; using WORLD_SIZE")
+    assert world == args.gpus, (world, args.gpus)
     local = local % max(torch.cuda.device_count(), 1)  # several ranks may share a GPU in rehearsal runs
     torch.cuda.set_device(local)
     dev = torch.device("cuda", local)

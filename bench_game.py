@@ -20,7 +20,7 @@ GPUs -> 1.25M entities per GPU, 20 rows x 50 features per entity covering each e
 ``--config game5pl`` = the same with power-law entity sizes (see ``generate_game_bench_data(sizes="powerlaw")``).
 
 Usage: python bench_game.py [--gpus N --steps K --warmup W] [--config small|game5|game5pl]; for N > 1 launch with
-torch.distributed.run.
+torch.distributed.run, or let the script start that launcher itself as a child process.
 """
 from __future__ import annotations
 
@@ -77,12 +77,18 @@ def main():
     for k, v in PRESETS[args.config].items():
         if getattr(args, k) is None:
             setattr(args, k, v)
+    # --gpus N without a launcher: run N ranks under torch.distributed.run as a child (before any GPU call)
+    from photon_ml_amd.parallel.launch import relaunch_if_needed
+    rc = relaunch_if_needed(args.gpus, __file__, sys.argv[1:])
+    if rc is not None:
+        sys.exit(rc)
 
     import numpy as np
     import torch
     from collections import OrderedDict
     from photon_ml_amd.parallel.dist import init_distributed, all_reduce_scalar, barrier, is_dist
     rank, world, local = init_distributed()
+    assert world == args.gpus, (world, args.gpus)
     if torch.cuda.is_available():
         local = local % torch.cuda.device_count()  # several ranks may share a GPU in rehearsal runs
         torch.cuda.set_device(local)

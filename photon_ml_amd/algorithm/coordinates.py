@@ -235,6 +235,10 @@ class RandomEffectCoordinate(Coordinate):
         self._returned = None
         if getattr(self, "_rs", None) is not None:
             self._rs.beta = None
+        comps = getattr(self, "_comps", None)
+        if comps is not None and comps[1] is not None:
+            comps[1].W = None
+        self._sub_W = None
 
     def initialize_model(self):
         ds = self.dataset
@@ -318,12 +322,18 @@ class RandomEffectCoordinate(Coordinate):
                                  ds.entity_ids, ds.dim, keys, vals, variances)
 
     def _update_segmented(self, model, offs, l1: float, l2: float):
-        """All entities as one block-diagonal problem (``SegmentedGLMData``): one TRON / L-BFGS over the
-        concatenated per-entity coefficient vector, per-entity convergence via segment reductions."""
+        """All entities as one block-diagonal problem (``SegmentedGLMData``). With the fused primal TRON
+        available (``optimization/entity_tron.py``) the entities are split into components — row-space batch,
+        fused per-entity TRON, leftover pass-path subset — each keeping its own solver state
+        (:meth:`_update_components`); otherwise one TRON / L-BFGS over the concatenated per-entity coefficient
+        vector with the row-space batch frozen."""
         ds, cfg = self.dataset, self.opt_config
         seg = ds.seg
         seg.o = offs.to(seg.y.device, torch.float64)[ds.seg_rows]
         seg._dzz_key = None
+        comps = self._components(l1, cfg.optimizer_config)
+        if comps is not None:
+            return self._update_components(comps, model, l1, l2)
         # previous update kept only beta (lazy primal model): the row-space solve warm-starts from it directly
         prev_lazy = self._W.get("seg") is _RS_WARM
         W0 = None if prev_lazy else self._warm_start_segmented(model)
@@ -419,6 +429,131 @@ class RandomEffectCoordinate(Coordinate):
         out = RandomEffectModel(self.data_config.random_effect_type, self.data_config.feature_shard_id, self.task,
                                 ds.entity_ids, ds.dim, ds.projection_keys_t, W, var)
         self._last = (out, res.W)
+        return out
+
+    def _components(self, l1: float, oc):
+        """Solver components of the segmented coordinate, built once per dataset: ``(rs, fused, sub)`` = the
+        row-space batch (wide entities, ``row_space.py``), the fused per-entity primal TRON batch
+        (``entity_tron.py``) and the leftover entities as a block-diagonal sub-problem for the pass path (any of
+        them None when empty). None when the fused primal TRON does not apply to this configuration or the
+        segmented CSR was already released by an earlier split."""
+        from ..optimization.entity_tron import EntityTronBatch, fused_eligible
+        opt = "TRON" if oc.optimizer_type == OptimizerType.TRON else "LBFGS"
+        ds = self.dataset
+        seg = ds.seg
+        if not fused_eligible(self.loss, opt, l1, oc.constraint_map, seg.y.device):
+            return None
+        cached = getattr(self, "_comps", None)
+        if cached is not None:
+            return cached
+        if getattr(ds, "_seg_csr", None) is None:
+            return None
+        with Timed(f"RE {self.coordinate_id}: solver components", log, logging.DEBUG):
+            rs = self._row_space(l1, oc)
+            rs = rs if rs is not None and rs.B else None
+            n_e = seg.row_ptr[1:] - seg.row_ptr[:-1]
+            done = rs.mask.clone() if rs is not None else torch.zeros(seg.B, dtype=torch.bool, device=seg.y.device)
+            fused = EntityTronBatch(ds, (~done) & (n_e > 0))
+            if fused.B:
+                done |= fused.mask
+            else:
+                fused = None
+            rest = (~done) & (n_e > 0)
+            sub = ds.entity_subset(rest) if bool(rest.any()) else None
+            ds.release_csr()
+        self._comps = (rs, fused, sub)
+        self._sub_W = None
+        log.debug("RE %s: %d row-space, %d fused primal, %d pass-path entities", self.coordinate_id,
+                  0 if rs is None else rs.B, 0 if fused is None else fused.B,
+                  0 if sub is None else sub.entities.numel())
+        return self._comps
+
+    def _update_components(self, comps, model, l1: float, l2: float):
+        """One update over the solver components (see :meth:`_components`). Each component warm-starts from its
+        own last solution (the row-space beta, the fused batch's packed W, the subset's W) unless the starting
+        model is not the one this coordinate returned last — then from that model's coefficients. Scores come
+        out of the solves (row space: L beta; fused: the kernel's margins; pass path: one forward pass over the
+        subset only), and the primal coefficient vector is assembled only when the model is read."""
+        from ..optimization.batched import batched_tron
+        rs, fused, sub = comps
+        ds, oc = self.dataset, self.opt_config.optimizer_config
+        seg = ds.seg
+        dev = seg.y.device
+        warm = self._W.get("seg")
+        foreign = warm is not _RS_WARM and model is not None and model.nnz > 0
+        W0 = self._warm_start_segmented(model) if foreign else None
+        t_start = time.time()
+        iters = torch.zeros(seg.B, dtype=torch.long, device=dev)
+        reasons = torch.zeros_like(iters)
+        z = torch.zeros(seg.y.numel(), dtype=torch.float64, device=dev)     # x.w per row (segmented order)
+        sum_sq = torch.zeros((), dtype=torch.float64, device=dev)
+        parts = {}
+        if rs is not None:
+            with Timed(f"RE {self.coordinate_id}: row-space solve", log, logging.DEBUG):
+                rres = rs.solve(self.loss, l2, "TRON", W0, oc.tolerance, oc.maximum_iterations,
+                                reuse_beta=not foreign)
+                _sync(rres.W)
+            iters.index_copy_(0, rs.ents, rres.iters)
+            reasons.index_copy_(0, rs.ents, rres.reason)
+            z += rs.margins(rres.W)
+            sum_sq += torch.where(rs.valid, rres.W, torch.zeros_like(rres.W)).square().sum()
+            parts["rs"] = rres.W
+        if fused is not None:
+            with Timed(f"RE {self.coordinate_id}: fused primal solve", log, logging.DEBUG):
+                fres = fused.solve(self.loss, l2, None if W0 is None else W0[fused.cols], seg.o[fused.rows],
+                                   oc.tolerance, oc.maximum_iterations)
+                _sync(fres.W)
+            iters.index_copy_(0, fused.ents, fres.iters)
+            reasons.index_copy_(0, fused.ents, fres.reason)
+            z.index_copy_(0, fused.rows, fres.z)
+            sum_sq += fres.W.square().sum()
+            parts["fused"] = fres.W
+        if sub is not None:
+            with Timed(f"RE {self.coordinate_id}: primal block-diagonal solve", log, logging.DEBUG):
+                if W0 is not None:
+                    W0s = W0[sub.cols].contiguous()
+                elif getattr(self, "_sub_W", None) is not None:
+                    W0s = self._sub_W
+                else:
+                    W0s = torch.zeros(sub.cols.numel(), dtype=torch.float64, device=dev)
+                sub.seg.o = seg.o[sub.rows]
+                sub.seg._dzz_key = None
+                res = batched_tron(sub.seg, self.loss, l2, W0s, oc.tolerance, oc.maximum_iterations)
+                _sync(res.W)
+            self._sub_W = res.W
+            iters.index_copy_(0, sub.entities, res.iters)
+            reasons.index_copy_(0, sub.entities, res.reason)
+            z.index_copy_(0, sub.rows, sub.seg.glm.matvec(res.W))
+            sum_sq += res.W.square().sum()
+            parts["sub"] = res.W
+        del W0
+
+        def primal(parts=parts):
+            """The primal coefficient vector over all entities (projected keys order)."""
+            W = rs.to_primal(parts["rs"]) if "rs" in parts else torch.zeros(ds.d_total, dtype=torch.float64,
+                                                                                device=dev)
+            if "fused" in parts:
+                W.index_copy_(0, fused.cols, parts["fused"])
+            if "sub" in parts:
+                W.index_copy_(0, sub.cols, parts["sub"])
+            return W
+
+        self._W["seg"] = _RS_WARM
+        self._rs_scores = z
+        act = self._active_mask(dev)
+        self.last_stats = random_effect_tracker_stats(iters[act], reasons[act], time.time() - t_start)
+        need_var = self.compute_variance and self.loss.twice_differentiable
+        if need_var:
+            W = primal()
+            var = 1.0 / (seg.hdiag(self.loss, W, l2) + EPSILON)
+            out = RandomEffectModel(self.data_config.random_effect_type, self.data_config.feature_shard_id,
+                                    self.task, ds.entity_ids, ds.dim, ds.projection_keys_t, W, var)
+        else:
+            self._lazy_W = primal
+            out = RandomEffectModel(self.data_config.random_effect_type, self.data_config.feature_shard_id,
+                                    self.task, ds.entity_ids, ds.dim, ds.projection_keys_t, primal, None,
+                                    sum_sq=float(sum_sq))
+        self._last = (out, None)
         return out
 
     def _active_mask(self, device) -> torch.Tensor:

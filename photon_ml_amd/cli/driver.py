@@ -91,8 +91,11 @@ def build_parser() -> argparse.ArgumentParser:
     p.add_argument("--coefficient-box-constraints")
     p.add_argument("--data-validation-type", default="VALIDATE_FULL")
     p.add_argument("--tree-aggregate-depth", type=int, default=1,
-                   help="accepted for compatibility, no effect: the Spark treeAggregate depth has no analogue; "
-                        "gradients are all-reduced by RCCL, which picks ring / tree itself")
+                   help="reduction depth of the reference's treeAggregate: >= 2 selects RCCL's tree all-reduce "
+                        "(unless --allreduce-algo says otherwise), 1 leaves the choice to RCCL")
+    p.add_argument("--allreduce-algo", choices=["auto", "ring", "tree"], default=None,
+                   help="RCCL all-reduce algorithm of the gradient reduction (NCCL_ALGO); default: from "
+                        "--tree-aggregate-depth")
     p.add_argument("--diagnostic-mode", default="NONE")
     p.add_argument("--training-diagnostics", type=parse_bool, default=None,
                    help="deprecated alias: true -> --diagnostic-mode ALL")
@@ -381,7 +384,10 @@ def read_text_model(path: str) -> Dict[float, Dict[Tuple[str, str], float]]:
 
 
 def main(argv=None) -> int:
-    Driver(parse_args_with_config(build_parser(), argv)).run()
+    args = parse_args_with_config(build_parser(), argv)
+    from ..parallel.dist import set_allreduce_algo
+    set_allreduce_algo(args.allreduce_algo, args.tree_aggregate_depth)
+    Driver(args).run()
     return 0
 
 

@@ -103,8 +103,11 @@ def build_parser() -> argparse.ArgumentParser:
     p.add_argument("--normalization", default="NONE")
     p.add_argument("--data-summary-directory")
     p.add_argument("--tree-aggregate-depth", type=int, default=1,
-                   help="accepted for compatibility, no effect: the Spark treeAggregate depth has no analogue; "
-                        "gradients are all-reduced by RCCL, which picks ring / tree itself")
+                   help="reduction depth of the reference's treeAggregate: >= 2 selects RCCL's tree all-reduce "
+                        "(unless --allreduce-algo says otherwise), 1 leaves the choice to RCCL")
+    p.add_argument("--allreduce-algo", choices=["auto", "ring", "tree"], default=None,
+                   help="RCCL all-reduce algorithm of the gradient reduction (NCCL_ALGO); default: from "
+                        "--tree-aggregate-depth")
     p.add_argument("--hyper-parameter-tuning", default="NONE")
     p.add_argument("--hyper-parameter-tuning-iterations", type=int, default=0)
     p.add_argument("--hyper-parameter-tuning-range", default="1e-4-1e4")
@@ -379,7 +382,8 @@ def optimization_config_to_string(config, coord_configs=None) -> str:
 def main(argv=None) -> int:
     args = parse_args_with_config(build_parser(), argv)
     if "LOCAL_RANK" in os.environ or "RANK" in os.environ:
-        from ..parallel.dist import init_distributed
+        from ..parallel.dist import init_distributed, set_allreduce_algo
+        set_allreduce_algo(args.allreduce_algo, args.tree_aggregate_depth)
         init_distributed()
     with Timed("Total time in training Driver"):
         GameTrainingDriver(args).run()

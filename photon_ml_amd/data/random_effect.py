@@ -454,6 +454,30 @@ class RandomEffectDataset:
         from ..ops.backend import make_glm_data
         from ..ops.device import DeviceGLMData
         from ..optimization.batched import SegmentedGLMData
+        seg = self.seg
+        sip, spos, sval, row_sel, col_sel, ent_new = self.entity_csr(mask)
+        dev = seg.y.device
+        mask = mask.to(dev)
+        B = int(mask.sum())
+        d_sub = int(col_sel.numel())
+        yy, ww = seg.y[row_sel], seg.w[row_sel]
+        if dev.type == "cuda":
+            glm = DeviceGLMData.from_device_csr(sip, spos, sval, yy, torch.zeros_like(yy), ww, max(d_sub, 1), dev,
+                                                "f64", col_windows=True)
+        else:
+            from .matrix import LabeledData as _LD
+            xs = sp.csr_matrix((sval.numpy(), spos.numpy(), sip.numpy()), shape=(row_sel.numel(), max(d_sub, 1)))
+            glm = make_glm_data(_LD(xs, yy.numpy(), np.zeros(row_sel.numel()), ww.numpy()), dev, "f64",
+                                col_windows=True)
+        sub = SegmentedGLMData(glm, ent_new[seg.row_entity[row_sel]], ent_new[seg.col_entity[col_sel]], B, yy, ww,
+                               torch.zeros_like(yy))
+        return SegmentSubset(sub, row_sel, col_sel, torch.nonzero(mask).squeeze(1))
+
+    def entity_csr(self, mask: torch.Tensor):
+        """Raw block-diagonal CSR of the entities in ``mask`` (from the kept segmented CSR, on the data's device):
+        ``(indptr, columns, values, row_sel, col_sel, ent_new)`` — int64 indptr over the selected rows, int64
+        columns renumbered to the selected coefficients (each entity's range stays contiguous), fp64 values; the
+        parent row / coefficient positions of the selection; and the parent-entity -> subset-entity numbering."""
         if getattr(self, "_seg_csr", None) is None:
             raise RuntimeError("entity_subset needs the segmented CSR (built once per dataset)")
         seg = self.seg
@@ -472,22 +496,9 @@ class RandomEffectDataset:
         src = torch.repeat_interleave(nip_d[:-1][row_sel] - sip[:-1], lens, output_size=nnz) + torch.arange(
             nnz, device=dev)
         spos = newcol[pos_d[src]]
-        sval = val_d[src]
+        sval = val_d[src].to(torch.float64)
         ent_new = torch.cumsum(mask.to(torch.int64), 0) - 1
-        B = int(mask.sum())
-        d_sub = int(col_sel.numel())
-        yy, ww = seg.y[row_sel], seg.w[row_sel]
-        if dev.type == "cuda":
-            glm = DeviceGLMData.from_device_csr(sip, spos, sval, yy, torch.zeros_like(yy), ww, max(d_sub, 1), dev,
-                                                "f64", col_windows=True)
-        else:
-            from .matrix import LabeledData as _LD
-            xs = sp.csr_matrix((sval.numpy(), spos.numpy(), sip.numpy()), shape=(row_sel.numel(), max(d_sub, 1)))
-            glm = make_glm_data(_LD(xs, yy.numpy(), np.zeros(row_sel.numel()), ww.numpy()), dev, "f64",
-                                col_windows=True)
-        sub = SegmentedGLMData(glm, ent_new[seg.row_entity[row_sel]], ent_new[seg.col_entity[col_sel]], B, yy, ww,
-                               torch.zeros_like(yy))
-        return SegmentSubset(sub, row_sel, col_sel, torch.nonzero(mask).squeeze(1))
+        return sip, spos, sval, row_sel, col_sel, ent_new
 
     def release_csr(self):
         self._seg_csr = None

@@ -102,7 +102,10 @@ class GameEstimator:
     def set_tree_aggregate_depth(self, d: int):
         if d <= 0:
             raise ValueError("tree aggregate depth must be > 0")
-        self.tree_aggregate_depth = d  # RCCL chooses ring/tree itself; kept for API parity
+        self.tree_aggregate_depth = d
+        # the reduction-shape knob maps to the RCCL all-reduce algorithm (depth >= 2 -> tree, else RCCL's choice)
+        from ..parallel.dist import set_allreduce_algo
+        set_allreduce_algo(tree_depth=d)
         return self
 
     def set_validation_evaluators(self, evs):

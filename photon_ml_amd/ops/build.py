@@ -19,6 +19,7 @@ PKG = Path(__file__).resolve().parents[1]
 HIP_SOURCES = {
     "glm": PKG / "ops" / "csrc" / "glm_kernels.hip",
     "game": PKG / "ops" / "csrc" / "game_kernels.hip",
+    "re": PKG / "ops" / "csrc" / "re_kernels.hip",
 }
 CPP_SOURCES = {
     "avro": PKG / "io" / "csrc" / "avro_codec.cpp",

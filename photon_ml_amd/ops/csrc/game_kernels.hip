@@ -352,7 +352,7 @@ int pml_gemm_nt(int M, int N, int K, const double* A, int lda, const double* Bm,
 int pml_seg_gram(int B, int n, int dmax, const long long* ents, const long long* row_ptr, const long long* col_ptr,
                  const long long* nip, const long long* pos, const double* val, double* K, void* stream) {
   if (B <= 0) return 0;
-  if (n < 1 || n > 64 || dmax < 0 || (size_t)dmax * sizeof(double) > 65536) return -22;
+  if (n < 1 || n > 64 || dmax < 0 || (size_t)dmax * sizeof(double) > 160 * 1024) return -22;
   hipLaunchKernelGGL(seg_gram_kernel, dim3((unsigned)B), dim3(64), (size_t)std::max(dmax, 1) * sizeof(double),
                      (hipStream_t)stream, B, n, ents, row_ptr, col_ptr, nip, pos, val, K);
   LAUNCH_CHECK();

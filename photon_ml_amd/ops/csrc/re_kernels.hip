@@ -1,0 +1,406 @@
+// photon_ml_amd — CDNA4 (gfx950 / MI355X) fused per-entity PRIMAL TRON for random effects.
+//
+// The reference solves every random-effect entity as its own small GLM (photon-api/.../algorithm/
+// RandomEffectCoordinate.scala:103-143 -> optimization/SingleNodeOptimizationProblem.scala:85-103 -> photon-lib/
+// .../optimization/TRON.scala:80-340). Entities with few rows are solved in their row space (rs_tron in
+// glm_kernels.hip); this file handles the others — typically 65 .. thousands of rows over ~1k projected
+// coefficients — WITHOUT a pass-per-Hessian-vector launch sequence over the whole block-diagonal problem:
+//
+// * one workgroup (4 waves) owns one entity for its whole solve: the coefficient-space vectors (w, g, step, r,
+//   d) and one accumulator per wave live in LDS (d_e <= dmax doubles each); the TRON control flow (truncated CG,
+//   trust-region radius, accept / reject, Photon convergence tests) runs on workgroup-uniform scalars;
+// * every Hessian-vector product X^T (D (X d)) is ONE read of the entity's CSR rows (a wave per row, lane k =
+//   non-zero k of the row: gather d[c] from LDS, DPP wave sum, scale by the cached D_i = w_i l''(z_i), scatter
+//   t x_ik into the wave's private LDS accumulator). The block-diagonal pass path reads the rows twice (CSR
+//   forward + CSC transpose copy) per product and launches per pass; here there is no CSC copy at all;
+// * deterministic: fixed-order DPP / readlane wave sums, per-wave accumulators combined in wave order, distinct
+//   columns inside a row (so one ds_add_f64 never has two lanes on one address within a row);
+// * per-row scratch in HBM: D and the margins x_i.w for the current iterate and the trial point (swapped on
+//   acceptance), so the final margins come out of the solve (scores without another pass).
+//
+// Semantics follow batched_tron / rs_tron_kernel: eta = (1e-4, .25, .75), sigma = (.25, .5, 4), delta0 = ||g0||,
+// first-iteration delta = min(delta, ||step||), CG tolerance 0.1 ||g||, <= max_cg CG steps, <= max_fail
+// consecutive rejections; reason codes 1 max-iter, 2 not-improving, 3 f-converged, 4 g-converged; tolerances
+// from the state at zero coefficients (photon-lib/.../optimization/Optimizer.scala:136-196).
+//
+// Built with: hipcc --offload-arch=gfx950 -O3 -shared -fPIC (photon_ml_amd/ops/build.py). C ABI, ctypes.
+
+#include <hip/hip_runtime.h>
+#include <stdint.h>
+
+#define LAUNCH_CHECK()                                         \
+  do {                                                         \
+    hipError_t e_ = hipGetLastError();                         \
+    if (e_ != hipSuccess) return (int)e_;                      \
+  } while (0)
+
+#define RE_NW 4                 // waves per workgroup (one entity)
+#define RE_THREADS (RE_NW * 64)
+#define RE_R 4                  // rows in flight per wave
+
+enum { LOSS_LOGISTIC = 0, LOSS_POISSON = 1, LOSS_SQUARED = 2 };
+
+__device__ __forceinline__ double log1p_exp(double x) { return x > 0.0 ? x + log1p(exp(-x)) : log1p(exp(x)); }
+
+__device__ __forceinline__ void pointwise_loss(int loss, double z, double y, double& l, double& dl, double& d2) {
+  if (loss == LOSS_LOGISTIC) {
+    const double s = 1.0 / (1.0 + exp(-z));
+    if (y > 0.5) { l = log1p_exp(-z); dl = s - 1.0; }
+    else { l = log1p_exp(z); dl = s; }
+    d2 = s * (1.0 - s);
+  } else if (loss == LOSS_POISSON) {
+    const double e = exp(z);
+    l = e - y * z; dl = e - y; d2 = e;
+  } else {
+    const double d = z - y;
+    l = 0.5 * d * d; dl = d; d2 = 1.0;
+  }
+}
+
+template <int CTRL>
+__device__ __forceinline__ double dpp_f64(double v) {
+  const long long b = __builtin_bit_cast(long long, v);
+  const int lo = __builtin_amdgcn_update_dpp(0, (int)b, CTRL, 0xF, 0xF, true);
+  const int hi = __builtin_amdgcn_update_dpp(0, (int)(b >> 32), CTRL, 0xF, 0xF, true);
+  return __builtin_bit_cast(double, ((long long)hi << 32) | (long long)(unsigned int)lo);
+}
+
+__device__ __forceinline__ double readlane_f64(double v, int l) {
+  const long long b = __builtin_bit_cast(long long, v);
+  const int lo = __builtin_amdgcn_readlane((int)b, l);
+  const int hi = __builtin_amdgcn_readlane((int)(b >> 32), l);
+  return __builtin_bit_cast(double, ((long long)hi << 32) | (long long)(unsigned int)lo);
+}
+
+// Sum over the 64 lanes of a wave, returned (bitwise identical) in every lane: DPP butterflies inside each
+// 16-lane row (every lane then holds its row's sum), then the four row sums in a fixed order.
+__device__ __forceinline__ double wave_total(double v) {
+  v += dpp_f64<0xB1>(v);    // quad_perm [1,0,3,2]
+  v += dpp_f64<0x4E>(v);    // quad_perm [2,3,0,1]
+  v += dpp_f64<0x141>(v);   // row_half_mirror
+  v += dpp_f64<0x140>(v);   // row_mirror
+  return (readlane_f64(v, 0) + readlane_f64(v, 16)) + (readlane_f64(v, 32) + readlane_f64(v, 48));
+}
+
+// Workgroup sums of K values (K <= 4), in every thread. ``red`` holds two [RE_NW][4] slots used alternately,
+// so one barrier per call suffices: a slot is rewritten only two calls later, after every thread has passed
+// the barrier of the call in between (all threads run the same, workgroup-uniform control flow).
+template <int K>
+__device__ __forceinline__ void block_sums(double (&v)[K], double* __restrict__ red, int& parity) {
+  const int lane = threadIdx.x & 63, w = threadIdx.x >> 6;
+#pragma unroll
+  for (int k = 0; k < K; ++k) v[k] = wave_total(v[k]);
+  double* slot = red + parity * (RE_NW * 4);
+  if (lane == 0) {
+#pragma unroll
+    for (int k = 0; k < K; ++k) slot[w * 4 + k] = v[k];
+  }
+  __syncthreads();
+#pragma unroll
+  for (int k = 0; k < K; ++k) {
+    double s = 0.0;
+#pragma unroll
+    for (int q = 0; q < RE_NW; ++q) s += slot[q * 4 + k];
+    v[k] = s;
+  }
+  parity ^= 1;
+}
+
+struct ReTronArgs {
+  const int* order;          // launch slot -> entity (largest entities first)
+  int n_launch;
+  const long long* row_ptr;  // [E + 1] entity row ranges
+  const long long* col_ptr;  // [E + 1] entity coefficient ranges (packed W)
+  const long long* nip;      // [N + 1] row -> non-zero range
+  const uint16_t* lcol;      // entity-local column of every non-zero (< d_e, distinct inside a row)
+  const double* val;         // value of every non-zero
+  const double* y;           // per-row label / offset / weight
+  const double* off;
+  const double* wt;
+  double* scr;               // per-row scratch [4][n_rows]: D (2 buffers), margins x.w (2 buffers)
+  long long n_rows;
+  double* W;                 // packed coefficients: in = warm start, out = solution
+  double* f;                 // per entity: final objective, iterations, reason code
+  int* iters;
+  int* reason;
+  double* zout;              // per row: x_i . w of the solution (no offset)
+  int loss;
+  double l2, tol;
+  int max_iter, max_fail, max_cg, dmax;
+};
+
+// One pass over the entity's rows [r0, r1).
+// MODE 0: Hessian-vector data term: acc_w += X^T (Dc * (X vec)).
+// MODE 1: value + gradient at vec: acc_w += X^T (wt * l'), fpart += wt * l (lane 0), Dn = wt * l'', Zn = x.vec.
+// MODE 2: value + gradient at zero (no gathers, no scratch writes).
+template <int MODE>
+__device__ __forceinline__ void row_pass(const ReTronArgs& a, long long r0, long long r1,
+                                         const double* __restrict__ vec, double* __restrict__ acc,
+                                         const double* __restrict__ Dc, double* __restrict__ Dn,
+                                         double* __restrict__ Zn, double& fpart) {
+  const int lane = threadIdx.x & 63, w = threadIdx.x >> 6;
+  for (long long base = r0 + (long long)w * RE_R; base < r1; base += (long long)RE_NW * RE_R) {
+    long long lo[RE_R], hi[RE_R];
+    int c[RE_R];
+    double v[RE_R], dot[RE_R], t[RE_R];
+#pragma unroll
+    for (int q = 0; q < RE_R; ++q) {
+      const long long i = base + q;
+      lo[q] = i < r1 ? a.nip[i] : 0;
+      hi[q] = i < r1 ? a.nip[i + 1] : 0;
+    }
+#pragma unroll
+    for (int q = 0; q < RE_R; ++q) {
+      const long long p = lo[q] + lane;
+      const bool in = p < hi[q];
+      c[q] = in ? (int)a.lcol[p] : 0;
+      v[q] = in ? a.val[p] : 0.0;
+    }
+#pragma unroll
+    for (int q = 0; q < RE_R; ++q) {
+      dot[q] = MODE == 2 ? 0.0 : v[q] * vec[c[q]];
+      if (MODE != 2) {
+        for (long long p = lo[q] + 64 + lane; p < hi[q]; p += 64) dot[q] = fma(a.val[p], vec[a.lcol[p]], dot[q]);
+      }
+    }
+#pragma unroll
+    for (int q = 0; q < RE_R; ++q) {
+      if (MODE != 2) dot[q] = wave_total(dot[q]);
+      const long long i = base + q;
+      const bool valid = i < r1;
+      if (MODE == 0) {
+        t[q] = valid ? Dc[i] * dot[q] : 0.0;
+      } else {
+        double l = 0.0, dl = 0.0, d2 = 0.0, wi = 0.0;
+        if (valid) {
+          wi = a.wt[i];
+          pointwise_loss(a.loss, dot[q] + a.off[i], a.y[i], l, dl, d2);
+          if (lane == 0) {
+            fpart += wi * l;
+            if (MODE == 1) { Dn[i] = wi * d2; Zn[i] = dot[q]; }
+          }
+        }
+        t[q] = wi * dl;
+      }
+    }
+#pragma unroll
+    for (int q = 0; q < RE_R; ++q) {
+      if (lo[q] + lane < hi[q]) atomicAdd(&acc[c[q]], t[q] * v[q]);
+      for (long long p = lo[q] + 64 + lane; p < hi[q]; p += 64) atomicAdd(&acc[a.lcol[p]], t[q] * a.val[p]);
+    }
+  }
+}
+
+__global__ __launch_bounds__(RE_THREADS) void re_tron_csr_kernel(ReTronArgs a) {
+  extern __shared__ __attribute__((aligned(16))) double smem[];
+  const int e = a.order[blockIdx.x];
+  const long long r0 = a.row_ptr[e], r1 = a.row_ptr[e + 1];
+  const long long c0 = a.col_ptr[e];
+  const int d = (int)(a.col_ptr[e + 1] - c0);
+  const int tid = threadIdx.x, w = tid >> 6, lane = tid & 63;
+  const int dm = a.dmax;
+  double* sW = smem;
+  double* sG = sW + dm;
+  double* sS = sG + dm;     // CG step
+  double* sR = sS + dm;     // CG residual
+  double* sD = sR + dm;     // CG direction; trial point during the function evaluation
+  double* acc = sD + dm;    // RE_NW accumulators; acc[0 .. d) = combined Hd (with l2 d) / trial gradient
+  double* red = acc + RE_NW * dm;
+  double* myacc = acc + w * dm;
+  double* D[2] = {a.scr, a.scr + a.n_rows};
+  double* Z[2] = {a.scr + 2 * a.n_rows, a.scr + 3 * a.n_rows};
+  int cur = 0, parity = 0;
+  double* Wg = a.W + c0;
+
+  // combine the wave accumulators into acc[0] (+ l2 * src), zeroing the others for the next pass
+  auto combine = [&](const double* __restrict__ src) {
+    __syncthreads();
+    for (int j = tid; j < d; j += RE_THREADS) {
+      double s = acc[j];
+#pragma unroll
+      for (int q = 1; q < RE_NW; ++q) s += acc[q * dm + j];
+      acc[j] = s + a.l2 * src[j];
+    }
+    __syncthreads();
+  };
+  auto zero_own = [&]() {
+    for (int j = lane; j < d; j += 64) myacc[j] = 0.0;
+  };
+  // value + gradient at vec (MODE 1: writes D / Z buffer ``nb``), gradient into acc[0 .. d)
+  auto value_grad = [&](const double* vec, int nb, bool at_zero) -> double {
+    __syncthreads();
+    zero_own();
+    double fp = 0.0;
+    if (at_zero) row_pass<2>(a, r0, r1, vec, myacc, nullptr, nullptr, nullptr, fp);
+    else row_pass<1>(a, r0, r1, vec, myacc, nullptr, D[nb], Z[nb], fp);
+    double reg = 0.0;
+    for (int j = tid; j < d; j += RE_THREADS) reg += vec[j] * vec[j];
+    double s2[2] = {fp, reg};
+    block_sums<2>(s2, red, parity);
+    combine(vec);
+    return s2[0] + 0.5 * a.l2 * s2[1];
+  };
+
+  for (int j = tid; j < d; j += RE_THREADS) sW[j] = Wg[j];
+  __syncthreads();
+  double f = value_grad(sW, cur, false);
+  double nz = 0.0, gg = 0.0;
+  for (int j = tid; j < d; j += RE_THREADS) {
+    sG[j] = acc[j];
+    nz += sW[j] != 0.0 ? 1.0 : 0.0;
+    gg += acc[j] * acc[j];
+  }
+  double s2[2] = {nz, gg};
+  block_sums<2>(s2, red, parity);
+  double f0z = f, g0n = sqrt(s2[1]);
+  if (s2[0] != 0.0) {
+    for (int j = tid; j < d; j += RE_THREADS) sS[j] = 0.0;   // zero vector for the state at zero
+    f0z = value_grad(sS, 0, true);
+    double g0[1] = {0.0};
+    for (int j = tid; j < d; j += RE_THREADS) g0[0] += acc[j] * acc[j];
+    block_sums<1>(g0, red, parity);
+    g0n = sqrt(g0[0]);
+  }
+  const double loss_tol = f0z * a.tol, grad_tol = g0n * a.tol;
+  double delta = sqrt(s2[1]);
+  int it = 0, fails = 0, reason = 0;
+  bool active = true;
+  if (delta == 0.0) { reason = 4; active = false; }
+  const double eta0 = 1e-4, eta1 = 0.25, eta2 = 0.75, sg1 = 0.25, sg2 = 0.5, sg3 = 4.0;
+  const int guard_max = a.max_iter * (a.max_fail + 1) + 5;
+  double gnorm2 = s2[1];
+  for (int guard = 0; active && guard < guard_max; ++guard) {
+    // ---- truncated CG at W (Hessian weights D[cur])
+    for (int j = tid; j < d; j += RE_THREADS) {
+      sS[j] = 0.0;
+      sR[j] = -sG[j];
+      sD[j] = -sG[j];
+    }
+    double rtr = gnorm2;
+    const double cg_tol = 0.1 * sqrt(gnorm2);
+    for (int k = 0; k < a.max_cg; ++k) {
+      if (!(sqrt(rtr > 0.0 ? rtr : 0.0) > cg_tol)) break;
+      __syncthreads();
+      zero_own();
+      double fp = 0.0;
+      row_pass<0>(a, r0, r1, sD, myacc, D[cur], nullptr, nullptr, fp);
+      combine(sD);                                   // acc[0 .. d) = Hd + l2 d
+      double s4[4] = {0.0, 0.0, 0.0, 0.0};
+      for (int j = tid; j < d; j += RE_THREADS) {
+        const double dj = sD[j], sj = sS[j];
+        s4[0] += dj * acc[j];
+        s4[1] += sj * dj;
+        s4[2] += sj * sj;
+        s4[3] += dj * dj;
+      }
+      block_sums<4>(s4, red, parity);
+      const double dhd = s4[0], std_ = s4[1], sts = s4[2], dtd = s4[3];
+      const double alpha = rtr / (dhd == 0.0 ? 1.0 : dhd);
+      double tn[1] = {0.0};
+      for (int j = tid; j < d; j += RE_THREADS) {
+        const double tr = sS[j] + alpha * sD[j];
+        tn[0] += tr * tr;
+      }
+      block_sums<1>(tn, red, parity);
+      const bool hit = sqrt(tn[0] > 0.0 ? tn[0] : 0.0) > delta;
+      double al = alpha;
+      if (hit) {
+        const double dsq = delta * delta;
+        const double q = std_ * std_ + dtd * (dsq - sts);
+        const double rad = sqrt(q > 0.0 ? q : 0.0);
+        const double den1 = std_ + rad;
+        al = std_ >= 0.0 ? (dsq - sts) / (den1 > 1e-300 ? den1 : 1e-300) : (rad - std_) / (dtd > 1e-300 ? dtd : 1e-300);
+      }
+      double rn[1] = {0.0};
+      for (int j = tid; j < d; j += RE_THREADS) {
+        sS[j] += al * sD[j];
+        const double r = sR[j] - al * acc[j];
+        sR[j] = r;
+        rn[0] += r * r;
+      }
+      block_sums<1>(rn, red, parity);
+      if (hit) break;
+      const double beta = rn[0] / (rtr == 0.0 ? 1.0 : rtr);
+      for (int j = tid; j < d; j += RE_THREADS) sD[j] = sR[j] + beta * sD[j];
+      rtr = rn[0];
+    }
+    // ---- trial point W + step (in the direction slot), trust-region update, acceptance
+    double s3[3] = {0.0, 0.0, 0.0};
+    for (int j = tid; j < d; j += RE_THREADS) {
+      const double sj = sS[j];
+      s3[0] += sG[j] * sj;
+      s3[1] += sj * sR[j];
+      s3[2] += sj * sj;
+      sD[j] = sW[j] + sj;
+    }
+    block_sums<3>(s3, red, parity);
+    const double gs = s3[0], pred = -0.5 * (gs - s3[1]), snorm = sqrt(s3[2]);
+    const double fn = value_grad(sD, cur ^ 1, false);   // trial gradient in acc[0 .. d)
+    const double actual = f - fn;
+    if (it == 0) delta = fmin(delta, snorm);
+    const double den = fn - f - gs;
+    const double alr = den <= 0.0 ? sg3 : fmax(sg1, -0.5 * gs / (den == 0.0 ? 1.0 : den));
+    double nd;
+    if (actual < eta0 * pred) nd = fmin(fmax(alr, sg1) * snorm, sg2 * delta);
+    else if (actual < eta1 * pred) nd = fmax(sg1 * delta, fmin(alr * snorm, sg2 * delta));
+    else if (actual < eta2 * pred) nd = fmax(sg1 * delta, fmin(alr * snorm, sg3 * delta));
+    else nd = fmax(delta, fmin(alr * snorm, sg3 * delta));
+    delta = nd;
+    const bool accept = actual > eta0 * pred;
+    const double f_prev = f;
+    if (accept) {
+      double g2[1] = {0.0};
+      for (int j = tid; j < d; j += RE_THREADS) {
+        sW[j] = sD[j];
+        const double gj = acc[j];
+        sG[j] = gj;
+        g2[0] += gj * gj;
+      }
+      block_sums<1>(g2, red, parity);
+      gnorm2 = g2[0];
+      f = fn;
+      cur ^= 1;
+      ++it;
+      fails = 0;
+    } else {
+      ++fails;
+    }
+    const bool not_impr = !accept && fails >= a.max_fail;
+    int rc = 0;
+    if (accept && sqrt(gnorm2) <= grad_tol) rc = 4;
+    if (accept && fabs(f - f_prev) <= loss_tol) rc = 3;
+    if (not_impr) rc = 2;
+    if ((accept || not_impr) && it >= a.max_iter) rc = 1;
+    if (rc > 0) { reason = rc; active = false; }
+  }
+  __syncthreads();
+  for (int j = tid; j < d; j += RE_THREADS) Wg[j] = sW[j];
+  if (a.zout != nullptr) {
+    const double* zc = Z[cur];
+    for (long long i = r0 + tid; i < r1; i += RE_THREADS) a.zout[i] = zc[i];
+  }
+  if (tid == 0) { a.f[e] = f; a.iters[e] = it; a.reason[e] = reason; }
+}
+
+extern "C" {
+
+// Shared memory of one workgroup for entities of at most ``dmax`` coefficients.
+size_t pml_re_tron_smem(int dmax) { return ((size_t)(5 + RE_NW) * dmax + 2 * RE_NW * 4) * sizeof(double); }
+
+int pml_re_tron_csr(const int* order, int n_launch, const long long* row_ptr, const long long* col_ptr,
+                    const long long* nip, const uint16_t* lcol, const double* val, const double* y,
+                    const double* off, const double* wt, double* scr, long long n_rows, double* W, double* f,
+                    int* iters, int* reason, double* zout, int loss, double l2, double tol, int max_iter,
+                    int max_fail, int max_cg, int dmax, hipStream_t st) {
+  if (n_launch <= 0) return 0;
+  if (dmax <= 0 || loss < 0 || loss > 2) return -22;
+  const size_t smem = pml_re_tron_smem(dmax);
+  if (smem > 160 * 1024) return -22;
+  ReTronArgs a{order, n_launch, row_ptr, col_ptr, nip, lcol, val, y, off, wt, scr, n_rows, W, f, iters, reason,
+               zout, loss, l2, tol, max_iter, max_fail, max_cg, dmax};
+  hipLaunchKernelGGL(re_tron_csr_kernel, dim3(n_launch), dim3(RE_THREADS), smem, st, a);
+  LAUNCH_CHECK();
+  return 0;
+}
+
+}  // extern "C"

@@ -496,12 +496,15 @@ def spmm_rows(x, PT: torch.Tensor) -> torch.Tensor:
     return Y
 
 
+SEG_GRAM_DMAX = 160 * 1024 // 8      # seg_gram_kernel's LDS image: one fp64 per projected column of the entity
+
+
 def seg_gram(ents: torch.Tensor, n: int, row_ptr: torch.Tensor, col_ptr: torch.Tensor, nip: torch.Tensor,
              pos: torch.Tensor, val: torch.Tensor) -> torch.Tensor:
     """Per-entity Gram matrices ``K [B, n, n]`` (``seg_gram_kernel``) of the entities ``ents`` of a block-diagonal
     CSR (rows grouped by entity: ``row_ptr``; entity column ranges: ``col_ptr``; ``nip/pos/val`` = int64 indptr,
     int64 global columns, fp64 values, distinct columns per row). Entities with fewer than ``n`` rows are zero
-    padded. Device only."""
+    padded. Every entity needs ``d_e <= SEG_GRAM_DMAX`` (LDS image). Device only."""
     lib = require_game_lib()
     dev = ents.device
     B = int(ents.numel())
@@ -513,6 +516,8 @@ def seg_gram(ents: torch.Tensor, n: int, row_ptr: torch.Tensor, col_ptr: torch.T
         assert x.dtype == torch.int64
     v = val.to(dev, torch.float64).contiguous()
     dmax = int((col_ptr[ents + 1] - col_ptr[ents]).max())
+    if dmax > SEG_GRAM_DMAX:
+        raise ValueError(f"seg_gram: an entity has {dmax} > {SEG_GRAM_DMAX} projected columns")
     check(lib.pml_seg_gram(B, n, dmax, t[0].data_ptr(), t[1].data_ptr(), t[2].data_ptr(), t[3].data_ptr(),
                            t[4].data_ptr(), v.data_ptr(), K.data_ptr(), stream_handle(dev)), "seg_gram")
     return K
@@ -530,6 +535,61 @@ def downsample_weights(y: torch.Tensor, w0: torch.Tensor, rate: float, binary: b
                              None if rowid is None else rowid.data_ptr(), y.numel(), seed & 0xFFFFFFFFFFFFFFFF,
                              float(rate), int(binary), out.data_ptr(), stream_handle(y.device)), "downsample")
     return out
+
+
+def re_lib() -> Optional[ctypes.CDLL]:
+    """Fused per-entity primal TRON (``ops/csrc/re_kernels.hip``)."""
+    lib = _load("re")
+    if lib is not None and not getattr(lib, "_pml_typed", False):
+        lib.pml_re_tron_csr.argtypes = ([c_void_p, c_int] + [c_void_p] * 9 + [ctypes.c_longlong] + [c_void_p] * 5
+                                        + [c_int, c_double, c_double, c_int, c_int, c_int, c_int, c_void_p])
+        lib.pml_re_tron_csr.restype = c_int
+        lib.pml_re_tron_smem.argtypes = [c_int]
+        lib.pml_re_tron_smem.restype = ctypes.c_size_t
+        lib._pml_typed = True
+    return lib
+
+
+def require_re_lib() -> ctypes.CDLL:
+    lib = re_lib()
+    if lib is None:
+        raise RuntimeError(
+            f"native random-effect kernel library missing ({lib_path('hip', 're')}); run python -m photon_ml_amd.ops.build")
+    return lib
+
+
+def re_tron_csr(order, row_ptr, col_ptr, nip, lcol, val, y, off, wt, scr, W, f, iters, reason, zout, loss_id: int,
+                l2: float, tol: float, max_iter: int, max_fail: int, max_cg: int, dmax: int) -> None:
+    """Fused per-entity primal TRON over the entities ``order`` (int32; one workgroup each) of a block-diagonal
+    CSR (``re_tron_csr_kernel``). Entity ``e`` owns rows ``row_ptr[e]:row_ptr[e+1]`` (int64) and coefficients
+    ``col_ptr[e]:col_ptr[e+1]`` of the packed ``W`` (fp64, in: warm start, out: solution); ``nip`` int64 row
+    pointers, ``lcol`` int16 entity-local columns (< d_e <= dmax, distinct inside a row), ``val`` fp64; ``y``,
+    ``off``, ``wt`` per row; ``scr`` fp64 scratch of 4 x rows; outputs ``f`` / ``iters`` / ``reason`` per
+    entity and ``zout`` (x_i . w per row). Device only; in place, nothing returned."""
+    lib = require_re_lib()
+    n_rows = y.numel()
+    B = int(order.numel())
+    ts = (order, row_ptr, col_ptr, nip, lcol, val, y, off, wt, scr, W, f, iters, reason, zout)
+    for t in ts:
+        assert t.is_cuda and t.is_contiguous() and t.device == W.device
+    assert order.dtype == torch.int32 and row_ptr.dtype == col_ptr.dtype == nip.dtype == torch.int64
+    assert lcol.dtype == torch.int16 and nip.numel() == n_rows + 1 and lcol.numel() == val.numel()
+    assert all(t.dtype == torch.float64 for t in (val, y, off, wt, scr, W, f, zout))
+    assert off.numel() == n_rows and wt.numel() == n_rows and zout.numel() == n_rows and scr.numel() >= 4 * n_rows
+    assert iters.dtype == reason.dtype == torch.int32 and dmax % 64 == 0
+    n_ent = row_ptr.numel() - 1
+    assert col_ptr.numel() == n_ent + 1 and W.numel() == int(col_ptr[-1]) and f.numel() == n_ent
+    if os.environ.get("PML_CHECK_KERNEL_INPUTS", "0") == "1" and B:
+        # the kernel indexes entities through ``order`` and sizes its LDS vectors by dmax
+        assert int(order.min()) >= 0 and int(order.max()) < n_ent, "re_tron order out of range"
+        oe = order.to(torch.int64)
+        assert int((col_ptr[oe + 1] - col_ptr[oe]).max()) <= dmax, "entity wider than the launch's LDS class"
+        assert int(row_ptr[-1]) == n_rows and int(nip[-1]) == val.numel(), "row / non-zero ranges inconsistent"
+    check(lib.pml_re_tron_csr(order.data_ptr(), B, row_ptr.data_ptr(), col_ptr.data_ptr(), nip.data_ptr(),
+                              lcol.data_ptr(), val.data_ptr(), y.data_ptr(), off.data_ptr(), wt.data_ptr(),
+                              scr.data_ptr(), n_rows, W.data_ptr(), f.data_ptr(), iters.data_ptr(),
+                              reason.data_ptr(), zout.data_ptr(), int(loss_id), float(l2), float(tol), int(max_iter),
+                              int(max_fail), int(max_cg), int(dmax), stream_handle(W.device)), "re_tron_csr")
 
 
 def check(rc: int, what: str):

@@ -1,0 +1,123 @@
+"""Fused per-entity PRIMAL TRON for random-effect entities outside the row-space batch.
+
+The reference runs one ``SingleNodeOptimizationProblem`` (TRON over the entity's local rows) per entity
+(``photon-api/.../algorithm/RandomEffectCoordinate.scala:103-143``,
+``photon-api/.../optimization/SingleNodeOptimizationProblem.scala:85-103``). Entities with few rows are solved
+in their row space (``row_space.py``); the rest — 65 .. thousands of rows over up to ``FUSED_DMAX`` projected
+coefficients — go here: ONE kernel launch per LDS size class (``re_tron_csr_kernel``,
+``ops/csrc/re_kernels.hip``) runs every entity's complete TRON in its own workgroup, with the entity's
+coefficient vectors in LDS and each Hessian-vector product a single read of its CSR rows. No host round trip,
+no global pass per CG step, entities converge independently (a converged entity stops reading its rows), and
+the margins of the solution come out of the solve.
+
+Entities wider than ``FUSED_DMAX`` or longer than ``FUSED_MAX_ROWS`` stay on the block-diagonal pass path
+(``batched.batched_tron`` over ``RandomEffectDataset.entity_subset``).
+"""
+from __future__ import annotations
+
+import os
+from dataclasses import dataclass
+from typing import Optional
+
+import torch
+
+FUSED_DMAX = 2048                    # LDS per workgroup: (5 + 4) x dmax doubles (<= 147 KB of the CU's 160 KB)
+FUSED_MAX_ROWS = int(os.environ.get("PML_RE_FUSED_MAX_ROWS", str(1 << 22)))
+FUSED_LOSSES = (0, 1, 2)             # logistic, Poisson, squared (the twice-differentiable losses)
+_CLASSES = (256, 512, 1024, 2048)    # LDS size classes (max coefficients per entity of a launch)
+
+
+def fused_enabled() -> bool:
+    return os.environ.get("PML_RE_FUSED", "1") != "0"
+
+
+def fused_eligible(loss, optimizer: str, l1: float, constraints, device) -> bool:
+    """The fused primal TRON applies to TRON with L2 / no regularization on the GPU for the smooth losses."""
+    return (fused_enabled() and optimizer == "TRON" and l1 == 0 and not constraints
+            and torch.device(device).type == "cuda" and getattr(loss, "loss_id", -1) in FUSED_LOSSES)
+
+
+@dataclass
+class FusedResult:
+    W: torch.Tensor          # packed coefficients of the batch's entities
+    f: torch.Tensor          # [B] final objective
+    iters: torch.Tensor      # [B]
+    reason: torch.Tensor     # [B] reason codes (batched.REASON_CODES)
+    z: torch.Tensor          # per batch row: x_i . w of the solution (no offset)
+
+
+class EntityTronBatch:
+    """The entities of a segmented random-effect coordinate that the fused kernel solves.
+
+    ``mask`` [E] bool: candidate entities (e.g. not handled in their row space). Entities with data and
+    ``d_e <= FUSED_DMAX``, ``n_e <= FUSED_MAX_ROWS`` are taken (``self.mask``); ``ents`` / ``rows`` / ``cols``
+    are their parent entity indices, parent row positions and parent coefficient positions."""
+
+    def __init__(self, ds, mask: torch.Tensor):
+        seg = ds.seg
+        dev = seg.y.device
+        n_e = seg.row_ptr[1:] - seg.row_ptr[:-1]
+        d_e = seg.col_ptr[1:] - seg.col_ptr[:-1]
+        sel = mask.to(dev) & (n_e > 0) & (d_e > 0) & (d_e <= FUSED_DMAX) & (n_e <= FUSED_MAX_ROWS)
+        self.mask = sel
+        self.ents = torch.nonzero(sel).squeeze(1)
+        self.B = int(self.ents.numel())
+        self.W: Optional[torch.Tensor] = None          # last solution (warm start of the next solve)
+        if self.B == 0:
+            return
+        nip, pos, val, row_sel, col_sel, _ = ds.entity_csr(sel)
+        self.rows, self.cols = row_sel, col_sel
+        ne, de = n_e[self.ents], d_e[self.ents]
+        self.row_ptr = torch.zeros(self.B + 1, dtype=torch.int64, device=dev)
+        torch.cumsum(ne, 0, out=self.row_ptr[1:])
+        self.col_ptr = torch.zeros(self.B + 1, dtype=torch.int64, device=dev)
+        torch.cumsum(de, 0, out=self.col_ptr[1:])
+        n_rows = int(self.row_ptr[-1])
+        row_ent = torch.repeat_interleave(torch.arange(self.B, device=dev), ne, output_size=n_rows)
+        row_nnz = nip[1:] - nip[:-1]
+        nnz = int(nip[-1])
+        nnz_ent = torch.repeat_interleave(row_ent, row_nnz, output_size=nnz)
+        lcol = pos - self.col_ptr[nnz_ent]
+        if os.environ.get("PML_CHECK_KERNEL_INPUTS", "0") == "1" and nnz:
+            # the kernel indexes LDS vectors of d_e entries with these
+            assert int(lcol.min()) >= 0 and bool((lcol < de[nnz_ent]).all()), "entity-local column out of range"
+        del nnz_ent, pos
+        self.lcol = lcol.to(torch.int16)                 # read as uint16 by the kernel (d_e <= 2048)
+        self.nip, self.val = nip, val
+        self.y, self.w = seg.y[row_sel].contiguous(), seg.w[row_sel].contiguous()
+        self.n_rows = n_rows
+        self.nnz = nnz
+        self.scr = torch.empty(4 * max(n_rows, 1), dtype=torch.float64, device=dev)
+        # launch classes by LDS size; inside a class the largest entities first (they bound the launch's tail)
+        ent_nnz = (nip[self.row_ptr[1:]] - nip[self.row_ptr[:-1]])
+        bounds = torch.tensor(_CLASSES, device=dev)
+        cls = torch.searchsorted(bounds, de)
+        self.launches = []
+        for c, dm in enumerate(_CLASSES):
+            idx = torch.nonzero(cls == c).squeeze(1)
+            if idx.numel() == 0:
+                continue
+            order = idx[torch.argsort(ent_nnz[idx], descending=True, stable=True)]
+            self.launches.append((dm, order.to(torch.int32).contiguous()))
+
+    def solve(self, loss, l2: float, W0: Optional[torch.Tensor], offsets: torch.Tensor, tol: float, max_iter: int,
+              max_fail: int = 5, max_cg: int = 20) -> FusedResult:
+        """Solve every entity of the batch from ``W0`` (packed over the batch's coefficients; None = the last
+        solution, or zeros the first time). ``offsets``: per batch row."""
+        from ..ops.native import re_tron_csr
+        dev = self.y.device
+        if W0 is None:
+            W0 = self.W if self.W is not None else torch.zeros(int(self.col_ptr[-1]), dtype=torch.float64,
+                                                                device=dev)
+        W = W0.to(torch.float64).contiguous().clone()
+        f = torch.empty(self.B, dtype=torch.float64, device=dev)
+        iters = torch.empty(self.B, dtype=torch.int32, device=dev)
+        reason = torch.empty(self.B, dtype=torch.int32, device=dev)
+        z = torch.empty(self.n_rows, dtype=torch.float64, device=dev)
+        off = offsets.to(dev, torch.float64).contiguous()
+        assert off.numel() == self.n_rows
+        for dm, order in self.launches:
+            re_tron_csr(order, self.row_ptr, self.col_ptr, self.nip, self.lcol, self.val, self.y, off, self.w,
+                        self.scr, W, f, iters, reason, z, loss.loss_id, l2, tol, max_iter, max_fail, max_cg, dm)
+        self.W = W
+        return FusedResult(W, f, iters.to(torch.long), reason.to(torch.long), z)

@@ -143,25 +143,43 @@ class RowSpaceBatch:
                                torch.full_like(valid, -1, dtype=torch.long))
             geo.append((e, n, valid, rows, torch.zeros(e.numel(), n, n, dtype=torch.float64, device=dev)))
         csr = _canonical_csr(csr, dev) if dev.type == "cuda" else None
+        # (class, members) whose Gram columns come from indicator passes: all of them without a canonical device
+        # CSR, else only the entities too wide for seg_gram_kernel's LDS image (d_e > SEG_GRAM_DMAX)
+        need_ind = []
         if csr is not None:
             # K_e straight from the block-diagonal CSR, one wave per entity (seg_gram_kernel)
-            from ..ops.native import seg_gram
-            for gi, (e, n, valid, rows, _K) in enumerate(geo):
-                geo[gi] = (e, n, valid, rows, seg_gram(e, n, seg.row_ptr, seg.col_ptr, *csr))
-            n_max = 0
+            from ..ops.native import SEG_GRAM_DMAX, seg_gram
+            for gi, (e, n, valid, rows, K) in enumerate(geo):
+                ok = d_e[e] <= SEG_GRAM_DMAX
+                if bool(ok.all()):
+                    geo[gi] = (e, n, valid, rows, seg_gram(e, n, seg.row_ptr, seg.col_ptr, *csr))
+                    continue
+                if bool(ok.any()):
+                    K[ok] = seg_gram(e[ok], n, seg.row_ptr, seg.col_ptr, *csr)
+                need_ind.append((gi, torch.nonzero(~ok).squeeze(1)))
+        else:
+            need_ind = [(gi, None) for gi in range(len(geo))]
+        n_max = max((geo[gi][1] for gi, _ in need_ind), default=0)
         ind = torch.zeros(N, dtype=torch.float64, device=dev) if n_max else None
         for j in range(n_max):
-            # column j of every K_e at once: indicator on row j of every handled entity with n_e > j
+            # column j of every K_e at once: indicator on row j of every such entity with n_e > j
             ind.zero_()
-            for _, n, valid, rows, _K in geo:
+            for gi, sel in need_ind:
+                _, n, valid, rows, _K = geo[gi]
                 if j < n:
-                    ind[rows[valid[:, j], j]] = 1.0
+                    v, r = (valid, rows) if sel is None else (valid[sel], rows[sel])
+                    ind[r[v[:, j], j]] = 1.0
             u = seg.glm.rmatvec(ind)                  # every entity's row j, at its own columns
             z = seg.glm.matvec(u)                      # (X_e X_e^T)[:, j] on the entity's rows
-            for _, n, valid, rows, K in geo:
+            for gi, sel in need_ind:
+                _, n, valid, rows, K = geo[gi]
                 if j < n:
-                    K[:, :, j] = torch.where(valid, z[rows.clamp(min=0)],
-                                             torch.zeros((), dtype=torch.float64, device=dev))
+                    v, r = (valid, rows) if sel is None else (valid[sel], rows[sel])
+                    col = torch.where(v, z[r.clamp(min=0)], torch.zeros((), dtype=torch.float64, device=dev))
+                    if sel is None:
+                        K[:, :, j] = col
+                    else:
+                        K[sel, :, j] = col
             del u, z
         del ind
         off = 0

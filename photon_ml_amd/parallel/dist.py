@@ -7,8 +7,13 @@ REPLICA of the optimizer state; each function evaluation all-reduces ONE packed 
 rank then applies the identical deterministic optimizer update, coefficients are never broadcast (C5 removed).
 
 Message sizing for xGMI: D = 1M fp64 = 8 MB per evaluation; a ring all-reduce moves 2(P-1)/P x 8 MB per rank
-(~14 MB at P = 8), i.e. ~0.1 ms on one 153 GB/s link against a ~30 ms evaluation pass, so a single un-bucketed
-collective per evaluation is the right shape here (bucketing would only add launches).
+(~14 MB at P = 8), i.e. ~0.1 ms on one 153 GB/s link against a ~40 ms evaluation pass. That is small, but not
+free at the END of a pass: :class:`DistributedGLMData` therefore buckets the gradient by column-tile ranges of
+equal transpose work and all-reduces each bucket while the transpose kernels of the later buckets still run
+(RCCL's stream waits on the compute stream per bucket), so only the last bucket's collective is exposed.
+
+The reference's ``treeAggregateDepth`` knob (``GameEstimator.scala:111-114, 587-592``) maps to the RCCL
+all-reduce algorithm (:func:`set_allreduce_algo`: ring / tree / RCCL's own choice).
 """
 from __future__ import annotations
 
@@ -52,6 +57,41 @@ def init_distributed(backend: Optional[str] = None, timeout_s: int = 1800) -> tu
             torch.cuda.set_device(local % torch.cuda.device_count())
         dist.init_process_group(backend=backend, timeout=datetime.timedelta(seconds=timeout_s))
     return rank, world, local
+
+
+ALLREDUCE_ALGOS = ("auto", "ring", "tree")
+_EXPLICIT_ALGO: Optional[str] = None
+
+
+def set_allreduce_algo(algo: Optional[str] = None, tree_depth: Optional[int] = None) -> str:
+    """Choose the RCCL all-reduce algorithm — the analogue of the reference's ``treeAggregateDepth``
+    (``photon-api/.../estimators/GameEstimator.scala:111-114``; auto depth 2 for D >= 200k at ``:587-592``):
+    ``ring`` / ``tree`` set ``NCCL_ALGO`` (which RCCL reads when it creates a communicator; torch creates them
+    lazily at the first collective, so call this before any collective runs), ``auto`` leaves RCCL's tuner in
+    charge. Without an explicit ``algo``, a tree-aggregate depth >= 2 selects ``tree`` (a hierarchical reduction,
+    like a deeper treeAggregate) and depth 1 ``auto``. A ``NCCL_ALGO`` already set in the environment wins.
+    An explicit ``algo`` (e.g. ``--allreduce-algo``) sticks: later depth-only calls do not change it. Returns
+    the effective choice."""
+    global _EXPLICIT_ALGO
+    if algo is None:
+        if _EXPLICIT_ALGO is not None:
+            return _EXPLICIT_ALGO
+        algo = "tree" if (tree_depth or 1) >= 2 else "auto"
+    else:
+        _EXPLICIT_ALGO = algo.lower()
+    algo = algo.lower()
+    if algo not in ALLREDUCE_ALGOS:
+        raise ValueError(f"unknown all-reduce algorithm {algo!r}, expected one of {ALLREDUCE_ALGOS}")
+    if "NCCL_ALGO" in os.environ and os.environ.get("PML_NCCL_ALGO_SET") != "1":
+        return os.environ["NCCL_ALGO"].lower()
+    if algo == "auto":
+        if os.environ.get("PML_NCCL_ALGO_SET") == "1":
+            os.environ.pop("NCCL_ALGO", None)
+            os.environ.pop("PML_NCCL_ALGO_SET", None)
+        return "auto"
+    os.environ["NCCL_ALGO"] = {"ring": "Ring", "tree": "Tree"}[algo]
+    os.environ["PML_NCCL_ALGO_SET"] = "1"       # ours, may be changed again
+    return algo
 
 
 def is_dist() -> bool:

@@ -9,8 +9,14 @@ The samplers return a new WEIGHT vector (0 = dropped). On the device path the da
 simply carries zero weight for this coordinate update, so no compaction/re-layout of the HBM streams is needed;
 the weights are rewritten in place by ``downsample_kernel`` (``ops/csrc/game_kernels.hip``, K20). The uniform of a
 row is a counter-based hash of (seed, global row id) — splitmix64, top 53 bits — computed identically here on the
-host, so the CPU path, the GPU path and every rank of a data-parallel job draw the same sample. Seeds are
-deterministic (``MathConst.RANDOM_SEED`` by default) as in the reference.
+host, so the CPU path, the GPU path and every rank of a data-parallel job draw the same sample.
+
+Seeds follow the reference: every down-sampling call draws a FRESH seed from one process-wide
+``java.util.Random(MathConst.RANDOM_SEED)`` sequence (``DownSampler.scala:38-46``: ``random.nextLong()``), so every
+fixed-effect update trains on a different sample, and the sequence of seeds is the reference's bit for bit
+(:class:`JavaRandom`; the per-row draws themselves are this framework's counter-based hash, not Java's LCG per
+Spark partition). Every rank runs the same updates in the same order, so the ranks of a data-parallel job draw
+the same seeds.
 """
 from __future__ import annotations
 
@@ -38,29 +44,71 @@ def row_uniforms(seed: int, row_ids: np.ndarray) -> np.ndarray:
     return (h >> np.uint64(11)).astype(np.float64) * (2.0 ** -53)
 
 
+class JavaRandom:
+    """``java.util.Random``'s 48-bit LCG (``nextLong`` only): the seed source of the reference's samplers."""
+    _MULT, _ADD, _MASK = 0x5DEECE66D, 0xB, (1 << 48) - 1
+
+    def __init__(self, seed: int):
+        self._s = (int(seed) ^ self._MULT) & self._MASK
+
+    def _next(self, bits: int) -> int:
+        self._s = (self._s * self._MULT + self._ADD) & self._MASK
+        v = self._s >> (48 - bits)
+        return v - (1 << bits) if v >= 1 << (bits - 1) else v     # Java int (signed 32-bit)
+
+    def next_long(self) -> int:
+        v = ((self._next(32) << 32) + self._next(32)) & 0xFFFFFFFFFFFFFFFF
+        return v - (1 << 64) if v >= 1 << 63 else v
+
+
+_SEEDS = JavaRandom(RANDOM_SEED)
+
+
+def next_seed() -> int:
+    """The next down-sampling seed of the process-wide sequence (``DownSampler.getSeed``)."""
+    return _SEEDS.next_long()
+
+
+def reset_seed_sequence(seed: int = RANDOM_SEED):
+    """Restart the seed sequence (a fresh process in the reference; tests and resumed runs)."""
+    global _SEEDS
+    _SEEDS = JavaRandom(seed)
+
+
 class DownSampler:
-    def __init__(self, rate: float, seed: int = RANDOM_SEED):
+    def __init__(self, rate: float, seed: Optional[int] = None):
+        """``seed``: a fixed seed for every call (tests); None = a fresh seed per call from the process-wide
+        reference sequence (:func:`next_seed`)."""
         if not (0.0 < rate < 1.0):
             raise ValueError(f"Invalid down-sampling rate {rate}; must be in (0, 1)")
         self.rate = float(rate)
-        self.seed = int(seed)
+        self.fixed_seed = None if seed is None else int(seed)
+        self.seed = self.fixed_seed if seed is not None else None   # seed of the last draw
 
     binary = False
 
-    def sample_weights(self, labels, weights, row_ids: Optional[np.ndarray] = None) -> np.ndarray:
-        """Host weights; ``row_ids`` = global row ids (default 0..n-1)."""
+    def draw_seed(self) -> int:
+        """Seed of one down-sampling call (a new draw per call unless the sampler has a fixed seed)."""
+        self.seed = self.fixed_seed if self.fixed_seed is not None else next_seed()
+        return self.seed
+
+    def sample_weights(self, labels, weights, row_ids: Optional[np.ndarray] = None,
+                       seed: Optional[int] = None) -> np.ndarray:
+        """Host weights; ``row_ids`` = global row ids (default 0..n-1); ``seed`` default: a new draw."""
         n = len(labels)
-        u = row_uniforms(self.seed, np.arange(n) if row_ids is None else row_ids)
+        seed = self.draw_seed() if seed is None else seed
+        u = row_uniforms(seed, np.arange(n) if row_ids is None else row_ids)
         w = np.asarray(weights, dtype=np.float64)
         if self.binary:
             pos = np.asarray(labels, dtype=np.float64) >= POSITIVE_RESPONSE_THRESHOLD
             return np.where(pos, w, np.where(u < self.rate, w / self.rate, 0.0))
         return np.where(u < self.rate, w, 0.0)
 
-    def sample_weights_device(self, labels, weights, row_ids=None, out=None):
+    def sample_weights_device(self, labels, weights, row_ids=None, out=None, seed: Optional[int] = None):
         """The same weights computed on the device (``downsample_kernel``), written into ``out`` if given."""
         from ..ops.native import downsample_weights
-        return downsample_weights(labels, weights, self.rate, self.binary, self.seed, row_ids, out)
+        seed = self.draw_seed() if seed is None else seed
+        return downsample_weights(labels, weights, self.rate, self.binary, seed, row_ids, out)
 
 
 class BinaryClassificationDownSampler(DownSampler):
@@ -73,7 +121,7 @@ class DefaultDownSampler(DownSampler):
     binary = False
 
 
-def down_sampler_for_task(task, rate: float, seed: int = RANDOM_SEED) -> DownSampler:
+def down_sampler_for_task(task, rate: float, seed: Optional[int] = None) -> DownSampler:
     task = TaskType.parse(task)
     if task in (TaskType.LOGISTIC_REGRESSION, TaskType.SMOOTHED_HINGE_LOSS_LINEAR_SVM):
         return BinaryClassificationDownSampler(rate, seed)

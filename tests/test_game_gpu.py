@@ -210,6 +210,7 @@ def test_entity_masked_passes_give_identical_solve(row_space, monkeypatch):
     import photon_ml_amd.optimization.batched as bt
     from photon_ml_amd.algorithm.coordinates import RandomEffectCoordinate
     monkeypatch.setenv("PML_RE_ROW_SPACE", row_space)
+    monkeypatch.setenv("PML_RE_FUSED", "0")       # the pass path (the fused primal TRON reads no masked passes)
     data, _ = generate_game_data(n_rows=30000, n_users=500, d_user=8, seed=25, task="LOGISTIC_REGRESSION")
     cfg = GLMOptimizationConfiguration(OptimizerConfig("TRON", 30, 1e-10), RegularizationContext("L2"), 1.0)
     out = {}
@@ -223,3 +224,98 @@ def test_entity_masked_passes_give_identical_solve(row_space, monkeypatch):
     assert np.array_equal(out[False][0], out[True][0])
     assert out[False][1] == out[True][1]
     assert torch.equal(out[False][2], out[True][2])
+
+
+def _re_two_updates(data, task, opt="TRON"):
+    from photon_ml_amd.algorithm.coordinates import RandomEffectCoordinate
+    cfg = GLMOptimizationConfiguration(OptimizerConfig(opt, 30, 1e-10), RegularizationContext("L2"), 1.0)
+    c = RandomEffectCoordinate("u", data, RandomEffectDataConfiguration("userId", "user"), cfg, task,
+                               device="cuda", layout="segmented")
+    m1 = c.update_model(c.initialize_model())
+    s1 = c.score(m1).cpu()
+    m2 = c.update_model(m1, partial_score=torch.from_numpy(np.sin(np.arange(data.n_rows)) * 0.2))
+    return c, m1.values.copy(), s1, m2.values.copy(), c.score(m2).cpu()
+
+
+@pytest.mark.parametrize("task", ["LOGISTIC_REGRESSION", "LINEAR_REGRESSION", "POISSON_REGRESSION"])
+@pytest.mark.parametrize("max_rows", [None, 200])
+def test_fused_entity_tron_matches_pass_path(task, max_rows, monkeypatch):
+    """The fused per-entity primal TRON (re_tron_csr_kernel: one workgroup per entity, the whole solve in one
+    launch) reproduces the block-diagonal pass-path TRON: same models, scores and iteration counts, across a
+    warm-started second update. ``max_rows``: larger entities stay on the pass path (mixed components)."""
+    import photon_ml_amd.optimization.entity_tron as et
+    # power-law users (zipf): entities from a few rows (row space) to thousands (fused / pass path), d_e = 12
+    data, _ = generate_game_data(n_rows=30000, n_users=700, d_user=12, seed=26, task=task)
+    out = {}
+    for fused in ("0", "1"):
+        monkeypatch.setenv("PML_RE_FUSED", fused)
+        monkeypatch.setattr(et, "FUSED_MAX_ROWS", max_rows or et.FUSED_MAX_ROWS)
+        c, v1, s1, v2, s2 = _re_two_updates(data, task)
+        if fused == "1":
+            rs, fz, sub = c._comps
+            assert fz is not None and fz.B > 0
+            assert (sub is not None) == (max_rows is not None)
+        out[fused] = (v1, s1, v2, s2, c.last_stats["mean_iterations"])
+    a, b = out["0"], out["1"]
+    for i in range(4):
+        torch.testing.assert_close(torch.as_tensor(b[i]), torch.as_tensor(a[i]), rtol=1e-6, atol=1e-8)
+    assert abs(a[4] - b[4]) < 0.05
+
+
+def test_fused_entity_tron_deterministic_and_matches_cpu(monkeypatch):
+    """Bitwise-reproducible fused solve (fixed-order DPP wave sums, per-wave LDS accumulators), and the same
+    model as the dense CPU batch solver (photon-api SingleNodeOptimizationProblem semantics per entity)."""
+    from photon_ml_amd.algorithm.coordinates import RandomEffectCoordinate
+    monkeypatch.setenv("PML_RE_FUSED", "1")
+    data, _ = generate_game_data(n_rows=8000, n_users=80, d_user=10, seed=27, task="LOGISTIC_REGRESSION")
+    r1 = _re_two_updates(data, "LOGISTIC_REGRESSION")
+    r2 = _re_two_updates(data, "LOGISTIC_REGRESSION")
+    assert r1[0]._comps[1] is not None
+    assert np.array_equal(r1[3], r2[3]) and torch.equal(r1[4], r2[4])
+    cfg = GLMOptimizationConfiguration(OptimizerConfig("TRON", 30, 1e-10), RegularizationContext("L2"), 1.0)
+    cpu = RandomEffectCoordinate("u", data, RandomEffectDataConfiguration("userId", "user"), cfg,
+                                 "LOGISTIC_REGRESSION", device="cpu", layout="dense")
+    m = cpu.update_model(cpu.initialize_model())
+    g = r1[0].update_model(None)
+    for e in m.entity_ids[:30]:
+        np.testing.assert_allclose(g.coefficients_of(e).means.numpy(), m.coefficients_of(e).means.numpy(),
+                                   rtol=1e-5, atol=1e-6)
+
+
+def test_row_space_gram_wide_entity_falls_back_to_indicator_passes():
+    """An entity with few rows but more projected columns than seg_gram_kernel's LDS image (d_e > SEG_GRAM_DMAX)
+    gets its Gram columns from indicator passes; the other entities of its size class still use the kernel, and
+    the factors match the all-indicator build."""
+    import scipy.sparse as sp
+    from photon_ml_amd.algorithm.coordinates import RandomEffectCoordinate
+    from photon_ml_amd.data.game_data import GameData
+    from photon_ml_amd.ops.native import SEG_GRAM_DMAX
+    from photon_ml_amd.optimization.row_space import RowSpaceBatch
+    rng = np.random.default_rng(31)
+    D = 3 * SEG_GRAM_DMAX
+    rows, cols, vals, ids = [], [], [], []
+    r = 0
+    for e in range(40):
+        n = 6 if e else 8
+        width = (SEG_GRAM_DMAX // 3 + 500) if e == 0 else 20   # entity 0: 8 x 7.3K distinct columns > dmax
+        for _ in range(n):
+            c = rng.choice(D - 1, size=width, replace=False)
+            rows += [r] * (width + 1)
+            cols += sorted(c.tolist()) + [D - 1]
+            vals += rng.normal(size=width).tolist() + [1.0]
+            ids.append(e)
+            r += 1
+    x = sp.csr_matrix((vals, (rows, cols)), shape=(r, D))
+    y = (rng.random(r) < 0.5).astype(float)
+    data = GameData(y, {"user": x}, {"userId": np.array(ids)})
+    cfg = GLMOptimizationConfiguration(OptimizerConfig("TRON", 30, 1e-10), RegularizationContext("L2"), 1.0)
+    c = RandomEffectCoordinate("u", data, RandomEffectDataConfiguration("userId", "user"), cfg,
+                               "LOGISTIC_REGRESSION", device="cuda", layout="segmented")
+    ds = c.dataset
+    d_e = ds.seg.col_ptr[1:] - ds.seg.col_ptr[:-1]
+    assert int(d_e.max()) > SEG_GRAM_DMAX
+    a = RowSpaceBatch(ds.seg, csr=ds._seg_csr)
+    b = RowSpaceBatch(ds.seg)
+    assert a.B == b.B == 40 and torch.equal(a.ents, b.ents)
+    for ka, kb in zip(a.classes, b.classes):
+        torch.testing.assert_close(ka.L, kb.L, rtol=1e-10, atol=1e-12)

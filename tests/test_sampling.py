@@ -4,8 +4,8 @@ import numpy as np
 import pytest
 import torch
 
-from photon_ml_amd.sampling.samplers import (BinaryClassificationDownSampler, DefaultDownSampler, row_uniforms,
-                                             down_sampler_for_task)
+from photon_ml_amd.sampling.samplers import (BinaryClassificationDownSampler, DefaultDownSampler, JavaRandom,
+                                             down_sampler_for_task, reset_seed_sequence, row_uniforms)
 
 
 def test_binary_down_sampler_semantics():
@@ -72,6 +72,7 @@ def test_fixed_effect_down_sampling_gpu_matches_cpu():
                                        down_sampling_rate=0.3)
     out = {}
     for dev in ("cpu", "cuda"):
+        reset_seed_sequence()          # both updates draw the first seed of the reference sequence
         c = FixedEffectCoordinate("g", data, FixedEffectDataConfiguration("global"), cfg, "LOGISTIC_REGRESSION",
                                   device=dev)
         m = c.update_model(c.initialize_model())
@@ -79,3 +80,45 @@ def test_fixed_effect_down_sampling_gpu_matches_cpu():
         if dev == "cuda":   # full weights restored for scoring after the update
             assert torch.equal(c.glm_data.wt.cpu().double(), torch.from_numpy(c.base_weights))
     torch.testing.assert_close(out["cuda"], out["cpu"], rtol=1e-6, atol=1e-8)
+
+
+def test_java_random_seed_sequence():
+    """java.util.Random's nextLong, bit for bit (values of the JDK: new Random(42).nextInt() / nextLong())."""
+    assert JavaRandom(42)._next(32) == -1170105035
+    assert JavaRandom(42).next_long() == -5025562857975149833
+    assert JavaRandom(0).next_long() == -4962768465676381896
+
+
+def test_fresh_sample_per_fixed_effect_update():
+    """Every down-sampling call draws a NEW seed from one Random(MathConst.RANDOM_SEED) sequence
+    (photon-lib/.../sampler/DownSampler.scala:38-46), so successive fixed-effect updates see different samples —
+    the seeds being the reference's nextLong() sequence."""
+    from photon_ml_amd.algorithm.coordinates import FixedEffectCoordinate
+    from photon_ml_amd.constants import RANDOM_SEED
+    from photon_ml_amd.data.game_data import generate_game_data
+    from photon_ml_amd.data.random_effect import FixedEffectDataConfiguration
+    from photon_ml_amd.optimization.config import GLMOptimizationConfiguration, OptimizerConfig, RegularizationContext
+    data, _ = generate_game_data(n_rows=3000, seed=9, task="LOGISTIC_REGRESSION")
+    cfg = GLMOptimizationConfiguration(OptimizerConfig("LBFGS", 5, 1e-10), RegularizationContext("L2"), 1.0,
+                                       down_sampling_rate=0.3)
+    reset_seed_sequence()
+    c = FixedEffectCoordinate("g", data, FixedEffectDataConfiguration("global"), cfg, "LOGISTIC_REGRESSION",
+                              device="cpu")
+    ref = JavaRandom(RANDOM_SEED)
+    seen = []
+    orig = c.sampler.sample_weights
+
+    def spy(*a, **k):
+        w = orig(*a, **k)
+        seen.append((c.sampler.seed, w.copy()))
+        return w
+
+    c.sampler.sample_weights = spy
+    m = c.update_model(c.initialize_model())
+    c.update_model(m)
+    assert [s for s, _ in seen] == [ref.next_long(), ref.next_long()]
+    assert not np.array_equal(seen[0][1], seen[1][1])
+    # a fixed-seed sampler (tests) keeps its sample
+    s = BinaryClassificationDownSampler(0.3, seed=5)
+    y, w = np.zeros(100), np.ones(100)
+    assert np.array_equal(s.sample_weights(y, w), s.sample_weights(y, w))
