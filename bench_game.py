@@ -66,7 +66,11 @@ def main():
     ap.add_argument("--sizes", choices=["uniform", "powerlaw"])
     ap.add_argument("--fe-iters", type=int, default=10)
     ap.add_argument("--re-iters", type=int, default=10)
-    ap.add_argument("--precision", default="bf16", choices=["bf16", "f32", "f64"])
+    ap.add_argument("--precision", default="bf16", choices=["bf16", "f32", "f64"],
+                    help="storage precision of the fixed-effect features (accumulation and optimizer state are fp64; "
+                         "random-effect features are always fp64)")
+    ap.add_argument("--host-data", action="store_true",
+                    help="generate the synthetic data with host numpy (minutes at config 5) instead of on the device")
     ap.add_argument("--seed", type=int, default=11)
     ap.add_argument("--log-level", default="WARNING",
                     help="framework log level (DEBUG shows the per-phase timings of the random-effect update)")
@@ -99,17 +103,23 @@ def main():
     from photon_ml_amd.algorithm.coordinates import (FixedEffectCoordinate, RandomEffectCoordinate,
                                                      ShardedRandomEffectCoordinate)
     from photon_ml_amd.data.random_effect import FixedEffectDataConfiguration, RandomEffectDataConfiguration
-    from photon_ml_amd.data.synthetic import generate_game_bench_data
+    from photon_ml_amd.data.synthetic import generate_game_bench_data, generate_game_bench_data_device
     from photon_ml_amd.evaluation.evaluators import build_evaluator
     from photon_ml_amd.optimization.config import (GLMOptimizationConfiguration, OptimizerConfig,
                                                    RegularizationContext)
 
     t0 = time.time()
-    data = generate_game_bench_data(args.entities_per_gpu, args.rows_per_entity, args.re_dim, args.re_nnz,
-                                    args.fe_dim, args.fe_nnz, seed=args.seed + 1000 * rank,
-                                    entity_offset=rank * args.entities_per_gpu, pool=args.pool,
-                                    int_ids=bool(args.int_ids), sizes=args.sizes or "uniform")
-    log(f"data generated in {time.time() - t0:.1f}s: {data.n_rows} rows/GPU")
+    gen_kw = dict(seed=args.seed + 1000 * rank, entity_offset=rank * args.entities_per_gpu, pool=args.pool,
+                  int_ids=bool(args.int_ids), sizes=args.sizes or "uniform")
+    if args.host_data or dev.type != "cuda":
+        data = generate_game_bench_data(args.entities_per_gpu, args.rows_per_entity, args.re_dim, args.re_nnz,
+                                        args.fe_dim, args.fe_nnz, **gen_kw)
+    else:
+        data = generate_game_bench_data_device(args.entities_per_gpu, args.rows_per_entity, args.re_dim, args.re_nnz,
+                                               args.fe_dim, args.fe_nnz, device=dev, **gen_kw)
+        torch.cuda.empty_cache()
+    log(f"data generated in {time.time() - t0:.1f}s ({'host' if args.host_data or dev.type != 'cuda' else 'device'}): "
+        f"{data.n_rows} rows/GPU")
     t0 = time.time()
     fe_cfg = GLMOptimizationConfiguration(OptimizerConfig("LBFGS", args.fe_iters, 1e-12),
                                           RegularizationContext("L2"), 1.0)

@@ -239,6 +239,113 @@ def generate_device_shard(n_rows: int, n_features: int, nnz_per_row: int, device
     return data, w_true
 
 
+def _device_csr_to_host(counts: torch.Tensor, cols: torch.Tensor, vals: torch.Tensor, n_cols: int) -> sp.csr_matrix:
+    """scipy CSR from per-row counts and the row-major (column, value) entries, all on the device."""
+    indptr = torch.zeros(counts.numel() + 1, dtype=torch.int64, device=counts.device)
+    torch.cumsum(counts, 0, out=indptr[1:])
+    x = sp.csr_matrix((vals.cpu().numpy(), cols.to(torch.int32).cpu().numpy(), indptr.cpu().numpy()),
+                      shape=(counts.numel(), n_cols))
+    x.has_sorted_indices = True
+    return x
+
+
+def generate_game_bench_data_device(n_entities: int, rows_per_entity: int, re_dim: int = 100, re_nnz: int = 10,
+                                    fe_dim: int = 100_000, fe_nnz: int = 30, re_vocab: int = 1 << 20, seed: int = 7,
+                                    entity_offset: int = 0, task: str = "LOGISTIC_REGRESSION", pool: str = "random",
+                                    int_ids: bool = False, sizes: str = "uniform", size_alpha: float = 1.3,
+                                    max_rows: int = 20000, device="cuda"):
+    """:func:`generate_game_bench_data` with every draw, sort and reduction on the device (torch), so benchmark
+    GAME data of config-5 size (25M rows, 2.1G non-zeros per GPU) takes seconds instead of minutes of host numpy;
+    only the finished CSR arrays cross to the host (the GameData container is host scipy). Same structure and
+    distributions (entity size law, Zipf fixed-effect features, per-entity feature pools, ground-truth labels),
+    different random streams; rows hold strictly increasing columns (canonical CSR, duplicates dropped)."""
+    from ..data.game_data import GameData
+    dev = torch.device(device)
+    gen = torch.Generator(device=dev)
+    gen.manual_seed(int(seed))
+    rnd = lambda *shape: torch.rand(shape, generator=gen, device=dev, dtype=torch.float64)
+    if sizes == "powerlaw":
+        if pool == "exact":
+            raise ValueError("pool='exact' needs equal entity sizes")
+        u = rnd(n_entities)
+        target = n_entities * rows_per_entity
+        xm = float(rows_per_entity) * (size_alpha - 1) / size_alpha
+        for _ in range(30):          # scale so that the capped Pareto sizes have the requested mean
+            cnt = torch.clamp(torch.ceil(xm * u ** (-1.0 / size_alpha)), max=max_rows).to(torch.int64)
+            tot = int(cnt.sum())
+            if abs(tot - target) <= 0.001 * target:
+                break
+            xm *= target / tot
+    elif sizes == "uniform":
+        cnt = torch.full((n_entities,), rows_per_entity, dtype=torch.int64, device=dev)
+    else:
+        raise ValueError(f"unknown entity size law {sizes!r}")
+    n = int(cnt.sum())
+    ent_sorted = torch.repeat_interleave(torch.arange(n_entities, device=dev), cnt, output_size=n)
+    perm = torch.randperm(n, generator=gen, device=dev)
+    ent = ent_sorted[perm]
+    # ---- fixed-effect shard: fe_nnz Zipf(1.1) columns per row (duplicates dropped) + the intercept
+    p = torch.arange(1, fe_dim, device=dev, dtype=torch.float64) ** -1.1
+    cdf = torch.cumsum(p, 0)
+    cdf /= cdf[-1].clone()
+    fcol = torch.searchsorted(cdf, rnd(n, fe_nnz)).clamp_(max=fe_dim - 2)
+    fcol, _ = torch.sort(fcol, dim=1)
+    keep = torch.ones_like(fcol, dtype=torch.bool)
+    keep[:, 1:] = fcol[:, 1:] != fcol[:, :-1]
+    fval = rnd(n, fe_nnz) + 0.5
+    fcol = torch.cat([fcol, torch.full((n, 1), fe_dim - 1, device=dev, dtype=fcol.dtype)], 1)
+    fval = torch.cat([fval, torch.ones(n, 1, device=dev, dtype=torch.float64)], 1)
+    keep = torch.cat([keep, torch.ones(n, 1, device=dev, dtype=torch.bool)], 1)
+    xg = _device_csr_to_host(keep.sum(1), fcol[keep], fval[keep], fe_dim)
+    wg = torch.randn(fe_dim, generator=gen, device=dev, dtype=torch.float64) * 0.2
+    wg[-1] = -0.5
+    zg = (fval * wg[fcol] * keep).sum(1)
+    del fcol, fval, keep
+    # ---- random-effect shard: pool slot k of entity e -> feature (hash(e) + k * stride) % re_vocab, + intercept
+    if pool == "exact":
+        if re_nnz > re_dim:
+            raise ValueError("pool='exact' needs re_nnz <= re_dim")
+        start = torch.zeros(n_entities, dtype=torch.int64, device=dev)
+        torch.cumsum(cnt[:-1], 0, out=start[1:])
+        within = perm - start[ent]          # row k = occurrence perm[k] - start[e] of its entity e
+        slot = (within[:, None] * re_nnz + torch.arange(re_nnz, device=dev)[None, :]) % re_dim
+        del within, start
+    else:
+        slot = torch.randint(0, re_dim, (n, re_nnz), generator=gen, device=dev)
+    del ent_sorted, perm
+    gid = ent + entity_offset
+    base = (gid * 2654435761) % (re_vocab - 1)
+    rcol = (base[:, None] + slot * 40503) % (re_vocab - 1)
+    rval = torch.randn(n, re_nnz, generator=gen, device=dev, dtype=torch.float64)
+    wgen = torch.Generator(device=dev)
+    wgen.manual_seed(int(seed) + 1)
+    w_slot = torch.randn(re_dim, generator=wgen, device=dev, dtype=torch.float64) * 0.5
+    rcol, order = torch.sort(rcol, dim=1)
+    slot = torch.gather(slot, 1, order)
+    rval = torch.gather(rval, 1, order)
+    del order
+    rkeep = torch.ones_like(rcol, dtype=torch.bool)
+    rkeep[:, 1:] = rcol[:, 1:] != rcol[:, :-1]
+    zr = (rval * w_slot[slot] * rkeep).sum(1) + 0.3 * torch.sin(gid.to(torch.float64))
+    del slot
+    rcol = torch.cat([rcol, torch.full((n, 1), re_vocab - 1, device=dev, dtype=rcol.dtype)], 1)
+    rval = torch.cat([rval, torch.ones(n, 1, device=dev, dtype=torch.float64)], 1)
+    rkeep = torch.cat([rkeep, torch.ones(n, 1, device=dev, dtype=torch.bool)], 1)
+    xr = _device_csr_to_host(rkeep.sum(1), rcol[rkeep], rval[rkeep], re_vocab)
+    del rcol, rval, rkeep
+    z = zg + zr
+    task = TaskType.parse(task)
+    if task == TaskType.LOGISTIC_REGRESSION:
+        y = (rnd(n) < torch.sigmoid(z)).to(torch.float64)
+    elif task == TaskType.POISSON_REGRESSION:
+        y = torch.poisson(torch.exp(torch.clamp(z * 0.3, -10, 3)), generator=gen)
+    else:
+        y = z + 0.1 * torch.randn(n, generator=gen, device=dev, dtype=torch.float64)
+    gid_h = gid.cpu().numpy()
+    ids = gid_h.copy() if int_ids else np.char.add("e", gid_h.astype(str)).astype(object)
+    return GameData(y.cpu().numpy(), {"global": xg, "entity": xr}, {"entityId": ids})
+
+
 def generate_game_bench_data(n_entities: int, rows_per_entity: int, re_dim: int = 100, re_nnz: int = 10,
                              fe_dim: int = 100_000, fe_nnz: int = 30, re_vocab: int = 1 << 20, seed: int = 7,
                              entity_offset: int = 0, task: str = "LOGISTIC_REGRESSION", pool: str = "random",

@@ -132,6 +132,9 @@ class GLMObjective:
         return d
 
 
+DEFERRED_DOTS = object()   # ``dots`` sentinel: the caller assigns (a, b, c) itself before the first eval
+
+
 class MarginLineSearch:
     """phi(t) = F(x0 + t d) for a GLM objective, evaluated from cached margins.
 
@@ -148,7 +151,7 @@ class MarginLineSearch:
         self.obj, self.data, self.x0, self.d = obj, data, x0, d
         l2 = obj.l2_weight
         self.l2 = l2
-        if l2 > 0:
+        if l2 > 0 and dots is not DEFERRED_DOTS:
             self.a, self.b, self.c = dots if dots is not None else vdots([(x0, x0), (x0, d), (d, d)])
 
     def eval(self, t: float):

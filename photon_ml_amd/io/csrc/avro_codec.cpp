@@ -18,6 +18,8 @@
 #include <cstring>
 #include <fstream>
 #include <atomic>
+#include <condition_variable>
+#include <mutex>
 #include <map>
 #include <memory>
 #include <random>
@@ -800,6 +802,12 @@ struct FileCols {
   Interner intern;
   std::string label_used;
   int64_t n = 0;
+  void swap_into(FileCols& other) {   // other <- this (an empty FileCols): releases other's memory
+    std::swap(label, other.label); std::swap(weight, other.weight); std::swap(offset, other.offset);
+    std::swap(uid, other.uid); std::swap(has_uid, other.has_uid); std::swap(tags, other.tags);
+    std::swap(bags, other.bags); std::swap(intern, other.intern); std::swap(label_used, other.label_used);
+    std::swap(n, other.n);
+  }
 };
 
 struct ColumnarOpts {
@@ -953,28 +961,12 @@ static py::dict read_columnar(const std::vector<std::string>& paths, const std::
   ColumnarOpts op{label_fields, weight_field, offset_field, uid_field, metadata_field, delimiter, bags_wanted,
                   id_tags};
   const size_t nfile = paths.size();
+  // Files are decoded by a worker pool and merged IN FILE ORDER by this thread as soon as each is done (then its
+  // columns are freed): decoded-but-unmerged files are bounded by the look-ahead window, so peak host memory is
+  // the merged dataset plus ~2 x threads files, not twice the dataset.
   std::vector<FileCols> files(nfile);
   std::vector<std::string> errors(nfile);
-  {
-    py::gil_scoped_release nogil;
-    unsigned nt = std::max(1u, std::thread::hardware_concurrency());
-    if (const char* e = std::getenv("PML_AVRO_THREADS")) nt = (unsigned)std::max(1, atoi(e));
-    nt = (unsigned)std::min<size_t>(nt, std::max<size_t>(nfile, 1));
-    std::atomic<size_t> next{0};
-    auto work = [&]() {
-      for (size_t f = next++; f < nfile; f = next++) {
-        try { decode_columnar_file(paths[f], op, files[f]); }
-        catch (const std::exception& ex) { errors[f] = ex.what(); }
-      }
-    };
-    std::vector<std::thread> pool;
-    for (unsigned t = 1; t < nt; ++t) pool.emplace_back(work);
-    work();
-    for (auto& t : pool) t.join();
-  }
-  for (size_t f = 0; f < nfile; ++f)
-    if (!errors[f].empty()) throw std::runtime_error(errors[f]);
-  // deterministic merge in file order
+  std::vector<uint8_t> done(nfile, 0);
   Interner intern;
   int64_t n = 0;
   std::string label_used;
@@ -983,9 +975,7 @@ static py::dict read_columnar(const std::vector<std::string>& paths, const std::
   std::vector<uint8_t> has_uid;
   std::vector<std::vector<std::string>> tags(id_tags.size());
   std::map<std::string, BagOut> bags;
-  for (auto& fc : files)
-    for (auto& b : fc.bags) bags[b.first];
-  for (auto& fc : files) {
+  auto merge_one = [&](FileCols& fc) {
     if (label_used.empty()) label_used = fc.label_used;
     std::vector<int32_t> remap(fc.intern.keys.size());
     for (size_t k = 0; k < remap.size(); ++k) remap[k] = intern.get(fc.intern.keys[k]);
@@ -996,6 +986,8 @@ static py::dict read_columnar(const std::vector<std::string>& paths, const std::
     has_uid.insert(has_uid.end(), fc.has_uid.begin(), fc.has_uid.end());
     for (size_t t = 0; t < tags.size(); ++t)
       for (auto& x : fc.tags[t]) tags[t].push_back(std::move(x));
+    for (auto& b : fc.bags)
+      if (!bags.count(b.first)) bags[b.first].rowptr.assign((size_t)n + 1, 0);   // bag first seen here: empty rows so far
     for (auto& b : bags) {
       BagOut& dst = b.second;
       auto src = fc.bags.find(b.first);
@@ -1009,8 +1001,56 @@ static py::dict read_columnar(const std::vector<std::string>& paths, const std::
       for (size_t r = 1; r < src->second.rowptr.size(); ++r) dst.rowptr.push_back(base + src->second.rowptr[r]);
     }
     n += fc.n;
-    std::vector<std::string>().swap(fc.intern.keys);   // release per-file memory as the merge proceeds
+    FileCols().swap_into(fc);
+  };
+  {
+    py::gil_scoped_release nogil;
+    unsigned nt = std::max(1u, std::thread::hardware_concurrency());
+    if (const char* e = std::getenv("PML_AVRO_THREADS")) nt = (unsigned)std::max(1, atoi(e));
+    nt = (unsigned)std::min<size_t>(nt, std::max<size_t>(nfile, 1));
+    const size_t ahead = 2 * (size_t)nt;      // files decoded beyond the merge position, at most
+    std::mutex mu;
+    std::condition_variable cv;
+    size_t next = 0, merged = 0;
+    auto work = [&]() {
+      while (true) {
+        size_t f;
+        {
+          std::unique_lock<std::mutex> lk(mu);
+          cv.wait(lk, [&] { return next >= nfile || next < merged + ahead; });
+          if (next >= nfile) return;
+          f = next++;
+        }
+        try { decode_columnar_file(paths[f], op, files[f]); }
+        catch (const std::exception& ex) { errors[f] = ex.what(); }
+        {
+          std::lock_guard<std::mutex> lk(mu);
+          done[f] = 1;
+        }
+        cv.notify_all();
+      }
+    };
+    std::vector<std::thread> pool;
+    for (unsigned t = 0; t < nt; ++t) pool.emplace_back(work);
+    bool failed = false;
+    for (size_t f = 0; f < nfile; ++f) {
+      {
+        std::unique_lock<std::mutex> lk(mu);
+        cv.wait(lk, [&] { return done[f] != 0; });
+      }
+      if (!errors[f].empty()) failed = true;
+      if (!failed) merge_one(files[f]);
+      else FileCols().swap_into(files[f]);
+      {
+        std::lock_guard<std::mutex> lk(mu);
+        merged = f + 1;
+      }
+      cv.notify_all();
+    }
+    for (auto& t : pool) t.join();
   }
+  for (size_t f = 0; f < nfile; ++f)
+    if (!errors[f].empty()) throw std::runtime_error(errors[f]);
   auto arr_d = [](std::vector<double>& v) { return py::array_t<double>((py::ssize_t)v.size(), v.data()); };
   py::dict out;
   out["n"] = n;

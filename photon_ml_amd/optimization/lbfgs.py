@@ -262,8 +262,11 @@ class LBFGS(Optimizer):
         if use_mls:
             t0 = (1.0 / pre[1] ** 0.5 if pre is not None else 1.0 / _norm(d)) if self._inner_iter == 0 else 1.0
             lazy = pre is not None and not isinstance(pre, list)
-            mls = objective.margin_line_search(data, x0, d, t0, dots=None if pre is None or lazy
-                                               else (pre[2], pre[3], pre[1]))
+            # a device ``pre`` is read after the direction pass is queued: the L2 dots are assigned then, not
+            # recomputed (vdots would cost three reductions and a host synchronisation of their own)
+            from ..function.objective import DEFERRED_DOTS
+            mls = objective.margin_line_search(data, x0, d, t0, dots=None if pre is None else
+                                               (DEFERRED_DOTS if lazy else (pre[2], pre[3], pre[1])))
             if lazy:
                 pre = pre.tolist()
                 if mls is not None and mls.l2 > 0:

@@ -10,7 +10,9 @@ persists final models; Spark lineage recomputation was its only recovery).
   warm-starts from the last one.
 
 Format: safetensors (tensors / numpy arrays only, nothing executable) + a JSON metadata string. Every rank of a
-process group writes its own file (entity-sharded random effects differ per rank).
+process group writes its own file (entity-sharded random effects differ per rank). ``format_version`` 2 stores
+entity-id tables length-prefixed and the writer's world size; version-less files of the first format (ids joined
+by newlines, no world size) still load.
 """
 from __future__ import annotations
 
@@ -23,6 +25,9 @@ import numpy as np
 import torch
 
 from ..constants import TaskType
+
+FORMAT_VERSION = 2
+log = __import__("logging").getLogger(__name__)
 
 
 def _rank() -> int:
@@ -43,8 +48,13 @@ def _strings_to_array(values) -> np.ndarray:
     return np.frombuffer(head + b"".join(enc), dtype=np.uint8).copy()
 
 
-def _array_to_strings(a: np.ndarray, n: int) -> np.ndarray:
+def _array_to_strings(a: np.ndarray, n: int, version: int = FORMAT_VERSION) -> np.ndarray:
     raw = bytes(np.ascontiguousarray(a).tobytes())
+    if version < 2:     # first format: UTF-8 ids joined by newlines
+        ids = raw.decode("utf-8").split("\n") if n else []
+        if len(ids) != n:
+            raise ValueError(f"checkpoint entity table holds {len(ids)} ids, metadata says {n}")
+        return np.array(ids, dtype=object)
     count = int(np.frombuffer(raw[:8], dtype="<i8")[0]) if len(raw) >= 8 else -1
     if count != n:
         raise ValueError(f"checkpoint entity table holds {count} ids, metadata says {n}")
@@ -82,7 +92,7 @@ def game_model_to_arrays(model, prefix: str) -> Tuple[Dict[str, np.ndarray], dic
     return arrays, meta
 
 
-def game_model_from_arrays(arrays: Dict[str, np.ndarray], meta: dict, prefix: str):
+def game_model_from_arrays(arrays: Dict[str, np.ndarray], meta: dict, prefix: str, version: int = FORMAT_VERSION):
     from ..models.game import FixedEffectModel, GameModel, RandomEffectModel
     from ..models.glm import Coefficients, model_for_task
     models = OrderedDict()
@@ -95,7 +105,7 @@ def game_model_from_arrays(arrays: Dict[str, np.ndarray], meta: dict, prefix: st
                                 None if var is None else torch.from_numpy(var.copy()))
             models[c["id"]] = FixedEffectModel(model_for_task(task, coef), c["shard"])
         else:
-            ents = _array_to_strings(arrays[key + ".entities"], c["n_entities"])
+            ents = _array_to_strings(arrays[key + ".entities"], c["n_entities"], version)
             models[c["id"]] = RandomEffectModel(c["re_type"], c["shard"], task, ents, c["dim"],
                                                 arrays[key + ".keys"], arrays[key + ".values"],
                                                 arrays.get(key + ".variances"))
@@ -143,7 +153,8 @@ class Checkpointer:
                 tag: str = ""):
         arrays, meta = game_model_to_arrays(model, "model/")
         meta = {"model": meta, "iteration": iteration, "next": next_coordinate, "tag": tag,
-                "history": history, "best_evals": best_evals, "world_size": _world()}
+                "history": history, "best_evals": best_evals, "world_size": _world(),
+                "format_version": FORMAT_VERSION}
         if best_model is not None:
             ba, bm = game_model_to_arrays(best_model, "best/")
             arrays.update(ba)
@@ -155,12 +166,19 @@ class Checkpointer:
         if got is None:
             return None
         arrays, meta = got
-        if meta.get("world_size", 1) != _world():
+        version = int(meta.get("format_version", 1))
+        if version > FORMAT_VERSION:
+            raise RuntimeError(f"checkpoint {self.path} has format version {version}; this build reads <= "
+                               f"{FORMAT_VERSION}")
+        if "world_size" not in meta:
+            log.warning("checkpoint %s does not record its world size (first format): resuming assumes the same "
+                        "number of ranks wrote it", self.path)
+        elif meta["world_size"] != _world():
             # entity-sharded random effects: each rank's file holds the entities that rank owned
-            raise RuntimeError(f"checkpoint {self.path} was written by {meta.get('world_size', 1)} ranks, "
+            raise RuntimeError(f"checkpoint {self.path} was written by {meta['world_size']} ranks, "
                                f"this run has {_world()}: resume with the same world size")
-        model = game_model_from_arrays(arrays, meta["model"], "model/")
-        best = game_model_from_arrays(arrays, meta["best"], "best/") if "best" in meta else None
+        model = game_model_from_arrays(arrays, meta["model"], "model/", version)
+        best = game_model_from_arrays(arrays, meta["best"], "best/", version) if "best" in meta else None
         return {"model": model, "iteration": meta["iteration"], "next": meta["next"], "best_model": best,
                 "best_evals": meta.get("best_evals"), "history": meta.get("history", []), "tag": meta.get("tag")}
 

@@ -141,3 +141,23 @@ def test_entity_ids_round_trip_any_characters_and_world_size_guard(tmp_path, mon
     c.save({"x": np.zeros(1)}, {"model": {"coordinates": []}, "iteration": 0, "next": 0, "world_size": 2})
     with pytest.raises(RuntimeError, match="world size"):
         c.load_cd()
+
+
+def test_first_format_checkpoint_still_loads(tmp_path):
+    """A version-less checkpoint of the first format (entity ids joined by newlines, no world size) resumes."""
+    from photon_ml_amd.utils import checkpoint as ck
+    ids = ["u1", "u2", "u3"]
+    legacy = np.frombuffer("\n".join(ids).encode("utf-8"), dtype=np.uint8).copy()
+    meta = {"model": {"coordinates": [{"id": "per-user", "kind": "random", "shard": "s", "re_type": "userId",
+                                       "task": "LINEAR_REGRESSION", "dim": 4, "n_entities": 3}]},
+            "iteration": 1, "next": 0}
+    arrays = {"model/per-user.keys": np.array([0, 5, 11], dtype=np.int64),
+              "model/per-user.values": np.array([1.0, 2.0, 3.0]), "model/per-user.entities": legacy}
+    c = ck.Checkpointer(str(tmp_path))
+    c.save(arrays, meta)
+    st = c.load_cd()
+    m = st["model"].get("per-user")
+    assert list(m.entity_ids) == ids and np.array_equal(m.values, [1.0, 2.0, 3.0])
+    c.save(arrays, dict(meta, format_version=ck.FORMAT_VERSION + 1))
+    with pytest.raises(RuntimeError, match="format version"):
+        c.load_cd()
