@@ -69,6 +69,10 @@ def main():
                          "the L-BFGS history sharded over features (all-gather w + reduce-scatter g per evaluation)")
     ap.add_argument("--layout", default="auto", choices=["auto", "tiled", "segmented"],
                     help="sparse layout: tiled (gather-coalesced, default when representable) or segmented")
+    ap.add_argument("--game", default="auto", choices=["auto", "on", "off"],
+                    help="after the timed GLM steps, also time BASELINE.json's GAME metric (coordinate-descent sweeps "
+                         "of config 5 with power-law entity sizes, bench_game.py --config game5pl) and report it as "
+                         "extra keys; auto = on for one GPU")
     args = ap.parse_args()
     cfg = CONFIGS[args.config]
     if args.rows_per_gpu is None:
@@ -152,9 +156,18 @@ def main():
         gnorm = st.grad_norm()
     elapsed = all_reduce_scalar(elapsed, "max", device=dev)
     passes = data.n_passes - passes0
+    n_rows_local, layout_name = data.n_rows, data.layout
     stalled = bool(getattr(opt, "_finished", False))
-    total_rows = int(all_reduce_scalar(data.n_rows, "sum", device=dev)) if is_dist() else data.n_rows
+    total_rows = int(all_reduce_scalar(n_rows_local, "sum", device=dev)) if is_dist() else n_rows_local
     value = total_rows * args.steps / elapsed
+    game = None
+    if args.game == "on" or (args.game == "auto" and world == 1 and args.config == "lbfgs"):
+        # free the GLM shard (115 GiB) before the GAME data is built on the same GPU
+        del data, gdata, opt, obj, w0
+        import gc
+        gc.collect()
+        torch.cuda.empty_cache()
+        game = game_extra(dev, rank, world)
     if rank == 0:
         log(f"final f={st.loss:.6e} |g|={gnorm:.3e} evals/step={passes / args.steps:.2f} "
             f"optimizer_stalled={stalled}")
@@ -180,12 +193,29 @@ def main():
                 "nnz_per_row": args.nnz,
                 "parallelism": f"dp{world}" + ("+fs" if sharded else ""),
                 "optimizer_state": args.optimizer_state,
-                "layout": data.layout,
+                "layout": layout_name,
             },
             "evals_per_step": passes / args.steps,
             "optimizer_stalled": stalled,
         }
+        if game is not None:
+            out.update(game)
         print(json.dumps(out), flush=True)
+
+
+def game_extra(dev, rank: int, world: int) -> dict:
+    """BASELINE.json's second metric (GAME coordinate-descent iterations/sec, config 5) on the power-law entity
+    preset, timed inside this run (bench_game.run: data generated on the device, 2 warmup + 3 timed sweeps, the
+    trained model materialised inside the timed region). Failures are reported, never fatal to the GLM line."""
+    import bench_game
+    try:
+        g = bench_game.run(bench_game.preset_args("game5pl", steps=3, warmup=2), dev, rank, world)
+    except Exception as e:  # pragma: no cover - reported in the record
+        return {"game5pl_error": repr(e)[:500]}
+    return {"game5pl_sweeps_per_sec": g["value"], "game5pl_ms_per_sweep": g["ms_per_step"],
+            "game5pl_config": dict(g["config"], fe_dtype=g["dtype"], re_dtype="fp64", steps=g["steps"],
+                                   warmup=g["warmup"], data_generation_s=round(g["data_generation_s"], 1),
+                                   coordinate_build_s=round(g["coordinate_build_s"], 1))}
 
 
 if __name__ == "__main__":

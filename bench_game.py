@@ -48,7 +48,7 @@ PRESETS = {
 }
 
 
-def main():
+def build_parser() -> argparse.ArgumentParser:
     ap = argparse.ArgumentParser()
     ap.add_argument("--gpus", type=int, default=1)
     ap.add_argument("--steps", type=int, default=3)
@@ -74,7 +74,22 @@ def main():
     ap.add_argument("--seed", type=int, default=11)
     ap.add_argument("--log-level", default="WARNING",
                     help="framework log level (DEBUG shows the per-phase timings of the random-effect update)")
-    args = ap.parse_args()
+    return ap
+
+
+def preset_args(config: str, **overrides) -> argparse.Namespace:
+    """Parsed defaults of a preset (what ``bench_game.py --config <config>`` uses), with overrides."""
+    args = build_parser().parse_args(["--config", config])
+    for k, v in PRESETS[config].items():
+        if getattr(args, k) is None:
+            setattr(args, k, v)
+    for k, v in overrides.items():
+        setattr(args, k, v)
+    return args
+
+
+def main():
+    args = build_parser().parse_args()
     import logging
     logging.basicConfig(stream=sys.stderr, format="[%(asctime)s %(name)s] %(message)s")
     logging.getLogger("photon_ml_amd").setLevel(args.log_level.upper())
@@ -99,6 +114,17 @@ def main():
         dev = torch.device("cuda", local)
     else:
         dev = torch.device("cpu")
+    rec = run(args, dev, rank, world)
+    if rank == 0:
+        print(json.dumps(rec), flush=True)
+
+
+def run(args, dev, rank: int = 0, world: int = 1) -> dict:
+    """Generate the preset's data, build the coordinates, run ``args.warmup`` untimed and ``args.steps`` timed
+    coordinate-descent sweeps; returns the JSON record (rank 0's view; max time over ranks)."""
+    import torch
+    from collections import OrderedDict
+    from photon_ml_amd.parallel.dist import all_reduce_scalar, barrier, is_dist
     from photon_ml_amd.algorithm.coordinate_descent import CoordinateDescent
     from photon_ml_amd.algorithm.coordinates import (FixedEffectCoordinate, RandomEffectCoordinate,
                                                      ShardedRandomEffectCoordinate)
@@ -118,7 +144,8 @@ def main():
         data = generate_game_bench_data_device(args.entities_per_gpu, args.rows_per_entity, args.re_dim, args.re_nnz,
                                                args.fe_dim, args.fe_nnz, device=dev, **gen_kw)
         torch.cuda.empty_cache()
-    log(f"data generated in {time.time() - t0:.1f}s ({'host' if args.host_data or dev.type != 'cuda' else 'device'}): "
+    t_data = time.time() - t0
+    log(f"data generated in {t_data:.1f}s ({'host' if args.host_data or dev.type != 'cuda' else 'device'}): "
         f"{data.n_rows} rows/GPU")
     t0 = time.time()
     fe_cfg = GLMOptimizationConfiguration(OptimizerConfig("LBFGS", args.fe_iters, 1e-12),
@@ -135,7 +162,8 @@ def main():
     ])
     if torch.cuda.is_available():
         torch.cuda.synchronize()
-    log(f"coordinates built in {time.time() - t0:.1f}s; RE: {coords['per-entity'].dataset.summary()}")
+    t_build = time.time() - t0
+    log(f"coordinates built in {t_build:.1f}s; RE: {coords['per-entity'].dataset.summary()}")
     train_eval = build_evaluator("LOGISTIC_LOSS", data.response, data.offsets, data.weights, device=dev)
     cd = CoordinateDescent(coords, train_eval, score_device=dev)
     model, _ = cd.run(args.warmup)
@@ -177,26 +205,28 @@ def main():
                 f"{fb:.3f}, transpose items {ft:.3f}")
         for rec in cd.history[-2 * args.steps:]:
             log(f"  iteration {rec.get('iteration')} coordinate {rec['coordinate']}: {rec['seconds']:.3f}s")
-        print(json.dumps({
-            "metric": "GAME coord-descent iters/sec (fixed + per-entity random effect)",
-            "value": args.steps / elapsed,
-            "unit": "CD iterations/sec",
-            "n_gpus": world,
-            "steps": args.steps,
-            "warmup": args.warmup,
-            "ms_per_step": 1000.0 * elapsed / args.steps,
-            "higher_is_better": True,
-            "scaling": "weak",
-            "vs_baseline": None,
-            "dtype": args.precision,
-            "data": "synthetic (Zipf fixed-effect features, per-entity private random-effect features)",
-            "config": {"model": "game_logistic_fe_lbfgs_re_tron", "preset": args.config, "global_batch": total_rows,
-                       "seq_len": None, "entity_sizes": args.sizes or "uniform",
-                       "entities": args.entities_per_gpu * world, "rows_per_entity": args.rows_per_entity,
-                       "re_dim": args.re_dim, "fe_dim": args.fe_dim, "fe_iters": args.fe_iters,
-                       "re_iters": args.re_iters, "parallelism": f"dp{world}+ep{world}"},
-            "examples_per_sec": total_rows * args.steps / elapsed,
-        }), flush=True)
+    return {
+        "metric": "GAME coord-descent iters/sec (fixed + per-entity random effect)",
+        "value": args.steps / elapsed,
+        "unit": "CD iterations/sec",
+        "n_gpus": world,
+        "steps": args.steps,
+        "warmup": args.warmup,
+        "ms_per_step": 1000.0 * elapsed / args.steps,
+        "higher_is_better": True,
+        "scaling": "weak",
+        "vs_baseline": None,
+        "dtype": args.precision,
+        "data": "synthetic (Zipf fixed-effect features, per-entity private random-effect features)",
+        "config": {"model": "game_logistic_fe_lbfgs_re_tron", "preset": args.config, "global_batch": total_rows,
+                   "seq_len": None, "entity_sizes": args.sizes or "uniform",
+                   "entities": args.entities_per_gpu * world, "rows_per_entity": args.rows_per_entity,
+                   "re_dim": args.re_dim, "fe_dim": args.fe_dim, "fe_iters": args.fe_iters,
+                   "re_iters": args.re_iters, "parallelism": f"dp{world}+ep{world}"},
+        "examples_per_sec": total_rows * args.steps / elapsed,
+        "data_generation_s": t_data,
+        "coordinate_build_s": t_build,
+    }
 
 
 if __name__ == "__main__":

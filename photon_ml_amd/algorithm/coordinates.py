@@ -699,23 +699,19 @@ class ShardedRandomEffectCoordinate(Coordinate):
         self._val_cache = {}
 
     def _route(self, data: GameData, router, ids) -> GameData:
+        """Move this coordinate's rows to the owners of their entities (C8): the feature rows (device-side
+        permutation + all-to-all), the per-row vectors, and the entity ids — integer ids as one int64
+        all-to-all, string ids as codes plus only the distinct names each owner needs
+        (``RowRouter.forward_strings``)."""
         re_type, shard = self.data_config.random_effect_type, self.data_config.feature_shard_id
         fwd = lambda a: router.forward(torch.from_numpy(np.ascontiguousarray(a))).numpy()
-        x = router.forward_csr(data.shard(shard))
-        # entity-id strings of the received rows: send the index into this rank's unique-id table with the row,
-        # and all-gather the (small) unique-id tables once
-        from torch import distributed as tdist
-        from ..parallel.dist import world_size
-        uniq, inv = np.unique(ids.astype(str), return_inverse=True)
-        tables = [None] * world_size()
-        tdist.all_gather_object(tables, list(uniq))
-        code = fwd(inv.astype(np.int64))
-        flat = np.array([s for t in tables for s in t], dtype=object)
-        base = np.concatenate([[0], np.cumsum([len(t) for t in tables])]).astype(np.int64)
-        recv_ids = flat[base[router.src_rank] + code] if len(code) else np.zeros(0, dtype=object)
-        tags = {re_type: recv_ids}
-        return GameData(fwd(data.response), {shard: x}, tags, fwd(data.offsets), fwd(data.weights),
-                        fwd(data.uids), None)
+        with Timed(f"RE {self.coordinate_id}: route rows to entity owners", log, logging.INFO):
+            x = router.forward_csr(data.shard(shard))
+            ids = np.asarray(ids)
+            recv_ids = fwd(ids.astype(np.int64)) if ids.dtype.kind in "iu" else router.forward_strings(ids)
+            tags = {re_type: recv_ids}
+            return GameData(fwd(data.response), {shard: x}, tags, fwd(data.offsets), fwd(data.weights),
+                            fwd(data.uids), None)
 
     @property
     def dataset(self):

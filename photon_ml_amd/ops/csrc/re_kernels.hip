@@ -129,15 +129,118 @@ struct ReTronArgs {
   int max_iter, max_fail, max_cg, dmax;
 };
 
-// One pass over the entity's rows [r0, r1).
+// Sum over the 16 lanes of a DPP row, in every lane of the row (fixed-order butterflies: deterministic).
+__device__ __forceinline__ double row16_total(double v) {
+  v += dpp_f64<0xB1>(v);    // quad_perm [1,0,3,2]
+  v += dpp_f64<0x4E>(v);    // quad_perm [2,3,0,1]
+  v += dpp_f64<0x141>(v);   // row_half_mirror
+  v += dpp_f64<0x140>(v);   // row_mirror
+  return v;
+}
+
+#define RE_G 16                      // lanes per row (one DPP row)
+#define RE_RPI (64 / RE_G)           // rows per wave instruction
+#define RE_U 3                       // instruction groups in flight per wave batch
+#define RE_BATCH (RE_RPI * RE_U)     // rows per wave batch
+#define RE_K 4                       // entries per lane kept in registers (rows of <= 64 entries in one go)
+
+// One pass over the entity's rows [r0, r1): a wave takes RE_BATCH consecutive rows at a time, RE_G lanes per
+// row (lane k of the row: entries k, k + 16, ...). The next batch's row pointers are fetched while the current
+// batch computes, and all RE_BATCH rows' entries are loaded before the first gather, so a batch costs about one
+// dependent global-memory latency.
 // MODE 0: Hessian-vector data term: acc_w += X^T (Dc * (X vec)).
-// MODE 1: value + gradient at vec: acc_w += X^T (wt * l'), fpart += wt * l (lane 0), Dn = wt * l'', Zn = x.vec.
+// MODE 1: value + gradient at vec: acc_w += X^T (wt * l'), fpart += wt * l, Dn = wt * l'', Zn = x.vec.
 // MODE 2: value + gradient at zero (no gathers, no scratch writes).
 template <int MODE>
 __device__ __forceinline__ void row_pass(const ReTronArgs& a, long long r0, long long r1,
                                          const double* __restrict__ vec, double* __restrict__ acc,
                                          const double* __restrict__ Dc, double* __restrict__ Dn,
                                          double* __restrict__ Zn, double& fpart) {
+  const int lane = threadIdx.x & 63, w = threadIdx.x >> 6;
+  const int grp = lane / RE_G, gl = lane % RE_G;
+  const long long step = (long long)RE_NW * RE_BATCH;
+  long long base = r0 + (long long)w * RE_BATCH;
+  // row pointers of a batch: lane j <= RE_BATCH holds nip[base + j] (clamped to the entity's last row)
+  auto fetch_ptr = [&](long long b) -> long long {
+    const long long i = b + (lane <= RE_BATCH ? lane : RE_BATCH);
+    return b < r1 ? a.nip[i < r1 ? i : r1] : 0;
+  };
+  long long np = fetch_ptr(base);
+  for (; base < r1; base += step) {
+    const long long np_next = fetch_ptr(base + step);
+    long long lo[RE_U], hi[RE_U];
+    int c[RE_U][RE_K];
+    double v[RE_U][RE_K], dot[RE_U], rs[RE_U][3];
+#pragma unroll
+    for (int u = 0; u < RE_U; ++u) {
+      const int q = u * RE_RPI + grp;
+      lo[u] = __shfl(np, q, 64);
+      hi[u] = __shfl(np, q + 1, 64);
+      const long long i = base + q;
+      const bool valid = i < r1;
+      if (MODE == 0) {
+        rs[u][0] = valid ? Dc[i] : 0.0;
+      } else {
+        rs[u][0] = valid ? a.wt[i] : 0.0;
+        rs[u][1] = valid ? a.off[i] : 0.0;
+        rs[u][2] = valid ? a.y[i] : 0.0;
+      }
+    }
+#pragma unroll
+    for (int u = 0; u < RE_U; ++u) {
+#pragma unroll
+      for (int k = 0; k < RE_K; ++k) {
+        const long long p = lo[u] + gl + RE_G * k;
+        const bool in = p < hi[u];
+        c[u][k] = in ? (int)a.lcol[p] : 0;
+        v[u][k] = in ? a.val[p] : 0.0;
+      }
+    }
+#pragma unroll
+    for (int u = 0; u < RE_U; ++u) {
+      double s = 0.0;
+      if (MODE != 2) {
+#pragma unroll
+        for (int k = 0; k < RE_K; ++k) s = fma(v[u][k], vec[c[u][k]], s);
+        for (long long p = lo[u] + gl + RE_G * RE_K; p < hi[u]; p += RE_G) s = fma(a.val[p], vec[a.lcol[p]], s);
+      }
+      dot[u] = s;
+    }
+#pragma unroll
+    for (int u = 0; u < RE_U; ++u) {
+      if (MODE != 2) dot[u] = row16_total(dot[u]);
+      const long long i = base + u * RE_RPI + grp;
+      const bool valid = i < r1;
+      double t;
+      if (MODE == 0) {
+        t = rs[u][0] * dot[u];
+      } else {
+        double l = 0.0, dl = 0.0, d2 = 0.0;
+        if (valid) {
+          pointwise_loss(a.loss, dot[u] + rs[u][1], rs[u][2], l, dl, d2);
+          if (gl == 0) {
+            fpart += rs[u][0] * l;
+            if (MODE == 1) { Dn[i] = rs[u][0] * d2; Zn[i] = dot[u]; }
+          }
+        }
+        t = rs[u][0] * dl;
+      }
+#pragma unroll
+      for (int k = 0; k < RE_K; ++k)
+        if (lo[u] + gl + RE_G * k < hi[u]) atomicAdd(&acc[c[u][k]], t * v[u][k]);
+      for (long long p = lo[u] + gl + RE_G * RE_K; p < hi[u]; p += RE_G) atomicAdd(&acc[a.lcol[p]], t * a.val[p]);
+    }
+    np = np_next;
+  }
+}
+
+// Previous row pass (wave per row, lane = entry; one row's entries per instruction) — kept for A/B
+// (PML_RE_ROWPASS=1).
+template <int MODE>
+__device__ __forceinline__ void row_pass_v1(const ReTronArgs& a, long long r0, long long r1,
+                                            const double* __restrict__ vec, double* __restrict__ acc,
+                                            const double* __restrict__ Dc, double* __restrict__ Dn,
+                                            double* __restrict__ Zn, double& fpart) {
   const int lane = threadIdx.x & 63, w = threadIdx.x >> 6;
   for (long long base = r0 + (long long)w * RE_R; base < r1; base += (long long)RE_NW * RE_R) {
     long long lo[RE_R], hi[RE_R];
@@ -191,6 +294,14 @@ __device__ __forceinline__ void row_pass(const ReTronArgs& a, long long r0, long
   }
 }
 
+template <int MODE, int V>
+__device__ __forceinline__ void rows(const ReTronArgs& a, long long r0, long long r1, const double* vec, double* acc,
+                                     const double* Dc, double* Dn, double* Zn, double& fpart) {
+  if constexpr (V == 1) row_pass_v1<MODE>(a, r0, r1, vec, acc, Dc, Dn, Zn, fpart);
+  else row_pass<MODE>(a, r0, r1, vec, acc, Dc, Dn, Zn, fpart);
+}
+
+template <int V>
 __global__ __launch_bounds__(RE_THREADS) void re_tron_csr_kernel(ReTronArgs a) {
   extern __shared__ __attribute__((aligned(16))) double smem[];
   const int e = a.order[blockIdx.x];
@@ -231,8 +342,8 @@ __global__ __launch_bounds__(RE_THREADS) void re_tron_csr_kernel(ReTronArgs a) {
     __syncthreads();
     zero_own();
     double fp = 0.0;
-    if (at_zero) row_pass<2>(a, r0, r1, vec, myacc, nullptr, nullptr, nullptr, fp);
-    else row_pass<1>(a, r0, r1, vec, myacc, nullptr, D[nb], Z[nb], fp);
+    if (at_zero) rows<2, V>(a, r0, r1, vec, myacc, nullptr, nullptr, nullptr, fp);
+    else rows<1, V>(a, r0, r1, vec, myacc, nullptr, D[nb], Z[nb], fp);
     double reg = 0.0;
     for (int j = tid; j < d; j += RE_THREADS) reg += vec[j] * vec[j];
     double s2[2] = {fp, reg};
@@ -283,7 +394,7 @@ __global__ __launch_bounds__(RE_THREADS) void re_tron_csr_kernel(ReTronArgs a) {
       __syncthreads();
       zero_own();
       double fp = 0.0;
-      row_pass<0>(a, r0, r1, sD, myacc, D[cur], nullptr, nullptr, fp);
+      rows<0, V>(a, r0, r1, sD, myacc, D[cur], nullptr, nullptr, fp);
       combine(sD);                                   // acc[0 .. d) = Hd + l2 d
       double s4[4] = {0.0, 0.0, 0.0, 0.0};
       for (int j = tid; j < d; j += RE_THREADS) {
@@ -382,7 +493,11 @@ __global__ __launch_bounds__(RE_THREADS) void re_tron_csr_kernel(ReTronArgs a) {
   if (tid == 0) { a.f[e] = f; a.iters[e] = it; a.reason[e] = reason; }
 }
 
+static int g_re_variant = 2;   // row pass: 2 = 16 lanes per row, batched (default); 1 = one row per wave
+
 extern "C" {
+
+void pml_re_set_variant(int v) { g_re_variant = v == 1 ? 1 : 2; }
 
 // Shared memory of one workgroup for entities of at most ``dmax`` coefficients.
 size_t pml_re_tron_smem(int dmax) { return ((size_t)(5 + RE_NW) * dmax + 2 * RE_NW * 4) * sizeof(double); }
@@ -398,7 +513,8 @@ int pml_re_tron_csr(const int* order, int n_launch, const long long* row_ptr, co
   if (smem > 160 * 1024) return -22;
   ReTronArgs a{order, n_launch, row_ptr, col_ptr, nip, lcol, val, y, off, wt, scr, n_rows, W, f, iters, reason,
                zout, loss, l2, tol, max_iter, max_fail, max_cg, dmax};
-  hipLaunchKernelGGL(re_tron_csr_kernel, dim3(n_launch), dim3(RE_THREADS), smem, st, a);
+  if (g_re_variant == 1) hipLaunchKernelGGL(re_tron_csr_kernel<1>, dim3(n_launch), dim3(RE_THREADS), smem, st, a);
+  else hipLaunchKernelGGL(re_tron_csr_kernel<2>, dim3(n_launch), dim3(RE_THREADS), smem, st, a);
   LAUNCH_CHECK();
   return 0;
 }

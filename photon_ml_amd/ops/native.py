@@ -546,6 +546,8 @@ def re_lib() -> Optional[ctypes.CDLL]:
         lib.pml_re_tron_csr.restype = c_int
         lib.pml_re_tron_smem.argtypes = [c_int]
         lib.pml_re_tron_smem.restype = ctypes.c_size_t
+        lib.pml_re_set_variant.argtypes = [c_int]
+        lib.pml_re_set_variant(int(os.environ.get("PML_RE_ROWPASS", "2")))
         lib._pml_typed = True
     return lib
 

@@ -179,26 +179,72 @@ class RowRouter:
         return out.to(send.device), rc
 
     def forward_csr(self, x: sp.csr_matrix) -> sp.csr_matrix:
-        """Route sparse rows (one all-to-all each for row lengths, column indices and values)."""
+        """Route sparse rows: one all-to-all each for row lengths, column indices and values. The entry
+        permutation runs with torch ops on the communication device (the GPU under RCCL, so the gathers of the
+        1G-entry shards of config 5 are device work and the collectives move device tensors)."""
         x = x.tocsr()
-        lens = np.diff(x.indptr).astype(np.int64)
-        rl = self.forward(torch.from_numpy(lens)).numpy()
-        order = self.perm
-        ol = lens[order]
+        dev = comm_device(self.group)
+        indptr = torch.from_numpy(x.indptr.astype(np.int64)).to(dev)
+        lens = indptr[1:] - indptr[:-1]
+        perm = self.perm_on(dev)
+        ol = lens[perm]
         tot = int(ol.sum())
-        # entry positions of the permuted rows, vectorised: start of each row repeated + offset within the row
-        first = np.repeat(x.indptr[order].astype(np.int64) - np.concatenate([[0], np.cumsum(ol)[:-1]]), ol)
-        ent = first + np.arange(tot, dtype=np.int64)
-        idx, val = x.indices[ent], x.data[ent]
-        nnz_send = [int(lens[order[a:b]].sum()) for a, b in _ranges(self.send_counts)]
-        nnz_recv = [int(rl[a:b].sum()) for a, b in _ranges(self.recv_counts)]
-        ri = torch.from_numpy(idx.astype(np.int64))
-        rv = torch.from_numpy(val.astype(np.float64))
+        start = torch.cumsum(ol, 0) - ol
+        ent = torch.repeat_interleave(indptr[:-1][perm] - start, ol, output_size=tot) + torch.arange(tot, device=dev)
+        ri = torch.from_numpy(x.indices).to(dev)[ent].to(torch.int64)
+        rv = torch.from_numpy(x.data).to(dev, torch.float64)[ent]
+        del ent
+        sc = torch.tensor(self.send_counts, dtype=torch.int64, device=dev)
+        seg = torch.repeat_interleave(torch.arange(len(self.send_counts), device=dev), sc, output_size=perm.numel())
+        nnz_send = torch.zeros(len(self.send_counts), dtype=torch.int64, device=dev).index_add_(0, seg, ol).tolist()
+        rl = self.forward(lens)
+        rseg = torch.repeat_interleave(torch.arange(len(self.recv_counts), device=dev),
+                                       torch.tensor(self.recv_counts, dtype=torch.int64, device=dev),
+                                       output_size=rl.numel())
+        nnz_recv = torch.zeros(len(self.recv_counts), dtype=torch.int64, device=dev).index_add_(0, rseg, rl).tolist()
         if is_dist():
             ri, _ = self._a2a(ri, nnz_send, nnz_recv)
             rv, _ = self._a2a(rv, nnz_send, nnz_recv)
-        indptr = np.concatenate([[0], np.cumsum(rl)]).astype(np.int64)
-        return sp.csr_matrix((rv.numpy(), ri.numpy(), indptr), shape=(self.n_recv, x.shape[1]))
+        rip = torch.zeros(rl.numel() + 1, dtype=torch.int64, device=dev)
+        torch.cumsum(rl, 0, out=rip[1:])
+        out = sp.csr_matrix((rv.cpu().numpy(), ri.to(torch.int32).cpu().numpy(), rip.cpu().numpy()),
+                            shape=(self.n_recv, x.shape[1]))
+        out.has_sorted_indices = bool(getattr(x, "has_sorted_indices", False))
+        return out
+
+    def forward_strings(self, ids: np.ndarray) -> np.ndarray:
+        """Route a per-row string column (e.g. entity ids): per-row codes into this rank's table of distinct
+        values (one int64 all-to-all) plus, to each destination, the UTF-8 bytes of only the distinct values its
+        rows use (two variable-size all-to-alls of lengths and bytes) — no object collectives, no table
+        all-gather."""
+        import pandas as pd
+        P = _world()
+        codes, uniq = pd.factorize(np.asarray(ids, dtype=object), sort=False)
+        codes = codes.astype(np.int64)
+        dest = np.empty(self.n_local, dtype=np.int64)
+        dest[self.perm] = np.repeat(np.arange(P), self.send_counts)
+        # distinct values needed per destination, renumbered per destination
+        pair = dest * max(len(uniq), 1) + codes
+        up, pinv = np.unique(pair, return_inverse=True)
+        u_dest, u_code = up // max(len(uniq), 1), up % max(len(uniq), 1)
+        first = np.searchsorted(u_dest, np.arange(P))
+        local_code = pinv - first[dest]                       # index into the destination's table
+        enc = [str(v).encode("utf-8") for v in uniq[u_code]]
+        blen = np.array([len(b) for b in enc], dtype=np.int64)
+        tab_counts = np.bincount(u_dest, minlength=P).tolist()
+        byte_counts = [int(blen[a:b].sum()) for a, b in _ranges(tab_counts)]
+        payload = np.frombuffer(b"".join(enc), dtype=np.uint8).copy() if enc else np.zeros(0, np.uint8)
+        rc = self.forward(torch.from_numpy(local_code)).numpy()
+        if is_dist():
+            rlen, rtab = all_to_all_varlen(torch.from_numpy(blen), tab_counts, self.group)
+            rbytes, _ = all_to_all_varlen(torch.from_numpy(payload), byte_counts, self.group)
+            rlen, rbytes = rlen.cpu().numpy(), bytes(rbytes.cpu().numpy())
+        else:
+            rlen, rtab, rbytes = blen, tab_counts, bytes(payload)
+        ends = np.cumsum(rlen)
+        names = np.array([rbytes[e - l:e].decode("utf-8") for e, l in zip(ends, rlen)], dtype=object)
+        tab_base = np.concatenate([[0], np.cumsum(rtab)[:-1]]).astype(np.int64)
+        return names[tab_base[self.src_rank] + rc] if len(rc) else np.zeros(0, dtype=object)
 
 
 def _ranges(counts: Sequence[int]):
