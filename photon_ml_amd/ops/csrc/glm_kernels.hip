@@ -1899,6 +1899,23 @@ __device__ __forceinline__ void group_sum2(double& a, double& b) {
   if constexpr (GL >= 16) { a += dpp_f64<0x140>(a); b += dpp_f64<0x140>(b); }
 }
 
+// five independent group sums, stage by stage (ILP 5)
+template <int GL>
+__device__ __forceinline__ void group_sum5(double (&v)[5]) {
+#pragma unroll
+  for (int j = 0; j < 5; ++j) v[j] += dpp_f64<0xB1>(v[j]);
+#pragma unroll
+  for (int j = 0; j < 5; ++j) v[j] += dpp_f64<0x4E>(v[j]);
+  if constexpr (GL >= 8) {
+#pragma unroll
+    for (int j = 0; j < 5; ++j) v[j] += dpp_f64<0x141>(v[j]);
+  }
+  if constexpr (GL >= 16) {
+#pragma unroll
+    for (int j = 0; j < 5; ++j) v[j] += dpp_f64<0x140>(v[j]);
+  }
+}
+
 template <int GL>
 __device__ __forceinline__ double group_sum(double v) {
   v += dpp_f64<0xB1>(v);                       // quad_perm [1,0,3,2]
@@ -1923,7 +1940,12 @@ struct RsGeom {
   static constexpr int WPB = REG ? 4 : WL;          // waves per workgroup (LDS sizes: WL, see variant 5)
 };
 
-template <int K, bool LREG, int WL>
+// MS (variant 6): ONE group-sum phase per CG step — d.Hd, step.d, d.d, r.Hd and Hd.Hd summed together (five
+// independent DPP chains), the trial norm and the new residual norm by algebra:
+//   ||step + a d||^2 = ||step||^2 + 2 a step.d + a^2 d.d,   ||r - a Hd||^2 = r.r - 2 a r.Hd + a^2 Hd.Hd
+// (clamped at 0). The baseline variant pays a serial sum for d.Hd, then one for the two norms, and a third when a
+// problem hits the trust region.
+template <int K, bool LREG, int WL, bool MS = false>
 __global__ __launch_bounds__(256) void rs_tron_dpp_kernel(
     int B, int n, const double* __restrict__ Lm, const double* __restrict__ Y, const double* __restrict__ O,
     const double* __restrict__ WT, double* __restrict__ Beta, double* __restrict__ Fout, int* __restrict__ Iters,
@@ -2129,6 +2151,47 @@ __global__ __launch_bounds__(256) void rs_tron_dpp_kernel(
 #pragma unroll
       for (int s = 0; s < R; ++s) u[s] *= Dw[s];
       mvt(u, Hl);
+      if constexpr (MS) {
+        double sv[5] = {0.0, 0.0, 0.0, 0.0, 0.0};
+#pragma unroll
+        for (int s = 0; s < R; ++s) {
+          Hl[s] += l2 * d[s];
+          sv[0] += d[s] * Hl[s];
+          sv[1] += step[s] * d[s];
+          sv[2] += d[s] * d[s];
+          sv[3] += r[s] * Hl[s];
+          sv[4] += Hl[s] * Hl[s];
+        }
+        group_sum5<GL>(sv);
+        const double dhd = sv[0], std_ = sv[1], dtd = sv[2], rh = sv[3], hh = sv[4];
+        const double alpha = rtr / (dhd == 0.0 ? 1.0 : dhd);
+        double tn = sts + 2.0 * alpha * std_ + alpha * alpha * dtd;
+        tn = tn > 0.0 ? tn : 0.0;
+        const double dsq = delta * delta;
+        const bool hit = tn > dsq;
+        double a = alpha;
+        if (hit) {
+          const double qd = std_ * std_ + dtd * (dsq - sts);
+          const double rad = sqrt(qd > 0.0 ? qd : 0.0);
+          const double den1 = std_ + rad;
+          a = std_ >= 0.0 ? (dsq - sts) / (den1 > 1e-300 ? den1 : 1e-300)
+                          : (rad - std_) / (dtd > 1e-300 ? dtd : 1e-300);
+        }
+        double rn = rtr - 2.0 * a * rh + a * a * hh;
+        rn = rn > 0.0 ? rn : 0.0;
+        const double beta = rn / (rtr == 0.0 ? 1.0 : rtr);
+        if (cg_on) {
+#pragma unroll
+          for (int s = 0; s < R; ++s) {
+            step[s] += a * d[s];
+            r[s] -= a * Hl[s];
+            if (!hit) d[s] = r[s] + beta * d[s];
+          }
+          if (!hit) { rtr = rn; sts = tn; }
+        }
+        cg_on = cg_on && !hit;
+        continue;
+      }
 #pragma unroll
       for (int s = 0; s < R; ++s) { Hl[s] += l2 * d[s]; t[s] = d[s] * Hl[s]; }
       const double dhd = gsum(t);
@@ -2230,7 +2293,7 @@ __global__ __launch_bounds__(256) void rs_tron_dpp_kernel(
   if (prob_on && i == 0) { Fout[b] = f; Iters[b] = it; Reason[b] = reason; }
 }
 
-template <int K, bool LREG, int WL = 2>
+template <int K, bool LREG, int WL = 2, bool MS = false>
 static void launch_rs_tron_dpp(int B, int n, const double* L, const double* y, const double* off, const double* wt,
                                double* beta, double* f, int* iters, int* reason, int loss, double l2, double tol,
                                int max_iter, int max_fail, int max_cg, hipStream_t st, const int* order) {
@@ -2238,7 +2301,7 @@ static void launch_rs_tron_dpp(int B, int n, const double* L, const double* y, c
   const long long waves = (B + Gm::P - 1) / Gm::P;
   const long long grid = (waves + Gm::WPB - 1) / Gm::WPB;
   const size_t lds = Gm::REG ? 0 : (size_t)Gm::WPB * Gm::P * Gm::PS * sizeof(double);
-  hipLaunchKernelGGL((rs_tron_dpp_kernel<K, LREG, WL>), dim3((unsigned)grid), dim3(Gm::WPB * 64), lds, st, B, n, L, y, off, wt,
+  hipLaunchKernelGGL((rs_tron_dpp_kernel<K, LREG, WL, MS>), dim3((unsigned)grid), dim3(Gm::WPB * 64), lds, st, B, n, L, y, off, wt,
                      beta, f, iters, reason, loss, l2, tol, max_iter, max_fail, max_cg, order);
 }
 
@@ -2748,6 +2811,8 @@ int pml_rs_tron(int B, int n, const double* L, const double* y, const double* of
                                          max_fail, max_cg, st, order)                                              \
    : V == 5 ? launch_rs_tron_dpp<KK, true, 1>(B, n, L, y, off, wt, beta, f, iters, reason, loss, l2, tol, max_iter, \
                                               max_fail, max_cg, st, order)                                         \
+   : V == 6 ? launch_rs_tron_dpp<KK, true, 1, true>(B, n, L, y, off, wt, beta, f, iters, reason, loss, l2, tol,    \
+                                                    max_iter, max_fail, max_cg, st, order)                         \
           : launch_rs_tron_dpp<KK, false>(B, n, L, y, off, wt, beta, f, iters, reason, loss, l2, tol, max_iter,   \
                                           max_fail, max_cg, st, order))
     if (n <= 4) RS_DPP(4);

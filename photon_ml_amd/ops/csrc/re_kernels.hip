@@ -82,7 +82,7 @@ __device__ __forceinline__ double wave_total(double v) {
   return (readlane_f64(v, 0) + readlane_f64(v, 16)) + (readlane_f64(v, 32) + readlane_f64(v, 48));
 }
 
-// Workgroup sums of K values (K <= 4), in every thread. ``red`` holds two [RE_NW][4] slots used alternately,
+// Workgroup sums of K values (K <= 8), in every thread. ``red`` holds two [RE_NW][8] slots used alternately,
 // so one barrier per call suffices: a slot is rewritten only two calls later, after every thread has passed
 // the barrier of the call in between (all threads run the same, workgroup-uniform control flow).
 template <int K>
@@ -90,17 +90,17 @@ __device__ __forceinline__ void block_sums(double (&v)[K], double* __restrict__ 
   const int lane = threadIdx.x & 63, w = threadIdx.x >> 6;
 #pragma unroll
   for (int k = 0; k < K; ++k) v[k] = wave_total(v[k]);
-  double* slot = red + parity * (RE_NW * 4);
+  double* slot = red + parity * (RE_NW * 8);
   if (lane == 0) {
 #pragma unroll
-    for (int k = 0; k < K; ++k) slot[w * 4 + k] = v[k];
+    for (int k = 0; k < K; ++k) slot[w * 8 + k] = v[k];
   }
   __syncthreads();
 #pragma unroll
   for (int k = 0; k < K; ++k) {
     double s = 0.0;
 #pragma unroll
-    for (int q = 0; q < RE_NW; ++q) s += slot[q * 4 + k];
+    for (int q = 0; q < RE_NW; ++q) s += slot[q * 8 + k];
     v[k] = s;
   }
   parity ^= 1;
@@ -124,6 +124,7 @@ struct ReTronArgs {
   int* iters;
   int* reason;
   double* zout;              // per row: x_i . w of the solution (no offset)
+  int* npass;                // optional, per entity: row passes run (function evaluations + Hessian-vector)
   int loss;
   double l2, tol;
   int max_iter, max_fail, max_cg, dmax;
@@ -320,120 +321,121 @@ __global__ __launch_bounds__(RE_THREADS) void re_tron_csr_kernel(ReTronArgs a) {
   double* myacc = acc + w * dm;
   double* D[2] = {a.scr, a.scr + a.n_rows};
   double* Z[2] = {a.scr + 2 * a.n_rows, a.scr + 3 * a.n_rows};
-  int cur = 0, parity = 0;
+  int cur = 0, parity = 0, npass = 0;
   double* Wg = a.W + c0;
 
-  // combine the wave accumulators into acc[0] (+ l2 * src), zeroing the others for the next pass
-  auto combine = [&](const double* __restrict__ src) {
-    __syncthreads();
-    for (int j = tid; j < d; j += RE_THREADS) {
-      double s = acc[j];
-#pragma unroll
-      for (int q = 1; q < RE_NW; ++q) s += acc[q * dm + j];
-      acc[j] = s + a.l2 * src[j];
-    }
-    __syncthreads();
-  };
   auto zero_own = [&]() {
     for (int j = lane; j < d; j += 64) myacc[j] = 0.0;
   };
-  // value + gradient at vec (MODE 1: writes D / Z buffer ``nb``), gradient into acc[0 .. d)
-  auto value_grad = [&](const double* vec, int nb, bool at_zero) -> double {
+  // value + gradient at vec (MODE 1: writes D / Z buffer ``nb``); the gradient lands in acc[0 .. d). One sweep
+  // combines the wave accumulators (fixed wave order) and forms ||vec||^2 and ||g||^2; three barriers in all.
+  auto value_grad = [&](const double* vec, int nb, bool at_zero, double& gg) -> double {
+    ++npass;
     __syncthreads();
     zero_own();
     double fp = 0.0;
     if (at_zero) rows<2, V>(a, r0, r1, vec, myacc, nullptr, nullptr, nullptr, fp);
     else rows<1, V>(a, r0, r1, vec, myacc, nullptr, D[nb], Z[nb], fp);
-    double reg = 0.0;
-    for (int j = tid; j < d; j += RE_THREADS) reg += vec[j] * vec[j];
-    double s2[2] = {fp, reg};
-    block_sums<2>(s2, red, parity);
-    combine(vec);
-    return s2[0] + 0.5 * a.l2 * s2[1];
+    __syncthreads();
+    double s3[3] = {fp, 0.0, 0.0};
+    for (int j = tid; j < d; j += RE_THREADS) {
+      double g = acc[j];
+#pragma unroll
+      for (int q = 1; q < RE_NW; ++q) g += acc[q * dm + j];
+      const double v = vec[j];
+      g += a.l2 * v;
+      acc[j] = g;
+      s3[1] += v * v;
+      s3[2] += g * g;
+    }
+    block_sums<3>(s3, red, parity);
+    gg = s3[2];
+    return s3[0] + 0.5 * a.l2 * s3[1];
   };
 
   for (int j = tid; j < d; j += RE_THREADS) sW[j] = Wg[j];
-  __syncthreads();
-  double f = value_grad(sW, cur, false);
-  double nz = 0.0, gg = 0.0;
+  double gnorm2;
+  double f = value_grad(sW, cur, false, gnorm2);
+  double nz[1] = {0.0};
   for (int j = tid; j < d; j += RE_THREADS) {
     sG[j] = acc[j];
-    nz += sW[j] != 0.0 ? 1.0 : 0.0;
-    gg += acc[j] * acc[j];
+    nz[0] += sW[j] != 0.0 ? 1.0 : 0.0;
   }
-  double s2[2] = {nz, gg};
-  block_sums<2>(s2, red, parity);
-  double f0z = f, g0n = sqrt(s2[1]);
-  if (s2[0] != 0.0) {
+  block_sums<1>(nz, red, parity);
+  double f0z = f, g0n = sqrt(gnorm2);
+  if (nz[0] != 0.0) {
     for (int j = tid; j < d; j += RE_THREADS) sS[j] = 0.0;   // zero vector for the state at zero
-    f0z = value_grad(sS, 0, true);
-    double g0[1] = {0.0};
-    for (int j = tid; j < d; j += RE_THREADS) g0[0] += acc[j] * acc[j];
-    block_sums<1>(g0, red, parity);
-    g0n = sqrt(g0[0]);
+    double g0;
+    f0z = value_grad(sS, 0, true, g0);
+    g0n = sqrt(g0);
   }
   const double loss_tol = f0z * a.tol, grad_tol = g0n * a.tol;
-  double delta = sqrt(s2[1]);
+  double delta = sqrt(gnorm2);
   int it = 0, fails = 0, reason = 0;
   bool active = true;
   if (delta == 0.0) { reason = 4; active = false; }
   const double eta0 = 1e-4, eta1 = 0.25, eta2 = 0.75, sg1 = 0.25, sg2 = 0.5, sg3 = 4.0;
   const int guard_max = a.max_iter * (a.max_fail + 1) + 5;
-  double gnorm2 = s2[1];
   for (int guard = 0; active && guard < guard_max; ++guard) {
-    // ---- truncated CG at W (Hessian weights D[cur])
+    // ---- truncated CG at W (Hessian weights D[cur]). Per CG step: the Hessian-vector pass, ONE sweep that
+    // combines the accumulators and forms d.Hd, step.d, d.d, r.Hd, Hd.Hd, one workgroup sum, and one update
+    // sweep; ||step + a d||^2 and ||r - a Hd||^2 follow by algebra (clamped at 0).
     for (int j = tid; j < d; j += RE_THREADS) {
       sS[j] = 0.0;
       sR[j] = -sG[j];
       sD[j] = -sG[j];
     }
-    double rtr = gnorm2;
-    const double cg_tol = 0.1 * sqrt(gnorm2);
+    double rtr = gnorm2, sts = 0.0;
+    const double cg_tol2 = 0.01 * gnorm2;        // (0.1 ||g||)^2
     for (int k = 0; k < a.max_cg; ++k) {
-      if (!(sqrt(rtr > 0.0 ? rtr : 0.0) > cg_tol)) break;
+      if (!(rtr > cg_tol2)) break;
+      ++npass;
       __syncthreads();
       zero_own();
       double fp = 0.0;
       rows<0, V>(a, r0, r1, sD, myacc, D[cur], nullptr, nullptr, fp);
-      combine(sD);                                   // acc[0 .. d) = Hd + l2 d
-      double s4[4] = {0.0, 0.0, 0.0, 0.0};
+      __syncthreads();
+      double s5[5] = {0.0, 0.0, 0.0, 0.0, 0.0};
       for (int j = tid; j < d; j += RE_THREADS) {
-        const double dj = sD[j], sj = sS[j];
-        s4[0] += dj * acc[j];
-        s4[1] += sj * dj;
-        s4[2] += sj * sj;
-        s4[3] += dj * dj;
+        double h = acc[j];
+#pragma unroll
+        for (int q = 1; q < RE_NW; ++q) h += acc[q * dm + j];
+        const double dj = sD[j];
+        h += a.l2 * dj;
+        acc[j] = h;
+        s5[0] += dj * h;
+        s5[1] += sS[j] * dj;
+        s5[2] += dj * dj;
+        s5[3] += sR[j] * h;
+        s5[4] += h * h;
       }
-      block_sums<4>(s4, red, parity);
-      const double dhd = s4[0], std_ = s4[1], sts = s4[2], dtd = s4[3];
+      block_sums<5>(s5, red, parity);
+      const double dhd = s5[0], std_ = s5[1], dtd = s5[2], rh = s5[3], hh = s5[4];
       const double alpha = rtr / (dhd == 0.0 ? 1.0 : dhd);
-      double tn[1] = {0.0};
-      for (int j = tid; j < d; j += RE_THREADS) {
-        const double tr = sS[j] + alpha * sD[j];
-        tn[0] += tr * tr;
-      }
-      block_sums<1>(tn, red, parity);
-      const bool hit = sqrt(tn[0] > 0.0 ? tn[0] : 0.0) > delta;
+      double tn = sts + 2.0 * alpha * std_ + alpha * alpha * dtd;
+      tn = tn > 0.0 ? tn : 0.0;
+      const double dsq = delta * delta;
+      const bool hit = tn > dsq;
       double al = alpha;
       if (hit) {
-        const double dsq = delta * delta;
         const double q = std_ * std_ + dtd * (dsq - sts);
         const double rad = sqrt(q > 0.0 ? q : 0.0);
         const double den1 = std_ + rad;
         al = std_ >= 0.0 ? (dsq - sts) / (den1 > 1e-300 ? den1 : 1e-300) : (rad - std_) / (dtd > 1e-300 ? dtd : 1e-300);
       }
-      double rn[1] = {0.0};
+      double rn = rtr - 2.0 * al * rh + al * al * hh;
+      rn = rn > 0.0 ? rn : 0.0;
+      const double beta = rn / (rtr == 0.0 ? 1.0 : rtr);
       for (int j = tid; j < d; j += RE_THREADS) {
-        sS[j] += al * sD[j];
+        const double dj = sD[j];
+        sS[j] += al * dj;
         const double r = sR[j] - al * acc[j];
         sR[j] = r;
-        rn[0] += r * r;
+        if (!hit) sD[j] = r + beta * dj;
       }
-      block_sums<1>(rn, red, parity);
       if (hit) break;
-      const double beta = rn[0] / (rtr == 0.0 ? 1.0 : rtr);
-      for (int j = tid; j < d; j += RE_THREADS) sD[j] = sR[j] + beta * sD[j];
-      rtr = rn[0];
+      rtr = rn;
+      sts = tn;
     }
     // ---- trial point W + step (in the direction slot), trust-region update, acceptance
     double s3[3] = {0.0, 0.0, 0.0};
@@ -446,7 +448,8 @@ __global__ __launch_bounds__(RE_THREADS) void re_tron_csr_kernel(ReTronArgs a) {
     }
     block_sums<3>(s3, red, parity);
     const double gs = s3[0], pred = -0.5 * (gs - s3[1]), snorm = sqrt(s3[2]);
-    const double fn = value_grad(sD, cur ^ 1, false);   // trial gradient in acc[0 .. d)
+    double gn2;
+    const double fn = value_grad(sD, cur ^ 1, false, gn2);   // trial gradient in acc[0 .. d)
     const double actual = f - fn;
     if (it == 0) delta = fmin(delta, snorm);
     const double den = fn - f - gs;
@@ -460,15 +463,11 @@ __global__ __launch_bounds__(RE_THREADS) void re_tron_csr_kernel(ReTronArgs a) {
     const bool accept = actual > eta0 * pred;
     const double f_prev = f;
     if (accept) {
-      double g2[1] = {0.0};
       for (int j = tid; j < d; j += RE_THREADS) {
         sW[j] = sD[j];
-        const double gj = acc[j];
-        sG[j] = gj;
-        g2[0] += gj * gj;
+        sG[j] = acc[j];
       }
-      block_sums<1>(g2, red, parity);
-      gnorm2 = g2[0];
+      gnorm2 = gn2;
       f = fn;
       cur ^= 1;
       ++it;
@@ -490,7 +489,10 @@ __global__ __launch_bounds__(RE_THREADS) void re_tron_csr_kernel(ReTronArgs a) {
     const double* zc = Z[cur];
     for (long long i = r0 + tid; i < r1; i += RE_THREADS) a.zout[i] = zc[i];
   }
-  if (tid == 0) { a.f[e] = f; a.iters[e] = it; a.reason[e] = reason; }
+  if (tid == 0) {
+    a.f[e] = f; a.iters[e] = it; a.reason[e] = reason;
+    if (a.npass != nullptr) a.npass[e] = npass;
+  }
 }
 
 static int g_re_variant = 2;   // row pass: 2 = 16 lanes per row, batched (default); 1 = one row per wave
@@ -500,19 +502,19 @@ extern "C" {
 void pml_re_set_variant(int v) { g_re_variant = v == 1 ? 1 : 2; }
 
 // Shared memory of one workgroup for entities of at most ``dmax`` coefficients.
-size_t pml_re_tron_smem(int dmax) { return ((size_t)(5 + RE_NW) * dmax + 2 * RE_NW * 4) * sizeof(double); }
+size_t pml_re_tron_smem(int dmax) { return ((size_t)(5 + RE_NW) * dmax + 2 * RE_NW * 8) * sizeof(double); }
 
 int pml_re_tron_csr(const int* order, int n_launch, const long long* row_ptr, const long long* col_ptr,
                     const long long* nip, const uint16_t* lcol, const double* val, const double* y,
                     const double* off, const double* wt, double* scr, long long n_rows, double* W, double* f,
-                    int* iters, int* reason, double* zout, int loss, double l2, double tol, int max_iter,
-                    int max_fail, int max_cg, int dmax, hipStream_t st) {
+                    int* iters, int* reason, double* zout, int* npass, int loss, double l2, double tol,
+                    int max_iter, int max_fail, int max_cg, int dmax, hipStream_t st) {
   if (n_launch <= 0) return 0;
   if (dmax <= 0 || loss < 0 || loss > 2) return -22;
   const size_t smem = pml_re_tron_smem(dmax);
   if (smem > 160 * 1024) return -22;
   ReTronArgs a{order, n_launch, row_ptr, col_ptr, nip, lcol, val, y, off, wt, scr, n_rows, W, f, iters, reason,
-               zout, loss, l2, tol, max_iter, max_fail, max_cg, dmax};
+               zout, npass, loss, l2, tol, max_iter, max_fail, max_cg, dmax};
   if (g_re_variant == 1) hipLaunchKernelGGL(re_tron_csr_kernel<1>, dim3(n_launch), dim3(RE_THREADS), smem, st, a);
   else hipLaunchKernelGGL(re_tron_csr_kernel<2>, dim3(n_launch), dim3(RE_THREADS), smem, st, a);
   LAUNCH_CHECK();

@@ -541,7 +541,7 @@ def re_lib() -> Optional[ctypes.CDLL]:
     """Fused per-entity primal TRON (``ops/csrc/re_kernels.hip``)."""
     lib = _load("re")
     if lib is not None and not getattr(lib, "_pml_typed", False):
-        lib.pml_re_tron_csr.argtypes = ([c_void_p, c_int] + [c_void_p] * 9 + [ctypes.c_longlong] + [c_void_p] * 5
+        lib.pml_re_tron_csr.argtypes = ([c_void_p, c_int] + [c_void_p] * 9 + [ctypes.c_longlong] + [c_void_p] * 6
                                         + [c_int, c_double, c_double, c_int, c_int, c_int, c_int, c_void_p])
         lib.pml_re_tron_csr.restype = c_int
         lib.pml_re_tron_smem.argtypes = [c_int]
@@ -561,13 +561,15 @@ def require_re_lib() -> ctypes.CDLL:
 
 
 def re_tron_csr(order, row_ptr, col_ptr, nip, lcol, val, y, off, wt, scr, W, f, iters, reason, zout, loss_id: int,
-                l2: float, tol: float, max_iter: int, max_fail: int, max_cg: int, dmax: int) -> None:
+                l2: float, tol: float, max_iter: int, max_fail: int, max_cg: int, dmax: int,
+                npass: Optional[torch.Tensor] = None) -> None:
     """Fused per-entity primal TRON over the entities ``order`` (int32; one workgroup each) of a block-diagonal
     CSR (``re_tron_csr_kernel``). Entity ``e`` owns rows ``row_ptr[e]:row_ptr[e+1]`` (int64) and coefficients
     ``col_ptr[e]:col_ptr[e+1]`` of the packed ``W`` (fp64, in: warm start, out: solution); ``nip`` int64 row
     pointers, ``lcol`` int16 entity-local columns (< d_e <= dmax, distinct inside a row), ``val`` fp64; ``y``,
     ``off``, ``wt`` per row; ``scr`` fp64 scratch of 4 x rows; outputs ``f`` / ``iters`` / ``reason`` per
-    entity and ``zout`` (x_i . w per row). Device only; in place, nothing returned."""
+    entity and ``zout`` (x_i . w per row); ``npass`` (optional int32 per entity): row passes run. Device only; in
+    place, nothing returned."""
     lib = require_re_lib()
     n_rows = y.numel()
     B = int(order.numel())
@@ -581,6 +583,8 @@ def re_tron_csr(order, row_ptr, col_ptr, nip, lcol, val, y, off, wt, scr, W, f, 
     assert iters.dtype == reason.dtype == torch.int32 and dmax % 64 == 0
     n_ent = row_ptr.numel() - 1
     assert col_ptr.numel() == n_ent + 1 and W.numel() == int(col_ptr[-1]) and f.numel() == n_ent
+    if npass is not None:
+        assert npass.is_cuda and npass.dtype == torch.int32 and npass.numel() == n_ent
     if os.environ.get("PML_CHECK_KERNEL_INPUTS", "0") == "1" and B:
         # the kernel indexes entities through ``order`` and sizes its LDS vectors by dmax
         assert int(order.min()) >= 0 and int(order.max()) < n_ent, "re_tron order out of range"
@@ -590,7 +594,9 @@ def re_tron_csr(order, row_ptr, col_ptr, nip, lcol, val, y, off, wt, scr, W, f, 
     check(lib.pml_re_tron_csr(order.data_ptr(), B, row_ptr.data_ptr(), col_ptr.data_ptr(), nip.data_ptr(),
                               lcol.data_ptr(), val.data_ptr(), y.data_ptr(), off.data_ptr(), wt.data_ptr(),
                               scr.data_ptr(), n_rows, W.data_ptr(), f.data_ptr(), iters.data_ptr(),
-                              reason.data_ptr(), zout.data_ptr(), int(loss_id), float(l2), float(tol), int(max_iter),
+                              reason.data_ptr(), zout.data_ptr(),
+                              None if npass is None else npass.data_ptr(), int(loss_id), float(l2), float(tol),
+                              int(max_iter),
                               int(max_fail), int(max_cg), int(dmax), stream_handle(W.device)), "re_tron_csr")
 
 

@@ -302,7 +302,7 @@ def test_batched_small_gemv_and_hv_match_torch(n):
                                          ("LOGISTIC", 16), ("POISSON", 18), ("LOGISTIC", 24), ("SQUARED", 29),
                                          ("LOGISTIC", 32)])
 @pytest.mark.parametrize("warm", [False, True])
-@pytest.mark.parametrize("variant", [0, 1, 2, 3, 4, 5])
+@pytest.mark.parametrize("variant", [0, 1, 2, 3, 4, 5, 6])
 def test_fused_row_space_tron_matches_batched_tron(loss_name, n, warm, variant):
     """rs_tron_kernel (whole per-problem TRON in one kernel) vs the vectorised batched TRON of
     optimization/batched.py on the same dense problems (fp64): same solutions, objective and iteration counts.
