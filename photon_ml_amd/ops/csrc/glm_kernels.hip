@@ -2510,6 +2510,62 @@ __global__ __launch_bounds__(256) void lbfgs_step_kernel(TwoLoopStep st, long lo
   }
 }
 
+
+// Vector-free two-loop ON THE DEVICE (Chen, Wang & Zhou 2014): H g is a combination of the basis
+// b = [s_0 .. s_{k-1}, y_0 .. y_{k-1}, g]; the recursion runs on the 2k + 1 coefficients using the Gram matrix
+// B = b b^T. Three launches and no host synchronisation: gram_kernel (ONE read of the 2k + 1 vectors, per-block
+// partials), gram_two_loop_kernel (one workgroup: sums the partials in block order — deterministic — and runs the
+// recursion on B in LDS; rho_i = 1 / B[i][k+i], initial scale B[k-1][2k-1] / B[2k-1][2k-1] of the newest pair),
+// lincomb_dev_kernel (ONE read of the basis, coefficients from device memory). The step chain it replaces costs
+// 2k + 1 dependent launches, each a full pass with a last-workgroup reduction.
+__global__ __launch_bounds__(256) void gram_two_loop_kernel(const double* __restrict__ partial, int grid, int k,
+                                                            double* __restrict__ coef, int negate) {
+  __shared__ double B[GRAM_MAXK * GRAM_MAXK];
+  const int kk = 2 * k + 1, np = kk * (kk + 1) / 2;
+  const int tid = threadIdx.x;
+  if (tid < np) {
+    double acc = 0.0;
+    for (int g = 0; g < grid; ++g) acc += partial[(long long)g * np + tid];
+    int p = tid, a = 0;
+    while (p >= kk - a) { p -= kk - a; ++a; }
+    B[a * kk + a + p] = acc;
+    B[(a + p) * kk + a] = acc;
+  }
+  __syncthreads();
+  if (tid != 0) return;
+  double delta[GRAM_MAXK], alpha[(GRAM_MAXK - 1) / 2];
+  for (int j = 0; j < kk; ++j) delta[j] = 0.0;
+  delta[2 * k] = 1.0;
+  for (int i = k - 1; i >= 0; --i) {
+    double dot = 0.0;
+    for (int j = 0; j < kk; ++j) dot = fma(delta[j], B[j * kk + i], dot);   // s_i . q
+    alpha[i] = dot / B[i * kk + k + i];                                     // rho_i = 1 / (s_i . y_i)
+    delta[k + i] -= alpha[i];
+  }
+  const double scale = B[(k - 1) * kk + 2 * k - 1] / B[(2 * k - 1) * kk + 2 * k - 1];
+  for (int j = 0; j < kk; ++j) delta[j] *= scale;
+  for (int i = 0; i < k; ++i) {
+    double dot = 0.0;
+    for (int j = 0; j < kk; ++j) dot = fma(delta[j], B[j * kk + k + i], dot);   // y_i . r
+    delta[i] += alpha[i] - dot / B[i * kk + k + i];
+  }
+  for (int j = 0; j < kk; ++j) coef[j] = negate ? -delta[j] : delta[j];
+}
+
+__global__ __launch_bounds__(256) void lincomb_dev_kernel(VecSet vs, int k, long long n, const double* __restrict__ coef,
+                                                          double* __restrict__ out) {
+  double c[GRAM_MAXK];
+#pragma unroll
+  for (int j = 0; j < GRAM_MAXK; ++j) c[j] = j < k ? coef[j] : 0.0;
+  for (long long i = (long long)blockIdx.x * 256 + threadIdx.x; i < n; i += (long long)gridDim.x * 256) {
+    double s = 0.0;
+#pragma unroll
+    for (int j = 0; j < GRAM_MAXK; ++j)
+      if (j < k) s = fma(c[j], vs.p[j][i], s);
+    out[i] = s;
+  }
+}
+
 extern "C" {
 
 // H g (negate: -H g) for a k-deep history (newest last): rho[j] = 1/s_j.y_j and gamma = s.y/y.y of the newest
@@ -2533,6 +2589,27 @@ int pml_two_loop_chain(int k, const double* const* s, const double* const* y, co
   for (int j = 0; j + 1 < k; ++j)    // q += c_j s_j; c[j+1] = alpha_{j+1} - rho_{j+1} (y_{j+1} . q)
     launch(TwoLoopStep{q, s[j], cc + j, 1.0, nullptr, y[j + 1], rho[j + 1], alpha + j + 1, cc + j + 1, 0});
   launch(TwoLoopStep{q, s[k - 1], cc + k - 1, 1.0, nullptr, nullptr, nullptr, nullptr, nullptr, negate});
+  LAUNCH_CHECK();
+  return 0;
+}
+
+// Grid of the device vector-free two-loop's Gram pass (partial buffer: grid x (2k+1)(2k+2)/2 doubles).
+int pml_two_loop_gram_grid(long long n) {
+  const long long t = (n + GRAM_TILE - 1) / GRAM_TILE;
+  return (int)std::max<long long>(1, std::min<long long>(t, 512));
+}
+
+int pml_two_loop_gram(int k, const double* const* s, const double* const* y, const double* g, long long n, double* q,
+                      double* partial, double* coef, int negate, void* stream) {
+  if (k < 1 || 2 * k + 1 > GRAM_MAXK || n <= 0) return -22;
+  VecSet vs{};
+  for (int j = 0; j < k; ++j) { vs.p[j] = s[j]; vs.p[k + j] = y[j]; }
+  vs.p[2 * k] = g;
+  const int kk = 2 * k + 1, grid = pml_two_loop_gram_grid(n);
+  hipLaunchKernelGGL(gram_kernel, dim3(grid), dim3(GRAM_TILE), 0, (hipStream_t)stream, vs, kk, n, partial);
+  hipLaunchKernelGGL(gram_two_loop_kernel, dim3(1), dim3(256), 0, (hipStream_t)stream, partial, grid, k, coef, negate);
+  const long long blocks = std::min<long long>((n + 255) / 256, 4096);
+  hipLaunchKernelGGL(lincomb_dev_kernel, dim3((unsigned)blocks), dim3(256), 0, (hipStream_t)stream, vs, kk, n, coef, q);
   LAUNCH_CHECK();
   return 0;
 }

@@ -116,6 +116,9 @@ def glm_lib() -> Optional[ctypes.CDLL]:
         lib.pml_lbfgs_pair.argtypes = [c_void_p] * 4 + [ctypes.c_longlong] + [c_void_p] * 6
         lib.pml_two_loop_chain.argtypes = [c_int] + [c_void_p] * 5 + [ctypes.c_longlong] + [c_void_p] * 4 + \
             [c_int, c_void_p]
+        lib.pml_two_loop_gram.argtypes = [c_int, c_void_p, c_void_p, c_void_p, ctypes.c_longlong, c_void_p, c_void_p,
+                                          c_void_p, c_int, c_void_p]
+        lib.pml_two_loop_gram_grid.argtypes = [ctypes.c_longlong]
         lib.pml_tl_set_deep.argtypes = [c_int, c_int]
         lib.pml_rs_set_variant.argtypes = [c_int]
         lib.pml_rs_set_variant(int(os.environ.get("PML_RS_VARIANT", "5")))
@@ -126,7 +129,8 @@ def glm_lib() -> Optional[ctypes.CDLL]:
         for f in ("pml_seg_fwd", "pml_seg_t", "pml_reduce_stats", "pml_build_blocks", "pml_tl_fwd", "pml_tl_t",
                   "pml_tl_maxbits", "pml_segdot", "pml_tl_fwd_multi", "pml_tl_t_multi", "pml_seg_cg_step",
                   "pml_seg_expand", "pml_bgemv", "pml_bhv", "pml_rs_tron", "pml_ls_eval", "pml_gram_grid", "pml_gram",
-                  "pml_lincomb", "pml_lbfgs_pair", "pml_two_loop_chain"):
+                  "pml_lincomb", "pml_lbfgs_pair", "pml_two_loop_chain", "pml_two_loop_gram",
+                  "pml_two_loop_gram_grid"):
             getattr(lib, f).restype = c_int
         lib.pml_set_config.argtypes = [c_int, c_int, c_int, c_int]
         lib._pml_typed = True
@@ -279,6 +283,36 @@ def two_loop(s, y, rho, gamma, g, negate: bool = False):
                                  P(*[r.data_ptr() for r in rho]), gamma.data_ptr(), g.data_ptr(), g.numel(),
                                  q.data_ptr(), sc[0].data_ptr(), sc[1].data_ptr(), sc[2].data_ptr(), int(negate),
                                  stream_handle(g.device)), "two_loop_chain")
+    return q
+
+
+_GRAM_LOOP_SCRATCH = {}
+
+
+def two_loop_gram(s, y, g, negate: bool = False):
+    """L-BFGS two-loop ``H g`` (``-H g``) by the vector-free recursion on the device: one Gram pass over the
+    2k + 1 vectors [s..., y..., g], the recursion in one workgroup, one linear-combination pass (3 launches, no
+    host synchronisation). History lists oldest first (as ``_History``); k <= 10. None when not applicable."""
+    k = len(s)
+    if not (0 < k and 2 * k + 1 <= GRAM_MAXK and len(y) == k and g.device.type == "cuda"
+            and g.dtype == torch.float64 and g.dim() == 1 and g.is_contiguous() and g.numel() > 0):
+        return None
+    if not all(v.device == g.device and v.dtype == torch.float64 and v.is_contiguous() and v.numel() == g.numel()
+               for v in list(s) + list(y)):
+        return None
+    lib = require_glm_lib()
+    n = g.numel()
+    kk = 2 * k + 1
+    need = lib.pml_two_loop_gram_grid(n) * (kk * (kk + 1) // 2)
+    sc = _GRAM_LOOP_SCRATCH.get(g.device)
+    if sc is None or sc[0].numel() < need:
+        sc = _GRAM_LOOP_SCRATCH[g.device] = (torch.empty(max(need, 1 << 16), dtype=torch.float64, device=g.device),
+                                             torch.empty(GRAM_MAXK, dtype=torch.float64, device=g.device))
+    P = ctypes.c_void_p * k
+    q = torch.empty_like(g)
+    check(lib.pml_two_loop_gram(k, P(*[v.data_ptr() for v in s]), P(*[v.data_ptr() for v in y]), g.data_ptr(), n,
+                                q.data_ptr(), sc[0].data_ptr(), sc[1].data_ptr(), int(negate),
+                                stream_handle(g.device)), "two_loop_gram")
     return q
 
 

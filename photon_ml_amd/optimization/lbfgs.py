@@ -41,6 +41,9 @@ DEVICE_TWO_LOOP = os.environ.get("PML_LBFGS_DEVICE_TWO_LOOP", "1") != "0"
 NATIVE_PAIR = os.environ.get("PML_LBFGS_NATIVE_PAIR", "1") != "0"
 # Two-loop as 2k + 1 fused HIP step kernels launched from C++ (no Python between launches); 0: torch recursion
 NATIVE_TWO_LOOP = os.environ.get("PML_LBFGS_NATIVE_TWO_LOOP", "1") != "0"
+# Device two-loop method for replicated vectors: "gram" = vector-free recursion on the device (one Gram pass, the
+# recursion in one workgroup, one combination pass: 3 launches), "chain" = the 2k + 1 step kernels
+TWO_LOOP_METHOD = os.environ.get("PML_LBFGS_TWO_LOOP", "gram")
 DEFAULT_NUM_CORRECTIONS = 10
 DEFAULT_TOLERANCE = 1.0e-7
 
@@ -118,8 +121,10 @@ class _History:
         """Two-loop with 0-d device scalars, no synchronisation: the fused HIP step-kernel chain
         (``ops.native.two_loop``), else torch dot products + fused scaled adds (same recursion and order)."""
         if NATIVE_TWO_LOOP:
-            from ..ops.native import two_loop
-            q = two_loop(self.s, self.y, self.rho_t, self.gamma_t, g, negate)
+            from ..ops.native import two_loop, two_loop_gram
+            q = two_loop_gram(self.s, self.y, g, negate) if TWO_LOOP_METHOD == "gram" else None
+            if q is None:
+                q = two_loop(self.s, self.y, self.rho_t, self.gamma_t, g, negate)
             if q is not None:
                 return q
         return self._apply_inverse_device_torch(g, negate)

@@ -490,7 +490,31 @@ def test_two_loop_step_chain_matches_recursion(k, n):
     torch.testing.assert_close(q, ref, rtol=1e-10, atol=1e-12 * float(ref.abs().max()))
     assert torch.equal(two_loop(h.s, h.y, h.rho_t, h.gamma_t, g), q)
     assert torch.equal(two_loop(h.s, h.y, h.rho_t, h.gamma_t, g, negate=True), -q)
-    assert torch.equal(h.apply_inverse(g, negate=True), -q)
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("k,n", [(1, 1), (2, 777), (10, 1_000_003), (7, 300_000)])
+def test_two_loop_gram_on_device_matches_recursion(k, n):
+    """Vector-free two-loop on the device (gram_kernel + gram_two_loop_kernel + lincomb_dev_kernel, no host
+    synchronisation) vs the fp64 torch two-loop on the same history; bitwise run-to-run; negate gives exactly
+    -H g; the optimizer's default device path is this method."""
+    from photon_ml_amd.ops.native import two_loop_gram
+    from photon_ml_amd.optimization import lbfgs
+    gen = torch.Generator(device="cuda").manual_seed(200 + k)
+    h = lbfgs._History(k)
+    for _ in range(k):
+        s = torch.randn(n, dtype=torch.float64, device="cuda", generator=gen)
+        y = s * (1.0 + torch.rand(n, dtype=torch.float64, device="cuda", generator=gen)) \
+            + 0.1 * torch.randn(n, dtype=torch.float64, device="cuda", generator=gen)
+        assert h.push(s, y)
+    g = torch.randn(n, dtype=torch.float64, device="cuda", generator=gen)
+    ref = h._apply_inverse_device_torch(g)
+    q = two_loop_gram(h.s, h.y, g)
+    torch.testing.assert_close(q, ref, rtol=1e-9, atol=1e-11 * float(ref.abs().max()))
+    assert torch.equal(two_loop_gram(h.s, h.y, g), q)
+    assert torch.equal(two_loop_gram(h.s, h.y, g, negate=True), -q)
+    if lbfgs.TWO_LOOP_METHOD == "gram":
+        assert torch.equal(h.apply_inverse(g, negate=True), -q)
 
 
 @pytest.mark.gpu
