@@ -2322,19 +2322,36 @@ __global__ __launch_bounds__(NTHREADS) void ls_eval_kernel(int n, double t, int 
   __shared__ double sh[2 * NTHREADS / 64];
   double F = 0.0, D = 0.0;
   const long long stride = (long long)gridDim.x * NTHREADS;
-  for (long long i = (long long)blockIdx.x * NTHREADS + threadIdx.x; i < n; i += stride) {
-    const double zdi = zd[i];
-    const double z = z0[i] + t * zdi;
-    const double w = static_cast<double>(wt[i]);
-    double l, dl, d2;
-    pointwise_loss(loss, z, static_cast<double>(y[i]), l, dl, d2);
-    F += w * l;
-    if (final_) {
-      coef[i] = static_cast<XT>(w * dl);
-      if (dzz) dzz[i] = static_cast<XT>(w * d2);
-      D += w * dl;
-    } else {
-      D += w * dl * zdi;
+  // four rows per thread per iteration, all loads issued before the loss arithmetic (memory-level parallelism:
+  // one dependent load chain per four rows); the per-thread accumulation order is fixed (deterministic)
+  constexpr int LU = 4;
+  for (long long i0 = (long long)blockIdx.x * NTHREADS + threadIdx.x; i0 < n; i0 += LU * stride) {
+    double zdv[LU], z0v[LU], yv[LU], wv[LU];
+#pragma unroll
+    for (int u = 0; u < LU; ++u) {
+      const long long i = i0 + u * stride;
+      const bool ok = i < n;
+      zdv[u] = ok ? zd[i] : 0.0;
+      z0v[u] = ok ? z0[i] : 0.0;
+      yv[u] = ok ? static_cast<double>(y[i]) : 0.0;
+      wv[u] = ok ? static_cast<double>(wt[i]) : 0.0;
+    }
+#pragma unroll
+    for (int u = 0; u < LU; ++u) {
+      const long long i = i0 + u * stride;
+      if (i >= n) break;
+      const double z = z0v[u] + t * zdv[u];
+      const double w = wv[u];
+      double l, dl, d2;
+      pointwise_loss(loss, z, yv[u], l, dl, d2);
+      F += w * l;
+      if (final_) {
+        coef[i] = static_cast<XT>(w * dl);
+        if (dzz) dzz[i] = static_cast<XT>(w * d2);
+        D += w * dl;
+      } else {
+        D += w * dl * zdv[u];
+      }
     }
   }
   block_sum2(F, D, sh);
