@@ -144,6 +144,13 @@ class VecKey:
         return self.copy.shape == w.shape and bool(torch.equal(self.copy, w.to(self.copy.device, self.copy.dtype)))
 
 
+def _window_align(chunk_rows: int, precision: str) -> int:
+    """Column-window start alignment: the transpose tile width of the chunks (1 when not tiled)."""
+    from .tiled import t_bits
+    cb = t_bits(chunk_rows, precision == "f64")
+    return 1 << cb if cb is not None else 1
+
+
 class DeviceGLMData(GLMComputable):
     """GLM row shard on one GPU evaluated with the native kernels."""
 
@@ -296,10 +303,12 @@ class DeviceGLMData(GLMComputable):
         csr, csc = [], []
         col_lo = []
         wins = []
+        align = _window_align(chunk_rows, precision)
         for a, b in zip(starts[:-1], starts[1:]):
             xc = x[a:b]
             if col_windows and xc.nnz:
                 lo, hi = int(xc.indices.min()), int(xc.indices.max()) + 1
+                lo -= lo % align          # tile-aligned windows: the shard-wide transpose can use global tiles
             else:
                 lo, hi = 0, d
             wins.append((lo, hi))
@@ -379,11 +388,13 @@ class DeviceGLMData(GLMComputable):
         starts = list(range(0, n, chunk_rows)) + [n] if n else [0, 0]
         ip = indptr[torch.tensor(starts, device=dev)].tolist()
         wins = []
+        align = _window_align(chunk_rows, precision)
         for i in range(len(starts) - 1):
             ea, eb = ip[i], ip[i + 1]
             if col_windows and eb > ea:
                 lo, hi = torch.aminmax(col[ea:eb])
-                wins.append((int(lo), int(hi) + 1))
+                lo = int(lo)
+                wins.append((lo - lo % align, int(hi) + 1))   # tile-aligned (see _window_align)
             else:
                 wins.append((0, dim))
         dmax = max([hi - lo for lo, hi in wins] + [1])
@@ -641,12 +652,18 @@ class DeviceGLMData(GLMComputable):
                                      self._multi_ptrs.data_ptr(), self.csr[0].il)
 
     def _build_multi_t(self):
+        """One-launch transpose over all chunks. Column-window chunks (block-diagonal random-effect problems) take
+        part when their windows start on tile boundaries: each chunk's items are shifted to global column tiles,
+        and a tile shared by two chunks' windows is combined like any split tile."""
         self._multi_t = None
-        if (not self.csc or any(ch.kind != "tl" for ch in self.csc) or len({ch.cbits for ch in self.csc}) != 1
-                or any(self.col_lo)):
+        if not self.csc or any(ch.kind != "tl" for ch in self.csc) or len({ch.cbits for ch in self.csc}) != 1:
+            return
+        C = 1 << self.csc[0].cbits
+        if any(lo % C for lo in self.col_lo):
             return
         from .tiled import TLTMulti
-        self._multi_t = TLTMulti(self.csc, self.row_starts, self.dim)
+        self._multi_t = TLTMulti(self.csc, self.row_starts, self.dim,
+                                 tile_offsets=[lo // C for lo in self.col_lo] if any(self.col_lo) else None)
         need = self._multi_t.parts_needed
         if need > self.parts.numel():
             self.parts = torch.zeros(need, dtype=torch.float64, device=self.device)
@@ -677,7 +694,9 @@ class DeviceGLMData(GLMComputable):
         self.n_t = getattr(self, "n_t", 0) + 1
         if getattr(self, "_multi_t", "unset") == "unset":
             self._build_multi_t()
-        if self._multi_t is not None and KERNEL_CONFIG.get("tl_multi", 1):
+        # masked passes (entity masks) keep the per-chunk launches: their live flags follow the per-chunk item order
+        if (self._multi_t is not None and KERNEL_CONFIG.get("tl_multi", 1)
+                and getattr(self, "_masked", None) is None):
             check(self.lib.pml_tl_t_multi(self.prec, ctypes.byref(self._multi_t.desc), x.data_ptr(), square,
                                           G.data_ptr(), self.parts.data_ptr(), stream_handle(self.device)),
                   "tl_t_multi")
@@ -1001,8 +1020,7 @@ class DeviceGLMData(GLMComputable):
         if rr.numel() < max(self.n_rows, 1):
             rr = torch.cat([rr, torch.zeros(max(self.n_rows, 1) - rr.numel(), dtype=self.vdt, device=self.device)])
         out = torch.zeros(self.dim, dtype=torch.float64, device=self.device)
-        for c in range(len(self.csc)):
-            self._t(c, rr, out, square=int(square))
+        self.t_all(rr, out, square=int(square))      # one launch when the shard-wide transpose applies
         return self._unperm(out)
 
     def margins(self, w, margin_shift: float = 0.0, with_offsets: bool = False):

@@ -462,14 +462,16 @@ class TLTMulti:
     Items of all chunks keep their launch order (chunk, item); each carries its chunk (stream pointers), its row
     base (offset into the shard-length row vector) and a partial-row slot. Tiles hit by more than one item in the
     whole shard are combined by the same two-level fixed-order combine as a single chunk's split tiles, so the
-    result is deterministic and independent of chunk scheduling. Requires chunk-independent column tiles (no
-    per-chunk column windows) and one ``cbits`` for all chunks.
+    result is deterministic and independent of chunk scheduling. Requires one ``cbits`` for all chunks and
+    column windows (if any) that start on tile boundaries (``tile_offsets``).
     """
 
     def __init__(self, chunks: Sequence["TLTChunk"], row_starts: Sequence[int], dim: int,
-                 tile_range: Optional[Tuple[int, int]] = None):
+                 tile_range: Optional[Tuple[int, int]] = None, tile_offsets: Optional[Sequence[int]] = None):
         """``tile_range`` = [t0, t1): only the items of those column tiles (a gradient BUCKET: columns
-        [t0 * C, t1 * C) are final after this launch + its combine, so their all-reduce can start)."""
+        [t0 * C, t1 * C) are final after this launch + its combine, so their all-reduce can start).
+        ``tile_offsets``: per chunk, the global tile of its local tile 0 (chunks stored in tile-aligned column
+        windows); tiles that several chunks' items share are combined like split tiles."""
         from .native import TLTMultiDesc
         dev = chunks[0].pack.device
         self.cbits = chunks[0].cbits
@@ -479,7 +481,8 @@ class TLTMulti:
         its = []
         for c, ch in enumerate(chunks):
             it = ch.items[: ch.nitems].cpu().numpy().astype(np.int64).reshape(-1, 6)
-            its.append(np.column_stack([np.full(len(it), c), it[:, 0], it[:, 1], it[:, 2],
+            toff = 0 if tile_offsets is None else int(tile_offsets[c])
+            its.append(np.column_stack([np.full(len(it), c), it[:, 0] + toff, it[:, 1], it[:, 2],
                                         np.full(len(it), row_starts[c]), it[:, 4], it[:, 5]]))
         it = np.concatenate(its) if its else np.zeros((0, 7), np.int64)
         if tile_range is not None:

@@ -214,6 +214,48 @@ def test_tl_multi_launch_matches_per_chunk(col_windows):
         assert torch.allclose(a, b, rtol=1e-12, atol=1e-12 * float(a.abs().max()))
 
 
+@pytest.mark.parametrize("precision", ["f64", "f32"])
+def test_tl_multi_transpose_engages_for_column_windows(precision):
+    """Block-diagonal-like (banded) data stored in per-chunk COLUMN WINDOWS (the random-effect layout): the
+    windows start on tile boundaries, the shard-wide one-launch transpose is built (global tiles, tiles shared by
+    two chunks combined), and it reproduces the per-chunk launches to rounding, bitwise run to run."""
+    import scipy.sparse as sp
+    from photon_ml_amd.data.matrix import LabeledData
+    from photon_ml_amd.ops.device import DeviceGLMData
+    from photon_ml_amd.ops.native import configure
+    rng = np.random.default_rng(5)
+    n, d = 12000, 30000
+    centre = (np.arange(n) * (d - 1200) // n + 600)
+    cols = np.sort(centre[:, None] + rng.integers(-500, 500, size=(n, 12)), axis=1)
+    keep = np.ones_like(cols, dtype=bool)
+    keep[:, 1:] = cols[:, 1:] != cols[:, :-1]
+    rows = np.repeat(np.arange(n), 12).reshape(n, 12)
+    x = sp.csr_matrix((rng.normal(size=int(keep.sum())), (rows[keep], cols[keep])), shape=(n, d))
+    data = LabeledData(x, (rng.random(n) < 0.5).astype(float))
+    dev = DeviceGLMData.from_labeled(data, "cuda", precision, chunk_rows=2000, layout="tiled", col_windows=True,
+                                     item_entries=700)
+    assert len(dev.csr) > 1 and any(dev.col_lo)
+    r = torch.from_numpy(rng.normal(size=n)).cuda()
+    out = {}
+    try:
+        for multi in (0, 1, 1):
+            configure(tl_multi=multi)
+            g = dev.rmatvec(r).clone()
+            if multi:
+                assert dev._multi_t is not None            # the one-launch path really ran
+                C = 1 << dev.csc[0].cbits
+                assert all(lo % C == 0 for lo in dev.col_lo)
+                if multi in out:
+                    assert torch.equal(g, out[multi])
+            out[multi] = g
+    finally:
+        configure(tl_multi=1)
+    ref = torch.from_numpy(x.T @ r.cpu().numpy()).cuda()
+    tol = 1e-12 if precision == "f64" else 1e-6
+    torch.testing.assert_close(out[1], out[0], rtol=1e-12, atol=1e-12 * float(out[0].abs().max()))
+    torch.testing.assert_close(out[1], ref, rtol=tol, atol=tol * float(ref.abs().max()))
+
+
 @pytest.mark.parametrize("pipe", [0, 1, 2])
 @pytest.mark.parametrize("precision", ["f64", "bf16"])
 def test_tl_stream_variants(pipe, precision):
