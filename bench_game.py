@@ -45,6 +45,11 @@ PRESETS = {
     # the small entities, the primal block-diagonal solve for the large ones (n_e > 64 or n_e > d_e)
     "game5pl": dict(entities_per_gpu=1_250_000, rows_per_entity=20, re_dim=1000, re_nnz=50, fe_dim=1_000_000,
                     fe_nnz=30, pool="random", int_ids=1, sizes="powerlaw"),
+    # tall-narrow per-entity models (e.g. per-user models over a few dozen user features, GLMix-style): 250K
+    # entities x 100 rows x 31 coefficients (30-feature pools + intercept) — every entity has more rows than
+    # coefficients, so each is solved with its exact Hessian on the matrix cores (re_tron_hess_kernel)
+    "game5tall": dict(entities_per_gpu=250_000, rows_per_entity=100, re_dim=30, re_nnz=10, fe_dim=1_000_000,
+                      fe_nnz=30, pool="random", int_ids=1),
 }
 
 

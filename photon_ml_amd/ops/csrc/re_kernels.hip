@@ -597,6 +597,271 @@ __global__ __launch_bounds__(RE_THREADS) void re_tron_csr_kernel(ReTronArgs a) {
   }
 }
 
+// ============================================================================================================
+// Tall-narrow entities (more rows than coefficients, d_e <= 64): TRON with the EXACT per-entity Hessian
+// H_e = X_e^T D X_e + l2 I formed once per outer iteration on the fp64 MATRIX CORES and kept in LDS; every
+// truncated-CG step is then a d_e x d_e LDS mat-vec instead of a pass over the entity's rows (per outer iteration:
+// one Hessian pass + one function evaluation, against 1 + #CG passes for re_tron_csr_kernel).
+// Hessian pass: rows are staged 64 at a time as a dense [64 x DP] LDS block (DP = d_e padded to 16) with their
+// weights D_i; the upper-triangle 16 x 16 tiles of H are spread over the 4 waves, and per group of 4 staged rows
+// every tile takes one v_mfma_f64_16x16x4f64: A[r][k] = X[k][16 ti + r], B[k][c] = D_k X[k][16 tj + c]
+// (lane l: r = c = l & 15, k = l >> 4; accumulator i of lane l holds C[(l >> 4) + 4 i][l & 15]). Fixed k order
+// per tile, each tile owned by one wave: deterministic. Diagonal tiles are stored as computed (not mirrored:
+// C[r][c] and C[c][r] round differently), off-diagonal tiles into both halves.
+// ============================================================================================================
+typedef double v4d __attribute__((ext_vector_type(4)));
+#define RH_ROWS 64
+
+template <int T>
+__global__ __launch_bounds__(RE_THREADS) void re_tron_hess_kernel(ReTronArgs a) {
+  constexpr int DP = 16 * T;
+  constexpr int NT = T * (T + 1) / 2;                 // upper-triangle tiles
+  constexpr int NTW = (NT + RE_NW - 1) / RE_NW;       // tiles per wave (at most)
+  extern __shared__ __attribute__((aligned(16))) double smem[];
+  const int e = a.order[blockIdx.x];
+  const long long r0 = a.row_ptr[e], r1 = a.row_ptr[e + 1];
+  const long long c0 = a.col_ptr[e];
+  const int d = (int)(a.col_ptr[e + 1] - c0);
+  const int tid = threadIdx.x, w = tid >> 6, lane = tid & 63;
+  double* H = smem;                       // [DP][DP]
+  double* Xs = H + DP * DP;               // [RH_ROWS][DP] staged rows
+  double* Ds = Xs + RH_ROWS * DP;         // [RH_ROWS] their Hessian weights
+  double* sW = Ds + RH_ROWS;
+  double* sG = sW + DP;
+  double* sS = sG + DP;
+  double* sR = sS + DP;
+  double* sD = sR + DP;
+  double* acc = sD + DP;                  // RE_NW accumulators of DP (function evaluations), acc[0..d) = result
+  double* red = acc + RE_NW * DP;
+  double* myacc = acc + w * DP;
+  double* D[2] = {a.scr, a.scr + a.n_rows};
+  double* Z[2] = {a.scr + 2 * a.n_rows, a.scr + 3 * a.n_rows};
+  int cur = 0, parity = 0, npass = 0;
+  double* Wg = a.W + c0;
+  // this wave's tiles (ti, tj), tj >= ti, round-robin over the waves
+  int tI[NTW], tJ[NTW];
+#pragma unroll
+  for (int q = 0; q < NTW; ++q) {
+    int t = w + RE_NW * q, ti = 0;
+    tI[q] = -1; tJ[q] = -1;
+    if (t < NT) {
+      while (t >= T - ti) { t -= T - ti; ++ti; }
+      tI[q] = ti; tJ[q] = ti + t;
+    }
+  }
+  auto zero_own = [&]() {
+    for (int j = lane; j < d; j += 64) myacc[j] = 0.0;
+  };
+  auto value_grad = [&](const double* vec, int nb, bool at_zero, double& gg) -> double {
+    ++npass;
+    __syncthreads();
+    zero_own();
+    double fp = 0.0;
+    if (at_zero) rows<2, 2>(a, r0, r1, vec, myacc, nullptr, nullptr, nullptr, fp);
+    else rows<1, 2>(a, r0, r1, vec, myacc, nullptr, D[nb], Z[nb], fp);
+    __syncthreads();
+    double s3[3] = {fp, 0.0, 0.0};
+    for (int j = tid; j < d; j += RE_THREADS) {
+      double g = acc[j];
+#pragma unroll
+      for (int q = 1; q < RE_NW; ++q) g += acc[q * DP + j];
+      const double v = vec[j];
+      g += a.l2 * v;
+      acc[j] = g;
+      s3[1] += v * v;
+      s3[2] += g * g;
+    }
+    block_sums<3>(s3, red, parity);
+    gg = s3[2];
+    return s3[0] + 0.5 * a.l2 * s3[1];
+  };
+  // H = X^T diag(D[cur]) X + l2 I on the matrix cores
+  auto form_hessian = [&]() {
+    ++npass;
+    const double* Dc = D[cur];
+    v4d cacc[NTW];
+#pragma unroll
+    for (int q = 0; q < NTW; ++q) cacc[q] = v4d{0.0, 0.0, 0.0, 0.0};
+    for (long long base = r0; base < r1; base += RH_ROWS) {
+      __syncthreads();
+      for (int j = tid; j < RH_ROWS * DP; j += RE_THREADS) Xs[j] = 0.0;
+      if (tid < RH_ROWS) Ds[tid] = base + tid < r1 ? Dc[base + tid] : 0.0;
+      __syncthreads();
+      for (int rr = w; rr < RH_ROWS; rr += RE_NW) {
+        const long long i = base + rr;
+        if (i >= r1) break;
+        for (long long p = a.nip[i] + lane; p < a.nip[i + 1]; p += 64) Xs[rr * DP + (int)a.lcol[p]] = a.val[p];
+      }
+      __syncthreads();
+      const int r = lane & 15;
+#pragma unroll 4
+      for (int kg = 0; kg < RH_ROWS / 4; ++kg) {
+        const int k = kg * 4 + (lane >> 4);
+        const double dk = Ds[k];
+        const double* xk = Xs + k * DP;
+#pragma unroll
+        for (int q = 0; q < NTW; ++q) {
+          if (tI[q] < 0) continue;
+          const double av = xk[tI[q] * 16 + r];
+          const double bv = dk * xk[tJ[q] * 16 + r];
+          cacc[q] = __builtin_amdgcn_mfma_f64_16x16x4f64(av, bv, cacc[q], 0, 0, 0);
+        }
+      }
+    }
+    __syncthreads();
+#pragma unroll
+    for (int q = 0; q < NTW; ++q) {
+      if (tI[q] < 0) continue;
+#pragma unroll
+      for (int i = 0; i < 4; ++i) {
+        const int row = tI[q] * 16 + (lane >> 4) + 4 * i, col = tJ[q] * 16 + (lane & 15);
+        H[row * DP + col] = cacc[q][i];
+        if (tI[q] != tJ[q]) H[col * DP + row] = cacc[q][i];
+      }
+    }
+    __syncthreads();
+    if (tid < d) H[tid * DP + tid] += a.l2;
+    __syncthreads();
+  };
+
+  for (int j = tid; j < DP; j += RE_THREADS) sW[j] = j < d ? Wg[j] : 0.0;
+  double gnorm2;
+  double f = value_grad(sW, cur, false, gnorm2);
+  double nz[1] = {0.0};
+  for (int j = tid; j < d; j += RE_THREADS) {
+    sG[j] = acc[j];
+    nz[0] += sW[j] != 0.0 ? 1.0 : 0.0;
+  }
+  block_sums<1>(nz, red, parity);
+  double f0z = f, g0n = sqrt(gnorm2);
+  if (nz[0] != 0.0) {
+    for (int j = tid; j < DP; j += RE_THREADS) sS[j] = 0.0;
+    double g0;
+    f0z = value_grad(sS, 0, true, g0);
+    g0n = sqrt(g0);
+  }
+  const double loss_tol = f0z * a.tol, grad_tol = g0n * a.tol;
+  double delta = sqrt(gnorm2);
+  int it = 0, fails = 0, reason = 0;
+  bool active = true, need_h = true;
+  if (delta == 0.0) { reason = 4; active = false; }
+  const double eta0 = 1e-4, eta1 = 0.25, eta2 = 0.75, sg1 = 0.25, sg2 = 0.5, sg3 = 4.0;
+  const int guard_max = a.max_iter * (a.max_fail + 1) + 5;
+  for (int guard = 0; active && guard < guard_max; ++guard) {
+    if (need_h) { form_hessian(); need_h = false; }
+    for (int j = tid; j < DP; j += RE_THREADS) {
+      sS[j] = 0.0;
+      const double gj = j < d ? sG[j] : 0.0;
+      sR[j] = -gj;
+      sD[j] = -gj;
+    }
+    double rtr = gnorm2, sts = 0.0;
+    const double cg_tol2 = 0.01 * gnorm2;
+    for (int k = 0; k < a.max_cg; ++k) {
+      if (!(rtr > cg_tol2)) break;
+      __syncthreads();
+      double s5[5] = {0.0, 0.0, 0.0, 0.0, 0.0};
+      for (int j = tid; j < d; j += RE_THREADS) {
+        const double* hr = H + j * DP;
+        double h0 = 0.0, h1 = 0.0;
+        int c = 0;
+        for (; c + 1 < d; c += 2) { h0 = fma(hr[c], sD[c], h0); h1 = fma(hr[c + 1], sD[c + 1], h1); }
+        if (c < d) h0 = fma(hr[c], sD[c], h0);
+        const double h = h0 + h1, dj = sD[j];
+        acc[j] = h;
+        s5[0] += dj * h;
+        s5[1] += sS[j] * dj;
+        s5[2] += dj * dj;
+        s5[3] += sR[j] * h;
+        s5[4] += h * h;
+      }
+      block_sums<5>(s5, red, parity);
+      const double dhd = s5[0], std_ = s5[1], dtd = s5[2], rh = s5[3], hh = s5[4];
+      const double alpha = rtr / (dhd == 0.0 ? 1.0 : dhd);
+      double tn = sts + 2.0 * alpha * std_ + alpha * alpha * dtd;
+      tn = tn > 0.0 ? tn : 0.0;
+      const double dsq = delta * delta;
+      const bool hit = tn > dsq;
+      double al = alpha;
+      if (hit) {
+        const double q = std_ * std_ + dtd * (dsq - sts);
+        const double rad = sqrt(q > 0.0 ? q : 0.0);
+        const double den1 = std_ + rad;
+        al = std_ >= 0.0 ? (dsq - sts) / (den1 > 1e-300 ? den1 : 1e-300) : (rad - std_) / (dtd > 1e-300 ? dtd : 1e-300);
+      }
+      double rn = rtr - 2.0 * al * rh + al * al * hh;
+      rn = rn > 0.0 ? rn : 0.0;
+      const double beta = rn / (rtr == 0.0 ? 1.0 : rtr);
+      __syncthreads();          // every row of H . d read sD before it changes
+      for (int j = tid; j < d; j += RE_THREADS) {
+        const double dj = sD[j];
+        sS[j] += al * dj;
+        const double rj = sR[j] - al * acc[j];
+        sR[j] = rj;
+        if (!hit) sD[j] = rj + beta * dj;
+      }
+      if (hit) break;
+      rtr = rn;
+      sts = tn;
+    }
+    double s3[3] = {0.0, 0.0, 0.0};
+    for (int j = tid; j < d; j += RE_THREADS) {
+      const double sj = sS[j];
+      s3[0] += sG[j] * sj;
+      s3[1] += sj * sR[j];
+      s3[2] += sj * sj;
+      sD[j] = sW[j] + sj;
+    }
+    block_sums<3>(s3, red, parity);
+    const double gs = s3[0], pred = -0.5 * (gs - s3[1]), snorm = sqrt(s3[2]);
+    double gn2;
+    const double fn = value_grad(sD, cur ^ 1, false, gn2);
+    const double actual = f - fn;
+    if (it == 0) delta = fmin(delta, snorm);
+    const double den = fn - f - gs;
+    const double alr = den <= 0.0 ? sg3 : fmax(sg1, -0.5 * gs / (den == 0.0 ? 1.0 : den));
+    double nd;
+    if (actual < eta0 * pred) nd = fmin(fmax(alr, sg1) * snorm, sg2 * delta);
+    else if (actual < eta1 * pred) nd = fmax(sg1 * delta, fmin(alr * snorm, sg2 * delta));
+    else if (actual < eta2 * pred) nd = fmax(sg1 * delta, fmin(alr * snorm, sg3 * delta));
+    else nd = fmax(delta, fmin(alr * snorm, sg3 * delta));
+    delta = nd;
+    const bool accept = actual > eta0 * pred;
+    const double f_prev = f;
+    if (accept) {
+      for (int j = tid; j < d; j += RE_THREADS) {
+        sW[j] = sD[j];
+        sG[j] = acc[j];
+      }
+      gnorm2 = gn2;
+      f = fn;
+      cur ^= 1;
+      ++it;
+      fails = 0;
+      need_h = true;
+    } else {
+      ++fails;
+    }
+    const bool not_impr = !accept && fails >= a.max_fail;
+    int rc = 0;
+    if (accept && sqrt(gnorm2) <= grad_tol) rc = 4;
+    if (accept && fabs(f - f_prev) <= loss_tol) rc = 3;
+    if (not_impr) rc = 2;
+    if ((accept || not_impr) && it >= a.max_iter) rc = 1;
+    if (rc > 0) { reason = rc; active = false; }
+  }
+  __syncthreads();
+  for (int j = tid; j < d; j += RE_THREADS) Wg[j] = sW[j];
+  if (a.zout != nullptr) {
+    const double* zc = Z[cur];
+    for (long long i = r0 + tid; i < r1; i += RE_THREADS) a.zout[i] = zc[i];
+  }
+  if (tid == 0) {
+    a.f[e] = f; a.iters[e] = it; a.reason[e] = reason;
+    if (a.npass != nullptr) a.npass[e] = npass;
+  }
+}
+
 static int g_re_variant = 2;   // row pass: 2 = 16 lanes per row, batched (default); 3 = the same, software-pipelined;
                                // 1 = one row per wave
 
@@ -621,6 +886,31 @@ int pml_re_tron_csr(const int* order, int n_launch, const long long* row_ptr, co
   if (g_re_variant == 1) hipLaunchKernelGGL(re_tron_csr_kernel<1>, dim3(n_launch), dim3(RE_THREADS), smem, st, a);
   else if (g_re_variant == 3) hipLaunchKernelGGL(re_tron_csr_kernel<3>, dim3(n_launch), dim3(RE_THREADS), smem, st, a);
   else hipLaunchKernelGGL(re_tron_csr_kernel<2>, dim3(n_launch), dim3(RE_THREADS), smem, st, a);
+  LAUNCH_CHECK();
+  return 0;
+}
+
+// Tall-narrow entities (d_e <= 64): LDS = H + staged rows + their weights + 5 vectors + accumulators + sums.
+size_t pml_re_tron_hess_smem(int dp) {
+  return ((size_t)dp * dp + (size_t)RH_ROWS * dp + RH_ROWS + (5 + RE_NW) * (size_t)dp + 2 * RE_NW * 8) * sizeof(double);
+}
+
+int pml_re_tron_hess(const int* order, int n_launch, const long long* row_ptr, const long long* col_ptr,
+                     const long long* nip, const uint16_t* lcol, const double* val, const double* y,
+                     const double* off, const double* wt, double* scr, long long n_rows, double* W, double* f,
+                     int* iters, int* reason, double* zout, int* npass, int loss, double l2, double tol,
+                     int max_iter, int max_fail, int max_cg, int dp, hipStream_t st) {
+  if (n_launch <= 0) return 0;
+  if (dp < 16 || dp > 64 || dp % 16 || loss < 0 || loss > 2) return -22;
+  const size_t smem = pml_re_tron_hess_smem(dp);
+  ReTronArgs a{order, n_launch, row_ptr, col_ptr, nip, lcol, val, y, off, wt, scr, n_rows, W, f, iters, reason,
+               zout, npass, loss, l2, tol, max_iter, max_fail, max_cg, dp};
+  switch (dp / 16) {
+    case 1: hipLaunchKernelGGL(re_tron_hess_kernel<1>, dim3(n_launch), dim3(RE_THREADS), smem, st, a); break;
+    case 2: hipLaunchKernelGGL(re_tron_hess_kernel<2>, dim3(n_launch), dim3(RE_THREADS), smem, st, a); break;
+    case 3: hipLaunchKernelGGL(re_tron_hess_kernel<3>, dim3(n_launch), dim3(RE_THREADS), smem, st, a); break;
+    default: hipLaunchKernelGGL(re_tron_hess_kernel<4>, dim3(n_launch), dim3(RE_THREADS), smem, st, a); break;
+  }
   LAUNCH_CHECK();
   return 0;
 }

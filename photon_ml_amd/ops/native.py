@@ -580,6 +580,10 @@ def re_lib() -> Optional[ctypes.CDLL]:
         lib.pml_re_tron_csr.restype = c_int
         lib.pml_re_tron_smem.argtypes = [c_int]
         lib.pml_re_tron_smem.restype = ctypes.c_size_t
+        lib.pml_re_tron_hess.argtypes = lib.pml_re_tron_csr.argtypes
+        lib.pml_re_tron_hess.restype = c_int
+        lib.pml_re_tron_hess_smem.argtypes = [c_int]
+        lib.pml_re_tron_hess_smem.restype = ctypes.c_size_t
         lib.pml_re_set_variant.argtypes = [c_int]
         lib.pml_re_set_variant(int(os.environ.get("PML_RE_ROWPASS", "2")))
         lib._pml_typed = True
@@ -596,14 +600,15 @@ def require_re_lib() -> ctypes.CDLL:
 
 def re_tron_csr(order, row_ptr, col_ptr, nip, lcol, val, y, off, wt, scr, W, f, iters, reason, zout, loss_id: int,
                 l2: float, tol: float, max_iter: int, max_fail: int, max_cg: int, dmax: int,
-                npass: Optional[torch.Tensor] = None) -> None:
+                npass: Optional[torch.Tensor] = None, hessian: bool = False) -> None:
     """Fused per-entity primal TRON over the entities ``order`` (int32; one workgroup each) of a block-diagonal
     CSR (``re_tron_csr_kernel``). Entity ``e`` owns rows ``row_ptr[e]:row_ptr[e+1]`` (int64) and coefficients
     ``col_ptr[e]:col_ptr[e+1]`` of the packed ``W`` (fp64, in: warm start, out: solution); ``nip`` int64 row
     pointers, ``lcol`` int16 entity-local columns (< d_e <= dmax, distinct inside a row), ``val`` fp64; ``y``,
     ``off``, ``wt`` per row; ``scr`` fp64 scratch of 4 x rows; outputs ``f`` / ``iters`` / ``reason`` per
-    entity and ``zout`` (x_i . w per row); ``npass`` (optional int32 per entity): row passes run. Device only; in
-    place, nothing returned."""
+    entity and ``zout`` (x_i . w per row); ``npass`` (optional int32 per entity): row passes run. ``hessian``:
+    the tall-narrow kernel (``re_tron_hess_kernel``: d_e <= dmax <= 64, dmax a multiple of 16; the per-entity
+    Hessian formed on the fp64 matrix cores, CG on it in LDS). Device only; in place, nothing returned."""
     lib = require_re_lib()
     n_rows = y.numel()
     B = int(order.numel())
@@ -614,7 +619,8 @@ def re_tron_csr(order, row_ptr, col_ptr, nip, lcol, val, y, off, wt, scr, W, f, 
     assert lcol.dtype == torch.int16 and nip.numel() == n_rows + 1 and lcol.numel() == val.numel()
     assert all(t.dtype == torch.float64 for t in (val, y, off, wt, scr, W, f, zout))
     assert off.numel() == n_rows and wt.numel() == n_rows and zout.numel() == n_rows and scr.numel() >= 4 * n_rows
-    assert iters.dtype == reason.dtype == torch.int32 and dmax % 64 == 0
+    assert iters.dtype == reason.dtype == torch.int32
+    assert (dmax % 16 == 0 and 16 <= dmax <= 64) if hessian else dmax % 64 == 0
     n_ent = row_ptr.numel() - 1
     assert col_ptr.numel() == n_ent + 1 and W.numel() == int(col_ptr[-1]) and f.numel() == n_ent
     if npass is not None:
@@ -625,7 +631,8 @@ def re_tron_csr(order, row_ptr, col_ptr, nip, lcol, val, y, off, wt, scr, W, f, 
         oe = order.to(torch.int64)
         assert int((col_ptr[oe + 1] - col_ptr[oe]).max()) <= dmax, "entity wider than the launch's LDS class"
         assert int(row_ptr[-1]) == n_rows and int(nip[-1]) == val.numel(), "row / non-zero ranges inconsistent"
-    check(lib.pml_re_tron_csr(order.data_ptr(), B, row_ptr.data_ptr(), col_ptr.data_ptr(), nip.data_ptr(),
+    fn = lib.pml_re_tron_hess if hessian else lib.pml_re_tron_csr
+    check(fn(order.data_ptr(), B, row_ptr.data_ptr(), col_ptr.data_ptr(), nip.data_ptr(),
                               lcol.data_ptr(), val.data_ptr(), y.data_ptr(), off.data_ptr(), wt.data_ptr(),
                               scr.data_ptr(), n_rows, W.data_ptr(), f.data_ptr(), iters.data_ptr(),
                               reason.data_ptr(), zout.data_ptr(),

@@ -8,7 +8,9 @@ coefficients — go here: ONE kernel launch per LDS size class (``re_tron_csr_ke
 ``ops/csrc/re_kernels.hip``) runs every entity's complete TRON in its own workgroup, with the entity's
 coefficient vectors in LDS and each Hessian-vector product a single read of its CSR rows. No host round trip,
 no global pass per CG step, entities converge independently (a converged entity stops reading its rows), and
-the margins of the solution come out of the solve.
+the margins of the solution come out of the solve. Tall-narrow entities (d_e <= 64) use ``re_tron_hess_kernel``
+instead: the exact per-entity Hessian X_e^T D X_e formed once per outer iteration on the fp64 matrix cores
+(``v_mfma_f64_16x16x4f64``) and kept in LDS, so truncated CG costs no pass over the rows at all.
 
 Entities wider than ``FUSED_DMAX`` or longer than ``FUSED_MAX_ROWS`` stay on the block-diagonal pass path
 (``batched.batched_tron`` over ``RandomEffectDataset.entity_subset``).
@@ -25,6 +27,8 @@ FUSED_DMAX = 2048                    # LDS per workgroup: (5 + 4) x dmax doubles
 FUSED_MAX_ROWS = int(os.environ.get("PML_RE_FUSED_MAX_ROWS", str(1 << 22)))
 FUSED_LOSSES = (0, 1, 2)             # logistic, Poisson, squared (the twice-differentiable losses)
 _CLASSES = (256, 512, 1024, 2048)    # LDS size classes (max coefficients per entity of a launch)
+_HESS_CLASSES = (16, 32, 48, 64)     # tall-narrow entities: d_e padded to these, exact Hessian on the matrix cores
+HESS_DMAX = 64 if os.environ.get("PML_RE_HESS", "1") != "0" else 0
 
 
 def fused_enabled() -> bool:
@@ -88,17 +92,20 @@ class EntityTronBatch:
         self.n_rows = n_rows
         self.nnz = nnz
         self.scr = torch.empty(4 * max(n_rows, 1), dtype=torch.float64, device=dev)
-        # launch classes by LDS size; inside a class the largest entities first (they bound the launch's tail)
+        # launch classes by LDS size; inside a class the largest entities first (they bound the launch's tail).
+        # Entities of at most HESS_DMAX coefficients (tall: the row space took the wide ones) run the exact-Hessian
+        # kernel (MFMA), the others the sparse Hessian-vector kernel.
         ent_nnz = (nip[self.row_ptr[1:]] - nip[self.row_ptr[:-1]])
-        bounds = torch.tensor(_CLASSES, device=dev)
-        cls = torch.searchsorted(bounds, de)
         self.launches = []
-        for c, dm in enumerate(_CLASSES):
-            idx = torch.nonzero(cls == c).squeeze(1)
-            if idx.numel() == 0:
-                continue
-            order = idx[torch.argsort(ent_nnz[idx], descending=True, stable=True)]
-            self.launches.append((dm, order.to(torch.int32).contiguous()))
+        hess = de <= HESS_DMAX
+        for classes, sel, is_h in ((_HESS_CLASSES, hess, True), (_CLASSES, ~hess, False)):
+            cls = torch.searchsorted(torch.tensor(classes, device=dev), de)
+            for c, dm in enumerate(classes):
+                idx = torch.nonzero(sel & (cls == c)).squeeze(1)
+                if idx.numel() == 0:
+                    continue
+                order = idx[torch.argsort(ent_nnz[idx], descending=True, stable=True)]
+                self.launches.append((dm, order.to(torch.int32).contiguous(), bool(is_h)))
 
     def solve(self, loss, l2: float, W0: Optional[torch.Tensor], offsets: torch.Tensor, tol: float, max_iter: int,
               max_fail: int = 5, max_cg: int = 20) -> FusedResult:
@@ -116,8 +123,9 @@ class EntityTronBatch:
         z = torch.empty(self.n_rows, dtype=torch.float64, device=dev)
         off = offsets.to(dev, torch.float64).contiguous()
         assert off.numel() == self.n_rows
-        for dm, order in self.launches:
+        for dm, order, is_h in self.launches:
             re_tron_csr(order, self.row_ptr, self.col_ptr, self.nip, self.lcol, self.val, self.y, off, self.w,
-                        self.scr, W, f, iters, reason, z, loss.loss_id, l2, tol, max_iter, max_fail, max_cg, dm)
+                        self.scr, W, f, iters, reason, z, loss.loss_id, l2, tol, max_iter, max_fail, max_cg, dm,
+                        hessian=is_h)
         self.W = W
         return FusedResult(W, f, iters.to(torch.long), reason.to(torch.long), z)

@@ -239,14 +239,18 @@ def _re_two_updates(data, task, opt="TRON"):
 
 @pytest.mark.parametrize("task", ["LOGISTIC_REGRESSION", "LINEAR_REGRESSION", "POISSON_REGRESSION"])
 @pytest.mark.parametrize("max_rows", [None, 200])
-def test_fused_entity_tron_matches_pass_path(task, max_rows, monkeypatch):
-    """The fused per-entity primal TRON (re_tron_csr_kernel: one workgroup per entity, the whole solve in one
-    launch) reproduces the block-diagonal pass-path TRON: same models, scores and iteration counts, across a
-    warm-started second update. ``max_rows``: larger entities stay on the pass path (mixed components)."""
+@pytest.mark.parametrize("d_user,hess", [(12, 64), (12, 0), (40, 64), (100, 64)])
+def test_fused_entity_tron_matches_pass_path(task, max_rows, d_user, hess, monkeypatch):
+    """The fused per-entity primal TRON (one workgroup per entity, the whole solve in one launch) reproduces the
+    block-diagonal pass-path TRON: same models, scores and iteration counts, across a warm-started second update.
+    ``hess`` = HESS_DMAX: entities of <= 64 coefficients run the exact-Hessian kernel (re_tron_hess_kernel, MFMA;
+    d_e 13 -> tile 16, 41 -> 48), wider ones (d_e 101) and hess = 0 the sparse Hessian-vector kernel.
+    ``max_rows``: larger entities stay on the pass path (mixed components)."""
     import photon_ml_amd.optimization.entity_tron as et
-    # power-law users (zipf): entities from a few rows (row space) to thousands (fused / pass path), d_e = 12
-    data, _ = generate_game_data(n_rows=30000, n_users=700, d_user=12, seed=26, task=task)
+    # power-law users (zipf): entities from a few rows (row space) to thousands (fused / pass path)
+    data, _ = generate_game_data(n_rows=30000, n_users=700, d_user=d_user, seed=26, task=task)
     out = {}
+    monkeypatch.setattr(et, "HESS_DMAX", hess)
     for fused in ("0", "1"):
         monkeypatch.setenv("PML_RE_FUSED", fused)
         monkeypatch.setattr(et, "FUSED_MAX_ROWS", max_rows or et.FUSED_MAX_ROWS)
@@ -255,6 +259,7 @@ def test_fused_entity_tron_matches_pass_path(task, max_rows, monkeypatch):
             rs, fz, sub = c._comps
             assert fz is not None and fz.B > 0
             assert (sub is not None) == (max_rows is not None)
+            assert any(h for _, _, h in fz.launches) == (hess > 0 and d_user < 64)
         out[fused] = (v1, s1, v2, s2, c.last_stats["mean_iterations"])
     a, b = out["0"], out["1"]
     for i in range(4):
