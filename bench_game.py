@@ -71,6 +71,9 @@ def build_parser() -> argparse.ArgumentParser:
     ap.add_argument("--sizes", choices=["uniform", "powerlaw"])
     ap.add_argument("--fe-iters", type=int, default=10)
     ap.add_argument("--re-iters", type=int, default=10)
+    ap.add_argument("--fe-down-sampling-rate", type=float, default=1.0,
+                    help="fixed-effect down-sampling rate (binary-classification sampler: every positive, negatives "
+                         "at this rate, re-weighted); < 1 trains each FE update on a row-sampled copy of the shard")
     ap.add_argument("--precision", default="bf16", choices=["bf16", "f32", "f64"],
                     help="storage precision of the fixed-effect features (accumulation and optimizer state are fp64; "
                          "random-effect features are always fp64)")
@@ -154,7 +157,7 @@ def run(args, dev, rank: int = 0, world: int = 1) -> dict:
         f"{data.n_rows} rows/GPU")
     t0 = time.time()
     fe_cfg = GLMOptimizationConfiguration(OptimizerConfig("LBFGS", args.fe_iters, 1e-12),
-                                          RegularizationContext("L2"), 1.0)
+                                          RegularizationContext("L2"), 1.0, args.fe_down_sampling_rate)
     re_cfg = GLMOptimizationConfiguration(OptimizerConfig("TRON", args.re_iters, 1e-12),
                                           RegularizationContext("L2"), 1.0)
     task = "LOGISTIC_REGRESSION"
@@ -189,6 +192,10 @@ def run(args, dev, rank: int = 0, world: int = 1) -> dict:
     log(f"fixed effect per sweep: {(getattr(fe_gd, 'n_fwd', 0) - fe_pass0[0]) / args.steps:.1f} forward + "
         f"{(getattr(fe_gd, 'n_t', 0) - fe_pass0[1]) / args.steps:.1f} transpose passes")
     loss = cd.history[-1].get("training_loss")
+    coord_ms = {}
+    for rec in cd.history[-2 * args.steps:]:
+        coord_ms.setdefault(rec["coordinate"], []).append(1000.0 * rec["seconds"])
+    coord_ms = {k: sum(v) / len(v) for k, v in coord_ms.items()}
     re_stats = coords["per-entity"].last_stats
     total_rows = int(all_reduce_scalar(float(data.n_rows)))
     if rank == 0:
@@ -227,7 +234,9 @@ def run(args, dev, rank: int = 0, world: int = 1) -> dict:
                    "seq_len": None, "entity_sizes": args.sizes or "uniform",
                    "entities": args.entities_per_gpu * world, "rows_per_entity": args.rows_per_entity,
                    "re_dim": args.re_dim, "fe_dim": args.fe_dim, "fe_iters": args.fe_iters,
-                   "re_iters": args.re_iters, "parallelism": f"dp{world}+ep{world}"},
+                   "re_iters": args.re_iters, "fe_down_sampling_rate": args.fe_down_sampling_rate,
+                   "parallelism": f"dp{world}+ep{world}"},
+        "coordinate_ms": coord_ms,
         "examples_per_sec": total_rows * args.steps / elapsed,
         "data_generation_s": t_data,
         "coordinate_build_s": t_build,

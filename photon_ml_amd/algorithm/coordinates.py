@@ -120,8 +120,9 @@ class FixedEffectCoordinate(Coordinate):
     def dim(self) -> int:
         return self.glm_data.dim
 
-    def _data_view(self):
-        return DistributedGLMData(self.glm_data) if is_dist() else self.glm_data
+    def _data_view(self, data=None):
+        data = self.glm_data if data is None else data
+        return DistributedGLMData(data) if is_dist() else data
 
     def initialize_model(self):
         return FixedEffectModel(model_for_task(self.task, Coefficients.zeros(self.dim)), self.shard_id)
@@ -143,11 +144,12 @@ class FixedEffectCoordinate(Coordinate):
             ps = partial_score.detach().to(base.device, torch.float64)
             off = base + (ps if rows is None else ps[rows])
         self.glm_data.set_offsets(off)
+        gd = self.glm_data
         if self.sampler is not None:
             self._apply_down_sampling()
-        gd = self.glm_data
+            gd = self._sampled_shard() or gd
         n0 = (getattr(gd, "n_fwd", 0), getattr(gd, "n_t", 0))
-        glm = self.problem.run(self._data_view(), model.glm if model is not None else None, dim=self.dim)
+        glm = self.problem.run(self._data_view(gd), model.glm if model is not None else None, dim=self.dim)
         self.last_tracker = self.problem.tracker
         if log.isEnabledFor(logging.DEBUG) and hasattr(gd, "n_passes"):
             log.debug("FE %s: %d forward + %d transpose passes in the update (%s iterations)", self.coordinate_id,
@@ -178,6 +180,17 @@ class FixedEffectCoordinate(Coordinate):
             return
         wts = self.sampler.sample_weights(self.labels, self.base_weights, self._row_ids())
         gd.set_weights(torch.from_numpy(np.asarray(wts, dtype=np.float64)))
+
+    def _sampled_shard(self):
+        """K20 work saving on the device path: the update runs on a copy of the shard that holds only the kept
+        rows' entries (``DeviceGLMData.row_sampled``), so at rate r each pass streams ~r of the data, as the
+        reference's physically down-sampled RDD does. ``PML_DS_COMPACT=0`` keeps the zero-weight full passes."""
+        gd = self.glm_data
+        wt = getattr(gd, "wt", None)
+        if (os.environ.get("PML_DS_COMPACT", "1") == "0" or not hasattr(gd, "row_sampled")
+                or not isinstance(wt, torch.Tensor) or not wt.is_cuda):
+            return None
+        return gd.row_sampled(wt[: gd.n_rows] > 0)
 
     def _restore_weights(self):
         wt = getattr(self.glm_data, "wt", None)

@@ -241,6 +241,102 @@ __global__ __launch_bounds__(256) void downsample_kernel(const T* __restrict__ y
   w[i] = (T)out;
 }
 
+// ------------------------------------------------------------------------------------------------------------
+// K20 work saving: row-sampled copy of one chunk of the tiled layout (ops/tiled.py, DeviceGLMData.row_sampled).
+// A down-sampled row (weight 0) adds nothing to any pass, so a fixed-effect update at rate r only needs the kept
+// rows' entries (the reference trains on a physically smaller sampled RDD: DistributedOptimizationProblem.scala
+// :145-160). Every work unit (forward row block / transpose item) keeps its table slot; its narrow and wide
+// entries are filtered by the row keep flags and rewritten as WIDE lane-interleaved rounds in the unit's logical
+// order (a filtered narrow round no longer spans < 64 keys). No sort: the filtered streams stay in unit order.
+// Segments of <= CMP_SEG rounds of one unit, one wave each: pass 0 counts the kept entries per segment, the host
+// turns the counts into per-unit round-aligned output starts (device cumsums) and pass 1 writes. Inside a round,
+// logical entry t = 64 k + lane is placed with a ballot + popcount per k, so the copy is deterministic.
+// key_is_row = 1 (transpose copy): an entry's chunk row is its key (pack >> sbits); 0 (forward copy): the unit's
+// first row plus its slot (pack & smask).
+// ------------------------------------------------------------------------------------------------------------
+#define CMP_SEG 8
+struct CmpArgs {
+  const int* units;             // unit table, 6 ints per unit: ... e_lo at col_e, e_hi at col_e + 1, n_lo, n_hi at 4, 5
+  int col_e, row_col;           // row_col: column of the unit's first chunk row (-1: key_is_row)
+  const int* seg;               // 3 ints per segment {unit, round_lo, round_hi}; rounds [0, n_hi - n_lo) are narrow
+  int nseg, sbits, key_is_row;
+  const uint32_t* pack;         // wide stream (interleaved)
+  const void* val;
+  const uint16_t* npack;        // narrow stream (interleaved 16-bit packs), one int32 base per round
+  const void* nval;
+  const int* nbase;
+  const unsigned char* keep;    // per chunk row: 1 = kept
+  int* seg_cnt;                 // pass 0 output
+  const long long* seg_first;   // pass 1: logical index (within its unit's output) of the segment's first kept entry
+  const long long* unit_lo;     // pass 1: physical output start of every unit (round-aligned)
+  uint32_t* opack;              // pass 1 outputs
+  void* oval;
+};
+
+template <typename VT, int PASS>
+__global__ __launch_bounds__(256) void tl_compact_kernel(CmpArgs a) {
+  const int lane = threadIdx.x & 63;
+  const int s = __builtin_amdgcn_readfirstlane(blockIdx.x * 4 + (threadIdx.x >> 6));
+  if (s >= a.nseg) return;                                   // wave-uniform
+  const int* sg = a.seg + 3 * (long long)s;
+  const int u = sg[0], r_lo = sg[1], r_hi = sg[2];
+  const int* ut = a.units + 6 * (long long)u;
+  const long long e_lo = ut[a.col_e];
+  const int nw = ut[a.col_e + 1] - ut[a.col_e];
+  const int n_lo = ut[4], nn = ut[5] - ut[4];
+  const uint32_t row0 = a.row_col >= 0 ? (uint32_t)ut[a.row_col] : 0u;
+  const uint32_t smask = (1u << a.sbits) - 1u;
+  const VT* val = (const VT*)a.val;
+  const VT* nval = (const VT*)a.nval;
+  long long ob = PASS ? a.seg_first[s] : 0;
+  const long long olo = PASS ? a.unit_lo[u] : 0;
+  const unsigned long long below = (1ull << lane) - 1ull;
+  int cnt = 0;
+  for (int r = r_lo; r < r_hi; ++r) {
+    uint32_t p[4];
+    VT v[4];
+    bool ok[4];
+    if (r < nn) {
+      const long long q = (long long)n_lo + r;
+      const int base = a.nbase[q];
+#pragma unroll
+      for (int k = 0; k < 4; ++k) {
+        const uint32_t p16 = a.npack[q * 256 + 4 * lane + k];
+        p[k] = ((uint32_t)(base + (int)(p16 >> a.sbits)) << a.sbits) | (p16 & smask);
+        v[k] = nval[q * 256 + 4 * lane + k];
+        ok[k] = true;
+      }
+    } else {
+      const int w = r - nn;
+#pragma unroll
+      for (int k = 0; k < 4; ++k) {
+        ok[k] = 256 * w + 64 * k + lane < nw;
+        const long long e = e_lo + 256LL * w + 4 * lane + k;
+        p[k] = ok[k] ? a.pack[e] : 0u;
+        v[k] = ok[k] ? val[e] : (VT)0;
+      }
+    }
+#pragma unroll
+    for (int k = 0; k < 4; ++k) {
+      const uint32_t row = a.key_is_row ? (p[k] >> a.sbits) : row0 + (p[k] & smask);
+      const bool kp = ok[k] && a.keep[row];
+      const unsigned long long m = __ballot(kp);
+      if (PASS) {
+        if (kp) {
+          const long long o = ob + __popcll(m & below);
+          const long long ph = olo + (o & ~255LL) + ((o & 63) << 2) + ((o & 255) >> 6);
+          a.opack[ph] = p[k];
+          ((VT*)a.oval)[ph] = v[k];
+        }
+        ob += __popcll(m);
+      } else {
+        cnt += __popcll(m);
+      }
+    }
+  }
+  if (!PASS && lane == 0) a.seg_cnt[s] = cnt;
+}
+
 
 // ------------------------------------------------------------------------------------------------------------
 // Per-entity Gram matrices K_e = X_e X_e^T of the row-space batch (optimization/row_space.py setup), straight
@@ -298,6 +394,25 @@ int pml_downsample(int f64, const void* y, const void* w0, const long long* rowi
   else
     hipLaunchKernelGGL(downsample_kernel<float>, dim3((unsigned)blocks), dim3(256), 0, (hipStream_t)stream,
                        (const float*)y, (const float*)w0, rowid, n, seed, rate, binary, (float*)w);
+  LAUNCH_CHECK();
+  return 0;
+}
+
+// pass 0: count, 1: write; vbytes = sizeof(value) (bf16 2, fp32 4, fp64 8)
+int pml_tl_compact(int pass, int vbytes, const CmpArgs* a, void* stream) {
+  if (a->nseg <= 0) return 0;
+  const dim3 grid((unsigned)((a->nseg + 3) / 4)), blk(256);
+  hipStream_t st = (hipStream_t)stream;
+#define CMP_LAUNCH(VT)                                                              \
+  do {                                                                              \
+    if (pass) hipLaunchKernelGGL((tl_compact_kernel<VT, 1>), grid, blk, 0, st, *a); \
+    else hipLaunchKernelGGL((tl_compact_kernel<VT, 0>), grid, blk, 0, st, *a);      \
+  } while (0)
+  if (vbytes == 2) CMP_LAUNCH(unsigned short);
+  else if (vbytes == 4) CMP_LAUNCH(unsigned int);
+  else if (vbytes == 8) CMP_LAUNCH(unsigned long long);
+  else return -22;
+#undef CMP_LAUNCH
   LAUNCH_CHECK();
   return 0;
 }

@@ -875,7 +875,9 @@ __device__ __forceinline__ void tl_stream_wide(const uint32_t* __restrict__ pack
 // Profiling ablations (experiment build only: -DPML_TL_EXPERIMENT, libpml_glm_abl.so, scripts/kbench.py
 // --ablate): bit 1 -> register sums instead of the LDS atomics, bit 2 -> no coefficient gathers / key-window loads
 // (x = 1), bit 4 -> fp32 products, bit 8 -> no wide-round gathers only, bit 16 -> no narrow key windows or
-// permutes only. The production build compiles TL_ABL to 0 (no runtime checks).
+// permutes only, bit 32 -> no wide-round gathers of keys below ((abl >> 8) << 10) (the upper bound of serving the
+// next tier of hot columns from an LDS table: those lanes skip the load). The production build compiles TL_ABL to 0
+// (no runtime checks).
 #ifdef PML_TL_EXPERIMENT
 __constant__ int c_tl_ablate = 0;
 #define TL_ABL c_tl_ablate
@@ -922,8 +924,12 @@ __device__ __forceinline__ void tl_stream_ring(const uint32_t* __restrict__ pack
   auto gather = [&](int r, const v4u& p, XT* xv) {
     const int e = e_lo + r * TL_ROUND + lane;
 #pragma unroll
-    for (int k = 0; k < TL_VEC; ++k)
-      xv[k] = (abl & 10) ? XT(1) : ldg(x + ((e + 64 * k < e_hi) ? (p[k] >> sbits) : 0u));
+    for (int k = 0; k < TL_VEC; ++k) {
+      const uint32_t key = (e + 64 * k < e_hi) ? (p[k] >> sbits) : 0u;
+      if (abl & 10) xv[k] = XT(1);
+      else if ((abl & 32) && key < ((uint32_t)abl >> 8) << 10) xv[k] = XT(1);
+      else xv[k] = ldg(x + key);
+    }
   };
   // prologue in the steady state's issue order (loads of rounds r0 .. r0+S-1, then gathers of r0 .. r0+D-1), so
   // the outstanding-load sequence at the loop head is the same from the prologue and from the back edge

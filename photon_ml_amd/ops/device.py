@@ -418,6 +418,38 @@ class DeviceGLMData(GLMComputable):
     def nbytes(self) -> int:
         return sum(c.nbytes() for c in self.csr + self.csc)
 
+    def row_sampled(self, keep: torch.Tensor) -> Optional["DeviceGLMData"]:
+        """K20 work saving: a shard over the SAME rows whose streams hold only the entries of the rows with
+        ``keep`` (bool / uint8 [n_rows]); None when the layout cannot be compacted (segmented or plain-order
+        streams). The reference trains each down-sampled fixed-effect update on a physically smaller RDD
+        (``DistributedOptimizationProblem.scala:145-160``); here the dropped rows keep their positions (zero
+        weight, margins = offsets) and their entries leave the streams, so every pass costs ~rate of a full one.
+
+        Built per update by ``tl_compact_kernel`` (two passes over the streams, no sort, one host sync for all
+        chunks): every unit keeps its table slot and the kept entries are stored as wide interleaved rounds. Row
+        vectors (labels, offsets, weights) are SHARED with this shard; margin caches are the copy's own."""
+        from .tiled import RowCompaction
+        if self.layout != "tiled" or not self.csr or not all(getattr(ch, "il", 0) for ch in self.csr + self.csc):
+            return None
+        keep = keep.to(self.device, torch.uint8).contiguous()
+        assert keep.numel() >= self.n_rows
+        jobs = []
+        for c in range(len(self.csr)):
+            kc = keep[self.row_starts[c]: self.row_starts[c + 1]]
+            jobs.append(RowCompaction(self.csr[c], kc, True))
+            jobs.append(RowCompaction(self.csc[c], kc, False))
+        sizes = torch.stack([torch.stack([j.total, j.kept]) for j in jobs]).tolist()    # the one host sync
+        out = [j.finish(int(t), int(k)) for j, (t, k) in zip(jobs, sizes)]
+        view = DeviceGLMData(out[0::2], out[1::2], self.row_starts, self.y, self.o, self.wt, self.dim,
+                             self.precision, self.device, None)
+        view.col_lo = list(self.col_lo)
+        view.old_of_new = self.old_of_new
+        if self.old_of_new is not None:
+            view.new_of_old = self.new_of_old
+        view.parts = self.parts           # same unit tables -> same partial-row scratch (same stream, in order)
+        view.sampled_from = self
+        return view
+
     def set_offsets(self, offsets):
         new = torch.as_tensor(offsets, device=self.device).to(self.vdt)
         zc = getattr(self, "z_cache", None)

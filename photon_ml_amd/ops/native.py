@@ -53,6 +53,15 @@ class TLTMultiDesc(ctypes.Structure):
                 ("ncu", c_int), ("nparts_total", c_int), ("il", c_int), ("live", c_void_p), ("live_mt", c_void_p)]
 
 
+class CmpArgs(ctypes.Structure):
+    """Arguments of the row-sampled tiled-chunk copy (``tl_compact_kernel``, ops/csrc/game_kernels.hip)."""
+    _fields_ = [("units", c_void_p), ("col_e", c_int), ("row_col", c_int), ("seg", c_void_p), ("nseg", c_int),
+                ("sbits", c_int), ("key_is_row", c_int), ("pack", c_void_p), ("val", c_void_p),
+                ("npack", c_void_p), ("nval", c_void_p), ("nbase", c_void_p), ("keep", c_void_p),
+                ("seg_cnt", c_void_p), ("seg_first", c_void_p), ("unit_lo", c_void_p), ("opack", c_void_p),
+                ("oval", c_void_p)]
+
+
 class TLTDesc(ctypes.Structure):
     _fields_ = [
         ("items", c_void_p), ("nitems", c_int), ("cbits", c_int), ("pack", c_void_p), ("val", c_void_p),
@@ -449,6 +458,8 @@ def game_lib() -> Optional[ctypes.CDLL]:
         lib.pml_downsample.argtypes = [c_int, c_void_p, c_void_p, c_void_p, ctypes.c_longlong, ctypes.c_ulonglong,
                                        c_double, c_int, c_void_p, c_void_p]
         lib.pml_seg_gram.argtypes = [c_int, c_int, c_int] + [c_void_p] * 8
+        lib.pml_tl_compact.argtypes = [c_int, c_int, ctypes.POINTER(CmpArgs), c_void_p]
+        lib.pml_tl_compact.restype = c_int
         for f in ("pml_score_rows", "pml_bgram", "pml_gemm_nt", "pml_spmm_rows", "pml_downsample"):
             getattr(lib, f).restype = c_int
         lib._pml_typed = True

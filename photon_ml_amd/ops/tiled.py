@@ -34,6 +34,7 @@ of more than 2^27 rows) fall back to the segmented-stream layout (:mod:`photon_m
 """
 from __future__ import annotations
 
+import ctypes
 import math
 import os
 from typing import Optional, Sequence, Tuple
@@ -560,3 +561,97 @@ def stream_ptr_table(chunks, device) -> torch.Tensor:
     """Per-chunk stream pointers of the shard-wide kernels: {pack, val, narrow pack, narrow val, narrow base}."""
     return torch.tensor([[ch.pack.data_ptr(), ch.val.data_ptr(), ch.npack.data_ptr(), ch.nval.data_ptr(),
                           ch.nbase.data_ptr()] for ch in chunks], dtype=torch.int64, device=device).reshape(-1)
+
+
+# ---- row-sampled copies (K20 down-sampling work saving: DeviceGLMData.row_sampled) ---------------------------
+CMP_SEG = 8              # rounds of one unit per compaction segment (tl_compact_kernel, one wave each)
+
+
+def _cmp_segments(ch):
+    """Segment table of a chunk's units (cached): int32 {unit, round_lo, round_hi} per segment, where a unit's
+    rounds are its narrow rounds followed by its wide rounds; plus each segment's unit and the unit's first
+    segment (int64)."""
+    cached = getattr(ch, "_cmp_seg", None)
+    if cached is not None:
+        return cached
+    t = ch._table().to(torch.int64)
+    dev = t.device
+    lo, hi = ch._ew
+    R = (t[:, 5] - t[:, 4]) + (t[:, hi] - t[:, lo] + IL_ROUND - 1) // IL_ROUND
+    ns = (R + CMP_SEG - 1) // CMP_SEG
+    S = int(ns.sum())
+    su = torch.repeat_interleave(torch.arange(t.shape[0], device=dev), ns, output_size=S)
+    first = (torch.cumsum(ns, 0) - ns)[su]
+    r_lo = (torch.arange(S, device=dev) - first) * CMP_SEG
+    r_hi = torch.minimum(r_lo + CMP_SEG, R[su])
+    seg = torch.stack([su, r_lo, r_hi], 1).to(torch.int32).contiguous()
+    ch._cmp_seg = (seg, su, first, S)
+    return ch._cmp_seg
+
+
+class RowCompaction:
+    """Row-sampled copy of one interleaved tiled chunk (forward or transpose copy) by ``tl_compact_kernel``:
+    the constructor queues the counting pass and the device-side scans (``total`` / ``kept`` stay on the device so
+    that all chunks of a shard need ONE host sync), :meth:`finish` allocates the compacted streams, queues the
+    writing pass and returns the new chunk. Every unit keeps its table slot (row block / transpose item, split-tile
+    partial rows and combine tables unchanged); the copy has no narrow section."""
+
+    def __init__(self, ch, keep: torch.Tensor, forward: bool):
+        from .native import CmpArgs, check, require_game_lib, stream_handle
+        if not ch.il:
+            raise ValueError("row-sampled copies need the interleaved layout")
+        self.ch, self.keep, self.forward = ch, keep, forward
+        dev = ch.pack.device
+        seg, su, first, S = _cmp_segments(ch)
+        table = ch._table()
+        lo, hi = ch._ew
+        self.seg_cnt = torch.zeros(max(S, 1), dtype=torch.int32, device=dev)
+        self._keep_alive = (seg, table, keep)
+        self.args = CmpArgs(table.data_ptr(), lo, 0 if forward else -1, seg.data_ptr(), S, ch._sbits,
+                            0 if forward else 1, ch.pack.data_ptr(), ch.val.data_ptr(), ch.npack.data_ptr(),
+                            ch.nval.data_ptr(), ch.nbase.data_ptr(), keep.data_ptr(), self.seg_cnt.data_ptr(),
+                            None, None, None, None)
+        self.lib, self.stream = require_game_lib(), stream_handle(dev)
+        self.vbytes = ch.val.element_size()
+        if S:
+            check(self.lib.pml_tl_compact(0, self.vbytes, ctypes.byref(self.args), self.stream), "tl_compact count")
+        cnt = self.seg_cnt[:S].to(torch.int64)
+        U = table.shape[0]
+        self.unit_cnt = torch.zeros(U, dtype=torch.int64, device=dev).index_add_(0, su, cnt)
+        padded = (self.unit_cnt + IL_ROUND - 1) // IL_ROUND * IL_ROUND
+        self.unit_lo = (torch.cumsum(padded, 0) - padded).contiguous()
+        excl = torch.cumsum(cnt, 0) - cnt
+        self.seg_first = (excl - excl[first]).contiguous() if S else excl
+        self.total, self.kept = padded.sum(), self.unit_cnt.sum()
+
+    def finish(self, total: int, kept: int):
+        import copy
+        from .native import TLFwdDesc, TLTDesc, check
+        ch = self.ch
+        dev = ch.pack.device
+        opack = torch.zeros(total + _PAD, dtype=torch.int32, device=dev)
+        oval = torch.zeros(total + _PAD, dtype=ch.val.dtype, device=dev)
+        a = self.args
+        a.seg_first, a.unit_lo = self.seg_first.data_ptr(), self.unit_lo.data_ptr()
+        a.opack, a.oval = opack.data_ptr(), oval.data_ptr()
+        if a.nseg:
+            check(self.lib.pml_tl_compact(1, self.vbytes, ctypes.byref(a), self.stream), "tl_compact write")
+        lo, hi = ch._ew
+        table = ch._table().to(torch.int64).clone()
+        table[:, lo] = self.unit_lo
+        table[:, hi] = self.unit_lo + self.unit_cnt
+        table[:, 4:6] = 0
+        table = table.to(torch.int32).contiguous()
+        nc = copy.copy(ch)
+        nc._cmp_seg = None
+        nc.pack, nc.val, nc.nnz = opack, oval, kept
+        nc._set_narrow(*_empty_narrow(oval))
+        if self.forward:
+            nc.blk = table
+            nc.desc = TLFwdDesc(table.data_ptr(), nc.nblk, nc.rbits, opack.data_ptr(), oval.data_ptr(), 1, nc.nar)
+        else:
+            nc.items = table
+            nc.desc = TLTDesc(table.data_ptr(), nc.nitems, nc.cbits, opack.data_ptr(), oval.data_ptr(),
+                              nc.mt_tiles.data_ptr(), nc.mt_ptr.data_ptr(), nc.nmt, nc.dim, nc.cu.data_ptr(), nc.ncu,
+                              nc.nparts, 1, nc.nar)
+        return nc
