@@ -309,7 +309,11 @@ class RandomEffectCoordinate(Coordinate):
             bd = BatchedGLMData(bucket.X, bucket.y, O, bucket.w)
             W0 = self._warm_start(b, bucket, model)
             oc = cfg.optimizer_config
-            if oc.optimizer_type == OptimizerType.TRON:
+            fz = self._dense_fused(b, bucket, l1)
+            if fz is not None:
+                r = fz.solve(self.loss, l2, W0, O, oc.tolerance, oc.maximum_iterations)
+                res = BatchedResult(r.W.to(W0.dtype), r.f, r.iters, r.reason)
+            elif oc.optimizer_type == OptimizerType.TRON:
                 res = batched_tron(bd, self.loss, l2, W0, oc.tolerance, oc.maximum_iterations)
             else:
                 res = batched_lbfgs(bd, self.loss, l2, W0, oc.tolerance, oc.maximum_iterations, l1=l1)
@@ -333,6 +337,20 @@ class RandomEffectCoordinate(Coordinate):
         variances = np.concatenate(vars_) if vars_ else None
         return RandomEffectModel(self.data_config.random_effect_type, self.data_config.feature_shard_id, self.task,
                                  ds.entity_ids, ds.dim, keys, vals, variances)
+
+    def _dense_fused(self, b: int, bucket, l1: float):
+        """The fused per-entity TRON of a dense bucket (``entity_tron.DenseEntityTronBatch``, built once per
+        bucket), or None when it does not apply (L-BFGS / OWL-QN, L1, constraints, CPU, non-smooth loss, d > 2048)."""
+        from ..optimization.entity_tron import FUSED_DMAX, DenseEntityTronBatch, fused_eligible
+        oc = self.opt_config.optimizer_config
+        opt = "TRON" if oc.optimizer_type == OptimizerType.TRON else "LBFGS"
+        if (not fused_eligible(self.loss, opt, l1, oc.constraint_map, bucket.X.device)
+                or bucket.X.shape[2] > FUSED_DMAX or bucket.X.numel() == 0):
+            return None
+        cache = self.__dict__.setdefault("_dense_fz", {})
+        if b not in cache:
+            cache[b] = DenseEntityTronBatch(bucket.X, bucket.y, bucket.w)
+        return cache[b]
 
     def _update_segmented(self, model, offs, l1: float, l2: float):
         """All entities as one block-diagonal problem (``SegmentedGLMData``). With the fused primal TRON

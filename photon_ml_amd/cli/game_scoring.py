@@ -38,8 +38,11 @@ def build_parser() -> argparse.ArgumentParser:
     p.add_argument("--model-id", default="N/A")
     p.add_argument("--log-data-and-model-stats", type=parse_bool, default=False)
     p.add_argument("--spill-scores-to-disk", type=parse_bool, default=False,
-                   help="accepted for compatibility, no effect: scores are device/host arrays aligned by row, "
-                        "there is no Spark RDD to persist (written once to the output directory)")
+                   help="score the rows in chunks straight into a memory-mapped score file under the output "
+                        "directory instead of keeping every score resident (the reference's MEMORY_AND_DISK "
+                        "persistence of the scores RDD); removed after the scores are written")
+    p.add_argument("--spill-chunk-rows", type=int, default=1 << 24,
+                   help="rows scored per device chunk with --spill-scores-to-disk")
     return p
 
 
@@ -94,7 +97,12 @@ class GameScoringDriver(GameDriverBase):
                                  device=a.device or None)
             self.scoring_device = tr.device
             self.log(f"scoring on {tr.device}")
-            scores, evals = tr.transform(data)
+            spill = None
+            if a.spill_scores_to_disk:
+                spill = os.path.join(a.root_output_directory, f".scores-spill-{rank():05d}.npy")
+                scores, evals = tr.transform_spilled(data, spill, a.spill_chunk_rows)
+            else:
+                scores, evals = tr.transform(data)
         if evals:
             for e, v in evals:
                 self.log(f"evaluation {e.name}: {v}")
@@ -105,6 +113,8 @@ class GameScoringDriver(GameDriverBase):
             has_label = not np.all(np.isnan(data.response))
             save_scores(out, scores.cpu().numpy(), data.offsets, data.response if has_label else None,
                         data.weights, data.raw_uids, a.model_id, data.id_tags or None, a.output_files_limit)
+        if spill is not None:
+            os.remove(spill)      # POSIX: the mapping behind the returned scores stays valid until released
         return {"scores": scores, "evaluations": evals, "data": data}
 
 

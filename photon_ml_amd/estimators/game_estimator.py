@@ -212,7 +212,9 @@ class GameTransformer:
 
     def transform(self, data: GameData):
         """Return (scores WITHOUT offsets, evaluations or None)."""
-        scores = self.model.score(data, self.device)
+        return self._evaluate(data, self.model.score(data, self.device))
+
+    def _evaluate(self, data: GameData, scores):
         evals = None
         if self.validation_evaluators:
             evals = []
@@ -220,6 +222,22 @@ class GameTransformer:
                 e = build_evaluator(parse_evaluator_type(n), data.response, data.offsets, data.weights, data.id_tags)
                 evals.append((e, e.evaluate(scores)))
         return scores, evals
+
+    def transform_spilled(self, data: GameData, path: str, chunk_rows: int = 1 << 24):
+        """:meth:`transform` for score sets that should not stay resident (``--spill-scores-to-disk``; the
+        reference persists the scores RDD with MEMORY_AND_DISK, ``GameScoringDriver.scala:55-70``): rows are
+        scored ``chunk_rows`` at a time on the device and each chunk goes straight into a memory-mapped fp64 file
+        at ``path`` (``.npy``), so device memory holds one chunk of scores and the host keeps only pages the OS
+        chooses to. Returns (CPU tensor over the mapped file, evaluations)."""
+        n = data.n_rows
+        mm = np.lib.format.open_memmap(path, mode="w+", dtype=np.float64, shape=(n,))
+        for lo in range(0, n, chunk_rows):
+            hi = min(n, lo + chunk_rows)
+            sub = data if (lo == 0 and hi == n) else data.subset(np.arange(lo, hi))
+            mm[lo:hi] = self.model.score(sub, self.device).detach().to("cpu", torch.float64).numpy()
+            del sub
+        mm.flush()
+        return self._evaluate(data, torch.from_numpy(mm))
 
 
 # --------------------------------------------------------------------------------------------------------------

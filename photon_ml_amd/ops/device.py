@@ -564,9 +564,9 @@ class DeviceGLMData(GLMComputable):
                 start_reduce(out[self.dim:])
                 self._packed_bucketed(self.coef, out[: self.dim], start_reduce, nb)
             else:
-                self.t_all(self.coef, out[: self.dim])
-                if self.old_of_new is not None:
-                    out[: self.dim] = self._unperm(out[: self.dim].clone())
+                G = self._grad_target(out)
+                self.t_all(self.coef, G)
+                self._grad_finish(G, out)
             self.n_passes += 1
             return out
 
@@ -931,6 +931,20 @@ class DeviceGLMData(GLMComputable):
     def _unperm(self, g: torch.Tensor) -> torch.Tensor:
         return g if self.old_of_new is None else g[self.new_of_old]
 
+    def _grad_target(self, out: torch.Tensor) -> torch.Tensor:
+        """Where a transpose pass accumulates the D-vector result: ``out[:dim]`` itself, or (relabelled columns)
+        a zeroed device-order scratch that :meth:`_grad_finish` gathers into ``out`` in ONE kernel."""
+        if self.old_of_new is None:
+            return out[: self.dim]
+        g = getattr(self, "_gscr", None)
+        if g is None or g.numel() != self.dim:
+            g = self._gscr = torch.empty(self.dim, dtype=torch.float64, device=self.device)
+        return g.zero_()
+
+    def _grad_finish(self, G: torch.Tensor, out: torch.Tensor):
+        if self.old_of_new is not None:
+            torch.index_select(G, 0, self.new_of_old, out=out[: self.dim])
+
     # ------------------------------------------------------------------
     def value_grad_packed(self, loss, w_eff, margin_shift) -> torch.Tensor:
         """Device tensor [D + 2] = (G, F, S) — packed so a DP wrapper can all-reduce it in one RCCL call."""
@@ -963,13 +977,13 @@ class DeviceGLMData(GLMComputable):
         return buf
 
     def _value_grad_packed(self, loss, w_eff, margin_shift) -> torch.Tensor:
-        out = torch.zeros(self.dim + 2, dtype=torch.float64, device=self.device)
-        G = out[: self.dim]
+        out = (torch.zeros if self.old_of_new is None else torch.empty)(self.dim + 2, dtype=torch.float64,
+                                                                        device=self.device)
+        G = self._grad_target(out)
         if self._zero_point(loss, w_eff):
             self._zero_coef(loss, margin_shift, out[self.dim:])
             self.t_all(self.coef, G)
-            if self.old_of_new is not None:
-                out[: self.dim] = self._unperm(G.clone())
+            self._grad_finish(G, out)
             self.n_passes += 1
             return out
         if self._cached_point(w_eff, margin_shift):
@@ -978,8 +992,7 @@ class DeviceGLMData(GLMComputable):
             if self.track_hessian and loss.twice_differentiable:
                 self._dzz_key, self._dzz_shift = VecKey(w_eff), float(margin_shift)
             self.t_all(self.coef, G)
-            if self.old_of_new is not None:
-                out[: self.dim] = self._unperm(G.clone())
+            self._grad_finish(G, out)
             self.n_passes += 1
             return out
         x = self._vec(w_eff)
@@ -991,8 +1004,7 @@ class DeviceGLMData(GLMComputable):
                 0, 0.0, None
         self.t_all(self.coef, G)
         out[self.dim:] = self._reduce_stats()
-        if self.old_of_new is not None:
-            out[: self.dim] = self._unperm(G.clone())
+        self._grad_finish(G, out)
         if dzz is not None:
             self._dzz_key = VecKey(w_eff)
             self._dzz_shift = float(margin_shift)
@@ -1019,14 +1031,14 @@ class DeviceGLMData(GLMComputable):
 
     def _hv_packed(self, loss, w_eff, margin_shift, v_eff, v_shift) -> torch.Tensor:
         self._ensure_dzz(loss, w_eff, margin_shift)
-        out = torch.zeros(self.dim + 2, dtype=torch.float64, device=self.device)
-        H = out[: self.dim]
+        out = (torch.zeros if self.old_of_new is None else torch.empty)(self.dim + 2, dtype=torch.float64,
+                                                                        device=self.device)
+        H = self._grad_target(out)
         x = self._vec(v_eff)
         self.fwd_all(x, FWD_HV, loss.loss_id, v_shift, self.coef, self.dzz, z_out=self._u_out())
         self.t_all(self.coef, H)
         out[self.dim:] = self._reduce_stats()
-        if self.old_of_new is not None:
-            out[: self.dim] = self._unperm(H.clone())
+        self._grad_finish(H, out)
         self.n_passes += 1
         return out
 

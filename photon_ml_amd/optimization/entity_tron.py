@@ -129,3 +129,46 @@ class EntityTronBatch:
                         hessian=is_h)
         self.W = W
         return FusedResult(W, f, iters.to(torch.long), reason.to(torch.long), z)
+
+
+class DenseEntityTronBatch:
+    """A dense size bucket ``X [B, n, d]`` (RANDOM / IDENTITY projections, or the dense layout of INDEX_MAP) solved
+    by the same fused kernels: every entity's padded rows presented as dense CSR rows (column ids 0..d-1, padding
+    rows carry weight 0), so d <= 64 buckets form the exact Hessian on the fp64 matrix cores and wider ones run
+    the sparse Hessian-vector kernel — one launch per bucket instead of the batched-GEMM TRON's per-CG-step torch
+    launches (``batched.batched_tron`` over ``BatchedGLMData``; same TRON semantics)."""
+
+    def __init__(self, X: torch.Tensor, y: torch.Tensor, w: torch.Tensor):
+        B, n, d = X.shape
+        if d > FUSED_DMAX:
+            raise ValueError(f"dense bucket of {d} coefficients exceeds FUSED_DMAX={FUSED_DMAX}")
+        dev = X.device
+        self.B, self.n, self.d = B, n, d
+        ar = lambda k, step: torch.arange(k + 1, dtype=torch.int64, device=dev) * step
+        self.row_ptr, self.col_ptr, self.nip = ar(B, n), ar(B, d), ar(B * n, d)
+        self.lcol = torch.arange(d, dtype=torch.int16, device=dev).repeat(B * n)
+        self.val = X.to(torch.float64).reshape(-1).contiguous()
+        self.y = y.to(torch.float64).reshape(-1).contiguous()
+        self.w = w.to(torch.float64).reshape(-1).contiguous()
+        self.scr = torch.empty(4 * max(B * n, 1), dtype=torch.float64, device=dev)
+        hess = d <= HESS_DMAX
+        classes = _HESS_CLASSES if hess else _CLASSES
+        dm = next(c for c in classes if c >= d)
+        self.launch = (dm, torch.arange(B, dtype=torch.int32, device=dev), hess)
+
+    def solve(self, loss, l2: float, W0: torch.Tensor, offsets: torch.Tensor, tol: float, max_iter: int,
+              max_fail: int = 5, max_cg: int = 20) -> FusedResult:
+        """``W0`` [B, d]; ``offsets`` [B, n]. Returns W [B, d] and margins z [B, n] (no offset)."""
+        from ..ops.native import re_tron_csr
+        B, n, d = self.B, self.n, self.d
+        dev = self.y.device
+        W = W0.to(dev, torch.float64).reshape(-1).contiguous().clone()
+        f = torch.empty(B, dtype=torch.float64, device=dev)
+        iters = torch.empty(B, dtype=torch.int32, device=dev)
+        reason = torch.empty(B, dtype=torch.int32, device=dev)
+        z = torch.empty(B * n, dtype=torch.float64, device=dev)
+        off = offsets.to(dev, torch.float64).reshape(-1).contiguous()
+        dm, order, is_h = self.launch
+        re_tron_csr(order, self.row_ptr, self.col_ptr, self.nip, self.lcol, self.val, self.y, off, self.w, self.scr,
+                    W, f, iters, reason, z, loss.loss_id, l2, tol, max_iter, max_fail, max_cg, dm, hessian=is_h)
+        return FusedResult(W.view(B, d), f, iters.to(torch.long), reason.to(torch.long), z.view(B, n))

@@ -12,6 +12,9 @@ contiguous feature slice of every optimizer vector, while the data stays row-sha
     optimizer:   every vector op runs on the D/P slice; every inner product is a local partial + all-reduce
                  (``optimization.vector_space.ShardedSpace``); the L-BFGS two-loop is the vector-free variant
                  (one batched Gram all-reduce per iteration, ``lbfgs._History._apply_inverse_gram``).
+    line search: in MARGIN space like the replicated path (the local row shard caches its margins): one
+                 all-gather of the direction + one forward pass, then 2 scalars all-reduced per trial; TRON trial
+                 points likewise come from the tracked step margins (no forward pass).
 
 Memory per rank for the optimizer drops from (2m + 4)·8·D to (2m + 4)·8·D/P + 16·D (the gathered w and the
 full-length local gradient of one pass). Communication per evaluation is unchanged versus the replicated
@@ -193,6 +196,92 @@ class FeatureShardedObjective:
         w = all_gather_shards(w_shard, self.layout, self.group)
         d = reduce_scatter_full(data.hdiag_sums(self.obj.loss, w).to(torch.float64), self.layout, self.group)
         return d + self.obj.l2_weight if self.obj.l2_weight > 0 else d
+
+    # ---- margin space (the local row shard caches its margins, as in the replicated path) ---------------------
+    def _gathered_grad(self, f: float, s: float, G: torch.Tensor, w_shard: torch.Tensor, l2_sq: float):
+        """(f, gradient slice) from a LOCAL pass result: reduce-scatter G, all-reduce (F, S), then the
+        normalization and L2 terms (``l2_sq`` = ||w||^2 of the whole vector)."""
+        g_shard = reduce_scatter_full(G.to(torch.float64), self.layout, self.group)
+        f, s = _all_reduce_small([f, s], G.device, self.group)
+        grad = self._finalize(g_shard, s)
+        if self.obj.l2_weight > 0:
+            f += 0.5 * self.obj.l2_weight * l2_sq
+            grad = grad + self.obj.l2_weight * w_shard
+        return f, grad
+
+    def margin_line_search(self, data, x0_shard: torch.Tensor, d_shard: torch.Tensor, t0: float = 1.0,
+                           dots=None):
+        """:meth:`GLMObjective.margin_line_search` with sharded x0 / d: ONE all-gather of the direction (x0 is
+        the accepted point, whose margins the local shard already holds), the direction pass over the local rows,
+        then every trial is an elementwise pass + a 2-scalar all-reduce; only the accepted step pays the transpose
+        pass and its reduce-scatter. Before this, every trial of the feature-sharded line search was a full
+        all-gather + forward + transpose + reduce-scatter."""
+        if not hasattr(data, "ls_begin"):
+            return None
+        norm = self.obj.normalization
+        x0 = all_gather_shards(x0_shard, self.layout, self.group)
+        d = all_gather_shards(d_shard, self.layout, self.group)
+        w0_eff, shift0 = norm.effective(x0)
+        d_eff = d * norm.factors.to(d) if norm.factors is not None else d
+        d_shift = -float(torch.dot(d_eff, norm.shifts.to(d_eff))) if norm.shifts is not None else 0.0
+        if not data.ls_begin(w0_eff, shift0, d_eff, d_shift, t0, self.obj.loss):
+            return None
+        return ShardedMarginLineSearch(self, data, x0_shard, d_shard, x0, d, dots)
+
+    # TRON trial point from margins (GLMObjective.step_begin / step_add / calculate_step)
+    def step_begin(self, data, w_shard: torch.Tensor) -> bool:
+        if not hasattr(data, "step_begin"):
+            return False
+        w_eff, shift = self.obj.normalization.effective(all_gather_shards(w_shard, self.layout, self.group))
+        return bool(data.step_begin(w_eff, shift))
+
+    def step_add(self, data, alpha: float):
+        data.step_add(alpha)
+
+    def calculate_step(self, data, w_shard: torch.Tensor):
+        self.n_value_grad += 1
+        norm = self.obj.normalization
+        w = all_gather_shards(w_shard, self.layout, self.group)
+        w_eff, shift = norm.effective(w)
+        f, s, G = data.ls_finish_sums(self.obj.loss, 1.0, w_eff, shift, norm.shifts is not None)
+        return self._gathered_grad(f, s, G, w_shard, float(torch.dot(w, w)) if self.obj.l2_weight > 0 else 0.0)
+
+
+class ShardedMarginLineSearch:
+    """phi(t) = F(x0 + t d) with sharded x0 / d (see :class:`photon_ml_amd.function.objective.MarginLineSearch`):
+    trials from the local cached margins + one all-reduce of (F, phi') each; ``a, b, c`` = x0.x0, x0.d, d.d of the
+    whole vectors (the caller's global dots, or from the gathered vectors: no collective)."""
+
+    def __init__(self, sobj: FeatureShardedObjective, data, x0_shard, d_shard, x0, d, dots=None):
+        from ..function.objective import DEFERRED_DOTS
+        self.sobj, self.data = sobj, data
+        self.x0_shard, self.d_shard = x0_shard, d_shard
+        self.l2 = sobj.obj.l2_weight
+        if self.l2 > 0 and dots is not DEFERRED_DOTS:
+            self.a, self.b, self.c = dots if dots is not None else torch.stack(
+                [torch.dot(x0, x0), torch.dot(x0, d), torch.dot(d, d)]).tolist()
+        self._x0, self._d = x0, d
+
+    def eval(self, t: float):
+        f, dd = self.data.ls_eval(self.sobj.obj.loss, t)
+        f, dd = _all_reduce_small([f, dd], self._d.device, self.sobj.group)
+        if self.l2 > 0:
+            f += 0.5 * self.l2 * (self.a + 2.0 * t * self.b + t * t * self.c)
+            dd += self.l2 * (self.b + t * self.c)
+        return f, dd
+
+    def finish(self, t: float):
+        """(x(t) slice, f(x(t)), gradient slice at x(t)): one transpose pass + its reduce-scatter."""
+        so = self.sobj
+        so.n_value_grad += 1
+        x_shard = self.x0_shard + t * self.d_shard
+        x = self._x0 + t * self._d
+        norm = so.obj.normalization
+        w_eff, shift = norm.effective(x)
+        f, s, G = self.data.ls_finish_sums(so.obj.loss, t, w_eff, shift, norm.shifts is not None)
+        l2_sq = (self.a + 2.0 * t * self.b + t * t * self.c) if self.l2 > 0 else 0.0
+        f, grad = so._gathered_grad(f, s, G, x_shard, l2_sq)
+        return x_shard, f, grad
 
 
 def optimize_feature_sharded(optimizer, objective: GLMObjective, data, initial: Optional[torch.Tensor] = None,

@@ -84,6 +84,14 @@ def test_training_then_scoring(game_avro, tmp_path):
     assert abs(sres["evaluations"][0][1] - best_val_auc) < 5e-3
     pred = np.array([r["predictionScore"] for r in recs])
     assert np.allclose(pred, sres["scores"].numpy() + sres["data"].offsets)
+    # --spill-scores-to-disk: chunked scoring into a memory-mapped file gives the same scores / evaluation
+    spout = tmp_path / "score-spill"
+    spres = game_scoring.GameScoringDriver(game_scoring.build_parser().parse_args(
+        [*sargs[:3], str(spout), *sargs[4:], "--spill-scores-to-disk", "true", "--spill-chunk-rows", "64"])).run()
+    assert np.array_equal(spres["scores"].numpy(), sres["scores"].numpy())
+    assert spres["evaluations"][0][1] == sres["evaluations"][0][1]
+    assert [r["predictionScore"] for r in load_scores(str(spout / "scores"))] == list(pred)
+    assert not [f for f in os.listdir(spout) if f.startswith(".scores-spill")]
 
 
 def test_output_dir_exists_fails(game_avro, tmp_path):

@@ -157,6 +157,30 @@ def test_random_projection_coordinate_on_gpu_matches_cpu():
     torch.testing.assert_close(sb, sa, rtol=1e-7, atol=1e-8)
 
 
+@pytest.mark.parametrize("task", ["LOGISTIC_REGRESSION", "POISSON_REGRESSION"])
+@pytest.mark.parametrize("d_user,proj", [(30, 6), (30, None), (90, None)])
+def test_dense_buckets_fused_tron_match_batched_tron(task, d_user, proj, monkeypatch):
+    """Dense size buckets (RANDOM projection, or INDEX_MAP on the dense layout) solved by the fused per-entity
+    kernels (``entity_tron.DenseEntityTronBatch``: exact Hessian on the matrix cores for d <= 64, sparse
+    Hessian-vector kernel above) == the batched-GEMM TRON (``batched.batched_tron``), across a warm start."""
+    from photon_ml_amd.algorithm.coordinates import RandomEffectCoordinate
+    from photon_ml_amd.projector import RandomProjection
+    data, _ = generate_game_data(n_rows=6000, n_users=40, d_user=d_user, seed=27, task=task)
+    cfg = GLMOptimizationConfiguration(OptimizerConfig("TRON", 100, 1e-10), RegularizationContext("L2"), 1.0)
+    kw = {} if proj is None else {"projector_type": RandomProjection(proj)}
+    dc = RandomEffectDataConfiguration("userId", "user", **kw)
+    out = {}
+    for fused in ("0", "1"):
+        monkeypatch.setenv("PML_RE_FUSED", fused)
+        c = RandomEffectCoordinate("u", data, dc, cfg, task, device="cuda", layout="dense")
+        m1 = c.update_model(c.initialize_model())
+        m2 = c.update_model(m1, partial_score=torch.from_numpy(np.cos(np.arange(data.n_rows)) * 0.2))
+        assert bool(getattr(c, "_dense_fz", None)) == (fused == "1")
+        out[fused] = (m1.values.copy(), m2.values.copy(), c.score(m2).cpu())
+    for a, b in zip(out["0"], out["1"]):
+        torch.testing.assert_close(torch.as_tensor(b), torch.as_tensor(a), rtol=1e-6, atol=1e-8)
+
+
 @pytest.mark.parametrize("cap,passive,ratio", [(20, 5, None), (7, 0, 0.05), (3, 2, 0.5)])
 def test_random_effect_build_on_gpu_matches_host(cap, passive, ratio, monkeypatch):
     """Reservoir (K21), passive set and Pearson selection (K13) on the GPU (radix sorts, segment sums) == host."""
