@@ -876,7 +876,9 @@ __device__ __forceinline__ void tl_stream_wide(const uint32_t* __restrict__ pack
 // --ablate): bit 1 -> register sums instead of the LDS atomics, bit 2 -> no coefficient gathers / key-window loads
 // (x = 1), bit 4 -> fp32 products, bit 8 -> no wide-round gathers only, bit 16 -> no narrow key windows or
 // permutes only, bit 32 -> no wide-round gathers of keys below ((abl >> 8) << 10) (the upper bound of serving the
-// next tier of hot columns from an LDS table: those lanes skip the load). The production build compiles TL_ABL to 0
+// next tier of hot columns from an LDS table: those lanes skip the load), bit 64 -> the same but only for gather
+// instructions whose 64 keys are all below the bound (the instruction is skipped; a wide section is sorted by key,
+// so these are its hot prefix). The production build compiles TL_ABL to 0
 // (no runtime checks).
 #ifdef PML_TL_EXPERIMENT
 __constant__ int c_tl_ablate = 0;
@@ -926,8 +928,10 @@ __device__ __forceinline__ void tl_stream_ring(const uint32_t* __restrict__ pack
 #pragma unroll
     for (int k = 0; k < TL_VEC; ++k) {
       const uint32_t key = (e + 64 * k < e_hi) ? (p[k] >> sbits) : 0u;
+      const bool hot = key < ((uint32_t)abl >> 8) << 10;
       if (abl & 10) xv[k] = XT(1);
-      else if ((abl & 32) && key < ((uint32_t)abl >> 8) << 10) xv[k] = XT(1);
+      else if ((abl & 32) && hot) xv[k] = XT(1);                    // per lane (exec-masked load)
+      else if ((abl & 64) && __ballot(!hot) == 0ull) xv[k] = XT(1);  // whole instruction skipped (all lanes hot)
       else xv[k] = ldg(x + key);
     }
   };

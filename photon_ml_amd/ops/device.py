@@ -425,9 +425,10 @@ class DeviceGLMData(GLMComputable):
         (``DistributedOptimizationProblem.scala:145-160``); here the dropped rows keep their positions (zero
         weight, margins = offsets) and their entries leave the streams, so every pass costs ~rate of a full one.
 
-        Built per update by ``tl_compact_kernel`` (two passes over the streams, no sort, one host sync for all
-        chunks): every unit keeps its table slot and the kept entries are stored as wide interleaved rounds. Row
-        vectors (labels, offsets, weights) are SHARED with this shard; margin caches are the copy's own."""
+        Built per update by ``tl_compact_kernel`` (two passes over the wide streams, no sort, one host sync for all
+        chunks): every unit keeps its table slot and its kept wide entries; the narrow sections (the cheap rounds)
+        are shared unfiltered (``tiled.RowCompaction``). Row vectors (labels, offsets, weights) are SHARED with
+        this shard; margin caches are the copy's own."""
         from .tiled import RowCompaction
         if self.layout != "tiled" or not self.csr or not all(getattr(ch, "il", 0) for ch in self.csr + self.csc):
             return None
@@ -719,12 +720,18 @@ class DeviceGLMData(GLMComputable):
         for c in range(len(self.csr)):
             self._fwd(c, x, mode, loss_id, shift, coef, dzz, z_out, with_offset, stats)
 
-    def t_all(self, x, G, square: int = 0):
+    def t_all(self, x, G, square: int = 0, build_multi: bool = True):
         """Transpose pass over every chunk: one launch + one shard-wide combine in the tiled layout
-        (``KERNEL_CONFIG['tl_multi']``), else per chunk."""
+        (``KERNEL_CONFIG['tl_multi']``), else per chunk. ``build_multi=False``: use the shard-wide tables only if
+        they exist already (a one-off product should not pay their host-side build: ~0.2 s for the 1.2M column
+        tiles of a config-5 random-effect shard)."""
         from .native import KERNEL_CONFIG
         self.n_t = getattr(self, "n_t", 0) + 1
         if getattr(self, "_multi_t", "unset") == "unset":
+            if not build_multi:
+                for c in range(len(self.csc)):
+                    self._t(c, x, G, square)
+                return
             self._build_multi_t()
         # masked passes (entity masks) keep the per-chunk launches: their live flags follow the per-chunk item order
         if (self._multi_t is not None and KERNEL_CONFIG.get("tl_multi", 1)
@@ -1058,13 +1065,14 @@ class DeviceGLMData(GLMComputable):
         """z = X w (fp64, no offsets)."""
         return self.margins(w, 0.0, False)
 
-    def rmatvec(self, r, square: bool = False) -> torch.Tensor:
-        """g = X^T r (``square``: (X.X)^T r) for a per-row vector r (fp64 result, original column order)."""
+    def rmatvec(self, r, square: bool = False, build_multi: bool = True) -> torch.Tensor:
+        """g = X^T r (``square``: (X.X)^T r) for a per-row vector r (fp64 result, original column order).
+        ``build_multi=False`` for one-off products (see :meth:`t_all`)."""
         rr = torch.as_tensor(r, device=self.device).to(self.vdt).contiguous()
         if rr.numel() < max(self.n_rows, 1):
             rr = torch.cat([rr, torch.zeros(max(self.n_rows, 1) - rr.numel(), dtype=self.vdt, device=self.device)])
         out = torch.zeros(self.dim, dtype=torch.float64, device=self.device)
-        self.t_all(rr, out, square=int(square))      # one launch when the shard-wide transpose applies
+        self.t_all(rr, out, square=int(square), build_multi=build_multi)
         return self._unperm(out)
 
     def margins(self, w, margin_shift: float = 0.0, with_offsets: bool = False):

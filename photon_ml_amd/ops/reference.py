@@ -62,7 +62,7 @@ class GLMComputable:
         """X w."""
         raise NotImplementedError
 
-    def rmatvec(self, r, square: bool = False):
+    def rmatvec(self, r, square: bool = False, build_multi: bool = True):
         """X^T r (``square``: (X.X)^T r)."""
         raise NotImplementedError
 
@@ -100,7 +100,7 @@ class TorchGLMData(GLMComputable):
     def matvec(self, w):
         return self._xv(w)
 
-    def rmatvec(self, r, square: bool = False):
+    def rmatvec(self, r, square: bool = False, build_multi: bool = True):
         r = torch.as_tensor(r, dtype=torch.float64, device=self.device)
         if self.n_rows == 0:
             return torch.zeros(self.dim, dtype=torch.float64, device=self.device)

@@ -568,24 +568,26 @@ CMP_SEG = 8              # rounds of one unit per compaction segment (tl_compact
 
 
 def _cmp_segments(ch):
-    """Segment table of a chunk's units (cached): int32 {unit, round_lo, round_hi} per segment, where a unit's
-    rounds are its narrow rounds followed by its wide rounds; plus each segment's unit and the unit's first
-    segment (int64)."""
+    """Segment table of a chunk's units (cached): int32 {unit, round_lo, round_hi} per segment over the unit's
+    WIDE rounds (a unit's rounds are numbered narrow first, then wide: [nn, nn + wide rounds)); plus each segment's
+    unit and the unit's first segment (int64)."""
     cached = getattr(ch, "_cmp_seg", None)
     if cached is not None:
         return cached
     t = ch._table().to(torch.int64)
     dev = t.device
     lo, hi = ch._ew
-    R = (t[:, 5] - t[:, 4]) + (t[:, hi] - t[:, lo] + IL_ROUND - 1) // IL_ROUND
+    nn = t[:, 5] - t[:, 4]
+    R = (t[:, hi] - t[:, lo] + IL_ROUND - 1) // IL_ROUND
     ns = (R + CMP_SEG - 1) // CMP_SEG
     S = int(ns.sum())
     su = torch.repeat_interleave(torch.arange(t.shape[0], device=dev), ns, output_size=S)
     first = (torch.cumsum(ns, 0) - ns)[su]
     r_lo = (torch.arange(S, device=dev) - first) * CMP_SEG
-    r_hi = torch.minimum(r_lo + CMP_SEG, R[su])
+    r_hi = torch.minimum(r_lo + CMP_SEG, R[su]) + nn[su]
+    r_lo = r_lo + nn[su]
     seg = torch.stack([su, r_lo, r_hi], 1).to(torch.int32).contiguous()
-    ch._cmp_seg = (seg, su, first, S)
+    ch._cmp_seg = (seg, su, first, S, IL_ROUND * int(nn.sum()))
     return ch._cmp_seg
 
 
@@ -594,7 +596,11 @@ class RowCompaction:
     the constructor queues the counting pass and the device-side scans (``total`` / ``kept`` stay on the device so
     that all chunks of a shard need ONE host sync), :meth:`finish` allocates the compacted streams, queues the
     writing pass and returns the new chunk. Every unit keeps its table slot (row block / transpose item, split-tile
-    partial rows and combine tables unchanged); the copy has no narrow section."""
+    partial rows and combine tables unchanged). Only the WIDE entries are filtered: the narrow section is shared
+    with the full chunk as is — a filtered narrow round would no longer span < 64 keys, and wide rounds cost 4.4x
+    a narrow round of texture-address time (``profiles/pmc_tl_multi_125M_r3.md``), so dropping narrow rounds made
+    a half-kept shard as slow as the full one. The dropped rows' narrow entries still run: with weight 0 their
+    per-row coefficient is 0 (no gradient) and their margins are never used."""
 
     def __init__(self, ch, keep: torch.Tensor, forward: bool):
         from .native import CmpArgs, check, require_game_lib, stream_handle
@@ -602,7 +608,7 @@ class RowCompaction:
             raise ValueError("row-sampled copies need the interleaved layout")
         self.ch, self.keep, self.forward = ch, keep, forward
         dev = ch.pack.device
-        seg, su, first, S = _cmp_segments(ch)
+        seg, su, first, S, self.n_narrow = _cmp_segments(ch)
         table = ch._table()
         lo, hi = ch._ew
         self.seg_cnt = torch.zeros(max(S, 1), dtype=torch.int32, device=dev)
@@ -640,12 +646,11 @@ class RowCompaction:
         table = ch._table().to(torch.int64).clone()
         table[:, lo] = self.unit_lo
         table[:, hi] = self.unit_lo + self.unit_cnt
-        table[:, 4:6] = 0
         table = table.to(torch.int32).contiguous()
-        nc = copy.copy(ch)
+        nc = copy.copy(ch)               # shares the narrow streams (npack / nval / nbase, table columns 4, 5)
         nc._cmp_seg = None
-        nc.pack, nc.val, nc.nnz = opack, oval, kept
-        nc._set_narrow(*_empty_narrow(oval))
+        nc.pack, nc.val = opack, oval
+        nc.nnz = kept + self.n_narrow
         if self.forward:
             nc.blk = table
             nc.desc = TLFwdDesc(table.data_ptr(), nc.nblk, nc.rbits, opack.data_ptr(), oval.data_ptr(), 1, nc.nar)

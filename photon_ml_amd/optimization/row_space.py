@@ -169,7 +169,7 @@ class RowSpaceBatch:
                 if j < n:
                     v, r = (valid, rows) if sel is None else (valid[sel], rows[sel])
                     ind[r[v[:, j], j]] = 1.0
-            u = seg.glm.rmatvec(ind)                  # every entity's row j, at its own columns
+            u = seg.glm.rmatvec(ind, build_multi=False)                # every entity's row j, at its own columns
             z = seg.glm.matvec(u)                      # (X_e X_e^T)[:, j] on the entity's rows
             for gi, sel in need_ind:
                 _, n, valid, rows, K = geo[gi]
@@ -226,7 +226,7 @@ class RowSpaceBatch:
         for c in self.classes:
             alpha = _bmv(c.Linv, c.view(beta), trans=True)               # L^{-T} beta
             r[c.rows[c.valid]] = alpha[c.valid]
-        return self.seg.glm.rmatvec(r)
+        return self.seg.glm.rmatvec(r, build_multi=False)     # once per update: no shard-wide tables
 
     def margins(self, beta: torch.Tensor) -> torch.Tensor:
         """Per-row X w (no offsets) of the handled entities = L beta, in the segmented row order."""

@@ -4,9 +4,7 @@
 set -o pipefail
 mkdir -p gpurun_out
 export TMPDIR=/tmp
-timeout -k 10 300 python -u scripts/hess_diag.py > gpurun_out/hess_diag.log 2>&1 || { echo "diag failed"; tail -30 gpurun_out/hess_diag.log; exit 1; }
-cat gpurun_out/hess_diag.log
-timeout -k 10 900 python -u -m pytest tests/test_downsample_gpu.py tests/test_sampling.py tests/test_game_gpu.py -m gpu -x -q --timeout 300 --timeout-method thread -k "not test_fused_entity_tron_matches_pass_path" > gpurun_out/pytest_b5.log 2>&1 || { echo "pytest failed"; tail -60 gpurun_out/pytest_b5.log; exit 1; }
+timeout -k 10 900 python -u -m pytest tests/test_downsample_gpu.py tests/test_sampling.py tests/test_game_gpu.py -m gpu -x -q --timeout 300 --timeout-method thread > gpurun_out/pytest_b5.log 2>&1 || { echo "pytest failed"; tail -60 gpurun_out/pytest_b5.log; exit 1; }
 tail -2 gpurun_out/pytest_b5.log
 for r in 1.0 0.1; do
   timeout -k 10 600 python -u bench_game.py --config game5 --steps 3 --warmup 2 --fe-down-sampling-rate $r > gpurun_out/game5_ds$r.json 2> gpurun_out/game5_ds$r.log || { echo "game5 ds $r failed"; tail -30 gpurun_out/game5_ds$r.log; exit 1; }

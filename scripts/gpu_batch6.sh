@@ -13,6 +13,12 @@ for st in feature-sharded replicated; do
   timeout -k 10 300 python -u bench.py --rows-per-gpu 16000000 --steps 5 --warmup 2 --game off --optimizer-state $st > gpurun_out/bench_16M_$st.json 2> gpurun_out/bench_16M_$st.log || { echo "bench $st failed"; tail -20 gpurun_out/bench_16M_$st.log; exit 1; }
   cut -c1-300 gpurun_out/bench_16M_$st.json
 done
+for r in 1.0 0.1; do
+  timeout -k 10 600 python -u bench_game.py --config game5 --steps 3 --warmup 2 --fe-down-sampling-rate $r > gpurun_out/game5_ds$r.json 2> gpurun_out/game5_ds$r.log || { echo "game5 ds $r failed"; tail -30 gpurun_out/game5_ds$r.log; exit 1; }
+  echo "rate $r:"; cut -c1-200 gpurun_out/game5_ds$r.json; grep -o '"coordinate_ms".*' gpurun_out/game5_ds$r.json
+done
+PML_GLM_LIB=photon_ml_amd/ops/_lib/libpml_glm_abl.so timeout -k 10 600 python -u scripts/kbench.py --rows 64000000 --reps 5 --tl-configs "2,4,3" --ablate 0 4160 8256 16448 32832 > gpurun_out/kbench_hot_uniform_64M.jsonl 2> gpurun_out/kbench_hot_uniform_64M.log || { echo "kbench failed"; tail -20 gpurun_out/kbench_hot_uniform_64M.log; exit 1; }
+cut -c1-100 gpurun_out/kbench_hot_uniform_64M.jsonl
 cd /tmp
 PML_TRACE=1 timeout -k 10 600 rocprofv3 --kernel-trace --marker-trace -d $R/gpurun_out/prof_g5 -o prof -- python3 $R/bench_game.py --config game5 --steps 1 --warmup 2 > $R/gpurun_out/gaps_g5.json 2> $R/gpurun_out/gaps_g5.log || { echo "game prof failed"; tail -30 $R/gpurun_out/gaps_g5.log; exit 1; }
 db=$(find $R/gpurun_out/prof_g5 -name "*.db" | head -1)

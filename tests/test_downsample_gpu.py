@@ -14,14 +14,20 @@ pytestmark = pytest.mark.gpu
 
 
 def _filtered_logical(ch, keep: torch.Tensor, forward: bool):
+    """The full chunk's logical entries (per unit: narrow, then wide) with the dropped rows' WIDE entries removed
+    (narrow sections are shared unfiltered)."""
     pk, vl = ch.logical()
     p = pk.to(torch.int64) & 0xFFFFFFFF
+    t = ch._table().to(torch.int64).to(p.device)
+    counts = ch.unit_counts().to(p.device)
+    unit = torch.repeat_interleave(torch.arange(t.shape[0], device=p.device), counts)
+    j = torch.arange(p.numel(), device=p.device) - (torch.cumsum(counts, 0) - counts)[unit]
+    narrow = j < 256 * (t[:, 5] - t[:, 4])[unit]
     if forward:
-        blk = torch.repeat_interleave(torch.arange(ch.nblk, device=p.device), ch.unit_counts().to(p.device))
-        row = (blk << ch.rbits) + (p & ((1 << ch.rbits) - 1))
+        row = (unit << ch.rbits) + (p & ((1 << ch.rbits) - 1))
     else:
         row = p >> ch.cbits
-    m = keep[row].bool()
+    m = narrow | keep[row].bool()
     return p[m], vl[m]
 
 
@@ -42,10 +48,11 @@ def test_row_sampled_shard_streams_and_passes(precision):
         for full, samp, fwd in ((data.csr[c], view.csr[c], True), (data.csc[c], view.csc[c], False)):
             p0, v0 = _filtered_logical(full, kc, fwd)
             p1, v1 = samp.logical()
-            assert samp.n_narrow_rounds == 0 and samp.nnz == p0.numel()
+            assert samp.n_narrow_rounds == full.n_narrow_rounds and samp.nnz == p0.numel()
             assert torch.equal(p1.to(torch.int64) & 0xFFFFFFFF, p0) and torch.equal(v1, v0)
         kept_nnz += view.csr[c].nnz
-    assert 0 < kept_nnz < 0.35 * sum(c.nnz for c in data.csr)
+    wide = sum(c.nnz - 256 * c.n_narrow_rounds for c in data.csr)
+    assert 0 < kept_nnz - sum(256 * c.n_narrow_rounds for c in data.csr) < 0.35 * wide
     # deterministic copy
     again = data.row_sampled(keep)
     for a, b in zip(view.csr + view.csc, again.csr + again.csc):

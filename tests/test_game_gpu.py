@@ -166,7 +166,8 @@ def test_dense_buckets_fused_tron_match_batched_tron(task, d_user, proj, monkeyp
     from photon_ml_amd.algorithm.coordinates import RandomEffectCoordinate
     from photon_ml_amd.projector import RandomProjection
     data, _ = generate_game_data(n_rows=6000, n_users=40, d_user=d_user, seed=27, task=task)
-    cfg = GLMOptimizationConfiguration(OptimizerConfig("TRON", 100, 1e-10), RegularizationContext("L2"), 1.0)
+    # tolerance 1e-14: see test_fused_entity_tron_matches_pass_path
+    cfg = GLMOptimizationConfiguration(OptimizerConfig("TRON", 100, 1e-14), RegularizationContext("L2"), 1.0)
     kw = {} if proj is None else {"projector_type": RandomProjection(proj)}
     dc = RandomEffectDataConfiguration("userId", "user", **kw)
     out = {}
@@ -177,8 +178,8 @@ def test_dense_buckets_fused_tron_match_batched_tron(task, d_user, proj, monkeyp
         m2 = c.update_model(m1, partial_score=torch.from_numpy(np.cos(np.arange(data.n_rows)) * 0.2))
         assert bool(getattr(c, "_dense_fz", None)) == (fused == "1")
         out[fused] = (m1.values.copy(), m2.values.copy(), c.score(m2).cpu())
-    for a, b in zip(out["0"], out["1"]):
-        torch.testing.assert_close(torch.as_tensor(b), torch.as_tensor(a), rtol=1e-6, atol=1e-8)
+    for a, b in zip(out["0"], out["1"]):   # tolerances: see test_fused_entity_tron_matches_pass_path
+        torch.testing.assert_close(torch.as_tensor(b), torch.as_tensor(a), rtol=1e-5, atol=1e-6)
 
 
 @pytest.mark.parametrize("cap,passive,ratio", [(20, 5, None), (7, 0, 0.05), (3, 2, 0.5)])
@@ -250,9 +251,9 @@ def test_entity_masked_passes_give_identical_solve(row_space, monkeypatch):
     assert torch.equal(out[False][2], out[True][2])
 
 
-def _re_two_updates(data, task, opt="TRON", max_iter=30):
+def _re_two_updates(data, task, opt="TRON", max_iter=30, tol=1e-10):
     from photon_ml_amd.algorithm.coordinates import RandomEffectCoordinate
-    cfg = GLMOptimizationConfiguration(OptimizerConfig(opt, max_iter, 1e-10), RegularizationContext("L2"), 1.0)
+    cfg = GLMOptimizationConfiguration(OptimizerConfig(opt, max_iter, tol), RegularizationContext("L2"), 1.0)
     c = RandomEffectCoordinate("u", data, RandomEffectDataConfiguration("userId", "user"), cfg, task,
                                device="cuda", layout="segmented")
     m1 = c.update_model(c.initialize_model())
@@ -269,9 +270,12 @@ def test_fused_entity_tron_matches_pass_path(task, max_rows, d_user, hess, monke
     block-diagonal pass-path TRON: same models, scores and iteration counts, across a warm-started second update.
     ``hess`` = HESS_DMAX: entities of <= 64 coefficients run the exact-Hessian kernel (re_tron_hess_kernel, MFMA;
     d_e 13 -> tile 16, 41 -> 48), wider ones (d_e 101) and hess = 0 the sparse Hessian-vector kernel.
-    ``max_rows``: larger entities stay on the pass path (mixed components). Enough iterations for every entity to
-    converge: an entity stopped at the iteration cap sits at a point that depends on rounding along the path (the
-    exact Hessian and the sparse Hessian-vector product round differently), a converged one does not."""
+    ``max_rows``: larger entities stay on the pass path (mixed components). TRON stops most entities on "function
+    values converged" / "objective is not improving", where the point reached depends on rounding along the path
+    (the exact Hessian, the fused and the pass-path Hessian-vector products all round differently): an objective
+    resolved to ~1e-16 relative pins the coefficients only to ~sqrt(2e-16 f / lambda_min), ~1e-6 here. Measured
+    for Poisson (``profiles/re_solver_agreement_poisson_d40.log``): the three solvers' models differ by up to 2e-6
+    at tolerance 1e-10 and 3e-8 at 1e-14, with identical iteration counts and stop reasons."""
     import photon_ml_amd.optimization.entity_tron as et
     # power-law users (zipf): entities from a few rows (row space) to thousands (fused / pass path)
     data, _ = generate_game_data(n_rows=30000, n_users=700, d_user=d_user, seed=26, task=task)
@@ -280,7 +284,7 @@ def test_fused_entity_tron_matches_pass_path(task, max_rows, d_user, hess, monke
     for fused in ("0", "1"):
         monkeypatch.setenv("PML_RE_FUSED", fused)
         monkeypatch.setattr(et, "FUSED_MAX_ROWS", max_rows or et.FUSED_MAX_ROWS)
-        c, v1, s1, v2, s2 = _re_two_updates(data, task, max_iter=100)
+        c, v1, s1, v2, s2 = _re_two_updates(data, task, max_iter=100, tol=1e-14)
         if fused == "1":
             rs, fz, sub = c._comps
             assert fz is not None and fz.B > 0
@@ -289,7 +293,7 @@ def test_fused_entity_tron_matches_pass_path(task, max_rows, d_user, hess, monke
         out[fused] = (v1, s1, v2, s2, c.last_stats["mean_iterations"])
     a, b = out["0"], out["1"]
     for i in range(4):
-        torch.testing.assert_close(torch.as_tensor(b[i]), torch.as_tensor(a[i]), rtol=1e-6, atol=1e-8)
+        torch.testing.assert_close(torch.as_tensor(b[i]), torch.as_tensor(a[i]), rtol=1e-5, atol=1e-6)
     assert abs(a[4] - b[4]) < 0.05
 
 
