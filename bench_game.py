@@ -71,6 +71,8 @@ def build_parser() -> argparse.ArgumentParser:
     ap.add_argument("--sizes", choices=["uniform", "powerlaw"])
     ap.add_argument("--fe-iters", type=int, default=10)
     ap.add_argument("--re-iters", type=int, default=10)
+    ap.add_argument("--label-bias", type=float, default=0.0,
+                    help="shift of the ground-truth logit (device data): -4 gives ~5 %% positives (click-like data)")
     ap.add_argument("--fe-down-sampling-rate", type=float, default=1.0,
                     help="fixed-effect down-sampling rate (binary-classification sampler: every positive, negatives "
                          "at this rate, re-weighted); < 1 trains each FE update on a row-sampled copy of the shard")
@@ -130,6 +132,7 @@ def main():
 def run(args, dev, rank: int = 0, world: int = 1) -> dict:
     """Generate the preset's data, build the coordinates, run ``args.warmup`` untimed and ``args.steps`` timed
     coordinate-descent sweeps; returns the JSON record (rank 0's view; max time over ranks)."""
+    import numpy as np
     import torch
     from collections import OrderedDict
     from photon_ml_amd.parallel.dist import all_reduce_scalar, barrier, is_dist
@@ -150,7 +153,8 @@ def run(args, dev, rank: int = 0, world: int = 1) -> dict:
                                         args.fe_dim, args.fe_nnz, **gen_kw)
     else:
         data = generate_game_bench_data_device(args.entities_per_gpu, args.rows_per_entity, args.re_dim, args.re_nnz,
-                                               args.fe_dim, args.fe_nnz, device=dev, **gen_kw)
+                                               args.fe_dim, args.fe_nnz, device=dev, label_bias=args.label_bias,
+                                               **gen_kw)
         torch.cuda.empty_cache()
     t_data = time.time() - t0
     log(f"data generated in {t_data:.1f}s ({'host' if args.host_data or dev.type != 'cuda' else 'device'}): "
@@ -235,6 +239,7 @@ def run(args, dev, rank: int = 0, world: int = 1) -> dict:
                    "entities": args.entities_per_gpu * world, "rows_per_entity": args.rows_per_entity,
                    "re_dim": args.re_dim, "fe_dim": args.fe_dim, "fe_iters": args.fe_iters,
                    "re_iters": args.re_iters, "fe_down_sampling_rate": args.fe_down_sampling_rate,
+                   "label_bias": args.label_bias, "positive_fraction": float(np.mean(data.response > 0.5)),
                    "parallelism": f"dp{world}+ep{world}"},
         "coordinate_ms": coord_ms,
         "examples_per_sec": total_rows * args.steps / elapsed,

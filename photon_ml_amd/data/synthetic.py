@@ -253,12 +253,14 @@ def generate_game_bench_data_device(n_entities: int, rows_per_entity: int, re_di
                                     fe_dim: int = 100_000, fe_nnz: int = 30, re_vocab: int = 1 << 20, seed: int = 7,
                                     entity_offset: int = 0, task: str = "LOGISTIC_REGRESSION", pool: str = "random",
                                     int_ids: bool = False, sizes: str = "uniform", size_alpha: float = 1.3,
-                                    max_rows: int = 20000, device="cuda"):
+                                    max_rows: int = 20000, device="cuda", label_bias: float = 0.0):
     """:func:`generate_game_bench_data` with every draw, sort and reduction on the device (torch), so benchmark
     GAME data of config-5 size (25M rows, 2.1G non-zeros per GPU) takes seconds instead of minutes of host numpy;
     only the finished CSR arrays cross to the host (the GameData container is host scipy). Same structure and
     distributions (entity size law, Zipf fixed-effect features, per-entity feature pools, ground-truth labels),
-    different random streams; rows hold strictly increasing columns (canonical CSR, duplicates dropped)."""
+    different random streams; rows hold strictly increasing columns (canonical CSR, duplicates dropped).
+    ``label_bias``: added to the ground-truth logit of logistic labels (e.g. -4: ~5 % positives, the imbalanced
+    click data the reference's binary-classification down-sampler is meant for)."""
     from ..data.game_data import GameData
     dev = torch.device(device)
     gen = torch.Generator(device=dev)
@@ -336,7 +338,7 @@ def generate_game_bench_data_device(n_entities: int, rows_per_entity: int, re_di
     z = zg + zr
     task = TaskType.parse(task)
     if task == TaskType.LOGISTIC_REGRESSION:
-        y = (rnd(n) < torch.sigmoid(z)).to(torch.float64)
+        y = (rnd(n) < torch.sigmoid(z + label_bias)).to(torch.float64)
     elif task == TaskType.POISSON_REGRESSION:
         y = torch.poisson(torch.exp(torch.clamp(z * 0.3, -10, 3)), generator=gen)
     else:

@@ -80,9 +80,14 @@ __device__ __forceinline__ double log1p_exp(double x) {
 // returns l, dl, d2l
 __device__ __forceinline__ void pointwise_loss(int loss, double z, double y, double& l, double& dl, double& d2) {
   if (loss == LOSS_LOGISTIC) {
-    double s = 1.0 / (1.0 + exp(-z));
-    if (y > 0.5) { l = log1p_exp(-z); dl = s - 1.0; }
-    else { l = log1p_exp(z); dl = s; }
+    // one exp, one log1p, one reciprocal: e = exp(-|z|) serves the sigmoid and both log(1 + exp(+-z))
+    // (log1p_exp(x) = max(x, 0) + log1p(exp(-|x|)), bit-identical to log1p_exp)
+    const double e = exp(-fabs(z));
+    const double lp = log1p(e);
+    const double r = 1.0 / (1.0 + e);
+    const double s = z >= 0.0 ? r : e * r;
+    if (y > 0.5) { l = (z < 0.0 ? -z : 0.0) + lp; dl = s - 1.0; }
+    else { l = (z > 0.0 ? z : 0.0) + lp; dl = s; }
     d2 = s * (1.0 - s);
   } else if (loss == LOSS_POISSON) {
     double e = exp(z);
@@ -98,6 +103,10 @@ __device__ __forceinline__ void pointwise_loss(int loss, double z, double y, dou
     dl = d * yy; d2 = 0.0;
   }
 }
+
+// weight x per-row term with an exact 0 for zero-weight rows whatever the term (down-sampled rows, row-sampled
+// copies whose dropped rows carry partial margins: an overflowed exp must not turn 0 x inf into NaN)
+__device__ __forceinline__ double wx(double w, double x) { return w != 0.0 ? w * x : 0.0; }
 
 __device__ __forceinline__ double wave_sum(double v) {
 #pragma unroll
@@ -381,9 +390,9 @@ __device__ __forceinline__ void fwd_finish(const FwdArgs<XT, RT>& a, int s, doub
     const double w = static_cast<double>(r.wt);
     double l, dl, d2;
     pointwise_loss(a.loss, z0v + a.t0 * zdn, static_cast<double>(r.y), l, dl, d2);
-    a.coef[s] = static_cast<XT>(w * dl);              // speculative: the transpose input if t0 is accepted
-    F += w * l;
-    S += w * dl * zdn;
+    a.coef[s] = static_cast<XT>(wx(w, dl));           // speculative: the transpose input if t0 is accepted
+    F += wx(w, l);
+    S += wx(w, dl * zdn);
     return;
   }
   if (a.mode == FWD_HV) {
@@ -399,13 +408,13 @@ __device__ __forceinline__ void fwd_finish(const FwdArgs<XT, RT>& a, int s, doub
   double l, dl, d2;
   pointwise_loss(a.loss, z, static_cast<double>(r.y), l, dl, d2);
   if (a.mode == FWD_VALUE_GRAD) {
-    a.coef[s] = static_cast<XT>(w * dl);
-    if (a.dzz) a.dzz[s] = static_cast<XT>(w * d2);
+    a.coef[s] = static_cast<XT>(wx(w, dl));
+    if (a.dzz) a.dzz[s] = static_cast<XT>(wx(w, d2));
     if (a.z_out) a.z_out[s] = z;  // margin cache for the margin-space line search (ls_eval_kernel)
-    F += w * l;
-    S += w * dl;
+    F += wx(w, l);
+    S += wx(w, dl);
   } else {  // FWD_DZZ
-    a.coef[s] = static_cast<XT>(w * d2);
+    a.coef[s] = static_cast<XT>(wx(w, d2));
   }
 }
 
@@ -2354,13 +2363,13 @@ __global__ __launch_bounds__(NTHREADS) void ls_eval_kernel(int n, double t, int 
       const double w = wv[u];
       double l, dl, d2;
       pointwise_loss(loss, z, yv[u], l, dl, d2);
-      F += w * l;
+      F += wx(w, l);
       if (final_) {
-        coef[i] = static_cast<XT>(w * dl);
-        if (dzz) dzz[i] = static_cast<XT>(w * d2);
-        D += w * dl;
+        coef[i] = static_cast<XT>(wx(w, dl));
+        if (dzz) dzz[i] = static_cast<XT>(wx(w, d2));
+        D += wx(w, dl);
       } else {
-        D += w * dl * zdv[u];
+        D += wx(w, dl * zdv[u]);
       }
     }
   }
@@ -2950,12 +2959,14 @@ int pml_rs_tron(int B, int n, const double* L, const double* y, const double* of
   return 0;
 }
 
-// Margin-space line-search evaluation; out[0..1] = (F, D) or (F, S) when final. stats: >= 2 * 1024 doubles.
+// Margin-space line-search evaluation; out[0..1] = (F, D) or (F, S) when final. stats: >= 2 * 4096 doubles.
 int pml_ls_eval(int prec, int n, double t, int loss, double* z0, const double* zd, const void* y, const void* wt,
                 int final_, void* coef, void* dzz, double* stats, double* out, void* stream) {
   if (n <= 0) return 0;
   hipStream_t st = (hipStream_t)stream;
-  const int nb = (int)std::min<long long>(1024, ((long long)n + NTHREADS - 1) / NTHREADS);
+  // up to 4096 workgroups (16 per CU): the per-row loss is a dependent fp64 exp / log1p / reciprocal chain, more
+  // waves in flight hide it (stats: >= 2 * 4096 doubles)
+  const int nb = (int)std::min<long long>(4096, ((long long)n + 4 * NTHREADS - 1) / (4 * NTHREADS));
   if (prec == 2)
     hipLaunchKernelGGL((ls_eval_kernel<double, double>), dim3(nb), dim3(NTHREADS), 0, st, n, t, loss, z0, zd,
                        (const double*)y, (const double*)wt, final_, (double*)coef, (double*)dzz, stats);

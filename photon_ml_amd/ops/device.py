@@ -118,6 +118,10 @@ class SegChunk:
 # PML_TRON_STATS=1: (kept forward blocks, kept transpose items) fractions of every entity-masked table rebuild
 MASK_STATS = [] if os.environ.get("PML_TRON_STATS") == "1" else None
 
+# row-sampled copies (down-sampling): below this kept fraction the narrow rounds are filtered too (a narrow round
+# costs ~80 of a wide round's ~352 texture-address cycles, so it pays to convert once fewer than ~23 % remain)
+NARROW_FILTER_BELOW = float(os.environ.get("PML_DS_NARROW_FILTER_BELOW", "0.23"))
+
 # keep the margin cache across offset changes (set_offsets shifts it); PML_OFFSET_SHIFT_CACHE=0 drops it instead
 OFFSET_SHIFT_CACHE = os.environ.get("PML_OFFSET_SHIFT_CACHE", "1") != "0"
 
@@ -429,17 +433,22 @@ class DeviceGLMData(GLMComputable):
         chunks): every unit keeps its table slot and its kept wide entries; the narrow sections (the cheap rounds)
         are shared unfiltered (``tiled.RowCompaction``). Row vectors (labels, offsets, weights) are SHARED with
         this shard; margin caches are the copy's own."""
-        from .tiled import RowCompaction
+        from .tiled import RowCompaction, stream_ptr_table
+        from .native import TLFwdMultiDesc
         if self.layout != "tiled" or not self.csr or not all(getattr(ch, "il", 0) for ch in self.csr + self.csc):
             return None
         keep = keep.to(self.device, torch.uint8).contiguous()
         assert keep.numel() >= self.n_rows
+        n = self.n_rows
+        # few rows kept: filter the narrow rounds too (all-wide copy); else share them (see RowCompaction)
+        frac = float(keep[:n].sum()) / max(n, 1)
+        filt = frac < NARROW_FILTER_BELOW
         jobs = []
         for c in range(len(self.csr)):
             kc = keep[self.row_starts[c]: self.row_starts[c + 1]]
-            jobs.append(RowCompaction(self.csr[c], kc, True))
-            jobs.append(RowCompaction(self.csc[c], kc, False))
-        sizes = torch.stack([torch.stack([j.total, j.kept]) for j in jobs]).tolist()    # the one host sync
+            jobs.append(RowCompaction(self.csr[c], kc, True, filt))
+            jobs.append(RowCompaction(self.csc[c], kc, False, filt))
+        sizes = torch.stack([torch.stack([j.total, j.kept]) for j in jobs]).tolist()    # one host sync
         out = [j.finish(int(t), int(k)) for j, (t, k) in zip(jobs, sizes)]
         view = DeviceGLMData(out[0::2], out[1::2], self.row_starts, self.y, self.o, self.wt, self.dim,
                              self.precision, self.device, None)
@@ -449,6 +458,33 @@ class DeviceGLMData(GLMComputable):
             view.new_of_old = self.new_of_old
         view.parts = self.parts           # same unit tables -> same partial-row scratch (same stream, in order)
         view.sampled_from = self
+        view.kept_fraction = frac
+        if getattr(self, "z_cache", None) is not None and getattr(self, "_z_key", None) is not None:
+            # the copy starts from this shard's cached margins (exact for the kept rows; the dropped rows' margins
+            # only ever meet weight 0): the update's first evaluation needs no forward pass
+            view.enable_margin_cache()
+            view.z_cache.copy_(self.z_cache)
+            view.zd.copy_(self.zd)
+            view._z_key, view._z_chain, view._tpend = self._z_key, self._z_chain, self._tpend
+        # shard-wide launch tables of the copy from this shard's (same units, new stream windows): no host-side
+        # rebuild per update
+        if getattr(self, "_multi", "unset") == "unset":
+            self._build_multi()
+        if self._multi is not None:
+            nb = self._multi_blk.clone()
+            cb = torch.cat([ch.blk for ch in view.csr])
+            nb[:, 3:5] = cb[:, 2:4]
+            nb[:, 6:8] = cb[:, 4:6]
+            view._multi_blk = nb
+            view._multi_ptrs = stream_ptr_table(view.csr, self.device)
+            view._multi = TLFwdMultiDesc(nb.data_ptr(), nb.shape[0], self._multi.rbits, view._multi_ptrs.data_ptr(),
+                                         self._multi.il)
+        if getattr(self, "_multi_t", "unset") == "unset":
+            self._build_multi_t()
+        view._multi_t = None if self._multi_t is None else self._multi_t.restreamed(view.csc)
+        gb = getattr(self, "_gbuckets", None)
+        if gb is not None and gb[1] is not None:
+            view._gbuckets = (gb[0], [(mt.restreamed(view.csc), c0, c1) for mt, c0, c1 in gb[1]])
         return view
 
     def set_offsets(self, offsets):
@@ -471,10 +507,10 @@ class DeviceGLMData(GLMComputable):
         self._dzz_key = None          # cached w l''(z) depends on the margins, hence on the offsets
 
     def mark_weights_changed(self):
-        """The row weights were rewritten in place (down-sampling): drop every cache that folds them in."""
+        """The row weights were rewritten in place (down-sampling): drop every cache that folds them in (w l'',
+        the first trial's (F, D)); the cached margins do not depend on the weights and stay valid."""
         self._dzz_key = None
-        self._z_key = None
-        self._step_base = None
+        self._ls_t0 = None
 
     # ---- margin-space line search (GLMObjective.margin_line_search / LBFGS): z(t) = z0 + t zd ----------------
     # State: the margins of the last accepted point are z0 + tpend * zd (the accepted step is materialised
@@ -488,7 +524,7 @@ class DeviceGLMData(GLMComputable):
             n = max(self.n_rows, 1)
             self.z_cache = torch.zeros(n, dtype=torch.float64, device=self.device)
             self.zd = torch.zeros(n, dtype=torch.float64, device=self.device)
-            self.ls_stats = torch.zeros(2 * 1024, dtype=torch.float64, device=self.device)
+            self.ls_stats = torch.zeros(2 * 4096, dtype=torch.float64, device=self.device)
             self.ls_out = torch.zeros(2, dtype=torch.float64, device=self.device)
             self._z_key, self._z_chain, self._tpend, self._ls_t0 = None, 0, 0.0, None
         return True
@@ -980,7 +1016,7 @@ class DeviceGLMData(GLMComputable):
     def ls_stats_buf(self) -> torch.Tensor:
         buf = getattr(self, "ls_stats", None)
         if buf is None:
-            self.ls_stats = buf = torch.zeros(2 * 1024, dtype=torch.float64, device=self.device)
+            self.ls_stats = buf = torch.zeros(2 * 4096, dtype=torch.float64, device=self.device)
         return buf
 
     def _value_grad_packed(self, loss, w_eff, margin_shift) -> torch.Tensor:

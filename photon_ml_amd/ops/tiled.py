@@ -486,8 +486,10 @@ class TLTMulti:
             its.append(np.column_stack([np.full(len(it), c), it[:, 0] + toff, it[:, 1], it[:, 2],
                                         np.full(len(it), row_starts[c]), it[:, 4], it[:, 5]]))
         it = np.concatenate(its) if its else np.zeros((0, 7), np.int64)
+        src_all = np.arange(len(it))
         if tile_range is not None:
-            it = it[(it[:, 1] >= tile_range[0]) & (it[:, 1] < tile_range[1])]
+            in_range = (it[:, 1] >= tile_range[0]) & (it[:, 1] < tile_range[1])
+            it = it[in_range]
         n = len(it)
         tile = it[:, 1]
         order = np.lexsort((np.arange(n), tile))          # grouped by tile, (chunk, item) order inside
@@ -508,8 +510,11 @@ class TLTMulti:
         self.nitems, self.nparts, self.ncu, self.nmt = n, int(km.sum()), int(nu.sum()), len(km)
         rows = np.column_stack([it[:, 0], it[:, 1], it[:, 2], it[:, 3], part, it[:, 4], it[:, 5],
                                 it[:, 6]]).astype(np.int32)
+        src = src_all if tile_range is None else src_all[in_range]
         if XCD_GROUPS > 1 and n > XCD_GROUPS:
-            rows = rows[xcd_order(it[:, 0], XCD_GROUPS)]
+            xo = xcd_order(it[:, 0], XCD_GROUPS)
+            rows, src = rows[xo], src[xo]
+        self._src = torch.from_numpy(src.astype(np.int64)).to(dev)   # row -> index into the chunks' concatenated items
         self.items = torch.tensor(rows.reshape(-1, 8), device=dev)
         self.mt_tiles = torch.tensor(np.r_[ts[starts][k > 1], 0].astype(np.int32)[: max(self.nmt, 1)], device=dev)
         self.mt_ptr = torch.tensor(np.r_[0, np.cumsum(nu)].astype(np.int32), device=dev)
@@ -524,6 +529,28 @@ class TLTMulti:
     @property
     def parts_needed(self) -> int:
         return (self.nparts + self.ncu) << self.cbits
+
+    def restreamed(self, chunks: Sequence["TLTChunk"]) -> "TLTMulti":
+        """The same launch over other streams of the SAME units (row-sampled copies, ``RowCompaction``): every
+        row's stream window and narrow range come from ``chunks``' item tables (one device gather), tiles,
+        partial-row slots and combine tables are shared. No host work beyond the pointer table."""
+        import copy
+        from .native import TLTMultiDesc
+        dev = self.items.device
+        cat = torch.cat([ch.items[: ch.nitems].to(torch.int64) for ch in chunks]) if chunks else None
+        rows = self.items.to(torch.int64).clone()
+        if self.nitems:
+            sel = cat[self._src]
+            rows[:, 2:4] = sel[:, 1:3]
+            rows[:, 6:8] = sel[:, 4:6]
+        new = copy.copy(self)
+        new.items = rows.to(torch.int32).contiguous()
+        new.ptrs = stream_ptr_table(chunks, dev)
+        new._chunks = list(chunks)
+        d = self.desc
+        new.desc = TLTMultiDesc(new.items.data_ptr(), d.nitems, d.cbits, new.ptrs.data_ptr(), d.mt_tiles, d.mt_ptr,
+                                d.nmt, d.dim, d.cu, d.ncu, d.nparts_total, d.il)
+        return new
 
     def emulate_rmatvec(self, r: torch.Tensor, square: bool = False) -> torch.Tensor:
         """Host emulation of the launch + combine (item partial rows, direct tiles, two-level combine)."""
@@ -567,28 +594,29 @@ def stream_ptr_table(chunks, device) -> torch.Tensor:
 CMP_SEG = 8              # rounds of one unit per compaction segment (tl_compact_kernel, one wave each)
 
 
-def _cmp_segments(ch):
-    """Segment table of a chunk's units (cached): int32 {unit, round_lo, round_hi} per segment over the unit's
-    WIDE rounds (a unit's rounds are numbered narrow first, then wide: [nn, nn + wide rounds)); plus each segment's
-    unit and the unit's first segment (int64)."""
-    cached = getattr(ch, "_cmp_seg", None)
-    if cached is not None:
-        return cached
+def _cmp_segments(ch, narrow: bool):
+    """Segment table of a chunk's units (cached per ``narrow``): int32 {unit, round_lo, round_hi} per segment, a
+    unit's rounds numbered narrow first, then wide ([nn, nn + wide rounds)); ``narrow=False``: the wide rounds
+    only. Plus each segment's unit, the unit's first segment (int64) and the chunk's narrow entry count."""
+    cache = ch.__dict__.setdefault("_cmp_seg", {})
+    if cache.get(narrow) is not None:
+        return cache[narrow]
     t = ch._table().to(torch.int64)
     dev = t.device
     lo, hi = ch._ew
     nn = t[:, 5] - t[:, 4]
-    R = (t[:, hi] - t[:, lo] + IL_ROUND - 1) // IL_ROUND
+    R = (t[:, hi] - t[:, lo] + IL_ROUND - 1) // IL_ROUND + (nn if narrow else 0)
     ns = (R + CMP_SEG - 1) // CMP_SEG
     S = int(ns.sum())
     su = torch.repeat_interleave(torch.arange(t.shape[0], device=dev), ns, output_size=S)
     first = (torch.cumsum(ns, 0) - ns)[su]
     r_lo = (torch.arange(S, device=dev) - first) * CMP_SEG
-    r_hi = torch.minimum(r_lo + CMP_SEG, R[su]) + nn[su]
-    r_lo = r_lo + nn[su]
+    r_hi = torch.minimum(r_lo + CMP_SEG, R[su])
+    if not narrow:
+        r_lo, r_hi = r_lo + nn[su], r_hi + nn[su]
     seg = torch.stack([su, r_lo, r_hi], 1).to(torch.int32).contiguous()
-    ch._cmp_seg = (seg, su, first, S, IL_ROUND * int(nn.sum()))
-    return ch._cmp_seg
+    cache[narrow] = (seg, su, first, S, IL_ROUND * int(nn.sum()))
+    return cache[narrow]
 
 
 class RowCompaction:
@@ -596,19 +624,23 @@ class RowCompaction:
     the constructor queues the counting pass and the device-side scans (``total`` / ``kept`` stay on the device so
     that all chunks of a shard need ONE host sync), :meth:`finish` allocates the compacted streams, queues the
     writing pass and returns the new chunk. Every unit keeps its table slot (row block / transpose item, split-tile
-    partial rows and combine tables unchanged). Only the WIDE entries are filtered: the narrow section is shared
-    with the full chunk as is — a filtered narrow round would no longer span < 64 keys, and wide rounds cost 4.4x
-    a narrow round of texture-address time (``profiles/pmc_tl_multi_125M_r3.md``), so dropping narrow rounds made
-    a half-kept shard as slow as the full one. The dropped rows' narrow entries still run: with weight 0 their
-    per-row coefficient is 0 (no gradient) and their margins are never used."""
+    partial rows and combine tables unchanged).
 
-    def __init__(self, ch, keep: torch.Tensor, forward: bool):
+    ``filter_narrow=False`` (most rows kept): only the WIDE entries are filtered and the narrow section is shared
+    with the full chunk as is — a filtered narrow round no longer spans < 64 keys, and a wide round costs 4.4x a
+    narrow round of texture-address time (``profiles/pmc_tl_multi_125M_r3.md``), so converting them made a
+    half-kept shard as slow as the full one; the dropped rows' narrow entries still run (weight 0: their per-row
+    coefficient is 0, their margins are never used). ``True`` (few rows kept, below ~80/352 of a round): the
+    narrow entries are filtered too and the copy is all wide rounds."""
+
+    def __init__(self, ch, keep: torch.Tensor, forward: bool, filter_narrow: bool = False):
         from .native import CmpArgs, check, require_game_lib, stream_handle
         if not ch.il:
             raise ValueError("row-sampled copies need the interleaved layout")
         self.ch, self.keep, self.forward = ch, keep, forward
         dev = ch.pack.device
-        seg, su, first, S, self.n_narrow = _cmp_segments(ch)
+        self.filter_narrow = bool(filter_narrow)
+        seg, su, first, S, self.n_narrow = _cmp_segments(ch, self.filter_narrow)
         table = ch._table()
         lo, hi = ch._ew
         self.seg_cnt = torch.zeros(max(S, 1), dtype=torch.int32, device=dev)
@@ -646,11 +678,17 @@ class RowCompaction:
         table = ch._table().to(torch.int64).clone()
         table[:, lo] = self.unit_lo
         table[:, hi] = self.unit_lo + self.unit_cnt
+        if self.filter_narrow:
+            table[:, 4:6] = 0
         table = table.to(torch.int32).contiguous()
         nc = copy.copy(ch)               # shares the narrow streams (npack / nval / nbase, table columns 4, 5)
-        nc._cmp_seg = None
+        nc._cmp_seg = {}
         nc.pack, nc.val = opack, oval
-        nc.nnz = kept + self.n_narrow
+        if self.filter_narrow:
+            nc._set_narrow(*_empty_narrow(oval))
+            nc.nnz = kept
+        else:
+            nc.nnz = kept + self.n_narrow
         if self.forward:
             nc.blk = table
             nc.desc = TLFwdDesc(table.data_ptr(), nc.nblk, nc.rbits, opack.data_ptr(), oval.data_ptr(), 1, nc.nar)

@@ -13,9 +13,9 @@ from photon_ml_amd.function.losses import LOGISTIC
 pytestmark = pytest.mark.gpu
 
 
-def _filtered_logical(ch, keep: torch.Tensor, forward: bool):
-    """The full chunk's logical entries (per unit: narrow, then wide) with the dropped rows' WIDE entries removed
-    (narrow sections are shared unfiltered)."""
+def _filtered_logical(ch, keep: torch.Tensor, forward: bool, filt: bool):
+    """The full chunk's logical entries (per unit: narrow, then wide) with the dropped rows' WIDE entries removed,
+    and their narrow entries too when ``filt`` (else narrow sections are shared unfiltered)."""
     pk, vl = ch.logical()
     p = pk.to(torch.int64) & 0xFFFFFFFF
     t = ch._table().to(torch.int64).to(p.device)
@@ -27,13 +27,17 @@ def _filtered_logical(ch, keep: torch.Tensor, forward: bool):
         row = (unit << ch.rbits) + (p & ((1 << ch.rbits) - 1))
     else:
         row = p >> ch.cbits
-    m = narrow | keep[row].bool()
+    m = keep[row].bool() if filt else (narrow | keep[row].bool())
     return p[m], vl[m]
 
 
+@pytest.mark.parametrize("filt", [False, True])
 @pytest.mark.parametrize("precision", ["f64", "bf16"])
-def test_row_sampled_shard_streams_and_passes(precision):
+def test_row_sampled_shard_streams_and_passes(precision, filt, monkeypatch):
+    """``filt``: the narrow rounds are filtered too (few rows kept) or shared (most rows kept)."""
     from photon_ml_amd.data.synthetic import generate_device_shard
+    from photon_ml_amd.ops import device
+    monkeypatch.setattr(device, "NARROW_FILTER_BELOW", 1.0 if filt else 0.0)
     data, _ = generate_device_shard(200_000, 50_000, 30, "cuda", precision, seed=6, chunk_rows=1 << 16,
                                     layout="tiled")
     assert sum(c.n_narrow_rounds for c in data.csr) > 0 and sum(c.n_narrow_rounds for c in data.csc) > 0
@@ -46,13 +50,18 @@ def test_row_sampled_shard_streams_and_passes(precision):
     for c in range(len(data.csr)):
         kc = keep[data.row_starts[c]: data.row_starts[c + 1]]
         for full, samp, fwd in ((data.csr[c], view.csr[c], True), (data.csc[c], view.csc[c], False)):
-            p0, v0 = _filtered_logical(full, kc, fwd)
+            p0, v0 = _filtered_logical(full, kc, fwd, filt)
             p1, v1 = samp.logical()
-            assert samp.n_narrow_rounds == full.n_narrow_rounds and samp.nnz == p0.numel()
+            assert samp.n_narrow_rounds == (0 if filt else full.n_narrow_rounds) and samp.nnz == p0.numel()
             assert torch.equal(p1.to(torch.int64) & 0xFFFFFFFF, p0) and torch.equal(v1, v0)
         kept_nnz += view.csr[c].nnz
-    wide = sum(c.nnz - 256 * c.n_narrow_rounds for c in data.csr)
-    assert 0 < kept_nnz - sum(256 * c.n_narrow_rounds for c in data.csr) < 0.35 * wide
+    if filt:
+        assert 0 < kept_nnz < 0.35 * sum(c.nnz for c in data.csr)
+    else:
+        wide = sum(c.nnz - 256 * c.n_narrow_rounds for c in data.csr)
+        assert 0 < kept_nnz - sum(256 * c.n_narrow_rounds for c in data.csr) < 0.35 * wide
+    # the copy's shard-wide launch tables are derived from the full shard's (no rebuild)
+    assert view._multi is not None and view._multi_t is not None
     # deterministic copy
     again = data.row_sampled(keep)
     for a, b in zip(view.csr + view.csc, again.csr + again.csc):
