@@ -1210,36 +1210,62 @@ __global__ __launch_bounds__(NW * 64) void tl_t_multi_kernel(const int* __restri
 //   level 1: unit u sums parts [cu[3u+1], cu[3u+2]) (<= TL_SEG consecutive items of one tile) -> l1[u * C + c]
 //   level 2: tile t (blockIdx.x) sums its units [mt_ptr[t], mt_ptr[t+1]) in order, one column per thread
 //            (blockIdx.y = column group), and adds into G.
+// Fixed-order sum of rows [r0, r1) of ``src`` (rows of C doubles) at column c = blockIdx.y * 64 + lane: the 4 waves
+// of the workgroup take contiguous quarters of the row range with 4 independent loads in flight per lane, and the
+// quarters are added in order through LDS (result in wave 0). Deterministic: the split depends only on r1 - r0.
+// (One thread per column looping over every row was latency bound: the hot tiles of a 125M-row shard hold ~200
+// level-1 rows each, and only nmt x C / 256 workgroups ran — 1 ms per pass, profiles/bench_125M_timed_window.md.)
+__device__ __forceinline__ double rows_sum64(const double* __restrict__ src, int C, int r0, int r1, int c,
+                                             double* sh) {
+  const int w = threadIdx.x >> 6, lane = threadIdx.x & 63;
+  const int n = r1 - r0;
+  const int q0 = r0 + (n * w) / 4, q1 = r0 + (n * (w + 1)) / 4;
+  double s0 = 0.0, s1 = 0.0, s2 = 0.0, s3 = 0.0;
+  if (c < C) {
+    int r = q0;
+    for (; r + 3 < q1; r += 4) {
+      s0 += src[(size_t)r * C + c];
+      s1 += src[(size_t)(r + 1) * C + c];
+      s2 += src[(size_t)(r + 2) * C + c];
+      s3 += src[(size_t)(r + 3) * C + c];
+    }
+    for (; r < q1; ++r) s0 += src[(size_t)r * C + c];
+  }
+  sh[w * 64 + lane] = (s0 + s1) + (s2 + s3);
+  __syncthreads();
+  return (sh[lane] + sh[64 + lane]) + (sh[128 + lane] + sh[192 + lane]);
+}
+
+// level 1: unit u (rows p0..p1 of one split tile's item partial rows) -> l1 row u. Grid (ncu, C / 64), 256 threads.
 __global__ __launch_bounds__(NTHREADS) void tl_t_combine1_kernel(const int* __restrict__ cu, int cbits,
                                                                  const double* __restrict__ parts,
                                                                  double* __restrict__ l1,
                                                                  const unsigned char* __restrict__ live_mt) {
+  __shared__ double sh[NTHREADS];
   const int u = blockIdx.x;
-  if (live_mt && !live_mt[cu[3 * u]]) return;
+  if (live_mt && !live_mt[cu[3 * u]]) return;           // whole workgroup
   const int C = 1 << cbits;
-  const int p0 = cu[3 * u + 1], p1 = cu[3 * u + 2];
-  for (int c = threadIdx.x; c < C; c += NTHREADS) {
-    double s = 0.0;
-    for (int p = p0; p < p1; ++p) s += parts[(size_t)p * C + c];
-    l1[(size_t)u * C + c] = s;
-  }
+  const int c = blockIdx.y * 64 + (threadIdx.x & 63);
+  const double s = rows_sum64(parts, C, cu[3 * u + 1], cu[3 * u + 2], c, sh);
+  if (threadIdx.x < 64 && c < C) l1[(size_t)u * C + c] = s;
 }
 
+// level 2: split tile t (its level-1 rows mt_ptr[t] .. mt_ptr[t+1]) -> G. Grid (nmt, C / 64), 256 threads.
 __global__ __launch_bounds__(NTHREADS) void tl_t_combine2_kernel(const int* __restrict__ mt_tiles,
                                                                  const int* __restrict__ mt_ptr, int cbits,
                                                                  const double* __restrict__ l1,
                                                                  double* __restrict__ G, int dim,
                                                                  const unsigned char* __restrict__ live_mt) {
+  __shared__ double sh[NTHREADS];
   const int t = blockIdx.x;
-  if (live_mt && !live_mt[t]) return;
+  if (live_mt && !live_mt[t]) return;                   // whole workgroup
   const int C = 1 << cbits;
-  const int c = blockIdx.y * NTHREADS + threadIdx.x;
-  if (c >= C) return;
-  const int u0 = mt_ptr[t], u1 = mt_ptr[t + 1];
-  double s = 0.0;
-  for (int u = u0; u < u1; ++u) s += l1[(size_t)u * C + c];
-  const int col = (mt_tiles[t] << cbits) + c;
-  if (col < dim) G[col] += s;
+  const int c = blockIdx.y * 64 + (threadIdx.x & 63);
+  const double s = rows_sum64(l1, C, mt_ptr[t], mt_ptr[t + 1], c, sh);
+  if (threadIdx.x < 64 && c < C) {
+    const int col = (mt_tiles[t] << cbits) + c;
+    if (col < dim) G[col] += s;
+  }
 }
 
 // ``il``: 1 = the streams are stored in the lane-interleaved layout (see tl_stream_il) -> pipeline P = 3.
@@ -1387,10 +1413,10 @@ static int tl_t_impl(const TLTDesc* c, const void* x, double* G, double* parts, 
   if (c->nmt > 0) {
     const int C = 1 << c->cbits;
     double* l1 = parts + (size_t)c->nparts_total * C;
-    hipLaunchKernelGGL(tl_t_combine1_kernel, dim3(c->ncu), dim3(NTHREADS), 0, st, c->cu, c->cbits, parts, l1,
-                       c->live_mt);
+    hipLaunchKernelGGL(tl_t_combine1_kernel, dim3(c->ncu, (C + 63) / 64), dim3(NTHREADS), 0, st, c->cu, c->cbits,
+                       parts, l1, c->live_mt);
     LAUNCH_CHECK();
-    hipLaunchKernelGGL(tl_t_combine2_kernel, dim3(c->nmt, (C + NTHREADS - 1) / NTHREADS), dim3(NTHREADS), 0, st,
+    hipLaunchKernelGGL(tl_t_combine2_kernel, dim3(c->nmt, (C + 63) / 64), dim3(NTHREADS), 0, st,
                        c->mt_tiles, c->mt_ptr, c->cbits, l1, G, c->dim, c->live_mt);
     LAUNCH_CHECK();
   }
@@ -1428,10 +1454,10 @@ static int tl_t_multi_impl(const TLTMultiDesc* c, const void* x, double* G, doub
   if (c->nmt > 0) {
     const int C = 1 << c->cbits;
     double* l1 = parts + (size_t)c->nparts_total * C;
-    hipLaunchKernelGGL(tl_t_combine1_kernel, dim3(c->ncu), dim3(NTHREADS), 0, st, c->cu, c->cbits, parts, l1,
-                       c->live_mt);
+    hipLaunchKernelGGL(tl_t_combine1_kernel, dim3(c->ncu, (C + 63) / 64), dim3(NTHREADS), 0, st, c->cu, c->cbits,
+                       parts, l1, c->live_mt);
     LAUNCH_CHECK();
-    hipLaunchKernelGGL(tl_t_combine2_kernel, dim3(c->nmt, (C + NTHREADS - 1) / NTHREADS), dim3(NTHREADS), 0, st,
+    hipLaunchKernelGGL(tl_t_combine2_kernel, dim3(c->nmt, (C + 63) / 64), dim3(NTHREADS), 0, st,
                        c->mt_tiles, c->mt_ptr, c->cbits, l1, G, c->dim, c->live_mt);
     LAUNCH_CHECK();
   }

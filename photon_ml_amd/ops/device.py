@@ -246,7 +246,30 @@ class DeviceGLMData(GLMComputable):
                     raise ValueError(f"chunk {c}: transpose column >= dim")
         if self.parts.numel() < max([c.parts_needed for c in self.csr + self.csc] + [1]):
             raise ValueError("partial-row scratch too small")
+        self._validate_multi()
         return True
+
+    def _validate_multi(self):
+        """The shard-wide launch tables (when built): every unit's stream window inside ITS chunk's streams,
+        narrow ranges inside the chunk's narrow section, the partial-row scratch large enough."""
+        mb = getattr(self, "_multi", None)
+        if mb is not None and not isinstance(mb, str):
+            t = self._multi_blk.cpu().to(torch.int64)
+            for c, ch in enumerate(self.csr):
+                r = t[t[:, 0] == c]
+                if ch.il and r.shape[0] and (int(r[:, 3].min()) < 0 or int((r[:, 3] + (r[:, 4] - r[:, 3] + 255) // 256 * 256).max())
+                                   > ch.pack.numel() or int(r[:, 7].max()) > ch.nbase.numel() * (ch.n_narrow_rounds > 0)):
+                    raise ValueError(f"chunk {c}: shard-wide forward table outside the chunk's streams")
+        mt = getattr(self, "_multi_t", None)
+        if mt is not None and not isinstance(mt, str):
+            if self.parts.numel() < mt.parts_needed:
+                raise ValueError("partial-row scratch too small for the shard-wide transpose")
+            t = mt.items.cpu().to(torch.int64)
+            for c, ch in enumerate(self.csc):
+                r = t[t[:, 0] == c]
+                if ch.il and r.shape[0] and (int(r[:, 2].min()) < 0 or int((r[:, 2] + (r[:, 3] - r[:, 2] + 255) // 256 * 256).max())
+                                   > ch.pack.numel() or int(r[:, 7].max()) > ch.nbase.numel() * (ch.n_narrow_rounds > 0)):
+                    raise ValueError(f"chunk {c}: shard-wide transpose table outside the chunk's streams")
 
     @staticmethod
     def _validate_narrow(c: int, ch, table: torch.Tensor, xlen: int, what: str):
@@ -440,6 +463,11 @@ class DeviceGLMData(GLMComputable):
         keep = keep.to(self.device, torch.uint8).contiguous()
         assert keep.numel() >= self.n_rows
         n = self.n_rows
+        # this shard's launch tables first: building them may grow the partial-row scratch the copy shares
+        if getattr(self, "_multi", "unset") == "unset":
+            self._build_multi()
+        if getattr(self, "_multi_t", "unset") == "unset":
+            self._build_multi_t()
         # few rows kept: filter the narrow rounds too (all-wide copy); else share them (see RowCompaction)
         frac = float(keep[:n].sum()) / max(n, 1)
         filt = frac < NARROW_FILTER_BELOW
@@ -456,7 +484,6 @@ class DeviceGLMData(GLMComputable):
         view.old_of_new = self.old_of_new
         if self.old_of_new is not None:
             view.new_of_old = self.new_of_old
-        view.parts = self.parts           # same unit tables -> same partial-row scratch (same stream, in order)
         view.sampled_from = self
         view.kept_fraction = frac
         if getattr(self, "z_cache", None) is not None and getattr(self, "_z_key", None) is not None:
@@ -468,8 +495,6 @@ class DeviceGLMData(GLMComputable):
             view._z_key, view._z_chain, view._tpend = self._z_key, self._z_chain, self._tpend
         # shard-wide launch tables of the copy from this shard's (same units, new stream windows): no host-side
         # rebuild per update
-        if getattr(self, "_multi", "unset") == "unset":
-            self._build_multi()
         if self._multi is not None:
             nb = self._multi_blk.clone()
             cb = torch.cat([ch.blk for ch in view.csr])
@@ -479,12 +504,15 @@ class DeviceGLMData(GLMComputable):
             view._multi_ptrs = stream_ptr_table(view.csr, self.device)
             view._multi = TLFwdMultiDesc(nb.data_ptr(), nb.shape[0], self._multi.rbits, view._multi_ptrs.data_ptr(),
                                          self._multi.il)
-        if getattr(self, "_multi_t", "unset") == "unset":
-            self._build_multi_t()
         view._multi_t = None if self._multi_t is None else self._multi_t.restreamed(view.csc)
         gb = getattr(self, "_gbuckets", None)
         if gb is not None and gb[1] is not None:
             view._gbuckets = (gb[0], [(mt.restreamed(view.csc), c0, c1) for mt, c0, c1 in gb[1]])
+        # same unit tables -> the same partial-row scratch (used in stream order); assigned last, after every
+        # table this shard built above could have grown it
+        view.parts = self.parts
+        if os.environ.get("PML_CHECK_KERNEL_INPUTS", "0") == "1":
+            view.validate()
         return view
 
     def set_offsets(self, offsets):
