@@ -63,6 +63,33 @@ class GLMObjective:
             grad = grad + self.l2_weight * w
         return f, grad
 
+    def zero_state_bound(self, data, z: torch.Tensor):
+        """(f(0), an upper bound of ||g(0)||, thunk of the exact ||g(0)||) from one elementwise pass, or None when
+        the backend cannot bound it (``zero_point_sums``). The optimizer scales its tolerances by f(0) and ||g(0)||
+        (Optimizer.scala, Appendix C.7); ||g(0)|| needs a transpose pass, but it is only compared with later
+        gradient norms, so a bound decides every iteration whose gradient is above it. g(0) = a (X^T c - s S)
+        with c = w l'(offsets), so ||g(0)|| <= max|a| (||X||_F ||c|| + ||s|| |S|)."""
+        fn = getattr(data, "zero_point_sums", None)
+        if fn is None:
+            return None
+        norm = self.normalization
+        _, shift = norm.effective(z)
+        try:
+            F, S, csq, xsq = fn(self.loss, shift)
+        except AttributeError:              # a wrapper whose local backend cannot bound it
+            return None
+        b = (xsq * csq) ** 0.5
+        if norm.shifts is not None:
+            b += float(torch.linalg.vector_norm(norm.shifts.to(torch.float64))) * abs(S)
+        if norm.factors is not None:
+            b *= float(norm.factors.to(torch.float64).abs().max())
+        b = b * (1.0 + 1e-6) + 1e-300             # rounding of the sums: stay an upper bound
+        self.n_value_grad += 1
+
+        def exact():
+            return float(torch.linalg.vector_norm(self.calculate(data, z)[1].to(torch.float64)))
+        return F, b, exact
+
     def margin_line_search(self, data, x0: torch.Tensor, d: torch.Tensor, t0: float = 1.0,
                            dots=None) -> Optional["MarginLineSearch"]:
         """Line search along x0 + t d in MARGIN space (GLM margins are affine in t), or None when the data
@@ -162,11 +189,17 @@ class MarginLineSearch:
         return f, dd
 
     def finish(self, t: float):
-        """(x(t), f(x(t)), gradient at x(t)) — one transpose pass."""
+        """(x(t), f(x(t)), gradient at x(t)) — one transpose pass. With a backend that keeps the sums on the
+        device (``ls_finish_device``) f is a 0-d device tensor: the caller reads it together with its next
+        synchronisation (L-BFGS: the history pair's scalars), not right after the transpose pass."""
         x = self.x0 + t * self.d
         norm = self.obj.normalization
         w_eff, shift = norm.effective(x)
-        f, s, g = self.data.ls_finish_sums(self.obj.loss, t, w_eff, shift, norm.shifts is not None)
+        fin = getattr(self.data, "ls_finish_device", None)
+        if fin is not None:
+            f, s, g = fin(self.obj.loss, t, w_eff, shift, norm.shifts is not None)
+        else:
+            f, s, g = self.data.ls_finish_sums(self.obj.loss, t, w_eff, shift, norm.shifts is not None)
         self.obj.n_value_grad += 1
         grad = norm.finalize_vector(g, s)
         if self.obj.l2_weight > 0:

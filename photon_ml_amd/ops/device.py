@@ -486,6 +486,7 @@ class DeviceGLMData(GLMComputable):
             view.new_of_old = self.new_of_old
         view.sampled_from = self
         view.kept_fraction = frac
+        view._frob_sq = self.frob_sq()    # the copy holds a subset of the entries: still an upper bound
         if getattr(self, "z_cache", None) is not None and getattr(self, "_z_key", None) is not None:
             # the copy starts from this shard's cached margins (exact for the kept rows; the dropped rows' margins
             # only ever meet weight 0): the update's first evaluation needs no forward pass
@@ -634,6 +635,11 @@ class DeviceGLMData(GLMComputable):
                 self._grad_finish(G, out)
             self.n_passes += 1
             return out
+
+    def ls_finish_device(self, loss, t: float, w_eff, shift, need_s: bool = True):
+        """:meth:`ls_finish_sums` with F and S left as 0-d device tensors (no host synchronisation)."""
+        out = self.ls_finish_packed(loss, t, w_eff, shift, need_s)
+        return out[self.dim], out[self.dim + 1], out[: self.dim]
 
     def ls_finish_sums(self, loss, t: float, w_eff, shift, need_s: bool = True):
         out = self.ls_finish_packed(loss, t, w_eff, shift, need_s)
@@ -1040,6 +1046,27 @@ class DeviceGLMData(GLMComputable):
         check(self.lib.pml_ls_eval(self.prec, n, 0.0, loss.loss_id, z0.data_ptr(), z0.data_ptr(), self.y.data_ptr(),
                                    self.wt.data_ptr(), 1, self.coef.data_ptr(), None, self.ls_stats_buf().data_ptr(),
                                    stats_out.data_ptr(), stream_handle(self.device)), "ls_eval(zero)")
+
+    def frob_sq(self) -> torch.Tensor:
+        """||X||_F^2 of the shard (sum of the squared stored values, fp64; 0-d device tensor, computed once)."""
+        c = getattr(self, "_frob_sq", None)
+        if c is None:
+            c = torch.zeros((), dtype=torch.float64, device=self.device)
+            for ch in self.csr:                 # forward copy: every non-zero once (padding entries are 0)
+                for v in (ch.val, getattr(ch, "nval", None)):
+                    if v is not None and v.numel():
+                        c += torch.linalg.vector_norm(v, dtype=torch.float64) ** 2
+            self._frob_sq = c
+        return c
+
+    def zero_point_sums(self, loss, margin_shift) -> list:
+        """[F, S, ||c||^2, ||X||_F^2] at w = 0 (c = w l'(offsets + shift)): one elementwise pass, one sync; the
+        zero point's gradient bound of GLMObjective.zero_state_bound."""
+        out = torch.empty(4, dtype=torch.float64, device=self.device)
+        self._zero_coef(loss, margin_shift, out[:2])
+        out[2] = torch.linalg.vector_norm(self.coef[: self.n_rows], dtype=torch.float64) ** 2
+        out[3] = self.frob_sq()
+        return out.tolist()
 
     def ls_stats_buf(self) -> torch.Tensor:
         buf = getattr(self, "ls_stats", None)

@@ -113,6 +113,13 @@ class TorchGLMData(GLMComputable):
         r = self.wt * dl
         return float(torch.sum(self.wt * l)), float(torch.sum(r)), self._xtv(r)
 
+    def zero_point_sums(self, loss, margin_shift):
+        """[F, S, ||c||^2, ||X||_F^2] at w = 0 (see DeviceGLMData.zero_point_sums)."""
+        l, dl = loss.loss_and_dz(self.o + margin_shift, self.y)
+        c = self.wt * dl
+        xsq = float(torch.sum(self.x.values() ** 2)) if self.n_rows else 0.0
+        return [float(torch.sum(self.wt * l)), float(torch.sum(c)), float(torch.dot(c, c)), xsq]
+
     def hv_sums(self, loss, w_eff, margin_shift, v_eff, v_shift):
         z = self._xv(w_eff) + margin_shift + self.o
         u = self._xv(v_eff) - v_shift

@@ -92,18 +92,21 @@ class _History:
                 self.rho_t.pop(0)
         return True
 
-    def push_pair(self, x, x0, g, g0):
+    def push_pair(self, x, x0, g, g0, extra: Optional[torch.Tensor] = None):
         """push(x - x0, g - g0); replicated device vectors: the pair and its scalars in ONE kernel
         (``ops.native.lbfgs_pair``) and one host synchronisation for the curvature test, which also returns
-        ||g||^2. Returns (pushed, ||g||^2 or None)."""
+        ||g||^2. ``extra``: a 0-d device scalar read in the same synchronisation (the accepted step's loss, left
+        on the device by the margin line search). Returns (pushed, ||g||^2 or None, extra as a float or None)."""
         if NATIVE_PAIR and _device_loop(g):
             from ..ops.native import lbfgs_pair
             r = lbfgs_pair(x, x0, g, g0)
             if r is not None:
                 s, y, out = r
-                sy, yy, _, _, gg = out.tolist()
+                vals = (out if extra is None else torch.cat([out, extra.reshape(1).to(out)])).tolist()
+                sy, yy, _, _, gg = vals[:5]
+                ex = vals[5] if extra is not None else None
                 if not (sy > 1e-300) or sy != sy:
-                    return False, gg
+                    return False, gg, ex
                 self.s.append(s)
                 self.y.append(y)
                 self.rho.append(1.0 / sy)
@@ -114,8 +117,8 @@ class _History:
                     self.y.pop(0)
                     self.rho.pop(0)
                     self.rho_t.pop(0)
-                return True, gg
-        return self.push(x - x0, g - g0), None
+                return True, gg, ex
+        return self.push(x - x0, g - g0), None, (None if extra is None else float(extra))
 
     def _apply_inverse_device(self, g: torch.Tensor, negate: bool = False) -> torch.Tensor:
         """Two-loop with 0-d device scalars, no synchronisation: the fused HIP step-kernel chain
@@ -324,7 +327,11 @@ class LBFGS(Optimizer):
             return state
         self._failed_once = False
         with trace_range("history push"):
-            _, gg = self.history.push_pair(x, state.coefficients, g, self._smooth_g)
+            # a device-scalar loss (margin line search) is read in the pair's synchronisation
+            f_dev = f if isinstance(f, torch.Tensor) else None
+            _, gg, f_host = self.history.push_pair(x, state.coefficients, g, self._smooth_g, extra=f_dev)
+            if f_dev is not None:
+                f = f_host
         self._smooth_f, self._smooth_g = f, g
         self._inner_iter += 1
         adj_f, adj_g = self._adjust(x, f, g)

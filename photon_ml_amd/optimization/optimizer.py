@@ -21,6 +21,9 @@ import torch
 from ..normalization.context import NormalizationContext, no_normalization
 from . import vector_space
 
+# the zero point's gradient norm (tolerance scale) as a cheap upper bound until needed: GLMObjective.zero_state_bound
+LAZY_ZERO_GRADIENT = __import__("os").environ.get("PML_LAZY_ZERO_GRADIENT", "1") != "0"
+
 
 class ConvergenceReason(str, enum.Enum):
     MAX_ITERATIONS = "max iterations reached"
@@ -119,6 +122,7 @@ class Optimizer:
         self.track_state = track_state
         self.loss_abs_tol = 0.0
         self.grad_abs_tol = 0.0
+        self._gtol_lazy = None     # (upper bound of grad_abs_tol, thunk of the exact ||g(0)||): see start()
         self.current: Optional[OptimizerState] = None
         self.previous: Optional[OptimizerState] = None
         self.tracker: Optional[OptimizationStatesTracker] = None
@@ -148,9 +152,20 @@ class Optimizer:
             return ConvergenceReason.OBJECTIVE_NOT_IMPROVING
         if prev is not None and abs(cur.loss - prev.loss) <= self.loss_abs_tol:
             return ConvergenceReason.FUNCTION_VALUES_CONVERGED
+        if self._gtol_lazy is not None:
+            if cur.grad_norm() > self._gtol_lazy[0]:
+                return None                    # above even the bound: the exact tolerance cannot be met
+            self._resolve_grad_tol()
         if cur.grad_norm() <= self.grad_abs_tol:
             return ConvergenceReason.GRADIENT_CONVERGED
         return None
+
+    def _resolve_grad_tol(self):
+        """The exact ||g(0)|| tolerance (one transpose pass at the zero point), computed the first time a
+        gradient norm falls below the bound."""
+        if self._gtol_lazy is not None:
+            self.grad_abs_tol = self._gtol_lazy[1]() * self.tolerance
+            self._gtol_lazy = None
 
     def is_done(self) -> bool:
         return self.convergence_reason() is not None
@@ -166,14 +181,27 @@ class Optimizer:
         w0 = self.normalization.model_to_transformed_space(initial.to(torch.float64))
         self.clear_inner_state()
         zero_state = None
+        self._gtol_lazy = None
+        lazy = None
         if not (skip_zero_tolerance_pass and vector_space.current().all_zero(w0)):
             # the zero point first, so the data's margin cache ends at w0 (the first line search then needs no
             # extra forward pass); tagged so a data backend can evaluate it without a pass over the non-zeros
             z = torch.zeros_like(w0)
             z._pml_zero = True
-            zero_state = self._calculate_state(objective, data, z)
+            bound = getattr(objective, "zero_state_bound", None) if LAZY_ZERO_GRADIENT else None
+            lazy = bound(data, z) if bound is not None else None
+            if lazy is None:
+                zero_state = self._calculate_state(objective, data, z)
         init_state = self._calculate_state(objective, data, w0)
-        self._set_abs_tolerances(init_state if zero_state is None else zero_state)
+        if lazy is not None:
+            # f(0) exactly (elementwise pass); ||g(0)|| only as an upper bound until a gradient norm comes close
+            # (the transpose pass at the zero point is then paid once, if ever): identical convergence decisions
+            f0, gbound, exact = lazy
+            self.loss_abs_tol = f0 * self.tolerance
+            self.grad_abs_tol = 0.0
+            self._gtol_lazy = (gbound * self.tolerance, exact)
+        else:
+            self._set_abs_tolerances(init_state if zero_state is None else zero_state)
         self._init(objective, data, init_state)
         self._update_current(init_state)
         return init_state
@@ -209,6 +237,7 @@ class Optimizer:
         def st(s: Optional[OptimizerState]):
             return None if s is None else {"coefficients": s.coefficients, "loss": s.loss, "gradient": s.gradient,
                                            "iter": s.iter}
+        self._resolve_grad_tol()
         return {"kind": type(self).__name__, "loss_abs_tol": self.loss_abs_tol, "grad_abs_tol": self.grad_abs_tol,
                 "current": st(self.current), "previous": st(self.previous), "inner": self._inner_state()}
 
@@ -216,6 +245,7 @@ class Optimizer:
         if sd["kind"] != type(self).__name__:
             raise ValueError(f"checkpoint of a {sd['kind']} cannot resume a {type(self).__name__}")
         self.clear_inner_state()
+        self._gtol_lazy = None
         self.loss_abs_tol, self.grad_abs_tol = sd["loss_abs_tol"], sd["grad_abs_tol"]
         mk = lambda d: None if d is None else OptimizerState(d["coefficients"], d["loss"], d["gradient"], d["iter"])
         self.previous, self.current = mk(sd["previous"]), mk(sd["current"])

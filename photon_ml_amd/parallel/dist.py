@@ -243,6 +243,16 @@ class DistributedGLMData:
         f, d = v.tolist()
         return f, d
 
+    def zero_point_sums(self, loss, margin_shift):
+        """[F, S, ||c||^2, ||X||_F^2] summed over the ranks (one 4-scalar all-reduce): by Cauchy-Schwarz
+        ||sum_r X_r^T c_r|| <= sqrt(sum ||X_r||_F^2) sqrt(sum ||c_r||^2), so the bound stays valid."""
+        if not hasattr(self.local, "zero_point_sums"):
+            raise AttributeError("zero_point_sums")
+        t = torch.tensor(self.local.zero_point_sums(loss, margin_shift), dtype=torch.float64,
+                         device=self._comm_device())
+        all_reduce_(t, group=self.group)
+        return t.tolist()
+
     def ls_finish_sums(self, loss, t: float, w_eff, shift, need_s: bool = True):
         if self.overlap and hasattr(self.local, "ls_finish_packed"):
             works = []

@@ -742,3 +742,24 @@ def test_rs_tron_problem_order_is_a_scheduling_hint_only():
         got = rs_tron(L, y, o, w, b0, 0, 1.0, 1e-7, 10, order=perm)
         for a, b in zip(ref, got):
             assert torch.equal(a, b), n
+
+
+@pytest.mark.parametrize("precision", ["f64", "bf16"])
+def test_zero_point_sums_bound_the_zero_gradient(precision):
+    """DeviceGLMData.zero_point_sums (one elementwise pass, no transpose): (F, S) at w = 0 as the tagged zero-point
+    evaluation, ||X||_F^2 as the host value, and the bound ||X||_F ||c|| above the exact ||g(0)||."""
+    from photon_ml_amd.function.objective import GLMObjective
+    from photon_ml_amd.ops.device import DeviceGLMData
+    data = make_data(n=6000, d=900, density=0.01)
+    if precision == "bf16":
+        data = _round_bf16(data)
+    dev = DeviceGLMData.from_labeled(data, "cuda", precision, chunk_rows=2500, layout="tiled", item_entries=5000)
+    F, S, csq, xsq = dev.zero_point_sums(LOGISTIC, 0.0)
+    z = torch.zeros(data.n_features, dtype=torch.float64, device="cuda")
+    z._pml_zero = True
+    f0, s0, g0 = dev.value_grad_sums(LOGISTIC, z, 0.0)
+    assert abs(F - f0) <= 1e-12 * abs(f0) and abs(S - s0) <= 1e-12 * max(1.0, abs(s0))
+    assert abs(xsq - float((data.x.data ** 2).sum())) <= 1e-9 * xsq
+    assert (xsq * csq) ** 0.5 >= float(torch.linalg.vector_norm(g0))
+    f, b, exact = GLMObjective(LOGISTIC, 1.0).zero_state_bound(dev, z)
+    assert f == F and b >= exact() > 0
