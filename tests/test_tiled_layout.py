@@ -120,6 +120,23 @@ def test_tl_shard_wide_transpose_emulation(chunk, item, hot):
     k_of_unit = np.bincount(it[it[:, 4] >= 0, 1])[mt.mt_tiles.numpy()[cu[:, 0]]]
     assert (cu[:, 2] - cu[:, 1] <= np.array([combine_seg(int(k)) for k in k_of_unit])).all()
     assert mt.mt_ptr.numpy()[-1] == mt.ncu
+    # re-streaming over copies of the same units (row-sampled shards) keeps every table but the stream windows
+    import copy as _copy
+    moved = []
+    for ch in chunks:
+        cc = _copy.copy(ch)
+        cc.items = ch.items.clone()
+        cc.items[:, 1] += 256          # shifted windows, as a compacted stream would have
+        cc.items[:, 2] += 256
+        moved.append(cc)
+    rt = mt.restreamed(moved)
+    rit = rt.items.numpy()
+    assert np.array_equal(rit[:, [0, 1, 4, 5, 6, 7]], it[:, [0, 1, 4, 5, 6, 7]])
+    assert np.array_equal(rit[:, 2:4], it[:, 2:4] + 256)
+    for tile_range in ((0, 1), (1, 3)):
+        bt = TLTMulti(chunks, starts, d, tile_range=tile_range)
+        bit = bt.restreamed(moved).items.numpy()
+        assert np.array_equal(bit[:, 2:4], bt.items.numpy()[:, 2:4] + 256)
 
 
 @pytest.mark.parametrize("il", [0, 1])
