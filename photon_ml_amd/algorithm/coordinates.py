@@ -158,9 +158,12 @@ class FixedEffectCoordinate(Coordinate):
         # restore full weights for scoring/evaluation
         if self.sampler is not None:
             self._restore_weights()
+        # the coefficients stay where the optimizer left them (the device): scoring reads the cached margins of
+        # this very tensor, the next update warm-starts from it without an 8-byte-per-feature host round trip and
+        # without a device comparison to re-identify it; writers / diagnostics copy to the host themselves
         return FixedEffectModel(glm.update_coefficients(
-            Coefficients(glm.coefficients.means.cpu(), None if glm.coefficients.variances is None
-                         else glm.coefficients.variances.cpu())), self.shard_id)
+            Coefficients(glm.coefficients.means.detach(), None if glm.coefficients.variances is None
+                         else glm.coefficients.variances.detach())), self.shard_id)
 
     def _row_ids(self) -> np.ndarray:
         """Global row ids of this coordinate's rows (the down-sampling hash input: rank-independent samples)."""

@@ -57,12 +57,16 @@ class NormalizationContext:
 
     # --- coefficient-space conversions (NormalizationContext.scala:64-111) ---
     def model_to_original_space(self, w: torch.Tensor) -> torch.Tensor:
+        if self.factors is None and self.shifts is None:
+            return w              # identity: the same tensor (the optimizers never write their iterates in place)
         out = w * self.factors.to(w) if self.factors is not None else w.clone()
         if self.shifts is not None:
             out[self.intercept_id] -= torch.dot(out, self.shifts.to(out))
         return out
 
     def model_to_transformed_space(self, w: torch.Tensor) -> torch.Tensor:
+        if self.factors is None and self.shifts is None:
+            return w              # identity (see model_to_original_space): cached margins recognise the tensor
         out = w.clone()
         if self.shifts is not None:
             out[self.intercept_id] += torch.dot(out, self.shifts.to(out))
