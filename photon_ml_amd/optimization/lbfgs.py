@@ -39,6 +39,9 @@ DEVICE_TWO_LOOP = os.environ.get("PML_LBFGS_DEVICE_TWO_LOOP", "1") != "0"
 # single-launch two-loop kernel was measured SLOWER than the torch recursion below: 20 grid barriers at ~25 us
 # each, 0.61 ms per direction vs ~0.2 ms; profiles/lbfgs_device_two_loop_ab.md.)
 NATIVE_PAIR = os.environ.get("PML_LBFGS_NATIVE_PAIR", "1") != "0"
+# queue the NEXT iteration's two-loop direction (with the new pair, as if accepted) before the pair's host
+# synchronisation: the GPU computes it while the host runs the curvature / convergence bookkeeping
+SPECULATE_DIRECTION = os.environ.get("PML_LBFGS_SPECULATE", "1") != "0"
 # Two-loop as 2k + 1 fused HIP step kernels launched from C++ (no Python between launches); 0: torch recursion
 NATIVE_TWO_LOOP = os.environ.get("PML_LBFGS_NATIVE_TWO_LOOP", "1") != "0"
 # Device two-loop method for replicated vectors: "gram" = vector-free recursion on the device (one Gram pass, the
@@ -92,21 +95,31 @@ class _History:
                 self.rho_t.pop(0)
         return True
 
-    def push_pair(self, x, x0, g, g0, extra: Optional[torch.Tensor] = None):
+    def _with_pair(self, s, y, rho_t, gamma_t) -> "_History":
+        """A copy of this history with one more (device) pair, for a speculative direction."""
+        h = _History(self.m)
+        h.s, h.y, h.rho_t = (self.s + [s])[-self.m:], (self.y + [y])[-self.m:], (self.rho_t + [rho_t])[-self.m:]
+        h.rho, h.gamma_t = [0.0] * len(h.s), gamma_t
+        return h
+
+    def push_pair(self, x, x0, g, g0, extra: Optional[torch.Tensor] = None, speculate=None):
         """push(x - x0, g - g0); replicated device vectors: the pair and its scalars in ONE kernel
         (``ops.native.lbfgs_pair``) and one host synchronisation for the curvature test, which also returns
         ||g||^2. ``extra``: a 0-d device scalar read in the same synchronisation (the accepted step's loss, left
-        on the device by the margin line search). Returns (pushed, ||g||^2 or None, extra as a float or None)."""
+        on the device by the margin line search). ``speculate(history_with_pair)``: queued before the
+        synchronisation; its result is returned only if the pair is accepted. Returns (pushed, ||g||^2 or None,
+        extra as a float or None, speculation or None)."""
         if NATIVE_PAIR and _device_loop(g):
             from ..ops.native import lbfgs_pair
             r = lbfgs_pair(x, x0, g, g0)
             if r is not None:
                 s, y, out = r
+                spec = speculate(self._with_pair(s, y, out[2], out[3])) if speculate is not None else None
                 vals = (out if extra is None else torch.cat([out, extra.reshape(1).to(out)])).tolist()
                 sy, yy, _, _, gg = vals[:5]
                 ex = vals[5] if extra is not None else None
                 if not (sy > 1e-300) or sy != sy:
-                    return False, gg, ex
+                    return False, gg, ex, None
                 self.s.append(s)
                 self.y.append(y)
                 self.rho.append(1.0 / sy)
@@ -117,8 +130,8 @@ class _History:
                     self.y.pop(0)
                     self.rho.pop(0)
                     self.rho_t.pop(0)
-                return True, gg, ex
-        return self.push(x - x0, g - g0), None, (None if extra is None else float(extra))
+                return True, gg, ex, spec
+        return self.push(x - x0, g - g0), None, (None if extra is None else float(extra)), None
 
     def _apply_inverse_device(self, g: torch.Tensor, negate: bool = False) -> torch.Tensor:
         """Two-loop with 0-d device scalars, no synchronisation: the fused HIP step-kernel chain
@@ -210,6 +223,7 @@ class LBFGS(Optimizer):
         # smooth (un-penalised) value/gradient at the current point, used for the history
         self._smooth_f = None
         self._smooth_g = None
+        self._spec = None        # (x, g, direction, prefetch) queued for the next iteration (push_pair)
 
     def clear_inner_state(self):
         super().clear_inner_state()
@@ -217,6 +231,7 @@ class LBFGS(Optimizer):
         self._failed_once = False
         self._finished = False
         self._inner_iter = 0
+        self._spec = None
 
     def _inner_state(self) -> dict:
         h = self.history
@@ -254,7 +269,10 @@ class LBFGS(Optimizer):
         of the margin line search would otherwise each synchronise); None elsewhere."""
         if not _device_loop(d):
             return None
-        x0, g = state.coefficients, state.gradient
+        return self._prefetch_of(state.coefficients, state.gradient, d)
+
+    @staticmethod
+    def _prefetch_of(x0: torch.Tensor, g: torch.Tensor, d: torch.Tensor) -> torch.Tensor:
         return torch.stack([torch.dot(g, d), torch.dot(d, d), torch.dot(x0, x0), torch.dot(x0, d)])
 
     def _search(self, objective, data, state: OptimizerState, d: torch.Tensor, pre=None):
@@ -305,10 +323,14 @@ class LBFGS(Optimizer):
         if self._finished:
             return state
         from ..utils.timing import trace_range
+        spec, self._spec = self._spec, None
         try:
             with trace_range("two-loop direction"):
-                d = self._direction(state)
-                pre = self._prefetch(state, d)
+                if spec is not None and spec[0] is state.coefficients and spec[1] is state.gradient:
+                    d, pre = spec[2], spec[3]             # queued during the last history push
+                else:
+                    d = self._direction(state)
+                    pre = self._prefetch(state, d)
                 # device: d.d > 0 decides later, in _search (d.d == 0 -- all zero or underflow -- checks exactly)
                 nonzero = pre is not None or vector_space.current().any_nonzero(d)
             if not nonzero:
@@ -329,9 +351,17 @@ class LBFGS(Optimizer):
         with trace_range("history push"):
             # a device-scalar loss (margin line search) is read in the pair's synchronisation
             f_dev = f if isinstance(f, torch.Tensor) else None
-            _, gg, f_host = self.history.push_pair(x, state.coefficients, g, self._smooth_g, extra=f_dev)
+            spec_fn = None
+            if (SPECULATE_DIRECTION and type(self)._direction is LBFGS._direction and not self.constraints
+                    and _device_loop(g)):
+                # plain L-BFGS: the next state is (x, g) as is (no L1 adjustment, no box projection)
+                spec_fn = lambda h: (lambda dn: (dn, self._prefetch_of(x, g, dn)))(h.apply_inverse(g, negate=True))
+            _, gg, f_host, nxt = self.history.push_pair(x, state.coefficients, g, self._smooth_g, extra=f_dev,
+                                                        speculate=spec_fn)
             if f_dev is not None:
                 f = f_host
+            if nxt is not None:
+                self._spec = (x, g, nxt[0], nxt[1])
         self._smooth_f, self._smooth_g = f, g
         self._inner_iter += 1
         adj_f, adj_g = self._adjust(x, f, g)
