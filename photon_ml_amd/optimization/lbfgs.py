@@ -114,7 +114,9 @@ class _History:
             r = lbfgs_pair(x, x0, g, g0)
             if r is not None:
                 s, y, out = r
-                spec = speculate(self._with_pair(s, y, out[2], out[3])) if speculate is not None else None
+                # the speculative history has device scalars only: it must take the device two-loop
+                spec = (speculate(self._with_pair(s, y, out[2], out[3]))
+                        if speculate is not None and len(self.rho_t) == len(self.s) else None)
                 vals = (out if extra is None else torch.cat([out, extra.reshape(1).to(out)])).tolist()
                 sy, yy, _, _, gg = vals[:5]
                 ex = vals[5] if extra is not None else None
@@ -353,7 +355,7 @@ class LBFGS(Optimizer):
             f_dev = f if isinstance(f, torch.Tensor) else None
             spec_fn = None
             if (SPECULATE_DIRECTION and type(self)._direction is LBFGS._direction and not self.constraints
-                    and _device_loop(g)):
+                    and _device_loop(g) and g.numel() < GRAM_MIN_DIM and not vector_space.current().sharded):
                 # plain L-BFGS: the next state is (x, g) as is (no L1 adjustment, no box projection)
                 spec_fn = lambda h: (lambda dn: (dn, self._prefetch_of(x, g, dn)))(h.apply_inverse(g, negate=True))
             _, gg, f_host, nxt = self.history.push_pair(x, state.coefficients, g, self._smooth_g, extra=f_dev,
