@@ -1056,86 +1056,6 @@ __device__ __forceinline__ void tl_stream_narrow(const uint16_t* __restrict__ np
   if (abl & 1) atomicAdd(&acc[lane], regsum);
 }
 
-// WINDOW rounds (ops/tiled.py ``split_window``): full wide rounds whose 256 sorted keys span fewer than 64 * NL
-// values, moved to the front of their unit's wide section (class A: NL = 4, span < 256; class B: NL = 8, span <
-// 512 — the moderately hot columns of the forward copy, the moderately dense rows of the transpose copy: ~40 % of
-// the wide rounds at the bench shape). The round's key window x[base, base + 64 NL) (base = its smallest key =
-// logical entry 0 = lane 0's first quad element, read with v_readlane: wave-uniform, no extra stream) is read with
-// NL coalesced 64-lane loads and parked in a wave-private LDS window; each entry then reads its value from LDS.
-// Texture-address cost per round (model of profiles/pmc_tl_multi_125M_r3.md): NL x 16 cycles instead of 4 x 64 for
-// the four divergent gathers of a wide round. Same 32-bit packs and value streams as the wide rounds; the builder
-// guarantees base + 64 NL <= len(x). Ring pipeline under the code-generation rules of tl_stream_ring; the window
-// loads of round r are issued BEFORE the stream loads of round r + S, so waiting for the window (vmcnt counts in
-// issue order) leaves the stream prefetch in flight. Fixed entry order per wave: deterministic.
-template <typename VT, typename XT, typename AT, bool SQ, int NW, int S, int NL>
-__device__ __forceinline__ void tl_stream_win(const uint32_t* __restrict__ pack, const VT* __restrict__ val,
-                                              const XT* __restrict__ x, int e_lo, int e_hi, int sbits, AT* acc,
-                                              XT* win) {
-  constexpr int R = S + 1;
-  constexpr uint32_t WMASK = 64u * NL - 1u;
-  typedef typename TLValT<VT>::T LT;
-  typedef typename TLVals<VT>::Raw Raw;
-  const int lane = threadIdx.x & 63;
-  const int w = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
-  const uint32_t smask = (1u << sbits) - 1u;
-  const int nr = (e_hi - e_lo + TL_ROUND - 1) / TL_ROUND;
-  const int r0 = (nr * w) / NW, r1 = (nr * (w + 1)) / NW;
-  if (r0 >= r1) return;
-  v4u pk[R];
-  Raw vr[R];
-  auto load_round = [&](int r, v4u& p, Raw& v) {
-    const int e = e_lo + min(r, r1 - 1) * TL_ROUND + lane * TL_VEC;   // clamped re-read past the end
-    p = ldg_nt((const v4u*)(pack + e));
-    v = TLVals<VT>::load(val + e);
-  };
-#pragma unroll
-  for (int i = 0; i < S; ++i) {
-    load_round(r0 + i, pk[i], vr[i]);
-    __builtin_amdgcn_sched_barrier(0);
-  }
-  for (int r = r0; r < r1; r += R) {
-#pragma unroll
-    for (int i = 0; i < R; ++i) {
-      const int rc = r + i;
-      const uint32_t base = (uint32_t)__builtin_amdgcn_readlane((int)pk[i][0], 0) >> sbits;
-      XT xw[NL];
-#pragma unroll
-      for (int q = 0; q < NL; ++q) xw[q] = ldg(x + base + 64 * q + lane);
-      __builtin_amdgcn_sched_barrier(0);
-      load_round(rc + S, pk[(i + S) % R], vr[(i + S) % R]);          // slot of round rc - 1 (consumed)
-      __builtin_amdgcn_sched_barrier(0);
-#pragma unroll
-      for (int q = 0; q < NL; ++q) win[64 * q + lane] = xw[q];
-      LT v[TL_VEC];
-      TLVals<VT>::get(vr[i], v);
-      const int e = e_lo + rc * TL_ROUND + lane;
-#pragma unroll
-      for (int k = 0; k < TL_VEC; ++k) {
-        const bool in = (e + 64 * k < e_hi) && (rc < r1);
-        const XT xv = win[in ? (((pk[i][k] >> sbits) - base) & WMASK) : 0u];
-        const AT vv = SQ ? static_cast<AT>(v[k]) * static_cast<AT>(v[k]) : static_cast<AT>(v[k]);
-        const AT add = in ? vv * static_cast<AT>(xv) : AT(0);         // select: no NaN from x
-        atomicAdd(&acc[in ? (pk[i][k] & smask) : 0u], add);
-      }
-      __builtin_amdgcn_sched_barrier(0);
-    }
-  }
-}
-#define TL_WIN_MAX 512          // largest window (class B) per wave, elements of x
-
-// Window rounds of one unit: ``med`` = nA | nB << 16 full rounds of classes A and B at the front of [e_lo, e_hi);
-// returns the start of the remaining (wide) rounds.
-template <typename VT, typename XT, typename AT, bool SQ, int NW>
-__device__ __forceinline__ int tl_stream_windows(int med, const uint32_t* __restrict__ pack,
-                                                 const VT* __restrict__ val, const XT* __restrict__ x, int e_lo,
-                                                 int sbits, AT* acc, XT* win) {
-  const int nA = med & 0xffff, nB = (int)((unsigned)med >> 16);
-  if (nA) tl_stream_win<VT, XT, AT, SQ, NW, 2, 4>(pack, val, x, e_lo, e_lo + TL_ROUND * nA, sbits, acc, win);
-  e_lo += TL_ROUND * nA;
-  if (nB) tl_stream_win<VT, XT, AT, SQ, NW, 2, 8>(pack, val, x, e_lo, e_lo + TL_ROUND * nB, sbits, acc, win);
-  return e_lo + TL_ROUND * nB;
-}
-
 // pipeline variant: P = 0 two-slot stream prefetch; P = 1 three-stage (stream r+2 / gather r+1 / accumulate r);
 // P = 2 two-slot, 8 entries per lane; P = 3 lane-interleaved layout (tl_stream_il)
 template <typename VT, typename XT, typename AT, bool SQ, int U, int NW, int P>
@@ -1150,17 +1070,15 @@ __device__ __forceinline__ void tl_stream(const uint32_t* __restrict__ pack, con
 }
 
 // Narrow-section streams of one chunk (see tl_stream_narrow); n_lo == n_hi: the unit has no narrow rounds.
-// med: optional per-unit window-round counts (nA | nB << 16, see tl_stream_windows), indexed like the unit table.
-struct TLNarrow { const uint16_t* pack; const void* val; const int* base; const int* med; };
+struct TLNarrow { const uint16_t* pack; const void* val; const int* base; };
 
 // Forward over row blocks. blk: 6 ints per block {row_lo, nrows, e_lo, e_hi, n_lo, n_hi} (chunk-local).
 template <typename VT, typename XT, typename RT, typename AT, int MAXR, int U, int NW, int P>
 __device__ __forceinline__ void tl_fwd_block(int b, int row_lo, int nrows, int e_lo, int e_hi, int n_lo, int n_hi,
                                              int rbits, const uint32_t* __restrict__ pack,
-                                             const VT* __restrict__ val, const TLNarrow& nar, int med,
+                                             const VT* __restrict__ val, const TLNarrow& nar,
                                              const XT* __restrict__ x, const FwdArgs<XT, RT>& a,
-                                             double* __restrict__ stats, AT (*acc)[MAXR], double* red,
-                                             XT (*win)[TL_WIN_MAX]) {
+                                             double* __restrict__ stats, AT (*acc)[MAXR], double* red) {
   const int R = 1 << rbits;
   for (int i = threadIdx.x; i < R; i += NW * 64)
 #pragma unroll
@@ -1170,8 +1088,6 @@ __device__ __forceinline__ void tl_fwd_block(int b, int row_lo, int nrows, int e
     tl_stream_narrow<VT, XT, AT, false, NW, (P >= 5 ? 4 : 2)>(nar.pack, (const VT*)nar.val, nar.base, n_lo, n_hi,
                                                               rbits, x,
                                             acc[threadIdx.x >> 6]);
-  if (med) e_lo = tl_stream_windows<VT, XT, AT, false, NW>(med, pack, val, x, e_lo, rbits, acc[threadIdx.x >> 6],
-                                                           win[threadIdx.x >> 6]);
   tl_stream<VT, XT, AT, false, U, NW, P>(pack, val, x, e_lo, e_hi, rbits, acc[threadIdx.x >> 6]);
   __syncthreads();
   double F = 0.0, S = 0.0;
@@ -1197,12 +1113,11 @@ __global__ __launch_bounds__(NW * 64) void tl_fwd_kernel(const int* __restrict__
                                                           const unsigned char* __restrict__ live) {
   __shared__ AT acc[NW][MAXR];
   __shared__ double red[2 * NW];
-  __shared__ XT win[NW][TL_WIN_MAX];
   const int b = blockIdx.x;
   if (live && !live[b]) return;
   const int* q = blk + 6 * b;
-  tl_fwd_block<VT, XT, RT, AT, MAXR, U, NW, P>(b, q[0], q[1], q[2], q[3], q[4], q[5], rbits, pack, val, nar,
-                                              nar.med ? nar.med[b] : 0, x, a, stats, acc, red, win);
+  tl_fwd_block<VT, XT, RT, AT, MAXR, U, NW, P>(b, q[0], q[1], q[2], q[3], q[4], q[5], rbits, pack, val, nar, x, a,
+                                              stats, acc, red);
 }
 
 // All chunks of a shard in ONE launch (no per-chunk tails / launch gaps): block table of 8 ints
@@ -1214,19 +1129,16 @@ __global__ __launch_bounds__(NW * 64) void tl_fwd_multi_kernel(const int* __rest
                                                                 const unsigned long long* __restrict__ ptrs,
                                                                 const XT* __restrict__ x, FwdArgs<XT, RT> a,
                                                                 double* __restrict__ stats,
-                                                                const unsigned char* __restrict__ live,
-                                                                const int* __restrict__ med) {
+                                                                const unsigned char* __restrict__ live) {
   __shared__ AT acc[NW][MAXR];
   __shared__ double red[2 * NW];
-  __shared__ XT win[NW][TL_WIN_MAX];
   const int b = blockIdx.x;
   if (live && !live[b]) return;
   const int* q = blk + 8 * b;
   const unsigned long long* pc = ptrs + 5 * q[0];
-  const TLNarrow nar = {(const uint16_t*)pc[2], (const void*)pc[3], (const int*)pc[4], nullptr};
+  const TLNarrow nar = {(const uint16_t*)pc[2], (const void*)pc[3], (const int*)pc[4]};
   tl_fwd_block<VT, XT, RT, AT, MAXR, U, NW, P>(b, q[1], q[2], q[3], q[4], q[6], q[7], rbits, (const uint32_t*)pc[0],
-                                              (const VT*)pc[1], nar, med ? med[b] : 0, x + q[5], a, stats, acc, red,
-                                              win);
+                                              (const VT*)pc[1], nar, x + q[5], a, stats, acc, red);
 }
 
 // Transpose over column-tile items. items: 4 ints {tile, e_lo, e_hi, part}; part < 0: the item is its tile's
@@ -1234,9 +1146,8 @@ __global__ __launch_bounds__(NW * 64) void tl_fwd_multi_kernel(const int* __rest
 template <typename VT, typename XT, typename AT, bool SQ, int MAXR, int U, int NW, int P>
 __device__ __forceinline__ void tl_t_item(int tile, int e_lo, int e_hi, int part, int n_lo, int n_hi, int cbits,
                                           const uint32_t* __restrict__ pack, const VT* __restrict__ val,
-                                          const TLNarrow& nar, int med, const XT* __restrict__ x,
-                                          double* __restrict__ G, int dim, double* __restrict__ parts,
-                                          AT (*acc)[MAXR], XT (*win)[TL_WIN_MAX]) {
+                                          const TLNarrow& nar, const XT* __restrict__ x, double* __restrict__ G,
+                                          int dim, double* __restrict__ parts, AT (*acc)[MAXR]) {
   const int C = 1 << cbits;
   for (int i = threadIdx.x; i < C; i += NW * 64)
 #pragma unroll
@@ -1246,8 +1157,6 @@ __device__ __forceinline__ void tl_t_item(int tile, int e_lo, int e_hi, int part
     tl_stream_narrow<VT, XT, AT, SQ, NW, (P >= 5 ? 4 : 2)>(nar.pack, (const VT*)nar.val, nar.base, n_lo, n_hi,
                                                            cbits, x,
                                          acc[threadIdx.x >> 6]);
-  if (med) e_lo = tl_stream_windows<VT, XT, AT, SQ, NW>(med, pack, val, x, e_lo, cbits, acc[threadIdx.x >> 6],
-                                                        win[threadIdx.x >> 6]);
   tl_stream<VT, XT, AT, SQ, U, NW, P>(pack, val, x, e_lo, e_hi, cbits, acc[threadIdx.x >> 6]);
   __syncthreads();
   const int c0 = tile << cbits;
@@ -1271,11 +1180,10 @@ __global__ __launch_bounds__(NW * 64) void tl_t_kernel(const int* __restrict__ i
                                                         double* __restrict__ parts,
                                                         const unsigned char* __restrict__ live) {
   __shared__ AT acc[NW][MAXR];
-  __shared__ XT win[NW][TL_WIN_MAX];
   if (live && !live[blockIdx.x]) return;
   const int* q = items + 6 * blockIdx.x;
-  tl_t_item<VT, XT, AT, SQ, MAXR, U, NW, P>(q[0], q[1], q[2], q[3], q[4], q[5], cbits, pack, val, nar,
-                                            nar.med ? nar.med[blockIdx.x] : 0, x, G, dim, parts, acc, win);
+  tl_t_item<VT, XT, AT, SQ, MAXR, U, NW, P>(q[0], q[1], q[2], q[3], q[4], q[5], cbits, pack, val, nar, x, G, dim,
+                                            parts, acc);
 }
 
 // All row chunks of a shard in one launch. items: 8 ints {chunk, tile, e_lo, e_hi, part, row_base, n_lo, n_hi};
@@ -1287,17 +1195,14 @@ __global__ __launch_bounds__(NW * 64) void tl_t_multi_kernel(const int* __restri
                                                               const unsigned long long* __restrict__ ptrs,
                                                               const XT* __restrict__ x, double* __restrict__ G,
                                                               int dim, double* __restrict__ parts,
-                                                              const unsigned char* __restrict__ live,
-                                                              const int* __restrict__ med) {
+                                                              const unsigned char* __restrict__ live) {
   __shared__ AT acc[NW][MAXR];
-  __shared__ XT win[NW][TL_WIN_MAX];
   if (live && !live[blockIdx.x]) return;
   const int* q = items + 8 * blockIdx.x;
   const unsigned long long* pc = ptrs + 5 * q[0];
-  const TLNarrow nar = {(const uint16_t*)pc[2], (const void*)pc[3], (const int*)pc[4], nullptr};
+  const TLNarrow nar = {(const uint16_t*)pc[2], (const void*)pc[3], (const int*)pc[4]};
   tl_t_item<VT, XT, AT, SQ, MAXR, U, NW, P>(q[1], q[2], q[3], q[4], q[6], q[7], cbits, (const uint32_t*)pc[0],
-                                            (const VT*)pc[1], nar, med ? med[blockIdx.x] : 0, x + q[5], G, dim,
-                                            parts, acc, win);
+                                            (const VT*)pc[1], nar, x + q[5], G, dim, parts, acc);
 }
 
 // Combine the partial rows of split tiles, deterministically, in two levels (a hot tile can have hundreds of
@@ -1369,7 +1274,7 @@ struct TLFwdDesc { const int* blk; int nblk; int rbits; const uint32_t* pack; co
                   const unsigned char* live; };
 // ptrs: 5 stream pointers per chunk (see tl_fwd_multi_kernel)
 struct TLFwdMultiDesc { const int* blk; int nblk; int rbits; const unsigned long long* ptrs; int il;
-                       const unsigned char* live; const int* med; };
+                       const unsigned char* live; };
 struct TLTDesc {
   const int* items; int nitems; int cbits; const uint32_t* pack; const void* val;
   const int* mt_tiles; const int* mt_ptr; int nmt; int dim;
@@ -1387,7 +1292,6 @@ struct TLTMultiDesc {
   const int* cu; int ncu; int nparts_total; int il;
   const unsigned char* live;
   const unsigned char* live_mt;
-  const int* med;             // optional per-item window-round counts (see tl_stream_windows)
 };
 
 // Runtime TL configuration: accumulator precision for bf16/f32 data (0 = fp32 LDS, 1 = fp64 LDS) and the number
@@ -1427,7 +1331,7 @@ static void tl_fwd_multi_launch(const TLFwdMultiDesc* c, const void* x, FwdArgs<
                                 hipStream_t st) {
 #define TLM(NW, P) hipLaunchKernelGGL((tl_fwd_multi_kernel<VT, XT, RT, AT, MAXR, 2, NW, P>), dim3(c->nblk), \
                                       dim3(NW * 64), 0, st, c->blk, c->rbits, c->ptrs, (const XT*)x, a, stats, \
-                                      c->live, c->med)
+                                      c->live)
   if (c->il) {
     if (g_tl_deep == 2) { if (g_tl_waves == 2) TLM(2, 6); else TLM(4, 6); }
     else if (g_tl_deep) { if (g_tl_waves == 2) TLM(2, 5); else TLM(4, 5); }
@@ -1523,7 +1427,7 @@ template <typename VT, typename XT, typename AT, bool SQ, int MAXR>
 static void tl_t_multi_launch(const TLTMultiDesc* c, const void* x, double* G, double* parts, hipStream_t st) {
 #define TLTM(NW, P) hipLaunchKernelGGL((tl_t_multi_kernel<VT, XT, AT, SQ, MAXR, 2, NW, P>), dim3(c->nitems), \
                                        dim3(NW * 64), 0, st, c->items, c->cbits, c->ptrs, (const XT*)x, G, \
-                                       c->dim, parts, c->live, c->med)
+                                       c->dim, parts, c->live)
   if (c->il) {
     if (g_tl_waves_t == 2) { if (g_tl_deep_t == 2) TLTM(2, 6); else if (g_tl_deep_t) TLTM(2, 5); else TLTM(2, 3); }
     else { if (g_tl_deep_t == 2) TLTM(4, 6); else if (g_tl_deep_t) TLTM(4, 5); else TLTM(4, 3); }

@@ -287,37 +287,6 @@ class DeviceGLMData(GLMComputable):
                 raise ValueError(f"chunk {c}: {what} narrow stream shorter than its rounds")
             if int(base.min()) < 0 or int(base.max()) + 64 > xlen:
                 raise ValueError(f"chunk {c}: {what} narrow key window outside the gathered vector")
-        DeviceGLMData._validate_windows(c, ch, table, xlen, what)
-
-    @staticmethod
-    def _validate_windows(c: int, ch, table: torch.Tensor, xlen: int, what: str):
-        """Window rounds (tiled.split_window): the first nA + nB rounds of every unit's wide window are whole rounds
-        inside it, and every key of a class-A / B round lies in [base, base + 256 / 512) with base = the round's
-        first key (lane 0's first entry, what the kernel reads) and base + 256 / 512 <= len(x)."""
-        med = getattr(ch, "med", None)
-        if med is None or table.shape[0] == 0:
-            return
-        from .tiled import IL_ROUND, WIN_A, WIN_B
-        md = med.cpu().to(torch.int64)
-        if md.numel() != table.shape[0]:
-            raise ValueError(f"chunk {c}: {what} window counts do not match the unit table")
-        nA, nB = md & 0xFFFF, md >> 16
-        lo, hi = ch._ew
-        e_lo, e_hi = table[:, lo], table[:, hi]
-        if bool((e_lo + IL_ROUND * (nA + nB) > e_hi).any()):
-            raise ValueError(f"chunk {c}: {what} window rounds beyond the unit's wide window")
-        n = nA + nB
-        if int(n.sum()) == 0:
-            return
-        u = torch.repeat_interleave(torch.arange(len(n)), n)
-        j = torch.arange(int(n.sum())) - (torch.cumsum(n, 0) - n)[u]
-        start = e_lo[u] + IL_ROUND * j
-        win = torch.where(j < nA[u], WIN_A, WIN_B)
-        keys = (ch.pack.cpu().to(torch.int64) & 0xFFFFFFFF)[start[:, None] + torch.arange(IL_ROUND)] >> ch._sbits
-        base = keys[:, 0]
-        if (bool((keys < base[:, None]).any()) or bool((keys - base[:, None] >= win[:, None]).any())
-                or bool((base + win > xlen).any())):
-            raise ValueError(f"chunk {c}: {what} window round keys outside their window")
 
     # ------------------------------------------------------------------
     @staticmethod
@@ -782,15 +751,8 @@ class DeviceGLMData(GLMComputable):
         from .native import TLFwdMultiDesc
         if len({ch.il for ch in self.csr}) != 1:
             return
-        # per-block window-round counts (tiled.split_window), global block order; None if no chunk has any
-        self._multi_med = None
-        if any(getattr(ch, "med", None) is not None for ch in self.csr):
-            self._multi_med = torch.cat([ch.med if getattr(ch, "med", None) is not None else
-                                         torch.zeros(ch.nblk, dtype=torch.int32, device=self.device)
-                                         for ch in self.csr]).contiguous()
         self._multi = TLFwdMultiDesc(self._multi_blk.data_ptr(), self._multi_blk.shape[0], self.csr[0].rbits,
-                                     self._multi_ptrs.data_ptr(), self.csr[0].il, None,
-                                     None if self._multi_med is None else self._multi_med.data_ptr())
+                                     self._multi_ptrs.data_ptr(), self.csr[0].il)
 
     def _build_multi_t(self):
         """One-launch transpose over all chunks. Column-window chunks (block-diagonal random-effect problems) take

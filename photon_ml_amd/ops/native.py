@@ -32,9 +32,8 @@ class SegChunkDesc(ctypes.Structure):
 
 
 class TLNarrow(ctypes.Structure):
-    """Narrow-section streams of one chunk (16-bit packs, values, one int32 base per round) and the optional
-    per-unit window-round counts ``med`` (nA | nB << 16, ``tiled.split_window``)."""
-    _fields_ = [("pack", c_void_p), ("val", c_void_p), ("base", c_void_p), ("med", c_void_p)]
+    """Narrow-section streams of one chunk (16-bit packs, values, one int32 base per round)."""
+    _fields_ = [("pack", c_void_p), ("val", c_void_p), ("base", c_void_p)]
 
 
 class TLFwdDesc(ctypes.Structure):
@@ -45,14 +44,13 @@ class TLFwdDesc(ctypes.Structure):
 class TLFwdMultiDesc(ctypes.Structure):
     """``ptrs``: 5 stream pointers per chunk {pack, val, narrow pack, narrow val, narrow base}."""
     _fields_ = [("blk", c_void_p), ("nblk", c_int), ("rbits", c_int), ("ptrs", c_void_p), ("il", c_int),
-                ("live", c_void_p), ("med", c_void_p)]
+                ("live", c_void_p)]
 
 
 class TLTMultiDesc(ctypes.Structure):
     _fields_ = [("items", c_void_p), ("nitems", c_int), ("cbits", c_int), ("ptrs", c_void_p),
                 ("mt_tiles", c_void_p), ("mt_ptr", c_void_p), ("nmt", c_int), ("dim", c_int), ("cu", c_void_p),
-                ("ncu", c_int), ("nparts_total", c_int), ("il", c_int), ("live", c_void_p), ("live_mt", c_void_p),
-                ("med", c_void_p)]
+                ("ncu", c_int), ("nparts_total", c_int), ("il", c_int), ("live", c_void_p), ("live_mt", c_void_p)]
 
 
 class CmpArgs(ctypes.Structure):

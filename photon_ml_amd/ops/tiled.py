@@ -197,49 +197,6 @@ def split_narrow(pack: torch.Tensor, val: torch.Tensor, n: torch.Tensor, sbits: 
 
 
 
-WINDOW = int(os.environ.get("PML_TL_WINDOW", "1"))
-WIN_A, WIN_B = 256, 512  # key spans of the two window-round classes (4 / 8 coalesced 64-lane loads per round)
-
-
-def split_window(pack: torch.Tensor, val: torch.Tensor, n: torch.Tensor, sbits: int, xlen: int,
-                 enable: bool = True):
-    """WINDOW ROUNDS (``tl_stream_win`` in ``glm_kernels.hip``): reorder the full rounds of every unit's wide
-    entries so that rounds whose 256 keys span fewer than ``WIN_A`` values come first (class A), then those
-    spanning fewer than ``WIN_B`` (class B), then the rest; a unit's partial last round stays last. The kernel reads
-    a class-A / B round's key window ``x[base, base + WIN)`` (base = the round's first key) with 4 / 8 coalesced
-    loads instead of four divergent gathers. Rounds move whole (the entries of a round and their order are kept),
-    so the layout stays a valid sorted-per-round stream.
-
-    ``pack`` (int64, ``key << sbits | slot``) / ``val`` hold units of ``n[u]`` consecutive entries, sorted by key.
-    Returns ``(pack, val, med)`` with ``med`` = int32 ``nA | nB << 16`` per unit, or None when no unit has a
-    window round."""
-    dev = pack.device
-    n = n.to(torch.int64)
-    U = n.numel()
-    g = n // IL_ROUND
-    G = int(g.sum())
-    if not (enable and WINDOW and G > 0 and xlen >= WIN_A) or int(g.max()) >= (1 << 16):
-        return pack, val, None
-    starts = torch.cumsum(n, 0) - n
-    gu = torch.repeat_interleave(torch.arange(U, device=dev), g, output_size=G)
-    gs = starts[gu] + IL_ROUND * (torch.arange(G, device=dev) - (torch.cumsum(g, 0) - g)[gu])
-    key = pack >> sbits
-    first, span = key[gs], key[gs + IL_ROUND - 1] - key[gs]
-    cls = torch.full((G,), 2, dtype=torch.int64, device=dev)
-    cls[(span < WIN_B) & (first + WIN_B <= xlen)] = 1
-    cls[(span < WIN_A) & (first + WIN_A <= xlen)] = 0
-    nA = torch.bincount(gu[cls == 0], minlength=U)
-    nB = torch.bincount(gu[cls == 1], minlength=U)
-    if int(nA.sum() + nB.sum()) == 0:
-        return pack, val, None
-    order = torch.sort(gu * 3 + cls, stable=True).indices     # rounds grouped by unit, classes A, B, rest
-    perm = torch.arange(pack.numel(), device=dev)
-    t = torch.arange(IL_ROUND, device=dev)
-    perm[(gs[:, None] + t).reshape(-1)] = (gs[order][:, None] + t).reshape(-1)
-    med = (nA | (nB << 16)).to(torch.int32).contiguous()
-    return pack[perm], val[perm], med
-
-
 def narrow_logical(npack: torch.Tensor, nval: torch.Tensor, nbase: torch.Tensor, r_lo, r_hi, sbits: int):
     """(pack32 as int64, val) of narrow rounds [r_lo, r_hi) in logical order."""
     r = torch.arange(int(r_lo), int(r_hi), device=npack.device)
@@ -256,13 +213,10 @@ class _NarrowMixin:
     """Narrow-section bookkeeping shared by the forward and transpose chunks (``table`` columns 4, 5 hold the
     per-unit narrow round range [n_lo, n_hi); the wide window is columns ``_ew``)."""
 
-    def _set_narrow(self, npack, nval, nbase, med: Optional[torch.Tensor] = None):
-        """``med``: per-unit window-round counts (``split_window``); None = no window rounds (e.g. row-sampled
-        copies, whose filtered wide rounds no longer have the spans they were classified by)."""
+    def _set_narrow(self, npack, nval, nbase):
         from .native import TLNarrow
-        self.npack, self.nval, self.nbase, self.med = npack, nval, nbase, med
-        self.nar = TLNarrow(npack.data_ptr(), nval.data_ptr(), nbase.data_ptr(),
-                            None if med is None else med.data_ptr())
+        self.npack, self.nval, self.nbase = npack, nval, nbase
+        self.nar = TLNarrow(npack.data_ptr(), nval.data_ptr(), nbase.data_ptr())
 
     @property
     def n_narrow_rounds(self) -> int:
@@ -332,7 +286,6 @@ class TLFwdChunk(_NarrowMixin):
         if self.il:
             wp, wv, wn, npk, nvl, nbs, nr = split_narrow(key & 0xFFFFFFFF, val[perm], e_hi - e_lo, self.rbits, dim)
             del key, perm
-            wp, wv, med = split_window(wp, wv, wn, self.rbits, dim)
             self.pack, self.val, e_lo = _interleave(_to_u32_bits(wp), wv, wn)
             e_hi = e_lo + wn
             n_hi = torch.cumsum(nr, 0)
@@ -342,10 +295,9 @@ class TLFwdChunk(_NarrowMixin):
             self.pack = _pad(_to_u32_bits(key & 0xFFFFFFFF))
             self.val = _pad(val[perm].contiguous())
             npk, nvl, nbs = _empty_narrow(val)
-            med = None
             del key, perm
         del rows
-        self._set_narrow(npk, nvl, nbs, med)
+        self._set_narrow(npk, nvl, nbs)
         self.blk = torch.stack([lo, hi - lo, e_lo, e_hi, n_lo, n_hi], 1).to(torch.int32).contiguous()
         self.nblk, self.m, self.nnz = nblk, m, nnz
         self.desc = TLFwdDesc(self.blk.data_ptr(), nblk, self.rbits, self.pack.data_ptr(), self.val.data_ptr(),
@@ -446,7 +398,6 @@ class TLTChunk(_NarrowMixin):
             cnt = torch.from_numpy(items[:, 2] - items[:, 1]).to(dev)
             wp, wv, wn, npk, nvl, nbs, nr = split_narrow(pack.to(torch.int64) & 0xFFFFFFFF, val, cnt, self.cbits, m)
             del pack, val
-            wp, wv, med = split_window(wp, wv, wn, self.cbits, m)
             self.pack, self.val, new_lo = _interleave(_to_u32_bits(wp), wv, wn)
             del wp, wv
             items[:, 1] = new_lo.cpu().numpy()
@@ -457,9 +408,8 @@ class TLTChunk(_NarrowMixin):
         else:
             self.pack, self.val = _pad(pack), _pad(val.contiguous())
             npk, nvl, nbs = _empty_narrow(val)
-            med = None
             del pack, val
-        self._set_narrow(npk, nvl, nbs, med)
+        self._set_narrow(npk, nvl, nbs)
         self.items = torch.tensor(items.astype(np.int32), device=dev)
         self.mt_tiles = torch.tensor(np.asarray(mt_tiles or [0], dtype=np.int32), device=dev)
         self.mt_ptr = torch.tensor(np.asarray(mt_ptr, dtype=np.int32), device=dev)
@@ -572,16 +522,9 @@ class TLTMulti:
                                if self.ncu else np.zeros((1, 3), np.int32), device=dev)
         self.ptrs = stream_ptr_table(chunks, dev)
         self._chunks = list(chunks)  # keep the streams alive
-        # per-item window-round counts (split_window) in launch order; None when no chunk has any
-        self.med = None
-        if n and any(getattr(ch, "med", None) is not None for ch in chunks):
-            cat = torch.cat([ch.med if getattr(ch, "med", None) is not None else
-                             torch.zeros(ch.nitems, dtype=torch.int32, device=dev) for ch in chunks])
-            self.med = cat[self._src].contiguous()
         self.desc = TLTMultiDesc(self.items.data_ptr(), n, self.cbits, self.ptrs.data_ptr(),
                                  self.mt_tiles.data_ptr(), self.mt_ptr.data_ptr(), self.nmt, dim,
-                                 self.cu.data_ptr(), self.ncu, self.nparts, self.il, None, None,
-                                 None if self.med is None else self.med.data_ptr())
+                                 self.cu.data_ptr(), self.ncu, self.nparts, self.il)
 
     @property
     def parts_needed(self) -> int:
@@ -601,7 +544,6 @@ class TLTMulti:
             rows[:, 2:4] = sel[:, 1:3]
             rows[:, 6:8] = sel[:, 4:6]
         new = copy.copy(self)
-        new.med = None                   # restreamed (row-sampled) copies have no window rounds
         new.items = rows.to(torch.int32).contiguous()
         new.ptrs = stream_ptr_table(chunks, dev)
         new._chunks = list(chunks)
@@ -746,7 +688,6 @@ class RowCompaction:
             nc._set_narrow(*_empty_narrow(oval))
             nc.nnz = kept
         else:
-            nc._set_narrow(ch.npack, ch.nval, ch.nbase)   # no window rounds: filtered rounds lost their spans
             nc.nnz = kept + self.n_narrow
         if self.forward:
             nc.blk = table

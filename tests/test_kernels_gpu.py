@@ -630,50 +630,6 @@ def test_narrow_rounds_match_wide_only_layout(precision, monkeypatch):
         assert torch.allclose(a, b, rtol=tol, atol=tol * float(b.abs().max()))
 
 
-@pytest.mark.parametrize("precision", ["f64", "bf16"])
-def test_window_rounds_match_gather_layout(precision, monkeypatch):
-    """Window rounds (tiled.split_window: rounds spanning < 256 / 512 keys read their key window with coalesced
-    loads into LDS, tl_stream_win) give the same value / gradient / Hessian products as the gather-only layout, in
-    the shard-wide and the per-chunk launches, bitwise reproducibly."""
-    from photon_ml_amd.data.synthetic import generate_device_shard
-    from photon_ml_amd.ops import tiled
-    from photon_ml_amd.ops.native import configure
-    out = {}
-    try:
-        for win, multi in ((0, 1), (1, 1), (1, 0)):
-            monkeypatch.setattr(tiled, "WINDOW", win)
-            configure(tl_multi=multi)
-            data, _ = generate_device_shard(200_000, 50_000, 30, "cuda", precision, seed=6, chunk_rows=1 << 16,
-                                            layout="tiled")
-            has = [c.med is not None for c in data.csr + data.csc]
-            assert all(has) == bool(win) and any(has) == bool(win), has
-            if win:
-                nA = sum(int((c.med & 0xFFFF).sum()) for c in data.csr + data.csc)
-                nB = sum(int((c.med >> 16).sum()) for c in data.csr + data.csc)
-                assert nA > 0 and nB > 0, (nA, nB)
-            assert data.validate()
-            data.track_hessian = True
-            w = (torch.randn(50_000, generator=torch.Generator().manual_seed(1), dtype=torch.float64) * 0.05)
-            w = w.float().double().cuda()
-            f, s, g = data.value_grad_sums(LOGISTIC, w, 0.01)
-            v = torch.randn(50_000, generator=torch.Generator().manual_seed(2), dtype=torch.float64).float().double()
-            h, _ = data.hv_sums(LOGISTIC, w, 0.01, v.cuda(), 0.0)
-            d = data.hdiag_sums(LOGISTIC, w)
-            out[(win, multi)] = (f, s, g, h, d)
-            f2, s2, g2 = data.value_grad_sums(LOGISTIC, w, 0.01)
-            assert f2 == f and s2 == s and torch.equal(g2, g)
-            del data
-    finally:
-        configure(tl_multi=1)
-    tol = 1e-12 if precision == "f64" else 1e-6
-    f0, s0, g0, h0, d0 = out[(0, 1)]
-    for key in ((1, 1), (1, 0)):
-        f1, s1, g1, h1, d1 = out[key]
-        assert abs(f1 - f0) <= tol * abs(f0) and abs(s1 - s0) <= tol * max(1.0, abs(s0))
-        for a, b in ((g1, g0), (h1, h0), (d1, d0)):
-            assert torch.allclose(a, b, rtol=tol, atol=tol * float(b.abs().max()))
-
-
 @pytest.mark.gpu
 def test_device_two_loop_matches_host_scalar_two_loop(monkeypatch):
     """L-BFGS two-loop with 0-d device scalars (no per-dot synchronisation) == the host-scalar recursion."""
