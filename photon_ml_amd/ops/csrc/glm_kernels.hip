@@ -2586,32 +2586,41 @@ __global__ __launch_bounds__(256) void gram_two_loop_kernel(const double* __rest
   const int kk = 2 * k + 1, np = kk * (kk + 1) / 2;
   const int tid = threadIdx.x;
   if (tid < np) {
-    double acc = 0.0;
-    for (int g = 0; g < grid; ++g) acc += partial[(long long)g * np + tid];
+    // 8 interleaved accumulators (8 independent loads in flight per thread instead of one dependent chain of
+    // `grid` loads: the serial loop was 0.13 ms per direction), added in a fixed order (deterministic)
+    double acc[8] = {0.0, 0.0, 0.0, 0.0, 0.0, 0.0, 0.0, 0.0};
+    int g = 0;
+    for (; g + 8 <= grid; g += 8) {
+#pragma unroll
+      for (int u = 0; u < 8; ++u) acc[u] += partial[(long long)(g + u) * np + tid];
+    }
+    for (int u = 0; g + u < grid; ++u) acc[u] += partial[(long long)(g + u) * np + tid];
+    const double s = ((acc[0] + acc[1]) + (acc[2] + acc[3])) + ((acc[4] + acc[5]) + (acc[6] + acc[7]));
     int p = tid, a = 0;
     while (p >= kk - a) { p -= kk - a; ++a; }
-    B[a * kk + a + p] = acc;
-    B[(a + p) * kk + a] = acc;
+    B[a * kk + a + p] = s;
+    B[(a + p) * kk + a] = s;
   }
   __syncthreads();
-  if (tid != 0) return;
-  double delta[GRAM_MAXK], alpha[(GRAM_MAXK - 1) / 2];
-  for (int j = 0; j < kk; ++j) delta[j] = 0.0;
-  delta[2 * k] = 1.0;
+  if (tid >= 64) return;
+  // the recursion on wave 0: lane j holds delta[j]; each dot product is one fixed-order wave sum (no per-thread
+  // arrays indexed at run time, which went to scratch memory)
+  const int j = tid;
+  const bool on = j < kk;
+  double delta = (j == 2 * k) ? 1.0 : 0.0;
+  double alpha_mine = 0.0;                    // lane i keeps alpha_i
   for (int i = k - 1; i >= 0; --i) {
-    double dot = 0.0;
-    for (int j = 0; j < kk; ++j) dot = fma(delta[j], B[j * kk + i], dot);   // s_i . q
-    alpha[i] = dot / B[i * kk + k + i];                                     // rho_i = 1 / (s_i . y_i)
-    delta[k + i] -= alpha[i];
+    const double dot = wave_sum(on ? delta * B[j * kk + i] : 0.0);          // s_i . q
+    const double al = dot / B[i * kk + k + i];                               // rho_i = 1 / (s_i . y_i)
+    if (j == i) alpha_mine = al;
+    if (j == k + i) delta -= al;
   }
-  const double scale = B[(k - 1) * kk + 2 * k - 1] / B[(2 * k - 1) * kk + 2 * k - 1];
-  for (int j = 0; j < kk; ++j) delta[j] *= scale;
+  delta *= B[(k - 1) * kk + 2 * k - 1] / B[(2 * k - 1) * kk + 2 * k - 1];
   for (int i = 0; i < k; ++i) {
-    double dot = 0.0;
-    for (int j = 0; j < kk; ++j) dot = fma(delta[j], B[j * kk + k + i], dot);   // y_i . r
-    delta[i] += alpha[i] - dot / B[i * kk + k + i];
+    const double dot = wave_sum(on ? delta * B[j * kk + k + i] : 0.0);      // y_i . r
+    if (j == i) delta += alpha_mine - dot / B[i * kk + k + i];
   }
-  for (int j = 0; j < kk; ++j) coef[j] = negate ? -delta[j] : delta[j];
+  if (on) coef[j] = negate ? -delta : delta;
 }
 
 __global__ __launch_bounds__(256) void lincomb_dev_kernel(VecSet vs, int k, long long n, const double* __restrict__ coef,
