@@ -358,6 +358,11 @@ struct FwdArgs {
   // FWD_LS (margin-space line search, direction pass): z_out = zd (in: previous direction, out: new one),
   // z0 = cached margins (materialised here: z0 += tpend * zd_prev), first trial t0 -> (F, D) stats + coef
   double* z0; double t0; double tpend;
+  // Column-phase forward (tl_fwd_multi, large D): the pass runs as P launches, each over one column range of
+  // every block, so the coefficient gathers of concurrently running work-groups stay inside an L2-sized slice of
+  // x. zphase 1: zacc[s] = sum (first phase, no epilogue); 2: zacc[s] += sum (middle); 3: sum += zacc[s], then
+  // the epilogue (last). Fixed phase order: deterministic. 0: one launch, no partial margins.
+  double* zacc; int zphase;
 };
 
 // Per-row epilogue inputs, prefetched at block start (coalesced, latency hidden behind the stream phase)
@@ -1096,6 +1101,10 @@ __device__ __forceinline__ void tl_fwd_block(int b, int row_lo, int nrows, int e
 #pragma unroll
     for (int w = 1; w < NW; ++w) z += static_cast<double>(acc[w][r]);
     const int s = row_lo + r;
+    if (a.zphase) {
+      if (a.zphase >= 2) z = a.zacc[s] + z;        // earlier phases first (fixed order)
+      if (a.zphase <= 2) { a.zacc[s] = z; continue; }
+    }
     fwd_finish(a, s, z, fwd_prefetch(a, s), F, S);
   }
   if (stats) {
@@ -1301,6 +1310,8 @@ static int g_ablate = 0;      // profiling ablation bits (0 in production)
 // FWD_LS arguments (set by pml_set_ls_args right before a direction pass; host-side, single stream)
 static double* g_ls_z0 = nullptr;
 static double g_ls_t0 = 0.0, g_ls_tpend = 0.0;
+static double* g_zacc = nullptr;   // column-phase forward (FwdArgs::zacc / zphase), tl_fwd_multi only
+static int g_zphase = 0;
 static int g_tl_acc64 = 1;   // measured on MI355X: ds_add_f64 accumulation is ~3x faster than ds_add_f32 here
 static int g_tl_waves = 4;     // forward
 static int g_tl_waves_t = 4;   // transpose
@@ -1995,7 +2006,7 @@ __global__ __launch_bounds__(256) void rs_tron_dpp_kernel(
     int B, int n, const double* __restrict__ Lm, const double* __restrict__ Y, const double* __restrict__ O,
     const double* __restrict__ WT, double* __restrict__ Beta, double* __restrict__ Fout, int* __restrict__ Iters,
     int* __restrict__ Reason, int loss, double l2, double tol, int max_iter, int max_fail, int max_cg,
-    const int* __restrict__ order) {
+    const int* __restrict__ order, double* __restrict__ Zout) {
   using Gm = RsGeom<K, LREG, WL>;
   constexpr int GL = Gm::GL, P = Gm::P, R = Gm::R, K1 = Gm::K1, SP = Gm::SP, PS = Gm::PS;
   extern __shared__ double smem[];
@@ -2335,19 +2346,29 @@ __global__ __launch_bounds__(256) void rs_tron_dpp_kernel(
 #pragma unroll
   for (int s = 0; s < R; ++s)
     if (on[s]) Beta[o[s]] = W[s];
+  if (Zout) {
+    // margins of the solution (L beta, no offsets) while L is still resident: the caller's scores need no
+    // separate batched GEMV pass that re-reads every L
+    double z[R];
+    mv(W, z);
+#pragma unroll
+    for (int s = 0; s < R; ++s)
+      if (on[s]) Zout[o[s]] = z[s];
+  }
   if (prob_on && i == 0) { Fout[b] = f; Iters[b] = it; Reason[b] = reason; }
 }
 
 template <int K, bool LREG, int WL = 2, bool MS = false>
 static void launch_rs_tron_dpp(int B, int n, const double* L, const double* y, const double* off, const double* wt,
                                double* beta, double* f, int* iters, int* reason, int loss, double l2, double tol,
-                               int max_iter, int max_fail, int max_cg, hipStream_t st, const int* order) {
+                               int max_iter, int max_fail, int max_cg, hipStream_t st, const int* order,
+                               double* zout) {
   using Gm = RsGeom<K, LREG, WL>;
   const long long waves = (B + Gm::P - 1) / Gm::P;
   const long long grid = (waves + Gm::WPB - 1) / Gm::WPB;
   const size_t lds = Gm::REG ? 0 : (size_t)Gm::WPB * Gm::P * Gm::PS * sizeof(double);
   hipLaunchKernelGGL((rs_tron_dpp_kernel<K, LREG, WL, MS>), dim3((unsigned)grid), dim3(Gm::WPB * 64), lds, st, B, n, L, y, off, wt,
-                     beta, f, iters, reason, loss, l2, tol, max_iter, max_fail, max_cg, order);
+                     beta, f, iters, reason, loss, l2, tol, max_iter, max_fail, max_cg, order, zout);
 }
 
 // ============================================================================================================
@@ -2701,6 +2722,7 @@ int pml_version() { return 1; }
 void pml_tl_set_deep(int fwd, int t) { g_tl_deep = fwd; g_tl_deep_t = t; }
 
 void pml_set_ls_args(double* z0, double t0, double tpend) { g_ls_z0 = z0; g_ls_t0 = t0; g_ls_tpend = tpend; }
+void pml_set_fwd_phase(double* zacc, int zphase) { g_zacc = zacc; g_zphase = zphase; }
 
 void pml_set_ablate(int a) {
   g_ablate = a;
@@ -2948,7 +2970,7 @@ void pml_rs_set_variant(int v) { g_rs_variant = v; }
 // (a scheduling hint only: results land in each problem's own slot whatever the order)
 int pml_rs_tron(int B, int n, const double* L, const double* y, const double* off, const double* wt, double* beta,
                 double* f, int* iters, int* reason, int loss, double l2, double tol, int max_iter, int max_fail,
-                int max_cg, const int* order, void* stream) {
+                int max_cg, const int* order, double* zout, void* stream) {
   if (B <= 0) return 0;
   if (n < 1 || n > 64 || loss < 0 || loss > 2) return -22;
   const int V = g_rs_variant;
@@ -2956,13 +2978,13 @@ int pml_rs_tron(int B, int n, const double* L, const double* y, const double* of
   if (V >= 3 && n <= 32) {
 #define RS_DPP(KK)                                                                                              \
   (V == 3 ? launch_rs_tron_dpp<KK, true>(B, n, L, y, off, wt, beta, f, iters, reason, loss, l2, tol, max_iter,    \
-                                         max_fail, max_cg, st, order)                                              \
+                                         max_fail, max_cg, st, order, zout)                                              \
    : V == 5 ? launch_rs_tron_dpp<KK, true, 1>(B, n, L, y, off, wt, beta, f, iters, reason, loss, l2, tol, max_iter, \
-                                              max_fail, max_cg, st, order)                                         \
+                                              max_fail, max_cg, st, order, zout)                                         \
    : V == 6 ? launch_rs_tron_dpp<KK, true, 1, true>(B, n, L, y, off, wt, beta, f, iters, reason, loss, l2, tol,    \
-                                                    max_iter, max_fail, max_cg, st, order)                         \
+                                                    max_iter, max_fail, max_cg, st, order, zout)                         \
           : launch_rs_tron_dpp<KK, false>(B, n, L, y, off, wt, beta, f, iters, reason, loss, l2, tol, max_iter,   \
-                                          max_fail, max_cg, st, order))
+                                          max_fail, max_cg, st, order, zout))
     if (n <= 4) RS_DPP(4);
     else if (n <= 8) RS_DPP(8);
     else if (n <= 12) RS_DPP(12);
@@ -2991,6 +3013,7 @@ int pml_rs_tron(int B, int n, const double* L, const double* y, const double* of
     hipLaunchKernelGGL(rs_tron_kernel<0>, dim3((unsigned)grid), dim3(nw * 64), nw * wave_lds, (hipStream_t)stream, B,
                        n, G, L, y, off, wt, beta, f, iters, reason, loss, l2, tol, max_iter, max_fail, max_cg);
   LAUNCH_CHECK();
+  if (zout) return pml_bgemv(B, n, L, beta, zout, 0, stream);   // these variants keep no L at exit
   return 0;
 }
 
@@ -3030,11 +3053,13 @@ int pml_tl_fwd_multi(int prec, const TLFwdMultiDesc* c, const void* x, int mode,
   hipStream_t st = (hipStream_t)stream;
   if (prec == 2) {
     FwdArgs<double, double> a{mode, loss, shift, (const double*)y, (const double*)off, (const double*)wt,
-                              (double*)coef, (double*)dzz, z_out, with_offset, 0, 0, g_ls_z0, g_ls_t0, g_ls_tpend};
+                              (double*)coef, (double*)dzz, z_out, with_offset, 0, 0, g_ls_z0, g_ls_t0, g_ls_tpend,
+                              g_zacc, g_zphase};
     return tl_fwd_multi_impl<double, double, double>(c, x, a, stats, st);
   }
   FwdArgs<float, float> a{mode, loss, shift, (const float*)y, (const float*)off, (const float*)wt,
-                          (float*)coef, (float*)dzz, z_out, with_offset, 0, 0, g_ls_z0, g_ls_t0, g_ls_tpend};
+                          (float*)coef, (float*)dzz, z_out, with_offset, 0, 0, g_ls_z0, g_ls_t0, g_ls_tpend,
+                          g_zacc, g_zphase};
   if (prec == 1) return tl_fwd_multi_impl<float, float, float>(c, x, a, stats, st);
   return tl_fwd_multi_impl<uint16_t, float, float>(c, x, a, stats, st);
 }

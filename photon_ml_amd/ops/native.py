@@ -119,6 +119,7 @@ def glm_lib() -> Optional[ctypes.CDLL]:
         lib.pml_bgemv.argtypes = [c_int, c_int, c_void_p, c_void_p, c_void_p, c_int, c_void_p]
         lib.pml_bhv.argtypes = [c_int, c_int, c_void_p, c_void_p, c_void_p, c_double, c_void_p, c_void_p]
         lib.pml_set_ls_args.argtypes = [c_void_p, c_double, c_double]
+        lib.pml_set_fwd_phase.argtypes = [c_void_p, c_int]
         lib.pml_gram_grid.argtypes = [ctypes.c_longlong]
         lib.pml_gram.argtypes = [c_void_p, c_int, ctypes.c_longlong, c_void_p, c_void_p]
         lib.pml_lincomb.argtypes = [c_void_p, c_void_p, c_int, ctypes.c_longlong, c_void_p, c_void_p]
@@ -134,7 +135,7 @@ def glm_lib() -> Optional[ctypes.CDLL]:
         lib.pml_ls_eval.argtypes = [c_int, c_int, c_double, c_int, c_void_p, c_void_p, c_void_p, c_void_p, c_int,
                                     c_void_p, c_void_p, c_void_p, c_void_p, c_void_p]
         lib.pml_rs_tron.argtypes = [c_int, c_int] + [c_void_p] * 8 + [c_int, c_double, c_double, c_int, c_int, c_int,
-                                                                      c_void_p, c_void_p]
+                                                                      c_void_p, c_void_p, c_void_p]
         for f in ("pml_seg_fwd", "pml_seg_t", "pml_reduce_stats", "pml_build_blocks", "pml_tl_fwd", "pml_tl_t",
                   "pml_tl_maxbits", "pml_segdot", "pml_tl_fwd_multi", "pml_tl_t_multi", "pml_seg_cg_step",
                   "pml_seg_expand", "pml_bgemv", "pml_bhv", "pml_rs_tron", "pml_ls_eval", "pml_gram_grid", "pml_gram",
@@ -359,9 +360,11 @@ def batched_hv(A: torch.Tensor, dw: torch.Tensor, v: torch.Tensor, l2: float = 0
 
 def rs_tron(L: torch.Tensor, y: torch.Tensor, o: torch.Tensor, w: torch.Tensor, beta0: torch.Tensor, loss_id: int,
             l2: float, tol: float, max_iter: int, max_fail: int = 5, max_cg: int = 20,
-            out: Optional[torch.Tensor] = None, order: Optional[torch.Tensor] = None):
+            out: Optional[torch.Tensor] = None, order: Optional[torch.Tensor] = None,
+            zout: Optional[torch.Tensor] = None):
     """Fused per-problem TRON over a batch of small dense GLMs (``rs_tron_kernel``): returns
-    (beta, f, iters, reason). Device only; n <= 64; losses logistic / Poisson / squared. ``out`` (contiguous
+    (beta, f, iters, reason). ``zout`` (contiguous fp64 [B, n]) receives the margins ``L beta`` of the solution
+    (written by the kernel while L is resident). Device only; n <= 64; losses logistic / Poisson / squared. ``out`` (contiguous
     fp64 [B, n]) receives the solution in place (it starts from ``beta0``; ``out`` may be ``beta0``). ``order``
     (int32 permutation of the B problems): waves take consecutive problems of it -- grouping problems of similar
     iteration counts cuts the time a wave waits for its slowest problem; the results do not depend on it."""
@@ -385,10 +388,13 @@ def rs_tron(L: torch.Tensor, y: torch.Tensor, o: torch.Tensor, w: torch.Tensor, 
         assert order.dtype == torch.int32 and order.is_cuda and order.shape == (B,) and order.is_contiguous()
         if os.environ.get("PML_CHECK_KERNEL_INPUTS", "0") == "1":   # the kernel indexes L / y / beta through it
             assert B == 0 or (int(order.min()) >= 0 and int(order.max()) < B), "rs_tron order out of range"
+    if zout is not None:
+        assert zout.shape == (B, n) and zout.dtype == torch.float64 and zout.is_contiguous() and zout.is_cuda
     check(lib.pml_rs_tron(B, n, ts[0].data_ptr(), ts[1].data_ptr(), ts[2].data_ptr(), ts[3].data_ptr(),
                           beta.data_ptr(), f.data_ptr(), iters.data_ptr(), reason.data_ptr(), int(loss_id), float(l2),
                           float(tol), int(max_iter), int(max_fail), int(max_cg),
-                          None if order is None else order.data_ptr(), stream_handle(L.device)), "rs_tron")
+                          None if order is None else order.data_ptr(),
+                          None if zout is None else zout.data_ptr(), stream_handle(L.device)), "rs_tron")
     return beta, f, iters.to(torch.long), reason.to(torch.long)
 
 

@@ -209,6 +209,11 @@ class RowSpaceBatch:
                       else torch.zeros(0, dtype=torch.bool, device=dev))
         self.rows = (torch.cat([c.rows.reshape(-1) for c in self.classes]) if self.classes
                      else torch.zeros(0, dtype=torch.long, device=dev))
+        # packed slot -> row of the valid slots, once (margins / to_primal scatter with them: no boolean-mask
+        # indexing, which costs a nonzero pass and a host synchronisation per call)
+        self.vslot = torch.nonzero(self.valid).squeeze(1)
+        self.vrow = self.rows[self.vslot]
+        self._z = None            # (beta, packed margins L beta) written by the fused solve
 
     def _slots(self, per_row: torch.Tensor) -> torch.Tensor:
         """Packed per-slot values of a per-row vector (0 in padding slots)."""
@@ -223,16 +228,20 @@ class RowSpaceBatch:
     def to_primal(self, beta: torch.Tensor) -> torch.Tensor:
         """w = X^T L^{-T} beta for the handled entities (zeros elsewhere): one transpose pass."""
         r = torch.zeros(self.seg.y.numel(), dtype=torch.float64, device=beta.device)
-        for c in self.classes:
-            alpha = _bmv(c.Linv, c.view(beta), trans=True)               # L^{-T} beta
-            r[c.rows[c.valid]] = alpha[c.valid]
+        if self.classes:
+            alpha = torch.cat([_bmv(c.Linv, c.view(beta), trans=True).reshape(-1) for c in self.classes])  # L^-T b
+            r[self.vrow] = alpha[self.vslot]
         return self.seg.glm.rmatvec(r, build_multi=False)     # once per update: no shard-wide tables
 
     def margins(self, beta: torch.Tensor) -> torch.Tensor:
-        """Per-row X w (no offsets) of the handled entities = L beta, in the segmented row order."""
+        """Per-row X w (no offsets) of the handled entities = L beta, in the segmented row order (the fused solve's
+        own margins when ``beta`` is its result: no pass over L)."""
         z = torch.zeros(self.seg.y.numel(), dtype=torch.float64, device=beta.device)
-        for c in self.classes:
-            z[c.rows[c.valid]] = _bmv(c.L, c.view(beta))[c.valid]
+        if self._z is not None and self._z[0] is beta:
+            zs = self._z[1]
+        else:
+            zs = torch.cat([_bmv(c.L, c.view(beta)).reshape(-1) for c in self.classes]) if self.classes else beta
+        z[self.vrow] = zs[self.vslot]
         return z
 
     def solve(self, loss, l2: float, optimizer: str, W0: Optional[torch.Tensor], tol: float, max_iter: int,
@@ -250,6 +259,7 @@ class RowSpaceBatch:
         fused = (optimizer == "TRON" and self.seg.y.is_cuda and getattr(loss, "loss_id", -1) in (0, 1, 2)
                  and os.environ.get("PML_RS_FUSED_TRON", "1") != "0")
         beta = torch.empty_like(beta0)
+        zs = torch.empty_like(beta0) if fused else None
         fs, its, rcs = [], [], []
         for c in self.classes:
             b0, oc = c.view(beta0), c.view(o)
@@ -262,7 +272,7 @@ class RowSpaceBatch:
                 if order is not None and order.numel() != c.L.shape[0]:
                     order = None
                 _, f, it, rc = rs_tron(c.L, c.y, oc, c.w, b0, loss.loss_id, l2, tol, max_iter, out=c.view(beta),
-                                       order=order)
+                                       order=order, zout=c.view(zs))
                 if RS_ORDER:
                     c.order = torch.argsort(it, stable=True).to(torch.int32)
             else:
@@ -270,6 +280,7 @@ class RowSpaceBatch:
                 solver = batched_tron if optimizer == "TRON" else batched_lbfgs
                 r = solver(data, loss, l2, b0, tol, max_iter)
                 c.view(beta).copy_(r.W)
+                zs = None
                 f, it, rc = r.f, r.iters, r.reason
             fs.append(f)
             its.append(it)
@@ -277,4 +288,5 @@ class RowSpaceBatch:
         res = BatchedResult(beta, torch.cat(fs) if fs and fs[0] is not None else None, torch.cat(its),
                             torch.cat(rcs))
         self.beta = res.W
+        self._z = None if zs is None else (res.W, zs)
         return res
