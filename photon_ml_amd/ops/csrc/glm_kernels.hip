@@ -358,11 +358,6 @@ struct FwdArgs {
   // FWD_LS (margin-space line search, direction pass): z_out = zd (in: previous direction, out: new one),
   // z0 = cached margins (materialised here: z0 += tpend * zd_prev), first trial t0 -> (F, D) stats + coef
   double* z0; double t0; double tpend;
-  // Column-phase forward (tl_fwd_multi, large D): the pass runs as P launches, each over one column range of
-  // every block, so the coefficient gathers of concurrently running work-groups stay inside an L2-sized slice of
-  // x. zphase 1: zacc[s] = sum (first phase, no epilogue); 2: zacc[s] += sum (middle); 3: sum += zacc[s], then
-  // the epilogue (last). Fixed phase order: deterministic. 0: one launch, no partial margins.
-  double* zacc; int zphase;
 };
 
 // Per-row epilogue inputs, prefetched at block start (coalesced, latency hidden behind the stream phase)
@@ -1101,10 +1096,6 @@ __device__ __forceinline__ void tl_fwd_block(int b, int row_lo, int nrows, int e
 #pragma unroll
     for (int w = 1; w < NW; ++w) z += static_cast<double>(acc[w][r]);
     const int s = row_lo + r;
-    if (a.zphase) {
-      if (a.zphase >= 2) z = a.zacc[s] + z;        // earlier phases first (fixed order)
-      if (a.zphase <= 2) { a.zacc[s] = z; continue; }
-    }
     fwd_finish(a, s, z, fwd_prefetch(a, s), F, S);
   }
   if (stats) {
@@ -1310,8 +1301,6 @@ static int g_ablate = 0;      // profiling ablation bits (0 in production)
 // FWD_LS arguments (set by pml_set_ls_args right before a direction pass; host-side, single stream)
 static double* g_ls_z0 = nullptr;
 static double g_ls_t0 = 0.0, g_ls_tpend = 0.0;
-static double* g_zacc = nullptr;   // column-phase forward (FwdArgs::zacc / zphase), tl_fwd_multi only
-static int g_zphase = 0;
 static int g_tl_acc64 = 1;   // measured on MI355X: ds_add_f64 accumulation is ~3x faster than ds_add_f32 here
 static int g_tl_waves = 4;     // forward
 static int g_tl_waves_t = 4;   // transpose
@@ -2722,7 +2711,6 @@ int pml_version() { return 1; }
 void pml_tl_set_deep(int fwd, int t) { g_tl_deep = fwd; g_tl_deep_t = t; }
 
 void pml_set_ls_args(double* z0, double t0, double tpend) { g_ls_z0 = z0; g_ls_t0 = t0; g_ls_tpend = tpend; }
-void pml_set_fwd_phase(double* zacc, int zphase) { g_zacc = zacc; g_zphase = zphase; }
 
 void pml_set_ablate(int a) {
   g_ablate = a;
@@ -3053,13 +3041,11 @@ int pml_tl_fwd_multi(int prec, const TLFwdMultiDesc* c, const void* x, int mode,
   hipStream_t st = (hipStream_t)stream;
   if (prec == 2) {
     FwdArgs<double, double> a{mode, loss, shift, (const double*)y, (const double*)off, (const double*)wt,
-                              (double*)coef, (double*)dzz, z_out, with_offset, 0, 0, g_ls_z0, g_ls_t0, g_ls_tpend,
-                              g_zacc, g_zphase};
+                              (double*)coef, (double*)dzz, z_out, with_offset, 0, 0, g_ls_z0, g_ls_t0, g_ls_tpend};
     return tl_fwd_multi_impl<double, double, double>(c, x, a, stats, st);
   }
   FwdArgs<float, float> a{mode, loss, shift, (const float*)y, (const float*)off, (const float*)wt,
-                          (float*)coef, (float*)dzz, z_out, with_offset, 0, 0, g_ls_z0, g_ls_t0, g_ls_tpend,
-                          g_zacc, g_zphase};
+                          (float*)coef, (float*)dzz, z_out, with_offset, 0, 0, g_ls_z0, g_ls_t0, g_ls_tpend};
   if (prec == 1) return tl_fwd_multi_impl<float, float, float>(c, x, a, stats, st);
   return tl_fwd_multi_impl<uint16_t, float, float>(c, x, a, stats, st);
 }

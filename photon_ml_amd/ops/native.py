@@ -119,7 +119,6 @@ def glm_lib() -> Optional[ctypes.CDLL]:
         lib.pml_bgemv.argtypes = [c_int, c_int, c_void_p, c_void_p, c_void_p, c_int, c_void_p]
         lib.pml_bhv.argtypes = [c_int, c_int, c_void_p, c_void_p, c_void_p, c_double, c_void_p, c_void_p]
         lib.pml_set_ls_args.argtypes = [c_void_p, c_double, c_double]
-        lib.pml_set_fwd_phase.argtypes = [c_void_p, c_int]
         lib.pml_gram_grid.argtypes = [ctypes.c_longlong]
         lib.pml_gram.argtypes = [c_void_p, c_int, ctypes.c_longlong, c_void_p, c_void_p]
         lib.pml_lincomb.argtypes = [c_void_p, c_void_p, c_int, ctypes.c_longlong, c_void_p, c_void_p]

@@ -767,44 +767,3 @@ def test_zero_point_sums_bound_the_zero_gradient(precision):
     f, b, exact = GLMObjective(LOGISTIC, 1.0).zero_state_bound(dev, z)
     assert f == F and b >= exact() > 0
 
-
-@pytest.mark.gpu
-@pytest.mark.parametrize("precision", ["bf16", "f64"])
-def test_column_phase_forward_matches_one_launch(precision, monkeypatch):
-    """Column-phase forward (wide shards: one launch per column slice, partial margins in a per-row fp64 buffer)
-    vs the one-launch forward on the same shard: margins, value+gradient, Hessian-vector and an L-BFGS run
-    through the margin-space line search (FWD_LS) agree to fp64 rounding; repeated phased passes are bitwise
-    equal (fixed phase order); the phased path really engaged (several phases, narrow rounds in the first)."""
-    import photon_ml_amd.ops.device as dv
-    from photon_ml_amd.data.synthetic import generate_device_shard
-    from photon_ml_amd.function.losses import LOGISTIC
-    from photon_ml_amd.function.objective import GLMObjective
-    from photon_ml_amd.optimization.lbfgs import LBFGS
-    res = {}
-    for cols in (0, 1 << 15):
-        monkeypatch.setattr(dv, "PHASE_COLS", cols)
-        data, w = generate_device_shard(200_000, 150_000, 30, "cuda", precision, chunk_rows=1 << 16,
-                                        layout="tiled", seed=5)
-        w = (w * 0.05).to(torch.float64)
-        z = data.margins(w, 0.1, True)
-        assert data._phases == (None if cols == 0 else 5)
-        if cols:
-            assert torch.equal(data.margins(w, 0.1, True), z)
-            assert int((data._phase_tabs[1][:, 7] - data._phase_tabs[1][:, 6]).abs().sum()) == 0
-            assert int((data._phase_tabs[0][:, 7] - data._phase_tabs[0][:, 6]).sum()) > 0
-        vg = data.value_grad_packed(LOGISTIC, w, 0.1)
-        data.track_hessian = True
-        data.value_grad_packed(LOGISTIC, w, 0.1)
-        v = torch.randn(data.dim, dtype=torch.float64, device="cuda", generator=torch.Generator(
-            device="cuda").manual_seed(3))
-        hv = data.hv_packed(LOGISTIC, w, 0.1, v, 0.0)
-        data.track_hessian = False
-        opt = LBFGS(tolerance=1e-12, max_iterations=6)
-        wo, fo = opt.optimize(GLMObjective(LOGISTIC, 1.0), data, torch.zeros(data.dim, dtype=torch.float64,
-                                                                            device="cuda"))
-        res[cols] = (z, vg, hv, wo, fo)
-    a, b = res[0], res[1 << 15]
-    for x, y in zip(a[:3], b[:3]):
-        torch.testing.assert_close(y, x, rtol=1e-11, atol=1e-9 * float(x.abs().max()))
-    torch.testing.assert_close(b[3], a[3], rtol=1e-7, atol=1e-9)
-    assert abs(b[4] - a[4]) <= 1e-9 * abs(a[4])
