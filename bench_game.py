@@ -185,12 +185,15 @@ def run(args, dev, rank: int = 0, world: int = 1) -> dict:
     fe_gd = coords["global"].glm_data
     fe_pass0 = (getattr(fe_gd, "n_fwd", 0), getattr(fe_gd, "n_t", 0))
     t1 = time.perf_counter()
-    model, _ = cd.run(args.steps, model)
-    for _, m in model:       # the trained model's coefficients are part of the timed work (row-space RE: lazy)
-        if hasattr(m, "materialize"):
-            m.materialize()
-    if torch.cuda.is_available():
-        torch.cuda.synchronize()
+    from photon_ml_amd.utils.timing import trace_range
+    with trace_range("timed sweeps"):
+        model, _ = cd.run(args.steps, model)
+        with trace_range("materialize model"):
+            for _, m in model:   # the trained model's coefficients are part of the timed work (row-space RE: lazy)
+                if hasattr(m, "materialize"):
+                    m.materialize()
+            if torch.cuda.is_available():
+                torch.cuda.synchronize()
     barrier()
     elapsed = all_reduce_scalar(time.perf_counter() - t1, "max")
     log(f"fixed effect per sweep: {(getattr(fe_gd, 'n_fwd', 0) - fe_pass0[0]) / args.steps:.1f} forward + "

@@ -909,9 +909,17 @@ __constant__ int c_tl_ablate = 0;
 //    accumulator starting at +0.0 never holds -0.0, so the added zeros change no bits);
 //  * a scheduling barrier keeps each step's loads ahead of its accumulation.
 // Same entry order per wave for every (S, D): the result is bitwise identical across variants.
+// WIDE-ROUND BASES (forward copies of shards whose column index does not fit 32 - rbits bits, ops/tiled.py):
+// the pack holds the key relative to one int32 base per physical round, read with a scalar load when the round's
+// streams are issued (``wbase``; a shard without bases passes a one-element zero table and stride 0, so the code
+// path is the same). Masked lanes gather x[0].
+__device__ const int g_zero_base[1] = {0};
+typedef const __attribute__((address_space(4))) int* const_int_p;
+
 template <typename VT, typename XT, typename AT, bool SQ, int NW, int S, int D>
 __device__ __forceinline__ void tl_stream_ring(const uint32_t* __restrict__ pack, const VT* __restrict__ val,
-                                               const XT* __restrict__ x, int e_lo, int e_hi, int sbits, AT* acc) {
+                                               const XT* __restrict__ x, int e_lo, int e_hi, int sbits, AT* acc,
+                                               const int* wbase) {
   constexpr int R = S + 1;
   static_assert(D < S && R % (D + 1) == 0, "gathers run ahead of loaded slots; the gather ring divides the slots");
   typedef typename TLValT<VT>::T LT;
@@ -924,19 +932,24 @@ __device__ __forceinline__ void tl_stream_ring(const uint32_t* __restrict__ pack
   if (r0 >= r1) return;
   v4u pk[R];
   Raw vr[R];
+  uint32_t bs[R];
   XT xg[D + 1][TL_VEC];
-  auto load_round = [&](int r, v4u& p, Raw& v) {
+  const int ws = wbase ? 1 : 0;
+  const const_int_p wb = (const_int_p)(wbase ? wbase : g_zero_base);
+  const int rb0 = e_lo / TL_ROUND;                     // physical round index of the unit's first round
+  auto load_round = [&](int r, v4u& p, Raw& v, uint32_t& b) {
     const int e = e_lo + min(r, r1 - 1) * TL_ROUND + lane * TL_VEC;
     p = ldg_nt((const v4u*)(pack + e));
     v = TLVals<VT>::load(val + e);
+    b = (uint32_t)wb[ws * (rb0 + min(r, r1 - 1))];
   };
   const int abl = TL_ABL;
   AT regsum = AT(0);
-  auto gather = [&](int r, const v4u& p, XT* xv) {
+  auto gather = [&](int r, const v4u& p, uint32_t b, XT* xv) {
     const int e = e_lo + r * TL_ROUND + lane;
 #pragma unroll
     for (int k = 0; k < TL_VEC; ++k) {
-      const uint32_t key = (e + 64 * k < e_hi) ? (p[k] >> sbits) : 0u;
+      const uint32_t key = (e + 64 * k < e_hi) ? b + (p[k] >> sbits) : 0u;
       const bool hot = key < ((uint32_t)abl >> 8) << 10;
       if (abl & 10) xv[k] = XT(1);
       else if ((abl & 32) && hot) xv[k] = XT(1);                    // per lane (exec-masked load)
@@ -948,21 +961,21 @@ __device__ __forceinline__ void tl_stream_ring(const uint32_t* __restrict__ pack
   // the outstanding-load sequence at the loop head is the same from the prologue and from the back edge
 #pragma unroll
   for (int i = 0; i < S; ++i) {
-    load_round(r0 + i, pk[i], vr[i]);
+    load_round(r0 + i, pk[i], vr[i], bs[i]);
     __builtin_amdgcn_sched_barrier(0);
   }
 #pragma unroll
   for (int i = 0; i < D; ++i) {
-    gather(r0 + i, pk[i], xg[i]);
+    gather(r0 + i, pk[i], bs[i], xg[i]);
     __builtin_amdgcn_sched_barrier(0);
   }
   for (int r = r0; r < r1; r += R) {
 #pragma unroll
     for (int i = 0; i < R; ++i) {
       const int rc = r + i;
-      load_round(rc + S, pk[(i + S) % R], vr[(i + S) % R]);          // slot of round rc - 1 (consumed)
+      load_round(rc + S, pk[(i + S) % R], vr[(i + S) % R], bs[(i + S) % R]);   // slot of round rc - 1 (consumed)
       __builtin_amdgcn_sched_barrier(0);
-      gather(rc + D, pk[(i + D) % R], xg[(i + D) % (D + 1)]);        // gathers of round rc + D
+      gather(rc + D, pk[(i + D) % R], bs[(i + D) % R], xg[(i + D) % (D + 1)]);   // gathers of round rc + D
       __builtin_amdgcn_sched_barrier(0);
       LT v[TL_VEC];
       TLVals<VT>::get(vr[i], v);
@@ -995,7 +1008,6 @@ __device__ __forceinline__ void tl_stream_ring(const uint32_t* __restrict__ pack
 // not in the vector-memory queue) one round ahead of the window load that needs them. Ring pipeline with S + 1
 // slots under the code-generation rules of tl_stream_ring. Accumulation order per wave is fixed (deterministic).
 template <typename T> __device__ __forceinline__ T lane_bcast(T v, int src) { return __shfl(v, src, 64); }
-typedef const __attribute__((address_space(4))) int* const_int_p;
 
 template <typename VT, typename XT, typename AT, bool SQ, int NW, int S = 2>
 __device__ __forceinline__ void tl_stream_narrow(const uint16_t* __restrict__ npk, const VT* __restrict__ nvl,
@@ -1060,17 +1072,19 @@ __device__ __forceinline__ void tl_stream_narrow(const uint16_t* __restrict__ np
 // P = 2 two-slot, 8 entries per lane; P = 3 lane-interleaved layout (tl_stream_il)
 template <typename VT, typename XT, typename AT, bool SQ, int U, int NW, int P>
 __device__ __forceinline__ void tl_stream(const uint32_t* __restrict__ pack, const VT* __restrict__ val,
-                                          const XT* __restrict__ x, int e_lo, int e_hi, int sbits, AT* acc) {
+                                          const XT* __restrict__ x, int e_lo, int e_hi, int sbits, AT* acc,
+                                          const int* wbase = nullptr) {
+  // wide-round bases exist only in the interleaved layout (P >= 3); the builder never sets them otherwise
   if (P == 1) tl_stream_p1<VT, XT, AT, SQ, U, NW>(pack, val, x, e_lo, e_hi, sbits, acc);
   else if (P == 2) tl_stream_wide<VT, XT, AT, SQ, NW, 2>(pack, val, x, e_lo, e_hi, sbits, acc);
-  else if (P == 3) tl_stream_ring<VT, XT, AT, SQ, NW, 2, 0>(pack, val, x, e_lo, e_hi, sbits, acc);
-  else if (P == 5) tl_stream_ring<VT, XT, AT, SQ, NW, 3, 1>(pack, val, x, e_lo, e_hi, sbits, acc);
-  else if (P == 6) tl_stream_ring<VT, XT, AT, SQ, NW, 5, 2>(pack, val, x, e_lo, e_hi, sbits, acc);
+  else if (P == 3) tl_stream_ring<VT, XT, AT, SQ, NW, 2, 0>(pack, val, x, e_lo, e_hi, sbits, acc, wbase);
+  else if (P == 5) tl_stream_ring<VT, XT, AT, SQ, NW, 3, 1>(pack, val, x, e_lo, e_hi, sbits, acc, wbase);
+  else if (P == 6) tl_stream_ring<VT, XT, AT, SQ, NW, 5, 2>(pack, val, x, e_lo, e_hi, sbits, acc, wbase);
   else tl_stream_p0<VT, XT, AT, SQ, U, NW>(pack, val, x, e_lo, e_hi, sbits, acc);
 }
 
 // Narrow-section streams of one chunk (see tl_stream_narrow); n_lo == n_hi: the unit has no narrow rounds.
-struct TLNarrow { const uint16_t* pack; const void* val; const int* base; };
+struct TLNarrow { const uint16_t* pack; const void* val; const int* base; const int* wbase; };
 
 // Forward over row blocks. blk: 6 ints per block {row_lo, nrows, e_lo, e_hi, n_lo, n_hi} (chunk-local).
 template <typename VT, typename XT, typename RT, typename AT, int MAXR, int U, int NW, int P>
@@ -1088,7 +1102,7 @@ __device__ __forceinline__ void tl_fwd_block(int b, int row_lo, int nrows, int e
     tl_stream_narrow<VT, XT, AT, false, NW, (P >= 5 ? 4 : 2)>(nar.pack, (const VT*)nar.val, nar.base, n_lo, n_hi,
                                                               rbits, x,
                                             acc[threadIdx.x >> 6]);
-  tl_stream<VT, XT, AT, false, U, NW, P>(pack, val, x, e_lo, e_hi, rbits, acc[threadIdx.x >> 6]);
+  tl_stream<VT, XT, AT, false, U, NW, P>(pack, val, x, e_lo, e_hi, rbits, acc[threadIdx.x >> 6], nar.wbase);
   __syncthreads();
   double F = 0.0, S = 0.0;
   for (int r = threadIdx.x; r < nrows; r += NW * 64) {
@@ -1122,7 +1136,8 @@ __global__ __launch_bounds__(NW * 64) void tl_fwd_kernel(const int* __restrict__
 
 // All chunks of a shard in ONE launch (no per-chunk tails / launch gaps): block table of 8 ints
 // {chunk, global row_lo, nrows, e_lo, e_hi, col_lo, n_lo, n_hi}; per-chunk stream pointers in device arrays
-// (ptrs[5 * chunk + {0: pack, 1: val, 2: narrow pack, 3: narrow val, 4: narrow base}]); row-data pointers in ``a``
+// (ptrs[6 * chunk + {0: pack, 1: val, 2: narrow pack, 3: narrow val, 4: narrow base, 5: wide-round bases or 0}]);
+// row-data pointers in ``a``
 // are shard-global; stats index = global block index.
 template <typename VT, typename XT, typename RT, typename AT, int MAXR, int U, int NW, int P>
 __global__ __launch_bounds__(NW * 64) void tl_fwd_multi_kernel(const int* __restrict__ blk, int rbits,
@@ -1135,8 +1150,8 @@ __global__ __launch_bounds__(NW * 64) void tl_fwd_multi_kernel(const int* __rest
   const int b = blockIdx.x;
   if (live && !live[b]) return;
   const int* q = blk + 8 * b;
-  const unsigned long long* pc = ptrs + 5 * q[0];
-  const TLNarrow nar = {(const uint16_t*)pc[2], (const void*)pc[3], (const int*)pc[4]};
+  const unsigned long long* pc = ptrs + 6 * q[0];
+  const TLNarrow nar = {(const uint16_t*)pc[2], (const void*)pc[3], (const int*)pc[4], (const int*)pc[5]};
   tl_fwd_block<VT, XT, RT, AT, MAXR, U, NW, P>(b, q[1], q[2], q[3], q[4], q[6], q[7], rbits, (const uint32_t*)pc[0],
                                               (const VT*)pc[1], nar, x + q[5], a, stats, acc, red);
 }
@@ -1157,7 +1172,7 @@ __device__ __forceinline__ void tl_t_item(int tile, int e_lo, int e_hi, int part
     tl_stream_narrow<VT, XT, AT, SQ, NW, (P >= 5 ? 4 : 2)>(nar.pack, (const VT*)nar.val, nar.base, n_lo, n_hi,
                                                            cbits, x,
                                          acc[threadIdx.x >> 6]);
-  tl_stream<VT, XT, AT, SQ, U, NW, P>(pack, val, x, e_lo, e_hi, cbits, acc[threadIdx.x >> 6]);
+  tl_stream<VT, XT, AT, SQ, U, NW, P>(pack, val, x, e_lo, e_hi, cbits, acc[threadIdx.x >> 6], nar.wbase);
   __syncthreads();
   const int c0 = tile << cbits;
   for (int c = threadIdx.x; c < C; c += NW * 64) {
@@ -1189,7 +1204,7 @@ __global__ __launch_bounds__(NW * 64) void tl_t_kernel(const int* __restrict__ i
 // All row chunks of a shard in one launch. items: 8 ints {chunk, tile, e_lo, e_hi, part, row_base, n_lo, n_hi};
 // a tile with a single item in the whole shard writes G directly, every other item writes a partial row that the
 // shard-wide combine sums in (chunk, item) order — deterministic and race-free across chunks. Stream pointers as
-// in tl_fwd_multi_kernel (5 per chunk).
+// in tl_fwd_multi_kernel (6 per chunk).
 template <typename VT, typename XT, typename AT, bool SQ, int MAXR, int U, int NW, int P>
 __global__ __launch_bounds__(NW * 64) void tl_t_multi_kernel(const int* __restrict__ items, int cbits,
                                                               const unsigned long long* __restrict__ ptrs,
@@ -1199,8 +1214,8 @@ __global__ __launch_bounds__(NW * 64) void tl_t_multi_kernel(const int* __restri
   __shared__ AT acc[NW][MAXR];
   if (live && !live[blockIdx.x]) return;
   const int* q = items + 8 * blockIdx.x;
-  const unsigned long long* pc = ptrs + 5 * q[0];
-  const TLNarrow nar = {(const uint16_t*)pc[2], (const void*)pc[3], (const int*)pc[4]};
+  const unsigned long long* pc = ptrs + 6 * q[0];
+  const TLNarrow nar = {(const uint16_t*)pc[2], (const void*)pc[3], (const int*)pc[4], (const int*)pc[5]};
   tl_t_item<VT, XT, AT, SQ, MAXR, U, NW, P>(q[1], q[2], q[3], q[4], q[6], q[7], cbits, (const uint32_t*)pc[0],
                                             (const VT*)pc[1], nar, x + q[5], G, dim, parts, acc);
 }
@@ -1272,7 +1287,7 @@ __global__ __launch_bounds__(NTHREADS) void tl_t_combine2_kernel(const int* __re
 // live: optional per-block flags (0 = skip the block: rows of converged entities in a block-diagonal problem)
 struct TLFwdDesc { const int* blk; int nblk; int rbits; const uint32_t* pack; const void* val; int il; TLNarrow nar;
                   const unsigned char* live; };
-// ptrs: 5 stream pointers per chunk (see tl_fwd_multi_kernel)
+// ptrs: 6 stream pointers per chunk (see tl_fwd_multi_kernel)
 struct TLFwdMultiDesc { const int* blk; int nblk; int rbits; const unsigned long long* ptrs; int il;
                        const unsigned char* live; };
 struct TLTDesc {

@@ -222,8 +222,11 @@ class DeviceGLMData(GLMComputable):
                 raise ValueError(f"chunk {c}: interleaved forward windows not round-aligned")
             ncols = int(self.dim) - self.col_lo[c]
             self._validate_narrow(c, f, b, ncols, "forward")
-            pk, _ = f.logical()
-            p = pk.cpu().to(torch.int64) & 0xFFFFFFFF
+            pk, _ = f.logical()                   # absolute (col << rbits) | row, also with wide-round bases
+            p = pk.cpu().to(torch.int64)
+            wb = getattr(f, "wbase", None)
+            if wb is not None and wb.numel() and int(wb.min()) < 0:
+                raise ValueError(f"chunk {c}: negative wide-round base")
             if p.numel() and int((p >> f.rbits).max()) >= ncols:
                 raise ValueError(f"chunk {c}: forward gather index >= column window")
             counts = f.unit_counts().cpu()
@@ -460,6 +463,8 @@ class DeviceGLMData(GLMComputable):
         from .native import TLFwdMultiDesc
         if self.layout != "tiled" or not self.csr or not all(getattr(ch, "il", 0) for ch in self.csr + self.csc):
             return None
+        if any(getattr(ch, "wbase", None) is not None for ch in self.csr):
+            return None      # compaction moves wide entries across rounds: their per-round key bases would not hold
         keep = keep.to(self.device, torch.uint8).contiguous()
         assert keep.numel() >= self.n_rows
         n = self.n_rows

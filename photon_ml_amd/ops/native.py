@@ -32,8 +32,9 @@ class SegChunkDesc(ctypes.Structure):
 
 
 class TLNarrow(ctypes.Structure):
-    """Narrow-section streams of one chunk (16-bit packs, values, one int32 base per round)."""
-    _fields_ = [("pack", c_void_p), ("val", c_void_p), ("base", c_void_p)]
+    """Narrow-section streams of one chunk (16-bit packs, values, one int32 base per round), plus the wide
+    section's per-round key bases (``wbase``, NULL when the wide packs hold absolute keys)."""
+    _fields_ = [("pack", c_void_p), ("val", c_void_p), ("base", c_void_p), ("wbase", c_void_p)]
 
 
 class TLFwdDesc(ctypes.Structure):

@@ -86,6 +86,7 @@ TL_VEC = 4               # entries per lane per round
 INTERLEAVE = int(os.environ.get("PML_TL_IL", "1"))
 NARROW = int(os.environ.get("PML_TL_NARROW", "1"))
 NARROW_W = 64            # key window loaded per narrow round (one wave64 load)
+WIDE_BASE = int(os.environ.get("PML_TL_WIDE_BASE", "1"))   # per-round key bases for wide shards (TLFwdChunk)
 
 
 def narrow_width(sbits: int) -> int:
@@ -213,10 +214,13 @@ class _NarrowMixin:
     """Narrow-section bookkeeping shared by the forward and transpose chunks (``table`` columns 4, 5 hold the
     per-unit narrow round range [n_lo, n_hi); the wide window is columns ``_ew``)."""
 
+    wbase = None          # forward copies only: int32 key base per physical wide round (see TLFwdChunk)
+
     def _set_narrow(self, npack, nval, nbase):
         from .native import TLNarrow
         self.npack, self.nval, self.nbase = npack, nval, nbase
-        self.nar = TLNarrow(npack.data_ptr(), nval.data_ptr(), nbase.data_ptr())
+        self.nar = TLNarrow(npack.data_ptr(), nval.data_ptr(), nbase.data_ptr(),
+                            None if self.wbase is None else self.wbase.data_ptr())
 
     @property
     def n_narrow_rounds(self) -> int:
@@ -249,7 +253,8 @@ class _NarrowMixin:
         wu = torch.repeat_interleave(torch.arange(U, device=dev), nw.to(dev))
         unit = torch.cat([nu, wu])
         order = torch.sort(unit, stable=True).indices
-        pk = torch.cat([npk[npos], wide_pack.to(torch.int64) & 0xFFFFFFFF])[order]
+        wp = wide_pack.to(torch.int64) & 0xFFFFFFFF if wide_pack.dtype == torch.int32 else wide_pack.to(torch.int64)
+        pk = torch.cat([npk[npos], wp])[order]
         vl = torch.cat([nvl[npos], wide_val])[order]
         return pk, vl
 
@@ -266,15 +271,23 @@ class TLFwdChunk(_NarrowMixin):
         rowptr = rowptr.to(dev, torch.int64)
         col = col.to(dev, torch.int64)
         m = rowptr.numel() - 1
-        self.rbits = fwd_bits(dim, val.dtype == torch.float64, rbits)
+        f64 = val.dtype == torch.float64
+        self.rbits = fwd_bits(dim, f64, rbits)
         if self.rbits is None:
             raise ValueError(f"tiled forward layout cannot pack dim={dim}")
+        # wide shards: (col << rbits) would overflow 32 bits at the wanted block size -> keys relative to one base
+        # per wide round (the full block size instead of 2^(32 - bits(D)) rows; see tl_stream_ring)
+        want = _cap(DEFAULT_RBITS if rbits is None else rbits, f64)
+        use_base = bool(self.il) and WIDE_BASE and want > self.rbits
+        if use_base:
+            self.rbits = want
         R = 1 << self.rbits
+        kbits = _bits(dim) + self.rbits                       # bits of (col << rbits) | row
         nnz = col.numel()
         rows = torch.repeat_interleave(torch.arange(m, device=dev), rowptr[1:] - rowptr[:-1]) if nnz else \
             torch.zeros(0, dtype=torch.int64, device=dev)
         pack = (col << self.rbits) | (rows & (R - 1))
-        key = ((rows >> self.rbits) << 32) | pack
+        key = ((rows >> self.rbits) << kbits) | pack
         key, perm = torch.sort(key, stable=True)
         nblk = (m + R - 1) // R
         b = torch.arange(nblk, device=dev)
@@ -284,15 +297,22 @@ class TLFwdChunk(_NarrowMixin):
         self._sbits, self._ew = self.rbits, (2, 3)
         n_lo = n_hi = torch.zeros(nblk, dtype=torch.int64, device=dev)
         if self.il:
-            wp, wv, wn, npk, nvl, nbs, nr = split_narrow(key & 0xFFFFFFFF, val[perm], e_hi - e_lo, self.rbits, dim)
+            wp, wv, wn, npk, nvl, nbs, nr = split_narrow(key & ((1 << kbits) - 1), val[perm], e_hi - e_lo,
+                                                         self.rbits, dim)
             del key, perm
+            if use_base:
+                wp = self._rebase(wp, wn)
+                if wp is None:      # a wide round spans more keys than 32 - rbits bits: plain packs, fewer rows
+                    del wv, npk, nvl, nbs
+                    self.__init__(rowptr, col, val, dim, fwd_bits(dim, f64, rbits), il)
+                    return
             self.pack, self.val, e_lo = _interleave(_to_u32_bits(wp), wv, wn)
             e_hi = e_lo + wn
             n_hi = torch.cumsum(nr, 0)
             n_lo = n_hi - nr
             del wp, wv
         else:
-            self.pack = _pad(_to_u32_bits(key & 0xFFFFFFFF))
+            self.pack = _pad(_to_u32_bits(key & ((1 << kbits) - 1)))
             self.val = _pad(val[perm].contiguous())
             npk, nvl, nbs = _empty_narrow(val)
             del key, perm
@@ -302,6 +322,33 @@ class TLFwdChunk(_NarrowMixin):
         self.nblk, self.m, self.nnz = nblk, m, nnz
         self.desc = TLFwdDesc(self.blk.data_ptr(), nblk, self.rbits, self.pack.data_ptr(), self.val.data_ptr(),
                               self.il, self.nar)
+
+    def _rebase(self, wp: torch.Tensor, wn: torch.Tensor) -> Optional[torch.Tensor]:
+        """Wide packs (int64 ``(key << rbits) | slot``, units of ``wn`` sorted entries) relative to the first key of
+        their round of the interleaved layout; sets ``self.wbase`` (int32 per physical round). None when some
+        round's key span does not fit 32 - rbits bits."""
+        dev = wp.device
+        n = wn.to(torch.int64)
+        tot = int(n.sum())
+        padded = (n + IL_ROUND - 1) // IL_ROUND * IL_ROUND
+        nrounds = int(padded.sum()) // IL_ROUND
+        wbase = torch.zeros(nrounds + 1, dtype=torch.int64, device=dev)
+        if tot:
+            unit = torch.repeat_interleave(torch.arange(n.numel(), device=dev), n, output_size=tot)
+            j = torch.arange(tot, device=dev) - (torch.cumsum(n, 0) - n)[unit]
+            rid = ((torch.cumsum(padded, 0) - padded)[unit] + j) // IL_ROUND     # same rounds as _interleave
+            del unit
+            key = wp >> self.rbits
+            first = (j % IL_ROUND) == 0
+            del j
+            wbase[rid[first]] = key[first]
+            rel = key - wbase[rid]
+            del rid, key, first
+            if int(rel.max()) >= 1 << (32 - self.rbits):
+                return None
+            wp = (rel << self.rbits) | (wp & ((1 << self.rbits) - 1))
+        self.wbase = wbase.to(torch.int32).contiguous()
+        return wp
 
     @property
     def nstats(self) -> int:
@@ -314,20 +361,24 @@ class TLFwdChunk(_NarrowMixin):
 
     def nbytes(self) -> int:
         return sum(t.numel() * t.element_size() for t in (self.blk, self.pack, self.val, self.npack, self.nval,
-                                                           self.nbase))
+                                                           self.nbase) + (() if self.wbase is None else (self.wbase,)))
 
     def logical(self):
         """(pack, val) of the non-zeros in unit order (per block: its narrow entries, then its wide entries, each
-        sorted by column), whatever the storage order."""
+        sorted by column), whatever the storage order; packs as non-negative int64 ``(col << rbits) | row``."""
         if not self.il:
-            return self.pack[: self.nnz], self.val[: self.nnz]
+            return self.pack[: self.nnz].to(torch.int64) & 0xFFFFFFFF, self.val[: self.nnz]
         ph = il_phys(self.blk[:, 2], self.blk[:, 3] - self.blk[:, 2])
-        return self._logical_all(self.pack[ph], self.val[ph])
+        wp = self.pack[ph].to(torch.int64) & 0xFFFFFFFF
+        if self.wbase is not None:
+            wp = ((self.wbase[ph // IL_ROUND].to(torch.int64) + (wp >> self.rbits)) << self.rbits) | (
+                wp & ((1 << self.rbits) - 1))
+        return self._logical_all(wp, self.val[ph])
 
     # host emulation of the kernel arithmetic (tests / CPU fallback)
     def emulate_matvec(self, x: torch.Tensor) -> torch.Tensor:
         pk, vl = self.logical()
-        p = pk.to(torch.int64) & 0xFFFFFFFF
+        p = pk.to(torch.int64)
         col = p >> self.rbits
         blk_of_entry = torch.repeat_interleave(torch.arange(self.nblk, device=p.device), self.unit_counts())
         row = (blk_of_entry << self.rbits) + (p & ((1 << self.rbits) - 1))
@@ -585,9 +636,12 @@ class TLTMulti:
 
 
 def stream_ptr_table(chunks, device) -> torch.Tensor:
-    """Per-chunk stream pointers of the shard-wide kernels: {pack, val, narrow pack, narrow val, narrow base}."""
+    """Per-chunk stream pointers of the shard-wide kernels: {pack, val, narrow pack, narrow val, narrow base,
+    wide-round bases (0: absolute keys)}."""
+    wb = lambda ch: 0 if getattr(ch, "wbase", None) is None else ch.wbase.data_ptr()
     return torch.tensor([[ch.pack.data_ptr(), ch.val.data_ptr(), ch.npack.data_ptr(), ch.nval.data_ptr(),
-                          ch.nbase.data_ptr()] for ch in chunks], dtype=torch.int64, device=device).reshape(-1)
+                          ch.nbase.data_ptr(), wb(ch)] for ch in chunks], dtype=torch.int64,
+                        device=device).reshape(-1)
 
 
 # ---- row-sampled copies (K20 down-sampling work saving: DeviceGLMData.row_sampled) ---------------------------

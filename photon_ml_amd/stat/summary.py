@@ -95,7 +95,7 @@ class BasicStatisticalSummary:
             if getattr(ch, "kind", None) != "tl":
                 raise ValueError("from_device needs the tiled layout")
             pk, vl = ch.logical()
-            col = ((pk.to(torch.int64) & 0xFFFFFFFF) >> ch.rbits) + data.col_lo[c]
+            col = (pk.to(torch.int64) >> ch.rbits) + data.col_lo[c]     # logical(): non-negative int64
             v = vl.to(f64)
             s1.index_add_(0, col, v)
             s2.index_add_(0, col, v * v)

@@ -767,3 +767,49 @@ def test_zero_point_sums_bound_the_zero_gradient(precision):
     f, b, exact = GLMObjective(LOGISTIC, 1.0).zero_state_bound(dev, z)
     assert f == F and b >= exact() > 0
 
+
+
+@pytest.mark.parametrize("precision", ["f64", "bf16"])
+def test_wide_round_bases_on_device(precision, monkeypatch):
+    """Wide shard (2^25 columns: plain packs would leave 7 row bits): the forward copy keeps 1024-row blocks with
+    per-round key bases (scalar-loaded by tl_stream_ring). Value+gradient, margins and Hessian-vector match the
+    fp64 reference and the plain-pack layout, through the one-launch and the per-chunk kernels."""
+    from photon_ml_amd.ops import tiled
+    from photon_ml_amd.ops.device import DeviceGLMData
+    from photon_ml_amd.ops.native import configure
+    rng = np.random.default_rng(8)
+    n, d, k = 6000, 1 << 25, 24
+    cols = np.concatenate([np.sort(rng.choice(d, k, replace=False)) for _ in range(n)])
+    cols[::4] = rng.integers(0, 64, size=cols[::4].size)
+    x = sp.csr_matrix((rng.normal(size=n * k), cols, np.arange(0, n * k + 1, k)), shape=(n, d))
+    x.sum_duplicates()
+    x.sort_indices()
+    y = (rng.random(n) < 0.5).astype(float)
+    data = LabeledData(x, y, offsets=rng.normal(size=n) * 0.1, weights=rng.random(n) + 0.5)
+    if precision == "bf16":
+        data = _round_bf16(data)
+    ref = TorchGLMData(data, "cpu")
+    w = torch.from_numpy(rng.normal(size=d) * 0.05).float().double()
+    v = torch.from_numpy(rng.normal(size=d)).float().double()
+    f0, s0, g0 = ref.value_grad_sums(LOGISTIC, w, 0.02)
+    tol = TOL[precision]
+    out = {}
+    for wb in (1, 0):
+        monkeypatch.setattr(tiled, "WIDE_BASE", wb)
+        dev = DeviceGLMData.from_labeled(data, "cuda", precision, chunk_rows=2500, layout="tiled")
+        assert all((ch.wbase is not None) == bool(wb) for ch in dev.csr)
+        assert all(ch.rbits == (10 if wb else 7) for ch in dev.csr)
+        for multi in (1, 0):
+            configure(tl_multi=multi)
+            try:
+                f1, s1, g1 = dev.value_grad_sums(LOGISTIC, w.cuda(), 0.02)
+                z1 = dev.margins(w.cuda(), 0.02, True)
+            finally:
+                configure(tl_multi=1)
+            assert abs(f1 - f0) <= tol * max(1.0, abs(f0)) and abs(s1 - s0) <= tol * max(1.0, abs(s0))
+            assert torch.allclose(g1.cpu(), g0, rtol=tol, atol=tol * float(g0.abs().max()))
+            torch.testing.assert_close(z1.cpu(), ref.margins(w, 0.02, True), rtol=tol, atol=tol * 10)
+        dev.track_hessian = True
+        dev.value_grad_sums(LOGISTIC, w.cuda(), 0.02)
+        out[wb] = dev.hv_sums(LOGISTIC, w.cuda(), 0.02, v.cuda(), 0.0)[0].cpu()
+    torch.testing.assert_close(out[1], out[0], rtol=1e-10, atol=1e-10 * float(out[0].abs().max()))

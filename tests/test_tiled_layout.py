@@ -179,3 +179,42 @@ def test_narrow_rounds_on_zipf_data_cpu():
     w, r = rng.normal(size=d), rng.normal(size=m)
     np.testing.assert_allclose(f.emulate_matvec(torch.from_numpy(w)).numpy(), x @ w, atol=1e-11)
     np.testing.assert_allclose(t.emulate_rmatvec(torch.from_numpy(r)).numpy(), x.T @ r, atol=1e-11)
+
+
+def test_wide_round_bases_keep_full_row_blocks():
+    """Wide shards: (col << rbits) does not fit 32 bits at 1024-row blocks, so the wide packs hold keys relative
+    to one base per physical round (``wbase``) instead of shrinking the blocks to 2^(32 - bits(D)) rows. The
+    logical entries decode to the same (column, row) pairs and the emulated product matches scipy; with bases
+    off the builder falls back to the smaller blocks."""
+    import numpy as np
+    import scipy.sparse as sp
+    import torch
+    from photon_ml_amd.ops import tiled
+    from photon_ml_amd.ops.tiled import TLFwdChunk
+    rng = np.random.default_rng(0)
+    n, d, k = 3000, 1 << 25, 30
+    cols = np.concatenate([np.sort(rng.choice(d, k, replace=False)) for _ in range(n)])
+    cols[::5] = rng.integers(0, 40, size=cols[::5].size)          # hot columns -> narrow rounds too
+    x = sp.csr_matrix((rng.random(n * k) + 0.5, cols, np.arange(0, n * k + 1, k)), shape=(n, d))
+    x.sum_duplicates()
+    x.sort_indices()
+    rp, c = torch.from_numpy(x.indptr.astype(np.int64)), torch.from_numpy(x.indices.astype(np.int64))
+    v = torch.from_numpy(x.data)
+    w = torch.from_numpy(rng.normal(size=d))
+    ref = torch.from_numpy(x @ w.numpy())
+    old = tiled.WIDE_BASE
+    try:
+        for wb in (0, 1):
+            tiled.WIDE_BASE = wb
+            ch = TLFwdChunk(rp, c, v, d)
+            assert ch.rbits == (10 if wb else 32 - 25)
+            assert (ch.wbase is not None) == bool(wb)
+            torch.testing.assert_close(ch.emulate_matvec(w), ref, rtol=1e-12, atol=1e-12)
+            pk, _ = ch.logical()
+            assert int(pk.min()) >= 0 and int((pk >> ch.rbits).max()) < d
+            if wb:
+                # every stored relative key fits its 32 - rbits bits and every base is a column of its round
+                rel = (ch.pack.to(torch.int64) & 0xFFFFFFFF) >> ch.rbits
+                assert int(rel.max()) < 1 << (32 - ch.rbits) and int(ch.wbase.max()) < d
+    finally:
+        tiled.WIDE_BASE = old
