@@ -119,15 +119,18 @@ def main():
     if is_dist() and not sharded:
         log(f"gradient all-reduce: {'overlapped, %d buckets' % gdata.buckets if gdata.overlap else 'one-shot'}")
 
+    # the optimizer runs exactly warmup + steps iterations (tolerance 0: no early stop), so nothing is queued for an
+    # iteration that never runs (L-BFGS speculates the next direction and its margin pass during the history push)
+    n_iter = args.warmup + args.steps
     if args.config == "owlqn":
         obj = GLMObjective(LOGISTIC, l2_weight=0.0)
-        opt = OWLQN(args.l1, tolerance=0.0, max_iterations=10 ** 9, track_state=False)
+        opt = OWLQN(args.l1, tolerance=0.0, max_iterations=n_iter, track_state=False)
     elif args.config == "tron":
         obj = GLMObjective(POISSON, l2_weight=args.l2)
-        opt = TRON(tolerance=0.0, max_iterations=10 ** 9, track_state=False)
+        opt = TRON(tolerance=0.0, max_iterations=n_iter, track_state=False)
     else:
         obj = GLMObjective(LOGISTIC, l2_weight=args.l2)
-        opt = LBFGS(tolerance=0.0, max_iterations=10 ** 9, track_state=False)
+        opt = LBFGS(tolerance=0.0, max_iterations=n_iter, track_state=False)
     import contextlib
     space = contextlib.nullcontext()
     w0 = torch.zeros(args.features, dtype=torch.float64, device=dev)

@@ -2545,6 +2545,51 @@ __global__ __launch_bounds__(256) void lbfgs_pair_kernel(const double* __restric
   }
 }
 
+// The L-BFGS line search's scalars of a new direction d at (x0, g) in one pass: out = [g.d, d.d, x0.x0, x0.d]
+// (descent test, first trial 1/||d||, zero-direction test, the L2 terms of the margin line search). Per-workgroup
+// partials reduced in workgroup order by the last workgroup (deterministic), as in lbfgs_pair_kernel. Replaces
+// four BLAS dot products (eight launches) and a stack.
+__global__ __launch_bounds__(256) void ls_dots_kernel(const double* __restrict__ x0, const double* __restrict__ g,
+                                                      const double* __restrict__ d, long long n,
+                                                      double* __restrict__ partial, unsigned* __restrict__ counter,
+                                                      double* __restrict__ out) {
+  __shared__ double sh[4];
+  __shared__ int last;
+  double a = 0.0, b = 0.0, c = 0.0, e = 0.0;
+  for (long long i = (long long)blockIdx.x * 256 + threadIdx.x; i < n; i += (long long)gridDim.x * 256) {
+    const double di = d[i], xi = x0[i];
+    a = fma(g[i], di, a);
+    b = fma(di, di, b);
+    c = fma(xi, xi, c);
+    e = fma(xi, di, e);
+  }
+  a = tl2_block_sum(a, sh);
+  b = tl2_block_sum(b, sh);
+  c = tl2_block_sum(c, sh);
+  e = tl2_block_sum(e, sh);
+  if (threadIdx.x == 0) {
+    double* pp = partial + 4 * blockIdx.x;
+    pp[0] = a; pp[1] = b; pp[2] = c; pp[3] = e;
+    __threadfence();
+    last = atomicAdd(counter, 1u) == gridDim.x - 1;
+  }
+  __syncthreads();
+  if (!last) return;
+  __threadfence();
+  a = 0.0; b = 0.0; c = 0.0; e = 0.0;
+  for (int j = threadIdx.x; j < (int)gridDim.x; j += 256) {
+    a += partial[4 * j]; b += partial[4 * j + 1]; c += partial[4 * j + 2]; e += partial[4 * j + 3];
+  }
+  a = tl2_block_sum(a, sh);
+  b = tl2_block_sum(b, sh);
+  c = tl2_block_sum(c, sh);
+  e = tl2_block_sum(e, sh);
+  if (threadIdx.x == 0) {
+    out[0] = a; out[1] = b; out[2] = c; out[3] = e;
+    *counter = 0u;
+  }
+}
+
 // L-BFGS two-loop recursion as a chain of 2k + 1 fused step kernels launched back to back from C++ (no host work
 // between them; a single cooperative launch with grid barriers was measured slower, profiles/
 // lbfgs_device_two_loop_ab.md). Step: x = src (g first, then q); x += sign * c * u; x *= gamma; store x (or -x);
@@ -2706,6 +2751,17 @@ int pml_two_loop_gram(int k, const double* const* s, const double* const* y, con
   hipLaunchKernelGGL(gram_two_loop_kernel, dim3(1), dim3(256), 0, (hipStream_t)stream, partial, grid, k, coef, negate);
   const long long blocks = std::min<long long>((n + 255) / 256, 4096);
   hipLaunchKernelGGL(lincomb_dev_kernel, dim3((unsigned)blocks), dim3(256), 0, (hipStream_t)stream, vs, kk, n, coef, q);
+  LAUNCH_CHECK();
+  return 0;
+}
+
+// out[4] = [g.d, d.d, x0.x0, x0.d]; partial: 4 * 1024 doubles; counter: one zeroed unsigned (re-armed).
+int pml_ls_dots(const double* x0, const double* g, const double* d, long long n, double* partial, unsigned* counter,
+                double* out, void* stream) {
+  if (n <= 0) return -22;
+  const int grid = (int)std::min<long long>(PAIR_GRID, (n + 255) / 256);
+  hipLaunchKernelGGL(ls_dots_kernel, dim3(grid), dim3(256), 0, (hipStream_t)stream, x0, g, d, n, partial, counter,
+                     out);
   LAUNCH_CHECK();
   return 0;
 }

@@ -124,6 +124,7 @@ def glm_lib() -> Optional[ctypes.CDLL]:
         lib.pml_gram.argtypes = [c_void_p, c_int, ctypes.c_longlong, c_void_p, c_void_p]
         lib.pml_lincomb.argtypes = [c_void_p, c_void_p, c_int, ctypes.c_longlong, c_void_p, c_void_p]
         lib.pml_lbfgs_pair.argtypes = [c_void_p] * 4 + [ctypes.c_longlong] + [c_void_p] * 6
+        lib.pml_ls_dots.argtypes = [c_void_p] * 3 + [ctypes.c_longlong] + [c_void_p] * 4
         lib.pml_two_loop_chain.argtypes = [c_int] + [c_void_p] * 5 + [ctypes.c_longlong] + [c_void_p] * 4 + \
             [c_int, c_void_p]
         lib.pml_two_loop_gram.argtypes = [c_int, c_void_p, c_void_p, c_void_p, ctypes.c_longlong, c_void_p, c_void_p,
@@ -139,7 +140,7 @@ def glm_lib() -> Optional[ctypes.CDLL]:
         for f in ("pml_seg_fwd", "pml_seg_t", "pml_reduce_stats", "pml_build_blocks", "pml_tl_fwd", "pml_tl_t",
                   "pml_tl_maxbits", "pml_segdot", "pml_tl_fwd_multi", "pml_tl_t_multi", "pml_seg_cg_step",
                   "pml_seg_expand", "pml_bgemv", "pml_bhv", "pml_rs_tron", "pml_ls_eval", "pml_gram_grid", "pml_gram",
-                  "pml_lincomb", "pml_lbfgs_pair", "pml_two_loop_chain", "pml_two_loop_gram",
+                  "pml_lincomb", "pml_lbfgs_pair", "pml_ls_dots", "pml_two_loop_chain", "pml_two_loop_gram",
                   "pml_two_loop_gram_grid"):
             getattr(lib, f).restype = c_int
         lib.pml_set_config.argtypes = [c_int, c_int, c_int, c_int]
@@ -263,6 +264,50 @@ def lbfgs_pair(x, x0, g, g0):
                              y.data_ptr(), sc[0].data_ptr(), sc[1].data_ptr(), out.data_ptr(),
                              stream_handle(x.device)), "lbfgs_pair")
     return s, y, out
+
+
+_LOSS_SCRATCH = {}
+
+
+def loss_sum(loss_id: int, z: torch.Tensor, y: torch.Tensor, w: torch.Tensor) -> Optional[torch.Tensor]:
+    """0-d device fp64 ``sum_i w_i l(z_i, y_i)`` in one fused pass (``ls_eval_kernel`` at t = 0 + a fixed-order
+    block reduction): the GAME training-loss evaluation after every coordinate update, instead of ~10 torch
+    elementwise passes. None when the inputs do not qualify (host tensors, other dtypes)."""
+    vs = (z, y, w)
+    if not (z.device.type == "cuda" and loss_id in (0, 1, 2, 3) and 0 < z.numel() < 2 ** 31
+            and all(v.device == z.device and v.dtype == torch.float64 and v.dim() == 1 and v.is_contiguous()
+                    and v.numel() == z.numel() for v in vs)):
+        return None
+    lib = require_glm_lib()
+    sc = _LOSS_SCRATCH.get(z.device)
+    if sc is None:
+        sc = _LOSS_SCRATCH[z.device] = torch.empty(2 * 4096, dtype=torch.float64, device=z.device)
+    out = torch.empty(2, dtype=torch.float64, device=z.device)
+    check(lib.pml_ls_eval(2, z.numel(), 0.0, int(loss_id), z.data_ptr(), z.data_ptr(), y.data_ptr(), w.data_ptr(),
+                          0, None, None, sc.data_ptr(), out.data_ptr(), stream_handle(z.device)), "loss_sum")
+    return out[0]
+
+
+_DOTS_SCRATCH = {}
+
+
+def ls_dots(x0, g, d):
+    """Device vector [g.d, d.d, x0.x0, x0.d] in one launch (``ls_dots_kernel``, deterministic last-workgroup
+    reduction); None when the inputs do not qualify."""
+    vs = (x0, g, d)
+    if not (d.device.type == "cuda" and all(v.device == d.device and v.dtype == torch.float64 and v.dim() == 1
+                                            and v.is_contiguous() and v.numel() == d.numel() for v in vs)
+            and d.numel() > 0):
+        return None
+    lib = require_glm_lib()
+    sc = _DOTS_SCRATCH.get(d.device)
+    if sc is None:
+        sc = _DOTS_SCRATCH[d.device] = (torch.empty(4 * 1024, dtype=torch.float64, device=d.device),
+                                        torch.zeros(1, dtype=torch.int32, device=d.device))
+    out = torch.empty(4, dtype=torch.float64, device=d.device)
+    check(lib.pml_ls_dots(x0.data_ptr(), g.data_ptr(), d.data_ptr(), d.numel(), sc[0].data_ptr(), sc[1].data_ptr(),
+                          out.data_ptr(), stream_handle(d.device)), "ls_dots")
+    return out
 
 
 _CHAIN_SCRATCH = {}

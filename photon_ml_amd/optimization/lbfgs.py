@@ -42,6 +42,10 @@ NATIVE_PAIR = os.environ.get("PML_LBFGS_NATIVE_PAIR", "1") != "0"
 # queue the NEXT iteration's two-loop direction (with the new pair, as if accepted) before the pair's host
 # synchronisation: the GPU computes it while the host runs the curvature / convergence bookkeeping
 SPECULATE_DIRECTION = os.environ.get("PML_LBFGS_SPECULATE", "1") != "0"
+# ... and also queue that direction's margin pass (the margin line search's first trial) before the synchronisation,
+# so the GPU never waits for the host between two iterations; skipped when the next iteration cannot run
+# (max_iterations), discarded when the pair is rejected or the data ran another pass in between
+SPECULATE_MARGINS = os.environ.get("PML_LBFGS_SPECULATE_MARGINS", "1") != "0"
 # Two-loop as 2k + 1 fused HIP step kernels launched from C++ (no Python between launches); 0: torch recursion
 NATIVE_TWO_LOOP = os.environ.get("PML_LBFGS_NATIVE_TWO_LOOP", "1") != "0"
 # Device two-loop method for replicated vectors: "gram" = vector-free recursion on the device (one Gram pass, the
@@ -225,7 +229,7 @@ class LBFGS(Optimizer):
         # smooth (un-penalised) value/gradient at the current point, used for the history
         self._smooth_f = None
         self._smooth_g = None
-        self._spec = None        # (x, g, direction, prefetch) queued for the next iteration (push_pair)
+        self._spec = None        # (x, g, direction, prefetch, margin search) queued for the next iteration
 
     def clear_inner_state(self):
         super().clear_inner_state()
@@ -275,12 +279,32 @@ class LBFGS(Optimizer):
 
     @staticmethod
     def _prefetch_of(x0: torch.Tensor, g: torch.Tensor, d: torch.Tensor) -> torch.Tensor:
+        if NATIVE_PAIR:
+            from ..ops.native import ls_dots
+            out = ls_dots(x0, g, d)              # one launch instead of four dot products and a stack
+            if out is not None:
+                return out
         return torch.stack([torch.dot(g, d), torch.dot(d, d), torch.dot(x0, x0), torch.dot(x0, d)])
 
-    def _search(self, objective, data, state: OptimizerState, d: torch.Tensor, pre=None):
+    @staticmethod
+    def _pass_count(data):
+        n = (getattr(data, "n_fwd", None), getattr(data, "n_t", None))
+        return None if n[0] is None else n
+
+    def _speculate_margins(self, objective, data, x, d):
+        """The next iteration's margin line search (direction pass queued now, t0 = 1), or None."""
+        if (not SPECULATE_MARGINS or not MARGIN_LINE_SEARCH or self.constraints
+                or not hasattr(objective, "margin_line_search") or self._pass_count(data) is None):
+            return None
+        from ..function.objective import DEFERRED_DOTS
+        mls = objective.margin_line_search(data, x, d, 1.0, dots=DEFERRED_DOTS)
+        return None if mls is None else (mls, self._pass_count(data))
+
+    def _search(self, objective, data, state: OptimizerState, d: torch.Tensor, pre=None, spec_mls=None):
         """``pre``: host list or device vector from :meth:`_prefetch`. A device vector is read AFTER the margin
         line search has queued its direction pass (iterations > 0: t0 = 1 is known), so the GPU runs that pass
-        while the host waits instead of idling through the synchronisation."""
+        while the host waits instead of idling through the synchronisation. ``spec_mls``: that search, already
+        started during the previous iteration's history push (used only if no pass ran since)."""
         x0 = state.coefficients
         from ..utils.timing import trace_range
         use_mls = MARGIN_LINE_SEARCH and not self.constraints and hasattr(objective, "margin_line_search")
@@ -293,8 +317,12 @@ class LBFGS(Optimizer):
             # a device ``pre`` is read after the direction pass is queued: the L2 dots are assigned then, not
             # recomputed (vdots would cost three reductions and a host synchronisation of their own)
             from ..function.objective import DEFERRED_DOTS
-            mls = objective.margin_line_search(data, x0, d, t0, dots=None if pre is None else
-                                               (DEFERRED_DOTS if lazy else (pre[2], pre[3], pre[1])))
+            if (spec_mls is not None and lazy and t0 == 1.0 and spec_mls[0].x0 is x0 and spec_mls[0].d is d
+                    and spec_mls[1] == self._pass_count(data)):
+                mls = spec_mls[0]
+            else:
+                mls = objective.margin_line_search(data, x0, d, t0, dots=None if pre is None else
+                                                   (DEFERRED_DOTS if lazy else (pre[2], pre[3], pre[1])))
             if lazy:
                 pre = pre.tolist()
                 if mls is not None and mls.l2 > 0:
@@ -328,8 +356,9 @@ class LBFGS(Optimizer):
         spec, self._spec = self._spec, None
         try:
             with trace_range("two-loop direction"):
+                spec_mls = None
                 if spec is not None and spec[0] is state.coefficients and spec[1] is state.gradient:
-                    d, pre = spec[2], spec[3]             # queued during the last history push
+                    d, pre, spec_mls = spec[2], spec[3], spec[4]   # queued during the last history push
                 else:
                     d = self._direction(state)
                     pre = self._prefetch(state, d)
@@ -338,7 +367,7 @@ class LBFGS(Optimizer):
             if not nonzero:
                 self._finished = True  # zero (pseudo-)gradient: stationary point
                 return state
-            x, f, g = self._search(objective, data, state, d, pre)
+            x, f, g = self._search(objective, data, state, d, pre, spec_mls)
         except _ZeroDirection:
             self._finished = True
             return state
@@ -355,15 +384,19 @@ class LBFGS(Optimizer):
             f_dev = f if isinstance(f, torch.Tensor) else None
             spec_fn = None
             if (SPECULATE_DIRECTION and type(self)._direction is LBFGS._direction and not self.constraints
-                    and _device_loop(g) and g.numel() < GRAM_MIN_DIM and not vector_space.current().sharded):
+                    and _device_loop(g) and g.numel() < GRAM_MIN_DIM and not vector_space.current().sharded
+                    and state.iter + 2 <= self.max_iterations):         # the next iteration can run
                 # plain L-BFGS: the next state is (x, g) as is (no L1 adjustment, no box projection)
-                spec_fn = lambda h: (lambda dn: (dn, self._prefetch_of(x, g, dn)))(h.apply_inverse(g, negate=True))
+                more = True
+                spec_fn = lambda h: (lambda dn: (dn, self._prefetch_of(x, g, dn),
+                                                 self._speculate_margins(objective, data, x, dn) if more else None))(
+                    h.apply_inverse(g, negate=True))
             _, gg, f_host, nxt = self.history.push_pair(x, state.coefficients, g, self._smooth_g, extra=f_dev,
                                                         speculate=spec_fn)
             if f_dev is not None:
                 f = f_host
             if nxt is not None:
-                self._spec = (x, g, nxt[0], nxt[1])
+                self._spec = (x, g, nxt[0], nxt[1], nxt[2])
         self._smooth_f, self._smooth_g = f, g
         self._inner_iter += 1
         adj_f, adj_g = self._adjust(x, f, g)
@@ -407,7 +440,7 @@ class OWLQN(LBFGS):
     def _prefetch(self, state, d):
         return None        # the orthant-masked direction is tested for zero before the search, as before
 
-    def _search(self, objective, data, state, d, pre=None):
+    def _search(self, objective, data, state, d, pre=None, spec_mls=None):
         x0 = state.coefficients
         pg = state.gradient
         orthant = torch.where(x0 != 0, torch.sign(x0), torch.sign(-pg))

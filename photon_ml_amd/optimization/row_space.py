@@ -214,6 +214,12 @@ class RowSpaceBatch:
         self.vslot = torch.nonzero(self.valid).squeeze(1)
         self.vrow = self.rows[self.vslot]
         self._z = None            # (beta, packed margins L beta) written by the fused solve
+        # the primal model (to_primal: one transpose pass over the block-diagonal data) is read once per model:
+        # build its shard-wide one-launch transpose tables here, with the rest of the setup, instead of running
+        # one launch per row chunk at every read (24 launches, 20.7 ms at config 5 vs one launch)
+        glm = getattr(seg, "glm", None)
+        if glm is not None and getattr(glm, "_multi_t", "unset") == "unset" and hasattr(glm, "_build_multi_t"):
+            glm._build_multi_t()
 
     def _slots(self, per_row: torch.Tensor) -> torch.Tensor:
         """Packed per-slot values of a per-row vector (0 in padding slots)."""

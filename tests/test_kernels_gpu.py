@@ -813,3 +813,35 @@ def test_wide_round_bases_on_device(precision, monkeypatch):
         dev.value_grad_sums(LOGISTIC, w.cuda(), 0.02)
         out[wb] = dev.hv_sums(LOGISTIC, w.cuda(), 0.02, v.cuda(), 0.0)[0].cpu()
     torch.testing.assert_close(out[1], out[0], rtol=1e-10, atol=1e-10 * float(out[0].abs().max()))
+
+
+@pytest.mark.parametrize("n", [1, 300, 1_000_003])
+def test_ls_dots_kernel(n):
+    """[g.d, d.d, x0.x0, x0.d] of a new L-BFGS direction in one launch vs torch fp64 dot products; bitwise equal
+    run to run (last-workgroup reduction in workgroup order)."""
+    from photon_ml_amd.ops.native import ls_dots
+    gen = torch.Generator(device="cuda").manual_seed(n)
+    x0, g, d = (torch.randn(n, dtype=torch.float64, device="cuda", generator=gen) for _ in range(3))
+    out = ls_dots(x0, g, d)
+    ref = torch.stack([torch.dot(g, d), torch.dot(d, d), torch.dot(x0, x0), torch.dot(x0, d)])
+    torch.testing.assert_close(out, ref, rtol=1e-12, atol=1e-12 * n)
+    assert torch.equal(ls_dots(x0, g, d), out)
+
+
+@pytest.mark.parametrize("name", ["LOGISTIC_LOSS", "POISSON_LOSS", "SQUARED_LOSS", "SMOOTHED_HINGE_LOSS"])
+def test_loss_evaluator_fused_kernel(name):
+    """Training-loss evaluators on device scores take the fused HIP pass (ls_eval_kernel at t = 0): same value as
+    the torch loss on the host to fp64 rounding."""
+    from photon_ml_amd.evaluation.evaluators import build_evaluator
+    from photon_ml_amd.ops.native import loss_sum
+    rng = np.random.default_rng(3)
+    n = 200_003
+    y = (rng.random(n) < 0.4).astype(float) if name != "POISSON_LOSS" else rng.poisson(2.0, n).astype(float)
+    if name == "SQUARED_LOSS":
+        y = rng.normal(size=n)
+    off, w, s = rng.normal(size=n) * 0.1, rng.random(n) + 0.5, rng.normal(size=n)
+    dev = build_evaluator(name, y, off, w, device="cuda")
+    host = build_evaluator(name, y, off, w, device="cpu")
+    v_dev, v_host = dev.evaluate(torch.from_numpy(s).cuda()), host.evaluate(torch.from_numpy(s))
+    assert abs(v_dev - v_host) <= 1e-11 * abs(v_host)
+    assert loss_sum(dev.loss.loss_id, torch.from_numpy(s + off).cuda(), dev.labels, dev.weights) is not None
