@@ -363,7 +363,8 @@ class RandomEffectCoordinate(Coordinate):
         vector with the row-space batch frozen."""
         ds, cfg = self.dataset, self.opt_config
         seg = ds.seg
-        seg.o = offs.to(seg.y.device, torch.float64)[ds.seg_rows]
+        offs = offs.to(seg.y.device, torch.float64)
+        seg.o = offs if getattr(ds, "seg_rows_identity", False) else offs[ds.seg_rows]
         seg._dzz_key = None
         comps = self._components(l1, cfg.optimizer_config)
         if comps is not None:
@@ -689,8 +690,11 @@ class RandomEffectCoordinate(Coordinate):
             # (or, when every entity was solved in its row space, L beta)
             rz = getattr(self, "_rs_scores", None)
             z = rz if rz is not None else ds.seg.glm.matvec(last[1])
-            out = torch.zeros(self.data.n_rows, dtype=torch.float64, device=z.device)
-            out[ds.seg_rows] = z
+            if getattr(ds, "seg_rows_identity", False) and z.numel() == self.data.n_rows:
+                out = z.clone()
+            else:
+                out = torch.zeros(self.data.n_rows, dtype=torch.float64, device=z.device)
+                out[ds.seg_rows] = z
             if len(ds.passive_rows):
                 pm = np.zeros(self.data.n_rows, dtype=bool)
                 pm[ds.passive_rows] = True

@@ -442,6 +442,10 @@ class RandomEffectDataset:
         self.projection_keys_t = ukeys
         self.col_entity_t = ukeys // D
         self.seg_rows = rows_t
+        # rows already grouped by entity and all active (generated / pre-sorted data): the per-update offset gather
+        # and score scatter through seg_rows are identities and are skipped
+        self.seg_rows_identity = bool(rows_t.numel() == len(y) and (
+            rows_t.numel() == 0 or bool((rows_t == torch.arange(rows_t.numel(), device=dev)).all())))
         self.seg = SegmentedGLMData(glm, e_row, self.col_entity_t, n_ent, yy, ww,
                                     torch.zeros_like(yy))
         self.d_total = d_total
