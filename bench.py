@@ -146,9 +146,14 @@ def main():
         for i in range(args.warmup):
             st = opt.step(obj, gdata)
             log(f"warmup {i + 1}/{args.warmup}: f={st.loss:.6e}")
+        if hasattr(opt, "drop_speculation"):
+            # the last warmup step queued the first timed step's direction + margin pass: drop it, so the timed
+            # window holds exactly `steps` forward and `steps` transpose passes
+            opt.drop_speculation()
         torch.cuda.synchronize()
         barrier()
         passes0 = data.n_passes
+        kpass0 = (getattr(data, "n_fwd", 0), getattr(data, "n_t", 0))
         t0 = time.perf_counter()
         with trace_range("bench timed steps"):  # roctx region (PML_TRACE=1) for timed-window profiles
             for i in range(args.steps):
@@ -159,6 +164,8 @@ def main():
         gnorm = st.grad_norm()
     elapsed = all_reduce_scalar(elapsed, "max", device=dev)
     passes = data.n_passes - passes0
+    # kernel passes launched inside the timed window (forward / transpose over the non-zeros)
+    kpass = (getattr(data, "n_fwd", 0) - kpass0[0], getattr(data, "n_t", 0) - kpass0[1])
     n_rows_local, layout_name = data.n_rows, data.layout
     stalled = bool(getattr(opt, "_finished", False))
     total_rows = int(all_reduce_scalar(n_rows_local, "sum", device=dev)) if is_dist() else n_rows_local
@@ -199,6 +206,8 @@ def main():
                 "layout": layout_name,
             },
             "evals_per_step": passes / args.steps,
+            "forward_passes_per_step": kpass[0] / args.steps,
+            "transpose_passes_per_step": kpass[1] / args.steps,
             "optimizer_stalled": stalled,
         }
         if game is not None:

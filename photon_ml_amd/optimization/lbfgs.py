@@ -60,6 +60,22 @@ def _device_loop(g: torch.Tensor) -> bool:
     return g.is_cuda and not vector_space.current().sharded and DEVICE_TWO_LOOP
 
 
+_PINNED = {}
+
+
+def _async_host(t: torch.Tensor):
+    """Queue a copy of the small device tensor ``t`` into a reused pinned host buffer; returns (buffer, event
+    recorded after the copy). The buffer is valid once the event has completed."""
+    key = t.device
+    buf = _PINNED.get(key)
+    if buf is None or buf.numel() < t.numel():
+        buf = _PINNED[key] = torch.empty(max(16, t.numel()), dtype=torch.float64, pin_memory=True)
+    buf[: t.numel()].copy_(t, non_blocking=True)
+    ev = torch.cuda.Event()
+    ev.record()
+    return buf, ev
+
+
 class _History:
     """Ring buffer of the last m (s, y) pairs plus rho = 1/(s.y) (host floats; for device vectors also 0-d
     device tensors rho_t and the newest pair's scaling s.y / y.y, so the two-loop never synchronises)."""
@@ -118,10 +134,15 @@ class _History:
             r = lbfgs_pair(x, x0, g, g0)
             if r is not None:
                 s, y, out = r
+                src = out if extra is None else torch.cat([out, extra.reshape(1).to(out)])
+                # the scalars leave the device BEFORE the speculative work is queued: the host resumes as soon as
+                # they are ready and does its bookkeeping while the GPU runs the next direction and margin pass
+                host, ev = _async_host(src)
                 # the speculative history has device scalars only: it must take the device two-loop
                 spec = (speculate(self._with_pair(s, y, out[2], out[3]))
                         if speculate is not None and len(self.rho_t) == len(self.s) else None)
-                vals = (out if extra is None else torch.cat([out, extra.reshape(1).to(out)])).tolist()
+                ev.synchronize()
+                vals = host[: src.numel()].tolist()
                 sy, yy, _, _, gg = vals[:5]
                 ex = vals[5] if extra is not None else None
                 if not (sy > 1e-300) or sy != sy:
@@ -230,6 +251,12 @@ class LBFGS(Optimizer):
         self._smooth_f = None
         self._smooth_g = None
         self._spec = None        # (x, g, direction, prefetch, margin search) queued for the next iteration
+
+    def drop_speculation(self):
+        """Forget the work queued for the next iteration (its direction and margin pass): that iteration then
+        computes both itself. Benchmarks call this between untimed and timed iterations, so no timed iteration's
+        work runs before the timer starts."""
+        self._spec = None
 
     def clear_inner_state(self):
         super().clear_inner_state()
