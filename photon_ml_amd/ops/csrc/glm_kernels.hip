@@ -1758,6 +1758,24 @@ __device__ __forceinline__ double swz_f64(double v) {
 // then broadcast ds_reads) instead of two ds_bpermute shuffles per element, with two accumulators.
 // V >= 2: group sums by DPP / swizzle steps instead of ds_bpermute butterflies (every step is symmetric, so all
 // lanes of a group hold bitwise the same sum).
+// L is lower triangular (Cholesky factor): only its n (n + 1) / 2 stored entries are staged, packed by rows
+// (row i at i (i + 1) / 2), which halves the LDS per problem -- for the n > 32 classes (one problem per wave) LDS
+// capped the occupancy at one wave per SIMD (33 KB per wave at n = 64). Full n x n rows are read from memory
+// (coalesced) and the upper triangle dropped.
+__device__ __forceinline__ void stage_lower(const double* __restrict__ A, long long b0, int count, int n,
+                                            double* sA) {
+  const int lane = threadIdx.x & 63;
+  const int nn = n * n, np = n * (n + 1) / 2;
+  const double* src = A + b0 * nn;
+  const int tot = count * nn;
+  for (int k = lane; k < tot; k += 64) {
+    const int p = k / nn, rem = k - p * nn;
+    const int i = rem / n, j = rem - i * n;
+    const double v = ldg_nt(src + k);
+    if (j <= i) sA[p * np + i * (i + 1) / 2 + j] = v;
+  }
+}
+
 template <int V>
 __global__ __launch_bounds__(NTHREADS) void rs_tron_kernel(
     int B, int n, int G, const double* __restrict__ Lm, const double* __restrict__ Y, const double* __restrict__ O,
@@ -1765,13 +1783,13 @@ __global__ __launch_bounds__(NTHREADS) void rs_tron_kernel(
     int* __restrict__ Reason, int loss, double l2, double tol, int max_iter, int max_fail, int max_cg) {
   extern __shared__ double smem[];
   const int lane = threadIdx.x & 63, w = threadIdx.x >> 6;
-  const int per = 64 / G, np = n * (n + 1);
+  const int per = 64 / G, np = n * (n + 1) / 2;    // packed lower triangle per problem
   double* sA = smem + w * per * (np + (V >= 1 ? G : 0));
   double* sv = sA + per * np + (lane / G) * G;   // V = 1: this problem's vector slot
   const long long b0 = ((long long)blockIdx.x * (blockDim.x >> 6) + w) * per;
   if (b0 >= B) return;
   const int count = (int)min((long long)per, B - b0);
-  stage_blocks(Lm, b0, count, n, sA);
+  stage_lower(Lm, b0, count, n, sA);
   const int g = lane / G, i = lane - g * G;
   const bool prob_on = g < count;
   const bool on = prob_on && i < n;
@@ -1804,18 +1822,23 @@ __global__ __launch_bounds__(NTHREADS) void rs_tron_kernel(
     __builtin_amdgcn_s_waitcnt(0);
     __builtin_amdgcn_wave_barrier();
   };
+  // packed lower triangle: L[r][c] (c <= r) at r (r + 1) / 2 + c; entries above the diagonal are 0 (reads past
+  // a row's end land in the next row and are masked)
   auto mv = [&](double v) {  // (L v)_i
+    const double* Lr = Lb + ii * (ii + 1) / 2;
     if constexpr (V >= 1) {
       put(v);
-      const double* Lr = Lb + ii * (n + 1);
       double a0 = 0.0, a1 = 0.0;
       int j = 0;
-      for (; j + 1 < n; j += 2) { a0 = fma(Lr[j], sv[j], a0); a1 = fma(Lr[j + 1], sv[j + 1], a1); }
-      if (j < n) a0 = fma(Lr[j], sv[j], a0);
+      for (; j + 1 < n; j += 2) {
+        a0 = fma(j <= ii ? Lr[j] : 0.0, sv[j], a0);
+        a1 = fma(j + 1 <= ii ? Lr[j + 1] : 0.0, sv[j + 1], a1);
+      }
+      if (j < n) a0 = fma(j <= ii ? Lr[j] : 0.0, sv[j], a0);
       return on ? a0 + a1 : 0.0;
     } else {
       double acc = 0.0;
-      for (int j = 0; j < n; ++j) acc = fma(Lb[ii * (n + 1) + j], __shfl(v, base + j, 64), acc);
+      for (int j = 0; j < n; ++j) acc = fma(j <= ii ? Lr[j] : 0.0, __shfl(v, base + j, 64), acc);
       return on ? acc : 0.0;
     }
   };
@@ -1825,14 +1848,14 @@ __global__ __launch_bounds__(NTHREADS) void rs_tron_kernel(
       double a0 = 0.0, a1 = 0.0;
       int r = 0;
       for (; r + 1 < n; r += 2) {
-        a0 = fma(Lb[r * (n + 1) + ii], sv[r], a0);
-        a1 = fma(Lb[(r + 1) * (n + 1) + ii], sv[r + 1], a1);
+        a0 = fma(r >= ii ? Lb[r * (r + 1) / 2 + ii] : 0.0, sv[r], a0);
+        a1 = fma(r + 1 >= ii ? Lb[(r + 1) * (r + 2) / 2 + ii] : 0.0, sv[r + 1], a1);
       }
-      if (r < n) a0 = fma(Lb[r * (n + 1) + ii], sv[r], a0);
+      if (r < n) a0 = fma(r >= ii ? Lb[r * (r + 1) / 2 + ii] : 0.0, sv[r], a0);
       return on ? a0 + a1 : 0.0;
     } else {
       double acc = 0.0;
-      for (int r = 0; r < n; ++r) acc = fma(Lb[r * (n + 1) + ii], __shfl(u, base + r, 64), acc);
+      for (int r = 0; r < n; ++r) acc = fma(r >= ii ? Lb[r * (r + 1) / 2 + ii] : 0.0, __shfl(u, base + r, 64), acc);
       return on ? acc : 0.0;
     }
   };
@@ -3059,7 +3082,7 @@ int pml_rs_tron(int B, int n, const double* L, const double* y, const double* of
   while (G < n) G <<= 1;
   const int per = 64 / G;
   const long long waves = (B + per - 1) / per;
-  const size_t wave_lds = (size_t)per * (n * (n + 1) + (V >= 1 ? G : 0)) * sizeof(double);
+  const size_t wave_lds = (size_t)per * (n * (n + 1) / 2 + (V >= 1 ? G : 0)) * sizeof(double);
   const int nw = (int)std::max<size_t>(1, std::min<size_t>(4, 65536 / wave_lds));
   const long long grid = (waves + nw - 1) / nw;
   if (V >= 2)
