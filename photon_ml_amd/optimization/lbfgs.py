@@ -414,9 +414,8 @@ class LBFGS(Optimizer):
                     and _device_loop(g) and g.numel() < GRAM_MIN_DIM and not vector_space.current().sharded
                     and state.iter + 2 <= self.max_iterations):         # the next iteration can run
                 # plain L-BFGS: the next state is (x, g) as is (no L1 adjustment, no box projection)
-                more = True
                 spec_fn = lambda h: (lambda dn: (dn, self._prefetch_of(x, g, dn),
-                                                 self._speculate_margins(objective, data, x, dn) if more else None))(
+                                                 self._speculate_margins(objective, data, x, dn)))(
                     h.apply_inverse(g, negate=True))
             _, gg, f_host, nxt = self.history.push_pair(x, state.coefficients, g, self._smooth_g, extra=f_dev,
                                                         speculate=spec_fn)
