@@ -46,6 +46,9 @@ SPECULATE_DIRECTION = os.environ.get("PML_LBFGS_SPECULATE", "1") != "0"
 # so the GPU never waits for the host between two iterations; skipped when the next iteration cannot run
 # (max_iterations), discarded when the pair is rejected or the data ran another pass in between
 SPECULATE_MARGINS = os.environ.get("PML_LBFGS_SPECULATE_MARGINS", "1") != "0"
+# ... only while the last loss drop exceeds this multiple of the loss tolerance (else the iteration likely stops on
+# the tolerance and the queued pass is wasted)
+SPECULATE_LOSS_MARGIN = float(os.environ.get("PML_LBFGS_SPECULATE_LOSS_MARGIN", "20"))
 # Two-loop as 2k + 1 fused HIP step kernels launched from C++ (no Python between launches); 0: torch recursion
 NATIVE_TWO_LOOP = os.environ.get("PML_LBFGS_NATIVE_TWO_LOOP", "1") != "0"
 # Device two-loop method for replicated vectors: "gram" = vector-free recursion on the device (one Gram pass, the
@@ -251,15 +254,34 @@ class LBFGS(Optimizer):
         self._smooth_f = None
         self._smooth_g = None
         self._spec = None        # (x, g, direction, prefetch, margin search) queued for the next iteration
+        self.wasted_spec_passes = 0   # speculative margin passes queued but never used (diagnostics)
 
     def drop_speculation(self):
         """Forget the work queued for the next iteration (its direction and margin pass): that iteration then
         computes both itself. Benchmarks call this between untimed and timed iterations, so no timed iteration's
         work runs before the timer starts."""
+        self._count_unused_spec()
         self._spec = None
+
+    def _count_unused_spec(self):
+        if self._spec is not None and self._spec[4] is not None:
+            self.wasted_spec_passes += 1
+
+    def _margin_speculation_pays(self, state: OptimizerState) -> bool:
+        """Whether to queue the next iteration's margin pass during the history push. The pass is wasted when the
+        iteration then stops on the loss tolerance (short warm-started GAME updates often do), so it is queued only
+        while the last loss drop is well above that tolerance (the drop shrinks geometrically near convergence)."""
+        if self.loss_abs_tol <= 0.0 or self.previous is None:
+            return True
+        try:
+            drop = float(self.previous.loss) - float(state.loss)
+        except (TypeError, ValueError):
+            return True
+        return drop > SPECULATE_LOSS_MARGIN * self.loss_abs_tol
 
     def clear_inner_state(self):
         super().clear_inner_state()
+        self._count_unused_spec()
         self.history.clear()
         self._failed_once = False
         self._finished = False
@@ -381,6 +403,8 @@ class LBFGS(Optimizer):
             return state
         from ..utils.timing import trace_range
         spec, self._spec = self._spec, None
+        if spec is not None and not (spec[0] is state.coefficients and spec[1] is state.gradient) and spec[4]:
+            self.wasted_spec_passes += 1
         try:
             with trace_range("two-loop direction"):
                 spec_mls = None
@@ -414,8 +438,10 @@ class LBFGS(Optimizer):
                     and _device_loop(g) and g.numel() < GRAM_MIN_DIM and not vector_space.current().sharded
                     and state.iter + 2 <= self.max_iterations):         # the next iteration can run
                 # plain L-BFGS: the next state is (x, g) as is (no L1 adjustment, no box projection)
+                with_mls = self._margin_speculation_pays(state)
                 spec_fn = lambda h: (lambda dn: (dn, self._prefetch_of(x, g, dn),
-                                                 self._speculate_margins(objective, data, x, dn)))(
+                                                 self._speculate_margins(objective, data, x, dn)
+                                                 if with_mls else None))(
                     h.apply_inverse(g, negate=True))
             _, gg, f_host, nxt = self.history.push_pair(x, state.coefficients, g, self._smooth_g, extra=f_dev,
                                                         speculate=spec_fn)

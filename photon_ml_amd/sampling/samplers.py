@@ -70,9 +70,20 @@ def next_seed() -> int:
 
 
 def reset_seed_sequence(seed: int = RANDOM_SEED):
-    """Restart the seed sequence (a fresh process in the reference; tests and resumed runs)."""
+    """Restart the seed sequence (a fresh process in the reference; tests)."""
     global _SEEDS
     _SEEDS = JavaRandom(seed)
+
+
+def seed_state() -> int:
+    """Position of the process-wide seed sequence (the LCG's 48-bit word): stored in GAME checkpoints so a resumed
+    run draws the same down-sampling seeds as an uninterrupted one."""
+    return int(_SEEDS._s)
+
+
+def set_seed_state(state: int):
+    """Restore a position saved by :func:`seed_state` (checkpoint resume)."""
+    _SEEDS._s = int(state) & JavaRandom._MASK
 
 
 class DownSampler:

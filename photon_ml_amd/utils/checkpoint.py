@@ -11,8 +11,9 @@ persists final models; Spark lineage recomputation was its only recovery).
 
 Format: safetensors (tensors / numpy arrays only, nothing executable) + a JSON metadata string. Every rank of a
 process group writes its own file (entity-sharded random effects differ per rank). ``format_version`` 2 stores
-entity-id tables length-prefixed and the writer's world size; version-less files of the first format (ids joined
-by newlines, no world size) still load.
+entity-id tables length-prefixed and the writer's world size; version-less files still load: those with a world
+size are length-prefixed (builds that predate the version field), the others are sniffed (first format: ids joined
+by newlines).
 """
 from __future__ import annotations
 
@@ -48,8 +49,21 @@ def _strings_to_array(values) -> np.ndarray:
     return np.frombuffer(head + b"".join(enc), dtype=np.uint8).copy()
 
 
-def _array_to_strings(a: np.ndarray, n: int, version: int = FORMAT_VERSION) -> np.ndarray:
+def _is_length_prefixed(raw: bytes, n: int) -> bool:
+    """True when ``raw`` parses as a length-prefixed table of exactly ``n`` ids (count header and lengths add up)."""
+    if len(raw) < 8 + 8 * n or int(np.frombuffer(raw[:8], dtype="<i8")[0]) != n:
+        return False
+    lens = np.frombuffer(raw[8:8 + 8 * n], dtype="<i8")
+    return bool((lens >= 0).all()) and 8 + 8 * n + int(lens.sum()) == len(raw)
+
+
+def _array_to_strings(a: np.ndarray, n: int, version: Optional[int] = FORMAT_VERSION) -> np.ndarray:
+    """Decode an entity-id table. ``version`` None = a file without ``format_version``: builds between the two
+    formats already wrote length-prefixed tables without the version field, so the layout is sniffed (a table
+    whose count header and lengths add up exactly is length-prefixed; otherwise newline-joined)."""
     raw = bytes(np.ascontiguousarray(a).tobytes())
+    if version is None:
+        version = 2 if _is_length_prefixed(raw, n) else 1
     if version < 2:     # first format: UTF-8 ids joined by newlines
         ids = raw.decode("utf-8").split("\n") if n else []
         if len(ids) != n:
@@ -92,7 +106,8 @@ def game_model_to_arrays(model, prefix: str) -> Tuple[Dict[str, np.ndarray], dic
     return arrays, meta
 
 
-def game_model_from_arrays(arrays: Dict[str, np.ndarray], meta: dict, prefix: str, version: int = FORMAT_VERSION):
+def game_model_from_arrays(arrays: Dict[str, np.ndarray], meta: dict, prefix: str,
+                           version: Optional[int] = FORMAT_VERSION):
     from ..models.game import FixedEffectModel, GameModel, RandomEffectModel
     from ..models.glm import Coefficients, model_for_task
     models = OrderedDict()
@@ -151,10 +166,11 @@ class Checkpointer:
     # ---- coordinate descent state
     def save_cd(self, model, iteration: int, next_coordinate: int, best_model, best_evals, history: List[dict],
                 tag: str = ""):
+        from ..sampling.samplers import seed_state
         arrays, meta = game_model_to_arrays(model, "model/")
         meta = {"model": meta, "iteration": iteration, "next": next_coordinate, "tag": tag,
                 "history": history, "best_evals": best_evals, "world_size": _world(),
-                "format_version": FORMAT_VERSION}
+                "format_version": FORMAT_VERSION, "sampler_seed_state": seed_state()}
         if best_model is not None:
             ba, bm = game_model_to_arrays(best_model, "best/")
             arrays.update(ba)
@@ -166,8 +182,10 @@ class Checkpointer:
         if got is None:
             return None
         arrays, meta = got
-        version = int(meta.get("format_version", 1))
-        if version > FORMAT_VERSION:
+        # no format_version: either the first (newline) format or a length-prefixed build that predates the field
+        # (those already recorded world_size); the id tables are sniffed per coordinate in that case
+        version = int(meta["format_version"]) if "format_version" in meta else (2 if "world_size" in meta else None)
+        if version is not None and version > FORMAT_VERSION:
             raise RuntimeError(f"checkpoint {self.path} has format version {version}; this build reads <= "
                                f"{FORMAT_VERSION}")
         if "world_size" not in meta:
@@ -177,6 +195,10 @@ class Checkpointer:
             # entity-sharded random effects: each rank's file holds the entities that rank owned
             raise RuntimeError(f"checkpoint {self.path} was written by {meta['world_size']} ranks, "
                                f"this run has {_world()}: resume with the same world size")
+        if "sampler_seed_state" in meta:
+            # down-sampling seeds continue where the interrupted run stopped (bitwise resume with down-sampling)
+            from ..sampling.samplers import set_seed_state
+            set_seed_state(meta["sampler_seed_state"])
         model = game_model_from_arrays(arrays, meta["model"], "model/", version)
         best = game_model_from_arrays(arrays, meta["best"], "best/", version) if "best" in meta else None
         return {"model": model, "iteration": meta["iteration"], "next": meta["next"], "best_model": best,

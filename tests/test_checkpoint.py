@@ -161,3 +161,58 @@ def test_first_format_checkpoint_still_loads(tmp_path):
     c.save(arrays, dict(meta, format_version=ck.FORMAT_VERSION + 1))
     with pytest.raises(RuntimeError, match="format version"):
         c.load_cd()
+
+
+@pytest.mark.parametrize("with_world_size", [True, False])
+def test_versionless_length_prefixed_checkpoint_loads(tmp_path, with_world_size):
+    """Builds between the two formats wrote length-prefixed id tables (and a world size) WITHOUT format_version;
+    such files must not be decoded as newline-joined ids. Without the world size the table is sniffed."""
+    from photon_ml_amd.utils import checkpoint as ck
+    ids = ["u1", "a\nb", "ü"]
+    meta = {"model": {"coordinates": [{"id": "per-user", "kind": "random", "shard": "s", "re_type": "userId",
+                                       "task": "LINEAR_REGRESSION", "dim": 4, "n_entities": 3}]},
+            "iteration": 1, "next": 0}
+    if with_world_size:
+        meta["world_size"] = 1
+    arrays = {"model/per-user.keys": np.array([0, 5, 11], dtype=np.int64),
+              "model/per-user.values": np.array([1.0, 2.0, 3.0]),
+              "model/per-user.entities": ck._strings_to_array(ids)}
+    c = ck.Checkpointer(str(tmp_path))
+    c.save(arrays, meta)
+    m = c.load_cd()["model"].get("per-user")
+    assert list(m.entity_ids) == ids
+
+
+def test_resume_with_down_sampling_draws_the_same_samples(tmp_path):
+    """The down-sampling seed sequence position is part of the checkpoint: a run resumed in a fresh
+    process trains its down-sampled fixed-effect updates on the same samples as an uninterrupted run."""
+    from photon_ml_amd.sampling.samplers import reset_seed_sequence
+
+    def setup():
+        data, val, coords, evs = _setup(seed=7)
+        cfg = GLMOptimizationConfiguration(OptimizerConfig("TRON", 30, 1e-9), RegularizationContext("L2"), 1.0, 0.5)
+        coords["g"] = FixedEffectCoordinate("g", data, FixedEffectDataConfiguration("global"), cfg,
+                                            "LOGISTIC_REGRESSION", device="cpu")
+        return coords, val, evs
+
+    reset_seed_sequence()
+    coords, val, evs = setup()
+    full_model, _ = CoordinateDescent(coords, None, val, evs).run(3)
+
+    reset_seed_sequence()
+    coords, val, evs = setup()
+    calls = {"n": 0}
+
+    def bomb(rec):
+        calls["n"] += 1
+        if calls["n"] == 4:   # after "g" of sweep 2 (its seed drawn), before "u"
+            raise Interrupt()
+    ck = Checkpointer(str(tmp_path), "cd")
+    with pytest.raises(Interrupt):
+        CoordinateDescent(coords, None, val, evs, event_callback=bomb).run(3, checkpointer=ck, tag="t")
+    reset_seed_sequence()     # a fresh process starts the sequence from the beginning
+    coords, val, evs = setup()
+    model, _ = CoordinateDescent(coords, None, val, evs).run(3, checkpointer=Checkpointer(str(tmp_path), "cd"),
+                                                            tag="t")
+    torch.testing.assert_close(model.get("g").glm.coefficients.means, full_model.get("g").glm.coefficients.means,
+                               rtol=0, atol=1e-10)
