@@ -71,8 +71,12 @@ def main():
                     help="sparse layout: tiled (gather-coalesced, default when representable) or segmented")
     ap.add_argument("--game", default="auto", choices=["auto", "on", "off"],
                     help="after the timed GLM steps, also time BASELINE.json's GAME metric (coordinate-descent sweeps "
-                         "of config 5 with power-law entity sizes, bench_game.py --config game5pl) and report it as "
-                         "extra keys; auto = on for one GPU")
+                         "of config 5 with power-law entity sizes, bench_game.py --config game5pl; entity-sharded over "
+                         "the ranks when N > 1) with bf16 and with fp64 fixed-effect features, reported as extra "
+                         "keys; auto = on for the lbfgs config")
+    ap.add_argument("--rehearsal", action="store_true",
+                    help="allow more ranks than physical devices (several ranks per GPU, or CPU ranks); the record "
+                         "then says rehearsal: true, and n_gpus counts devices, not ranks")
     args = ap.parse_args()
     cfg = CONFIGS[args.config]
     if args.rows_per_gpu is None:
@@ -87,11 +91,17 @@ def main():
 
     import torch
     from photon_ml_amd.parallel.dist import init_distributed, DistributedGLMData, all_reduce_scalar, barrier, is_dist
+    from photon_ml_amd.parallel.dist import distinct_devices
     rank, world, local = init_distributed()
     assert world == args.gpus, (world, args.gpus)
     local = local % max(torch.cuda.device_count(), 1)  # several ranks may share a GPU in rehearsal runs
     torch.cuda.set_device(local)
     dev = torch.device("cuda", local)
+    n_dev = distinct_devices(dev)
+    if n_dev < world and not args.rehearsal:
+        log(f"error: {world} ranks on {n_dev} physical device(s): refusing to report them as {world} GPUs "
+            f"(pass --rehearsal for a multi-rank rehearsal on fewer devices)")
+        sys.exit(2)
 
     from photon_ml_amd.data.synthetic import generate_device_shard
     from photon_ml_amd.utils.timing import trace_range
@@ -171,7 +181,7 @@ def main():
     total_rows = int(all_reduce_scalar(n_rows_local, "sum", device=dev)) if is_dist() else n_rows_local
     value = total_rows * args.steps / elapsed
     game = None
-    if args.game == "on" or (args.game == "auto" and world == 1 and args.config == "lbfgs"):
+    if args.game == "on" or (args.game == "auto" and args.config == "lbfgs"):
         # free the GLM shard (115 GiB) before the GAME data is built on the same GPU
         del data, gdata, opt, obj, w0
         import gc
@@ -185,7 +195,8 @@ def main():
             "metric": cfg["metric"],
             "value": value,
             "unit": "examples/sec",
-            "n_gpus": world,
+            "n_gpus": n_dev,
+            "n_ranks": world,
             "steps": args.steps,
             "warmup": args.warmup,
             "ms_per_step": 1000.0 * elapsed / args.steps,
@@ -210,6 +221,8 @@ def main():
             "transpose_passes_per_step": kpass[1] / args.steps,
             "optimizer_stalled": stalled,
         }
+        if args.rehearsal:
+            out["rehearsal"] = True
         if game is not None:
             out.update(game)
         print(json.dumps(out), flush=True)
@@ -218,16 +231,38 @@ def main():
 def game_extra(dev, rank: int, world: int) -> dict:
     """BASELINE.json's second metric (GAME coordinate-descent iterations/sec, config 5) on the power-law entity
     preset, timed inside this run (bench_game.run: data generated on the device, 2 warmup + 3 timed sweeps, the
-    trained model materialised inside the timed region). Failures are reported, never fatal to the GLM line."""
+    trained model materialised inside the timed region; entity-sharded random effects when world > 1). Timed twice
+    on the same data: bf16 fixed-effect feature storage (``game5pl_*``) and fp64, the reference's precision
+    (``game5pl_f64_*``). Failures are reported, never fatal to the GLM line."""
+    import gc
     import bench_game
+    import torch
+    out = {}
     try:
-        g = bench_game.run(bench_game.preset_args("game5pl", steps=3, warmup=2), dev, rank, world)
+        args = bench_game.preset_args("game5pl", steps=3, warmup=2)
+        data, t_data = bench_game.make_data(args, dev, rank)
     except Exception as e:  # pragma: no cover - reported in the record
         return {"game5pl_error": repr(e)[:500]}
-    return {"game5pl_sweeps_per_sec": g["value"], "game5pl_ms_per_sweep": g["ms_per_step"],
-            "game5pl_config": dict(g["config"], fe_dtype=g["dtype"], re_dtype="fp64", steps=g["steps"],
-                                   warmup=g["warmup"], data_generation_s=round(g["data_generation_s"], 1),
-                                   coordinate_build_s=round(g["coordinate_build_s"], 1))}
+    for prec, pre in (("bf16", "game5pl"), ("f64", "game5pl_f64")):
+        try:
+            args.precision = prec
+            g = bench_game.run(args, dev, rank, world, data=data, t_data=t_data)
+        except Exception as e:  # pragma: no cover - reported in the record
+            out[f"{pre}_error"] = repr(e)[:500]
+            continue
+        finally:
+            gc.collect()
+            torch.cuda.empty_cache()
+        out.update({f"{pre}_sweeps_per_sec": g["value"], f"{pre}_ms_per_sweep": g["ms_per_step"],
+                    f"{pre}_sweep_ms_min": g["sweep_ms_min"], f"{pre}_sweep_ms_median": g["sweep_ms_median"],
+                    f"{pre}_coordinate_ms": g["coordinate_ms"]})
+        if prec == "bf16":
+            out["game5pl_config"] = dict(g["config"], fe_dtype=g["dtype"], re_dtype="fp64", steps=g["steps"],
+                                         warmup=g["warmup"], data_generation_s=round(g["data_generation_s"], 1),
+                                         coordinate_build_s=round(g["coordinate_build_s"], 1))
+        else:
+            out["game5pl_f64_coordinate_build_s"] = round(g["coordinate_build_s"], 1)
+    return out
 
 
 if __name__ == "__main__":

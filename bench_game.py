@@ -82,6 +82,8 @@ def build_parser() -> argparse.ArgumentParser:
     ap.add_argument("--host-data", action="store_true",
                     help="generate the synthetic data with host numpy (minutes at config 5) instead of on the device")
     ap.add_argument("--seed", type=int, default=11)
+    ap.add_argument("--rehearsal", action="store_true",
+                    help="allow more ranks than physical devices (record: rehearsal true, n_gpus = devices)")
     ap.add_argument("--log-level", default="WARNING",
                     help="framework log level (DEBUG shows the per-phase timings of the random-effect update)")
     return ap
@@ -124,27 +126,24 @@ def main():
         dev = torch.device("cuda", local)
     else:
         dev = torch.device("cpu")
+    from photon_ml_amd.parallel.dist import distinct_devices
+    n_dev = distinct_devices(dev)
+    if n_dev < world and not args.rehearsal:
+        log(f"error: {world} ranks on {n_dev} physical device(s): refusing to report them as {world} GPUs "
+            f"(pass --rehearsal for a multi-rank rehearsal on fewer devices)")
+        sys.exit(2)
     rec = run(args, dev, rank, world)
+    rec["n_gpus"], rec["n_ranks"] = n_dev, world
+    if args.rehearsal:
+        rec["rehearsal"] = True
     if rank == 0:
         print(json.dumps(rec), flush=True)
 
 
-def run(args, dev, rank: int = 0, world: int = 1) -> dict:
-    """Generate the preset's data, build the coordinates, run ``args.warmup`` untimed and ``args.steps`` timed
-    coordinate-descent sweeps; returns the JSON record (rank 0's view; max time over ranks)."""
-    import numpy as np
+def make_data(args, dev, rank: int = 0):
+    """The preset's synthetic data for this rank (device generator on a GPU); returns (data, seconds)."""
     import torch
-    from collections import OrderedDict
-    from photon_ml_amd.parallel.dist import all_reduce_scalar, barrier, is_dist
-    from photon_ml_amd.algorithm.coordinate_descent import CoordinateDescent
-    from photon_ml_amd.algorithm.coordinates import (FixedEffectCoordinate, RandomEffectCoordinate,
-                                                     ShardedRandomEffectCoordinate)
-    from photon_ml_amd.data.random_effect import FixedEffectDataConfiguration, RandomEffectDataConfiguration
     from photon_ml_amd.data.synthetic import generate_game_bench_data, generate_game_bench_data_device
-    from photon_ml_amd.evaluation.evaluators import build_evaluator
-    from photon_ml_amd.optimization.config import (GLMOptimizationConfiguration, OptimizerConfig,
-                                                   RegularizationContext)
-
     t0 = time.time()
     gen_kw = dict(seed=args.seed + 1000 * rank, entity_offset=rank * args.entities_per_gpu, pool=args.pool,
                   int_ids=bool(args.int_ids), sizes=args.sizes or "uniform")
@@ -159,6 +158,27 @@ def run(args, dev, rank: int = 0, world: int = 1) -> dict:
     t_data = time.time() - t0
     log(f"data generated in {t_data:.1f}s ({'host' if args.host_data or dev.type != 'cuda' else 'device'}): "
         f"{data.n_rows} rows/GPU")
+    return data, t_data
+
+
+def run(args, dev, rank: int = 0, world: int = 1, data=None, t_data: float = 0.0) -> dict:
+    """Generate the preset's data (unless given), build the coordinates (fixed-effect storage precision
+    ``args.precision``), run ``args.warmup`` untimed and ``args.steps`` timed coordinate-descent sweeps; returns the
+    JSON record (rank 0's view; max time over ranks) with the per-sweep min / median next to the mean."""
+    import numpy as np
+    import torch
+    from collections import OrderedDict
+    from photon_ml_amd.parallel.dist import all_reduce_scalar, barrier, is_dist
+    from photon_ml_amd.algorithm.coordinate_descent import CoordinateDescent
+    from photon_ml_amd.algorithm.coordinates import (FixedEffectCoordinate, RandomEffectCoordinate,
+                                                     ShardedRandomEffectCoordinate)
+    from photon_ml_amd.data.random_effect import FixedEffectDataConfiguration, RandomEffectDataConfiguration
+    from photon_ml_amd.evaluation.evaluators import build_evaluator
+    from photon_ml_amd.optimization.config import (GLMOptimizationConfiguration, OptimizerConfig,
+                                                   RegularizationContext)
+
+    if data is None:
+        data, t_data = make_data(args, dev, rank)
     t0 = time.time()
     fe_cfg = GLMOptimizationConfiguration(OptimizerConfig("LBFGS", args.fe_iters, 1e-12),
                                           RegularizationContext("L2"), 1.0, args.fe_down_sampling_rate)
@@ -175,15 +195,22 @@ def run(args, dev, rank: int = 0, world: int = 1) -> dict:
     if torch.cuda.is_available():
         torch.cuda.synchronize()
     t_build = time.time() - t0
-    log(f"coordinates built in {t_build:.1f}s; RE: {coords['per-entity'].dataset.summary()}")
+    log(f"coordinates built in {t_build:.1f}s (fixed effect {args.precision}); RE: "
+        f"{coords['per-entity'].dataset.summary()}")
     train_eval = build_evaluator("LOGISTIC_LOSS", data.response, data.offsets, data.weights, device=dev)
-    cd = CoordinateDescent(coords, train_eval, score_device=dev)
+    sweep_end = []
+    n_coords = len(coords)
+    # the training loss after every coordinate update is a host float (a synchronisation), so these stamps are
+    # device-complete times; one stamp per sweep (after its last coordinate)
+    cb = lambda rec: sweep_end.append(time.perf_counter()) if rec["coordinate"] == list(coords)[-1] else None
+    cd = CoordinateDescent(coords, train_eval, score_device=dev, event_callback=cb)
     model, _ = cd.run(args.warmup)
     if torch.cuda.is_available():
         torch.cuda.synchronize()
     barrier()
     fe_gd = coords["global"].glm_data
     fe_pass0 = (getattr(fe_gd, "n_fwd", 0), getattr(fe_gd, "n_t", 0))
+    sweep_end.clear()
     t1 = time.perf_counter()
     from photon_ml_amd.utils.timing import trace_range
     with trace_range("timed sweeps"):
@@ -195,9 +222,14 @@ def run(args, dev, rank: int = 0, world: int = 1) -> dict:
             if torch.cuda.is_available():
                 torch.cuda.synchronize()
     barrier()
-    elapsed = all_reduce_scalar(time.perf_counter() - t1, "max")
+    t_end = time.perf_counter()
+    elapsed = all_reduce_scalar(t_end - t1, "max")
+    stamps = [t1] + sweep_end[-args.steps:]
+    sweeps_ms = [1000.0 * (b - a) for a, b in zip(stamps[:-1], stamps[1:])]
+    sweeps_ms = [all_reduce_scalar(v, "max") for v in sweeps_ms]
     log(f"fixed effect per sweep: {(getattr(fe_gd, 'n_fwd', 0) - fe_pass0[0]) / args.steps:.1f} forward + "
-        f"{(getattr(fe_gd, 'n_t', 0) - fe_pass0[1]) / args.steps:.1f} transpose passes")
+        f"{(getattr(fe_gd, 'n_t', 0) - fe_pass0[1]) / args.steps:.1f} transpose passes; sweeps (ms): "
+        f"{', '.join(f'{v:.1f}' for v in sweeps_ms)}")
     loss = cd.history[-1].get("training_loss")
     coord_ms = {}
     for rec in cd.history[-2 * args.steps:]:
@@ -224,6 +256,7 @@ def run(args, dev, rank: int = 0, world: int = 1) -> dict:
                 f"{fb:.3f}, transpose items {ft:.3f}")
         for rec in cd.history[-2 * args.steps:]:
             log(f"  iteration {rec.get('iteration')} coordinate {rec['coordinate']}: {rec['seconds']:.3f}s")
+    del cd, coords, model, train_eval
     return {
         "metric": "GAME coord-descent iters/sec (fixed + per-entity random effect)",
         "value": args.steps / elapsed,
@@ -232,6 +265,8 @@ def run(args, dev, rank: int = 0, world: int = 1) -> dict:
         "steps": args.steps,
         "warmup": args.warmup,
         "ms_per_step": 1000.0 * elapsed / args.steps,
+        "sweep_ms_min": min(sweeps_ms) if sweeps_ms else None,
+        "sweep_ms_median": float(np.median(sweeps_ms)) if sweeps_ms else None,
         "higher_is_better": True,
         "scaling": "weak",
         "vs_baseline": None,

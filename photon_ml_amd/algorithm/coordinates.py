@@ -723,34 +723,53 @@ class ShardedRandomEffectCoordinate(Coordinate):
     def __init__(self, coordinate_id: str, data: GameData, data_config: RandomEffectDataConfiguration,
                  opt_config: GLMOptimizationConfiguration, task, compute_variance: bool = False, device=None,
                  dtype=torch.float64):
-        from ..parallel.sharding import EntityPartitioner, RowRouter, stable_hash64
+        from ..parallel.sharding import EntityPartitioner, RowRouter, entity_keys
         self.coordinate_id = coordinate_id
         self.data_config = data_config
         self.device = torch.device(device) if device is not None else default_device()
         re_type, shard = data_config.random_effect_type, data_config.feature_shard_id
         ids = np.asarray(data.id_tags[re_type])
-        keys = stable_hash64(ids)
-        self.partitioner = EntityPartitioner.build(keys)
-        self.router = RowRouter(self.partitioner.owner(keys))
-        self.recv_data = self._route(data, self.router, ids)
+        self.route_times = {}
+        t0 = time.perf_counter()
+        # entity keys, the partitioner's histograms and the routing permutation all on the device (C8 / C9)
+        keys = entity_keys(ids, self.device)
+        self.partitioner = EntityPartitioner.build_t(keys)
+        self.router = RowRouter(self.partitioner.owner_t(keys))
+        del keys
+        self._sync()
+        self.route_times["partition"] = time.perf_counter() - t0
+        self.recv_data = self._route(data, self.router, ids, self.route_times)
         self.inner = RandomEffectCoordinate(coordinate_id, self.recv_data, data_config, opt_config, task,
                                             compute_variance, device, dtype)
         self._val_cache = {}
 
-    def _route(self, data: GameData, router, ids) -> GameData:
-        """Move this coordinate's rows to the owners of their entities (C8): the feature rows (device-side
-        permutation + all-to-all), the per-row vectors, and the entity ids — integer ids as one int64
-        all-to-all, string ids as codes plus only the distinct names each owner needs
-        (``RowRouter.forward_strings``)."""
+    def _sync(self):
+        if self.device.type == "cuda":
+            torch.cuda.synchronize(self.device)
+
+    def _route(self, data: GameData, router, ids, times: Optional[dict] = None) -> GameData:
+        """Move this coordinate's rows to the owners of their entities (C8): the feature rows stay device tensors
+        end to end (device permutation + all-to-all, kept as a :class:`DeviceCSR` for the device dataset build),
+        the per-row vectors and integer entity ids as one all-to-all each; string ids as codes plus only the
+        distinct names each owner needs (``RowRouter.forward_strings``). ``times``: per-phase seconds."""
         re_type, shard = self.data_config.random_effect_type, self.data_config.feature_shard_id
-        fwd = lambda a: router.forward(torch.from_numpy(np.ascontiguousarray(a))).numpy()
+        dev = self.device
+        fwd = lambda a: router.forward(torch.from_numpy(np.ascontiguousarray(a)).to(dev)).cpu().numpy()
+        times = {} if times is None else times
         with Timed(f"RE {self.coordinate_id}: route rows to entity owners", log, logging.INFO):
-            x = router.forward_csr(data.shard(shard))
+            t0 = time.perf_counter()
+            x = router.forward_csr_device(data.shard(shard), dev)
+            self._sync()
+            t1 = time.perf_counter()
             ids = np.asarray(ids)
             recv_ids = fwd(ids.astype(np.int64)) if ids.dtype.kind in "iu" else router.forward_strings(ids)
             tags = {re_type: recv_ids}
-            return GameData(fwd(data.response), {shard: x}, tags, fwd(data.offsets), fwd(data.weights),
-                            fwd(data.uids), None)
+            out = GameData(fwd(data.response), {shard: x}, tags, fwd(data.offsets), fwd(data.weights),
+                           fwd(data.uids), None)
+            t2 = time.perf_counter()
+            times.update(rows=t1 - t0, vectors=t2 - t1)
+            log.info("RE %s routing: %s", self.coordinate_id, {k: round(v, 3) for k, v in times.items()})
+            return out
 
     @property
     def dataset(self):
@@ -778,11 +797,11 @@ class ShardedRandomEffectCoordinate(Coordinate):
 
     def score_validation(self, model, vdata: GameData) -> torch.Tensor:
         """Route validation rows to entity owners once (cached per dataset), score there, route back."""
-        from ..parallel.sharding import RowRouter, stable_hash64
+        from ..parallel.sharding import RowRouter, entity_keys
         key = id(vdata)
         if key not in self._val_cache:
             ids = np.asarray(vdata.id_tags[self.data_config.random_effect_type])
-            router = RowRouter(self.partitioner.owner(stable_hash64(ids)))
+            router = RowRouter(self.partitioner.owner_t(entity_keys(ids, self.device)))
             self._val_cache[key] = (router, self._route(vdata, router, ids))
         router, recv = self._val_cache[key]
         s = model.score(recv, self.device).to(torch.float64)

@@ -14,8 +14,60 @@ import numpy as np
 import scipy.sparse as sp
 
 
+class DeviceCSR:
+    """A CSR feature shard resident on a device (torch tensors): what entity-sharded routing produces, handed to
+    the device random-effect build and the scoring kernels without a host round trip. Minimal
+    scipy-like surface (``shape``, ``nnz``, ``tocsr``, row subsets); :meth:`to_scipy` copies to the host for the
+    host-only code paths."""
+
+    def __init__(self, indptr, indices, data, shape, has_sorted_indices: bool = False):
+        import torch
+        self.indptr = indptr.to(torch.int64)
+        self.indices = indices
+        self.data = data.to(torch.float64)
+        self.shape = (int(shape[0]), int(shape[1]))
+        self.has_sorted_indices = bool(has_sorted_indices)
+        self._pml_dev_cache = {}
+
+    @property
+    def device(self):
+        return self.data.device
+
+    @property
+    def nnz(self) -> int:
+        return int(self.data.numel())
+
+    def tocsr(self):
+        return self
+
+    def to_scipy(self) -> sp.csr_matrix:
+        m = sp.csr_matrix((self.data.cpu().numpy(), self.indices.cpu().numpy().astype(np.int32, copy=False),
+                           self.indptr.cpu().numpy()), shape=self.shape)
+        m.has_sorted_indices = self.has_sorted_indices
+        return m
+
+    def __getitem__(self, rows) -> "DeviceCSR":
+        """Row subset (an index array / mask over rows), gathered on the device."""
+        import torch
+        dev = self.data.device
+        r = torch.as_tensor(np.asarray(rows) if not isinstance(rows, torch.Tensor) else rows, device=dev)
+        if r.dtype == torch.bool:
+            r = torch.nonzero(r).squeeze(1)
+        r = r.to(torch.int64)
+        lens = (self.indptr[1:] - self.indptr[:-1])[r]
+        ip = torch.zeros(r.numel() + 1, dtype=torch.int64, device=dev)
+        torch.cumsum(lens, 0, out=ip[1:])
+        tot = int(ip[-1])
+        src = torch.repeat_interleave(self.indptr[:-1][r] - ip[:-1], lens, output_size=tot)
+        src += torch.arange(tot, device=dev)
+        return DeviceCSR(ip, self.indices[src], self.data[src], (r.numel(), self.shape[1]), self.has_sorted_indices)
+
+
 def as_csr(x, n_cols: Optional[int] = None) -> sp.csr_matrix:
-    """Coerce dense arrays / scipy matrices to canonical float64 CSR with sorted indices."""
+    """Coerce dense arrays / scipy matrices to canonical float64 CSR with sorted indices (device-resident
+    :class:`DeviceCSR` shards pass through unchanged)."""
+    if isinstance(x, DeviceCSR):
+        return x
     if sp.issparse(x):
         m = x.tocsr().astype(np.float64)
     else:

@@ -26,7 +26,7 @@ import torch
 from ..constants import EPSILON
 from ..projector.projectors import (IndexMapProjection, ProjectorKind, ProjectorType, gaussian_projection_matrix)
 from .game_data import GameData
-from .matrix import LabeledData
+from .matrix import DeviceCSR, LabeledData
 
 
 @dataclass
@@ -132,6 +132,10 @@ class RandomEffectDataset:
         self.dtype = dtype
         re_type, shard_id = config.random_effect_type, config.feature_shard_id
         x = data.shard(shard_id)
+        if isinstance(x, DeviceCSR) and not (
+                self.device.type == "cuda" and layout in ("auto", "segmented")
+                and config.projector_type.kind == ProjectorKind.INDEX_MAP and config.features_to_samples_ratio is None):
+            x = x.to_scipy()      # device-resident rows (entity-sharded routing) on a host-only build path
         self.dim = x.shape[1]
         ids = data.id_tags[re_type]
         ids_s = ids.astype(str) if ids.dtype == object else ids
@@ -406,7 +410,12 @@ class RandomEffectDataset:
         from ..optimization.batched import SegmentedGLMData
         dev, D = self.device, self.dim
         xa = xa.tocsr()
-        ip = torch.from_numpy(xa.indptr.astype(np.int64)).to(dev)
+        if isinstance(xa, DeviceCSR):        # routed rows already on the device: no host copy
+            ip = xa.indptr.to(dev)
+            x_ind, x_val = xa.indices.to(dev), xa.data.to(dev)
+        else:
+            ip = torch.from_numpy(xa.indptr.astype(np.int64)).to(dev)
+            x_ind, x_val = torch.from_numpy(xa.indices).to(dev), torch.from_numpy(xa.data).to(dev, torch.float64)
         ea_t = torch.from_numpy(ea.astype(np.int64)).to(dev)
         order = torch.argsort(ea_t, stable=True)
         lens = (ip[1:] - ip[:-1])[order]
@@ -416,14 +425,20 @@ class RandomEffectDataset:
         src = torch.repeat_interleave(ip[:-1][order] - nip[:-1], lens, output_size=nnz)
         src += torch.arange(nnz, device=dev)
         del ip
-        col = torch.from_numpy(xa.indices).to(dev)[src].to(torch.int64)
-        val = torch.from_numpy(xa.data).to(dev, torch.float64)[src]
-        del src
+        col = x_ind[src].to(torch.int64)
+        val = x_val[src]
+        del src, x_ind, x_val
         e_row = ea_t[order]
         key = torch.repeat_interleave(e_row, lens, output_size=nnz) * D + col
         del col, lens
         allk = key
-        if len(passive_rows):
+        if len(passive_rows) and isinstance(x, DeviceCSR):
+            sub = x[passive_rows]
+            plen = sub.indptr[1:] - sub.indptr[:-1]
+            pe = torch.from_numpy(ent[passive_rows].astype(np.int64)).to(dev)
+            pk = torch.repeat_interleave(pe, plen.to(dev), output_size=sub.nnz) * D + sub.indices.to(dev, torch.int64)
+            allk = torch.cat([key, pk])
+        elif len(passive_rows):
             cp = x[passive_rows].tocoo()
             pk = torch.from_numpy(ent[passive_rows][cp.row].astype(np.int64) * D + cp.col.astype(np.int64))
             allk = torch.cat([key, pk.to(dev)])

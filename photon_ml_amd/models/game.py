@@ -21,6 +21,7 @@ import scipy.sparse as sp
 import torch
 
 from ..constants import TaskType
+from ..data.matrix import DeviceCSR
 from .glm import Coefficients, GeneralizedLinearModel, model_for_task
 
 
@@ -37,6 +38,10 @@ def _csr_to_torch(x: sp.csr_matrix, device):
         except AttributeError:  # pragma: no cover - exotic sparse subclasses
             pass
     key = str(dev)
+    if key not in cache and isinstance(x, DeviceCSR):
+        ip = x.indptr.to(dev)
+        row = torch.repeat_interleave(torch.arange(x.shape[0], device=dev), ip[1:] - ip[:-1], output_size=x.nnz)
+        cache[key] = (row, x.indices.to(dev, torch.int64), x.data.to(dev), ip)
     if key not in cache:
         x = x.tocsr()
         indptr = np.asarray(x.indptr, dtype=np.int64)
@@ -86,7 +91,7 @@ class FixedEffectModel:
         if x.shape[1] != means.numel():
             raise ValueError(f"shard {self.feature_shard_id} dim {x.shape[1]} != model dim {means.numel()}")
         dev = torch.device(device)
-        if dev.type == "cpu":
+        if dev.type == "cpu" and not isinstance(x, DeviceCSR):
             w = means.cpu().numpy()
             return torch.from_numpy(np.asarray(x @ w).reshape(-1))
         row, col, val, indptr = _csr_to_torch(x, dev)

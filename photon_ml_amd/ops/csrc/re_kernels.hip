@@ -598,185 +598,301 @@ __global__ __launch_bounds__(RE_THREADS) void re_tron_csr_kernel(ReTronArgs a) {
 }
 
 // ============================================================================================================
-// Tall-narrow entities (more rows than coefficients, d_e <= 64): TRON with the EXACT per-entity Hessian
-// H_e = X_e^T D X_e + l2 I formed once per outer iteration on the fp64 MATRIX CORES and kept in LDS; every
-// truncated-CG step is then a d_e x d_e LDS mat-vec instead of a pass over the entity's rows (per outer iteration:
-// one Hessian pass + one function evaluation, against 1 + #CG passes for re_tron_csr_kernel).
-// Hessian pass: rows are staged 64 at a time as a dense [64 x DP] LDS block (DP = d_e padded to 16) with their
-// weights D_i; the upper-triangle 16 x 16 tiles of H are spread over the 4 waves, and per group of 4 staged rows
-// every tile takes one v_mfma_f64_16x16x4f64: A[r][k] = X[k][16 ti + r], B[k][c] = D_k X[k][16 tj + c]
-// (lane l: r = c = l & 15, k = l >> 4; accumulator i of lane l holds C[(l >> 4) + 4 i][l & 15]). Fixed k order
-// per tile, each tile owned by one wave: deterministic. Diagonal tiles are stored as computed (not mirrored:
-// C[r][c] and C[c][r] round differently), off-diagonal tiles into both halves.
+// Tall-narrow entities (d_e <= 64 coefficients, typically more rows than coefficients): ONE WAVE PER ENTITY, the
+// whole TRON with the EXACT per-entity Hessian H_e = X_e^T D X_e + l2 I. No workgroup barriers: the waves of a
+// workgroup are independent entities, every reduction is a DPP / readlane wave sum, LDS hand-offs between the
+// lanes of one wave are ordered by wave_sync (in-order LDS per wave + a compiler fence).
+// * Coefficient-space vectors live in registers: lane j holds w_j, g_j, step_j, r_j, dir_j (j < d_e <= 64).
+// * Row passes stage RT_RB = 16 rows at a time as a dense [16][DP + 4] LDS block (row stride DP + 4: the
+//   quad-per-row margin reads are bank-conflict free): the entries are scattered from registers and zeroed again
+//   after use, and the NEXT block's entries (and the row pointers two blocks ahead) are already in flight while a
+//   block computes, so a pass costs about one global-memory latency, not one per block.
+// * Margins: a lane quad per row; gradient: lane j sums X[r][j] t_r over the 16 rows in a fixed order (no
+//   atomics: deterministic by construction).
+// * Hessian: per 4 staged rows one v_mfma_f64_16x16x4f64 per upper-triangle 16 x 16 tile (all tiles in the one
+//   wave, fixed k order), written to LDS EXACTLY symmetric (diagonal tiles mirrored from their upper half), so a
+//   CG step reads column j of H (consecutive lanes: conflict-free) for (H d)_j. For d_e <= 32 (FH) the Hessian
+//   at the trial point is formed INSIDE the trial point's function evaluation into a second LDS buffer (adopted
+//   when the step is accepted): one row pass per TRON iteration. Wider entities run a separate Hessian pass.
 // ============================================================================================================
 typedef double v4d __attribute__((ext_vector_type(4)));
-#define RH_ROWS 64
+#define RT_RB 16
+
+__device__ __forceinline__ void wave_sync() {
+  __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
+  __builtin_amdgcn_wave_barrier();
+  __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
+}
+
+// Sum over the 4 lanes of a quad, in every lane of the quad (fixed order).
+__device__ __forceinline__ double quad_total(double v) {
+  v += dpp_f64<0xB1>(v);    // quad_perm [1,0,3,2]
+  v += dpp_f64<0x4E>(v);    // quad_perm [2,3,0,1]
+  return v;
+}
+
+template <int LOSS>
+__device__ __forceinline__ void loss_t(double z, double y, double& l, double& dl, double& d2) {
+  if constexpr (LOSS == LOSS_LOGISTIC) {
+    // one exp, one log1p, one reciprocal, no branches (as pointwise_loss in glm_kernels.hip):
+    // e = exp(-|z|) serves the sigmoid and log(1 + exp(+-z)) = max(+-z, 0) + log1p(e)
+    const double e = exp(-fabs(z));
+    const double lp = log1p(e);
+    const double r = 1.0 / (1.0 + e);
+    const double s = z >= 0.0 ? r : e * r;
+    const bool pos = y > 0.5;
+    const double zz = pos ? -z : z;
+    l = (zz > 0.0 ? zz : 0.0) + lp;
+    dl = pos ? s - 1.0 : s;
+    d2 = s * (1.0 - s);
+  } else if constexpr (LOSS == LOSS_POISSON) {
+    const double e = exp(z);
+    l = e - y * z; dl = e - y; d2 = e;
+  } else {
+    const double d = z - y;
+    l = 0.5 * d * d; dl = d; d2 = 1.0;
+  }
+}
 
 template <int T>
-__global__ __launch_bounds__(RE_THREADS) void re_tron_hess_kernel(ReTronArgs a) {
-  constexpr int DP = 16 * T;
-  constexpr int NT = T * (T + 1) / 2;                 // upper-triangle tiles
-  constexpr int NTW = (NT + RE_NW - 1) / RE_NW;       // tiles per wave (at most)
+struct TallCfg {
+  static constexpr int DP = 16 * T;                  // padded coefficient count
+  static constexpr int XS = DP + 4;                  // staged row stride (doubles)
+  static constexpr bool FH = T <= 2;                 // Hessian fused into the function evaluation (2 H buffers)
+  static constexpr int WORDS = (FH ? 2 : 1) * DP * DP + RT_RB * XS + DP + 2 * RT_RB;   // LDS doubles per wave
+};
+
+template <int T, int LOSS>
+__global__ __launch_bounds__(64) void re_tron_tall_kernel(ReTronArgs a) {
+  using C = TallCfg<T>;
+  constexpr int DP = C::DP, XS = C::XS, NT = T * (T + 1) / 2, KE = T;
+  constexpr bool FH = C::FH;
   extern __shared__ __attribute__((aligned(16))) double smem[];
+  const int lane = threadIdx.x;
   const int e = a.order[blockIdx.x];
+  double* const H0 = smem;                              // [DP][DP] Hessian buffers, exactly symmetric
+  double* const H1 = smem + (FH ? DP * DP : 0);
+  double* Xs = smem + (FH ? 2 : 1) * DP * DP;           // [RT_RB][XS] staged rows (zero between blocks)
+  double* sV = Xs + RT_RB * XS;                         // [DP] vector broadcast to the lanes (margins / CG)
+  double* sT = sV + DP;                                 // [RT_RB] per staged row: gradient weight t_r
+  double* sD = sT + RT_RB;                              // [RT_RB] per staged row: Hessian weight D_r
+  int hc = 0;                                           // (hc ? H1 : H0) = Hessian at the current point
   const long long r0 = a.row_ptr[e], r1 = a.row_ptr[e + 1];
   const long long c0 = a.col_ptr[e];
   const int d = (int)(a.col_ptr[e + 1] - c0);
-  const int tid = threadIdx.x, w = tid >> 6, lane = tid & 63;
-  double* H = smem;                       // [DP][DP]
-  double* Xs = H + DP * DP;               // [RH_ROWS][DP] staged rows
-  double* Ds = Xs + RH_ROWS * DP;         // [RH_ROWS] their Hessian weights
-  double* sW = Ds + RH_ROWS;
-  double* sG = sW + DP;
-  double* sS = sG + DP;
-  double* sR = sS + DP;
-  double* sD = sR + DP;
-  double* acc = sD + DP;                  // RE_NW accumulators of DP (function evaluations), acc[0..d) = result
-  double* red = acc + RE_NW * DP;
-  double* myacc = acc + w * DP;
+  const bool own = lane < d;                            // lane j owns coefficient j
   double* D[2] = {a.scr, a.scr + a.n_rows};
   double* Z[2] = {a.scr + 2 * a.n_rows, a.scr + 3 * a.n_rows};
-  int cur = 0, parity = 0, npass = 0;
+  int cur = 0, npass = 0;
   double* Wg = a.W + c0;
-  // this wave's tiles (ti, tj), tj >= ti, round-robin over the waves
-  int tI[NTW], tJ[NTW];
-#pragma unroll
-  for (int q = 0; q < NTW; ++q) {
-    int t = w + RE_NW * q, ti = 0;
-    tI[q] = -1; tJ[q] = -1;
-    if (t < NT) {
-      while (t >= T - ti) { t -= T - ti; ++ti; }
-      tI[q] = ti; tJ[q] = ti + t;
-    }
-  }
-  auto zero_own = [&]() {
-    for (int j = lane; j < d; j += 64) myacc[j] = 0.0;
+  const int grp = lane >> 4, gl = lane & 15;
+  // entity-local 32-bit offsets from per-entity bases (one VGPR per address)
+  const long long e0 = a.nip[r0];
+  const uint16_t* __restrict__ lcol = a.lcol + e0;
+  const double* __restrict__ val = a.val + e0;
+  const int nrows = (int)(r1 - r0);
+  for (int i = lane; i < RT_RB * XS; i += 64) Xs[i] = 0.0;
+
+  struct Blk {
+    int c[RT_RB / 4][KE];
+    double v[RT_RB / 4][KE];
+    double rs[3];
   };
-  auto value_grad = [&](const double* vec, int nb, bool at_zero, double& gg) -> double {
-    ++npass;
-    __syncthreads();
-    zero_own();
-    double fp = 0.0;
-    if (at_zero) rows<2, 2>(a, r0, r1, vec, myacc, nullptr, nullptr, nullptr, fp);
-    else rows<1, 2>(a, r0, r1, vec, myacc, nullptr, D[nb], Z[nb], fp);
-    __syncthreads();
-    double s3[3] = {fp, 0.0, 0.0};
-    for (int j = tid; j < d; j += RE_THREADS) {
-      double g = acc[j];
-#pragma unroll
-      for (int q = 1; q < RE_NW; ++q) g += acc[q * DP + j];
-      const double v = vec[j];
-      g += a.l2 * v;
-      acc[j] = g;
-      s3[1] += v * v;
-      s3[2] += g * g;
-    }
-    block_sums<3>(s3, red, parity);
-    gg = s3[2];
-    return s3[0] + 0.5 * a.l2 * s3[1];
+  // row pointers of block b (lane q <= RT_RB: entity-local offset of row b + q)
+  auto fetch_np = [&](int b) -> int {
+    const int ip = b + (lane <= RT_RB ? lane : RT_RB);
+    return b < nrows ? (int)(a.nip[r0 + (ip < nrows ? ip : nrows)] - e0) : 0;
   };
-  // H = X^T diag(D[cur]) X + l2 I on the matrix cores
-  auto form_hessian = [&]() {
-    ++npass;
-    const double* Dc = D[cur];
-    v4d cacc[NTW];
+  // issue the loads of block b (entries + per-row scalars: mode 0 = D[cur] in rs[0], else wt / off / y)
+  auto issue = [&](Blk& B, int b, int np, int mode) {
+    B.rs[0] = B.rs[1] = B.rs[2] = 0.0;
+    if (lane < RT_RB && b + lane < nrows) {
+      const long long i = r0 + b + lane;
+      if (mode == 0) B.rs[0] = D[cur][i];
+      else { B.rs[0] = a.wt[i]; B.rs[1] = a.off[i]; B.rs[2] = a.y[i]; }
+    }
 #pragma unroll
-    for (int q = 0; q < NTW; ++q) cacc[q] = v4d{0.0, 0.0, 0.0, 0.0};
-    for (long long base = r0; base < r1; base += RH_ROWS) {
-      __syncthreads();
-      for (int j = tid; j < RH_ROWS * DP; j += RE_THREADS) Xs[j] = 0.0;
-      if (tid < RH_ROWS) Ds[tid] = base + tid < r1 ? Dc[base + tid] : 0.0;
-      __syncthreads();
-      for (int rr = w; rr < RH_ROWS; rr += RE_NW) {
-        const long long i = base + rr;
-        if (i >= r1) break;
-        for (long long p = a.nip[i] + lane; p < a.nip[i + 1]; p += 64) Xs[rr * DP + (int)a.lcol[p]] = a.val[p];
+    for (int u = 0; u < RT_RB / 4; ++u) {
+      const int q = u * 4 + grp;
+      const int lo = __shfl(np, q, 64), hi = __shfl(np, q + 1, 64);
+#pragma unroll
+      for (int k = 0; k < KE; ++k) {
+        const int p = lo + gl + 16 * k;
+        const bool in = p < hi;
+        B.c[u][k] = in ? (int)lcol[p] : -1;
+        B.v[u][k] = in ? val[p] : 0.0;
       }
-      __syncthreads();
-      const int r = lane & 15;
-#pragma unroll 4
-      for (int kg = 0; kg < RH_ROWS / 4; ++kg) {
-        const int k = kg * 4 + (lane >> 4);
-        const double dk = Ds[k];
-        const double* xk = Xs + k * DP;
+    }
+  };
+  auto scatter = [&](const Blk& B, bool zero) {
 #pragma unroll
-        for (int q = 0; q < NTW; ++q) {
-          if (tI[q] < 0) continue;
-          const double av = xk[tI[q] * 16 + r];
-          const double bv = dk * xk[tJ[q] * 16 + r];
-          cacc[q] = __builtin_amdgcn_mfma_f64_16x16x4f64(av, bv, cacc[q], 0, 0, 0);
+    for (int u = 0; u < RT_RB / 4; ++u)
+#pragma unroll
+      for (int k = 0; k < KE; ++k)
+        if (B.c[u][k] >= 0) Xs[(u * 4 + grp) * XS + B.c[u][k]] = zero ? 0.0 : B.v[u][k];
+  };
+  // Pipelined pass over the entity's blocks: body(b, B) runs with block b staged in Xs (and its loads in B.rs).
+  auto pass = [&](int mode, auto&& body) {
+    Blk A, B2;
+    int np = fetch_np(0);
+    issue(A, 0, np, mode);
+    np = fetch_np(RT_RB);
+    for (int b = 0; b < nrows; b += 2 * RT_RB) {
+      const bool hasB = b + RT_RB < nrows;
+      if (hasB) issue(B2, b + RT_RB, np, mode);
+      np = fetch_np(b + 2 * RT_RB);
+      scatter(A, false);
+      wave_sync();
+      body(b, A);
+      wave_sync();
+      scatter(A, true);
+      if (!hasB) break;
+      const bool hasA = b + 2 * RT_RB < nrows;
+      if (hasA) issue(A, b + 2 * RT_RB, np, mode);
+      np = fetch_np(b + 3 * RT_RB);
+      scatter(B2, false);
+      wave_sync();
+      body(b + RT_RB, B2);
+      wave_sync();
+      scatter(B2, true);
+      if (!hasA) break;
+    }
+  };
+  // MFMA accumulation of X_blk^T diag(w) X_blk for the staged block (w in LDS ``sw``)
+  auto hess_block = [&](v4d (&cacc)[NT], const double* sw) {
+    const int rr = lane & 15, kk = lane >> 4;
+#pragma unroll 1
+    for (int kg = 0; kg < RT_RB / 4; ++kg) {
+      const int k = kg * 4 + kk;
+      const double dk = sw[k];
+      const double* xk = Xs + k * XS;
+      int t = 0;
+#pragma unroll
+      for (int ti = 0; ti < T; ++ti)
+#pragma unroll
+        for (int tj = ti; tj < T; ++tj, ++t)
+          cacc[t] = __builtin_amdgcn_mfma_f64_16x16x4f64(xk[ti * 16 + rr], dk * xk[tj * 16 + rr], cacc[t], 0, 0, 0);
+    }
+  };
+  auto store_hess = [&](v4d (&cacc)[NT], double* H) {
+    int t = 0;
+#pragma unroll
+    for (int ti = 0; ti < T; ++ti)
+#pragma unroll
+      for (int tj = ti; tj < T; ++tj, ++t)
+#pragma unroll
+        for (int i = 0; i < 4; ++i) {
+          // accumulator i of lane l holds C[(l >> 4) + 4 i][l & 15] of the tile
+          const int lr = (lane >> 4) + 4 * i, lc = lane & 15;
+          const int row = ti * 16 + lr, col = tj * 16 + lc;
+          if (ti != tj || lr <= lc) {
+            H[row * DP + col] = cacc[t][i];
+            H[col * DP + row] = cacc[t][i];
+          }
         }
-      }
-    }
-    __syncthreads();
-#pragma unroll
-    for (int q = 0; q < NTW; ++q) {
-      if (tI[q] < 0) continue;
-#pragma unroll
-      for (int i = 0; i < 4; ++i) {
-        const int row = tI[q] * 16 + (lane >> 4) + 4 * i, col = tJ[q] * 16 + (lane & 15);
-        H[row * DP + col] = cacc[q][i];
-        if (tI[q] != tJ[q]) H[col * DP + row] = cacc[q][i];
-      }
-    }
-    __syncthreads();
-    if (tid < d) H[tid * DP + tid] += a.l2;
-    __syncthreads();
+    wave_sync();
+    if (lane < DP) H[lane * DP + lane] += a.l2;
+    wave_sync();
   };
 
-  for (int j = tid; j < DP; j += RE_THREADS) sW[j] = j < d ? Wg[j] : 0.0;
-  double gnorm2;
-  double f = value_grad(sW, cur, false, gnorm2);
-  double nz[1] = {0.0};
-  for (int j = tid; j < d; j += RE_THREADS) {
-    sG[j] = acc[j];
-    nz[0] += sW[j] != 0.0 ? 1.0 : 0.0;
-  }
-  block_sums<1>(nz, red, parity);
+  // value + gradient at the lane-held vector ``vj`` (written to sV here). mode 1: writes Z buffer ``nb`` (and D
+  // when the Hessian has its own pass); mode 2 (the state at zero): no scratch writes. ``Hout`` (FH only): the
+  // Hessian at vj is formed in the same pass. Returns f; gj = this lane's gradient component (l2 included).
+  auto value_grad = [&](double vj, int mode, int nb, double& gj, double* Hout) -> double {
+    ++npass;
+    if (lane < DP) sV[lane] = own ? vj : 0.0;
+    const int r = lane >> 2, q = lane & 3;
+    double fp = 0.0, g = 0.0;
+    v4d cacc[NT];
+#pragma unroll
+    for (int t = 0; t < NT; ++t) cacc[t] = v4d{0.0, 0.0, 0.0, 0.0};
+    pass(1, [&](int b, const Blk& B) {
+      double s = 0.0;
+#pragma unroll 4
+      for (int cc = 0; cc < DP / 4; ++cc) s = fma(Xs[r * XS + q + 4 * cc], sV[q + 4 * cc], s);
+      s = quad_total(s);
+      const double wt = __shfl(B.rs[0], r, 64), of = __shfl(B.rs[1], r, 64), yy = __shfl(B.rs[2], r, 64);
+      double t = 0.0, h = 0.0;
+      if (b + r < nrows) {
+        const long long i = r0 + b + r;
+        double l, dl, d2;
+        loss_t<LOSS>(s + of, yy, l, dl, d2);
+        t = wt * dl;
+        h = wt * d2;
+        if (q == 0) {
+          fp += wt * l;
+          if (mode == 1) {
+            Z[nb][i] = s;
+            if (!FH) D[nb][i] = h;
+          }
+        }
+      }
+      if (q == 0) { sT[r] = t; sD[r] = h; }
+      wave_sync();
+      if (lane < DP) {
+#pragma unroll 4
+        for (int rr = 0; rr < RT_RB; ++rr) g = fma(Xs[rr * XS + lane], sT[rr], g);
+      }
+      if (FH && Hout != nullptr) hess_block(cacc, sD);
+    });
+    if (FH && Hout != nullptr) store_hess(cacc, Hout);
+    gj = own ? g + a.l2 * vj : 0.0;
+    return wave_total(fp) + 0.5 * a.l2 * wave_total(own ? vj * vj : 0.0);
+  };
+  // separate Hessian pass at the current point (entities wider than 32): H = X^T diag(D[cur]) X + l2 I
+  auto form_hessian = [&]() {
+    ++npass;
+    v4d cacc[NT];
+#pragma unroll
+    for (int t = 0; t < NT; ++t) cacc[t] = v4d{0.0, 0.0, 0.0, 0.0};
+    pass(0, [&](int b, const Blk& B) {
+      if (lane < RT_RB) sD[lane] = B.rs[0];
+      wave_sync();
+      hess_block(cacc, sD);
+    });
+    store_hess(cacc, (hc ? H1 : H0));
+  };
+
+  double Wj = own ? Wg[lane] : 0.0, Gj;
+  double f = value_grad(Wj, 1, cur, Gj, FH ? (hc ? H1 : H0) : nullptr);
+  double gnorm2 = wave_total(Gj * Gj);
+  const double nz = wave_total(own && Wj != 0.0 ? 1.0 : 0.0);
   double f0z = f, g0n = sqrt(gnorm2);
-  if (nz[0] != 0.0) {
-    for (int j = tid; j < DP; j += RE_THREADS) sS[j] = 0.0;
-    double g0;
-    f0z = value_grad(sS, 0, true, g0);
-    g0n = sqrt(g0);
+  if (nz != 0.0) {
+    double g0j;
+    f0z = value_grad(0.0, 2, 0, g0j, nullptr);
+    g0n = sqrt(wave_total(g0j * g0j));
   }
   const double loss_tol = f0z * a.tol, grad_tol = g0n * a.tol;
   double delta = sqrt(gnorm2);
   int it = 0, fails = 0, reason = 0;
-  bool active = true, need_h = true;
+  bool active = true, need_h = !FH;
   if (delta == 0.0) { reason = 4; active = false; }
   const double eta0 = 1e-4, eta1 = 0.25, eta2 = 0.75, sg1 = 0.25, sg2 = 0.5, sg3 = 4.0;
   const int guard_max = a.max_iter * (a.max_fail + 1) + 5;
   for (int guard = 0; active && guard < guard_max; ++guard) {
     if (need_h) { form_hessian(); need_h = false; }
-    for (int j = tid; j < DP; j += RE_THREADS) {
-      sS[j] = 0.0;
-      const double gj = j < d ? sG[j] : 0.0;
-      sR[j] = -gj;
-      sD[j] = -gj;
-    }
+    const double* H = (hc ? H1 : H0);
+    // ---- truncated CG on the LDS Hessian: per step one column-read mat-vec and five wave sums
+    double Sj = 0.0, Rj = -Gj, Dj = -Gj;
     double rtr = gnorm2, sts = 0.0;
     const double cg_tol2 = 0.01 * gnorm2;
     for (int k = 0; k < a.max_cg; ++k) {
       if (!(rtr > cg_tol2)) break;
-      __syncthreads();
-      double s5[5] = {0.0, 0.0, 0.0, 0.0, 0.0};
-      for (int j = tid; j < d; j += RE_THREADS) {
-        const double* hr = H + j * DP;
-        double h0 = 0.0, h1 = 0.0;
-        int c = 0;
-        for (; c + 1 < d; c += 2) { h0 = fma(hr[c], sD[c], h0); h1 = fma(hr[c + 1], sD[c + 1], h1); }
-        if (c < d) h0 = fma(hr[c], sD[c], h0);
-        const double h = h0 + h1, dj = sD[j];
-        acc[j] = h;
-        s5[0] += dj * h;
-        s5[1] += sS[j] * dj;
-        s5[2] += dj * dj;
-        s5[3] += sR[j] * h;
-        s5[4] += h * h;
+      if (lane < DP) sV[lane] = Dj;
+      wave_sync();
+      double h0 = 0.0, h1 = 0.0;
+      if (lane < DP) {
+#pragma unroll 2
+        for (int cc = 0; cc < DP; cc += 2) {
+          h0 = fma(H[cc * DP + lane], sV[cc], h0);
+          h1 = fma(H[(cc + 1) * DP + lane], sV[cc + 1], h1);
+        }
       }
-      block_sums<5>(s5, red, parity);
-      const double dhd = s5[0], std_ = s5[1], dtd = s5[2], rh = s5[3], hh = s5[4];
+      wave_sync();
+      const double hj = own ? h0 + h1 : 0.0;
+      const double dhd = wave_total(Dj * hj), std_ = wave_total(Sj * Dj), dtd = wave_total(Dj * Dj);
+      const double rh = wave_total(Rj * hj), hh = wave_total(hj * hj);
       const double alpha = rtr / (dhd == 0.0 ? 1.0 : dhd);
       double tn = sts + 2.0 * alpha * std_ + alpha * alpha * dtd;
       tn = tn > 0.0 ? tn : 0.0;
@@ -784,38 +900,27 @@ __global__ __launch_bounds__(RE_THREADS) void re_tron_hess_kernel(ReTronArgs a) 
       const bool hit = tn > dsq;
       double al = alpha;
       if (hit) {
-        const double q = std_ * std_ + dtd * (dsq - sts);
-        const double rad = sqrt(q > 0.0 ? q : 0.0);
+        const double qq = std_ * std_ + dtd * (dsq - sts);
+        const double rad = sqrt(qq > 0.0 ? qq : 0.0);
         const double den1 = std_ + rad;
         al = std_ >= 0.0 ? (dsq - sts) / (den1 > 1e-300 ? den1 : 1e-300) : (rad - std_) / (dtd > 1e-300 ? dtd : 1e-300);
       }
       double rn = rtr - 2.0 * al * rh + al * al * hh;
       rn = rn > 0.0 ? rn : 0.0;
       const double beta = rn / (rtr == 0.0 ? 1.0 : rtr);
-      __syncthreads();          // every row of H . d read sD before it changes
-      for (int j = tid; j < d; j += RE_THREADS) {
-        const double dj = sD[j];
-        sS[j] += al * dj;
-        const double rj = sR[j] - al * acc[j];
-        sR[j] = rj;
-        if (!hit) sD[j] = rj + beta * dj;
-      }
+      Sj += al * Dj;
+      Rj -= al * hj;
       if (hit) break;
+      Dj = Rj + beta * Dj;
       rtr = rn;
       sts = tn;
     }
-    double s3[3] = {0.0, 0.0, 0.0};
-    for (int j = tid; j < d; j += RE_THREADS) {
-      const double sj = sS[j];
-      s3[0] += sG[j] * sj;
-      s3[1] += sj * sR[j];
-      s3[2] += sj * sj;
-      sD[j] = sW[j] + sj;
-    }
-    block_sums<3>(s3, red, parity);
-    const double gs = s3[0], pred = -0.5 * (gs - s3[1]), snorm = sqrt(s3[2]);
-    double gn2;
-    const double fn = value_grad(sD, cur ^ 1, false, gn2);
+    // ---- trial point (its Hessian formed in the same pass when FH), trust-region update, acceptance
+    const double gs = wave_total(Gj * Sj), pred = -0.5 * (gs - wave_total(Sj * Rj)), snorm = sqrt(wave_total(Sj * Sj));
+    const double Tj = own ? Wj + Sj : 0.0;
+    double Gn;
+    const double fn = value_grad(Tj, 1, cur ^ 1, Gn, FH ? (hc ? H0 : H1) : nullptr);
+    const double gn2 = wave_total(Gn * Gn);
     const double actual = f - fn;
     if (it == 0) delta = fmin(delta, snorm);
     const double den = fn - f - gs;
@@ -829,16 +934,15 @@ __global__ __launch_bounds__(RE_THREADS) void re_tron_hess_kernel(ReTronArgs a) 
     const bool accept = actual > eta0 * pred;
     const double f_prev = f;
     if (accept) {
-      for (int j = tid; j < d; j += RE_THREADS) {
-        sW[j] = sD[j];
-        sG[j] = acc[j];
-      }
+      Wj = Tj;
+      Gj = Gn;
       gnorm2 = gn2;
       f = fn;
       cur ^= 1;
       ++it;
       fails = 0;
-      need_h = true;
+      if (FH) hc ^= 1;
+      else need_h = true;
     } else {
       ++fails;
     }
@@ -850,15 +954,417 @@ __global__ __launch_bounds__(RE_THREADS) void re_tron_hess_kernel(ReTronArgs a) 
     if ((accept || not_impr) && it >= a.max_iter) rc = 1;
     if (rc > 0) { reason = rc; active = false; }
   }
-  __syncthreads();
-  for (int j = tid; j < d; j += RE_THREADS) Wg[j] = sW[j];
+  if (own) Wg[lane] = Wj;
   if (a.zout != nullptr) {
     const double* zc = Z[cur];
-    for (long long i = r0 + tid; i < r1; i += RE_THREADS) a.zout[i] = zc[i];
+    for (long long i = r0 + lane; i < r1; i += 64) a.zout[i] = zc[i];
   }
-  if (tid == 0) {
+  if (lane == 0) {
     a.f[e] = f; a.iters[e] = it; a.reason[e] = reason;
     if (a.npass != nullptr) a.npass[e] = npass;
+  }
+}
+
+// ============================================================================================================
+// REGISTER-RESIDENT fused primal TRON (wide entities: d_e <= 1024, rows of <= 64 non-zeros).
+// The fused kernel above streams an entity's CSR rows from memory for every Hessian-vector product (~36 row
+// passes per solve at ~3.6 TB/s). Here the rows are loaded ONCE into VGPRs and every later pass runs on-chip:
+// * a workgroup of RS_NW = 8 waves holds up to RS_CAP = 8 x 4 x S rows: row r -> slot group sg = r / 4, wave
+//   sg % 8, register slot sg / 8; 16 lanes per row, lane k of the row keeps entries k, k + 16, k + 32, k + 48
+//   (fp64 value + packed u16 column). Per-row D (current / trial), margins (current / trial), weight, offset and
+//   label sit in LDS; the coefficient vectors and one accumulator per wave in LDS as in the streaming kernel.
+// * entities longer than RS_CAP rows are split over a CLUSTER of k workgroups (member m holds rows
+//   [m RS_CAP, (m + 1) RS_CAP)): after every row pass each member publishes its partial sum (d doubles + the
+//   loss), the members meet at a cluster barrier (agent-scope release / acquire on a per-task counter), and
+//   every member sums the k partials in member order. All control flow then derives from identical sums, so the
+//   k replicas of the TRON state stay bitwise identical and no other exchange is needed.
+// * ONE persistent launch (one workgroup per CU, grid = resident capacity) serves every task: a workgroup
+//   dequeues a ticket (one atomic), a task with k members owns k consecutive tickets (largest tasks first).
+//   Tickets are taken in order by running workgroups only, so the earliest incomplete cluster is always filled
+//   by workgroups finishing earlier tasks: deadlock-free while k <= the resident workgroups. Every wait is
+//   bounded anyway (~1 s, then a global error flag releases every waiter and the host raises).
+// Deterministic: fixed-order DPP row sums, per-wave LDS accumulators combined in wave order, member partials
+// combined in member order (same LDS ds_add_f64 lane-order assumption as the streaming kernel inside a wave).
+// ============================================================================================================
+#define RS_NW 8
+#define RS_THREADS (RS_NW * 64)
+#define RS_DMAX 1024
+#define RES_S 12              // register slots per wave (rows per workgroup = 8 x 4 x RES_S)
+
+template <int K>
+__device__ __forceinline__ void block_sums8(double (&v)[K], double* __restrict__ red, int& parity) {
+  const int lane = threadIdx.x & 63, w = threadIdx.x >> 6;
+#pragma unroll
+  for (int k = 0; k < K; ++k) v[k] = wave_total(v[k]);
+  double* slot = red + parity * (RS_NW * 8);
+  if (lane == 0) {
+#pragma unroll
+    for (int k = 0; k < K; ++k) slot[w * 8 + k] = v[k];
+  }
+  __syncthreads();
+#pragma unroll
+  for (int k = 0; k < K; ++k) {
+    double s = 0.0;
+#pragma unroll
+    for (int q = 0; q < RS_NW; ++q) s += slot[q * 8 + k];
+    v[k] = s;
+  }
+  parity ^= 1;
+}
+
+struct ResTasks {
+  int* ticket;               // dequeue counter (zero before the launch)
+  const int* task_ent;       // [n_tasks] entity
+  const int* task_t0;        // [n_tasks + 1] first ticket of each task (task j has task_t0[j+1] - task_t0[j] members)
+  int n_tasks;
+  unsigned* bar;             // [n_tasks] cluster barrier counters (zero before the launch)
+  double* ws;                // [n_tickets][2][RS_DMAX + 8] member partials (double-buffered by pass parity)
+  int* err;                  // set when a cluster wait timed out (the results are then invalid)
+};
+
+// Cluster barrier of the k members of one task (k > 1). Producer: every wave drains its stores, workgroup barrier,
+// one lane releases at agent scope and adds to the task's counter; consumer: relaxed polls of the counter, one
+// agent-scope acquire, workgroup barrier (MI355X_MICROARCH.md, valid hand-off forms). Bounded: ~1 s, then err.
+__device__ __forceinline__ void cluster_barrier(unsigned* bar, unsigned target, int* err) {
+  asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+  __syncthreads();
+  if (threadIdx.x == 0) {
+    __builtin_amdgcn_fence(__ATOMIC_RELEASE, "agent");
+    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+    __hip_atomic_fetch_add(bar, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    const unsigned long long t0 = __builtin_amdgcn_s_memrealtime();
+    while (__hip_atomic_load(bar, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) < target) {
+      if (__hip_atomic_load(err, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) != 0) break;
+      if (__builtin_amdgcn_s_memrealtime() - t0 > 100000000ull) {      // 1 s at the 100 MHz constant clock
+        __hip_atomic_store(err, 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+        break;
+      }
+      __builtin_amdgcn_s_sleep(2);
+    }
+    __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "agent");
+    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+  }
+  __syncthreads();
+}
+
+template <int S, int LOSS>
+__global__ __launch_bounds__(RS_THREADS) void re_tron_res_kernel(ReTronArgs a, ResTasks tk) {
+  constexpr int CAP = RS_NW * 4 * S;
+  extern __shared__ __attribute__((aligned(16))) double smem[];
+  const int tid = threadIdx.x, w = tid >> 6, lane = tid & 63;
+  const int grp = lane >> 4, gl = lane & 15;
+  constexpr int DM = RS_DMAX, DMS = RS_DMAX + 8;   // + a dummy slot (index DM) for the empty register entries
+  double* sV = smem;                  // [DMS] gathered vector: CG direction / trial point (sV[DM] == 0)
+  double* sH = sV + DMS;              // combined Hessian-vector product / trial gradient
+  double* sW = sH + DM;
+  double* sG = sW + DM;
+  double* sS = sG + DM;              // CG step
+  double* sR = sS + DM;              // CG residual
+  double* acc = sR + DM;             // [RS_NW][DMS] per-wave accumulators (zero between passes)
+  double* rD = acc + RS_NW * DMS;    // [2][CAP] per local row: Hessian weight D (current / trial)
+  double* rZ = rD + 2 * CAP;         // [2][CAP] margins x.w (current / trial)
+  double* rW = rZ + 2 * CAP;         // [CAP] weight
+  double* rO = rW + CAP;             // [CAP] offset
+  double* rY = rO + CAP;             // [CAP] label
+  double* red = rY + CAP;            // [2][RS_NW][8]
+  double* myacc = acc + w * DMS;
+  __shared__ int sTicket;
+  for (int i = tid; i < RS_NW * DMS; i += RS_THREADS) acc[i] = 0.0;
+  if (tid < 8) sV[DM + tid] = 0.0;
+
+  for (;;) {
+    __syncthreads();
+    if (tid == 0) sTicket = atomicAdd(tk.ticket, 1);
+    __syncthreads();
+    const int t = sTicket;
+    if (t >= tk.task_t0[tk.n_tasks]) break;
+    // task of ticket t: the last j with task_t0[j] <= t
+    int lo = 0, hi = tk.n_tasks - 1;
+    while (lo < hi) {
+      const int mid = (lo + hi + 1) >> 1;
+      if (tk.task_t0[mid] <= t) lo = mid; else hi = mid - 1;
+    }
+    const int j = lo, m = t - tk.task_t0[j], k = tk.task_t0[j + 1] - tk.task_t0[j];
+    const int e = tk.task_ent[j];
+    unsigned* bar = tk.bar + j;
+    unsigned epoch = 0;
+    double* wsm = tk.ws + (size_t)tk.task_t0[j] * 2 * (DM + 8);   // member 0's partials; member q at + q * 2 (DM + 8)
+    const long long r0 = a.row_ptr[e];
+    const long long rb = r0 + (long long)m * CAP;                  // this member's first row
+    const int nloc = (int)min((long long)CAP, a.row_ptr[e + 1] - rb);
+    const long long c0 = a.col_ptr[e];
+    const int d = (int)(a.col_ptr[e + 1] - c0);
+    int cur = 0, parity = 0, npass = 0, wpar = 0;
+    double* Wg = a.W + c0;
+
+    // ---- load this member's rows into registers, its row scalars into LDS
+    double xv[S][4];
+    uint32_t xc[S][2];
+    // number of register slots of this wave holding rows: sg = s * RS_NW + w < ceil(nloc / 4)
+    const int nsg = (nloc + 3) >> 2;
+    const int ns = nsg > w ? (nsg - w + RS_NW - 1) / RS_NW : 0;
+    {
+      // member-local 32-bit entry offsets (one VGPR per address); loads issued 4 slots at a time
+      const long long eb = a.nip[rb];
+      const uint16_t* __restrict__ lc = a.lcol + eb;
+      const double* __restrict__ vl = a.val + eb;
+#pragma unroll
+      for (int s = 0; s < S; ++s) {
+        const int r = ((s * RS_NW + w) << 2) + grp;
+        int p0 = 0, p1 = 0;
+        if (s < ns && r < nloc) { p0 = (int)(a.nip[rb + r] - eb); p1 = (int)(a.nip[rb + r + 1] - eb); }
+        uint32_t cc[4];
+#pragma unroll
+        for (int q = 0; q < 4; ++q) {
+          const int p = p0 + gl + 16 * q;
+          const bool in = p < p1;
+          xv[s][q] = in ? vl[p] : 0.0;
+          cc[q] = in ? (uint32_t)lc[p] : (uint32_t)DM;
+        }
+        xc[s][0] = cc[0] | (cc[1] << 16);
+        xc[s][1] = cc[2] | (cc[3] << 16);
+        if ((s & 3) == 3) __builtin_amdgcn_sched_barrier(0);
+      }
+    }
+    for (int r = tid; r < nloc; r += RS_THREADS) {
+      rW[r] = a.wt[rb + r];
+      rO[r] = a.off[rb + r];
+      rY[r] = a.y[rb + r];
+    }
+    for (int jj = tid; jj < d; jj += RS_THREADS) sW[jj] = Wg[jj];
+
+    // One pass over the resident rows. MODE 0: myacc += X^T (D_cur * (X sV)); MODE 1: value + gradient at sV
+    // (myacc += X^T (w l'), fpart, trial D / margins -> rD / rZ slot nb); MODE 2: value + gradient at zero.
+    auto pass = [&](int mode, int nb, double& fpart) __attribute__((always_inline)) {
+      const double* Dc = rD + cur * CAP;
+#pragma unroll
+      for (int s = 0; s < S; ++s) {
+        if (s < ns) {
+          int r = ((s * RS_NW + w) << 2) + grp;
+          uint32_t p0 = xc[s][0], p1 = xc[s][1];
+          // opaque per pass: keeps the compiler from hoisting the decoded LDS addresses of every entry and row
+          // out of the solve loops (that doubled the registers of the resident rows)
+          asm volatile("" : "+v"(p0), "+v"(p1), "+v"(r));
+          const bool valid = r < nloc;
+          const uint32_t c[4] = {p0 & 0xFFFFu, p0 >> 16, p1 & 0xFFFFu, p1 >> 16};
+          double dot = 0.0;
+          if (mode != 2) {
+#pragma unroll
+            for (int q = 0; q < 4; ++q) dot = fma(xv[s][q], sV[c[q]], dot);
+            dot = row16_total(dot);
+          }
+          double tt = 0.0;
+          if (valid) {
+            if (mode == 0) {
+              tt = Dc[r] * dot;
+            } else {
+              const double wt = rW[r];
+              double l, dl, d2;
+              loss_t<LOSS>(dot + rO[r], rY[r], l, dl, d2);
+              tt = wt * dl;
+              if (gl == 0) {
+                fpart += wt * l;
+                if (mode == 1) { rD[nb * CAP + r] = wt * d2; rZ[nb * CAP + r] = dot; }
+              }
+            }
+          }
+#pragma unroll
+          for (int q = 0; q < 4; ++q) atomicAdd(&myacc[c[q]], tt * xv[s][q]);
+        }
+        __builtin_amdgcn_sched_barrier(0);   // one slot at a time: no hoisting of later slots' gathers
+      }
+    };
+    // Combine the wave accumulators of this member (and zero them), then the members' partials: out[jj] =
+    // sum, for jj < d, in every member identically. ``fp`` (this workgroup's loss part, already block-summed)
+    // is combined the same way and returned.
+    auto combine = [&](double* out, double fp) __attribute__((always_inline)) -> double {
+      __syncthreads();
+      if (k == 1) {
+        for (int jj = tid; jj < d; jj += RS_THREADS) {
+          double h = 0.0;
+#pragma unroll
+          for (int q = 0; q < RS_NW; ++q) { h += acc[q * DMS + jj]; acc[q * DMS + jj] = 0.0; }
+          out[jj] = h;
+        }
+        __syncthreads();
+        return fp;
+      }
+      double* mine = wsm + (size_t)(m * 2 + wpar) * (DM + 8);
+      for (int jj = tid; jj < d; jj += RS_THREADS) {
+        double h = 0.0;
+#pragma unroll
+        for (int q = 0; q < RS_NW; ++q) { h += acc[q * DMS + jj]; acc[q * DMS + jj] = 0.0; }
+        mine[jj] = h;
+      }
+      if (tid == 0) mine[DM] = fp;
+      ++epoch;
+      cluster_barrier(bar, epoch * (unsigned)k, tk.err);
+      for (int jj = tid; jj < d; jj += RS_THREADS) {
+        double h = 0.0;
+        for (int q = 0; q < k; ++q) h += wsm[(size_t)(q * 2 + wpar) * (DM + 8) + jj];
+        out[jj] = h;
+      }
+      double f = 0.0;
+      for (int q = 0; q < k; ++q) f += wsm[(size_t)(q * 2 + wpar) * (DM + 8) + DM];
+      wpar ^= 1;
+      __syncthreads();
+      return f;
+    };
+    // value + gradient at vec (LDS, written to sV first): gradient (l2 included) -> sH; returns f, gg = ||g||^2.
+    auto value_grad = [&](const double* vec, int mode, int nb, double& gg) __attribute__((always_inline)) -> double {
+      ++npass;
+      __syncthreads();
+      if (vec != sV)
+        for (int jj = tid; jj < d; jj += RS_THREADS) sV[jj] = mode == 2 ? 0.0 : vec[jj];
+      __syncthreads();
+      double fp[1] = {0.0};
+      pass(mode, nb, fp[0]);
+      block_sums8<1>(fp, red, parity);
+      const double f = combine(sH, fp[0]);
+      double s2[2] = {0.0, 0.0};
+      for (int jj = tid; jj < d; jj += RS_THREADS) {
+        const double v = sV[jj];
+        const double g = sH[jj] + a.l2 * v;
+        sH[jj] = g;
+        s2[0] += v * v;
+        s2[1] += g * g;
+      }
+      block_sums8<2>(s2, red, parity);
+      gg = s2[1];
+      return f + 0.5 * a.l2 * s2[0];
+    };
+
+    double gnorm2;
+    double f = value_grad(sW, 1, cur, gnorm2);
+    double nz[1] = {0.0};
+    for (int jj = tid; jj < d; jj += RS_THREADS) {
+      sG[jj] = sH[jj];
+      nz[0] += sW[jj] != 0.0 ? 1.0 : 0.0;
+    }
+    block_sums8<1>(nz, red, parity);
+    double f0z = f, g0n = sqrt(gnorm2);
+    if (nz[0] != 0.0) {
+      double g0;
+      f0z = value_grad(sS, 2, 0, g0);
+      g0n = sqrt(g0);
+    }
+    const double loss_tol = f0z * a.tol, grad_tol = g0n * a.tol;
+    double delta = sqrt(gnorm2);
+    int it = 0, fails = 0, reason = 0;
+    bool active = true;
+    if (delta == 0.0) { reason = 4; active = false; }
+    const double eta0 = 1e-4, eta1 = 0.25, eta2 = 0.75, sg1 = 0.25, sg2 = 0.5, sg3 = 4.0;
+    const int guard_max = a.max_iter * (a.max_fail + 1) + 5;
+    for (int guard = 0; active && guard < guard_max; ++guard) {
+      for (int jj = tid; jj < d; jj += RS_THREADS) {
+        sS[jj] = 0.0;
+        sR[jj] = -sG[jj];
+        sV[jj] = -sG[jj];
+      }
+      double rtr = gnorm2, sts = 0.0;
+      const double cg_tol2 = 0.01 * gnorm2;
+      for (int kk = 0; kk < a.max_cg; ++kk) {
+        if (!(rtr > cg_tol2)) break;
+        ++npass;
+        __syncthreads();
+        double fpz = 0.0;
+        pass(0, 0, fpz);
+        combine(sH, 0.0);
+        double s5[5] = {0.0, 0.0, 0.0, 0.0, 0.0};
+        for (int jj = tid; jj < d; jj += RS_THREADS) {
+          const double dj = sV[jj];
+          const double h = sH[jj] + a.l2 * dj;
+          sH[jj] = h;
+          s5[0] += dj * h;
+          s5[1] += sS[jj] * dj;
+          s5[2] += dj * dj;
+          s5[3] += sR[jj] * h;
+          s5[4] += h * h;
+        }
+        block_sums8<5>(s5, red, parity);
+        const double dhd = s5[0], std_ = s5[1], dtd = s5[2], rh = s5[3], hh = s5[4];
+        const double alpha = rtr / (dhd == 0.0 ? 1.0 : dhd);
+        double tn = sts + 2.0 * alpha * std_ + alpha * alpha * dtd;
+        tn = tn > 0.0 ? tn : 0.0;
+        const double dsq = delta * delta;
+        const bool hit = tn > dsq;
+        double al = alpha;
+        if (hit) {
+          const double qq = std_ * std_ + dtd * (dsq - sts);
+          const double rad = sqrt(qq > 0.0 ? qq : 0.0);
+          const double den1 = std_ + rad;
+          al = std_ >= 0.0 ? (dsq - sts) / (den1 > 1e-300 ? den1 : 1e-300) : (rad - std_) / (dtd > 1e-300 ? dtd : 1e-300);
+        }
+        double rn = rtr - 2.0 * al * rh + al * al * hh;
+        rn = rn > 0.0 ? rn : 0.0;
+        const double beta = rn / (rtr == 0.0 ? 1.0 : rtr);
+        for (int jj = tid; jj < d; jj += RS_THREADS) {
+          const double dj = sV[jj];
+          sS[jj] += al * dj;
+          const double r = sR[jj] - al * sH[jj];
+          sR[jj] = r;
+          if (!hit) sV[jj] = r + beta * dj;
+        }
+        if (hit) break;
+        rtr = rn;
+        sts = tn;
+      }
+      // ---- trial point W + step (into sV), trust-region update, acceptance
+      __syncthreads();
+      double s3[3] = {0.0, 0.0, 0.0};
+      for (int jj = tid; jj < d; jj += RS_THREADS) {
+        const double sj = sS[jj];
+        s3[0] += sG[jj] * sj;
+        s3[1] += sj * sR[jj];
+        s3[2] += sj * sj;
+        sV[jj] = sW[jj] + sj;
+      }
+      block_sums8<3>(s3, red, parity);
+      const double gs = s3[0], pred = -0.5 * (gs - s3[1]), snorm = sqrt(s3[2]);
+      double gn2;
+      const double fn = value_grad(sV, 1, cur ^ 1, gn2);     // trial gradient in sH
+      const double actual = f - fn;
+      if (it == 0) delta = fmin(delta, snorm);
+      const double den = fn - f - gs;
+      const double alr = den <= 0.0 ? sg3 : fmax(sg1, -0.5 * gs / (den == 0.0 ? 1.0 : den));
+      double nd;
+      if (actual < eta0 * pred) nd = fmin(fmax(alr, sg1) * snorm, sg2 * delta);
+      else if (actual < eta1 * pred) nd = fmax(sg1 * delta, fmin(alr * snorm, sg2 * delta));
+      else if (actual < eta2 * pred) nd = fmax(sg1 * delta, fmin(alr * snorm, sg3 * delta));
+      else nd = fmax(delta, fmin(alr * snorm, sg3 * delta));
+      delta = nd;
+      const bool accept = actual > eta0 * pred;
+      const double f_prev = f;
+      if (accept) {
+        for (int jj = tid; jj < d; jj += RS_THREADS) {
+          sW[jj] = sV[jj];
+          sG[jj] = sH[jj];
+        }
+        gnorm2 = gn2;
+        f = fn;
+        cur ^= 1;
+        ++it;
+        fails = 0;
+      } else {
+        ++fails;
+      }
+      const bool not_impr = !accept && fails >= a.max_fail;
+      int rc = 0;
+      if (accept && sqrt(gnorm2) <= grad_tol) rc = 4;
+      if (accept && fabs(f - f_prev) <= loss_tol) rc = 3;
+      if (not_impr) rc = 2;
+      if ((accept || not_impr) && it >= a.max_iter) rc = 1;
+      if (rc > 0) { reason = rc; active = false; }
+    }
+    __syncthreads();
+    if (m == 0)
+      for (int jj = tid; jj < d; jj += RS_THREADS) Wg[jj] = sW[jj];
+    if (a.zout != nullptr)
+      for (int r = tid; r < nloc; r += RS_THREADS) a.zout[rb + r] = rZ[cur * CAP + r];
+    if (tid == 0 && m == 0) {
+      a.f[e] = f; a.iters[e] = it; a.reason[e] = reason;
+      if (a.npass != nullptr) a.npass[e] = npass;
+    }
   }
 }
 
@@ -890,9 +1396,14 @@ int pml_re_tron_csr(const int* order, int n_launch, const long long* row_ptr, co
   return 0;
 }
 
-// Tall-narrow entities (d_e <= 64): LDS = H + staged rows + their weights + 5 vectors + accumulators + sums.
+// Tall-narrow entities (d_e <= 64): one wave (= one workgroup) per entity; LDS per workgroup.
 size_t pml_re_tron_hess_smem(int dp) {
-  return ((size_t)dp * dp + (size_t)RH_ROWS * dp + RH_ROWS + (5 + RE_NW) * (size_t)dp + 2 * RE_NW * 8) * sizeof(double);
+  switch (dp / 16) {
+    case 1: return (size_t)TallCfg<1>::WORDS * sizeof(double);
+    case 2: return (size_t)TallCfg<2>::WORDS * sizeof(double);
+    case 3: return (size_t)TallCfg<3>::WORDS * sizeof(double);
+    default: return (size_t)TallCfg<4>::WORDS * sizeof(double);
+  }
 }
 
 int pml_re_tron_hess(const int* order, int n_launch, const long long* row_ptr, const long long* col_ptr,
@@ -905,14 +1416,71 @@ int pml_re_tron_hess(const int* order, int n_launch, const long long* row_ptr, c
   const size_t smem = pml_re_tron_hess_smem(dp);
   ReTronArgs a{order, n_launch, row_ptr, col_ptr, nip, lcol, val, y, off, wt, scr, n_rows, W, f, iters, reason,
                zout, npass, loss, l2, tol, max_iter, max_fail, max_cg, dp};
+#define RT_LAUNCH_L(T, L)                                                                                  \
+  hipLaunchKernelGGL((re_tron_tall_kernel<T, L>), dim3(n_launch), dim3(64), smem, st, a)
+#define RT_LAUNCH(T)                                  \
+  do {                                                \
+    if (loss == LOSS_LOGISTIC) RT_LAUNCH_L(T, 0);     \
+    else if (loss == LOSS_POISSON) RT_LAUNCH_L(T, 1); \
+    else RT_LAUNCH_L(T, 2);                           \
+  } while (0)
   switch (dp / 16) {
-    case 1: hipLaunchKernelGGL(re_tron_hess_kernel<1>, dim3(n_launch), dim3(RE_THREADS), smem, st, a); break;
-    case 2: hipLaunchKernelGGL(re_tron_hess_kernel<2>, dim3(n_launch), dim3(RE_THREADS), smem, st, a); break;
-    case 3: hipLaunchKernelGGL(re_tron_hess_kernel<3>, dim3(n_launch), dim3(RE_THREADS), smem, st, a); break;
-    default: hipLaunchKernelGGL(re_tron_hess_kernel<4>, dim3(n_launch), dim3(RE_THREADS), smem, st, a); break;
+    case 1: RT_LAUNCH(1); break;
+    case 2: RT_LAUNCH(2); break;
+    case 3: RT_LAUNCH(3); break;
+    default: RT_LAUNCH(4); break;
   }
+#undef RT_LAUNCH
+#undef RT_LAUNCH_L
   LAUNCH_CHECK();
   return 0;
+}
+
+
+// Register-resident kernel: LDS per workgroup, rows per workgroup.
+static size_t res_smem(int S) {
+  const size_t cap = (size_t)RS_NW * 4 * S;
+  return ((size_t)(6 + RS_NW) * (RS_DMAX + 8) + 7 * cap + 2 * RS_NW * 8) * sizeof(double);
+}
+int pml_re_res_cap() { return RS_NW * 4 * RES_S; }
+int pml_re_res_dmax() { return RS_DMAX; }
+size_t pml_re_res_ws_doubles(int n_tickets) { return (size_t)n_tickets * 2 * (RS_DMAX + 8); }
+
+// Persistent launch over ``n_tasks`` tasks (task_ent / task_t0 as in ResTasks); ``ticket`` (1 int), ``bar``
+// (n_tasks unsigned) and ``err`` (1 int) are zeroed here on the stream; ``ws``: pml_re_res_ws_doubles(n_tickets).
+int pml_re_tron_res(const int* task_ent, const int* task_t0, int n_tasks, int* ticket, unsigned* bar, double* ws,
+                    int* err, int grid, const long long* row_ptr, const long long* col_ptr, const long long* nip,
+                    const uint16_t* lcol, const double* val, const double* y, const double* off, const double* wt,
+                    double* W, double* f, int* iters, int* reason, double* zout, int* npass, int loss, double l2,
+                    double tol, int max_iter, int max_fail, int max_cg, hipStream_t st) {
+  if (n_tasks <= 0) return 0;
+  if (loss < 0 || loss > 2 || grid <= 0) return -22;
+  const size_t smem = res_smem(RES_S);
+  if (smem > 160 * 1024) return -22;
+  if (hipMemsetAsync(ticket, 0, sizeof(int), st) != hipSuccess) return -5;
+  if (hipMemsetAsync(bar, 0, sizeof(unsigned) * n_tasks, st) != hipSuccess) return -5;
+  if (hipMemsetAsync(err, 0, sizeof(int), st) != hipSuccess) return -5;
+  ReTronArgs a{nullptr, 0, row_ptr, col_ptr, nip, lcol, val, y, off, wt, nullptr, 0, W, f, iters, reason,
+               zout, npass, loss, l2, tol, max_iter, max_fail, max_cg, RS_DMAX};
+  ResTasks tk{ticket, task_ent, task_t0, n_tasks, bar, ws, err};
+  if (loss == LOSS_LOGISTIC)
+    hipLaunchKernelGGL((re_tron_res_kernel<RES_S, 0>), dim3(grid), dim3(RS_THREADS), smem, st, a, tk);
+  else if (loss == LOSS_POISSON)
+    hipLaunchKernelGGL((re_tron_res_kernel<RES_S, 1>), dim3(grid), dim3(RS_THREADS), smem, st, a, tk);
+  else
+    hipLaunchKernelGGL((re_tron_res_kernel<RES_S, 2>), dim3(grid), dim3(RS_THREADS), smem, st, a, tk);
+  LAUNCH_CHECK();
+  return 0;
+}
+
+// Workgroups of the resident kernel that fit on the device at once (occupancy API x CUs; 0 on error).
+int pml_re_res_grid() {
+  int dev = 0, cus = 0, per = 0;
+  if (hipGetDevice(&dev) != hipSuccess) return 0;
+  if (hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, dev) != hipSuccess) return 0;
+  if (hipOccupancyMaxActiveBlocksPerMultiprocessor(&per, (const void*)re_tron_res_kernel<RES_S, 0>, RS_THREADS,
+                                                   res_smem(RES_S)) != hipSuccess) return 0;
+  return cus * per;
 }
 
 }  // extern "C"

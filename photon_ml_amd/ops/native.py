@@ -648,6 +648,14 @@ def re_lib() -> Optional[ctypes.CDLL]:
         lib.pml_re_tron_hess_smem.restype = ctypes.c_size_t
         lib.pml_re_set_variant.argtypes = [c_int]
         lib.pml_re_set_variant(int(os.environ.get("PML_RE_ROWPASS", "2")))
+        lib.pml_re_tron_res.argtypes = ([c_void_p, c_void_p, c_int] + [c_void_p] * 4 + [c_int] + [c_void_p] * 14
+                                        + [c_int, c_double, c_double, c_int, c_int, c_int, c_void_p])
+        lib.pml_re_tron_res.restype = c_int
+        lib.pml_re_res_cap.restype = c_int
+        lib.pml_re_res_dmax.restype = c_int
+        lib.pml_re_res_grid.restype = c_int
+        lib.pml_re_res_ws_doubles.argtypes = [c_int]
+        lib.pml_re_res_ws_doubles.restype = ctypes.c_size_t
         lib._pml_typed = True
     return lib
 
@@ -701,6 +709,58 @@ def re_tron_csr(order, row_ptr, col_ptr, nip, lcol, val, y, off, wt, scr, W, f, 
                               None if npass is None else npass.data_ptr(), int(loss_id), float(l2), float(tol),
                               int(max_iter),
                               int(max_fail), int(max_cg), int(dmax), stream_handle(W.device)), "re_tron_csr")
+
+
+def re_res_params():
+    """(rows per workgroup, max coefficients, resident workgroups on the current device) of the register-resident
+    fused TRON (``re_tron_res_kernel``)."""
+    lib = require_re_lib()
+    return int(lib.pml_re_res_cap()), int(lib.pml_re_res_dmax()), int(lib.pml_re_res_grid())
+
+
+def re_tron_res(task_ent, task_t0, ws, grid: int, row_ptr, col_ptr, nip, lcol, val, y, off, wt, W, f, iters, reason,
+                zout, loss_id: int, l2: float, tol: float, max_iter: int, max_fail: int, max_cg: int,
+                npass: Optional[torch.Tensor] = None) -> torch.Tensor:
+    """Register-resident fused per-entity primal TRON (``re_tron_res_kernel``): ONE persistent launch of ``grid``
+    workgroups over the tasks ``task_ent`` (int32 entity per task, largest first) where task j is solved by the
+    ``task_t0[j+1] - task_t0[j]`` workgroups of tickets ``task_t0[j] ..`` (a cluster when > 1; clusters first,
+    ``ws`` holding 2 (dmax + 8) doubles per cluster ticket). Same data / outputs as :func:`re_tron_csr`. Returns
+    the device error flag (int32[1]; non-zero = a cluster wait timed out and the results are invalid)."""
+    lib = require_re_lib()
+    n_rows = y.numel()
+    n_tasks = int(task_ent.numel())
+    dev = W.device
+    for t in (task_ent, task_t0, ws, row_ptr, col_ptr, nip, lcol, val, y, off, wt, W, f, iters, reason, zout):
+        assert t.is_cuda and t.is_contiguous() and t.device == dev
+    assert task_ent.dtype == task_t0.dtype == torch.int32 and task_t0.numel() == n_tasks + 1
+    assert row_ptr.dtype == col_ptr.dtype == nip.dtype == torch.int64 and lcol.dtype == torch.int16
+    assert all(t.dtype == torch.float64 for t in (val, y, off, wt, W, f, zout, ws))
+    assert nip.numel() == n_rows + 1 and off.numel() == n_rows and zout.numel() == n_rows
+    cap, dmax, _ = re_res_params()
+    if os.environ.get("PML_CHECK_KERNEL_INPUTS", "0") == "1" and n_tasks:
+        te = task_ent.to(torch.int64)
+        k = (task_t0[1:] - task_t0[:-1]).to(torch.int64)
+        n_e = row_ptr[te + 1] - row_ptr[te]
+        assert int(te.min()) >= 0 and int(te.max()) < row_ptr.numel() - 1, "task entity out of range"
+        assert bool((k >= 1).all()) and int(k.max()) <= grid, "cluster larger than the resident grid"
+        assert bool((n_e <= k * cap).all()) and bool((n_e > (k - 1) * cap).all()), "rows do not match members"
+        assert int((col_ptr[te + 1] - col_ptr[te]).max()) <= dmax, "entity wider than the resident kernel"
+        kk = k.tolist()
+        cl = [i for i, v in enumerate(kk) if v > 1]
+        assert cl == list(range(len(cl))), "cluster tasks must come first"
+        need = int(task_t0[len(cl)]) if cl else 0
+        assert ws.numel() >= need * 2 * (dmax + 8), "cluster workspace too small"
+    ticket = torch.empty(1, dtype=torch.int32, device=dev)
+    bar = torch.empty(max(n_tasks, 1), dtype=torch.int32, device=dev)
+    err = torch.empty(1, dtype=torch.int32, device=dev)
+    check(lib.pml_re_tron_res(task_ent.data_ptr(), task_t0.data_ptr(), n_tasks, ticket.data_ptr(), bar.data_ptr(),
+                              ws.data_ptr(), err.data_ptr(), int(grid), row_ptr.data_ptr(), col_ptr.data_ptr(),
+                              nip.data_ptr(), lcol.data_ptr(), val.data_ptr(), y.data_ptr(), off.data_ptr(),
+                              wt.data_ptr(), W.data_ptr(), f.data_ptr(), iters.data_ptr(), reason.data_ptr(),
+                              zout.data_ptr(), None if npass is None else npass.data_ptr(), int(loss_id), float(l2),
+                              float(tol), int(max_iter), int(max_fail), int(max_cg), stream_handle(dev)),
+          "re_tron_res")
+    return err
 
 
 def check(rc: int, what: str):

@@ -29,6 +29,11 @@ FUSED_LOSSES = (0, 1, 2)             # logistic, Poisson, squared (the twice-dif
 _CLASSES = (256, 512, 1024, 2048)    # LDS size classes (max coefficients per entity of a launch)
 _HESS_CLASSES = (16, 32, 48, 64)     # tall-narrow entities: d_e padded to these, exact Hessian on the matrix cores
 HESS_DMAX = 64 if os.environ.get("PML_RE_HESS", "1") != "0" else 0
+# register-resident kernel (re_tron_res_kernel): entities of <= 1024 coefficients whose rows have <= 64 non-zeros;
+# entities longer than one workgroup's rows are split over a cluster of up to RES_KMAX workgroups
+RESIDENT = os.environ.get("PML_RE_RESIDENT", "1") != "0"
+RES_ROW_NNZ = 64
+RES_KMAX = int(os.environ.get("PML_RE_RES_KMAX", "128"))
 
 
 def fused_enabled() -> bool:
@@ -98,7 +103,33 @@ class EntityTronBatch:
         ent_nnz = (nip[self.row_ptr[1:]] - nip[self.row_ptr[:-1]])
         self.launches = []
         hess = de <= HESS_DMAX
-        for classes, sel, is_h in ((_HESS_CLASSES, hess, True), (_CLASSES, ~hess, False)):
+        # register-resident tasks (one persistent launch): clusters (k > 1 workgroups) first, largest first
+        self.res = None
+        stream_sel = ~hess
+        if RESIDENT and bool(stream_sel.any()):
+            from ..ops.native import re_res_params
+            cap, rdmax, grid = re_res_params()
+            kmax = min(RES_KMAX, grid // 2)
+            ent_maxrow = torch.zeros(self.B, dtype=torch.int64, device=dev).scatter_reduce_(
+                0, row_ent, row_nnz, reduce="amax", include_self=True)
+            k_e = (ne + cap - 1) // cap
+            res = stream_sel & (de <= rdmax) & (ent_maxrow <= RES_ROW_NNZ) & (k_e <= kmax)
+            if bool(res.any()):
+                idx = torch.nonzero(res).squeeze(1)
+                # clusters first (descending k), then single-workgroup entities by descending non-zeros
+                key = k_e[idx] * (int(ent_nnz.max()) + 1) + ent_nnz[idx]
+                idx = idx[torch.argsort(key, descending=True, stable=True)]
+                kk = k_e[idx]
+                t0 = torch.zeros(idx.numel() + 1, dtype=torch.int64, device=dev)
+                torch.cumsum(kk, 0, out=t0[1:])
+                n_cl_tickets = int(kk[kk > 1].sum())
+                from ..ops.native import require_re_lib
+                ws_n = int(require_re_lib().pml_re_res_ws_doubles(max(n_cl_tickets, 1)))
+                self.res = dict(ent=idx.to(torch.int32).contiguous(), t0=t0.to(torch.int32).contiguous(),
+                                ws=torch.empty(ws_n, dtype=torch.float64, device=dev), grid=grid,
+                                n=int(idx.numel()), clusters=int((kk > 1).sum()), tickets=int(t0[-1]))
+                stream_sel = stream_sel & ~res
+        for classes, sel, is_h in ((_HESS_CLASSES, hess, True), (_CLASSES, stream_sel, False)):
             cls = torch.searchsorted(torch.tensor(classes, device=dev), de)
             for c, dm in enumerate(classes):
                 idx = torch.nonzero(sel & (cls == c)).squeeze(1)
@@ -123,10 +154,20 @@ class EntityTronBatch:
         z = torch.empty(self.n_rows, dtype=torch.float64, device=dev)
         off = offsets.to(dev, torch.float64).contiguous()
         assert off.numel() == self.n_rows
+        err = None
+        if self.res is not None:
+            from ..ops.native import re_tron_res
+            r = self.res
+            err = re_tron_res(r["ent"], r["t0"], r["ws"], r["grid"], self.row_ptr, self.col_ptr, self.nip, self.lcol,
+                              self.val, self.y, off, self.w, W, f, iters, reason, z, loss.loss_id, l2, tol, max_iter,
+                              max_fail, max_cg)
         for dm, order, is_h in self.launches:
             re_tron_csr(order, self.row_ptr, self.col_ptr, self.nip, self.lcol, self.val, self.y, off, self.w,
                         self.scr, W, f, iters, reason, z, loss.loss_id, l2, tol, max_iter, max_fail, max_cg, dm,
                         hessian=is_h)
+        if err is not None and int(err.item()) != 0:
+            raise RuntimeError("register-resident random-effect TRON: a workgroup cluster wait timed out "
+                               "(results invalid); rerun with PML_RE_RESIDENT=0")
         self.W = W
         return FusedResult(W, f, iters.to(torch.long), reason.to(torch.long), z)
 

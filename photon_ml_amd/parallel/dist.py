@@ -129,6 +129,31 @@ def barrier(group=None):
         dist.barrier(group=group)
 
 
+def device_identity(device) -> str:
+    """A string naming the PHYSICAL device a rank computes on: host + PCI domain/bus/device + UUID for a GPU,
+    host + "cpu" otherwise. Two ranks sharing one GPU (rehearsal runs) get the same identity."""
+    import socket
+    host = socket.gethostname()
+    d = torch.device(device)
+    if d.type != "cuda":
+        return f"{host}:cpu"
+    idx = d.index if d.index is not None else torch.cuda.current_device()
+    p = torch.cuda.get_device_properties(idx)
+    pci = f"{getattr(p, 'pci_domain_id', 0):04x}:{getattr(p, 'pci_bus_id', 0):02x}:{getattr(p, 'pci_device_id', 0):02x}"
+    return f"{host}:{pci}:{getattr(p, 'uuid', '')}"
+
+
+def distinct_devices(device) -> int:
+    """Number of distinct physical devices over all ranks (all-gather of :func:`device_identity`). Benchmarks
+    report THIS as ``n_gpus`` (the rank count goes in ``n_ranks``)."""
+    ident = device_identity(device)
+    if not is_dist():
+        return 1
+    out = [None] * world_size()
+    dist.all_gather_object(out, ident)
+    return len(set(out))
+
+
 def check_finite_(t: torch.Tensor, what: str):
     """NaN/Inf guard on an all-reduced buffer (SURVEY §5 failure detection)."""
     if not bool(torch.isfinite(t).all()):

@@ -36,6 +36,34 @@ def stable_hash64(ids: np.ndarray) -> np.ndarray:
     return pd.util.hash_array(ids.astype(str).astype(object)).view(np.int64)
 
 
+def _lsr(t: torch.Tensor, k: int) -> torch.Tensor:
+    """Logical right shift of int64 tensors (torch's >> is arithmetic)."""
+    return (t >> k) & ((1 << (64 - k)) - 1)
+
+
+_HM1 = int(np.uint64(0xBF58476D1CE4E5B9).view(np.int64))
+_HM2 = int(np.uint64(0x94D049BB133111EB).view(np.int64))
+
+
+def entity_keys(ids, device=None) -> torch.Tensor:
+    """:func:`stable_hash64` of the entity ids as an int64 tensor on ``device``. Integer ids are hashed ON the
+    device (pandas' int64 hash is a splitmix64 finaliser; bitwise identical, so ownership does not depend on the
+    path); string ids go through pandas on the host once."""
+    dev = torch.device(device) if device is not None else torch.device("cpu")
+    if isinstance(ids, torch.Tensor):
+        t = ids.to(dev, torch.int64)
+    else:
+        a = np.asarray(ids)
+        if a.dtype.kind not in "iu":
+            return torch.from_numpy(stable_hash64(a)).to(dev)
+        t = torch.from_numpy(np.ascontiguousarray(a.astype(np.int64, copy=False))).to(dev)
+    t = t ^ _lsr(t, 30)
+    t = t * _HM1
+    t = t ^ _lsr(t, 27)
+    t = t * _HM2
+    return t ^ _lsr(t, 31)
+
+
 def comm_device(group=None) -> torch.device:
     if is_dist() and dist.get_backend(group) == "nccl":
         return torch.device("cuda", torch.cuda.current_device())
@@ -94,26 +122,46 @@ class EntityPartitioner:
         self.top_keys, self.top_owner = self.top_keys[srt], self.top_owner[srt]
 
     def owner(self, keys: np.ndarray) -> np.ndarray:
-        keys = np.asarray(keys, dtype=np.int64)
-        out = (keys.view(np.uint64) % np.uint64(self.n_parts)).astype(np.int64)
+        return self.owner_t(torch.from_numpy(np.asarray(keys, dtype=np.int64))).numpy()
+
+    def owner_t(self, keys: torch.Tensor) -> torch.Tensor:
+        """Owning rank of each key, computed where ``keys`` live (hash = key as uint64 mod n_parts, the bin-packed
+        top entities from their table)."""
+        keys = keys.to(torch.int64)
+        P = self.n_parts
+        out = torch.where(keys < 0, (keys.remainder(P) + (1 << 64) % P) % P, keys.remainder(P))
         if len(self.top_keys):
-            pos = np.searchsorted(self.top_keys, keys)
-            pos_c = np.minimum(pos, len(self.top_keys) - 1)
-            hit = self.top_keys[pos_c] == keys
-            out[hit] = self.top_owner[pos_c[hit]]
+            tk = self._top_on(keys.device)
+            pos = torch.searchsorted(tk[0], keys).clamp(max=tk[0].numel() - 1)
+            hit = tk[0][pos] == keys
+            out = torch.where(hit, tk[1][pos], out)
         return out
+
+    def _top_on(self, device):
+        cache = self.__dict__.setdefault("_top_cache", {})
+        key = str(device)
+        if key not in cache:
+            cache[key] = (torch.from_numpy(self.top_keys).to(device), torch.from_numpy(self.top_owner).to(device))
+        return cache[key]
 
     @staticmethod
     def build(local_keys: np.ndarray, group=None, top_k: int = TOP_ENTITIES) -> "EntityPartitioner":
         """All-gather per-rank (key, count) histograms (C9) and build the same partitioner everywhere."""
-        uk, cnt = np.unique(np.asarray(local_keys, dtype=np.int64), return_counts=True)
-        ks = all_gather_varlen(torch.from_numpy(uk), group)
-        cs = all_gather_varlen(torch.from_numpy(cnt.astype(np.int64)), group)
-        keys = torch.cat(ks).numpy()
-        counts = torch.cat(cs).numpy()
-        gk, inv = np.unique(keys, return_inverse=True)
-        gc = np.bincount(inv, weights=counts).astype(np.int64)
-        return EntityPartitioner(gk, gc, _world(), top_k)
+        return EntityPartitioner.build_t(torch.from_numpy(np.asarray(local_keys, dtype=np.int64)), group, top_k)
+
+    @staticmethod
+    def build_t(local_keys: torch.Tensor, group=None, top_k: int = TOP_ENTITIES) -> "EntityPartitioner":
+        """:meth:`build` with the histograms formed where ``local_keys`` live (the GPU under RCCL: unique +
+        counts, the gathered histograms' merge and the top-k selection are device sorts); only the top_k
+        (key, count) pairs reach the host for the bin packing."""
+        uk, cnt = torch.unique(local_keys.to(torch.int64), sorted=True, return_counts=True)
+        keys = torch.cat(all_gather_varlen(uk, group))
+        counts = torch.cat(all_gather_varlen(cnt.to(torch.int64), group))
+        gk, inv = torch.unique(keys, sorted=True, return_inverse=True)
+        gc = torch.zeros(gk.numel(), dtype=torch.int64, device=gk.device).index_add_(0, inv, counts)
+        # count descending, key ascending (gk is ascending and the sort is stable) -- as np.lexsort((keys, -counts))
+        top = torch.sort(-gc, stable=True).indices[:top_k]
+        return EntityPartitioner(gk[top].cpu().numpy(), gc[top].cpu().numpy(), _world(), top_k)
 
 
 class RowRouter:
@@ -128,13 +176,22 @@ class RowRouter:
     memory, because gloo collectives take CPU tensors.
     """
 
-    def __init__(self, dest: np.ndarray, group=None):
+    def __init__(self, dest, group=None):
         self.group = group
-        dest = np.asarray(dest, dtype=np.int64)
-        self.n_local = len(dest)
         P = _world()
-        self.perm = np.argsort(dest, kind="stable")          # local rows grouped by destination
-        self.send_counts = np.bincount(dest, minlength=P).tolist()
+        self._perm_on = {}
+        if isinstance(dest, torch.Tensor):       # device route: the permutation is a device sort
+            dest = dest.to(torch.int64)
+            perm_t = torch.argsort(dest, stable=True)
+            self._perm_on[str(perm_t.device)] = perm_t
+            self.perm = perm_t.cpu().numpy()
+            self.send_counts = torch.bincount(dest, minlength=P).tolist()
+            self.n_local = int(dest.numel())
+        else:
+            dest = np.asarray(dest, dtype=np.int64)
+            self.n_local = len(dest)
+            self.perm = np.argsort(dest, kind="stable")          # local rows grouped by destination
+            self.send_counts = np.bincount(dest, minlength=P).tolist()
         # exchange counts
         if is_dist():
             dev = comm_device(group)
@@ -146,7 +203,6 @@ class RowRouter:
             self.recv_counts = list(self.send_counts)
         self.n_recv = int(sum(self.recv_counts))
         self.src_rank = np.repeat(np.arange(P), self.recv_counts)
-        self._perm_on = {}
 
     def perm_on(self, device) -> torch.Tensor:
         """The routing permutation as an int64 tensor on ``device`` (uploaded once per device)."""
@@ -211,6 +267,47 @@ class RowRouter:
                             shape=(self.n_recv, x.shape[1]))
         out.has_sorted_indices = bool(getattr(x, "has_sorted_indices", False))
         return out
+
+    def forward_csr_device(self, x, device) -> "DeviceCSR":
+        """Route sparse rows and KEEP them on ``device`` (a :class:`DeviceCSR`): row lengths, column indices and
+        values each one all-to-all of device tensors under RCCL, the entry permutation a device gather — no scipy
+        and no host copy of the routed rows (they go straight to the device random-effect build)."""
+        from ..data.matrix import DeviceCSR
+        dev = torch.device(device)
+        cdev = comm_device(self.group)
+        if isinstance(x, DeviceCSR):
+            indptr, x_ind, x_val = x.indptr.to(cdev), x.indices.to(cdev), x.data.to(cdev)
+        else:
+            x = x.tocsr()
+            indptr = torch.from_numpy(x.indptr.astype(np.int64)).to(cdev)
+            x_ind = torch.from_numpy(x.indices).to(cdev)
+            x_val = torch.from_numpy(x.data).to(cdev, torch.float64)
+        lens = indptr[1:] - indptr[:-1]
+        perm = self.perm_on(cdev)
+        ol = lens[perm]
+        tot = int(ol.sum())
+        start = torch.cumsum(ol, 0) - ol
+        ent = torch.repeat_interleave(indptr[:-1][perm] - start, ol, output_size=tot) + torch.arange(tot, device=cdev)
+        ri = x_ind[ent].to(torch.int32)
+        rv = x_val[ent]
+        del ent, x_ind, x_val
+        P = len(self.send_counts)
+        seg = torch.repeat_interleave(torch.arange(P, device=cdev),
+                                      torch.tensor(self.send_counts, dtype=torch.int64, device=cdev),
+                                      output_size=perm.numel())
+        nnz_send = torch.zeros(P, dtype=torch.int64, device=cdev).index_add_(0, seg, ol).tolist()
+        rl = self.forward(lens)
+        rseg = torch.repeat_interleave(torch.arange(P, device=cdev),
+                                       torch.tensor(self.recv_counts, dtype=torch.int64, device=cdev),
+                                       output_size=rl.numel())
+        nnz_recv = torch.zeros(P, dtype=torch.int64, device=cdev).index_add_(0, rseg, rl).tolist()
+        if is_dist():
+            ri, _ = self._a2a(ri, nnz_send, nnz_recv)
+            rv, _ = self._a2a(rv, nnz_send, nnz_recv)
+        rip = torch.zeros(rl.numel() + 1, dtype=torch.int64, device=cdev)
+        torch.cumsum(rl, 0, out=rip[1:])
+        return DeviceCSR(rip.to(dev), ri.to(dev), rv.to(dev), (self.n_recv, x.shape[1]),
+                         bool(getattr(x, "has_sorted_indices", False)))
 
     def forward_strings(self, ids: np.ndarray) -> np.ndarray:
         """Route a per-row string column (e.g. entity ids): per-row codes into this rank's table of distinct

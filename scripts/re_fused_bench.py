@@ -1,11 +1,13 @@
-"""Microbenchmark of the fused per-entity primal TRON (re_tron_csr_kernel) on game5pl-like entities.
+"""Microbenchmark of the fused per-entity primal TRON on game5pl-like entities: the streaming kernel
+(re_tron_csr_kernel: rows re-read from memory every pass) vs the register-resident kernel (re_tron_res_kernel: rows
+loaded once into VGPRs, heavy entities split over workgroup clusters).
 
 Entities: power-law sizes (Pareto 1.3, 65 .. 20000 rows, the entities the row-space batch does not take at config
 5), 1000-feature pools + intercept (d_e <= 1001), 50 distinct pool features per row with N(0,1) values, logistic
-labels. Times the whole batch, the largest entities alone, and the rest alone — whether the launch is bound by
-its longest entity (one workgroup) or by aggregate throughput.
+labels. Times the whole batch, the largest entities alone, and the rest alone (tail vs throughput bound), and
+compares the two kernels' models.
 
-usage: python scripts/re_fused_bench.py [n_entities=43000] [variant list, e.g. 2,1]
+usage: python scripts/re_fused_bench.py [n_entities=43000] [kernels, e.g. stream,res]
 """
 import os
 import sys
@@ -14,10 +16,10 @@ import time
 sys.path.insert(0, os.path.join(os.path.dirname(os.path.abspath(__file__)), ".."))
 import torch
 
-from photon_ml_amd.ops.native import re_lib, re_tron_csr
+from photon_ml_amd.ops.native import re_lib, re_res_params, re_tron_csr, re_tron_res
 
 E = int(sys.argv[1]) if len(sys.argv) > 1 else 43_000
-VARIANTS = [int(v) for v in sys.argv[2].split(",")] if len(sys.argv) > 2 else [2]
+KERNELS = sys.argv[2].split(",") if len(sys.argv) > 2 else ["stream", "res"]
 dev = torch.device("cuda")
 g = torch.Generator(device=dev).manual_seed(1)
 u = torch.rand(E, generator=g, device=dev, dtype=torch.float64)
@@ -48,37 +50,65 @@ print(f"{E} entities, {N} rows, {N * NNZ / 1e6:.0f}M non-zeros, max n_e {int(n_e
 order_all = torch.argsort(n_e, descending=True).to(torch.int32)
 top = order_all[:64].contiguous()
 rest = order_all[64:].contiguous()
+cap, _, grid = re_res_params()
 
 
-def run(order, reps=3):
+def res_tasks(order):
+    ents = order.to(torch.int64)
+    k = (n_e[ents] + cap - 1) // cap
+    key = k * (int(n_e.max()) * NNZ + 1) + n_e[ents] * NNZ
+    ents = ents[torch.argsort(key, descending=True, stable=True)]
+    k = (n_e[ents] + cap - 1) // cap
+    t0 = torch.zeros(ents.numel() + 1, dtype=torch.int64, device=dev)
+    torch.cumsum(k, 0, out=t0[1:])
+    ncl = int(k[k > 1].sum())
+    ws = torch.empty(int(re_lib().pml_re_res_ws_doubles(max(ncl, 1))), dtype=torch.float64, device=dev)
+    return ents.to(torch.int32).contiguous(), t0.to(torch.int32).contiguous(), ws, int((k > 1).sum())
+
+
+def run(kernel, order, reps=3):
     W = torch.zeros(E * d, dtype=torch.float64, device=dev)
     f = torch.empty(E, dtype=torch.float64, device=dev)
     it = torch.empty(E, dtype=torch.int32, device=dev)
     rc = torch.empty(E, dtype=torch.int32, device=dev)
     z = torch.empty(N, dtype=torch.float64, device=dev)
     npass = torch.zeros(E, dtype=torch.int32, device=dev)
-    args = (row_ptr, col_ptr, nip, lcol, val, y, off, wt, scr)
-    re_tron_csr(order, *args, W, f, it, rc, z, 0, 1.0, 1e-12, 10, 5, 20, 1024, npass=npass)
+    if kernel == "res":
+        te, t0, ws, ncl = res_tasks(order)
+
+        def call(np_=None):
+            return re_tron_res(te, t0, ws, grid, row_ptr, col_ptr, nip, lcol, val, y, off, wt, W, f, it, rc, z, 0,
+                               1.0, 1e-12, 10, 5, 20, npass=np_)
+    else:
+        def call(np_=None):
+            re_tron_csr(order, row_ptr, col_ptr, nip, lcol, val, y, off, wt, scr, W, f, it, rc, z, 0, 1.0, 1e-12, 10,
+                        5, 20, 1024, npass=np_)
+            return None
+    err = call(npass)
     torch.cuda.synchronize()
+    assert err is None or int(err.item()) == 0, "cluster wait timed out"
     t = time.perf_counter()
     for _ in range(reps):
         W.zero_()
-        re_tron_csr(order, *args, W, f, it, rc, z, 0, 1.0, 1e-12, 10, 5, 20, 1024)
+        call()
     torch.cuda.synchronize()
     ms = (time.perf_counter() - t) / reps * 1e3
     sel = order.to(torch.int64)
     # bytes per row pass: 10 per non-zero (int16 column + fp64 value) + ~16 per row (row pointer, D / y, off, wt)
     gb = float((npass[sel].double() * (n_e[sel] * (NNZ * 10 + 16)).double()).sum()) / 1e9
-    return ms, it, gb, float(npass[sel].double().mean())
+    return ms, it.clone(), gb, float(npass[sel].double().mean()), W.clone(), z.clone()
 
 
-lib = re_lib()
-for v in VARIANTS:
-    lib.pml_re_set_variant(v)
-    t_all, it, gb, mp = run(order_all)
-    t_top, _, gb_top, mp_top = run(top)
-    t_rest, _, gb_rest, _ = run(rest)
-    print(f"variant {v}: all {t_all:.2f} ms ({gb:.1f} GB streamed, {gb / t_all:.2f} TB/s, mean passes/entity "
-          f"{mp:.1f}) | 64 largest alone {t_top:.2f} ms ({gb_top / t_top:.2f} TB/s, {mp_top:.1f} passes) | "
-          f"the rest {t_rest:.2f} ms ({gb_rest / t_rest:.2f} TB/s) | mean TRON iterations {it.double().mean():.2f}",
-          flush=True)
+models = {}
+for kern in KERNELS:
+    t_all, it, gb, mp, W, z = run(kern, order_all)
+    models[kern] = (W, z, it)
+    t_top, _, gb_top, mp_top, _, _ = run(kern, top)
+    t_rest, _, gb_rest, _, _, _ = run(kern, rest)
+    print(f"{kern}: all {t_all:.2f} ms ({gb:.1f} GB of row passes, {gb / t_all:.2f} TB/s equivalent, mean passes/entity "
+          f"{mp:.1f}) | 64 largest alone {t_top:.2f} ms | the rest {t_rest:.2f} ms | mean TRON iterations "
+          f"{it.double().mean():.3f}", flush=True)
+if len(models) == 2:
+    (Wa, za, ia), (Wb, zb, ib) = models.values()
+    print(f"max |W diff| {float((Wa - Wb).abs().max()):.3e}, max |z diff| {float((za - zb).abs().max()):.3e}, "
+          f"iteration counts equal for {float((ia == ib).double().mean()) * 100:.2f} % of entities", flush=True)

@@ -42,16 +42,23 @@ def test_multi_gpu_without_launcher_starts_torchrun_child(monkeypatch):
     assert seen["env"]["HSA_ENABLE_IPC_MODE_LEGACY"] == "0"
 
 
-def test_bench_game_gpus_2_without_launcher_reports_two_ranks():
-    """End to end on the CPU (gloo): the record says 2 GPUs because 2 ranks ran, not because of the flag."""
+def test_bench_game_two_ranks_on_one_device_refuse_or_say_rehearsal():
+    """End to end on the CPU (gloo): 2 ranks share one physical device (the host CPU), so the record may not call
+    them 2 GPUs — without --rehearsal the run refuses (exit 2); with it, n_gpus counts DEVICES (1) and n_ranks the
+    ranks (2), and the record says rehearsal."""
     env = {k: v for k, v in os.environ.items() if k not in ("WORLD_SIZE", "RANK", "LOCAL_RANK")}
-    p = subprocess.run([sys.executable, "bench_game.py", "--gpus", "2", "--config", "small", "--entities-per-gpu",
-                        "200", "--rows-per-entity", "4", "--re-dim", "10", "--re-nnz", "3", "--fe-dim", "500",
-                        "--fe-nnz", "5", "--steps", "1", "--warmup", "1", "--fe-iters", "2", "--re-iters", "2"],
-                       cwd=os.path.dirname(HERE), env=env, capture_output=True, text=True, timeout=600)
+    base = [sys.executable, "bench_game.py", "--gpus", "2", "--config", "small", "--entities-per-gpu", "200",
+            "--rows-per-entity", "4", "--re-dim", "10", "--re-nnz", "3", "--fe-dim", "500", "--fe-nnz", "5",
+            "--steps", "1", "--warmup", "1", "--fe-iters", "2", "--re-iters", "2"]
+    p = subprocess.run(base, cwd=os.path.dirname(HERE), env=env, capture_output=True, text=True, timeout=600)
+    assert p.returncode != 0, p.stderr[-2000:]     # the ranks exit 2; torchrun reports the failure
+    assert "refusing to report them as 2 GPUs" in p.stderr
+    p = subprocess.run(base + ["--rehearsal"], cwd=os.path.dirname(HERE), env=env, capture_output=True, text=True,
+                       timeout=600)
     assert p.returncode == 0, p.stderr[-3000:]
     rec = json.loads([ln for ln in p.stdout.splitlines() if ln.strip()][-1])
-    assert rec["n_gpus"] == 2 and rec["config"]["parallelism"] == "dp2+ep2"
+    assert rec["n_gpus"] == 1 and rec["n_ranks"] == 2 and rec["rehearsal"] is True
+    assert rec["config"]["parallelism"] == "dp2+ep2"
     assert rec["config"]["global_batch"] == 2 * 200 * 4
 
 
