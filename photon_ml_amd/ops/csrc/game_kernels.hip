@@ -7,8 +7,6 @@
 //   feature ids / values, models/game.py): each lane binary-searches its feature in the row's entity segment.
 //   Reference: photon-api/.../model/FixedEffectModel.scala:132-144, RandomEffectModel.scala:256-297.
 // * MFMA kernels (dense GEMM-shaped work on the matrix cores, fp64 v_mfma_f64_16x16x4f64):
-//   - bgram_mfma_kernel  — batched Gram K_b = A_b A_b^T of small dense blocks (row-space random-effect
-//     re-parametrisation, optimization/row_space.py);
 //   - gemm_nt_mfma_kernel — C = A B^T: back-projection of projected coefficients W P (and variances) of the
 //     random projection (projector/ProjectionMatrix.scala:95-124);
 // * spmm_rows_kernel — K15 forward random projection X P^T of sparse rows (ProjectionMatrix.scala:48-63).
@@ -85,66 +83,6 @@ __device__ __forceinline__ v4d mfma_f64_16x16x4(double a, double b, v4d c) {
   return __builtin_amdgcn_mfma_f64_16x16x4f64(a, b, c, 0, 0, 0);
 }
 
-// Batched Gram: for every block b, K_b[i][j] = sum_k A_b[i][k] A_b[j][k], A_b row-major [n x m] (stride lda
-// between rows, sa between blocks), K_b row-major [n x n] (stride sk between blocks). One work-group (4 waves)
-// per block; the block's rows are staged through LDS in K-slices of 64 columns; each wave owns output tiles
-// (ti, tj) with tj >= ti (the Gram is symmetric: the lower triangle is mirrored on store).
-#define GR_TK 64
-#define GR_MAXN 64
-__global__ __launch_bounds__(256) void bgram_mfma_kernel(int B, int n, int m, const double* __restrict__ A,
-                                                          long long sa, int lda, double* __restrict__ K,
-                                                          long long sk) {
-  __shared__ double tile[GR_MAXN][GR_TK + 1];
-  const int b = blockIdx.x;
-  if (b >= B) return;
-  const double* Ab = A + (long long)b * sa;
-  const int lane = threadIdx.x & 63, wv = threadIdx.x >> 6;
-  const int nt = (n + 15) / 16;
-  const int ntiles = nt * (nt + 1) / 2;
-  v4d acc[4];                                            // up to 4 tiles per wave (n <= 64 -> <= 10 tiles / 4 waves)
-#pragma unroll
-  for (int t = 0; t < 4; ++t) acc[t] = v4d{0.0, 0.0, 0.0, 0.0};
-  for (int k0 = 0; k0 < m; k0 += GR_TK) {
-    const int kw = min(GR_TK, m - k0);
-    __syncthreads();
-    for (int idx = threadIdx.x; idx < GR_MAXN * GR_TK; idx += 256) {
-      const int r = idx / GR_TK, c = idx % GR_TK;
-      tile[r][c] = (r < n && c < kw) ? Ab[(long long)r * lda + k0 + c] : 0.0;
-    }
-    __syncthreads();
-#pragma unroll
-    for (int t = 0; t < 4; ++t) {
-      const int id = wv + 4 * t;
-      if (id >= ntiles) break;
-      int ti = 0, rem = id;
-      while (rem >= nt - ti) { rem -= nt - ti; ++ti; }
-      const int tj = ti + rem;
-      for (int kk = 0; kk < kw; kk += 4) {
-        const double a = tile[16 * ti + (lane & 15)][kk + (lane >> 4)];
-        const double bb = tile[16 * tj + (lane & 15)][kk + (lane >> 4)];
-        acc[t] = mfma_f64_16x16x4(a, bb, acc[t]);
-      }
-    }
-  }
-  double* Kb = K + (long long)b * sk;
-#pragma unroll
-  for (int t = 0; t < 4; ++t) {
-    const int id = wv + 4 * t;
-    if (id >= ntiles) break;
-    int ti = 0, rem = id;
-    while (rem >= nt - ti) { rem -= nt - ti; ++ti; }
-    const int tj = ti + rem;
-    const int cj = 16 * tj + (lane & 15);
-#pragma unroll
-    for (int i = 0; i < 4; ++i) {
-      const int ri = 16 * ti + (lane >> 4) + 4 * i;
-      if (ri < n && cj < n) {
-        Kb[(long long)ri * n + cj] = acc[t][i];
-        Kb[(long long)cj * n + ri] = acc[t][i];
-      }
-    }
-  }
-}
 
 // C[M x N] = A[M x K] * B[N x K]^T (all row-major fp64, leading dimensions lda / ldb / ldc). Work-group = 4 waves
 // = a 32 x 32 output tile (2 x 2 wave tiles of 16 x 16); K staged through LDS in slices of 32. Grid over output
@@ -444,13 +382,6 @@ int pml_score_rows(const long long* indptr, const int* col, const double* val, l
   return 0;
 }
 
-int pml_bgram(int B, int n, int m, const double* A, long long sa, int lda, double* K, long long sk, void* stream) {
-  if (B <= 0) return 0;
-  if (n < 1 || n > GR_MAXN || m < 0) return -22;
-  hipLaunchKernelGGL(bgram_mfma_kernel, dim3(B), dim3(256), 0, (hipStream_t)stream, B, n, m, A, sa, lda, K, sk);
-  LAUNCH_CHECK();
-  return 0;
-}
 
 int pml_gemm_nt(int M, int N, int K, const double* A, int lda, const double* Bm, int ldb, double* C, int ldc,
                 void* stream) {

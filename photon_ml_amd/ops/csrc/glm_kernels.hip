@@ -1327,17 +1327,31 @@ static int g_rs_variant = 5;   // rs_tron variant: 0-2 rs_tron_kernel<V>; for n 
 static int g_tl_deep = 0;      // interleaved forward: 0 two-slot pipeline (P = 3), 1 deep S4/D1 (P = 5), 2 S6/D2 (P = 6)
 static int g_tl_deep_t = 0;    // interleaved transpose: same
 
+// Production builds compile only the production stream pipelines (interleaved layout: P = 3, plain: P = 0), the
+// production wave counts (forward 2, transpose 4) and fp64 LDS accumulation; the A/B variants behind the runtime
+// knobs (tl_pipe, tl_deep, tl_waves, tl_acc64) exist only in the experiment build (-DPML_TL_EXPERIMENT,
+// ops/build.py build_experiment, loaded with PML_GLM_LIB), where the knobs select them.
+#ifdef PML_TL_EXPERIMENT
+#define TL_KNOB(x) (x)
+#define TL_WAVES_F g_tl_waves
+#define TL_WAVES_T g_tl_waves_t
+#else
+#define TL_KNOB(x) 0
+#define TL_WAVES_F 2
+#define TL_WAVES_T 4
+#endif
+
 template <typename VT, typename XT, typename RT, typename AT, int MAXR>
 static void tl_fwd_launch(const TLFwdDesc* c, const void* x, FwdArgs<XT, RT> a, double* stats, hipStream_t st) {
 #define TLF(NW, P) hipLaunchKernelGGL((tl_fwd_kernel<VT, XT, RT, AT, MAXR, 2, NW, P>), dim3(c->nblk), dim3(NW * 64), 0, \
                                     st, c->blk, c->rbits, c->pack, (const VT*)c->val, c->nar, (const XT*)x, a, stats, \
                                     c->live)
   if (c->il) {
-    if (g_tl_waves <= 2) { if (g_tl_deep == 2) TLF(2, 6); else if (g_tl_deep) TLF(2, 5); else TLF(2, 3); }
-    else { if (g_tl_deep == 2) TLF(4, 6); else if (g_tl_deep) TLF(4, 5); else TLF(4, 3); }
+    if (TL_WAVES_F <= 2) { if (TL_KNOB(g_tl_deep) == 2) TLF(2, 6); else if (TL_KNOB(g_tl_deep)) TLF(2, 5); else TLF(2, 3); }
+    else { if (TL_KNOB(g_tl_deep) == 2) TLF(4, 6); else if (TL_KNOB(g_tl_deep)) TLF(4, 5); else TLF(4, 3); }
   }
-  else if (g_tl_waves == 2) { if (g_tl_pipe == 1) TLF(2, 1); else TLF(2, 0); }
-  else { if (g_tl_pipe == 1) TLF(4, 1); else TLF(4, 0); }
+  else if (TL_WAVES_F == 2) { if (TL_KNOB(g_tl_pipe) == 1) TLF(2, 1); else TLF(2, 0); }
+  else { if (TL_KNOB(g_tl_pipe) == 1) TLF(4, 1); else TLF(4, 0); }
 #undef TLF
 }
 
@@ -1348,12 +1362,12 @@ static void tl_fwd_multi_launch(const TLFwdMultiDesc* c, const void* x, FwdArgs<
                                       dim3(NW * 64), 0, st, c->blk, c->rbits, c->ptrs, (const XT*)x, a, stats, \
                                       c->live)
   if (c->il) {
-    if (g_tl_deep == 2) { if (g_tl_waves == 2) TLM(2, 6); else TLM(4, 6); }
-    else if (g_tl_deep) { if (g_tl_waves == 2) TLM(2, 5); else TLM(4, 5); }
-    else { if (g_tl_waves == 2) TLM(2, 3); else TLM(4, 3); }
+    if (TL_KNOB(g_tl_deep) == 2) { if (TL_WAVES_F == 2) TLM(2, 6); else TLM(4, 6); }
+    else if (TL_KNOB(g_tl_deep)) { if (TL_WAVES_F == 2) TLM(2, 5); else TLM(4, 5); }
+    else { if (TL_WAVES_F == 2) TLM(2, 3); else TLM(4, 3); }
   }
-  else if (g_tl_waves == 2) { if (g_tl_pipe == 2) TLM(2, 2); else TLM(2, 0); }
-  else { if (g_tl_pipe == 2) TLM(4, 2); else TLM(4, 0); }
+  else if (TL_WAVES_F == 2) { if (TL_KNOB(g_tl_pipe) == 2) TLM(2, 2); else TLM(2, 0); }
+  else { if (TL_KNOB(g_tl_pipe) == 2) TLM(4, 2); else TLM(4, 0); }
 #undef TLM
 }
 
@@ -1362,7 +1376,7 @@ static int tl_fwd_multi_impl(const TLFwdMultiDesc* c, const void* x, FwdArgs<XT,
                              hipStream_t st) {
   if (c->nblk <= 0) return 0;
   if (c->rbits < 1 || c->rbits > 11) return -22;
-  const bool f64 = sizeof(XT) == 8 || g_tl_acc64;
+  const bool f64 = sizeof(XT) == 8 || !TL_KNOB(!g_tl_acc64);
   if (f64) {
     if (c->rbits <= 10) tl_fwd_multi_launch<VT, XT, RT, double, 1024>(c, x, a, stats, st);
     else tl_fwd_multi_launch<VT, XT, RT, double, 2048>(c, x, a, stats, st);
@@ -1378,7 +1392,7 @@ template <typename VT, typename XT, typename RT>
 static int tl_fwd_impl(const TLFwdDesc* c, const void* x, FwdArgs<XT, RT> a, double* stats, hipStream_t st) {
   if (c->nblk <= 0) return 0;
   if (c->rbits < 1 || c->rbits > TL_MAXBITS) return -22;
-  const bool f64 = sizeof(XT) == 8 || g_tl_acc64;
+  const bool f64 = sizeof(XT) == 8 || !TL_KNOB(!g_tl_acc64);
   if (f64) {
     if (c->rbits > 11) return -22;  // fp64 LDS: 4 waves x 2048 rows = 64 KB
     if (c->rbits <= 10) tl_fwd_launch<VT, XT, RT, double, 1024>(c, x, a, stats, st);
@@ -1400,11 +1414,11 @@ static void tl_t_launch(const TLTDesc* c, const void* x, double* G, double* part
                                     st, c->items, c->cbits, c->pack, (const VT*)c->val, c->nar, (const XT*)x, G, c->dim, \
                                     parts, c->live)
   if (c->il) {
-    if (g_tl_waves_t == 2) { if (g_tl_deep_t == 2) TLT(2, 6); else if (g_tl_deep_t) TLT(2, 5); else TLT(2, 3); }
-    else { if (g_tl_deep_t == 2) TLT(4, 6); else if (g_tl_deep_t) TLT(4, 5); else TLT(4, 3); }
+    if (TL_WAVES_T == 2) { if (TL_KNOB(g_tl_deep_t) == 2) TLT(2, 6); else if (TL_KNOB(g_tl_deep_t)) TLT(2, 5); else TLT(2, 3); }
+    else { if (TL_KNOB(g_tl_deep_t) == 2) TLT(4, 6); else if (TL_KNOB(g_tl_deep_t)) TLT(4, 5); else TLT(4, 3); }
   }
-  else if (g_tl_waves_t == 2) { if (g_tl_pipe_t == 1) TLT(2, 1); else TLT(2, 0); }
-  else { if (g_tl_pipe_t == 1) TLT(4, 1); else TLT(4, 0); }
+  else if (TL_WAVES_T == 2) { if (TL_KNOB(g_tl_pipe_t) == 1) TLT(2, 1); else TLT(2, 0); }
+  else { if (TL_KNOB(g_tl_pipe_t) == 1) TLT(4, 1); else TLT(4, 0); }
 #undef TLT
 }
 
@@ -1412,7 +1426,7 @@ template <typename VT, typename XT, bool SQ>
 static int tl_t_impl(const TLTDesc* c, const void* x, double* G, double* parts, hipStream_t st) {
   if (c->nitems <= 0) return 0;
   if (c->cbits < 1 || c->cbits > TL_MAXBITS) return -22;
-  const bool f64 = sizeof(XT) == 8 || g_tl_acc64;
+  const bool f64 = sizeof(XT) == 8 || !TL_KNOB(!g_tl_acc64);
   if (f64) {
     if (c->cbits > 11) return -22;
     if (c->cbits <= 10) tl_t_launch<VT, XT, double, SQ, 1024>(c, x, G, parts, st);
@@ -1444,11 +1458,11 @@ static void tl_t_multi_launch(const TLTMultiDesc* c, const void* x, double* G, d
                                        dim3(NW * 64), 0, st, c->items, c->cbits, c->ptrs, (const XT*)x, G, \
                                        c->dim, parts, c->live)
   if (c->il) {
-    if (g_tl_waves_t == 2) { if (g_tl_deep_t == 2) TLTM(2, 6); else if (g_tl_deep_t) TLTM(2, 5); else TLTM(2, 3); }
-    else { if (g_tl_deep_t == 2) TLTM(4, 6); else if (g_tl_deep_t) TLTM(4, 5); else TLTM(4, 3); }
+    if (TL_WAVES_T == 2) { if (TL_KNOB(g_tl_deep_t) == 2) TLTM(2, 6); else if (TL_KNOB(g_tl_deep_t)) TLTM(2, 5); else TLTM(2, 3); }
+    else { if (TL_KNOB(g_tl_deep_t) == 2) TLTM(4, 6); else if (TL_KNOB(g_tl_deep_t)) TLTM(4, 5); else TLTM(4, 3); }
   }
-  else if (g_tl_waves_t == 2) { if (g_tl_pipe_t == 2) TLTM(2, 2); else TLTM(2, 0); }
-  else { if (g_tl_pipe_t == 2) TLTM(4, 2); else TLTM(4, 0); }
+  else if (TL_WAVES_T == 2) { if (TL_KNOB(g_tl_pipe_t) == 2) TLTM(2, 2); else TLTM(2, 0); }
+  else { if (TL_KNOB(g_tl_pipe_t) == 2) TLTM(4, 2); else TLTM(4, 0); }
 #undef TLTM
 }
 
@@ -1456,7 +1470,7 @@ template <typename VT, typename XT, bool SQ>
 static int tl_t_multi_impl(const TLTMultiDesc* c, const void* x, double* G, double* parts, hipStream_t st) {
   if (c->nitems <= 0) return 0;
   if (c->cbits < 1 || c->cbits > 11) return -22;
-  const bool f64 = sizeof(XT) == 8 || g_tl_acc64;
+  const bool f64 = sizeof(XT) == 8 || !TL_KNOB(!g_tl_acc64);
   if (f64) {
     if (c->cbits <= 10) tl_t_multi_launch<VT, XT, double, SQ, 1024>(c, x, G, parts, st);
     else tl_t_multi_launch<VT, XT, double, SQ, 2048>(c, x, G, parts, st);
@@ -2925,6 +2939,7 @@ int pml_reduce_stats(const double* stats, int n, double* out, int accumulate, do
 
 // ---- tiled layout entry points ------------------------------------------------------------------------------
 int pml_tl_maxbits() { return TL_MAXBITS; }
+int pml_tl_experiment() { return TL_KNOB(1); }
 void pml_tl_config(int acc64, int waves, int waves_t, int pipe) {
   g_tl_acc64 = acc64; g_tl_waves = (waves == 1 || waves == 2) ? waves : 4; g_tl_waves_t = waves_t == 2 ? 2 : 4; g_tl_pipe = pipe & 3; g_tl_pipe_t = (pipe >> 2) & 3;
 }

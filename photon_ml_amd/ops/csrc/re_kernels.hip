@@ -36,7 +36,6 @@
 
 #define RE_NW 4                 // waves per workgroup (one entity)
 #define RE_THREADS (RE_NW * 64)
-#define RE_R 4                  // rows in flight per wave
 
 enum { LOSS_LOGISTIC = 0, LOSS_POISSON = 1, LOSS_SQUARED = 2 };
 
@@ -235,176 +234,6 @@ __device__ __forceinline__ void row_pass(const ReTronArgs& a, long long r0, long
   }
 }
 
-// Variant 3: the batch loop software-pipelined — while batch b computes (LDS gathers, DPP sums, loss, LDS
-// scatters) the entries of batch b + 1 are already in flight, so a wave keeps memory requests outstanding through
-// its arithmetic instead of alternating load / compute. Two register slots of RE_U3 row groups each.
-#define RE_U3 2
-#define RE_BATCH3 (RE_RPI * RE_U3)
-template <int MODE>
-__device__ __forceinline__ void row_pass_pipe(const ReTronArgs& a, long long r0, long long r1,
-                                              const double* __restrict__ vec, double* __restrict__ acc,
-                                              const double* __restrict__ Dc, double* __restrict__ Dn,
-                                              double* __restrict__ Zn, double& fpart) {
-  const int lane = threadIdx.x & 63, w = threadIdx.x >> 6;
-  const int grp = lane / RE_G, gl = lane % RE_G;
-  const long long step = (long long)RE_NW * RE_BATCH3;
-  struct Slot {
-    long long base, lo[RE_U3], hi[RE_U3];
-    int c[RE_U3][RE_K];
-    double v[RE_U3][RE_K], rs[RE_U3][3];
-  };
-  auto fetch_ptr = [&](long long b) -> long long {
-    const long long i = b + (lane <= RE_BATCH3 ? lane : RE_BATCH3);
-    return b < r1 ? a.nip[i < r1 ? i : r1] : 0;
-  };
-  auto load = [&](Slot& sl, long long b, long long np) {
-    sl.base = b;
-#pragma unroll
-    for (int u = 0; u < RE_U3; ++u) {
-      const int q = u * RE_RPI + grp;
-      sl.lo[u] = __shfl(np, q, 64);
-      sl.hi[u] = __shfl(np, q + 1, 64);
-      const long long i = b + q;
-      const bool valid = i < r1;
-      if (MODE == 0) {
-        sl.rs[u][0] = valid ? Dc[i] : 0.0;
-      } else {
-        sl.rs[u][0] = valid ? a.wt[i] : 0.0;
-        sl.rs[u][1] = valid ? a.off[i] : 0.0;
-        sl.rs[u][2] = valid ? a.y[i] : 0.0;
-      }
-#pragma unroll
-      for (int k = 0; k < RE_K; ++k) {
-        const long long p = sl.lo[u] + gl + RE_G * k;
-        const bool in = p < sl.hi[u];
-        sl.c[u][k] = in ? (int)a.lcol[p] : 0;
-        sl.v[u][k] = in ? a.val[p] : 0.0;
-      }
-    }
-  };
-  auto process = [&](const Slot& sl) {
-#pragma unroll
-    for (int u = 0; u < RE_U3; ++u) {
-      double dot = 0.0;
-      if (MODE != 2) {
-#pragma unroll
-        for (int k = 0; k < RE_K; ++k) dot = fma(sl.v[u][k], vec[sl.c[u][k]], dot);
-        for (long long p = sl.lo[u] + gl + RE_G * RE_K; p < sl.hi[u]; p += RE_G) dot = fma(a.val[p], vec[a.lcol[p]], dot);
-        dot = row16_total(dot);
-      }
-      const long long i = sl.base + u * RE_RPI + grp;
-      const bool valid = i < r1;
-      double t;
-      if (MODE == 0) {
-        t = sl.rs[u][0] * dot;
-      } else {
-        double l = 0.0, dl = 0.0, d2 = 0.0;
-        if (valid) {
-          pointwise_loss(a.loss, dot + sl.rs[u][1], sl.rs[u][2], l, dl, d2);
-          if (gl == 0) {
-            fpart += sl.rs[u][0] * l;
-            if (MODE == 1) { Dn[i] = sl.rs[u][0] * d2; Zn[i] = dot; }
-          }
-        }
-        t = sl.rs[u][0] * dl;
-      }
-#pragma unroll
-      for (int k = 0; k < RE_K; ++k)
-        if (sl.lo[u] + gl + RE_G * k < sl.hi[u]) atomicAdd(&acc[sl.c[u][k]], t * sl.v[u][k]);
-      for (long long p = sl.lo[u] + gl + RE_G * RE_K; p < sl.hi[u]; p += RE_G)
-        atomicAdd(&acc[a.lcol[p]], t * a.val[p]);
-    }
-  };
-  long long base = r0 + (long long)w * RE_BATCH3;
-  if (base >= r1) return;
-  Slot A, B;
-  long long np = fetch_ptr(base);
-  load(A, base, np);
-  np = fetch_ptr(base + step);
-  for (;; base += 2 * step) {
-    // A holds batch `base`; B gets batch base + step while A computes
-    const bool hasB = base + step < r1;
-    if (hasB) load(B, base + step, np);
-    np = fetch_ptr(base + 2 * step);
-    process(A);
-    if (!hasB) break;
-    const bool hasA = base + 2 * step < r1;
-    if (hasA) load(A, base + 2 * step, np);
-    np = fetch_ptr(base + 3 * step);
-    process(B);
-    if (!hasA) break;
-  }
-}
-
-// Previous row pass (wave per row, lane = entry; one row's entries per instruction) — kept for A/B
-// (PML_RE_ROWPASS=1).
-template <int MODE>
-__device__ __forceinline__ void row_pass_v1(const ReTronArgs& a, long long r0, long long r1,
-                                            const double* __restrict__ vec, double* __restrict__ acc,
-                                            const double* __restrict__ Dc, double* __restrict__ Dn,
-                                            double* __restrict__ Zn, double& fpart) {
-  const int lane = threadIdx.x & 63, w = threadIdx.x >> 6;
-  for (long long base = r0 + (long long)w * RE_R; base < r1; base += (long long)RE_NW * RE_R) {
-    long long lo[RE_R], hi[RE_R];
-    int c[RE_R];
-    double v[RE_R], dot[RE_R], t[RE_R];
-#pragma unroll
-    for (int q = 0; q < RE_R; ++q) {
-      const long long i = base + q;
-      lo[q] = i < r1 ? a.nip[i] : 0;
-      hi[q] = i < r1 ? a.nip[i + 1] : 0;
-    }
-#pragma unroll
-    for (int q = 0; q < RE_R; ++q) {
-      const long long p = lo[q] + lane;
-      const bool in = p < hi[q];
-      c[q] = in ? (int)a.lcol[p] : 0;
-      v[q] = in ? a.val[p] : 0.0;
-    }
-#pragma unroll
-    for (int q = 0; q < RE_R; ++q) {
-      dot[q] = MODE == 2 ? 0.0 : v[q] * vec[c[q]];
-      if (MODE != 2) {
-        for (long long p = lo[q] + 64 + lane; p < hi[q]; p += 64) dot[q] = fma(a.val[p], vec[a.lcol[p]], dot[q]);
-      }
-    }
-#pragma unroll
-    for (int q = 0; q < RE_R; ++q) {
-      if (MODE != 2) dot[q] = wave_total(dot[q]);
-      const long long i = base + q;
-      const bool valid = i < r1;
-      if (MODE == 0) {
-        t[q] = valid ? Dc[i] * dot[q] : 0.0;
-      } else {
-        double l = 0.0, dl = 0.0, d2 = 0.0, wi = 0.0;
-        if (valid) {
-          wi = a.wt[i];
-          pointwise_loss(a.loss, dot[q] + a.off[i], a.y[i], l, dl, d2);
-          if (lane == 0) {
-            fpart += wi * l;
-            if (MODE == 1) { Dn[i] = wi * d2; Zn[i] = dot[q]; }
-          }
-        }
-        t[q] = wi * dl;
-      }
-    }
-#pragma unroll
-    for (int q = 0; q < RE_R; ++q) {
-      if (lo[q] + lane < hi[q]) atomicAdd(&acc[c[q]], t[q] * v[q]);
-      for (long long p = lo[q] + 64 + lane; p < hi[q]; p += 64) atomicAdd(&acc[a.lcol[p]], t[q] * a.val[p]);
-    }
-  }
-}
-
-template <int MODE, int V>
-__device__ __forceinline__ void rows(const ReTronArgs& a, long long r0, long long r1, const double* vec, double* acc,
-                                     const double* Dc, double* Dn, double* Zn, double& fpart) {
-  if constexpr (V == 1) row_pass_v1<MODE>(a, r0, r1, vec, acc, Dc, Dn, Zn, fpart);
-  else if constexpr (V == 3) row_pass_pipe<MODE>(a, r0, r1, vec, acc, Dc, Dn, Zn, fpart);
-  else row_pass<MODE>(a, r0, r1, vec, acc, Dc, Dn, Zn, fpart);
-}
-
-template <int V>
 __global__ __launch_bounds__(RE_THREADS) void re_tron_csr_kernel(ReTronArgs a) {
   extern __shared__ __attribute__((aligned(16))) double smem[];
   const int e = a.order[blockIdx.x];
@@ -436,8 +265,8 @@ __global__ __launch_bounds__(RE_THREADS) void re_tron_csr_kernel(ReTronArgs a) {
     __syncthreads();
     zero_own();
     double fp = 0.0;
-    if (at_zero) rows<2, V>(a, r0, r1, vec, myacc, nullptr, nullptr, nullptr, fp);
-    else rows<1, V>(a, r0, r1, vec, myacc, nullptr, D[nb], Z[nb], fp);
+    if (at_zero) row_pass<2>(a, r0, r1, vec, myacc, nullptr, nullptr, nullptr, fp);
+    else row_pass<1>(a, r0, r1, vec, myacc, nullptr, D[nb], Z[nb], fp);
     __syncthreads();
     double s3[3] = {fp, 0.0, 0.0};
     for (int j = tid; j < d; j += RE_THREADS) {
@@ -495,7 +324,7 @@ __global__ __launch_bounds__(RE_THREADS) void re_tron_csr_kernel(ReTronArgs a) {
       __syncthreads();
       zero_own();
       double fp = 0.0;
-      rows<0, V>(a, r0, r1, sD, myacc, D[cur], nullptr, nullptr, fp);
+      row_pass<0>(a, r0, r1, sD, myacc, D[cur], nullptr, nullptr, fp);
       __syncthreads();
       double s5[5] = {0.0, 0.0, 0.0, 0.0, 0.0};
       for (int j = tid; j < d; j += RE_THREADS) {
@@ -1368,12 +1197,7 @@ __global__ __launch_bounds__(RS_THREADS) void re_tron_res_kernel(ReTronArgs a, R
   }
 }
 
-static int g_re_variant = 2;   // row pass: 2 = 16 lanes per row, batched (default); 3 = the same, software-pipelined;
-                               // 1 = one row per wave
-
 extern "C" {
-
-void pml_re_set_variant(int v) { g_re_variant = (v == 1 || v == 3) ? v : 2; }
 
 // Shared memory of one workgroup for entities of at most ``dmax`` coefficients.
 size_t pml_re_tron_smem(int dmax) { return ((size_t)(5 + RE_NW) * dmax + 2 * RE_NW * 8) * sizeof(double); }
@@ -1389,9 +1213,7 @@ int pml_re_tron_csr(const int* order, int n_launch, const long long* row_ptr, co
   if (smem > 160 * 1024) return -22;
   ReTronArgs a{order, n_launch, row_ptr, col_ptr, nip, lcol, val, y, off, wt, scr, n_rows, W, f, iters, reason,
                zout, npass, loss, l2, tol, max_iter, max_fail, max_cg, dmax};
-  if (g_re_variant == 1) hipLaunchKernelGGL(re_tron_csr_kernel<1>, dim3(n_launch), dim3(RE_THREADS), smem, st, a);
-  else if (g_re_variant == 3) hipLaunchKernelGGL(re_tron_csr_kernel<3>, dim3(n_launch), dim3(RE_THREADS), smem, st, a);
-  else hipLaunchKernelGGL(re_tron_csr_kernel<2>, dim3(n_launch), dim3(RE_THREADS), smem, st, a);
+  hipLaunchKernelGGL(re_tron_csr_kernel, dim3(n_launch), dim3(RE_THREADS), smem, st, a);
   LAUNCH_CHECK();
   return 0;
 }

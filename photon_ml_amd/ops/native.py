@@ -172,6 +172,13 @@ def configure(**kw):
     return dict(KERNEL_CONFIG)
 
 
+def tl_experiment_build() -> bool:
+    """True when the loaded GLM library is the experiment build (-DPML_TL_EXPERIMENT): only there do the stream
+    pipeline / wave-count / accumulation knobs select A/B kernel variants."""
+    lib = glm_lib()
+    return lib is not None and bool(lib.pml_tl_experiment())
+
+
 def require_glm_lib() -> ctypes.CDLL:
     lib = glm_lib()
     if lib is None:
@@ -500,8 +507,6 @@ def game_lib() -> Optional[ctypes.CDLL]:
     if lib is not None and not getattr(lib, "_pml_typed", False):
         lib.pml_score_rows.argtypes = [c_void_p, c_void_p, c_void_p, ctypes.c_longlong, c_void_p, c_void_p,
                                        c_void_p, c_void_p, c_void_p, c_void_p]
-        lib.pml_bgram.argtypes = [c_int, c_int, c_int, c_void_p, ctypes.c_longlong, c_int, c_void_p,
-                                  ctypes.c_longlong, c_void_p]
         lib.pml_gemm_nt.argtypes = [c_int, c_int, c_int, c_void_p, c_int, c_void_p, c_int, c_void_p, c_int,
                                     c_void_p]
         lib.pml_spmm_rows.argtypes = [c_void_p, c_void_p, c_void_p, ctypes.c_longlong, c_void_p, c_int, c_void_p,
@@ -511,7 +516,7 @@ def game_lib() -> Optional[ctypes.CDLL]:
         lib.pml_seg_gram.argtypes = [c_int, c_int, c_int] + [c_void_p] * 8
         lib.pml_tl_compact.argtypes = [c_int, c_int, ctypes.POINTER(CmpArgs), c_void_p]
         lib.pml_tl_compact.restype = c_int
-        for f in ("pml_score_rows", "pml_bgram", "pml_gemm_nt", "pml_spmm_rows", "pml_downsample"):
+        for f in ("pml_score_rows", "pml_gemm_nt", "pml_spmm_rows", "pml_downsample"):
             getattr(lib, f).restype = c_int
         lib._pml_typed = True
     return lib
@@ -543,19 +548,6 @@ def score_rows(indptr: torch.Tensor, col32: torch.Tensor, val: torch.Tensor, w: 
     check(lib.pml_score_rows(indptr.data_ptr(), col32.data_ptr(), val.data_ptr(), n, w.data_ptr(), p(ent), p(eptr),
                              p(efeat), out.data_ptr(), stream_handle(val.device)), "score_rows")
     return out
-
-
-def batched_gram(A: torch.Tensor) -> torch.Tensor:
-    """``K[b] = A[b] A[b]^T`` for a batch of dense fp64 blocks [B, n, m] with n <= 64 (``bgram_mfma_kernel``,
-    fp64 MFMA on the matrix cores); ``bmm`` off the GPU or for larger n."""
-    if A.device.type != "cuda" or A.shape[1] > 64 or A.dtype != torch.float64:
-        return torch.bmm(A, A.transpose(1, 2))
-    lib = require_game_lib()
-    A = A.contiguous()
-    B, n, m = A.shape
-    K = torch.empty(B, n, n, dtype=torch.float64, device=A.device)
-    check(lib.pml_bgram(B, n, m, A.data_ptr(), n * m, m, K.data_ptr(), n * n, stream_handle(A.device)), "bgram")
-    return K
 
 
 def gemm_nt(A: torch.Tensor, Bm: torch.Tensor) -> torch.Tensor:
@@ -646,8 +638,6 @@ def re_lib() -> Optional[ctypes.CDLL]:
         lib.pml_re_tron_hess.restype = c_int
         lib.pml_re_tron_hess_smem.argtypes = [c_int]
         lib.pml_re_tron_hess_smem.restype = ctypes.c_size_t
-        lib.pml_re_set_variant.argtypes = [c_int]
-        lib.pml_re_set_variant(int(os.environ.get("PML_RE_ROWPASS", "2")))
         lib.pml_re_tron_res.argtypes = ([c_void_p, c_void_p, c_int] + [c_void_p] * 4 + [c_int] + [c_void_p] * 14
                                         + [c_int, c_double, c_double, c_int, c_int, c_int, c_void_p])
         lib.pml_re_tron_res.restype = c_int

@@ -1,5 +1,5 @@
 """Timing + fp64 parity of the hand-written MFMA kernels (game_kernels.hip): gemm_nt (the RANDOM projection's
-back-map shape: [entities x k] x [D x k]^T) and the batched small Gram matrices. Run under rocprofv3 --pmc with
+back-map shape: [entities x k] x [D x k]^T). Run under rocprofv3 --pmc with
 SQ_INSTS_VALU_MFMA_* counters for the MFMA evidence (profiles/pmc_mfma_kernels.txt)."""
 import os
 import sys
@@ -8,7 +8,7 @@ import time
 sys.path.insert(0, os.path.join(os.path.dirname(os.path.abspath(__file__)), ".."))
 import torch
 
-from photon_ml_amd.ops.native import batched_gram, gemm_nt
+from photon_ml_amd.ops.native import gemm_nt
 
 g = torch.Generator(device="cuda").manual_seed(0)
 for M, N, K in ((20000, 4096, 128), (4096, 4096, 1024)):
@@ -24,16 +24,3 @@ for M, N, K in ((20000, 4096, 128), (4096, 4096, 1024)):
     torch.cuda.synchronize()
     ms = (time.perf_counter() - t) / 5 * 1e3
     print(f"gemm_nt {M}x{N}x{K}: {ms:.3f} ms, {2 * M * N * K / ms / 1e9:.1f} TFLOP/s fp64, rel err {err:.1e}", flush=True)
-for B_, n, m in ((100000, 20, 64), (20000, 64, 256)):
-    A = torch.randn(B_, n, m, dtype=torch.float64, device="cuda", generator=g)
-    K = batched_gram(A)
-    ref = A @ A.transpose(1, 2)
-    err = float((K - ref).abs().max() / ref.abs().max())
-    torch.cuda.synchronize()
-    t = time.perf_counter()
-    for _ in range(5):
-        batched_gram(A)
-    torch.cuda.synchronize()
-    ms = (time.perf_counter() - t) / 5 * 1e3
-    print(f"bgram {B_}x{n}x{m}: {ms:.3f} ms, {2 * B_ * n * n * m / ms / 1e9:.1f} TFLOP/s fp64, rel err {err:.1e}",
-          flush=True)

@@ -114,18 +114,6 @@ def test_scoring_kernel_paths_and_masks():
     torch.testing.assert_close(half.score(sub, "cuda").cpu(), half.score(sub, "cpu"), rtol=1e-12, atol=1e-12)
 
 
-@pytest.mark.parametrize("n,m", [(1, 1), (7, 5), (16, 64), (20, 100), (33, 7), (64, 130)])
-def test_batched_gram_mfma_matches_fp64(n, m):
-    """bgram_mfma_kernel (fp64 MFMA 16x16x4 on the matrix cores) == torch fp64 bmm."""
-    from photon_ml_amd.ops.native import batched_gram
-    g = torch.Generator(device="cuda").manual_seed(n * 1000 + m)
-    A = torch.randn(37, n, m, generator=g, device="cuda", dtype=torch.float64)
-    K = batched_gram(A)
-    ref = torch.bmm(A, A.transpose(1, 2))
-    torch.testing.assert_close(K, ref, rtol=1e-12, atol=1e-11 * max(1, m))
-    assert torch.equal(K, K.transpose(1, 2))
-
-
 @pytest.mark.parametrize("M,N,K", [(1, 1, 1), (5, 40, 3), (100, 33, 64), (257, 129, 1000), (64, 2000, 17)])
 def test_gemm_nt_mfma_matches_fp64(M, N, K):
     from photon_ml_amd.ops.native import gemm_nt
