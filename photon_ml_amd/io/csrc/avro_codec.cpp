@@ -737,47 +737,56 @@ static bool is_bag(const Node* n) {
   return has_name && has_value;
 }
 
-// Feature-key interner: ids in first-appearance order; an open-addressing table of (hash, id) pairs (one probe
-// is usually one cache line, unlike a node-based map whose lookups chase two or three pointers).
+// Feature-key interner: ids in first-appearance order; an open-addressing table of 16-byte slots {id + 1, key
+// length, 16 hash bits, the key's first 8 bytes}. A probe is one cache line, and keys of <= 8 bytes (and most
+// misses) are decided inside the slot without touching the key arena -- at millions of distinct keys per file
+// the arena access was the second cache miss of every lookup.
 struct Interner {
+  struct Slot { uint32_t id; uint16_t len; uint16_t h; uint64_t pfx; };
   std::vector<std::string> keys;
-  std::vector<uint32_t> slot_id;    // id + 1, 0 = empty
-  std::vector<uint32_t> slot_h;
+  std::vector<Slot> slots;
   size_t mask = 0;
-  static uint64_t hash(const std::string& k) {
+  static uint64_t hash(const char* p, size_t n) {
     uint64_t h = 1469598103934665603ull;               // FNV-1a, then a final mix
-    for (unsigned char c : k) { h ^= c; h *= 1099511628211ull; }
+    for (size_t i = 0; i < n; ++i) { h ^= (unsigned char)p[i]; h *= 1099511628211ull; }
     h ^= h >> 29; h *= 0xBF58476D1CE4E5B9ull; h ^= h >> 32;
     return h;
   }
+  static uint64_t prefix(const char* p, size_t n) {
+    uint64_t v = 0;
+    memcpy(&v, p, n < 8 ? n : 8);
+    return v;
+  }
   void grow() {
-    const size_t cap = std::max<size_t>(1024, slot_id.size() * 2);
-    std::vector<uint32_t> id(cap, 0), hh(cap, 0);
+    const size_t cap = std::max<size_t>(1024, slots.size() * 2);
+    std::vector<Slot> ns(cap, Slot{0, 0, 0, 0});
     const size_t m = cap - 1;
-    for (size_t i = 0; i < slot_id.size(); ++i) {
-      if (!slot_id[i]) continue;
-      size_t j = slot_h[i] & m;
-      while (id[j]) j = (j + 1) & m;
-      id[j] = slot_id[i];
-      hh[j] = slot_h[i];
+    for (const Slot& sl : slots) {
+      if (!sl.id) continue;
+      const std::string& k = keys[sl.id - 1];
+      size_t j = hash(k.data(), k.size()) & m;
+      while (ns[j].id) j = (j + 1) & m;
+      ns[j] = sl;
     }
-    slot_id.swap(id);
-    slot_h.swap(hh);
+    slots.swap(ns);
     mask = m;
   }
   int32_t get(const std::string& k) {
-    if ((keys.size() + 1) * 2 > slot_id.size()) grow();
-    const uint64_t h64 = hash(k);
-    const uint32_t h = (uint32_t)h64;
+    if ((keys.size() + 1) * 2 > slots.size()) grow();
+    const uint64_t h64 = hash(k.data(), k.size());
+    const uint16_t h = (uint16_t)(h64 >> 48);
+    const uint16_t len = (uint16_t)std::min<size_t>(k.size(), 0xFFFF);
+    const uint64_t pf = prefix(k.data(), k.size());
     size_t j = h64 & mask;
-    while (slot_id[j]) {
-      if (slot_h[j] == h && keys[slot_id[j] - 1] == k) return (int32_t)(slot_id[j] - 1);
+    while (slots[j].id) {
+      const Slot& sl = slots[j];
+      if (sl.h == h && sl.len == len && sl.pfx == pf && (k.size() <= 8 || keys[sl.id - 1] == k))
+        return (int32_t)(sl.id - 1);
       j = (j + 1) & mask;
     }
     const int32_t id = (int32_t)keys.size();
     keys.push_back(k);
-    slot_id[j] = (uint32_t)id + 1;
-    slot_h[j] = h;
+    slots[j] = Slot{(uint32_t)id + 1, len, h, pf};
     return id;
   }
 };
@@ -797,7 +806,8 @@ struct FileCols {
   std::vector<double> label, weight, offset;
   std::vector<std::string> uid;
   std::vector<uint8_t> has_uid;
-  std::vector<std::vector<std::string>> tags;     // per requested id tag
+  std::vector<std::vector<int32_t>> tags;         // per requested id tag: code of each record's value
+  std::vector<Interner> tag_intern;               // per requested id tag: its distinct values (missing = "")
   std::map<std::string, BagOut> bags;
   Interner intern;
   std::string label_used;
@@ -805,6 +815,7 @@ struct FileCols {
   void swap_into(FileCols& other) {   // other <- this (an empty FileCols): releases other's memory
     std::swap(label, other.label); std::swap(weight, other.weight); std::swap(offset, other.offset);
     std::swap(uid, other.uid); std::swap(has_uid, other.has_uid); std::swap(tags, other.tags);
+    std::swap(tag_intern, other.tag_intern);
     std::swap(bags, other.bags); std::swap(intern, other.intern); std::swap(label_used, other.label_used);
     std::swap(n, other.n);
   }
@@ -824,6 +835,7 @@ static void decode_columnar_file(const std::string& path, const ColumnarOpts& op
   std::map<std::string, int> tag_index;
   for (size_t t = 0; t < op.id_tags.size(); ++t) tag_index.emplace(op.id_tags[t], (int)t);
   fc.tags.assign(op.id_tags.size(), {});
+  fc.tag_intern.assign(op.id_tags.size(), Interner());
   // field roles: 0 skip, 1 label, 2 weight, 3 offset, 4 uid, 5 meta, 6 bag, 7 tag
   std::vector<int> role(nf, 0), tag_of(nf, -1);
   std::vector<BagOut*> bag_of(nf, nullptr);
@@ -946,7 +958,8 @@ static void decode_columnar_file(const std::string& path, const ColumnarOpts& op
       }
       fc.label.push_back(lab); fc.weight.push_back(wt); fc.offset.push_back(off);
       fc.uid.push_back(hu ? u : std::string()); fc.has_uid.push_back(hu ? 1 : 0);
-      for (size_t t = 0; t < rec_tags.size(); ++t) fc.tags[t].push_back(rec_has[t] ? rec_tags[t] : std::string());
+      for (size_t t = 0; t < rec_tags.size(); ++t)
+        fc.tags[t].push_back(fc.tag_intern[t].get(rec_has[t] ? rec_tags[t] : std::string()));
       for (auto& b : fc.bags) b.second.rowptr.push_back((int64_t)b.second.keys.size());
       ++fc.n;
     }
@@ -957,7 +970,7 @@ static py::dict read_columnar(const std::vector<std::string>& paths, const std::
                               const std::string& weight_field, const std::string& offset_field,
                               const std::string& uid_field, const std::string& metadata_field,
                               const std::vector<std::string>& bags_wanted, const std::vector<std::string>& id_tags,
-                              const std::string& delimiter) {
+                              const std::string& delimiter, bool tag_strings) {
   ColumnarOpts op{label_fields, weight_field, offset_field, uid_field, metadata_field, delimiter, bags_wanted,
                   id_tags};
   const size_t nfile = paths.size();
@@ -973,7 +986,8 @@ static py::dict read_columnar(const std::vector<std::string>& paths, const std::
   std::vector<double> label, weight, offset;
   std::vector<std::string> uid;
   std::vector<uint8_t> has_uid;
-  std::vector<std::vector<std::string>> tags(id_tags.size());
+  std::vector<std::vector<int32_t>> tags(id_tags.size());
+  std::vector<Interner> tag_intern(id_tags.size());
   std::map<std::string, BagOut> bags;
   auto merge_one = [&](FileCols& fc) {
     if (label_used.empty()) label_used = fc.label_used;
@@ -984,8 +998,11 @@ static py::dict read_columnar(const std::vector<std::string>& paths, const std::
     offset.insert(offset.end(), fc.offset.begin(), fc.offset.end());
     for (auto& x : fc.uid) uid.push_back(std::move(x));
     has_uid.insert(has_uid.end(), fc.has_uid.begin(), fc.has_uid.end());
-    for (size_t t = 0; t < tags.size(); ++t)
-      for (auto& x : fc.tags[t]) tags[t].push_back(std::move(x));
+    for (size_t t = 0; t < tags.size(); ++t) {
+      std::vector<int32_t> tr(fc.tag_intern[t].keys.size());
+      for (size_t k = 0; k < tr.size(); ++k) tr[k] = tag_intern[t].get(fc.tag_intern[t].keys[k]);
+      for (int32_t c : fc.tags[t]) tags[t].push_back(tr[(size_t)c]);
+    }
     for (auto& b : fc.bags)
       if (!bags.count(b.first)) bags[b.first].rowptr.assign((size_t)n + 1, 0);   // bag first seen here: empty rows so far
     for (auto& b : bags) {
@@ -1060,9 +1077,22 @@ static py::dict read_columnar(const std::vector<std::string>& paths, const std::
   out["offset"] = arr_d(offset);
   out["uid"] = py::cast(uid);
   out["has_uid"] = py::array_t<uint8_t>((py::ssize_t)has_uid.size(), has_uid.data());
-  py::dict tg;
-  for (size_t t = 0; t < id_tags.size(); ++t) tg[py::str(id_tags[t])] = py::cast(tags[t]);
+  py::dict tg, tc;
+  for (size_t t = 0; t < id_tags.size(); ++t) {
+    // codes into the tag's table of distinct values (first-appearance order); per-record strings on request only
+    tc[py::str(id_tags[t])] = py::make_tuple(py::array_t<int32_t>((py::ssize_t)tags[t].size(), tags[t].data()),
+                                             py::cast(tag_intern[t].keys));
+    if (tag_strings) {
+      py::list l((py::ssize_t)tags[t].size());
+      std::vector<py::str> tab;
+      tab.reserve(tag_intern[t].keys.size());
+      for (auto& k : tag_intern[t].keys) tab.emplace_back(k);
+      for (size_t i = 0; i < tags[t].size(); ++i) l[(py::ssize_t)i] = tab[(size_t)tags[t][i]];
+      tg[py::str(id_tags[t])] = l;
+    }
+  }
   out["id_tags"] = tg;
+  out["id_tag_codes"] = tc;
   py::dict bg;
   for (auto& b : bags) {
     bg[py::str(b.first)] = py::make_tuple(py::array_t<int64_t>((py::ssize_t)b.second.rowptr.size(), b.second.rowptr.data()),
@@ -1074,6 +1104,174 @@ static py::dict read_columnar(const std::vector<std::string>& paths, const std::
   return out;
 }
 
+// ============================================================================================================
+// Shard assembly: the bags' (row pointer, interned key, value) triplets of the decoded records -> one shard CSR
+// (keys mapped through the shard's index map, unmapped keys dropped, the intercept appended, every row sorted by
+// column, duplicate features detected). Row ranges in parallel; the output is what _bags_to_csr produces
+// (photon-client/.../data/avro/AvroDataReader.scala:317-353: merged bags, intercept, duplicate rejection).
+// ============================================================================================================
+static py::tuple assemble_shard(int64_t n, py::list parts, py::array_t<int64_t, py::array::c_style> vocab_to_col,
+                                int64_t dim, int64_t intercept_col, bool check_duplicates, int threads) {
+  struct Part { const int64_t* rp; const int32_t* k; const double* v; };
+  std::vector<Part> ps;
+  std::vector<py::object> keep;
+  for (auto h : parts) {
+    py::tuple t = py::reinterpret_borrow<py::tuple>(h);
+    auto rp = t[0].cast<py::array_t<int64_t, py::array::c_style | py::array::forcecast>>();
+    auto k = t[1].cast<py::array_t<int32_t, py::array::c_style | py::array::forcecast>>();
+    auto v = t[2].cast<py::array_t<double, py::array::c_style | py::array::forcecast>>();
+    if (rp.size() != n + 1) throw std::runtime_error("assemble_shard: row pointer length != n + 1");
+    if (k.size() != v.size() || (int64_t)k.size() != rp.data()[n]) throw std::runtime_error("assemble_shard: sizes");
+    ps.push_back({rp.data(), k.data(), v.data()});
+    keep.push_back(rp); keep.push_back(k); keep.push_back(v);
+  }
+  const int64_t* vc = vocab_to_col.data();
+  const int64_t nv = (int64_t)vocab_to_col.size();
+  unsigned nt = threads > 0 ? (unsigned)threads : std::max(1u, std::thread::hardware_concurrency());
+  if (const char* e = std::getenv("PML_AVRO_THREADS")) nt = (unsigned)std::max(1, atoi(e));
+  nt = (unsigned)std::max<int64_t>(1, std::min<int64_t>(nt, n / 4096 + 1));
+  std::vector<int64_t> indptr((size_t)n + 1, 0);
+  std::vector<int64_t> dup_row(nt, -1), dup_col(nt, -1);
+  auto col_of = [&](int32_t key) -> int64_t { return key >= 0 && key < nv ? vc[key] : -1; };
+  {
+    py::gil_scoped_release nogil;
+    auto range = [&](unsigned t, int64_t& a, int64_t& b) { a = n * t / nt; b = n * (t + 1) / nt; };
+    std::vector<std::thread> pool;
+    for (unsigned t = 0; t < nt; ++t)
+      pool.emplace_back([&, t] {
+        int64_t a, b; range(t, a, b);
+        for (int64_t r = a; r < b; ++r) {
+          int64_t c = intercept_col >= 0 ? 1 : 0;
+          for (auto& p : ps)
+            for (int64_t q = p.rp[r]; q < p.rp[r + 1]; ++q) c += col_of(p.k[q]) >= 0;
+          indptr[(size_t)r + 1] = c;
+        }
+      });
+    for (auto& th : pool) th.join();
+  }
+  for (int64_t r = 0; r < n; ++r) indptr[(size_t)r + 1] += indptr[(size_t)r];
+  const int64_t nnz = indptr[(size_t)n];
+  const bool wide = std::max(dim, nnz) >= ((int64_t)1 << 31);
+  py::array_t<double> data(nnz);
+  py::array idx = wide ? (py::array)py::array_t<int64_t>(nnz) : (py::array)py::array_t<int32_t>(nnz);
+  double* dp = data.mutable_data();
+  int32_t* i32 = wide ? nullptr : (int32_t*)idx.mutable_data();
+  int64_t* i64 = wide ? (int64_t*)idx.mutable_data() : nullptr;
+  std::vector<int64_t> out_ptr;
+  {
+    py::gil_scoped_release nogil;
+    std::vector<std::thread> pool;
+    for (unsigned t = 0; t < nt; ++t)
+      pool.emplace_back([&, t] {
+        const int64_t a = n * t / nt, b = n * (t + 1) / nt;
+        std::vector<std::pair<int64_t, double>> row;
+        for (int64_t r = a; r < b; ++r) {
+          row.clear();
+          for (auto& p : ps)
+            for (int64_t q = p.rp[r]; q < p.rp[r + 1]; ++q) {
+              const int64_t c = col_of(p.k[q]);
+              if (c >= 0) row.emplace_back(c, p.v[q]);
+            }
+          if (intercept_col >= 0) row.emplace_back(intercept_col, 1.0);
+          std::stable_sort(row.begin(), row.end(),
+                           [](const std::pair<int64_t, double>& x, const std::pair<int64_t, double>& y) {
+                             return x.first < y.first;
+                           });
+          int64_t o = indptr[(size_t)r];
+          for (size_t j = 0; j < row.size(); ++j) {
+            if (j > 0 && row[j].first == row[j - 1].first && dup_row[t] < 0) {
+              dup_row[t] = r;
+              dup_col[t] = row[j].first;
+            }
+            dp[o] = row[j].second;
+            if (i32) i32[o] = (int32_t)row[j].first; else i64[o] = row[j].first;
+            ++o;
+          }
+        }
+      });
+    for (auto& th : pool) th.join();
+  }
+  int64_t first_dup = -1, first_col = -1;
+  for (unsigned t = 0; t < nt; ++t)
+    if (dup_row[t] >= 0) { first_dup = dup_row[t]; first_col = dup_col[t]; break; }
+  py::array_t<int64_t> ip((py::ssize_t)indptr.size(), indptr.data());
+  return py::make_tuple(ip, idx, data, first_dup, first_col);
+}
+
+// Synthetic TrainingExample OCF (photon-avro-schemas TrainingExample: uid, label, features[{name, term, value}],
+// weight, offset, metadataMap{userId}) written natively for ingest benchmarks: ``nnz_per_record`` distinct
+// features per record from a Zipf-like vocabulary of ``vocab`` names, ``n_entities`` user ids.
+static int64_t gen_training_examples(const std::string& path, int64_t n_records, int nnz_per_record, int64_t vocab,
+                                     int64_t n_entities, uint64_t seed, const std::string& codec, int block_records) {
+  py::gil_scoped_release nogil;
+  static const char* schema =
+      "{\"type\":\"record\",\"name\":\"TrainingExampleAvro\",\"namespace\":\"com.linkedin.photon.avro.generated\","
+      "\"fields\":[{\"name\":\"uid\",\"type\":[\"null\",\"string\"],\"default\":null},"
+      "{\"name\":\"label\",\"type\":\"double\"},"
+      "{\"name\":\"features\",\"type\":{\"type\":\"array\",\"items\":{\"type\":\"record\",\"name\":"
+      "\"FeatureAvro\",\"fields\":[{\"name\":\"name\",\"type\":\"string\"},{\"name\":\"term\",\"type\":"
+      "\"string\"},{\"name\":\"value\",\"type\":\"double\"}]}}},"
+      "{\"name\":\"weight\",\"type\":[\"null\",\"double\"],\"default\":null},"
+      "{\"name\":\"offset\",\"type\":[\"null\",\"double\"],\"default\":null},"
+      "{\"name\":\"metadataMap\",\"type\":[\"null\",{\"type\":\"map\",\"values\":\"string\"}],"
+      "\"default\":null}]}";
+  std::string out("Obj\x01", 4);
+  Writer hdr;
+  hdr.varlong(2);
+  hdr.str("avro.schema"); hdr.str(schema);
+  hdr.str("avro.codec"); hdr.str(codec);
+  hdr.varlong(0);
+  out += hdr.buf;
+  std::mt19937_64 rng(seed);
+  std::string sync(16, '\0');
+  for (int i = 0; i < 16; ++i) sync[i] = (char)(rng() & 0xFF);
+  out += sync;
+  std::uniform_real_distribution<double> U(0.0, 1.0);
+  std::normal_distribution<double> N01(0.0, 1.0);
+  std::vector<int64_t> feats;
+  int64_t written = 0;
+  std::ofstream f(path, std::ios::binary);
+  if (!f) throw std::runtime_error("cannot write " + path);
+  f.write(out.data(), (std::streamsize)out.size());
+  for (int64_t i = 0; i < n_records;) {
+    const int64_t m = std::min<int64_t>(n_records - i, std::max(block_records, 1));
+    Writer body;
+    for (int64_t k = 0; k < m; ++k, ++i) {
+      body.varlong(1); body.str("u" + std::to_string(seed) + "_" + std::to_string(i));
+      body.dbl(U(rng) < 0.3 ? 1.0 : 0.0);
+      feats.clear();
+      while ((int)feats.size() < nnz_per_record) {   // distinct Zipf-like feature ids (u^3 skew)
+        const double u = U(rng);
+        const int64_t id = std::min<int64_t>(vocab - 1, (int64_t)(u * u * u * (double)vocab));
+        if (std::find(feats.begin(), feats.end(), id) == feats.end()) feats.push_back(id);
+      }
+      body.varlong((int64_t)feats.size());
+      for (int64_t id : feats) { body.str("f" + std::to_string(id)); body.str(""); body.dbl(N01(rng)); }
+      body.varlong(0);
+      body.varlong(0);                 // weight: null
+      body.varlong(0);                 // offset: null
+      body.varlong(1);                 // metadataMap: map
+      body.varlong(1); body.str("userId"); body.str("e" + std::to_string((int64_t)(U(rng) * (double)n_entities)));
+      body.varlong(0);
+      written += (int64_t)feats.size();
+    }
+    std::string payload;
+    if (codec == "null") payload = body.buf;
+    else if (codec == "deflate") payload = deflate_raw(body.buf, 1);
+    else if (codec == "snappy") {
+      payload = snappy_compress(body.buf);
+      uint32_t c = crc32_iso(body.buf);
+      payload.push_back((char)(c >> 24)); payload.push_back((char)(c >> 16));
+      payload.push_back((char)(c >> 8)); payload.push_back((char)c);
+    } else throw std::runtime_error("unsupported codec " + codec);
+    Writer bh; bh.varlong(m); bh.varlong((int64_t)payload.size());
+    f.write(bh.buf.data(), (std::streamsize)bh.buf.size());
+    f.write(payload.data(), (std::streamsize)payload.size());
+    f.write(sync.data(), 16);
+  }
+  return written;
+}
+
 PYBIND11_MODULE(libpml_avro, m) {
   m.doc() = "photon_ml_amd native Avro OCF codec";
   m.def("read_ocf", &read_ocf, "Decode an OCF file -> (schema_json, [records], codec)");
@@ -1082,7 +1280,12 @@ PYBIND11_MODULE(libpml_avro, m) {
         py::arg("codec") = "deflate", py::arg("block_records") = 4096);
   m.def("read_columnar", &read_columnar, py::arg("paths"), py::arg("label_fields"), py::arg("weight_field"),
         py::arg("offset_field"), py::arg("uid_field"), py::arg("metadata_field"), py::arg("bags"),
-        py::arg("id_tags"), py::arg("delimiter") = std::string("\x01"));
+        py::arg("id_tags"), py::arg("delimiter") = std::string("\x01"), py::arg("tag_strings") = true);
+  m.def("assemble_shard", &assemble_shard, py::arg("n"), py::arg("parts"), py::arg("vocab_to_col"), py::arg("dim"),
+        py::arg("intercept_col"), py::arg("check_duplicates"), py::arg("threads") = 0);
+  m.def("gen_training_examples", &gen_training_examples, py::arg("path"), py::arg("n_records"),
+        py::arg("nnz_per_record"), py::arg("vocab"), py::arg("n_entities"), py::arg("seed"),
+        py::arg("codec") = std::string("deflate"), py::arg("block_records") = 4096);
   m.def("snappy_compress", [](const std::string& s) { return py::bytes(snappy_compress(s)); });
   m.def("snappy_roundtrip", [](const std::string& s) {
     std::string c = snappy_compress(s);

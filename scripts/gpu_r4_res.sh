@@ -9,3 +9,4 @@ tail -1 gpurun_out/r4res/pytest.log
 unset PML_CHECK_KERNEL_INPUTS
 timeout -k 10 300 python -u scripts/re_fused_bench.py 43000 stream,res > gpurun_out/r4res/bench.log 2>&1 || { echo "bench failed"; tail -30 gpurun_out/r4res/bench.log; exit 1; }
 cat gpurun_out/r4res/bench.log | grep -v amdgpu.ids
+timeout -k 10 300 python -u scripts/fe_ops_profile.py game5pl gpurun_out/r4res/fe_ops.txt > gpurun_out/r4res/fe_ops.log 2>&1 || { echo "fe ops profile failed"; tail -20 gpurun_out/r4res/fe_ops.log; }

@@ -199,3 +199,38 @@ def test_bags_to_csr_matches_coo_reference():
     ref = sp.csr_matrix((v[ok], (r[ok], c[ok])), shape=(n, dim))
     ref.sort_indices()
     assert (m != ref).nnz == 0 and m.has_sorted_indices
+
+
+@pytest.mark.parametrize("intercept", [True, False])
+def test_native_shard_assembly_matches_python(intercept):
+    """assemble_shard (C++, row ranges in parallel) == the numpy assembly: keys mapped through the index map
+    (unmapped ones dropped), bags concatenated, the intercept appended, rows column-sorted; duplicates reported
+    (first row / column) or summed."""
+    from photon_ml_amd.io import data_reader as dr
+    rng = np.random.default_rng(5)
+    n, vocab, dim = 3000, 500, 400
+    parts = []
+    for _ in range(2):
+        lens = rng.integers(0, 12, n)
+        rp = np.concatenate([[0], np.cumsum(lens)]).astype(np.int64)
+        keys = np.concatenate([rng.choice(vocab, size=l, replace=False) for l in lens]).astype(np.int32)
+        parts.append((rp, keys, rng.normal(size=len(keys))))
+    v2c = rng.permutation(vocab).astype(np.int64)
+    v2c[v2c >= dim - 1] = -1              # keys outside the index map are dropped (dim - 1: the intercept)
+    # two bags may hold the same feature: make the columns of the second bag disjoint to test the clean path
+    v2c_b = v2c.copy()
+    icpt = dim - 1 if intercept else None
+    clean = [parts[0], (parts[1][0], parts[1][1], parts[1][2])]
+    ref = dr._bags_to_csr(n, [parts[0]], v2c_b, dim, icpt, True)
+    got = dr._assemble(n, [parts[0]], v2c_b, dim, icpt, True)
+    assert np.array_equal(ref.indptr, got.indptr) and np.array_equal(ref.indices, got.indices)
+    assert np.array_equal(ref.data, got.data)
+    with pytest.raises(dr.DuplicateFeatureError) as e1:
+        dr._bags_to_csr(n, clean, v2c, dim, icpt, True)
+    with pytest.raises(dr.DuplicateFeatureError) as e2:
+        dr._assemble(n, clean, v2c, dim, icpt, True)
+    assert str(e1.value) == str(e2.value)
+    a = dr._bags_to_csr(n, clean, v2c, dim, icpt, False)
+    b = dr._assemble(n, clean, v2c, dim, icpt, False)
+    assert np.array_equal(a.indptr, b.indptr) and np.array_equal(a.indices, b.indices)
+    np.testing.assert_allclose(a.data, b.data, rtol=1e-15, atol=0)
