@@ -158,17 +158,28 @@ __device__ __forceinline__ void row_pass(const ReTronArgs& a, long long r0, long
                                          double* __restrict__ Zn, double& fpart) {
   const int lane = threadIdx.x & 63, w = threadIdx.x >> 6;
   const int grp = lane / RE_G, gl = lane % RE_G;
-  const long long step = (long long)RE_NW * RE_BATCH;
-  long long base = r0 + (long long)w * RE_BATCH;
+  // entity-local 32-bit row / entry offsets from per-entity bases: one VGPR per address instead of 64-bit math
+  const int nrows = (int)(r1 - r0);
+  const long long e0 = a.nip[r0];
+  const long long* __restrict__ nip = a.nip + r0;
+  const uint16_t* __restrict__ lcol = a.lcol + e0;
+  const double* __restrict__ val = a.val + e0;
+  const double* __restrict__ wt = a.wt + r0;
+  const double* __restrict__ off = a.off + r0;
+  const double* __restrict__ yv = a.y + r0;
+  if (MODE == 0) Dc += r0;
+  if (MODE == 1) { Dn += r0; Zn += r0; }
+  const int step = RE_NW * RE_BATCH;
+  int base = w * RE_BATCH;
   // row pointers of a batch: lane j <= RE_BATCH holds nip[base + j] (clamped to the entity's last row)
-  auto fetch_ptr = [&](long long b) -> long long {
-    const long long i = b + (lane <= RE_BATCH ? lane : RE_BATCH);
-    return b < r1 ? a.nip[i < r1 ? i : r1] : 0;
+  auto fetch_ptr = [&](int b) -> int {
+    const int i = b + (lane <= RE_BATCH ? lane : RE_BATCH);
+    return b < nrows ? (int)(nip[i < nrows ? i : nrows] - e0) : 0;
   };
-  long long np = fetch_ptr(base);
-  for (; base < r1; base += step) {
-    const long long np_next = fetch_ptr(base + step);
-    long long lo[RE_U], hi[RE_U];
+  int np = fetch_ptr(base);
+  for (; base < nrows; base += step) {
+    const int np_next = fetch_ptr(base + step);
+    int lo[RE_U], hi[RE_U];
     int c[RE_U][RE_K];
     double v[RE_U][RE_K], dot[RE_U], rs[RE_U][3];
 #pragma unroll
@@ -176,24 +187,24 @@ __device__ __forceinline__ void row_pass(const ReTronArgs& a, long long r0, long
       const int q = u * RE_RPI + grp;
       lo[u] = __shfl(np, q, 64);
       hi[u] = __shfl(np, q + 1, 64);
-      const long long i = base + q;
-      const bool valid = i < r1;
+      const int i = base + q;
+      const bool valid = i < nrows;
       if (MODE == 0) {
         rs[u][0] = valid ? Dc[i] : 0.0;
       } else {
-        rs[u][0] = valid ? a.wt[i] : 0.0;
-        rs[u][1] = valid ? a.off[i] : 0.0;
-        rs[u][2] = valid ? a.y[i] : 0.0;
+        rs[u][0] = valid ? wt[i] : 0.0;
+        rs[u][1] = valid ? off[i] : 0.0;
+        rs[u][2] = valid ? yv[i] : 0.0;
       }
     }
 #pragma unroll
     for (int u = 0; u < RE_U; ++u) {
 #pragma unroll
       for (int k = 0; k < RE_K; ++k) {
-        const long long p = lo[u] + gl + RE_G * k;
+        const int p = lo[u] + gl + RE_G * k;
         const bool in = p < hi[u];
-        c[u][k] = in ? (int)a.lcol[p] : 0;
-        v[u][k] = in ? a.val[p] : 0.0;
+        c[u][k] = in ? (int)lcol[p] : 0;
+        v[u][k] = in ? val[p] : 0.0;
       }
     }
 #pragma unroll
@@ -202,15 +213,15 @@ __device__ __forceinline__ void row_pass(const ReTronArgs& a, long long r0, long
       if (MODE != 2) {
 #pragma unroll
         for (int k = 0; k < RE_K; ++k) s = fma(v[u][k], vec[c[u][k]], s);
-        for (long long p = lo[u] + gl + RE_G * RE_K; p < hi[u]; p += RE_G) s = fma(a.val[p], vec[a.lcol[p]], s);
+        for (int p = lo[u] + gl + RE_G * RE_K; p < hi[u]; p += RE_G) s = fma(val[p], vec[lcol[p]], s);
       }
       dot[u] = s;
     }
 #pragma unroll
     for (int u = 0; u < RE_U; ++u) {
       if (MODE != 2) dot[u] = row16_total(dot[u]);
-      const long long i = base + u * RE_RPI + grp;
-      const bool valid = i < r1;
+      const int i = base + u * RE_RPI + grp;
+      const bool valid = i < nrows;
       double t;
       if (MODE == 0) {
         t = rs[u][0] * dot[u];
@@ -228,7 +239,7 @@ __device__ __forceinline__ void row_pass(const ReTronArgs& a, long long r0, long
 #pragma unroll
       for (int k = 0; k < RE_K; ++k)
         if (lo[u] + gl + RE_G * k < hi[u]) atomicAdd(&acc[c[u][k]], t * v[u][k]);
-      for (long long p = lo[u] + gl + RE_G * RE_K; p < hi[u]; p += RE_G) atomicAdd(&acc[a.lcol[p]], t * a.val[p]);
+      for (int p = lo[u] + gl + RE_G * RE_K; p < hi[u]; p += RE_G) atomicAdd(&acc[lcol[p]], t * val[p]);
     }
     np = np_next;
   }
@@ -837,6 +848,7 @@ __device__ __forceinline__ void block_sums8(double (&v)[K], double* __restrict__
 #pragma unroll
     for (int q = 0; q < RS_NW; ++q) s += slot[q * 8 + k];
     v[k] = s;
+    __builtin_amdgcn_sched_barrier(0);    // one value at a time (8 LDS reads), not 8 x K reads in flight
   }
   parity ^= 1;
 }
@@ -895,7 +907,7 @@ __global__ __launch_bounds__(RS_THREADS) void re_tron_res_kernel(ReTronArgs a, R
   double* rW = rZ + 2 * CAP;         // [CAP] weight
   double* rO = rW + CAP;             // [CAP] offset
   double* rY = rO + CAP;             // [CAP] label
-  double* red = rY + CAP;            // [2][RS_NW][8]
+  double* red = rY + CAP;            // [2][RS_NW][8], then [16] TRON scalars
   double* myacc = acc + w * DMS;
   __shared__ int sTicket;
   for (int i = tid; i < RS_NW * DMS; i += RS_THREADS) acc[i] = 0.0;
@@ -1063,37 +1075,50 @@ __global__ __launch_bounds__(RS_THREADS) void re_tron_res_kernel(ReTronArgs a, R
       return f + 0.5 * a.l2 * s2[0];
     };
 
-    double gnorm2;
-    double f = value_grad(sW, 1, cur, gnorm2);
+    // The TRON scalars live in LDS (every thread writes the same value, so no extra barriers): across the row
+    // passes nothing but the resident rows and a few indices stays in VGPRs (no spills into the pass loop).
+    double* T = red + 2 * RS_NW * 8;      // [16] scalar state
+    int* TI = (int*)(T + 12);             // it, fails, reason, active
+    enum { F = 0, GN2 = 1, DELTA = 2, LTOL = 3, GTOL = 4, RTR = 5, STS = 6, CGTOL = 7 };
+    {
+      double gnorm2;
+      const double f = value_grad(sW, 1, cur, gnorm2);
+      T[F] = f;
+      T[GN2] = gnorm2;
+    }
     double nz[1] = {0.0};
     for (int jj = tid; jj < d; jj += RS_THREADS) {
       sG[jj] = sH[jj];
       nz[0] += sW[jj] != 0.0 ? 1.0 : 0.0;
     }
     block_sums8<1>(nz, red, parity);
-    double f0z = f, g0n = sqrt(gnorm2);
-    if (nz[0] != 0.0) {
-      double g0;
-      f0z = value_grad(sS, 2, 0, g0);
-      g0n = sqrt(g0);
+    {
+      double f0z = T[F], g0n = sqrt(T[GN2]);
+      if (nz[0] != 0.0) {
+        double g0;
+        f0z = value_grad(sS, 2, 0, g0);
+        g0n = sqrt(g0);
+      }
+      T[LTOL] = f0z * a.tol;
+      T[GTOL] = g0n * a.tol;
+      T[DELTA] = sqrt(T[GN2]);
+      TI[0] = 0; TI[1] = 0; TI[2] = T[DELTA] == 0.0 ? 4 : 0; TI[3] = T[DELTA] == 0.0 ? 0 : 1;
     }
-    const double loss_tol = f0z * a.tol, grad_tol = g0n * a.tol;
-    double delta = sqrt(gnorm2);
-    int it = 0, fails = 0, reason = 0;
-    bool active = true;
-    if (delta == 0.0) { reason = 4; active = false; }
     const double eta0 = 1e-4, eta1 = 0.25, eta2 = 0.75, sg1 = 0.25, sg2 = 0.5, sg3 = 4.0;
     const int guard_max = a.max_iter * (a.max_fail + 1) + 5;
-    for (int guard = 0; active && guard < guard_max; ++guard) {
+    for (int guard = 0; TI[3] && guard < guard_max; ++guard) {
       for (int jj = tid; jj < d; jj += RS_THREADS) {
         sS[jj] = 0.0;
         sR[jj] = -sG[jj];
         sV[jj] = -sG[jj];
       }
-      double rtr = gnorm2, sts = 0.0;
-      const double cg_tol2 = 0.01 * gnorm2;
+      T[RTR] = T[GN2];
+      T[STS] = 0.0;
+      T[CGTOL] = 0.01 * T[GN2];
       for (int kk = 0; kk < a.max_cg; ++kk) {
-        if (!(rtr > cg_tol2)) break;
+        // state read BEFORE this step's barriers: a faster thread overwrites RTR / STS after the block sum
+        const double rtr = T[RTR], sts = T[STS], delta = T[DELTA];
+        if (!(rtr > T[CGTOL])) break;
         ++npass;
         __syncthreads();
         double fpz = 0.0;
@@ -1135,8 +1160,8 @@ __global__ __launch_bounds__(RS_THREADS) void re_tron_res_kernel(ReTronArgs a, R
           if (!hit) sV[jj] = r + beta * dj;
         }
         if (hit) break;
-        rtr = rn;
-        sts = tn;
+        T[RTR] = rn;
+        T[STS] = tn;
       }
       // ---- trial point W + step (into sV), trust-region update, acceptance
       __syncthreads();
@@ -1150,6 +1175,10 @@ __global__ __launch_bounds__(RS_THREADS) void re_tron_res_kernel(ReTronArgs a, R
       }
       block_sums8<3>(s3, red, parity);
       const double gs = s3[0], pred = -0.5 * (gs - s3[1]), snorm = sqrt(s3[2]);
+      // state read BEFORE the trial evaluation's barriers (a faster thread rewrites it after them)
+      const double f = T[F], gn2_old = T[GN2];
+      double delta = T[DELTA];
+      int it = TI[0], fails = TI[1];
       double gn2;
       const double fn = value_grad(sV, 1, cur ^ 1, gn2);     // trial gradient in sH
       const double actual = f - fn;
@@ -1161,29 +1190,33 @@ __global__ __launch_bounds__(RS_THREADS) void re_tron_res_kernel(ReTronArgs a, R
       else if (actual < eta1 * pred) nd = fmax(sg1 * delta, fmin(alr * snorm, sg2 * delta));
       else if (actual < eta2 * pred) nd = fmax(sg1 * delta, fmin(alr * snorm, sg3 * delta));
       else nd = fmax(delta, fmin(alr * snorm, sg3 * delta));
-      delta = nd;
+      T[DELTA] = nd;
       const bool accept = actual > eta0 * pred;
-      const double f_prev = f;
+      double fc = f, gnc = gn2_old;
       if (accept) {
         for (int jj = tid; jj < d; jj += RS_THREADS) {
           sW[jj] = sV[jj];
           sG[jj] = sH[jj];
         }
-        gnorm2 = gn2;
-        f = fn;
+        gnc = gn2;
+        fc = fn;
         cur ^= 1;
         ++it;
         fails = 0;
       } else {
         ++fails;
       }
+      T[GN2] = gnc;
+      T[F] = fc;
       const bool not_impr = !accept && fails >= a.max_fail;
       int rc = 0;
-      if (accept && sqrt(gnorm2) <= grad_tol) rc = 4;
-      if (accept && fabs(f - f_prev) <= loss_tol) rc = 3;
+      if (accept && sqrt(gnc) <= T[GTOL]) rc = 4;
+      if (accept && fabs(fc - f) <= T[LTOL]) rc = 3;
       if (not_impr) rc = 2;
       if ((accept || not_impr) && it >= a.max_iter) rc = 1;
-      if (rc > 0) { reason = rc; active = false; }
+      TI[0] = it;
+      TI[1] = fails;
+      if (rc > 0) { TI[2] = rc; TI[3] = 0; }
     }
     __syncthreads();
     if (m == 0)
@@ -1191,7 +1224,7 @@ __global__ __launch_bounds__(RS_THREADS) void re_tron_res_kernel(ReTronArgs a, R
     if (a.zout != nullptr)
       for (int r = tid; r < nloc; r += RS_THREADS) a.zout[rb + r] = rZ[cur * CAP + r];
     if (tid == 0 && m == 0) {
-      a.f[e] = f; a.iters[e] = it; a.reason[e] = reason;
+      a.f[e] = T[F]; a.iters[e] = TI[0]; a.reason[e] = TI[2];
       if (a.npass != nullptr) a.npass[e] = npass;
     }
   }
@@ -1262,7 +1295,7 @@ int pml_re_tron_hess(const int* order, int n_launch, const long long* row_ptr, c
 // Register-resident kernel: LDS per workgroup, rows per workgroup.
 static size_t res_smem(int S) {
   const size_t cap = (size_t)RS_NW * 4 * S;
-  return ((size_t)(6 + RS_NW) * (RS_DMAX + 8) + 7 * cap + 2 * RS_NW * 8) * sizeof(double);
+  return ((size_t)(6 + RS_NW) * (RS_DMAX + 8) + 7 * cap + 2 * RS_NW * 8 + 16) * sizeof(double);
 }
 int pml_re_res_cap() { return RS_NW * 4 * RES_S; }
 int pml_re_res_dmax() { return RS_DMAX; }

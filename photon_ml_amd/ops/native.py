@@ -81,6 +81,8 @@ def _load(name: str, auto_build: bool = True) -> Optional[ctypes.CDLL]:
     path = lib_path("hip", name)
     if name == "glm" and os.environ.get("PML_GLM_LIB"):   # experiment builds (ops/build.py build_experiment)
         path = Path(os.environ["PML_GLM_LIB"])
+    if name == "re" and os.environ.get("PML_RE_LIB"):     # A/B builds of the random-effect kernels (profiling)
+        path = Path(os.environ["PML_RE_LIB"])
     if not path.exists() and auto_build and os.environ.get("PML_NO_AUTOBUILD") != "1":
         try:
             build_hip(name)

@@ -29,9 +29,15 @@ FUSED_LOSSES = (0, 1, 2)             # logistic, Poisson, squared (the twice-dif
 _CLASSES = (256, 512, 1024, 2048)    # LDS size classes (max coefficients per entity of a launch)
 _HESS_CLASSES = (16, 32, 48, 64)     # tall-narrow entities: d_e padded to these, exact Hessian on the matrix cores
 HESS_DMAX = 64 if os.environ.get("PML_RE_HESS", "1") != "0" else 0
-# register-resident kernel (re_tron_res_kernel): entities of <= 1024 coefficients whose rows have <= 64 non-zeros;
-# entities longer than one workgroup's rows are split over a cluster of up to RES_KMAX workgroups
-RESIDENT = os.environ.get("PML_RE_RESIDENT", "1") != "0"
+# Register-resident kernel (re_tron_res_kernel): rows held in VGPRs, entities longer than one workgroup's rows split
+# over a cluster of up to RES_KMAX workgroups. Measured on game5pl-like entities (profiles/re_resident_ab_r4.md):
+# it halves the time of the LARGEST entities (64 largest alone: 29.5 -> 15.3 ms) but runs the small / mid ones at
+# half the streaming kernel's throughput (8-wave barriers and per-wave accumulator combines dominate their short
+# passes). Policy ``auto``: only entities whose single-workgroup streaming solve would outlast the whole streaming
+# launch (more than 1/RES_TAIL_SHARE of the batch's non-zeros) go to clusters; ``force``: every eligible entity;
+# ``0``: none.
+RESIDENT = os.environ.get("PML_RE_RESIDENT", "auto")
+RES_TAIL_SHARE = 256
 RES_ROW_NNZ = 64
 RES_KMAX = int(os.environ.get("PML_RE_RES_KMAX", "128"))
 
@@ -67,7 +73,11 @@ class EntityTronBatch:
         dev = seg.y.device
         n_e = seg.row_ptr[1:] - seg.row_ptr[:-1]
         d_e = seg.col_ptr[1:] - seg.col_ptr[:-1]
+        # the kernels address an entity's entries with 32-bit offsets from its first entry
+        e_nnz = seg.glm.nnz_per_entity() if hasattr(seg.glm, "nnz_per_entity") else None
         sel = mask.to(dev) & (n_e > 0) & (d_e > 0) & (d_e <= FUSED_DMAX) & (n_e <= FUSED_MAX_ROWS)
+        if e_nnz is not None:
+            sel &= e_nnz.to(dev) < (1 << 31)
         self.mask = sel
         self.ents = torch.nonzero(sel).squeeze(1)
         self.B = int(self.ents.numel())
@@ -101,12 +111,14 @@ class EntityTronBatch:
         # Entities of at most HESS_DMAX coefficients (tall: the row space took the wide ones) run the exact-Hessian
         # kernel (MFMA), the others the sparse Hessian-vector kernel.
         ent_nnz = (nip[self.row_ptr[1:]] - nip[self.row_ptr[:-1]])
+        if nnz and int(ent_nnz.max()) >= (1 << 31):
+            raise ValueError("an entity of the fused batch has >= 2^31 non-zeros (32-bit kernel offsets)")
         self.launches = []
         hess = de <= HESS_DMAX
         # register-resident tasks (one persistent launch): clusters (k > 1 workgroups) first, largest first
         self.res = None
         stream_sel = ~hess
-        if RESIDENT and bool(stream_sel.any()):
+        if RESIDENT != "0" and bool(stream_sel.any()):
             from ..ops.native import re_res_params
             cap, rdmax, grid = re_res_params()
             kmax = min(RES_KMAX, grid // 2)
@@ -114,6 +126,9 @@ class EntityTronBatch:
                 0, row_ent, row_nnz, reduce="amax", include_self=True)
             k_e = (ne + cap - 1) // cap
             res = stream_sel & (de <= rdmax) & (ent_maxrow <= RES_ROW_NNZ) & (k_e <= kmax)
+            if RESIDENT != "force":
+                # tail entities only: one workgroup streaming such an entity would outlast the whole launch
+                res &= ent_nnz * RES_TAIL_SHARE > int(ent_nnz[stream_sel].sum())
             if bool(res.any()):
                 idx = torch.nonzero(res).squeeze(1)
                 # clusters first (descending k), then single-workgroup entities by descending non-zeros

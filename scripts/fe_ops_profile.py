@@ -40,10 +40,18 @@ from torch.profiler import ProfilerActivity, profile
 with profile(activities=[ProfilerActivity.CPU, ProfilerActivity.CUDA], with_stack=True) as prof:
     fe.update_model(model.get("global"), partial)
     torch.cuda.synchronize()
-tab = prof.key_averages(group_by_stack_n=8).table(sort_by="self_cuda_time_total", row_limit=60,
-                                                    max_name_column_width=60, max_src_column_width=150)
-cnt = prof.key_averages(group_by_stack_n=8).table(sort_by="count", row_limit=40, max_name_column_width=60,
-                                                  max_src_column_width=150)
+ops = collections.Counter()
+for e in prof.events():
+    if not e.name.startswith("aten::") or e.name in ("aten::empty", "aten::empty_strided", "aten::view",
+                                                     "aten::as_strided", "aten::resize_", "aten::item"):
+        continue
+    if getattr(e, "cpu_parent", None) is not None and e.cpu_parent.name.startswith("aten::"):
+        continue                                   # count top-level aten calls only
+    fr = [f for f in (e.stack or []) if "photon_ml_amd" in f]
+    ops[(e.name, fr[0] if fr else "?", fr[1] if len(fr) > 1 else "")] += 1
+lines = [f"{n:4d}  {name:28s} {f0}  <- {f1}" for (name, f0, f1), n in ops.most_common(60)]
+tab = "\n".join(lines)
+cnt = prof.key_averages().table(sort_by="self_cuda_time_total", row_limit=40)
 print(tab)
 if out:
     open(out, "w").write(tab + "\n\n" + cnt)

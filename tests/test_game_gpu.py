@@ -342,3 +342,28 @@ def test_row_space_gram_wide_entity_falls_back_to_indicator_passes():
     assert a.B == b.B == 40 and torch.equal(a.ents, b.ents)
     for ka, kb in zip(a.classes, b.classes):
         torch.testing.assert_close(ka.L, kb.L, rtol=1e-10, atol=1e-12)
+
+
+@pytest.mark.parametrize("task", ["LOGISTIC_REGRESSION", "POISSON_REGRESSION"])
+def test_resident_cluster_tron_matches_streaming(task, monkeypatch):
+    """The register-resident fused TRON (rows in VGPRs; entities longer than one workgroup's rows solved by a
+    CLUSTER of workgroups meeting at agent-scope barriers) reproduces the streaming fused kernel: same models to
+    rounding and the same iteration counts, across a warm-started second update. ``force`` sends every eligible
+    entity to it (the power-law users span 1 .. several clusters of 384 rows)."""
+    import photon_ml_amd.optimization.entity_tron as et
+    data, _ = generate_game_data(n_rows=60000, n_users=300, d_user=40, seed=28, task=task)
+    out = {}
+    for mode in ("0", "force"):
+        monkeypatch.setattr(et, "RESIDENT", mode)
+        monkeypatch.setattr(et, "HESS_DMAX", 0)          # d_e 41: the sparse kernels, not the tall one
+        c, v1, s1, v2, s2 = _re_two_updates(data, task, max_iter=50, tol=1e-12)
+        fz = c._comps[1]
+        if mode == "force":
+            assert fz.res is not None and fz.res["clusters"] > 0 and fz.res["n"] == fz.B
+        else:
+            assert fz.res is None
+        out[mode] = (v1, s1, v2, s2, c.last_stats["mean_iterations"])
+    a, b = out["0"], out["force"]
+    for i in range(4):
+        torch.testing.assert_close(torch.as_tensor(b[i]), torch.as_tensor(a[i]), rtol=1e-6, atol=1e-7)
+    assert a[4] == b[4]
