@@ -364,6 +364,8 @@ def test_resident_cluster_tron_matches_streaming(task, monkeypatch):
             assert fz.res is None
         out[mode] = (v1, s1, v2, s2, c.last_stats["mean_iterations"])
     a, b = out["0"], out["force"]
+    # the two kernels sum in different orders (8 vs 4 wave accumulators, member partials): models agree to the
+    # rounding-path limit discussed in test_fused_entity_tron_matches_pass_path
     for i in range(4):
-        torch.testing.assert_close(torch.as_tensor(b[i]), torch.as_tensor(a[i]), rtol=1e-6, atol=1e-7)
-    assert a[4] == b[4]
+        torch.testing.assert_close(torch.as_tensor(b[i]), torch.as_tensor(a[i]), rtol=1e-5, atol=1e-6)
+    assert abs(a[4] - b[4]) < 0.05
