@@ -627,7 +627,7 @@ class RandomEffectCoordinate(Coordinate):
         if os.environ.get("PML_RE_ROW_SPACE", "1") == "0" or not row_space_eligible(l1, oc.constraint_map):
             return None
         if getattr(self, "_rs", None) is None:
-            self._rs = RowSpaceBatch(self.dataset.seg, nmax=int(os.environ.get("PML_RS_NMAX", "64")),
+            self._rs = RowSpaceBatch(self.dataset.seg, nmax=int(os.environ.get("PML_RS_NMAX", "128")),
                                      csr=getattr(self.dataset, "_seg_csr", None))
         return self._rs
 

@@ -278,7 +278,7 @@ __global__ __launch_bounds__(256) void tl_compact_kernel(CmpArgs a) {
 
 // ------------------------------------------------------------------------------------------------------------
 // Per-entity Gram matrices K_e = X_e X_e^T of the row-space batch (optimization/row_space.py setup), straight
-// from the block-diagonal CSR: one wave per entity of a size class (n_e <= n <= 64 rows; K zero padded to n x n).
+// from the block-diagonal CSR: one wave per entity of a size class (n_e <= n <= 192 rows; K zero padded to n x n).
 // Row i of the entity is scattered into a dense LDS image of the entity's projected columns [cb, cb + d_e), then
 // lane j takes the sparse dot product of row j with the image (row j's entries in stored order: deterministic
 // fp64) and the image is cleared entry by entry. Rows must hold distinct columns (canonical CSR; checked on the
@@ -301,22 +301,26 @@ __global__ __launch_bounds__(64) void seg_gram_kernel(int B, int n, const long l
   const int de = (int)(col_ptr[e + 1] - cb);
   for (int c = lane; c < de; c += 64) img[c] = 0.0;
   __syncthreads();
-  const bool mine = lane < ne;
-  const long long jb = mine ? nip[r0 + lane] : 0, je = mine ? nip[r0 + lane + 1] : 0;
   double* Kb = K + b * (long long)n * n;
   for (int i = 0; i < ne; ++i) {
     const long long ib = nip[r0 + i], ie = nip[r0 + i + 1];
     for (long long t = ib + lane; t < ie; t += 64) img[pos[t] - cb] = val[t];
     __syncthreads();
-    double acc = 0.0;
-    for (long long t = jb; t < je; ++t) acc = fma(val[t], img[pos[t] - cb], acc);
-    if (lane < n) Kb[(long long)lane * n + i] = mine ? acc : 0.0;
+    // lane takes rows j = lane, lane + 64, lane + 128 (n <= 192)
+    for (int j = lane; j < n; j += 64) {
+      double acc = 0.0;
+      if (j < ne) {
+        const long long jb = nip[r0 + j], je = nip[r0 + j + 1];
+        for (long long t = jb; t < je; ++t) acc = fma(val[t], img[pos[t] - cb], acc);
+      }
+      Kb[(long long)j * n + i] = acc;
+    }
     __syncthreads();
     for (long long t = ib + lane; t < ie; t += 64) img[pos[t] - cb] = 0.0;
     __syncthreads();
   }
   for (int i = ne; i < n; ++i)
-    if (lane < n) Kb[(long long)lane * n + i] = 0.0;
+    for (int j = lane; j < n; j += 64) Kb[(long long)j * n + i] = 0.0;
 }
 
 extern "C" {
@@ -398,7 +402,7 @@ int pml_gemm_nt(int M, int N, int K, const double* A, int lda, const double* Bm,
 int pml_seg_gram(int B, int n, int dmax, const long long* ents, const long long* row_ptr, const long long* col_ptr,
                  const long long* nip, const long long* pos, const double* val, double* K, void* stream) {
   if (B <= 0) return 0;
-  if (n < 1 || n > 64 || dmax < 0 || (size_t)dmax * sizeof(double) > 160 * 1024) return -22;
+  if (n < 1 || n > 192 || dmax < 0 || (size_t)dmax * sizeof(double) > 160 * 1024) return -22;
   hipLaunchKernelGGL(seg_gram_kernel, dim3((unsigned)B), dim3(64), (size_t)std::max(dmax, 1) * sizeof(double),
                      (hipStream_t)stream, B, n, ents, row_ptr, col_ptr, nip, pos, val, K);
   LAUNCH_CHECK();

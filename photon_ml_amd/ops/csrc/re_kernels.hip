@@ -806,6 +806,234 @@ __global__ __launch_bounds__(64) void re_tron_tall_kernel(ReTronArgs a) {
 }
 
 // ============================================================================================================
+// Row-space TRON for WIDE entities of 64 < n_e <= 192 rows (optimization/row_space.py: the entity's problem is the
+// dense GLM with the n x n lower-triangular design matrix L_e, K_e = X_e X_e^T = L_e L_e^T). The n <= 64 classes
+// run rs_tron_kernel / rs_tron_dpp_kernel (glm_kernels.hip); here ONE WAVE owns one problem with E = ceil(n / 64)
+// vector entries per lane (lane l: entries l, l + 64, ...), L's packed lower triangle is staged once into the
+// wave's LDS, every sum is a DPP / readlane wave sum (no workgroup barriers) and the whole TRON runs in the kernel.
+// Against the primal fused kernel on such an entity (d_e ~ 1000 coefficients, ~50 non-zeros per row) every CG
+// step is two LDS-resident triangular mat-vecs over n-length vectors instead of a pass over the rows' non-zeros
+// plus d-length vector work. Same TRON semantics as rs_tron_kernel (photon-lib/.../optimization/TRON.scala).
+// ============================================================================================================
+template <int E, int LOSS>
+__global__ __launch_bounds__(64) void rs_tron_big_kernel(int B, int n, const double* __restrict__ Lm,
+                                                         const double* __restrict__ Y, const double* __restrict__ O,
+                                                         const double* __restrict__ WT, double* __restrict__ Beta,
+                                                         double* __restrict__ Fout, int* __restrict__ Iters,
+                                                         int* __restrict__ Reason, double* __restrict__ Zout,
+                                                         double l2, double tol, int max_iter, int max_fail,
+                                                         int max_cg) {
+  extern __shared__ __attribute__((aligned(16))) double smem[];
+  const int lane = threadIdx.x;
+  const long long b = blockIdx.x;
+  if (b >= B) return;
+  const int np = n * (n + 1) / 2;
+  double* Lp = smem;              // packed lower triangle: L[r][c] (c <= r) at r (r + 1) / 2 + c
+  double* sv = smem + np;         // [n] vector broadcast to the lanes
+  const double* Lb = Lm + b * (long long)n * n;
+  for (int r = 0; r < n; ++r)
+    for (int c = lane; c <= r; c += 64) Lp[r * (r + 1) / 2 + c] = Lb[(long long)r * n + c];
+  bool on[E];
+  double y[E], off[E], wt[E], W[E];
+#pragma unroll
+  for (int e = 0; e < E; ++e) {
+    const int i = lane + 64 * e;
+    on[e] = i < n;
+    const long long o = b * n + (on[e] ? i : 0);
+    y[e] = on[e] ? Y[o] : 0.0;
+    off[e] = on[e] ? O[o] : 0.0;
+    wt[e] = on[e] ? WT[o] : 0.0;
+    W[e] = on[e] ? Beta[o] : 0.0;
+  }
+  wave_sync();
+  auto gsum = [&](const double (&v)[E]) -> double {
+    double s = 0.0;
+#pragma unroll
+    for (int e = 0; e < E; ++e) s += v[e];
+    return wave_total(s);
+  };
+  auto gsum2 = [&](const double (&u)[E], const double (&v)[E]) -> double {
+    double s = 0.0;
+#pragma unroll
+    for (int e = 0; e < E; ++e) s = fma(u[e], v[e], s);
+    return wave_total(s);
+  };
+  auto put = [&](const double (&v)[E]) {
+#pragma unroll
+    for (int e = 0; e < E; ++e)
+      if (on[e]) sv[lane + 64 * e] = v[e];
+    wave_sync();
+  };
+  auto mv = [&](const double (&v)[E], double (&out)[E]) {     // (L v)_i
+    put(v);
+#pragma unroll
+    for (int e = 0; e < E; ++e) {
+      const int i = on[e] ? lane + 64 * e : 0;
+      const double* Lr = Lp + i * (i + 1) / 2;
+      double a0 = 0.0, a1 = 0.0;
+      int j = 0;
+      for (; j + 1 <= i; j += 2) {
+        a0 = fma(Lr[j], sv[j], a0);
+        a1 = fma(Lr[j + 1], sv[j + 1], a1);
+      }
+      if (j <= i) a0 = fma(Lr[j], sv[j], a0);
+      out[e] = on[e] ? a0 + a1 : 0.0;
+    }
+    wave_sync();                       // sv reads done before the next put
+  };
+  auto mvt = [&](const double (&u)[E], double (&out)[E]) {    // (L^T u)_i
+    put(u);
+#pragma unroll
+    for (int e = 0; e < E; ++e) {
+      const int i = on[e] ? lane + 64 * e : 0;
+      double a0 = 0.0, a1 = 0.0;
+      int r = i;
+      for (; r + 1 < n; r += 2) {
+        a0 = fma(Lp[r * (r + 1) / 2 + i], sv[r], a0);
+        a1 = fma(Lp[(r + 1) * (r + 2) / 2 + i], sv[r + 1], a1);
+      }
+      if (r < n) a0 = fma(Lp[r * (r + 1) / 2 + i], sv[r], a0);
+      out[e] = on[e] ? a0 + a1 : 0.0;
+    }
+    wave_sync();
+  };
+  // value, gradient and Hessian weights at v; z (margins L v, no offset) kept for the output
+  auto vg = [&](const double (&v)[E], double& f, double (&gr)[E], double (&Dw)[E], double (&z)[E]) {
+    mv(v, z);
+    double t[E], fl[E];
+#pragma unroll
+    for (int e = 0; e < E; ++e) {
+      double l = 0.0, dl = 0.0, d2 = 0.0;
+      if (on[e]) loss_t<LOSS>(z[e] + off[e], y[e], l, dl, d2);
+      fl[e] = wt[e] * l + 0.5 * l2 * v[e] * v[e];
+      t[e] = wt[e] * dl;
+      Dw[e] = wt[e] * d2;
+    }
+    f = gsum(fl);
+    mvt(t, gr);
+#pragma unroll
+    for (int e = 0; e < E; ++e) gr[e] = on[e] ? gr[e] + l2 * v[e] : 0.0;
+  };
+  const double eta0 = 1e-4, eta1 = 0.25, eta2 = 0.75, s1 = 0.25, s2 = 0.5, s3 = 4.0;
+  double f, gr[E], Dw[E], Z[E];
+  vg(W, f, gr, Dw, Z);
+  double f0z, g0n;
+  double nzv[E];
+#pragma unroll
+  for (int e = 0; e < E; ++e) nzv[e] = W[e] != 0.0 ? 1.0 : 0.0;
+  if (gsum(nzv) == 0.0) {
+    f0z = f;
+    g0n = sqrt(gsum2(gr, gr));
+  } else {
+    double zero[E], g0[E], D0[E], z0[E];
+#pragma unroll
+    for (int e = 0; e < E; ++e) zero[e] = 0.0;
+    vg(zero, f0z, g0, D0, z0);
+    g0n = sqrt(gsum2(g0, g0));
+  }
+  const double loss_tol = f0z * tol, grad_tol = g0n * tol;
+  double delta = sqrt(gsum2(gr, gr));
+  int it = 0, fails = 0, reason = 0;
+  bool active = true;
+  if (delta == 0.0) { reason = 4; active = false; }
+  const int guard_max = max_iter * (max_fail + 1) + 5;
+  for (int guard = 0; active && guard < guard_max; ++guard) {
+    // ---- truncated CG at W (Hessian weights Dw of the current iterate)
+    double step[E], r[E], d[E];
+#pragma unroll
+    for (int e = 0; e < E; ++e) { step[e] = 0.0; r[e] = -gr[e]; d[e] = r[e]; }
+    double rtr = gsum2(r, r);
+    const double cg_tol = 0.1 * sqrt(gsum2(gr, gr));
+    for (int k = 0; k < max_cg; ++k) {
+      if (!(sqrt(rtr > 0.0 ? rtr : 0.0) > cg_tol)) break;
+      double Ld[E], Hd[E], Hl[E];
+      mv(d, Ld);
+#pragma unroll
+      for (int e = 0; e < E; ++e) Ld[e] *= Dw[e];
+      mvt(Ld, Hd);
+#pragma unroll
+      for (int e = 0; e < E; ++e) Hl[e] = Hd[e] + l2 * d[e];
+      const double dhd = gsum2(d, Hl), std_ = gsum2(step, d), sts = gsum2(step, step), dtd = gsum2(d, d);
+      const double alpha = rtr / (dhd == 0.0 ? 1.0 : dhd);
+      double tr[E];
+#pragma unroll
+      for (int e = 0; e < E; ++e) tr[e] = step[e] + alpha * d[e];
+      const double tn = gsum2(tr, tr);
+      const bool hit = sqrt(tn > 0.0 ? tn : 0.0) > delta;
+      double a = alpha;
+      if (hit) {
+        const double dsq = delta * delta;
+        const double q = std_ * std_ + dtd * (dsq - sts);
+        const double rad = sqrt(q > 0.0 ? q : 0.0);
+        const double den1 = std_ + rad;
+        a = std_ >= 0.0 ? (dsq - sts) / (den1 > 1e-300 ? den1 : 1e-300) : (rad - std_) / (dtd > 1e-300 ? dtd : 1e-300);
+      }
+      double rn_v[E];
+#pragma unroll
+      for (int e = 0; e < E; ++e) {
+        step[e] = step[e] + a * d[e];
+        rn_v[e] = r[e] - a * Hl[e];
+      }
+      const double rn = gsum2(rn_v, rn_v);
+      const double beta = rn / (rtr == 0.0 ? 1.0 : rtr);
+#pragma unroll
+      for (int e = 0; e < E; ++e) {
+        r[e] = rn_v[e];
+        if (!hit) d[e] = rn_v[e] + beta * d[e];
+      }
+      if (hit) break;
+      rtr = rn;
+    }
+    // ---- trial point, trust-region update, acceptance
+    double Wn[E];
+#pragma unroll
+    for (int e = 0; e < E; ++e) Wn[e] = W[e] + step[e];
+    const double gs = gsum2(gr, step);
+    const double pred = -0.5 * (gs - gsum2(step, r));
+    double fn, gn[E], Dn[E], Zn[E];
+    vg(Wn, fn, gn, Dn, Zn);
+    const double actual = f - fn;
+    const double snorm = sqrt(gsum2(step, step));
+    if (it == 0) delta = fmin(delta, snorm);
+    const double den = fn - f - gs;
+    const double al = den <= 0.0 ? s3 : fmax(s1, -0.5 * gs / (den == 0.0 ? 1.0 : den));
+    double nd;
+    if (actual < eta0 * pred) nd = fmin(fmax(al, s1) * snorm, s2 * delta);
+    else if (actual < eta1 * pred) nd = fmax(s1 * delta, fmin(al * snorm, s2 * delta));
+    else if (actual < eta2 * pred) nd = fmax(s1 * delta, fmin(al * snorm, s3 * delta));
+    else nd = fmax(delta, fmin(al * snorm, s3 * delta));
+    delta = nd;
+    const bool accept = actual > eta0 * pred;
+    const double f_prev = f;
+    if (accept) {
+#pragma unroll
+      for (int e = 0; e < E; ++e) { W[e] = Wn[e]; gr[e] = gn[e]; Dw[e] = Dn[e]; Z[e] = Zn[e]; }
+      f = fn;
+      ++it;
+      fails = 0;
+    } else {
+      ++fails;
+    }
+    const bool not_impr = !accept && fails >= max_fail;
+    const double gnorm = sqrt(gsum2(gr, gr));
+    int rc = 0;
+    if (accept && gnorm <= grad_tol) rc = 4;
+    if (accept && fabs(f - f_prev) <= loss_tol) rc = 3;
+    if (not_impr) rc = 2;
+    if ((accept || not_impr) && it >= max_iter) rc = 1;
+    if (rc > 0) { reason = rc; active = false; }
+  }
+#pragma unroll
+  for (int e = 0; e < E; ++e) {
+    if (!on[e]) continue;
+    const long long o = b * n + lane + 64 * e;
+    Beta[o] = W[e];
+    if (Zout != nullptr) Zout[o] = Z[e];
+  }
+  if (lane == 0) { Fout[b] = f; Iters[b] = it; Reason[b] = reason; }
+}
+
+// ============================================================================================================
 // REGISTER-RESIDENT fused primal TRON (wide entities: d_e <= 1024, rows of <= 64 non-zeros).
 // The fused kernel above streams an entity's CSR rows from memory for every Hessian-vector product (~36 row
 // passes per solve at ~3.6 TB/s). Here the rows are loaded ONCE into VGPRs and every later pass runs on-chip:
@@ -1336,6 +1564,27 @@ int pml_re_res_grid() {
   if (hipOccupancyMaxActiveBlocksPerMultiprocessor(&per, (const void*)re_tron_res_kernel<RES_S, 0>, RS_THREADS,
                                                    res_smem(RES_S)) != hipSuccess) return 0;
   return cus * per;
+}
+
+
+// Row-space TRON for 64 < n <= 192 (one wave per problem, packed L in LDS).
+int pml_rs_tron_big(int B, int n, const double* L, const double* y, const double* off, const double* wt,
+                    double* beta, double* f, int* iters, int* reason, double* zout, int loss, double l2, double tol,
+                    int max_iter, int max_fail, int max_cg, hipStream_t st) {
+  if (B <= 0) return 0;
+  if (n < 1 || n > 192 || loss < 0 || loss > 2) return -22;
+  const size_t smem = ((size_t)n * (n + 1) / 2 + n) * sizeof(double);
+  if (smem > 160 * 1024) return -22;
+#define RSB(E, LS) hipLaunchKernelGGL((rs_tron_big_kernel<E, LS>), dim3(B), dim3(64), smem, st, B, n, L, y, off, wt, \
+                                      beta, f, iters, reason, zout, l2, tol, max_iter, max_fail, max_cg)
+#define RSB_E(E) do { if (loss == 0) RSB(E, 0); else if (loss == 1) RSB(E, 1); else RSB(E, 2); } while (0)
+  if (n <= 64) RSB_E(1);
+  else if (n <= 128) RSB_E(2);
+  else RSB_E(3);
+#undef RSB_E
+#undef RSB
+  LAUNCH_CHECK();
+  return 0;
 }
 
 }  // extern "C"

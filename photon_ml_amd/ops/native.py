@@ -418,12 +418,13 @@ def rs_tron(L: torch.Tensor, y: torch.Tensor, o: torch.Tensor, w: torch.Tensor, 
             zout: Optional[torch.Tensor] = None):
     """Fused per-problem TRON over a batch of small dense GLMs (``rs_tron_kernel``): returns
     (beta, f, iters, reason). ``zout`` (contiguous fp64 [B, n]) receives the margins ``L beta`` of the solution
-    (written by the kernel while L is resident). Device only; n <= 64; losses logistic / Poisson / squared. ``out`` (contiguous
+    (written by the kernel while L is resident). Device only; n <= 192 (n > 64: ``rs_tron_big_kernel``, one wave
+    per problem); losses logistic / Poisson / squared. ``out`` (contiguous
     fp64 [B, n]) receives the solution in place (it starts from ``beta0``; ``out`` may be ``beta0``). ``order``
     (int32 permutation of the B problems): waves take consecutive problems of it -- grouping problems of similar
     iteration counts cuts the time a wave waits for its slowest problem; the results do not depend on it."""
-    lib = require_glm_lib()
     B, n, _ = L.shape
+    lib = require_re_lib() if n > 64 else require_glm_lib()
     ts = [t.contiguous() for t in (L, y, o, w)]
     for t in ts:
         assert t.dtype == torch.float64 and t.is_cuda
@@ -444,6 +445,13 @@ def rs_tron(L: torch.Tensor, y: torch.Tensor, o: torch.Tensor, w: torch.Tensor, 
             assert B == 0 or (int(order.min()) >= 0 and int(order.max()) < B), "rs_tron order out of range"
     if zout is not None:
         assert zout.shape == (B, n) and zout.dtype == torch.float64 and zout.is_contiguous() and zout.is_cuda
+    if n > 64:
+        # one wave per problem, packed L in LDS (re_kernels.hip rs_tron_big_kernel); problem order not used
+        check(lib.pml_rs_tron_big(B, n, ts[0].data_ptr(), ts[1].data_ptr(), ts[2].data_ptr(), ts[3].data_ptr(),
+                                  beta.data_ptr(), f.data_ptr(), iters.data_ptr(), reason.data_ptr(),
+                                  None if zout is None else zout.data_ptr(), int(loss_id), float(l2), float(tol),
+                                  int(max_iter), int(max_fail), int(max_cg), stream_handle(L.device)), "rs_tron_big")
+        return beta, f, iters.to(torch.long), reason.to(torch.long)
     check(lib.pml_rs_tron(B, n, ts[0].data_ptr(), ts[1].data_ptr(), ts[2].data_ptr(), ts[3].data_ptr(),
                           beta.data_ptr(), f.data_ptr(), iters.data_ptr(), reason.data_ptr(), int(loss_id), float(l2),
                           float(tol), int(max_iter), int(max_fail), int(max_cg),
@@ -643,6 +651,9 @@ def re_lib() -> Optional[ctypes.CDLL]:
         lib.pml_re_tron_res.argtypes = ([c_void_p, c_void_p, c_int] + [c_void_p] * 4 + [c_int] + [c_void_p] * 14
                                         + [c_int, c_double, c_double, c_int, c_int, c_int, c_void_p])
         lib.pml_re_tron_res.restype = c_int
+        lib.pml_rs_tron_big.argtypes = [c_int, c_int] + [c_void_p] * 9 + [c_int, c_double, c_double, c_int, c_int,
+                                                                         c_int, c_void_p]
+        lib.pml_rs_tron_big.restype = c_int
         lib.pml_re_res_cap.restype = c_int
         lib.pml_re_res_dmax.restype = c_int
         lib.pml_re_res_grid.restype = c_int

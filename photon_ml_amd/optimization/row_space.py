@@ -62,6 +62,18 @@ def _tri_inverse_lower(L: torch.Tensor) -> torch.Tensor:
     return X
 
 
+def _tri_inverse_solve(L: torch.Tensor, chunk: int = 512) -> torch.Tensor:
+    """Inverse of a batch of lower-triangular matrices by batched triangular solves against the identity (the
+    forward substitution of :func:`_tri_inverse_lower` costs O(B n^3) elementwise traffic, too much beyond n = 64)."""
+    B, n, _ = L.shape
+    out = torch.empty_like(L)
+    eye = torch.eye(n, dtype=L.dtype, device=L.device)
+    for s in range(0, B, chunk):
+        e = min(B, s + chunk)
+        out[s:e] = torch.linalg.solve_triangular(L[s:e], eye.expand(e - s, n, n), upper=False)
+    return out
+
+
 def _canonical_csr(csr, dev):
     """The (indptr, columns, values) block-diagonal CSR on ``dev`` when every row's columns are strictly
     increasing (what the per-entity Gram kernel needs), else None."""
@@ -85,7 +97,9 @@ def row_space_eligible(l1: float, constraints=None) -> bool:
 # is padded to the largest n_e among its members (not to the bound). One padded batch over power-law entity
 # sizes (most entities have a handful of rows, a few have 64) would cost every problem the largest n^2 in
 # memory and in the fused kernel's lane group; per class the kernel uses G = pow2 >= n lanes per problem.
-SIZE_CLASSES = (1, 2, 4, 8, 12, 16, 24, 32, 48, 64)
+SIZE_CLASSES = (1, 2, 4, 8, 12, 16, 24, 32, 48, 64, 80, 96, 112, 128, 160, 192)
+ROW_SPACE_NMAX = 192      # rs_tron_big_kernel / seg_gram_kernel limit (one wave per problem, packed L in LDS)
+RS_BIG_NNZ_RATIO = float(os.environ.get("PML_RS_BIG_NNZ_RATIO", "0.6"))   # n > 64: mean row nnz >= ratio x n
 
 
 class _SizeClass:
@@ -95,7 +109,8 @@ class _SizeClass:
         self.ents, self.n, self.L, self.rows, self.valid, self.w, self.y = ents, n, L, rows, valid, w, y
         self.B = int(ents.numel())
         self.off = off                                                   # offset in the packed beta vector
-        self.Linv = _tri_inverse_lower(L)                                # [B, n, n], lower
+        # [B, n, n], lower: forward substitution for small n, batched triangular solves beyond
+        self.Linv = _tri_inverse_lower(L) if n <= 64 else _tri_inverse_solve(L)
 
     def view(self, flat: torch.Tensor) -> torch.Tensor:
         return flat[self.off:self.off + self.B * self.n].view(self.B, self.n)
@@ -112,11 +127,21 @@ class RowSpaceBatch:
     ``valid`` and the solver results follow the same order."""
 
     def __init__(self, seg, nmax: int = 64, csr=None):
+        nmax = min(int(nmax), ROW_SPACE_NMAX)
         self.seg = seg
         dev = seg.y.device
         n_e = seg.row_ptr[1:] - seg.row_ptr[:-1]
         d_e = seg.col_ptr[1:] - seg.col_ptr[:-1]
         cand = (n_e > 0) & (n_e <= nmax) & (n_e <= d_e)
+        if nmax > 64 and csr is not None:
+            # beyond 64 rows a row-space CG step (two LDS-resident triangular mat-vecs, ~n^2 / 2 FMAs each) pays
+            # only when the entity's rows are dense enough: measured break-even on game5pl-like entities at ~0.5 n
+            # non-zeros per row (rs_tron_big_kernel 10.7 ms vs primal 9.8 ms for 65..128-row entities of 51
+            # non-zeros, profiles/row_space_big_r4.md); sparser entities stay on the primal fused path
+            nip = csr[0].to(n_e.device)
+            ent_nnz = nip[seg.row_ptr[1:]] - nip[seg.row_ptr[:-1]]
+            dense_enough = ent_nnz.double() >= RS_BIG_NNZ_RATIO * n_e.double() * n_e.double()
+            cand &= (n_e <= 64) | dense_enough
         ents = torch.nonzero(cand).squeeze(1)
         self.n_entities = seg.B
         self.classes = []

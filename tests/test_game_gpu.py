@@ -369,3 +369,45 @@ def test_resident_cluster_tron_matches_streaming(task, monkeypatch):
     for i in range(4):
         torch.testing.assert_close(torch.as_tensor(b[i]), torch.as_tensor(a[i]), rtol=1e-5, atol=1e-6)
     assert abs(a[4] - b[4]) < 0.05
+
+
+@pytest.mark.parametrize("task", ["LOGISTIC_REGRESSION", "POISSON_REGRESSION"])
+def test_row_space_big_classes_match_primal(task, monkeypatch):
+    """Wide entities of 64 < n_e <= 192 rows (d_e > n_e) are solved in their row space by rs_tron_big_kernel (one
+    wave per problem, packed L in LDS; K_e from seg_gram_kernel, 3 rows per lane): same models, scores and
+    iteration counts as the primal fused solve (the row-space map is an isometry: TRON takes the same steps)."""
+    import scipy.sparse as sp
+    from photon_ml_amd.data.game_data import GameData
+    rng = np.random.default_rng(41)
+    D, rows, cols, vals, ids = 4000, [], [], [], []
+    r = 0
+    sizes = [70, 90, 128, 150, 190, 66, 100] * 6
+    for e, n in enumerate(sizes):
+        pool = rng.choice(D - 1, size=400, replace=False)
+        for _ in range(n):
+            c = np.sort(rng.choice(pool, size=30, replace=False))
+            rows += [r] * 31
+            cols += c.tolist() + [D - 1]
+            vals += rng.normal(size=30).tolist() + [1.0]
+            ids.append(e)
+            r += 1
+    x = sp.csr_matrix((vals, (rows, cols)), shape=(r, D))
+    z = np.asarray(x.sum(axis=1)).ravel() * 0.05
+    y = (rng.random(r) < 1 / (1 + np.exp(-z))).astype(float) if task == "LOGISTIC_REGRESSION" else \
+        rng.poisson(np.exp(np.clip(z, -3, 2))).astype(float)
+    data = GameData(y, {"user": x}, {"userId": np.array(ids)})
+    import photon_ml_amd.optimization.row_space as rsm
+    out = {}
+    monkeypatch.setenv("PML_RS_NMAX", "192")
+    monkeypatch.setattr(rsm, "RS_BIG_NNZ_RATIO", 0.0)     # every wide entity in row space (sparse rows here)
+    for rs in ("0", "1"):
+        monkeypatch.setenv("PML_RE_ROW_SPACE", rs)
+        c, v1, s1, v2, s2 = _re_two_updates(data, task, max_iter=50, tol=1e-12)
+        if rs == "1":
+            rsb = c._comps[0]
+            assert rsb is not None and rsb.B == len(sizes) and max(cl.n for cl in rsb.classes) > 128
+        out[rs] = (v1, s1, v2, s2, c.last_stats["mean_iterations"])
+    a, b = out["0"], out["1"]
+    for i in range(4):
+        torch.testing.assert_close(torch.as_tensor(b[i]), torch.as_tensor(a[i]), rtol=1e-5, atol=1e-6)
+    assert abs(a[4] - b[4]) < 0.05
