@@ -39,15 +39,21 @@
 
 enum { LOSS_LOGISTIC = 0, LOSS_POISSON = 1, LOSS_SQUARED = 2 };
 
-__device__ __forceinline__ double log1p_exp(double x) { return x > 0.0 ? x + log1p(exp(-x)) : log1p(exp(x)); }
-
-__device__ __forceinline__ void pointwise_loss(int loss, double z, double y, double& l, double& dl, double& d2) {
-  if (loss == LOSS_LOGISTIC) {
-    const double s = 1.0 / (1.0 + exp(-z));
-    if (y > 0.5) { l = log1p_exp(-z); dl = s - 1.0; }
-    else { l = log1p_exp(z); dl = s; }
+template <int LOSS>
+__device__ __forceinline__ void loss_t(double z, double y, double& l, double& dl, double& d2) {
+  if constexpr (LOSS == LOSS_LOGISTIC) {
+    // one exp, one log1p, one reciprocal, no branches (as pointwise_loss in glm_kernels.hip):
+    // e = exp(-|z|) serves the sigmoid and log(1 + exp(+-z)) = max(+-z, 0) + log1p(e)
+    const double e = exp(-fabs(z));
+    const double lp = log1p(e);
+    const double r = 1.0 / (1.0 + e);
+    const double s = z >= 0.0 ? r : e * r;
+    const bool pos = y > 0.5;
+    const double zz = pos ? -z : z;
+    l = (zz > 0.0 ? zz : 0.0) + lp;
+    dl = pos ? s - 1.0 : s;
     d2 = s * (1.0 - s);
-  } else if (loss == LOSS_POISSON) {
+  } else if constexpr (LOSS == LOSS_POISSON) {
     const double e = exp(z);
     l = e - y * z; dl = e - y; d2 = e;
   } else {
@@ -127,6 +133,7 @@ struct ReTronArgs {
   int loss;
   double l2, tol;
   int max_iter, max_fail, max_cg, dmax;
+  double* gsc;               // lean kernel: gradient at W, per coefficient (packed like W)
 };
 
 // Sum over the 16 lanes of a DPP row, in every lane of the row (fixed-order butterflies: deterministic).
@@ -140,18 +147,17 @@ __device__ __forceinline__ double row16_total(double v) {
 
 #define RE_G 16                      // lanes per row (one DPP row)
 #define RE_RPI (64 / RE_G)           // rows per wave instruction
-#define RE_U 3                       // instruction groups in flight per wave batch
-#define RE_BATCH (RE_RPI * RE_U)     // rows per wave batch
+#define RE_U 4                       // row groups in flight per wave batch (re_tron_csr_kernel; 3: +2.4 %)
 #define RE_K 4                       // entries per lane kept in registers (rows of <= 64 entries in one go)
 
-// One pass over the entity's rows [r0, r1): a wave takes RE_BATCH consecutive rows at a time, RE_G lanes per
+// One pass over the entity's rows [r0, r1): a wave takes BATCH = 4 U consecutive rows at a time, RE_G lanes per
 // row (lane k of the row: entries k, k + 16, ...). The next batch's row pointers are fetched while the current
-// batch computes, and all RE_BATCH rows' entries are loaded before the first gather, so a batch costs about one
+// batch computes, and all BATCH rows' entries are loaded before the first gather, so a batch costs about one
 // dependent global-memory latency.
 // MODE 0: Hessian-vector data term: acc_w += X^T (Dc * (X vec)).
 // MODE 1: value + gradient at vec: acc_w += X^T (wt * l'), fpart += wt * l, Dn = wt * l'', Zn = x.vec.
 // MODE 2: value + gradient at zero (no gathers, no scratch writes).
-template <int MODE>
+template <int MODE, int LOSS, int U = RE_U>
 __device__ __forceinline__ void row_pass(const ReTronArgs& a, long long r0, long long r1,
                                          const double* __restrict__ vec, double* __restrict__ acc,
                                          const double* __restrict__ Dc, double* __restrict__ Dn,
@@ -169,21 +175,22 @@ __device__ __forceinline__ void row_pass(const ReTronArgs& a, long long r0, long
   const double* __restrict__ yv = a.y + r0;
   if (MODE == 0) Dc += r0;
   if (MODE == 1) { Dn += r0; Zn += r0; }
-  const int step = RE_NW * RE_BATCH;
-  int base = w * RE_BATCH;
-  // row pointers of a batch: lane j <= RE_BATCH holds nip[base + j] (clamped to the entity's last row)
+  constexpr int BATCH = RE_RPI * U;
+  const int step = RE_NW * BATCH;
+  int base = w * BATCH;
+  // row pointers of a batch: lane j <= BATCH holds nip[base + j] (clamped to the entity's last row)
   auto fetch_ptr = [&](int b) -> int {
-    const int i = b + (lane <= RE_BATCH ? lane : RE_BATCH);
+    const int i = b + (lane <= BATCH ? lane : BATCH);
     return b < nrows ? (int)(nip[i < nrows ? i : nrows] - e0) : 0;
   };
   int np = fetch_ptr(base);
   for (; base < nrows; base += step) {
     const int np_next = fetch_ptr(base + step);
-    int lo[RE_U], hi[RE_U];
-    int c[RE_U][RE_K];
-    double v[RE_U][RE_K], dot[RE_U], rs[RE_U][3];
+    int lo[U], hi[U];
+    int c[U][RE_K];
+    double v[U][RE_K], dot[U], rs[U][3];
 #pragma unroll
-    for (int u = 0; u < RE_U; ++u) {
+    for (int u = 0; u < U; ++u) {
       const int q = u * RE_RPI + grp;
       lo[u] = __shfl(np, q, 64);
       hi[u] = __shfl(np, q + 1, 64);
@@ -198,7 +205,7 @@ __device__ __forceinline__ void row_pass(const ReTronArgs& a, long long r0, long
       }
     }
 #pragma unroll
-    for (int u = 0; u < RE_U; ++u) {
+    for (int u = 0; u < U; ++u) {
 #pragma unroll
       for (int k = 0; k < RE_K; ++k) {
         const int p = lo[u] + gl + RE_G * k;
@@ -208,7 +215,7 @@ __device__ __forceinline__ void row_pass(const ReTronArgs& a, long long r0, long
       }
     }
 #pragma unroll
-    for (int u = 0; u < RE_U; ++u) {
+    for (int u = 0; u < U; ++u) {
       double s = 0.0;
       if (MODE != 2) {
 #pragma unroll
@@ -218,7 +225,7 @@ __device__ __forceinline__ void row_pass(const ReTronArgs& a, long long r0, long
       dot[u] = s;
     }
 #pragma unroll
-    for (int u = 0; u < RE_U; ++u) {
+    for (int u = 0; u < U; ++u) {
       if (MODE != 2) dot[u] = row16_total(dot[u]);
       const int i = base + u * RE_RPI + grp;
       const bool valid = i < nrows;
@@ -228,7 +235,7 @@ __device__ __forceinline__ void row_pass(const ReTronArgs& a, long long r0, long
       } else {
         double l = 0.0, dl = 0.0, d2 = 0.0;
         if (valid) {
-          pointwise_loss(a.loss, dot[u] + rs[u][1], rs[u][2], l, dl, d2);
+          loss_t<LOSS>(dot[u] + rs[u][1], rs[u][2], l, dl, d2);
           if (gl == 0) {
             fpart += rs[u][0] * l;
             if (MODE == 1) { Dn[i] = rs[u][0] * d2; Zn[i] = dot[u]; }
@@ -245,6 +252,7 @@ __device__ __forceinline__ void row_pass(const ReTronArgs& a, long long r0, long
   }
 }
 
+template <int LOSS>
 __global__ __launch_bounds__(RE_THREADS) void re_tron_csr_kernel(ReTronArgs a) {
   extern __shared__ __attribute__((aligned(16))) double smem[];
   const int e = a.order[blockIdx.x];
@@ -276,8 +284,8 @@ __global__ __launch_bounds__(RE_THREADS) void re_tron_csr_kernel(ReTronArgs a) {
     __syncthreads();
     zero_own();
     double fp = 0.0;
-    if (at_zero) row_pass<2>(a, r0, r1, vec, myacc, nullptr, nullptr, nullptr, fp);
-    else row_pass<1>(a, r0, r1, vec, myacc, nullptr, D[nb], Z[nb], fp);
+    if (at_zero) row_pass<2, LOSS>(a, r0, r1, vec, myacc, nullptr, nullptr, nullptr, fp);
+    else row_pass<1, LOSS>(a, r0, r1, vec, myacc, nullptr, D[nb], Z[nb], fp);
     __syncthreads();
     double s3[3] = {fp, 0.0, 0.0};
     for (int j = tid; j < d; j += RE_THREADS) {
@@ -335,7 +343,7 @@ __global__ __launch_bounds__(RE_THREADS) void re_tron_csr_kernel(ReTronArgs a) {
       __syncthreads();
       zero_own();
       double fp = 0.0;
-      row_pass<0>(a, r0, r1, sD, myacc, D[cur], nullptr, nullptr, fp);
+      row_pass<0, LOSS>(a, r0, r1, sD, myacc, D[cur], nullptr, nullptr, fp);
       __syncthreads();
       double s5[5] = {0.0, 0.0, 0.0, 0.0, 0.0};
       for (int j = tid; j < d; j += RE_THREADS) {
@@ -437,6 +445,236 @@ __global__ __launch_bounds__(RE_THREADS) void re_tron_csr_kernel(ReTronArgs a) {
   }
 }
 
+// Lean streaming TRON (d_e <= 1024): the same solve as re_tron_csr_kernel with only the GATHERED vector and the
+// per-wave accumulators in LDS ((1 + RE_NW) x dmax doubles: 40 KB at dmax 1024, so four workgroups = 16 waves per
+// CU instead of two). A thread owns coefficients j = tid + 256 q (q < J) for the whole solve: their CG step and
+// residual live in its registers, the gradient at W in global scratch (a.gsc) and W itself is updated in place
+// in a.W (both are touched once per TRON iteration by their owner thread only). Held to <= 168 VGPRs (3 waves
+// per SIMD): small and mid entities are latency-bound (a pass is a few dependent batches), so more entities in
+// flight per CU is more streaming throughput.
+// Measured on 43K game5pl-like entities (scripts/re_fused_bench.py, profiles/re_lean_ab_r4.md): 3 waves per SIMD
+// (<= 168 VGPRs, 12 waves per CU) with one row group per batch in function evaluations and three in Hessian-vector
+// passes; 4 waves per SIMD spills in the row loop (80 ms vs 61 ms for re_tron_csr_kernel)
+#define LEAN_WPE 3
+#define LEAN_UF 1
+#define LEAN_UH 3
+template <int LOSS, int J>
+__global__ __launch_bounds__(RE_THREADS) __attribute__((amdgpu_waves_per_eu(LEAN_WPE, LEAN_WPE)))
+void re_tron_lean_kernel(ReTronArgs a) {
+  extern __shared__ __attribute__((aligned(16))) double smem[];
+  const int e = a.order[blockIdx.x];
+  const long long r0 = a.row_ptr[e], r1 = a.row_ptr[e + 1];
+  const long long c0 = a.col_ptr[e];
+  const int d = (int)(a.col_ptr[e + 1] - c0);
+  const int tid = threadIdx.x, w = tid >> 6, lane = tid & 63;
+  const int dm = a.dmax;
+  double* sD = smem;        // CG direction; W / the trial point during a function evaluation
+  double* acc = sD + dm;    // RE_NW accumulators; acc[0 .. d) = combined gradient after a function evaluation
+  double* red = acc + RE_NW * dm;
+  double* myacc = acc + w * dm;
+  double* D[2] = {a.scr, a.scr + a.n_rows};
+  double* Z[2] = {a.scr + 2 * a.n_rows, a.scr + 3 * a.n_rows};
+  double* Wg = a.W + c0;
+  double* Gg = a.gsc + c0;
+  int cur = 0, parity = 0, npass = 0;
+  double S[J], R[J];
+
+  auto combined = [&](int j) -> double {
+    double g = acc[j];
+#pragma unroll
+    for (int q = 1; q < RE_NW; ++q) g += acc[q * dm + j];
+    return g;
+  };
+  // value + gradient at sD (or at zero); gradient -> acc[0 .. d)
+  auto value_grad = [&](bool at_zero, int nb, double& gg) -> double {
+    ++npass;
+    __syncthreads();
+    for (int j = lane; j < d; j += 64) myacc[j] = 0.0;
+    double fp = 0.0;
+    if (at_zero) row_pass<2, LOSS, LEAN_UF>(a, r0, r1, sD, myacc, nullptr, nullptr, nullptr, fp);
+    else row_pass<1, LOSS, LEAN_UF>(a, r0, r1, sD, myacc, nullptr, D[nb], Z[nb], fp);
+    __syncthreads();
+    double s3[3] = {fp, 0.0, 0.0};
+#pragma unroll
+    for (int q = 0; q < J; ++q) {
+      const int j = tid + RE_THREADS * q;
+      if (j < d) {
+        const double v = at_zero ? 0.0 : sD[j];
+        const double g = combined(j) + a.l2 * v;
+        acc[j] = g;
+        s3[1] += v * v;
+        s3[2] += g * g;
+      }
+    }
+    block_sums<3>(s3, red, parity);
+    gg = s3[2];
+    return s3[0] + 0.5 * a.l2 * s3[1];
+  };
+
+#pragma unroll
+  for (int q = 0; q < J; ++q) {
+    const int j = tid + RE_THREADS * q;
+    if (j < d) sD[j] = Wg[j];
+  }
+  double gnorm2;
+  double f = value_grad(false, cur, gnorm2);
+  double nz[1] = {0.0};
+#pragma unroll
+  for (int q = 0; q < J; ++q) {
+    const int j = tid + RE_THREADS * q;
+    if (j < d) {
+      Gg[j] = acc[j];
+      nz[0] += sD[j] != 0.0 ? 1.0 : 0.0;
+    }
+  }
+  block_sums<1>(nz, red, parity);
+  double f0z = f, g0n = sqrt(gnorm2);
+  if (nz[0] != 0.0) {
+    double g0;
+    f0z = value_grad(true, 0, g0);
+    g0n = sqrt(g0);
+  }
+  const double loss_tol = f0z * a.tol, grad_tol = g0n * a.tol;
+  double delta = sqrt(gnorm2);
+  int it = 0, fails = 0, reason = 0;
+  bool active = true;
+  if (delta == 0.0) { reason = 4; active = false; }
+  const double eta0 = 1e-4, eta1 = 0.25, eta2 = 0.75, sg1 = 0.25, sg2 = 0.5, sg3 = 4.0;
+  const int guard_max = a.max_iter * (a.max_fail + 1) + 5;
+  for (int guard = 0; active && guard < guard_max; ++guard) {
+    // truncated CG at W: one Hessian-vector pass, one combine sweep with the five dot products, one update sweep
+#pragma unroll
+    for (int q = 0; q < J; ++q) {
+      const int j = tid + RE_THREADS * q;
+      const double g = j < d ? Gg[j] : 0.0;
+      S[q] = 0.0;
+      R[q] = -g;
+      if (j < d) sD[j] = -g;
+    }
+    double rtr = gnorm2, sts = 0.0;
+    const double cg_tol2 = 0.01 * gnorm2;        // (0.1 ||g||)^2
+    for (int k = 0; k < a.max_cg; ++k) {
+      if (!(rtr > cg_tol2)) break;
+      ++npass;
+      __syncthreads();
+      for (int j = lane; j < d; j += 64) myacc[j] = 0.0;
+      double fp = 0.0;
+      row_pass<0, LOSS, LEAN_UH>(a, r0, r1, sD, myacc, D[cur], nullptr, nullptr, fp);
+      __syncthreads();
+      double s5[5] = {0.0, 0.0, 0.0, 0.0, 0.0};
+      double H[J];
+#pragma unroll
+      for (int q = 0; q < J; ++q) {
+        const int j = tid + RE_THREADS * q;
+        H[q] = 0.0;
+        if (j < d) {
+          const double dj = sD[j];
+          const double h = combined(j) + a.l2 * dj;
+          H[q] = h;
+          s5[0] += dj * h;
+          s5[1] += S[q] * dj;
+          s5[2] += dj * dj;
+          s5[3] += R[q] * h;
+          s5[4] += h * h;
+        }
+      }
+      block_sums<5>(s5, red, parity);
+      const double dhd = s5[0], std_ = s5[1], dtd = s5[2], rh = s5[3], hh = s5[4];
+      const double alpha = rtr / (dhd == 0.0 ? 1.0 : dhd);
+      double tn = sts + 2.0 * alpha * std_ + alpha * alpha * dtd;
+      tn = tn > 0.0 ? tn : 0.0;
+      const double dsq = delta * delta;
+      const bool hit = tn > dsq;
+      double al = alpha;
+      if (hit) {
+        const double qq = std_ * std_ + dtd * (dsq - sts);
+        const double rad = sqrt(qq > 0.0 ? qq : 0.0);
+        const double den1 = std_ + rad;
+        al = std_ >= 0.0 ? (dsq - sts) / (den1 > 1e-300 ? den1 : 1e-300) : (rad - std_) / (dtd > 1e-300 ? dtd : 1e-300);
+      }
+      double rn = rtr - 2.0 * al * rh + al * al * hh;
+      rn = rn > 0.0 ? rn : 0.0;
+      const double beta = rn / (rtr == 0.0 ? 1.0 : rtr);
+#pragma unroll
+      for (int q = 0; q < J; ++q) {
+        const int j = tid + RE_THREADS * q;
+        if (j < d) {
+          const double dj = sD[j];
+          S[q] += al * dj;
+          const double r = R[q] - al * H[q];
+          R[q] = r;
+          if (!hit) sD[j] = r + beta * dj;
+        }
+      }
+      if (hit) break;
+      rtr = rn;
+      sts = tn;
+    }
+    // trial point W + step (in sD), trust-region update, acceptance
+    double s3[3] = {0.0, 0.0, 0.0};
+#pragma unroll
+    for (int q = 0; q < J; ++q) {
+      const int j = tid + RE_THREADS * q;
+      if (j < d) {
+        const double sj = S[q];
+        s3[0] += Gg[j] * sj;
+        s3[1] += sj * R[q];
+        s3[2] += sj * sj;
+        sD[j] = Wg[j] + sj;
+      }
+    }
+    block_sums<3>(s3, red, parity);
+    const double gs = s3[0], pred = -0.5 * (gs - s3[1]), snorm = sqrt(s3[2]);
+    double gn2;
+    const double fn = value_grad(false, cur ^ 1, gn2);   // trial gradient in acc[0 .. d)
+    const double actual = f - fn;
+    if (it == 0) delta = fmin(delta, snorm);
+    const double den = fn - f - gs;
+    const double alr = den <= 0.0 ? sg3 : fmax(sg1, -0.5 * gs / (den == 0.0 ? 1.0 : den));
+    double nd;
+    if (actual < eta0 * pred) nd = fmin(fmax(alr, sg1) * snorm, sg2 * delta);
+    else if (actual < eta1 * pred) nd = fmax(sg1 * delta, fmin(alr * snorm, sg2 * delta));
+    else if (actual < eta2 * pred) nd = fmax(sg1 * delta, fmin(alr * snorm, sg3 * delta));
+    else nd = fmax(delta, fmin(alr * snorm, sg3 * delta));
+    delta = nd;
+    const bool accept = actual > eta0 * pred;
+    const double f_prev = f;
+    if (accept) {
+#pragma unroll
+      for (int q = 0; q < J; ++q) {
+        const int j = tid + RE_THREADS * q;
+        if (j < d) {
+          Wg[j] = sD[j];
+          Gg[j] = acc[j];
+        }
+      }
+      gnorm2 = gn2;
+      f = fn;
+      cur ^= 1;
+      ++it;
+      fails = 0;
+    } else {
+      ++fails;
+    }
+    const bool not_impr = !accept && fails >= a.max_fail;
+    int rc = 0;
+    if (accept && sqrt(gnorm2) <= grad_tol) rc = 4;
+    if (accept && fabs(f - f_prev) <= loss_tol) rc = 3;
+    if (not_impr) rc = 2;
+    if ((accept || not_impr) && it >= a.max_iter) rc = 1;
+    if (rc > 0) { reason = rc; active = false; }
+  }
+  __syncthreads();
+  if (a.zout != nullptr) {
+    const double* zc = Z[cur];
+    for (long long i = r0 + tid; i < r1; i += RE_THREADS) a.zout[i] = zc[i];
+  }
+  if (tid == 0) {
+    a.f[e] = f; a.iters[e] = it; a.reason[e] = reason;
+    if (a.npass != nullptr) a.npass[e] = npass;
+  }
+}
+
 // ============================================================================================================
 // Tall-narrow entities (d_e <= 64 coefficients, typically more rows than coefficients): ONE WAVE PER ENTITY, the
 // whole TRON with the EXACT per-entity Hessian H_e = X_e^T D X_e + l2 I. No workgroup barriers: the waves of a
@@ -469,29 +707,6 @@ __device__ __forceinline__ double quad_total(double v) {
   v += dpp_f64<0xB1>(v);    // quad_perm [1,0,3,2]
   v += dpp_f64<0x4E>(v);    // quad_perm [2,3,0,1]
   return v;
-}
-
-template <int LOSS>
-__device__ __forceinline__ void loss_t(double z, double y, double& l, double& dl, double& d2) {
-  if constexpr (LOSS == LOSS_LOGISTIC) {
-    // one exp, one log1p, one reciprocal, no branches (as pointwise_loss in glm_kernels.hip):
-    // e = exp(-|z|) serves the sigmoid and log(1 + exp(+-z)) = max(+-z, 0) + log1p(e)
-    const double e = exp(-fabs(z));
-    const double lp = log1p(e);
-    const double r = 1.0 / (1.0 + e);
-    const double s = z >= 0.0 ? r : e * r;
-    const bool pos = y > 0.5;
-    const double zz = pos ? -z : z;
-    l = (zz > 0.0 ? zz : 0.0) + lp;
-    dl = pos ? s - 1.0 : s;
-    d2 = s * (1.0 - s);
-  } else if constexpr (LOSS == LOSS_POISSON) {
-    const double e = exp(z);
-    l = e - y * z; dl = e - y; d2 = e;
-  } else {
-    const double d = z - y;
-    l = 0.5 * d * d; dl = d; d2 = 1.0;
-  }
 }
 
 template <int T>
@@ -1458,6 +1673,13 @@ __global__ __launch_bounds__(RS_THREADS) void re_tron_res_kernel(ReTronArgs a, R
   }
 }
 
+template <int LOSS>
+static void lean_launch(const ReTronArgs& a, int n_launch, size_t smem, hipStream_t st) {
+  if (a.dmax <= 256) hipLaunchKernelGGL((re_tron_lean_kernel<LOSS, 1>), dim3(n_launch), dim3(RE_THREADS), smem, st, a);
+  else if (a.dmax <= 512) hipLaunchKernelGGL((re_tron_lean_kernel<LOSS, 2>), dim3(n_launch), dim3(RE_THREADS), smem, st, a);
+  else hipLaunchKernelGGL((re_tron_lean_kernel<LOSS, 4>), dim3(n_launch), dim3(RE_THREADS), smem, st, a);
+}
+
 extern "C" {
 
 // Shared memory of one workgroup for entities of at most ``dmax`` coefficients.
@@ -1474,7 +1696,30 @@ int pml_re_tron_csr(const int* order, int n_launch, const long long* row_ptr, co
   if (smem > 160 * 1024) return -22;
   ReTronArgs a{order, n_launch, row_ptr, col_ptr, nip, lcol, val, y, off, wt, scr, n_rows, W, f, iters, reason,
                zout, npass, loss, l2, tol, max_iter, max_fail, max_cg, dmax};
-  hipLaunchKernelGGL(re_tron_csr_kernel, dim3(n_launch), dim3(RE_THREADS), smem, st, a);
+  if (loss == LOSS_LOGISTIC) hipLaunchKernelGGL(re_tron_csr_kernel<0>, dim3(n_launch), dim3(RE_THREADS), smem, st, a);
+  else if (loss == LOSS_POISSON) hipLaunchKernelGGL(re_tron_csr_kernel<1>, dim3(n_launch), dim3(RE_THREADS), smem, st, a);
+  else hipLaunchKernelGGL(re_tron_csr_kernel<2>, dim3(n_launch), dim3(RE_THREADS), smem, st, a);
+  LAUNCH_CHECK();
+  return 0;
+}
+
+// Lean streaming kernel (dmax <= 1024): LDS (1 + RE_NW) x dmax doubles; ``gsc`` scratch of one double per
+// coefficient (packed like W); W is updated in place.
+size_t pml_re_tron_lean_smem(int dmax) { return ((size_t)(1 + RE_NW) * dmax + 2 * RE_NW * 8) * sizeof(double); }
+
+int pml_re_tron_lean(const int* order, int n_launch, const long long* row_ptr, const long long* col_ptr,
+                     const long long* nip, const uint16_t* lcol, const double* val, const double* y,
+                     const double* off, const double* wt, double* scr, long long n_rows, double* W, double* f,
+                     int* iters, int* reason, double* zout, int* npass, int loss, double l2, double tol,
+                     int max_iter, int max_fail, int max_cg, int dmax, double* gsc, hipStream_t st) {
+  if (n_launch <= 0) return 0;
+  if (dmax <= 0 || dmax > 1024 || loss < 0 || loss > 2 || gsc == nullptr) return -22;
+  const size_t smem = pml_re_tron_lean_smem(dmax);
+  ReTronArgs a{order, n_launch, row_ptr, col_ptr, nip, lcol, val, y, off, wt, scr, n_rows, W, f, iters, reason,
+               zout, npass, loss, l2, tol, max_iter, max_fail, max_cg, dmax, gsc};
+  if (loss == LOSS_LOGISTIC) lean_launch<0>(a, n_launch, smem, st);
+  else if (loss == LOSS_POISSON) lean_launch<1>(a, n_launch, smem, st);
+  else lean_launch<2>(a, n_launch, smem, st);
   LAUNCH_CHECK();
   return 0;
 }

@@ -645,6 +645,8 @@ def re_lib() -> Optional[ctypes.CDLL]:
         lib.pml_re_tron_smem.argtypes = [c_int]
         lib.pml_re_tron_smem.restype = ctypes.c_size_t
         lib.pml_re_tron_hess.argtypes = lib.pml_re_tron_csr.argtypes
+        lib.pml_re_tron_lean.argtypes = lib.pml_re_tron_csr.argtypes[:-1] + [c_void_p, c_void_p]
+        lib.pml_re_tron_lean.restype = c_int
         lib.pml_re_tron_hess.restype = c_int
         lib.pml_re_tron_hess_smem.argtypes = [c_int]
         lib.pml_re_tron_hess_smem.restype = ctypes.c_size_t
@@ -671,9 +673,14 @@ def require_re_lib() -> ctypes.CDLL:
     return lib
 
 
+# the lean streaming kernel takes launch classes up to this many coefficients (PML_RE_LEAN=0: never)
+RE_LEAN_DMAX = 1024 if os.environ.get("PML_RE_LEAN", "1") != "0" else 0
+
+
 def re_tron_csr(order, row_ptr, col_ptr, nip, lcol, val, y, off, wt, scr, W, f, iters, reason, zout, loss_id: int,
                 l2: float, tol: float, max_iter: int, max_fail: int, max_cg: int, dmax: int,
-                npass: Optional[torch.Tensor] = None, hessian: bool = False) -> None:
+                npass: Optional[torch.Tensor] = None, hessian: bool = False, gsc: Optional[torch.Tensor] = None,
+                lean: Optional[bool] = None) -> None:
     """Fused per-entity primal TRON over the entities ``order`` (int32; one workgroup each) of a block-diagonal
     CSR (``re_tron_csr_kernel``). Entity ``e`` owns rows ``row_ptr[e]:row_ptr[e+1]`` (int64) and coefficients
     ``col_ptr[e]:col_ptr[e+1]`` of the packed ``W`` (fp64, in: warm start, out: solution); ``nip`` int64 row
@@ -681,7 +688,9 @@ def re_tron_csr(order, row_ptr, col_ptr, nip, lcol, val, y, off, wt, scr, W, f, 
     ``off``, ``wt`` per row; ``scr`` fp64 scratch of 4 x rows; outputs ``f`` / ``iters`` / ``reason`` per
     entity and ``zout`` (x_i . w per row); ``npass`` (optional int32 per entity): row passes run. ``hessian``:
     the tall-narrow kernel (``re_tron_hess_kernel``: d_e <= dmax <= 64, dmax a multiple of 16; the per-entity
-    Hessian formed on the fp64 matrix cores, CG on it in LDS). Device only; in place, nothing returned."""
+    Hessian formed on the fp64 matrix cores, CG on it in LDS). ``lean`` (default: dmax <= 1024): the
+    ``re_tron_lean_kernel`` (only the gathered vector + accumulators in LDS, four workgroups per CU) with ``gsc``
+    (fp64 scratch like ``W``; allocated when None). Device only; in place, nothing returned."""
     lib = require_re_lib()
     n_rows = y.numel()
     B = int(order.numel())
@@ -704,14 +713,22 @@ def re_tron_csr(order, row_ptr, col_ptr, nip, lcol, val, y, off, wt, scr, W, f, 
         oe = order.to(torch.int64)
         assert int((col_ptr[oe + 1] - col_ptr[oe]).max()) <= dmax, "entity wider than the launch's LDS class"
         assert int(row_ptr[-1]) == n_rows and int(nip[-1]) == val.numel(), "row / non-zero ranges inconsistent"
+    if lean is None:
+        lean = not hessian and dmax <= RE_LEAN_DMAX
+    args = [order.data_ptr(), B, row_ptr.data_ptr(), col_ptr.data_ptr(), nip.data_ptr(), lcol.data_ptr(),
+            val.data_ptr(), y.data_ptr(), off.data_ptr(), wt.data_ptr(), scr.data_ptr(), n_rows, W.data_ptr(),
+            f.data_ptr(), iters.data_ptr(), reason.data_ptr(), zout.data_ptr(),
+            None if npass is None else npass.data_ptr(), int(loss_id), float(l2), float(tol), int(max_iter),
+            int(max_fail), int(max_cg), int(dmax)]
+    if lean:
+        assert not hessian and dmax <= 1024
+        if gsc is None:
+            gsc = torch.empty_like(W)
+        assert gsc.is_cuda and gsc.dtype == torch.float64 and gsc.numel() >= W.numel() and gsc.device == W.device
+        check(lib.pml_re_tron_lean(*args, gsc.data_ptr(), stream_handle(W.device)), "re_tron_lean")
+        return
     fn = lib.pml_re_tron_hess if hessian else lib.pml_re_tron_csr
-    check(fn(order.data_ptr(), B, row_ptr.data_ptr(), col_ptr.data_ptr(), nip.data_ptr(),
-                              lcol.data_ptr(), val.data_ptr(), y.data_ptr(), off.data_ptr(), wt.data_ptr(),
-                              scr.data_ptr(), n_rows, W.data_ptr(), f.data_ptr(), iters.data_ptr(),
-                              reason.data_ptr(), zout.data_ptr(),
-                              None if npass is None else npass.data_ptr(), int(loss_id), float(l2), float(tol),
-                              int(max_iter),
-                              int(max_fail), int(max_cg), int(dmax), stream_handle(W.device)), "re_tron_csr")
+    check(fn(*args, stream_handle(W.device)), "re_tron_csr")
 
 
 def re_res_params():

@@ -107,6 +107,7 @@ class EntityTronBatch:
         self.n_rows = n_rows
         self.nnz = nnz
         self.scr = torch.empty(4 * max(n_rows, 1), dtype=torch.float64, device=dev)
+        self.gsc = torch.empty(int(self.col_ptr[-1]), dtype=torch.float64, device=dev)   # lean kernel: gradient
         # launch classes by LDS size; inside a class the largest entities first (they bound the launch's tail).
         # Entities of at most HESS_DMAX coefficients (tall: the row space took the wide ones) run the exact-Hessian
         # kernel (MFMA), the others the sparse Hessian-vector kernel.
@@ -179,7 +180,7 @@ class EntityTronBatch:
         for dm, order, is_h in self.launches:
             re_tron_csr(order, self.row_ptr, self.col_ptr, self.nip, self.lcol, self.val, self.y, off, self.w,
                         self.scr, W, f, iters, reason, z, loss.loss_id, l2, tol, max_iter, max_fail, max_cg, dm,
-                        hessian=is_h)
+                        hessian=is_h, gsc=self.gsc)
         if err is not None and int(err.item()) != 0:
             raise RuntimeError("register-resident random-effect TRON: a workgroup cluster wait timed out "
                                "(results invalid); rerun with PML_RE_RESIDENT=0")

@@ -1,6 +1,7 @@
-"""Microbenchmark of the fused per-entity primal TRON on game5pl-like entities: the streaming kernel
-(re_tron_csr_kernel: rows re-read from memory every pass) vs the register-resident kernel (re_tron_res_kernel: rows
-loaded once into VGPRs, heavy entities split over workgroup clusters).
+"""Microbenchmark of the fused per-entity primal TRON on game5pl-like entities: the streaming kernels
+(``stream`` = re_tron_csr_kernel, ``lean`` = re_tron_lean_kernel: rows re-read from memory every pass) vs the
+register-resident kernel (``res`` = re_tron_res_kernel: rows loaded once into VGPRs, heavy entities split over
+workgroup clusters).
 
 Entities: power-law sizes (Pareto 1.3, 65 .. 20000 rows, the entities the row-space batch does not take at config
 5), 1000-feature pools + intercept (d_e <= 1001), 50 distinct pool features per row with N(0,1) values, logistic
@@ -82,7 +83,7 @@ def run(kernel, order, reps=3):
     else:
         def call(np_=None):
             re_tron_csr(order, row_ptr, col_ptr, nip, lcol, val, y, off, wt, scr, W, f, it, rc, z, 0, 1.0, 1e-12, 10,
-                        5, 20, 1024, npass=np_)
+                        5, 20, 1024, npass=np_, lean=kernel == "lean")
             return None
     err = call(npass)
     torch.cuda.synchronize()

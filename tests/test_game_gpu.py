@@ -411,3 +411,30 @@ def test_row_space_big_classes_match_primal(task, monkeypatch):
     for i in range(4):
         torch.testing.assert_close(torch.as_tensor(b[i]), torch.as_tensor(a[i]), rtol=1e-5, atol=1e-6)
     assert abs(a[4] - b[4]) < 0.05
+
+
+@pytest.mark.parametrize("task,d_user", [("LOGISTIC_REGRESSION", 40), ("POISSON_REGRESSION", 40),
+                                         ("LOGISTIC_REGRESSION", 700), ("LINEAR_REGRESSION", 300)])
+def test_lean_streaming_tron_matches_csr_kernel(task, d_user, monkeypatch):
+    """re_tron_lean_kernel (CG step / residual in registers, gradient in global scratch, W updated in place; only
+    the gathered vector and the wave accumulators in LDS) runs the same sums in the same order as
+    re_tron_csr_kernel: the same models, scores and iteration counts to rounding, across a warm-started second
+    update, for every LDS class it serves (J = 1, 2, 4 coefficients per thread)."""
+    import photon_ml_amd.ops.native as nat
+    import photon_ml_amd.optimization.entity_tron as et
+    data, _ = generate_game_data(n_rows=40000, n_users=200, d_user=d_user, seed=31, task=task)
+    out = {}
+    for lean in (0, 1024):
+        monkeypatch.setattr(nat, "RE_LEAN_DMAX", lean)
+        monkeypatch.setattr(et, "HESS_DMAX", 0)          # the sparse kernels, not the tall one
+        monkeypatch.setenv("PML_RE_ROW_SPACE", "0")
+        c, v1, s1, v2, s2 = _re_two_updates(data, task, max_iter=50, tol=1e-12)
+        out[lean] = (v1, s1, v2, s2, c.last_stats["mean_iterations"])
+    a, b = out[0], out[1024]
+    for i in range(4):
+        ta, tb = torch.as_tensor(a[i]), torch.as_tensor(b[i])
+        print(f"max |diff| {float((ta - tb).abs().max()):.3e}")
+        # fp-contraction may fuse differently around the register / global-memory vectors: rounding-level
+        # differences, amplified along the TRON path as in test_fused_entity_tron_matches_pass_path
+        torch.testing.assert_close(tb, ta, rtol=1e-5, atol=1e-6)
+    assert abs(a[4] - b[4]) < 0.05
