@@ -256,6 +256,8 @@ def game_extra(dev, rank: int, world: int) -> dict:
         out.update({f"{pre}_sweeps_per_sec": g["value"], f"{pre}_ms_per_sweep": g["ms_per_step"],
                     f"{pre}_sweep_ms_min": g["sweep_ms_min"], f"{pre}_sweep_ms_median": g["sweep_ms_median"],
                     f"{pre}_coordinate_ms": g["coordinate_ms"]})
+        if g.get("route_s"):
+            out[f"{pre}_route_s"] = g["route_s"]
         if prec == "bf16":
             out["game5pl_config"] = dict(g["config"], fe_dtype=g["dtype"], re_dtype="fp64", steps=g["steps"],
                                          warmup=g["warmup"], data_generation_s=round(g["data_generation_s"], 1),

@@ -197,6 +197,9 @@ def run(args, dev, rank: int = 0, world: int = 1, data=None, t_data: float = 0.0
     t_build = time.time() - t0
     log(f"coordinates built in {t_build:.1f}s (fixed effect {args.precision}); RE: "
         f"{coords['per-entity'].dataset.summary()}")
+    # entity-sharded build: per-phase routing seconds (max over ranks)
+    route_s = {k: round(all_reduce_scalar(v, "max"), 3)
+               for k, v in sorted(getattr(coords["per-entity"], "route_times", {}).items())}
     train_eval = build_evaluator("LOGISTIC_LOSS", data.response, data.offsets, data.weights, device=dev)
     sweep_end = []
     n_coords = len(coords)
@@ -261,7 +264,8 @@ def run(args, dev, rank: int = 0, world: int = 1, data=None, t_data: float = 0.0
         "metric": "GAME coord-descent iters/sec (fixed + per-entity random effect)",
         "value": args.steps / elapsed,
         "unit": "CD iterations/sec",
-        "n_gpus": world,
+        "n_gpus": world,            # main() replaces it with the distinct-device count
+        "n_ranks": world,
         "steps": args.steps,
         "warmup": args.warmup,
         "ms_per_step": 1000.0 * elapsed / args.steps,
@@ -283,6 +287,7 @@ def run(args, dev, rank: int = 0, world: int = 1, data=None, t_data: float = 0.0
         "examples_per_sec": total_rows * args.steps / elapsed,
         "data_generation_s": t_data,
         "coordinate_build_s": t_build,
+        **({"route_s": route_s} if route_s else {}),
     }
 
 

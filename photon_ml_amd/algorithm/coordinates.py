@@ -758,7 +758,7 @@ class ShardedRandomEffectCoordinate(Coordinate):
         times = {} if times is None else times
         with Timed(f"RE {self.coordinate_id}: route rows to entity owners", log, logging.INFO):
             t0 = time.perf_counter()
-            x = router.forward_csr_device(data.shard(shard), dev)
+            x = router.forward_csr_device(data.shard(shard), dev, times)
             self._sync()
             t1 = time.perf_counter()
             ids = np.asarray(ids)

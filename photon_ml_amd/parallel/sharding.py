@@ -15,6 +15,7 @@ shuffles. Entity ownership is computed identically on every rank from all-gather
 from __future__ import annotations
 
 import heapq
+import time
 from typing import List, Optional, Sequence, Tuple
 
 import numpy as np
@@ -164,6 +165,31 @@ class EntityPartitioner:
         return EntityPartitioner(gk[top].cpu().numpy(), gc[top].cpu().numpy(), _world(), top_k)
 
 
+class _PhaseClock:
+    """Accumulates wall seconds per named phase into ``times`` (no-op when None); synchronises the device the
+    phase ran on first, so a phase's asynchronous kernels are charged to it."""
+
+    def __init__(self, times: Optional[dict], dev):
+        self.times, self.dev = times, torch.device(dev)
+        self.t = time.perf_counter()
+        if times is not None:
+            self._sync(self.dev)
+            self.t = time.perf_counter()
+
+    @staticmethod
+    def _sync(dev):
+        if dev.type == "cuda":
+            torch.cuda.synchronize(dev)
+
+    def __call__(self, name: str, dev=None):
+        if self.times is None:
+            return
+        self._sync(torch.device(dev) if dev is not None else self.dev)
+        now = time.perf_counter()
+        self.times[name] = self.times.get(name, 0.0) + now - self.t
+        self.t = now
+
+
 class RowRouter:
     """Fixed permutation between this rank's sample rows and the rows it owns after routing by ``dest``.
 
@@ -230,9 +256,23 @@ class RowRouter:
     def _a2a(self, send: torch.Tensor, sc: List[int], rc: List[int]):
         dev = comm_device(self.group)
         tail = tuple(send.shape[1:])
-        out = torch.empty((sum(rc),) + tail, dtype=send.dtype, device=dev)
-        dist.all_to_all_single(out, send.to(dev).contiguous(), rc, sc, group=self.group)
-        return out.to(send.device), rc
+        if dev.type == "cuda" or len(sc) == 1:
+            # RCCL: one collective over device buffers (the self segment is a device-local copy inside it)
+            out = torch.empty((sum(rc),) + tail, dtype=send.dtype, device=dev)
+            dist.all_to_all_single(out, send.to(dev).contiguous(), rc, sc, group=self.group)
+            return out.to(send.device), rc
+        # host-staged backend (gloo): the segment this rank keeps never leaves its device; only the others
+        # are staged through the host and exchanged
+        me = _rank()
+        so, ro = int(sum(sc[:me])), int(sum(rc[:me]))
+        keep = send[so:so + sc[me]]
+        sc2, rc2 = list(sc), list(rc)
+        sc2[me] = rc2[me] = 0
+        send2 = torch.cat([send[:so], send[so + sc[me]:]]).to(dev).contiguous()
+        got = torch.empty((sum(rc2),) + tail, dtype=send.dtype, device=dev)
+        dist.all_to_all_single(got, send2, rc2, sc2, group=self.group)
+        got = got.to(send.device)
+        return torch.cat([got[:ro], keep, got[ro:]]), rc
 
     def forward_csr(self, x: sp.csr_matrix) -> sp.csr_matrix:
         """Route sparse rows: one all-to-all each for row lengths, column indices and values. The entry
@@ -268,13 +308,17 @@ class RowRouter:
         out.has_sorted_indices = bool(getattr(x, "has_sorted_indices", False))
         return out
 
-    def forward_csr_device(self, x, device) -> "DeviceCSR":
+    def forward_csr_device(self, x, device, times: Optional[dict] = None) -> "DeviceCSR":
         """Route sparse rows and KEEP them on ``device`` (a :class:`DeviceCSR`): row lengths, column indices and
         values each one all-to-all of device tensors under RCCL, the entry permutation a device gather — no scipy
-        and no host copy of the routed rows (they go straight to the device random-effect build)."""
+        and no host copy of the routed rows (they go straight to the device random-effect build). ``times``:
+        seconds of the phases (conversion to tensors, entry permutation, collectives, assembly), accumulated."""
         from ..data.matrix import DeviceCSR
         dev = torch.device(device)
-        cdev = comm_device(self.group)
+        # the entry permutation runs on the target device whenever it is a GPU (also under a host-staged
+        # backend: a device gather, then only the outgoing segments cross the host in _a2a)
+        cdev = dev if dev.type == "cuda" else comm_device(self.group)
+        clock = _PhaseClock(times, cdev)
         if isinstance(x, DeviceCSR):
             indptr, x_ind, x_val = x.indptr.to(cdev), x.indices.to(cdev), x.data.to(cdev)
         else:
@@ -282,6 +326,7 @@ class RowRouter:
             indptr = torch.from_numpy(x.indptr.astype(np.int64)).to(cdev)
             x_ind = torch.from_numpy(x.indices).to(cdev)
             x_val = torch.from_numpy(x.data).to(cdev, torch.float64)
+        clock("csr_convert")
         lens = indptr[1:] - indptr[:-1]
         perm = self.perm_on(cdev)
         ol = lens[perm]
@@ -296,6 +341,7 @@ class RowRouter:
                                       torch.tensor(self.send_counts, dtype=torch.int64, device=cdev),
                                       output_size=perm.numel())
         nnz_send = torch.zeros(P, dtype=torch.int64, device=cdev).index_add_(0, seg, ol).tolist()
+        clock("csr_permute")
         rl = self.forward(lens)
         rseg = torch.repeat_interleave(torch.arange(P, device=cdev),
                                        torch.tensor(self.recv_counts, dtype=torch.int64, device=cdev),
@@ -304,10 +350,13 @@ class RowRouter:
         if is_dist():
             ri, _ = self._a2a(ri, nnz_send, nnz_recv)
             rv, _ = self._a2a(rv, nnz_send, nnz_recv)
+        clock("csr_collective")
         rip = torch.zeros(rl.numel() + 1, dtype=torch.int64, device=cdev)
         torch.cumsum(rl, 0, out=rip[1:])
-        return DeviceCSR(rip.to(dev), ri.to(dev), rv.to(dev), (self.n_recv, x.shape[1]),
-                         bool(getattr(x, "has_sorted_indices", False)))
+        out = DeviceCSR(rip.to(dev), ri.to(dev), rv.to(dev), (self.n_recv, x.shape[1]),
+                        bool(getattr(x, "has_sorted_indices", False)))
+        clock("csr_assemble", dev)
+        return out
 
     def forward_strings(self, ids: np.ndarray) -> np.ndarray:
         """Route a per-row string column (e.g. entity ids): per-row codes into this rank's table of distinct

@@ -30,6 +30,15 @@ def main():
     ap.add_argument("--keep", action="store_true", help="keep the generated files")
     ap.add_argument("--out", default=None, help="JSON record path")
     args = ap.parse_args()
+    import threading
+    t_start = time.perf_counter()
+    done = threading.Event()
+
+    def heartbeat():   # long stages print nothing themselves: a line every 30 s shows the run is alive
+        while not done.wait(30.0):
+            print(f"  ... {time.perf_counter() - t_start:.0f}s, peak RSS "
+                  f"{resource.getrusage(resource.RUSAGE_SELF).ru_maxrss / 2**20:.1f} GiB", flush=True)
+    threading.Thread(target=heartbeat, daemon=True).start()
     from photon_ml_amd.io.avro import native
     from photon_ml_amd.io.data_reader import AvroDataReader, FeatureShardConfiguration
     os.makedirs(args.dir, exist_ok=True)
@@ -70,6 +79,7 @@ def main():
     if args.out:
         with open(args.out, "w") as f:
             json.dump(rec, f, indent=1)
+    done.set()
     if not args.keep:
         for p in paths:
             os.remove(p)
