@@ -5,7 +5,9 @@ Reference:
     ``name\\u0001term`` keys of each feature shard's bags (+ the intercept when the shard has one), partition them
     and write one PalDB store per (shard, partition) under the output directory.
     Here: one memory-mapped hash-table store per partition built by the native ``io/csrc/index_map.cpp``
-    (:func:`photon_ml_amd.io.index_map.build_offheap_index_map`), loaded with ``OffHeapIndexMap``.
+    (:func:`photon_ml_amd.io.index_map.build_offheap_index_map`), loaded with ``OffHeapIndexMap``; or, with
+    ``--index-format paldb``, PalDB V1 stores byte-compatible with the reference's
+    (:func:`photon_ml_amd.io.paldb.build_paldb_index_map`, ``FeatureIndexingDriver.scala:262-291``).
   * ``photon-client/.../data/avro/NameAndTermFeatureBagsDriver.scala`` +
     ``NameAndTermFeatureSetContainer.scala`` — write, per feature bag, the set of ``name\\tterm`` lines under
     ``<output>/<bag>`` (read back by ``--feature-bags-directory`` of the GAME drivers).
@@ -30,6 +32,7 @@ from typing import Dict, List, Sequence
 from ..constants import split_feature_key
 from ..io.avro import avro_files, native
 from ..io.index_map import build_offheap_index_map
+from ..io.paldb import build_paldb_index_map
 from ..utils.timing import Timed
 from .game_training import process_output_dir, resolve_paths
 from .params import parse_bool, parse_feature_shard_configuration, split_list
@@ -68,6 +71,9 @@ def build_parser() -> argparse.ArgumentParser:
             s.add_argument("--num-storage-partitions", type=int, default=1)
             s.add_argument("--minimum-input-partitions", type=int, default=1)
             s.add_argument("--feature-shard-configurations", action="append", required=True)
+            s.add_argument("--index-format", default="native", choices=["native", "paldb"],
+                           help="native: this framework's mmap stores; paldb: PalDB V1 stores readable by the "
+                                "reference's PalDBIndexMap (paldb-partition-<shard>-<i>.dat)")
         else:
             s.add_argument("--feature-bags-keys", required=True)
     return p
@@ -89,8 +95,10 @@ def run_indexing(a) -> Dict[str, object]:
     for sid, cfg in shards.items():
         ks = sorted({k for b in cfg.feature_bags for k in keys[b]})
         with Timed(f"Build index map {sid}"):
-            maps[sid] = build_offheap_index_map(ks, a.root_output_directory, sid, a.num_storage_partitions,
-                                                add_intercept=cfg.has_intercept)
+            build = build_paldb_index_map if getattr(a, "index_format", "native") == "paldb" else \
+                build_offheap_index_map
+            maps[sid] = build(ks, a.root_output_directory, sid, a.num_storage_partitions,
+                              add_intercept=cfg.has_intercept)
     return maps
 
 

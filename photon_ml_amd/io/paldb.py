@@ -21,10 +21,18 @@ stores shipped with the reference, e.g. ``GameIntegTest/input/feature-indexes``)
 
 The reader enumerates every slot (no hashing needed) and builds an in-memory two-way map; the loaded map is a
 regular :class:`~photon_ml_amd.io.index_map.IndexMap` (and can be re-stored in the native mmap format with
-``build_offheap_index_map``). Writing PalDB is not supported (the framework writes its own native stores).
+``build_offheap_index_map``).
+
+The writer (:func:`write_store`, :func:`build_paldb_index_map`; reference ``PalDBIndexMapBuilder.scala:27-98``,
+``FeatureIndexingDriver.scala:262-291``) produces stores that PalDB's own reader can query: a key sits in slot
+``(murmur3_32(serialized key, seed 42) & 0x7fffffff) % slots`` or the next free one (linear probing), ``slots =
+round(count / 0.75)`` per key length, each key length's data stream starts with one reserved byte (offset 0 marks
+an empty slot) and a slot is the serialized key plus the varint data offset, padded to the block's widest offset.
+The hash, slot counts and layout are pinned against the reference's shipped stores (``tests/test_paldb.py``).
 """
 from __future__ import annotations
 
+import math
 import mmap
 import os
 import struct
@@ -92,6 +100,132 @@ def _deserialize(buf, pos: int):
             units.append(u)
         return struct.pack(f">{n}H", *units).decode("utf-16-be"), pos
     raise ValueError(f"unsupported PalDB serialization code {code}")
+
+
+def murmur3_32(data: bytes, seed: int = 42) -> int:
+    """MurmurHash3 x86 32-bit (PalDB ``HashUtils``: seed 42, then ``& 0x7fffffff``)."""
+    c1, c2, m = 0xCC9E2D51, 0x1B873593, 0xFFFFFFFF
+    h = seed & m
+    nb = len(data) // 4
+    for (k,) in struct.iter_unpack("<I", data[:4 * nb]):
+        k = (k * c1) & m
+        k = ((k << 15) | (k >> 17)) & m
+        h ^= (k * c2) & m
+        h = ((h << 13) | (h >> 19)) & m
+        h = (h * 5 + 0xE6546B64) & m
+    tail = data[4 * nb:]
+    if tail:
+        k = 0
+        for i, b in enumerate(tail):
+            k |= b << (8 * i)
+        k = (k * c1) & m
+        k = ((k << 15) | (k >> 17)) & m
+        h ^= (k * c2) & m
+    h ^= len(data)
+    h ^= h >> 16
+    h = (h * 0x85EBCA6B) & m
+    h ^= h >> 13
+    h = (h * 0xC2B2AE35) & m
+    return h ^ (h >> 16)
+
+
+def _pack_varint(v: int) -> bytes:
+    """LongPacker.packLong (non-negative)."""
+    out = bytearray()
+    while v >= 0x80:
+        out.append((v & 0x7F) | 0x80)
+        v >>= 7
+    out.append(v)
+    return bytes(out)
+
+
+def _serialize(v) -> bytes:
+    """PalDB StorageSerialization of an int or a string (the only types an index store holds)."""
+    if isinstance(v, (int, np.integer)) and not isinstance(v, bool):
+        v = int(v)
+        if -1 <= v <= 8:
+            return bytes([v + 5])
+        if 0 <= v < 255:                                        # 255 itself is packed (reference stores)
+            return bytes([14, v])
+        return bytes([15]) + _pack_varint(-v) if v < 0 else bytes([16]) + _pack_varint(v)
+    if isinstance(v, str):
+        units = struct.unpack(f">{len(v.encode('utf-16-be')) // 2}H", v.encode("utf-16-be"))
+        return bytes([_STRING]) + _pack_varint(len(units)) + b"".join(_pack_varint(u) for u in units)
+    raise TypeError(f"PalDB index stores hold ints and strings, not {type(v).__name__}")
+
+
+def write_store(path: str, items, timestamp_ms: Optional[int] = None) -> None:
+    """Write ``items`` (iterable of (key, value) pairs; ints / strings; keys distinct) as one PalDB V1 store.
+    Values are laid out per key length in insertion order."""
+    import time as _time
+    blocks: Dict[int, list] = {}
+    for k, v in items:
+        kb, vb = _serialize(k), _serialize(v)
+        blocks.setdefault(len(kb), []).append((kb, vb))
+    lengths = sorted(blocks)
+    meta, index_parts, data_parts = [], [], []
+    index_off = data_off = 0
+    for L in lengths:
+        ents = blocks[L]
+        count = len(ents)
+        slots = int(math.floor(count / 0.75 + 0.5))           # Java Math.round(count / loadFactor)
+        data = bytearray(b"\x00")                             # offset 0 = empty slot
+        offs = []
+        for _, vb in ents:
+            offs.append(len(data))
+            data += _pack_varint(len(vb)) + vb
+        slot_size = L + max(len(_pack_varint(o)) for o in offs)
+        index = bytearray(slots * slot_size)
+        used = bytearray(slots)
+        for (kb, _), o in zip(ents, offs):
+            s = (murmur3_32(kb) & 0x7FFFFFFF) % slots
+            while used[s]:
+                s = (s + 1) % slots
+            used[s] = 1
+            rec = kb + _pack_varint(o)
+            index[s * slot_size:s * slot_size + len(rec)] = rec
+        meta.append((L, count, slots, slot_size, index_off, data_off))
+        index_parts.append(bytes(index))
+        data_parts.append(bytes(data))
+        index_off += len(index)
+        data_off += len(data)
+    magic = MAGIC.encode("utf-8")
+    head = bytearray(struct.pack(">H", len(magic)) + magic)
+    head += struct.pack(">q", int(_time.time() * 1000) if timestamp_ms is None else int(timestamp_ms))
+    head += struct.pack(">iii", sum(m[1] for m in meta), len(meta), max(lengths, default=0))
+    for L, count, slots, slot_size, io, do in meta:
+        head += struct.pack(">iiiiiq", L, count, slots, slot_size, io, do)
+    head += struct.pack(">i", 0)                                # no custom serializers
+    index_start = len(head) + 12
+    head += struct.pack(">iq", index_start, index_start + index_off)
+    tmp = path + ".tmp"
+    with open(tmp, "wb") as fh:
+        fh.write(bytes(head))
+        for b in index_parts:
+            fh.write(b)
+        for b in data_parts:
+            fh.write(b)
+    os.replace(tmp, path)
+
+
+def build_paldb_index_map(keys, directory: str, namespace: str, n_partitions: int = 1,
+                          add_intercept: bool = True) -> "PalDBIndexMap":
+    """FeatureIndexingDriver with PalDB output: distinct feature keys hash-partitioned like Spark's
+    ``HashPartitioner`` (:func:`partition_of`), local indices 0.. in sorted key order per partition, one store per
+    partition holding both directions (key -> local index, local index -> key)."""
+    from .index_map import INTERCEPT_KEY
+    keys = list(dict.fromkeys(keys))
+    if add_intercept and INTERCEPT_KEY not in keys:
+        keys.append(INTERCEPT_KEY)
+    os.makedirs(directory, exist_ok=True)
+    parts: List[List[str]] = [[] for _ in range(n_partitions)]
+    for k in keys:
+        parts[partition_of(k, n_partitions)].append(k)
+    for p, ks in enumerate(parts):
+        ks.sort()
+        items = [(k, i) for i, k in enumerate(ks)] + [(i, k) for i, k in enumerate(ks)]
+        write_store(store_file(directory, namespace, p), items)
+    return PalDBIndexMap(directory, namespace, n_partitions)
 
 
 def read_store(path: str) -> Dict[object, object]:
