@@ -221,6 +221,8 @@ def main():
             "transpose_passes_per_step": kpass[1] / args.steps,
             "optimizer_stalled": stalled,
         }
+        from photon_ml_amd.ops.native import check_lds_add_order
+        out["lds_add_order"] = check_lds_add_order(dev)     # determinism premise, verified on this device
         if args.rehearsal:
             out["rehearsal"] = True
         if game is not None:

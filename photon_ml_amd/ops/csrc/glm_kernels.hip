@@ -2744,6 +2744,24 @@ __global__ __launch_bounds__(256) void lincomb_dev_kernel(VecSet vs, int k, long
   }
 }
 
+// ------------------------------------------------------------------------------------------------------------
+// Determinism probe for the one ISA-unpinned assumption above: the order in which the LDS applies the lanes of ONE
+// ds_add_f64 instruction that all hit the same address. Trial t: the 64 lanes of a wave add v[t][lane] (values of
+// widely spread magnitudes, so the rounded sum depends on the order) into one LDS double. The host compares the
+// results with the lane-ascending sequential sum (ops.native.check_lds_add_order), once per process.
+__global__ __launch_bounds__(64) void lds_add_order_probe_kernel(const double* __restrict__ v, double* __restrict__ out,
+                                                                 int trials) {
+  __shared__ double cell;
+  for (int t = 0; t < trials; ++t) {
+    if (threadIdx.x == 0) cell = 0.0;
+    __syncthreads();
+    atomicAdd(&cell, v[t * 64 + threadIdx.x]);
+    __syncthreads();
+    if (threadIdx.x == 0) out[t] = cell;
+    __syncthreads();
+  }
+}
+
 extern "C" {
 
 // H g (negate: -H g) for a k-deep history (newest last): rho[j] = 1/s_j.y_j and gamma = s.y/y.y of the newest
@@ -3157,6 +3175,13 @@ int pml_tl_fwd_multi(int prec, const TLFwdMultiDesc* c, const void* x, int mode,
                           (float*)coef, (float*)dzz, z_out, with_offset, 0, 0, g_ls_z0, g_ls_t0, g_ls_tpend};
   if (prec == 1) return tl_fwd_multi_impl<float, float, float>(c, x, a, stats, st);
   return tl_fwd_multi_impl<uint16_t, float, float>(c, x, a, stats, st);
+}
+
+int pml_lds_add_order_probe(const double* v, double* out, int trials, hipStream_t st) {
+  if (trials <= 0) return -22;
+  hipLaunchKernelGGL(lds_add_order_probe_kernel, dim3(1), dim3(64), 0, st, v, out, trials);
+  LAUNCH_CHECK();
+  return 0;
 }
 
 }  // extern "C"

@@ -12,6 +12,7 @@ import os
 from pathlib import Path
 from typing import Optional
 
+import numpy as np
 import torch  # noqa: F401  (must precede loading the HIP libraries)
 
 from .build import build_hip, lib_path
@@ -107,6 +108,8 @@ def glm_lib() -> Optional[ctypes.CDLL]:
         lib.pml_seg_t.argtypes = [c_int, ctypes.POINTER(SegChunkDesc), c_void_p, c_int, c_void_p, c_void_p,
                                   c_void_p]
         lib.pml_reduce_stats.argtypes = [c_void_p, c_int, c_void_p, c_int, c_void_p, c_void_p]
+        lib.pml_lds_add_order_probe.argtypes = [c_void_p, c_void_p, c_int, c_void_p]
+        lib.pml_lds_add_order_probe.restype = c_int
         lib.pml_tl_fwd.argtypes = [c_int, ctypes.POINTER(TLFwdDesc), c_void_p, c_int, c_int, c_double, c_void_p,
                                    c_void_p, c_void_p, c_void_p, c_void_p, c_void_p, c_int, c_void_p, c_void_p]
         lib.pml_tl_t.argtypes = [c_int, ctypes.POINTER(TLTDesc), c_void_p, c_int, c_void_p, c_void_p, c_void_p]
@@ -633,6 +636,49 @@ def downsample_weights(y: torch.Tensor, w0: torch.Tensor, rate: float, binary: b
                              None if rowid is None else rowid.data_ptr(), y.numel(), seed & 0xFFFFFFFFFFFFFFFF,
                              float(rate), int(binary), out.data_ptr(), stream_handle(y.device)), "downsample")
     return out
+
+
+_LDS_ORDER: dict = {}
+
+
+def check_lds_add_order(device=None, trials: int = 512) -> dict:
+    """Verify on ``device`` (once per process and device) the one ordering the bitwise determinism of the
+    LDS-accumulating kernels rests on (glm_kernels.hip TL kernels, re_kernels.hip row passes): the lanes of one
+    ds_add_f64 that hit the same address are applied in ascending lane order. ``trials`` waves add 64 values of
+    spread magnitudes (the rounded sum depends on the order) into one LDS cell; the results are compared with the
+    sequential lane-order sums and with a second run. Returns ``{"lane_order": bool, "repeatable": bool,
+    "mismatches": int}``; ``PML_REQUIRE_DETERMINISM=1`` turns a failure into an error, otherwise it is logged
+    once (results stay correct to rounding, but run-to-run bitwise equality is no longer guaranteed)."""
+    dev = torch.device(device) if device is not None else torch.device("cuda", torch.cuda.current_device())
+    key = str(dev)
+    if key in _LDS_ORDER:
+        return _LDS_ORDER[key]
+    lib = glm_lib()
+    if lib is None:
+        raise RuntimeError(f"native GLM kernel library missing ({lib_path('hip', 'glm')})")
+    rng = np.random.default_rng(20261017)
+    v = rng.standard_normal((trials, 64)) * np.exp2(rng.integers(-30, 31, (trials, 64)))
+    ref = np.zeros(trials)
+    for lane in range(64):                      # sequential, lane-ascending fp64 sums
+        ref = ref + v[:, lane]
+    vt = torch.from_numpy(v).to(dev)
+    outs = []
+    for _ in range(2):
+        o = torch.empty(trials, dtype=torch.float64, device=dev)
+        check(lib.pml_lds_add_order_probe(vt.data_ptr(), o.data_ptr(), int(trials), stream_handle(dev)),
+              "lds_add_order_probe")
+        outs.append(o.cpu().numpy())
+    mism = int((outs[0] != ref).sum())
+    res = {"lane_order": mism == 0, "repeatable": bool((outs[0] == outs[1]).all()), "mismatches": mism}
+    _LDS_ORDER[key] = res
+    if not (res["lane_order"] and res["repeatable"]):
+        msg = (f"LDS same-address ds_add_f64 order check failed on {dev}: {res} — kernel results stay correct to "
+               f"rounding, run-to-run bitwise equality is not guaranteed on this device")
+        if os.environ.get("PML_REQUIRE_DETERMINISM", "0") == "1":
+            raise RuntimeError(msg)
+        import logging
+        logging.getLogger(__name__).warning(msg)
+    return res
 
 
 def re_lib() -> Optional[ctypes.CDLL]:

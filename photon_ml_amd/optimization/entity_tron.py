@@ -82,6 +82,9 @@ class EntityTronBatch:
         self.ents = torch.nonzero(sel).squeeze(1)
         self.B = int(self.ents.numel())
         self.W: Optional[torch.Tensor] = None          # last solution (warm start of the next solve)
+        if dev.type == "cuda":
+            from ..ops.native import check_lds_add_order
+            check_lds_add_order(dev)                   # row passes accumulate with same-address ds_add_f64
         if self.B == 0:
             return
         nip, pos, val, row_sel, col_sel, _ = ds.entity_csr(sel)

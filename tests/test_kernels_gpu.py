@@ -849,3 +849,13 @@ def test_loss_evaluator_fused_kernel(name):
     v_dev, v_host = dev.evaluate(torch.from_numpy(s).cuda()), host.evaluate(torch.from_numpy(s))
     assert abs(v_dev - v_host) <= 1e-11 * abs(v_host)
     assert loss_sum(dev.loss.loss_id, torch.from_numpy(s + off).cuda(), dev.labels, dev.weights) is not None
+
+
+@pytest.mark.gpu
+def test_lds_same_address_add_order_is_lane_order():
+    """The determinism premise of the LDS-accumulating kernels: lanes of ONE ds_add_f64 on one address are applied
+    in ascending lane order, every time (probe kernel vs sequential host sums, 512 order-sensitive trials x 2)."""
+    from photon_ml_amd.ops.native import check_lds_add_order
+    res = check_lds_add_order(torch.device("cuda", 0))
+    assert res["repeatable"], res
+    assert res["lane_order"], res
