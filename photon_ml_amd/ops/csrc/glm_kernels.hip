@@ -1710,6 +1710,36 @@ __global__ __launch_bounds__(NTHREADS) void bgemv_kernel(int B, int n, const dou
   if (on) y[(b0 + g) * n + i] = acc;
 }
 
+// 64 < n <= 192: one wave per problem straight from global memory (the block no longer fits a wave's LDS share);
+// lane i owns rows i, i + 64, i + 128. x is staged in LDS (broadcast reads); A^T reads are coalesced over lanes,
+// A reads walk each row (successive j hit the same cache lines: L1 hits).
+__global__ __launch_bounds__(256) void bgemv_wide_kernel(int B, int n, const double* __restrict__ A,
+                                                         const double* __restrict__ x, double* __restrict__ y,
+                                                         int trans) {
+  __shared__ double sx[4][192];
+  const int lane = threadIdx.x & 63, w = threadIdx.x >> 6;
+  const long long b = (long long)blockIdx.x * 4 + w;
+  if (b >= B) return;
+  const double* Ab = A + b * n * n;
+  for (int j = lane; j < n; j += 64) sx[w][j] = x[b * n + j];
+  __builtin_amdgcn_s_waitcnt(0);
+  __builtin_amdgcn_wave_barrier();
+  double acc[3] = {0.0, 0.0, 0.0};
+  for (int j = 0; j < n; ++j) {
+    const double xj = sx[w][j];
+#pragma unroll
+    for (int r = 0; r < 3; ++r) {
+      const int i = lane + 64 * r;
+      if (i < n) acc[r] = fma(trans ? Ab[(long long)j * n + i] : Ab[(long long)i * n + j], xj, acc[r]);
+    }
+  }
+#pragma unroll
+  for (int r = 0; r < 3; ++r) {
+    const int i = lane + 64 * r;
+    if (i < n) y[b * n + i] = acc[r];
+  }
+}
+
 // out = A^T (dw .* (A v)) + l2 v  (Hessian-vector product of the batched dense GLM, one read of each block)
 __global__ __launch_bounds__(NTHREADS) void bhv_kernel(int B, int n, const double* __restrict__ A,
                                                         const double* __restrict__ dw, const double* __restrict__ v,
@@ -3053,7 +3083,13 @@ int pml_lincomb(const double* const* ptrs, const double* coefs, int k, long long
 
 int pml_bgemv(int B, int n, const double* A, const double* x, double* y, int trans, void* stream) {
   if (B <= 0) return 0;
-  if (n < 1 || n > 64) return -22;
+  if (n < 1 || n > 192) return -22;
+  if (n > 64) {
+    hipLaunchKernelGGL(bgemv_wide_kernel, dim3((unsigned)((B + 3) / 4)), dim3(256), 0, (hipStream_t)stream, B, n, A,
+                       x, y, trans);
+    LAUNCH_CHECK();
+    return 0;
+  }
   const long long waves = (B + (64 / n) - 1) / (64 / n);
   const size_t wave_lds = (size_t)(64 / n) * n * (n + 1) * sizeof(double);
   const int nw = (int)std::max<size_t>(1, std::min<size_t>(4, 65536 / wave_lds));  // <= 64 KB LDS per workgroup

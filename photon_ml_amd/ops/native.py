@@ -384,9 +384,10 @@ def two_loop_gram(s, y, g, negate: bool = False):
 
 
 def batched_gemv(A: torch.Tensor, x: torch.Tensor, trans: bool = False) -> torch.Tensor:
-    """``y[b] = A[b] x[b]`` (or ``A[b]^T x[b]``) for a batch of small square fp64 matrices (n <= 64):
-    ``bgemv_kernel`` on the device, ``bmm`` on the host."""
-    if A.device.type != "cuda" or A.shape[-1] > 64 or A.shape[-1] != A.shape[-2]:
+    """``y[b] = A[b] x[b]`` (or ``A[b]^T x[b]``) for a batch of small square fp64 matrices (n <= 192):
+    ``bgemv_kernel`` (n <= 64, blocks staged in LDS) / ``bgemv_wide_kernel`` on the device, ``bmm`` on the host
+    (and beyond 192: the library GEMM, whose first call in a process pays ~50 ms of kernel loading)."""
+    if A.device.type != "cuda" or A.shape[-1] > 192 or A.shape[-1] != A.shape[-2]:
         M = A.transpose(1, 2) if trans else A
         return torch.bmm(M, x.unsqueeze(-1)).squeeze(-1)
     lib = require_glm_lib()

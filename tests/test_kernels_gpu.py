@@ -323,9 +323,10 @@ def test_seg_expand_kernel():
 
 
 @pytest.mark.gpu
-@pytest.mark.parametrize("n", [1, 5, 20, 32, 64])
+@pytest.mark.parametrize("n", [1, 5, 20, 32, 64, 65, 130, 192])
 def test_batched_small_gemv_and_hv_match_torch(n):
-    """bgemv_kernel / bhv_kernel (row-space random-effect solve) vs fp64 torch bmm references."""
+    """bgemv_kernel / bgemv_wide_kernel (n > 64) / bhv_kernel (row-space random-effect solve) vs fp64 torch bmm
+    references."""
     from photon_ml_amd.ops.native import batched_gemv, batched_hv
     g = torch.Generator(device="cuda").manual_seed(n)
     B = 1003
