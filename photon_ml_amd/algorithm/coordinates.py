@@ -523,16 +523,29 @@ class RandomEffectCoordinate(Coordinate):
         z = torch.zeros(seg.y.numel(), dtype=torch.float64, device=dev)     # x.w per row (segmented order)
         sum_sq = torch.zeros((), dtype=torch.float64, device=dev)
         parts = {}
-        if rs is not None:
+
+        def run_rs():
             with Timed(f"RE {self.coordinate_id}: row-space solve", log, logging.DEBUG):
                 rres = rs.solve(self.loss, l2, "TRON", W0, oc.tolerance, oc.maximum_iterations,
                                 reuse_beta=not foreign)
                 _sync(rres.W)
-            iters.index_copy_(0, rs.ents, rres.iters)
-            reasons.index_copy_(0, rs.ents, rres.reason)
-            z += rs.margins(rres.W)
-            sum_sq += torch.where(rs.valid, rres.W, torch.zeros_like(rres.W)).square().sum()
-            parts["rs"] = rres.W
+            return (rres, rs.margins(rres.W),
+                    torch.where(rs.valid, rres.W, torch.zeros_like(rres.W)).square().sum())
+
+        # the row-space and fused solves touch disjoint entities: with both present the row-space kernels run on a
+        # side stream, concurrently with the fused launch (they fill its tail and its host-side gaps)
+        overlap = (rs is not None and fused is not None and dev.type == "cuda"
+                   and os.environ.get("PML_RE_OVERLAP", "1") != "0")
+        rs_out = None
+        if rs is not None and not overlap:
+            rs_out = run_rs()
+        main = side = None
+        if overlap:
+            main = torch.cuda.current_stream(dev)
+            if getattr(self, "_side_stream", None) is None:
+                self._side_stream = torch.cuda.Stream(dev)
+            side = self._side_stream
+            side.wait_stream(main)                 # offsets / warm starts written on the main stream
         if fused is not None:
             with Timed(f"RE {self.coordinate_id}: fused primal solve", log, logging.DEBUG):
                 fres = fused.solve(self.loss, l2, None if W0 is None else W0[fused.cols], seg.o[fused.rows],
@@ -540,6 +553,11 @@ class RandomEffectCoordinate(Coordinate):
                 _sync(fres.W)
             iters.index_copy_(0, fused.ents, fres.iters)
             reasons.index_copy_(0, fused.ents, fres.reason)
+            if overlap:
+                with torch.cuda.stream(side):
+                    rs_out = run_rs()
+                for t in (rs_out[0].W, rs_out[0].iters, rs_out[0].reason, rs_out[1], rs_out[2]):
+                    t.record_stream(main)
             z.index_copy_(0, fused.rows, fres.z)
             sum_sq += fres.W.square().sum()
             parts["fused"] = fres.W
@@ -561,6 +579,15 @@ class RandomEffectCoordinate(Coordinate):
             z.index_copy_(0, sub.rows, sub.seg.glm.matvec(res.W))
             sum_sq += res.W.square().sum()
             parts["sub"] = res.W
+        if rs_out is not None:
+            if overlap:
+                main.wait_stream(side)
+            rres, z_rs, ss_rs = rs_out
+            iters.index_copy_(0, rs.ents, rres.iters)
+            reasons.index_copy_(0, rs.ents, rres.reason)
+            z += z_rs
+            sum_sq += ss_rs
+            parts["rs"] = rres.W
         del W0
 
         def primal(parts=parts):

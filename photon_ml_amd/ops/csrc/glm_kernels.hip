@@ -1824,7 +1824,8 @@ template <int V>
 __global__ __launch_bounds__(NTHREADS) void rs_tron_kernel(
     int B, int n, int G, const double* __restrict__ Lm, const double* __restrict__ Y, const double* __restrict__ O,
     const double* __restrict__ WT, double* __restrict__ Beta, double* __restrict__ Fout, int* __restrict__ Iters,
-    int* __restrict__ Reason, int loss, double l2, double tol, int max_iter, int max_fail, int max_cg) {
+    int* __restrict__ Reason, int loss, double l2, double tol, int max_iter, int max_fail, int max_cg,
+    double* __restrict__ Zout) {
   extern __shared__ double smem[];
   const int lane = threadIdx.x & 63, w = threadIdx.x >> 6;
   const int per = 64 / G, np = n * (n + 1) / 2;    // packed lower triangle per problem
@@ -1999,6 +2000,10 @@ __global__ __launch_bounds__(NTHREADS) void rs_tron_kernel(
   }
   if (on) Beta[o] = W;
   if (prob_on && i == 0) { Fout[b] = f; Iters[b] = it; Reason[b] = reason; }
+  if (Zout != nullptr) {
+    const double z = mv(W);       // the solution's margins L beta while L is still in LDS (no re-read of L)
+    if (on) Zout[o] = z;
+  }
 }
 
 // ============================================================================================================
@@ -3156,15 +3161,14 @@ int pml_rs_tron(int B, int n, const double* L, const double* y, const double* of
   const long long grid = (waves + nw - 1) / nw;
   if (V >= 2)
     hipLaunchKernelGGL(rs_tron_kernel<2>, dim3((unsigned)grid), dim3(nw * 64), nw * wave_lds, (hipStream_t)stream, B,
-                       n, G, L, y, off, wt, beta, f, iters, reason, loss, l2, tol, max_iter, max_fail, max_cg);
+                       n, G, L, y, off, wt, beta, f, iters, reason, loss, l2, tol, max_iter, max_fail, max_cg, zout);
   else if (V == 1)
     hipLaunchKernelGGL(rs_tron_kernel<1>, dim3((unsigned)grid), dim3(nw * 64), nw * wave_lds, (hipStream_t)stream, B,
-                       n, G, L, y, off, wt, beta, f, iters, reason, loss, l2, tol, max_iter, max_fail, max_cg);
+                       n, G, L, y, off, wt, beta, f, iters, reason, loss, l2, tol, max_iter, max_fail, max_cg, zout);
   else
     hipLaunchKernelGGL(rs_tron_kernel<0>, dim3((unsigned)grid), dim3(nw * 64), nw * wave_lds, (hipStream_t)stream, B,
-                       n, G, L, y, off, wt, beta, f, iters, reason, loss, l2, tol, max_iter, max_fail, max_cg);
+                       n, G, L, y, off, wt, beta, f, iters, reason, loss, l2, tol, max_iter, max_fail, max_cg, zout);
   LAUNCH_CHECK();
-  if (zout) return pml_bgemv(B, n, L, beta, zout, 0, stream);   // these variants keep no L at exit
   return 0;
 }
 
