@@ -323,6 +323,41 @@ __global__ __launch_bounds__(64) void seg_gram_kernel(int B, int n, const long l
     for (int j = lane; j < n; j += 64) Kb[(long long)j * n + i] = 0.0;
 }
 
+// Row-space back-map w_e = X_e^T r_e for the entities ents[B] (random-effect model materialisation,
+// optimization/row_space.py to_primal): one wave per entity, the entity's projected columns accumulated in LDS
+// (d_e doubles), rows in order and the entries of one row on distinct lanes with distinct columns, so every LDS
+// address is updated in a fixed order (deterministic) and no two lanes of one instruction collide. Reads only the
+// handled entities' rows (the shard-wide transpose pass read every entity's).
+__global__ __launch_bounds__(64) void rs_primal_kernel(const long long* __restrict__ ents,
+                                                       const long long* __restrict__ row_ptr,
+                                                       const long long* __restrict__ col_ptr,
+                                                       const long long* __restrict__ nip,
+                                                       const long long* __restrict__ pos,
+                                                       const double* __restrict__ val, const double* __restrict__ r,
+                                                       double* __restrict__ W) {
+  extern __shared__ double acc[];
+  const int lane = threadIdx.x;
+  const long long e = ents[blockIdx.x];
+  const long long r0 = row_ptr[e], r1 = row_ptr[e + 1], c0 = col_ptr[e];
+  const int d = (int)(col_ptr[e + 1] - c0);
+  for (int j = lane; j < d; j += 64) acc[j] = 0.0;
+  __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
+  __builtin_amdgcn_wave_barrier();
+  __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
+  for (long long i = r0; i < r1; ++i) {
+    const double a = r[i];
+    const long long k0 = nip[i], k1 = nip[i + 1];
+    for (long long k = k0 + lane; k < k1; k += 64) {
+      const int c = (int)(pos[k] - c0);
+      acc[c] += a * val[k];
+    }
+    __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
+    __builtin_amdgcn_wave_barrier();
+    __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
+  }
+  for (int j = lane; j < d; j += 64) W[c0 + j] = acc[j];
+}
+
 extern "C" {
 
 int pml_downsample(int f64, const void* y, const void* w0, const long long* rowid, long long n,
@@ -405,6 +440,19 @@ int pml_seg_gram(int B, int n, int dmax, const long long* ents, const long long*
   if (n < 1 || n > 192 || dmax < 0 || (size_t)dmax * sizeof(double) > 160 * 1024) return -22;
   hipLaunchKernelGGL(seg_gram_kernel, dim3((unsigned)B), dim3(64), (size_t)std::max(dmax, 1) * sizeof(double),
                      (hipStream_t)stream, B, n, ents, row_ptr, col_ptr, nip, pos, val, K);
+  LAUNCH_CHECK();
+  return 0;
+}
+
+// W (packed projected coefficients) of the entities ents[B] = X_e^T r over their rows; dmax = max projected columns
+// of those entities (LDS per wave). Other entities' coefficients are left untouched.
+int pml_rs_primal(int B, int dmax, const long long* ents, const long long* row_ptr, const long long* col_ptr,
+                  const long long* nip, const long long* pos, const double* val, const double* r, double* W,
+                  void* stream) {
+  if (B <= 0) return 0;
+  if (dmax < 0 || (size_t)dmax * sizeof(double) > 64 * 1024) return -22;
+  hipLaunchKernelGGL(rs_primal_kernel, dim3((unsigned)B), dim3(64), (size_t)std::max(dmax, 1) * sizeof(double),
+                     (hipStream_t)stream, ents, row_ptr, col_ptr, nip, pos, val, r, W);
   LAUNCH_CHECK();
   return 0;
 }

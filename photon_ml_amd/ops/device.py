@@ -162,8 +162,9 @@ class DeviceGLMData(GLMComputable):
                  dim: int, precision: str = "f64", device="cuda", old_of_new: Optional[torch.Tensor] = None):
         self.lib = require_glm_lib()
         self.device = torch.device(device)
-        from .native import check_lds_add_order
-        self.lds_add_order = check_lds_add_order(self.device)   # the kernels' bitwise determinism (once per process)
+        if self.device.type == "cuda":
+            from .native import check_lds_add_order
+            check_lds_add_order(self.device)       # the kernels' bitwise determinism premise (once per process)
         self.prec = PRECISIONS[precision]
         self.precision = precision
         self.vdt = VEC_DTYPE[self.prec]

@@ -528,6 +528,8 @@ def game_lib() -> Optional[ctypes.CDLL]:
         lib.pml_downsample.argtypes = [c_int, c_void_p, c_void_p, c_void_p, ctypes.c_longlong, ctypes.c_ulonglong,
                                        c_double, c_int, c_void_p, c_void_p]
         lib.pml_seg_gram.argtypes = [c_int, c_int, c_int] + [c_void_p] * 8
+        lib.pml_rs_primal.argtypes = [c_int, c_int] + [c_void_p] * 9
+        lib.pml_rs_primal.restype = c_int
         lib.pml_tl_compact.argtypes = [c_int, c_int, ctypes.POINTER(CmpArgs), c_void_p]
         lib.pml_tl_compact.restype = c_int
         for f in ("pml_score_rows", "pml_gemm_nt", "pml_spmm_rows", "pml_downsample"):
@@ -625,6 +627,33 @@ def seg_gram(ents: torch.Tensor, n: int, row_ptr: torch.Tensor, col_ptr: torch.T
     return K
 
 
+RS_PRIMAL_DMAX = 64 * 1024 // 8     # rs_primal_kernel: one fp64 LDS slot per projected column of the entity
+
+
+def rs_primal(ents: torch.Tensor, row_ptr, col_ptr, nip, pos, val, r: torch.Tensor, W: torch.Tensor) -> None:
+    """``W[col_ptr[e]:col_ptr[e+1]] = X_e^T r[rows of e]`` for the entities ``ents`` (int64) of a block-diagonal
+    CSR (``nip``/``pos``/``val``: int64 indptr, int64 global columns, fp64 values; columns of an entity inside
+    its ``col_ptr`` range, distinct inside a row) — ``rs_primal_kernel``, one wave per entity. In place on ``W``
+    (fp64, packed like ``col_ptr``); every entity needs ``d_e <= RS_PRIMAL_DMAX``. Device only."""
+    lib = require_game_lib()
+    dev = W.device
+    B = int(ents.numel())
+    if B == 0:
+        return
+    t = [x.to(dev).contiguous() for x in (ents, row_ptr, col_ptr, nip, pos)]
+    for x in t:
+        assert x.dtype == torch.int64
+    v = val.to(dev, torch.float64).contiguous()
+    assert r.dtype == torch.float64 and r.is_contiguous() and W.dtype == torch.float64 and W.is_contiguous()
+    assert r.numel() >= int(row_ptr[-1]) and W.numel() >= int(col_ptr[-1])
+    dmax = int((col_ptr[ents + 1] - col_ptr[ents]).max())
+    if dmax > RS_PRIMAL_DMAX:
+        raise ValueError(f"rs_primal: an entity has {dmax} > {RS_PRIMAL_DMAX} projected columns")
+    check(lib.pml_rs_primal(B, dmax, t[0].data_ptr(), t[1].data_ptr(), t[2].data_ptr(), t[3].data_ptr(),
+                            t[4].data_ptr(), v.data_ptr(), r.data_ptr(), W.data_ptr(), stream_handle(dev)),
+          "rs_primal")
+
+
 def downsample_weights(y: torch.Tensor, w0: torch.Tensor, rate: float, binary: bool, seed: int,
                        rowid: Optional[torch.Tensor] = None, out: Optional[torch.Tensor] = None) -> torch.Tensor:
     """K20 weight rewrite on the device (``downsample_kernel``); ``rowid`` = global row ids (int64) of the rows."""
@@ -651,6 +680,8 @@ def check_lds_add_order(device=None, trials: int = 512) -> dict:
     "mismatches": int}``; ``PML_REQUIRE_DETERMINISM=1`` turns a failure into an error, otherwise it is logged
     once (results stay correct to rounding, but run-to-run bitwise equality is no longer guaranteed)."""
     dev = torch.device(device) if device is not None else torch.device("cuda", torch.cuda.current_device())
+    if dev.type != "cuda":
+        return {"skipped": "not a GPU device"}
     key = str(dev)
     if key in _LDS_ORDER:
         return _LDS_ORDER[key]

@@ -168,6 +168,7 @@ class RowSpaceBatch:
                                torch.full_like(valid, -1, dtype=torch.long))
             geo.append((e, n, valid, rows, torch.zeros(e.numel(), n, n, dtype=torch.float64, device=dev)))
         csr = _canonical_csr(csr, dev) if dev.type == "cuda" else None
+        self._csr = csr                     # the per-entity back-map kernel reads it (to_primal)
         # (class, members) whose Gram columns come from indicator passes: all of them without a canonical device
         # CSR, else only the entities too wide for seg_gram_kernel's LDS image (d_e > SEG_GRAM_DMAX)
         need_ind = []
@@ -262,8 +263,20 @@ class RowSpaceBatch:
         if self.classes:
             alpha = torch.cat([_bmv(c.Linv, c.view(beta), trans=True).reshape(-1) for c in self.classes])  # L^-T b
             r[self.vrow] = alpha[self.vslot]
-        # (an entity-masked pass skipping the other entities' column tiles measured slower here: the masked path
-        # keeps per-chunk launches, 10.1 vs 9.0 ms on game5pl, plus a one-time mask geometry build in the window)
+        csr = getattr(self, "_csr", None)
+        if csr is not None and self.classes:
+            # per-entity back-map over the handled entities' rows only (rs_primal_kernel, one wave per entity);
+            # the shard-wide transpose pass read every entity's rows (9.0 ms on game5pl)
+            from ..ops.native import RS_PRIMAL_DMAX, rs_primal
+            seg = self.seg
+            if getattr(self, "_primal_ents", None) is None:
+                d_e = seg.col_ptr[self.ents + 1] - seg.col_ptr[self.ents]
+                self._primal_ents = (self.ents[d_e <= RS_PRIMAL_DMAX].contiguous(), bool((d_e > RS_PRIMAL_DMAX).any()))
+            ents, wide = self._primal_ents
+            if not wide:
+                W = torch.zeros(int(seg.col_ptr[-1]), dtype=torch.float64, device=beta.device)
+                rs_primal(ents, seg.row_ptr, seg.col_ptr, csr[0], csr[1], csr[2], r, W)
+                return W
         return self.seg.glm.rmatvec(r, build_multi=False)     # once per update: no shard-wide tables
 
     def margins(self, beta: torch.Tensor) -> torch.Tensor:
