@@ -453,11 +453,18 @@ __global__ __launch_bounds__(RE_THREADS) void re_tron_csr_kernel(ReTronArgs a) {
 // per SIMD): small and mid entities are latency-bound (a pass is a few dependent batches), so more entities in
 // flight per CU is more streaming throughput.
 // Measured on 43K game5pl-like entities (scripts/re_fused_bench.py, profiles/re_lean_ab_r4.md): 3 waves per SIMD
-// (<= 168 VGPRs, 12 waves per CU) with one row group per batch in function evaluations and three in Hessian-vector
-// passes; 4 waves per SIMD spills in the row loop (80 ms vs 61 ms for re_tron_csr_kernel)
+// (<= 168 VGPRs, 12 waves per CU) with two row groups per batch in function evaluations (one: same total, the 64
+// largest entities 33.6 instead of 28.1 ms) and three in Hessian-vector passes (four: +15 %); 4 waves per SIMD
+// spills in the row loop (80 ms vs 61 ms for re_tron_csr_kernel)
+#ifndef LEAN_WPE                 // (guarded: the A/B scripts build variants with -D)
 #define LEAN_WPE 3
-#define LEAN_UF 1
+#endif
+#ifndef LEAN_UF
+#define LEAN_UF 2
+#endif
+#ifndef LEAN_UH
 #define LEAN_UH 3
+#endif
 template <int LOSS, int J>
 __global__ __launch_bounds__(RE_THREADS) __attribute__((amdgpu_waves_per_eu(LEAN_WPE, LEAN_WPE)))
 void re_tron_lean_kernel(ReTronArgs a) {

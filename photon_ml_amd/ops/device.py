@@ -625,7 +625,8 @@ class DeviceGLMData(GLMComputable):
                     self.track_hessian and loss.twice_differentiable):
                 out[self.dim] = self._ls_t0_dev[0]
                 if need_s:
-                    out[self.dim + 1] = self.coef[: self.n_rows].to(torch.float64).sum()
+                    # one fp64-accumulating reduction over the stored coefficients (no fp64 copy of the row vector)
+                    torch.sum(self.coef[: self.n_rows], dim=0, dtype=torch.float64, out=out[self.dim + 1])
             else:
                 self._ls(loss, t, 1, out[self.dim:])
             self._tpend = float(t)
