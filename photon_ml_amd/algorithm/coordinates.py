@@ -524,10 +524,10 @@ class RandomEffectCoordinate(Coordinate):
         sum_sq = torch.zeros((), dtype=torch.float64, device=dev)
         parts = {}
 
-        def run_rs():
+        def run_rs(prep=None):
             with Timed(f"RE {self.coordinate_id}: row-space solve", log, logging.DEBUG):
                 rres = rs.solve(self.loss, l2, "TRON", W0, oc.tolerance, oc.maximum_iterations,
-                                reuse_beta=not foreign)
+                                reuse_beta=not foreign, prep=prep)
                 _sync(rres.W)
             return (rres, rs.margins(rres.W),
                     torch.where(rs.valid, rres.W, torch.zeros_like(rres.W)).square().sum())
@@ -540,12 +540,18 @@ class RandomEffectCoordinate(Coordinate):
         if rs is not None and not overlap:
             rs_out = run_rs()
         main = side = None
+        rs_prep = None
         if overlap:
+            # the row-space solve's input passes (warm-start copy, per-slot offsets) run here, on the idle device,
+            # before the fused launch takes every CU
+            rs_prep = rs.prepare(W0, reuse_beta=not foreign)
             main = torch.cuda.current_stream(dev)
             if getattr(self, "_side_stream", None) is None:
                 self._side_stream = torch.cuda.Stream(dev)
             side = self._side_stream
             side.wait_stream(main)                 # offsets / warm starts written on the main stream
+            for t in rs_prep:
+                t.record_stream(side)              # allocated on the main stream, read on the side stream
         if fused is not None:
             with Timed(f"RE {self.coordinate_id}: fused primal solve", log, logging.DEBUG):
                 fres = fused.solve(self.loss, l2, None if W0 is None else W0[fused.cols], seg.o[fused.rows],
@@ -555,7 +561,7 @@ class RandomEffectCoordinate(Coordinate):
             reasons.index_copy_(0, fused.ents, fres.reason)
             if overlap:
                 with torch.cuda.stream(side):
-                    rs_out = run_rs()
+                    rs_out = run_rs(rs_prep)
                 for t in (rs_out[0].W, rs_out[0].iters, rs_out[0].reason, rs_out[1], rs_out[2]):
                     t.record_stream(main)
             z.index_copy_(0, fused.rows, fres.z)

@@ -192,8 +192,18 @@ class MarginLineSearch:
         """(x(t), f(x(t)), gradient at x(t)) — one transpose pass. With a backend that keeps the sums on the
         device (``ls_finish_device``) f is a 0-d device tensor: the caller reads it together with its next
         synchronisation (L-BFGS: the history pair's scalars), not right after the transpose pass."""
-        x = self.x0 + t * self.d
         norm = self.obj.normalization
+        fused = getattr(self.data, "ls_finish_fused", None)
+        if (fused is not None and norm.factors is None and norm.shifts is None and self.x0.is_cuda
+                and self.x0.dtype == self.d.dtype == torch.float64 and self.x0.is_contiguous()
+                and self.d.is_contiguous()):
+            # the step, the transpose pass and the gradient epilogue (g + l2 x) with one launch after the pass
+            x, f, grad = fused(self.obj.loss, t, self.x0, self.d, self.obj.l2_weight)
+            self.obj.n_value_grad += 1
+            if self.obj.l2_weight > 0:
+                f = f + 0.5 * self.l2 * (self.a + 2.0 * t * self.b + t * t * self.c)
+            return x, f, grad
+        x = self.x0 + t * self.d
         w_eff, shift = norm.effective(x)
         fin = getattr(self.data, "ls_finish_device", None)
         if fin is not None:

@@ -2780,6 +2780,44 @@ __global__ __launch_bounds__(256) void lincomb_dev_kernel(VecSet vs, int k, long
 }
 
 // ------------------------------------------------------------------------------------------------------------
+// Per-iteration vector epilogues of the GLM line search (one launch each instead of a torch op chain):
+// * perm_cast_kernel: the coefficient vector in the shard's device column order and gather precision,
+//   out[i] = (XT) w[perm[i]] (perm null: a cast) — the input of every forward pass (was an index gather + a cast);
+// * ls_step_grad_kernel: the accepted step x = x0 + t d and the full gradient g = G[perm[i]] + l2 x (perm null:
+//   G[i]), with G the transpose pass's result in device column order (was an index_select, two scaled adds and
+//   two more elementwise kernels). Products and sums are rounded separately (no FMA contraction), so x and g are
+//   bitwise the values of the torch expressions x0 + t * d and g + l2 * x they replace.
+template <typename XT>
+__global__ __launch_bounds__(256) void perm_cast_kernel(const double* __restrict__ w, const long long* __restrict__ perm,
+                                                         long long n, XT* __restrict__ out) {
+  for (long long i = (long long)blockIdx.x * 256 + threadIdx.x; i < n; i += (long long)gridDim.x * 256)
+    out[i] = static_cast<XT>(perm ? w[perm[i]] : w[i]);
+}
+
+// out[i] = src[idx[i]] (0 where idx[i] < 0): packed per-slot values of a per-row vector (row-space batches:
+// padding slots carry index -1) in one pass instead of a clamp, a gather and a select.
+__global__ __launch_bounds__(256) void masked_gather_kernel(const double* __restrict__ src,
+                                                            const long long* __restrict__ idx, long long n,
+                                                            double* __restrict__ out) {
+  for (long long i = (long long)blockIdx.x * 256 + threadIdx.x; i < n; i += (long long)gridDim.x * 256) {
+    const long long j = idx[i];
+    out[i] = j >= 0 ? src[j] : 0.0;
+  }
+}
+
+__global__ __launch_bounds__(256) void ls_step_grad_kernel(const double* __restrict__ x0, const double* __restrict__ d,
+                                                           double t, const double* __restrict__ G,
+                                                           const long long* __restrict__ perm, double l2, long long n,
+                                                           double* __restrict__ x, double* __restrict__ g) {
+  for (long long i = (long long)blockIdx.x * 256 + threadIdx.x; i < n; i += (long long)gridDim.x * 256) {
+    const double xi = __dadd_rn(x0[i], __dmul_rn(t, d[i]));
+    x[i] = xi;
+    const double gi = perm ? G[perm[i]] : G[i];
+    g[i] = l2 != 0.0 ? __dadd_rn(gi, __dmul_rn(l2, xi)) : gi;
+  }
+}
+
+// ------------------------------------------------------------------------------------------------------------
 // Determinism probe for the one ISA-unpinned assumption above: the order in which the LDS applies the lanes of ONE
 // ds_add_f64 instruction that all hit the same address. Trial t: the 64 lanes of a wave add v[t][lane] (values of
 // widely spread magnitudes, so the rounded sum depends on the order) into one LDS double. The host compares the
@@ -2864,6 +2902,37 @@ int pml_lbfgs_pair(const double* x, const double* x0, const double* g, const dou
   const int grid = (int)std::min<long long>(PAIR_GRID, (n + 255) / 256);
   hipLaunchKernelGGL(lbfgs_pair_kernel, dim3(grid), dim3(256), 0, (hipStream_t)stream, x, x0, g, g0, n, s, y, partial,
                      counter, out);
+  LAUNCH_CHECK();
+  return 0;
+}
+
+static int vec_grid(long long n) { return (int)std::min<long long>(8192, (n + 255) / 256); }
+
+// prec: 2 -> fp64 output, else fp32 (the forward pass's gather precision)
+int pml_perm_cast(const double* w, const long long* perm, long long n, int prec, void* out, void* stream) {
+  if (n <= 0) return 0;
+  if (prec == 2)
+    hipLaunchKernelGGL(perm_cast_kernel<double>, dim3(vec_grid(n)), dim3(256), 0, (hipStream_t)stream, w, perm, n,
+                       (double*)out);
+  else
+    hipLaunchKernelGGL(perm_cast_kernel<float>, dim3(vec_grid(n)), dim3(256), 0, (hipStream_t)stream, w, perm, n,
+                       (float*)out);
+  LAUNCH_CHECK();
+  return 0;
+}
+
+int pml_masked_gather(const double* src, const long long* idx, long long n, double* out, void* stream) {
+  if (n <= 0) return 0;
+  hipLaunchKernelGGL(masked_gather_kernel, dim3(vec_grid(n)), dim3(256), 0, (hipStream_t)stream, src, idx, n, out);
+  LAUNCH_CHECK();
+  return 0;
+}
+
+int pml_ls_step_grad(const double* x0, const double* d, double t, const double* G, const long long* perm, double l2,
+                     long long n, double* x, double* g, void* stream) {
+  if (n <= 0) return 0;
+  hipLaunchKernelGGL(ls_step_grad_kernel, dim3(vec_grid(n)), dim3(256), 0, (hipStream_t)stream, x0, d, t, G, perm,
+                     l2, n, x, g);
   LAUNCH_CHECK();
   return 0;
 }

@@ -130,6 +130,13 @@ def glm_lib() -> Optional[ctypes.CDLL]:
         lib.pml_lincomb.argtypes = [c_void_p, c_void_p, c_int, ctypes.c_longlong, c_void_p, c_void_p]
         lib.pml_lbfgs_pair.argtypes = [c_void_p] * 4 + [ctypes.c_longlong] + [c_void_p] * 6
         lib.pml_ls_dots.argtypes = [c_void_p] * 3 + [ctypes.c_longlong] + [c_void_p] * 4
+        lib.pml_perm_cast.argtypes = [c_void_p, c_void_p, ctypes.c_longlong, c_int, c_void_p, c_void_p]
+        lib.pml_perm_cast.restype = c_int
+        lib.pml_ls_step_grad.argtypes = [c_void_p, c_void_p, c_double, c_void_p, c_void_p, c_double,
+                                         ctypes.c_longlong, c_void_p, c_void_p, c_void_p]
+        lib.pml_ls_step_grad.restype = c_int
+        lib.pml_masked_gather.argtypes = [c_void_p, c_void_p, ctypes.c_longlong, c_void_p, c_void_p]
+        lib.pml_masked_gather.restype = c_int
         lib.pml_two_loop_chain.argtypes = [c_int] + [c_void_p] * 5 + [ctypes.c_longlong] + [c_void_p] * 4 + \
             [c_int, c_void_p]
         lib.pml_two_loop_gram.argtypes = [c_int, c_void_p, c_void_p, c_void_p, ctypes.c_longlong, c_void_p, c_void_p,
@@ -320,6 +327,54 @@ def ls_dots(x0, g, d):
     check(lib.pml_ls_dots(x0.data_ptr(), g.data_ptr(), d.data_ptr(), d.numel(), sc[0].data_ptr(), sc[1].data_ptr(),
                           out.data_ptr(), stream_handle(d.device)), "ls_dots")
     return out
+
+
+def perm_cast(w: torch.Tensor, perm: Optional[torch.Tensor], dtype: torch.dtype) -> torch.Tensor:
+    """``w[perm].to(dtype)`` (``perm`` None: ``w.to(dtype)``) in one launch (``perm_cast_kernel``): a forward
+    pass's coefficient input. ``w`` fp64 device vector, ``perm`` int64, ``dtype`` float32 / float64."""
+    assert w.is_cuda and w.dtype == torch.float64 and w.dim() == 1 and w.is_contiguous()
+    assert dtype in (torch.float32, torch.float64)
+    n = w.numel() if perm is None else perm.numel()
+    if perm is not None:
+        assert perm.device == w.device and perm.dtype == torch.int64 and perm.is_contiguous()
+        if os.environ.get("PML_CHECK_KERNEL_INPUTS", "0") == "1" and n:
+            assert 0 <= int(perm.min()) and int(perm.max()) < w.numel(), "perm_cast index out of range"
+    out = torch.empty(n, dtype=dtype, device=w.device)
+    check(require_glm_lib().pml_perm_cast(w.data_ptr(), None if perm is None else perm.data_ptr(), n,
+                                          2 if dtype == torch.float64 else 1, out.data_ptr(), stream_handle(w.device)),
+          "perm_cast")
+    return out
+
+
+def masked_gather(src: torch.Tensor, idx: torch.Tensor) -> torch.Tensor:
+    """``out[i] = src[idx[i]]``, 0 where ``idx[i] < 0`` (``masked_gather_kernel``, one pass). ``src`` fp64 device
+    vector, ``idx`` int64 (values < len(src))."""
+    assert src.is_cuda and src.dtype == torch.float64 and src.is_contiguous()
+    assert idx.device == src.device and idx.dtype == torch.int64 and idx.is_contiguous()
+    if os.environ.get("PML_CHECK_KERNEL_INPUTS", "0") == "1" and idx.numel():
+        assert int(idx.max()) < src.numel(), "masked_gather index out of range"
+    out = torch.empty(idx.shape, dtype=torch.float64, device=src.device)
+    check(require_glm_lib().pml_masked_gather(src.data_ptr(), idx.data_ptr(), idx.numel(), out.data_ptr(),
+                                              stream_handle(src.device)), "masked_gather")
+    return out
+
+
+def ls_step_grad(x0: torch.Tensor, d: torch.Tensor, t: float, G: torch.Tensor, perm: Optional[torch.Tensor],
+                 l2: float):
+    """The accepted line-search step and its full gradient in one launch (``ls_step_grad_kernel``):
+    ``x = x0 + t * d`` and ``g = G[perm] + l2 * x`` (``perm`` None: ``G``), bitwise the torch expressions. All fp64
+    device vectors of one length (``G`` in the data's device column order)."""
+    n = x0.numel()
+    for v in (x0, d, G):
+        assert v.is_cuda and v.dtype == torch.float64 and v.dim() == 1 and v.is_contiguous() and v.device == x0.device
+    assert d.numel() == n and G.numel() >= n
+    if perm is not None:
+        assert perm.device == x0.device and perm.dtype == torch.int64 and perm.numel() == n and perm.is_contiguous()
+    x, g = torch.empty_like(x0), torch.empty_like(x0)
+    check(require_glm_lib().pml_ls_step_grad(x0.data_ptr(), d.data_ptr(), float(t), G.data_ptr(),
+                                             None if perm is None else perm.data_ptr(), float(l2), n, x.data_ptr(),
+                                             g.data_ptr(), stream_handle(x0.device)), "ls_step_grad")
+    return x, g
 
 
 _CHAIN_SCRATCH = {}

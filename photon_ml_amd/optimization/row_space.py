@@ -99,6 +99,7 @@ def row_space_eligible(l1: float, constraints=None) -> bool:
 # memory and in the fused kernel's lane group; per class the kernel uses G = pow2 >= n lanes per problem.
 SIZE_CLASSES = (1, 2, 4, 8, 12, 16, 24, 32, 48, 64, 80, 96, 112, 128, 160, 192)
 ROW_SPACE_NMAX = 192      # rs_tron_big_kernel / seg_gram_kernel limit (one wave per problem, packed L in LDS)
+RS_CLASS_DESC = os.environ.get("PML_RS_CLASS_ORDER", "desc") == "desc"
 RS_BIG_NNZ_RATIO = float(os.environ.get("PML_RS_BIG_NNZ_RATIO", "0.6"))   # n > 64: mean row nnz >= ratio x n
 
 
@@ -248,7 +249,11 @@ class RowSpaceBatch:
             glm._build_multi_t()
 
     def _slots(self, per_row: torch.Tensor) -> torch.Tensor:
-        """Packed per-slot values of a per-row vector (0 in padding slots)."""
+        """Packed per-slot values of a per-row vector (0 in padding slots, whose row index is -1)."""
+        if (per_row.is_cuda and per_row.dtype == torch.float64 and per_row.is_contiguous()
+                and self.rows.device == per_row.device):
+            from ..ops.native import masked_gather
+            return masked_gather(per_row, self.rows)            # one pass
         return torch.where(self.valid, per_row[self.rows.clamp(min=0)],
                            torch.zeros((), dtype=per_row.dtype, device=per_row.device))
 
@@ -290,24 +295,44 @@ class RowSpaceBatch:
         z[self.vrow] = zs[self.vslot]
         return z
 
-    def solve(self, loss, l2: float, optimizer: str, W0: Optional[torch.Tensor], tol: float, max_iter: int,
-              reuse_beta: bool = True) -> BatchedResult:
-        """Solve the handled entities; returns the batched result over the ``B`` row-space problems (``W`` is
-        the packed coefficient vector; ``iters`` / ``reason`` / ``f`` follow ``ents``)."""
-        dev = self.seg.y.device
+    def _warm_beta(self, W0: Optional[torch.Tensor], reuse_beta: bool) -> torch.Tensor:
         if reuse_beta and self.beta is not None:
-            beta0 = self.beta
-        elif W0 is not None and bool((W0 != 0).any()):
-            beta0 = self.beta_from_primal(W0)
-        else:
-            beta0 = torch.zeros(self.size, dtype=torch.float64, device=dev)
-        o = self._slots(self.seg.o)
+            return self.beta
+        if W0 is not None and bool((W0 != 0).any()):
+            return self.beta_from_primal(W0)
+        return torch.zeros(self.size, dtype=torch.float64, device=self.seg.y.device)
+
+    def prepare(self, W0: Optional[torch.Tensor], reuse_beta: bool = True):
+        """The solve's inputs, queued on the CURRENT stream: ``(beta, o)`` = a fresh copy of the warm start (the
+        fused kernels solve in place in it) and the per-slot offsets. Lets a caller that runs :meth:`solve` on a
+        side stream, concurrently with other work, do these passes first on an idle device (under a concurrent
+        fused primal launch they ran on leftover CUs: ~14 ms instead of ~0.5 ms on game5pl)."""
+        return self._warm_beta(W0, reuse_beta).clone(), self._slots(self.seg.o)
+
+    def solve(self, loss, l2: float, optimizer: str, W0: Optional[torch.Tensor], tol: float, max_iter: int,
+              reuse_beta: bool = True, prep=None) -> BatchedResult:
+        """Solve the handled entities; returns the batched result over the ``B`` row-space problems (``W`` is
+        the packed coefficient vector; ``iters`` / ``reason`` / ``f`` follow ``ents``). ``prep``: the result of
+        :meth:`prepare` (then ``W0`` / ``reuse_beta`` are not used)."""
+        dev = self.seg.y.device
         fused = (optimizer == "TRON" and self.seg.y.is_cuda and getattr(loss, "loss_id", -1) in (0, 1, 2)
                  and os.environ.get("PML_RS_FUSED_TRON", "1") != "0")
-        beta = torch.empty_like(beta0)
+        if prep is not None:
+            beta, o = prep              # solved in place: the warm start is already in ``beta``
+            beta0 = beta
+        else:
+            beta0 = self._warm_beta(W0, reuse_beta)
+            o = self._slots(self.seg.o)
+            beta = torch.empty_like(beta0)
         zs = torch.empty_like(beta0) if fused else None
         fs, its, rcs = [], [], []
-        for c in self.classes:
+        res_of = {}
+        # launch order: the widest classes first (fewest problems, longest per-problem chains: the launches that fill
+        # the device worst go where a concurrent fused primal launch fills it, the many-problem classes last)
+        order_c = sorted(range(len(self.classes)), key=lambda i: -self.classes[i].n) if RS_CLASS_DESC else \
+            range(len(self.classes))
+        for ci in order_c:
+            c = self.classes[ci]
             b0, oc = c.view(beta0), c.view(o)
             if fused:
                 # whole per-entity TRON in one kernel, L resident in LDS (ops/csrc/glm_kernels.hip rs_tron_kernel)
@@ -328,6 +353,9 @@ class RowSpaceBatch:
                 c.view(beta).copy_(r.W)
                 zs = None
                 f, it, rc = r.f, r.iters, r.reason
+            res_of[ci] = (f, it, rc)
+        for ci in range(len(self.classes)):
+            f, it, rc = res_of[ci]
             fs.append(f)
             its.append(it)
             rcs.append(rc)

@@ -55,15 +55,21 @@ cd = CoordinateDescent(coords, ev, score_device=dev)
 model, _ = cd.run(2)
 torch.cuda.synchronize()
 text = []
-for cid in ("global", "per-entity"):
-    log = Calls()
-    with log:
-        model, _ = cd.run(1, model) if cid == "global" else (model, None)
-    if cid == "per-entity":
-        break
-    torch.cuda.synchronize()
-    text.append(f"# one coordinate-descent sweep (both coordinates + training loss): {sum(log.c.values())} torch calls")
-    text += [f"{n:4d}  {name:32s} {where}" for (name, where), n in log.c.most_common(70)]
+log = Calls()
+with log:
+    model, _ = cd.run(1, model)
+torch.cuda.synchronize()
+text.append(f"# one coordinate-descent sweep (both coordinates + training loss): {sum(log.c.values())} torch calls")
+text += [f"{n:4d}  {name:32s} {where}" for (name, where), n in log.c.most_common(70)]
+# the random-effect coordinate update alone (calls made inside RandomEffectCoordinate.update_model)
+re_coord = coords["per-entity"]
+partial = cd.coordinates["global"].score(model.get("global"))
+log = Calls()
+with log:
+    re_coord.update_model(model.get("per-entity"), partial)
+torch.cuda.synchronize()
+text.append(f"# random-effect coordinate update alone: {sum(log.c.values())} torch calls")
+text += [f"{n:4d}  {name:32s} {where}" for (name, where), n in log.c.most_common(80)]
 print("\n".join(text))
 if out:
     open(out, "w").write("\n".join(text) + "\n")

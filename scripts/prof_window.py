@@ -99,6 +99,18 @@ def main(db, sub, out=None):
     lines += ["", "| innermost region of the gap | gaps | idle ms |", "|---|---:|---:|"]
     for k, (n, t) in sorted(greg.items(), key=lambda kv: -kv[1][1])[:15]:
         lines.append(f"| {k} | {n} | {t / 1e6:.3f} |")
+    # timeline: every kernel of the window in start order (offset from the window start, duration, the queue /
+    # stream column when the database has one) -- the critical path of windows with side-stream work
+    qcol = next((x for x in ("stream_id", "queue_id", "stream", "queue") if x in kc), None)
+    if qcol is not None:
+        tl = list(c.execute(f"select {kn}, {ks}, {ke}, {qcol} from {kv} where {ks} >= ? and {ke} <= ? order by {ks}",
+                            (t0, t1)))
+    else:
+        tl = [(n, s, e, "-") for n, s, e in ks_]
+    lines += ["", f"Timeline ({qcol or 'no queue column'}):", "", "| start ms | dur ms | queue | kernel |",
+              "|---:|---:|---|---|"]
+    for n, s, e, q in tl:
+        lines.append(f"| {(s - t0) / 1e6:.3f} | {(e - s) / 1e6:.3f} | {q} | `{short(n)}` |")
     text = "\n".join(lines)
     print(text)
     if out:
