@@ -189,6 +189,8 @@ def generate_device_shard(n_rows: int, n_features: int, nnz_per_row: int, device
     new_of_old32 = new_of_old.to(torch.int32)
     del counts
     csr, csc = [], []
+    from ..ops.tiled import shard_t_config
+    cbits, item_entries = shard_t_config(n_rows * k, n_rows, n_features, chunk_rows)
     for ci, ((a, b), (idx, val)) in enumerate(zip(zip(starts[:-1], starts[1:]), raw)):
         m = b - a
         idx = new_of_old32[idx.to(torch.int64)]
@@ -197,7 +199,7 @@ def generate_device_shard(n_rows: int, n_features: int, nnz_per_row: int, device
             col = idx.to(torch.int64)
             del idx
             csr.append(TLFwdChunk(rp, col, val, n_features))
-            csc.append(TLTChunk(rp, col, val, n_features, chunk_rows))
+            csc.append(TLTChunk(rp, col, val, n_features, chunk_rows, cbits=cbits, item_entries=item_entries))
             raw[ci] = None
             del col, val, rp
             if progress is not None:

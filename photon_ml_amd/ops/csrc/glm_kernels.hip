@@ -2809,11 +2809,12 @@ __global__ __launch_bounds__(256) void ls_step_grad_kernel(const double* __restr
                                                            double t, const double* __restrict__ G,
                                                            const long long* __restrict__ perm, double l2, long long n,
                                                            double* __restrict__ x, double* __restrict__ g) {
+#pragma clang fp contract(off)   // (HIP's __dmul_rn / __dadd_rn are plain operators: no FMA contraction here)
   for (long long i = (long long)blockIdx.x * 256 + threadIdx.x; i < n; i += (long long)gridDim.x * 256) {
-    const double xi = __dadd_rn(x0[i], __dmul_rn(t, d[i]));
+    const double xi = x0[i] + t * d[i];
     x[i] = xi;
     const double gi = perm ? G[perm[i]] : G[i];
-    g[i] = l2 != 0.0 ? __dadd_rn(gi, __dmul_rn(l2, xi)) : gi;
+    g[i] = l2 != 0.0 ? gi + l2 * xi : gi;
   }
 }
 

@@ -347,6 +347,10 @@ class DeviceGLMData(GLMComputable):
             wins.append((lo, hi))
         dmax = max([hi - lo for lo, hi in wins] + [1])
         layout = resolve_layout(layout, dmax, chunk_rows)
+        cbits = None
+        if layout == "tiled" and not col_windows and item_entries is None:
+            from .tiled import shard_t_config
+            cbits, item_entries = shard_t_config(int(x.nnz), n, d, chunk_rows)
         for (a, b), (lo, hi) in zip(zip(starts[:-1], starts[1:]), wins):
             xc = x[a:b]
             col_lo.append(lo)
@@ -358,7 +362,7 @@ class DeviceGLMData(GLMComputable):
                 col = torch.from_numpy(xc.indices.astype(np.int64)).to(dev)
                 val = torch.from_numpy(xc.data.astype(np.float64)).to(dev).to(vdt)
                 csr.append(TLFwdChunk(rp, col, val, dc))
-                csc.append(TLTChunk(rp, col, val, dc, chunk_rows, item_entries=item_entries))
+                csc.append(TLTChunk(rp, col, val, dc, chunk_rows, cbits=cbits, item_entries=item_entries))
                 continue
             sp_ = (xc.indptr - xc.indptr[0]).astype(np.int32)
             csr.append(SegChunk(sp_, torch.from_numpy(xc.indices.astype(np.int32)),
@@ -433,6 +437,10 @@ class DeviceGLMData(GLMComputable):
         dmax = max([hi - lo for lo, hi in wins] + [1])
         if resolve_layout("auto", dmax, chunk_rows) != "tiled":
             raise ValueError(f"from_device_csr needs the tiled layout (window {dmax} columns)")
+        cbits = None
+        if not col_windows and item_entries is None:
+            from .tiled import shard_t_config
+            cbits, item_entries = shard_t_config(int(ip[-1] - ip[0]), n, dim, chunk_rows)
         csr, csc, col_lo = [], [], []
         for i, (lo, hi) in enumerate(wins):
             a, b = starts[i], starts[i + 1]
@@ -441,7 +449,7 @@ class DeviceGLMData(GLMComputable):
             c = col[ea:eb] - lo if lo else col[ea:eb]
             v = val[ea:eb].to(dev).to(vdt)
             csr.append(TLFwdChunk(rp, c, v, hi - lo))
-            csc.append(TLTChunk(rp, c, v, hi - lo, chunk_rows, item_entries=item_entries))
+            csc.append(TLTChunk(rp, c, v, hi - lo, chunk_rows, cbits=cbits, item_entries=item_entries))
             col_lo.append(lo)
             del c, v
         out = DeviceGLMData(csr, csc, starts, y, offsets, weights, dim, precision, dev, None)

@@ -112,6 +112,25 @@ def t_bits(chunk_rows: int, f64: bool = False, want: Optional[int] = None) -> Op
     return c if c >= TL_MINBITS else None
 
 
+# Sparse shards: when a 1024-column tile of a row chunk holds fewer than this many entries on average, the transpose
+# copies use 2048-column tiles and 128K-entry items instead (measured on the game5pl fixed-effect shard, 25M rows x
+# 30 non-zeros over 1M features, ~31K entries per tile and chunk: FE coordinate 34.65 -> 32.83 ms; the headline
+# shard, ~102K entries per tile and chunk, is faster with the defaults: 37.88 vs 38.12 ms/step;
+# profiles/tl_tile_knobs_r4.md). PML_TL_CBITS / PML_TL_ITEM_ENTRIES override.
+SPARSE_TILE_ENTRIES = 1 << 16
+
+
+def shard_t_config(nnz: int, n_rows: int, dim: int, chunk_rows: int):
+    """``(cbits, item_entries)`` for the transpose copies of a whole shard (one choice for every chunk: the
+    shard-wide transpose needs one tile width); ``(None, None)`` = the defaults."""
+    if "PML_TL_CBITS" in os.environ or "PML_TL_ITEM_ENTRIES" in os.environ or n_rows <= 0 or dim < (1 << 16):
+        return None, None                      # (small feature spaces keep the defaults: a few tiles at most)
+    per_tile = (nnz / n_rows) * min(chunk_rows, n_rows) / math.ceil(dim / 1024)
+    if per_tile < SPARSE_TILE_ENTRIES:
+        return 11, 1 << 17
+    return None, None
+
+
 def tl_supported(dim: int, chunk_rows: int) -> bool:
     return fwd_bits(dim) is not None and t_bits(chunk_rows) is not None
 
