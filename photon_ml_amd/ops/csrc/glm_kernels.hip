@@ -2503,43 +2503,86 @@ __global__ __launch_bounds__(NTHREADS) void ls_eval_kernel(int n, double t, int 
 
 // ------------------------------------------------------------------------------------------------------------
 // Gram matrix of a few (k <= 22) long fp64 vectors and their linear combination: the vector-free L-BFGS two-loop
-// (optimization/lbfgs.py _History._apply_inverse_gram). One pass over the k vectors each: a tile of 256 elements
-// of every vector is staged in LDS (rows padded to 257 doubles: distinct rows land in distinct banks), then
-// thread p < k(k+1)/2 owns pair (a, b) and accumulates sum_e tile[a][e] tile[b][e] in fp64; per-workgroup
-// partials [grid, npairs] are summed on the host side (deterministic). The pointers travel by value in the
-// kernel arguments (no pointer-table upload).
+// (optimization/lbfgs.py _History._apply_inverse_gram). The Gram matrix B = V V^T of the k x n basis V is
+// GEMM-shaped, so it runs on the fp64 matrix cores (v_mfma_f64_16x16x4f64): the k <= 32 vectors pad to two
+// 16-row tiles, and every 4 elements cost three MFMAs per wave (tiles (0,0), (0,1), (1,1); B = A^T, so one
+// register per tile serves both operands). Fragments (gfx950): lane l holds V[row = 16 i + (l & 15)][element of
+// k-lane l >> 4] for tile i; accumulator q of lane l holds C[(l >> 4) + 4 q][l & 15]. Each wave streams its share of
+// the elements straight into registers (64 elements per iteration in 16-B loads, no LDS staging; the LDS-staged
+// scalar version was LDS-bound: two LDS reads per FMA, 67 us at n = 1M, k = 21). The 4 waves' tiles are added in
+// wave order through LDS and each workgroup writes its partial upper triangle [grid, k (k + 1) / 2] (pair p =
+// (a, a + j) in row-major order over a), summed in workgroup order by the consumer: deterministic.
 #define GRAM_MAXK 22
-#define GRAM_TILE 256
+#define GRAM_TILE 256            // elements per workgroup tile in the grid formulas (pml_*_grid)
+#define GRAM_ES 8                // 16-B loads per vector and lane per wave iteration (2 MFMA k-steps each)
 struct VecSet { const double* p[GRAM_MAXK]; double c[GRAM_MAXK]; };
+typedef double v4d_g __attribute__((ext_vector_type(4)));
 
-__global__ __launch_bounds__(GRAM_TILE) void gram_kernel(VecSet vs, int k, long long n, double* __restrict__ partial) {
-  __shared__ double sm[GRAM_MAXK][GRAM_TILE + 1];
-  const int tid = threadIdx.x;
-  const int np = k * (k + 1) / 2;
-  int pa = 0, pb = 0;
-  if (tid < np) {
-    int p = tid, a = 0;
-    while (p >= k - a) { p -= k - a; ++a; }
-    pa = a; pb = a + p;
+__global__ __launch_bounds__(256) void gram_kernel(VecSet vs, int k, long long n, double* __restrict__ partial) {
+  __shared__ double sm[4][32][33];
+  const int lane = threadIdx.x & 63, w = threadIdx.x >> 6;
+  const int r = lane & 15, sub = lane >> 4;
+  // this lane's two vectors (rows r and 16 + r; null past k): uniform loads of the by-value pointer table + selects
+  const double* p0 = nullptr;
+  const double* p1 = nullptr;
+#pragma unroll
+  for (int j = 0; j < GRAM_MAXK; ++j) {
+    if (j == r && j < k) p0 = vs.p[j];
+    if (j == 16 + r && j < k) p1 = vs.p[j];
   }
-  double acc = 0.0;
-  const long long ntiles = (n + GRAM_TILE - 1) / GRAM_TILE;
-  for (long long t = blockIdx.x; t < ntiles; t += gridDim.x) {
-    const long long i = t * GRAM_TILE + tid;
-    for (int j = 0; j < k; ++j) sm[j][tid] = i < n ? __builtin_nontemporal_load(vs.p[j] + i) : 0.0;
-    __syncthreads();
-    if (tid < np) {
-      double s0 = 0.0, s1 = 0.0;
-#pragma unroll 8
-      for (int e = 0; e < GRAM_TILE; e += 2) {
-        s0 = fma(sm[pa][e], sm[pb][e], s0);
-        s1 = fma(sm[pa][e + 1], sm[pb][e + 1], s1);
-      }
-      acc += s0 + s1;
+  v4d_g c00 = {0.0, 0.0, 0.0, 0.0}, c01 = c00, c11 = c00;
+  auto step = [&](double x0, double x1) {
+    c00 = __builtin_amdgcn_mfma_f64_16x16x4f64(x0, x0, c00, 0, 0, 0);
+    c01 = __builtin_amdgcn_mfma_f64_16x16x4f64(x0, x1, c01, 0, 0, 0);
+    c11 = __builtin_amdgcn_mfma_f64_16x16x4f64(x1, x1, c11, 0, 0, 0);
+  };
+  // Any element order works as long as the element of (k-step, k-lane) does not depend on the row: k-lane ``sub``
+  // of load j reads elements e0 + 8 j + 2 sub + {0, 1} (one 16-B load), so the 4 lanes of a row read 64 contiguous
+  // bytes per instruction and a wave iteration streams 64 elements of each vector with GRAM_ES 16-B loads in flight.
+  constexpr int WE = 8 * GRAM_ES;                       // elements per wave iteration
+  const long long stride = (long long)gridDim.x * 4 * WE;
+  const long long nfull = n - n % WE;                   // whole wave iterations (16-B aligned pairs)
+  typedef double v2d_g __attribute__((ext_vector_type(2)));
+  const v2d_g z2 = {0.0, 0.0};
+  long long e0 = ((long long)blockIdx.x * 4 + w) * WE;
+  for (; e0 < nfull; e0 += stride) {
+    v2d_g a0[GRAM_ES], a1[GRAM_ES];
+#pragma unroll
+    for (int j = 0; j < GRAM_ES; ++j) {
+      const long long e = e0 + 8 * j + 2 * sub;
+      a0[j] = p0 ? __builtin_nontemporal_load((const v2d_g*)(p0 + e)) : z2;
+      a1[j] = p1 ? __builtin_nontemporal_load((const v2d_g*)(p1 + e)) : z2;
     }
-    __syncthreads();
+#pragma unroll
+    for (int j = 0; j < GRAM_ES; ++j) {
+      step(a0[j][0], a1[j][0]);
+      step(a0[j][1], a1[j][1]);
+    }
   }
-  if (tid < np) partial[(long long)blockIdx.x * np + tid] = acc;
+  if (e0 < n) {                                         // the one partial wave iteration (elements past n are 0)
+    for (int j = 0; j < GRAM_ES; ++j)
+      for (int h = 0; h < 2; ++h) {
+        const long long e = e0 + 8 * j + 2 * sub + h;
+        const double x0 = (p0 && e < n) ? p0[e] : 0.0, x1 = (p1 && e < n) ? p1[e] : 0.0;
+        step(x0, x1);
+      }
+  }
+  // this wave's 32 x 32 (upper blocks) -> LDS, then the 4 waves added in order
+#pragma unroll
+  for (int q = 0; q < 4; ++q) {
+    const int row = sub + 4 * q;
+    sm[w][row][r] = c00[q];
+    sm[w][row][16 + r] = c01[q];
+    sm[w][16 + row][16 + r] = c11[q];
+  }
+  __syncthreads();
+  const int np = k * (k + 1) / 2;
+  for (int t = threadIdx.x; t < np; t += 256) {
+    int p = t, a = 0;
+    while (p >= k - a) { p -= k - a; ++a; }
+    const int bb = a + p;
+    partial[(long long)blockIdx.x * np + t] = ((sm[0][a][bb] + sm[1][a][bb]) + sm[2][a][bb]) + sm[3][a][bb];
+  }
 }
 
 __global__ __launch_bounds__(256) void lincomb_kernel(VecSet vs, int k, long long n, double* __restrict__ out) {
@@ -2722,22 +2765,31 @@ __global__ __launch_bounds__(256) void lbfgs_step_kernel(TwoLoopStep st, long lo
 // recursion on B in LDS; rho_i = 1 / B[i][k+i], initial scale B[k-1][2k-1] / B[2k-1][2k-1] of the newest pair),
 // lincomb_dev_kernel (ONE read of the basis, coefficients from device memory). The step chain it replaces costs
 // 2k + 1 dependent launches, each a full pass with a last-workgroup reduction.
-__global__ __launch_bounds__(256) void gram_two_loop_kernel(const double* __restrict__ partial, int grid, int k,
-                                                            double* __restrict__ coef, int negate) {
+#define GTL_THREADS 1024
+__global__ __launch_bounds__(GTL_THREADS) void gram_two_loop_kernel(const double* __restrict__ partial, int grid,
+                                                                    int k, double* __restrict__ coef, int negate) {
   __shared__ double B[GRAM_MAXK * GRAM_MAXK];
+  __shared__ double quarter[4][256];
   const int kk = 2 * k + 1, np = kk * (kk + 1) / 2;
   const int tid = threadIdx.x;
-  if (tid < np) {
-    // 8 interleaved accumulators (8 independent loads in flight per thread instead of one dependent chain of
-    // `grid` loads: the serial loop was 0.13 ms per direction), added in a fixed order (deterministic)
+  // pair t = tid & 255 (< np <= 253), quarter qq = tid >> 8 of the workgroup partials: each thread sums its quarter
+  // of the rows with 8 interleaved accumulators (independent loads in flight; a single thread per pair over all
+  // rows was a 30 us latency chain), then the quarters are added in order (deterministic)
+  const int t = tid & 255, qq = tid >> 8;
+  if (t < np) {
+    const int g0 = (grid * qq) / 4, g1 = (grid * (qq + 1)) / 4;
     double acc[8] = {0.0, 0.0, 0.0, 0.0, 0.0, 0.0, 0.0, 0.0};
-    int g = 0;
-    for (; g + 8 <= grid; g += 8) {
+    int g = g0;
+    for (; g + 8 <= g1; g += 8) {
 #pragma unroll
-      for (int u = 0; u < 8; ++u) acc[u] += partial[(long long)(g + u) * np + tid];
+      for (int u = 0; u < 8; ++u) acc[u] += partial[(long long)(g + u) * np + t];
     }
-    for (int u = 0; g + u < grid; ++u) acc[u] += partial[(long long)(g + u) * np + tid];
-    const double s = ((acc[0] + acc[1]) + (acc[2] + acc[3])) + ((acc[4] + acc[5]) + (acc[6] + acc[7]));
+    for (int u = 0; g + u < g1; ++u) acc[u] += partial[(long long)(g + u) * np + t];
+    quarter[qq][t] = ((acc[0] + acc[1]) + (acc[2] + acc[3])) + ((acc[4] + acc[5]) + (acc[6] + acc[7]));
+  }
+  __syncthreads();
+  if (tid < np) {
+    const double s = ((quarter[0][tid] + quarter[1][tid]) + quarter[2][tid]) + quarter[3][tid];
     int p = tid, a = 0;
     while (p >= kk - a) { p -= kk - a; ++a; }
     B[a * kk + a + p] = s;
@@ -2877,7 +2929,8 @@ int pml_two_loop_gram(int k, const double* const* s, const double* const* y, con
   vs.p[2 * k] = g;
   const int kk = 2 * k + 1, grid = pml_two_loop_gram_grid(n);
   hipLaunchKernelGGL(gram_kernel, dim3(grid), dim3(GRAM_TILE), 0, (hipStream_t)stream, vs, kk, n, partial);
-  hipLaunchKernelGGL(gram_two_loop_kernel, dim3(1), dim3(256), 0, (hipStream_t)stream, partial, grid, k, coef, negate);
+  hipLaunchKernelGGL(gram_two_loop_kernel, dim3(1), dim3(GTL_THREADS), 0, (hipStream_t)stream, partial, grid, k, coef,
+                     negate);
   const long long blocks = std::min<long long>((n + 255) / 256, 4096);
   hipLaunchKernelGGL(lincomb_dev_kernel, dim3((unsigned)blocks), dim3(256), 0, (hipStream_t)stream, vs, kk, n, coef, q);
   LAUNCH_CHECK();

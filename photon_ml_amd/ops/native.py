@@ -232,8 +232,8 @@ def _fast_vecs(vs) -> bool:
 
 def gram(vs) -> torch.Tensor:
     """Device fp64 [k, k] matrix of all inner products of k <= 22 equal-length device vectors, ONE pass over
-    them (``gram_kernel``), or None when the inputs do not qualify."""
-    if not _fast_vecs(vs):
+    them (``gram_kernel``, fp64 MFMA; 16-B aligned vectors), or None when the inputs do not qualify."""
+    if not _fast_vecs(vs) or any(v.data_ptr() % 16 for v in vs):
         return None
     lib = require_glm_lib()
     k, n = len(vs), vs[0].numel()
@@ -420,8 +420,8 @@ def two_loop_gram(s, y, g, negate: bool = False):
             and g.dtype == torch.float64 and g.dim() == 1 and g.is_contiguous() and g.numel() > 0):
         return None
     if not all(v.device == g.device and v.dtype == torch.float64 and v.is_contiguous() and v.numel() == g.numel()
-               for v in list(s) + list(y)):
-        return None
+               and v.data_ptr() % 16 == 0 for v in list(s) + list(y) + [g]):
+        return None                    # (the MFMA Gram kernel reads 16-B pairs)
     lib = require_glm_lib()
     n = g.numel()
     kk = 2 * k + 1
