@@ -237,6 +237,24 @@ class RandomEffectCoordinate(Coordinate):
         self._returned = None  # the model object the last update returned (its solver state is in _W / _rs)
         self.last_stats = {}
 
+    # The tracker statistics of the last update (random_effect_tracker_stats) are reduced on first read: the masked
+    # selection of active entities and the dozen small reductions behind them (a stream synchronisation) stay off
+    # the coordinate-descent critical path unless someone looks at them.
+    @property
+    def last_stats(self) -> dict:
+        thunk = self.__dict__.get("_stats_thunk")
+        if thunk is not None:
+            self.__dict__["_stats"] = thunk()
+            self.__dict__["_stats_thunk"] = None
+        return self.__dict__.get("_stats", {})
+
+    @last_stats.setter
+    def last_stats(self, value: dict):
+        self.__dict__["_stats"], self.__dict__["_stats_thunk"] = value, None
+
+    def _defer_stats(self, iters: torch.Tensor, reasons: torch.Tensor, act: torch.Tensor, seconds: float):
+        self.__dict__["_stats_thunk"] = lambda: random_effect_tracker_stats(iters[act], reasons[act], seconds)
+
     def set_config(self, opt_config: GLMOptimizationConfiguration):
         rt = opt_config.regularization_context.regularization_type
         if opt_config.optimizer_config.optimizer_type == OptimizerType.TRON and rt in (
@@ -435,7 +453,7 @@ class RandomEffectCoordinate(Coordinate):
             n_iter = torch.zeros(seg.B, dtype=torch.long, device=beta.device).index_copy(0, rs.ents, rres.iters)
             n_reason = torch.zeros(seg.B, dtype=torch.long, device=beta.device).index_copy(0, rs.ents, rres.reason)
             act = self._active_mask(n_iter.device)
-            self.last_stats = random_effect_tracker_stats(n_iter[act], n_reason[act], time.time() - t_start)
+            self._defer_stats(n_iter, n_reason, act, time.time() - t_start)
             sum_sq = float(torch.linalg.vector_norm(torch.where(rs.valid, beta, torch.zeros_like(beta)))) ** 2
             out = RandomEffectModel(self.data_config.random_effect_type, self.data_config.feature_shard_id, self.task,
                                     ds.entity_ids, ds.dim, ds.projection_keys_t, self._lazy_W, None, sum_sq=sum_sq)
@@ -453,7 +471,7 @@ class RandomEffectCoordinate(Coordinate):
         res = BatchedResult(W_all, None, iters, reasons)
         self._W["seg"] = res.W
         act = self._active_mask(res.iters.device)
-        self.last_stats = random_effect_tracker_stats(res.iters[act], res.reason[act], time.time() - t_start)
+        self._defer_stats(res.iters, res.reason, act, time.time() - t_start)
         W = res.W.detach()
         var = None
         if self.compute_variance and self.loss.twice_differentiable:
@@ -609,7 +627,7 @@ class RandomEffectCoordinate(Coordinate):
         self._W["seg"] = _RS_WARM
         self._rs_scores = z
         act = self._active_mask(dev)
-        self.last_stats = random_effect_tracker_stats(iters[act], reasons[act], time.time() - t_start)
+        self._defer_stats(iters, reasons, act, time.time() - t_start)
         need_var = self.compute_variance and self.loss.twice_differentiable
         if need_var:
             W = primal()
