@@ -102,8 +102,21 @@ def _cap(want: int, f64: bool) -> int:
     return min(want, TL_MAXBITS_F64 if f64 else TL_MAXBITS)
 
 
+# fp64 shards over wide feature spaces use 2048-row forward blocks: an fp64 coefficient gather covers half the
+# columns per cache line of an fp32 one, so the denser keys of a bigger block pay there (game5pl fp64 fixed effect:
+# 54.4 -> 52.2 ms per coordinate update; the bf16 shards are faster with 1024-row blocks: 32.2 vs 33.2 ms;
+# profiles/tl_tile_knobs_r4.md). PML_TL_RBITS overrides.
+F64_WIDE_RBITS = 11
+
+
+def default_rbits(dim: int, f64: bool) -> int:
+    if f64 and dim >= (1 << 16) and "PML_TL_RBITS" not in os.environ:
+        return F64_WIDE_RBITS
+    return DEFAULT_RBITS
+
+
 def fwd_bits(dim: int, f64: bool = False, want: Optional[int] = None) -> Optional[int]:
-    r = min(_cap(DEFAULT_RBITS if want is None else want, f64), 32 - _bits(dim))
+    r = min(_cap(default_rbits(dim, f64) if want is None else want, f64), 32 - _bits(dim))
     return r if r >= TL_MINBITS else None
 
 
@@ -296,7 +309,7 @@ class TLFwdChunk(_NarrowMixin):
             raise ValueError(f"tiled forward layout cannot pack dim={dim}")
         # wide shards: (col << rbits) would overflow 32 bits at the wanted block size -> keys relative to one base
         # per wide round (the full block size instead of 2^(32 - bits(D)) rows; see tl_stream_ring)
-        want = _cap(DEFAULT_RBITS if rbits is None else rbits, f64)
+        want = _cap(default_rbits(dim, f64) if rbits is None else rbits, f64)
         use_base = bool(self.il) and WIDE_BASE and want > self.rbits
         if use_base:
             self.rbits = want

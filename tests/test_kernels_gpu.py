@@ -803,7 +803,7 @@ def test_wide_round_bases_on_device(precision, monkeypatch):
         monkeypatch.setattr(tiled, "WIDE_BASE", wb)
         dev = DeviceGLMData.from_labeled(data, "cuda", precision, chunk_rows=2500, layout="tiled")
         assert all((ch.wbase is not None) == bool(wb) for ch in dev.csr)
-        assert all(ch.rbits == (10 if wb else 7) for ch in dev.csr)
+        assert all(ch.rbits == (tiled.default_rbits(d, precision == "f64") if wb else 7) for ch in dev.csr)
         for multi in (1, 0):
             configure(tl_multi=multi)
             try:

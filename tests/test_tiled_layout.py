@@ -207,7 +207,7 @@ def test_wide_round_bases_keep_full_row_blocks():
         for wb in (0, 1):
             tiled.WIDE_BASE = wb
             ch = TLFwdChunk(rp, c, v, d)
-            assert ch.rbits == (10 if wb else 32 - 25)
+            assert ch.rbits == (tiled.default_rbits(d, True) if wb else 32 - 25)
             assert (ch.wbase is not None) == bool(wb)
             torch.testing.assert_close(ch.emulate_matvec(w), ref, rtol=1e-12, atol=1e-12)
             pk, _ = ch.logical()
