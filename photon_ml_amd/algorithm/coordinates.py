@@ -140,10 +140,16 @@ class FixedEffectCoordinate(Coordinate):
     def update_model(self, model: FixedEffectModel, partial_score: Optional[torch.Tensor] = None):
         base, rows = self._device_row_data()
         off = base
+        fused = False
         if partial_score is not None:
             ps = partial_score.detach().to(base.device, torch.float64)
-            off = base + (ps if rows is None else ps[rows])
-        self.glm_data.set_offsets(off)
+            ps = ps if rows is None else ps[rows]
+            fn = getattr(self.glm_data, "set_offsets_sum", None)
+            fused = fn is not None and fn(base, ps)          # sum + cast + margin shift in one pass
+            if not fused:
+                off = base + ps
+        if not fused:
+            self.glm_data.set_offsets(off)
         gd = self.glm_data
         if self.sampler is not None:
             self._apply_down_sampling()

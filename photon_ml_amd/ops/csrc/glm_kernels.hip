@@ -2857,6 +2857,21 @@ __global__ __launch_bounds__(256) void masked_gather_kernel(const double* __rest
   }
 }
 
+// GAME fixed-effect offsets for the next update in one pass: o = (RT)(base + partial) and, when the cached margins
+// are kept, z += (double) o_new - (double) o_old (the margins shift by the offset change) -- the torch chain it
+// replaces (an add, a cast, two casts, a subtraction, an in-place add, a copy) rounded the same way.
+template <typename RT>
+__global__ __launch_bounds__(256) void offset_update_kernel(const double* __restrict__ base,
+                                                            const double* __restrict__ part, long long n,
+                                                            RT* __restrict__ o, double* __restrict__ z) {
+#pragma clang fp contract(off)
+  for (long long i = (long long)blockIdx.x * 256 + threadIdx.x; i < n; i += (long long)gridDim.x * 256) {
+    const RT nw = static_cast<RT>(base[i] + part[i]);
+    if (z) z[i] = z[i] + (static_cast<double>(nw) - static_cast<double>(o[i]));
+    o[i] = nw;
+  }
+}
+
 __global__ __launch_bounds__(256) void ls_step_grad_kernel(const double* __restrict__ x0, const double* __restrict__ d,
                                                            double t, const double* __restrict__ G,
                                                            const long long* __restrict__ perm, double l2, long long n,
@@ -2978,6 +2993,20 @@ int pml_perm_cast(const double* w, const long long* perm, long long n, int prec,
 int pml_masked_gather(const double* src, const long long* idx, long long n, double* out, void* stream) {
   if (n <= 0) return 0;
   hipLaunchKernelGGL(masked_gather_kernel, dim3(vec_grid(n)), dim3(256), 0, (hipStream_t)stream, src, idx, n, out);
+  LAUNCH_CHECK();
+  return 0;
+}
+
+// prec 2: fp64 row vectors, else fp32; z may be null (no margin cache)
+int pml_offset_update(const double* base, const double* part, long long n, int prec, void* o, double* z,
+                      void* stream) {
+  if (n <= 0) return 0;
+  if (prec == 2)
+    hipLaunchKernelGGL(offset_update_kernel<double>, dim3(vec_grid(n)), dim3(256), 0, (hipStream_t)stream, base, part,
+                       n, (double*)o, z);
+  else
+    hipLaunchKernelGGL(offset_update_kernel<float>, dim3(vec_grid(n)), dim3(256), 0, (hipStream_t)stream, base, part,
+                       n, (float*)o, z);
   LAUNCH_CHECK();
   return 0;
 }

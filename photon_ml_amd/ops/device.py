@@ -532,6 +532,29 @@ class DeviceGLMData(GLMComputable):
             view.validate()
         return view
 
+    def set_offsets_sum(self, base: torch.Tensor, part: torch.Tensor) -> bool:
+        """:meth:`set_offsets` of ``base + part`` (fp64 device vectors of the shard's rows) in one fused pass
+        (``offset_update_kernel``: the sum, the cast to the row precision and the cached-margin shift); False when
+        the inputs do not qualify (then nothing was changed)."""
+        n = self.n_rows
+        if not (n > 0 and base.is_cuda and part.is_cuda and base.dtype == part.dtype == torch.float64
+                and base.numel() == part.numel() == n == self.o.numel() and base.is_contiguous()
+                and part.is_contiguous() and base.device == self.o.device == part.device):
+            return False
+        from .native import offset_update
+        zc = getattr(self, "z_cache", None)
+        shift = (zc is not None and getattr(self, "_z_key", None) is not None and self._z_chain + 1 < self.LS_REFRESH
+                 and getattr(self, "_masked", None) is None and OFFSET_SHIFT_CACHE)
+        offset_update(base, part, self.o, zc[:n] if shift else None)
+        if shift:
+            self._z_chain += 1
+            self._ls_t0 = None
+        else:
+            self._z_key = None
+        self._step_base = None
+        self._dzz_key = None
+        return True
+
     def set_offsets(self, offsets):
         new = torch.as_tensor(offsets, device=self.device).to(self.vdt)
         zc = getattr(self, "z_cache", None)

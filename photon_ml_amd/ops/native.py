@@ -137,6 +137,8 @@ def glm_lib() -> Optional[ctypes.CDLL]:
         lib.pml_ls_step_grad.restype = c_int
         lib.pml_masked_gather.argtypes = [c_void_p, c_void_p, ctypes.c_longlong, c_void_p, c_void_p]
         lib.pml_masked_gather.restype = c_int
+        lib.pml_offset_update.argtypes = [c_void_p, c_void_p, ctypes.c_longlong, c_int, c_void_p, c_void_p, c_void_p]
+        lib.pml_offset_update.restype = c_int
         lib.pml_two_loop_chain.argtypes = [c_int] + [c_void_p] * 5 + [ctypes.c_longlong] + [c_void_p] * 4 + \
             [c_int, c_void_p]
         lib.pml_two_loop_gram.argtypes = [c_int, c_void_p, c_void_p, c_void_p, ctypes.c_longlong, c_void_p, c_void_p,
@@ -344,6 +346,21 @@ def perm_cast(w: torch.Tensor, perm: Optional[torch.Tensor], dtype: torch.dtype)
                                           2 if dtype == torch.float64 else 1, out.data_ptr(), stream_handle(w.device)),
           "perm_cast")
     return out
+
+
+def offset_update(base: torch.Tensor, part: torch.Tensor, o: torch.Tensor, z: Optional[torch.Tensor]) -> None:
+    """In place, one pass (``offset_update_kernel``): ``o = (base + part).to(o.dtype)`` and, with ``z``,
+    ``z += o_new - o_old`` in fp64. ``base``, ``part``, ``z`` fp64 and ``o`` fp32 / fp64 device vectors of one
+    length."""
+    n = base.numel()
+    for t in (base, part, o) + (() if z is None else (z,)):
+        assert t.is_cuda and t.is_contiguous() and t.numel() == n and t.device == base.device
+    assert base.dtype == part.dtype == torch.float64 and o.dtype in (torch.float32, torch.float64)
+    assert z is None or z.dtype == torch.float64
+    check(require_glm_lib().pml_offset_update(base.data_ptr(), part.data_ptr(), n,
+                                              2 if o.dtype == torch.float64 else 1, o.data_ptr(),
+                                              None if z is None else z.data_ptr(), stream_handle(base.device)),
+          "offset_update")
 
 
 def masked_gather(src: torch.Tensor, idx: torch.Tensor) -> torch.Tensor:
