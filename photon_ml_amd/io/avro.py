@@ -10,7 +10,7 @@ import json
 import os
 from typing import Iterable, List, Optional, Sequence
 
-from ..ops.build import build_cpp, lib_path
+from ..ops.build import StaleLibraryError, expected_id, verified_path
 
 _MOD = None
 
@@ -18,12 +18,12 @@ _MOD = None
 def native():
     global _MOD
     if _MOD is None:
-        path = lib_path("cpp", "avro")
-        if not path.exists():
-            build_cpp("avro")
+        path = verified_path("cpp", "avro")       # stale builds are rebuilt or refused (ops/build.py build ids)
         spec = importlib.util.spec_from_file_location("libpml_avro", str(path))
         mod = importlib.util.module_from_spec(spec)
         spec.loader.exec_module(mod)
+        if mod.build_id() != expected_id("cpp", "avro"):
+            raise StaleLibraryError(f"{path}: loaded build id {mod.build_id()} != the tree's sources")
         _MOD = mod
     return _MOD
 

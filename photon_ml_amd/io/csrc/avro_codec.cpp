@@ -30,6 +30,13 @@
 #include <unordered_map>
 #include <vector>
 
+// Build id (photon_ml_amd/ops/build.py: content hash of the sources + compile command, -DPML_BUILD_ID=...): the
+// loaders compare it with the tree's sources and refuse a stale library.
+#ifndef PML_BUILD_ID
+#define PML_BUILD_ID "unstamped-build!"
+#endif
+__attribute__((used)) static const char pml_build_stamp[] = "PML_BUILD_ID=" PML_BUILD_ID;
+
 namespace py = pybind11;
 
 // ============================================================================================================
@@ -1273,6 +1280,7 @@ static int64_t gen_training_examples(const std::string& path, int64_t n_records,
 }
 
 PYBIND11_MODULE(libpml_avro, m) {
+  m.def("build_id", []() { return std::string(pml_build_stamp + 13); });
   m.doc() = "photon_ml_amd native Avro OCF codec";
   m.def("read_ocf", &read_ocf, "Decode an OCF file -> (schema_json, [records], codec)");
   m.def("read_schema", &read_schema);

@@ -20,6 +20,13 @@
 #include <cstdio>
 #include <vector>
 
+// Build id (photon_ml_amd/ops/build.py: content hash of the sources + compile command, -DPML_BUILD_ID=...): the
+// loaders compare it with the tree's sources and refuse a stale library.
+#ifndef PML_BUILD_ID
+#define PML_BUILD_ID "unstamped-build!"
+#endif
+__attribute__((used)) static const char pml_build_stamp[] = "PML_BUILD_ID=" PML_BUILD_ID;
+
 static inline uint64_t fnv1a(const char* s, size_t n) {
   uint64_t h = 1469598103934665603ULL;
   for (size_t i = 0; i < n; ++i) { h ^= (unsigned char)s[i]; h *= 1099511628211ULL; }
@@ -36,6 +43,8 @@ struct IndexMapFile {
 };
 
 extern "C" {
+
+const char* pml_build_id() { return pml_build_stamp + 13; }
 
 // keys: concatenated bytes; offs: int64[n + 1]. Returns 0 on success, -1 on I/O error, -2 on duplicate key.
 int pml_im_build(const char* keys, const int64_t* offs, int64_t n, const char* path) {

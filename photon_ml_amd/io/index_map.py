@@ -20,7 +20,7 @@ from typing import Dict, Iterable, List, Optional, Sequence
 import numpy as np
 
 from ..constants import DELIMITER, INTERCEPT_KEY, feature_key, split_feature_key
-from ..ops.build import build_cpp, lib_path
+from ..ops.build import StaleLibraryError, expected_id, verified_path
 
 
 class IndexMap:
@@ -129,10 +129,11 @@ _IMLIB = None
 def _imlib():
     global _IMLIB
     if _IMLIB is None:
-        path = lib_path("cpp", "indexmap")
-        if not path.exists():
-            build_cpp("indexmap")
+        path = verified_path("cpp", "indexmap")   # stale builds are rebuilt or refused (ops/build.py build ids)
         lib = ctypes.CDLL(str(path))
+        lib.pml_build_id.restype = ctypes.c_char_p
+        if lib.pml_build_id().decode() != expected_id("cpp", "indexmap"):
+            raise StaleLibraryError(f"{path}: loaded build id {lib.pml_build_id().decode()} != the tree's sources")
         lib.pml_im_build.argtypes = [ctypes.c_char_p, ctypes.c_void_p, ctypes.c_int64, ctypes.c_char_p]
         lib.pml_im_open.argtypes = [ctypes.c_char_p]
         lib.pml_im_open.restype = ctypes.c_void_p

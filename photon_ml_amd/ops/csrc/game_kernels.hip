@@ -19,6 +19,13 @@
 
 #include <algorithm>
 
+// Build id (photon_ml_amd/ops/build.py: content hash of the sources + compile command, -DPML_BUILD_ID=...): the
+// loaders compare it with the tree's sources and refuse a stale library.
+#ifndef PML_BUILD_ID
+#define PML_BUILD_ID "unstamped-build!"
+#endif
+__attribute__((used)) static const char pml_build_stamp[] = "PML_BUILD_ID=" PML_BUILD_ID;
+
 #define LAUNCH_CHECK()                                         \
   do {                                                         \
     hipError_t e_ = hipGetLastError();                         \
@@ -359,6 +366,8 @@ __global__ __launch_bounds__(64) void rs_primal_kernel(const long long* __restri
 }
 
 extern "C" {
+
+const char* pml_build_id() { return pml_build_stamp + 13; }
 
 int pml_downsample(int f64, const void* y, const void* w0, const long long* rowid, long long n,
                    unsigned long long seed, double rate, int binary, void* w, void* stream) {

@@ -2022,6 +2022,13 @@ __global__ __launch_bounds__(NTHREADS) void rs_tron_kernel(
 // ============================================================================================================
 #include "rs_dpp_blocks.h"
 
+// Build id (photon_ml_amd/ops/build.py: content hash of the sources + compile command, -DPML_BUILD_ID=...): the
+// loaders compare it with the tree's sources and refuse a stale library.
+#ifndef PML_BUILD_ID
+#define PML_BUILD_ID "unstamped-build!"
+#endif
+__attribute__((used)) static const char pml_build_stamp[] = "PML_BUILD_ID=" PML_BUILD_ID;
+
 // two independent group sums, stage by stage (ILP 2 on the DPP / add latency chain)
 template <int GL>
 __device__ __forceinline__ void group_sum2(double& a, double& b) {
@@ -2904,6 +2911,8 @@ __global__ __launch_bounds__(64) void lds_add_order_probe_kernel(const double* _
 }
 
 extern "C" {
+
+const char* pml_build_id() { return pml_build_stamp + 13; }
 
 // H g (negate: -H g) for a k-deep history (newest last): rho[j] = 1/s_j.y_j and gamma = s.y/y.y of the newest
 // pair are device scalars; coef: 2k doubles of device scratch; partial: 1024 doubles; counter: one zeroed unsigned.

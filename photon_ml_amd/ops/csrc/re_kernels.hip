@@ -28,6 +28,13 @@
 #include <hip/hip_runtime.h>
 #include <stdint.h>
 
+// Build id (photon_ml_amd/ops/build.py: content hash of the sources + compile command, -DPML_BUILD_ID=...): the
+// loaders compare it with the tree's sources and refuse a stale library.
+#ifndef PML_BUILD_ID
+#define PML_BUILD_ID "unstamped-build!"
+#endif
+__attribute__((used)) static const char pml_build_stamp[] = "PML_BUILD_ID=" PML_BUILD_ID;
+
 #define LAUNCH_CHECK()                                         \
   do {                                                         \
     hipError_t e_ = hipGetLastError();                         \
@@ -62,6 +69,41 @@ __device__ __forceinline__ void loss_t(double z, double y, double& l, double& dl
   }
 }
 
+// loss_t split in two (the same operations, so the same bits): loss_dl gives l' and what loss_rest needs for
+// l and l'' (logistic: e = exp(-|z|) and the sigmoid s; Poisson: e^z). The vectorised row pass scatters with l'
+// while the batch's entries are in registers and evaluates the rest (log1p) after they are dead.
+template <int LOSS>
+__device__ __forceinline__ double loss_dl(double z, double y, double& e, double& s) {
+  if constexpr (LOSS == LOSS_LOGISTIC) {
+    e = exp(-fabs(z));
+    const double r = 1.0 / (1.0 + e);
+    s = z >= 0.0 ? r : e * r;
+    return y > 0.5 ? s - 1.0 : s;
+  } else if constexpr (LOSS == LOSS_POISSON) {
+    e = exp(z);
+    s = 0.0;
+    return e - y;
+  } else {
+    e = 0.0; s = 0.0;
+    return z - y;
+  }
+}
+
+template <int LOSS>
+__device__ __forceinline__ void loss_rest(double z, double y, double e, double s, double& l, double& d2) {
+  if constexpr (LOSS == LOSS_LOGISTIC) {
+    const double lp = log1p(e);
+    const double zz = y > 0.5 ? -z : z;
+    l = (zz > 0.0 ? zz : 0.0) + lp;
+    d2 = s * (1.0 - s);
+  } else if constexpr (LOSS == LOSS_POISSON) {
+    l = e - y * z; d2 = e;
+  } else {
+    const double d = z - y;
+    l = 0.5 * d * d; d2 = 1.0;
+  }
+}
+
 template <int CTRL>
 __device__ __forceinline__ double dpp_f64(double v) {
   const long long b = __builtin_bit_cast(long long, v);
@@ -87,6 +129,16 @@ __device__ __forceinline__ double wave_total(double v) {
   return (readlane_f64(v, 0) + readlane_f64(v, 16)) + (readlane_f64(v, 32) + readlane_f64(v, 48));
 }
 
+// A workgroup-uniform value re-tagged as wave-uniform (readfirstlane): it is held in SGPRs, not VGPRs.
+__device__ __forceinline__ long long uniform_i64(long long v) {
+  const int lo = __builtin_amdgcn_readfirstlane((int)v);
+  const int hi = __builtin_amdgcn_readfirstlane((int)(v >> 32));
+  return ((long long)hi << 32) | (long long)(unsigned int)lo;
+}
+__device__ __forceinline__ double uniform_f64(double v) {
+  return __builtin_bit_cast(double, uniform_i64(__builtin_bit_cast(long long, v)));
+}
+
 // Workgroup sums of K values (K <= 8), in every thread. ``red`` holds two [RE_NW][8] slots used alternately,
 // so one barrier per call suffices: a slot is rewritten only two calls later, after every thread has passed
 // the barrier of the call in between (all threads run the same, workgroup-uniform control flow).
@@ -106,7 +158,7 @@ __device__ __forceinline__ void block_sums(double (&v)[K], double* __restrict__ 
     double s = 0.0;
 #pragma unroll
     for (int q = 0; q < RE_NW; ++q) s += slot[q * 8 + k];
-    v[k] = s;
+    v[k] = uniform_f64(s);      // identical in every thread
   }
   parity ^= 1;
 }
@@ -247,6 +299,148 @@ __device__ __forceinline__ void row_pass(const ReTronArgs& a, long long r0, long
       for (int k = 0; k < RE_K; ++k)
         if (lo[u] + gl + RE_G * k < hi[u]) atomicAdd(&acc[c[u][k]], t * v[u][k]);
       for (int p = lo[u] + gl + RE_G * RE_K; p < hi[u]; p += RE_G) atomicAdd(&acc[lcol[p]], t * val[p]);
+    }
+    np = np_next;
+  }
+}
+
+// ------------------------------------------------------------------------------------------------------------
+// Vectorised row pass (lean kernel). Same work as row_pass, but lane gl of a row's 16 lanes owns the 4-entry
+// QUAD (lo & ~3) + 4 gl (+ 64 per extra chunk) of the row: its 4 columns arrive in ONE 8-byte buffer load and
+// its 4 values in TWO 16-byte buffer loads (row_pass: 4 + 4 narrow loads, one 64-bit address each). Entries of
+// the quad outside [lo, hi) belong to the neighbouring rows and are masked. Buffer resources (wave-uniform
+// SGPRs) over the entity's aligned entry range make every per-lane address a 32-bit byte offset, so a batch of
+// 4 U rows holds ~14 U VGPRs of loaded data and the kernel fits the register budget of 4 waves per SIMD.
+// Requires the entry arrays to be readable up to the next multiple of 4 entries (EntityTronBatch pads them).
+typedef int re_v2i __attribute__((ext_vector_type(2)));
+
+typedef int re_v4i __attribute__((ext_vector_type(4)));
+
+__device__ __forceinline__ double re_f64(int lo, int hi) {
+  return __builtin_bit_cast(double, ((long long)hi << 32) | (long long)(unsigned int)lo);
+}
+
+template <int MODE, int LOSS, int U>
+__device__ __forceinline__ void row_pass_v(const ReTronArgs& a, long long r0, long long r1,
+                                           const double* __restrict__ vec, double* __restrict__ acc,
+                                           const double* __restrict__ Dc, double* __restrict__ Dn,
+                                           double* __restrict__ Zn, double& fpart) {
+  const int lane = threadIdx.x & 63, w = threadIdx.x >> 6;
+  const int grp = lane / RE_G, gl = lane % RE_G;
+  const int nrows = (int)(r1 - r0);
+  // quad-aligned entity entry range, made wave-uniform (SGPRs) so the buffer resources need no waterfall loop
+  const long long e0 = uniform_i64(a.nip[r0]) & ~3LL;
+  const long long e1 = (uniform_i64(a.nip[r1]) + 3) & ~3LL;
+  const int nrec = (int)(e1 - e0);
+  const __amdgpu_buffer_rsrc_t rc = __builtin_amdgcn_make_buffer_rsrc((void*)(a.lcol + e0), (short)0, nrec * 2,
+                                                                       0x00020000);
+  const __amdgpu_buffer_rsrc_t rv = __builtin_amdgcn_make_buffer_rsrc((void*)(a.val + e0), (short)0, nrec * 8,
+                                                                       0x00020000);
+  const long long* __restrict__ nip = a.nip + r0;
+  const double* __restrict__ wt = a.wt + r0;
+  const double* __restrict__ off = a.off + r0;
+  const double* __restrict__ yv = a.y + r0;
+  if (MODE == 0) Dc += r0;
+  if (MODE == 1) { Dn += r0; Zn += r0; }
+  constexpr int BATCH = RE_RPI * U;
+  const int step = RE_NW * BATCH;
+  int base = w * BATCH;
+  auto fetch_ptr = [&](int b) -> int {
+    const int i = b + (lane <= BATCH ? lane : BATCH);
+    return b < nrows ? (int)(nip[i < nrows ? i : nrows] - e0) : 0;
+  };
+  // the quad of entries [q, q + 4) masked to [lo, hi): columns (0 outside) and values (0.0 outside)
+  auto load_quad = [&](int q, int lo, int hi, int (&c)[4], double (&v)[4]) {
+    const re_v2i cw = __builtin_amdgcn_raw_buffer_load_b64(rc, q * 2, 0, 0);
+    const re_v4i va = __builtin_amdgcn_raw_buffer_load_b128(rv, q * 8, 0, 0);
+    const re_v4i vb = __builtin_amdgcn_raw_buffer_load_b128(rv, q * 8 + 16, 0, 0);
+    const int cc[4] = {cw.x & 0xFFFF, (int)((unsigned)cw.x >> 16), cw.y & 0xFFFF, (int)((unsigned)cw.y >> 16)};
+    const double vv[4] = {re_f64(va.x, va.y), re_f64(va.z, va.w), re_f64(vb.x, vb.y), re_f64(vb.z, vb.w)};
+#pragma unroll
+    for (int k = 0; k < 4; ++k) {
+      const bool in = q + k >= lo && q + k < hi;
+      c[k] = in ? cc[k] : 0;
+      v[k] = in ? vv[k] : 0.0;
+    }
+  };
+  int np = fetch_ptr(base);
+  for (; base < nrows; base += step) {
+    const int np_next = fetch_ptr(base + step);
+    int lo[U], hi[U];
+    int c[U][4];
+    double v[U][4], dot[U], rs[U][3];
+#pragma unroll
+    for (int u = 0; u < U; ++u) {
+      const int q = u * RE_RPI + grp;
+      lo[u] = __shfl(np, q, 64);
+      hi[u] = __shfl(np, q + 1, 64);
+      const int i = base + q;
+      const bool valid = i < nrows;
+      if (MODE == 0) {
+        rs[u][0] = valid ? Dc[i] : 0.0;
+      } else {
+        rs[u][0] = valid ? wt[i] : 0.0;
+        rs[u][1] = valid ? off[i] : 0.0;
+        rs[u][2] = valid ? yv[i] : 0.0;
+      }
+    }
+#pragma unroll
+    for (int u = 0; u < U; ++u) load_quad((lo[u] & ~3) + 4 * gl, lo[u], hi[u], c[u], v[u]);
+#pragma unroll
+    for (int u = 0; u < U; ++u) {
+      double s = 0.0;
+      if (MODE != 2) {
+#pragma unroll
+        for (int k = 0; k < 4; ++k) s = fma(v[u][k], vec[c[u][k]], s);
+        for (int q = (lo[u] & ~3) + 4 * gl + 64; q < hi[u]; q += 64) {   // rows longer than one chunk
+          int ct[4];
+          double vt[4];
+          load_quad(q, lo[u], hi[u], ct, vt);
+#pragma unroll
+          for (int k = 0; k < 4; ++k) s = fma(vt[k], vec[ct[k]], s);
+        }
+      }
+      dot[u] = s;
+    }
+    double le[U], ls[U];        // loss_dl -> loss_rest hand-off (function evaluations)
+#pragma unroll
+    for (int u = 0; u < U; ++u) {
+      if (MODE != 2) dot[u] = row16_total(dot[u]);
+      const int i = base + u * RE_RPI + grp;
+      const bool valid = i < nrows;
+      double t;
+      if (MODE == 0) {
+        t = rs[u][0] * dot[u];
+      } else {
+        double dl = 0.0;
+        le[u] = 0.0; ls[u] = 0.0;
+        if (valid) dl = loss_dl<LOSS>(dot[u] + rs[u][1], rs[u][2], le[u], ls[u]);
+        t = rs[u][0] * dl;
+      }
+      const int q0 = (lo[u] & ~3) + 4 * gl;
+#pragma unroll
+      for (int k = 0; k < 4; ++k)
+        if (q0 + k >= lo[u] && q0 + k < hi[u]) atomicAdd(&acc[c[u][k]], t * v[u][k]);
+      for (int q = q0 + 64; q < hi[u]; q += 64) {
+        int ct[4];
+        double vt[4];
+        load_quad(q, lo[u], hi[u], ct, vt);
+#pragma unroll
+        for (int k = 0; k < 4; ++k)
+          if (q + k >= lo[u] && q + k < hi[u]) atomicAdd(&acc[ct[k]], t * vt[k]);
+      }
+    }
+    if (MODE != 0) {
+#pragma unroll
+      for (int u = 0; u < U; ++u) {
+        const int i = base + u * RE_RPI + grp;
+        if (i < nrows && gl == 0) {
+          double l, d2;
+          loss_rest<LOSS>(dot[u] + rs[u][1], rs[u][2], le[u], ls[u], l, d2);
+          fpart += rs[u][0] * l;
+          if (MODE == 1) { Dn[i] = rs[u][0] * d2; Zn[i] = dot[u]; }
+        }
+      }
     }
     np = np_next;
   }
@@ -456,7 +650,15 @@ __global__ __launch_bounds__(RE_THREADS) void re_tron_csr_kernel(ReTronArgs a) {
 // (<= 168 VGPRs, 12 waves per CU) with two row groups per batch in function evaluations (one: same total, the 64
 // largest entities 33.6 instead of 28.1 ms) and three in Hessian-vector passes (four: +15 %); 4 waves per SIMD
 // spills in the row loop (80 ms vs 61 ms for re_tron_csr_kernel)
-#ifndef LEAN_WPE                 // (guarded: the A/B scripts build variants with -D)
+#ifndef LEAN_VEC                 // (guarded: the A/B scripts build variants with -D)
+#define LEAN_VEC 1               // 1: vectorised quad row pass (row_pass_v), 0: row_pass
+#endif
+#if LEAN_VEC
+#define LEAN_PASS row_pass_v
+#else
+#define LEAN_PASS row_pass
+#endif
+#ifndef LEAN_WPE
 #define LEAN_WPE 3
 #endif
 #ifndef LEAN_UF
@@ -469,10 +671,10 @@ template <int LOSS, int J>
 __global__ __launch_bounds__(RE_THREADS) __attribute__((amdgpu_waves_per_eu(LEAN_WPE, LEAN_WPE)))
 void re_tron_lean_kernel(ReTronArgs a) {
   extern __shared__ __attribute__((aligned(16))) double smem[];
-  const int e = a.order[blockIdx.x];
-  const long long r0 = a.row_ptr[e], r1 = a.row_ptr[e + 1];
-  const long long c0 = a.col_ptr[e];
-  const int d = (int)(a.col_ptr[e + 1] - c0);
+  const int e = __builtin_amdgcn_readfirstlane(a.order[blockIdx.x]);
+  const long long r0 = uniform_i64(a.row_ptr[e]), r1 = uniform_i64(a.row_ptr[e + 1]);
+  const long long c0 = uniform_i64(a.col_ptr[e]);
+  const int d = (int)(uniform_i64(a.col_ptr[e + 1]) - c0);
   const int tid = threadIdx.x, w = tid >> 6, lane = tid & 63;
   const int dm = a.dmax;
   double* sD = smem;        // CG direction; W / the trial point during a function evaluation
@@ -498,8 +700,8 @@ void re_tron_lean_kernel(ReTronArgs a) {
     __syncthreads();
     for (int j = lane; j < d; j += 64) myacc[j] = 0.0;
     double fp = 0.0;
-    if (at_zero) row_pass<2, LOSS, LEAN_UF>(a, r0, r1, sD, myacc, nullptr, nullptr, nullptr, fp);
-    else row_pass<1, LOSS, LEAN_UF>(a, r0, r1, sD, myacc, nullptr, D[nb], Z[nb], fp);
+    if (at_zero) LEAN_PASS<2, LOSS, LEAN_UF>(a, r0, r1, sD, myacc, nullptr, nullptr, nullptr, fp);
+    else LEAN_PASS<1, LOSS, LEAN_UF>(a, r0, r1, sD, myacc, nullptr, D[nb], Z[nb], fp);
     __syncthreads();
     double s3[3] = {fp, 0.0, 0.0};
 #pragma unroll
@@ -566,7 +768,7 @@ void re_tron_lean_kernel(ReTronArgs a) {
       __syncthreads();
       for (int j = lane; j < d; j += 64) myacc[j] = 0.0;
       double fp = 0.0;
-      row_pass<0, LOSS, LEAN_UH>(a, r0, r1, sD, myacc, D[cur], nullptr, nullptr, fp);
+      LEAN_PASS<0, LOSS, LEAN_UH>(a, r0, r1, sD, myacc, D[cur], nullptr, nullptr, fp);
       __syncthreads();
       double s5[5] = {0.0, 0.0, 0.0, 0.0, 0.0};
       double H[J];
@@ -614,8 +816,8 @@ void re_tron_lean_kernel(ReTronArgs a) {
         }
       }
       if (hit) break;
-      rtr = rn;
-      sts = tn;
+      rtr = uniform_f64(rn);
+      sts = uniform_f64(tn);
     }
     // trial point W + step (in sD), trust-region update, acceptance
     double s3[3] = {0.0, 0.0, 0.0};
@@ -635,7 +837,7 @@ void re_tron_lean_kernel(ReTronArgs a) {
     double gn2;
     const double fn = value_grad(false, cur ^ 1, gn2);   // trial gradient in acc[0 .. d)
     const double actual = f - fn;
-    if (it == 0) delta = fmin(delta, snorm);
+    if (it == 0) delta = uniform_f64(fmin(delta, snorm));
     const double den = fn - f - gs;
     const double alr = den <= 0.0 ? sg3 : fmax(sg1, -0.5 * gs / (den == 0.0 ? 1.0 : den));
     double nd;
@@ -643,7 +845,7 @@ void re_tron_lean_kernel(ReTronArgs a) {
     else if (actual < eta1 * pred) nd = fmax(sg1 * delta, fmin(alr * snorm, sg2 * delta));
     else if (actual < eta2 * pred) nd = fmax(sg1 * delta, fmin(alr * snorm, sg3 * delta));
     else nd = fmax(delta, fmin(alr * snorm, sg3 * delta));
-    delta = nd;
+    delta = uniform_f64(nd);
     const bool accept = actual > eta0 * pred;
     const double f_prev = f;
     if (accept) {
@@ -1688,6 +1890,8 @@ static void lean_launch(const ReTronArgs& a, int n_launch, size_t smem, hipStrea
 }
 
 extern "C" {
+
+const char* pml_build_id() { return pml_build_stamp + 13; }
 
 // Shared memory of one workgroup for entities of at most ``dmax`` coefficients.
 size_t pml_re_tron_smem(int dmax) { return ((size_t)(5 + RE_NW) * dmax + 2 * RE_NW * 8) * sizeof(double); }

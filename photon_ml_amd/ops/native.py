@@ -15,7 +15,7 @@ from typing import Optional
 import numpy as np
 import torch  # noqa: F401  (must precede loading the HIP libraries)
 
-from .build import build_hip, lib_path
+from .build import StaleLibraryError, expected_id, lib_path, verified_path
 
 c_int = ctypes.c_int
 c_double = ctypes.c_double
@@ -77,22 +77,30 @@ _LIBS = {}
 
 
 def _load(name: str, auto_build: bool = True) -> Optional[ctypes.CDLL]:
+    """Load ``libpml_<name>.so``. The in-tree library must carry the build id of the tree's sources
+    (``ops/build.py``): a stale one is rebuilt when hipcc is available and otherwise raises
+    :class:`~photon_ml_amd.ops.build.StaleLibraryError` — it is never loaded. None when the library is missing
+    and cannot be built (CPU-only installs). ``PML_GLM_LIB`` / ``PML_RE_LIB`` name explicit A/B or profiling
+    builds, which are loaded as given."""
     if name in _LIBS:
         return _LIBS[name]
-    path = lib_path("hip", name)
-    if name == "glm" and os.environ.get("PML_GLM_LIB"):   # experiment builds (ops/build.py build_experiment)
-        path = Path(os.environ["PML_GLM_LIB"])
-    if name == "re" and os.environ.get("PML_RE_LIB"):     # A/B builds of the random-effect kernels (profiling)
-        path = Path(os.environ["PML_RE_LIB"])
-    if not path.exists() and auto_build and os.environ.get("PML_NO_AUTOBUILD") != "1":
+    override = {"glm": "PML_GLM_LIB", "re": "PML_RE_LIB"}.get(name)
+    if override and os.environ.get(override):
+        path = Path(os.environ[override])
+        want = None
+    else:
         try:
-            build_hip(name)
-        except Exception:  # pragma: no cover - toolchain missing
-            pass
-    if not path.exists():
-        _LIBS[name] = None
-        return None
+            path = verified_path("hip", name, auto_build=auto_build)
+        except FileNotFoundError:
+            _LIBS[name] = None
+            return None
+        want = expected_id("hip", name)
     lib = ctypes.CDLL(str(path), mode=ctypes.RTLD_GLOBAL)
+    if want is not None:
+        lib.pml_build_id.restype = ctypes.c_char_p
+        got = lib.pml_build_id().decode()
+        if got != want:
+            raise StaleLibraryError(f"{path}: loaded build id {got} != {want} of the tree's sources")
     _LIBS[name] = lib
     return lib
 
@@ -825,6 +833,7 @@ def require_re_lib() -> ctypes.CDLL:
 
 # the lean streaming kernel takes launch classes up to this many coefficients (PML_RE_LEAN=0: never)
 RE_LEAN_DMAX = 1024 if os.environ.get("PML_RE_LEAN", "1") != "0" else 0
+LEAN_MAX_ENTITY_NNZ = 1 << 27          # lean kernel: an entity's values in one 32-bit buffer range (bytes < 2^31)
 
 
 def re_tron_csr(order, row_ptr, col_ptr, nip, lcol, val, y, off, wt, scr, W, f, iters, reason, zout, loss_id: int,
@@ -852,9 +861,12 @@ def re_tron_csr(order, row_ptr, col_ptr, nip, lcol, val, y, off, wt, scr, W, f, 
     assert all(t.dtype == torch.float64 for t in (val, y, off, wt, scr, W, f, zout))
     assert off.numel() == n_rows and wt.numel() == n_rows and zout.numel() == n_rows and scr.numel() >= 4 * n_rows
     assert iters.dtype == reason.dtype == torch.int32
-    assert (dmax % 16 == 0 and 16 <= dmax <= 64) if hessian else dmax % 64 == 0
+    if lean is None:
+        lean = not hessian and dmax <= RE_LEAN_DMAX
+    # lean launches size LDS to the launch's widest entity (a multiple of 8: four workgroups per CU up to 1008)
+    assert (dmax % 16 == 0 and 16 <= dmax <= 64) if hessian else dmax % (8 if lean else 64) == 0
     n_ent = row_ptr.numel() - 1
-    assert col_ptr.numel() == n_ent + 1 and W.numel() == int(col_ptr[-1]) and f.numel() == n_ent
+    assert col_ptr.numel() == n_ent + 1 and f.numel() == n_ent
     if npass is not None:
         assert npass.is_cuda and npass.dtype == torch.int32 and npass.numel() == n_ent
     if os.environ.get("PML_CHECK_KERNEL_INPUTS", "0") == "1" and B:
@@ -862,9 +874,14 @@ def re_tron_csr(order, row_ptr, col_ptr, nip, lcol, val, y, off, wt, scr, W, f, 
         assert int(order.min()) >= 0 and int(order.max()) < n_ent, "re_tron order out of range"
         oe = order.to(torch.int64)
         assert int((col_ptr[oe + 1] - col_ptr[oe]).max()) <= dmax, "entity wider than the launch's LDS class"
-        assert int(row_ptr[-1]) == n_rows and int(nip[-1]) == val.numel(), "row / non-zero ranges inconsistent"
-    if lean is None:
-        lean = not hessian and dmax <= RE_LEAN_DMAX
+        assert W.numel() == int(col_ptr[-1]), "packed coefficients / column ranges inconsistent"
+        nnz = int(nip[-1])
+        assert int(row_ptr[-1]) == n_rows and nnz <= val.numel(), "row / non-zero ranges inconsistent"
+        if lean:
+            # quad row pass (row_pass_v): aligned 4-entry quads, 32-bit buffer ranges per entity
+            assert val.numel() >= (nnz + 3) // 4 * 4, "lean kernel needs entry arrays padded to 4"
+            e_nnz = nip[row_ptr[oe + 1]] - nip[row_ptr[oe]]
+            assert int(e_nnz.max()) < LEAN_MAX_ENTITY_NNZ, "entity too long for the lean kernel's buffer ranges"
     args = [order.data_ptr(), B, row_ptr.data_ptr(), col_ptr.data_ptr(), nip.data_ptr(), lcol.data_ptr(),
             val.data_ptr(), y.data_ptr(), off.data_ptr(), wt.data_ptr(), scr.data_ptr(), n_rows, W.data_ptr(),
             f.data_ptr(), iters.data_ptr(), reason.data_ptr(), zout.data_ptr(),

@@ -42,6 +42,22 @@ RES_ROW_NNZ = 64
 RES_KMAX = int(os.environ.get("PML_RE_RES_KMAX", "128"))
 
 
+def _pad4(t: torch.Tensor) -> torch.Tensor:
+    """``t`` followed by 4 zero entries (the lean kernel's quad loads may touch up to 3 entries past a row)."""
+    out = torch.zeros(t.numel() + 4, dtype=t.dtype, device=t.device)
+    out[:t.numel()] = t
+    return out
+
+
+def _launch_dmax(dm: int, de: torch.Tensor, is_h: bool) -> int:
+    """LDS width of a launch: the class width, except that lean launches (dm <= 1024) take their widest entity
+    rounded up to 8 — a 1008-wide lean workgroup needs 40.8 KB of LDS, so FOUR fit a CU (1024 wide: three)."""
+    from ..ops.native import RE_LEAN_DMAX
+    if is_h or dm > RE_LEAN_DMAX:
+        return dm
+    return min(dm, (int(de.max()) + 7) // 8 * 8)
+
+
 def fused_enabled() -> bool:
     return os.environ.get("PML_RE_FUSED", "1") != "0"
 
@@ -104,8 +120,10 @@ class EntityTronBatch:
             # the kernel indexes LDS vectors of d_e entries with these
             assert int(lcol.min()) >= 0 and bool((lcol < de[nnz_ent]).all()), "entity-local column out of range"
         del nnz_ent, pos
-        self.lcol = lcol.to(torch.int16)                 # read as uint16 by the kernel (d_e <= 2048)
-        self.nip, self.val = nip, val
+        # read as uint16 by the kernels (d_e <= 2048); the lean kernel reads aligned 4-entry quads, so both entry
+        # arrays carry 4 slack entries past the last row
+        self.lcol = _pad4(lcol.to(torch.int16))
+        self.nip, self.val = nip, _pad4(val)
         self.y, self.w = seg.y[row_sel].contiguous(), seg.w[row_sel].contiguous()
         self.n_rows = n_rows
         self.nnz = nnz
@@ -118,6 +136,8 @@ class EntityTronBatch:
         if nnz and int(ent_nnz.max()) >= (1 << 31):
             raise ValueError("an entity of the fused batch has >= 2^31 non-zeros (32-bit kernel offsets)")
         self.launches = []
+        from ..ops.native import LEAN_MAX_ENTITY_NNZ
+        self.lean_ok = bool(int(ent_nnz.max()) < LEAN_MAX_ENTITY_NNZ) if nnz else True
         hess = de <= HESS_DMAX
         # register-resident tasks (one persistent launch): clusters (k > 1 workgroups) first, largest first
         self.res = None
@@ -155,7 +175,8 @@ class EntityTronBatch:
                 if idx.numel() == 0:
                     continue
                 order = idx[torch.argsort(ent_nnz[idx], descending=True, stable=True)]
-                self.launches.append((dm, order.to(torch.int32).contiguous(), bool(is_h)))
+                self.launches.append((_launch_dmax(dm, de[idx], is_h or not self.lean_ok),
+                                      order.to(torch.int32).contiguous(), bool(is_h)))
 
     def solve(self, loss, l2: float, W0: Optional[torch.Tensor], offsets: torch.Tensor, tol: float, max_iter: int,
               max_fail: int = 5, max_cg: int = 20) -> FusedResult:
@@ -183,7 +204,7 @@ class EntityTronBatch:
         for dm, order, is_h in self.launches:
             re_tron_csr(order, self.row_ptr, self.col_ptr, self.nip, self.lcol, self.val, self.y, off, self.w,
                         self.scr, W, f, iters, reason, z, loss.loss_id, l2, tol, max_iter, max_fail, max_cg, dm,
-                        hessian=is_h, gsc=self.gsc)
+                        hessian=is_h, gsc=self.gsc, lean=None if self.lean_ok else False)
         if err is not None and int(err.item()) != 0:
             raise RuntimeError("register-resident random-effect TRON: a workgroup cluster wait timed out "
                                "(results invalid); rerun with PML_RE_RESIDENT=0")
@@ -206,15 +227,16 @@ class DenseEntityTronBatch:
         self.B, self.n, self.d = B, n, d
         ar = lambda k, step: torch.arange(k + 1, dtype=torch.int64, device=dev) * step
         self.row_ptr, self.col_ptr, self.nip = ar(B, n), ar(B, d), ar(B * n, d)
-        self.lcol = torch.arange(d, dtype=torch.int16, device=dev).repeat(B * n)
-        self.val = X.to(torch.float64).reshape(-1).contiguous()
+        self.lcol = _pad4(torch.arange(d, dtype=torch.int16, device=dev).repeat(B * n))
+        self.val = _pad4(X.to(torch.float64).reshape(-1))
         self.y = y.to(torch.float64).reshape(-1).contiguous()
         self.w = w.to(torch.float64).reshape(-1).contiguous()
         self.scr = torch.empty(4 * max(B * n, 1), dtype=torch.float64, device=dev)
         hess = d <= HESS_DMAX
         classes = _HESS_CLASSES if hess else _CLASSES
         dm = next(c for c in classes if c >= d)
-        self.launch = (dm, torch.arange(B, dtype=torch.int32, device=dev), hess)
+        self.launch = (_launch_dmax(dm, torch.tensor([d]), hess), torch.arange(B, dtype=torch.int32, device=dev),
+                       hess)
 
     def solve(self, loss, l2: float, W0: torch.Tensor, offsets: torch.Tensor, tol: float, max_iter: int,
               max_fail: int = 5, max_cg: int = 20) -> FusedResult:

@@ -37,10 +37,13 @@ a = torch.randint(0, d - 1, (N, 1), generator=g, device=dev)
 s_ = strides[torch.randint(0, strides.numel(), (N, 1), generator=g, device=dev)]
 cols = (a + torch.arange(NNZ - 1, device=dev)[None, :] * s_) % (d - 1)
 cols, _ = torch.sort(cols, dim=1)
-lcol = torch.cat([cols, torch.full((N, 1), d - 1, device=dev)], 1).reshape(-1).to(torch.int16)
+lcol = torch.zeros(N * NNZ + 4, dtype=torch.int16, device=dev)      # + 4: the lean kernel's quad loads
+lcol[:N * NNZ] = torch.cat([cols, torch.full((N, 1), d - 1, device=dev)], 1).reshape(-1).to(torch.int16)
 del cols
-val = torch.randn(N * NNZ, generator=g, device=dev, dtype=torch.float64)
-val.view(N, NNZ)[:, -1] = 1.0
+val = torch.zeros(N * NNZ + 4, dtype=torch.float64, device=dev)
+val[:N * NNZ] = torch.randn(N * NNZ, generator=g, device=dev, dtype=torch.float64)
+val[:N * NNZ].view(N, NNZ)[:, -1] = 1.0
+DMAX = int(os.environ.get("PML_BENCH_DMAX", "1008"))     # lean launches: widest entity rounded up to 8
 nip = torch.arange(N + 1, dtype=torch.int64, device=dev) * NNZ
 y = (torch.rand(N, generator=g, device=dev) < 0.4).double()
 off = torch.zeros(N, dtype=torch.float64, device=dev)
@@ -83,7 +86,7 @@ def run(kernel, order, reps=3):
     else:
         def call(np_=None):
             re_tron_csr(order, row_ptr, col_ptr, nip, lcol, val, y, off, wt, scr, W, f, it, rc, z, 0, 1.0, 1e-12, 10,
-                        5, 20, 1024, npass=np_, lean=kernel == "lean")
+                        5, 20, DMAX if kernel == "lean" else 1024, npass=np_, lean=kernel == "lean")
             return None
     err = call(npass)
     torch.cuda.synchronize()
