@@ -576,6 +576,7 @@ class RandomEffectCoordinate(Coordinate):
             side.wait_stream(main)                 # offsets / warm starts written on the main stream
             for t in rs_prep:
                 t.record_stream(side)              # allocated on the main stream, read on the side stream
+        fres = None
         if fused is not None:
             with Timed(f"RE {self.coordinate_id}: fused primal solve", log, logging.DEBUG):
                 fres = fused.solve(self.loss, l2, None if W0 is None else W0[fused.cols], seg.o[fused.rows],
@@ -609,10 +610,14 @@ class RandomEffectCoordinate(Coordinate):
             z.index_copy_(0, sub.rows, sub.seg.glm.matvec(res.W))
             sum_sq += res.W.square().sum()
             parts["sub"] = res.W
+        if fres is not None and rs_out is None:
+            fres.check_error()
         if rs_out is not None:
             if overlap:
                 main.wait_stream(side)
             rres, z_rs, ss_rs = rs_out
+            if fres is not None:
+                fres.check_error()                 # after the side-stream launch was queued
             iters.index_copy_(0, rs.ents, rres.iters)
             reasons.index_copy_(0, rs.ents, rres.reason)
             z += z_rs

@@ -122,5 +122,17 @@ def main(argv=None) -> int:
     return 0
 
 
+def indexing_main(argv=None) -> int:
+    """``feature-indexing`` launcher: the reference's FeatureIndexingDriver
+    (photon-client/.../index/FeatureIndexingDriver.scala:298-320) = ``feature_tools index``."""
+    return main(["index"] + list(sys.argv[1:] if argv is None else argv))
+
+
+def bags_main(argv=None) -> int:
+    """``feature-bags`` launcher: the reference's NameAndTermFeatureBagsDriver
+    (photon-client/.../data/avro/NameAndTermFeatureBagsDriver.scala:198-220) = ``feature_tools bags``."""
+    return main(["bags"] + list(sys.argv[1:] if argv is None else argv))
+
+
 if __name__ == "__main__":
     sys.exit(main())

@@ -75,6 +75,14 @@ class FusedResult:
     iters: torch.Tensor      # [B]
     reason: torch.Tensor     # [B] reason codes (batched.REASON_CODES)
     z: torch.Tensor          # per batch row: x_i . w of the solution (no offset)
+    err: Optional[torch.Tensor] = None   # device error flag of the register-resident launch (check_error)
+
+    def check_error(self) -> None:
+        """Raise if the register-resident launch reported a cluster wait timeout. Reads the device flag (a host
+        synchronisation with the launch), so callers run it only after queueing their concurrent work."""
+        if self.err is not None and int(self.err.item()) != 0:
+            raise RuntimeError("register-resident random-effect TRON: a workgroup cluster wait timed out "
+                               "(results invalid); rerun with PML_RE_RESIDENT=0")
 
 
 class EntityTronBatch:
@@ -205,11 +213,10 @@ class EntityTronBatch:
             re_tron_csr(order, self.row_ptr, self.col_ptr, self.nip, self.lcol, self.val, self.y, off, self.w,
                         self.scr, W, f, iters, reason, z, loss.loss_id, l2, tol, max_iter, max_fail, max_cg, dm,
                         hessian=is_h, gsc=self.gsc, lean=None if self.lean_ok else False)
-        if err is not None and int(err.item()) != 0:
-            raise RuntimeError("register-resident random-effect TRON: a workgroup cluster wait timed out "
-                               "(results invalid); rerun with PML_RE_RESIDENT=0")
         self.W = W
-        return FusedResult(W, f, iters.to(torch.long), reason.to(torch.long), z)
+        # the error flag stays on the device: reading it here would wait for the whole launch before the caller
+        # can queue concurrent work (the row-space side stream); callers call FusedResult.check_error() later
+        return FusedResult(W, f, iters.to(torch.long), reason.to(torch.long), z, err)
 
 
 class DenseEntityTronBatch:

@@ -169,7 +169,6 @@ class RowSpaceBatch:
                                torch.full_like(valid, -1, dtype=torch.long))
             geo.append((e, n, valid, rows, torch.zeros(e.numel(), n, n, dtype=torch.float64, device=dev)))
         csr = _canonical_csr(csr, dev) if dev.type == "cuda" else None
-        self._csr = csr                     # the per-entity back-map kernel reads it (to_primal)
         # (class, members) whose Gram columns come from indicator passes: all of them without a canonical device
         # CSR, else only the entities too wide for seg_gram_kernel's LDS image (d_e > SEG_GRAM_DMAX)
         need_ind = []
@@ -240,6 +239,9 @@ class RowSpaceBatch:
         # indexing, which costs a nonzero pass and a host synchronisation per call)
         self.vslot = torch.nonzero(self.valid).squeeze(1)
         self.vrow = self.rows[self.vslot]
+        # the per-entity back-map (to_primal) reads only the handled entities' rows: a compact copy of them, not
+        # the whole segmented CSR (which the dataset frees once the sub-problems are built)
+        self._primal_csr = self._compact_csr(csr) if csr is not None else None
         self._z = None            # (beta, packed margins L beta) written by the fused solve
         # the primal model (to_primal: one transpose pass over the block-diagonal data) is read once per model:
         # build its shard-wide one-launch transpose tables here, with the rest of the setup, instead of running
@@ -247,6 +249,41 @@ class RowSpaceBatch:
         glm = getattr(seg, "glm", None)
         if glm is not None and getattr(glm, "_multi_t", "unset") == "unset" and hasattr(glm, "_build_multi_t"):
             glm._build_multi_t()
+
+    def _compact_csr(self, csr):
+        """(ents, row_ptr, col_ptr, nip, pos, val, rows) for ``rs_primal`` over the handled entities' rows only,
+        or None when an entity is too wide for its LDS accumulator. Entity k of the compact list is addressed as
+        index 2k of interleaved range arrays: ``row_ptr[2k:2k+2]`` its compact rows, ``col_ptr[2k:2k+2]`` its
+        coefficient range in the packed primal vector; ``rows`` maps compact rows back to segmented rows."""
+        from ..ops.native import RS_PRIMAL_DMAX
+        seg = self.seg
+        if self.B == 0:
+            return None
+        ents = self.ents
+        dev = ents.device
+        c_lo, c_hi = seg.col_ptr[ents], seg.col_ptr[ents + 1]
+        if bool(((c_hi - c_lo) > RS_PRIMAL_DMAX).any()):
+            return None
+        r_lo = seg.row_ptr[ents]
+        ne = seg.row_ptr[ents + 1] - r_lo
+        rcum = torch.zeros(self.B + 1, dtype=torch.int64, device=dev)
+        torch.cumsum(ne, 0, out=rcum[1:])
+        nr = int(rcum[-1])
+        rows = torch.repeat_interleave(r_lo - rcum[:-1], ne, output_size=nr) + torch.arange(nr, device=dev)
+        nip, pos, val = csr
+        k0 = nip[rows]
+        nk = nip[rows + 1] - k0
+        nip_c = torch.zeros(nr + 1, dtype=torch.int64, device=dev)
+        torch.cumsum(nk, 0, out=nip_c[1:])
+        nnz = int(nip_c[-1])
+        ent_idx = torch.repeat_interleave(k0 - nip_c[:-1], nk, output_size=nnz) + torch.arange(nnz, device=dev)
+        row_ptr = torch.stack([rcum[:-1], rcum[1:]], 1).reshape(-1)
+        col_ptr = torch.stack([c_lo, c_hi], 1).reshape(-1)
+        # trailing entries: the wrapper's range checks read the last element as the total
+        row_ptr = torch.cat([row_ptr, rcum[-1:]])
+        col_ptr = torch.cat([col_ptr, seg.col_ptr[-1:]])
+        ents2 = torch.arange(self.B, dtype=torch.int64, device=dev) * 2
+        return ents2, row_ptr, col_ptr, nip_c, pos[ent_idx], val[ent_idx], rows
 
     def _slots(self, per_row: torch.Tensor) -> torch.Tensor:
         """Packed per-slot values of a per-row vector (0 in padding slots, whose row index is -1)."""
@@ -268,20 +305,16 @@ class RowSpaceBatch:
         if self.classes:
             alpha = torch.cat([_bmv(c.Linv, c.view(beta), trans=True).reshape(-1) for c in self.classes])  # L^-T b
             r[self.vrow] = alpha[self.vslot]
-        csr = getattr(self, "_csr", None)
-        if csr is not None and self.classes:
-            # per-entity back-map over the handled entities' rows only (rs_primal_kernel, one wave per entity);
-            # the shard-wide transpose pass read every entity's rows (9.0 ms on game5pl)
-            from ..ops.native import RS_PRIMAL_DMAX, rs_primal
-            seg = self.seg
-            if getattr(self, "_primal_ents", None) is None:
-                d_e = seg.col_ptr[self.ents + 1] - seg.col_ptr[self.ents]
-                self._primal_ents = (self.ents[d_e <= RS_PRIMAL_DMAX].contiguous(), bool((d_e > RS_PRIMAL_DMAX).any()))
-            ents, wide = self._primal_ents
-            if not wide:
-                W = torch.zeros(int(seg.col_ptr[-1]), dtype=torch.float64, device=beta.device)
-                rs_primal(ents, seg.row_ptr, seg.col_ptr, csr[0], csr[1], csr[2], r, W)
-                return W
+        pc = getattr(self, "_primal_csr", None)
+        if pc is not None and self.classes:
+            # per-entity back-map over the handled entities' rows only (rs_primal_kernel, one wave per entity, on
+            # the compact copy of their rows); the shard-wide transpose pass read every entity's rows (9.0 ms on
+            # game5pl)
+            from ..ops.native import rs_primal
+            ents2, row_ptr, col_ptr, nip, pos, val, rows = pc
+            W = torch.zeros(int(self.seg.col_ptr[-1]), dtype=torch.float64, device=beta.device)
+            rs_primal(ents2, row_ptr, col_ptr, nip, pos, val, r[rows].contiguous(), W)
+            return W
         return self.seg.glm.rmatvec(r, build_multi=False)     # once per update: no shard-wide tables
 
     def margins(self, beta: torch.Tensor) -> torch.Tensor:

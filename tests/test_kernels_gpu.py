@@ -256,15 +256,15 @@ def test_tl_multi_transpose_engages_for_column_windows(precision):
     torch.testing.assert_close(out[1], ref, rtol=tol, atol=tol * float(ref.abs().max()))
 
 
-@pytest.mark.parametrize("pipe", [0, 1, 2])
+@pytest.mark.parametrize("pipe", [0, pytest.param(1, marks=pytest.mark.experiment),
+                                  pytest.param(2, marks=pytest.mark.experiment)])
 @pytest.mark.parametrize("precision", ["f64", "bf16"])
 def test_tl_stream_variants(pipe, precision):
     """Every stream pipeline variant (two-slot, three-stage, two-slot 8 entries/lane) x per-chunk / shard-wide
-    launches against the fp64 reference."""
+    launches against the fp64 reference (the non-production pipelines exist only in the experiment build:
+    ``experiment``-marked, collected only when PML_GLM_LIB names that build)."""
     from photon_ml_amd.ops.device import DeviceGLMData
-    from photon_ml_amd.ops.native import configure, tl_experiment_build
-    if pipe and not tl_experiment_build():
-        pytest.skip("non-production stream pipelines exist only in the experiment build")
+    from photon_ml_amd.ops.native import configure
     data = make_data(n=7000, d=900, density=0.01, seed=6)
     if precision == "bf16":
         data = _round_bf16(data)
@@ -341,20 +341,20 @@ def test_batched_small_gemv_and_hv_match_torch(n):
     torch.testing.assert_close(batched_hv(A, dw, x, 0.7), hv, rtol=1e-12, atol=1e-11)
 
 
+_RS_SIZES = [("LOGISTIC", 20), ("POISSON", 7), ("SQUARED", 33), ("LOGISTIC", 64), ("LOGISTIC", 1)]
+_RS_SIZES_DPP = [("LOGISTIC", 4), ("POISSON", 8), ("SQUARED", 11), ("LOGISTIC", 16), ("POISSON", 18),
+                 ("LOGISTIC", 24), ("SQUARED", 29), ("LOGISTIC", 32)]
+
+
 @pytest.mark.gpu
-@pytest.mark.parametrize("loss_name,n", [("LOGISTIC", 20), ("POISSON", 7), ("SQUARED", 33), ("LOGISTIC", 64),
-                                         ("LOGISTIC", 1), ("LOGISTIC", 4), ("POISSON", 8), ("SQUARED", 11),
-                                         ("LOGISTIC", 16), ("POISSON", 18), ("LOGISTIC", 24), ("SQUARED", 29),
-                                         ("LOGISTIC", 32)])
+@pytest.mark.parametrize("loss_name,n,variant", [(l, n, v) for v in range(7) for l, n in _RS_SIZES]
+                         + [(l, n, v) for v in range(3, 7) for l, n in _RS_SIZES_DPP])
 @pytest.mark.parametrize("warm", [False, True])
-@pytest.mark.parametrize("variant", [0, 1, 2, 3, 4, 5, 6])
 def test_fused_row_space_tron_matches_batched_tron(loss_name, n, warm, variant):
     """rs_tron_kernel (whole per-problem TRON in one kernel) vs the vectorised batched TRON of
     optimization/batched.py on the same dense problems (fp64): same solutions, objective and iteration counts.
     Every matrix-vector / group-sum variant of the kernel (bpermute shuffles, LDS vector slot, DPP sums) and
     the DPP64-broadcast kernel of variant 3 at every padded size K (4 .. 32; n < K pads with zeros)."""
-    if variant < 3 and n not in (20, 7, 33, 64, 1):
-        pytest.skip("sizes of the variant-3 kernel classes")
     import os
     from photon_ml_amd.function import losses
     from photon_ml_amd.ops.native import require_glm_lib, rs_tron
@@ -482,8 +482,7 @@ def test_tron_margin_space_trial_on_device(precision, layout, norm):
 @pytest.mark.gpu
 @pytest.mark.parametrize("deep", [1, 2])
 @pytest.mark.parametrize("precision", ["bf16", "f64"])
-@pytest.mark.skipif("not __import__('photon_ml_amd.ops.native', fromlist=['x']).tl_experiment_build()",
-                    reason="A/B pipeline variants exist only in the experiment build (PML_GLM_LIB=libpml_glm_abl.so)")
+@pytest.mark.experiment           # A/B pipeline variants exist only in the experiment build (PML_GLM_LIB)
 def test_deep_pipeline_variants_are_bitwise_equal(deep, precision):
     """Deeper software pipelines of the interleaved / narrow streams (more rounds of stream and gathers in flight
     per wave) keep each wave's accumulation order: bitwise identical value, gradient and Hessian products."""
