@@ -233,7 +233,8 @@ def main():
 def game_extra(dev, rank: int, world: int) -> dict:
     """BASELINE.json's second metric (GAME coordinate-descent iterations/sec, config 5) on the power-law entity
     preset, timed inside this run (bench_game.run: data generated on the device, 2 warmup + 3 timed sweeps, the
-    trained model materialised inside the timed region; entity-sharded random effects when world > 1). Timed twice
+    trained model materialised inside the timed region; entity-sharded random effects when world > 1; the cold
+    first warm-up sweep, every model from zero, is reported next to the warm mean). Timed twice
     on the same data: bf16 fixed-effect feature storage (``game5pl_*``) and fp64, the reference's precision
     (``game5pl_f64_*``). Failures are reported, never fatal to the GLM line."""
     import gc
@@ -257,7 +258,9 @@ def game_extra(dev, rank: int, world: int) -> dict:
             torch.cuda.empty_cache()
         out.update({f"{pre}_sweeps_per_sec": g["value"], f"{pre}_ms_per_sweep": g["ms_per_step"],
                     f"{pre}_sweep_ms_min": g["sweep_ms_min"], f"{pre}_sweep_ms_median": g["sweep_ms_median"],
-                    f"{pre}_coordinate_ms": g["coordinate_ms"]})
+                    f"{pre}_coordinate_ms": g["coordinate_ms"],
+                    f"{pre}_cold_first_sweep_ms": g.get("cold_first_sweep_ms"),
+                    f"{pre}_cold_first_sweep_coordinate_ms": g.get("cold_first_sweep_coordinate_ms")})
         if g.get("route_s"):
             out[f"{pre}_route_s"] = g["route_s"]
         if prec == "bf16":

@@ -84,6 +84,9 @@ def build_parser() -> argparse.ArgumentParser:
     ap.add_argument("--seed", type=int, default=11)
     ap.add_argument("--rehearsal", action="store_true",
                     help="allow more ranks than physical devices (record: rehearsal true, n_gpus = devices)")
+    ap.add_argument("--no-placement", action="store_true",
+                    help="multi-rank: route the random-effect rows per coordinate instead of placing every row on "
+                         "its entity owner at ingest")
     ap.add_argument("--log-level", default="WARNING",
                     help="framework log level (DEBUG shows the per-phase timings of the random-effect update)")
     return ap
@@ -179,6 +182,17 @@ def run(args, dev, rank: int = 0, world: int = 1, data=None, t_data: float = 0.0
 
     if data is None:
         data, t_data = make_data(args, dev, rank)
+    t_place = None
+    if is_dist() and not args.no_placement:
+        # entity-aligned placement at ingest (parallel/placement.py): every row moves once to the owner of its
+        # entity, the fixed effect trains on the placed rows, the random-effect coordinate routes nothing per update
+        from photon_ml_amd.parallel.placement import place_rows_by_entity
+        tp = time.time()
+        data = place_rows_by_entity(data, "entityId", dev)
+        if torch.cuda.is_available():
+            torch.cuda.synchronize()
+        t_place = all_reduce_scalar(time.time() - tp, "max")
+        log(f"rows placed on their entity owners in {t_place:.1f}s ({data.placement.rows_moved} rows moved)")
     t0 = time.time()
     fe_cfg = GLMOptimizationConfiguration(OptimizerConfig("LBFGS", args.fe_iters, 1e-12),
                                           RegularizationContext("L2"), 1.0, args.fe_down_sampling_rate)
@@ -207,10 +221,16 @@ def run(args, dev, rank: int = 0, world: int = 1, data=None, t_data: float = 0.0
     # device-complete times; one stamp per sweep (after its last coordinate)
     cb = lambda rec: sweep_end.append(time.perf_counter()) if rec["coordinate"] == list(coords)[-1] else None
     cd = CoordinateDescent(coords, train_eval, score_device=dev, event_callback=cb)
+    barrier()
+    t_cold = time.perf_counter()
     model, _ = cd.run(args.warmup)
     if torch.cuda.is_available():
         torch.cuda.synchronize()
     barrier()
+    # the COLD first sweep (every model from zero: the random effects run the most TRON iterations; first-use
+    # setup included) — what a one-iteration GAME run (the reference default) costs; warm-up sweep 1
+    cold_ms = all_reduce_scalar(1000.0 * (sweep_end[0] - t_cold), "max") if sweep_end else None
+    cold_coord_ms = {rec["coordinate"]: 1000.0 * rec["seconds"] for rec in cd.history[:n_coords]}
     fe_gd = coords["global"].glm_data
     fe_pass0 = (getattr(fe_gd, "n_fwd", 0), getattr(fe_gd, "n_t", 0))
     sweep_end.clear()
@@ -259,7 +279,8 @@ def run(args, dev, rank: int = 0, world: int = 1, data=None, t_data: float = 0.0
                 f"{fb:.3f}, transpose items {ft:.3f}")
         for rec in cd.history[-2 * args.steps:]:
             log(f"  iteration {rec.get('iteration')} coordinate {rec['coordinate']}: {rec['seconds']:.3f}s")
-    del cd, coords, model, train_eval
+    route_coords = {k: c for k, c in coords.items() if hasattr(c, "routed_bytes")}
+    del cd, model, train_eval
     return {
         "metric": "GAME coord-descent iters/sec (fixed + per-entity random effect)",
         "value": args.steps / elapsed,
@@ -270,6 +291,8 @@ def run(args, dev, rank: int = 0, world: int = 1, data=None, t_data: float = 0.0
         "warmup": args.warmup,
         "ms_per_step": 1000.0 * elapsed / args.steps,
         "sweep_ms_min": min(sweeps_ms) if sweeps_ms else None,
+        "cold_first_sweep_ms": cold_ms,
+        "cold_first_sweep_coordinate_ms": cold_coord_ms,
         "sweep_ms_median": float(np.median(sweeps_ms)) if sweeps_ms else None,
         "higher_is_better": True,
         "scaling": "weak",
@@ -288,6 +311,9 @@ def run(args, dev, rank: int = 0, world: int = 1, data=None, t_data: float = 0.0
         "data_generation_s": t_data,
         "coordinate_build_s": t_build,
         **({"route_s": route_s} if route_s else {}),
+        **({"placement_s": t_place} if t_place is not None else {}),
+        "routed_bytes_per_update": {k: int(all_reduce_scalar(float(getattr(c, "routed_bytes", 0)), "max"))
+                                    for k, c in route_coords.items()},
     }
 
 

@@ -792,15 +792,24 @@ class ShardedRandomEffectCoordinate(Coordinate):
         re_type, shard = data_config.random_effect_type, data_config.feature_shard_id
         ids = np.asarray(data.id_tags[re_type])
         self.route_times = {}
-        t0 = time.perf_counter()
-        # entity keys, the partitioner's histograms and the routing permutation all on the device (C8 / C9)
-        keys = entity_keys(ids, self.device)
-        self.partitioner = EntityPartitioner.build_t(keys)
-        self.router = RowRouter(self.partitioner.owner_t(keys))
-        del keys
-        self._sync()
-        self.route_times["partition"] = time.perf_counter() - t0
-        self.recv_data = self._route(data, self.router, ids, self.route_times)
+        self.routed_bytes = 0            # bytes of residual / score vectors this rank sent away, last update
+        placement = getattr(data, "placement", None)
+        if placement is not None and placement.re_type == re_type:
+            # rows were placed on their entity owners at ingest (parallel/placement.py): this is the PRIMARY
+            # coordinate, every row is already local — no routing at build and none per update
+            self.partitioner = placement.partitioner
+            self.router = None
+            self.recv_data = data
+        else:
+            t0 = time.perf_counter()
+            # entity keys, the partitioner's histograms and the routing permutation all on the device (C8 / C9)
+            keys = entity_keys(ids, self.device)
+            self.partitioner = EntityPartitioner.build_t(keys)
+            self.router = RowRouter(self.partitioner.owner_t(keys))
+            del keys
+            self._sync()
+            self.route_times["partition"] = time.perf_counter() - t0
+            self.recv_data = self._route(data, self.router, ids, self.route_times)
         self.inner = RandomEffectCoordinate(coordinate_id, self.recv_data, data_config, opt_config, task,
                                             compute_variance, device, dtype)
         self._val_cache = {}
@@ -847,14 +856,33 @@ class ShardedRandomEffectCoordinate(Coordinate):
     def initialize_model(self):
         return self.inner.initialize_model()
 
+    @property
+    def placed(self) -> bool:
+        """True for the primary coordinate of entity-placed data (identity routing)."""
+        return self.router is None
+
+    def _off_rank_bytes(self) -> int:
+        """Bytes of one fp64 per-row vector this rank sends to other ranks through the router."""
+        if self.router is None:
+            return 0
+        from ..parallel.dist import rank
+        return 8 * int(sum(self.router.send_counts) - self.router.send_counts[rank()])
+
     def update_model(self, model, partial_score: Optional[torch.Tensor] = None):
         # partial scores go to the entity owners on the device (no host staging under RCCL, see RowRouter)
-        p = None if partial_score is None else self.router.forward(
-            partial_score.detach().to(self.device, torch.float64))
+        self.routed_bytes = 0
+        if partial_score is None or self.router is None:
+            p = None if partial_score is None else partial_score.detach().to(self.device, torch.float64)
+        else:
+            p = self.router.forward(partial_score.detach().to(self.device, torch.float64))
+            self.routed_bytes += self._off_rank_bytes()
         return self.inner.update_model(model, p)
 
     def score(self, model) -> torch.Tensor:
         s = self.inner.score(model).detach().to(self.device, torch.float64)
+        if self.router is None:
+            return s
+        self.routed_bytes += self._off_rank_bytes()
         return self.router.backward(s)
 
     def score_validation(self, model, vdata: GameData) -> torch.Tensor:

@@ -112,6 +112,14 @@ class GameEstimator:
         self.validation_evaluators = [e if isinstance(e, str) else e.name for e in evs]
         return self
 
+    def set_entity_placement(self, coordinate: Optional[str] = "auto"):
+        """Multi-GPU only: place every training row on the owner of its entity in one random-effect coordinate at
+        the start of ``fit`` (parallel/placement.py), so that coordinate needs no per-update routing and the fixed
+        effects train on the placed rows. ``"auto"``: the first random-effect coordinate of the update sequence;
+        None: no placement (every random-effect coordinate routes its rows)."""
+        self.entity_placement = coordinate
+        return self
+
     def set_warm_start(self, b: bool):
         self.use_warm_start = bool(b)
         return self
@@ -155,6 +163,22 @@ class GameEstimator:
                                                     self.compute_variance, self.device, self.precision)
         return coords
 
+    def _place(self, data: GameData, seq) -> GameData:
+        """Entity-aligned placement of the training rows (see :meth:`set_entity_placement`)."""
+        want = getattr(self, "entity_placement", "auto")
+        if not is_dist() or want is None:
+            return data
+        re_cids = [c for c in seq if isinstance(self.coordinate_data_configurations[c], RandomEffectDataConfiguration)]
+        cid = re_cids[0] if want == "auto" and re_cids else want
+        if cid not in re_cids:
+            return data
+        from ..parallel.placement import place_rows_by_entity
+        re_type = self.coordinate_data_configurations[cid].random_effect_type
+        if getattr(getattr(data, "placement", None), "re_type", None) == re_type:
+            return data
+        dev = self.device if self.device is not None else default_device()
+        return place_rows_by_entity(data, re_type, dev)
+
     def _validation_evaluators(self, validation: GameData):
         names = self.validation_evaluators or [default_validation_evaluator(self.training_task)]
         return [build_evaluator(parse_evaluator_type(n), validation.response, validation.offsets, validation.weights,
@@ -169,6 +193,7 @@ class GameEstimator:
             missing = [c for c in seq if c not in cfg]
             if missing:
                 raise ValueError(f"optimization configuration missing coordinates {missing}")
+        data = self._place(data, seq)
         self.coordinates = self._build_coordinates(data, configurations[0], seq)
         train_eval = build_evaluator(training_loss_evaluator_type(self.training_task), data.response, data.offsets,
                                      data.weights)

@@ -312,6 +312,8 @@ class DeviceGLMData(GLMComputable):
         if dev.type == "cuda" and n and resolve_layout(layout, d, chunk_rows) == "tiled":
             return DeviceGLMData._from_labeled_device(x, data, dev, precision, chunk_rows, relabel, item_entries,
                                                       col_windows)
+        if hasattr(x, "to_scipy"):                      # DeviceCSR on the host-side (segmented) build path
+            x = x.to_scipy()
         old_of_new = None
         from ..parallel.dist import is_dist
         shared = relabel and is_dist() and not col_windows
@@ -384,9 +386,12 @@ class DeviceGLMData(GLMComputable):
         relabel, the chunking, the column windows and the layout sorts all run on the device (the host path sliced
         the CSR per chunk with scipy: 6.7 of 14.6 s at GAME config 5)."""
         n, d = x.shape
-        indptr = torch.from_numpy(np.ascontiguousarray(x.indptr, dtype=np.int64)).to(dev)
-        col = torch.from_numpy(np.ascontiguousarray(x.indices)).to(dev).to(torch.int64)
-        val = torch.from_numpy(np.ascontiguousarray(x.data)).to(dev)
+        if isinstance(x.indptr, torch.Tensor):        # a DeviceCSR (entity-placed / routed rows): no host copy
+            indptr, col, val = x.indptr.to(dev), x.indices.to(dev).to(torch.int64), x.data.to(dev)
+        else:
+            indptr = torch.from_numpy(np.ascontiguousarray(x.indptr, dtype=np.int64)).to(dev)
+            col = torch.from_numpy(np.ascontiguousarray(x.indices)).to(dev).to(torch.int64)
+            val = torch.from_numpy(np.ascontiguousarray(x.data)).to(dev)
         old_of_new = None
         from ..parallel.dist import is_dist
         shared = relabel and is_dist() and not col_windows

@@ -64,6 +64,66 @@ def game_worker(rank, world, port, out):
         dist.destroy_process_group()
 
 
+def placed_worker(rank, world, port, out):
+    """Entity-aligned placement (parallel/placement.py) vs per-update routing: (a) the primary random-effect
+    coordinate alone on the same partial scores — bitwise-equal models and scores, zero routed bytes; (b) a whole
+    GAME fit with and without placement."""
+    _init(rank, world, port)
+    import torch
+    from photon_ml_amd.algorithm.coordinates import ShardedRandomEffectCoordinate
+    from photon_ml_amd.data.game_data import generate_game_data
+    from photon_ml_amd.data.random_effect import FixedEffectDataConfiguration, RandomEffectDataConfiguration
+    from photon_ml_amd.estimators.game_estimator import GameEstimator
+    from photon_ml_amd.optimization.config import (GLMOptimizationConfiguration, OptimizerConfig,
+                                                   RegularizationContext)
+    from photon_ml_amd.parallel.placement import place_rows_by_entity
+    data, _ = generate_game_data(n_rows=3000, n_users=40, n_items=25, seed=31, task="LOGISTIC_REGRESSION")
+    tr = data.subset(np.arange(2400))
+    tr_l = tr.subset(np.arange(rank, tr.n_rows, world))
+    cfg = GLMOptimizationConfiguration(OptimizerConfig("TRON", 50, 1e-10), RegularizationContext("L2"), 1.0)
+    dc = RandomEffectDataConfiguration("userId", "user")
+    placed = place_rows_by_entity(tr_l, "userId", "cpu")
+    assert placed.placement.re_type == "userId"
+    # partial scores per ORIGINAL row (deterministic function of the uid), carried to the placed rows by uid
+    ps_of = lambda d: torch.from_numpy(np.sin(d.uids.astype(np.float64)) * 0.3)
+    res = {}
+    for name, d in (("routed", tr_l), ("placed", placed)):
+        c = ShardedRandomEffectCoordinate("per-user", d, dc, cfg, "LOGISTIC_REGRESSION", device="cpu")
+        assert c.placed == (name == "placed")
+        m = c.update_model(c.initialize_model(), ps_of(d))
+        s = c.score(m)
+        rb = c.routed_bytes
+        m2 = c.update_model(m, ps_of(d) * 0.5)
+        res[name] = (m2, s, d.uids, rb)
+    (ma, sa, ua, rba), (mb, sb, ub, rbb) = res["routed"], res["placed"]
+    assert rbb == 0 and (world == 1 or rba > 0), (rba, rbb)
+    assert sorted(ma.entity_ids) == sorted(mb.entity_ids)
+    for e in ma.entity_ids:
+        assert np.array_equal(ma.coefficients_of(e).means.numpy(), mb.coefficients_of(e).means.numpy()), e
+    # scores: per uid, bitwise
+    sa_by, sb_by = dict(zip(ua.tolist(), sa.numpy().tolist())), dict(zip(ub.tolist(), sb.numpy().tolist()))
+    np.save(f"{out}/placed_scores_r{rank}.npy", np.array([[u, sb_by[u]] for u in sorted(sb_by)]))
+    np.save(f"{out}/routed_scores_r{rank}.npy", np.array([[u, sa_by[u]] for u in sorted(sa_by)]))
+    # (b) whole fits
+    for mode in ("auto", None):
+        est = (GameEstimator(device="cpu").set_training_task("LOGISTIC_REGRESSION")
+               .set_coordinate_data_configurations({"global": FixedEffectDataConfiguration("global"),
+                                                    "per-user": dc,
+                                                    "per-item": RandomEffectDataConfiguration("itemId", "item")})
+               .set_coordinate_update_sequence(["global", "per-user", "per-item"])
+               .set_coordinate_descent_iterations(2).set_entity_placement(mode))
+        r = est.fit(tr_l, None, [{"global": cfg, "per-user": cfg, "per-item": cfg}])[0]
+        tag = "auto" if mode else "none"
+        assert est.coordinates["per-user"].placed == (mode == "auto")
+        assert not est.coordinates["per-item"].placed
+        np.save(f"{out}/fit_{tag}_fe_r{rank}.npy", r.model.get("global").glm.coefficients.means.numpy())
+        np.save(f"{out}/fit_{tag}_bytes_r{rank}.npy", np.array([est.coordinates["per-user"].routed_bytes,
+                                                               est.coordinates["per-item"].routed_bytes]))
+    import torch.distributed as dist
+    dist.barrier()
+    dist.destroy_process_group()
+
+
 def sharding_worker(rank, world, port, out):
     _init(rank, world, port)
     import scipy.sparse as sp
@@ -129,5 +189,6 @@ def fsdp_worker(rank, world, port, out):
 
 
 if __name__ == "__main__":
-    fn = {"glm": glm_worker, "game": game_worker, "sharding": sharding_worker, "fsdp": fsdp_worker}[sys.argv[1]]
+    fn = {"glm": glm_worker, "game": game_worker, "sharding": sharding_worker, "fsdp": fsdp_worker,
+          "placed": placed_worker}[sys.argv[1]]
     fn(int(sys.argv[2]), int(sys.argv[3]), int(sys.argv[4]), sys.argv[5])

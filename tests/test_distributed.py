@@ -146,3 +146,23 @@ def test_forced_one_rank_group_is_bitwise_single_process(tmp_path):
     assert np.array_equal(np.load(tmp_path / "forced/game_fe_r0.npy"), np.load(tmp_path / "plain/game_fe_r0.npy"))
     np.testing.assert_allclose(np.load(tmp_path / "forced/game_eval_r0.npy"),
                                np.load(tmp_path / "plain/game_eval_r0.npy"), rtol=1e-12)
+
+
+def test_entity_placement_makes_primary_coordinate_route_free(tmp_path):
+    """Rows placed on their primary-entity owners at ingest: the primary random-effect coordinate reproduces the
+    per-update-routed one bitwise (same rows in the same order on the owner) and moves zero bytes per update; the
+    other random-effect coordinate still routes; whole fits with and without placement agree."""
+    _launch("placed", tmp_path)
+    # routed scores come back to the rows' source ranks, placed ones stay on the owners: compare per uid
+    cat = lambda kind: (lambda a: a[np.argsort(a[:, 0])])(
+        np.concatenate([np.load(tmp_path / f"{kind}_scores_r{r}.npy") for r in range(2)]))
+    a, b = cat("routed"), cat("placed")
+    assert a.shape == b.shape == (2400, 2) and np.array_equal(a, b)
+    for r in range(2):
+        nb = np.load(tmp_path / f"fit_auto_bytes_r{r}.npy")
+        assert nb[0] == 0 and nb[1] > 0
+        assert np.load(tmp_path / f"fit_none_bytes_r{r}.npy")[0] > 0
+    fa0, fa1 = np.load(tmp_path / "fit_auto_fe_r0.npy"), np.load(tmp_path / "fit_auto_fe_r1.npy")
+    assert np.array_equal(fa0, fa1)
+    # the fixed effect sums its per-rank gradients over other row sets: equal to rounding
+    np.testing.assert_allclose(fa0, np.load(tmp_path / "fit_none_fe_r0.npy"), rtol=1e-7, atol=1e-9)
