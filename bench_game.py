@@ -45,6 +45,11 @@ PRESETS = {
     # the small entities, the primal block-diagonal solve for the large ones (n_e > 64 or n_e > d_e)
     "game5pl": dict(entities_per_gpu=1_250_000, rows_per_entity=20, re_dim=1000, re_nnz=50, fe_dim=1_000_000,
                     fe_nnz=30, pool="random", int_ids=1, sizes="powerlaw"),
+    # game5pl plus a heavy tail: four entities of 45K rows (register-resident workgroup clusters of ~118 members)
+    # and three of 150K .. 1M rows (beyond one resident launch: the block-diagonal pass path on its own stream)
+    "game5heavy": dict(entities_per_gpu=1_250_000, rows_per_entity=20, re_dim=1000, re_nnz=50, fe_dim=1_000_000,
+                       fe_nnz=30, pool="random", int_ids=1, sizes="powerlaw",
+                       heavy_rows=(45_000, 45_000, 45_000, 45_000, 150_000, 400_000, 1_000_000)),
     # tall-narrow per-entity models (e.g. per-user models over a few dozen user features, GLMix-style): 250K
     # entities x 100 rows x 31 coefficients (30-feature pools + intercept) — every entity has more rows than
     # coefficients, so each is solved with its exact Hessian on the matrix cores (re_tron_hess_kernel)
@@ -69,6 +74,8 @@ def build_parser() -> argparse.ArgumentParser:
     ap.add_argument("--pool", choices=["random", "exact"])
     ap.add_argument("--int-ids", type=int)
     ap.add_argument("--sizes", choices=["uniform", "powerlaw"])
+    ap.add_argument("--heavy-rows", type=lambda v: tuple(int(x) for x in v.split(",") if x),
+                    help="comma-separated row counts of extra heavy entities (replacing the first entities' sizes)")
     ap.add_argument("--fe-iters", type=int, default=10)
     ap.add_argument("--re-iters", type=int, default=10)
     ap.add_argument("--label-bias", type=float, default=0.0,
@@ -156,7 +163,7 @@ def make_data(args, dev, rank: int = 0):
     else:
         data = generate_game_bench_data_device(args.entities_per_gpu, args.rows_per_entity, args.re_dim, args.re_nnz,
                                                args.fe_dim, args.fe_nnz, device=dev, label_bias=args.label_bias,
-                                               **gen_kw)
+                                               heavy_rows=args.heavy_rows or (), **gen_kw)
         torch.cuda.empty_cache()
     t_data = time.time() - t0
     log(f"data generated in {t_data:.1f}s ({'host' if args.host_data or dev.type != 'cuda' else 'device'}): "

@@ -576,6 +576,21 @@ class RandomEffectCoordinate(Coordinate):
             side.wait_stream(main)                 # offsets / warm starts written on the main stream
             for t in rs_prep:
                 t.record_stream(side)              # allocated on the main stream, read on the side stream
+        # the pass-path entities (e.g. a heavy tail too long for the fused kernels) likewise run on their own
+        # stream next to the fused launch: their passes are grid-wide and their host-side control only waits on
+        # that stream
+        sub_async = (sub is not None and fused is not None and dev.type == "cuda"
+                     and os.environ.get("PML_RE_OVERLAP", "1") != "0")
+        sub_stream = None
+        sub_in = None
+        if sub_async:
+            main = torch.cuda.current_stream(dev)
+            if getattr(self, "_sub_stream", None) is None:
+                self._sub_stream = torch.cuda.Stream(dev)
+            sub_stream = self._sub_stream
+            sub_in = self._sub_inputs(sub, seg, W0)          # on the main stream, before the fused launch
+            sub_stream.wait_stream(main)
+            sub_in.record_stream(sub_stream)
         fres = None
         if fused is not None:
             with Timed(f"RE {self.coordinate_id}: fused primal solve", log, logging.DEBUG):
@@ -594,20 +609,19 @@ class RandomEffectCoordinate(Coordinate):
             parts["fused"] = fres.W
         if sub is not None:
             with Timed(f"RE {self.coordinate_id}: primal block-diagonal solve", log, logging.DEBUG):
-                if W0 is not None:
-                    W0s = W0[sub.cols].contiguous()
-                elif getattr(self, "_sub_W", None) is not None:
-                    W0s = self._sub_W
+                if sub_async:
+                    with torch.cuda.stream(sub_stream):
+                        res, z_sub = self._solve_sub(sub, sub_in, l2, oc)
+                    main.wait_stream(sub_stream)
+                    for t in (res.W, res.iters, res.reason, z_sub):
+                        t.record_stream(main)
                 else:
-                    W0s = torch.zeros(sub.cols.numel(), dtype=torch.float64, device=dev)
-                sub.seg.o = seg.o[sub.rows]
-                sub.seg._dzz_key = None
-                res = batched_tron(sub.seg, self.loss, l2, W0s, oc.tolerance, oc.maximum_iterations)
+                    res, z_sub = self._solve_sub(sub, self._sub_inputs(sub, seg, W0), l2, oc)
                 _sync(res.W)
             self._sub_W = res.W
             iters.index_copy_(0, sub.entities, res.iters)
             reasons.index_copy_(0, sub.entities, res.reason)
-            z.index_copy_(0, sub.rows, sub.seg.glm.matvec(res.W))
+            z.index_copy_(0, sub.rows, z_sub)
             sum_sq += res.W.square().sum()
             parts["sub"] = res.W
         if fres is not None and rs_out is None:
@@ -652,6 +666,27 @@ class RandomEffectCoordinate(Coordinate):
                                     sum_sq=float(sum_sq))
         self._last = (out, None)
         return out
+
+    def _sub_inputs(self, sub, seg, W0) -> torch.Tensor:
+        """Warm start of the pass-path subset (its offsets are set on ``sub.seg`` here too)."""
+        if W0 is not None:
+            W0s = W0[sub.cols].contiguous()
+        elif getattr(self, "_sub_W", None) is not None:
+            W0s = self._sub_W
+        else:
+            W0s = torch.zeros(sub.cols.numel(), dtype=torch.float64, device=seg.y.device)
+        sub.seg.o = seg.o[sub.rows]
+        sub.seg._dzz_key = None
+        return W0s
+
+    def _solve_sub(self, sub, W0s, l2: float, oc):
+        """Block-diagonal TRON over the pass-path subset (on the current stream); (result, its margins)."""
+        from ..optimization.batched import batched_tron
+        o = sub.seg.o
+        if o.is_cuda:
+            o.record_stream(torch.cuda.current_stream(o.device))     # formed on the main stream
+        res = batched_tron(sub.seg, self.loss, l2, W0s, oc.tolerance, oc.maximum_iterations)
+        return res, sub.seg.glm.matvec(res.W)
 
     def _active_mask(self, device) -> torch.Tensor:
         """Entities with active data (bool, on ``device``; uploaded once)."""

@@ -255,14 +255,16 @@ def generate_game_bench_data_device(n_entities: int, rows_per_entity: int, re_di
                                     fe_dim: int = 100_000, fe_nnz: int = 30, re_vocab: int = 1 << 20, seed: int = 7,
                                     entity_offset: int = 0, task: str = "LOGISTIC_REGRESSION", pool: str = "random",
                                     int_ids: bool = False, sizes: str = "uniform", size_alpha: float = 1.3,
-                                    max_rows: int = 20000, device="cuda", label_bias: float = 0.0):
+                                    max_rows: int = 20000, device="cuda", label_bias: float = 0.0,
+                                    heavy_rows=()):
     """:func:`generate_game_bench_data` with every draw, sort and reduction on the device (torch), so benchmark
     GAME data of config-5 size (25M rows, 2.1G non-zeros per GPU) takes seconds instead of minutes of host numpy;
     only the finished CSR arrays cross to the host (the GameData container is host scipy). Same structure and
     distributions (entity size law, Zipf fixed-effect features, per-entity feature pools, ground-truth labels),
     different random streams; rows hold strictly increasing columns (canonical CSR, duplicates dropped).
     ``label_bias``: added to the ground-truth logit of logistic labels (e.g. -4: ~5 % positives, the imbalanced
-    click data the reference's binary-classification down-sampler is meant for)."""
+    click data the reference's binary-classification down-sampler is meant for). ``heavy_rows``: row counts that
+    replace the drawn sizes of the first entities (a heavy tail beyond ``max_rows``)."""
     from ..data.game_data import GameData
     dev = torch.device(device)
     gen = torch.Generator(device=dev)
@@ -284,6 +286,8 @@ def generate_game_bench_data_device(n_entities: int, rows_per_entity: int, re_di
         cnt = torch.full((n_entities,), rows_per_entity, dtype=torch.int64, device=dev)
     else:
         raise ValueError(f"unknown entity size law {sizes!r}")
+    if len(heavy_rows):
+        cnt[:len(heavy_rows)] = torch.tensor([int(r) for r in heavy_rows], dtype=torch.int64, device=dev)
     n = int(cnt.sum())
     ent_sorted = torch.repeat_interleave(torch.arange(n_entities, device=dev), cnt, output_size=n)
     perm = torch.randperm(n, generator=gen, device=dev)

@@ -102,6 +102,22 @@ class EntityTronBatch:
         sel = mask.to(dev) & (n_e > 0) & (d_e > 0) & (d_e <= FUSED_DMAX) & (n_e <= FUSED_MAX_ROWS)
         if e_nnz is not None:
             sel &= e_nnz.to(dev) < (1 << 31)
+        self.n_heavy = 0
+        if RESIDENT == "auto" and dev.type == "cuda" and getattr(ds, "_seg_csr", None) is not None:
+            # tail entities too long for one register-resident launch (more rows than RES_KMAX workgroups hold,
+            # or wider than its LDS image): one streaming workgroup would outlast the whole launch, so they go to
+            # the block-diagonal pass path (grid-wide passes, run on its own stream next to this launch)
+            from ..ops.native import re_res_params
+            cap, rdmax, grid = re_res_params()
+            kmax = min(RES_KMAX, grid // 2)
+            nip_all = ds._seg_csr[0].to(dev)
+            en = nip_all[seg.row_ptr[1:]] - nip_all[seg.row_ptr[:-1]]
+            stream = sel & (d_e > HESS_DMAX)
+            if bool(stream.any()):
+                tail = stream & (en * RES_TAIL_SHARE > int(en[stream].sum()))
+                heavy = tail & (((n_e + cap - 1) // cap > kmax) | (d_e > rdmax))
+                self.n_heavy = int(heavy.sum())
+                sel &= ~heavy
         self.mask = sel
         self.ents = torch.nonzero(sel).squeeze(1)
         self.B = int(self.ents.numel())

@@ -156,3 +156,22 @@ def test_device_csr_router_matches_scipy_router():
     assert torch.equal(b.indptr.cpu(), torch.from_numpy(a.indptr.astype(np.int64)))
     assert torch.equal(b.indices.cpu().to(torch.int64), torch.from_numpy(a.indices.astype(np.int64)))
     assert torch.equal(b.data.cpu(), torch.from_numpy(a.data.astype(np.float64)))
+
+
+def test_heavy_tail_entities_take_the_pass_path_on_their_own_stream(monkeypatch):
+    """Tail entities longer than one register-resident launch holds (here: RES_KMAX = 4 workgroups of 384 rows)
+    leave the fused batch for the block-diagonal pass path, which runs on its own stream next to the fused launch:
+    the same models and scores as the serial order (bitwise), and close to the all-streaming solve."""
+    import photon_ml_amd.optimization.entity_tron as et
+    monkeypatch.setattr(et, "RES_KMAX", 4)
+    data, _ = generate_game_data(n_rows=60000, n_users=300, d_user=40, seed=28, task="LOGISTIC_REGRESSION")
+    ra = _re_update(data, "LOGISTIC_REGRESSION", True, monkeypatch)
+    rs, fz, sub = ra[0]._comps
+    assert fz is not None and fz.n_heavy > 0 and sub is not None and sub.entities.numel() >= fz.n_heavy
+    rb = _re_update(data, "LOGISTIC_REGRESSION", False, monkeypatch)
+    for i in range(1, 5):
+        assert np.array_equal(np.asarray(ra[i]), np.asarray(rb[i])), i
+    rc = _re_update(data, "LOGISTIC_REGRESSION", True, monkeypatch, resident="0")
+    assert rc[0]._comps[1].n_heavy == 0
+    for i in range(1, 5):
+        torch.testing.assert_close(torch.as_tensor(ra[i]), torch.as_tensor(rc[i]), rtol=1e-5, atol=1e-6)

@@ -360,6 +360,8 @@ def test_resident_cluster_tron_matches_streaming(task, monkeypatch):
         fz = c._comps[1]
         if mode == "force":
             assert fz.res is not None and fz.res["clusters"] > 0 and fz.res["n"] == fz.B
+            t0 = fz.res["t0"].cpu()
+            assert int((t0[1:] - t0[:-1]).max()) >= 8        # clusters of >= 8 member workgroups
         else:
             assert fz.res is None
         out[mode] = (v1, s1, v2, s2, c.last_stats["mean_iterations"])
