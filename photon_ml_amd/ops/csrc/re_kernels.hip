@@ -651,7 +651,7 @@ __global__ __launch_bounds__(RE_THREADS) void re_tron_csr_kernel(ReTronArgs a) {
 // largest entities 33.6 instead of 28.1 ms) and three in Hessian-vector passes (four: +15 %); 4 waves per SIMD
 // spills in the row loop (80 ms vs 61 ms for re_tron_csr_kernel)
 #ifndef LEAN_VEC                 // (guarded: the A/B scripts build variants with -D)
-#define LEAN_VEC 1               // 1: vectorised quad row pass (row_pass_v), 0: row_pass
+#define LEAN_VEC 0               // 1: vectorised quad row pass (row_pass_v, measured slower), 0: row_pass
 #endif
 #if LEAN_VEC
 #define LEAN_PASS row_pass_v

@@ -15,5 +15,5 @@ for ctrs in "SQ_WAVE_CYCLES SQ_WAIT_ANY SQ_WAIT_INST_ANY SQ_ACTIVE_INST_ANY SQ_B
   timeout -s KILL 240 rocprofv3 --kernel-trace --pmc $ctrs -d $out/p$i -o p --output-format csv -- python3 scripts/re_fused_bench.py 43000 lean > $out/b$i.log 2>&1 || { echo "pmc pass $i failed"; tail -5 $out/b$i.log; exit 1; }
 done
 python3 scripts/pmc_summary.py $out "re_tron" $out/summary.txt
-find $out -name "*.csv" -size +20M -delete
+find $out -name "*.csv" -delete
 cat $out/summary.txt

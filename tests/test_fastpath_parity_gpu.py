@@ -85,8 +85,10 @@ def test_perm_cast_is_bitwise_gather_then_cast(precision):
     assert torch.equal(perm_cast(w, p, dev.vdt), w[p].to(dev.vdt))
 
 
-def _re_update(data, task, overlap, monkeypatch, resident="auto"):
+def _re_update(data, task, overlap, monkeypatch, resident="auto", hess=True):
     import photon_ml_amd.optimization.entity_tron as et
+    if not hess:
+        monkeypatch.setattr(et, "HESS_DMAX", 0)          # d_e 41: the sparse streaming kernels, not the tall one
     from photon_ml_amd.algorithm.coordinates import RandomEffectCoordinate
     from photon_ml_amd.data.random_effect import RandomEffectDataConfiguration
     from photon_ml_amd.optimization.config import (GLMOptimizationConfiguration, OptimizerConfig,
@@ -135,7 +137,7 @@ def test_resident_error_check_runs_after_the_side_stream_launch(monkeypatch):
     monkeypatch.setattr(RowSpaceBatch, "solve", solve)
     monkeypatch.setattr(et.FusedResult, "check_error", check)
     data, _ = generate_game_data(n_rows=60000, n_users=300, d_user=40, seed=28, task="LOGISTIC_REGRESSION")
-    c = _re_update(data, "LOGISTIC_REGRESSION", True, monkeypatch, resident="force")[0]
+    c = _re_update(data, "LOGISTIC_REGRESSION", True, monkeypatch, resident="force", hess=False)[0]
     fz = c._comps[1]
     assert fz.res is not None and fz.res["n"] > 0
     assert "check_error" in events
@@ -165,13 +167,13 @@ def test_heavy_tail_entities_take_the_pass_path_on_their_own_stream(monkeypatch)
     import photon_ml_amd.optimization.entity_tron as et
     monkeypatch.setattr(et, "RES_KMAX", 4)
     data, _ = generate_game_data(n_rows=60000, n_users=300, d_user=40, seed=28, task="LOGISTIC_REGRESSION")
-    ra = _re_update(data, "LOGISTIC_REGRESSION", True, monkeypatch)
+    ra = _re_update(data, "LOGISTIC_REGRESSION", True, monkeypatch, hess=False)
     rs, fz, sub = ra[0]._comps
     assert fz is not None and fz.n_heavy > 0 and sub is not None and sub.entities.numel() >= fz.n_heavy
-    rb = _re_update(data, "LOGISTIC_REGRESSION", False, monkeypatch)
+    rb = _re_update(data, "LOGISTIC_REGRESSION", False, monkeypatch, hess=False)
     for i in range(1, 5):
         assert np.array_equal(np.asarray(ra[i]), np.asarray(rb[i])), i
-    rc = _re_update(data, "LOGISTIC_REGRESSION", True, monkeypatch, resident="0")
+    rc = _re_update(data, "LOGISTIC_REGRESSION", True, monkeypatch, resident="0", hess=False)
     assert rc[0]._comps[1].n_heavy == 0
     for i in range(1, 5):
         torch.testing.assert_close(torch.as_tensor(ra[i]), torch.as_tensor(rc[i]), rtol=1e-5, atol=1e-6)
