@@ -139,6 +139,17 @@ class _LossEvaluator(Evaluator):
     higher_is_better = False
     loss = None
 
+    def evaluate(self, scores) -> float:
+        s = _t(scores, self.labels.device)
+        if s.is_cuda and s.dtype == torch.float64:
+            # scores + offsets folded into the fused loss pass (no separate N-length add)
+            from ..ops.native import loss_sum
+            t = loss_sum(self.loss.loss_id, s.contiguous(), self.labels, self.weights, offsets=self.offsets)
+            if t is not None:
+                v = float(t)
+                return _allsum(v)[0] if self.distributed else v
+        return self._evaluate(s + self.offsets)
+
     def _evaluate(self, s):
         v = None
         if s.is_cuda:

@@ -2879,6 +2879,23 @@ __global__ __launch_bounds__(256) void offset_update_kernel(const double* __rest
   }
 }
 
+// Scores of the optimizer's last accepted point from the cached margins: out = (z0 + t zd) [- o] in one pass
+// (DeviceGLMData.margins; the torch sequence clone / add_(alpha = t) / cast / sub_ was four passes). z0 + t zd is
+// one fma (one rounding), then the offset subtraction.
+template <typename RT>
+__global__ __launch_bounds__(256) void cached_margins_kernel(const double* __restrict__ z0,
+                                                             const double* __restrict__ zd, double t,
+                                                             const RT* __restrict__ o, long long n,
+                                                             double* __restrict__ out) {
+#pragma clang fp contract(off)
+  for (long long i = (long long)blockIdx.x * 256 + threadIdx.x; i < n; i += (long long)gridDim.x * 256) {
+    double z = z0[i];
+    if (zd) z = fma(t, zd[i], z);
+    if (o) z = z - static_cast<double>(o[i]);
+    out[i] = z;
+  }
+}
+
 __global__ __launch_bounds__(256) void ls_step_grad_kernel(const double* __restrict__ x0, const double* __restrict__ d,
                                                            double t, const double* __restrict__ G,
                                                            const long long* __restrict__ perm, double l2, long long n,
@@ -3016,6 +3033,19 @@ int pml_offset_update(const double* base, const double* part, long long n, int p
   else
     hipLaunchKernelGGL(offset_update_kernel<float>, dim3(vec_grid(n)), dim3(256), 0, (hipStream_t)stream, base, part,
                        n, (float*)o, z);
+  LAUNCH_CHECK();
+  return 0;
+}
+
+int pml_cached_margins(const double* z0, const double* zd, double t, int prec, const void* o, long long n,
+                       double* out, void* stream) {
+  if (n <= 0) return 0;
+  if (prec == 2 || o == nullptr)
+    hipLaunchKernelGGL(cached_margins_kernel<double>, dim3(vec_grid(n)), dim3(256), 0, (hipStream_t)stream, z0, zd,
+                       t, (const double*)o, n, out);
+  else
+    hipLaunchKernelGGL(cached_margins_kernel<float>, dim3(vec_grid(n)), dim3(256), 0, (hipStream_t)stream, z0, zd,
+                       t, (const float*)o, n, out);
   LAUNCH_CHECK();
   return 0;
 }

@@ -305,6 +305,88 @@ __device__ __forceinline__ void row_pass(const ReTronArgs& a, long long r0, long
 }
 
 // ------------------------------------------------------------------------------------------------------------
+// Software-pipelined Hessian-vector pass (lean kernel, MODE 0 of row_pass): the entries of batch b + 1 are in
+// flight while batch b is gathered, reduced and scattered (row pointers two batches ahead), so a batch costs its
+// compute plus whatever of one memory latency the compute does not cover, instead of a full latency each. Two
+// register sets of U row groups. Same sums in the same order as row_pass<0> (bitwise the same products).
+template <int U>
+__device__ __forceinline__ void hv_pass_pipe(const ReTronArgs& a, long long r0, long long r1,
+                                             const double* __restrict__ vec, double* __restrict__ acc,
+                                             const double* __restrict__ Dc) {
+  const int lane = threadIdx.x & 63, w = threadIdx.x >> 6;
+  const int grp = lane / RE_G, gl = lane % RE_G;
+  const int nrows = (int)(r1 - r0);
+  const long long e0 = a.nip[r0];
+  const long long* __restrict__ nip = a.nip + r0;
+  const uint16_t* __restrict__ lcol = a.lcol + e0;
+  const double* __restrict__ val = a.val + e0;
+  Dc += r0;
+  constexpr int BATCH = RE_RPI * U;
+  const int step = RE_NW * BATCH;
+  auto fetch_ptr = [&](int b) -> int {
+    const int i = b + (lane <= BATCH ? lane : BATCH);
+    return b < nrows ? (int)(nip[i < nrows ? i : nrows] - e0) : 0;
+  };
+  struct Set {
+    int lo[U], hi[U];
+    int c[U][RE_K];
+    double v[U][RE_K], d[U];
+  };
+  auto load = [&](int b, int np, Set& s) {
+#pragma unroll
+    for (int u = 0; u < U; ++u) {
+      const int q = u * RE_RPI + grp;
+      s.lo[u] = __shfl(np, q, 64);
+      s.hi[u] = __shfl(np, q + 1, 64);
+      const int i = b + q;
+      s.d[u] = i < nrows ? Dc[i] : 0.0;
+    }
+#pragma unroll
+    for (int u = 0; u < U; ++u) {
+#pragma unroll
+      for (int k = 0; k < RE_K; ++k) {
+        const int p = s.lo[u] + gl + RE_G * k;
+        const bool in = p < s.hi[u];
+        s.c[u][k] = in ? (int)lcol[p] : 0;
+        s.v[u][k] = in ? val[p] : 0.0;
+      }
+    }
+  };
+  auto compute = [&](const Set& s) {
+    double dot[U];
+#pragma unroll
+    for (int u = 0; u < U; ++u) {
+      double x = 0.0;
+#pragma unroll
+      for (int k = 0; k < RE_K; ++k) x = fma(s.v[u][k], vec[s.c[u][k]], x);
+      for (int p = s.lo[u] + gl + RE_G * RE_K; p < s.hi[u]; p += RE_G) x = fma(val[p], vec[lcol[p]], x);
+      dot[u] = x;
+    }
+#pragma unroll
+    for (int u = 0; u < U; ++u) {
+      const double t = s.d[u] * row16_total(dot[u]);
+#pragma unroll
+      for (int k = 0; k < RE_K; ++k)
+        if (s.lo[u] + gl + RE_G * k < s.hi[u]) atomicAdd(&acc[s.c[u][k]], t * s.v[u][k]);
+      for (int p = s.lo[u] + gl + RE_G * RE_K; p < s.hi[u]; p += RE_G) atomicAdd(&acc[lcol[p]], t * val[p]);
+    }
+  };
+  int base = w * BATCH;
+  if (base >= nrows) return;
+  Set cur, nxt;
+  load(base, fetch_ptr(base), cur);
+  int np_next = fetch_ptr(base + step);
+  for (; base < nrows; base += step) {
+    const int nb = base + step;
+    const int np_after = fetch_ptr(nb + step);     // row pointers two batches ahead
+    if (nb < nrows) load(nb, np_next, nxt);        // next batch's entries in flight during this batch's compute
+    compute(cur);
+    cur = nxt;
+    np_next = np_after;
+  }
+}
+
+// ------------------------------------------------------------------------------------------------------------
 // Vectorised row pass (lean kernel). Same work as row_pass, but lane gl of a row's 16 lanes owns the 4-entry
 // QUAD (lo & ~3) + 4 gl (+ 64 per extra chunk) of the row: its 4 columns arrive in ONE 8-byte buffer load and
 // its 4 values in TWO 16-byte buffer loads (row_pass: 4 + 4 narrow loads, one 64-bit address each). Entries of
@@ -658,6 +740,9 @@ __global__ __launch_bounds__(RE_THREADS) void re_tron_csr_kernel(ReTronArgs a) {
 #else
 #define LEAN_PASS row_pass
 #endif
+#ifndef LEAN_PIPE
+#define LEAN_PIPE 0              // > 0: software-pipelined Hessian-vector passes (hv_pass_pipe<LEAN_PIPE>)
+#endif
 #ifndef LEAN_WPE
 #define LEAN_WPE 3
 #endif
@@ -768,7 +853,11 @@ void re_tron_lean_kernel(ReTronArgs a) {
       __syncthreads();
       for (int j = lane; j < d; j += 64) myacc[j] = 0.0;
       double fp = 0.0;
+#if LEAN_PIPE > 0
+      hv_pass_pipe<LEAN_PIPE>(a, r0, r1, sD, myacc, D[cur]);
+#else
       LEAN_PASS<0, LOSS, LEAN_UH>(a, r0, r1, sD, myacc, D[cur], nullptr, nullptr, fp);
+#endif
       __syncthreads();
       double s5[5] = {0.0, 0.0, 0.0, 0.0, 0.0};
       double H[J];

@@ -1253,6 +1253,10 @@ class DeviceGLMData(GLMComputable):
             # the margins of the optimizer's last accepted point are cached (z0 + t_pending zd, offsets included):
             # scoring the returned model needs no forward pass
             n = self.n_rows
+            if self.z_cache.is_cuda and self.o.dtype in (torch.float32, torch.float64):
+                from .native import cached_margins           # one pass instead of clone / add_ / cast / sub_
+                return cached_margins(self.z_cache, self.zd if self._tpend else None, self._tpend,
+                                      None if with_offsets else self.o, n)
             z = self.z_cache[:n].clone()
             if self._tpend:
                 z.add_(self.zd[:n], alpha=self._tpend)

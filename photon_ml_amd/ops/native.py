@@ -146,6 +146,9 @@ def glm_lib() -> Optional[ctypes.CDLL]:
         lib.pml_masked_gather.argtypes = [c_void_p, c_void_p, ctypes.c_longlong, c_void_p, c_void_p]
         lib.pml_masked_gather.restype = c_int
         lib.pml_offset_update.argtypes = [c_void_p, c_void_p, ctypes.c_longlong, c_int, c_void_p, c_void_p, c_void_p]
+        lib.pml_cached_margins.argtypes = [c_void_p, c_void_p, c_double, c_int, c_void_p, ctypes.c_longlong,
+                                           c_void_p, c_void_p]
+        lib.pml_cached_margins.restype = c_int
         lib.pml_offset_update.restype = c_int
         lib.pml_two_loop_chain.argtypes = [c_int] + [c_void_p] * 5 + [ctypes.c_longlong] + [c_void_p] * 4 + \
             [c_int, c_void_p]
@@ -298,11 +301,13 @@ def lbfgs_pair(x, x0, g, g0):
 _LOSS_SCRATCH = {}
 
 
-def loss_sum(loss_id: int, z: torch.Tensor, y: torch.Tensor, w: torch.Tensor) -> Optional[torch.Tensor]:
-    """0-d device fp64 ``sum_i w_i l(z_i, y_i)`` in one fused pass (``ls_eval_kernel`` at t = 0 + a fixed-order
-    block reduction): the GAME training-loss evaluation after every coordinate update, instead of ~10 torch
-    elementwise passes. None when the inputs do not qualify (host tensors, other dtypes)."""
-    vs = (z, y, w)
+def loss_sum(loss_id: int, z: torch.Tensor, y: torch.Tensor, w: torch.Tensor,
+             offsets: Optional[torch.Tensor] = None) -> Optional[torch.Tensor]:
+    """0-d device fp64 ``sum_i w_i l(z_i + o_i, y_i)`` in one fused pass (``ls_eval_kernel`` + a fixed-order block
+    reduction; ``offsets`` o enter as the kernel's direction at t = 1, so z + 1.0 o rounds exactly like z + o): the
+    GAME training-loss evaluation after every coordinate update, instead of ~10 torch elementwise passes. None when
+    the inputs do not qualify (host tensors, other dtypes)."""
+    vs = (z, y, w) if offsets is None else (z, y, w, offsets)
     if not (z.device.type == "cuda" and loss_id in (0, 1, 2, 3) and 0 < z.numel() < 2 ** 31
             and all(v.device == z.device and v.dtype == torch.float64 and v.dim() == 1 and v.is_contiguous()
                     and v.numel() == z.numel() for v in vs)):
@@ -312,7 +317,8 @@ def loss_sum(loss_id: int, z: torch.Tensor, y: torch.Tensor, w: torch.Tensor) ->
     if sc is None:
         sc = _LOSS_SCRATCH[z.device] = torch.empty(2 * 4096, dtype=torch.float64, device=z.device)
     out = torch.empty(2, dtype=torch.float64, device=z.device)
-    check(lib.pml_ls_eval(2, z.numel(), 0.0, int(loss_id), z.data_ptr(), z.data_ptr(), y.data_ptr(), w.data_ptr(),
+    zd, t = (z, 0.0) if offsets is None else (offsets, 1.0)
+    check(lib.pml_ls_eval(2, z.numel(), t, int(loss_id), z.data_ptr(), zd.data_ptr(), y.data_ptr(), w.data_ptr(),
                           0, None, None, sc.data_ptr(), out.data_ptr(), stream_handle(z.device)), "loss_sum")
     return out[0]
 
@@ -369,6 +375,22 @@ def offset_update(base: torch.Tensor, part: torch.Tensor, o: torch.Tensor, z: Op
                                               2 if o.dtype == torch.float64 else 1, o.data_ptr(),
                                               None if z is None else z.data_ptr(), stream_handle(base.device)),
           "offset_update")
+
+
+def cached_margins(z0: torch.Tensor, zd: Optional[torch.Tensor], t: float, o: Optional[torch.Tensor],
+                   n: int) -> torch.Tensor:
+    """``(z0[:n] + t zd[:n]) - o[:n]`` (``zd`` / ``o`` None: term left out) as a new fp64 vector in one pass
+    (``cached_margins_kernel``: z0 + t zd as one fma, then the offset subtraction)."""
+    for v in (z0, zd, o):
+        assert v is None or (v.is_cuda and v.is_contiguous() and v.numel() >= n and v.device == z0.device)
+    assert z0.dtype == torch.float64 and (zd is None or zd.dtype == torch.float64)
+    assert o is None or o.dtype in (torch.float32, torch.float64)
+    out = torch.empty(max(n, 1), dtype=torch.float64, device=z0.device)[:n]
+    check(require_glm_lib().pml_cached_margins(z0.data_ptr(), None if zd is None else zd.data_ptr(), float(t),
+                                               2 if o is None or o.dtype == torch.float64 else 1,
+                                               None if o is None else o.data_ptr(), n, out.data_ptr(),
+                                               stream_handle(z0.device)), "cached_margins")
+    return out
 
 
 def masked_gather(src: torch.Tensor, idx: torch.Tensor) -> torch.Tensor:

@@ -16,6 +16,15 @@ def main(root, pattern="tl_|seg_|segdot", out=None):
                     continue
                 short = re.sub(r"\(.*", "", name).replace("void ", "")
                 acc[short][r["Counter_Name"]].append(float(r["Counter_Value"]))
+    # mean dispatch duration from the kernel traces of the same runs (effective clock = GRBM_GUI_ACTIVE / 8 / time)
+    for f in glob.glob(f"{root}/**/*kernel_trace.csv", recursive=True):
+        with open(f) as fh:
+            for r in csv.DictReader(fh):
+                name = r.get("Kernel_Name", "")
+                if not re.search(pattern, name) or "Start_Timestamp" not in r:
+                    continue
+                short = re.sub(r"\(.*", "", name).replace("void ", "")
+                acc[short]["duration_us"].append((float(r["End_Timestamp"]) - float(r["Start_Timestamp"])) / 1e3)
     lines = []
     for k in sorted(acc):
         lines.append(f"## {k}")

@@ -177,3 +177,35 @@ def test_heavy_tail_entities_take_the_pass_path_on_their_own_stream(monkeypatch)
     assert rc[0]._comps[1].n_heavy == 0
     for i in range(1, 5):
         torch.testing.assert_close(torch.as_tensor(ra[i]), torch.as_tensor(rc[i]), rtol=1e-5, atol=1e-6)
+
+
+@pytest.mark.parametrize("precision", ["f64", "bf16"])
+def test_cached_margins_kernel_matches_torch(precision):
+    """``DeviceGLMData.margins`` from the cached margins in one pass (``cached_margins_kernel``: fma(t, zd, z0) - o)
+    vs the torch sequence clone / add_ / cast / sub_ (the same values to the single fma rounding)."""
+    from photon_ml_amd.ops.native import cached_margins
+    g = torch.Generator(device="cuda").manual_seed(3)
+    n = 100_003
+    z0 = torch.randn(n + 5, generator=g, device="cuda", dtype=torch.float64)
+    zd = torch.randn(n + 5, generator=g, device="cuda", dtype=torch.float64)
+    o = torch.randn(n, generator=g, device="cuda", dtype=torch.float64).to(
+        torch.float64 if precision == "f64" else torch.float32)
+    t = 0.37
+    ref = (z0[:n] + t * zd[:n]) - o.to(torch.float64)
+    out = cached_margins(z0, zd, t, o, n)
+    assert out.shape == (n,)
+    torch.testing.assert_close(out, ref, rtol=1e-15, atol=1e-15)
+    assert torch.equal(cached_margins(z0, None, 0.0, None, n), z0[:n])
+    assert torch.equal(cached_margins(z0, None, 0.0, o, n), z0[:n] - o.to(torch.float64))
+    # through the data object: the scores of the last accepted point equal a fresh forward pass
+    data, dev = _dev_data(precision)
+    obj = GLMObjective(LOGISTIC, l2_weight=1.0)
+    from photon_ml_amd.optimization.lbfgs import LBFGS
+    opt = LBFGS(tolerance=1e-12, max_iterations=3)
+    opt.start(obj, dev, torch.zeros(dev.dim, dtype=torch.float64, device="cuda"))
+    for _ in range(3):
+        st = opt.step(obj, dev)
+    z_cached = dev.margins(st.coefficients)
+    dev.z_cache = None                                   # force the forward pass
+    z_fwd = dev.margins(st.coefficients)
+    torch.testing.assert_close(z_cached, z_fwd, rtol=1e-9, atol=1e-9)
