@@ -201,6 +201,9 @@ __device__ __forceinline__ double row16_total(double v) {
 #define RE_RPI (64 / RE_G)           // rows per wave instruction
 #define RE_U 4                       // row groups in flight per wave batch (re_tron_csr_kernel; 3: +2.4 %)
 #define RE_K 4                       // entries per lane kept in registers (rows of <= 64 entries in one go)
+#ifndef RE_ABL
+#define RE_ABL 0                     // profiling-only ablation mask (see row_pass); 0 in production
+#endif
 
 // One pass over the entity's rows [r0, r1): a wave takes BATCH = 4 U consecutive rows at a time, RE_G lanes per
 // row (lane k of the row: entries k, k + 16, ...). The next batch's row pointers are fetched while the current
@@ -273,6 +276,19 @@ __device__ __forceinline__ void row_pass(const ReTronArgs& a, long long r0, long
 #pragma unroll
         for (int k = 0; k < RE_K; ++k) s = fma(v[u][k], vec[c[u][k]], s);
         for (int p = lo[u] + gl + RE_G * RE_K; p < hi[u]; p += RE_G) s = fma(val[p], vec[lcol[p]], s);
+#if RE_ABL
+        // profiling ablations (scripts/gpu_r5_s5.sh): the same math plus one extra LDS gather (2) or one extra
+        // value load (4) per entry, scaled by a runtime zero -- their marginal cost, at identical iterates
+        const double zero = a.l2 - a.l2;
+#pragma unroll
+        for (int k = 0; k < RE_K; ++k) {
+          if (RE_ABL & 2) s = fma(zero, vec[c[u][k] >> 1], s);
+          if (RE_ABL & 4) {
+            const int p = lo[u] + gl + RE_G * k;
+            s = fma(zero, p < hi[u] ? ((volatile const double*)val)[p] : 0.0, s);
+          }
+        }
+#endif
       }
       dot[u] = s;
     }
@@ -297,92 +313,15 @@ __device__ __forceinline__ void row_pass(const ReTronArgs& a, long long r0, long
       }
 #pragma unroll
       for (int k = 0; k < RE_K; ++k)
-        if (lo[u] + gl + RE_G * k < hi[u]) atomicAdd(&acc[c[u][k]], t * v[u][k]);
+        if (lo[u] + gl + RE_G * k < hi[u]) {
+          atomicAdd(&acc[c[u][k]], t * v[u][k]);
+#if RE_ABL & 1
+          atomicAdd(&acc[c[u][k]], (a.l2 - a.l2) * v[u][k]);   // profiling: one extra LDS atomic per entry
+#endif
+        }
       for (int p = lo[u] + gl + RE_G * RE_K; p < hi[u]; p += RE_G) atomicAdd(&acc[lcol[p]], t * val[p]);
     }
     np = np_next;
-  }
-}
-
-// ------------------------------------------------------------------------------------------------------------
-// Software-pipelined Hessian-vector pass (lean kernel, MODE 0 of row_pass): the entries of batch b + 1 are in
-// flight while batch b is gathered, reduced and scattered (row pointers two batches ahead), so a batch costs its
-// compute plus whatever of one memory latency the compute does not cover, instead of a full latency each. Two
-// register sets of U row groups. Same sums in the same order as row_pass<0> (bitwise the same products).
-template <int U>
-__device__ __forceinline__ void hv_pass_pipe(const ReTronArgs& a, long long r0, long long r1,
-                                             const double* __restrict__ vec, double* __restrict__ acc,
-                                             const double* __restrict__ Dc) {
-  const int lane = threadIdx.x & 63, w = threadIdx.x >> 6;
-  const int grp = lane / RE_G, gl = lane % RE_G;
-  const int nrows = (int)(r1 - r0);
-  const long long e0 = a.nip[r0];
-  const long long* __restrict__ nip = a.nip + r0;
-  const uint16_t* __restrict__ lcol = a.lcol + e0;
-  const double* __restrict__ val = a.val + e0;
-  Dc += r0;
-  constexpr int BATCH = RE_RPI * U;
-  const int step = RE_NW * BATCH;
-  auto fetch_ptr = [&](int b) -> int {
-    const int i = b + (lane <= BATCH ? lane : BATCH);
-    return b < nrows ? (int)(nip[i < nrows ? i : nrows] - e0) : 0;
-  };
-  struct Set {
-    int lo[U], hi[U];
-    int c[U][RE_K];
-    double v[U][RE_K], d[U];
-  };
-  auto load = [&](int b, int np, Set& s) {
-#pragma unroll
-    for (int u = 0; u < U; ++u) {
-      const int q = u * RE_RPI + grp;
-      s.lo[u] = __shfl(np, q, 64);
-      s.hi[u] = __shfl(np, q + 1, 64);
-      const int i = b + q;
-      s.d[u] = i < nrows ? Dc[i] : 0.0;
-    }
-#pragma unroll
-    for (int u = 0; u < U; ++u) {
-#pragma unroll
-      for (int k = 0; k < RE_K; ++k) {
-        const int p = s.lo[u] + gl + RE_G * k;
-        const bool in = p < s.hi[u];
-        s.c[u][k] = in ? (int)lcol[p] : 0;
-        s.v[u][k] = in ? val[p] : 0.0;
-      }
-    }
-  };
-  auto compute = [&](const Set& s) {
-    double dot[U];
-#pragma unroll
-    for (int u = 0; u < U; ++u) {
-      double x = 0.0;
-#pragma unroll
-      for (int k = 0; k < RE_K; ++k) x = fma(s.v[u][k], vec[s.c[u][k]], x);
-      for (int p = s.lo[u] + gl + RE_G * RE_K; p < s.hi[u]; p += RE_G) x = fma(val[p], vec[lcol[p]], x);
-      dot[u] = x;
-    }
-#pragma unroll
-    for (int u = 0; u < U; ++u) {
-      const double t = s.d[u] * row16_total(dot[u]);
-#pragma unroll
-      for (int k = 0; k < RE_K; ++k)
-        if (s.lo[u] + gl + RE_G * k < s.hi[u]) atomicAdd(&acc[s.c[u][k]], t * s.v[u][k]);
-      for (int p = s.lo[u] + gl + RE_G * RE_K; p < s.hi[u]; p += RE_G) atomicAdd(&acc[lcol[p]], t * val[p]);
-    }
-  };
-  int base = w * BATCH;
-  if (base >= nrows) return;
-  Set cur, nxt;
-  load(base, fetch_ptr(base), cur);
-  int np_next = fetch_ptr(base + step);
-  for (; base < nrows; base += step) {
-    const int nb = base + step;
-    const int np_after = fetch_ptr(nb + step);     // row pointers two batches ahead
-    if (nb < nrows) load(nb, np_next, nxt);        // next batch's entries in flight during this batch's compute
-    compute(cur);
-    cur = nxt;
-    np_next = np_after;
   }
 }
 
@@ -740,9 +679,6 @@ __global__ __launch_bounds__(RE_THREADS) void re_tron_csr_kernel(ReTronArgs a) {
 #else
 #define LEAN_PASS row_pass
 #endif
-#ifndef LEAN_PIPE
-#define LEAN_PIPE 0              // > 0: software-pipelined Hessian-vector passes (hv_pass_pipe<LEAN_PIPE>)
-#endif
 #ifndef LEAN_WPE
 #define LEAN_WPE 3
 #endif
@@ -853,11 +789,7 @@ void re_tron_lean_kernel(ReTronArgs a) {
       __syncthreads();
       for (int j = lane; j < d; j += 64) myacc[j] = 0.0;
       double fp = 0.0;
-#if LEAN_PIPE > 0
-      hv_pass_pipe<LEAN_PIPE>(a, r0, r1, sD, myacc, D[cur]);
-#else
       LEAN_PASS<0, LOSS, LEAN_UH>(a, r0, r1, sD, myacc, D[cur], nullptr, nullptr, fp);
-#endif
       __syncthreads();
       double s5[5] = {0.0, 0.0, 0.0, 0.0, 0.0};
       double H[J];

@@ -208,4 +208,7 @@ def test_cached_margins_kernel_matches_torch(precision):
     z_cached = dev.margins(st.coefficients)
     dev.z_cache = None                                   # force the forward pass
     z_fwd = dev.margins(st.coefficients)
-    torch.testing.assert_close(z_cached, z_fwd, rtol=1e-9, atol=1e-9)
+    # (bf16 / fp32 shards: a pass gathers the coefficients cast to fp32, the cached margins come from the cast
+    # direction; they agree to that rounding)
+    tol = 1e-9 if precision == "f64" else 2e-6
+    torch.testing.assert_close(z_cached, z_fwd, rtol=tol, atol=tol)
