@@ -69,41 +69,6 @@ __device__ __forceinline__ void loss_t(double z, double y, double& l, double& dl
   }
 }
 
-// loss_t split in two (the same operations, so the same bits): loss_dl gives l' and what loss_rest needs for
-// l and l'' (logistic: e = exp(-|z|) and the sigmoid s; Poisson: e^z). The vectorised row pass scatters with l'
-// while the batch's entries are in registers and evaluates the rest (log1p) after they are dead.
-template <int LOSS>
-__device__ __forceinline__ double loss_dl(double z, double y, double& e, double& s) {
-  if constexpr (LOSS == LOSS_LOGISTIC) {
-    e = exp(-fabs(z));
-    const double r = 1.0 / (1.0 + e);
-    s = z >= 0.0 ? r : e * r;
-    return y > 0.5 ? s - 1.0 : s;
-  } else if constexpr (LOSS == LOSS_POISSON) {
-    e = exp(z);
-    s = 0.0;
-    return e - y;
-  } else {
-    e = 0.0; s = 0.0;
-    return z - y;
-  }
-}
-
-template <int LOSS>
-__device__ __forceinline__ void loss_rest(double z, double y, double e, double s, double& l, double& d2) {
-  if constexpr (LOSS == LOSS_LOGISTIC) {
-    const double lp = log1p(e);
-    const double zz = y > 0.5 ? -z : z;
-    l = (zz > 0.0 ? zz : 0.0) + lp;
-    d2 = s * (1.0 - s);
-  } else if constexpr (LOSS == LOSS_POISSON) {
-    l = e - y * z; d2 = e;
-  } else {
-    const double d = z - y;
-    l = 0.5 * d * d; d2 = 1.0;
-  }
-}
-
 template <int CTRL>
 __device__ __forceinline__ double dpp_f64(double v) {
   const long long b = __builtin_bit_cast(long long, v);
@@ -326,38 +291,27 @@ __device__ __forceinline__ void row_pass(const ReTronArgs& a, long long r0, long
 }
 
 // ------------------------------------------------------------------------------------------------------------
-// Vectorised row pass (lean kernel). Same work as row_pass, but lane gl of a row's 16 lanes owns the 4-entry
-// QUAD (lo & ~3) + 4 gl (+ 64 per extra chunk) of the row: its 4 columns arrive in ONE 8-byte buffer load and
-// its 4 values in TWO 16-byte buffer loads (row_pass: 4 + 4 narrow loads, one 64-bit address each). Entries of
-// the quad outside [lo, hi) belong to the neighbouring rows and are masked. Buffer resources (wave-uniform
-// SGPRs) over the entity's aligned entry range make every per-lane address a 32-bit byte offset, so a batch of
-// 4 U rows holds ~14 U VGPRs of loaded data and the kernel fits the register budget of 4 waves per SIMD.
-// Requires the entry arrays to be readable up to the next multiple of 4 entries (EntityTronBatch pads them).
-typedef int re_v2i __attribute__((ext_vector_type(2)));
-
-typedef int re_v4i __attribute__((ext_vector_type(4)));
-
-__device__ __forceinline__ double re_f64(int lo, int hi) {
-  return __builtin_bit_cast(double, ((long long)hi << 32) | (long long)(unsigned int)lo);
-}
+// Quad row pass (lean kernel, rows padded to whole quads of 4 entries: EntityTronBatch pads with column 0 / value
+// 0.0, which add exactly nothing). Lane gl of a row's 16 lanes owns the quad gl (+ 16 per extra chunk): its 4
+// columns arrive in ONE 8-byte load and its 4 values in TWO 16-byte loads, where row_pass issues 4 + 4 narrow
+// loads. The kernel is bound by the texture path's per-instruction work (profiles/re_lean_ablation_r5.md: one
+// extra value load per entry costs +67 %, one extra LDS atomic +8 %), so 3 instead of 8 loads per 4 entries.
+// Only a quad past the row end is masked (no per-entry masks).
+typedef double re_d2 __attribute__((ext_vector_type(2)));
+typedef unsigned re_u2 __attribute__((ext_vector_type(2)));
 
 template <int MODE, int LOSS, int U>
-__device__ __forceinline__ void row_pass_v(const ReTronArgs& a, long long r0, long long r1,
+__device__ __forceinline__ void row_pass_q(const ReTronArgs& a, long long r0, long long r1,
                                            const double* __restrict__ vec, double* __restrict__ acc,
                                            const double* __restrict__ Dc, double* __restrict__ Dn,
                                            double* __restrict__ Zn, double& fpart) {
   const int lane = threadIdx.x & 63, w = threadIdx.x >> 6;
   const int grp = lane / RE_G, gl = lane % RE_G;
   const int nrows = (int)(r1 - r0);
-  // quad-aligned entity entry range, made wave-uniform (SGPRs) so the buffer resources need no waterfall loop
-  const long long e0 = uniform_i64(a.nip[r0]) & ~3LL;
-  const long long e1 = (uniform_i64(a.nip[r1]) + 3) & ~3LL;
-  const int nrec = (int)(e1 - e0);
-  const __amdgpu_buffer_rsrc_t rc = __builtin_amdgcn_make_buffer_rsrc((void*)(a.lcol + e0), (short)0, nrec * 2,
-                                                                       0x00020000);
-  const __amdgpu_buffer_rsrc_t rv = __builtin_amdgcn_make_buffer_rsrc((void*)(a.val + e0), (short)0, nrec * 8,
-                                                                       0x00020000);
+  const long long e0 = a.nip[r0];                           // a multiple of 4 (padded rows)
   const long long* __restrict__ nip = a.nip + r0;
+  const re_u2* __restrict__ cq = (const re_u2*)(a.lcol + e0);   // quad q: 4 columns
+  const re_d2* __restrict__ vq = (const re_d2*)(a.val + e0);    // quad q: values at 2q, 2q + 1
   const double* __restrict__ wt = a.wt + r0;
   const double* __restrict__ off = a.off + r0;
   const double* __restrict__ yv = a.y + r0;
@@ -366,35 +320,26 @@ __device__ __forceinline__ void row_pass_v(const ReTronArgs& a, long long r0, lo
   constexpr int BATCH = RE_RPI * U;
   const int step = RE_NW * BATCH;
   int base = w * BATCH;
+  // row pointers of a batch, in quads: lane j <= BATCH holds nip[base + j] / 4
   auto fetch_ptr = [&](int b) -> int {
     const int i = b + (lane <= BATCH ? lane : BATCH);
-    return b < nrows ? (int)(nip[i < nrows ? i : nrows] - e0) : 0;
+    return b < nrows ? (int)((nip[i < nrows ? i : nrows] - e0) >> 2) : 0;
   };
-  // the quad of entries [q, q + 4) masked to [lo, hi): columns (0 outside) and values (0.0 outside)
-  auto load_quad = [&](int q, int lo, int hi, int (&c)[4], double (&v)[4]) {
-    const re_v2i cw = __builtin_amdgcn_raw_buffer_load_b64(rc, q * 2, 0, 0);
-    const re_v4i va = __builtin_amdgcn_raw_buffer_load_b128(rv, q * 8, 0, 0);
-    const re_v4i vb = __builtin_amdgcn_raw_buffer_load_b128(rv, q * 8 + 16, 0, 0);
-    const int cc[4] = {cw.x & 0xFFFF, (int)((unsigned)cw.x >> 16), cw.y & 0xFFFF, (int)((unsigned)cw.y >> 16)};
-    const double vv[4] = {re_f64(va.x, va.y), re_f64(va.z, va.w), re_f64(vb.x, vb.y), re_f64(vb.z, vb.w)};
-#pragma unroll
-    for (int k = 0; k < 4; ++k) {
-      const bool in = q + k >= lo && q + k < hi;
-      c[k] = in ? cc[k] : 0;
-      v[k] = in ? vv[k] : 0.0;
-    }
+  auto cols = [](re_u2 c, int (&k)[4]) {
+    k[0] = (int)(c.x & 0xFFFFu); k[1] = (int)(c.x >> 16); k[2] = (int)(c.y & 0xFFFFu); k[3] = (int)(c.y >> 16);
   };
   int np = fetch_ptr(base);
   for (; base < nrows; base += step) {
     const int np_next = fetch_ptr(base + step);
-    int lo[U], hi[U];
-    int c[U][4];
-    double v[U][4], dot[U], rs[U][3];
+    int qa[U], qb[U];
+    re_u2 c[U];
+    re_d2 v0[U], v1[U];
+    double dot[U], rs[U][3];
 #pragma unroll
     for (int u = 0; u < U; ++u) {
       const int q = u * RE_RPI + grp;
-      lo[u] = __shfl(np, q, 64);
-      hi[u] = __shfl(np, q + 1, 64);
+      qa[u] = __shfl(np, q, 64) + gl;                         // this lane's quad
+      qb[u] = __shfl(np, q + 1, 64);                          // the row's end (quads)
       const int i = base + q;
       const bool valid = i < nrows;
       if (MODE == 0) {
@@ -406,24 +351,36 @@ __device__ __forceinline__ void row_pass_v(const ReTronArgs& a, long long r0, lo
       }
     }
 #pragma unroll
-    for (int u = 0; u < U; ++u) load_quad((lo[u] & ~3) + 4 * gl, lo[u], hi[u], c[u], v[u]);
+    for (int u = 0; u < U; ++u) {
+      const bool in = qa[u] < qb[u];
+      const int qq = in ? qa[u] : 0;
+      c[u] = cq[qq];
+      v0[u] = vq[2 * qq];
+      v1[u] = vq[2 * qq + 1];
+      if (!in) { c[u] = re_u2{0u, 0u}; v0[u] = re_d2{0.0, 0.0}; v1[u] = re_d2{0.0, 0.0}; }
+    }
 #pragma unroll
     for (int u = 0; u < U; ++u) {
       double s = 0.0;
       if (MODE != 2) {
-#pragma unroll
-        for (int k = 0; k < 4; ++k) s = fma(v[u][k], vec[c[u][k]], s);
-        for (int q = (lo[u] & ~3) + 4 * gl + 64; q < hi[u]; q += 64) {   // rows longer than one chunk
-          int ct[4];
-          double vt[4];
-          load_quad(q, lo[u], hi[u], ct, vt);
-#pragma unroll
-          for (int k = 0; k < 4; ++k) s = fma(vt[k], vec[ct[k]], s);
+        int k[4];
+        cols(c[u], k);
+        s = fma(v0[u].x, vec[k[0]], s);
+        s = fma(v0[u].y, vec[k[1]], s);
+        s = fma(v1[u].x, vec[k[2]], s);
+        s = fma(v1[u].y, vec[k[3]], s);
+        for (int qq = qa[u] + RE_G; qq < qb[u]; qq += RE_G) {     // rows longer than 64 entries
+          int kt[4];
+          cols(cq[qq], kt);
+          const re_d2 a0 = vq[2 * qq], a1 = vq[2 * qq + 1];
+          s = fma(a0.x, vec[kt[0]], s);
+          s = fma(a0.y, vec[kt[1]], s);
+          s = fma(a1.x, vec[kt[2]], s);
+          s = fma(a1.y, vec[kt[3]], s);
         }
       }
       dot[u] = s;
     }
-    double le[U], ls[U];        // loss_dl -> loss_rest hand-off (function evaluations)
 #pragma unroll
     for (int u = 0; u < U; ++u) {
       if (MODE != 2) dot[u] = row16_total(dot[u]);
@@ -433,34 +390,32 @@ __device__ __forceinline__ void row_pass_v(const ReTronArgs& a, long long r0, lo
       if (MODE == 0) {
         t = rs[u][0] * dot[u];
       } else {
-        double dl = 0.0;
-        le[u] = 0.0; ls[u] = 0.0;
-        if (valid) dl = loss_dl<LOSS>(dot[u] + rs[u][1], rs[u][2], le[u], ls[u]);
+        double l = 0.0, dl = 0.0, d2 = 0.0;
+        if (valid) {
+          loss_t<LOSS>(dot[u] + rs[u][1], rs[u][2], l, dl, d2);
+          if (gl == 0) {
+            fpart += rs[u][0] * l;
+            if (MODE == 1) { Dn[i] = rs[u][0] * d2; Zn[i] = dot[u]; }
+          }
+        }
         t = rs[u][0] * dl;
       }
-      const int q0 = (lo[u] & ~3) + 4 * gl;
-#pragma unroll
-      for (int k = 0; k < 4; ++k)
-        if (q0 + k >= lo[u] && q0 + k < hi[u]) atomicAdd(&acc[c[u][k]], t * v[u][k]);
-      for (int q = q0 + 64; q < hi[u]; q += 64) {
-        int ct[4];
-        double vt[4];
-        load_quad(q, lo[u], hi[u], ct, vt);
-#pragma unroll
-        for (int k = 0; k < 4; ++k)
-          if (q + k >= lo[u] && q + k < hi[u]) atomicAdd(&acc[ct[k]], t * vt[k]);
+      if (qa[u] < qb[u]) {
+        int k[4];
+        cols(c[u], k);
+        atomicAdd(&acc[k[0]], t * v0[u].x);
+        atomicAdd(&acc[k[1]], t * v0[u].y);
+        atomicAdd(&acc[k[2]], t * v1[u].x);
+        atomicAdd(&acc[k[3]], t * v1[u].y);
       }
-    }
-    if (MODE != 0) {
-#pragma unroll
-      for (int u = 0; u < U; ++u) {
-        const int i = base + u * RE_RPI + grp;
-        if (i < nrows && gl == 0) {
-          double l, d2;
-          loss_rest<LOSS>(dot[u] + rs[u][1], rs[u][2], le[u], ls[u], l, d2);
-          fpart += rs[u][0] * l;
-          if (MODE == 1) { Dn[i] = rs[u][0] * d2; Zn[i] = dot[u]; }
-        }
+      for (int qq = qa[u] + RE_G; qq < qb[u]; qq += RE_G) {
+        int kt[4];
+        cols(cq[qq], kt);
+        const re_d2 a0 = vq[2 * qq], a1 = vq[2 * qq + 1];
+        atomicAdd(&acc[kt[0]], t * a0.x);
+        atomicAdd(&acc[kt[1]], t * a0.y);
+        atomicAdd(&acc[kt[2]], t * a1.x);
+        atomicAdd(&acc[kt[3]], t * a1.y);
       }
     }
     np = np_next;
@@ -671,14 +626,13 @@ __global__ __launch_bounds__(RE_THREADS) void re_tron_csr_kernel(ReTronArgs a) {
 // (<= 168 VGPRs, 12 waves per CU) with two row groups per batch in function evaluations (one: same total, the 64
 // largest entities 33.6 instead of 28.1 ms) and three in Hessian-vector passes (four: +15 %); 4 waves per SIMD
 // spills in the row loop (80 ms vs 61 ms for re_tron_csr_kernel)
-#ifndef LEAN_VEC                 // (guarded: the A/B scripts build variants with -D)
-#define LEAN_VEC 0               // 1: vectorised quad row pass (row_pass_v, measured slower), 0: row_pass
-#endif
-#if LEAN_VEC
-#define LEAN_PASS row_pass_v
-#else
-#define LEAN_PASS row_pass
-#endif
+// row pass of the lean kernel: quads over padded rows (Q) or the strided row_pass
+template <bool Q, int MODE, int LOSS, int U>
+__device__ __forceinline__ void lean_pass(const ReTronArgs& a, long long r0, long long r1, const double* vec,
+                                          double* acc, const double* Dc, double* Dn, double* Zn, double& fpart) {
+  if constexpr (Q) row_pass_q<MODE, LOSS, U>(a, r0, r1, vec, acc, Dc, Dn, Zn, fpart);
+  else row_pass<MODE, LOSS, U>(a, r0, r1, vec, acc, Dc, Dn, Zn, fpart);
+}
 #ifndef LEAN_WPE
 #define LEAN_WPE 3
 #endif
@@ -688,7 +642,7 @@ __global__ __launch_bounds__(RE_THREADS) void re_tron_csr_kernel(ReTronArgs a) {
 #ifndef LEAN_UH
 #define LEAN_UH 3
 #endif
-template <int LOSS, int J>
+template <int LOSS, int J, bool Q>
 __global__ __launch_bounds__(RE_THREADS) __attribute__((amdgpu_waves_per_eu(LEAN_WPE, LEAN_WPE)))
 void re_tron_lean_kernel(ReTronArgs a) {
   extern __shared__ __attribute__((aligned(16))) double smem[];
@@ -721,8 +675,8 @@ void re_tron_lean_kernel(ReTronArgs a) {
     __syncthreads();
     for (int j = lane; j < d; j += 64) myacc[j] = 0.0;
     double fp = 0.0;
-    if (at_zero) LEAN_PASS<2, LOSS, LEAN_UF>(a, r0, r1, sD, myacc, nullptr, nullptr, nullptr, fp);
-    else LEAN_PASS<1, LOSS, LEAN_UF>(a, r0, r1, sD, myacc, nullptr, D[nb], Z[nb], fp);
+    if (at_zero) lean_pass<Q, 2, LOSS, LEAN_UF>(a, r0, r1, sD, myacc, nullptr, nullptr, nullptr, fp);
+    else lean_pass<Q, 1, LOSS, LEAN_UF>(a, r0, r1, sD, myacc, nullptr, D[nb], Z[nb], fp);
     __syncthreads();
     double s3[3] = {fp, 0.0, 0.0};
 #pragma unroll
@@ -789,7 +743,7 @@ void re_tron_lean_kernel(ReTronArgs a) {
       __syncthreads();
       for (int j = lane; j < d; j += 64) myacc[j] = 0.0;
       double fp = 0.0;
-      LEAN_PASS<0, LOSS, LEAN_UH>(a, r0, r1, sD, myacc, D[cur], nullptr, nullptr, fp);
+      lean_pass<Q, 0, LOSS, LEAN_UH>(a, r0, r1, sD, myacc, D[cur], nullptr, nullptr, fp);
       __syncthreads();
       double s5[5] = {0.0, 0.0, 0.0, 0.0, 0.0};
       double H[J];
@@ -1903,11 +1857,11 @@ __global__ __launch_bounds__(RS_THREADS) void re_tron_res_kernel(ReTronArgs a, R
   }
 }
 
-template <int LOSS>
+template <int LOSS, bool Q>
 static void lean_launch(const ReTronArgs& a, int n_launch, size_t smem, hipStream_t st) {
-  if (a.dmax <= 256) hipLaunchKernelGGL((re_tron_lean_kernel<LOSS, 1>), dim3(n_launch), dim3(RE_THREADS), smem, st, a);
-  else if (a.dmax <= 512) hipLaunchKernelGGL((re_tron_lean_kernel<LOSS, 2>), dim3(n_launch), dim3(RE_THREADS), smem, st, a);
-  else hipLaunchKernelGGL((re_tron_lean_kernel<LOSS, 4>), dim3(n_launch), dim3(RE_THREADS), smem, st, a);
+  if (a.dmax <= 256) hipLaunchKernelGGL((re_tron_lean_kernel<LOSS, 1, Q>), dim3(n_launch), dim3(RE_THREADS), smem, st, a);
+  else if (a.dmax <= 512) hipLaunchKernelGGL((re_tron_lean_kernel<LOSS, 2, Q>), dim3(n_launch), dim3(RE_THREADS), smem, st, a);
+  else hipLaunchKernelGGL((re_tron_lean_kernel<LOSS, 4, Q>), dim3(n_launch), dim3(RE_THREADS), smem, st, a);
 }
 
 extern "C" {
@@ -1943,15 +1897,22 @@ int pml_re_tron_lean(const int* order, int n_launch, const long long* row_ptr, c
                      const long long* nip, const uint16_t* lcol, const double* val, const double* y,
                      const double* off, const double* wt, double* scr, long long n_rows, double* W, double* f,
                      int* iters, int* reason, double* zout, int* npass, int loss, double l2, double tol,
-                     int max_iter, int max_fail, int max_cg, int dmax, double* gsc, hipStream_t st) {
+                     int max_iter, int max_fail, int max_cg, int dmax, double* gsc, int quad, hipStream_t st) {
   if (n_launch <= 0) return 0;
   if (dmax <= 0 || dmax > 1024 || loss < 0 || loss > 2 || gsc == nullptr) return -22;
   const size_t smem = pml_re_tron_lean_smem(dmax);
   ReTronArgs a{order, n_launch, row_ptr, col_ptr, nip, lcol, val, y, off, wt, scr, n_rows, W, f, iters, reason,
                zout, npass, loss, l2, tol, max_iter, max_fail, max_cg, dmax, gsc};
-  if (loss == LOSS_LOGISTIC) lean_launch<0>(a, n_launch, smem, st);
-  else if (loss == LOSS_POISSON) lean_launch<1>(a, n_launch, smem, st);
-  else lean_launch<2>(a, n_launch, smem, st);
+  // quad: every row padded to a multiple of 4 entries (row_pass_q), else the strided row_pass
+  if (quad) {
+    if (loss == LOSS_LOGISTIC) lean_launch<0, true>(a, n_launch, smem, st);
+    else if (loss == LOSS_POISSON) lean_launch<1, true>(a, n_launch, smem, st);
+    else lean_launch<2, true>(a, n_launch, smem, st);
+  } else {
+    if (loss == LOSS_LOGISTIC) lean_launch<0, false>(a, n_launch, smem, st);
+    else if (loss == LOSS_POISSON) lean_launch<1, false>(a, n_launch, smem, st);
+    else lean_launch<2, false>(a, n_launch, smem, st);
+  }
   LAUNCH_CHECK();
   return 0;
 }

@@ -825,7 +825,7 @@ def re_lib() -> Optional[ctypes.CDLL]:
         lib.pml_re_tron_smem.argtypes = [c_int]
         lib.pml_re_tron_smem.restype = ctypes.c_size_t
         lib.pml_re_tron_hess.argtypes = lib.pml_re_tron_csr.argtypes
-        lib.pml_re_tron_lean.argtypes = lib.pml_re_tron_csr.argtypes[:-1] + [c_void_p, c_void_p]
+        lib.pml_re_tron_lean.argtypes = lib.pml_re_tron_csr.argtypes[:-1] + [c_void_p, c_int, c_void_p]
         lib.pml_re_tron_lean.restype = c_int
         lib.pml_re_tron_hess.restype = c_int
         lib.pml_re_tron_hess_smem.argtypes = [c_int]
@@ -855,13 +855,12 @@ def require_re_lib() -> ctypes.CDLL:
 
 # the lean streaming kernel takes launch classes up to this many coefficients (PML_RE_LEAN=0: never)
 RE_LEAN_DMAX = 1024 if os.environ.get("PML_RE_LEAN", "1") != "0" else 0
-LEAN_MAX_ENTITY_NNZ = 1 << 27          # lean kernel: an entity's values in one 32-bit buffer range (bytes < 2^31)
 
 
 def re_tron_csr(order, row_ptr, col_ptr, nip, lcol, val, y, off, wt, scr, W, f, iters, reason, zout, loss_id: int,
                 l2: float, tol: float, max_iter: int, max_fail: int, max_cg: int, dmax: int,
                 npass: Optional[torch.Tensor] = None, hessian: bool = False, gsc: Optional[torch.Tensor] = None,
-                lean: Optional[bool] = None) -> None:
+                lean: Optional[bool] = None, quad: bool = False) -> None:
     """Fused per-entity primal TRON over the entities ``order`` (int32; one workgroup each) of a block-diagonal
     CSR (``re_tron_csr_kernel``). Entity ``e`` owns rows ``row_ptr[e]:row_ptr[e+1]`` (int64) and coefficients
     ``col_ptr[e]:col_ptr[e+1]`` of the packed ``W`` (fp64, in: warm start, out: solution); ``nip`` int64 row
@@ -870,8 +869,10 @@ def re_tron_csr(order, row_ptr, col_ptr, nip, lcol, val, y, off, wt, scr, W, f, 
     entity and ``zout`` (x_i . w per row); ``npass`` (optional int32 per entity): row passes run. ``hessian``:
     the tall-narrow kernel (``re_tron_hess_kernel``: d_e <= dmax <= 64, dmax a multiple of 16; the per-entity
     Hessian formed on the fp64 matrix cores, CG on it in LDS). ``lean`` (default: dmax <= 1024): the
-    ``re_tron_lean_kernel`` (only the gathered vector + accumulators in LDS, four workgroups per CU) with ``gsc``
-    (fp64 scratch like ``W``; allocated when None). Device only; in place, nothing returned."""
+    ``re_tron_lean_kernel`` (only the gathered vector + accumulators in LDS) with ``gsc`` (fp64 scratch like ``W``;
+    allocated when None); ``quad``: every row of the batch is padded to whole quads of 4 entries (column 0, value
+    0.0), and the lean kernel reads 4 columns / 4 values per lane load (row_pass_q). Device only; in place, nothing
+    returned."""
     lib = require_re_lib()
     n_rows = y.numel()
     B = int(order.numel())
@@ -899,11 +900,9 @@ def re_tron_csr(order, row_ptr, col_ptr, nip, lcol, val, y, off, wt, scr, W, f, 
         assert W.numel() == int(col_ptr[-1]), "packed coefficients / column ranges inconsistent"
         nnz = int(nip[-1])
         assert int(row_ptr[-1]) == n_rows and nnz <= val.numel(), "row / non-zero ranges inconsistent"
-        if lean:
-            # quad row pass (row_pass_v): aligned 4-entry quads, 32-bit buffer ranges per entity
-            assert val.numel() >= (nnz + 3) // 4 * 4, "lean kernel needs entry arrays padded to 4"
-            e_nnz = nip[row_ptr[oe + 1]] - nip[row_ptr[oe]]
-            assert int(e_nnz.max()) < LEAN_MAX_ENTITY_NNZ, "entity too long for the lean kernel's buffer ranges"
+        if lean and quad:
+            # quad row pass (row_pass_q): every row starts on a quad and holds whole quads
+            assert bool((nip % 4 == 0).all()), "quad lean kernel needs rows padded to multiples of 4 entries"
     args = [order.data_ptr(), B, row_ptr.data_ptr(), col_ptr.data_ptr(), nip.data_ptr(), lcol.data_ptr(),
             val.data_ptr(), y.data_ptr(), off.data_ptr(), wt.data_ptr(), scr.data_ptr(), n_rows, W.data_ptr(),
             f.data_ptr(), iters.data_ptr(), reason.data_ptr(), zout.data_ptr(),
@@ -914,7 +913,7 @@ def re_tron_csr(order, row_ptr, col_ptr, nip, lcol, val, y, off, wt, scr, W, f, 
         if gsc is None:
             gsc = torch.empty_like(W)
         assert gsc.is_cuda and gsc.dtype == torch.float64 and gsc.numel() >= W.numel() and gsc.device == W.device
-        check(lib.pml_re_tron_lean(*args, gsc.data_ptr(), stream_handle(W.device)), "re_tron_lean")
+        check(lib.pml_re_tron_lean(*args, gsc.data_ptr(), int(bool(quad)), stream_handle(W.device)), "re_tron_lean")
         return
     fn = lib.pml_re_tron_hess if hessian else lib.pml_re_tron_csr
     check(fn(*args, stream_handle(W.device)), "re_tron_csr")

@@ -42,11 +42,26 @@ RES_ROW_NNZ = 64
 RES_KMAX = int(os.environ.get("PML_RE_RES_KMAX", "128"))
 
 
-def _pad4(t: torch.Tensor) -> torch.Tensor:
-    """``t`` followed by 4 zero entries (the lean kernel's quad loads may touch up to 3 entries past a row)."""
-    out = torch.zeros(t.numel() + 4, dtype=t.dtype, device=t.device)
-    out[:t.numel()] = t
-    return out
+QUAD_MIN_ROW_NNZ = 12      # pad rows to whole quads when the mean row holds >= 12 entries (<= 25 % padding)
+
+
+def pad_rows_to_quads(nip: torch.Tensor, lcol: torch.Tensor, val: torch.Tensor):
+    """Rows padded to multiples of 4 entries with column 0 / value 0.0 (which add exactly nothing to a margin and
+    exactly 0 to an accumulator): ``(nip, lcol, val)`` of the padded CSR. The lean kernel then reads every row as
+    whole quads (row_pass_q); the other fused kernels read the padded rows unchanged."""
+    dev = nip.device
+    rn = nip[1:] - nip[:-1]
+    pn = (rn + 3) // 4 * 4
+    nip_p = torch.zeros_like(nip)
+    torch.cumsum(pn, 0, out=nip_p[1:])
+    nnz, nnz_p = int(nip[-1]), int(nip_p[-1])
+    row = torch.repeat_interleave(torch.arange(rn.numel(), device=dev), rn, output_size=nnz)
+    dst = nip_p[row] + (torch.arange(nnz, device=dev) - nip[row])
+    lcol_p = torch.zeros(nnz_p, dtype=lcol.dtype, device=dev)
+    val_p = torch.zeros(nnz_p, dtype=val.dtype, device=dev)
+    lcol_p[dst] = lcol[:nnz]
+    val_p[dst] = val[:nnz]
+    return nip_p, lcol_p, val_p
 
 
 def _launch_dmax(dm: int, de: torch.Tensor, is_h: bool) -> int:
@@ -144,10 +159,17 @@ class EntityTronBatch:
             # the kernel indexes LDS vectors of d_e entries with these
             assert int(lcol.min()) >= 0 and bool((lcol < de[nnz_ent]).all()), "entity-local column out of range"
         del nnz_ent, pos
-        # read as uint16 by the kernels (d_e <= 2048); the lean kernel reads aligned 4-entry quads, so both entry
-        # arrays carry 4 slack entries past the last row
-        self.lcol = _pad4(lcol.to(torch.int16))
-        self.nip, self.val = nip, _pad4(val)
+        self.lcol = lcol.to(torch.int16)                 # read as uint16 by the kernel (d_e <= 2048)
+        self.nip, self.val = nip, val
+        # rows padded to whole quads for the lean kernel's 4-entry loads (when rows are long enough that the padding
+        # costs little); the streaming and resident kernels read the padded rows unchanged
+        # (not with tall-narrow launches: re_tron_tall_kernel stages rows by ASSIGNMENT into a dense block, where a
+        # column-0 padding entry could overwrite the real column 0)
+        self.quad = (nnz > 0 and nnz >= QUAD_MIN_ROW_NNZ * n_rows and os.environ.get("PML_RE_QUAD", "1") != "0"
+                     and not bool((de <= HESS_DMAX).any()))
+        if self.quad:
+            self.nip, self.lcol, self.val = pad_rows_to_quads(self.nip, self.lcol, self.val)
+            nip = self.nip
         self.y, self.w = seg.y[row_sel].contiguous(), seg.w[row_sel].contiguous()
         self.n_rows = n_rows
         self.nnz = nnz
@@ -160,8 +182,6 @@ class EntityTronBatch:
         if nnz and int(ent_nnz.max()) >= (1 << 31):
             raise ValueError("an entity of the fused batch has >= 2^31 non-zeros (32-bit kernel offsets)")
         self.launches = []
-        from ..ops.native import LEAN_MAX_ENTITY_NNZ
-        self.lean_ok = bool(int(ent_nnz.max()) < LEAN_MAX_ENTITY_NNZ) if nnz else True
         hess = de <= HESS_DMAX
         # register-resident tasks (one persistent launch): clusters (k > 1 workgroups) first, largest first
         self.res = None
@@ -199,8 +219,8 @@ class EntityTronBatch:
                 if idx.numel() == 0:
                     continue
                 order = idx[torch.argsort(ent_nnz[idx], descending=True, stable=True)]
-                self.launches.append((_launch_dmax(dm, de[idx], is_h or not self.lean_ok),
-                                      order.to(torch.int32).contiguous(), bool(is_h)))
+                self.launches.append((_launch_dmax(dm, de[idx], is_h), order.to(torch.int32).contiguous(),
+                                      bool(is_h)))
 
     def solve(self, loss, l2: float, W0: Optional[torch.Tensor], offsets: torch.Tensor, tol: float, max_iter: int,
               max_fail: int = 5, max_cg: int = 20) -> FusedResult:
@@ -228,7 +248,7 @@ class EntityTronBatch:
         for dm, order, is_h in self.launches:
             re_tron_csr(order, self.row_ptr, self.col_ptr, self.nip, self.lcol, self.val, self.y, off, self.w,
                         self.scr, W, f, iters, reason, z, loss.loss_id, l2, tol, max_iter, max_fail, max_cg, dm,
-                        hessian=is_h, gsc=self.gsc, lean=None if self.lean_ok else False)
+                        hessian=is_h, gsc=self.gsc, quad=self.quad)
         self.W = W
         # the error flag stays on the device: reading it here would wait for the whole launch before the caller
         # can queue concurrent work (the row-space side stream); callers call FusedResult.check_error() later
@@ -250,8 +270,11 @@ class DenseEntityTronBatch:
         self.B, self.n, self.d = B, n, d
         ar = lambda k, step: torch.arange(k + 1, dtype=torch.int64, device=dev) * step
         self.row_ptr, self.col_ptr, self.nip = ar(B, n), ar(B, d), ar(B * n, d)
-        self.lcol = _pad4(torch.arange(d, dtype=torch.int16, device=dev).repeat(B * n))
-        self.val = _pad4(X.to(torch.float64).reshape(-1))
+        self.lcol = torch.arange(d, dtype=torch.int16, device=dev).repeat(B * n)
+        self.val = X.to(torch.float64).reshape(-1).contiguous()
+        self.quad = d >= QUAD_MIN_ROW_NNZ and d > HESS_DMAX and os.environ.get("PML_RE_QUAD", "1") != "0"
+        if self.quad:
+            self.nip, self.lcol, self.val = pad_rows_to_quads(self.nip, self.lcol, self.val)
         self.y = y.to(torch.float64).reshape(-1).contiguous()
         self.w = w.to(torch.float64).reshape(-1).contiguous()
         self.scr = torch.empty(4 * max(B * n, 1), dtype=torch.float64, device=dev)
@@ -275,5 +298,6 @@ class DenseEntityTronBatch:
         off = offsets.to(dev, torch.float64).reshape(-1).contiguous()
         dm, order, is_h = self.launch
         re_tron_csr(order, self.row_ptr, self.col_ptr, self.nip, self.lcol, self.val, self.y, off, self.w, self.scr,
-                    W, f, iters, reason, z, loss.loss_id, l2, tol, max_iter, max_fail, max_cg, dm, hessian=is_h)
+                    W, f, iters, reason, z, loss.loss_id, l2, tol, max_iter, max_fail, max_cg, dm, hessian=is_h,
+                    quad=self.quad)
         return FusedResult(W.view(B, d), f, iters.to(torch.long), reason.to(torch.long), z.view(B, n))

@@ -37,14 +37,17 @@ a = torch.randint(0, d - 1, (N, 1), generator=g, device=dev)
 s_ = strides[torch.randint(0, strides.numel(), (N, 1), generator=g, device=dev)]
 cols = (a + torch.arange(NNZ - 1, device=dev)[None, :] * s_) % (d - 1)
 cols, _ = torch.sort(cols, dim=1)
-lcol = torch.zeros(N * NNZ + 4, dtype=torch.int16, device=dev)      # + 4: the lean kernel's quad loads
-lcol[:N * NNZ] = torch.cat([cols, torch.full((N, 1), d - 1, device=dev)], 1).reshape(-1).to(torch.int16)
+lcol = torch.cat([cols, torch.full((N, 1), d - 1, device=dev)], 1).reshape(-1).to(torch.int16)
 del cols
-val = torch.zeros(N * NNZ + 4, dtype=torch.float64, device=dev)
-val[:N * NNZ] = torch.randn(N * NNZ, generator=g, device=dev, dtype=torch.float64)
-val[:N * NNZ].view(N, NNZ)[:, -1] = 1.0
+val = torch.randn(N * NNZ, generator=g, device=dev, dtype=torch.float64)
+val.view(N, NNZ)[:, -1] = 1.0
 DMAX = int(os.environ.get("PML_BENCH_DMAX", "1008"))     # lean launches: widest entity rounded up to 8
+QUAD = os.environ.get("PML_BENCH_QUAD", "1") != "0"     # lean kernel on rows padded to whole quads
 nip = torch.arange(N + 1, dtype=torch.int64, device=dev) * NNZ
+nip_q, lcol_q, val_q = nip, lcol, val
+if QUAD:
+    from photon_ml_amd.optimization.entity_tron import pad_rows_to_quads
+    nip_q, lcol_q, val_q = pad_rows_to_quads(nip, lcol, val)
 y = (torch.rand(N, generator=g, device=dev) < 0.4).double()
 off = torch.zeros(N, dtype=torch.float64, device=dev)
 wt = torch.ones(N, dtype=torch.float64, device=dev)
@@ -85,8 +88,10 @@ def run(kernel, order, reps=3):
                                1.0, 1e-12, 10, 5, 20, npass=np_)
     else:
         def call(np_=None):
-            re_tron_csr(order, row_ptr, col_ptr, nip, lcol, val, y, off, wt, scr, W, f, it, rc, z, 0, 1.0, 1e-12, 10,
-                        5, 20, DMAX if kernel == "lean" else 1024, npass=np_, lean=kernel == "lean")
+            q = kernel == "lean" and QUAD
+            re_tron_csr(order, row_ptr, col_ptr, nip_q if q else nip, lcol_q if q else lcol, val_q if q else val, y,
+                        off, wt, scr, W, f, it, rc, z, 0, 1.0, 1e-12, 10, 5, 20, DMAX if kernel == "lean" else 1024,
+                        npass=np_, lean=kernel == "lean", quad=q)
             return None
     err = call(npass)
     torch.cuda.synchronize()
