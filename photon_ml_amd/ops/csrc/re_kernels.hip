@@ -153,6 +153,13 @@ struct ReTronArgs {
   double* gsc;               // lean kernel: gradient at W, per coefficient (packed like W)
 };
 
+// Loads through the global address space: a generic pointer read through the kernel-argument struct becomes a FLAT
+// load, which also counts in lgkmcnt -- every LDS wait would then wait for it too.
+template <typename T>
+__device__ __forceinline__ T gld(const T* p) {
+  return *(const __attribute__((address_space(1))) T*)p;
+}
+
 // Sum over the 16 lanes of a DPP row, in every lane of the row (fixed-order butterflies: deterministic).
 __device__ __forceinline__ double row16_total(double v) {
   v += dpp_f64<0xB1>(v);    // quad_perm [1,0,3,2]
@@ -198,14 +205,17 @@ __device__ __forceinline__ void row_pass(const ReTronArgs& a, long long r0, long
   constexpr int BATCH = RE_RPI * U;
   const int step = RE_NW * BATCH;
   int base = w * BATCH;
-  // row pointers of a batch: lane j <= BATCH holds nip[base + j] (clamped to the entity's last row)
-  auto fetch_ptr = [&](int b) -> int {
+  // row pointers of a batch, prefetched one batch ahead: lane j <= BATCH holds nip[base + j] (clamped to the
+  // entity's end). The load is unconditional and its raw value is only converted at its use in the next batch, so
+  // the prefetch never waits (a conditional load / immediate conversion put a full memory round trip per batch)
+  auto fetch_raw = [&](int b) -> long long {
     const int i = b + (lane <= BATCH ? lane : BATCH);
-    return b < nrows ? (int)(nip[i < nrows ? i : nrows] - e0) : 0;
+    return gld(nip + (i < nrows ? i : nrows));
   };
-  int np = fetch_ptr(base);
+  long long npr = fetch_raw(base);
   for (; base < nrows; base += step) {
-    const int np_next = fetch_ptr(base + step);
+    const int np = (int)(npr - e0);
+    const long long npr_next = fetch_raw(base + step);
     int lo[U], hi[U];
     int c[U][RE_K];
     double v[U][RE_K], dot[U], rs[U][3];
@@ -216,12 +226,13 @@ __device__ __forceinline__ void row_pass(const ReTronArgs& a, long long r0, long
       hi[u] = __shfl(np, q + 1, 64);
       const int i = base + q;
       const bool valid = i < nrows;
+      const int ic = valid ? i : 0;
       if (MODE == 0) {
-        rs[u][0] = valid ? Dc[i] : 0.0;
+        rs[u][0] = valid ? gld(Dc + ic) : 0.0;
       } else {
-        rs[u][0] = valid ? wt[i] : 0.0;
-        rs[u][1] = valid ? off[i] : 0.0;
-        rs[u][2] = valid ? yv[i] : 0.0;
+        rs[u][0] = valid ? gld(wt + ic) : 0.0;
+        rs[u][1] = valid ? gld(off + ic) : 0.0;
+        rs[u][2] = valid ? gld(yv + ic) : 0.0;
       }
     }
 #pragma unroll
@@ -286,7 +297,7 @@ __device__ __forceinline__ void row_pass(const ReTronArgs& a, long long r0, long
         }
       for (int p = lo[u] + gl + RE_G * RE_K; p < hi[u]; p += RE_G) atomicAdd(&acc[lcol[p]], t * val[p]);
     }
-    np = np_next;
+    npr = npr_next;
   }
 }
 
@@ -299,6 +310,25 @@ __device__ __forceinline__ void row_pass(const ReTronArgs& a, long long r0, long
 // Only a quad past the row end is masked (no per-entry masks).
 typedef double re_d2 __attribute__((ext_vector_type(2)));
 typedef unsigned re_u2 __attribute__((ext_vector_type(2)));
+
+// Four LDS gathers in flight together (one wait for all four): left to itself the compiler issues each gather,
+// waits for it and consumes it before the next (register pressure), which serialises four LDS round trips per
+// lane per row group. ``vec`` is a __shared__ array; the byte offsets are its LDS addresses.
+__device__ __forceinline__ void lds_gather4(const double* vec, int c0, int c1, int c2, int c3, double& g0, double& g1,
+                                            double& g2, double& g3) {
+  const unsigned b = (unsigned)(uintptr_t)(const __attribute__((address_space(3))) double*)vec;
+  const unsigned a0 = b + 8u * (unsigned)c0, a1 = b + 8u * (unsigned)c1, a2 = b + 8u * (unsigned)c2,
+                 a3 = b + 8u * (unsigned)c3;
+  asm volatile(
+      "ds_read_b64 %0, %4\n\t"
+      "ds_read_b64 %1, %5\n\t"
+      "ds_read_b64 %2, %6\n\t"
+      "ds_read_b64 %3, %7\n\t"
+      "s_waitcnt lgkmcnt(0)"
+      : "=&v"(g0), "=&v"(g1), "=&v"(g2), "=&v"(g3)
+      : "v"(a0), "v"(a1), "v"(a2), "v"(a3)
+      : "memory");
+}
 
 template <int MODE, int LOSS, int U>
 __device__ __forceinline__ void row_pass_q(const ReTronArgs& a, long long r0, long long r1,
@@ -320,17 +350,18 @@ __device__ __forceinline__ void row_pass_q(const ReTronArgs& a, long long r0, lo
   constexpr int BATCH = RE_RPI * U;
   const int step = RE_NW * BATCH;
   int base = w * BATCH;
-  // row pointers of a batch, in quads: lane j <= BATCH holds nip[base + j] / 4
-  auto fetch_ptr = [&](int b) -> int {
+  // row pointers of a batch, in quads: lane j <= BATCH holds nip[base + j] / 4 (prefetched as in row_pass)
+  auto fetch_raw = [&](int b) -> long long {
     const int i = b + (lane <= BATCH ? lane : BATCH);
-    return b < nrows ? (int)((nip[i < nrows ? i : nrows] - e0) >> 2) : 0;
+    return gld(nip + (i < nrows ? i : nrows));
   };
   auto cols = [](re_u2 c, int (&k)[4]) {
     k[0] = (int)(c.x & 0xFFFFu); k[1] = (int)(c.x >> 16); k[2] = (int)(c.y & 0xFFFFu); k[3] = (int)(c.y >> 16);
   };
-  int np = fetch_ptr(base);
+  long long npr = fetch_raw(base);
   for (; base < nrows; base += step) {
-    const int np_next = fetch_ptr(base + step);
+    const int np = (int)((npr - e0) >> 2);
+    const long long npr_next = fetch_raw(base + step);
     int qa[U], qb[U];
     re_u2 c[U];
     re_d2 v0[U], v1[U];
@@ -342,21 +373,22 @@ __device__ __forceinline__ void row_pass_q(const ReTronArgs& a, long long r0, lo
       qb[u] = __shfl(np, q + 1, 64);                          // the row's end (quads)
       const int i = base + q;
       const bool valid = i < nrows;
+      const int ic = valid ? i : 0;
       if (MODE == 0) {
-        rs[u][0] = valid ? Dc[i] : 0.0;
+        rs[u][0] = valid ? gld(Dc + ic) : 0.0;
       } else {
-        rs[u][0] = valid ? wt[i] : 0.0;
-        rs[u][1] = valid ? off[i] : 0.0;
-        rs[u][2] = valid ? yv[i] : 0.0;
+        rs[u][0] = valid ? gld(wt + ic) : 0.0;
+        rs[u][1] = valid ? gld(off + ic) : 0.0;
+        rs[u][2] = valid ? gld(yv + ic) : 0.0;
       }
     }
 #pragma unroll
     for (int u = 0; u < U; ++u) {
       const bool in = qa[u] < qb[u];
       const int qq = in ? qa[u] : 0;
-      c[u] = cq[qq];
-      v0[u] = vq[2 * qq];
-      v1[u] = vq[2 * qq + 1];
+      c[u] = gld(cq + qq);
+      v0[u] = gld(vq + 2 * qq);
+      v1[u] = gld(vq + 2 * qq + 1);
       if (!in) { c[u] = re_u2{0u, 0u}; v0[u] = re_d2{0.0, 0.0}; v1[u] = re_d2{0.0, 0.0}; }
     }
 #pragma unroll
@@ -365,10 +397,12 @@ __device__ __forceinline__ void row_pass_q(const ReTronArgs& a, long long r0, lo
       if (MODE != 2) {
         int k[4];
         cols(c[u], k);
-        s = fma(v0[u].x, vec[k[0]], s);
-        s = fma(v0[u].y, vec[k[1]], s);
-        s = fma(v1[u].x, vec[k[2]], s);
-        s = fma(v1[u].y, vec[k[3]], s);
+        double g[4];
+        lds_gather4(vec, k[0], k[1], k[2], k[3], g[0], g[1], g[2], g[3]);
+        s = fma(v0[u].x, g[0], s);
+        s = fma(v0[u].y, g[1], s);
+        s = fma(v1[u].x, g[2], s);
+        s = fma(v1[u].y, g[3], s);
         for (int qq = qa[u] + RE_G; qq < qb[u]; qq += RE_G) {     // rows longer than 64 entries
           int kt[4];
           cols(cq[qq], kt);
@@ -418,7 +452,7 @@ __device__ __forceinline__ void row_pass_q(const ReTronArgs& a, long long r0, lo
         atomicAdd(&acc[kt[3]], t * a1.y);
       }
     }
-    np = np_next;
+    npr = npr_next;
   }
 }
 
