@@ -1323,7 +1323,9 @@ static int g_tl_pipe = 0;      // forward stream pipeline variant (see tl_stream
 static int g_tl_pipe_t = 0;    // transpose stream pipeline variant
 static int g_rs_variant = 5;   // rs_tron variant: 0-2 rs_tron_kernel<V>; for n <= 32: 3 (5: one wave per workgroup
                                 // for the LDS sizes, finer LDS occupancy granularity) rs_tron_dpp_kernel (L in registers
-                                // for n <= 16), 4 the same with L in LDS for every size (scripts/rs_tron_bench.py)
+                                // for n <= 16; n in (20, 32]: packed lower triangle in LDS), 4 the same with L in
+                                // LDS for every size, 6 one group-sum phase per CG step, 7 packed triangle for every
+                                // n > 16 (scripts/rs_tron_bench.py, profiles/rs_tron_roofline.md)
 static int g_tl_deep = 0;      // interleaved forward: 0 two-slot pipeline (P = 3), 1 deep S4/D1 (P = 5), 2 S6/D2 (P = 6)
 static int g_tl_deep_t = 0;    // interleaved transpose: same
 
@@ -2064,7 +2066,16 @@ __device__ __forceinline__ double group_sum(double v) {
   return v;
 }
 
-template <int K, bool LREG, int WL = 2>
+// Masked reads of the packed triangle. SEL = false: a conditional read, which the compiler puts under an exec mask
+// (SALU work; K = 32: 15.1 ms); SEL = true: an unconditional read + select (3 VALU per double, but fewer live
+// registers: K = 24 fits 3 waves / SIMD with 6 spilled VGPRs instead of 22; 9.8 vs 10.3 ms)
+__device__ __forceinline__ double tri_sel(double x, bool keep) {
+  asm("" : "+v"(x));
+  return keep ? x : 0.0;
+}
+#define tri_keep(x, keep) (Gm::SEL ? tri_sel((x), (keep)) : ((keep) ? (x) : 0.0))
+
+template <int K, bool LREG, int WL = 2, bool TRI = false>
 struct RsGeom {
   static constexpr int GL = K <= 4 ? 4 : (K <= 8 ? 8 : 16);
   static constexpr int P = 64 / GL;                 // problems per wave
@@ -2072,7 +2083,12 @@ struct RsGeom {
   static constexpr bool REG = LREG && R == 1;       // L in registers (else LDS)
   static constexpr int K1 = K > 16 ? K - 16 : 1;    // terms of the second column block
   static constexpr int SP = K + 1;                  // LDS row stride (doubles)
-  static constexpr int PS0 = K * SP;
+  // TRI (variant 7, K > 16): L packed as its lower triangle by rows, L[r][c] at r (r + 1) / 2 + c. The products
+  // read whole 16-entry blocks and mask the entries above the diagonal; the last of them (column i + 16 at row
+  // K - 1, i = 15) lies 32 - K + ... past the triangle, so the problem slot is padded to cover it
+  static constexpr int TRI_N = (K * (K + 1) / 2 > (K - 1) * K / 2 + 32) ? K * (K + 1) / 2 : (K - 1) * K / 2 + 32;
+  static constexpr int PS0 = (TRI && R == 2) ? TRI_N : K * SP;
+  static constexpr bool SEL = K == 24;             // masked reads: select (else exec-masked reads; tri_keep)
   // problem stride = 16 mod 32 doubles (measured: dropping the pad to fit 12 one-wave workgroups per CU at K = 20
   // gains nothing over variant 5, 7.66 vs 7.69 ms, and loses 3 % at K = 24)
   static constexpr int PS = PS0 + (((16 - PS0 % 32) % 32) + 32) % 32;
@@ -2084,14 +2100,29 @@ struct RsGeom {
 //   ||step + a d||^2 = ||step||^2 + 2 a step.d + a^2 d.d,   ||r - a Hd||^2 = r.r - 2 a r.Hd + a^2 Hd.Hd
 // (clamped at 0). The baseline variant pays a serial sum for d.Hd, then one for the two norms, and a third when a
 // problem hits the trust region.
-template <int K, bool LREG, int WL, bool MS = false>
-__global__ __launch_bounds__(256) void rs_tron_dpp_kernel(
+// occupancy asked of the register allocator (waves per SIMD): the packed-triangle K = 20 build lands 1 VGPR over
+// the 3-wave budget of 168 without it
+#ifndef RS_WPE20
+#define RS_WPE20 3
+#endif
+#ifndef RS_WPE24
+#define RS_WPE24 3
+#endif
+#ifndef RS_WPE32
+#define RS_WPE32 1
+#endif
+template <int K, bool TRI>
+constexpr int rs_dpp_wpe() { return !TRI ? 1 : K == 20 ? RS_WPE20 : K == 24 ? RS_WPE24 : K == 32 ? RS_WPE32 : 1; }
+
+template <int K, bool LREG, int WL, bool MS = false, bool TRI = false>
+__global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(rs_dpp_wpe<K, TRI>()))) void rs_tron_dpp_kernel(
     int B, int n, const double* __restrict__ Lm, const double* __restrict__ Y, const double* __restrict__ O,
     const double* __restrict__ WT, double* __restrict__ Beta, double* __restrict__ Fout, int* __restrict__ Iters,
     int* __restrict__ Reason, int loss, double l2, double tol, int max_iter, int max_fail, int max_cg,
     const int* __restrict__ order, double* __restrict__ Zout) {
-  using Gm = RsGeom<K, LREG, WL>;
+  using Gm = RsGeom<K, LREG, WL, TRI>;
   constexpr int GL = Gm::GL, P = Gm::P, R = Gm::R, K1 = Gm::K1, SP = Gm::SP, PS = Gm::PS;
+  constexpr bool PK = TRI && R == 2;              // packed lower triangle in LDS
   extern __shared__ double smem[];
   const int lane = threadIdx.x & 63, w = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
   const int q = lane / GL, i = lane % GL;
@@ -2124,6 +2155,26 @@ __global__ __launch_bounds__(256) void rs_tron_dpp_kernel(
       Lr[k] = ok ? Lb[(long long)i * n + k] : 0.0;
       Lc[k] = ok ? Lb[(long long)k * n + i] : 0.0;
     }
+  } else if constexpr (PK) {
+    // this wave's P problems, read row-major (coalesced) and stored packed; slot tails (the masked over-reads
+    // past the triangle) zero
+    const int wb = w * P * PS;
+    for (int idx = lane; idx < P * (PS - Gm::TRI_N + K * K); idx += 64) {
+      const int qq = idx / (PS - Gm::TRI_N + K * K), rem = idx - qq * (PS - Gm::TRI_N + K * K);
+      if (rem < K * K) {
+        const int r = rem / K, c = rem - r * K;
+        if (c <= r) {
+          double v = 0.0;
+          if (b0 + qq < B && r < n && c < n) v = Lm[prob(b0 + qq) * nn + (long long)r * n + c];
+          smem[wb + qq * PS + r * (r + 1) / 2 + c] = v;
+        }
+      } else {
+        smem[wb + qq * PS + K * (K + 1) / 2 + (rem - K * K)] = 0.0;
+      }
+    }
+    __builtin_amdgcn_s_waitcnt(0);
+    __builtin_amdgcn_wave_barrier();
+    lq = wb + q * PS;
   } else {
     const int wb = w * P * PS;
     for (int idx = lane; idx < P * PS; idx += 64) {
@@ -2167,6 +2218,26 @@ __global__ __launch_bounds__(256) void rs_tron_dpp_kernel(
 #pragma unroll
       for (int k = 0; k < K; ++k) m[k] = smem[base + k];
       out[0] = on[0] ? reg_mv(v[0], m) : 0.0;
+    } else if constexpr (PK) {
+      // rows i and i + 16 of the packed triangle; entries above the diagonal (k > i in the diagonal blocks) read
+      // the next row and are masked to 0 (the same products as the padded layout's stored zeros)
+      double m[16], m1[K1];
+      const int i1 = min(i + 16, K - 1);
+      int b0i = lq + i * (i + 1) / 2, b1i = lq + i1 * (i1 + 1) / 2;
+      asm volatile("" : "+v"(b0i), "+v"(b1i));
+#pragma unroll
+      for (int k = 0; k < 16; ++k) m[k] = tri_keep(smem[b0i + k], k <= i);
+      double a0 = 0.0, a1 = 0.0;
+      bcf<16, 16>(a0, a1, v[0], m);
+#pragma unroll
+      for (int k = 0; k < 16; ++k) m[k] = smem[b1i + k];
+#pragma unroll
+      for (int k = 0; k < K1; ++k) m1[k] = tri_keep(smem[b1i + 16 + k], k <= i);
+      double c0 = 0.0, c1 = 0.0;
+      bcf<16, 16>(c0, c1, v[0], m);
+      bcf<16, K1>(c0, c1, v[1], m1);
+      out[0] = on[0] ? a0 + a1 : 0.0;
+      out[1] = on[1] ? c0 + c1 : 0.0;
     } else {
       double m[16], m1[K1];
       // re-read L from LDS in every product: laundering the (integer) base keeps the compiler from hoisting
@@ -2198,6 +2269,24 @@ __global__ __launch_bounds__(256) void rs_tron_dpp_kernel(
 #pragma unroll
       for (int k = 0; k < K; ++k) m[k] = smem[base + k * SP];
       out[0] = on[0] ? reg_mv(u[0], m) : 0.0;
+    } else if constexpr (PK) {
+      // columns i and i + 16: L[k][c] at k (k + 1) / 2 + c; above-diagonal entries (k < c) masked
+      double m[16], m1[K1], m2[K1];
+      int c0i = lq + i, c1i = lq + min(i + 16, K - 1);
+      asm volatile("" : "+v"(c0i), "+v"(c1i));
+#pragma unroll
+      for (int k = 0; k < 16; ++k) m[k] = tri_keep(smem[c0i + k * (k + 1) / 2], k >= i);
+#pragma unroll
+      for (int k = 0; k < K1; ++k) {
+        m1[k] = smem[c0i + (16 + k) * (17 + k) / 2];
+        m2[k] = tri_keep(smem[c1i + (16 + k) * (17 + k) / 2], k >= i);
+      }
+      double a0 = 0.0, a1 = 0.0, c0 = 0.0, c1 = 0.0;
+      bcf<16, 16>(a0, a1, u[0], m);
+      bcf<16, K1>(a0, a1, u[1], m1);
+      bcf<16, K1>(c0, c1, u[1], m2);
+      out[0] = on[0] ? a0 + a1 : 0.0;
+      out[1] = on[1] ? c0 + c1 : 0.0;
     } else {
       double m[16], m1[K1], m2[K1];
       int c0i = lq + i, c1i = lq + min(i + 16, K - 1);
@@ -2441,16 +2530,16 @@ __global__ __launch_bounds__(256) void rs_tron_dpp_kernel(
   if (prob_on && i == 0) { Fout[b] = f; Iters[b] = it; Reason[b] = reason; }
 }
 
-template <int K, bool LREG, int WL = 2, bool MS = false>
+template <int K, bool LREG, int WL = 2, bool MS = false, bool TRI = false>
 static void launch_rs_tron_dpp(int B, int n, const double* L, const double* y, const double* off, const double* wt,
                                double* beta, double* f, int* iters, int* reason, int loss, double l2, double tol,
                                int max_iter, int max_fail, int max_cg, hipStream_t st, const int* order,
                                double* zout) {
-  using Gm = RsGeom<K, LREG, WL>;
+  using Gm = RsGeom<K, LREG, WL, TRI>;
   const long long waves = (B + Gm::P - 1) / Gm::P;
   const long long grid = (waves + Gm::WPB - 1) / Gm::WPB;
   const size_t lds = Gm::REG ? 0 : (size_t)Gm::WPB * Gm::P * Gm::PS * sizeof(double);
-  hipLaunchKernelGGL((rs_tron_dpp_kernel<K, LREG, WL, MS>), dim3((unsigned)grid), dim3(Gm::WPB * 64), lds, st, B, n, L, y, off, wt,
+  hipLaunchKernelGGL((rs_tron_dpp_kernel<K, LREG, WL, MS, TRI>), dim3((unsigned)grid), dim3(Gm::WPB * 64), lds, st, B, n, L, y, off, wt,
                      beta, f, iters, reason, loss, l2, tol, max_iter, max_fail, max_cg, order, zout);
 }
 
@@ -3326,10 +3415,15 @@ int pml_rs_tron(int B, int n, const double* L, const double* y, const double* of
 #define RS_DPP(KK)                                                                                              \
   (V == 3 ? launch_rs_tron_dpp<KK, true>(B, n, L, y, off, wt, beta, f, iters, reason, loss, l2, tol, max_iter,    \
                                          max_fail, max_cg, st, order, zout)                                              \
-   : V == 5 ? launch_rs_tron_dpp<KK, true, 1>(B, n, L, y, off, wt, beta, f, iters, reason, loss, l2, tol, max_iter, \
-                                              max_fail, max_cg, st, order, zout)                                         \
+   : V == 5 ? (KK > 20 ? launch_rs_tron_dpp<KK, true, 1, false, true>(B, n, L, y, off, wt, beta, f, iters, reason,  \
+                                                                     loss, l2, tol, max_iter, max_fail, max_cg, st,    \
+                                                                     order, zout)                                      \
+                        : launch_rs_tron_dpp<KK, true, 1>(B, n, L, y, off, wt, beta, f, iters, reason, loss, l2, tol,  \
+                                                          max_iter, max_fail, max_cg, st, order, zout))                \
    : V == 6 ? launch_rs_tron_dpp<KK, true, 1, true>(B, n, L, y, off, wt, beta, f, iters, reason, loss, l2, tol,    \
                                                     max_iter, max_fail, max_cg, st, order, zout)                         \
+   : V == 7 ? launch_rs_tron_dpp<KK, true, 1, false, true>(B, n, L, y, off, wt, beta, f, iters, reason, loss, l2, \
+                                                           tol, max_iter, max_fail, max_cg, st, order, zout)             \
           : launch_rs_tron_dpp<KK, false>(B, n, L, y, off, wt, beta, f, iters, reason, loss, l2, tol, max_iter,   \
                                           max_fail, max_cg, st, order, zout))
     if (n <= 4) RS_DPP(4);

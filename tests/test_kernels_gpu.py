@@ -348,7 +348,7 @@ _RS_SIZES_DPP = [("LOGISTIC", 4), ("POISSON", 8), ("SQUARED", 11), ("LOGISTIC", 
 
 @pytest.mark.gpu
 @pytest.mark.parametrize("loss_name,n,variant", [(l, n, v) for v in range(7) for l, n in _RS_SIZES]
-                         + [(l, n, v) for v in range(3, 7) for l, n in _RS_SIZES_DPP])
+                         + [(l, n, v) for v in range(3, 8) for l, n in _RS_SIZES_DPP])
 @pytest.mark.parametrize("warm", [False, True])
 def test_fused_row_space_tron_matches_batched_tron(loss_name, n, warm, variant):
     """rs_tron_kernel (whole per-problem TRON in one kernel) vs the vectorised batched TRON of
@@ -364,6 +364,36 @@ def test_fused_row_space_tron_matches_batched_tron(loss_name, n, warm, variant):
         _check_rs_tron(loss_name, n, warm, losses, rs_tron)
     finally:
         lib.pml_rs_set_variant(int(os.environ.get("PML_RS_VARIANT", "5")))
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("n", [17, 20, 21, 24, 27, 32])
+def test_rs_tron_packed_triangle_is_bitwise_equal(n):
+    """The packed lower-triangle LDS layout (variant 7; the default for n in (20, 32]) masks the entries above the
+    diagonal that the padded layout (variant 4) stores as zeros: the same products in the same order, so the same
+    solutions, objectives, iteration counts and margins bit for bit."""
+    import os
+    from photon_ml_amd.ops.native import require_glm_lib, rs_tron
+    lib = require_glm_lib()
+    g = torch.Generator(device="cuda").manual_seed(n)
+    B = 1001
+    L = torch.tril(torch.randn(B, n, n, dtype=torch.float64, device="cuda", generator=g)) * 0.5
+    L.diagonal(dim1=1, dim2=2).copy_(torch.rand(B, n, dtype=torch.float64, device="cuda", generator=g) + 0.5)
+    y = (torch.randn(B, n, dtype=torch.float64, device="cuda", generator=g) > 0).double()
+    o = 0.1 * torch.randn(B, n, dtype=torch.float64, device="cuda", generator=g)
+    w = torch.rand(B, n, dtype=torch.float64, device="cuda", generator=g) + 0.5
+    b0 = torch.zeros(B, n, dtype=torch.float64, device="cuda")
+    outs = []
+    try:
+        for v in (4, 5, 7):
+            lib.pml_rs_set_variant(v)
+            zout = torch.empty_like(b0)
+            outs.append((*rs_tron(L, y, o, w, b0, 0, 0.7, 1e-9, 30, zout=zout), zout))
+    finally:
+        lib.pml_rs_set_variant(int(os.environ.get("PML_RS_VARIANT", "5")))
+    for other in outs[1:]:
+        for a, b in zip(outs[0], other):
+            assert torch.equal(a, b)
 
 
 def _check_rs_tron(loss_name, n, warm, losses, rs_tron):
