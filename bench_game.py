@@ -287,6 +287,9 @@ def run(args, dev, rank: int = 0, world: int = 1, data=None, t_data: float = 0.0
         for rec in cd.history[-2 * args.steps:]:
             log(f"  iteration {rec.get('iteration')} coordinate {rec['coordinate']}: {rec['seconds']:.3f}s")
     route_coords = {k: c for k, c in coords.items() if hasattr(c, "routed_bytes")}
+    routing = coords["per-entity"].solver_routing() if hasattr(coords["per-entity"], "solver_routing") else {}
+    if rank == 0 and routing:
+        log(f"RE solver routing: {routing}")
     del cd, model, train_eval
     return {
         "metric": "GAME coord-descent iters/sec (fixed + per-entity random effect)",
@@ -319,6 +322,7 @@ def run(args, dev, rank: int = 0, world: int = 1, data=None, t_data: float = 0.0
         "coordinate_build_s": t_build,
         **({"route_s": route_s} if route_s else {}),
         **({"placement_s": t_place} if t_place is not None else {}),
+        **({"re_solver_routing": routing} if routing else {}),
         "routed_bytes_per_update": {k: int(all_reduce_scalar(float(getattr(c, "routed_bytes", 0)), "max"))
                                     for k, c in route_coords.items()},
     }

@@ -527,6 +527,27 @@ class RandomEffectCoordinate(Coordinate):
                   0 if sub is None else sub.entities.numel())
         return self._comps
 
+    def solver_routing(self) -> dict:
+        """Where this coordinate's entities are solved (after its first update): row-space / fused primal /
+        pass-path counts, the fused batch's register-resident clusters and launches. Diagnostics for benchmarks."""
+        comps = getattr(self, "_comps", None)
+        if comps is None:
+            return {}
+        rs, fused, sub = comps
+        out = {"row_space": 0 if rs is None else int(rs.B), "fused": 0 if fused is None else int(fused.B),
+               "pass_path": 0 if sub is None else int(sub.entities.numel())}
+        if fused is not None:
+            out["fused_launches"] = len(fused.launches)
+            out["heavy_to_pass_path"] = int(fused.n_heavy)
+            out["quad_rows"] = bool(fused.quad)
+            r = fused.res
+            if r is not None:
+                k = r["t0"][1:] - r["t0"][:-1]
+                out["resident"] = {"entities": r["n"], "clusters": r["clusters"], "workgroups": r["tickets"],
+                                   "largest_cluster": int(k.max()), "clusters_ge8": int((k >= 8).sum()),
+                                   "error_flag_checks": int(getattr(self, "_res_checks", 0))}
+        return out
+
     def _update_components(self, comps, model, l1: float, l2: float):
         """One update over the solver components (see :meth:`_components`). Each component warm-starts from its
         own last solution (the row-space beta, the fused batch's packed W, the subset's W) unless the starting
@@ -626,12 +647,14 @@ class RandomEffectCoordinate(Coordinate):
             parts["sub"] = res.W
         if fres is not None and rs_out is None:
             fres.check_error()
+            self._res_checks = getattr(self, "_res_checks", 0) + (fres.err is not None)
         if rs_out is not None:
             if overlap:
                 main.wait_stream(side)
             rres, z_rs, ss_rs = rs_out
             if fres is not None:
                 fres.check_error()                 # after the side-stream launch was queued
+                self._res_checks = getattr(self, "_res_checks", 0) + (fres.err is not None)
             iters.index_copy_(0, rs.ents, rres.iters)
             reasons.index_copy_(0, rs.ents, rres.reason)
             z += z_rs
@@ -884,6 +907,9 @@ class ShardedRandomEffectCoordinate(Coordinate):
     @property
     def last_stats(self):
         return self.inner.last_stats
+
+    def solver_routing(self) -> dict:
+        return self.inner.solver_routing()
 
     def set_config(self, opt_config):
         self.inner.set_config(opt_config)

@@ -1516,6 +1516,71 @@ __global__ __launch_bounds__(NTHREADS) void segdot_kernel(const double* __restri
   if (lane == 0) out[wv] = s;
 }
 
+// Long segments (a heavy-tail entity's 10^5..10^6 rows): one wave per segment serialises ~len / 64 dependent loads
+// (a 1M-row segment: ~4.5 ms). segdot_long_kernel: the first `nseg_w` waves take the SHORT segments as above (long
+// ones skip); the next waves take fixed chunks [w C, (w + 1) C) of the elements and sum the parts of the (at most
+// two) LONG segments that overlap the chunk: head[w] for the segment holding the chunk's first element, tail[w] for
+// one that starts inside the chunk. segdot_combine_kernel adds a long segment's parts in chunk order. Fixed
+// partition, fixed order: deterministic (not bitwise equal to the one-wave form, whose lane strides differ).
+#define SEGDOT_C 4096
+__device__ __forceinline__ int seg_of(const long long* __restrict__ ptr, int nseg, long long i) {
+  int lo = 0, hi = nseg - 1;                  // last s with ptr[s] <= i
+  while (lo < hi) {
+    const int mid = (lo + hi + 1) >> 1;
+    if (ptr[mid] <= i) lo = mid; else hi = mid - 1;
+  }
+  return lo;
+}
+
+__device__ __forceinline__ double seg_range_sum(const double* __restrict__ a, const double* __restrict__ b, int mode,
+                                                long long lo, long long hi, int lane) {
+  double s = 0.0;
+  for (long long i = lo + lane; i < hi; i += 64) {
+    const double x = a[i];
+    s += mode == 0 ? x * b[i] : (mode == 1 ? x : fabs(x));
+  }
+  return wave_sum(s);
+}
+
+__global__ __launch_bounds__(NTHREADS) void segdot_long_kernel(const double* __restrict__ a,
+                                                               const double* __restrict__ b, int mode,
+                                                               const long long* __restrict__ ptr, int nseg,
+                                                               int nseg_w, long long n, double* __restrict__ head,
+                                                               double* __restrict__ tail, double* __restrict__ out) {
+  const int wv = (blockIdx.x * NTHREADS + threadIdx.x) >> 6;
+  const int lane = threadIdx.x & 63;
+  if (wv < nseg_w) {
+    if (wv >= nseg) return;
+    const long long lo = ptr[wv], hi = ptr[wv + 1];
+    if (hi - lo > SEGDOT_C) return;
+    const double s = seg_range_sum(a, b, mode, lo, hi, lane);
+    if (lane == 0) out[wv] = s;
+    return;
+  }
+  const long long w = wv - nseg_w;
+  const long long c0 = w * SEGDOT_C, c1 = c0 + SEGDOT_C < n ? c0 + SEGDOT_C : n;
+  if (c0 >= n) return;
+  const int s0 = seg_of(ptr, nseg, c0), s1 = seg_of(ptr, nseg, c1 - 1);
+  double h = 0.0, t = 0.0;
+  if (ptr[s0 + 1] - ptr[s0] > SEGDOT_C) h = seg_range_sum(a, b, mode, c0, ptr[s0 + 1] < c1 ? ptr[s0 + 1] : c1, lane);
+  if (s1 != s0 && ptr[s1 + 1] - ptr[s1] > SEGDOT_C) t = seg_range_sum(a, b, mode, ptr[s1], c1, lane);
+  if (lane == 0) { head[w] = h; tail[w] = t; }
+}
+
+__global__ __launch_bounds__(NTHREADS) void segdot_combine_kernel(const long long* __restrict__ ptr, int nseg,
+                                                                  const double* __restrict__ head,
+                                                                  const double* __restrict__ tail,
+                                                                  double* __restrict__ out) {
+  const int s = blockIdx.x * NTHREADS + threadIdx.x;
+  if (s >= nseg) return;
+  const long long lo = ptr[s], hi = ptr[s + 1];
+  if (hi - lo <= SEGDOT_C) return;
+  const long long w0 = lo / SEGDOT_C, w1 = (hi - 1) / SEGDOT_C;
+  double acc = lo == w0 * SEGDOT_C ? head[w0] : tail[w0];
+  for (long long w = w0 + 1; w <= w1; ++w) acc += head[w];
+  out[s] = acc;
+}
+
 // Segment expansion: out[i] = src[e] for i in [ptr[e], ptr[e+1]) — per-entity scalars broadcast to the
 // concatenated coefficient vector without reading an int64 index per element (one wave per segment).
 template <typename T>
@@ -3483,6 +3548,23 @@ int pml_segdot(const double* a, const double* b, int mode, const long long* ptr,
   const int per = NTHREADS / 64;
   hipLaunchKernelGGL(segdot_kernel, dim3((nseg + per - 1) / per), dim3(NTHREADS), 0, (hipStream_t)stream, a, b,
                      mode, ptr, nseg, out);
+  LAUNCH_CHECK();
+  return 0;
+}
+
+// segments longer than SEGDOT_C present (the caller knows its segment table): scratch >= 2 ceil(n / SEGDOT_C)
+int pml_segdot_long(const double* a, const double* b, int mode, const long long* ptr, int nseg, long long n,
+                    double* scratch, double* out, void* stream) {
+  if (nseg <= 0) return 0;
+  const int per = NTHREADS / 64;
+  const long long nch = (n + SEGDOT_C - 1) / SEGDOT_C;
+  const long long nseg_w = ((long long)nseg + per - 1) / per * per;
+  hipStream_t st = (hipStream_t)stream;
+  hipLaunchKernelGGL(segdot_long_kernel, dim3((unsigned)((nseg_w + nch + per - 1) / per)), dim3(NTHREADS), 0, st, a, b,
+                     mode, ptr, nseg, (int)nseg_w, n, scratch, scratch + nch, out);
+  LAUNCH_CHECK();
+  hipLaunchKernelGGL(segdot_combine_kernel, dim3((nseg + NTHREADS - 1) / NTHREADS), dim3(NTHREADS), 0, st, ptr, nseg,
+                     scratch, scratch + nch, out);
   LAUNCH_CHECK();
   return 0;
 }

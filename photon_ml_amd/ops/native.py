@@ -128,6 +128,8 @@ def glm_lib() -> Optional[ctypes.CDLL]:
                                          c_void_p, c_void_p, c_void_p, c_void_p, c_void_p, c_void_p, c_int, c_void_p,
                                          c_void_p]
         lib.pml_segdot.argtypes = [c_void_p, c_void_p, c_int, c_void_p, c_int, c_void_p, c_void_p]
+        lib.pml_segdot_long.argtypes = [c_void_p, c_void_p, c_int, c_void_p, c_int, ctypes.c_longlong, c_void_p,
+                                        c_void_p, c_void_p]
         lib.pml_seg_expand.argtypes = [c_void_p, c_int, c_void_p, c_void_p, c_int, c_void_p]
         lib.pml_seg_cg_step.argtypes = [c_void_p, c_int] + [c_void_p] * 7 + [c_double, c_void_p]
         lib.pml_bgemv.argtypes = [c_int, c_int, c_void_p, c_void_p, c_void_p, c_int, c_void_p]
@@ -163,7 +165,7 @@ def glm_lib() -> Optional[ctypes.CDLL]:
         lib.pml_rs_tron.argtypes = [c_int, c_int] + [c_void_p] * 8 + [c_int, c_double, c_double, c_int, c_int, c_int,
                                                                       c_void_p, c_void_p, c_void_p]
         for f in ("pml_seg_fwd", "pml_seg_t", "pml_reduce_stats", "pml_build_blocks", "pml_tl_fwd", "pml_tl_t",
-                  "pml_tl_maxbits", "pml_segdot", "pml_tl_fwd_multi", "pml_tl_t_multi", "pml_seg_cg_step",
+                  "pml_tl_maxbits", "pml_segdot", "pml_segdot_long", "pml_tl_fwd_multi", "pml_tl_t_multi", "pml_seg_cg_step",
                   "pml_seg_expand", "pml_bgemv", "pml_bhv", "pml_rs_tron", "pml_ls_eval", "pml_gram_grid", "pml_gram",
                   "pml_lincomb", "pml_lbfgs_pair", "pml_ls_dots", "pml_two_loop_chain", "pml_two_loop_gram",
                   "pml_two_loop_gram_grid"):
@@ -229,9 +231,24 @@ def segdot(a: torch.Tensor, b: Optional[torch.Tensor], ptr: torch.Tensor, mode: 
     a = a.contiguous()
     b = a if b is None else b.contiguous()
     out = torch.empty(nseg, dtype=torch.float64, device=a.device)
+    # the longest segment, measured once per segment table (one host read; the tables are built once per
+    # dataset): segments longer than SEGDOT_CHUNK are split over chunk waves (pml_segdot_long)
+    maxlen = getattr(ptr, "_pml_maxlen", None)
+    if maxlen is None:
+        maxlen = int((ptr[1:] - ptr[:-1]).max()) if nseg else 0
+        ptr._pml_maxlen = maxlen
+    if maxlen > SEGDOT_CHUNK:
+        n = a.numel()
+        scratch = torch.empty(2 * ((n + SEGDOT_CHUNK - 1) // SEGDOT_CHUNK), dtype=torch.float64, device=a.device)
+        check(lib.pml_segdot_long(a.data_ptr(), b.data_ptr(), mode, ptr.data_ptr(), nseg, n, scratch.data_ptr(),
+                                  out.data_ptr(), stream_handle(a.device)), "segdot_long")
+        return out
     check(lib.pml_segdot(a.data_ptr(), b.data_ptr(), mode, ptr.data_ptr(), nseg, out.data_ptr(),
                          stream_handle(a.device)), "segdot")
     return out
+
+
+SEGDOT_CHUNK = 4096        # = SEGDOT_C in glm_kernels.hip
 
 
 GRAM_MAXK = 22

@@ -182,6 +182,35 @@ def test_segdot_kernel():
         assert torch.equal(got, again)
 
 
+def test_segdot_long_segments():
+    """Heavy-tail segment tables (segments of 10^5..10^6 elements next to empty and short ones, boundaries on and
+    off the 4096-element chunk grid): the chunked path (pml_segdot_long) matches the fp64 reference and is
+    deterministic."""
+    from photon_ml_amd.ops.native import SEGDOT_CHUNK, segdot
+    rng = np.random.default_rng(3)
+    lens = rng.integers(0, 40, size=5000)
+    lens[[7, 8, 9]] = [0, 100_000, 0]
+    lens[100] = 1_000_000
+    lens[101] = SEGDOT_CHUNK + 1
+    lens[4999] = 3 * SEGDOT_CHUNK
+    # a long segment starting exactly on a chunk boundary
+    head = int(lens[:200].sum())
+    lens[200] = (-head) % SEGDOT_CHUNK + SEGDOT_CHUNK
+    lens[201] = 2 * SEGDOT_CHUNK
+    ptr = torch.from_numpy(np.concatenate([[0], np.cumsum(lens)]).astype(np.int64))
+    assert int(ptr[201]) % SEGDOT_CHUNK == 0
+    n = int(ptr[-1])
+    a = torch.from_numpy(rng.normal(size=n))
+    b = torch.from_numpy(rng.normal(size=n))
+    for mode in (0, 1, 2):
+        ref = segdot(a, b, ptr, mode)
+        pc = ptr.cuda()
+        got = segdot(a.cuda(), b.cuda(), pc, mode)
+        assert pc._pml_maxlen > SEGDOT_CHUNK
+        torch.testing.assert_close(got.cpu(), ref, rtol=1e-11, atol=1e-9)
+        assert torch.equal(got, segdot(a.cuda(), b.cuda(), pc, mode))
+
+
 @pytest.mark.parametrize("col_windows", [False, True])
 def test_tl_multi_launch_matches_per_chunk(col_windows):
     """Shard-wide launches (forward: all chunks' blocks; transpose: all chunks' items + one combine) vs one launch
