@@ -1325,7 +1325,8 @@ static int g_rs_variant = 5;   // rs_tron variant: 0-2 rs_tron_kernel<V>; for n 
                                 // for the LDS sizes, finer LDS occupancy granularity) rs_tron_dpp_kernel (L in registers
                                 // for n <= 16; n in (20, 32]: packed lower triangle in LDS), 4 the same with L in
                                 // LDS for every size, 6 one group-sum phase per CG step, 7 packed triangle for every
-                                // n > 16 (scripts/rs_tron_bench.py, profiles/rs_tron_roofline.md)
+                                // n > 16; n > 32: 5 / 8 one problem per wave with permlane block rotation
+                                // (scripts/rs_tron_bench.py, profiles/rs_tron_roofline.md)
 static int g_tl_deep = 0;      // interleaved forward: 0 two-slot pipeline (P = 3), 1 deep S4/D1 (P = 5), 2 S6/D2 (P = 6)
 static int g_tl_deep_t = 0;    // interleaved transpose: same
 
@@ -2097,12 +2098,41 @@ __global__ __launch_bounds__(NTHREADS) void rs_tron_kernel(
 __attribute__((used)) static const char pml_build_stamp[] = "PML_BUILD_ID=" PML_BUILD_ID;
 
 // two independent group sums, stage by stage (ILP 2 on the DPP / add latency chain)
+// Cross-row exchanges of a double for 64-lane problem groups (CDNA4 v_permlane16_swap / v_permlane32_swap, no LDS
+// crossbar). pl_swap<16>(x) = (A, B) with A = [x0, x0, x2, x2], B = [x1, x1, x3, x3] per 16-lane row (rows 0-3);
+// pl_swap<32>(x): A = [x0, x1, x0, x1], B = [x2, x3, x2, x3]. A + B is the xor-16 / xor-32 butterfly sum, in the
+// same operand order on every lane (bitwise equal everywhere).
+template <int D>
+__device__ __forceinline__ void pl_swap(double x, double& A, double& B) {
+  const long long b = __builtin_bit_cast(long long, x);
+  const unsigned lo = (unsigned)b, hi = (unsigned)(b >> 32);
+  unsigned alo, ahi, blo, bhi;
+  if constexpr (D == 16) {
+    const auto rl = __builtin_amdgcn_permlane16_swap(lo, lo, false, false);
+    const auto rh = __builtin_amdgcn_permlane16_swap(hi, hi, false, false);
+    alo = rl[0]; blo = rl[1]; ahi = rh[0]; bhi = rh[1];
+  } else {
+    const auto rl = __builtin_amdgcn_permlane32_swap(lo, lo, false, false);
+    const auto rh = __builtin_amdgcn_permlane32_swap(hi, hi, false, false);
+    alo = rl[0]; blo = rl[1]; ahi = rh[0]; bhi = rh[1];
+  }
+  A = __builtin_bit_cast(double, ((unsigned long long)ahi << 32) | alo);
+  B = __builtin_bit_cast(double, ((unsigned long long)bhi << 32) | blo);
+}
+template <int D>
+__device__ __forceinline__ double pl_sum(double x) {
+  double A, B;
+  pl_swap<D>(x, A, B);
+  return A + B;
+}
+
 template <int GL>
 __device__ __forceinline__ void group_sum2(double& a, double& b) {
   a += dpp_f64<0xB1>(a); b += dpp_f64<0xB1>(b);
   a += dpp_f64<0x4E>(a); b += dpp_f64<0x4E>(b);
   if constexpr (GL >= 8) { a += dpp_f64<0x141>(a); b += dpp_f64<0x141>(b); }
   if constexpr (GL >= 16) { a += dpp_f64<0x140>(a); b += dpp_f64<0x140>(b); }
+  if constexpr (GL >= 64) { a = pl_sum<16>(a); b = pl_sum<16>(b); a = pl_sum<32>(a); b = pl_sum<32>(b); }
 }
 
 // five independent group sums, stage by stage (ILP 5)
@@ -2120,6 +2150,12 @@ __device__ __forceinline__ void group_sum5(double (&v)[5]) {
 #pragma unroll
     for (int j = 0; j < 5; ++j) v[j] += dpp_f64<0x140>(v[j]);
   }
+  if constexpr (GL >= 64) {
+#pragma unroll
+    for (int j = 0; j < 5; ++j) v[j] = pl_sum<16>(v[j]);
+#pragma unroll
+    for (int j = 0; j < 5; ++j) v[j] = pl_sum<32>(v[j]);
+  }
 }
 
 template <int GL>
@@ -2128,6 +2164,7 @@ __device__ __forceinline__ double group_sum(double v) {
   v += dpp_f64<0x4E>(v);                       // quad_perm [2,3,0,1]
   if constexpr (GL >= 8) v += dpp_f64<0x141>(v);   // row_half_mirror
   if constexpr (GL >= 16) v += dpp_f64<0x140>(v);  // row_mirror
+  if constexpr (GL >= 64) { v = pl_sum<16>(v); v = pl_sum<32>(v); }
   return v;
 }
 
@@ -2139,21 +2176,26 @@ __device__ __forceinline__ double tri_sel(double x, bool keep) {
   return keep ? x : 0.0;
 }
 #define tri_keep(x, keep) (Gm::SEL ? tri_sel((x), (keep)) : ((keep) ? (x) : 0.0))
+#ifndef RS_SEL64
+#define RS_SEL64 1
+#endif
 
 template <int K, bool LREG, int WL = 2, bool TRI = false>
 struct RsGeom {
-  static constexpr int GL = K <= 4 ? 4 : (K <= 8 ? 8 : 16);
+  // K = 48 / 64 (variant 8): one problem per wave, lane i holds entry i (GL = 64)
+  static constexpr int GL = K <= 4 ? 4 : (K <= 8 ? 8 : (K <= 32 ? 16 : 64));
   static constexpr int P = 64 / GL;                 // problems per wave
-  static constexpr int R = (K + 15) / 16;           // vector entries per lane
-  static constexpr bool REG = LREG && R == 1;       // L in registers (else LDS)
-  static constexpr int K1 = K > 16 ? K - 16 : 1;    // terms of the second column block
+  static constexpr int R = GL == 64 ? 1 : (K + 15) / 16;   // vector entries per lane
+  static constexpr bool REG = LREG && R == 1 && GL <= 16;  // L in registers (else LDS)
+  static constexpr int K1 = K > 16 && GL == 16 ? K - 16 : 1;   // terms of the second column block
   static constexpr int SP = K + 1;                  // LDS row stride (doubles)
   // TRI (variant 7, K > 16): L packed as its lower triangle by rows, L[r][c] at r (r + 1) / 2 + c. The products
   // read whole 16-entry blocks and mask the entries above the diagonal; the last of them (column i + 16 at row
   // K - 1, i = 15) lies 32 - K + ... past the triangle, so the problem slot is padded to cover it
-  static constexpr int TRI_N = (K * (K + 1) / 2 > (K - 1) * K / 2 + 32) ? K * (K + 1) / 2 : (K - 1) * K / 2 + 32;
-  static constexpr int PS0 = (TRI && R == 2) ? TRI_N : K * SP;
-  static constexpr bool SEL = K == 24;             // masked reads: select (else exec-masked reads; tri_keep)
+  static constexpr int TRI_N = GL == 64 ? 64 * 65 / 2   // GL = 64: unconditional reads of rows / columns < 64
+                               : (K * (K + 1) / 2 > (K - 1) * K / 2 + 32) ? K * (K + 1) / 2 : (K - 1) * K / 2 + 32;
+  static constexpr int PS0 = (TRI && (R == 2 || GL == 64)) ? TRI_N : K * SP;
+  static constexpr bool SEL = K == 24 || RS_SEL64;   // masked reads: select (else exec-masked reads; tri_keep)
   // problem stride = 16 mod 32 doubles (measured: dropping the pad to fit 12 one-wave workgroups per CU at K = 20
   // gains nothing over variant 5, 7.66 vs 7.69 ms, and loses 3 % at K = 24)
   static constexpr int PS = PS0 + (((16 - PS0 % 32) % 32) + 32) % 32;
@@ -2176,8 +2218,20 @@ struct RsGeom {
 #ifndef RS_WPE32
 #define RS_WPE32 1
 #endif
+#ifndef RS_SERIAL_BLOCKS
+#define RS_SERIAL_BLOCKS 0     // K = 48 / 64: each 16-column block's LDS reads wait for the previous block's FMAs
+#endif
+#ifndef RS_WPE48
+#define RS_WPE48 1
+#endif
+#ifndef RS_WPE64
+#define RS_WPE64 1
+#endif
 template <int K, bool TRI>
-constexpr int rs_dpp_wpe() { return !TRI ? 1 : K == 20 ? RS_WPE20 : K == 24 ? RS_WPE24 : K == 32 ? RS_WPE32 : 1; }
+constexpr int rs_dpp_wpe() {
+  return !TRI ? 1 : K == 20 ? RS_WPE20 : K == 24 ? RS_WPE24 : K == 32 ? RS_WPE32 : K == 48 ? RS_WPE48
+                  : K == 64 ? RS_WPE64 : 1;
+}
 
 template <int K, bool LREG, int WL, bool MS = false, bool TRI = false>
 __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(rs_dpp_wpe<K, TRI>()))) void rs_tron_dpp_kernel(
@@ -2187,7 +2241,7 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(rs_dpp_wpe<
     const int* __restrict__ order, double* __restrict__ Zout) {
   using Gm = RsGeom<K, LREG, WL, TRI>;
   constexpr int GL = Gm::GL, P = Gm::P, R = Gm::R, K1 = Gm::K1, SP = Gm::SP, PS = Gm::PS;
-  constexpr bool PK = TRI && R == 2;              // packed lower triangle in LDS
+  constexpr bool PK = TRI && (R == 2 || GL == 64);   // packed lower triangle in LDS
   extern __shared__ double smem[];
   const int lane = threadIdx.x & 63, w = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
   const int q = lane / GL, i = lane % GL;
@@ -2254,7 +2308,7 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(rs_dpp_wpe<
   }
   // sum_k m[k] * (entry k of the lane's problem vector), L in registers
   auto reg_mv = [&](double v, const double (&m)[R == 1 ? K : 1]) {
-    if constexpr (R != 1) {
+    if constexpr (R != 1 || GL > 16) {
       return 0.0;
     } else if constexpr (GL == 16) {
       double a0 = 0.0, a1 = 0.0;
@@ -2276,13 +2330,41 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(rs_dpp_wpe<
   auto mv = [&](const double (&v)[R], double (&out)[R]) {
     if constexpr (Gm::REG) {
       out[0] = on[0] ? reg_mv(v[0], Lr) : 0.0;
-    } else if constexpr (R == 1) {
+    } else if constexpr (R == 1 && GL <= 16) {
       double m[K];
       int base = lq + i * SP;
       asm volatile("" : "+v"(base));   // re-read L from LDS in every product (no hoisting into registers)
 #pragma unroll
       for (int k = 0; k < K; ++k) m[k] = smem[base + k];
       out[0] = on[0] ? reg_mv(v[0], m) : 0.0;
+    } else if constexpr (GL == 64) {
+      // one problem per wave, lane i = 16 a + ii holds entry i. Column block b = a ^ s of the vector reaches row a
+      // through a permlane swap (s = 1: xor 16, s = 2: xor 32, s = 3: both), then row_newbcast:k broadcasts its
+      // entry k into the FMA. L rows from the packed triangle; blocks above the diagonal (b > a) and entries
+      // k > ii of the diagonal block are masked (exec-masked reads)
+      const int a = i >> 4, ii = i & 15;
+      double S[4], A, Bv;
+      S[0] = v[0];
+      pl_swap<16>(v[0], A, Bv);
+      S[1] = (a & 1) ? A : Bv;
+      pl_swap<32>(v[0], A, Bv);
+      S[2] = (a & 2) ? A : Bv;
+      pl_swap<32>(S[1], A, Bv);
+      S[3] = (a & 2) ? A : Bv;
+      int rb = lq + i * (i + 1) / 2;
+      asm volatile("" : "+v"(rb));
+      double a0 = 0.0, a1 = 0.0;
+#pragma unroll
+      for (int s = 0; s < 4; ++s) {
+        int cb = rb + 16 * (a ^ s);
+        if (RS_SERIAL_BLOCKS) asm volatile("" : "+v"(cb) : "v"(a0));   // block s's reads after block s - 1's FMAs
+        const bool below = (a ^ s) < a && i < K;
+        double m[16];
+#pragma unroll
+        for (int k = 0; k < 16; ++k) m[k] = tri_keep(smem[cb + k], s == 0 ? (k <= ii && i < K) : below);
+        bcf<16, 16>(a0, a1, S[s], m);
+      }
+      out[0] = on[0] ? a0 + a1 : 0.0;
     } else if constexpr (PK) {
       // rows i and i + 16 of the packed triangle; entries above the diagonal (k > i in the diagonal blocks) read
       // the next row and are masked to 0 (the same products as the padded layout's stored zeros)
@@ -2327,13 +2409,42 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(rs_dpp_wpe<
   auto mvt = [&](const double (&u)[R], double (&out)[R]) {
     if constexpr (Gm::REG) {
       out[0] = on[0] ? reg_mv(u[0], Lc) : 0.0;
-    } else if constexpr (R == 1) {
+    } else if constexpr (R == 1 && GL <= 16) {
       double m[K];
       int base = lq + i;
       asm volatile("" : "+v"(base));
 #pragma unroll
       for (int k = 0; k < K; ++k) m[k] = smem[base + k * SP];
       out[0] = on[0] ? reg_mv(u[0], m) : 0.0;
+    } else if constexpr (GL == 64) {
+      // (L^T u)_c for lane c = i: rows r = 16 b + k of column c, b = a ^ s, at r (r + 1) / 2 + c; kept when r >= c
+      // (b > a, or b == a and k >= ii) and r < K
+      const int a = i >> 4, ii = i & 15;
+      double S[4], A, Bv;
+      S[0] = u[0];
+      pl_swap<16>(u[0], A, Bv);
+      S[1] = (a & 1) ? A : Bv;
+      pl_swap<32>(u[0], A, Bv);
+      S[2] = (a & 2) ? A : Bv;
+      pl_swap<32>(S[1], A, Bv);
+      S[3] = (a & 2) ? A : Bv;
+      double a0 = 0.0, a1 = 0.0;
+#pragma unroll
+      for (int s = 0; s < 4; ++s) {
+        const int b = a ^ s;
+        int cbase = lq + i + 8 * b * (16 * b + 1);     // column c at row 16 b: T(16 b) + c
+        if (RS_SERIAL_BLOCKS) asm volatile("" : "+v"(cbase) : "v"(a0));
+        else asm volatile("" : "+v"(cbase));
+        const bool above = b > a && 16 * b < K;
+        double m[16];
+#pragma unroll
+        for (int k = 0; k < 16; ++k) {
+          const bool keep = (s == 0 ? k >= ii : above) && 16 * b + k < K;
+          m[k] = tri_keep(smem[cbase + 16 * b * k + k * (k + 1) / 2], keep);
+        }
+        bcf<16, 16>(a0, a1, S[s], m);
+      }
+      out[0] = on[0] ? a0 + a1 : 0.0;
     } else if constexpr (PK) {
       // columns i and i + 16: L[k][c] at k (k + 1) / 2 + c; above-diagonal entries (k < c) masked
       double m[16], m1[K1], m2[K1];
@@ -3480,7 +3591,7 @@ int pml_rs_tron(int B, int n, const double* L, const double* y, const double* of
 #define RS_DPP(KK)                                                                                              \
   (V == 3 ? launch_rs_tron_dpp<KK, true>(B, n, L, y, off, wt, beta, f, iters, reason, loss, l2, tol, max_iter,    \
                                          max_fail, max_cg, st, order, zout)                                              \
-   : V == 5 ? (KK > 20 ? launch_rs_tron_dpp<KK, true, 1, false, true>(B, n, L, y, off, wt, beta, f, iters, reason,  \
+   : (V == 5 || V == 8) ? (KK > 20 ? launch_rs_tron_dpp<KK, true, 1, false, true>(B, n, L, y, off, wt, beta, f, iters, reason,  \
                                                                      loss, l2, tol, max_iter, max_fail, max_cg, st,    \
                                                                      order, zout)                                      \
                         : launch_rs_tron_dpp<KK, true, 1>(B, n, L, y, off, wt, beta, f, iters, reason, loss, l2, tol,  \
@@ -3499,6 +3610,18 @@ int pml_rs_tron(int B, int n, const double* L, const double* y, const double* of
     else if (n <= 24) RS_DPP(24);
     else RS_DPP(32);
 #undef RS_DPP
+    LAUNCH_CHECK();
+    return 0;
+  }
+  // n in (32, 64]: one problem per wave, DPP-broadcast FMAs over permlane-rotated column blocks (variant 8, the
+  // default: 1.57x at n = 64, 1.15x at n = 48 over rs_tron_kernel<2>; profiles/rs_tron_roofline.md)
+  if ((V == 5 || V == 8) && n > 32) {
+    if (n <= 48)
+      launch_rs_tron_dpp<48, false, 1, false, true>(B, n, L, y, off, wt, beta, f, iters, reason, loss, l2, tol,
+                                                    max_iter, max_fail, max_cg, st, order, zout);
+    else
+      launch_rs_tron_dpp<64, false, 1, false, true>(B, n, L, y, off, wt, beta, f, iters, reason, loss, l2, tol,
+                                                    max_iter, max_fail, max_cg, st, order, zout);
     LAUNCH_CHECK();
     return 0;
   }

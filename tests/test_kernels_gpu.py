@@ -371,13 +371,15 @@ def test_batched_small_gemv_and_hv_match_torch(n):
 
 
 _RS_SIZES = [("LOGISTIC", 20), ("POISSON", 7), ("SQUARED", 33), ("LOGISTIC", 64), ("LOGISTIC", 1)]
+_RS_SIZES_WIDE = [("POISSON", 40), ("LOGISTIC", 48), ("SQUARED", 49), ("LOGISTIC", 57), ("POISSON", 64)]
 _RS_SIZES_DPP = [("LOGISTIC", 4), ("POISSON", 8), ("SQUARED", 11), ("LOGISTIC", 16), ("POISSON", 18),
                  ("LOGISTIC", 24), ("SQUARED", 29), ("LOGISTIC", 32)]
 
 
 @pytest.mark.gpu
 @pytest.mark.parametrize("loss_name,n,variant", [(l, n, v) for v in range(7) for l, n in _RS_SIZES]
-                         + [(l, n, v) for v in range(3, 8) for l, n in _RS_SIZES_DPP])
+                         + [(l, n, v) for v in range(3, 8) for l, n in _RS_SIZES_DPP]
+                         + [(l, n, 8) for l, n in _RS_SIZES + _RS_SIZES_WIDE])
 @pytest.mark.parametrize("warm", [False, True])
 def test_fused_row_space_tron_matches_batched_tron(loss_name, n, warm, variant):
     """rs_tron_kernel (whole per-problem TRON in one kernel) vs the vectorised batched TRON of
