@@ -100,6 +100,11 @@ def row_space_eligible(l1: float, constraints=None) -> bool:
 SIZE_CLASSES = (1, 2, 4, 8, 12, 16, 24, 32, 48, 64, 80, 96, 112, 128, 160, 192)
 ROW_SPACE_NMAX = 192      # rs_tron_big_kernel / seg_gram_kernel limit (one wave per problem, packed L in LDS)
 RS_CLASS_DESC = os.environ.get("PML_RS_CLASS_ORDER", "desc") == "desc"
+# fused class launches spread over this many streams (the current one + RS_STREAMS - 1 more), classes assigned
+# longest-first to the least-loaded stream by B n^2. Off by default: on game5pl one stream runs ~41 ms of class
+# launches back to back next to the fused primal launch, yet two streams measured slower (RE 44.4-45.0 vs 43.6 ms,
+# scripts/gpu_r5_s10.sh): the classes then also compete with each other for the CUs the primal launch leaves
+RS_STREAMS = max(1, int(os.environ.get("PML_RS_STREAMS", "1")))
 RS_BIG_NNZ_RATIO = float(os.environ.get("PML_RS_BIG_NNZ_RATIO", "0.6"))   # n > 64: mean row nnz >= ratio x n
 
 
@@ -364,7 +369,25 @@ class RowSpaceBatch:
         # the device worst go where a concurrent fused primal launch fills it, the many-problem classes last)
         order_c = sorted(range(len(self.classes)), key=lambda i: -self.classes[i].n) if RS_CLASS_DESC else \
             range(len(self.classes))
-        for ci in order_c:
+        streams = [None]
+        if fused and dev.type == "cuda" and RS_STREAMS > 1 and len(self.classes) > 1:
+            main = torch.cuda.current_stream(dev)
+            if getattr(self, "_streams", None) is None:
+                self._streams = [torch.cuda.Stream(dev) for _ in range(RS_STREAMS - 1)]
+            streams = [main] + self._streams
+            for st in self._streams:
+                st.wait_stream(main)                       # warm starts / offsets written on the caller's stream
+                for t in (beta, beta0, o, zs):
+                    t.record_stream(st)
+            load = [0] * len(streams)
+            lane = {}
+            for ci in sorted(range(len(self.classes)), key=lambda i: -self.classes[i].B * self.classes[i].n ** 2):
+                k = min(range(len(streams)), key=lambda j: load[j])
+                lane[ci] = k
+                load[k] += self.classes[ci].B * self.classes[ci].n ** 2
+
+        def solve_class(ci):
+            nonlocal zs
             c = self.classes[ci]
             b0, oc = c.view(beta0), c.view(o)
             if fused:
@@ -379,14 +402,25 @@ class RowSpaceBatch:
                                        order=order, zout=c.view(zs))
                 if RS_ORDER:
                     c.order = torch.argsort(it, stable=True).to(torch.int32)
+                return f, it, rc
+            data = BatchedGLMData(c.L, c.y, oc, c.w)
+            solver = batched_tron if optimizer == "TRON" else batched_lbfgs
+            r = solver(data, loss, l2, b0, tol, max_iter)
+            c.view(beta).copy_(r.W)
+            zs = None
+            return r.f, r.iters, r.reason
+
+        for ci in order_c:
+            st = streams[lane[ci]] if len(streams) > 1 else None
+            if st is None or st is streams[0]:
+                res_of[ci] = solve_class(ci)
             else:
-                data = BatchedGLMData(c.L, c.y, oc, c.w)
-                solver = batched_tron if optimizer == "TRON" else batched_lbfgs
-                r = solver(data, loss, l2, b0, tol, max_iter)
-                c.view(beta).copy_(r.W)
-                zs = None
-                f, it, rc = r.f, r.iters, r.reason
-            res_of[ci] = (f, it, rc)
+                with torch.cuda.stream(st):
+                    res_of[ci] = solve_class(ci)
+                for t in res_of[ci]:
+                    t.record_stream(streams[0])
+        for st in streams[1:]:
+            streams[0].wait_stream(st)
         for ci in range(len(self.classes)):
             f, it, rc = res_of[ci]
             fs.append(f)
