@@ -508,11 +508,13 @@ class RandomEffectCoordinate(Coordinate):
         if getattr(ds, "_seg_csr", None) is None:
             return None
         with Timed(f"RE {self.coordinate_id}: solver components", log, logging.DEBUG):
-            rs = self._row_space(l1, oc)
-            rs = rs if rs is not None and rs.B else None
+            with Timed(f"RE {self.coordinate_id}: row-space batch", log, logging.DEBUG):
+                rs = self._row_space(l1, oc)
+                rs = rs if rs is not None and rs.B else None
             n_e = seg.row_ptr[1:] - seg.row_ptr[:-1]
             done = rs.mask.clone() if rs is not None else torch.zeros(seg.B, dtype=torch.bool, device=seg.y.device)
-            fused = EntityTronBatch(ds, (~done) & (n_e > 0))
+            with Timed(f"RE {self.coordinate_id}: fused primal batch", log, logging.DEBUG):
+                fused = EntityTronBatch(ds, (~done) & (n_e > 0))
             if fused.B:
                 done |= fused.mask
             else:

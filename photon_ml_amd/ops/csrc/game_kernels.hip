@@ -291,6 +291,10 @@ __global__ __launch_bounds__(256) void tl_compact_kernel(CmpArgs a) {
 // fp64) and the image is cleared entry by entry. Rows must hold distinct columns (canonical CSR; checked on the
 // host). Replaces 2 x n full passes of the GLM kernels over the whole coordinate (one indicator column per pass).
 // ------------------------------------------------------------------------------------------------------------
+// S rows per scatter round (template): rows i0 .. i0 + S - 1 go into S interleaved image slots (img[c S + s]), and
+// one walk over row j's entries feeds S accumulators -- S times fewer walks (global reads + dependent chains) than
+// one row per round, the same fma sequence per K entry (bitwise equal for every S).
+template <int S>
 __global__ __launch_bounds__(64) void seg_gram_kernel(int B, int n, const long long* __restrict__ ents,
                                                       const long long* __restrict__ row_ptr,
                                                       const long long* __restrict__ col_ptr,
@@ -306,24 +310,39 @@ __global__ __launch_bounds__(64) void seg_gram_kernel(int B, int n, const long l
   const int ne = (int)(row_ptr[e + 1] - r0);
   const long long cb = col_ptr[e];
   const int de = (int)(col_ptr[e + 1] - cb);
-  for (int c = lane; c < de; c += 64) img[c] = 0.0;
+  for (int c = lane; c < de * S; c += 64) img[c] = 0.0;
   __syncthreads();
   double* Kb = K + b * (long long)n * n;
-  for (int i = 0; i < ne; ++i) {
-    const long long ib = nip[r0 + i], ie = nip[r0 + i + 1];
-    for (long long t = ib + lane; t < ie; t += 64) img[pos[t] - cb] = val[t];
+  for (int i0 = 0; i0 < ne; i0 += S) {
+    const int ns = ne - i0 < S ? ne - i0 : S;
+    for (int s = 0; s < ns; ++s) {
+      const long long ib = nip[r0 + i0 + s], ie = nip[r0 + i0 + s + 1];
+      for (long long t = ib + lane; t < ie; t += 64) img[(pos[t] - cb) * S + s] = val[t];
+    }
     __syncthreads();
     // lane takes rows j = lane, lane + 64, lane + 128 (n <= 192)
     for (int j = lane; j < n; j += 64) {
-      double acc = 0.0;
+      double acc[S];
+#pragma unroll
+      for (int s = 0; s < S; ++s) acc[s] = 0.0;
       if (j < ne) {
         const long long jb = nip[r0 + j], je = nip[r0 + j + 1];
-        for (long long t = jb; t < je; ++t) acc = fma(val[t], img[pos[t] - cb], acc);
+        for (long long t = jb; t < je; ++t) {
+          const double v = val[t];
+          const double* im = img + (pos[t] - cb) * S;
+#pragma unroll
+          for (int s = 0; s < S; ++s) acc[s] = fma(v, im[s], acc[s]);
+        }
       }
-      Kb[(long long)j * n + i] = acc;
+#pragma unroll
+      for (int s = 0; s < S; ++s)
+        if (s < ns) Kb[(long long)j * n + i0 + s] = acc[s];
     }
     __syncthreads();
-    for (long long t = ib + lane; t < ie; t += 64) img[pos[t] - cb] = 0.0;
+    for (int s = 0; s < ns; ++s) {
+      const long long ib = nip[r0 + i0 + s], ie = nip[r0 + i0 + s + 1];
+      for (long long t = ib + lane; t < ie; t += 64) img[(pos[t] - cb) * S + s] = 0.0;
+    }
     __syncthreads();
   }
   for (int i = ne; i < n; ++i)
@@ -442,13 +461,32 @@ int pml_gemm_nt(int M, int N, int K, const double* A, int lda, const double* Bm,
 }
 
 
+static int g_seg_gram_s = 0;   // rows per scatter round of seg_gram_kernel (0: by LDS size; A/B: pml_seg_gram_set_s)
+void pml_seg_gram_set_s(int s) { g_seg_gram_s = (s == 1 || s == 2 || s == 4 || s == 8) ? s : 0; }
+
 // K [B, n, n] for the entities ents[B]; dmax = max projected columns of those entities (LDS image size).
 int pml_seg_gram(int B, int n, int dmax, const long long* ents, const long long* row_ptr, const long long* col_ptr,
                  const long long* nip, const long long* pos, const double* val, double* K, void* stream) {
   if (B <= 0) return 0;
   if (n < 1 || n > 192 || dmax < 0 || (size_t)dmax * sizeof(double) > 160 * 1024) return -22;
-  hipLaunchKernelGGL(seg_gram_kernel, dim3((unsigned)B), dim3(64), (size_t)std::max(dmax, 1) * sizeof(double),
-                     (hipStream_t)stream, B, n, ents, row_ptr, col_ptr, nip, pos, val, K);
+  // rows per scatter round: as many as keep the image <= 32 KB (>= 5 one-wave workgroups per CU)
+  const size_t d8 = (size_t)std::max(dmax, 1) * sizeof(double);
+  const int S = g_seg_gram_s > 0 ? g_seg_gram_s : (d8 * 8 <= 32768 ? 8 : d8 * 4 <= 32768 ? 4 : d8 * 2 <= 32768 ? 2 : 1);
+  const size_t lds = d8 * (size_t)S;
+  if (lds > 160 * 1024) return -22;
+  hipStream_t st = (hipStream_t)stream;
+  if (S == 8)
+    hipLaunchKernelGGL(seg_gram_kernel<8>, dim3((unsigned)B), dim3(64), lds, st, B, n, ents, row_ptr, col_ptr, nip, pos,
+                       val, K);
+  else if (S == 4)
+    hipLaunchKernelGGL(seg_gram_kernel<4>, dim3((unsigned)B), dim3(64), lds, st, B, n, ents, row_ptr, col_ptr, nip, pos,
+                       val, K);
+  else if (S == 2)
+    hipLaunchKernelGGL(seg_gram_kernel<2>, dim3((unsigned)B), dim3(64), lds, st, B, n, ents, row_ptr, col_ptr, nip, pos,
+                       val, K);
+  else
+    hipLaunchKernelGGL(seg_gram_kernel<1>, dim3((unsigned)B), dim3(64), lds, st, B, n, ents, row_ptr, col_ptr, nip, pos,
+                       val, K);
   LAUNCH_CHECK();
   return 0;
 }

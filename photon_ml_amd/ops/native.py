@@ -647,6 +647,7 @@ def game_lib() -> Optional[ctypes.CDLL]:
         lib.pml_downsample.argtypes = [c_int, c_void_p, c_void_p, c_void_p, ctypes.c_longlong, ctypes.c_ulonglong,
                                        c_double, c_int, c_void_p, c_void_p]
         lib.pml_seg_gram.argtypes = [c_int, c_int, c_int] + [c_void_p] * 8
+        lib.pml_seg_gram_set_s.argtypes = [c_int]
         lib.pml_rs_primal.argtypes = [c_int, c_int] + [c_void_p] * 9
         lib.pml_rs_primal.restype = c_int
         lib.pml_tl_compact.argtypes = [c_int, c_int, ctypes.POINTER(CmpArgs), c_void_p]

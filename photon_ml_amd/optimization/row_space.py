@@ -33,6 +33,7 @@ from typing import Optional
 
 import torch
 
+from ..utils.timing import trace_range
 from .batched import BatchedGLMData, BatchedResult, batched_lbfgs, batched_tron
 
 # rs_tron problem order from the previous solve's iteration counts (PML_RS_ORDER=1). Off by default: measured
@@ -116,7 +117,8 @@ class _SizeClass:
         self.B = int(ents.numel())
         self.off = off                                                   # offset in the packed beta vector
         # [B, n, n], lower: forward substitution for small n, batched triangular solves beyond
-        self.Linv = _tri_inverse_lower(L) if n <= 64 else _tri_inverse_solve(L)
+        with trace_range(f"row-space: triangular inverse n={n}"):
+            self.Linv = _tri_inverse_lower(L) if n <= 64 else _tri_inverse_solve(L)
 
     def view(self, flat: torch.Tensor) -> torch.Tensor:
         return flat[self.off:self.off + self.B * self.n].view(self.B, self.n)
@@ -173,6 +175,8 @@ class RowSpaceBatch:
             rows = torch.where(valid, seg.row_ptr[e].unsqueeze(1) + ar,
                                torch.full_like(valid, -1, dtype=torch.long))
             geo.append((e, n, valid, rows, torch.zeros(e.numel(), n, n, dtype=torch.float64, device=dev)))
+        gram = trace_range("row-space: Gram matrices")
+        gram.__enter__()
         csr = _canonical_csr(csr, dev) if dev.type == "cuda" else None
         # (class, members) whose Gram columns come from indicator passes: all of them without a canonical device
         # CSR, else only the entities too wide for seg_gram_kernel's LDS image (d_e > SEG_GRAM_DMAX)
@@ -213,12 +217,14 @@ class RowSpaceBatch:
                         K[sel, :, j] = col
             del u, z
         del ind
+        gram.__exit__(None, None, None)
         off = 0
         kept = []
         for e, n, valid, rows, K in geo:
             # entities of other classes / the primal path also received u components (rows never mix)
             K += torch.diag_embed((~valid).to(torch.float64))
-            L, info = torch.linalg.cholesky_ex(K)
+            with trace_range(f"row-space: Cholesky n={n}"):
+                L, info = torch.linalg.cholesky_ex(K)
             del K
             ok = info == 0
             if not bool(ok.any()):

@@ -215,6 +215,35 @@ def test_row_space_gram_kernel_matches_indicator_passes():
     torch.testing.assert_close(a.to_primal(ra.W), b.to_primal(rb.W), rtol=1e-6, atol=1e-8)
 
 
+def test_seg_gram_rows_per_round_bitwise():
+    """seg_gram_kernel with 1, 2, 4 or 8 rows per scatter round (interleaved image slots, one walk of row j per
+    round): the same fma sequence per K entry, so K is bitwise equal for every S."""
+    from photon_ml_amd.algorithm.coordinates import RandomEffectCoordinate
+    from photon_ml_amd.ops.native import require_game_lib, seg_gram
+    from photon_ml_amd.optimization.row_space import _canonical_csr
+    data, _ = generate_game_data(n_rows=8000, n_users=300, d_user=60, seed=5, task="LOGISTIC_REGRESSION")
+    cfg = GLMOptimizationConfiguration(OptimizerConfig("TRON", 10, 1e-8), RegularizationContext("L2"), 1.0)
+    c = RandomEffectCoordinate("u", data, RandomEffectDataConfiguration("userId", "user"), cfg,
+                               "LOGISTIC_REGRESSION", device="cuda", layout="segmented")
+    seg = c.dataset.seg
+    csr = _canonical_csr(c.dataset._seg_csr, torch.device("cuda"))
+    assert csr is not None
+    n_e = seg.row_ptr[1:] - seg.row_ptr[:-1]
+    ents = torch.nonzero((n_e > 0) & (n_e <= 64)).squeeze(1)
+    n = int(n_e[ents].max())
+    lib = require_game_lib()
+    outs = []
+    try:
+        for S in (1, 2, 4, 8):
+            lib.pml_seg_gram_set_s(S)
+            outs.append(seg_gram(ents, n, seg.row_ptr, seg.col_ptr, *csr))
+    finally:
+        lib.pml_seg_gram_set_s(0)
+    for K in outs[1:]:
+        assert torch.equal(K, outs[0])
+    assert float(outs[0].abs().sum()) > 0
+
+
 @pytest.mark.parametrize("row_space", ["0", "1"])
 def test_entity_masked_passes_give_identical_solve(row_space, monkeypatch):
     """The block-diagonal TRON skipping the row blocks / column tiles of entities that stopped iterating
