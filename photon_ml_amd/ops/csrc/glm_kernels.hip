@@ -1781,6 +1781,53 @@ __global__ __launch_bounds__(NTHREADS) void bgemv_kernel(int B, int n, const dou
 // 64 < n <= 192: one wave per problem straight from global memory (the block no longer fits a wave's LDS share);
 // lane i owns rows i, i + 64, i + 128. x is staged in LDS (broadcast reads); A^T reads are coalesced over lanes,
 // A reads walk each row (successive j hit the same cache lines: L1 hits).
+// Batched triangular solves with the row-space Cholesky factors (optimization/row_space.py: beta = L^-1 z, the
+// primal back-map's L^-T beta), replacing an explicitly formed inverse (O(n^3) per problem at setup and a second
+// n x n matrix per problem in HBM). One wave per problem: L's lower triangle staged packed in LDS (coalesced row
+// reads; n <= 192: <= 148 KB), lane k holds entries k, k + 64, k + 128; n dependent steps, each: the pivot entry
+// from its owner lane (shuffle), divided by the diagonal (every lane: same value), then one fma per entry below
+// (L y = x) or above (L^T y = x) the pivot.
+__global__ __launch_bounds__(64) void btrsv_kernel(int B, int n, const double* __restrict__ L,
+                                                   const double* __restrict__ x, double* __restrict__ y, int trans) {
+  extern __shared__ double sl[];
+  const int lane = threadIdx.x;
+  const long long b = blockIdx.x;
+  if (b >= B) return;
+  const double* Lb = L + b * (long long)n * n;
+  for (int t = lane; t < n * n; t += 64) {
+    const int r = t / n, c = t - r * n;
+    if (c <= r) sl[r * (r + 1) / 2 + c] = Lb[t];
+  }
+  __syncthreads();
+  double v[3];
+#pragma unroll
+  for (int s = 0; s < 3; ++s) {
+    const int k = lane + 64 * s;
+    v[s] = k < n ? x[b * n + k] : 0.0;
+  }
+  for (int step = 0; step < n; ++step) {
+    const int i = trans ? n - 1 - step : step;
+    const int si = i >> 6;
+    const double bi = __shfl(si == 0 ? v[0] : (si == 1 ? v[1] : v[2]), i & 63, 64);
+    const double yi = bi / sl[i * (i + 1) / 2 + i];
+#pragma unroll
+    for (int s = 0; s < 3; ++s) {
+      const int k = lane + 64 * s;
+      if (k == i) {
+        v[s] = yi;
+      } else if (k < n && (trans ? k < i : k > i)) {
+        const double lki = trans ? sl[i * (i + 1) / 2 + k] : sl[k * (k + 1) / 2 + i];
+        v[s] = fma(-lki, yi, v[s]);
+      }
+    }
+  }
+#pragma unroll
+  for (int s = 0; s < 3; ++s) {
+    const int k = lane + 64 * s;
+    if (k < n) y[b * n + k] = v[s];
+  }
+}
+
 __global__ __launch_bounds__(256) void bgemv_wide_kernel(int B, int n, const double* __restrict__ A,
                                                          const double* __restrict__ x, double* __restrict__ y,
                                                          int trans) {
@@ -3538,6 +3585,15 @@ int pml_lincomb(const double* const* ptrs, const double* coefs, int k, long long
   for (int j = 0; j < k; ++j) { vs.p[j] = ptrs[j]; vs.c[j] = coefs[j]; }
   const long long blocks = std::min<long long>((n + 255) / 256, 4096);
   hipLaunchKernelGGL(lincomb_kernel, dim3((unsigned)blocks), dim3(256), 0, (hipStream_t)stream, vs, k, n, out);
+  LAUNCH_CHECK();
+  return 0;
+}
+
+int pml_btrsv(int B, int n, const double* L, const double* x, double* y, int trans, void* stream) {
+  if (B <= 0) return 0;
+  if (n < 1 || n > 192) return -22;
+  hipLaunchKernelGGL(btrsv_kernel, dim3((unsigned)B), dim3(64), (size_t)(n * (n + 1) / 2) * sizeof(double),
+                     (hipStream_t)stream, B, n, L, x, y, trans);
   LAUNCH_CHECK();
   return 0;
 }

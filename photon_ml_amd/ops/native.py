@@ -133,6 +133,7 @@ def glm_lib() -> Optional[ctypes.CDLL]:
         lib.pml_seg_expand.argtypes = [c_void_p, c_int, c_void_p, c_void_p, c_int, c_void_p]
         lib.pml_seg_cg_step.argtypes = [c_void_p, c_int] + [c_void_p] * 7 + [c_double, c_void_p]
         lib.pml_bgemv.argtypes = [c_int, c_int, c_void_p, c_void_p, c_void_p, c_int, c_void_p]
+        lib.pml_btrsv.argtypes = [c_int, c_int, c_void_p, c_void_p, c_void_p, c_int, c_void_p]
         lib.pml_bhv.argtypes = [c_int, c_int, c_void_p, c_void_p, c_void_p, c_double, c_void_p, c_void_p]
         lib.pml_set_ls_args.argtypes = [c_void_p, c_double, c_double]
         lib.pml_gram_grid.argtypes = [ctypes.c_longlong]
@@ -166,7 +167,7 @@ def glm_lib() -> Optional[ctypes.CDLL]:
                                                                       c_void_p, c_void_p, c_void_p]
         for f in ("pml_seg_fwd", "pml_seg_t", "pml_reduce_stats", "pml_build_blocks", "pml_tl_fwd", "pml_tl_t",
                   "pml_tl_maxbits", "pml_segdot", "pml_segdot_long", "pml_tl_fwd_multi", "pml_tl_t_multi", "pml_seg_cg_step",
-                  "pml_seg_expand", "pml_bgemv", "pml_bhv", "pml_rs_tron", "pml_ls_eval", "pml_gram_grid", "pml_gram",
+                  "pml_seg_expand", "pml_bgemv", "pml_btrsv", "pml_bhv", "pml_rs_tron", "pml_ls_eval", "pml_gram_grid", "pml_gram",
                   "pml_lincomb", "pml_lbfgs_pair", "pml_ls_dots", "pml_two_loop_chain", "pml_two_loop_gram",
                   "pml_two_loop_gram_grid"):
             getattr(lib, f).restype = c_int
@@ -516,6 +517,23 @@ def batched_gemv(A: torch.Tensor, x: torch.Tensor, trans: bool = False) -> torch
     y = torch.empty_like(x)
     check(lib.pml_bgemv(B, n, A.data_ptr(), x.data_ptr(), y.data_ptr(), int(trans), stream_handle(A.device)),
           "bgemv")
+    return y
+
+
+def batched_trsv(L: torch.Tensor, x: torch.Tensor, trans: bool = False) -> torch.Tensor:
+    """``y[b] = L[b]^-1 x[b]`` (or ``L[b]^-T x[b]``) for a batch of lower-triangular fp64 matrices (n <= 192):
+    ``btrsv_kernel`` (one wave per problem, packed triangle in LDS) on the device, ``solve_triangular`` on the
+    host."""
+    if L.device.type != "cuda" or L.shape[-1] > 192 or L.shape[-1] != L.shape[-2]:
+        M = L.transpose(1, 2) if trans else L
+        return torch.linalg.solve_triangular(M, x.unsqueeze(-1), upper=trans).squeeze(-1)
+    lib = require_glm_lib()
+    L, x = L.contiguous(), x.contiguous()
+    B, n, _ = L.shape
+    assert L.dtype == torch.float64 and x.dtype == torch.float64 and x.shape == (B, n)
+    y = torch.empty_like(x)
+    check(lib.pml_btrsv(B, n, L.data_ptr(), x.data_ptr(), y.data_ptr(), int(trans), stream_handle(L.device)),
+          "btrsv")
     return y
 
 

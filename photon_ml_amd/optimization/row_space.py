@@ -48,31 +48,12 @@ def _bmv(A: torch.Tensor, x: torch.Tensor, trans: bool = False) -> torch.Tensor:
     return batched_gemv(A, x, trans)
 
 
-def _tri_inverse_lower(L: torch.Tensor) -> torch.Tensor:
-    """Inverse of a batch of lower-triangular matrices by forward substitution vectorised over the batch
-    (n steps of elementwise ops). rocBLAS' batched trsv runs one tiny solve per launch slot — measured 123 ms
-    for 250K 20x20 systems on MI355X, vs a few ms here — and the inverse is reused by every later projection."""
-    B, n, _ = L.shape
-    X = torch.zeros_like(L)
-    eye = torch.eye(n, dtype=L.dtype, device=L.device)
-    for i in range(n):
-        acc = eye[i].expand(B, n)
-        if i:
-            acc = acc - (L[:, i, :i].unsqueeze(-1) * X[:, :i, :]).sum(1)
-        X[:, i, :] = acc / L[:, i, i:i + 1]
-    return X
-
-
-def _tri_inverse_solve(L: torch.Tensor, chunk: int = 512) -> torch.Tensor:
-    """Inverse of a batch of lower-triangular matrices by batched triangular solves against the identity (the
-    forward substitution of :func:`_tri_inverse_lower` costs O(B n^3) elementwise traffic, too much beyond n = 64)."""
-    B, n, _ = L.shape
-    out = torch.empty_like(L)
-    eye = torch.eye(n, dtype=L.dtype, device=L.device)
-    for s in range(0, B, chunk):
-        e = min(B, s + chunk)
-        out[s:e] = torch.linalg.solve_triangular(L[s:e], eye.expand(e - s, n, n), upper=False)
-    return out
+def _btrsv(L: torch.Tensor, x: torch.Tensor, trans: bool = False) -> torch.Tensor:
+    """Batched triangular solves L^-1 x / L^-T x with the classes' Cholesky factors (HIP kernel on the device). The
+    factors are never inverted: an explicit inverse cost O(B n^3) at setup (75 ms for game5pl's n = 80 class) and a
+    second n x n matrix per problem in HBM, for products needed only by the primal back-map and foreign warm starts."""
+    from ..ops.native import batched_trsv
+    return batched_trsv(L, x, trans)
 
 
 def _canonical_csr(csr, dev):
@@ -116,9 +97,6 @@ class _SizeClass:
         self.ents, self.n, self.L, self.rows, self.valid, self.w, self.y = ents, n, L, rows, valid, w, y
         self.B = int(ents.numel())
         self.off = off                                                   # offset in the packed beta vector
-        # [B, n, n], lower: forward substitution for small n, batched triangular solves beyond
-        with trace_range(f"row-space: triangular inverse n={n}"):
-            self.Linv = _tri_inverse_lower(L) if n <= 64 else _tri_inverse_solve(L)
 
     def view(self, flat: torch.Tensor) -> torch.Tensor:
         return flat[self.off:self.off + self.B * self.n].view(self.B, self.n)
@@ -308,13 +286,13 @@ class RowSpaceBatch:
     def beta_from_primal(self, W: torch.Tensor) -> torch.Tensor:
         """Orthogonal projection of primal coefficients onto the row space: beta = L^{-1} X w (packed)."""
         z = self._slots(self.seg.glm.matvec(W))
-        return torch.cat([_bmv(c.Linv, c.view(z)).reshape(-1) for c in self.classes])
+        return torch.cat([_btrsv(c.L, c.view(z)).reshape(-1) for c in self.classes])
 
     def to_primal(self, beta: torch.Tensor) -> torch.Tensor:
         """w = X^T L^{-T} beta for the handled entities (zeros elsewhere): one transpose pass."""
         r = torch.zeros(self.seg.y.numel(), dtype=torch.float64, device=beta.device)
         if self.classes:
-            alpha = torch.cat([_bmv(c.Linv, c.view(beta), trans=True).reshape(-1) for c in self.classes])  # L^-T b
+            alpha = torch.cat([_btrsv(c.L, c.view(beta), trans=True).reshape(-1) for c in self.classes])  # L^-T b
             r[self.vrow] = alpha[self.vslot]
         pc = getattr(self, "_primal_csr", None)
         if pc is not None and self.classes:

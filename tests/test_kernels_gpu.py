@@ -370,6 +370,24 @@ def test_batched_small_gemv_and_hv_match_torch(n):
     torch.testing.assert_close(batched_hv(A, dw, x, 0.7), hv, rtol=1e-12, atol=1e-11)
 
 
+@pytest.mark.parametrize("n", [1, 7, 33, 64, 65, 80, 128, 192])
+@pytest.mark.parametrize("trans", [False, True])
+def test_batched_trsv_matches_solve_triangular(n, trans):
+    """btrsv_kernel (one wave per problem, packed factor in LDS) == torch's triangular solve (fp64 reference) for
+    L y = x and L^T y = x."""
+    from photon_ml_amd.ops.native import batched_trsv
+    g = torch.Generator(device="cuda").manual_seed(n + 1000 * trans)
+    B = 333
+    A = torch.randn(B, n, n + 3, dtype=torch.float64, device="cuda", generator=g)
+    L = torch.linalg.cholesky(A @ A.transpose(1, 2) + 0.1 * torch.eye(n, dtype=torch.float64, device="cuda"))
+    x = torch.randn(B, n, dtype=torch.float64, device="cuda", generator=g)
+    got = batched_trsv(L, x, trans)
+    M = L.transpose(1, 2) if trans else L
+    ref = torch.linalg.solve_triangular(M, x.unsqueeze(-1), upper=trans).squeeze(-1)
+    torch.testing.assert_close(got, ref, rtol=1e-10, atol=1e-10)
+    torch.testing.assert_close(torch.bmm(M, got.unsqueeze(-1)).squeeze(-1), x, rtol=1e-9, atol=1e-9)
+
+
 _RS_SIZES = [("LOGISTIC", 20), ("POISSON", 7), ("SQUARED", 33), ("LOGISTIC", 64), ("LOGISTIC", 1)]
 _RS_SIZES_WIDE = [("POISSON", 40), ("LOGISTIC", 48), ("SQUARED", 49), ("LOGISTIC", 57), ("POISSON", 64)]
 _RS_SIZES_DPP = [("LOGISTIC", 4), ("POISSON", 8), ("SQUARED", 11), ("LOGISTIC", 16), ("POISSON", 18),
