@@ -2226,6 +2226,9 @@ __device__ __forceinline__ double tri_sel(double x, bool keep) {
 #ifndef RS_SEL64
 #define RS_SEL64 1
 #endif
+#ifndef RS_BLK64
+#define RS_BLK64 1
+#endif
 
 template <int K, bool LREG, int WL = 2, bool TRI = false>
 struct RsGeom {
@@ -2241,8 +2244,15 @@ struct RsGeom {
   // K - 1, i = 15) lies 32 - K + ... past the triangle, so the problem slot is padded to cover it
   static constexpr int TRI_N = GL == 64 ? 64 * 65 / 2   // GL = 64: unconditional reads of rows / columns < 64
                                : (K * (K + 1) / 2 > (K - 1) * K / 2 + 32) ? K * (K + 1) / 2 : (K - 1) * K / 2 + 32;
-  static constexpr int PS0 = (TRI && (R == 2 || GL == 64)) ? TRI_N : K * SP;
-  static constexpr bool SEL = K == 24 || RS_SEL64;   // masked reads: select (else exec-masked reads; tri_keep)
+  // BLK (GL = 64): L as its lower-triangle 16 x 16 blocks (rows padded to 17 doubles: conflict-free row and column
+  // reads) plus one all-zero block that every above-diagonal block reference points to -- no masks at all
+  static constexpr int NBK = (K + 15) / 16;
+  // (K = 48: 9.51 -> 6.89 ms per 200K problems, 145 instead of 210 VGPRs; at K = 64 the 11 blocks' LDS costs more
+  // occupancy than the masks: 12.3 ms packed vs 13.1 ms blocks)
+  static constexpr bool BLK = GL == 64 && K == 48 && RS_BLK64;
+  static constexpr int ZB = NBK * (NBK + 1) / 2;      // the zero block's index
+  static constexpr int PS0 = BLK ? (ZB + 1) * 272 : (TRI && (R == 2 || GL == 64)) ? TRI_N : K * SP;
+  static constexpr bool SEL = K == 24 || (GL == 64 && RS_SEL64);   // masked reads: select (else exec-masked; tri_keep)
   // problem stride = 16 mod 32 doubles (measured: dropping the pad to fit 12 one-wave workgroups per CU at K = 20
   // gains nothing over variant 5, 7.66 vs 7.69 ms, and loses 3 % at K = 24)
   static constexpr int PS = PS0 + (((16 - PS0 % 32) % 32) + 32) % 32;
@@ -2321,6 +2331,23 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(rs_dpp_wpe<
       Lr[k] = ok ? Lb[(long long)i * n + k] : 0.0;
       Lc[k] = ok ? Lb[(long long)k * n + i] : 0.0;
     }
+  } else if constexpr (Gm::BLK) {
+    // one problem per wave: zero the slot (zero block, upper halves of the diagonal blocks, row pads), then the
+    // lower triangle into its blocks
+    const int wb = w * PS;
+    for (int idx = lane; idx < PS; idx += 64) smem[wb + idx] = 0.0;
+    __builtin_amdgcn_s_waitcnt(0);
+    __builtin_amdgcn_wave_barrier();
+    if (prob_on) {
+      const double* Lb = Lm + b * nn;
+      for (int idx = lane; idx < n * n; idx += 64) {
+        const int r = idx / n, c = idx - r * n;
+        if (c <= r) smem[wb + ((r >> 4) * ((r >> 4) + 1) / 2 + (c >> 4)) * 272 + (r & 15) * 17 + (c & 15)] = Lb[idx];
+      }
+    }
+    __builtin_amdgcn_s_waitcnt(0);
+    __builtin_amdgcn_wave_barrier();
+    lq = wb;
   } else if constexpr (PK) {
     // this wave's P problems, read row-major (coalesced) and stored packed; slot tails (the masked over-reads
     // past the triangle) zero
@@ -2398,9 +2425,23 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(rs_dpp_wpe<
       S[2] = (a & 2) ? A : Bv;
       pl_swap<32>(S[1], A, Bv);
       S[3] = (a & 2) ? A : Bv;
+      double a0 = 0.0, a1 = 0.0;
+      if constexpr (Gm::BLK) {
+#pragma unroll
+        for (int s = 0; s < 4; ++s) {
+          const int bb = a ^ s;
+          int base = lq + ((a < Gm::NBK && bb <= a) ? a * (a + 1) / 2 + bb : Gm::ZB) * 272 + ii * 17;
+          asm volatile("" : "+v"(base));
+          double m[16];
+#pragma unroll
+          for (int k = 0; k < 16; ++k) m[k] = smem[base + k];
+          bcf<16, 16>(a0, a1, S[s], m);
+        }
+        out[0] = on[0] ? a0 + a1 : 0.0;
+        return;
+      }
       int rb = lq + i * (i + 1) / 2;
       asm volatile("" : "+v"(rb));
-      double a0 = 0.0, a1 = 0.0;
 #pragma unroll
       for (int s = 0; s < 4; ++s) {
         int cb = rb + 16 * (a ^ s);
@@ -2476,6 +2517,20 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(rs_dpp_wpe<
       pl_swap<32>(S[1], A, Bv);
       S[3] = (a & 2) ? A : Bv;
       double a0 = 0.0, a1 = 0.0;
+      if constexpr (Gm::BLK) {
+#pragma unroll
+        for (int s = 0; s < 4; ++s) {
+          const int bb = a ^ s;
+          int base = lq + ((bb < Gm::NBK && a <= bb) ? bb * (bb + 1) / 2 + a : Gm::ZB) * 272 + ii;
+          asm volatile("" : "+v"(base));
+          double m[16];
+#pragma unroll
+          for (int k = 0; k < 16; ++k) m[k] = smem[base + 17 * k];
+          bcf<16, 16>(a0, a1, S[s], m);
+        }
+        out[0] = on[0] ? a0 + a1 : 0.0;
+        return;
+      }
 #pragma unroll
       for (int s = 0; s < 4; ++s) {
         const int b = a ^ s;

@@ -37,7 +37,7 @@ HESS_DMAX = 64 if os.environ.get("PML_RE_HESS", "1") != "0" else 0
 # launch (more than 1/RES_TAIL_SHARE of the batch's non-zeros) go to clusters; ``force``: every eligible entity;
 # ``0``: none.
 RESIDENT = os.environ.get("PML_RE_RESIDENT", "auto")
-RES_TAIL_SHARE = 256
+RES_TAIL_SHARE = int(os.environ.get("PML_RE_RES_TAIL_SHARE", "256"))
 RES_ROW_NNZ = 64
 RES_KMAX = int(os.environ.get("PML_RE_RES_KMAX", "128"))
 
