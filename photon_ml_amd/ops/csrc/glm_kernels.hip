@@ -1783,48 +1783,54 @@ __global__ __launch_bounds__(NTHREADS) void bgemv_kernel(int B, int n, const dou
 // A reads walk each row (successive j hit the same cache lines: L1 hits).
 // Batched triangular solves with the row-space Cholesky factors (optimization/row_space.py: beta = L^-1 z, the
 // primal back-map's L^-T beta), replacing an explicitly formed inverse (O(n^3) per problem at setup and a second
-// n x n matrix per problem in HBM). One wave per problem: L's lower triangle staged packed in LDS (coalesced row
-// reads; n <= 192: <= 148 KB), lane k holds entries k, k + 64, k + 128; n dependent steps, each: the pivot entry
+// n x n matrix per problem in HBM). 64 / G problems per wave (G = pow2 >= n lanes each, one problem beyond 32):
+// the lower triangles staged packed in LDS (coalesced reads; n <= 192: <= 148 KB), lane k of a problem holds entries
+// k, k + 64, k + 128; n dependent steps, each: the pivot entry
 // from its owner lane (shuffle), divided by the diagonal (every lane: same value), then one fma per entry below
 // (L y = x) or above (L^T y = x) the pivot.
-__global__ __launch_bounds__(64) void btrsv_kernel(int B, int n, const double* __restrict__ L,
+__global__ __launch_bounds__(64) void btrsv_kernel(int B, int n, int G, const double* __restrict__ L,
                                                    const double* __restrict__ x, double* __restrict__ y, int trans) {
+  // G = lanes per problem (pow2 >= n, <= 64): 64 / G problems per wave for n <= 32
   extern __shared__ double sl[];
   const int lane = threadIdx.x;
-  const long long b = blockIdx.x;
-  if (b >= B) return;
-  const double* Lb = L + b * (long long)n * n;
-  for (int t = lane; t < n * n; t += 64) {
-    const int r = t / n, c = t - r * n;
-    if (c <= r) sl[r * (r + 1) / 2 + c] = Lb[t];
+  const int P = 64 / G, q = lane / G, il = lane - q * G, tn = n * (n + 1) / 2;
+  const long long b0 = (long long)blockIdx.x * P;
+  if (b0 >= B) return;
+  const int cnt = (int)min((long long)P, B - b0);
+  for (int t = lane; t < cnt * n * n; t += 64) {
+    const int qq = t / (n * n), rem = t - qq * n * n, r = rem / n, c = rem - r * n;
+    if (c <= r) sl[qq * tn + r * (r + 1) / 2 + c] = L[(b0 + qq) * n * n + rem];
   }
   __syncthreads();
+  const bool pon = q < cnt;
+  const long long b = b0 + (pon ? q : 0);
+  const double* sq = sl + (pon ? q : 0) * tn;
   double v[3];
 #pragma unroll
   for (int s = 0; s < 3; ++s) {
-    const int k = lane + 64 * s;
-    v[s] = k < n ? x[b * n + k] : 0.0;
+    const int k = il + 64 * s;
+    v[s] = pon && k < n ? x[b * n + k] : 0.0;
   }
   for (int step = 0; step < n; ++step) {
     const int i = trans ? n - 1 - step : step;
     const int si = i >> 6;
-    const double bi = __shfl(si == 0 ? v[0] : (si == 1 ? v[1] : v[2]), i & 63, 64);
-    const double yi = bi / sl[i * (i + 1) / 2 + i];
+    const double bi = __shfl(si == 0 ? v[0] : (si == 1 ? v[1] : v[2]), q * G + (i & 63), 64);
+    const double yi = bi / sq[i * (i + 1) / 2 + i];
 #pragma unroll
     for (int s = 0; s < 3; ++s) {
-      const int k = lane + 64 * s;
+      const int k = il + 64 * s;
       if (k == i) {
         v[s] = yi;
       } else if (k < n && (trans ? k < i : k > i)) {
-        const double lki = trans ? sl[i * (i + 1) / 2 + k] : sl[k * (k + 1) / 2 + i];
+        const double lki = trans ? sq[i * (i + 1) / 2 + k] : sq[k * (k + 1) / 2 + i];
         v[s] = fma(-lki, yi, v[s]);
       }
     }
   }
 #pragma unroll
   for (int s = 0; s < 3; ++s) {
-    const int k = lane + 64 * s;
-    if (k < n) y[b * n + k] = v[s];
+    const int k = il + 64 * s;
+    if (pon && k < n) y[b * n + k] = v[s];
   }
 }
 
@@ -3647,8 +3653,11 @@ int pml_lincomb(const double* const* ptrs, const double* coefs, int k, long long
 int pml_btrsv(int B, int n, const double* L, const double* x, double* y, int trans, void* stream) {
   if (B <= 0) return 0;
   if (n < 1 || n > 192) return -22;
-  hipLaunchKernelGGL(btrsv_kernel, dim3((unsigned)B), dim3(64), (size_t)(n * (n + 1) / 2) * sizeof(double),
-                     (hipStream_t)stream, B, n, L, x, y, trans);
+  int G = 1;
+  while (G < n && G < 64) G <<= 1;
+  const int P = 64 / G;
+  hipLaunchKernelGGL(btrsv_kernel, dim3((unsigned)((B + P - 1) / P)), dim3(64),
+                     (size_t)P * (n * (n + 1) / 2) * sizeof(double), (hipStream_t)stream, B, n, G, L, x, y, trans);
   LAUNCH_CHECK();
   return 0;
 }
