@@ -594,7 +594,7 @@ class RandomEffectCoordinate(Coordinate):
             rs_prep = rs.prepare(W0, reuse_beta=not foreign)
             main = torch.cuda.current_stream(dev)
             if getattr(self, "_side_stream", None) is None:
-                self._side_stream = torch.cuda.Stream(dev)
+                self._side_stream = torch.cuda.Stream(dev, priority=int(os.environ.get("PML_RE_SIDE_PRIORITY", "0")))
             side = self._side_stream
             side.wait_stream(main)                 # offsets / warm starts written on the main stream
             for t in rs_prep:
@@ -609,7 +609,11 @@ class RandomEffectCoordinate(Coordinate):
         if sub_async:
             main = torch.cuda.current_stream(dev)
             if getattr(self, "_sub_stream", None) is None:
-                self._sub_stream = torch.cuda.Stream(dev)
+                # the pass path is a long chain of short launches next to the saturating fused launch: a
+                # high-priority stream lets its workgroups take CUs first as they free up (PML_RE_SUB_PRIORITY;
+                # game5heavy RE 62.4 -> 61.0 ms; the row-space side stream measured no better at high priority,
+                # scripts/gpu_r5_prio.sh)
+                self._sub_stream = torch.cuda.Stream(dev, priority=int(os.environ.get("PML_RE_SUB_PRIORITY", "-1")))
             sub_stream = self._sub_stream
             sub_in = self._sub_inputs(sub, seg, W0)          # on the main stream, before the fused launch
             sub_stream.wait_stream(main)
