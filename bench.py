@@ -263,6 +263,10 @@ def game_extra(dev, rank: int, world: int) -> dict:
                     f"{pre}_cold_first_sweep_coordinate_ms": g.get("cold_first_sweep_coordinate_ms")})
         if g.get("route_s"):
             out[f"{pre}_route_s"] = g["route_s"]
+        # multi-rank runs: rows placed on their entity owners at ingest, bytes the RE update still routes
+        for k in ("placement_s", "routed_bytes_per_update", "re_solver_routing"):
+            if g.get(k) is not None and (k != "routed_bytes_per_update" or world > 1):
+                out[f"{pre}_{k}"] = g[k]
         if prec == "bf16":
             out["game5pl_config"] = dict(g["config"], fe_dtype=g["dtype"], re_dtype="fp64", steps=g["steps"],
                                          warmup=g["warmup"], data_generation_s=round(g["data_generation_s"], 1),
