@@ -1786,8 +1786,8 @@ __global__ __launch_bounds__(NTHREADS) void bgemv_kernel(int B, int n, const dou
 // n x n matrix per problem in HBM). 64 / G problems per wave (G = pow2 >= n lanes each, one problem beyond 32):
 // the lower triangles staged packed in LDS (coalesced reads; n <= 192: <= 148 KB), lane k of a problem holds entries
 // k, k + 64, k + 128; n dependent steps, each: the pivot entry
-// from its owner lane (shuffle), divided by the diagonal (every lane: same value), then one fma per entry below
-// (L y = x) or above (L^T y = x) the pivot.
+// from its owner lane (readlane with one problem per wave, else a shuffle) times the diagonal's reciprocal (every
+// lane: same value), then one fma per entry below (L y = x) or above (L^T y = x) the pivot.
 __global__ __launch_bounds__(64) void btrsv_kernel(int B, int n, int G, const double* __restrict__ L,
                                                    const double* __restrict__ x, double* __restrict__ y, int trans) {
   // G = lanes per problem (pow2 >= n, <= 64): 64 / G problems per wave for n <= 32
@@ -1802,9 +1802,17 @@ __global__ __launch_bounds__(64) void btrsv_kernel(int B, int n, int G, const do
     if (c <= r) sl[qq * tn + r * (r + 1) / 2 + c] = L[(b0 + qq) * n * n + rem];
   }
   __syncthreads();
+  // reciprocals of the diagonal, once: the n dependent steps then multiply instead of dividing
+  double* rinv = sl + P * tn;
+  for (int t = lane; t < cnt * n; t += 64) {
+    const int qq = t / n, r = t - qq * n;
+    rinv[qq * n + r] = 1.0 / sl[qq * tn + r * (r + 1) / 2 + r];
+  }
+  __syncthreads();
   const bool pon = q < cnt;
   const long long b = b0 + (pon ? q : 0);
   const double* sq = sl + (pon ? q : 0) * tn;
+  const double* rq = rinv + (pon ? q : 0) * n;
   double v[3];
 #pragma unroll
   for (int s = 0; s < 3; ++s) {
@@ -1814,8 +1822,16 @@ __global__ __launch_bounds__(64) void btrsv_kernel(int B, int n, int G, const do
   for (int step = 0; step < n; ++step) {
     const int i = trans ? n - 1 - step : step;
     const int si = i >> 6;
-    const double bi = __shfl(si == 0 ? v[0] : (si == 1 ? v[1] : v[2]), q * G + (i & 63), 64);
-    const double yi = bi / sq[i * (i + 1) / 2 + i];
+    const double vi = si == 0 ? v[0] : (si == 1 ? v[1] : v[2]);
+    double bi;
+    if (P == 1) {       // one problem per wave: the pivot's lane is wave-uniform (readlane, no LDS crossbar)
+      const long long u = __builtin_bit_cast(long long, vi);
+      const int lo = __builtin_amdgcn_readlane((int)u, i & 63), hi = __builtin_amdgcn_readlane((int)(u >> 32), i & 63);
+      bi = __builtin_bit_cast(double, ((long long)hi << 32) | (long long)(unsigned)lo);
+    } else {
+      bi = __shfl(vi, q * G + (i & 63), 64);
+    }
+    const double yi = bi * rq[i];
 #pragma unroll
     for (int s = 0; s < 3; ++s) {
       const int k = il + 64 * s;
@@ -2281,9 +2297,6 @@ struct RsGeom {
 #ifndef RS_WPE32
 #define RS_WPE32 1
 #endif
-#ifndef RS_SERIAL_BLOCKS
-#define RS_SERIAL_BLOCKS 0     // K = 48 / 64: each 16-column block's LDS reads wait for the previous block's FMAs
-#endif
 #ifndef RS_WPE48
 #define RS_WPE48 1
 #endif
@@ -2450,8 +2463,7 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(rs_dpp_wpe<
       asm volatile("" : "+v"(rb));
 #pragma unroll
       for (int s = 0; s < 4; ++s) {
-        int cb = rb + 16 * (a ^ s);
-        if (RS_SERIAL_BLOCKS) asm volatile("" : "+v"(cb) : "v"(a0));   // block s's reads after block s - 1's FMAs
+        const int cb = rb + 16 * (a ^ s);
         const bool below = (a ^ s) < a && i < K;
         double m[16];
 #pragma unroll
@@ -2541,8 +2553,7 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(rs_dpp_wpe<
       for (int s = 0; s < 4; ++s) {
         const int b = a ^ s;
         int cbase = lq + i + 8 * b * (16 * b + 1);     // column c at row 16 b: T(16 b) + c
-        if (RS_SERIAL_BLOCKS) asm volatile("" : "+v"(cbase) : "v"(a0));
-        else asm volatile("" : "+v"(cbase));
+        asm volatile("" : "+v"(cbase));
         const bool above = b > a && 16 * b < K;
         double m[16];
 #pragma unroll
@@ -3657,7 +3668,7 @@ int pml_btrsv(int B, int n, const double* L, const double* x, double* y, int tra
   while (G < n && G < 64) G <<= 1;
   const int P = 64 / G;
   hipLaunchKernelGGL(btrsv_kernel, dim3((unsigned)((B + P - 1) / P)), dim3(64),
-                     (size_t)P * (n * (n + 1) / 2) * sizeof(double), (hipStream_t)stream, B, n, G, L, x, y, trans);
+                     (size_t)P * (n * (n + 1) / 2 + n) * sizeof(double), (hipStream_t)stream, B, n, G, L, x, y, trans);
   LAUNCH_CHECK();
   return 0;
 }

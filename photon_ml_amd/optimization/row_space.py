@@ -231,6 +231,14 @@ class RowSpaceBatch:
         # the per-entity back-map (to_primal) reads only the handled entities' rows: a compact copy of them, not
         # the whole segmented CSR (which the dataset frees once the sub-problems are built)
         self._primal_csr = self._compact_csr(csr) if csr is not None else None
+        # slot of every compact back-map row in the packed solution: the back-map gathers its row weights straight
+        # from L^-T beta (no zero-filled per-row vector, scatter and gather over the whole coordinate)
+        self._primal_slot = None
+        if self._primal_csr is not None:
+            slot_of_row = torch.full((seg.y.numel(),), -1, dtype=torch.int64, device=dev)
+            slot_of_row[self.vrow] = self.vslot
+            self._primal_slot = slot_of_row[self._primal_csr[-1]]
+            del slot_of_row
         self._z = None            # (beta, packed margins L beta) written by the fused solve
         # the primal model (to_primal: one transpose pass over the block-diagonal data) is read once per model:
         # build its shard-wide one-launch transpose tables here, with the rest of the setup, instead of running
@@ -290,20 +298,21 @@ class RowSpaceBatch:
 
     def to_primal(self, beta: torch.Tensor) -> torch.Tensor:
         """w = X^T L^{-T} beta for the handled entities (zeros elsewhere): one transpose pass."""
-        r = torch.zeros(self.seg.y.numel(), dtype=torch.float64, device=beta.device)
-        if self.classes:
-            alpha = torch.cat([_btrsv(c.L, c.view(beta), trans=True).reshape(-1) for c in self.classes])  # L^-T b
-            r[self.vrow] = alpha[self.vslot]
+        alpha = torch.cat([_btrsv(c.L, c.view(beta), trans=True).reshape(-1) for c in self.classes]) \
+            if self.classes else None                                                           # L^-T beta
         pc = getattr(self, "_primal_csr", None)
-        if pc is not None and self.classes:
+        if pc is not None and alpha is not None:
             # per-entity back-map over the handled entities' rows only (rs_primal_kernel, one wave per entity, on
             # the compact copy of their rows); the shard-wide transpose pass read every entity's rows (9.0 ms on
             # game5pl)
             from ..ops.native import rs_primal
             ents2, row_ptr, col_ptr, nip, pos, val, rows = pc
             W = torch.zeros(int(self.seg.col_ptr[-1]), dtype=torch.float64, device=beta.device)
-            rs_primal(ents2, row_ptr, col_ptr, nip, pos, val, r[rows].contiguous(), W)
+            rs_primal(ents2, row_ptr, col_ptr, nip, pos, val, alpha[self._primal_slot], W)
             return W
+        r = torch.zeros(self.seg.y.numel(), dtype=torch.float64, device=beta.device)
+        if alpha is not None:
+            r[self.vrow] = alpha[self.vslot]
         return self.seg.glm.rmatvec(r, build_multi=False)     # once per update: no shard-wide tables
 
     def margins(self, beta: torch.Tensor) -> torch.Tensor:
