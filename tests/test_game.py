@@ -334,3 +334,19 @@ def test_canonical_csr_check():
     dup = torch.tensor([3, 7, 1, 4, 4, 0])
     assert _canonical_csr((nip, dup, torch.ones(6)), torch.device("cpu")) is None
     assert _canonical_csr(None, torch.device("cpu")) is None
+
+
+@pytest.mark.parametrize("trans", [False, True])
+def test_batched_trsv_host_path(trans):
+    """batched_trsv on the host (torch's triangular solve; the device runs btrsv_kernel): L y = x / L^T y = x for a
+    batch of Cholesky factors, the row-space back-map's and warm-start projection's only use of the factors."""
+    from photon_ml_amd.ops.native import batched_trsv
+    g = torch.Generator().manual_seed(3 + trans)
+    A = torch.randn(17, 9, 12, dtype=torch.float64, generator=g)
+    L = torch.linalg.cholesky(A @ A.transpose(1, 2))
+    x = torch.randn(17, 9, dtype=torch.float64, generator=g)
+    y = batched_trsv(L, x, trans)
+    M = L.transpose(1, 2) if trans else L
+    torch.testing.assert_close(torch.bmm(M, y.unsqueeze(-1)).squeeze(-1), x, rtol=1e-10, atol=1e-10)
+    torch.testing.assert_close(y, torch.bmm(torch.linalg.inv(M), x.unsqueeze(-1)).squeeze(-1), rtol=1e-9,
+                               atol=1e-9)
