@@ -2433,8 +2433,9 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(rs_dpp_wpe<
     } else if constexpr (GL == 64) {
       // one problem per wave, lane i = 16 a + ii holds entry i. Column block b = a ^ s of the vector reaches row a
       // through a permlane swap (s = 1: xor 16, s = 2: xor 32, s = 3: both), then row_newbcast:k broadcasts its
-      // entry k into the FMA. L rows from the packed triangle; blocks above the diagonal (b > a) and entries
-      // k > ii of the diagonal block are masked (exec-masked reads)
+      // entry k into the FMA. BLK (K = 48): rows of the stored 16 x 16 blocks, above-diagonal blocks read the zero
+      // block; otherwise rows of the packed triangle with blocks above the diagonal (b > a) and entries k > ii of
+      // the diagonal block masked (tri_keep: select)
       const int a = i >> 4, ii = i & 15;
       double S[4], A, Bv;
       S[0] = v[0];
