@@ -2267,13 +2267,13 @@ struct RsGeom {
   static constexpr int TRI_N = GL == 64 ? 64 * 65 / 2   // GL = 64: unconditional reads of rows / columns < 64
                                : (K * (K + 1) / 2 > (K - 1) * K / 2 + 32) ? K * (K + 1) / 2 : (K - 1) * K / 2 + 32;
   // BLK (GL = 64): L as its lower-triangle 16 x 16 blocks (rows padded to 17 doubles: conflict-free row and column
-  // reads) plus one all-zero block that every above-diagonal block reference points to -- no masks at all
+  // reads); a product term whose block lies above the diagonal reads a stored block and takes a zero vector block
+  // instead (the source is uniform over a DPP row) -- no masks at all
   static constexpr int NBK = (K + 15) / 16;
   // (K = 48: 9.51 -> 6.89 ms per 200K problems, 145 instead of 210 VGPRs; at K = 64 the 11 blocks' LDS costs more
   // occupancy than the masks: 12.3 ms packed vs 13.1 ms blocks)
   static constexpr bool BLK = GL == 64 && K == 48 && RS_BLK64;
-  static constexpr int ZB = NBK * (NBK + 1) / 2;      // the zero block's index
-  static constexpr int PS0 = BLK ? (ZB + 1) * 272 : (TRI && (R == 2 || GL == 64)) ? TRI_N : K * SP;
+  static constexpr int PS0 = BLK ? NBK * (NBK + 1) / 2 * 272 : (TRI && (R == 2 || GL == 64)) ? TRI_N : K * SP;
   static constexpr bool SEL = K == 24 || (GL == 64 && RS_SEL64);   // masked reads: select (else exec-masked; tri_keep)
   // problem stride = 16 mod 32 doubles (measured: dropping the pad to fit 12 one-wave workgroups per CU at K = 20
   // gains nothing over variant 5, 7.66 vs 7.69 ms, and loses 3 % at K = 24)
@@ -2351,8 +2351,8 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(rs_dpp_wpe<
       Lc[k] = ok ? Lb[(long long)k * n + i] : 0.0;
     }
   } else if constexpr (Gm::BLK) {
-    // one problem per wave: zero the slot (zero block, upper halves of the diagonal blocks, row pads), then the
-    // lower triangle into its blocks
+    // one problem per wave: zero the slot (upper halves of the diagonal blocks, row pads), then the lower triangle
+    // into its blocks
     const int wb = w * PS;
     for (int idx = lane; idx < PS; idx += 64) smem[wb + idx] = 0.0;
     __builtin_amdgcn_s_waitcnt(0);
@@ -2433,9 +2433,9 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(rs_dpp_wpe<
     } else if constexpr (GL == 64) {
       // one problem per wave, lane i = 16 a + ii holds entry i. Column block b = a ^ s of the vector reaches row a
       // through a permlane swap (s = 1: xor 16, s = 2: xor 32, s = 3: both), then row_newbcast:k broadcasts its
-      // entry k into the FMA. BLK (K = 48): rows of the stored 16 x 16 blocks, above-diagonal blocks read the zero
-      // block; otherwise rows of the packed triangle with blocks above the diagonal (b > a) and entries k > ii of
-      // the diagonal block masked (tri_keep: select)
+      // entry k into the FMA. BLK (K = 48): rows of the stored 16 x 16 blocks, above-diagonal terms multiply a
+      // zero vector block; otherwise rows of the packed triangle with blocks above the diagonal (b > a) and entries
+      // k > ii of the diagonal block masked (tri_keep: select)
       const int a = i >> 4, ii = i & 15;
       double S[4], A, Bv;
       S[0] = v[0];
@@ -2450,12 +2450,13 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(rs_dpp_wpe<
 #pragma unroll
         for (int s = 0; s < 4; ++s) {
           const int bb = a ^ s;
-          int base = lq + ((a < Gm::NBK && bb <= a) ? a * (a + 1) / 2 + bb : Gm::ZB) * 272 + ii * 17;
+          const bool lower = a < Gm::NBK && bb <= a;
+          int base = lq + (lower ? a * (a + 1) / 2 + bb : 0) * 272 + ii * 17;
           asm volatile("" : "+v"(base));
           double m[16];
 #pragma unroll
           for (int k = 0; k < 16; ++k) m[k] = smem[base + k];
-          bcf<16, 16>(a0, a1, S[s], m);
+          bcf<16, 16>(a0, a1, lower ? S[s] : 0.0, m);
         }
         out[0] = on[0] ? a0 + a1 : 0.0;
         return;
@@ -2540,12 +2541,13 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(rs_dpp_wpe<
 #pragma unroll
         for (int s = 0; s < 4; ++s) {
           const int bb = a ^ s;
-          int base = lq + ((bb < Gm::NBK && a <= bb) ? bb * (bb + 1) / 2 + a : Gm::ZB) * 272 + ii;
+          const bool lower = bb < Gm::NBK && a <= bb;
+          int base = lq + (lower ? bb * (bb + 1) / 2 + a : 0) * 272 + ii;
           asm volatile("" : "+v"(base));
           double m[16];
 #pragma unroll
           for (int k = 0; k < 16; ++k) m[k] = smem[base + 17 * k];
-          bcf<16, 16>(a0, a1, S[s], m);
+          bcf<16, 16>(a0, a1, lower ? S[s] : 0.0, m);
         }
         out[0] = on[0] ? a0 + a1 : 0.0;
         return;
