@@ -2252,6 +2252,7 @@ __device__ __forceinline__ double tri_sel(double x, bool keep) {
 #define RS_BLK64 1
 #endif
 
+
 template <int K, bool LREG, int WL = 2, bool TRI = false>
 struct RsGeom {
   // K = 48 / 64 (variant 8): one problem per wave, lane i holds entry i (GL = 64)
@@ -2270,9 +2271,9 @@ struct RsGeom {
   // reads); a product term whose block lies above the diagonal reads a stored block and takes a zero vector block
   // instead (the source is uniform over a DPP row) -- no masks at all
   static constexpr int NBK = (K + 15) / 16;
-  // (K = 48: 9.51 -> 6.89 ms per 200K problems, 145 instead of 210 VGPRs; at K = 64 the 11 blocks' LDS costs more
-  // occupancy than the masks: 12.3 ms packed vs 13.1 ms blocks)
-  static constexpr bool BLK = GL == 64 && K == 48 && RS_BLK64;
+  // (200K problems: K = 48 9.51 -> 6.6 ms, 145 instead of 210 VGPRs; K = 64 12.3 -> 11.9 ms, 10 blocks = 21.8 KB
+  // per wave; profiles/rs_tron_roofline.md)
+  static constexpr bool BLK = GL == 64 && RS_BLK64;
   static constexpr int PS0 = BLK ? NBK * (NBK + 1) / 2 * 272 : (TRI && (R == 2 || GL == 64)) ? TRI_N : K * SP;
   static constexpr bool SEL = K == 24 || (GL == 64 && RS_SEL64);   // masked reads: select (else exec-masked; tri_keep)
   // problem stride = 16 mod 32 doubles (measured: dropping the pad to fit 12 one-wave workgroups per CU at K = 20
