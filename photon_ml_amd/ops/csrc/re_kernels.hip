@@ -671,7 +671,7 @@ __device__ __forceinline__ void lean_pass(const ReTronArgs& a, long long r0, lon
 #define LEAN_WPE 3
 #endif
 #ifndef LEAN_UF
-#define LEAN_UF 2
+#define LEAN_UF 1
 #endif
 #ifndef LEAN_UH
 #define LEAN_UH 3
