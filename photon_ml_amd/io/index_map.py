@@ -146,6 +146,23 @@ def _imlib():
                                            ctypes.c_void_p]
         lib.pml_im_name.argtypes = [ctypes.c_void_p, ctypes.c_int64, ctypes.c_char_p, ctypes.c_int64]
         lib.pml_im_name.restype = ctypes.c_int64
+        # PalDB V1 stores (io/paldb.py)
+        vp, i64, i32 = ctypes.c_void_p, ctypes.c_int64, ctypes.c_int32
+        lib.pml_pdb_last_error.restype = ctypes.c_char_p
+        lib.pml_pdb_partitions.argtypes = [ctypes.c_char_p, i64, i64, i32, vp]
+        lib.pml_pdb_write_store.argtypes = [ctypes.c_char_p, ctypes.c_char_p, i64, i64, i64]
+        lib.pml_pdb_build.argtypes = [ctypes.c_char_p, i64, i64, i32, ctypes.c_char_p, i64, i64, vp]
+        lib.pml_pdb_open.argtypes = [ctypes.c_char_p, i64, i32]
+        lib.pml_pdb_open.restype = vp
+        lib.pml_pdb_close.argtypes = [vp]
+        lib.pml_pdb_size.argtypes = [vp]
+        lib.pml_pdb_size.restype = i64
+        lib.pml_pdb_part_offset.argtypes = [vp, i32]
+        lib.pml_pdb_part_offset.restype = i64
+        lib.pml_pdb_get_indices.argtypes = [vp, ctypes.c_char_p, i64, i64, vp]
+        lib.pml_pdb_get_names.argtypes = [vp, vp, i64, ctypes.POINTER(ctypes.c_char_p), vp]
+        lib.pml_pdb_get_names.restype = i64
+        lib.pml_pdb_free.argtypes = [ctypes.c_char_p]
         _IMLIB = lib
     return _IMLIB
 
@@ -276,8 +293,8 @@ def index_map_from_feature_bags(bags_dir: str, bags: Sequence[str], add_intercep
 
 def open_index_map(directory: str, namespace: str, n_partitions: int = 1) -> IndexMap:
     """Off-heap index map of one namespace (feature shard): the reference's PalDB stores
-    (``paldb-partition-<ns>-<i>.dat``, read by :mod:`photon_ml_amd.io.paldb`) when present, else the native mmap
-    stores written by the feature-indexing driver."""
+    (``paldb-partition-<ns>-<i>.dat``, mmap'd and probed natively, :mod:`photon_ml_amd.io.paldb`) when present, else
+    the native mmap stores written by the feature-indexing driver."""
     from .paldb import PalDBIndexMap, has_paldb_stores
     if has_paldb_stores(directory, namespace):
         return PalDBIndexMap(directory, namespace, n_partitions)

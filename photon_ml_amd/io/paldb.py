@@ -19,19 +19,24 @@ stores shipped with the reference, e.g. ``GameIntegTest/input/feature-indexes``)
 * serialization: small ints as one code byte (``-1 .. 8`` -> ``4 .. 13``), ``14`` + one unsigned byte,
   ``15`` / ``16`` + varint (negative / positive), strings ``103`` + varint length + one varint per UTF-16 unit.
 
-The reader enumerates every slot (no hashing needed) and builds an in-memory two-way map; the loaded map is a
-regular :class:`~photon_ml_amd.io.index_map.IndexMap` (and can be re-stored in the native mmap format with
-``build_offheap_index_map``).
+**Production path: native** (``io/csrc/index_map.cpp``, ``pml_pdb_*``). :class:`PalDBIndexMap` mmaps the stores
+and answers batched ``get_indices`` / ``get_feature_names`` with PalDB's own lookup — serialize the key, slot
+``(murmur3_32(serialized key, seed 42) & 0x7fffffff) % slots`` of its key-length block, linear probing until the key
+or an empty slot (offset 0) — one C call per batch, partition by Java ``String.hashCode`` in C++; nothing is
+deserialised at open, no Python dict is built, and processes on one host share the page cache (the reference keeps
+the stores open off-heap the same way). :func:`build_paldb_index_map` partitions, sorts, de-duplicates and writes
+every store in C++ (``pml_pdb_build``).
 
-The writer (:func:`write_store`, :func:`build_paldb_index_map`; reference ``PalDBIndexMapBuilder.scala:27-98``,
-``FeatureIndexingDriver.scala:262-291``) produces stores that PalDB's own reader can query: a key sits in slot
-``(murmur3_32(serialized key, seed 42) & 0x7fffffff) % slots`` or the next free one (linear probing), ``slots =
-round(count / 0.75)`` per key length, each key length's data stream starts with one reserved byte (offset 0 marks
-an empty slot) and a slot is the serialized key plus the varint data offset, padded to the block's widest offset.
-The hash, slot counts and layout are pinned against the reference's shipped stores (``tests/test_paldb.py``).
+The writer layout (reference ``PalDBIndexMapBuilder.scala:27-98``, ``FeatureIndexingDriver.scala:262-291``):
+``slots = round(count / 0.75)`` per key length, each key length's data stream starts with one reserved byte (offset
+0 marks an empty slot) and a slot is the serialized key plus the varint data offset, padded to the block's widest
+offset. The pure-Python :func:`write_store` / :func:`read_store` below are the byte-level specification the native
+code is tested against (``tests/test_paldb.py``: both writers reproduce the reference's shipped stores byte for byte;
+the native reader agrees with the slot-enumerating Python reader on every key); they are not on the load path.
 """
 from __future__ import annotations
 
+import ctypes
 import math
 import mmap
 import os
@@ -208,24 +213,62 @@ def write_store(path: str, items, timestamp_ms: Optional[int] = None) -> None:
     os.replace(tmp, path)
 
 
+def _nul_join(strings) -> bytes:
+    """Strings as one NUL-separated UTF-8 blob (the native ABI's batch format)."""
+    # a key holding a NUL shifts the separator count: the native side checks it against the key count and fails
+    return "\0".join(strings).encode("utf-8", "surrogatepass")
+
+
+def _lib():
+    from .index_map import _imlib
+    return _imlib()
+
+
+def _err() -> str:
+    return _lib().pml_pdb_last_error().decode("utf-8", "replace")
+
+
+def write_store_native(path: str, keys_in_index_order, timestamp_ms: Optional[int] = None) -> None:
+    """One two-way store (key i -> i, i -> key i) written by the native writer (same bytes as :func:`write_store`
+    of those items)."""
+    import time as _time
+    keys = list(keys_in_index_order)
+    blob = _nul_join(keys)
+    ts = int(_time.time() * 1000) if timestamp_ms is None else int(timestamp_ms)
+    if _lib().pml_pdb_write_store(path.encode(), blob, len(blob), len(keys), ts) != 0:
+        raise OSError(f"PalDB store {path}: {_err()}")
+
+
 def build_paldb_index_map(keys, directory: str, namespace: str, n_partitions: int = 1,
-                          add_intercept: bool = True) -> "PalDBIndexMap":
+                          add_intercept: bool = True, timestamp_ms: Optional[int] = None) -> "PalDBIndexMap":
     """FeatureIndexingDriver with PalDB output: distinct feature keys hash-partitioned like Spark's
-    ``HashPartitioner`` (:func:`partition_of`), local indices 0.. in sorted key order per partition, one store per
-    partition holding both directions (key -> local index, local index -> key)."""
+    ``HashPartitioner`` (Java ``String.hashCode``), local indices 0.. in sorted key order per partition, one store per
+    partition holding both directions (key -> local index, local index -> key). Partitioning, sorting,
+    de-duplication and the store bytes are native (``pml_pdb_build``, partitions written in parallel)."""
+    import time as _time
     from .index_map import INTERCEPT_KEY
-    keys = list(dict.fromkeys(keys))
-    if add_intercept and INTERCEPT_KEY not in keys:
-        keys.append(INTERCEPT_KEY)
+    keys = list(keys)
+    if add_intercept:
+        keys.append(INTERCEPT_KEY)              # de-duplicated natively
     os.makedirs(directory, exist_ok=True)
-    parts: List[List[str]] = [[] for _ in range(n_partitions)]
-    for k in keys:
-        parts[partition_of(k, n_partitions)].append(k)
-    for p, ks in enumerate(parts):
-        ks.sort()
-        items = [(k, i) for i, k in enumerate(ks)] + [(i, k) for i, k in enumerate(ks)]
-        write_store(store_file(directory, namespace, p), items)
+    blob = _nul_join(keys)
+    paths = _nul_join(store_file(directory, namespace, p) for p in range(n_partitions))
+    sizes = np.zeros(n_partitions, dtype=np.int64)
+    ts = int(_time.time() * 1000) if timestamp_ms is None else int(timestamp_ms)
+    rc = _lib().pml_pdb_build(blob, len(blob), len(keys), n_partitions, paths, len(paths), ts, sizes.ctypes.data)
+    if rc != 0:
+        raise OSError(f"PalDB index build in {directory}: {_err()} ({rc})")
     return PalDBIndexMap(directory, namespace, n_partitions)
+
+
+def partitions_native(keys, n_partitions: int) -> np.ndarray:
+    """:func:`partition_of` of many keys in one native call."""
+    keys = list(keys)
+    blob = _nul_join(keys)
+    out = np.empty(len(keys), dtype=np.int32)
+    if _lib().pml_pdb_partitions(blob, len(blob), len(keys), n_partitions, out.ctypes.data) != 0:
+        raise ValueError(_err())
+    return out
 
 
 def read_store(path: str) -> Dict[object, object]:
@@ -289,42 +332,62 @@ def has_paldb_stores(directory: str, namespace: str) -> bool:
 
 
 class PalDBIndexMap(IndexMap):
-    """Read-only index map over the ``n_partitions`` PalDB stores of one namespace (feature shard)."""
+    """Read-only index map over the ``n_partitions`` PalDB stores of one namespace (feature shard), mmap'd and
+    queried natively (``PalDBIndexMap.scala:75-93`` getIndex, ``118-160`` getFeatureName). Global index = local
+    index + the preceding partitions' sizes (store key count / 2)."""
 
     def __init__(self, directory: str, namespace: str, n_partitions: int):
         self.n_partitions = n_partitions
-        self.offsets: List[int] = []
-        self._k2i: Dict[str, int] = {}
-        names: List[Optional[str]] = []
-        size = 0
-        for p in range(n_partitions):
-            kv = read_store(store_file(directory, namespace, p))
-            self.offsets.append(size)
-            local = {k: v for k, v in kv.items() if isinstance(k, str)}
-            rev = {k: v for k, v in kv.items() if isinstance(k, int)}
-            if len(local) != len(rev) or any(rev.get(i) != k for k, i in local.items()):
-                raise ValueError(f"PalDB store {namespace}/{p}: name->index and index->name disagree")
-            n_local = len(local)
-            if sorted(local.values()) != list(range(n_local)):
-                raise ValueError(f"PalDB store {namespace}/{p}: local indices are not 0..{n_local - 1}")
-            part_names: List[Optional[str]] = [None] * n_local
-            for k, i in local.items():
-                self._k2i[k] = size + i
-                part_names[i] = k
-            names.extend(part_names)
-            size += n_local
-        self._names = names
-        self._dim = size
+        self.directory, self.namespace = directory, namespace
+        paths = _nul_join(store_file(directory, namespace, p) for p in range(n_partitions))
+        self._h = _lib().pml_pdb_open(paths, len(paths), n_partitions)
+        if not self._h:
+            raise ValueError(f"PalDB index {directory}/{namespace}: {_err()}")
+        self._dim = int(_lib().pml_pdb_size(self._h))
+        self.offsets: List[int] = [int(_lib().pml_pdb_part_offset(self._h, p)) for p in range(n_partitions)]
+
+    def __del__(self):
+        h = getattr(self, "_h", None)
+        if h:
+            try:
+                _lib().pml_pdb_close(h)
+            except Exception:  # pragma: no cover - interpreter shutdown
+                pass
+            self._h = None
 
     def get_index(self, key: str) -> int:
-        return self._k2i.get(key, -1)
+        return int(self.get_indices([key])[0])
 
     def get_indices(self, keys) -> np.ndarray:
-        g = self._k2i.get
-        return np.fromiter((g(k, -1) for k in keys), dtype=np.int64, count=len(keys))
+        keys = list(keys)
+        out = np.empty(len(keys), dtype=np.int64)
+        if not keys:
+            return out
+        blob = _nul_join(keys)
+        if _lib().pml_pdb_get_indices(self._h, blob, len(blob), len(keys), out.ctypes.data) != 0:
+            raise ValueError(f"PalDB lookup: {_err()}")
+        return out
+
+    def get_feature_names(self, indices) -> List[Optional[str]]:
+        """Feature keys of many global indices (None where absent), one native call."""
+        idx = np.ascontiguousarray(np.asarray(indices, dtype=np.int64).reshape(-1))
+        n = idx.size
+        if n == 0:
+            return []
+        found = np.zeros(n, dtype=np.uint8)
+        lib = _lib()
+        ptr = ctypes.c_char_p()
+        size = int(lib.pml_pdb_get_names(self._h, idx.ctypes.data, n, ctypes.byref(ptr), found.ctypes.data))
+        try:
+            names = ctypes.string_at(ptr, size).decode("utf-8", "surrogatepass").split("\0")
+        finally:
+            lib.pml_pdb_free(ptr)
+        if found.all():
+            return names
+        return [k if f else None for k, f in zip(names, found)]
 
     def get_feature_name(self, idx: int) -> Optional[str]:
-        return self._names[idx] if 0 <= idx < self._dim else None
+        return self.get_feature_names([idx])[0] if 0 <= idx < self._dim else None
 
     @property
     def feature_dimension(self) -> int:
@@ -334,4 +397,4 @@ class PalDBIndexMap(IndexMap):
         return self._dim
 
     def keys_in_order(self) -> List[str]:
-        return list(self._names)
+        return self.get_feature_names(np.arange(self._dim, dtype=np.int64))

@@ -110,20 +110,39 @@ def expected_id(kind: str, name: str, sanitize: bool = None) -> str:
     return build_id(CPP_SOURCES[name], _cpp_flags(name, sanitize))
 
 
-def _compile(cmd: List[str], out: Path, verbose: bool) -> None:
-    if verbose:
-        print(" ".join(cmd), flush=True)
-    subprocess.run(cmd, check=True)
-    os.replace(str(out) + ".tmp", out)
+def _compile(cmd_of, out: Path, bid: str, force: bool, verbose: bool) -> None:
+    """Build ``out`` (stamped ``bid``) unless it already carries that stamp. Concurrent builders (torchrun ranks,
+    xdist workers that all find the library stale) serialise on an ``fcntl`` lock next to the library and re-check
+    the stamp once they hold it; each compiles into its own temporary file, replaced atomically."""
+    import fcntl
+    if not force and read_stamp(out) == bid:
+        return
+    out.parent.mkdir(parents=True, exist_ok=True)
+    with open(str(out) + ".lock", "a+") as lk:
+        fcntl.flock(lk, fcntl.LOCK_EX)
+        try:
+            if not force and read_stamp(out) == bid:       # another process built it while we waited
+                return
+            tmp = f"{out}.{os.getpid()}.tmp"
+            cmd = cmd_of(tmp)
+            if verbose:
+                print(" ".join(cmd), flush=True)
+            try:
+                subprocess.run(cmd, check=True)
+                os.replace(tmp, out)
+            finally:
+                if os.path.exists(tmp):
+                    os.unlink(tmp)
+        finally:
+            fcntl.flock(lk, fcntl.LOCK_UN)
 
 
 def compile_hip(src: Path, out: Path, extra: List[str] = (), force: bool = False, verbose: bool = False) -> Path:
     """hipcc ``src`` into ``out`` stamped with its build id; skipped when ``out`` already carries that id."""
     flags = _hip_flags(extra)
     bid = build_id(src, flags)
-    if force or read_stamp(out) != bid:
-        out.parent.mkdir(parents=True, exist_ok=True)
-        _compile([_hipcc(), *flags, f'-DPML_BUILD_ID="{bid}"', str(src), "-o", str(out) + ".tmp"], out, verbose)
+    _compile(lambda tmp: [_hipcc(), *flags, f'-DPML_BUILD_ID="{bid}"', str(src), "-o", tmp], out, bid, force,
+             verbose)
     return out
 
 
@@ -131,13 +150,13 @@ def compile_cpp(src: Path, out: Path, name: str, sanitize: bool = False, force: 
                 verbose: bool = False) -> Path:
     flags = _cpp_flags(name, sanitize)
     bid = build_id(src, flags)
-    if force or read_stamp(out) != bid:
+
+    def cmd(tmp):
         import sysconfig
         import pybind11
         inc = ["-I" + sysconfig.get_paths()["include"], "-I" + pybind11.get_include()]
-        out.parent.mkdir(parents=True, exist_ok=True)
-        _compile(["g++", *flags, f'-DPML_BUILD_ID="{bid}"', *inc, str(src), "-o", str(out) + ".tmp", "-lz"], out,
-                 verbose)
+        return ["g++", *flags, f'-DPML_BUILD_ID="{bid}"', *inc, str(src), "-o", tmp, "-lz"]
+    _compile(cmd, out, bid, force, verbose)
     return out
 
 

@@ -182,3 +182,91 @@ def test_indexing_driver_writes_paldb(tmp_path):
     assert os.path.exists(out / "paldb-partition-global-0.dat")
     m = open_index_map(str(out), "global", 2)
     assert isinstance(m, PalDBIndexMap) and len(m) == 14       # 13 heart features + intercept
+
+
+# ---------------------------------------------------------------------------------------------------------------
+# Native PalDB path (io/csrc/index_map.cpp pml_pdb_*): the production reader / writer, checked against the
+# slot-enumerating Python reader (read_store) and the Python writer (write_store), the byte-level specification.
+STORES = [os.path.join(FIX, "paldb_heart", "paldb-partition-global-0.dat"),
+          os.path.join(FIX, "paldb_heart", "paldb-partition-global-1.dat"),
+          os.path.join(FIX, "paldb_heart_icpt", "paldb-partition-global-0.dat"),
+          os.path.join(FIX, "paldb_heart_icpt", "paldb-partition-global-1.dat"),
+          os.path.join(GAME, "feature-indexes", "paldb-partition-shard1-0.dat"),
+          os.path.join(GAME, "feature-indexes", "paldb-partition-shard2-0.dat"),
+          os.path.join(GAME, "feature-indexes", "paldb-partition-shard3-0.dat")]
+
+
+@pytest.mark.parametrize("path", STORES)
+def test_native_writer_reproduces_reference_stores_bytewise(path, tmp_path):
+    import struct
+    from photon_ml_amd.io.paldb import write_store_native
+    if not os.path.exists(path):
+        pytest.skip("reference store not present")
+    kv = read_store(path)
+    by_index = [k for _, k in sorted((v, k) for k, v in kv.items() if isinstance(k, str))]
+    ref = open(path, "rb").read()
+    ts = struct.unpack_from(">q", ref, 10)[0]
+    out = str(tmp_path / "n.dat")
+    write_store_native(out, by_index, ts)
+    assert open(out, "rb").read() == ref
+
+
+@pytest.mark.parametrize("path", STORES)
+def test_native_reader_agrees_with_slot_enumeration(path):
+    """Every key of a reference store found by PalDB's probe in the native reader, with the value the Python
+    slot-enumerating reader decodes; absent keys give -1 / None."""
+    if not os.path.exists(path):
+        pytest.skip("reference store not present")
+    d, f = os.path.split(path)
+    ns = f[len("paldb-partition-"):-len("-0.dat")]
+    n_parts = len([x for x in os.listdir(d) if x.startswith(f"paldb-partition-{ns}-")])
+    m = PalDBIndexMap(d, ns, n_parts)
+    p = int(f[:-4].rsplit("-", 1)[1])
+    kv = read_store(path)
+    names = [k for k in kv if isinstance(k, str)]
+    got = m.get_indices(names)
+    np.testing.assert_array_equal(got, [m.offsets[p] + kv[k] for k in names])
+    assert m.get_feature_names(got) == names
+    assert m.get_indices(["not-a-feature" + DELIM, ""]).tolist() == [-1, -1]
+    assert m.get_feature_names([-1, len(m), len(m) + 5]) == [None, None, None]
+
+
+def test_native_build_matches_python_writer_and_partitions(tmp_path):
+    """pml_pdb_build (partition, sort, de-duplicate, write) gives the bytes of the Python writer over the same
+    sorted partitions; partitions follow Java String.hashCode (incl. non-BMP characters and empty terms)."""
+    from photon_ml_amd.io.paldb import (build_paldb_index_map, partitions_native, store_file, write_store)
+    keys = [key(f"f{i % 53}", str(i)) for i in range(5000)] + [key("été", "x"), key("n", ""), key("😀", "t"),
+                                                               key("f1", "1")]   # one duplicate
+    m = build_paldb_index_map(keys, str(tmp_path / "n"), "g", 4, add_intercept=True, timestamp_ms=123456789)
+    distinct = sorted(set(keys) | {INTERCEPT_KEY})
+    assert len(m) == len(distinct)
+    parts = partitions_native(distinct, 4)
+    assert parts.tolist() == [partition_of(k, 4) for k in distinct]
+    for p in range(4):
+        ks = sorted(k for k, q in zip(distinct, parts) if q == p)
+        ref = str(tmp_path / f"py{p}.dat")
+        write_store(ref, [(k, i) for i, k in enumerate(ks)] + [(i, k) for i, k in enumerate(ks)], 123456789)
+        assert open(store_file(str(tmp_path / "n"), "g", p), "rb").read() == open(ref, "rb").read()
+    idx = m.get_indices(distinct)
+    assert sorted(idx.tolist()) == list(range(len(m)))
+    assert m.get_feature_names(idx) == distinct
+    assert m.keys_in_order() == [distinct[i] for i in np.argsort(idx)]
+
+
+def test_native_paldb_scale(tmp_path):
+    """200k keys over 2 partitions: build, open and batched lookups well under a second each (the 10M-key record is
+    profiles/paldb_native_r6.md)."""
+    import time
+    keys = [key(f"feat{i % 1000}", f"t{i}") for i in range(200_000)]
+    t = time.time()
+    from photon_ml_amd.io.paldb import build_paldb_index_map
+    build_paldb_index_map(keys, str(tmp_path), "s", 2)
+    t_build = time.time() - t
+    t = time.time()
+    m = PalDBIndexMap(str(tmp_path), "s", 2)
+    t_open = time.time() - t
+    t = time.time()
+    idx = m.get_indices(keys)
+    t_get = time.time() - t
+    assert len(m) == 200_001 and (idx >= 0).all() and len(set(idx.tolist())) == 200_000
+    assert t_open < 0.1 and t_get < 2.0 and t_build < 5.0, (t_build, t_open, t_get)
