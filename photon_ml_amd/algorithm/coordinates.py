@@ -22,7 +22,7 @@ import numpy as np
 import torch
 
 from ..constants import EPSILON, TaskType
-from ..utils.timing import Timed
+from ..utils.timing import Timed, phase
 from ..data.game_data import GameData
 from ..data.random_effect import FixedEffectDataConfiguration, RandomEffectDataConfiguration, RandomEffectDataset
 from ..function.losses import loss_for_task
@@ -97,14 +97,16 @@ class FixedEffectCoordinate(Coordinate):
         self.shard_id = data_config.feature_shard_id
         self.task = TaskType.parse(task)
         self.device = torch.device(device) if device is not None else default_device()
-        labeled = data.labeled(self.shard_id)
-        if local_rows is not None:  # row sharding for multi-GPU data parallelism
-            labeled = labeled.subset(local_rows)
-        self.local_rows = local_rows
-        self.base_offsets = labeled.offsets.copy()
-        self.base_weights = labeled.weights.copy()
-        self.labels = labeled.y
-        self.glm_data = make_glm_data(labeled, self.device, precision)
+        with phase(f"FE {coordinate_id} build: shard view"):
+            labeled = data.labeled(self.shard_id)
+            if local_rows is not None:  # row sharding for multi-GPU data parallelism
+                labeled = labeled.subset(local_rows)
+            self.local_rows = local_rows
+            self.base_offsets = labeled.offsets.copy()
+            self.base_weights = labeled.weights.copy()
+            self.labels = labeled.y
+        with phase(f"FE {coordinate_id} build: device layout"):
+            self.glm_data = make_glm_data(labeled, self.device, precision)
         self.compute_variance = compute_variance
         self.normalization = normalization
         self.set_config(opt_config)
@@ -234,8 +236,9 @@ class RandomEffectCoordinate(Coordinate):
         self.task = TaskType.parse(task)
         self.loss = loss_for_task(self.task)
         self.device = torch.device(device) if device is not None else default_device()
-        self.dataset = RandomEffectDataset(data, data_config, self.device, dtype, entity_subset=entity_subset,
-                                           layout=layout)
+        with phase(f"RE {coordinate_id} build: dataset"):
+            self.dataset = RandomEffectDataset(data, data_config, self.device, dtype, entity_subset=entity_subset,
+                                               layout=layout)
         self.compute_variance = compute_variance
         self.base_offsets = torch.from_numpy(data.offsets).to(self.device)
         self.set_config(opt_config)

@@ -69,7 +69,7 @@ def as_csr(x, n_cols: Optional[int] = None) -> sp.csr_matrix:
     if isinstance(x, DeviceCSR):
         return x
     if sp.issparse(x):
-        m = x.tocsr().astype(np.float64)
+        m = x.tocsr().astype(np.float64, copy=False)     # no copy of an fp64 CSR (8 GB+ at GAME config 5)
     else:
         m = sp.csr_matrix(np.asarray(x, dtype=np.float64))
     if n_cols is not None and m.shape[1] != n_cols:

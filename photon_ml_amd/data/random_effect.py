@@ -27,6 +27,7 @@ from ..constants import EPSILON
 from ..projector.projectors import (IndexMapProjection, ProjectorKind, ProjectorType, gaussian_projection_matrix)
 from .game_data import GameData
 from .matrix import DeviceCSR, LabeledData
+from ..utils.timing import phase
 
 
 @dataclass
@@ -138,14 +139,15 @@ class RandomEffectDataset:
             x = x.to_scipy()      # device-resident rows (entity-sharded routing) on a host-only build path
         self.dim = x.shape[1]
         ids = data.id_tags[re_type]
-        ids_s = ids.astype(str) if ids.dtype == object else ids
-        if self.device.type == "cuda" and np.issubdtype(ids_s.dtype, np.integer) and len(ids_s):
-            # integer entity ids: sorted unique + inverse on the device (np.unique: 1.3 s at 25M rows)
-            u, inv = torch.unique(torch.from_numpy(np.ascontiguousarray(ids_s)).to(self.device), sorted=True,
-                                  return_inverse=True)
-            self.entity_ids, ent = u.cpu().numpy().astype(ids_s.dtype, copy=False), inv.cpu().numpy()
-        else:
-            self.entity_ids, ent = np.unique(ids_s, return_inverse=True)
+        with phase("RE dataset: entity ids"):
+            ids_s = ids.astype(str) if ids.dtype == object else ids
+            if self.device.type == "cuda" and np.issubdtype(ids_s.dtype, np.integer) and len(ids_s):
+                # integer entity ids: sorted unique + inverse on the device (np.unique: 1.3 s at 25M rows)
+                u, inv = torch.unique(torch.from_numpy(np.ascontiguousarray(ids_s)).to(self.device), sorted=True,
+                                      return_inverse=True)
+                self.entity_ids, ent = u.cpu().numpy().astype(ids_s.dtype, copy=False), inv.cpu().numpy()
+            else:
+                self.entity_ids, ent = np.unique(ids_s, return_inverse=True)
         n_ent = len(self.entity_ids)
         n = data.n_rows
         self.n_rows = n
@@ -225,7 +227,8 @@ class RandomEffectDataset:
         wts = weight_mult * data.weights
         if layout == "segmented" and self.device.type == "cuda":
             # GPU build: projection + entity-sorted block-diagonal layout computed on the device
-            self._make_segmented_device(x, xa, ea, ent, active_rows, passive_rows, data.response, wts, n_ent)
+            with phase("RE dataset: segmented layout"):
+                self._make_segmented_device(x, xa, ea, ent, active_rows, passive_rows, data.response, wts, n_ent)
             self.d_local = self.projection.local_dims()
             return
         # ---- projection
@@ -410,12 +413,15 @@ class RandomEffectDataset:
         from ..optimization.batched import SegmentedGLMData
         dev, D = self.device, self.dim
         xa = xa.tocsr()
-        if isinstance(xa, DeviceCSR):        # routed rows already on the device: no host copy
-            ip = xa.indptr.to(dev)
-            x_ind, x_val = xa.indices.to(dev), xa.data.to(dev)
-        else:
-            ip = torch.from_numpy(xa.indptr.astype(np.int64)).to(dev)
-            x_ind, x_val = torch.from_numpy(xa.indices).to(dev), torch.from_numpy(xa.data).to(dev, torch.float64)
+        with phase("RE segmented: upload"):
+            if isinstance(xa, DeviceCSR):        # routed rows already on the device: no host copy
+                ip = xa.indptr.to(dev)
+                x_ind, x_val = xa.indices.to(dev), xa.data.to(dev)
+            else:
+                ip = torch.from_numpy(xa.indptr.astype(np.int64)).to(dev)
+                x_ind, x_val = torch.from_numpy(xa.indices).to(dev), torch.from_numpy(xa.data).to(dev, torch.float64)
+        sort_phase = phase("RE segmented: entity sort + projection keys")
+        sort_phase.__enter__()
         ea_t = torch.from_numpy(ea.astype(np.int64)).to(dev)
         order = torch.argsort(ea_t, stable=True)
         lens = (ip[1:] - ip[:-1])[order]
@@ -451,8 +457,10 @@ class RandomEffectDataset:
         rows_t = torch.from_numpy(active_rows.astype(np.int64)).to(dev)[order]
         yy = torch.from_numpy(np.asarray(y, dtype=np.float64)).to(dev)[rows_t]
         ww = torch.from_numpy(np.asarray(wts, dtype=np.float64)).to(dev)[rows_t]
-        glm = DeviceGLMData.from_device_csr(nip, pos, val, yy, torch.zeros_like(yy), ww, max(d_total, 1), dev,
-                                            "f64", col_windows=True)
+        sort_phase.__exit__(None, None, None)
+        with phase("RE segmented: tiled layout"):
+            glm = DeviceGLMData.from_device_csr(nip, pos, val, yy, torch.zeros_like(yy), ww, max(d_total, 1), dev,
+                                                "f64", col_windows=True)
         self._seg_csr = (nip, pos, val)   # kept until the primal sub-problem is built (entity_subset), then freed
         self.projection_keys_t = ukeys
         self.col_entity_t = ukeys // D

@@ -247,7 +247,7 @@ def _device_csr_to_host(counts: torch.Tensor, cols: torch.Tensor, vals: torch.Te
     torch.cumsum(counts, 0, out=indptr[1:])
     x = sp.csr_matrix((vals.cpu().numpy(), cols.to(torch.int32).cpu().numpy(), indptr.cpu().numpy()),
                       shape=(counts.numel(), n_cols))
-    x.has_sorted_indices = True
+    x.has_canonical_format = True          # strictly increasing columns per row (sorted, no duplicates)
     return x
 
 

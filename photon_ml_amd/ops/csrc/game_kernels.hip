@@ -384,6 +384,49 @@ __global__ __launch_bounds__(64) void rs_primal_kernel(const long long* __restri
   for (int j = lane; j < d; j += 64) W[c0 + j] = acc[j];
 }
 
+// ---------------------------------------------------------------------------------------------------------------
+// Histogram of integer keys (torch.bincount) for inputs with very hot keys: the fixed-effect relabel counts 775M
+// column ids of which one (the intercept) occurs in EVERY row and a Zipf head in most, so plain global atomics
+// serialise on a few addresses (torch's kernelHistogram1D: 443 ms at GAME config 5). Each workgroup aggregates its
+// slice in an LDS open-addressing table (HIST_SLOTS keys, linear probing, HIST_PROBES tries) and flushes one global
+// atomic per distinct key it holds; keys that find no slot go straight to global atomics (they are the rare ones).
+// Integer counts: the result does not depend on the order of the atomics.
+#define HIST_SLOTS 4096
+#define HIST_PROBES 8
+#define HIST_THREADS 256
+template <typename KT>
+__global__ __launch_bounds__(HIST_THREADS) void key_hist_kernel(const KT* __restrict__ keys, long long n,
+                                                                long long per_block, long long nbins,
+                                                                unsigned long long* __restrict__ counts) {
+  __shared__ int s_key[HIST_SLOTS];
+  __shared__ unsigned int s_cnt[HIST_SLOTS];
+  for (int i = threadIdx.x; i < HIST_SLOTS; i += HIST_THREADS) { s_key[i] = -1; s_cnt[i] = 0; }
+  __syncthreads();
+  const long long a = (long long)blockIdx.x * per_block;
+  const long long b = a + per_block < n ? a + per_block : n;
+  for (long long i = a + threadIdx.x; i < b; i += HIST_THREADS) {
+    const long long k = (long long)keys[i];
+    if (k < 0 || k >= nbins) continue;                       // the wrapper validates; never index out of range
+    bool done = false;
+    if (k < 0x7fffffffLL) {
+      const int ki = (int)k;
+      unsigned int h = ((unsigned int)ki * 2654435761u) >> (32 - 12);
+      for (int p = 0; p < HIST_PROBES && !done; ++p) {
+        const int s = (int)((h + (unsigned int)p) & (HIST_SLOTS - 1));
+        int cur = s_key[s];
+        if (cur == -1) cur = atomicCAS(&s_key[s], -1, ki) == -1 ? ki : s_key[s];
+        if (cur == ki) { atomicAdd(&s_cnt[s], 1u); done = true; }
+      }
+    }
+    if (!done) atomicAdd(&counts[k], 1ULL);
+  }
+  __syncthreads();
+  for (int s = threadIdx.x; s < HIST_SLOTS; s += HIST_THREADS) {
+    const int k = s_key[s];
+    if (k >= 0 && s_cnt[s]) atomicAdd(&counts[k], (unsigned long long)s_cnt[s]);
+  }
+}
+
 extern "C" {
 
 const char* pml_build_id() { return pml_build_stamp + 13; }
@@ -503,4 +546,20 @@ int pml_rs_primal(int B, int dmax, const long long* ents, const long long* row_p
   LAUNCH_CHECK();
   return 0;
 }
+// counts[nbins] += histogram of keys[n] (int32 if k32 else int64); counts must be zeroed by the caller
+int pml_key_hist(int k32, const void* keys, long long n, long long nbins, unsigned long long* counts, void* stream) {
+  if (n <= 0) return 0;
+  const long long per_block = 1 << 16;
+  const long long blocks = (n + per_block - 1) / per_block;
+  if (blocks > 0x7fffffffLL) return -22;
+  if (k32)
+    hipLaunchKernelGGL(key_hist_kernel<int>, dim3((unsigned)blocks), dim3(HIST_THREADS), 0, (hipStream_t)stream,
+                       (const int*)keys, n, per_block, nbins, counts);
+  else
+    hipLaunchKernelGGL(key_hist_kernel<long long>, dim3((unsigned)blocks), dim3(HIST_THREADS), 0,
+                       (hipStream_t)stream, (const long long*)keys, n, per_block, nbins, counts);
+  LAUNCH_CHECK();
+  return 0;
+}
+
 }  // extern "C"

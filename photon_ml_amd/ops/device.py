@@ -28,7 +28,7 @@ from ..data.matrix import LabeledData
 from .native import SegChunkDesc, check, require_glm_lib, stream_handle
 from .reference import GLMComputable
 from .tiled import DEFAULT_ITEM_ENTRIES, TLFwdChunk, TLTChunk, tl_supported
-from ..utils.timing import trace_range
+from ..utils.timing import phase, trace_range
 
 LAYOUTS = ("auto", "tiled", "segmented")
 
@@ -386,17 +386,21 @@ class DeviceGLMData(GLMComputable):
         relabel, the chunking, the column windows and the layout sorts all run on the device (the host path sliced
         the CSR per chunk with scipy: 6.7 of 14.6 s at GAME config 5)."""
         n, d = x.shape
-        if isinstance(x.indptr, torch.Tensor):        # a DeviceCSR (entity-placed / routed rows): no host copy
-            indptr, col, val = x.indptr.to(dev), x.indices.to(dev).to(torch.int64), x.data.to(dev)
-        else:
-            indptr = torch.from_numpy(np.ascontiguousarray(x.indptr, dtype=np.int64)).to(dev)
-            col = torch.from_numpy(np.ascontiguousarray(x.indices)).to(dev).to(torch.int64)
-            val = torch.from_numpy(np.ascontiguousarray(x.data)).to(dev)
+        with phase("tiled build: upload"):
+            if isinstance(x.indptr, torch.Tensor):        # a DeviceCSR (entity-placed / routed rows): no host copy
+                indptr, col, val = x.indptr.to(dev), x.indices.to(dev).to(torch.int64), x.data.to(dev)
+            else:
+                indptr = torch.from_numpy(np.ascontiguousarray(x.indptr, dtype=np.int64)).to(dev)
+                col = torch.from_numpy(np.ascontiguousarray(x.indices)).to(dev).to(torch.int64)
+                val = torch.from_numpy(np.ascontiguousarray(x.data)).to(dev)
         old_of_new = None
         from ..parallel.dist import is_dist
         shared = relabel and is_dist() and not col_windows
+        relabel_phase = phase("tiled build: hottest-first relabel")
+        relabel_phase.__enter__()
         if shared or (relabel and col.numel() > 0):
-            counts = torch.bincount(col, minlength=d)
+            from .native import key_histogram
+            counts = key_histogram(col, d)          # hot columns (intercept, Zipf head): LDS-aggregated counts
             if shared:
                 import torch.distributed as tdist
                 from ..parallel.sharding import comm_device
@@ -409,6 +413,7 @@ class DeviceGLMData(GLMComputable):
             col = non[col]
             old_of_new = (oon, non)
             del counts
+        relabel_phase.__exit__(None, None, None)
         out = DeviceGLMData.from_device_csr(indptr, col, val, torch.from_numpy(data.y), torch.from_numpy(data.offsets),
                                             torch.from_numpy(data.weights), d, dev, precision, chunk_rows,
                                             item_entries=item_entries, col_windows=col_windows)
@@ -447,6 +452,8 @@ class DeviceGLMData(GLMComputable):
             from .tiled import shard_t_config
             cbits, item_entries = shard_t_config(int(ip[-1] - ip[0]), n, dim, chunk_rows)
         csr, csc, col_lo = [], [], []
+        chunk_phase = phase(f"tiled build: {len(wins)} chunk layouts")
+        chunk_phase.__enter__()
         for i, (lo, hi) in enumerate(wins):
             a, b = starts[i], starts[i + 1]
             ea, eb = ip[i], ip[i + 1]
@@ -457,6 +464,7 @@ class DeviceGLMData(GLMComputable):
             csc.append(TLTChunk(rp, c, v, hi - lo, chunk_rows, cbits=cbits, item_entries=item_entries))
             col_lo.append(lo)
             del c, v
+        chunk_phase.__exit__(None, None, None)
         out = DeviceGLMData(csr, csc, starts, y, offsets, weights, dim, precision, dev, None)
         out.col_lo = col_lo
         return out

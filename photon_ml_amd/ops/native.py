@@ -668,6 +668,8 @@ def game_lib() -> Optional[ctypes.CDLL]:
         lib.pml_seg_gram_set_s.argtypes = [c_int]
         lib.pml_rs_primal.argtypes = [c_int, c_int] + [c_void_p] * 9
         lib.pml_rs_primal.restype = c_int
+        lib.pml_key_hist.argtypes = [c_int, c_void_p, ctypes.c_longlong, ctypes.c_longlong, c_void_p, c_void_p]
+        lib.pml_key_hist.restype = c_int
         lib.pml_tl_compact.argtypes = [c_int, c_int, ctypes.POINTER(CmpArgs), c_void_p]
         lib.pml_tl_compact.restype = c_int
         for f in ("pml_score_rows", "pml_gemm_nt", "pml_spmm_rows", "pml_downsample"):
@@ -702,6 +704,33 @@ def score_rows(indptr: torch.Tensor, col32: torch.Tensor, val: torch.Tensor, w: 
     check(lib.pml_score_rows(indptr.data_ptr(), col32.data_ptr(), val.data_ptr(), n, w.data_ptr(), p(ent), p(eptr),
                              p(efeat), out.data_ptr(), stream_handle(val.device)), "score_rows")
     return out
+
+
+def key_histogram(keys: torch.Tensor, nbins: int) -> torch.Tensor:
+    """``torch.bincount(keys, minlength=nbins)`` (int64) for keys in [0, nbins) with very hot keys
+    (``key_hist_kernel``: per-workgroup LDS aggregation, one global atomic per distinct key per workgroup instead of
+    one per occurrence). Exact integer counts. torch.bincount off the GPU."""
+    if keys.device.type != "cuda":
+        return torch.bincount(keys.to(torch.int64), minlength=nbins)
+    lib = require_game_lib()
+    if keys.dtype not in (torch.int32, torch.int64):
+        keys = keys.to(torch.int64)
+    keys = keys.contiguous()
+    counts = torch.zeros(max(int(nbins), 1), dtype=torch.int64, device=keys.device)
+    if keys.numel():
+        lo, hi = torch.aminmax(keys)
+        if int(lo) < 0 or int(hi) >= nbins:
+            raise ValueError(f"key_histogram: keys outside [0, {nbins})")
+        check(lib.pml_key_hist(int(keys.dtype == torch.int32), keys.data_ptr(), keys.numel(), int(nbins),
+                               counts.data_ptr(), stream_handle(keys.device)), "key_hist")
+    return counts[:nbins]
+
+
+def sorted_counts(sorted_keys: torch.Tensor, nbins: int) -> torch.Tensor:
+    """Per-bin counts of NON-DECREASING keys in [0, nbins) (bincount without atomics: run boundaries by binary
+    search)."""
+    b = torch.searchsorted(sorted_keys, torch.arange(nbins + 1, device=sorted_keys.device, dtype=sorted_keys.dtype))
+    return b[1:] - b[:-1]
 
 
 def gemm_nt(A: torch.Tensor, Bm: torch.Tensor) -> torch.Tensor:

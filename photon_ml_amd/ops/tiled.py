@@ -222,7 +222,12 @@ def split_narrow(pack: torch.Tensor, val: torch.Tensor, n: torch.Tensor, sbits: 
     npack = il(torch.where(p16 >= 32768, p16 - 65536, p16).to(torch.int16)).contiguous()
     nval = il(val[idx]).contiguous()
     nbase = base.to(torch.int32).contiguous()
-    nrounds = torch.bincount(gu[nar], minlength=U).to(torch.int64)
+    # narrow rounds per unit: gu is non-decreasing (units' rounds are consecutive), so a prefix sum of the flags read
+    # at the unit boundaries (torch.bincount on these long runs of one bin serialised its atomics)
+    cs = torch.zeros(nar.numel() + 1, dtype=torch.int64, device=dev)
+    torch.cumsum(nar.to(torch.int64), 0, out=cs[1:])
+    ge = torch.cumsum(gcount, 0)
+    nrounds = cs[ge] - cs[ge - gcount]
     keep = torch.ones(pack.numel(), dtype=torch.bool, device=dev)
     keep[idx.reshape(-1)] = False
     del idx, p16
@@ -444,13 +449,14 @@ class TLTChunk(_NarrowMixin):
         key = (tile << 32) | pack
         del rows, pack
         key, perm = torch.sort(key, stable=True)
+        del tile
+        ntiles = (dim + C - 1) // C
+        # entries per tile from the sorted keys (tile = key >> 32): binary search, no atomics
+        tptr = torch.searchsorted(key >> 32, torch.arange(ntiles + 1, device=dev)).cpu().numpy().astype(np.int64)
+        counts = np.diff(tptr)
         pack = _to_u32_bits(key & 0xFFFFFFFF)
         val = val[perm]
         del key, perm
-        ntiles = (dim + C - 1) // C
-        counts = torch.bincount(tile, minlength=ntiles).cpu().numpy().astype(np.int64)
-        del tile
-        tptr = np.concatenate([[0], np.cumsum(counts)])
         nz = np.nonzero(counts)[0]
         n_it = np.maximum(1, -(-counts[nz] // item_entries))
         # items of every non-empty tile, vectorised: item i of a tile of k items covers [a + (b-a) i / k, ...)

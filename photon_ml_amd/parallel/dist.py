@@ -160,6 +160,19 @@ def check_finite_(t: torch.Tensor, what: str):
         raise FloatingPointError(f"non-finite values in all-reduced {what}")
 
 
+def read_tail_checked(buf: torch.Tensor, start: int, what: str, guard: bool = True) -> list:
+    """``buf[start:]`` as host floats, with the NaN/Inf guard of the WHOLE buffer riding on the same readback: the
+    finiteness flag is reduced on the device and appended to the tail, so guarding costs no extra host
+    synchronisation per collective (the [F, S] scalars are read anyway)."""
+    tail = buf[start:]
+    if not guard:
+        return tail.tolist()
+    vals = torch.cat([tail, torch.isfinite(buf).all().to(buf.dtype).reshape(1)]).tolist()
+    if vals[-1] != 1.0:
+        raise FloatingPointError(f"non-finite values in all-reduced {what}")
+    return vals[:-1]
+
+
 class DistributedGLMData:
     """Wraps a local row shard; every aggregate is summed over the process group with one collective."""
 
@@ -212,8 +225,6 @@ class DistributedGLMData:
                 w.wait()
         if self.local.old_of_new is not None:
             buf[: self.dim] = self.local._unperm(buf[: self.dim].clone())
-        if self.nan_guard:
-            check_finite_(buf, fn)
         return buf
 
     def _packed(self, fn, *args) -> torch.Tensor:
@@ -238,9 +249,7 @@ class DistributedGLMData:
                 buf = tmp.to(buf.device)
             else:
                 all_reduce_(buf, group=self.group)
-        if self.nan_guard:
-            check_finite_(buf, fn)
-        return buf
+        return buf      # the NaN guard rides on the caller's scalar readback (read_tail_checked)
 
     # margin-space line search: trials need two scalars per rank; the accepted step one (overlapped) reduction
     def ls_begin(self, w0_eff, shift0, d_eff, d_shift, t0: float = 1.0, loss=None) -> bool:
@@ -263,9 +272,7 @@ class DistributedGLMData:
         dev = self._comm_device()
         v = torch.tensor([f, d], dtype=torch.float64, device=dev)
         all_reduce_(v, group=self.group)
-        if self.nan_guard:
-            check_finite_(v, "line search")
-        f, d = v.tolist()
+        f, d = read_tail_checked(v, 0, "line search", self.nan_guard)
         return f, d
 
     def zero_point_sums(self, loss, margin_shift):
@@ -298,19 +305,18 @@ class DistributedGLMData:
             tmp = buf.to(dev)
             all_reduce_(tmp, group=self.group)
             buf = tmp.to(buf.device)
-        if self.nan_guard:
-            check_finite_(buf, "ls_finish")
-        fs = buf[self.dim:].tolist()
+        fs = read_tail_checked(buf, self.dim, "ls_finish", self.nan_guard)
         return fs[0], fs[1], buf[: self.dim]
 
     def value_grad_sums(self, loss, w_eff, margin_shift):
         buf = self._packed("value_grad", loss, w_eff, margin_shift)
-        fs = buf[self.dim:].tolist()
+        fs = read_tail_checked(buf, self.dim, "value_grad", self.nan_guard)
         return fs[0], fs[1], buf[: self.dim]
 
     def hv_sums(self, loss, w_eff, margin_shift, v_eff, v_shift):
         buf = self._packed("hv", loss, w_eff, margin_shift, v_eff, v_shift)
-        return buf[: self.dim], float(buf[self.dim + 1])
+        fs = read_tail_checked(buf, self.dim, "hv", self.nan_guard)
+        return buf[: self.dim], fs[1]
 
     def hdiag_sums(self, loss, w):
         d = self.local.hdiag_sums(loss, w).to(torch.float64)

@@ -75,7 +75,8 @@ class IndexMapProjection:
     @staticmethod
     def from_sorted_keys(keys_t, n_entities: int, dim: int) -> "IndexMapProjection":
         import torch
-        cnt = torch.bincount(keys_t // dim, minlength=n_entities)
+        from ..ops.native import sorted_counts
+        cnt = sorted_counts(keys_t // dim, n_entities)     # sorted keys: per-entity runs by binary search
         ptr = np.zeros(n_entities + 1, dtype=np.int64)
         ptr[1:] = np.cumsum(cnt.cpu().numpy())
         return IndexMapProjection(ptr, None, dim, keys_t=keys_t)

@@ -22,6 +22,16 @@ from .watchdog import heartbeat
 TIMELINE = defaultdict(list)
 _TRACE = os.environ.get("PML_TRACE", "0") == "1"
 _TIMELINE_PATH = os.environ.get("PML_TIMELINE")
+# PML_SYNC_TIMED=1: every Timed block synchronises the device on entry and exit, so its wall time is the device-
+# complete time of the work queued inside it (phase tables of the one-shot build / cold sweep; never in a timed run)
+_SYNC = os.environ.get("PML_SYNC_TIMED", "0") == "1"
+
+
+def _device_sync():
+    if _SYNC:
+        import torch
+        if torch.cuda.is_available() and torch.cuda.is_initialized():
+            torch.cuda.synchronize()
 
 
 def _roctx_push(name: str):
@@ -59,12 +69,14 @@ class Timed:
         self.level = level
 
     def __enter__(self):
+        _device_sync()
         self._pushed = _roctx_push(self.msg)
         self.wall0 = time.time()
         self.t0 = time.perf_counter()
         return self
 
     def __exit__(self, *exc):
+        _device_sync()
         heartbeat()
         self.elapsed = time.perf_counter() - self.t0
         if self._pushed:
@@ -84,6 +96,11 @@ def trace_range(name: str):
         heartbeat()
         if pushed:
             _roctx_pop()
+
+
+def phase(msg: str) -> Timed:
+    """A DEBUG-level ``Timed`` block for build / setup phases (device-complete with ``PML_SYNC_TIMED=1``)."""
+    return Timed(msg, logging.getLogger("photon_ml_amd.phase"), logging.DEBUG)
 
 
 def timed(msg: str, fn, *args, logger=None, **kw):

@@ -50,7 +50,8 @@ def main(db, sub, out=None):
     if not sel:
         print("no region matching", sub, "; names:", sorted({r[0] for r in regs})[:50])
         return
-    name, t0, t1 = sel[-1]
+    import os
+    name, t0, t1 = sel[int(os.environ.get("PML_WIN_INDEX", "-1"))]     # which matching region (default: the last)
     ks_ = list(c.execute(f"select {kn}, {ks}, {ke} from {kv} where {ks} >= ? and {ke} <= ? order by {ks}", (t0, t1)))
     busy = sum(e - s for _, s, e in ks_)
     lines.append(f"# window `{name}`: wall {(t1 - t0) / 1e6:.3f} ms, kernels {len(ks_)}, kernel time "
@@ -102,7 +103,9 @@ def main(db, sub, out=None):
     # timeline: every kernel of the window in start order (offset from the window start, duration, the queue /
     # stream column when the database has one) -- the critical path of windows with side-stream work
     qcol = next((x for x in ("stream_id", "queue_id", "stream", "queue") if x in kc), None)
-    if qcol is not None:
+    if os.environ.get("PML_WIN_TIMELINE", "1") == "0":
+        tl = []
+    elif qcol is not None:
         tl = list(c.execute(f"select {kn}, {ks}, {ke}, {qcol} from {kv} where {ks} >= ? and {ke} <= ? order by {ks}",
                             (t0, t1)))
     else:

@@ -147,7 +147,7 @@ def sharding_worker(rank, world, port, out):
     from photon_ml_amd.ops.device import DeviceGLMData
     from photon_ml_amd.parallel.dist import DistributedGLMData
     data, _ = generate_glm_data("LOGISTIC_REGRESSION", 2000, 300, density=0.05, seed=3)
-    local = data.subset(np.arange(rank * 700, 1300 + rank * 700))
+    local = data.subset(np.arange(rank, data.n_rows, world))         # different row shards, uneven for world 3, 8
     dev = DeviceGLMData.from_labeled(local, "cpu", "f64", chunk_rows=512, layout="tiled")
     assert DistributedGLMData(dev).overlap
     np.save(f"{out}/perm_r{rank}.npy", dev.old_of_new.numpy())
@@ -188,7 +188,58 @@ def fsdp_worker(rank, world, port, out):
     dist.destroy_process_group()
 
 
+def sparse_re_data():
+    """GAME data with a third random-effect type of only TWO entities (``regionId``): at world 4 / 8 most ranks own
+    no entity of it (empty local problems, empty routing sends, empty model parts)."""
+    from photon_ml_amd.data.game_data import generate_game_data
+    data, _ = generate_game_data(n_rows=3000, n_users=40, n_items=25, seed=31, task="LOGISTIC_REGRESSION")
+    data.id_tags["regionId"] = np.array([f"r{int(i[1:]) % 2}" if isinstance(i, str) else int(i) % 2
+                                         for i in data.id_tags["itemId"]], dtype=object)
+    data.shards["region"] = data.shards["item"]
+    return data
+
+
+def sparse_re_estimator(device="cpu"):
+    from photon_ml_amd.data.random_effect import FixedEffectDataConfiguration, RandomEffectDataConfiguration
+    from photon_ml_amd.estimators.game_estimator import GameEstimator
+    return (GameEstimator(device=device).set_training_task("LOGISTIC_REGRESSION")
+            .set_coordinate_data_configurations({"global": FixedEffectDataConfiguration("global"),
+                                                 "per-user": RandomEffectDataConfiguration("userId", "user"),
+                                                 "per-region": RandomEffectDataConfiguration("regionId", "region")})
+            .set_coordinate_update_sequence(["global", "per-user", "per-region"])
+            .set_coordinate_descent_iterations(2)
+            .set_validation_evaluators(["AUC", "AUC:regionId", "LOGISTIC_LOSS"]))
+
+
+def sparse_re_worker(rank, world, port, out):
+    """A random-effect type with fewer entities than ranks: ranks owning none of them still run the coordinate
+    (zero local entities), the evaluators and the per-rank model parts; the result equals the single process."""
+    _init(rank, world, port)
+    from photon_ml_amd.io.index_map import DefaultIndexMap
+    from photon_ml_amd.io.model_io import save_game_model
+    from photon_ml_amd.optimization.config import (GLMOptimizationConfiguration, OptimizerConfig,
+                                                   RegularizationContext)
+    data = sparse_re_data()
+    tr, va = data.subset(np.arange(2400)), data.subset(np.arange(2400, 3000))
+    tr_l = tr.subset(np.arange(rank, tr.n_rows, world))
+    va_l = va.subset(np.arange(rank, va.n_rows, world))
+    cfg = GLMOptimizationConfiguration(OptimizerConfig("TRON", 50, 1e-10), RegularizationContext("L2"), 1.0)
+    est = sparse_re_estimator()
+    res = est.fit(tr_l, va_l, [{"global": cfg, "per-user": cfg, "per-region": cfg}])[0]
+    owned = len(est.coordinates["per-region"].dataset.entity_ids) if hasattr(
+        est.coordinates["per-region"], "dataset") else -1
+    np.save(f"{out}/sparse_owned_r{rank}.npy", np.array([owned]))
+    np.save(f"{out}/sparse_fe_r{rank}.npy", res.model.get("global").glm.coefficients.means.numpy())
+    np.save(f"{out}/sparse_eval_r{rank}.npy", np.array([v for _, v in res.evaluations]))
+    maps = {s: DefaultIndexMap.from_keys([f"f{j}\u0001t" for j in range(data.shards[s].shape[1])])
+            for s in data.shards}
+    save_game_model(res.model, f"{out}/model", maps, opt_configs=res.config)
+    import torch.distributed as dist
+    dist.barrier()
+    dist.destroy_process_group()
+
+
 if __name__ == "__main__":
     fn = {"glm": glm_worker, "game": game_worker, "sharding": sharding_worker, "fsdp": fsdp_worker,
-          "placed": placed_worker}[sys.argv[1]]
+          "placed": placed_worker, "sparse_re": sparse_re_worker}[sys.argv[1]]
     fn(int(sys.argv[2]), int(sys.argv[3]), int(sys.argv[4]), sys.argv[5])

@@ -978,3 +978,23 @@ def test_rs_primal_backmap_matches_dense_reference():
     W2 = torch.full_like(W, 7.0)
     rs_primal(*args, W2)
     assert torch.equal(W, W2)
+
+
+@pytest.mark.parametrize("dtype", [torch.int32, torch.int64])
+def test_key_histogram_matches_bincount(dtype):
+    """key_hist_kernel (LDS-aggregated counts for hot keys) == torch.bincount on the CPU: a key in every 'row'
+    (intercept), a Zipf head and a long cold tail (LDS table overflow -> global atomics)."""
+    from photon_ml_amd.ops.native import key_histogram, sorted_counts
+    g = torch.Generator().manual_seed(3)
+    n, nb = 3_000_000, 200_000
+    z = torch.clamp((torch.rand(n, generator=g, dtype=torch.float64) ** -1.3).to(torch.int64), max=nb - 2)
+    keys = torch.cat([z, torch.full((n // 30,), nb - 1, dtype=torch.int64),
+                      torch.randint(0, nb, (n // 3,), generator=g)])
+    keys = keys[torch.randperm(keys.numel(), generator=g)].to(dtype)
+    ref = torch.bincount(keys.to(torch.int64), minlength=nb)
+    got = key_histogram(keys.cuda(), nb).cpu()
+    assert torch.equal(got, ref)
+    s = torch.sort(keys.cuda().to(torch.int64)).values
+    assert torch.equal(sorted_counts(s, nb).cpu(), ref)
+    with pytest.raises(ValueError):
+        key_histogram(torch.tensor([0, nb], device="cuda"), nb)
