@@ -74,6 +74,11 @@ def main():
                          "of config 5 with power-law entity sizes, bench_game.py --config game5pl; entity-sharded over "
                          "the ranks when N > 1) with bf16 and with fp64 fixed-effect features, reported as extra "
                          "keys; auto = on for the lbfgs config")
+    ap.add_argument("--configs-extra", default="auto", choices=["auto", "on", "off"],
+                    help="after the headline (and GAME), also time BASELINE.json configs 3 (OWL-QN, 10M features) and "
+                         "4 (Poisson TRON) at fp64 feature storage (the reference's precision; rows reduced to what "
+                         "fits in HBM, stated in the keys) and bf16, reported as extra keys; auto = on for the lbfgs "
+                         "config on one rank")
     ap.add_argument("--rehearsal", action="store_true",
                     help="allow more ranks than physical devices (several ranks per GPU, or CPU ranks); the record "
                          "then says rehearsal: true, and n_gpus counts devices, not ranks")
@@ -103,91 +108,22 @@ def main():
             f"(pass --rehearsal for a multi-rank rehearsal on fewer devices)")
         sys.exit(2)
 
-    from photon_ml_amd.data.synthetic import generate_device_shard
-    from photon_ml_amd.utils.timing import trace_range
-    from photon_ml_amd.function.losses import LOGISTIC, POISSON
-    from photon_ml_amd.function.objective import GLMObjective
-    from photon_ml_amd.optimization.lbfgs import LBFGS, OWLQN
-    from photon_ml_amd.optimization.tron import TRON
-
-    t_gen = time.time()
-    last = [time.time()]
-
-    def progress(i, n):
-        if time.time() - last[0] > 20 or i == n:
-            last[0] = time.time()
-            log(f"generated chunk {i}/{n}")
-
-    data, _ = generate_device_shard(args.rows_per_gpu, args.features, args.nnz, dev, args.precision,
-                                    seed=args.seed, chunk_rows=args.chunk_rows, rank=rank, progress=progress,
-                                    layout=args.layout, task=cfg["task"])
-    torch.cuda.synchronize()
-    log(f"data ready in {time.time() - t_gen:.1f}s: {data.n_rows} rows/GPU, {data.nbytes() / 2**30:.1f} GiB/GPU, "
-        f"layout={data.layout}")
+    res = glm_run(args.config, args.rows_per_gpu, args.features, args.nnz, args.precision, args.steps, args.warmup,
+                  dev, rank, world, args)
+    elapsed, st, gnorm, passes, kpass = res["elapsed"], res["state"], res["gnorm"], res["passes"], res["kpass"]
+    n_rows_local, layout_name, stalled, total_rows = res["n_rows"], res["layout"], res["stalled"], res["total_rows"]
     sharded = args.optimizer_state == "feature-sharded"
-    gdata = DistributedGLMData(data) if is_dist() and not sharded else data
-    if is_dist() and not sharded:
-        log(f"gradient all-reduce: {'overlapped, %d buckets' % gdata.buckets if gdata.overlap else 'one-shot'}")
-
-    # the optimizer runs exactly warmup + steps iterations (tolerance 0: no early stop), so nothing is queued for an
-    # iteration that never runs (L-BFGS speculates the next direction and its margin pass during the history push)
-    n_iter = args.warmup + args.steps
-    if args.config == "owlqn":
-        obj = GLMObjective(LOGISTIC, l2_weight=0.0)
-        opt = OWLQN(args.l1, tolerance=0.0, max_iterations=n_iter, track_state=False)
-    elif args.config == "tron":
-        obj = GLMObjective(POISSON, l2_weight=args.l2)
-        opt = TRON(tolerance=0.0, max_iterations=n_iter, track_state=False)
-    else:
-        obj = GLMObjective(LOGISTIC, l2_weight=args.l2)
-        opt = LBFGS(tolerance=0.0, max_iterations=n_iter, track_state=False)
-    import contextlib
-    space = contextlib.nullcontext()
-    w0 = torch.zeros(args.features, dtype=torch.float64, device=dev)
-    if sharded:
-        from photon_ml_amd.optimization.vector_space import ShardedSpace, active_space
-        from photon_ml_amd.parallel.feature_sharding import FeatureShardLayout, FeatureShardedObjective
-        layout = FeatureShardLayout.current(args.features)
-        obj = FeatureShardedObjective(obj, layout)
-        w0 = layout.slice(w0).clone()
-        space = active_space(ShardedSpace())
-    with space:
-        opt.start(obj, gdata, w0, skip_zero_tolerance_pass=True)
-        for i in range(args.warmup):
-            st = opt.step(obj, gdata)
-            log(f"warmup {i + 1}/{args.warmup}: f={st.loss:.6e}")
-        if hasattr(opt, "drop_speculation"):
-            # the last warmup step queued the first timed step's direction + margin pass: drop it, so the timed
-            # window holds exactly `steps` forward and `steps` transpose passes
-            opt.drop_speculation()
-        torch.cuda.synchronize()
-        barrier()
-        passes0 = data.n_passes
-        kpass0 = (getattr(data, "n_fwd", 0), getattr(data, "n_t", 0))
-        t0 = time.perf_counter()
-        with trace_range("bench timed steps"):  # roctx region (PML_TRACE=1) for timed-window profiles
-            for i in range(args.steps):
-                st = opt.step(obj, gdata)
-            torch.cuda.synchronize()
-        barrier()
-        elapsed = time.perf_counter() - t0
-        gnorm = st.grad_norm()
-    elapsed = all_reduce_scalar(elapsed, "max", device=dev)
-    passes = data.n_passes - passes0
-    # kernel passes launched inside the timed window (forward / transpose over the non-zeros)
-    kpass = (getattr(data, "n_fwd", 0) - kpass0[0], getattr(data, "n_t", 0) - kpass0[1])
-    n_rows_local, layout_name = data.n_rows, data.layout
-    stalled = bool(getattr(opt, "_finished", False))
-    total_rows = int(all_reduce_scalar(n_rows_local, "sum", device=dev)) if is_dist() else n_rows_local
     value = total_rows * args.steps / elapsed
+    del res
+    import gc
+    gc.collect()
+    torch.cuda.empty_cache()
     game = None
     if args.game == "on" or (args.game == "auto" and args.config == "lbfgs"):
-        # free the GLM shard (115 GiB) before the GAME data is built on the same GPU
-        del data, gdata, opt, obj, w0
-        import gc
-        gc.collect()
-        torch.cuda.empty_cache()
         game = game_extra(dev, rank, world)
+    cfgx = None
+    if args.configs_extra == "on" or (args.configs_extra == "auto" and args.config == "lbfgs" and world == 1):
+        cfgx = configs_extra(dev, rank, world, args)
     if rank == 0:
         log(f"final f={st.loss:.6e} |g|={gnorm:.3e} evals/step={passes / args.steps:.2f} "
             f"optimizer_stalled={stalled}")
@@ -227,7 +163,141 @@ def main():
             out["rehearsal"] = True
         if game is not None:
             out.update(game)
+        if cfgx is not None:
+            out.update(cfgx)
         print(json.dumps(out), flush=True)
+
+
+# feature-storage bytes per non-zero of a tiled shard (forward + transpose copies, measured: bf16 115.5 GiB for
+# 125M x 100) -- sizes the fp64 runs of configs 3 / 4 to the device memory
+BYTES_PER_NNZ = {"bf16": 10.5, "f32": 16.5, "f64": 24.5}
+
+
+def glm_run(config: str, rows: int, features: int, nnz: int, precision: str, steps: int, warmup: int, dev, rank: int,
+            world: int, args) -> dict:
+    """Generate the shard of ``config`` on the device and time ``steps`` optimizer iterations after ``warmup``
+    untimed ones (max over ranks); the shard is freed on return."""
+    import torch
+    from photon_ml_amd.parallel.dist import DistributedGLMData, all_reduce_scalar, barrier, is_dist
+    from photon_ml_amd.data.synthetic import generate_device_shard
+    from photon_ml_amd.utils.timing import trace_range
+    from photon_ml_amd.function.losses import LOGISTIC, POISSON
+    from photon_ml_amd.function.objective import GLMObjective
+    from photon_ml_amd.optimization.lbfgs import LBFGS, OWLQN
+    from photon_ml_amd.optimization.tron import TRON
+    cfg = CONFIGS[config]
+    t_gen = time.time()
+    last = [time.time()]
+
+    def progress(i, n):
+        if time.time() - last[0] > 20 or i == n:
+            last[0] = time.time()
+            log(f"generated chunk {i}/{n}")
+
+    data, _ = generate_device_shard(rows, features, nnz, dev, precision, seed=args.seed, chunk_rows=args.chunk_rows,
+                                    rank=rank, progress=progress, layout=args.layout, task=cfg["task"])
+    torch.cuda.synchronize()
+    t_data = time.time() - t_gen
+    log(f"[{config} {precision}] data ready in {t_data:.1f}s: {data.n_rows} rows/GPU, "
+        f"{data.nbytes() / 2**30:.1f} GiB/GPU, layout={data.layout}")
+    sharded = args.optimizer_state == "feature-sharded"
+    gdata = DistributedGLMData(data) if is_dist() and not sharded else data
+    if is_dist() and not sharded:
+        log(f"gradient all-reduce: {'overlapped, %d buckets' % gdata.buckets if gdata.overlap else 'one-shot'}")
+    # the optimizer runs exactly warmup + steps iterations (tolerance 0: no early stop), so nothing is queued for an
+    # iteration that never runs (L-BFGS speculates the next direction and its margin pass during the history push)
+    n_iter = warmup + steps
+    if config == "owlqn":
+        obj = GLMObjective(LOGISTIC, l2_weight=0.0)
+        opt = OWLQN(args.l1, tolerance=0.0, max_iterations=n_iter, track_state=False)
+    elif config == "tron":
+        obj = GLMObjective(POISSON, l2_weight=args.l2)
+        opt = TRON(tolerance=0.0, max_iterations=n_iter, track_state=False)
+    else:
+        obj = GLMObjective(LOGISTIC, l2_weight=args.l2)
+        opt = LBFGS(tolerance=0.0, max_iterations=n_iter, track_state=False)
+    import contextlib
+    space = contextlib.nullcontext()
+    w0 = torch.zeros(features, dtype=torch.float64, device=dev)
+    if sharded:
+        from photon_ml_amd.optimization.vector_space import ShardedSpace, active_space
+        from photon_ml_amd.parallel.feature_sharding import FeatureShardLayout, FeatureShardedObjective
+        layout = FeatureShardLayout.current(features)
+        obj = FeatureShardedObjective(obj, layout)
+        w0 = layout.slice(w0).clone()
+        space = active_space(ShardedSpace())
+    with space:
+        opt.start(obj, gdata, w0, skip_zero_tolerance_pass=True)
+        for i in range(warmup):
+            st = opt.step(obj, gdata)
+            log(f"[{config} {precision}] warmup {i + 1}/{warmup}: f={st.loss:.6e}")
+        if hasattr(opt, "drop_speculation"):
+            # the last warmup step queued the first timed step's direction + margin pass: drop it, so the timed
+            # window holds exactly `steps` forward and `steps` transpose passes
+            opt.drop_speculation()
+        torch.cuda.synchronize()
+        barrier()
+        passes0 = data.n_passes
+        kpass0 = (getattr(data, "n_fwd", 0), getattr(data, "n_t", 0))
+        t0 = time.perf_counter()
+        with trace_range("bench timed steps"):  # roctx region (PML_TRACE=1) for timed-window profiles
+            for i in range(steps):
+                st = opt.step(obj, gdata)
+            torch.cuda.synchronize()
+        barrier()
+        elapsed = time.perf_counter() - t0
+        gnorm = st.grad_norm()
+    elapsed = all_reduce_scalar(elapsed, "max", device=dev)
+    kpass = (getattr(data, "n_fwd", 0) - kpass0[0], getattr(data, "n_t", 0) - kpass0[1])
+    out = {"elapsed": elapsed, "state": st, "gnorm": gnorm, "passes": data.n_passes - passes0, "kpass": kpass,
+           "n_rows": data.n_rows, "layout": data.layout, "stalled": bool(getattr(opt, "_finished", False)),
+           "total_rows": int(all_reduce_scalar(data.n_rows, "sum", device=dev)) if is_dist() else data.n_rows,
+           "gib": data.nbytes() / 2**30, "data_s": t_data}
+    del data, gdata, opt, obj, w0
+    return out
+
+
+def configs_extra(dev, rank: int, world: int, args) -> dict:
+    """BASELINE.json configs 3 (logistic OWL-QN, 1B x 10M over 8 GPUs = 125M rows/GPU x 10M features) and 4 (Poisson
+    TRON, 500M rows over 8 GPUs = 62.5M rows/GPU), timed in this run at fp64 feature storage -- the reference computes
+    in Double -- with the rows reduced to what fits in this device's memory (stated as ``rows_per_gpu`` next to the
+    config's ``config_rows_per_gpu``), and at bf16 (the full row count) for context. Keys ``owlqn10m_<dtype>_*`` and
+    ``tron_poisson_<dtype>_*``; each carries its own steps / warmup / passes per step. Failures are reported, never
+    fatal to the headline line."""
+    import gc
+    import torch
+    out = {}
+    runs = (("owlqn", "owlqn10m", "f64", 5, 2), ("owlqn", "owlqn10m", "bf16", 5, 2),
+            ("tron", "tron_poisson", "f64", 3, 1), ("tron", "tron_poisson", "bf16", 3, 1))
+    for config, key, prec, steps, warmup in runs:
+        cfg = CONFIGS[config]
+        pre = f"{key}_{prec}"
+        try:
+            gc.collect()
+            torch.cuda.empty_cache()
+            free, _ = torch.cuda.mem_get_info(dev)
+            fit = int(0.82 * free / (args.nnz * BYTES_PER_NNZ[prec])) // (1 << 20) * (1 << 20)
+            rows = min(cfg["rows_per_gpu"], fit)
+            r = glm_run(config, rows, cfg["features"], args.nnz, prec, steps, warmup, dev, rank, world, args)
+            out[f"{pre}_ms_per_step"] = 1000.0 * r["elapsed"] / steps
+            out[f"{pre}_examples_per_sec"] = r["total_rows"] * steps / r["elapsed"]
+            out[f"{pre}_config"] = {
+                "model": cfg["model"], "metric": cfg["metric"], "dtype": prec, "rows_per_gpu": r["n_rows"],
+                "config_rows_per_gpu": cfg["rows_per_gpu"], "rows_reduced_to_fit": r["n_rows"] < cfg["rows_per_gpu"],
+                "features": cfg["features"], "nnz_per_row": args.nnz, "steps": steps, "warmup": warmup,
+                "evals_per_step": r["passes"] / steps, "forward_passes_per_step": r["kpass"][0] / steps,
+                "transpose_passes_per_step": r["kpass"][1] / steps, "shard_gib": round(r["gib"], 1),
+                "optimizer_stalled": r["stalled"], "data_generation_s": round(r["data_s"], 1)}
+            log(f"[{config} {prec}] {out[f'{pre}_ms_per_step']:.2f} ms/step over {r['n_rows']} rows "
+                f"({r['passes'] / steps:.1f} evaluations/step)")
+            del r
+        except Exception as e:  # pragma: no cover - reported in the record
+            out[f"{pre}_error"] = repr(e)[:500]
+            log(f"[{config} {prec}] failed: {e!r}"[:400])
+        finally:
+            gc.collect()
+            torch.cuda.empty_cache()
+    return out
 
 
 def game_extra(dev, rank: int, world: int) -> dict:

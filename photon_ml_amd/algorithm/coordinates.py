@@ -38,6 +38,9 @@ from ..sampling.samplers import down_sampler_for_task
 
 
 log = logging.getLogger(__name__)
+# data-only solver setup (FE launch tables, RE solver components) at coordinate construction (PML_EAGER_SETUP=0:
+# lazily in the first update, as before round 6)
+EAGER_SETUP = os.environ.get("PML_EAGER_SETUP", "1") != "0"
 
 
 def _sync(t):
@@ -107,6 +110,15 @@ class FixedEffectCoordinate(Coordinate):
             self.labels = labeled.y
         with phase(f"FE {coordinate_id} build: device layout"):
             self.glm_data = make_glm_data(labeled, self.device, precision)
+        gd = self.glm_data
+        if EAGER_SETUP and hasattr(gd, "_build_multi"):
+            # every pass of every update uses the shard-wide launch tables: build them with the layout (one-time data
+            # setup), not inside the first update
+            with phase(f"FE {coordinate_id} build: launch tables"):
+                if getattr(gd, "_multi", "unset") == "unset":
+                    gd._build_multi()
+                if getattr(gd, "_multi_t", "unset") == "unset":
+                    gd._build_multi_t()
         self.compute_variance = compute_variance
         self.normalization = normalization
         self.set_config(opt_config)
@@ -245,6 +257,14 @@ class RandomEffectCoordinate(Coordinate):
         self._W = {}  # projected-space warm-start state per bucket
         self._returned = None  # the model object the last update returned (its solver state is in _W / _rs)
         self.last_stats = {}
+        if EAGER_SETUP and self.dataset.layout == "segmented" and self.device.type == "cuda":
+            # the solver components (row-space Gram factors, the fused batch's gathered rows, launch classes) depend
+            # on the data only: built with the dataset, as the reference builds its RandomEffectDataSet up front
+            # (RandomEffectDataSet.scala:239-279), so the first coordinate-descent update is a solve
+            cfg = self.opt_config
+            reg, lam = cfg.regularization_context, cfg.regularization_weight
+            with phase(f"RE {coordinate_id} build: solver components"):
+                self._components(reg.l1_weight(lam), cfg.optimizer_config)
 
     # The tracker statistics of the last update (random_effect_tracker_stats) are reduced on first read: the masked
     # selection of active entities and the dozen small reductions behind them (a stream synchronisation) stay off

@@ -527,6 +527,14 @@ class RandomEffectDataset:
         ent_new = torch.cumsum(mask.to(torch.int64), 0) - 1
         return sip, spos, sval, row_sel, col_sel, ent_new
 
+    def entity_rows(self, mask: torch.Tensor):
+        """``(row_sel, col_sel)``: parent row positions and parent coefficient positions of the entities in
+        ``mask`` (each entity's rows and coefficient range stay contiguous and in order). No non-zero-sized work:
+        callers gather the rows' entries themselves (``ops.native.csr_gather_rows``)."""
+        seg = self.seg
+        mask = mask.to(seg.y.device)
+        return torch.nonzero(mask[seg.row_entity]).squeeze(1), torch.nonzero(mask[seg.col_entity]).squeeze(1)
+
     def release_csr(self):
         self._seg_csr = None
 

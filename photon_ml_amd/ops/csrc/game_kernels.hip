@@ -294,8 +294,12 @@ __global__ __launch_bounds__(256) void tl_compact_kernel(CmpArgs a) {
 // S rows per scatter round (template): rows i0 .. i0 + S - 1 go into S interleaved image slots (img[c S + s]), and
 // one walk over row j's entries feeds S accumulators -- S times fewer walks (global reads + dependent chains) than
 // one row per round, the same fma sequence per K entry (bitwise equal for every S).
-template <int S>
-__global__ __launch_bounds__(64) void seg_gram_kernel(int B, int n, const long long* __restrict__ ents,
+// STAGE: the entity's entries (local column as uint16, value) and row offsets are first copied into LDS with
+// coalesced whole-wave loads; the per-lane walks over row j then read LDS instead of issuing one uncoalesced global
+// load per entry (64 lanes on 64 different rows) -- the dependent chain of a walk is LDS-latency bound, not
+// HBM-latency bound. Same fma sequence, bitwise equal to the unstaged walk.
+template <int S, bool STAGE>
+__global__ __launch_bounds__(64) void seg_gram_kernel(int B, int n, int dmax, const long long* __restrict__ ents,
                                                       const long long* __restrict__ row_ptr,
                                                       const long long* __restrict__ col_ptr,
                                                       const long long* __restrict__ nip,
@@ -310,14 +314,32 @@ __global__ __launch_bounds__(64) void seg_gram_kernel(int B, int n, const long l
   const int ne = (int)(row_ptr[e + 1] - r0);
   const long long cb = col_ptr[e];
   const int de = (int)(col_ptr[e + 1] - cb);
+  const long long e0 = nip[r0];
+  const int enz = (int)(nip[r0 + ne] - e0);
+  // staged layout after the image: values [enz] doubles, local columns [enz] uint16, row offsets [ne + 1] int
+  double* sval = img + (size_t)dmax * S;
+  unsigned short* scol = (unsigned short*)(sval + enz);
+  int* sptr = (int*)(scol + ((enz + 3) & ~3));
   for (int c = lane; c < de * S; c += 64) img[c] = 0.0;
+  if (STAGE) {
+    for (int t = lane; t < enz; t += 64) {
+      sval[t] = val[e0 + t];
+      scol[t] = (unsigned short)(pos[e0 + t] - cb);
+    }
+    for (int i = lane; i <= ne; i += 64) sptr[i] = (int)(nip[r0 + i] - e0);
+  }
   __syncthreads();
   double* Kb = K + b * (long long)n * n;
   for (int i0 = 0; i0 < ne; i0 += S) {
     const int ns = ne - i0 < S ? ne - i0 : S;
     for (int s = 0; s < ns; ++s) {
-      const long long ib = nip[r0 + i0 + s], ie = nip[r0 + i0 + s + 1];
-      for (long long t = ib + lane; t < ie; t += 64) img[(pos[t] - cb) * S + s] = val[t];
+      if (STAGE) {
+        const int ib = sptr[i0 + s], ie = sptr[i0 + s + 1];
+        for (int t = ib + lane; t < ie; t += 64) img[(int)scol[t] * S + s] = sval[t];
+      } else {
+        const long long ib = nip[r0 + i0 + s], ie = nip[r0 + i0 + s + 1];
+        for (long long t = ib + lane; t < ie; t += 64) img[(pos[t] - cb) * S + s] = val[t];
+      }
     }
     __syncthreads();
     // lane takes rows j = lane, lane + 64, lane + 128 (n <= 192)
@@ -326,12 +348,22 @@ __global__ __launch_bounds__(64) void seg_gram_kernel(int B, int n, const long l
 #pragma unroll
       for (int s = 0; s < S; ++s) acc[s] = 0.0;
       if (j < ne) {
-        const long long jb = nip[r0 + j], je = nip[r0 + j + 1];
-        for (long long t = jb; t < je; ++t) {
-          const double v = val[t];
-          const double* im = img + (pos[t] - cb) * S;
+        if (STAGE) {
+          const int jb = sptr[j], je = sptr[j + 1];
+          for (int t = jb; t < je; ++t) {
+            const double v = sval[t];
+            const double* im = img + (int)scol[t] * S;
 #pragma unroll
-          for (int s = 0; s < S; ++s) acc[s] = fma(v, im[s], acc[s]);
+            for (int s = 0; s < S; ++s) acc[s] = fma(v, im[s], acc[s]);
+          }
+        } else {
+          const long long jb = nip[r0 + j], je = nip[r0 + j + 1];
+          for (long long t = jb; t < je; ++t) {
+            const double v = val[t];
+            const double* im = img + (pos[t] - cb) * S;
+#pragma unroll
+            for (int s = 0; s < S; ++s) acc[s] = fma(v, im[s], acc[s]);
+          }
         }
       }
 #pragma unroll
@@ -340,13 +372,58 @@ __global__ __launch_bounds__(64) void seg_gram_kernel(int B, int n, const long l
     }
     __syncthreads();
     for (int s = 0; s < ns; ++s) {
-      const long long ib = nip[r0 + i0 + s], ie = nip[r0 + i0 + s + 1];
-      for (long long t = ib + lane; t < ie; t += 64) img[(pos[t] - cb) * S + s] = 0.0;
+      if (STAGE) {
+        const int ib = sptr[i0 + s], ie = sptr[i0 + s + 1];
+        for (int t = ib + lane; t < ie; t += 64) img[(int)scol[t] * S + s] = 0.0;
+      } else {
+        const long long ib = nip[r0 + i0 + s], ie = nip[r0 + i0 + s + 1];
+        for (long long t = ib + lane; t < ie; t += 64) img[(pos[t] - cb) * S + s] = 0.0;
+      }
     }
     __syncthreads();
   }
   for (int i = ne; i < n; ++i)
     for (int j = lane; j < n; j += 64) Kb[(long long)j * n + i] = 0.0;
+}
+
+// Batched Cholesky of the row-space Gram matrices (replaces torch.linalg.cholesky_ex = rocSOLVER dpotf2: 48
+// launches per class set and a one-off library initialisation on the cold path). One wave per problem, the lower
+// triangle packed in LDS (n (n + 1) / 2 doubles: <= 148 KB at n = 192), left-looking: column j's entries are dot
+// products of row prefixes, lanes over rows i >= j. Rows i >= nv[b] (padding slots) are the identity. Writes the
+// full n x n factor (upper triangle zero) over K; info[b] = 0, or j + 1 for the first non-positive / non-finite
+// pivot (then the factor is not used).
+__global__ __launch_bounds__(64) void batched_chol_kernel(int B, int n, const long long* __restrict__ nv,
+                                                          double* __restrict__ K, int* __restrict__ info) {
+  extern __shared__ double Lp[];
+  const int lane = threadIdx.x;
+  const long long b = blockIdx.x;
+  if (b >= B) return;
+  const int m = (int)nv[b];
+  double* Kb = K + b * (long long)n * n;
+  for (int i = lane; i < n; i += 64)
+    for (int k = 0; k <= i; ++k)
+      Lp[i * (i + 1) / 2 + k] = (i < m && k < m) ? Kb[(long long)i * n + k] : (i == k ? 1.0 : 0.0);
+  __syncthreads();
+  int bad = 0;
+  for (int j = 0; j < m && !bad; ++j) {
+    const int rj = j * (j + 1) / 2;
+    double djj = Lp[rj + j];
+    for (int k = 0; k < j; ++k) djj = fma(-Lp[rj + k], Lp[rj + k], djj);
+    __syncthreads();
+    if (!(djj > 0.0) || !isfinite(djj)) { bad = j + 1; break; }
+    const double ljj = sqrt(djj);
+    for (int i = j + 1 + lane; i < m; i += 64) {
+      const int ri = i * (i + 1) / 2;
+      double a = Lp[ri + j];
+      for (int k = 0; k < j; ++k) a = fma(-Lp[ri + k], Lp[rj + k], a);
+      Lp[ri + j] = a / ljj;
+    }
+    if (lane == 0) Lp[rj + j] = ljj;
+    __syncthreads();
+  }
+  if (lane == 0) info[b] = bad;
+  for (int i = lane; i < n; i += 64)
+    for (int k = 0; k < n; ++k) Kb[(long long)i * n + k] = k <= i ? Lp[i * (i + 1) / 2 + k] : 0.0;
 }
 
 // Row-space back-map w_e = X_e^T r_e for the entities ents[B] (random-effect model materialisation,
@@ -424,6 +501,37 @@ __global__ __launch_bounds__(HIST_THREADS) void key_hist_kernel(const KT* __rest
   for (int s = threadIdx.x; s < HIST_SLOTS; s += HIST_THREADS) {
     const int k = s_key[s];
     if (k >= 0 && s_cnt[s]) atomicAdd(&counts[k], (unsigned long long)s_cnt[s]);
+  }
+}
+
+// ---------------------------------------------------------------------------------------------------------------
+// Row gather of a CSR into a new CSR (random-effect solver setup: the fused primal batch's rows, the row-space
+// back-map's compact copy). Row r of the output = row rows[r] of the input, starting at optr[r] with
+// optr[r + 1] - optr[r] >= its length slots (extra slots zero-filled: the lean kernel's quad padding); columns minus
+// cbase[r] (entity-local) when cbase is given, stored as CT (int16 / int64). One wave per row, coalesced copies:
+// replaces a chain of torch repeat_interleave / gather / scatter passes over every non-zero.
+template <typename CT>
+__global__ __launch_bounds__(256) void csr_gather_rows_kernel(const long long* __restrict__ nip,
+                                                              const long long* __restrict__ pos,
+                                                              const double* __restrict__ val,
+                                                              const long long* __restrict__ rows, long long nr,
+                                                              const long long* __restrict__ optr,
+                                                              const long long* __restrict__ cbase,
+                                                              CT* __restrict__ ocol, double* __restrict__ oval) {
+  const long long r = (long long)blockIdx.x * 4 + (threadIdx.x >> 6);
+  const int lane = threadIdx.x & 63;
+  if (r >= nr) return;
+  const long long src = nip[rows[r]], len = nip[rows[r] + 1] - src;
+  const long long dst = optr[r], dlen = optr[r + 1] - dst;
+  const long long base = cbase != nullptr ? cbase[r] : 0;
+  for (long long t = lane; t < dlen; t += 64) {
+    if (t < len) {
+      ocol[dst + t] = (CT)(pos[src + t] - base);
+      oval[dst + t] = val[src + t];
+    } else {
+      ocol[dst + t] = (CT)0;
+      oval[dst + t] = 0.0;
+    }
   }
 }
 
@@ -507,29 +615,46 @@ int pml_gemm_nt(int M, int N, int K, const double* A, int lda, const double* Bm,
 static int g_seg_gram_s = 0;   // rows per scatter round of seg_gram_kernel (0: by LDS size; A/B: pml_seg_gram_set_s)
 void pml_seg_gram_set_s(int s) { g_seg_gram_s = (s == 1 || s == 2 || s == 4 || s == 8) ? s : 0; }
 
-// K [B, n, n] for the entities ents[B]; dmax = max projected columns of those entities (LDS image size).
-int pml_seg_gram(int B, int n, int dmax, const long long* ents, const long long* row_ptr, const long long* col_ptr,
-                 const long long* nip, const long long* pos, const double* val, double* K, void* stream) {
+// K [B, n, n] for the entities ents[B]; dmax = max projected columns of those entities (LDS image size); maxnnz = max
+// non-zeros of one of those entities (> 0: stage the entries in LDS when they fit, see seg_gram_kernel STAGE).
+int pml_seg_gram(int B, int n, int dmax, long long maxnnz, const long long* ents, const long long* row_ptr,
+                 const long long* col_ptr, const long long* nip, const long long* pos, const double* val, double* K,
+                 void* stream) {
   if (B <= 0) return 0;
   if (n < 1 || n > 192 || dmax < 0 || (size_t)dmax * sizeof(double) > 160 * 1024) return -22;
   // rows per scatter round: as many as keep the image <= 32 KB (>= 5 one-wave workgroups per CU)
   const size_t d8 = (size_t)std::max(dmax, 1) * sizeof(double);
   const int S = g_seg_gram_s > 0 ? g_seg_gram_s : (d8 * 8 <= 32768 ? 8 : d8 * 4 <= 32768 ? 4 : d8 * 2 <= 32768 ? 2 : 1);
-  const size_t lds = d8 * (size_t)S;
+  const size_t img = d8 * (size_t)S;
+  const size_t stage = maxnnz > 0 ? (size_t)maxnnz * 10 + 8 + (size_t)(n + 1) * 4 + 16 : 0;
+  const bool staged = maxnnz > 0 && img + stage <= 64 * 1024;
+  const size_t lds = staged ? img + stage : img;
   if (lds > 160 * 1024) return -22;
   hipStream_t st = (hipStream_t)stream;
-  if (S == 8)
-    hipLaunchKernelGGL(seg_gram_kernel<8>, dim3((unsigned)B), dim3(64), lds, st, B, n, ents, row_ptr, col_ptr, nip, pos,
-                       val, K);
-  else if (S == 4)
-    hipLaunchKernelGGL(seg_gram_kernel<4>, dim3((unsigned)B), dim3(64), lds, st, B, n, ents, row_ptr, col_ptr, nip, pos,
-                       val, K);
-  else if (S == 2)
-    hipLaunchKernelGGL(seg_gram_kernel<2>, dim3((unsigned)B), dim3(64), lds, st, B, n, ents, row_ptr, col_ptr, nip, pos,
-                       val, K);
-  else
-    hipLaunchKernelGGL(seg_gram_kernel<1>, dim3((unsigned)B), dim3(64), lds, st, B, n, ents, row_ptr, col_ptr, nip, pos,
-                       val, K);
+#define SEG_GRAM_LAUNCH(SS)                                                                                       \
+  do {                                                                                                           \
+    if (staged)                                                                                                  \
+      hipLaunchKernelGGL((seg_gram_kernel<SS, true>), dim3((unsigned)B), dim3(64), lds, st, B, n, std::max(dmax, 1), \
+                         ents, row_ptr, col_ptr, nip, pos, val, K);                                              \
+    else                                                                                                         \
+      hipLaunchKernelGGL((seg_gram_kernel<SS, false>), dim3((unsigned)B), dim3(64), lds, st, B, n, std::max(dmax, 1), \
+                         ents, row_ptr, col_ptr, nip, pos, val, K);                                              \
+  } while (0)
+  if (S == 8) SEG_GRAM_LAUNCH(8);
+  else if (S == 4) SEG_GRAM_LAUNCH(4);
+  else if (S == 2) SEG_GRAM_LAUNCH(2);
+  else SEG_GRAM_LAUNCH(1);
+#undef SEG_GRAM_LAUNCH
+  LAUNCH_CHECK();
+  return 0;
+}
+
+// In-place Cholesky of K [B, n, n] (n <= 192); nv[b] = valid rows of problem b (the rest: identity); info[B].
+int pml_batched_chol(int B, int n, const long long* nv, double* K, int* info, void* stream) {
+  if (B <= 0) return 0;
+  if (n < 1 || n > 192) return -22;
+  const size_t lds = (size_t)n * (n + 1) / 2 * sizeof(double);
+  hipLaunchKernelGGL(batched_chol_kernel, dim3((unsigned)B), dim3(64), lds, (hipStream_t)stream, B, n, nv, K, info);
   LAUNCH_CHECK();
   return 0;
 }
@@ -558,6 +683,23 @@ int pml_key_hist(int k32, const void* keys, long long n, long long nbins, unsign
   else
     hipLaunchKernelGGL(key_hist_kernel<long long>, dim3((unsigned)blocks), dim3(HIST_THREADS), 0,
                        (hipStream_t)stream, (const long long*)keys, n, per_block, nbins, counts);
+  LAUNCH_CHECK();
+  return 0;
+}
+
+// out (col as int16 if c16 else int64, val fp64) = rows[nr] of (nip, pos, val) at optr, minus cbase (may be null)
+int pml_csr_gather_rows(int c16, const long long* nip, const long long* pos, const double* val, const long long* rows,
+                        long long nr, const long long* optr, const long long* cbase, void* ocol, double* oval,
+                        void* stream) {
+  if (nr <= 0) return 0;
+  const long long blocks = (nr + 3) / 4;
+  if (blocks > 0x7fffffffLL) return -22;
+  if (c16)
+    hipLaunchKernelGGL(csr_gather_rows_kernel<short>, dim3((unsigned)blocks), dim3(256), 0, (hipStream_t)stream, nip,
+                       pos, val, rows, nr, optr, cbase, (short*)ocol, oval);
+  else
+    hipLaunchKernelGGL(csr_gather_rows_kernel<long long>, dim3((unsigned)blocks), dim3(256), 0, (hipStream_t)stream,
+                       nip, pos, val, rows, nr, optr, cbase, (long long*)ocol, oval);
   LAUNCH_CHECK();
   return 0;
 }

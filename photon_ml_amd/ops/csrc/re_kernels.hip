@@ -151,6 +151,7 @@ struct ReTronArgs {
   double l2, tol;
   int max_iter, max_fail, max_cg, dmax;
   double* gsc;               // lean kernel: gradient at W, per coefficient (packed like W)
+  const double* xf2;         // lean kernel, optional: ||X_e||_F^2 per entity (lazy zero-point gradient norm)
 };
 
 // Loads through the global address space: a generic pointer read through the kernel-argument struct becomes a FLAT
@@ -747,12 +748,33 @@ void re_tron_lean_kernel(ReTronArgs a) {
   }
   block_sums<1>(nz, red, parity);
   double f0z = f, g0n = sqrt(gnorm2);
+  bool g0_lazy = false;
   if (nz[0] != 0.0) {
-    double g0;
-    f0z = value_grad(true, 0, g0);
-    g0n = sqrt(g0);
+    if (a.xf2 != nullptr) {
+      // warm start: the tolerances scale with the zero point's f(0) and ||g(0)|| (Optimizer.scala). f(0) needs only
+      // the rows' offsets; ||g(0)|| = ||X_e^T c|| <= ||X_e||_F ||c|| (c_i = w_i l'(o_i)) stands in until a gradient
+      // norm comes below the bound's tolerance -- then the exact pass at zero runs (convergence decisions are
+      // those of the exact norm). No pass over the entity's entries for the common case.
+      double s2[2] = {0.0, 0.0};
+      for (long long i = r0 + tid; i < r1; i += RE_THREADS) {
+        double l, dl, d2;
+        loss_t<LOSS>(gld(a.off + i), gld(a.y + i), l, dl, d2);
+        const double wi = gld(a.wt + i);
+        s2[0] += wi * l;
+        s2[1] += (wi * dl) * (wi * dl);
+      }
+      block_sums<2>(s2, red, parity);
+      f0z = s2[0];
+      g0n = sqrt(gld(a.xf2 + e) * s2[1]) * (1.0 + 1e-6) + 1e-300;
+      g0_lazy = true;
+    } else {
+      double g0;
+      f0z = value_grad(true, 0, g0);
+      g0n = sqrt(g0);
+    }
   }
-  const double loss_tol = f0z * a.tol, grad_tol = g0n * a.tol;
+  const double loss_tol = f0z * a.tol;
+  double grad_tol = g0n * a.tol;
   double delta = sqrt(gnorm2);
   int it = 0, fails = 0, reason = 0;
   bool active = true;
@@ -875,6 +897,13 @@ void re_tron_lean_kernel(ReTronArgs a) {
       ++fails;
     }
     const bool not_impr = !accept && fails >= a.max_fail;
+    if (accept && g0_lazy && sqrt(gnorm2) <= grad_tol) {
+      // the bound no longer decides: the exact ||g(0)|| (a pass at zero; acc is free, Gg holds the gradient)
+      double g0;
+      (void)value_grad(true, 0, g0);
+      grad_tol = sqrt(g0) * a.tol;
+      g0_lazy = false;
+    }
     int rc = 0;
     if (accept && sqrt(gnorm2) <= grad_tol) rc = 4;
     if (accept && fabs(f - f_prev) <= loss_tol) rc = 3;
@@ -1931,12 +1960,13 @@ int pml_re_tron_lean(const int* order, int n_launch, const long long* row_ptr, c
                      const long long* nip, const uint16_t* lcol, const double* val, const double* y,
                      const double* off, const double* wt, double* scr, long long n_rows, double* W, double* f,
                      int* iters, int* reason, double* zout, int* npass, int loss, double l2, double tol,
-                     int max_iter, int max_fail, int max_cg, int dmax, double* gsc, int quad, hipStream_t st) {
+                     int max_iter, int max_fail, int max_cg, int dmax, double* gsc, int quad, const double* xf2,
+                     hipStream_t st) {
   if (n_launch <= 0) return 0;
   if (dmax <= 0 || dmax > 1024 || loss < 0 || loss > 2 || gsc == nullptr) return -22;
   const size_t smem = pml_re_tron_lean_smem(dmax);
   ReTronArgs a{order, n_launch, row_ptr, col_ptr, nip, lcol, val, y, off, wt, scr, n_rows, W, f, iters, reason,
-               zout, npass, loss, l2, tol, max_iter, max_fail, max_cg, dmax, gsc};
+               zout, npass, loss, l2, tol, max_iter, max_fail, max_cg, dmax, gsc, xf2};
   // quad: every row padded to a multiple of 4 entries (row_pass_q), else the strided row_pass
   if (quad) {
     if (loss == LOSS_LOGISTIC) lean_launch<0, true>(a, n_launch, smem, st);

@@ -234,10 +234,13 @@ def segdot(a: torch.Tensor, b: Optional[torch.Tensor], ptr: torch.Tensor, mode: 
     out = torch.empty(nseg, dtype=torch.float64, device=a.device)
     # the longest segment, measured once per segment table (one host read; the tables are built once per
     # dataset): segments longer than SEGDOT_CHUNK are split over chunk waves (pml_segdot_long)
-    maxlen = getattr(ptr, "_pml_maxlen", None)
-    if maxlen is None:
+    # cached with the tensor's version counter: an in-place change of the table (e.g. cumsum(out=ptr)) re-measures
+    cached = getattr(ptr, "_pml_maxlen", None)
+    if cached is not None and cached[0] == ptr._version:
+        maxlen = cached[1]
+    else:
         maxlen = int((ptr[1:] - ptr[:-1]).max()) if nseg else 0
-        ptr._pml_maxlen = maxlen
+        ptr._pml_maxlen = (ptr._version, maxlen)
     if maxlen > SEGDOT_CHUNK:
         n = a.numel()
         scratch = torch.empty(2 * ((n + SEGDOT_CHUNK - 1) // SEGDOT_CHUNK), dtype=torch.float64, device=a.device)
@@ -664,10 +667,15 @@ def game_lib() -> Optional[ctypes.CDLL]:
                                       c_void_p]
         lib.pml_downsample.argtypes = [c_int, c_void_p, c_void_p, c_void_p, ctypes.c_longlong, ctypes.c_ulonglong,
                                        c_double, c_int, c_void_p, c_void_p]
-        lib.pml_seg_gram.argtypes = [c_int, c_int, c_int] + [c_void_p] * 8
+        lib.pml_seg_gram.argtypes = [c_int, c_int, c_int, ctypes.c_longlong] + [c_void_p] * 8
+        lib.pml_batched_chol.argtypes = [c_int, c_int, c_void_p, c_void_p, c_void_p, c_void_p]
+        lib.pml_batched_chol.restype = c_int
         lib.pml_seg_gram_set_s.argtypes = [c_int]
         lib.pml_rs_primal.argtypes = [c_int, c_int] + [c_void_p] * 9
         lib.pml_rs_primal.restype = c_int
+        lib.pml_csr_gather_rows.argtypes = [c_int, c_void_p, c_void_p, c_void_p, c_void_p, ctypes.c_longlong,
+                                            c_void_p, c_void_p, c_void_p, c_void_p, c_void_p]
+        lib.pml_csr_gather_rows.restype = c_int
         lib.pml_key_hist.argtypes = [c_int, c_void_p, ctypes.c_longlong, ctypes.c_longlong, c_void_p, c_void_p]
         lib.pml_key_hist.restype = c_int
         lib.pml_tl_compact.argtypes = [c_int, c_int, ctypes.POINTER(CmpArgs), c_void_p]
@@ -726,6 +734,41 @@ def key_histogram(keys: torch.Tensor, nbins: int) -> torch.Tensor:
     return counts[:nbins]
 
 
+def csr_gather_rows(nip: torch.Tensor, pos: torch.Tensor, val: torch.Tensor, rows: torch.Tensor, optr: torch.Tensor,
+                    cbase: Optional[torch.Tensor] = None, col_dtype=torch.int64):
+    """Rows ``rows`` of the CSR ``(nip, pos, val)`` (int64 / int64 / fp64) as a new CSR whose row r starts at
+    ``optr[r]`` and spans ``optr[r + 1] - optr[r] >=`` its length slots (the rest zero: padding); columns minus
+    ``cbase[r]`` when given, as ``col_dtype`` (int16 or int64). Returns ``(cols, vals)``
+    (``csr_gather_rows_kernel``; torch off the GPU)."""
+    nr = int(rows.numel())
+    total = int(optr[-1]) if nr else 0
+    dev = val.device
+    assert col_dtype in (torch.int16, torch.int64) and optr.numel() == nr + 1
+    ocol = torch.empty(total, dtype=col_dtype, device=dev)
+    oval = torch.empty(total, dtype=torch.float64, device=dev)
+    if nr == 0:
+        return ocol, oval
+    if dev.type != "cuda":
+        lens = nip[rows + 1] - nip[rows]
+        dl = optr[1:] - optr[:-1]
+        r = torch.repeat_interleave(torch.arange(nr, device=dev), dl, output_size=total)
+        t = torch.arange(total, device=dev) - optr[:-1][r]
+        ok = t < lens[r]
+        src = torch.where(ok, nip[rows][r] + t, torch.zeros_like(t))
+        base = cbase[r] if cbase is not None else 0
+        ocol.copy_(torch.where(ok, pos[src] - base, torch.zeros_like(t)).to(col_dtype))
+        oval.copy_(torch.where(ok, val[src], torch.zeros((), dtype=torch.float64, device=dev)))
+        return ocol, oval
+    for t_ in (nip, pos, rows, optr) + (() if cbase is None else (cbase,)):
+        assert t_.dtype == torch.int64 and t_.is_cuda and t_.is_contiguous()
+    assert val.dtype == torch.float64 and val.is_contiguous()
+    check(require_game_lib().pml_csr_gather_rows(
+        int(col_dtype == torch.int16), nip.data_ptr(), pos.data_ptr(), val.data_ptr(), rows.data_ptr(), nr,
+        optr.data_ptr(), None if cbase is None else cbase.data_ptr(), ocol.data_ptr(), oval.data_ptr(),
+        stream_handle(dev)), "csr_gather_rows")
+    return ocol, oval
+
+
 def sorted_counts(sorted_keys: torch.Tensor, nbins: int) -> torch.Tensor:
     """Per-bin counts of NON-DECREASING keys in [0, nbins) (bincount without atomics: run boundaries by binary
     search)."""
@@ -771,7 +814,8 @@ SEG_GRAM_DMAX = 160 * 1024 // 8      # seg_gram_kernel's LDS image: one fp64 per
 
 
 def seg_gram(ents: torch.Tensor, n: int, row_ptr: torch.Tensor, col_ptr: torch.Tensor, nip: torch.Tensor,
-             pos: torch.Tensor, val: torch.Tensor) -> torch.Tensor:
+             pos: torch.Tensor, val: torch.Tensor, dmax: Optional[int] = None,
+             maxnnz: Optional[int] = None) -> torch.Tensor:
     """Per-entity Gram matrices ``K [B, n, n]`` (``seg_gram_kernel``) of the entities ``ents`` of a block-diagonal
     CSR (rows grouped by entity: ``row_ptr``; entity column ranges: ``col_ptr``; ``nip/pos/val`` = int64 indptr,
     int64 global columns, fp64 values, distinct columns per row). Entities with fewer than ``n`` rows are zero
@@ -786,12 +830,41 @@ def seg_gram(ents: torch.Tensor, n: int, row_ptr: torch.Tensor, col_ptr: torch.T
     for x in t:
         assert x.dtype == torch.int64
     v = val.to(dev, torch.float64).contiguous()
-    dmax = int((col_ptr[ents + 1] - col_ptr[ents]).max())
+    if dmax is None or maxnnz is None:
+        # widest entity (LDS image) and most non-zeros of one entity (LDS staging of its entries): one readback
+        e_lo, e_hi = row_ptr[ents], row_ptr[ents + 1]
+        dmax, maxnnz = (int(x) for x in torch.stack([(col_ptr[ents + 1] - col_ptr[ents]).max(),
+                                                      (nip[e_hi] - nip[e_lo]).max()]).tolist())
     if dmax > SEG_GRAM_DMAX:
         raise ValueError(f"seg_gram: an entity has {dmax} > {SEG_GRAM_DMAX} projected columns")
-    check(lib.pml_seg_gram(B, n, dmax, t[0].data_ptr(), t[1].data_ptr(), t[2].data_ptr(), t[3].data_ptr(),
+    stage = int(maxnnz) if os.environ.get("PML_SEG_GRAM_STAGE", "1") != "0" else 0
+    check(lib.pml_seg_gram(B, n, dmax, stage, t[0].data_ptr(), t[1].data_ptr(), t[2].data_ptr(), t[3].data_ptr(),
                            t[4].data_ptr(), v.data_ptr(), K.data_ptr(), stream_handle(dev)), "seg_gram")
     return K
+
+
+def batched_cholesky(K: torch.Tensor, nv: torch.Tensor):
+    """In-place lower Cholesky factors of the fp64 batch ``K [B, n, n]`` (n <= 192; ``batched_chol_kernel``, one wave
+    per problem, packed triangle in LDS); rows / columns ``>= nv[b]`` of problem b are treated as the identity.
+    Returns ``(K, info)``: info[b] = 0, or the 1-based column of the first non-positive pivot (that factor is
+    unusable, as with ``torch.linalg.cholesky_ex``)."""
+    B, n, n2 = K.shape
+    assert n == n2 and K.dtype == torch.float64 and K.is_contiguous()
+    info = torch.zeros(B, dtype=torch.int32, device=K.device)
+    if B == 0:
+        return K, info
+    if not K.is_cuda or n > 192:
+        ar = torch.arange(n, device=K.device)
+        pad = ar.unsqueeze(0) >= nv.to(K.device).unsqueeze(1)
+        Kp = torch.where(pad.unsqueeze(1) | pad.unsqueeze(2), torch.zeros((), dtype=K.dtype, device=K.device), K)
+        Kp = Kp + torch.diag_embed(pad.to(K.dtype))
+        L, inf = torch.linalg.cholesky_ex(Kp)
+        K.copy_(L)
+        return K, inf.to(torch.int32)
+    nv = nv.to(K.device, torch.int64).contiguous()
+    check(require_game_lib().pml_batched_chol(B, n, nv.data_ptr(), K.data_ptr(), info.data_ptr(),
+                                              stream_handle(K.device)), "batched_chol")
+    return K, info
 
 
 RS_PRIMAL_DMAX = 64 * 1024 // 8     # rs_primal_kernel: one fp64 LDS slot per projected column of the entity
@@ -890,7 +963,7 @@ def re_lib() -> Optional[ctypes.CDLL]:
         lib.pml_re_tron_smem.argtypes = [c_int]
         lib.pml_re_tron_smem.restype = ctypes.c_size_t
         lib.pml_re_tron_hess.argtypes = lib.pml_re_tron_csr.argtypes
-        lib.pml_re_tron_lean.argtypes = lib.pml_re_tron_csr.argtypes[:-1] + [c_void_p, c_int, c_void_p]
+        lib.pml_re_tron_lean.argtypes = lib.pml_re_tron_csr.argtypes[:-1] + [c_void_p, c_int, c_void_p, c_void_p]
         lib.pml_re_tron_lean.restype = c_int
         lib.pml_re_tron_hess.restype = c_int
         lib.pml_re_tron_hess_smem.argtypes = [c_int]
@@ -925,7 +998,7 @@ RE_LEAN_DMAX = 1024 if os.environ.get("PML_RE_LEAN", "1") != "0" else 0
 def re_tron_csr(order, row_ptr, col_ptr, nip, lcol, val, y, off, wt, scr, W, f, iters, reason, zout, loss_id: int,
                 l2: float, tol: float, max_iter: int, max_fail: int, max_cg: int, dmax: int,
                 npass: Optional[torch.Tensor] = None, hessian: bool = False, gsc: Optional[torch.Tensor] = None,
-                lean: Optional[bool] = None, quad: bool = False) -> None:
+                lean: Optional[bool] = None, quad: bool = False, xf2: Optional[torch.Tensor] = None) -> None:
     """Fused per-entity primal TRON over the entities ``order`` (int32; one workgroup each) of a block-diagonal
     CSR (``re_tron_csr_kernel``). Entity ``e`` owns rows ``row_ptr[e]:row_ptr[e+1]`` (int64) and coefficients
     ``col_ptr[e]:col_ptr[e+1]`` of the packed ``W`` (fp64, in: warm start, out: solution); ``nip`` int64 row
@@ -936,8 +1009,10 @@ def re_tron_csr(order, row_ptr, col_ptr, nip, lcol, val, y, off, wt, scr, W, f, 
     Hessian formed on the fp64 matrix cores, CG on it in LDS). ``lean`` (default: dmax <= 1024): the
     ``re_tron_lean_kernel`` (only the gathered vector + accumulators in LDS) with ``gsc`` (fp64 scratch like ``W``;
     allocated when None); ``quad``: every row of the batch is padded to whole quads of 4 entries (column 0, value
-    0.0), and the lean kernel reads 4 columns / 4 values per lane load (row_pass_q). Device only; in place, nothing
-    returned."""
+    0.0), and the lean kernel reads 4 columns / 4 values per lane load (row_pass_q). ``xf2`` (lean only, optional,
+    fp64 per entity): ``||X_e||_F^2``; a warm start then scales its gradient tolerance by the bound
+    ``||X_e||_F ||c||`` of ``||g(0)||`` and runs the pass at zero only if a gradient norm reaches it. Device only; in
+    place, nothing returned."""
     lib = require_re_lib()
     n_rows = y.numel()
     B = int(order.numel())
@@ -978,7 +1053,10 @@ def re_tron_csr(order, row_ptr, col_ptr, nip, lcol, val, y, off, wt, scr, W, f, 
         if gsc is None:
             gsc = torch.empty_like(W)
         assert gsc.is_cuda and gsc.dtype == torch.float64 and gsc.numel() >= W.numel() and gsc.device == W.device
-        check(lib.pml_re_tron_lean(*args, gsc.data_ptr(), int(bool(quad)), stream_handle(W.device)), "re_tron_lean")
+        if xf2 is not None:
+            assert xf2.is_cuda and xf2.dtype == torch.float64 and xf2.numel() == n_ent and xf2.is_contiguous()
+        check(lib.pml_re_tron_lean(*args, gsc.data_ptr(), int(bool(quad)), None if xf2 is None else xf2.data_ptr(),
+                                   stream_handle(W.device)), "re_tron_lean")
         return
     fn = lib.pml_re_tron_hess if hessian else lib.pml_re_tron_csr
     check(fn(*args, stream_handle(W.device)), "re_tron_csr")

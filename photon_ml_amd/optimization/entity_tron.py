@@ -43,6 +43,9 @@ RES_KMAX = int(os.environ.get("PML_RE_RES_KMAX", "128"))
 
 
 QUAD_MIN_ROW_NNZ = 12      # pad rows to whole quads when the mean row holds >= 12 entries (<= 25 % padding)
+# warm starts bound ||g(0)|| by ||X_e||_F ||c|| instead of a row pass at zero (re_tron_lean_kernel; PML_RE_LAZY_G0=0:
+# always the exact pass)
+LAZY_G0 = os.environ.get("PML_RE_LAZY_G0", "1") != "0"
 
 
 def pad_rows_to_quads(nip: torch.Tensor, lcol: torch.Tensor, val: torch.Tensor):
@@ -142,39 +145,62 @@ class EntityTronBatch:
             check_lds_add_order(dev)                   # row passes accumulate with same-address ds_add_f64
         if self.B == 0:
             return
-        nip, pos, val, row_sel, col_sel, _ = ds.entity_csr(sel)
-        self.rows, self.cols = row_sel, col_sel
         ne, de = n_e[self.ents], d_e[self.ents]
         self.row_ptr = torch.zeros(self.B + 1, dtype=torch.int64, device=dev)
         torch.cumsum(ne, 0, out=self.row_ptr[1:])
         self.col_ptr = torch.zeros(self.B + 1, dtype=torch.int64, device=dev)
         torch.cumsum(de, 0, out=self.col_ptr[1:])
         n_rows = int(self.row_ptr[-1])
+        if dev.type == "cuda":
+            # the batch's rows straight from the parent CSR by one gather kernel (entity-local int16 columns, rows
+            # padded to whole quads when the lean kernel reads quads): no nnz-sized torch index / scatter chain
+            from ..ops.native import csr_gather_rows
+            row_sel, col_sel = ds.entity_rows(sel)
+            pnip, ppos, pval = (t.to(dev) for t in ds._seg_csr)
+            row_nnz = pnip[row_sel + 1] - pnip[row_sel]
+            nnz = int(row_nnz.sum())
+            self.quad = (nnz > 0 and nnz >= QUAD_MIN_ROW_NNZ * n_rows and os.environ.get("PML_RE_QUAD", "1") != "0"
+                         and not bool((de <= HESS_DMAX).any()))
+            plen = (row_nnz + 3) // 4 * 4 if self.quad else row_nnz
+            nip = torch.zeros(n_rows + 1, dtype=torch.int64, device=dev)
+            torch.cumsum(plen, 0, out=nip[1:])
+            cbase = seg.col_ptr[seg.row_entity[row_sel]]               # parent column of the entity's local 0
+            self.lcol, val = csr_gather_rows(pnip, ppos, pval, row_sel, nip, cbase, torch.int16)
+            del cbase, plen
+            if os.environ.get("PML_CHECK_KERNEL_INPUTS", "0") == "1" and nnz:
+                assert int(self.lcol.min()) >= 0 and int(self.lcol.max()) < int(de.max()), "local column range"
+            self.nip, self.val = nip, val
+        else:
+            nip, pos, val, row_sel, col_sel, _ = ds.entity_csr(sel)
+            row_ent = torch.repeat_interleave(torch.arange(self.B, device=dev), ne, output_size=n_rows)
+            row_nnz = nip[1:] - nip[:-1]
+            nnz = int(nip[-1])
+            nnz_ent = torch.repeat_interleave(row_ent, row_nnz, output_size=nnz)
+            lcol = pos - self.col_ptr[nnz_ent]
+            del nnz_ent, pos
+            self.lcol = lcol.to(torch.int16)                 # read as uint16 by the kernel (d_e <= 2048)
+            self.nip, self.val = nip, val
+            # rows padded to whole quads for the lean kernel's 4-entry loads (when rows are long enough that the
+            # padding costs little); the streaming and resident kernels read the padded rows unchanged
+            # (not with tall-narrow launches: re_tron_tall_kernel stages rows by ASSIGNMENT into a dense block,
+            # where a column-0 padding entry could overwrite the real column 0)
+            self.quad = (nnz > 0 and nnz >= QUAD_MIN_ROW_NNZ * n_rows and os.environ.get("PML_RE_QUAD", "1") != "0"
+                         and not bool((de <= HESS_DMAX).any()))
+            if self.quad:
+                self.nip, self.lcol, self.val = pad_rows_to_quads(self.nip, self.lcol, self.val)
+                nip = self.nip
+        self.rows, self.cols = row_sel, col_sel
         row_ent = torch.repeat_interleave(torch.arange(self.B, device=dev), ne, output_size=n_rows)
-        row_nnz = nip[1:] - nip[:-1]
-        nnz = int(nip[-1])
-        nnz_ent = torch.repeat_interleave(row_ent, row_nnz, output_size=nnz)
-        lcol = pos - self.col_ptr[nnz_ent]
-        if os.environ.get("PML_CHECK_KERNEL_INPUTS", "0") == "1" and nnz:
-            # the kernel indexes LDS vectors of d_e entries with these
-            assert int(lcol.min()) >= 0 and bool((lcol < de[nnz_ent]).all()), "entity-local column out of range"
-        del nnz_ent, pos
-        self.lcol = lcol.to(torch.int16)                 # read as uint16 by the kernel (d_e <= 2048)
-        self.nip, self.val = nip, val
-        # rows padded to whole quads for the lean kernel's 4-entry loads (when rows are long enough that the padding
-        # costs little); the streaming and resident kernels read the padded rows unchanged
-        # (not with tall-narrow launches: re_tron_tall_kernel stages rows by ASSIGNMENT into a dense block, where a
-        # column-0 padding entry could overwrite the real column 0)
-        self.quad = (nnz > 0 and nnz >= QUAD_MIN_ROW_NNZ * n_rows and os.environ.get("PML_RE_QUAD", "1") != "0"
-                     and not bool((de <= HESS_DMAX).any()))
-        if self.quad:
-            self.nip, self.lcol, self.val = pad_rows_to_quads(self.nip, self.lcol, self.val)
-            nip = self.nip
         self.y, self.w = seg.y[row_sel].contiguous(), seg.w[row_sel].contiguous()
         self.n_rows = n_rows
         self.nnz = nnz
         self.scr = torch.empty(4 * max(n_rows, 1), dtype=torch.float64, device=dev)
         self.gsc = torch.empty(int(self.col_ptr[-1]), dtype=torch.float64, device=dev)   # lean kernel: gradient
+        # ||X_e||_F^2 per entity (the lean kernel's bound of the zero point's gradient norm on warm starts)
+        self.xf2 = None
+        if LAZY_G0 and dev.type == "cuda":
+            ent_len = self.nip[self.row_ptr[1:]] - self.nip[self.row_ptr[:-1]]
+            self.xf2 = torch.segment_reduce(self.val * self.val, "sum", lengths=ent_len).contiguous()
         # launch classes by LDS size; inside a class the largest entities first (they bound the launch's tail).
         # Entities of at most HESS_DMAX coefficients (tall: the row space took the wide ones) run the exact-Hessian
         # kernel (MFMA), the others the sparse Hessian-vector kernel.
@@ -248,7 +274,7 @@ class EntityTronBatch:
         for dm, order, is_h in self.launches:
             re_tron_csr(order, self.row_ptr, self.col_ptr, self.nip, self.lcol, self.val, self.y, off, self.w,
                         self.scr, W, f, iters, reason, z, loss.loss_id, l2, tol, max_iter, max_fail, max_cg, dm,
-                        hessian=is_h, gsc=self.gsc, quad=self.quad)
+                        hessian=is_h, gsc=self.gsc, quad=self.quad, xf2=self.xf2)
         self.W = W
         # the error flag stays on the device: reading it here would wait for the whole launch before the caller
         # can queue concurrent work (the row-space side stream); callers call FusedResult.check_error() later

@@ -141,36 +141,56 @@ class RowSpaceBatch:
         ne_all = n_e[ents]
         bounds = torch.tensor([b for b in SIZE_CLASSES if b < nmax] + [nmax], device=dev)
         cls_of = torch.searchsorted(bounds, ne_all)                    # smallest bound >= n_e
-        members = [(ents[cls_of == c], ne_all[cls_of == c]) for c in range(bounds.numel())]
-        members = [(e, ne) for e, ne in members if e.numel()]
-        n_max = int(ne_all.max())
+        # class members in entity order: one stable sort by class, the class sizes in one readback, then the
+        # per-class row / width / non-zero maxima in a second one (no boolean selection + sync per class)
+        order = torch.argsort(cls_of, stable=True)
+        ents_s, ne_s = ents[order], ne_all[order]
+        from ..ops.native import sorted_counts
+        cnt = sorted_counts(cls_of[order], bounds.numel()).tolist()
+        de_s = d_e[ents_s]
+        csr = _canonical_csr(csr, dev) if dev.type == "cuda" else None
+        if csr is not None:
+            enz_s = csr[0][seg.row_ptr[ents_s + 1]] - csr[0][seg.row_ptr[ents_s]]
+        spans, lo = [], 0
+        for c in cnt:
+            spans.append((lo, lo + c))
+            lo += c
+        spans = [sp for sp in spans if sp[1] > sp[0]]
+        stats = torch.stack([torch.stack([ne_s[a:b].max(), de_s[a:b].max()] +
+                                         ([enz_s[a:b].max()] if csr is not None else []))
+                             for a, b in spans]).tolist() if spans else []
+        members = [(ents_s[a:b], ne_s[a:b], st) for (a, b), st in zip(spans, stats)]
         N = seg.y.numel()
         geo = []
-        for e, ne in members:
-            n = int(ne.max())
+        for e, ne, st in members:
+            n = int(st[0])
             ar = torch.arange(n, device=dev)
             valid = ar.unsqueeze(0) < ne.unsqueeze(1)                  # [B_c, n]
             rows = torch.where(valid, seg.row_ptr[e].unsqueeze(1) + ar,
                                torch.full_like(valid, -1, dtype=torch.long))
-            geo.append((e, n, valid, rows, torch.zeros(e.numel(), n, n, dtype=torch.float64, device=dev)))
+            geo.append((e, n, valid, rows, None, ne, st))
         gram = trace_range("row-space: Gram matrices")
         gram.__enter__()
-        csr = _canonical_csr(csr, dev) if dev.type == "cuda" else None
         # (class, members) whose Gram columns come from indicator passes: all of them without a canonical device
         # CSR, else only the entities too wide for seg_gram_kernel's LDS image (d_e > SEG_GRAM_DMAX)
         need_ind = []
         if csr is not None:
             # K_e straight from the block-diagonal CSR, one wave per entity (seg_gram_kernel)
             from ..ops.native import SEG_GRAM_DMAX, seg_gram
-            for gi, (e, n, valid, rows, K) in enumerate(geo):
-                ok = d_e[e] <= SEG_GRAM_DMAX
-                if bool(ok.all()):
-                    geo[gi] = (e, n, valid, rows, seg_gram(e, n, seg.row_ptr, seg.col_ptr, *csr))
+            for gi, (e, n, valid, rows, _, ne, st) in enumerate(geo):
+                if int(st[1]) <= SEG_GRAM_DMAX:
+                    geo[gi] = (e, n, valid, rows, seg_gram(e, n, seg.row_ptr, seg.col_ptr, *csr, dmax=int(st[1]),
+                                                            maxnnz=int(st[2])), ne, st)
                     continue
+                ok = d_e[e] <= SEG_GRAM_DMAX
+                K = torch.zeros(e.numel(), n, n, dtype=torch.float64, device=dev)
                 if bool(ok.any()):
                     K[ok] = seg_gram(e[ok], n, seg.row_ptr, seg.col_ptr, *csr)
+                geo[gi] = (e, n, valid, rows, K, ne, st)
                 need_ind.append((gi, torch.nonzero(~ok).squeeze(1)))
         else:
+            geo = [(e, n, valid, rows, torch.zeros(e.numel(), n, n, dtype=torch.float64, device=dev), ne, st)
+                   for e, n, valid, rows, _, ne, st in geo]
             need_ind = [(gi, None) for gi in range(len(geo))]
         n_max = max((geo[gi][1] for gi, _ in need_ind), default=0)
         ind = torch.zeros(N, dtype=torch.float64, device=dev) if n_max else None
@@ -178,14 +198,14 @@ class RowSpaceBatch:
             # column j of every K_e at once: indicator on row j of every such entity with n_e > j
             ind.zero_()
             for gi, sel in need_ind:
-                _, n, valid, rows, _K = geo[gi]
+                _, n, valid, rows, *_r = geo[gi]
                 if j < n:
                     v, r = (valid, rows) if sel is None else (valid[sel], rows[sel])
                     ind[r[v[:, j], j]] = 1.0
             u = seg.glm.rmatvec(ind, build_multi=False)                # every entity's row j, at its own columns
             z = seg.glm.matvec(u)                      # (X_e X_e^T)[:, j] on the entity's rows
             for gi, sel in need_ind:
-                _, n, valid, rows, K = geo[gi]
+                _, n, valid, rows, K, *_r = geo[gi]
                 if j < n:
                     v, r = (valid, rows) if sel is None else (valid[sel], rows[sel])
                     col = torch.where(v, z[r.clamp(min=0)], torch.zeros((), dtype=torch.float64, device=dev))
@@ -196,18 +216,23 @@ class RowSpaceBatch:
             del u, z
         del ind
         gram.__exit__(None, None, None)
+        # factors: one batched Cholesky launch per class (padding slots = identity); the pivots of every class are
+        # checked with ONE readback, and only a class with a failed factor pays a boolean selection
+        from ..ops.native import batched_cholesky
+        infos = []
+        for gi, (e, n, valid, rows, K, ne, st) in enumerate(geo):
+            with trace_range(f"row-space: Cholesky n={n}"):
+                _, info = batched_cholesky(K, ne)
+            infos.append(info)
+        all_ok = torch.stack([(i == 0).all() for i in infos]).tolist() if infos else []
         off = 0
         kept = []
-        for e, n, valid, rows, K in geo:
-            # entities of other classes / the primal path also received u components (rows never mix)
-            K += torch.diag_embed((~valid).to(torch.float64))
-            with trace_range(f"row-space: Cholesky n={n}"):
-                L, info = torch.linalg.cholesky_ex(K)
-            del K
-            ok = info == 0
-            if not bool(ok.any()):
-                continue
-            L, rows, valid, e = L[ok].contiguous(), rows[ok], valid[ok], e[ok]
+        for (e, n, valid, rows, L, ne, st), info, good in zip(geo, infos, all_ok):
+            if not good:
+                ok = info == 0
+                if not bool(ok.any()):
+                    continue
+                L, rows, valid, e = L[ok].contiguous(), rows[ok], valid[ok], e[ok]
             zero = torch.zeros((), dtype=torch.float64, device=dev)
             w = torch.where(valid, seg.w[rows.clamp(min=0)], zero)
             y = torch.where(valid, seg.y[rows.clamp(min=0)], zero)
@@ -215,6 +240,7 @@ class RowSpaceBatch:
             off += c.B * n
             self.classes.append(c)
             kept.append(e)
+        del geo
         self.ents = torch.cat(kept) if kept else ents[:0]
         self.B = int(self.ents.numel())
         self.n = max((c.n for c in self.classes), default=0)
@@ -243,8 +269,10 @@ class RowSpaceBatch:
         # the primal model (to_primal: one transpose pass over the block-diagonal data) is read once per model:
         # build its shard-wide one-launch transpose tables here, with the rest of the setup, instead of running
         # one launch per row chunk at every read (24 launches, 20.7 ms at config 5 vs one launch)
+        # (not needed when the per-entity back-map covers every handled entity: rs_primal reads the compact copy)
         glm = getattr(seg, "glm", None)
-        if glm is not None and getattr(glm, "_multi_t", "unset") == "unset" and hasattr(glm, "_build_multi_t"):
+        if (self._primal_csr is None and glm is not None and getattr(glm, "_multi_t", "unset") == "unset"
+                and hasattr(glm, "_build_multi_t")):
             glm._build_multi_t()
 
     def _compact_csr(self, csr):
@@ -272,15 +300,15 @@ class RowSpaceBatch:
         nk = nip[rows + 1] - k0
         nip_c = torch.zeros(nr + 1, dtype=torch.int64, device=dev)
         torch.cumsum(nk, 0, out=nip_c[1:])
-        nnz = int(nip_c[-1])
-        ent_idx = torch.repeat_interleave(k0 - nip_c[:-1], nk, output_size=nnz) + torch.arange(nnz, device=dev)
+        from ..ops.native import csr_gather_rows
+        pos_c, val_c = csr_gather_rows(nip, pos, val, rows, nip_c)       # one gather kernel over the rows
         row_ptr = torch.stack([rcum[:-1], rcum[1:]], 1).reshape(-1)
         col_ptr = torch.stack([c_lo, c_hi], 1).reshape(-1)
         # trailing entries: the wrapper's range checks read the last element as the total
         row_ptr = torch.cat([row_ptr, rcum[-1:]])
         col_ptr = torch.cat([col_ptr, seg.col_ptr[-1:]])
         ents2 = torch.arange(self.B, dtype=torch.int64, device=dev) * 2
-        return ents2, row_ptr, col_ptr, nip_c, pos[ent_idx], val[ent_idx], rows
+        return ents2, row_ptr, col_ptr, nip_c, pos_c, val_c, rows
 
     def _slots(self, per_row: torch.Tensor) -> torch.Tensor:
         """Packed per-slot values of a per-row vector (0 in padding slots, whose row index is -1)."""
@@ -371,7 +399,8 @@ class RowSpaceBatch:
             for st in self._streams:
                 st.wait_stream(main)                       # warm starts / offsets written on the caller's stream
                 for t in (beta, beta0, o, zs):
-                    t.record_stream(st)
+                    if t is not None:          # zs: None off the fused path; beta0 may alias beta
+                        t.record_stream(st)
             load = [0] * len(streams)
             lane = {}
             for ci in sorted(range(len(self.classes)), key=lambda i: -self.classes[i].B * self.classes[i].n ** 2):

@@ -15,23 +15,28 @@ def main(db, sub, index="0"):
     rv = next(v for v in ("regions", "markers", "region") if v in views)
     av = next((v for v in ("regions_and_samples", "hip_api", "api") if v in views), None)
     rc = cols(rv)
-    rn = next(x for x in ("name", "message") if x in rc)
-    probe = list(c.execute(f"select * from {rv} limit 500"))
-    for i, x in enumerate(rc):
-        vals = {r[i] for r in probe if isinstance(r[i], str)}
-        if len(vals) > 1 and any(" " in v for v in vals):
-            rn = x
-            break
-    regs = list(c.execute(f"select {rn}, start, end from {rv} order by start"))
-    sel = [r for r in regs if sub in (r[0] or "")]
-    if not sel:
-        print("no region", sub)
+    textcols = [x for x in rc if x not in ("start", "end")]
+    # the roctx message column: the text column whose values contain the region substring
+    msg = None
+    for x in textcols:
+        try:
+            if c.execute(f"select count(*) from {rv} where {x} like ?", (f"%{sub}%",)).fetchone()[0]:
+                msg = x
+                break
+        except sqlite3.Error:
+            continue
+    if msg is None:
+        print("no region", sub, "; region columns:", rc)
+        print(list(c.execute(f"select * from {rv} limit 5")))
         return
+    api_name = "name" if "name" in rc else msg
+    sel = list(c.execute(f"select {msg}, start, end from {rv} where {msg} like ? order by start", (f"%{sub}%",)))
+    regs = list(c.execute(f"select {api_name}, start, end from {rv} order by start"))
     name, t0, t1 = sel[int(index)]
     # every region row in the window whose name is not a roctx message is an API call
     api = defaultdict(lambda: [0, 0, 0])
     for n, s, e in regs:
-        if s >= t0 and e <= t1 and n and not n.startswith("{"):
+        if s >= t0 and e <= t1 and n and not n.startswith("{") and not n.startswith("roctx"):
             k = re.sub(r"\(.*$", "", n)[:60]
             api[k][0] += 1
             api[k][1] += e - s

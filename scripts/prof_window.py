@@ -45,6 +45,14 @@ def main(db, sub, out=None):
         print("region columns:", rc)
         for r in probe[:3]:
             print(r)
+    # with API tracing the first rows are HIP calls: take the text column that actually holds the region name
+    for x in textcols:
+        try:
+            if c.execute(f"select count(*) from {rv} where {x} like ?", (f"%{sub}%",)).fetchone()[0]:
+                rn = x
+                break
+        except sqlite3.Error:
+            continue
     regs = list(c.execute(f"select {rn}, {rs}, {re_} from {rv} order by {rs}"))
     sel = [r for r in regs if sub in (r[0] or "")]
     if not sel:

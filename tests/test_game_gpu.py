@@ -190,10 +190,11 @@ def test_random_effect_build_on_gpu_matches_host(cap, passive, ratio, monkeypatc
     assert np.array_equal(xa.indptr, xb.indptr) and np.array_equal(xa.indices, xb.indices)
 
 
-def test_row_space_gram_kernel_matches_indicator_passes():
+def test_row_space_gram_kernel_matches_indicator_passes(monkeypatch):
     """seg_gram_kernel (K_e from the block-diagonal CSR, one wave per entity) == the Gram columns formed by
     indicator passes through the transpose and forward GLM kernels, per size class; the solve on either set of
     factors gives the same model."""
+    monkeypatch.setattr("photon_ml_amd.algorithm.coordinates.EAGER_SETUP", False)   # keeps the raw CSR
     from photon_ml_amd.algorithm.coordinates import RandomEffectCoordinate
     from photon_ml_amd.optimization.row_space import RowSpaceBatch
     data, _ = generate_game_data(n_rows=6000, n_users=400, d_user=40, seed=24, task="LOGISTIC_REGRESSION")
@@ -215,9 +216,10 @@ def test_row_space_gram_kernel_matches_indicator_passes():
     torch.testing.assert_close(a.to_primal(ra.W), b.to_primal(rb.W), rtol=1e-6, atol=1e-8)
 
 
-def test_seg_gram_rows_per_round_bitwise():
+def test_seg_gram_rows_per_round_bitwise(monkeypatch):
     """seg_gram_kernel with 1, 2, 4 or 8 rows per scatter round (interleaved image slots, one walk of row j per
     round): the same fma sequence per K entry, so K is bitwise equal for every S."""
+    monkeypatch.setattr("photon_ml_amd.algorithm.coordinates.EAGER_SETUP", False)   # keeps the raw CSR
     from photon_ml_amd.algorithm.coordinates import RandomEffectCoordinate
     from photon_ml_amd.ops.native import require_game_lib, seg_gram
     from photon_ml_amd.optimization.row_space import _canonical_csr
@@ -233,15 +235,47 @@ def test_seg_gram_rows_per_round_bitwise():
     n = int(n_e[ents].max())
     lib = require_game_lib()
     outs = []
+    import os
     try:
         for S in (1, 2, 4, 8):
             lib.pml_seg_gram_set_s(S)
-            outs.append(seg_gram(ents, n, seg.row_ptr, seg.col_ptr, *csr))
+            for stage in ("0", "1"):     # entries read from global memory / staged in LDS first
+                os.environ["PML_SEG_GRAM_STAGE"] = stage
+                outs.append(seg_gram(ents, n, seg.row_ptr, seg.col_ptr, *csr))
     finally:
         lib.pml_seg_gram_set_s(0)
+        os.environ.pop("PML_SEG_GRAM_STAGE", None)
     for K in outs[1:]:
         assert torch.equal(K, outs[0])
     assert float(outs[0].abs().sum()) > 0
+
+
+@pytest.mark.parametrize("n", [1, 5, 8, 33, 64, 130])
+def test_batched_cholesky_kernel(n):
+    """batched_chol_kernel == torch.linalg.cholesky (fp64, 1e-12) on SPD Gram matrices with padding slots
+    (rows >= nv[b] become the identity); a non-positive pivot is reported in info like LAPACK."""
+    from photon_ml_amd.ops.native import batched_cholesky
+    g = torch.Generator().manual_seed(n)
+    B = 300
+    X = torch.randn(B, n, n + 7, generator=g, dtype=torch.float64)
+    K = X @ X.transpose(1, 2)
+    nv = torch.randint(1, n + 1, (B,), generator=g)
+    nv[0] = n
+    ar = torch.arange(n)
+    pad = ar.unsqueeze(0) >= nv.unsqueeze(1)
+    Kp = torch.where(pad.unsqueeze(1) | pad.unsqueeze(2), torch.zeros(()), K) + torch.diag_embed(pad.double())
+    ref = torch.linalg.cholesky(Kp)
+    Kd = K.cuda().contiguous()
+    if n > 1:
+        Kd[1, 1, 1] = -1.0                      # not positive definite at column 2 (nv[1] may exclude it)
+    L, info = batched_cholesky(Kd, nv.cuda())
+    L, info = L.cpu(), info.cpu()
+    keep = torch.ones(B, dtype=torch.bool)
+    if n > 1:
+        keep[1] = False
+        assert int(info[1]) == (2 if int(nv[1]) >= 2 else 0)
+    assert int(info[keep].abs().sum()) == 0
+    torch.testing.assert_close(L[keep], ref[keep], rtol=1e-12, atol=1e-12)
 
 
 @pytest.mark.parametrize("row_space", ["0", "1"])
@@ -334,10 +368,11 @@ def test_fused_entity_tron_deterministic_and_matches_cpu(monkeypatch):
                                    rtol=1e-5, atol=1e-6)
 
 
-def test_row_space_gram_wide_entity_falls_back_to_indicator_passes():
+def test_row_space_gram_wide_entity_falls_back_to_indicator_passes(monkeypatch):
     """An entity with few rows but more projected columns than seg_gram_kernel's LDS image (d_e > SEG_GRAM_DMAX)
     gets its Gram columns from indicator passes; the other entities of its size class still use the kernel, and
     the factors match the all-indicator build."""
+    monkeypatch.setattr("photon_ml_amd.algorithm.coordinates.EAGER_SETUP", False)   # keeps the raw CSR
     import scipy.sparse as sp
     from photon_ml_amd.algorithm.coordinates import RandomEffectCoordinate
     from photon_ml_amd.data.game_data import GameData

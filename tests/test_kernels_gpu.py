@@ -206,7 +206,7 @@ def test_segdot_long_segments():
         ref = segdot(a, b, ptr, mode)
         pc = ptr.cuda()
         got = segdot(a.cuda(), b.cuda(), pc, mode)
-        assert pc._pml_maxlen > SEGDOT_CHUNK
+        assert pc._pml_maxlen[1] > SEGDOT_CHUNK and pc._pml_maxlen[0] == pc._version
         torch.testing.assert_close(got.cpu(), ref, rtol=1e-11, atol=1e-9)
         assert torch.equal(got, segdot(a.cuda(), b.cuda(), pc, mode))
 
@@ -998,3 +998,27 @@ def test_key_histogram_matches_bincount(dtype):
     assert torch.equal(sorted_counts(s, nb).cpu(), ref)
     with pytest.raises(ValueError):
         key_histogram(torch.tensor([0, nb], device="cuda"), nb)
+
+
+@pytest.mark.parametrize("col_dtype", [torch.int16, torch.int64])
+def test_csr_gather_rows_matches_torch(col_dtype):
+    """csr_gather_rows_kernel (row gather + quad padding + entity-local columns) == the torch reference path."""
+    from photon_ml_amd.ops.native import csr_gather_rows
+    g = torch.Generator().manual_seed(5)
+    R = 5000
+    lens = torch.randint(0, 90, (R,), generator=g)
+    nip = torch.zeros(R + 1, dtype=torch.int64)
+    torch.cumsum(lens, 0, out=nip[1:])
+    nnz = int(nip[-1])
+    pos = torch.randint(0, 30000, (nnz,), generator=g)
+    val = torch.randn(nnz, generator=g, dtype=torch.float64)
+    rows = torch.sort(torch.randperm(R, generator=g)[:3000]).values
+    rl = lens[rows]
+    plen = (rl + 3) // 4 * 4
+    optr = torch.zeros(rows.numel() + 1, dtype=torch.int64)
+    torch.cumsum(plen, 0, out=optr[1:])
+    cbase = torch.randint(0, 28000, (rows.numel(),), generator=g) if col_dtype == torch.int16 else None
+    ref = csr_gather_rows(nip, pos, val, rows, optr, cbase, col_dtype)
+    cu = lambda t: None if t is None else t.cuda()
+    got = csr_gather_rows(cu(nip), cu(pos), cu(val), cu(rows), cu(optr), cu(cbase), col_dtype)
+    assert torch.equal(got[0].cpu(), ref[0]) and torch.equal(got[1].cpu(), ref[1])
