@@ -326,7 +326,10 @@ def game_extra(dev, rank: int, world: int) -> dict:
         finally:
             gc.collect()
             torch.cuda.empty_cache()
-        out.update({f"{pre}_sweeps_per_sec": g["value"], f"{pre}_ms_per_sweep": g["ms_per_step"],
+        out.update({f"{pre}_runtime_warmup_s": round(g["runtime_warmup_s"], 3),
+                    f"{pre}_coordinate_build_s": round(g["coordinate_build_s"], 3),
+                    f"{pre}_one_shot_s": round(g["one_shot_s"], 3),
+                    f"{pre}_sweeps_per_sec": g["value"], f"{pre}_ms_per_sweep": g["ms_per_step"],
                     f"{pre}_sweep_ms_min": g["sweep_ms_min"], f"{pre}_sweep_ms_median": g["sweep_ms_median"],
                     f"{pre}_coordinate_ms": g["coordinate_ms"],
                     f"{pre}_cold_first_sweep_ms": g.get("cold_first_sweep_ms"),
@@ -340,9 +343,7 @@ def game_extra(dev, rank: int, world: int) -> dict:
         if prec == "bf16":
             out["game5pl_config"] = dict(g["config"], fe_dtype=g["dtype"], re_dtype="fp64", steps=g["steps"],
                                          warmup=g["warmup"], data_generation_s=round(g["data_generation_s"], 1),
-                                         coordinate_build_s=round(g["coordinate_build_s"], 1))
-        else:
-            out["game5pl_f64_coordinate_build_s"] = round(g["coordinate_build_s"], 1)
+                                         coordinate_build_s=round(g["coordinate_build_s"], 3))
     return out
 
 

@@ -200,6 +200,10 @@ def run(args, dev, rank: int = 0, world: int = 1, data=None, t_data: float = 0.0
             torch.cuda.synchronize()
         t_place = all_reduce_scalar(time.time() - tp, "max")
         log(f"rows placed on their entity owners in {t_place:.1f}s ({data.placement.rows_moved} rows moved)")
+    # the process's first kernel launches (code-object loads, rocBLAS handle, stream creation): measured on their own
+    # (ops/warmup.py), so neither the build nor the cold sweep absorbs them; 0.0 when an earlier run paid them
+    from photon_ml_amd.ops.warmup import runtime_warmup
+    t_warm = all_reduce_scalar(runtime_warmup(dev), "max")
     t0 = time.time()
     fe_cfg = GLMOptimizationConfiguration(OptimizerConfig("LBFGS", args.fe_iters, 1e-12),
                                           RegularizationContext("L2"), 1.0, args.fe_down_sampling_rate)
@@ -319,7 +323,11 @@ def run(args, dev, rank: int = 0, world: int = 1, data=None, t_data: float = 0.0
         "coordinate_ms": coord_ms,
         "examples_per_sec": total_rows * args.steps / elapsed,
         "data_generation_s": t_data,
+        "runtime_warmup_s": t_warm,
         "coordinate_build_s": t_build,
+        # what a one-shot (reference-default, one coordinate-descent iteration) run costs after its data is loaded:
+        # warm-up + coordinate build + the cold first sweep
+        "one_shot_s": t_warm + t_build + (cold_ms or 0.0) / 1000.0,
         **({"route_s": route_s} if route_s else {}),
         **({"placement_s": t_place} if t_place is not None else {}),
         **({"re_solver_routing": routing} if routing else {}),

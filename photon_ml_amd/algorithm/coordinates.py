@@ -264,7 +264,16 @@ class RandomEffectCoordinate(Coordinate):
             cfg = self.opt_config
             reg, lam = cfg.regularization_context, cfg.regularization_weight
             with phase(f"RE {coordinate_id} build: solver components"):
-                self._components(reg.l1_weight(lam), cfg.optimizer_config)
+                comps = self._components(reg.l1_weight(lam), cfg.optimizer_config)
+                if comps is not None and os.environ.get("PML_RE_OVERLAP", "1") != "0":
+                    # the side streams of the concurrent row-space / pass-path solves (creating a prioritised stream
+                    # is ~16 ms on first use): made with the components, not inside the first update
+                    if comps[0] is not None and comps[1] is not None:
+                        self._side_stream = torch.cuda.Stream(
+                            self.device, priority=int(os.environ.get("PML_RE_SIDE_PRIORITY", "0")))
+                    if comps[2] is not None and comps[1] is not None:
+                        self._sub_stream = torch.cuda.Stream(
+                            self.device, priority=int(os.environ.get("PML_RE_SUB_PRIORITY", "-1")))
 
     # The tracker statistics of the last update (random_effect_tracker_stats) are reduced on first read: the masked
     # selection of active entities and the dozen small reductions behind them (a stream synchronisation) stay off

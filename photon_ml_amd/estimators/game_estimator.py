@@ -150,6 +150,11 @@ class GameEstimator:
         return seq
 
     def _build_coordinates(self, data: GameData, first_cfg: Dict[str, GLMOptimizationConfiguration], seq):
+        from ..ops.warmup import runtime_warmup
+        from ..utils.timing import Timed
+        dev = self.device if self.device is not None else default_device()
+        with Timed("Device runtime warm-up (first kernel launches of the process)"):
+            self.runtime_warmup_s = runtime_warmup(dev)
         coords = OrderedDict()
         for cid in seq:
             dc = self.coordinate_data_configurations[cid]

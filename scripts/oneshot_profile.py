@@ -56,13 +56,13 @@ def main():
                 pstats.Stats(prof, stream=f).sort_stats(a.cprofile_sort).print_stats(80)
         phases = {k: round(1000.0 * sum(v), 2) for k, v in TIMELINE.items()}
         counts = {k: len(v) for k, v in TIMELINE.items()}
-        run = {"coordinate_build_s": round(rec["coordinate_build_s"], 3),
+        run = {"runtime_warmup_s": round(rec["runtime_warmup_s"], 3), "coordinate_build_s": round(rec["coordinate_build_s"], 3),
                "cold_first_sweep_ms": round(rec["cold_first_sweep_ms"], 2),
                "cold_first_sweep_coordinate_ms": {k: round(v, 2) for k, v in rec["cold_first_sweep_coordinate_ms"].items()},
                "warm_sweep_ms": round(rec["ms_per_step"], 2), "phases_ms": phases, "phase_counts": counts}
         out["runs"][prec] = run
         print(f"\n## {a.config}, fixed-effect features {prec} (run {i + 1} of the process)\n")
-        print(f"coordinate build {run['coordinate_build_s']:.3f} s, cold first sweep {run['cold_first_sweep_ms']:.1f} ms "
+        print(f"runtime warm-up {run['runtime_warmup_s']:.3f} s, coordinate build {run['coordinate_build_s']:.3f} s, cold first sweep {run['cold_first_sweep_ms']:.1f} ms "
               f"{run['cold_first_sweep_coordinate_ms']}, warm sweep {run['warm_sweep_ms']:.1f} ms\n")
         print("| phase | calls | ms |\n|---|---:|---:|")
         for k, v in phases.items():
