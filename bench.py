@@ -78,7 +78,7 @@ def main():
                     help="after the headline (and GAME), also time BASELINE.json configs 3 (OWL-QN, 10M features) and "
                          "4 (Poisson TRON) at fp64 feature storage (the reference's precision; rows reduced to what "
                          "fits in HBM, stated in the keys) and bf16, reported as extra keys; auto = on for the lbfgs "
-                         "config on one rank")
+                         "config at its full size on one rank")
     ap.add_argument("--rehearsal", action="store_true",
                     help="allow more ranks than physical devices (several ranks per GPU, or CPU ranks); the record "
                          "then says rehearsal: true, and n_gpus counts devices, not ranks")
@@ -122,7 +122,9 @@ def main():
     if args.game == "on" or (args.game == "auto" and args.config == "lbfgs"):
         game = game_extra(dev, rank, world)
     cfgx = None
-    if args.configs_extra == "on" or (args.configs_extra == "auto" and args.config == "lbfgs" and world == 1):
+    full_size = args.rows_per_gpu == cfg["rows_per_gpu"] and args.features == cfg["features"]
+    if args.configs_extra == "on" or (args.configs_extra == "auto" and args.config == "lbfgs" and world == 1
+                                      and full_size):
         cfgx = configs_extra(dev, rank, world, args)
     if rank == 0:
         log(f"final f={st.loss:.6e} |g|={gnorm:.3e} evals/step={passes / args.steps:.2f} "

@@ -24,6 +24,7 @@ import torch
 from ..constants import EPSILON, TaskType
 from ..utils.timing import Timed, phase
 from ..data.game_data import GameData
+from ..data.matrix import DeviceCSR
 from ..data.random_effect import FixedEffectDataConfiguration, RandomEffectDataConfiguration, RandomEffectDataset
 from ..function.losses import loss_for_task
 from ..models.game import FixedEffectModel, RandomEffectModel
@@ -111,6 +112,12 @@ class FixedEffectCoordinate(Coordinate):
         with phase(f"FE {coordinate_id} build: device layout"):
             self.glm_data = make_glm_data(labeled, self.device, precision)
         gd = self.glm_data
+        x = data.shards.get(self.shard_id)
+        if (isinstance(x, DeviceCSR) and x.data.is_cuda and hasattr(gd, "_build_multi")
+                and os.environ.get("PML_FE_OFFLOAD_SHARD", "1") != "0"):
+            # rows placed / routed to this rank arrive as a device CSR; the tiled layout now holds them, so the CSR
+            # goes to host memory instead of doubling the shard's HBM footprint for the whole fit
+            x.offload_to_host()
         if EAGER_SETUP and hasattr(gd, "_build_multi"):
             # every pass of every update uses the shard-wide launch tables: build them with the layout (one-time data
             # setup), not inside the first update

@@ -40,6 +40,13 @@ class DeviceCSR:
     def tocsr(self):
         return self
 
+    def offload_to_host(self) -> None:
+        """Move the arrays to host memory in place (same object, CPU tensors): for a shard whose device layout has
+        been built elsewhere (the fixed effect's tiled DeviceGLMData), so the routed copy does not double its HBM
+        footprint for the rest of the fit. Later device consumers ``.to(device)`` it again."""
+        self.indptr, self.indices, self.data = self.indptr.cpu(), self.indices.cpu(), self.data.cpu()
+        self._pml_dev_cache = {}
+
     def to_scipy(self) -> sp.csr_matrix:
         m = sp.csr_matrix((self.data.cpu().numpy(), self.indices.cpu().numpy().astype(np.int32, copy=False),
                            self.indptr.cpu().numpy()), shape=self.shape)

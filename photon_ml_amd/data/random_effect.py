@@ -449,7 +449,15 @@ class RandomEffectDataset:
             pk = torch.from_numpy(ent[passive_rows][cp.row].astype(np.int64) * D + cp.col.astype(np.int64))
             allk = torch.cat([key, pk.to(dev)])
         ukeys = torch.unique(allk, sorted=True)
+        n_keys_in = int(allk.numel())
         del allk
+        # cheap integrity checks of the device build (first / last key, no more keys than entries): a corrupt
+        # projection would send every later per-entity gather out of bounds on the device
+        if ukeys.numel():
+            lo_k, hi_k = (int(v) for v in torch.stack([ukeys[0], ukeys[-1]]).tolist())
+            if lo_k < 0 or hi_k >= n_ent * D or ukeys.numel() > n_keys_in:
+                raise RuntimeError(f"random-effect projection keys out of range: [{lo_k}, {hi_k}] for {n_ent} "
+                                   f"entities x {D} features, {ukeys.numel()} keys from {n_keys_in} entries")
         self.projection = IndexMapProjection.from_sorted_keys(ukeys, n_ent, D)
         pos = torch.searchsorted(ukeys, key)
         del key
@@ -533,6 +541,10 @@ class RandomEffectDataset:
         callers gather the rows' entries themselves (``ops.native.csr_gather_rows``)."""
         seg = self.seg
         mask = mask.to(seg.y.device)
+        if os.environ.get("PML_CHECK_KERNEL_INPUTS", "0") == "1":
+            for name, t in (("row", seg.row_entity), ("column", seg.col_entity)):
+                if t.numel() and (int(t.min()) < 0 or int(t.max()) >= mask.numel()):
+                    raise RuntimeError(f"{name} entity index out of range [0, {mask.numel()})")
         return torch.nonzero(mask[seg.row_entity]).squeeze(1), torch.nonzero(mask[seg.col_entity]).squeeze(1)
 
     def release_csr(self):

@@ -15,6 +15,7 @@ shuffles. Entity ownership is computed identically on every rank from all-gather
 from __future__ import annotations
 
 import heapq
+import os
 import time
 from typing import List, Optional, Sequence, Tuple
 
@@ -190,6 +191,10 @@ class _PhaseClock:
         self.t = now
 
 
+# largest RCCL all-to-all per call and rank (see RowRouter._a2a_device)
+A2A_MAX_BYTES = int(os.environ.get("PML_A2A_MAX_BYTES", str(1 << 30)))
+
+
 class RowRouter:
     """Fixed permutation between this rank's sample rows and the rows it owns after routing by ``dest``.
 
@@ -256,11 +261,10 @@ class RowRouter:
     def _a2a(self, send: torch.Tensor, sc: List[int], rc: List[int]):
         dev = comm_device(self.group)
         tail = tuple(send.shape[1:])
-        if dev.type == "cuda" or len(sc) == 1:
-            # RCCL: one collective over device buffers (the self segment is a device-local copy inside it)
-            out = torch.empty((sum(rc),) + tail, dtype=send.dtype, device=dev)
-            dist.all_to_all_single(out, send.to(dev).contiguous(), rc, sc, group=self.group)
-            return out.to(send.device), rc
+        if dev.type == "cuda":
+            return self._a2a_device(send.to(dev).contiguous(), sc, rc, tail).to(send.device), rc
+        if len(sc) == 1:
+            return send, rc                 # one host-staged rank: the self segment is the whole buffer
         # host-staged backend (gloo): the segment this rank keeps never leaves its device; only the others
         # are staged through the host and exchanged
         me = _rank()
@@ -273,6 +277,39 @@ class RowRouter:
         dist.all_to_all_single(got, send2, rc2, sc2, group=self.group)
         got = got.to(send.device)
         return torch.cat([got[:ro], keep, got[ro:]]), rc
+
+    def _a2a_device(self, send: torch.Tensor, sc: List[int], rc: List[int], tail) -> torch.Tensor:
+        """RCCL all-to-all of device buffers in rounds of at most ``A2A_MAX_BYTES`` per rank: a single
+        ``all_to_all_single`` over a multi-GB buffer (the 1.2G-entry random-effect shard of GAME config 5 is 5-10 GB
+        per array) was measured to leave the tail of the output unwritten (a one-rank RCCL group, round 6:
+        ``profiles/rccl_a2a_chunking_r6.md``). Every rank runs the same number of rounds (one max all-reduce);
+        in round k each peer segment contributes its k-th of that many equal slices, so sender and receiver agree
+        on every slice size from the segment length alone."""
+        from .dist import all_reduce_scalar
+        row_bytes = send.element_size() * int(np.prod(tail)) if tail else send.element_size()
+        out = torch.empty((sum(rc),) + tuple(tail), dtype=send.dtype, device=send.device)
+        need = max(sum(sc), sum(rc)) * row_bytes
+        rounds = int(all_reduce_scalar(float(-(-need // A2A_MAX_BYTES)), "max", group=self.group))
+        if rounds <= 1:
+            dist.all_to_all_single(out, send, rc, sc, group=self.group)
+            return out
+
+        def slices(counts, k):
+            offs = np.concatenate([[0], np.cumsum(counts)])
+            cs = [-(-c // rounds) for c in counts]
+            return [(int(offs[p] + min(k * cs[p], counts[p])), int(offs[p] + min((k + 1) * cs[p], counts[p])))
+                    for p in range(len(counts))]
+        for k in range(rounds):
+            ss, rs = slices(sc, k), slices(rc, k)
+            part = torch.cat([send[a:b] for a, b in ss]) if ss else send[:0]
+            got = torch.empty((sum(b - a for a, b in rs),) + tuple(tail), dtype=send.dtype, device=send.device)
+            dist.all_to_all_single(got, part, [b - a for a, b in rs], [b - a for a, b in ss], group=self.group)
+            o = 0
+            for a, b in rs:
+                out[a:b] = got[o:o + b - a]
+                o += b - a
+            del part, got
+        return out
 
     def forward_csr(self, x: sp.csr_matrix) -> sp.csr_matrix:
         """Route sparse rows: one all-to-all each for row lengths, column indices and values. The entry

@@ -188,6 +188,33 @@ def fsdp_worker(rank, world, port, out):
     dist.destroy_process_group()
 
 
+def a2a_worker(rank, world, port, out):
+    """RowRouter._a2a_device in several rounds (tiny A2A_MAX_BYTES) == one all-to-all, for uneven segments
+    (including empty ones) and a 2-d payload."""
+    _init(rank, world, port)
+    import torch.distributed as dist
+    from photon_ml_amd.parallel import sharding
+    from photon_ml_amd.parallel.sharding import RowRouter
+    rng = np.random.default_rng(100 + rank)
+    sc = [int(v) for v in rng.integers(0, 40, world)]
+    sc[(rank + 1) % world] = 0                                   # an empty segment
+    rc_t = torch.tensor(sc, dtype=torch.int64)
+    allc = [torch.zeros(world, dtype=torch.int64) for _ in range(world)]
+    dist.all_gather(allc, rc_t)
+    rc = [int(allc[q][rank]) for q in range(world)]
+    send = torch.arange(sum(sc) * 3, dtype=torch.float64).reshape(-1, 3) + 1000 * rank
+    ref = torch.empty((sum(rc), 3), dtype=torch.float64)
+    dist.all_to_all_single(ref, send, rc, sc)
+    router = RowRouter.__new__(RowRouter)
+    router.group = None
+    for limit in (8, 50, 1 << 30):
+        sharding.A2A_MAX_BYTES = limit
+        got = router._a2a_device(send, sc, rc, (3,))
+        assert torch.equal(got, ref), (rank, limit)
+    np.save(f"{out}/a2a_r{rank}.npy", np.array([1]))
+    dist.destroy_process_group()
+
+
 def sparse_re_data():
     """GAME data with a third random-effect type of only TWO entities (``regionId``): at world 4 / 8 most ranks own
     no entity of it (empty local problems, empty routing sends, empty model parts)."""
@@ -241,5 +268,5 @@ def sparse_re_worker(rank, world, port, out):
 
 if __name__ == "__main__":
     fn = {"glm": glm_worker, "game": game_worker, "sharding": sharding_worker, "fsdp": fsdp_worker,
-          "placed": placed_worker, "sparse_re": sparse_re_worker}[sys.argv[1]]
+          "placed": placed_worker, "sparse_re": sparse_re_worker, "a2a": a2a_worker}[sys.argv[1]]
     fn(int(sys.argv[2]), int(sys.argv[3]), int(sys.argv[4]), sys.argv[5])

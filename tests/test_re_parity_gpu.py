@@ -170,3 +170,37 @@ def test_production_re_kernel_matches_cpu_tron_fp64(case, monkeypatch):
         assert its3[e] == it_ref, (case, "warm converged", e, its3[e], it_ref)
         err = np.abs(W3[e] - w_ref).max() / max(np.abs(w_ref).max(), 1e-300)
         assert err < 1e-6, (case, "warm converged", e, err)
+
+
+def test_dense_bucket_quad_rows_longer_than_64_match_cpu_tron(monkeypatch):
+    """DenseEntityTronBatch (dense size buckets: every padded row is a dense CSR row of d entries) with d > 64 and
+    quad rows: each row is longer than the 64 entries one lane group covers per round, so the lean kernel's tail
+    loop over further quads runs. Iteration-limited and converged fits match the CPU float64 TRON per entity."""
+    import photon_ml_amd.algorithm.coordinates as co
+    from photon_ml_amd.algorithm.coordinates import RandomEffectCoordinate
+    from photon_ml_amd.data.random_effect import RandomEffectDataConfiguration
+    from photon_ml_amd.optimization.config import (GLMOptimizationConfiguration, OptimizerConfig,
+                                                   RegularizationContext)
+    data = make_entities([80, 95, 70, 100] * 6, 100, 0, seed=3, dense_pool=True)
+    for tol, max_iter, bound in ((0.0, 4, 1e-9), (1e-8, 60, 1e-6)):
+        captured = {}
+        real = co.random_effect_tracker_stats
+
+        def spy(it, rs, sec):
+            captured["it"] = it.numpy().copy()
+            return real(it, rs, sec)
+        monkeypatch.setattr(co, "random_effect_tracker_stats", spy)
+        cfg = GLMOptimizationConfiguration(OptimizerConfig("TRON", max_iter, tol), RegularizationContext("L2"), 1.0)
+        c = RandomEffectCoordinate("u", data, RandomEffectDataConfiguration("userId", "user"), cfg,
+                                   "LOGISTIC_REGRESSION", device="cuda", layout="dense")
+        m = c.update_model(c.initialize_model())
+        fz = [c._dense_fused(b, bk, 0.0) for b, bk in enumerate(c.dataset.buckets)]
+        assert all(f is not None and f.quad and f.d > 64 for f in fz)
+        ents = np.concatenate([bk.entities for bk in c.dataset.buckets])
+        its = {c.dataset.entity_ids[k]: int(captured["it"][i]) for i, k in enumerate(ents)}
+        ref = cpu_tron(data, 1.0, tol, max_iter)
+        for e, (w_ref, it_ref, _) in ref.items():
+            assert its[e] == it_ref, (tol, e, its[e], it_ref)
+            w = np.asarray(m.coefficients_of(e).means, dtype=np.float64)
+            err = np.abs(w - w_ref).max() / max(np.abs(w_ref).max(), 1e-300)
+            assert err < bound, (tol, e, err)
