@@ -1279,6 +1279,132 @@ static int64_t gen_training_examples(const std::string& path, int64_t n_records,
   return written;
 }
 
+// BayesianLinearModelAvro records straight from flat model arrays (GAME model save; reference
+// ModelProcessingUtils.saveGameModelToHDFS / AvroUtils): model k = coefficients [ptr[k], ptr[k+1]) with feature
+// codes ``code`` (indices into the NUL-separated ``names`` blob of "name<delim>term" keys), values ``means`` and
+// optional ``variances``. Per model: coefficients with |mean| > threshold, ordered by decreasing |mean| (stable), as
+// name/term/value triples. Blocks of ``block_records`` models are encoded and compressed on all cores, written in
+// order; the bytes equal write_ocf of the same records (same header, sync marker and codec settings).
+static int64_t write_linear_models(const std::string& path, const std::string& schema_json, py::list model_ids,
+                                   py::array_t<int64_t, py::array::c_style | py::array::forcecast> ptr,
+                                   py::array_t<int64_t, py::array::c_style | py::array::forcecast> code,
+                                   py::array_t<double, py::array::c_style | py::array::forcecast> means,
+                                   py::object variances, const std::string& names, const std::string& model_class,
+                                   py::object loss_function, double threshold, const std::string& codec,
+                                   int block_records, const std::string& delimiter) {
+  const int64_t M = (int64_t)py::len(model_ids);
+  if (ptr.size() != M + 1) throw std::runtime_error("ptr must hold n_models + 1 offsets");
+  std::vector<std::string> ids((size_t)M);
+  for (int64_t k = 0; k < M; ++k) ids[(size_t)k] = py::str(model_ids[(size_t)k]).cast<std::string>();
+  const int64_t* P = ptr.data();
+  const int64_t* C = code.data();
+  const double* V = means.data();
+  py::array_t<double, py::array::c_style | py::array::forcecast> var_arr;
+  const double* VAR = nullptr;
+  if (!variances.is_none()) {
+    var_arr = variances.cast<py::array_t<double, py::array::c_style | py::array::forcecast>>();
+    if (var_arr.size() != means.size()) throw std::runtime_error("variances / means length mismatch");
+    VAR = var_arr.data();
+  }
+  if (code.size() != means.size() || (M && P[M] > (int64_t)means.size())) throw std::runtime_error("bad offsets");
+  const bool has_loss = !loss_function.is_none();
+  const std::string loss = has_loss ? loss_function.cast<std::string>() : std::string();
+  // name / term of every code
+  std::vector<std::pair<std::string, std::string>> nt;
+  {
+    size_t a = 0;
+    while (a <= names.size()) {
+      size_t z = names.find('\0', a);
+      if (z == std::string::npos) z = names.size();
+      std::string key = names.substr(a, z - a);
+      size_t d = delimiter.empty() ? std::string::npos : key.find(delimiter);
+      if (d == std::string::npos) nt.emplace_back(key, std::string());
+      else nt.emplace_back(key.substr(0, d), key.substr(d + delimiter.size()));
+      a = z + 1;
+      if (z == names.size()) break;
+    }
+  }
+  for (int64_t t = 0; t < (M ? P[M] : 0); ++t)
+    if (C[t] < 0 || C[t] >= (int64_t)nt.size()) throw std::runtime_error("feature code outside the names table");
+  const int64_t B = std::max(block_records, 1);
+  const int64_t nblocks = (M + B - 1) / B;
+  std::vector<std::string> payloads((size_t)nblocks);
+  {
+    py::gil_scoped_release nogil;
+    std::atomic<int64_t> next{0};
+    auto work = [&]() {
+      std::vector<int64_t> kept;
+      for (int64_t blk; (blk = next.fetch_add(1)) < nblocks;) {
+        Writer body;
+        for (int64_t k = blk * B; k < std::min(M, (blk + 1) * B); ++k) {
+          kept.clear();
+          for (int64_t t = P[k]; t < P[k + 1]; ++t)
+            if (std::fabs(V[t]) > threshold) kept.push_back(t);
+          std::stable_sort(kept.begin(), kept.end(),
+                           [&](int64_t a, int64_t b) { return std::fabs(V[a]) > std::fabs(V[b]); });
+          body.str(ids[(size_t)k]);
+          body.str(model_class);
+          if (!kept.empty()) {
+            body.varlong((int64_t)kept.size());
+            for (int64_t t : kept) { body.str(nt[(size_t)C[t]].first); body.str(nt[(size_t)C[t]].second); body.dbl(V[t]); }
+          }
+          body.varlong(0);
+          if (VAR) {
+            body.varlong(1);
+            if (!kept.empty()) {
+              body.varlong((int64_t)kept.size());
+              for (int64_t t : kept) { body.str(nt[(size_t)C[t]].first); body.str(nt[(size_t)C[t]].second); body.dbl(VAR[t]); }
+            }
+            body.varlong(0);
+          } else {
+            body.varlong(0);
+          }
+          if (has_loss) { body.varlong(1); body.str(loss); } else body.varlong(0);
+        }
+        std::string payload;
+        if (codec == "null") payload = body.buf;
+        else if (codec == "deflate") payload = deflate_raw(body.buf, 6);
+        else if (codec == "snappy") {
+          payload = snappy_compress(body.buf);
+          uint32_t c = crc32_iso(body.buf);
+          payload.push_back((char)(c >> 24)); payload.push_back((char)(c >> 16));
+          payload.push_back((char)(c >> 8)); payload.push_back((char)c);
+        }
+        payloads[(size_t)blk] = std::move(payload);
+      }
+    };
+    if (codec != "null" && codec != "deflate" && codec != "snappy") throw std::runtime_error("unsupported codec " + codec);
+    const int nt_ = (int)std::max<int64_t>(1, std::min<int64_t>(nblocks, std::max(1u, std::thread::hardware_concurrency())));
+    std::vector<std::thread> th;
+    for (int i = 1; i < nt_; ++i) th.emplace_back(work);
+    work();
+    for (auto& t : th) t.join();
+  }
+  std::string out("Obj\x01", 4);
+  Writer hdr;
+  hdr.varlong(2);
+  hdr.str("avro.schema"); hdr.str(schema_json);
+  hdr.str("avro.codec"); hdr.str(codec);
+  hdr.varlong(0);
+  out += hdr.buf;
+  std::string sync(16, '\0');
+  std::mt19937_64 rng(0x5eed1234abcdULL ^ (uint64_t)M);
+  for (int i = 0; i < 16; ++i) sync[i] = (char)(rng() & 0xFF);
+  out += sync;
+  std::ofstream f(path, std::ios::binary);
+  if (!f) throw std::runtime_error("cannot write " + path);
+  f.write(out.data(), (std::streamsize)out.size());
+  for (int64_t blk = 0; blk < nblocks; ++blk) {
+    const int64_t m = std::min(M, (blk + 1) * B) - blk * B;
+    Writer bh; bh.varlong(m); bh.varlong((int64_t)payloads[(size_t)blk].size());
+    f.write(bh.buf.data(), (std::streamsize)bh.buf.size());
+    f.write(payloads[(size_t)blk].data(), (std::streamsize)payloads[(size_t)blk].size());
+    f.write(sync.data(), 16);
+  }
+  if (!f) throw std::runtime_error("write failed: " + path);
+  return M;
+}
+
 PYBIND11_MODULE(libpml_avro, m) {
   m.def("build_id", []() { return std::string(pml_build_stamp + 13); });
   m.doc() = "photon_ml_amd native Avro OCF codec";
@@ -1286,6 +1412,10 @@ PYBIND11_MODULE(libpml_avro, m) {
   m.def("read_schema", &read_schema);
   m.def("write_ocf", &write_ocf, py::arg("path"), py::arg("schema_json"), py::arg("records"),
         py::arg("codec") = "deflate", py::arg("block_records") = 4096);
+  m.def("write_linear_models", &write_linear_models, py::arg("path"), py::arg("schema_json"), py::arg("model_ids"),
+        py::arg("ptr"), py::arg("code"), py::arg("means"), py::arg("variances"), py::arg("names"),
+        py::arg("model_class"), py::arg("loss_function"), py::arg("threshold"), py::arg("codec") = "deflate",
+        py::arg("block_records") = 4096, py::arg("delimiter") = std::string("\x01"));
   m.def("read_columnar", &read_columnar, py::arg("paths"), py::arg("label_fields"), py::arg("weight_field"),
         py::arg("offset_field"), py::arg("uid_field"), py::arg("metadata_field"), py::arg("bags"),
         py::arg("id_tags"), py::arg("delimiter") = std::string("\x01"), py::arg("tag_strings") = true);

@@ -30,6 +30,9 @@ from ..models.glm import FQCN, LOSS_FQCN, Coefficients, model_for_task, task_fro
 from .avro import BAYESIAN_LINEAR_MODEL, read_records, write_records, avro_files
 from .index_map import IndexMap
 
+# random-effect models are written by the native encoder (write_linear_models); 0: per-record Python dictionaries
+NATIVE_MODEL_WRITER = os.environ.get("PML_NATIVE_MODEL_WRITER", "1") != "0"
+
 FIXED_EFFECT = "fixed-effect"
 RANDOM_EFFECT = "random-effect"
 ID_INFO = "id-info"
@@ -49,6 +52,47 @@ def _ntv(values: np.ndarray, idx: np.ndarray, index_map: IndexMap):
         n, t = split_feature_key(key)
         out.append({"name": n, "term": t, "value": float(v)})
     return out, idx[order]
+
+
+def _feature_names(index_map: IndexMap, idx: np.ndarray):
+    """Feature keys of the indices ``idx`` (batched where the map supports it)."""
+    if hasattr(index_map, "get_feature_names"):
+        names = index_map.get_feature_names(idx)
+    elif hasattr(index_map, "index_to_key"):
+        tab = index_map.index_to_key
+        names = [tab[i] if 0 <= i < len(tab) else None for i in idx.tolist()]
+    else:
+        names = [index_map.get_feature_name(int(i)) for i in idx]
+    for i, n in zip(idx, names):
+        if n is None:
+            raise KeyError(f"Feature index {i} not found in the feature map")
+    return names
+
+
+def write_linear_models(path: str, model_ids, ptr: np.ndarray, feat: np.ndarray, means: np.ndarray,
+                        variances: Optional[np.ndarray], index_map: IndexMap, task: TaskType):
+    """BayesianLinearModelAvro records of many models (model k = coefficients ``ptr[k]:ptr[k+1]`` at feature indices
+    ``feat``) in one native call: the coefficient filter (|w| > MODEL_SPARSITY_THRESHOLD), the ordering by |w| and
+    the Avro encoding + compression run in C++ over all cores; only the names of the features that occur are looked
+    up. Same bytes as ``write_records`` of the ``glm_to_avro_record`` dictionaries (``tests/test_estimator_io.py``).
+    Reference: ``photon-client/.../io/ModelProcessingUtils.scala`` (saveGameModelToHDFS)."""
+    from .avro import native
+    from ..constants import DELIMITER
+    feat = np.ascontiguousarray(feat, dtype=np.int64)
+    means = np.ascontiguousarray(means, dtype=np.float64)
+    keep = np.abs(means) > MODEL_SPARSITY_THRESHOLD      # names only for coefficients that are written
+    uniq = np.unique(feat[keep])
+    code = np.searchsorted(uniq, feat) if len(uniq) else np.zeros(len(feat), np.int64)
+    code[~keep] = 0
+    names = _feature_names(index_map, uniq) if len(uniq) else [""]
+    blob = "\0".join(names).encode("utf-8")
+    os.makedirs(os.path.dirname(os.path.abspath(path)), exist_ok=True)
+    native().write_linear_models(str(path), json.dumps(BAYESIAN_LINEAR_MODEL), [str(m) for m in model_ids],
+                                 np.ascontiguousarray(ptr, dtype=np.int64), code.astype(np.int64),
+                                 np.ascontiguousarray(means, dtype=np.float64),
+                                 None if variances is None else np.ascontiguousarray(variances, dtype=np.float64),
+                                 blob, FQCN[task], LOSS_FQCN.get(task), float(MODEL_SPARSITY_THRESHOLD), "deflate",
+                                 4096, DELIMITER)
 
 
 def glm_to_avro_record(model_id: str, task: TaskType, means: np.ndarray, variances: Optional[np.ndarray],
@@ -109,10 +153,15 @@ def save_game_model(model: GameModel, out_dir: str, index_maps: Dict[str, IndexM
             with open(os.path.join(d, ID_INFO), "w") as f:
                 f.write(m.feature_shard_id + "\n")
             c = m.glm.coefficients
-            rec = glm_to_avro_record(FIXED_EFFECT, task, c.means.cpu().numpy(),
-                                     None if c.variances is None else c.variances.cpu().numpy(),
-                                     index_maps[m.feature_shard_id])
-            write_records(os.path.join(d, COEFFICIENTS, "part-00000.avro"), BAYESIAN_LINEAR_MODEL, [rec])
+            means = c.means.cpu().numpy()
+            var = None if c.variances is None else c.variances.cpu().numpy()
+            path = os.path.join(d, COEFFICIENTS, "part-00000.avro")
+            if NATIVE_MODEL_WRITER:
+                write_linear_models(path, [FIXED_EFFECT], np.array([0, len(means)]), np.arange(len(means)), means,
+                                    var, index_maps[m.feature_shard_id], task)
+            else:
+                rec = glm_to_avro_record(FIXED_EFFECT, task, means, var, index_maps[m.feature_shard_id])
+                write_records(path, BAYESIAN_LINEAR_MODEL, [rec])
         elif isinstance(m, RandomEffectModel):
             d = os.path.join(out_dir, RANDOM_EFFECT, cid)
             os.makedirs(os.path.join(d, COEFFICIENTS), exist_ok=True)
@@ -120,24 +169,31 @@ def save_game_model(model: GameModel, out_dir: str, index_maps: Dict[str, IndexM
                 with open(os.path.join(d, ID_INFO), "w") as f:
                     f.write(m.random_effect_type + "\n" + m.feature_shard_id + "\n")
             im = index_maps[m.feature_shard_id]
-            ent = m.keys // m.dim
-            feat = m.keys % m.dim
+            keys, vals = m.keys, m.values
+            ent = keys // m.dim
+            feat = keys % m.dim
             bounds = np.searchsorted(ent, np.arange(m.n_entities + 1))
-            recs = []
-            for e in range(m.n_entities):
-                a, b = bounds[e], bounds[e + 1]
-                if b <= a:
-                    continue
-                recs.append(glm_to_avro_record(str(m.entity_ids[e]), task, m.values[a:b],
-                                               None if m.variances is None else m.variances[a:b], im, feat[a:b]))
-            n_files = max(1, (len(recs) + entities_per_file - 1) // entities_per_file)
+            present = np.nonzero(bounds[1:] > bounds[:-1])[0]          # entities with coefficients
+            n_files = max(1, (len(present) + entities_per_file - 1) // entities_per_file)
             if re_file_limit is not None:
                 n_files = max(1, min(n_files, re_file_limit))
-            per = (len(recs) + n_files - 1) // n_files if recs else 0
+            per = (len(present) + n_files - 1) // n_files if len(present) else 0
             prefix = f"part-r{r:05d}-" if sharded else "part-"
             for i in range(n_files):
-                write_records(os.path.join(d, COEFFICIENTS, f"{prefix}{i:05d}.avro"), BAYESIAN_LINEAR_MODEL,
-                              recs[i * per:(i + 1) * per])
+                ents = present[i * per:(i + 1) * per]
+                path = os.path.join(d, COEFFICIENTS, f"{prefix}{i:05d}.avro")
+                if NATIVE_MODEL_WRITER:
+                    # the entities' coefficient ranges are contiguous and in order: one slice per file
+                    lo = bounds[ents[0]] if len(ents) else 0
+                    hi = bounds[ents[-1] + 1] if len(ents) else 0
+                    ptr = np.concatenate([bounds[ents], [hi]]) - lo if len(ents) else np.zeros(1, np.int64)
+                    write_linear_models(path, [str(m.entity_ids[e]) for e in ents], ptr, feat[lo:hi], vals[lo:hi],
+                                        None if m.variances is None else m.variances[lo:hi], im, task)
+                    continue
+                recs = [glm_to_avro_record(str(m.entity_ids[e]), task, vals[bounds[e]:bounds[e + 1]],
+                                           None if m.variances is None else m.variances[bounds[e]:bounds[e + 1]],
+                                           im, feat[bounds[e]:bounds[e + 1]]) for e in ents]
+                write_records(path, BAYESIAN_LINEAR_MODEL, recs)
         else:
             raise TypeError(f"unknown model type {type(m)}")
 

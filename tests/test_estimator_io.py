@@ -5,6 +5,7 @@
 * ModelProcessingUtilsTest save/load round trip; Avro codec round trips incl. reference files.
 """
 import json
+from collections import OrderedDict
 import os
 
 import numpy as np
@@ -234,3 +235,45 @@ def test_native_shard_assembly_matches_python(intercept):
     b = dr._assemble(n, clean, v2c, dim, icpt, False)
     assert np.array_equal(a.indptr, b.indptr) and np.array_equal(a.indices, b.indices)
     np.testing.assert_allclose(a.data, b.data, rtol=1e-15, atol=0)
+
+
+def test_native_model_writer_is_byte_identical(tmp_path, monkeypatch):
+    """save_game_model with the native BayesianLinearModel encoder (io/model_io.write_linear_models) writes the
+    same bytes as the per-record Python dictionaries: fixed effect with variances, random effect over several
+    files, tiny coefficients dropped, |w| ordering with ties."""
+    import filecmp
+    from photon_ml_amd.constants import TaskType
+    from photon_ml_amd.io import model_io
+    from photon_ml_amd.io.index_map import DefaultIndexMap
+    from photon_ml_amd.models.game import FixedEffectModel, GameModel, RandomEffectModel
+    from photon_ml_amd.models.glm import Coefficients, model_for_task
+    rng = np.random.default_rng(4)
+    D = 300
+    im = DefaultIndexMap.from_keys([f"f{j}\u0001t{j % 4}" for j in range(D)] + ["(INTERCEPT)\u0001"])
+    task = TaskType.LOGISTIC_REGRESSION
+    w = rng.normal(size=D + 1)
+    w[::9] = 1e-7
+    w[5] = w[6]
+    fe = FixedEffectModel(model_for_task(task, Coefficients(torch.from_numpy(w), torch.from_numpy(rng.random(D + 1)))),
+                          "g")
+    n_ent = 23
+    keys, vals = [], []
+    for e in range(n_ent):
+        f = np.sort(rng.choice(D + 1, size=int(rng.integers(0, 30)), replace=False))
+        keys.append(e * (D + 1) + f)
+        vals.append(rng.normal(size=f.size) * np.where(rng.random(f.size) < 0.2, 1e-6, 1.0))
+    re = RandomEffectModel("userId", "g", task, np.array([f"u{e}" for e in range(n_ent)]), D + 1,
+                           np.concatenate(keys), np.concatenate(vals))
+    model = GameModel(OrderedDict([("fixed", fe), ("per-user", re)]))
+    for flag, out in (("1", tmp_path / "native"), ("0", tmp_path / "python")):
+        monkeypatch.setattr(model_io, "NATIVE_MODEL_WRITER", flag == "1")
+        model_io.save_game_model(model, str(out), {"g": im}, task=task, entities_per_file=7)
+    cmp = filecmp.dircmp(tmp_path / "native", tmp_path / "python")
+
+    def same(c):
+        assert not c.left_only and not c.right_only and not c.diff_files, (c.left, c.diff_files)
+        (_, mismatch, errors) = filecmp.cmpfiles(c.left, c.right, c.common_files, shallow=False)
+        assert not mismatch and not errors, mismatch
+        for sub in c.subdirs.values():
+            same(sub)
+    same(cmp)

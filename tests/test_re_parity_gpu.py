@@ -182,14 +182,15 @@ def test_dense_bucket_quad_rows_longer_than_64_match_cpu_tron(monkeypatch):
     from photon_ml_amd.optimization.config import (GLMOptimizationConfiguration, OptimizerConfig,
                                                    RegularizationContext)
     data = make_entities([80, 95, 70, 100] * 6, 100, 0, seed=3, dense_pool=True)
-    for tol, max_iter, bound in ((0.0, 4, 1e-9), (1e-8, 60, 1e-6)):
-        captured = {}
-        real = co.random_effect_tracker_stats
+    real = co.random_effect_tracker_stats
+    captured = {}
 
-        def spy(it, rs, sec):
-            captured["it"] = it.numpy().copy()
-            return real(it, rs, sec)
-        monkeypatch.setattr(co, "random_effect_tracker_stats", spy)
+    def spy(it, rs, sec):
+        captured["it"] = it.numpy().copy()
+        return real(it, rs, sec)
+    monkeypatch.setattr(co, "random_effect_tracker_stats", spy)
+    for tol, max_iter, bound in ((0.0, 4, 1e-9), (1e-8, 60, 1e-6)):
+        captured.clear()
         cfg = GLMOptimizationConfiguration(OptimizerConfig("TRON", max_iter, tol), RegularizationContext("L2"), 1.0)
         c = RandomEffectCoordinate("u", data, RandomEffectDataConfiguration("userId", "user"), cfg,
                                    "LOGISTIC_REGRESSION", device="cuda", layout="dense")
