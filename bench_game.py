@@ -264,6 +264,11 @@ def run(args, dev, rank: int = 0, world: int = 1, data=None, t_data: float = 0.0
     log(f"fixed effect per sweep: {(getattr(fe_gd, 'n_fwd', 0) - fe_pass0[0]) / args.steps:.1f} forward + "
         f"{(getattr(fe_gd, 'n_t', 0) - fe_pass0[1]) / args.steps:.1f} transpose passes; sweeps (ms): "
         f"{', '.join(f'{v:.1f}' for v in sweeps_ms)}")
+    fe_opt = getattr(getattr(coords["global"], "problem", None), "optimizer", None)
+    fe_plans = {k: getattr(fe_opt, k) for k in ("plans_used", "plans_rejected", "wasted_spec_passes")
+                if hasattr(fe_opt, k)}
+    if fe_plans:
+        log(f"fixed-effect L-BFGS plans (whole run): {fe_plans}")
     loss = cd.history[-1].get("training_loss")
     coord_ms = {}
     for rec in cd.history[-2 * args.steps:]:
@@ -307,6 +312,7 @@ def run(args, dev, rank: int = 0, world: int = 1, data=None, t_data: float = 0.0
         "sweep_ms_min": min(sweeps_ms) if sweeps_ms else None,
         "cold_first_sweep_ms": cold_ms,
         "cold_first_sweep_coordinate_ms": cold_coord_ms,
+        "fe_lbfgs_plans": fe_plans,
         "sweep_ms_median": float(np.median(sweeps_ms)) if sweeps_ms else None,
         "higher_is_better": True,
         "scaling": "weak",

@@ -26,6 +26,9 @@ class GameData:
     weights: Optional[np.ndarray] = None
     uids: Optional[np.ndarray] = None
     raw_uids: Optional[np.ndarray] = None  # original (string) uids from the input records, for score output
+    # id tag -> (codes, distinct values, the tag array they encode): the reader's factorisation of a string id tag,
+    # reused by the random-effect build instead of a sort of every row's string (valid only for that very array)
+    id_factors: Optional[Dict[str, tuple]] = None
 
     def __post_init__(self):
         n = len(self.response)

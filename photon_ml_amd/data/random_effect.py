@@ -119,6 +119,30 @@ class Bucket:
     d_local: np.ndarray       # projected dim per entity
 
 
+def sorted_factors(codes: np.ndarray, table) -> Optional[tuple]:
+    """``np.unique(ids.astype(str), return_inverse=True)`` from a factorisation ``ids = table[codes]``: the sort
+    runs over the distinct values only. None when two distinct values print to the same string (mixed id types),
+    which only the per-row path merges the same way."""
+    us = np.asarray(table, dtype=object).astype(str)
+    order = np.argsort(us, kind="stable")
+    u = us[order]
+    if len(u) > 1 and bool((u[1:] == u[:-1]).any()):
+        return None
+    rank = np.empty(len(order), dtype=np.int64)
+    rank[order] = np.arange(len(order), dtype=np.int64)
+    return u, rank[np.asarray(codes, dtype=np.int64)]
+
+
+def factorize_ids(ids: np.ndarray) -> Optional[tuple]:
+    """:func:`sorted_factors` of a per-row object array through a hash factorisation (4x faster than np.unique of
+    the strings at 10M rows); None for missing values (pandas would print them as "nan", np.unique as "None")."""
+    import pandas as pd
+    codes, uniq = pd.factorize(ids, sort=False, use_na_sentinel=False)
+    if bool(pd.isna(uniq).any()):
+        return None
+    return sorted_factors(codes, uniq)
+
+
 class RandomEffectDataset:
     """Active/passive data of one random-effect coordinate, projected and bucketed."""
 
@@ -140,8 +164,16 @@ class RandomEffectDataset:
         self.dim = x.shape[1]
         ids = data.id_tags[re_type]
         with phase("RE dataset: entity ids"):
-            ids_s = ids.astype(str) if ids.dtype == object else ids
-            if self.device.type == "cuda" and np.issubdtype(ids_s.dtype, np.integer) and len(ids_s):
+            fac = (getattr(data, "id_factors", None) or {}).get(re_type)
+            got = None
+            if fac is not None and fac[2] is ids and len(fac[0]) == len(ids):
+                got = sorted_factors(fac[0], fac[1])          # the reader's codes: no per-row string work
+            elif ids.dtype == object and len(ids):
+                got = factorize_ids(ids)
+            ids_s = ids.astype(str) if got is None and ids.dtype == object else ids
+            if got is not None:
+                self.entity_ids, ent = got
+            elif self.device.type == "cuda" and np.issubdtype(ids_s.dtype, np.integer) and len(ids_s):
                 # integer entity ids: sorted unique + inverse on the device (np.unique: 1.3 s at 25M rows)
                 u, inv = torch.unique(torch.from_numpy(np.ascontiguousarray(ids_s)).to(self.device), sorted=True,
                                       return_inverse=True)

@@ -91,17 +91,18 @@ class GLMObjective:
         return F, b, exact
 
     def margin_line_search(self, data, x0: torch.Tensor, d: torch.Tensor, t0: float = 1.0,
-                           dots=None) -> Optional["MarginLineSearch"]:
+                           dots=None, ls_opts: Optional[dict] = None) -> Optional["MarginLineSearch"]:
         """Line search along x0 + t d in MARGIN space (GLM margins are affine in t), or None when the data
-        backend cannot cache margins. ``dots``: (x0.x0, x0.d, d.d) when the caller already has them. See
-        :class:`MarginLineSearch`."""
+        backend cannot cache margins. ``dots``: (x0.x0, x0.d, d.d) when the caller already has them.
+        ``ls_opts``: extra keywords of the backend's ``ls_begin`` (a speculative pass, see
+        ``DeviceGLMData.ls_begin``). See :class:`MarginLineSearch`."""
         if not hasattr(data, "ls_begin"):
             return None
         norm = self.normalization
         w0_eff, shift0 = norm.effective(x0)
         d_eff = d * norm.factors.to(d) if norm.factors is not None else d
         d_shift = -float(torch.dot(d_eff, norm.shifts.to(d_eff))) if norm.shifts is not None else 0.0
-        if not data.ls_begin(w0_eff, shift0, d_eff, d_shift, t0, self.loss):
+        if not data.ls_begin(w0_eff, shift0, d_eff, d_shift, t0, self.loss, **(ls_opts or {})):
             return None
         return MarginLineSearch(self, data, x0, d, dots)
 
@@ -160,6 +161,10 @@ class GLMObjective:
 
 
 DEFERRED_DOTS = object()   # ``dots`` sentinel: the caller assigns (a, b, c) itself before the first eval
+# trial steps evaluated together once a line search needs a second trial (1: one pass per trial). Off by default:
+# measured on game5pl (profiles/lbfgs_plans_r6.md) the 6-step pass costs 0.97 ms -- the fp64 logistic loss at six
+# margins per row is compute-bound -- and L-BFGS's first search then still needed three zoom trials.
+LS_LADDER = int(__import__("os").environ.get("PML_LS_LADDER", "1"))
 
 
 class MarginLineSearch:
@@ -178,11 +183,36 @@ class MarginLineSearch:
         self.obj, self.data, self.x0, self.d = obj, data, x0, d
         l2 = obj.l2_weight
         self.l2 = l2
+        self._trials = {}
+        self._n_eval = 0
         if l2 > 0 and dots is not DEFERRED_DOTS:
             self.a, self.b, self.c = dots if dots is not None else vdots([(x0, x0), (x0, d), (d, d)])
 
     def eval(self, t: float):
-        f, dd = self.data.ls_eval(self.obj.loss, t)
+        """phi(t), phi'(t). From the second trial on, a backend with ``ls_eval_many`` evaluates the strong Wolfe
+        search's whole extrapolation ladder t, 1.5 t, 2.25 t, ... (LS_LADDER steps) in one pass and one readback:
+        a first step that is too short (L-BFGS's first iteration, t0 = 1 / ||d||) then costs one pass, not one
+        pass and one host round trip per trial. Same values as trial-by-trial evaluation (bitwise)."""
+        self._n_eval += 1
+        t = float(t)
+        got = self._trials.get(t)
+        if got is None:
+            many = getattr(self.data, "ls_eval_many", None)
+            if many is not None and LS_LADDER > 1 and self._n_eval > 1:
+                from ..optimization.line_search import EXTRAPOLATION
+                ts = [t]
+                for _ in range(LS_LADDER - 1):
+                    ts.append(ts[-1] * EXTRAPOLATION)
+                for tk, v in zip(ts, many(self.obj.loss, ts)):
+                    self._trials[tk] = v
+                got = self._trials[t]
+            else:
+                got = self.data.ls_eval(self.obj.loss, t)
+        f, dd = got
+        return self.adjust(f, dd, t)
+
+    def adjust(self, f: float, dd: float, t: float):
+        """phi(t) and phi'(t) from the data terms (F, D) at t: the L2 terms from the cached inner products."""
         if self.l2 > 0:
             f += 0.5 * self.l2 * (self.a + 2.0 * t * self.b + t * t * self.c)
             dd += self.l2 * (self.b + t * self.c)

@@ -53,19 +53,32 @@ class IndexMap:
 
 
 class DefaultIndexMap(IndexMap):
-    def __init__(self, key_to_index: Dict[str, int]):
-        self.key_to_index = dict(key_to_index)
-        self._dim = (max(self.key_to_index.values()) + 1) if self.key_to_index else 0
+    def __init__(self, key_to_index: Optional[Dict[str, int]] = None, index_to_key: Optional[List[str]] = None):
+        """From a key -> index dict, or from the distinct keys in index order (``index_to_key``: the dict is then
+        built on the first key lookup -- a reader that maps its vocabulary by sorting needs none)."""
+        if index_to_key is not None:
+            self.index_to_key = list(index_to_key)
+            self._dim = len(self.index_to_key)
+            self._k2i = None
+            return
+        self._k2i = dict(key_to_index or {})
+        self._dim = (max(self._k2i.values()) + 1) if self._k2i else 0
         self.index_to_key = [None] * self._dim
-        for k, i in self.key_to_index.items():
+        for k, i in self._k2i.items():
             self.index_to_key[i] = k
+
+    @property
+    def key_to_index(self) -> Dict[str, int]:
+        if self._k2i is None:
+            self._k2i = {k: i for i, k in enumerate(self.index_to_key)}
+        return self._k2i
 
     @staticmethod
     def from_keys(keys: Iterable[str], add_intercept: bool = False) -> "DefaultIndexMap":
         ks = list(dict.fromkeys(keys))
         if add_intercept and INTERCEPT_KEY not in ks:
             ks.append(INTERCEPT_KEY)
-        return DefaultIndexMap({k: i for i, k in enumerate(ks)})
+        return DefaultIndexMap(index_to_key=ks)
 
     def get_index(self, key):
         return self.key_to_index.get(key, -1)

@@ -32,6 +32,12 @@ from .index_map import IndexMap
 
 # random-effect models are written by the native encoder (write_linear_models); 0: per-record Python dictionaries
 NATIVE_MODEL_WRITER = os.environ.get("PML_NATIVE_MODEL_WRITER", "1") != "0"
+# Avro codec of the model files. The reference saves them through Hadoop's AvroOutputFormat without output
+# compression configured (AvroUtils.saveAsAvro), i.e. uncompressed; "deflate" / "snappy" are available (a 3.5 GB
+# random-effect model took ~50 s to deflate on 16 cores, its values barely compress).
+MODEL_CODEC = os.environ.get("PML_MODEL_CODEC", "null")
+# uncompressed bytes per Avro block (Avro's own writers cut blocks at a sync interval of this order)
+BLOCK_BYTES = 1 << 20
 
 FIXED_EFFECT = "fixed-effect"
 RANDOM_EFFECT = "random-effect"
@@ -69,6 +75,14 @@ def _feature_names(index_map: IndexMap, idx: np.ndarray):
     return names
 
 
+def block_records(n_models: int, n_kept: int, with_variances: bool) -> int:
+    """Models per Avro block for ~BLOCK_BYTES uncompressed blocks (an estimate from the kept-coefficient count:
+    ~24 bytes per name/term/value triple), so a file of large per-entity models still splits into many blocks that
+    encode in parallel. The same for the native and the Python writers (same bytes)."""
+    per = 96 + 24 * (2 if with_variances else 1) * n_kept / max(n_models, 1)
+    return int(min(4096, max(1, BLOCK_BYTES // per)))
+
+
 def write_linear_models(path: str, model_ids, ptr: np.ndarray, feat: np.ndarray, means: np.ndarray,
                         variances: Optional[np.ndarray], index_map: IndexMap, task: TaskType):
     """BayesianLinearModelAvro records of many models (model k = coefficients ``ptr[k]:ptr[k+1]`` at feature indices
@@ -81,8 +95,15 @@ def write_linear_models(path: str, model_ids, ptr: np.ndarray, feat: np.ndarray,
     feat = np.ascontiguousarray(feat, dtype=np.int64)
     means = np.ascontiguousarray(means, dtype=np.float64)
     keep = np.abs(means) > MODEL_SPARSITY_THRESHOLD      # names only for coefficients that are written
-    uniq = np.unique(feat[keep])
-    code = np.searchsorted(uniq, feat) if len(uniq) else np.zeros(len(feat), np.int64)
+    # distinct kept features and each coefficient's code by a marks table over the feature space (O(n); a sort /
+    # binary search of 300M coefficients took most of a 3.5 GB model's save)
+    dim = int(feat.max()) + 1 if len(feat) else 0
+    seen = np.zeros(dim, dtype=bool)
+    seen[feat[keep]] = True
+    uniq = np.flatnonzero(seen)
+    lut = np.zeros(dim, dtype=np.int64)
+    lut[uniq] = np.arange(len(uniq), dtype=np.int64)
+    code = lut[feat]
     code[~keep] = 0
     names = _feature_names(index_map, uniq) if len(uniq) else [""]
     blob = "\0".join(names).encode("utf-8")
@@ -91,8 +112,8 @@ def write_linear_models(path: str, model_ids, ptr: np.ndarray, feat: np.ndarray,
                                  np.ascontiguousarray(ptr, dtype=np.int64), code.astype(np.int64),
                                  np.ascontiguousarray(means, dtype=np.float64),
                                  None if variances is None else np.ascontiguousarray(variances, dtype=np.float64),
-                                 blob, FQCN[task], LOSS_FQCN.get(task), float(MODEL_SPARSITY_THRESHOLD), "deflate",
-                                 4096, DELIMITER)
+                                 blob, FQCN[task], LOSS_FQCN.get(task), float(MODEL_SPARSITY_THRESHOLD), MODEL_CODEC,
+                                 block_records(len(ptr) - 1, int(keep.sum()), variances is not None), DELIMITER)
 
 
 def glm_to_avro_record(model_id: str, task: TaskType, means: np.ndarray, variances: Optional[np.ndarray],
@@ -161,7 +182,7 @@ def save_game_model(model: GameModel, out_dir: str, index_maps: Dict[str, IndexM
                                     var, index_maps[m.feature_shard_id], task)
             else:
                 rec = glm_to_avro_record(FIXED_EFFECT, task, means, var, index_maps[m.feature_shard_id])
-                write_records(path, BAYESIAN_LINEAR_MODEL, [rec])
+                write_records(path, BAYESIAN_LINEAR_MODEL, [rec], codec=MODEL_CODEC, block_records=1)
         elif isinstance(m, RandomEffectModel):
             d = os.path.join(out_dir, RANDOM_EFFECT, cid)
             os.makedirs(os.path.join(d, COEFFICIENTS), exist_ok=True)
@@ -193,7 +214,9 @@ def save_game_model(model: GameModel, out_dir: str, index_maps: Dict[str, IndexM
                 recs = [glm_to_avro_record(str(m.entity_ids[e]), task, vals[bounds[e]:bounds[e + 1]],
                                            None if m.variances is None else m.variances[bounds[e]:bounds[e + 1]],
                                            im, feat[bounds[e]:bounds[e + 1]]) for e in ents]
-                write_records(path, BAYESIAN_LINEAR_MODEL, recs)
+                write_records(path, BAYESIAN_LINEAR_MODEL, recs, codec=MODEL_CODEC,
+                              block_records=block_records(len(recs), sum(len(r["means"]) for r in recs),
+                                                          m.variances is not None))
         else:
             raise TypeError(f"unknown model type {type(m)}")
 

@@ -358,6 +358,10 @@ struct FwdArgs {
   // FWD_LS (margin-space line search, direction pass): z_out = zd (in: previous direction, out: new one),
   // z0 = cached margins (materialised here: z0 += tpend * zd_prev), first trial t0 -> (F, D) stats + coef
   double* z0; double t0; double tpend;
+  // FWD_LS inputs: the margins z0 and the previous direction's margins are READ from here (the same buffers as
+  // z0 / z_out for an in-place pass; the other buffer pair of the double-buffered margin cache for a speculative
+  // pass, which must leave the current pair intact in case its line-search step is rejected)
+  const double* z0_in; const double* zd_in;
 };
 
 // Per-row epilogue inputs, prefetched at block start (coalesced, latency hidden behind the stream phase)
@@ -369,7 +373,7 @@ __device__ __forceinline__ RowIn<XT, RT> fwd_prefetch(const FwdArgs<XT, RT>& a, 
   RowIn<XT, RT> r;
   r.y = RT(0); r.off = RT(0); r.wt = RT(0); r.d = XT(0); r.z0 = 0.0; r.zd = 0.0;
   if (a.mode == FWD_MARGIN) { if (a.with_offset) r.off = a.off[s]; }
-  else if (a.mode == FWD_LS) { r.y = a.y[s]; r.wt = a.wt[s]; r.z0 = a.z0[s]; r.zd = a.z_out[s]; }
+  else if (a.mode == FWD_LS) { r.y = a.y[s]; r.wt = a.wt[s]; r.z0 = a.z0_in[s]; r.zd = a.zd_in[s]; }
   else if (a.mode == FWD_HV) { r.d = a.dzz[s]; }
   else { r.y = a.y[s]; r.off = a.off[s]; r.wt = a.wt[s]; }
   return r;
@@ -1316,6 +1320,14 @@ static int g_ablate = 0;      // profiling ablation bits (0 in production)
 // FWD_LS arguments (set by pml_set_ls_args right before a direction pass; host-side, single stream)
 static double* g_ls_z0 = nullptr;
 static double g_ls_t0 = 0.0, g_ls_tpend = 0.0;
+static const double* g_ls_z0_in = nullptr;   // pml_set_ls_in: read-side buffers (null: the output buffers)
+static const double* g_ls_zd_in = nullptr;
+template <typename A>
+static inline A& with_ls_in(A& a) {
+  a.z0_in = g_ls_z0_in ? g_ls_z0_in : g_ls_z0;
+  a.zd_in = g_ls_zd_in ? g_ls_zd_in : a.z_out;
+  return a;
+}
 static int g_tl_acc64 = 1;   // measured on MI355X: ds_add_f64 accumulation is ~3x faster than ds_add_f32 here
 static int g_tl_waves = 4;     // forward
 static int g_tl_waves_t = 4;   // transpose
@@ -2896,6 +2908,61 @@ __global__ __launch_bounds__(NTHREADS) void ls_eval_kernel(int n, double t, int 
 }
 
 
+// Several trial steps of one line search in ONE pass over the rows: F(t_k), D(t_k) for K step lengths (the strong
+// Wolfe search's extrapolation ladder t, 1.5 t, 2.25 t, ... after a first trial that is too short). The rows are
+// read once; every (t_k) sum follows exactly the single-step kernel's grid, per-thread row order, block sum and
+// reduction, so each (F, D) pair is bitwise what ls_eval_kernel returns for that t alone. stats: [K][2 * nb].
+#define LS_MULTI_MAX 6
+struct LsTs { double t[LS_MULTI_MAX]; };
+
+template <typename RT, int K>
+__global__ __launch_bounds__(NTHREADS) void ls_eval_multi_kernel(int n, LsTs ts, int loss,
+                                                                  const double* __restrict__ z0,
+                                                                  const double* __restrict__ zd,
+                                                                  const RT* __restrict__ y, const RT* __restrict__ wt,
+                                                                  double* __restrict__ stats) {
+  __shared__ double sh[2 * NTHREADS / 64];
+  double F[K], D[K];
+#pragma unroll
+  for (int k = 0; k < K; ++k) { F[k] = 0.0; D[k] = 0.0; }
+  const long long stride = (long long)gridDim.x * NTHREADS;
+  constexpr int LU = 4;
+  for (long long i0 = (long long)blockIdx.x * NTHREADS + threadIdx.x; i0 < n; i0 += LU * stride) {
+    double zdv[LU], z0v[LU], yv[LU], wv[LU];
+#pragma unroll
+    for (int u = 0; u < LU; ++u) {
+      const long long i = i0 + u * stride;
+      const bool ok = i < n;
+      zdv[u] = ok ? zd[i] : 0.0;
+      z0v[u] = ok ? z0[i] : 0.0;
+      yv[u] = ok ? static_cast<double>(y[i]) : 0.0;
+      wv[u] = ok ? static_cast<double>(wt[i]) : 0.0;
+    }
+#pragma unroll
+    for (int u = 0; u < LU; ++u) {
+      const long long i = i0 + u * stride;
+      if (i >= n) break;
+      const double w = wv[u];
+#pragma unroll
+      for (int k = 0; k < K; ++k) {
+        const double t = ts.t[k];
+        const double z = z0v[u] + t * zdv[u];
+        double l, dl, d2;
+        pointwise_loss(loss, z, yv[u], l, dl, d2);
+        F[k] += wx(w, l);
+        D[k] += wx(w, dl * zdv[u]);
+      }
+    }
+  }
+  const int nb = gridDim.x;
+#pragma unroll
+  for (int k = 0; k < K; ++k) {
+    double f = F[k], d = D[k];
+    block_sum2(f, d, sh);
+    if (threadIdx.x == 0) { stats[2 * nb * k + 2 * blockIdx.x] = f; stats[2 * nb * k + 2 * blockIdx.x + 1] = d; }
+  }
+}
+
 // ------------------------------------------------------------------------------------------------------------
 // Gram matrix of a few (k <= 22) long fp64 vectors and their linear combination: the vector-free L-BFGS two-loop
 // (optimization/lbfgs.py _History._apply_inverse_gram). The Gram matrix B = V V^T of the k x n basis V is
@@ -3006,6 +3073,38 @@ __device__ __forceinline__ double tl2_block_sum(double v, double* sh) {
 // them in workgroup order (deterministic) and re-arms the counter. Replaces 2 subtractions, 3 dot products
 // (6 launches), a stack and 2 scalar divisions.
 #define PAIR_GRID 1024
+#define PAIR_E 4          // elements per thread per iteration, all loads issued before the first use
+typedef double v2d_p __attribute__((ext_vector_type(2)));
+
+// E consecutive elements from i (zeros past n): 16-byte loads when the whole group is in range and p is 16-byte
+// aligned (wave-uniform test), else element loads.
+template <int E>
+__device__ __forceinline__ void load_e(const double* __restrict__ p, long long i, long long n, double (&v)[E]) {
+  if (i + E <= n && (((uintptr_t)p) & 15) == 0) {
+#pragma unroll
+    for (int j = 0; j < E; j += 2) {
+      const v2d_p q = *(const v2d_p*)(p + i + j);
+      v[j] = q.x;
+      v[j + 1] = q.y;
+    }
+  } else {
+#pragma unroll
+    for (int j = 0; j < E; ++j) v[j] = i + j < n ? p[i + j] : 0.0;
+  }
+}
+
+template <int E>
+__device__ __forceinline__ void store_e(double* __restrict__ p, long long i, long long n, const double (&v)[E]) {
+  if (i + E <= n && (((uintptr_t)p) & 15) == 0) {
+#pragma unroll
+    for (int j = 0; j < E; j += 2) *(v2d_p*)(p + i + j) = v2d_p{v[j], v[j + 1]};
+  } else {
+#pragma unroll
+    for (int j = 0; j < E; ++j)
+      if (i + j < n) p[i + j] = v[j];
+  }
+}
+
 __global__ __launch_bounds__(256) void lbfgs_pair_kernel(const double* __restrict__ x, const double* __restrict__ x0,
                                                          const double* __restrict__ g, const double* __restrict__ g0,
                                                          long long n, double* __restrict__ s, double* __restrict__ y,
@@ -3014,14 +3113,23 @@ __global__ __launch_bounds__(256) void lbfgs_pair_kernel(const double* __restric
   __shared__ double sh[4];
   __shared__ int last;
   double sy = 0.0, yy = 0.0, gg = 0.0;
-  for (long long i = (long long)blockIdx.x * 256 + threadIdx.x; i < n; i += (long long)gridDim.x * 256) {
-    const double gi = g[i];
-    const double si = x[i] - x0[i], yi = gi - g0[i];
-    s[i] = si;
-    y[i] = yi;
-    sy = fma(si, yi, sy);
-    yy = fma(yi, yi, yy);
-    gg = fma(gi, gi, gg);
+  const long long stride = (long long)gridDim.x * 256 * PAIR_E;
+  for (long long i = ((long long)blockIdx.x * 256 + threadIdx.x) * PAIR_E; i < n; i += stride) {
+    double xa[PAIR_E], xb[PAIR_E], ga[PAIR_E], gb[PAIR_E], sv[PAIR_E], yv[PAIR_E];
+    load_e(x, i, n, xa);
+    load_e(x0, i, n, xb);
+    load_e(g, i, n, ga);
+    load_e(g0, i, n, gb);
+#pragma unroll
+    for (int j = 0; j < PAIR_E; ++j) {
+      sv[j] = xa[j] - xb[j];
+      yv[j] = ga[j] - gb[j];
+      sy = fma(sv[j], yv[j], sy);
+      yy = fma(yv[j], yv[j], yy);
+      gg = fma(ga[j], ga[j], gg);
+    }
+    store_e(s, i, n, sv);
+    store_e(y, i, n, yv);
   }
   sy = tl2_block_sum(sy, sh);
   yy = tl2_block_sum(yy, sh);
@@ -3066,12 +3174,19 @@ __global__ __launch_bounds__(256) void ls_dots_kernel(const double* __restrict__
   __shared__ double sh[4];
   __shared__ int last;
   double a = 0.0, b = 0.0, c = 0.0, e = 0.0;
-  for (long long i = (long long)blockIdx.x * 256 + threadIdx.x; i < n; i += (long long)gridDim.x * 256) {
-    const double di = d[i], xi = x0[i];
-    a = fma(g[i], di, a);
-    b = fma(di, di, b);
-    c = fma(xi, xi, c);
-    e = fma(xi, di, e);
+  const long long stride = (long long)gridDim.x * 256 * PAIR_E;
+  for (long long i = ((long long)blockIdx.x * 256 + threadIdx.x) * PAIR_E; i < n; i += stride) {
+    double dv[PAIR_E], xv[PAIR_E], gv[PAIR_E];
+    load_e(d, i, n, dv);
+    load_e(x0, i, n, xv);
+    load_e(g, i, n, gv);
+#pragma unroll
+    for (int j = 0; j < PAIR_E; ++j) {
+      a = fma(gv[j], dv[j], a);
+      b = fma(dv[j], dv[j], b);
+      c = fma(xv[j], xv[j], c);
+      e = fma(xv[j], dv[j], e);
+    }
   }
   a = tl2_block_sum(a, sh);
   b = tl2_block_sum(b, sh);
@@ -3370,7 +3485,7 @@ int pml_two_loop_gram(int k, const double* const* s, const double* const* y, con
 int pml_ls_dots(const double* x0, const double* g, const double* d, long long n, double* partial, unsigned* counter,
                 double* out, void* stream) {
   if (n <= 0) return -22;
-  const int grid = (int)std::min<long long>(PAIR_GRID, (n + 255) / 256);
+  const int grid = (int)std::min<long long>(PAIR_GRID, (n + 256 * PAIR_E - 1) / (256 * PAIR_E));
   hipLaunchKernelGGL(ls_dots_kernel, dim3(grid), dim3(256), 0, (hipStream_t)stream, x0, g, d, n, partial, counter,
                      out);
   LAUNCH_CHECK();
@@ -3382,7 +3497,7 @@ int pml_ls_dots(const double* x0, const double* g, const double* d, long long n,
 int pml_lbfgs_pair(const double* x, const double* x0, const double* g, const double* g0, long long n, double* s,
                    double* y, double* partial, unsigned* counter, double* out, void* stream) {
   if (n <= 0) return -22;
-  const int grid = (int)std::min<long long>(PAIR_GRID, (n + 255) / 256);
+  const int grid = (int)std::min<long long>(PAIR_GRID, (n + 256 * PAIR_E - 1) / (256 * PAIR_E));
   hipLaunchKernelGGL(lbfgs_pair_kernel, dim3(grid), dim3(256), 0, (hipStream_t)stream, x, x0, g, g0, n, s, y, partial,
                      counter, out);
   LAUNCH_CHECK();
@@ -3451,6 +3566,7 @@ int pml_version() { return 1; }
 void pml_tl_set_deep(int fwd, int t) { g_tl_deep = fwd; g_tl_deep_t = t; }
 
 void pml_set_ls_args(double* z0, double t0, double tpend) { g_ls_z0 = z0; g_ls_t0 = t0; g_ls_tpend = tpend; }
+void pml_set_ls_in(const double* z0_in, const double* zd_in) { g_ls_z0_in = z0_in; g_ls_zd_in = zd_in; }
 
 void pml_set_ablate(int a) {
   g_ablate = a;
@@ -3526,12 +3642,12 @@ int pml_seg_fwd(int prec, const SegChunkDesc* c, const void* x, int mode, int lo
   if (prec == 2) {
     FwdArgs<double, double> a{mode, loss, shift, (const double*)y, (const double*)off, (const double*)wt,
                               (double*)coef, (double*)dzz, z_out, with_offset, g_ablate, 0, g_ls_z0, g_ls_t0, g_ls_tpend};
-    return fwd_impl<double, double, double, double>(c, x, a, stats, long_stats, parts, st);
+    return fwd_impl<double, double, double, double>(c, x, with_ls_in(a), stats, long_stats, parts, st);
   }
   FwdArgs<float, float> a{mode, loss, shift, (const float*)y, (const float*)off, (const float*)wt,
                           (float*)coef, (float*)dzz, z_out, with_offset, g_ablate, 0, g_ls_z0, g_ls_t0, g_ls_tpend};
-  if (prec == 1) return fwd_impl<float, float, float, float>(c, x, a, stats, long_stats, parts, st);
-  return fwd_impl<uint16_t, float, float, float>(c, x, a, stats, long_stats, parts, st);
+  if (prec == 1) return fwd_impl<float, float, float, float>(c, x, with_ls_in(a), stats, long_stats, parts, st);
+  return fwd_impl<uint16_t, float, float, float>(c, x, with_ls_in(a), stats, long_stats, parts, st);
 }
 
 
@@ -3583,12 +3699,12 @@ int pml_tl_fwd(int prec, const TLFwdDesc* c, const void* x, int mode, int loss, 
   if (prec == 2) {
     FwdArgs<double, double> a{mode, loss, shift, (const double*)y, (const double*)off, (const double*)wt,
                               (double*)coef, (double*)dzz, z_out, with_offset, g_ablate, 0, g_ls_z0, g_ls_t0, g_ls_tpend};
-    return tl_fwd_impl<double, double, double>(c, x, a, stats, st);
+    return tl_fwd_impl<double, double, double>(c, x, with_ls_in(a), stats, st);
   }
   FwdArgs<float, float> a{mode, loss, shift, (const float*)y, (const float*)off, (const float*)wt,
                           (float*)coef, (float*)dzz, z_out, with_offset, g_ablate, 0, g_ls_z0, g_ls_t0, g_ls_tpend};
-  if (prec == 1) return tl_fwd_impl<float, float, float>(c, x, a, stats, st);
-  return tl_fwd_impl<uint16_t, float, float>(c, x, a, stats, st);
+  if (prec == 1) return tl_fwd_impl<float, float, float>(c, x, with_ls_in(a), stats, st);
+  return tl_fwd_impl<uint16_t, float, float>(c, x, with_ls_in(a), stats, st);
 }
 
 int pml_tl_t(int prec, const TLTDesc* c, const void* x, int square, double* G, double* parts, void* stream) {
@@ -3800,6 +3916,31 @@ int pml_ls_eval(int prec, int n, double t, int loss, double* z0, const double* z
   return 0;
 }
 
+// ls_eval at K <= LS_MULTI_MAX step lengths in one pass: out[2k .. 2k + 1] = (F, D) at ts[k], each bitwise the
+// single-step result. stats: >= K * 2 * 4096 doubles.
+int pml_ls_eval_multi(int prec, int n, int K, const double* ts, int loss, const double* z0, const double* zd,
+                      const void* y, const void* wt, double* stats, double* out, void* stream) {
+  if (n <= 0) return 0;
+  if (K < 1 || K > LS_MULTI_MAX) return (int)hipErrorInvalidValue;
+  hipStream_t st = (hipStream_t)stream;
+  const int nb = (int)std::min<long long>(4096, ((long long)n + 4 * NTHREADS - 1) / (4 * NTHREADS));   // as pml_ls_eval
+  LsTs a;
+  for (int k = 0; k < LS_MULTI_MAX; ++k) a.t[k] = k < K ? ts[k] : 0.0;
+#define LSM(RT_, K_) hipLaunchKernelGGL((ls_eval_multi_kernel<RT_, K_>), dim3(nb), dim3(NTHREADS), 0, st, n, a, loss, \
+                                        z0, zd, (const RT_*)y, (const RT_*)wt, stats)
+#define LSM_K(RT_) switch (K) { case 1: LSM(RT_, 1); break; case 2: LSM(RT_, 2); break; case 3: LSM(RT_, 3); break; \
+                                case 4: LSM(RT_, 4); break; case 5: LSM(RT_, 5); break; default: LSM(RT_, 6); break; }
+  if (prec == 2) { LSM_K(double) } else { LSM_K(float) }
+#undef LSM_K
+#undef LSM
+  LAUNCH_CHECK();
+  for (int k = 0; k < K; ++k) {
+    hipLaunchKernelGGL(reduce_stats_kernel, dim3(1), dim3(NTHREADS), 0, st, stats + 2 * nb * k, nb, out + 2 * k, 0);
+    LAUNCH_CHECK();
+  }
+  return 0;
+}
+
 int pml_segdot(const double* a, const double* b, int mode, const long long* ptr, int nseg, double* out,
                void* stream) {
   if (nseg <= 0) return 0;
@@ -3834,12 +3975,12 @@ int pml_tl_fwd_multi(int prec, const TLFwdMultiDesc* c, const void* x, int mode,
   if (prec == 2) {
     FwdArgs<double, double> a{mode, loss, shift, (const double*)y, (const double*)off, (const double*)wt,
                               (double*)coef, (double*)dzz, z_out, with_offset, 0, 0, g_ls_z0, g_ls_t0, g_ls_tpend};
-    return tl_fwd_multi_impl<double, double, double>(c, x, a, stats, st);
+    return tl_fwd_multi_impl<double, double, double>(c, x, with_ls_in(a), stats, st);
   }
   FwdArgs<float, float> a{mode, loss, shift, (const float*)y, (const float*)off, (const float*)wt,
                           (float*)coef, (float*)dzz, z_out, with_offset, 0, 0, g_ls_z0, g_ls_t0, g_ls_tpend};
-  if (prec == 1) return tl_fwd_multi_impl<float, float, float>(c, x, a, stats, st);
-  return tl_fwd_multi_impl<uint16_t, float, float>(c, x, a, stats, st);
+  if (prec == 1) return tl_fwd_multi_impl<float, float, float>(c, x, with_ls_in(a), stats, st);
+  return tl_fwd_multi_impl<uint16_t, float, float>(c, x, with_ls_in(a), stats, st);
 }
 
 int pml_lds_add_order_probe(const double* v, double* out, int trials, hipStream_t st) {

@@ -129,23 +129,27 @@ OFFSET_SHIFT_CACHE = os.environ.get("PML_OFFSET_SHIFT_CACHE", "1") != "0"
 class VecKey:
     """Identity of the coefficient vector a cached device quantity (margins, w l'') was computed at. The same
     tensor object at the same version matches without touching the device (the optimizer hands the accepted point
-    back unchanged); anything else falls back to a device comparison with a saved copy (one host sync)."""
+    back unchanged); another tensor matches if its values equal the keyed tensor's (one device comparison and host
+    sync), provided the keyed tensor has not been modified in place since (else: no match, the quantity is
+    recomputed). Holds a reference, not a copy: an 8 MB device copy per accepted step at D = 1M was one of the
+    L-BFGS iteration's copy launches."""
 
-    __slots__ = ("copy", "src", "ver")
+    __slots__ = ("src", "ver")
 
     def __init__(self, w: torch.Tensor):
-        self.copy = w.detach().clone()
         self.src = w
         self.ver = w._version
 
     @property
     def shape(self):
-        return self.copy.shape
+        return self.src.shape
 
     def matches(self, w: torch.Tensor) -> bool:
         if w is self.src and w._version == self.ver:
             return True
-        return self.copy.shape == w.shape and bool(torch.equal(self.copy, w.to(self.copy.device, self.copy.dtype)))
+        if self.src._version != self.ver or self.src.shape != w.shape:
+            return False
+        return bool(torch.equal(self.src, w.to(self.src.device, self.src.dtype)))
 
 
 def _window_align(chunk_rows: int, precision: str) -> int:
@@ -615,28 +619,82 @@ class DeviceGLMData(GLMComputable):
         return (key is not None and key[1] == float(shift) and self._z_chain < self.LS_REFRESH
                 and key[0].matches(w_eff))
 
-    def ls_begin(self, w0_eff, shift0, d_eff, d_shift, t0: float = 1.0, loss=None) -> bool:
+    def ls_begin(self, w0_eff, shift0, d_eff, d_shift, t0: float = 1.0, loss=None, alt: bool = False,
+                 stats_out: Optional[torch.Tensor] = None) -> bool:
         """Direction pass (FWD_LS): zd = X d_eff + d_shift, materialises the pending step into z0, and evaluates
-        the first trial t0 (F, D and the speculative gradient input coef = w l'(z(t0)))."""
+        the first trial t0 (F, D and the speculative gradient input coef = w l'(z(t0))).
+
+        ``alt``: a SPECULATIVE pass (L-BFGS plans the next iteration before the current step is validated,
+        ``optimization/lbfgs.py``): the margins are read from the current buffer pair and written to the other
+        one, which becomes current, so :meth:`ls_restore` of an earlier :meth:`ls_checkpoint` gets the untouched
+        pair back. Refused (False, nothing queued) when the margins would first need a forward pass or the layout
+        has no shard-wide launch. ``stats_out``: 2 fp64 device values that receive the first trial's (F, D)."""
         if loss is None:
             return False
         if getattr(self, "z_cache", None) is None:
+            if alt:
+                return False
             self.enable_margin_cache()   # from now on every value+gradient pass also stores its margins
         if not self._z_valid_for(w0_eff, shift0):
+            if alt:
+                return False
             self.fwd_all(self._vec(w0_eff), FWD_MARGIN, 0, shift0, None, None, z_out=self.z_cache, with_offset=1,
                          stats=False)
             self._z_key, self._z_chain, self._tpend = (VecKey(w0_eff), float(shift0)), 0, 0.0
+        if alt:
+            from .native import KERNEL_CONFIG
+            if getattr(self, "_multi", "unset") == "unset":
+                self._build_multi()
+            if (self._multi is None or not KERNEL_CONFIG.get("tl_multi", 1)
+                    or getattr(self, "_masked", None) is not None):
+                return False
         with trace_range("K1' direction pass (margins of d + first trial)"):
-            self.lib.pml_set_ls_args(self.z_cache.data_ptr(), float(t0), float(self._tpend))
-            self.fwd_all(self._vec(d_eff), FWD_LS, loss.loss_id, d_shift, self.coef, None, z_out=self.zd)
-            self.lib.pml_set_ls_args(None, 0.0, 0.0)
+            if alt:
+                zin, din = self.z_cache, self.zd
+                if getattr(self, "_zalt", None) is None:
+                    self._zalt = (torch.empty_like(zin), torch.empty_like(din))
+                zout, dout = self._zalt
+                self.lib.pml_set_ls_in(zin.data_ptr(), din.data_ptr())
+            else:
+                zout, dout = self.z_cache, self.zd
+            self.lib.pml_set_ls_args(zout.data_ptr(), float(t0), float(self._tpend))
+            try:
+                self.fwd_all(self._vec(d_eff), FWD_LS, loss.loss_id, d_shift, self.coef, None, z_out=dout)
+            finally:
+                self.lib.pml_set_ls_args(None, 0.0, 0.0)
+                if alt:
+                    self.lib.pml_set_ls_in(None, None)
+            if alt:
+                self.z_cache, self.zd, self._zalt = zout, dout, (zin, din)
             self._tpend = 0.0
             self._ls_t0 = float(t0)
+            self._coef_stale = False
             # local (F, D) at t0, on the device: read by the first ls_eval (the caller synchronises once, after
             # everything this iteration needs has been queued), copied device-to-device by ls_finish_packed
-            self._ls_t0_dev = self._reduce_stats().clone()
+            if stats_out is None:
+                stats_out = torch.empty(2, dtype=torch.float64, device=self.device)
+            self._ls_t0_dev = self._reduce_stats(stats_out)
             self._ls_t0_host = None
         return True
+
+    _LS_STATE = ("z_cache", "zd", "_zalt", "_tpend", "_ls_t0", "_ls_t0_dev", "_ls_t0_host", "_z_key", "_z_chain",
+                 "_track_u", "_dzz_key", "_dzz_shift", "_coef_stale", "_step_base")
+
+    def ls_checkpoint(self) -> dict:
+        """The margin-space line-search state (which buffer pair is current, the pending step, the cached first
+        trial, the margin key): host references only, no device work. See :meth:`ls_begin` (``alt``)."""
+        return {k: getattr(self, k, None) for k in self._LS_STATE}
+
+    def ls_restore(self, ck: dict, t0_host=None):
+        """Back to a :meth:`ls_checkpoint` (speculative passes queued since then are abandoned: they wrote only the
+        other buffer pair and scratch). The row vector ``coef`` may since have been overwritten, so the first
+        trial's gradient input is recomputed if that step is accepted after all; ``t0_host``: the first trial's
+        (F, D) already read back, so the line search does not read them again."""
+        for k, v in ck.items():
+            setattr(self, k, v)
+        self._coef_stale = True
+        if t0_host is not None and self._ls_t0 is not None:
+            self._ls_t0_host = tuple(float(v) for v in t0_host)
 
     @property
     def _ls_t0_vals(self):
@@ -659,14 +717,36 @@ class DeviceGLMData(GLMComputable):
             f, d = self.ls_out.tolist()
         return f, d
 
+    LS_MULTI_MAX = 6
+
+    def ls_eval_many(self, loss, ts):
+        """:meth:`ls_eval` at several step lengths (<= LS_MULTI_MAX) in one pass over the rows and one readback:
+        list of (F, D), each bitwise the single-step result (``ls_eval_multi_kernel``)."""
+        ts = [float(t) for t in ts]
+        if not (0 < len(ts) <= self.LS_MULTI_MAX) or not self.z_cache.is_cuda:
+            return [self.ls_eval(loss, t) for t in ts]
+        with trace_range("line-search trials (margin space, one pass)"):
+            need = len(ts) * 2 * 4096
+            if getattr(self, "_ls_multi_stats", None) is None or self._ls_multi_stats.numel() < need:
+                self._ls_multi_stats = torch.empty(self.LS_MULTI_MAX * 2 * 4096, dtype=torch.float64,
+                                                   device=self.device)
+            out = torch.empty(2 * len(ts), dtype=torch.float64, device=self.device)
+            arr = (ctypes.c_double * len(ts))(*ts)
+            check(self.lib.pml_ls_eval_multi(self.prec, self.n_rows, len(ts), arr, loss.loss_id,
+                                             self.z_cache.data_ptr(), self.zd.data_ptr(), self.y.data_ptr(),
+                                             self.wt.data_ptr(), self._ls_multi_stats.data_ptr(), out.data_ptr(),
+                                             stream_handle(self.device)), "ls_eval_multi")
+            v = out.tolist()
+        return [(v[2 * k], v[2 * k + 1]) for k in range(len(ts))]
+
     def ls_finish_packed(self, loss, t: float, w_eff, shift, need_s: bool = True, start_reduce=None,
                          nb: int = 0) -> torch.Tensor:
         """Accepted step: gradient input coef = w l'(z(t)) (already there when t is the first trial), then ONLY
         the transpose pass: packed local [G | F | S]. z0 <- z(t) is deferred to the next direction pass."""
         with trace_range("K1 gradient at the accepted step (transpose pass)"):
             out = torch.zeros(self.dim + 2, dtype=torch.float64, device=self.device)
-            if self._ls_t0 is not None and float(t) == self._ls_t0 and not (
-                    self.track_hessian and loss.twice_differentiable):
+            if self._ls_t0 is not None and float(t) == self._ls_t0 and not getattr(self, "_coef_stale", False) \
+                    and not (self.track_hessian and loss.twice_differentiable):
                 out[self.dim] = self._ls_t0_dev[0]
                 if need_s:
                     # one fp64-accumulating reduction over the stored coefficients (no fp64 copy of the row vector)
@@ -697,7 +777,7 @@ class DeviceGLMData(GLMComputable):
         objective's torch epilogue (x0 + t * d, gradient + l2 * x), which it replaces (5 launches -> 1)."""
         from .native import ls_step_grad
         with trace_range("K1 gradient at the accepted step (transpose pass)"):
-            first = (self._ls_t0 is not None and float(t) == self._ls_t0
+            first = (self._ls_t0 is not None and float(t) == self._ls_t0 and not getattr(self, "_coef_stale", False)
                      and not (self.track_hessian and loss.twice_differentiable))
             if first:
                 F = self._ls_t0_dev[0]
@@ -743,8 +823,7 @@ class DeviceGLMData(GLMComputable):
         if not self._z_valid_for(w_eff, shift):
             base = getattr(self, "_step_base", None)
             if (base is not None and base[0] is not None and base[0][1] == float(shift)
-                    and base[0][0].shape == w_eff.shape and base[1] < self.LS_REFRESH
-                    and bool(torch.equal(base[0][0], w_eff.to(base[0][0].device, base[0][0].dtype)))):
+                    and base[1] < self.LS_REFRESH and base[0][0].matches(w_eff)):
                 self._z_key, self._z_chain = base     # rejected trial: z0 still holds the margins at w
             else:
                 self.fwd_all(self._vec(w_eff), FWD_MARGIN, 0, shift, None, None, z_out=self.z_cache, with_offset=1,
@@ -1071,8 +1150,8 @@ class DeviceGLMData(GLMComputable):
         k = torch.arange(self.dim, device=self.device, dtype=torch.float64)
         return float((self.old_of_new.to(torch.float64) * torch.sin(k * 0.618 + 0.1)).sum()) + 1.0
 
-    def _reduce_stats(self) -> torch.Tensor:
-        out = self.out2
+    def _reduce_stats(self, out: Optional[torch.Tensor] = None) -> torch.Tensor:
+        out = self.out2 if out is None else out
         st = stream_handle(self.device)
         check(self.lib.pml_reduce_stats(self.stats.data_ptr(), self.blk_off[-1], out.data_ptr(), 0,
                                         self.red_scratch.data_ptr(), st), "reduce")

@@ -136,6 +136,7 @@ def glm_lib() -> Optional[ctypes.CDLL]:
         lib.pml_btrsv.argtypes = [c_int, c_int, c_void_p, c_void_p, c_void_p, c_int, c_void_p]
         lib.pml_bhv.argtypes = [c_int, c_int, c_void_p, c_void_p, c_void_p, c_double, c_void_p, c_void_p]
         lib.pml_set_ls_args.argtypes = [c_void_p, c_double, c_double]
+        lib.pml_set_ls_in.argtypes = [c_void_p, c_void_p]
         lib.pml_gram_grid.argtypes = [ctypes.c_longlong]
         lib.pml_gram.argtypes = [c_void_p, c_int, ctypes.c_longlong, c_void_p, c_void_p]
         lib.pml_lincomb.argtypes = [c_void_p, c_void_p, c_int, ctypes.c_longlong, c_void_p, c_void_p]
@@ -163,6 +164,9 @@ def glm_lib() -> Optional[ctypes.CDLL]:
         lib.pml_rs_set_variant(int(os.environ.get("PML_RS_VARIANT", "5")))
         lib.pml_ls_eval.argtypes = [c_int, c_int, c_double, c_int, c_void_p, c_void_p, c_void_p, c_void_p, c_int,
                                     c_void_p, c_void_p, c_void_p, c_void_p, c_void_p]
+        lib.pml_ls_eval_multi.argtypes = [c_int, c_int, c_int, ctypes.POINTER(c_double), c_int, c_void_p, c_void_p,
+                                          c_void_p, c_void_p, c_void_p, c_void_p, c_void_p]
+        lib.pml_ls_eval_multi.restype = c_int
         lib.pml_rs_tron.argtypes = [c_int, c_int] + [c_void_p] * 8 + [c_int, c_double, c_double, c_int, c_int, c_int,
                                                                       c_void_p, c_void_p, c_void_p]
         for f in ("pml_seg_fwd", "pml_seg_t", "pml_reduce_stats", "pml_build_blocks", "pml_tl_fwd", "pml_tl_t",
@@ -298,9 +302,10 @@ def lincomb(coefs, vs):
 _PAIR_SCRATCH = {}
 
 
-def lbfgs_pair(x, x0, g, g0):
+def lbfgs_pair(x, x0, g, g0, out=None):
     """New L-BFGS history pair in one launch (``lbfgs_pair_kernel``): returns ``(s, y, out)`` with s = x - x0,
-    y = g - g0 and the device vector out = [s.y, y.y, 1/s.y, s.y/y.y, g.g]; None when the inputs do not qualify."""
+    y = g - g0 and the device vector out = [s.y, y.y, 1/s.y, s.y/y.y, g.g] (written into ``out`` when given: 5
+    contiguous fp64 device values); None when the inputs do not qualify."""
     vs = (x, x0, g, g0)
     if not (x.device.type == "cuda" and all(v.device == x.device and v.dtype == torch.float64 and v.dim() == 1
                                             and v.is_contiguous() and v.numel() == x.numel() for v in vs)
@@ -312,7 +317,9 @@ def lbfgs_pair(x, x0, g, g0):
         sc = _PAIR_SCRATCH[x.device] = (torch.empty(3 * 1024, dtype=torch.float64, device=x.device),
                                         torch.zeros(1, dtype=torch.int32, device=x.device))
     s, y = torch.empty_like(x), torch.empty_like(x)
-    out = torch.empty(5, dtype=torch.float64, device=x.device)
+    if out is None:
+        out = torch.empty(5, dtype=torch.float64, device=x.device)
+    assert out.device == x.device and out.dtype == torch.float64 and out.numel() == 5 and out.is_contiguous()
     check(lib.pml_lbfgs_pair(x.data_ptr(), x0.data_ptr(), g.data_ptr(), g0.data_ptr(), x.numel(), s.data_ptr(),
                              y.data_ptr(), sc[0].data_ptr(), sc[1].data_ptr(), out.data_ptr(),
                              stream_handle(x.device)), "lbfgs_pair")
@@ -347,9 +354,9 @@ def loss_sum(loss_id: int, z: torch.Tensor, y: torch.Tensor, w: torch.Tensor,
 _DOTS_SCRATCH = {}
 
 
-def ls_dots(x0, g, d):
+def ls_dots(x0, g, d, out=None):
     """Device vector [g.d, d.d, x0.x0, x0.d] in one launch (``ls_dots_kernel``, deterministic last-workgroup
-    reduction); None when the inputs do not qualify."""
+    reduction; into ``out`` when given); None when the inputs do not qualify."""
     vs = (x0, g, d)
     if not (d.device.type == "cuda" and all(v.device == d.device and v.dtype == torch.float64 and v.dim() == 1
                                             and v.is_contiguous() and v.numel() == d.numel() for v in vs)
@@ -360,7 +367,9 @@ def ls_dots(x0, g, d):
     if sc is None:
         sc = _DOTS_SCRATCH[d.device] = (torch.empty(4 * 1024, dtype=torch.float64, device=d.device),
                                         torch.zeros(1, dtype=torch.int32, device=d.device))
-    out = torch.empty(4, dtype=torch.float64, device=d.device)
+    if out is None:
+        out = torch.empty(4, dtype=torch.float64, device=d.device)
+    assert out.device == d.device and out.dtype == torch.float64 and out.numel() == 4 and out.is_contiguous()
     check(lib.pml_ls_dots(x0.data_ptr(), g.data_ptr(), d.data_ptr(), d.numel(), sc[0].data_ptr(), sc[1].data_ptr(),
                           out.data_ptr(), stream_handle(d.device)), "ls_dots")
     return out

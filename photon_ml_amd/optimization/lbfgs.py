@@ -49,6 +49,17 @@ SPECULATE_MARGINS = os.environ.get("PML_LBFGS_SPECULATE_MARGINS", "1") != "0"
 # ... only while the last loss drop exceeds this multiple of the loss tolerance (else the iteration likely stops on
 # the tolerance and the queued pass is wasted)
 SPECULATE_LOSS_MARGIN = float(os.environ.get("PML_LBFGS_SPECULATE_LOSS_MARGIN", "20"))
+# Whole-iteration plans: with the margin line search on a device backend, an iteration's direction, its margin pass,
+# the gradient at the first trial step t = 1 and its history pair are queued as one chain, with two readbacks: A
+# (the line-search scalars, right after the margin pass) and B (the pair's scalars). The host validates t = 1 on A
+# while the GPU already runs the speculative gradient pass, queues the NEXT iteration's chain, and only then waits
+# for B: the GPU does not wait for the host between the passes or between iterations. A plan is used only when the
+# strong-Wolfe search accepts t = 1 at its first trial and the pair passes the curvature test -- the decisions the
+# unplanned iteration takes, on the same values, so the iterates are bitwise those of PML_LBFGS_PLAN=0. Otherwise
+# the data backend's margin state is restored (``ls_restore``: a speculative pass writes the other buffer pair) and
+# the iteration runs the ordinary search from the plan's direction pass (a rejected t = 1 wastes one gradient pass).
+PLAN = os.environ.get("PML_LBFGS_PLAN", "1") != "0"
+PLAN_TEST_REJECT = 0        # tests only: treat every n-th planned step as rejected (exercises the fallback)
 # Two-loop as 2k + 1 fused HIP step kernels launched from C++ (no Python between launches); 0: torch recursion
 NATIVE_TWO_LOOP = os.environ.get("PML_LBFGS_NATIVE_TWO_LOOP", "1") != "0"
 # Device two-loop method for replicated vectors: "gram" = vector-free recursion on the device (one Gram pass, the
@@ -77,6 +88,40 @@ def _async_host(t: torch.Tensor):
     ev = torch.cuda.Event()
     ev.record()
     return buf, ev
+
+
+_RING = {}
+
+
+def _pinned_slot(device, n: int = 16) -> torch.Tensor:
+    """A pinned host buffer from a small per-device ring (plan readbacks: at most two plans are outstanding)."""
+    ring = _RING.get(device)
+    if ring is None:
+        ring = _RING[device] = [[torch.empty(n, dtype=torch.float64, pin_memory=True) for _ in range(4)], 0]
+    bufs, i = ring
+    ring[1] = (i + 1) % len(bufs)
+    return bufs[i]
+
+
+class _Plan:
+    """Work queued for the iteration that starts at (x, g): direction ``d``, its line-search dots ``pre`` (device
+    vector or host list) and ``mls``. A DEEP plan (``deep``) also holds the margin search of ``d`` (``mls``: the
+    MarginLineSearch object), the step to t = 1 (``x1``, ``g1``), the history pair (``s``, ``y``, ``out``), the
+    readbacks A = [pre (4), (F, D) of the first trial] (``host`` + ``ev_a``) and B = pair scalars (5) (``host[6:]``
+    + ``ev``), and the data backend's margin state before the plan (``ck_start``), after its direction pass
+    (``ck_fwd``) and after its gradient pass (``ck_fin``). A shallow plan's ``mls`` is (MarginLineSearch, pass
+    count) or None, as before."""
+
+    def __init__(self, x, g, d, pre=None, mls=None):
+        self.x, self.g, self.d, self.pre, self.mls = x, g, d, pre, mls
+        self.deep = False
+        self.data = self.passes = self.host = self.ev = self.ev_a = None
+        self.x1 = self.g1 = self.s = self.y = self.out = None
+        self.ck_start = self.ck_fwd = self.ck_fin = None
+
+
+class _Unplanned(Exception):
+    """The line search wants a trial other than the planned t = 1."""
 
 
 class _History:
@@ -125,13 +170,26 @@ class _History:
         h.rho, h.gamma_t = [0.0] * len(h.s), gamma_t
         return h
 
+    def commit(self, s, y, sy: float, rho_t, gamma_t):
+        """Append a pair whose scalars are known (host s.y; device 1/s.y and s.y/y.y)."""
+        self.s.append(s)
+        self.y.append(y)
+        self.rho.append(1.0 / sy)
+        self.rho_t.append(rho_t)
+        self.gamma_t = gamma_t
+        if len(self.s) > self.m:
+            self.s.pop(0)
+            self.y.pop(0)
+            self.rho.pop(0)
+            self.rho_t.pop(0)
+
     def push_pair(self, x, x0, g, g0, extra: Optional[torch.Tensor] = None, speculate=None):
         """push(x - x0, g - g0); replicated device vectors: the pair and its scalars in ONE kernel
         (``ops.native.lbfgs_pair``) and one host synchronisation for the curvature test, which also returns
         ||g||^2. ``extra``: a 0-d device scalar read in the same synchronisation (the accepted step's loss, left
         on the device by the margin line search). ``speculate(history_with_pair)``: queued before the
-        synchronisation; its result is returned only if the pair is accepted. Returns (pushed, ||g||^2 or None,
-        extra as a float or None, speculation or None)."""
+        synchronisation (its result is returned either way: the caller abandons it when the pair is rejected).
+        Returns (pushed, ||g||^2 or None, extra as a float or None, speculation or None)."""
         if NATIVE_PAIR and _device_loop(g):
             from ..ops.native import lbfgs_pair
             r = lbfgs_pair(x, x0, g, g0)
@@ -149,17 +207,8 @@ class _History:
                 sy, yy, _, _, gg = vals[:5]
                 ex = vals[5] if extra is not None else None
                 if not (sy > 1e-300) or sy != sy:
-                    return False, gg, ex, None
-                self.s.append(s)
-                self.y.append(y)
-                self.rho.append(1.0 / sy)
-                self.rho_t.append(out[2])
-                self.gamma_t = out[3]
-                if len(self.s) > self.m:
-                    self.s.pop(0)
-                    self.y.pop(0)
-                    self.rho.pop(0)
-                    self.rho_t.pop(0)
+                    return False, gg, ex, spec
+                self.commit(s, y, sy, out[2], out[3])
                 return True, gg, ex, spec
         return self.push(x - x0, g - g0), None, (None if extra is None else float(extra)), None
 
@@ -253,19 +302,35 @@ class LBFGS(Optimizer):
         # smooth (un-penalised) value/gradient at the current point, used for the history
         self._smooth_f = None
         self._smooth_g = None
-        self._spec = None        # (x, g, direction, prefetch, margin search) queued for the next iteration
+        self._spec = None        # _Plan queued for the next iteration
         self.wasted_spec_passes = 0   # speculative margin passes queued but never used (diagnostics)
+        self.plans_used = 0           # iterations run from a deep plan (diagnostics)
+        self.plans_rejected = 0       # deep plans whose step the line search did not accept at t = 1
 
     def drop_speculation(self):
         """Forget the work queued for the next iteration (its direction and margin pass): that iteration then
         computes both itself. Benchmarks call this between untimed and timed iterations, so no timed iteration's
         work runs before the timer starts."""
-        self._count_unused_spec()
+        self._abandon(self._spec)
         self._spec = None
 
-    def _count_unused_spec(self):
-        if self._spec is not None and self._spec[4] is not None:
+    def _abandon(self, plan: Optional[_Plan]):
+        """Drop a queued plan. A deep plan's speculative passes moved the data backend's margin state forward:
+        it is restored (unless other passes have run on that data since, which then own the state)."""
+        if plan is None:
+            return
+        if plan.deep or plan.mls is not None:
             self.wasted_spec_passes += 1
+        if plan.deep and plan.data is not None and plan.passes == self._pass_count(plan.data):
+            plan.data.ls_restore(plan.ck_start)
+
+    def is_done(self) -> bool:
+        done = super().is_done()
+        if done and self._spec is not None:
+            # no further iteration: leave the data at the last ACCEPTED point (its cached margins are read next)
+            self._abandon(self._spec)
+            self._spec = None
+        return done
 
     def _margin_speculation_pays(self, state: OptimizerState) -> bool:
         """Whether to queue the next iteration's margin pass during the history push. The pass is wasted when the
@@ -281,7 +346,7 @@ class LBFGS(Optimizer):
 
     def clear_inner_state(self):
         super().clear_inner_state()
-        self._count_unused_spec()
+        self._abandon(self._spec)
         self.history.clear()
         self._failed_once = False
         self._finished = False
@@ -349,6 +414,57 @@ class LBFGS(Optimizer):
         mls = objective.margin_line_search(data, x, d, 1.0, dots=DEFERRED_DOTS)
         return None if mls is None else (mls, self._pass_count(data))
 
+    def _queue_plan(self, objective, data, x, g, h: "_History", with_mls: bool, allow_inplace: bool) -> _Plan:
+        """Queue the iteration that starts at (x, g) with history ``h``: its direction and line-search dots, and
+        (``with_mls``) its margin pass -- as a DEEP plan (also the gradient at t = 1, the history pair and one
+        readback; the pass writes the backend's other margin buffer pair) where the backend supports it, else
+        in place (only when ``allow_inplace``: the current step is already accepted)."""
+        dn = h.apply_inverse(g, negate=True)
+        deep = (PLAN and with_mls and SPECULATE_MARGINS and MARGIN_LINE_SEARCH
+                and callable(getattr(data, "ls_checkpoint", None)) and callable(getattr(data, "ls_finish_fused", None))
+                and hasattr(objective, "margin_line_search")
+                and getattr(objective.normalization, "factors", None) is None
+                and getattr(objective.normalization, "shifts", None) is None
+                and self._pass_count(data) is not None and dn.is_contiguous() and x.is_contiguous())
+        if deep:
+            from ..function.objective import DEFERRED_DOTS
+            from ..ops.native import lbfgs_pair, ls_dots
+            pack = torch.empty(16, dtype=torch.float64, device=g.device)
+            pre = ls_dots(x, g, dn, out=pack[0:4])
+            if pre is not None:
+                plan = _Plan(x, g, dn, pre)
+                plan.ck_start = data.ls_checkpoint()
+                mls = objective.margin_line_search(data, x, dn, 1.0, dots=DEFERRED_DOTS,
+                                                   ls_opts={"alt": True, "stats_out": pack[4:6]})
+                if mls is not None:
+                    plan.ck_fwd = data.ls_checkpoint()
+                    host = _pinned_slot(g.device)
+                    host[:6].copy_(pack[:6], non_blocking=True)          # readback A: pre + first trial
+                    ev_a = torch.cuda.Event()
+                    ev_a.record()
+                    x1, _, g1 = data.ls_finish_fused(objective.loss, 1.0, x, dn, objective.l2_weight)
+                    objective.n_value_grad += 1
+                    r = lbfgs_pair(x1, x, g1, g, out=pack[6:11])
+                    if r is not None:
+                        plan.deep, plan.mls, plan.data = True, mls, data
+                        plan.x1, plan.g1 = x1, g1
+                        plan.s, plan.y, plan.out = r
+                        plan.ck_fin = data.ls_checkpoint()
+                        plan.passes = self._pass_count(data)
+                        plan.host, plan.ev_a = host, ev_a
+                        plan.host[6:11].copy_(pack[6:11], non_blocking=True)   # readback B: pair scalars
+                        plan.ev = torch.cuda.Event()
+                        plan.ev.record()
+                        return plan
+                    data.ls_restore(plan.ck_fwd)
+                    plan.mls = (mls, self._pass_count(data))
+                    return plan
+                if allow_inplace:
+                    plan.mls = self._speculate_margins(objective, data, x, dn)
+                return plan
+        return _Plan(x, g, dn, self._prefetch_of(x, g, dn),
+                     self._speculate_margins(objective, data, x, dn) if with_mls and allow_inplace else None)
+
     def _search(self, objective, data, state: OptimizerState, d: torch.Tensor, pre=None, spec_mls=None):
         """``pre``: host list or device vector from :meth:`_prefetch`. A device vector is read AFTER the margin
         line search has queued its direction pass (iterations > 0: t0 = 1 is known), so the GPU runs that pass
@@ -366,16 +482,16 @@ class LBFGS(Optimizer):
             # a device ``pre`` is read after the direction pass is queued: the L2 dots are assigned then, not
             # recomputed (vdots would cost three reductions and a host synchronisation of their own)
             from ..function.objective import DEFERRED_DOTS
-            if (spec_mls is not None and lazy and t0 == 1.0 and spec_mls[0].x0 is x0 and spec_mls[0].d is d
-                    and spec_mls[1] == self._pass_count(data)):
+            if (spec_mls is not None and pre is not None and t0 == 1.0 and spec_mls[0].x0 is x0
+                    and spec_mls[0].d is d and spec_mls[1] == self._pass_count(data)):
                 mls = spec_mls[0]
             else:
                 mls = objective.margin_line_search(data, x0, d, t0, dots=None if pre is None else
                                                    (DEFERRED_DOTS if lazy else (pre[2], pre[3], pre[1])))
             if lazy:
                 pre = pre.tolist()
-                if mls is not None and mls.l2 > 0:
-                    mls.a, mls.b, mls.c = pre[2], pre[3], pre[1]
+            if mls is not None and mls.l2 > 0 and pre is not None:
+                mls.a, mls.b, mls.c = pre[2], pre[3], pre[1]
         with trace_range("line-search setup"):
             if pre is not None:
                 g0 = pre[0]
@@ -401,15 +517,86 @@ class LBFGS(Optimizer):
     def _run_one_iteration(self, objective, data, state: OptimizerState) -> OptimizerState:
         if self._finished:
             return state
-        from ..utils.timing import trace_range
         spec, self._spec = self._spec, None
-        if spec is not None and not (spec[0] is state.coefficients and spec[1] is state.gradient) and spec[4]:
-            self.wasted_spec_passes += 1
+        use = spec is not None and spec.x is state.coefficients and spec.g is state.gradient
+        if use and spec.deep and not (spec.data is data and spec.passes == self._pass_count(data)):
+            use = False
+        if spec is not None and not use:
+            self._abandon(spec)
+            spec = None
+        if spec is not None and spec.deep:
+            return self._run_planned(objective, data, state, spec)
+        return self._run_unplanned(objective, data, state, spec)
+
+    def _run_planned(self, objective, data, state: OptimizerState, p: _Plan) -> OptimizerState:
+        """One iteration from a deep plan: read its line-search scalars (readback A; the GPU meanwhile runs the
+        speculative gradient pass), take the line search's decision on them; if t = 1 stands, queue the NEXT plan
+        (as if the pair passes), then read the pair's scalars (readback B) and commit, else fall back to the
+        ordinary search."""
+        from ..utils.timing import trace_range
+        with trace_range("plan readback A"):
+            p.ev_a.synchronize()
+            vals = p.host[:6].tolist()
+        pre, F, D = vals[0:4], vals[4], vals[5]
+        mls = p.mls
+        if mls.l2 > 0:
+            mls.a, mls.b, mls.c = pre[2], pre[3], pre[1]
+
+        def first_trial_only(t):
+            if t != 1.0:
+                raise _Unplanned()
+            return (*mls.adjust(F, D, 1.0), None)
+
+        accepted = None
+        self._plans_seen = getattr(self, "_plans_seen", 0) + 1
+        pre_real = pre
+        if PLAN_TEST_REJECT and self._plans_seen % PLAN_TEST_REJECT == 0:
+            pre = pre[:1] + [0.0] + pre[2:]           # forced fallback (the search itself uses the real values)
+        if pre[1] > 0 and pre[0] < 0:
+            try:
+                t, f, _, _ = strong_wolfe(first_trial_only, state.loss, pre[0], 1.0)
+                accepted = f if t == 1.0 else None
+            except (_Unplanned, LineSearchFailed):
+                accepted = None
+        if accepted is None:
+            # the ordinary search from this plan's direction pass (the margins at x and X d are intact)
+            self.plans_rejected += 1
+            data.ls_restore(p.ck_fwd, t0_host=(F, D))
+            return self._run_unplanned(objective, data, state,
+                                       _Plan(p.x, p.g, p.d, pre_real, (mls, self._pass_count(data))))
+        nxt = None
+        with trace_range("plan of the next iteration"):
+            if state.iter + 2 <= self.max_iterations and len(self.history.rho_t) == len(self.history.s):
+                h = self.history._with_pair(p.s, p.y, p.out[2], p.out[3])
+                nxt = self._queue_plan(objective, data, p.x1, p.g1, h, self._margin_speculation_pays(state),
+                                       allow_inplace=False)
+        with trace_range("plan readback B"):
+            p.ev.synchronize()
+            vals = p.host[6:11].tolist()
+        sy, gg = vals[0], vals[4]
+        self.plans_used += 1
+        if not (sy > 1e-300) or sy != sy:
+            # the step stands, the pair does not: the next plan assumed it
+            self._abandon(nxt)
+            nxt = None
+            data.ls_restore(p.ck_fin)
+        else:
+            self.history.commit(p.s, p.y, sy, p.out[2], p.out[3])
+        self._spec = nxt
+        self._failed_once = False
+        self._smooth_f, self._smooth_g = accepted, p.g1
+        self._inner_iter += 1
+        new = OptimizerState(p.x1, accepted, p.g1, state.iter + 1)
+        new._grad_norm = gg ** 0.5
+        return new
+
+    def _run_unplanned(self, objective, data, state: OptimizerState, spec: Optional[_Plan] = None) -> OptimizerState:
+        from ..utils.timing import trace_range
         try:
             with trace_range("two-loop direction"):
                 spec_mls = None
-                if spec is not None and spec[0] is state.coefficients and spec[1] is state.gradient:
-                    d, pre, spec_mls = spec[2], spec[3], spec[4]   # queued during the last history push
+                if spec is not None:
+                    d, pre, spec_mls = spec.d, spec.pre, spec.mls   # queued during the last history push
                 else:
                     d = self._direction(state)
                     pre = self._prefetch(state, d)
@@ -439,16 +626,15 @@ class LBFGS(Optimizer):
                     and state.iter + 2 <= self.max_iterations):         # the next iteration can run
                 # plain L-BFGS: the next state is (x, g) as is (no L1 adjustment, no box projection)
                 with_mls = self._margin_speculation_pays(state)
-                spec_fn = lambda h: (lambda dn: (dn, self._prefetch_of(x, g, dn),
-                                                 self._speculate_margins(objective, data, x, dn)
-                                                 if with_mls else None))(
-                    h.apply_inverse(g, negate=True))
-            _, gg, f_host, nxt = self.history.push_pair(x, state.coefficients, g, self._smooth_g, extra=f_dev,
-                                                        speculate=spec_fn)
+                spec_fn = lambda h: self._queue_plan(objective, data, x, g, h, with_mls, allow_inplace=True)
+            pushed, gg, f_host, nxt = self.history.push_pair(x, state.coefficients, g, self._smooth_g, extra=f_dev,
+                                                             speculate=spec_fn)
             if f_dev is not None:
                 f = f_host
-            if nxt is not None:
-                self._spec = (x, g, nxt[0], nxt[1], nxt[2])
+            if nxt is not None and not pushed:
+                self._abandon(nxt)
+                nxt = None
+            self._spec = nxt
         self._smooth_f, self._smooth_g = f, g
         self._inner_iter += 1
         adj_f, adj_g = self._adjust(x, f, g)

@@ -13,6 +13,9 @@ from __future__ import annotations
 import math
 
 
+EXTRAPOLATION = 1.5     # strong Wolfe: the next trial after a short one is t * EXTRAPOLATION
+
+
 class LineSearchFailed(RuntimeError):
     pass
 
@@ -76,7 +79,7 @@ def strong_wolfe(phi, f0: float, g0: float, t_init: float = 1.0, c1: float = 1e-
         if gt >= 0:
             return zoom(t, ft, gt, pt, t_prev, f_prev, g_prev, p_prev)
         t_prev, f_prev, g_prev, p_prev = t, ft, gt, pt
-        t = t * 1.5
+        t = t * EXTRAPOLATION
     if p_prev is not None and f_prev < f0:
         return t_prev, f_prev, g_prev, p_prev
     raise LineSearchFailed("line search exceeded max iterations")

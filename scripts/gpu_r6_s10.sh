@@ -1,0 +1,21 @@
+#!/bin/bash
+# Round 6 step 10: A/B of the L-BFGS plans and the batched extrapolation ladder on game5pl bf16, + warm FE window.
+set -o pipefail
+R=$GRAFT_REPO_ROOT
+out=$R/gpurun_out/r6s10
+mkdir -p $out
+export TMPDIR=/tmp
+cd $R
+timeout -k 10 300 python -u -m pytest -x -q --timeout 200 --timeout-method thread tests/test_lbfgs_plan_gpu.py > $out/pytest.log 2>&1 || { echo "pytest failed"; tail -40 $out/pytest.log; exit 1; }
+tail -1 $out/pytest.log
+for cfg in "0 1" "1 1" "0 6" "1 6"; do
+  set -- $cfg
+  PML_LBFGS_PLAN=$1 PML_LS_LADDER=$2 timeout -k 10 300 python -u bench_game.py --config game5pl --steps 8 --warmup 3 --precision bf16 > $out/bench_p$1_l$2.json 2> $out/bench_p$1_l$2.log || { echo "bench $cfg failed"; tail -30 $out/bench_p$1_l$2.log; exit 1; }
+  python3 -c "import json; d=json.load(open('$out/bench_p$1_l$2.json')); print('plan $1 ladder $2', round(d['ms_per_step'],2), round(d['sweep_ms_median'],2), {k: round(v,2) for k,v in d['coordinate_ms'].items()}, d.get('fe_lbfgs_plans'))"
+  grep "forward +" $out/bench_p$1_l$2.log | sed 's/.*fixed effect/fixed effect/'
+done
+cd /tmp
+PML_TRACE=1 timeout -k 10 400 rocprofv3 --kernel-trace --marker-trace -d $out/prof -o prof -- python3 $R/scripts/oneshot_profile.py --precisions bf16 > $out/prof_run.md 2> $out/prof_run.log || { echo "prof failed"; tail -30 $out/prof_run.log; exit 1; }
+db=$(find $out/prof -name "*.db" | head -1)
+PML_WIN_INDEX=-1 python3 $R/scripts/prof_window.py "$db" "Update coordinate global" $out/win_fe_warm.md > /dev/null; sed -n 1,40p $out/win_fe_warm.md; grep -A20 "Idle gaps" $out/win_fe_warm.md
+rm -f $db

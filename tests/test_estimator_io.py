@@ -277,3 +277,42 @@ def test_native_model_writer_is_byte_identical(tmp_path, monkeypatch):
         for sub in c.subdirs.values():
             same(sub)
     same(cmp)
+
+
+def test_sorted_factors_match_np_unique():
+    """The random-effect build's entity ids from a factorisation (reader codes / pandas) equal np.unique of the
+    per-row strings; values that print alike (1 and "1") fall back to the per-row path."""
+    from photon_ml_amd.data.random_effect import factorize_ids, sorted_factors
+    rng = np.random.default_rng(3)
+    table = np.array(["u10", "u2", "b", "ä", "u1", "", "zz"], dtype=object)
+    codes = rng.integers(0, len(table), 500)
+    ids = table[codes]
+    u, inv = sorted_factors(codes, table)
+    ru, rinv = np.unique(ids.astype(str), return_inverse=True)
+    assert np.array_equal(u, ru) and np.array_equal(inv, rinv)
+    u, inv = factorize_ids(ids)
+    assert np.array_equal(u, ru) and np.array_equal(inv, rinv)
+    assert factorize_ids(np.array([1, "1", "x"], dtype=object)) is None          # 1 and "1" print alike
+    assert factorize_ids(np.array(["a", None, "b"], dtype=object)) is None       # missing values
+
+
+def test_reader_vocab_map_is_the_sorted_key_map():
+    """The reader's sort-based vocabulary map equals DefaultIndexMap.from_keys(sorted(used keys)) + lookups."""
+    from photon_ml_amd.constants import INTERCEPT_KEY
+    from photon_ml_amd.io.data_reader import _sorted_vocab_map
+    from photon_ml_amd.io.index_map import DefaultIndexMap
+    rng = np.random.default_rng(5)
+    vocab = [f"f{int(v)}\u0001t{int(v) % 3}" for v in rng.permutation(2000)] + ["é\u0001", "Z\u0001", "a b\u0001x"]
+    used = np.sort(rng.choice(len(vocab), 700, replace=False))
+    for icpt in (False, True):
+        im, v2c = _sorted_vocab_map(vocab, used, icpt)
+        ref = DefaultIndexMap.from_keys(sorted(vocab[i] for i in used), add_intercept=icpt)
+        assert im.index_to_key == ref.index_to_key
+        assert np.array_equal(v2c, ref.get_indices(vocab))
+        assert im.get_index(INTERCEPT_KEY) == ref.get_index(INTERCEPT_KEY)
+    # the intercept key present in the data: the dictionary path, same result
+    vocab2 = vocab + [INTERCEPT_KEY]
+    used2 = np.append(used, len(vocab2) - 1)
+    im, v2c = _sorted_vocab_map(vocab2, used2, True)
+    ref = DefaultIndexMap.from_keys(sorted(vocab2[i] for i in used2), add_intercept=True)
+    assert im.index_to_key == ref.index_to_key and np.array_equal(v2c, ref.get_indices(vocab2))

@@ -513,6 +513,7 @@ def test_margin_space_line_search_on_device(precision, monkeypatch):
     from photon_ml_amd.ops.device import DeviceGLMData
     data, _ = generate_glm_data("LOGISTIC_REGRESSION", 20000, 300, density=0.05, seed=9)
     out = {}
+    monkeypatch.setattr(lb, "PLAN", False)     # pass counts of the search itself (a rejected plan wastes one)
     for mode in (False, True):
         monkeypatch.setattr(lb, "MARGIN_LINE_SEARCH", mode)
         dev = DeviceGLMData.from_labeled(data, "cuda", precision, chunk_rows=8192, layout="tiled")
