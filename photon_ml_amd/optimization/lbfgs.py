@@ -58,7 +58,10 @@ SPECULATE_LOSS_MARGIN = float(os.environ.get("PML_LBFGS_SPECULATE_LOSS_MARGIN", 
 # unplanned iteration takes, on the same values, so the iterates are bitwise those of PML_LBFGS_PLAN=0. Otherwise
 # the data backend's margin state is restored (``ls_restore``: a speculative pass writes the other buffer pair) and
 # the iteration runs the ordinary search from the plan's direction pass (a rejected t = 1 wastes one gradient pass).
-PLAN = os.environ.get("PML_LBFGS_PLAN", "1") != "0"
+# Off by default: on game5pl the planned fixed-effect update ran 30.5 instead of 31.5 ms inside a profiled window
+# (97.8 % busy, idle gaps 1.38 -> 0.65 ms), but end to end it was no faster (FE 32.4 / 33.2 vs 32.1 / 32.2 ms bf16,
+# 52.9 vs 52.5 fp64): each rejected t = 1 (6 of 115 plans) wastes a gradient pass (profiles/lbfgs_plans_r6.md).
+PLAN = os.environ.get("PML_LBFGS_PLAN", "0") != "0"
 PLAN_TEST_REJECT = 0        # tests only: treat every n-th planned step as rejected (exercises the fallback)
 # Two-loop as 2k + 1 fused HIP step kernels launched from C++ (no Python between launches); 0: torch recursion
 NATIVE_TWO_LOOP = os.environ.get("PML_LBFGS_NATIVE_TWO_LOOP", "1") != "0"

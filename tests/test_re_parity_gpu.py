@@ -205,3 +205,22 @@ def test_dense_bucket_quad_rows_longer_than_64_match_cpu_tron(monkeypatch):
             w = np.asarray(m.coefficients_of(e).means, dtype=np.float64)
             err = np.abs(w - w_ref).max() / max(np.abs(w_ref).max(), 1e-300)
             assert err < bound, (tol, e, err)
+
+
+def test_row_space_classes_over_two_streams_match_one_stream(monkeypatch):
+    """PML_RS_STREAMS=2 (size classes spread over a second stream, opt-in) solves exactly what the one-stream
+    launch order solves: same kernels on the same inputs, so bitwise equal W and iteration counts; cold and warm
+    (a warm start passes beta0, which the cold start leaves None: record_stream must skip it)."""
+    from photon_ml_amd.optimization import row_space
+    data = make_entities([20] * 30 + [32] * 20 + [48] * 12 + [64] * 8, 150, 12, seed=17)
+    out = {}
+    for ns in (1, 2):
+        monkeypatch.setattr(row_space, "RS_STREAMS", ns)
+        W, its, c, m = gpu_fit(data, 1.0, 1e-8, 30, monkeypatch)
+        W2, its2, _, _ = gpu_fit(data, 1.0, 1e-8, 30, monkeypatch, offsets=np.cos(np.arange(data.n_rows)) * 0.2,
+                                 start=m)
+        out[ns] = (W, its, W2, its2)
+    (a, ia, a2, ia2), (b, ib, b2, ib2) = out[1], out[2]
+    assert ia == ib and ia2 == ib2
+    for e in a:
+        assert np.array_equal(np.asarray(a[e]), np.asarray(b[e])) and np.array_equal(np.asarray(a2[e]), np.asarray(b2[e]))
