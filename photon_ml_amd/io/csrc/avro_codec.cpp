@@ -754,10 +754,33 @@ struct Interner {
   std::vector<Slot> slots;
   size_t mask = 0;
   static uint64_t hash(const char* p, size_t n) {
-    uint64_t h = 1469598103934665603ull;               // FNV-1a, then a final mix
-    for (size_t i = 0; i < n; ++i) { h ^= (unsigned char)p[i]; h *= 1099511628211ull; }
+    // 8 bytes per multiply (the byte-wise FNV-1a loop was ~40 cycles of a ~300-cycle lookup), then a final mix
+    uint64_t h = 0x9E3779B97F4A7C15ull ^ (uint64_t)n;
+    size_t i = 0;
+    for (; i + 8 <= n; i += 8) {
+      uint64_t w;
+      memcpy(&w, p + i, 8);
+      h = (h ^ w) * 0xFF51AFD7ED558CCDull;
+      h ^= h >> 32;
+    }
+    if (i < n) {
+      uint64_t w = 0;
+      memcpy(&w, p + i, n - i);
+      h = (h ^ w) * 0xC4CEB9FE1A85EC53ull;
+    }
     h ^= h >> 29; h *= 0xBF58476D1CE4E5B9ull; h ^= h >> 32;
     return h;
+  }
+  void reserve(size_t n_keys) {                       // slots for n_keys without rehashing on the way
+    size_t cap = 1024;
+    while (cap < 2 * (n_keys + 1)) cap *= 2;
+    keys.reserve(n_keys);
+    if (slots.empty()) {
+      slots.assign(cap, Slot{0, 0, 0, 0});
+      mask = cap - 1;
+      return;
+    }
+    while (slots.size() < cap) grow();
   }
   static uint64_t prefix(const char* p, size_t n) {
     uint64_t v = 0;
@@ -832,10 +855,14 @@ struct ColumnarOpts {
   std::vector<std::string> label_fields;
   std::string weight_field, offset_field, uid_field, metadata_field, delimiter;
   std::vector<std::string> bags_wanted, id_tags;
+  // distinct feature keys of the largest file decoded so far in this call: later files size their interner for it
+  // up front instead of doubling through ~10 rehashes (files of one dataset have similar vocabularies)
+  std::atomic<size_t>* intern_hint = nullptr;
 };
 
 static void decode_columnar_file(const std::string& path, const ColumnarOpts& op, FileCols& fc) {
   OCF o(path);
+  if (op.intern_hint) fc.intern.reserve(op.intern_hint->load());
   const Node* root = o.schema->root;
   if (root->t != AT::RECORD) throw std::runtime_error("top-level Avro schema must be a record: " + path);
   const size_t nf = root->fields.size();
@@ -971,6 +998,10 @@ static void decode_columnar_file(const std::string& path, const ColumnarOpts& op
       ++fc.n;
     }
   }
+  if (op.intern_hint) {
+    size_t cur = op.intern_hint->load();
+    while (fc.intern.keys.size() > cur && !op.intern_hint->compare_exchange_weak(cur, fc.intern.keys.size())) {}
+  }
 }
 
 static py::dict read_columnar(const std::vector<std::string>& paths, const std::vector<std::string>& label_fields,
@@ -978,8 +1009,9 @@ static py::dict read_columnar(const std::vector<std::string>& paths, const std::
                               const std::string& uid_field, const std::string& metadata_field,
                               const std::vector<std::string>& bags_wanted, const std::vector<std::string>& id_tags,
                               const std::string& delimiter, bool tag_strings) {
+  std::atomic<size_t> intern_hint{0};
   ColumnarOpts op{label_fields, weight_field, offset_field, uid_field, metadata_field, delimiter, bags_wanted,
-                  id_tags};
+                  id_tags, &intern_hint};
   const size_t nfile = paths.size();
   // Files are decoded by a worker pool and merged IN FILE ORDER by this thread as soon as each is done (then its
   // columns are freed): decoded-but-unmerged files are bounded by the look-ahead window, so peak host memory is
