@@ -265,8 +265,8 @@ def run(args, dev, rank: int = 0, world: int = 1, data=None, t_data: float = 0.0
         f"{(getattr(fe_gd, 'n_t', 0) - fe_pass0[1]) / args.steps:.1f} transpose passes; sweeps (ms): "
         f"{', '.join(f'{v:.1f}' for v in sweeps_ms)}")
     fe_opt = getattr(getattr(coords["global"], "problem", None), "optimizer", None)
-    fe_plans = {k: getattr(fe_opt, k) for k in ("plans_used", "plans_rejected", "wasted_spec_passes")
-                if hasattr(fe_opt, k)}
+    fe_plans = {k: getattr(fe_opt, k) for k in ("plans_used", "plans_rejected", "wasted_spec_passes", "gated_seen",
+                                                 "gated_used") if hasattr(fe_opt, k)}
     if fe_plans:
         log(f"fixed-effect L-BFGS plans (whole run): {fe_plans}")
     loss = cd.history[-1].get("training_loss")

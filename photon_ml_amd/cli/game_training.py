@@ -192,7 +192,9 @@ class GameDriverBase:
         return []
 
     def read(self, paths, index_maps):
-        return AvroDataReader(self.columns).read(rank_files(paths), self.shard_configs, index_maps, self.id_tags())
+        # training never reports per-record uids (scores are written by game-scoring): skip their strings
+        return AvroDataReader(self.columns).read(rank_files(paths), self.shard_configs, index_maps, self.id_tags(),
+                                                 uids=False)
 
 
 class GameTrainingDriver(GameDriverBase):

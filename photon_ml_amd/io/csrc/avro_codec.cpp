@@ -1013,67 +1013,63 @@ static py::dict read_columnar(const std::vector<std::string>& paths, const std::
   ColumnarOpts op{label_fields, weight_field, offset_field, uid_field, metadata_field, delimiter, bags_wanted,
                   id_tags, &intern_hint};
   const size_t nfile = paths.size();
-  // Files are decoded by a worker pool and merged IN FILE ORDER by this thread as soon as each is done (then its
-  // columns are freed): decoded-but-unmerged files are bounded by the look-ahead window, so peak host memory is
-  // the merged dataset plus ~2 x threads files, not twice the dataset.
+  // Files are decoded by a worker pool. This thread walks them IN FILE ORDER as each is done and takes the only
+  // order-dependent decisions -- global ids of the feature keys and id-tag values (first appearance), every file's
+  // row and entry offsets; the columns themselves are then copied by all threads, each file straight into its slice
+  // of the output arrays (the serial append of round 5 was most of a 10M-record read on 16 threads). A file's
+  // decoded columns are freed once copied.
   std::vector<FileCols> files(nfile);
   std::vector<std::string> errors(nfile);
   std::vector<uint8_t> done(nfile, 0);
   Interner intern;
   int64_t n = 0;
   std::string label_used;
-  std::vector<double> label, weight, offset;
-  std::vector<std::string> uid;
-  std::vector<uint8_t> has_uid;
-  std::vector<std::vector<int32_t>> tags(id_tags.size());
   std::vector<Interner> tag_intern(id_tags.size());
-  std::map<std::string, BagOut> bags;
-  auto merge_one = [&](FileCols& fc) {
+  std::map<std::string, int64_t> bag_total;                  // bag -> entries so far (std::map: sorted output)
+  struct FilePlan {
+    int64_t row0 = 0;
+    std::vector<int32_t> remap;                               // file key id -> global key id
+    std::vector<std::vector<int32_t>> tag_remap;              // per tag: file code -> global code
+    std::map<std::string, int64_t> nnz0;                      // bag -> first entry of this file's slice
+  };
+  std::vector<FilePlan> plan(nfile);
+  auto plan_one = [&](size_t f) {
+    FileCols& fc = files[f];
+    FilePlan& pl = plan[f];
     if (label_used.empty()) label_used = fc.label_used;
-    std::vector<int32_t> remap(fc.intern.keys.size());
-    for (size_t k = 0; k < remap.size(); ++k) remap[k] = intern.get(fc.intern.keys[k]);
-    label.insert(label.end(), fc.label.begin(), fc.label.end());
-    weight.insert(weight.end(), fc.weight.begin(), fc.weight.end());
-    offset.insert(offset.end(), fc.offset.begin(), fc.offset.end());
-    for (auto& x : fc.uid) uid.push_back(std::move(x));
-    has_uid.insert(has_uid.end(), fc.has_uid.begin(), fc.has_uid.end());
-    for (size_t t = 0; t < tags.size(); ++t) {
-      std::vector<int32_t> tr(fc.tag_intern[t].keys.size());
+    pl.row0 = n;
+    pl.remap.resize(fc.intern.keys.size());
+    for (size_t k = 0; k < pl.remap.size(); ++k) pl.remap[k] = intern.get(fc.intern.keys[k]);
+    fc.intern = Interner();                                  // the file's key strings are no longer needed
+    pl.tag_remap.resize(id_tags.size());
+    for (size_t t = 0; t < id_tags.size(); ++t) {
+      auto& tr = pl.tag_remap[t];
+      tr.resize(fc.tag_intern[t].keys.size());
       for (size_t k = 0; k < tr.size(); ++k) tr[k] = tag_intern[t].get(fc.tag_intern[t].keys[k]);
-      for (int32_t c : fc.tags[t]) tags[t].push_back(tr[(size_t)c]);
     }
-    for (auto& b : fc.bags)
-      if (!bags.count(b.first)) bags[b.first].rowptr.assign((size_t)n + 1, 0);   // bag first seen here: empty rows so far
-    for (auto& b : bags) {
-      BagOut& dst = b.second;
+    for (auto& b : fc.bags) bag_total.emplace(b.first, 0);
+    for (auto& b : bag_total) {
+      pl.nnz0[b.first] = b.second;
       auto src = fc.bags.find(b.first);
-      const int64_t base = (int64_t)dst.keys.size();
-      if (src == fc.bags.end()) {
-        dst.rowptr.insert(dst.rowptr.end(), (size_t)fc.n, base);
-        continue;
-      }
-      for (int32_t k : src->second.keys) dst.keys.push_back(remap[(size_t)k]);
-      dst.vals.insert(dst.vals.end(), src->second.vals.begin(), src->second.vals.end());
-      for (size_t r = 1; r < src->second.rowptr.size(); ++r) dst.rowptr.push_back(base + src->second.rowptr[r]);
+      if (src != fc.bags.end()) b.second += (int64_t)src->second.keys.size();
     }
     n += fc.n;
-    FileCols().swap_into(fc);
   };
+  unsigned nt = std::max(1u, std::thread::hardware_concurrency());
+  if (const char* e = std::getenv("PML_AVRO_THREADS")) nt = (unsigned)std::max(1, atoi(e));
   {
     py::gil_scoped_release nogil;
-    unsigned nt = std::max(1u, std::thread::hardware_concurrency());
-    if (const char* e = std::getenv("PML_AVRO_THREADS")) nt = (unsigned)std::max(1, atoi(e));
-    nt = (unsigned)std::min<size_t>(nt, std::max<size_t>(nfile, 1));
-    const size_t ahead = 2 * (size_t)nt;      // files decoded beyond the merge position, at most
+    const unsigned nd = (unsigned)std::min<size_t>(nt, std::max<size_t>(nfile, 1));
+    const size_t ahead = 2 * (size_t)nd;      // files decoded beyond the planning position, at most
     std::mutex mu;
     std::condition_variable cv;
-    size_t next = 0, merged = 0;
+    size_t next = 0, planned = 0;
     auto work = [&]() {
       while (true) {
         size_t f;
         {
           std::unique_lock<std::mutex> lk(mu);
-          cv.wait(lk, [&] { return next >= nfile || next < merged + ahead; });
+          cv.wait(lk, [&] { return next >= nfile || next < planned + ahead; });
           if (next >= nfile) return;
           f = next++;
         }
@@ -1087,7 +1083,7 @@ static py::dict read_columnar(const std::vector<std::string>& paths, const std::
       }
     };
     std::vector<std::thread> pool;
-    for (unsigned t = 0; t < nt; ++t) pool.emplace_back(work);
+    for (unsigned t = 0; t < nd; ++t) pool.emplace_back(work);
     bool failed = false;
     for (size_t f = 0; f < nfile; ++f) {
       {
@@ -1095,11 +1091,11 @@ static py::dict read_columnar(const std::vector<std::string>& paths, const std::
         cv.wait(lk, [&] { return done[f] != 0; });
       }
       if (!errors[f].empty()) failed = true;
-      if (!failed) merge_one(files[f]);
+      if (!failed) plan_one(f);
       else FileCols().swap_into(files[f]);
       {
         std::lock_guard<std::mutex> lk(mu);
-        merged = f + 1;
+        planned = f + 1;
       }
       cv.notify_all();
     }
@@ -1107,37 +1103,100 @@ static py::dict read_columnar(const std::vector<std::string>& paths, const std::
   }
   for (size_t f = 0; f < nfile; ++f)
     if (!errors[f].empty()) throw std::runtime_error(errors[f]);
-  auto arr_d = [](std::vector<double>& v) { return py::array_t<double>((py::ssize_t)v.size(), v.data()); };
+  // output arrays (allocated with the GIL), filled by file in parallel without it
+  py::array_t<double> a_label(n), a_weight(n), a_offset(n);
+  py::array_t<uint8_t> a_has_uid(n);
+  std::vector<py::array_t<int32_t>> a_tags;
+  for (size_t t = 0; t < id_tags.size(); ++t) a_tags.emplace_back(n);
+  struct BagArrays { py::array_t<int64_t> rowptr; py::array_t<int32_t> keys; py::array_t<double> vals; };
+  std::map<std::string, BagArrays> a_bags;
+  for (auto& b : bag_total)
+    a_bags.emplace(b.first, BagArrays{py::array_t<int64_t>(n + 1), py::array_t<int32_t>(b.second),
+                                      py::array_t<double>(b.second)});
+  bool any_uid = false;
+  for (auto& fc : files)
+    for (uint8_t h : fc.has_uid) if (h) { any_uid = true; break; }
+  py::list uid_list(any_uid ? n : 0);
+  if (any_uid) {                                              // Python strings: with the GIL, in order
+    py::ssize_t i = 0;
+    for (auto& fc : files)
+      for (auto& u : fc.uid) uid_list[i++] = py::str(u);
+  }
+  {
+    double* pl_ = a_label.mutable_data();
+    double* pw = a_weight.mutable_data();
+    double* po = a_offset.mutable_data();
+    uint8_t* ph = a_has_uid.mutable_data();
+    std::vector<int32_t*> ptag;
+    for (auto& a : a_tags) ptag.push_back(a.mutable_data());
+    struct BagPtrs { int64_t* rp; int32_t* k; double* v; };
+    std::map<std::string, BagPtrs> pb;
+    for (auto& b : a_bags) pb[b.first] = BagPtrs{b.second.rowptr.mutable_data(), b.second.keys.mutable_data(),
+                                                 b.second.vals.mutable_data()};
+    for (auto& b : pb) b.second.rp[0] = 0;
+    py::gil_scoped_release nogil;
+    std::atomic<size_t> nextf{0};
+    auto fill = [&]() {
+      for (size_t f; (f = nextf.fetch_add(1)) < nfile;) {
+        FileCols& fc = files[f];
+        const FilePlan& pl = plan[f];
+        const int64_t r0 = pl.row0, m = fc.n;
+        if (m) {
+          memcpy(pl_ + r0, fc.label.data(), sizeof(double) * m);
+          memcpy(pw + r0, fc.weight.data(), sizeof(double) * m);
+          memcpy(po + r0, fc.offset.data(), sizeof(double) * m);
+          memcpy(ph + r0, fc.has_uid.data(), m);
+        }
+        for (size_t t = 0; t < ptag.size(); ++t)
+          for (int64_t i = 0; i < m; ++i) ptag[t][r0 + i] = pl.tag_remap[t][(size_t)fc.tags[t][(size_t)i]];
+        for (auto& b : pb) {
+          const int64_t base = pl.nnz0.at(b.first);
+          auto src = fc.bags.find(b.first);
+          if (src == fc.bags.end()) {
+            for (int64_t r = 1; r <= m; ++r) b.second.rp[r0 + r] = base;
+            continue;
+          }
+          const BagOut& bo = src->second;
+          const size_t nk = bo.keys.size();
+          for (size_t q = 0; q < nk; ++q) b.second.k[base + (int64_t)q] = pl.remap[(size_t)bo.keys[q]];
+          if (nk) memcpy(b.second.v + base, bo.vals.data(), sizeof(double) * nk);
+          for (int64_t r = 1; r <= m; ++r) b.second.rp[r0 + r] = base + bo.rowptr[(size_t)r];
+        }
+        FileCols().swap_into(fc);
+      }
+    };
+    std::vector<std::thread> pool;
+    const unsigned nf = (unsigned)std::max<size_t>(1, std::min<size_t>(nt, nfile));
+    for (unsigned t = 1; t < nf; ++t) pool.emplace_back(fill);
+    fill();
+    for (auto& t : pool) t.join();
+  }
   py::dict out;
   out["n"] = n;
   out["label_field"] = label_used;
-  out["label"] = arr_d(label);
-  out["weight"] = arr_d(weight);
-  out["offset"] = arr_d(offset);
-  out["uid"] = py::cast(uid);
-  out["has_uid"] = py::array_t<uint8_t>((py::ssize_t)has_uid.size(), has_uid.data());
+  out["label"] = a_label;
+  out["weight"] = a_weight;
+  out["offset"] = a_offset;
+  out["uid"] = uid_list;
+  out["has_uid"] = a_has_uid;
   py::dict tg, tc;
   for (size_t t = 0; t < id_tags.size(); ++t) {
     // codes into the tag's table of distinct values (first-appearance order); per-record strings on request only
-    tc[py::str(id_tags[t])] = py::make_tuple(py::array_t<int32_t>((py::ssize_t)tags[t].size(), tags[t].data()),
-                                             py::cast(tag_intern[t].keys));
+    tc[py::str(id_tags[t])] = py::make_tuple(a_tags[t], py::cast(tag_intern[t].keys));
     if (tag_strings) {
-      py::list l((py::ssize_t)tags[t].size());
+      const int32_t* codes = a_tags[t].data();
+      py::list l((py::ssize_t)n);
       std::vector<py::str> tab;
       tab.reserve(tag_intern[t].keys.size());
       for (auto& k : tag_intern[t].keys) tab.emplace_back(k);
-      for (size_t i = 0; i < tags[t].size(); ++i) l[(py::ssize_t)i] = tab[(size_t)tags[t][i]];
+      for (int64_t i = 0; i < n; ++i) l[(py::ssize_t)i] = tab[(size_t)codes[i]];
       tg[py::str(id_tags[t])] = l;
     }
   }
   out["id_tags"] = tg;
   out["id_tag_codes"] = tc;
   py::dict bg;
-  for (auto& b : bags) {
-    bg[py::str(b.first)] = py::make_tuple(py::array_t<int64_t>((py::ssize_t)b.second.rowptr.size(), b.second.rowptr.data()),
-                                          py::array_t<int32_t>((py::ssize_t)b.second.keys.size(), b.second.keys.data()),
-                                          py::array_t<double>((py::ssize_t)b.second.vals.size(), b.second.vals.data()));
-  }
+  for (auto& b : a_bags) bg[py::str(b.first)] = py::make_tuple(b.second.rowptr, b.second.keys, b.second.vals);
   out["bags"] = bg;
   out["vocab"] = py::cast(intern.keys);
   return out;

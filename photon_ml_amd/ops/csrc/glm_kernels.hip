@@ -1214,8 +1214,10 @@ __global__ __launch_bounds__(NW * 64) void tl_t_multi_kernel(const int* __restri
                                                               const unsigned long long* __restrict__ ptrs,
                                                               const XT* __restrict__ x, double* __restrict__ G,
                                                               int dim, double* __restrict__ parts,
-                                                              const unsigned char* __restrict__ live) {
+                                                              const unsigned char* __restrict__ live,
+                                                              const int* __restrict__ gate) {
   __shared__ AT acc[NW][MAXR];
+  if (gate && *gate == 0) return;                       // gated pass (pml_set_gate): the step it serves was rejected
   if (live && !live[blockIdx.x]) return;
   const int* q = items + 8 * blockIdx.x;
   const unsigned long long* pc = ptrs + 6 * q[0];
@@ -1320,6 +1322,7 @@ static int g_ablate = 0;      // profiling ablation bits (0 in production)
 // FWD_LS arguments (set by pml_set_ls_args right before a direction pass; host-side, single stream)
 static double* g_ls_z0 = nullptr;
 static double g_ls_t0 = 0.0, g_ls_tpend = 0.0;
+static const int* g_gate = nullptr;           // pml_set_gate: device flag read by the shard-wide transpose launch
 static const double* g_ls_z0_in = nullptr;   // pml_set_ls_in: read-side buffers (null: the output buffers)
 static const double* g_ls_zd_in = nullptr;
 template <typename A>
@@ -1471,7 +1474,7 @@ template <typename VT, typename XT, typename AT, bool SQ, int MAXR>
 static void tl_t_multi_launch(const TLTMultiDesc* c, const void* x, double* G, double* parts, hipStream_t st) {
 #define TLTM(NW, P) hipLaunchKernelGGL((tl_t_multi_kernel<VT, XT, AT, SQ, MAXR, 2, NW, P>), dim3(c->nitems), \
                                        dim3(NW * 64), 0, st, c->items, c->cbits, c->ptrs, (const XT*)x, G, \
-                                       c->dim, parts, c->live)
+                                       c->dim, parts, c->live, g_gate)
   if (c->il) {
     if (TL_WAVES_T == 2) { if (TL_KNOB(g_tl_deep_t) == 2) TLTM(2, 6); else if (TL_KNOB(g_tl_deep_t)) TLTM(2, 5); else TLTM(2, 3); }
     else { if (TL_KNOB(g_tl_deep_t) == 2) TLTM(4, 6); else if (TL_KNOB(g_tl_deep_t)) TLTM(4, 5); else TLTM(4, 3); }
@@ -2963,6 +2966,28 @@ __global__ __launch_bounds__(NTHREADS) void ls_eval_multi_kernel(int n, LsTs ts,
   }
 }
 
+// The strong-Wolfe search's first trial at t = 1 decided ON THE DEVICE, so the gradient pass at the step it would
+// accept can be queued right behind the direction pass, gated on this flag (``gate``; the transpose workgroups exit
+// at once when it is 0): no host round trip between the two passes. pre = [g.d, d.d, x0.x0, x0.d] (ls_dots), fd =
+// (F, D) of the trial (the direction pass's reduction). out = [pre, F, D, accept] for the host, which takes the
+// same decision on the same values (line_search.strong_wolfe) and keeps the gated results only when both agree.
+// Every expression is the host's, in the host's evaluation order, without contraction.
+__global__ void ls_gate_kernel(const double* __restrict__ pre, const double* __restrict__ fd, double f0, double l2,
+                               double c1, double c2, double* __restrict__ out, int* __restrict__ gate) {
+#pragma clang fp contract(off)
+  if (threadIdx.x != 0 || blockIdx.x != 0) return;
+  const double g0 = pre[0], dd = pre[1], a = pre[2], b = pre[3], t = 1.0;
+  double f = fd[0], dphi = fd[1];
+  if (l2 > 0.0) {
+    f = f + 0.5 * l2 * ((a + 2.0 * t * b) + t * t * dd);
+    dphi = dphi + l2 * (b + t * dd);
+  }
+  int acc = 0;
+  if (dd > 0.0 && g0 < 0.0 && isfinite(f) && !(f > f0 + c1 * t * g0) && fabs(dphi) <= -c2 * g0) acc = 1;
+  out[0] = g0; out[1] = dd; out[2] = a; out[3] = b; out[4] = fd[0]; out[5] = fd[1]; out[6] = (double)acc;
+  *gate = acc;
+}
+
 // ------------------------------------------------------------------------------------------------------------
 // Gram matrix of a few (k <= 22) long fp64 vectors and their linear combination: the vector-free L-BFGS two-loop
 // (optimization/lbfgs.py _History._apply_inverse_gram). The Gram matrix B = V V^T of the k x n basis V is
@@ -3548,6 +3573,13 @@ void pml_tl_set_deep(int fwd, int t) { g_tl_deep = fwd; g_tl_deep_t = t; }
 
 void pml_set_ls_args(double* z0, double t0, double tpend) { g_ls_z0 = z0; g_ls_t0 = t0; g_ls_tpend = tpend; }
 void pml_set_ls_in(const double* z0_in, const double* zd_in) { g_ls_z0_in = z0_in; g_ls_zd_in = zd_in; }
+void pml_set_gate(const int* gate) { g_gate = gate; }
+int pml_ls_gate(const double* pre, const double* fd, double f0, double l2, double c1, double c2, double* out,
+                int* gate, void* stream) {
+  hipLaunchKernelGGL(ls_gate_kernel, dim3(1), dim3(64), 0, (hipStream_t)stream, pre, fd, f0, l2, c1, c2, out, gate);
+  LAUNCH_CHECK();
+  return 0;
+}
 
 void pml_set_ablate(int a) {
   g_ablate = a;

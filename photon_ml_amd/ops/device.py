@@ -717,6 +717,34 @@ class DeviceGLMData(GLMComputable):
             f, d = self.ls_out.tolist()
         return f, d
 
+    def ls_gate_supported(self) -> bool:
+        """The gated first-trial finish (:meth:`ls_finish_gated`) needs the shard-wide transpose launch."""
+        from .native import KERNEL_CONFIG
+        if getattr(self, "_multi_t", "unset") == "unset":
+            self._build_multi_t()
+        return (self._multi_t is not None and KERNEL_CONFIG.get("tl_multi", 1) and getattr(self, "_masked", None) is None
+                and getattr(self, "_ls_t0", None) == 1.0 and not getattr(self, "_coef_stale", False)
+                and getattr(self, "_ls_t0_dev", None) is not None and self.z_cache.is_cuda)
+
+    def ls_finish_gated(self, loss, pre: torch.Tensor, f0: float, l2: float, c1: float, c2: float,
+                        x0: torch.Tensor, d: torch.Tensor):
+        """Queue, behind the direction pass, the strong-Wolfe decision on its first trial t = 1
+        (``ls_gate_kernel``) and the accepted-step epilogue of :meth:`ls_finish_fused` at t = 1 with its transpose
+        workgroups gated on that decision: returns ``(scalars, x, F, g)`` with ``scalars`` the 7-vector [pre, F, D,
+        accept] for ONE host readback. The host keeps (x, F, g) only if it accepts t = 1 too; otherwise it restores
+        an :meth:`ls_checkpoint` taken before this call (the gated pass did no work)."""
+        out = torch.empty(8, dtype=torch.float64, device=self.device)
+        gate = torch.empty(1, dtype=torch.int32, device=self.device)
+        check(self.lib.pml_ls_gate(pre.data_ptr(), self._ls_t0_dev.data_ptr(), float(f0), float(l2), float(c1),
+                                   float(c2), out.data_ptr(), gate.data_ptr(), stream_handle(self.device)), "ls_gate")
+        self.lib.pml_set_gate(gate.data_ptr())
+        try:
+            x, F, g = self.ls_finish_fused(loss, 1.0, x0, d, l2)
+        finally:
+            self.lib.pml_set_gate(None)
+        self._gate_keep = gate          # alive until the gated launch has run (stream order)
+        return out, x, F, g
+
     LS_MULTI_MAX = 6
 
     def ls_eval_many(self, loss, ts):

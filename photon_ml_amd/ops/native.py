@@ -137,6 +137,10 @@ def glm_lib() -> Optional[ctypes.CDLL]:
         lib.pml_bhv.argtypes = [c_int, c_int, c_void_p, c_void_p, c_void_p, c_double, c_void_p, c_void_p]
         lib.pml_set_ls_args.argtypes = [c_void_p, c_double, c_double]
         lib.pml_set_ls_in.argtypes = [c_void_p, c_void_p]
+        lib.pml_set_gate.argtypes = [c_void_p]
+        lib.pml_ls_gate.argtypes = [c_void_p, c_void_p, c_double, c_double, c_double, c_double, c_void_p, c_void_p,
+                                    c_void_p]
+        lib.pml_ls_gate.restype = c_int
         lib.pml_gram_grid.argtypes = [ctypes.c_longlong]
         lib.pml_gram.argtypes = [c_void_p, c_int, ctypes.c_longlong, c_void_p, c_void_p]
         lib.pml_lincomb.argtypes = [c_void_p, c_void_p, c_int, ctypes.c_longlong, c_void_p, c_void_p]

@@ -63,6 +63,13 @@ SPECULATE_LOSS_MARGIN = float(os.environ.get("PML_LBFGS_SPECULATE_LOSS_MARGIN", 
 # 52.9 vs 52.5 fp64): each rejected t = 1 (6 of 115 plans) wastes a gradient pass (profiles/lbfgs_plans_r6.md).
 PLAN = os.environ.get("PML_LBFGS_PLAN", "0") != "0"
 PLAN_TEST_REJECT = 0        # tests only: treat every n-th planned step as rejected (exercises the fallback)
+# Gated first-trial finish (iterations > 0, margin line search on a device backend): the strong-Wolfe decision on the
+# first trial t = 1 is also taken on the device, right after the direction pass, and the gradient pass at that step
+# is queued behind it, gated on the decision (its workgroups exit when the step is rejected): the GPU does not wait
+# for the host's round trip between the two passes, and a rejection costs no pass. The host reads [pre, F, D, device
+# decision] once, decides on the same values itself and uses the gated results only when both accept.
+GATED_FINISH = os.environ.get("PML_LBFGS_GATED", "1") != "0"
+GATED_TEST_DISAGREE = False   # tests only: pretend the device rejected every gated step (exercises the restore)
 # Two-loop as 2k + 1 fused HIP step kernels launched from C++ (no Python between launches); 0: torch recursion
 NATIVE_TWO_LOOP = os.environ.get("PML_LBFGS_NATIVE_TWO_LOOP", "1") != "0"
 # Device two-loop method for replicated vectors: "gram" = vector-free recursion on the device (one Gram pass, the
@@ -491,7 +498,15 @@ class LBFGS(Optimizer):
             else:
                 mls = objective.margin_line_search(data, x0, d, t0, dots=None if pre is None else
                                                    (DEFERRED_DOTS if lazy else (pre[2], pre[3], pre[1])))
-            if lazy:
+            if (lazy and mls is not None and t0 == 1.0 and GATED_FINISH and callable(getattr(data, "ls_finish_gated", None))
+                    and callable(getattr(data, "ls_finish_fused", None))
+                    and mls.x0 is x0 and mls.d is d and getattr(objective.normalization, "factors", None) is None
+                    and getattr(objective.normalization, "shifts", None) is None and data.ls_gate_supported()):
+                got = self._gated_first_trial(objective, data, state, mls, pre)
+                if got is not None:
+                    return got
+                pre = self._gated_pre
+            elif lazy:
                 pre = pre.tolist()
             if mls is not None and mls.l2 > 0 and pre is not None:
                 mls.a, mls.b, mls.c = pre[2], pre[3], pre[1]
@@ -516,6 +531,44 @@ class LBFGS(Optimizer):
 
         t, _, _, (x, f, g) = strong_wolfe(phi, state.loss, g0, t0)
         return x, f, g
+
+    def _gated_first_trial(self, objective, data, state: OptimizerState, mls, pre_dev: torch.Tensor):
+        """The gated finish (GATED_FINISH): returns (x, f, g) of the accepted t = 1, or None after restoring the
+        data's line-search state (the search then continues from its first trial; ``self._gated_pre`` holds the
+        host copy of ``pre``)."""
+        from ..function.objective import DEFERRED_DOTS  # noqa: F401  (mls built with deferred dots)
+        from .line_search import strong_wolfe as _sw
+        ck = data.ls_checkpoint()
+        c1, c2 = 1e-4, 0.9
+        vals_t, x1, F1, g1 = data.ls_finish_gated(objective.loss, pre_dev, state.loss, mls.l2, c1, c2, mls.x0, mls.d)
+        vals = vals_t[:7].tolist()
+        pre, F, D, dev_acc = vals[0:4], vals[4], vals[5], vals[6] == 1.0
+        self._gated_pre = pre
+        if mls.l2 > 0:
+            mls.a, mls.b, mls.c = pre[2], pre[3], pre[1]
+
+        def first_trial_only(t):
+            if t != 1.0:
+                raise _Unplanned()
+            return (*mls.adjust(F, D, 1.0), None)
+
+        host_acc = False
+        if pre[1] > 0 and pre[0] < 0:
+            try:
+                t, _, _, _ = _sw(first_trial_only, state.loss, pre[0], 1.0, c1, c2)
+                host_acc = t == 1.0
+            except (_Unplanned, LineSearchFailed):
+                host_acc = False
+        self.gated_seen = getattr(self, "gated_seen", 0) + 1
+        if host_acc and dev_acc and not GATED_TEST_DISAGREE:
+            self.gated_used = getattr(self, "gated_used", 0) + 1
+            objective.n_value_grad += 1
+            f = F1
+            if mls.l2 > 0:
+                f = f + 0.5 * mls.l2 * (mls.a + 2.0 * 1.0 * mls.b + 1.0 * 1.0 * mls.c)
+            return x1, f, g1
+        data.ls_restore(ck, t0_host=(F, D))
+        return None
 
     def _run_one_iteration(self, objective, data, state: OptimizerState) -> OptimizerState:
         if self._finished:

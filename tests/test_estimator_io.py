@@ -153,6 +153,7 @@ def test_parallel_columnar_decode_is_deterministic(tmp_path, monkeypatch):
     from photon_ml_amd.io.data_writer import game_example_schema
     rng = np.random.default_rng(5)
     schema = game_example_schema(["features", "other"])
+    written = []
     for part in range(5):
         recs = []
         for i in range(200 + 37 * part):
@@ -161,6 +162,12 @@ def test_parallel_columnar_decode_is_deterministic(tmp_path, monkeypatch):
                          "features": [{"name": f"f{c}", "term": "t", "value": float(c)} for c in cols],
                          "other": [{"name": f"o{part}", "term": "", "value": 1.0}], "metadataMap": {}})
         avro.write_records(str(tmp_path / f"part-{part}.avro"), schema, recs, codec="snappy" if part % 2 else "deflate")
+        written.extend(recs)
+    # a last file without the "other" bag: its rows have no "other" entries
+    recs = [{"uid": f"x-{i}", "response": 1.0, "weight": 2.0, "offset": 0.5,
+             "features": [{"name": "fz", "term": "", "value": 3.0}], "metadataMap": {}} for i in range(11)]
+    avro.write_records(str(tmp_path / "part-9.avro"), game_example_schema(["features"]), recs)
+    written.extend(recs)
     files = sorted(str(p) for p in tmp_path.iterdir())
     outs = []
     for th in ("1", "4"):
@@ -168,11 +175,20 @@ def test_parallel_columnar_decode_is_deterministic(tmp_path, monkeypatch):
         outs.append(avro.native().read_columnar(files, ["response"], "weight", "offset", "uid", "metadataMap",
                                                 ["features", "other"], [], "\x01"))
     a, b = outs
-    assert a["n"] == b["n"] == sum(200 + 37 * p for p in range(5))
+    assert a["n"] == b["n"] == sum(200 + 37 * p for p in range(5)) + 11
     assert list(a["vocab"]) == list(b["vocab"]) and list(a["uid"]) == list(b["uid"])
     for bag in ("features", "other"):
         for x, y in zip(a["bags"][bag], b["bags"][bag]):
             np.testing.assert_array_equal(x, y)
+    # against the records themselves (row order = file order, first-appearance vocabulary)
+    vocab = list(a["vocab"])
+    assert list(a["uid"]) == [r["uid"] for r in written]
+    np.testing.assert_array_equal(a["weight"], [r["weight"] for r in written])
+    for bag in ("features", "other"):
+        rp, keys, vals = a["bags"][bag]
+        for i, r in enumerate(written):
+            got = [(vocab[k], v) for k, v in zip(keys[rp[i]:rp[i + 1]], vals[rp[i]:rp[i + 1]])]
+            assert got == [(f"{e['name']}\x01{e['term']}", e["value"]) for e in r.get(bag, [])], (bag, i)
 
 
 def test_bags_to_csr_matches_coo_reference():

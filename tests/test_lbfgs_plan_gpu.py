@@ -92,3 +92,51 @@ def test_ls_eval_many_is_bitwise_the_single_trials(precision):
         assert (F, D) == (F1, D1), (t, F, F1, D, D1)
     for k in (1, 3):
         assert data.ls_eval_many(LOGISTIC, ts[:k]) == many[:k]
+
+
+def _fit_gated(monkeypatch, gated, disagree=False, precision="f64"):
+    import photon_ml_amd.optimization.lbfgs as lb
+    monkeypatch.setattr(lb, "GATED_FINISH", gated)
+    monkeypatch.setattr(lb, "GATED_TEST_DISAGREE", disagree)
+    return _fit(monkeypatch, False, precision=precision, warm=True)
+
+
+@pytest.mark.parametrize("precision", ["f64", "bf16"])
+def test_gated_first_trial_finish_is_bitwise_the_host_path(precision, monkeypatch):
+    """The device-decided, gated gradient pass at t = 1 (ls_gate_kernel + gated tl_t_multi) gives bitwise the
+    iterates of the host-decided finish; when the host does not keep the gated results (forced here), restoring the
+    line-search state and searching again matches to rounding (the first trial's gradient input is recomputed)."""
+    ref, _, _ = _fit_gated(monkeypatch, False, precision=precision)
+    got, data, _ = _fit_gated(monkeypatch, True, precision=precision)
+    for (w0, f0, i0, _, _), (w1, f1, i1, _, _) in zip(ref, got):
+        assert i0 == i1 and f0 == f1 and torch.equal(w0, w1)
+    dis, _, _ = _fit_gated(monkeypatch, True, disagree=True, precision=precision)
+    for (w0, f0, i0, _, _), (w1, f1, i1, _, _) in zip(ref, dis):
+        assert i0 == i1 and abs(f0 - f1) <= 1e-12 * abs(f0) and torch.allclose(w0, w1, rtol=1e-9, atol=1e-12)
+
+
+def test_gated_transpose_does_no_work_when_the_gate_is_closed():
+    """pml_set_gate with a 0 flag: the shard-wide transpose leaves its output untouched; with 1 it is the plain
+    pass."""
+    from photon_ml_amd.function.losses import LOGISTIC
+    data = _problem(9)
+    c = torch.randn(data.n_rows, dtype=torch.float64, device="cuda").to(data.coef.dtype)
+    G_ref = torch.zeros(data.dim, dtype=torch.float64, device="cuda")
+    data.t_all(c, G_ref)
+    gate = torch.zeros(1, dtype=torch.int32, device="cuda")
+    for flag in (0, 1):
+        gate.fill_(flag)
+        G = torch.full((data.dim,), 7.0, dtype=torch.float64, device="cuda")
+        if flag:
+            G.zero_()
+        data.parts.zero_()          # (split tiles are combined from this scratch even when no item ran)
+        data.lib.pml_set_gate(gate.data_ptr())
+        try:
+            data.t_all(c, G)
+        finally:
+            data.lib.pml_set_gate(None)
+        torch.cuda.synchronize()
+        if flag:
+            assert torch.equal(G, G_ref)
+        else:
+            assert bool((G == 7.0).all())       # no item ran; the split-tile combine added zeros
