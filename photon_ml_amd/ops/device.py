@@ -730,20 +730,28 @@ class DeviceGLMData(GLMComputable):
                         x0: torch.Tensor, d: torch.Tensor):
         """Queue, behind the direction pass, the strong-Wolfe decision on its first trial t = 1
         (``ls_gate_kernel``) and the accepted-step epilogue of :meth:`ls_finish_fused` at t = 1 with its transpose
-        workgroups gated on that decision: returns ``(scalars, x, F, g)`` with ``scalars`` the 7-vector [pre, F, D,
-        accept] for ONE host readback. The host keeps (x, F, g) only if it accepts t = 1 too; otherwise it restores
+        workgroups gated on that decision: returns ``(scalars, x, F, g)`` with ``scalars`` the host list [pre, F, D,
+        accept] (ONE readback, queued before the gated pass and waited for right after queueing it). The host keeps (x, F, g) only if it accepts t = 1 too; otherwise it restores
         an :meth:`ls_checkpoint` taken before this call (the gated pass did no work)."""
         out = torch.empty(8, dtype=torch.float64, device=self.device)
         gate = torch.empty(1, dtype=torch.int32, device=self.device)
         check(self.lib.pml_ls_gate(pre.data_ptr(), self._ls_t0_dev.data_ptr(), float(f0), float(l2), float(c1),
                                    float(c2), out.data_ptr(), gate.data_ptr(), stream_handle(self.device)), "ls_gate")
+        # the readback is queued BEFORE the gated pass: a blocking copy after it would wait for the whole pass
+        host = getattr(self, "_gate_host", None)
+        if host is None:
+            host = self._gate_host = torch.empty(8, dtype=torch.float64, pin_memory=True)
+        host[:7].copy_(out[:7], non_blocking=True)
+        ev = torch.cuda.Event()
+        ev.record()
         self.lib.pml_set_gate(gate.data_ptr())
         try:
             x, F, g = self.ls_finish_fused(loss, 1.0, x0, d, l2)
         finally:
             self.lib.pml_set_gate(None)
         self._gate_keep = gate          # alive until the gated launch has run (stream order)
-        return out, x, F, g
+        ev.synchronize()
+        return host[:7].tolist(), x, F, g
 
     LS_MULTI_MAX = 6
 

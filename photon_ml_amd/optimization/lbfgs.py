@@ -540,8 +540,7 @@ class LBFGS(Optimizer):
         from .line_search import strong_wolfe as _sw
         ck = data.ls_checkpoint()
         c1, c2 = 1e-4, 0.9
-        vals_t, x1, F1, g1 = data.ls_finish_gated(objective.loss, pre_dev, state.loss, mls.l2, c1, c2, mls.x0, mls.d)
-        vals = vals_t[:7].tolist()
+        vals, x1, F1, g1 = data.ls_finish_gated(objective.loss, pre_dev, state.loss, mls.l2, c1, c2, mls.x0, mls.d)
         pre, F, D, dev_acc = vals[0:4], vals[4], vals[5], vals[6] == 1.0
         self._gated_pre = pre
         if mls.l2 > 0:
