@@ -67,8 +67,10 @@ PLAN_TEST_REJECT = 0        # tests only: treat every n-th planned step as rejec
 # first trial t = 1 is also taken on the device, right after the direction pass, and the gradient pass at that step
 # is queued behind it, gated on the decision (its workgroups exit when the step is rejected): the GPU does not wait
 # for the host's round trip between the two passes, and a rejection costs no pass. The host reads [pre, F, D, device
-# decision] once, decides on the same values itself and uses the gated results only when both accept.
-GATED_FINISH = os.environ.get("PML_LBFGS_GATED", "1") != "0"
+# decision] once, decides on the same values itself and uses the gated results only when both accept. Off by default:
+# bitwise the host-decided iterates, but end to end no faster on game5pl (FE bf16 32.39 / 31.98 vs 32.27 / 31.93 ms,
+# fp64 51.67 vs 52.23; profiles/lbfgs_plans_r6.md).
+GATED_FINISH = os.environ.get("PML_LBFGS_GATED", "0") != "0"
 GATED_TEST_DISAGREE = False   # tests only: pretend the device rejected every gated step (exercises the restore)
 # Two-loop as 2k + 1 fused HIP step kernels launched from C++ (no Python between launches); 0: torch recursion
 NATIVE_TWO_LOOP = os.environ.get("PML_LBFGS_NATIVE_TWO_LOOP", "1") != "0"
