@@ -126,6 +126,11 @@ class FixedEffectCoordinate(Coordinate):
                     gd._build_multi()
                 if getattr(gd, "_multi_t", "unset") == "unset":
                     gd._build_multi_t()
+            if hasattr(gd, "frob_sq"):
+                # ||X||_F^2 (the zero point's gradient bound of every update) depends on the data only: computed with
+                # the layout, not in the first update (it was ~100 small launches of the cold first sweep)
+                with phase(f"FE {coordinate_id} build: Frobenius norm"):
+                    gd.frob_sq()
         self.compute_variance = compute_variance
         self.normalization = normalization
         self.set_config(opt_config)

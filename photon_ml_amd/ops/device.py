@@ -1255,11 +1255,15 @@ class DeviceGLMData(GLMComputable):
         """||X||_F^2 of the shard (sum of the squared stored values, fp64; 0-d device tensor, computed once)."""
         c = getattr(self, "_frob_sq", None)
         if c is None:
-            c = torch.zeros((), dtype=torch.float64, device=self.device)
-            for ch in self.csr:                 # forward copy: every non-zero once (padding entries are 0)
+            # forward copy: every non-zero once (padding entries are 0); one fp64 dot per stream, summed in order
+            parts = []
+            for ch in self.csr:
                 for v in (ch.val, getattr(ch, "nval", None)):
                     if v is not None and v.numel():
-                        c += torch.linalg.vector_norm(v, dtype=torch.float64) ** 2
+                        v64 = v.reshape(-1).to(torch.float64)
+                        parts.append(torch.dot(v64, v64))
+                        del v64
+            c = torch.stack(parts).sum() if parts else torch.zeros((), dtype=torch.float64, device=self.device)
             self._frob_sq = c
         return c
 
