@@ -566,6 +566,11 @@ class RandomEffectCoordinate(Coordinate):
             rest = (~done) & (n_e > 0)
             sub = ds.entity_subset(rest) if bool(rest.any()) else None
             ds.release_csr()
+            # do the three components' coefficient ranges cover the whole packed vector? Then the model's primal
+            # vector needs no zero fill before they write it (each component writes whole entity ranges)
+            cov = 0 if rs is None else int((seg.col_ptr[rs.ents + 1] - seg.col_ptr[rs.ents]).sum())
+            cov += (0 if fused is None else int(fused.cols.numel())) + (0 if sub is None else int(sub.cols.numel()))
+            self._w_covered = cov == int(seg.col_ptr[-1])
         self._comps = (rs, fused, sub)
         self._sub_W = None
         log.debug("RE %s: %d row-space, %d fused primal, %d pass-path entities", self.coordinate_id,
@@ -714,8 +719,8 @@ class RandomEffectCoordinate(Coordinate):
 
         def primal(parts=parts):
             """The primal coefficient vector over all entities (projected keys order)."""
-            W = rs.to_primal(parts["rs"]) if "rs" in parts else torch.zeros(ds.d_total, dtype=torch.float64,
-                                                                                device=dev)
+            W = rs.to_primal(parts["rs"], fill=not getattr(self, "_w_covered", False)) if "rs" in parts else \
+                torch.zeros(ds.d_total, dtype=torch.float64, device=dev)
             if "fused" in parts:
                 W.index_copy_(0, fused.cols, parts["fused"])
             if "sub" in parts:

@@ -431,11 +431,14 @@ __global__ __launch_bounds__(64) void batched_chol_kernel(int B, int n, const lo
 // (d_e doubles), rows in order and the entries of one row on distinct lanes with distinct columns, so every LDS
 // address is updated in a fixed order (deterministic) and no two lanes of one instruction collide. Reads only the
 // handled entities' rows (the shard-wide transpose pass read every entity's).
+// PT: int64 or int32 packed positions (int32 when the packed vector has < 2^31 coefficients: 4 bytes less per entry
+// of a bandwidth-bound pass)
+template <typename PT>
 __global__ __launch_bounds__(64) void rs_primal_kernel(const long long* __restrict__ ents,
                                                        const long long* __restrict__ row_ptr,
                                                        const long long* __restrict__ col_ptr,
                                                        const long long* __restrict__ nip,
-                                                       const long long* __restrict__ pos,
+                                                       const PT* __restrict__ pos,
                                                        const double* __restrict__ val, const double* __restrict__ r,
                                                        double* __restrict__ W) {
   extern __shared__ double acc[];
@@ -451,7 +454,7 @@ __global__ __launch_bounds__(64) void rs_primal_kernel(const long long* __restri
     const double a = r[i];
     const long long k0 = nip[i], k1 = nip[i + 1];
     for (long long k = k0 + lane; k < k1; k += 64) {
-      const int c = (int)(pos[k] - c0);
+      const int c = (int)((long long)pos[k] - c0);
       acc[c] += a * val[k];
     }
     __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
@@ -661,13 +664,19 @@ int pml_batched_chol(int B, int n, const long long* nv, double* K, int* info, vo
 
 // W (packed projected coefficients) of the entities ents[B] = X_e^T r over their rows; dmax = max projected columns
 // of those entities (LDS per wave). Other entities' coefficients are left untouched.
+// pos32: positions are int32 (else int64).
 int pml_rs_primal(int B, int dmax, const long long* ents, const long long* row_ptr, const long long* col_ptr,
-                  const long long* nip, const long long* pos, const double* val, const double* r, double* W,
-                  void* stream) {
+                  const long long* nip, const void* pos, const double* val, const double* r, double* W,
+                  void* stream, int pos32) {
   if (B <= 0) return 0;
   if (dmax < 0 || (size_t)dmax * sizeof(double) > 64 * 1024) return -22;
-  hipLaunchKernelGGL(rs_primal_kernel, dim3((unsigned)B), dim3(64), (size_t)std::max(dmax, 1) * sizeof(double),
-                     (hipStream_t)stream, ents, row_ptr, col_ptr, nip, pos, val, r, W);
+  const size_t lds = (size_t)std::max(dmax, 1) * sizeof(double);
+  if (pos32)
+    hipLaunchKernelGGL(rs_primal_kernel<int>, dim3((unsigned)B), dim3(64), lds, (hipStream_t)stream, ents, row_ptr,
+                       col_ptr, nip, (const int*)pos, val, r, W);
+  else
+    hipLaunchKernelGGL(rs_primal_kernel<long long>, dim3((unsigned)B), dim3(64), lds, (hipStream_t)stream, ents,
+                       row_ptr, col_ptr, nip, (const long long*)pos, val, r, W);
   LAUNCH_CHECK();
   return 0;
 }

@@ -536,18 +536,23 @@ def batched_gemv(A: torch.Tensor, x: torch.Tensor, trans: bool = False) -> torch
     return y
 
 
-def batched_trsv(L: torch.Tensor, x: torch.Tensor, trans: bool = False) -> torch.Tensor:
+def batched_trsv(L: torch.Tensor, x: torch.Tensor, trans: bool = False,
+                 out: Optional[torch.Tensor] = None) -> torch.Tensor:
     """``y[b] = L[b]^-1 x[b]`` (or ``L[b]^-T x[b]``) for a batch of lower-triangular fp64 matrices (n <= 192):
     ``btrsv_kernel`` (one wave per problem, packed triangle in LDS) on the device, ``solve_triangular`` on the
-    host."""
+    host. ``out``: a contiguous [B, n] fp64 tensor to write ``y`` into (not aliasing ``x``)."""
     if L.device.type != "cuda" or L.shape[-1] > 192 or L.shape[-1] != L.shape[-2]:
         M = L.transpose(1, 2) if trans else L
-        return torch.linalg.solve_triangular(M, x.unsqueeze(-1), upper=trans).squeeze(-1)
+        y = torch.linalg.solve_triangular(M, x.unsqueeze(-1), upper=trans).squeeze(-1)
+        return y if out is None else out.copy_(y)
     lib = require_glm_lib()
     L, x = L.contiguous(), x.contiguous()
     B, n, _ = L.shape
     assert L.dtype == torch.float64 and x.dtype == torch.float64 and x.shape == (B, n)
-    y = torch.empty_like(x)
+    if out is not None:
+        assert out.shape == x.shape and out.dtype == torch.float64 and out.is_contiguous() and out.device == x.device
+        assert out.data_ptr() != x.data_ptr()
+    y = torch.empty_like(x) if out is None else out
     check(lib.pml_btrsv(B, n, L.data_ptr(), x.data_ptr(), y.data_ptr(), int(trans), stream_handle(L.device)),
           "btrsv")
     return y
@@ -684,7 +689,7 @@ def game_lib() -> Optional[ctypes.CDLL]:
         lib.pml_batched_chol.argtypes = [c_int, c_int, c_void_p, c_void_p, c_void_p, c_void_p]
         lib.pml_batched_chol.restype = c_int
         lib.pml_seg_gram_set_s.argtypes = [c_int]
-        lib.pml_rs_primal.argtypes = [c_int, c_int] + [c_void_p] * 9
+        lib.pml_rs_primal.argtypes = [c_int, c_int] + [c_void_p] * 9 + [c_int]
         lib.pml_rs_primal.restype = c_int
         lib.pml_csr_gather_rows.argtypes = [c_int, c_void_p, c_void_p, c_void_p, c_void_p, ctypes.c_longlong,
                                             c_void_p, c_void_p, c_void_p, c_void_p, c_void_p]
@@ -840,8 +845,9 @@ def seg_gram(ents: torch.Tensor, n: int, row_ptr: torch.Tensor, col_ptr: torch.T
     if B == 0:
         return K
     t = [x.to(dev).contiguous() for x in (ents, row_ptr, col_ptr, nip, pos)]
-    for x in t:
+    for x in t[:4]:
         assert x.dtype == torch.int64
+    assert t[4].dtype in (torch.int64, torch.int32)
     v = val.to(dev, torch.float64).contiguous()
     if dmax is None or maxnnz is None:
         # widest entity (LDS image) and most non-zeros of one entity (LDS staging of its entries): one readback
@@ -885,7 +891,7 @@ RS_PRIMAL_DMAX = 64 * 1024 // 8     # rs_primal_kernel: one fp64 LDS slot per pr
 
 def rs_primal(ents: torch.Tensor, row_ptr, col_ptr, nip, pos, val, r: torch.Tensor, W: torch.Tensor) -> None:
     """``W[col_ptr[e]:col_ptr[e+1]] = X_e^T r[rows of e]`` for the entities ``ents`` (int64) of a block-diagonal
-    CSR (``nip``/``pos``/``val``: int64 indptr, int64 global columns, fp64 values; columns of an entity inside
+    CSR (``nip``/``pos``/``val``: int64 indptr, int64 or int32 global columns, fp64 values; columns of an entity inside
     its ``col_ptr`` range, distinct inside a row) — ``rs_primal_kernel``, one wave per entity. In place on ``W``
     (fp64, packed like ``col_ptr``); every entity needs ``d_e <= RS_PRIMAL_DMAX``. Device only."""
     lib = require_game_lib()
@@ -894,8 +900,9 @@ def rs_primal(ents: torch.Tensor, row_ptr, col_ptr, nip, pos, val, r: torch.Tens
     if B == 0:
         return
     t = [x.to(dev).contiguous() for x in (ents, row_ptr, col_ptr, nip, pos)]
-    for x in t:
+    for x in t[:4]:
         assert x.dtype == torch.int64
+    assert t[4].dtype in (torch.int64, torch.int32)
     v = val.to(dev, torch.float64).contiguous()
     assert r.dtype == torch.float64 and r.is_contiguous() and W.dtype == torch.float64 and W.is_contiguous()
     assert r.numel() >= int(row_ptr[-1]) and W.numel() >= int(col_ptr[-1])
@@ -903,7 +910,8 @@ def rs_primal(ents: torch.Tensor, row_ptr, col_ptr, nip, pos, val, r: torch.Tens
     if dmax > RS_PRIMAL_DMAX:
         raise ValueError(f"rs_primal: an entity has {dmax} > {RS_PRIMAL_DMAX} projected columns")
     check(lib.pml_rs_primal(B, dmax, t[0].data_ptr(), t[1].data_ptr(), t[2].data_ptr(), t[3].data_ptr(),
-                            t[4].data_ptr(), v.data_ptr(), r.data_ptr(), W.data_ptr(), stream_handle(dev)),
+                            t[4].data_ptr(), v.data_ptr(), r.data_ptr(), W.data_ptr(), stream_handle(dev),
+                            int(t[4].dtype == torch.int32)),
           "rs_primal")
 
 

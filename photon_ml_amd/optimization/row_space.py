@@ -48,12 +48,12 @@ def _bmv(A: torch.Tensor, x: torch.Tensor, trans: bool = False) -> torch.Tensor:
     return batched_gemv(A, x, trans)
 
 
-def _btrsv(L: torch.Tensor, x: torch.Tensor, trans: bool = False) -> torch.Tensor:
+def _btrsv(L: torch.Tensor, x: torch.Tensor, trans: bool = False, out: Optional[torch.Tensor] = None) -> torch.Tensor:
     """Batched triangular solves L^-1 x / L^-T x with the classes' Cholesky factors (HIP kernel on the device). The
     factors are never inverted: an explicit inverse cost O(B n^3) at setup (75 ms for game5pl's n = 80 class) and a
     second n x n matrix per problem in HBM, for products needed only by the primal back-map and foreign warm starts."""
     from ..ops.native import batched_trsv
-    return batched_trsv(L, x, trans)
+    return batched_trsv(L, x, trans, out=out)
 
 
 def _canonical_csr(csr, dev):
@@ -81,7 +81,11 @@ def row_space_eligible(l1: float, constraints=None) -> bool:
 # memory and in the fused kernel's lane group; per class the kernel uses G = pow2 >= n lanes per problem.
 SIZE_CLASSES = (1, 2, 4, 8, 12, 16, 24, 32, 48, 64, 80, 96, 112, 128, 160, 192)
 ROW_SPACE_NMAX = 192      # rs_tron_big_kernel / seg_gram_kernel limit (one wave per problem, packed L in LDS)
-RS_CLASS_DESC = os.environ.get("PML_RS_CLASS_ORDER", "desc") == "desc"
+# class launch order: "desc" widest first; "asc"; "small_first" = classes of n <= RS_SMALL_N first, then widest
+# first (the small classes then never run alone after a concurrent fused primal launch has finished)
+RS_CLASS_ORDER = os.environ.get("PML_RS_CLASS_ORDER", "desc")
+RS_CLASS_DESC = RS_CLASS_ORDER == "desc"
+RS_SMALL_N = int(os.environ.get("PML_RS_SMALL_N", "12"))
 # fused class launches spread over this many streams (the current one + RS_STREAMS - 1 more), classes assigned
 # longest-first to the least-loaded stream by B n^2. Off by default: on game5pl one stream runs ~41 ms of class
 # launches back to back next to the fused primal launch, yet two streams measured slower (RE 44.4-45.0 vs 43.6 ms,
@@ -302,6 +306,8 @@ class RowSpaceBatch:
         torch.cumsum(nk, 0, out=nip_c[1:])
         from ..ops.native import csr_gather_rows
         pos_c, val_c = csr_gather_rows(nip, pos, val, rows, nip_c)       # one gather kernel over the rows
+        if int(seg.col_ptr[-1]) < 2 ** 31:
+            pos_c = pos_c.to(torch.int32)          # 4 bytes less per entry of the (bandwidth-bound) back-map pass
         row_ptr = torch.stack([rcum[:-1], rcum[1:]], 1).reshape(-1)
         col_ptr = torch.stack([c_lo, c_hi], 1).reshape(-1)
         # trailing entries: the wrapper's range checks read the last element as the total
@@ -324,10 +330,22 @@ class RowSpaceBatch:
         z = self._slots(self.seg.glm.matvec(W))
         return torch.cat([_btrsv(c.L, c.view(z)).reshape(-1) for c in self.classes])
 
-    def to_primal(self, beta: torch.Tensor) -> torch.Tensor:
-        """w = X^T L^{-T} beta for the handled entities (zeros elsewhere): one transpose pass."""
-        alpha = torch.cat([_btrsv(c.L, c.view(beta), trans=True).reshape(-1) for c in self.classes]) \
-            if self.classes else None                                                           # L^-T beta
+    def _alpha(self, beta: torch.Tensor) -> Optional[torch.Tensor]:
+        """L^-T beta for every class, written in place into one packed vector (no per-class results and
+        concatenation). The classes' solves run back to back on one stream: spread over four streams they took
+        the same 2.6 ms on game5pl (the batch is throughput-bound, not launch-bound; `profiles/materialize_r6.md`)."""
+        if not self.classes:
+            return None
+        alpha = torch.empty_like(beta)
+        for c in self.classes:
+            _btrsv(c.L, c.view(beta), trans=True, out=c.view(alpha))
+        return alpha
+
+    def to_primal(self, beta: torch.Tensor, fill: bool = True) -> torch.Tensor:
+        """w = X^T L^{-T} beta for the handled entities (zeros elsewhere): one transpose pass. ``fill=False``: the
+        caller writes every coefficient outside the handled entities' ranges itself, so they are left unset (the
+        zero fill of a model-sized vector: 0.8 ms on game5pl's 540M coefficients)."""
+        alpha = self._alpha(beta)                                                               # L^-T beta
         pc = getattr(self, "_primal_csr", None)
         if pc is not None and alpha is not None:
             # per-entity back-map over the handled entities' rows only (rs_primal_kernel, one wave per entity, on
@@ -335,7 +353,8 @@ class RowSpaceBatch:
             # game5pl)
             from ..ops.native import rs_primal
             ents2, row_ptr, col_ptr, nip, pos, val, rows = pc
-            W = torch.zeros(int(self.seg.col_ptr[-1]), dtype=torch.float64, device=beta.device)
+            d_total = int(self.seg.col_ptr[-1])
+            W = (torch.zeros if fill else torch.empty)(d_total, dtype=torch.float64, device=beta.device)
             rs_primal(ents2, row_ptr, col_ptr, nip, pos, val, alpha[self._primal_slot], W)
             return W
         r = torch.zeros(self.seg.y.numel(), dtype=torch.float64, device=beta.device)
@@ -388,8 +407,12 @@ class RowSpaceBatch:
         res_of = {}
         # launch order: the widest classes first (fewest problems, longest per-problem chains: the launches that fill
         # the device worst go where a concurrent fused primal launch fills it, the many-problem classes last)
-        order_c = sorted(range(len(self.classes)), key=lambda i: -self.classes[i].n) if RS_CLASS_DESC else \
-            range(len(self.classes))
+        if RS_CLASS_ORDER == "small_first":
+            order_c = sorted(range(len(self.classes)),
+                             key=lambda i: (self.classes[i].n > RS_SMALL_N, -self.classes[i].n))
+        else:
+            order_c = sorted(range(len(self.classes)), key=lambda i: -self.classes[i].n) if RS_CLASS_DESC else \
+                range(len(self.classes))
         streams = [None]
         if fused and dev.type == "cuda" and RS_STREAMS > 1 and len(self.classes) > 1:
             main = torch.cuda.current_stream(dev)

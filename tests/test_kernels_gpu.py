@@ -979,6 +979,11 @@ def test_rs_primal_backmap_matches_dense_reference():
     W2 = torch.full_like(W, 7.0)
     rs_primal(*args, W2)
     assert torch.equal(W, W2)
+    # int32 packed positions (what the row-space batch keeps when the packed vector has < 2^31 coefficients)
+    args32 = args[:4] + (t(X.indices, torch.int32),) + args[5:]
+    W3 = torch.full_like(W, 7.0)
+    rs_primal(*args32, W3)
+    assert torch.equal(W, W3)
 
 
 @pytest.mark.parametrize("dtype", [torch.int32, torch.int64])
