@@ -107,12 +107,12 @@ __device__ __forceinline__ double uniform_f64(double v) {
 // Workgroup sums of K values (K <= 8), in every thread. ``red`` holds two [RE_NW][8] slots used alternately,
 // so one barrier per call suffices: a slot is rewritten only two calls later, after every thread has passed
 // the barrier of the call in between (all threads run the same, workgroup-uniform control flow).
-template <int K>
+template <int K, int NW = RE_NW>
 __device__ __forceinline__ void block_sums(double (&v)[K], double* __restrict__ red, int& parity) {
   const int lane = threadIdx.x & 63, w = threadIdx.x >> 6;
 #pragma unroll
   for (int k = 0; k < K; ++k) v[k] = wave_total(v[k]);
-  double* slot = red + parity * (RE_NW * 8);
+  double* slot = red + parity * (NW * 8);
   if (lane == 0) {
 #pragma unroll
     for (int k = 0; k < K; ++k) slot[w * 8 + k] = v[k];
@@ -122,7 +122,7 @@ __device__ __forceinline__ void block_sums(double (&v)[K], double* __restrict__ 
   for (int k = 0; k < K; ++k) {
     double s = 0.0;
 #pragma unroll
-    for (int q = 0; q < RE_NW; ++q) s += slot[q * 8 + k];
+    for (int q = 0; q < NW; ++q) s += slot[q * 8 + k];
     v[k] = uniform_f64(s);      // identical in every thread
   }
   parity ^= 1;
@@ -185,7 +185,7 @@ __device__ __forceinline__ double row16_total(double v) {
 // MODE 0: Hessian-vector data term: acc_w += X^T (Dc * (X vec)).
 // MODE 1: value + gradient at vec: acc_w += X^T (wt * l'), fpart += wt * l, Dn = wt * l'', Zn = x.vec.
 // MODE 2: value + gradient at zero (no gathers, no scratch writes).
-template <int MODE, int LOSS, int U = RE_U>
+template <int MODE, int LOSS, int U = RE_U, int NW = RE_NW>
 __device__ __forceinline__ void row_pass(const ReTronArgs& a, long long r0, long long r1,
                                          const double* __restrict__ vec, double* __restrict__ acc,
                                          const double* __restrict__ Dc, double* __restrict__ Dn,
@@ -204,7 +204,7 @@ __device__ __forceinline__ void row_pass(const ReTronArgs& a, long long r0, long
   if (MODE == 0) Dc += r0;
   if (MODE == 1) { Dn += r0; Zn += r0; }
   constexpr int BATCH = RE_RPI * U;
-  const int step = RE_NW * BATCH;
+  const int step = NW * BATCH;
   int base = w * BATCH;
   // row pointers of a batch, prefetched one batch ahead: lane j <= BATCH holds nip[base + j] (clamped to the
   // entity's end). The load is unconditional and its raw value is only converted at its use in the next batch, so
@@ -331,7 +331,7 @@ __device__ __forceinline__ void lds_gather4(const double* vec, int c0, int c1, i
       : "memory");
 }
 
-template <int MODE, int LOSS, int U>
+template <int MODE, int LOSS, int U, int NW = RE_NW>
 __device__ __forceinline__ void row_pass_q(const ReTronArgs& a, long long r0, long long r1,
                                            const double* __restrict__ vec, double* __restrict__ acc,
                                            const double* __restrict__ Dc, double* __restrict__ Dn,
@@ -349,7 +349,7 @@ __device__ __forceinline__ void row_pass_q(const ReTronArgs& a, long long r0, lo
   if (MODE == 0) Dc += r0;
   if (MODE == 1) { Dn += r0; Zn += r0; }
   constexpr int BATCH = RE_RPI * U;
-  const int step = RE_NW * BATCH;
+  const int step = NW * BATCH;
   int base = w * BATCH;
   // row pointers of a batch, in quads: lane j <= BATCH holds nip[base + j] / 4 (prefetched as in row_pass)
   auto fetch_raw = [&](int b) -> long long {
@@ -661,12 +661,17 @@ __global__ __launch_bounds__(RE_THREADS) void re_tron_csr_kernel(ReTronArgs a) {
 // (<= 168 VGPRs, 12 waves per CU) with two row groups per batch in function evaluations (one: same total, the 64
 // largest entities 33.6 instead of 28.1 ms) and three in Hessian-vector passes (four: +15 %); 4 waves per SIMD
 // spills in the row loop (80 ms vs 61 ms for re_tron_csr_kernel)
+// waves per lean workgroup (one entity): an A/B switch of the profiling builds (production: RE_NW)
+#ifndef LEAN_NW
+#define LEAN_NW RE_NW
+#endif
+#define LEAN_THREADS (LEAN_NW * 64)
 // row pass of the lean kernel: quads over padded rows (Q) or the strided row_pass
 template <bool Q, int MODE, int LOSS, int U>
 __device__ __forceinline__ void lean_pass(const ReTronArgs& a, long long r0, long long r1, const double* vec,
                                           double* acc, const double* Dc, double* Dn, double* Zn, double& fpart) {
-  if constexpr (Q) row_pass_q<MODE, LOSS, U>(a, r0, r1, vec, acc, Dc, Dn, Zn, fpart);
-  else row_pass<MODE, LOSS, U>(a, r0, r1, vec, acc, Dc, Dn, Zn, fpart);
+  if constexpr (Q) row_pass_q<MODE, LOSS, U, LEAN_NW>(a, r0, r1, vec, acc, Dc, Dn, Zn, fpart);
+  else row_pass<MODE, LOSS, U, LEAN_NW>(a, r0, r1, vec, acc, Dc, Dn, Zn, fpart);
 }
 #ifndef LEAN_WPE
 #define LEAN_WPE 3
@@ -678,7 +683,7 @@ __device__ __forceinline__ void lean_pass(const ReTronArgs& a, long long r0, lon
 #define LEAN_UH 3
 #endif
 template <int LOSS, int J, bool Q>
-__global__ __launch_bounds__(RE_THREADS) __attribute__((amdgpu_waves_per_eu(LEAN_WPE, LEAN_WPE)))
+__global__ __launch_bounds__(LEAN_THREADS) __attribute__((amdgpu_waves_per_eu(LEAN_WPE, LEAN_WPE)))
 void re_tron_lean_kernel(ReTronArgs a) {
   extern __shared__ __attribute__((aligned(16))) double smem[];
   const int e = __builtin_amdgcn_readfirstlane(a.order[blockIdx.x]);
@@ -688,8 +693,8 @@ void re_tron_lean_kernel(ReTronArgs a) {
   const int tid = threadIdx.x, w = tid >> 6, lane = tid & 63;
   const int dm = a.dmax;
   double* sD = smem;        // CG direction; W / the trial point during a function evaluation
-  double* acc = sD + dm;    // RE_NW accumulators; acc[0 .. d) = combined gradient after a function evaluation
-  double* red = acc + RE_NW * dm;
+  double* acc = sD + dm;    // LEAN_NW accumulators; acc[0 .. d) = combined gradient after a function evaluation
+  double* red = acc + LEAN_NW * dm;
   double* myacc = acc + w * dm;
   double* D[2] = {a.scr, a.scr + a.n_rows};
   double* Z[2] = {a.scr + 2 * a.n_rows, a.scr + 3 * a.n_rows};
@@ -701,7 +706,7 @@ void re_tron_lean_kernel(ReTronArgs a) {
   auto combined = [&](int j) -> double {
     double g = acc[j];
 #pragma unroll
-    for (int q = 1; q < RE_NW; ++q) g += acc[q * dm + j];
+    for (int q = 1; q < LEAN_NW; ++q) g += acc[q * dm + j];
     return g;
   };
   // value + gradient at sD (or at zero); gradient -> acc[0 .. d)
@@ -716,7 +721,7 @@ void re_tron_lean_kernel(ReTronArgs a) {
     double s3[3] = {fp, 0.0, 0.0};
 #pragma unroll
     for (int q = 0; q < J; ++q) {
-      const int j = tid + RE_THREADS * q;
+      const int j = tid + LEAN_THREADS * q;
       if (j < d) {
         const double v = at_zero ? 0.0 : sD[j];
         const double g = combined(j) + a.l2 * v;
@@ -725,14 +730,14 @@ void re_tron_lean_kernel(ReTronArgs a) {
         s3[2] += g * g;
       }
     }
-    block_sums<3>(s3, red, parity);
+    block_sums<3, LEAN_NW>(s3, red, parity);
     gg = s3[2];
     return s3[0] + 0.5 * a.l2 * s3[1];
   };
 
 #pragma unroll
   for (int q = 0; q < J; ++q) {
-    const int j = tid + RE_THREADS * q;
+    const int j = tid + LEAN_THREADS * q;
     if (j < d) sD[j] = Wg[j];
   }
   double gnorm2;
@@ -740,13 +745,13 @@ void re_tron_lean_kernel(ReTronArgs a) {
   double nz[1] = {0.0};
 #pragma unroll
   for (int q = 0; q < J; ++q) {
-    const int j = tid + RE_THREADS * q;
+    const int j = tid + LEAN_THREADS * q;
     if (j < d) {
       Gg[j] = acc[j];
       nz[0] += sD[j] != 0.0 ? 1.0 : 0.0;
     }
   }
-  block_sums<1>(nz, red, parity);
+  block_sums<1, LEAN_NW>(nz, red, parity);
   double f0z = f, g0n = sqrt(gnorm2);
   bool g0_lazy = false;
   if (nz[0] != 0.0) {
@@ -756,14 +761,14 @@ void re_tron_lean_kernel(ReTronArgs a) {
       // norm comes below the bound's tolerance -- then the exact pass at zero runs (convergence decisions are
       // those of the exact norm). No pass over the entity's entries for the common case.
       double s2[2] = {0.0, 0.0};
-      for (long long i = r0 + tid; i < r1; i += RE_THREADS) {
+      for (long long i = r0 + tid; i < r1; i += LEAN_THREADS) {
         double l, dl, d2;
         loss_t<LOSS>(gld(a.off + i), gld(a.y + i), l, dl, d2);
         const double wi = gld(a.wt + i);
         s2[0] += wi * l;
         s2[1] += (wi * dl) * (wi * dl);
       }
-      block_sums<2>(s2, red, parity);
+      block_sums<2, LEAN_NW>(s2, red, parity);
       f0z = s2[0];
       g0n = sqrt(gld(a.xf2 + e) * s2[1]) * (1.0 + 1e-6) + 1e-300;
       g0_lazy = true;
@@ -785,7 +790,7 @@ void re_tron_lean_kernel(ReTronArgs a) {
     // truncated CG at W: one Hessian-vector pass, one combine sweep with the five dot products, one update sweep
 #pragma unroll
     for (int q = 0; q < J; ++q) {
-      const int j = tid + RE_THREADS * q;
+      const int j = tid + LEAN_THREADS * q;
       const double g = j < d ? Gg[j] : 0.0;
       S[q] = 0.0;
       R[q] = -g;
@@ -805,7 +810,7 @@ void re_tron_lean_kernel(ReTronArgs a) {
       double H[J];
 #pragma unroll
       for (int q = 0; q < J; ++q) {
-        const int j = tid + RE_THREADS * q;
+        const int j = tid + LEAN_THREADS * q;
         H[q] = 0.0;
         if (j < d) {
           const double dj = sD[j];
@@ -818,7 +823,7 @@ void re_tron_lean_kernel(ReTronArgs a) {
           s5[4] += h * h;
         }
       }
-      block_sums<5>(s5, red, parity);
+      block_sums<5, LEAN_NW>(s5, red, parity);
       const double dhd = s5[0], std_ = s5[1], dtd = s5[2], rh = s5[3], hh = s5[4];
       const double alpha = rtr / (dhd == 0.0 ? 1.0 : dhd);
       double tn = sts + 2.0 * alpha * std_ + alpha * alpha * dtd;
@@ -837,7 +842,7 @@ void re_tron_lean_kernel(ReTronArgs a) {
       const double beta = rn / (rtr == 0.0 ? 1.0 : rtr);
 #pragma unroll
       for (int q = 0; q < J; ++q) {
-        const int j = tid + RE_THREADS * q;
+        const int j = tid + LEAN_THREADS * q;
         if (j < d) {
           const double dj = sD[j];
           S[q] += al * dj;
@@ -854,7 +859,7 @@ void re_tron_lean_kernel(ReTronArgs a) {
     double s3[3] = {0.0, 0.0, 0.0};
 #pragma unroll
     for (int q = 0; q < J; ++q) {
-      const int j = tid + RE_THREADS * q;
+      const int j = tid + LEAN_THREADS * q;
       if (j < d) {
         const double sj = S[q];
         s3[0] += Gg[j] * sj;
@@ -863,7 +868,7 @@ void re_tron_lean_kernel(ReTronArgs a) {
         sD[j] = Wg[j] + sj;
       }
     }
-    block_sums<3>(s3, red, parity);
+    block_sums<3, LEAN_NW>(s3, red, parity);
     const double gs = s3[0], pred = -0.5 * (gs - s3[1]), snorm = sqrt(s3[2]);
     double gn2;
     const double fn = value_grad(false, cur ^ 1, gn2);   // trial gradient in acc[0 .. d)
@@ -882,7 +887,7 @@ void re_tron_lean_kernel(ReTronArgs a) {
     if (accept) {
 #pragma unroll
       for (int q = 0; q < J; ++q) {
-        const int j = tid + RE_THREADS * q;
+        const int j = tid + LEAN_THREADS * q;
         if (j < d) {
           Wg[j] = sD[j];
           Gg[j] = acc[j];
@@ -914,7 +919,7 @@ void re_tron_lean_kernel(ReTronArgs a) {
   __syncthreads();
   if (a.zout != nullptr) {
     const double* zc = Z[cur];
-    for (long long i = r0 + tid; i < r1; i += RE_THREADS) a.zout[i] = zc[i];
+    for (long long i = r0 + tid; i < r1; i += LEAN_THREADS) a.zout[i] = zc[i];
   }
   if (tid == 0) {
     a.f[e] = f; a.iters[e] = it; a.reason[e] = reason;
@@ -1922,9 +1927,12 @@ __global__ __launch_bounds__(RS_THREADS) void re_tron_res_kernel(ReTronArgs a, R
 
 template <int LOSS, bool Q>
 static void lean_launch(const ReTronArgs& a, int n_launch, size_t smem, hipStream_t st) {
-  if (a.dmax <= 256) hipLaunchKernelGGL((re_tron_lean_kernel<LOSS, 1, Q>), dim3(n_launch), dim3(RE_THREADS), smem, st, a);
-  else if (a.dmax <= 512) hipLaunchKernelGGL((re_tron_lean_kernel<LOSS, 2, Q>), dim3(n_launch), dim3(RE_THREADS), smem, st, a);
-  else hipLaunchKernelGGL((re_tron_lean_kernel<LOSS, 4, Q>), dim3(n_launch), dim3(RE_THREADS), smem, st, a);
+  // J coefficients per thread: the smallest of 1 / 2 / 4 with J x LEAN_THREADS >= dmax (dmax <= 1024)
+  if (a.dmax <= LEAN_THREADS)
+    hipLaunchKernelGGL((re_tron_lean_kernel<LOSS, 1, Q>), dim3(n_launch), dim3(LEAN_THREADS), smem, st, a);
+  else if (a.dmax <= 2 * LEAN_THREADS)
+    hipLaunchKernelGGL((re_tron_lean_kernel<LOSS, 2, Q>), dim3(n_launch), dim3(LEAN_THREADS), smem, st, a);
+  else hipLaunchKernelGGL((re_tron_lean_kernel<LOSS, 4, Q>), dim3(n_launch), dim3(LEAN_THREADS), smem, st, a);
 }
 
 extern "C" {
@@ -1954,7 +1962,7 @@ int pml_re_tron_csr(const int* order, int n_launch, const long long* row_ptr, co
 
 // Lean streaming kernel (dmax <= 1024): LDS (1 + RE_NW) x dmax doubles; ``gsc`` scratch of one double per
 // coefficient (packed like W); W is updated in place.
-size_t pml_re_tron_lean_smem(int dmax) { return ((size_t)(1 + RE_NW) * dmax + 2 * RE_NW * 8) * sizeof(double); }
+size_t pml_re_tron_lean_smem(int dmax) { return ((size_t)(1 + LEAN_NW) * dmax + 2 * LEAN_NW * 8) * sizeof(double); }
 
 int pml_re_tron_lean(const int* order, int n_launch, const long long* row_ptr, const long long* col_ptr,
                      const long long* nip, const uint16_t* lcol, const double* val, const double* y,
