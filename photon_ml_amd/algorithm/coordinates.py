@@ -625,7 +625,9 @@ class RandomEffectCoordinate(Coordinate):
                 rres = rs.solve(self.loss, l2, "TRON", W0, oc.tolerance, oc.maximum_iterations,
                                 reuse_beta=not foreign, prep=prep)
                 _sync(rres.W)
-            return (rres, rs.margins(rres.W),
+            # the handled rows' margins go straight into the update's per-row vector (the fused / pass-path rows
+            # are disjoint), not into a zero vector added afterwards
+            return (rres, rs.margins(rres.W, out=z),
                     torch.where(rs.valid, rres.W, torch.zeros_like(rres.W)).square().sum())
 
         # the row-space and fused solves touch disjoint entities: with both present the row-space kernels run on a
@@ -712,7 +714,8 @@ class RandomEffectCoordinate(Coordinate):
                 self._res_checks = getattr(self, "_res_checks", 0) + (fres.err is not None)
             iters.index_copy_(0, rs.ents, rres.iters)
             reasons.index_copy_(0, rs.ents, rres.reason)
-            z += z_rs
+            if z_rs is not z:
+                z += z_rs
             sum_sq += ss_rs
             parts["rs"] = rres.W
         del W0

@@ -1812,9 +1812,26 @@ __global__ __launch_bounds__(64) void btrsv_kernel(int B, int n, int G, const do
   const long long b0 = (long long)blockIdx.x * P;
   if (b0 >= B) return;
   const int cnt = (int)min((long long)P, B - b0);
-  for (int t = lane; t < cnt * n * n; t += 64) {
-    const int qq = t / (n * n), rem = t - qq * n * n, r = rem / n, c = rem - r * n;
-    if (c <= r) sl[qq * tn + r * (r + 1) / 2 + c] = L[(b0 + qq) * n * n + rem];
+  // stage the lower triangles: BT_UNROLL loads in flight per lane before their LDS stores (one load at a time made
+  // the staging a chain of dependent global-memory round trips: 0.67 ms for 18K problems of n = 64); entries above
+  // the diagonal are not loaded
+  const int nn = n * n, total = cnt * nn;
+  const double* Lb = L + b0 * nn;
+  constexpr int BT_UNROLL = 8;
+  for (int t0 = 0; t0 < total; t0 += 64 * BT_UNROLL) {
+    double v[BT_UNROLL];
+    int dst[BT_UNROLL];
+#pragma unroll
+    for (int k = 0; k < BT_UNROLL; ++k) {
+      const int t = t0 + 64 * k + lane;
+      const int qq = t / nn, rem = t - qq * nn, r = rem / n, c = rem - r * n;
+      const bool on = t < total && c <= r;
+      dst[k] = on ? qq * tn + r * (r + 1) / 2 + c : -1;
+      v[k] = on ? Lb[t] : 0.0;
+    }
+#pragma unroll
+    for (int k = 0; k < BT_UNROLL; ++k)
+      if (dst[k] >= 0) sl[dst[k]] = v[k];
   }
   __syncthreads();
   // reciprocals of the diagonal, once: the n dependent steps then multiply instead of dividing

@@ -1246,7 +1246,10 @@ class DeviceGLMData(GLMComputable):
         forward pass over the non-zeros would only add zeros to the offsets. The reference evaluates this point to
         set its tolerances (Optimizer.scala, Appendix C.7)."""
         n = self.n_rows
-        z0 = self.o[:n].to(torch.float64) + float(margin_shift)
+        o = self.o[:n]
+        # fp64 offsets and no shift: the kernel reads them in place (it never writes z0 / zd)
+        z0 = o if (o.dtype == torch.float64 and float(margin_shift) == 0.0 and o.is_contiguous()) else \
+            o.to(torch.float64) + float(margin_shift)
         check(self.lib.pml_ls_eval(self.prec, n, 0.0, loss.loss_id, z0.data_ptr(), z0.data_ptr(), self.y.data_ptr(),
                                    self.wt.data_ptr(), 1, self.coef.data_ptr(), None, self.ls_stats_buf().data_ptr(),
                                    stats_out.data_ptr(), stream_handle(self.device)), "ls_eval(zero)")

@@ -362,10 +362,11 @@ class RowSpaceBatch:
             r[self.vrow] = alpha[self.vslot]
         return self.seg.glm.rmatvec(r, build_multi=False)     # once per update: no shard-wide tables
 
-    def margins(self, beta: torch.Tensor) -> torch.Tensor:
+    def margins(self, beta: torch.Tensor, out: Optional[torch.Tensor] = None) -> torch.Tensor:
         """Per-row X w (no offsets) of the handled entities = L beta, in the segmented row order (the fused solve's
-        own margins when ``beta`` is its result: no pass over L)."""
-        z = torch.zeros(self.seg.y.numel(), dtype=torch.float64, device=beta.device)
+        own margins when ``beta`` is its result: no pass over L). ``out``: a per-row vector to write the handled
+        rows into (its other rows are left as they are); default a fresh zero vector."""
+        z = torch.zeros(self.seg.y.numel(), dtype=torch.float64, device=beta.device) if out is None else out
         if self._z is not None and self._z[0] is beta:
             zs = self._z[1]
         else:

@@ -386,6 +386,8 @@ def test_batched_trsv_matches_solve_triangular(n, trans):
     ref = torch.linalg.solve_triangular(M, x.unsqueeze(-1), upper=trans).squeeze(-1)
     torch.testing.assert_close(got, ref, rtol=1e-10, atol=1e-10)
     torch.testing.assert_close(torch.bmm(M, got.unsqueeze(-1)).squeeze(-1), x, rtol=1e-9, atol=1e-9)
+    out = torch.full_like(x, float("nan"))
+    assert batched_trsv(L, x, trans, out=out) is out and torch.equal(out, got)      # in place, bitwise
 
 
 _RS_SIZES = [("LOGISTIC", 20), ("POISSON", 7), ("SQUARED", 33), ("LOGISTIC", 64), ("LOGISTIC", 1)]
