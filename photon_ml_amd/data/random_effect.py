@@ -143,6 +143,34 @@ def factorize_ids(ids: np.ndarray) -> Optional[tuple]:
     return sorted_factors(codes, uniq)
 
 
+
+# PML_LAZY_SEG_LAYOUT=0 builds the random-effect coordinate's pass layout eagerly with the dataset (as before round 6)
+LAZY_SEG_LAYOUT = os.environ.get("PML_LAZY_SEG_LAYOUT", "1") != "0"
+
+
+class LazyGLMData:
+    """A GLM pass backend built on first use: any attribute access builds it (once) and delegates. ``built`` tells
+    whether that has happened (without building)."""
+
+    def __init__(self, build):
+        self._build = build
+        self._obj = None
+
+    @property
+    def built(self) -> bool:
+        return self._obj is not None
+
+    def _get(self):
+        if self._obj is None:
+            self._obj = self._build()
+            self._build = None             # drops the closure's references to the CSR inputs
+        return self._obj
+
+    def __getattr__(self, name):
+        if name.startswith("__") or name in ("_build", "_obj"):
+            raise AttributeError(name)
+        return getattr(self._get(), name)
+
 class RandomEffectDataset:
     """Active/passive data of one random-effect coordinate, projected and bucketed."""
 
@@ -498,9 +526,14 @@ class RandomEffectDataset:
         yy = torch.from_numpy(np.asarray(y, dtype=np.float64)).to(dev)[rows_t]
         ww = torch.from_numpy(np.asarray(wts, dtype=np.float64)).to(dev)[rows_t]
         sort_phase.__exit__(None, None, None)
-        with phase("RE segmented: tiled layout"):
-            glm = DeviceGLMData.from_device_csr(nip, pos, val, yy, torch.zeros_like(yy), ww, max(d_total, 1), dev,
-                                                "f64", col_windows=True)
+        # the block-diagonal pass layout (tiled forward / transpose tables) is built on its first use: with the fused
+        # solvers (row space, per-entity primal TRON) a GAME run typically never runs a pass over the whole
+        # coordinate (game5pl: 0.6 s of the 2.0 s build), and the CSR below serves the solver setup
+        def build_glm(nip=nip, pos=pos, val=val, yy=yy, ww=ww, d=max(d_total, 1)):
+            with phase("RE segmented: tiled layout"):
+                return DeviceGLMData.from_device_csr(nip, pos, val, yy, torch.zeros_like(yy), ww, d, dev, "f64",
+                                                     col_windows=True)
+        glm = LazyGLMData(build_glm) if LAZY_SEG_LAYOUT else build_glm()
         self._seg_csr = (nip, pos, val)   # kept until the primal sub-problem is built (entity_subset), then freed
         self.projection_keys_t = ukeys
         self.col_entity_t = ukeys // D

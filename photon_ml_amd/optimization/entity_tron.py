@@ -116,7 +116,11 @@ class EntityTronBatch:
         n_e = seg.row_ptr[1:] - seg.row_ptr[:-1]
         d_e = seg.col_ptr[1:] - seg.col_ptr[:-1]
         # the kernels address an entity's entries with 32-bit offsets from its first entry
-        e_nnz = seg.glm.nnz_per_entity() if hasattr(seg.glm, "nnz_per_entity") else None
+        csr = getattr(ds, "_seg_csr", None)
+        e_nnz = None
+        if csr is not None:
+            nip_all = csr[0].to(dev)
+            e_nnz = nip_all[seg.row_ptr[1:]] - nip_all[seg.row_ptr[:-1]]
         sel = mask.to(dev) & (n_e > 0) & (d_e > 0) & (d_e <= FUSED_DMAX) & (n_e <= FUSED_MAX_ROWS)
         if e_nnz is not None:
             sel &= e_nnz.to(dev) < (1 << 31)
