@@ -205,6 +205,10 @@ def run(args, dev, rank: int = 0, world: int = 1, data=None, t_data: float = 0.0
     from photon_ml_amd.ops.warmup import runtime_warmup
     t_warm = all_reduce_scalar(runtime_warmup(dev), "max")
     t0 = time.time()
+    # as GameEstimator does: the random-effect shard is copied to the device while the GPU builds the fixed-effect
+    # layout (host shards only; placed shards are already device-resident)
+    if hasattr(data, "prefetch_shard"):
+        data.prefetch_shard("entity", dev)
     fe_cfg = GLMOptimizationConfiguration(OptimizerConfig("LBFGS", args.fe_iters, 1e-12),
                                           RegularizationContext("L2"), 1.0, args.fe_down_sampling_rate)
     re_cfg = GLMOptimizationConfiguration(OptimizerConfig("TRON", args.re_iters, 1e-12),

@@ -51,6 +51,55 @@ class GameData:
             raise KeyError(f"feature shard {shard_id} not present (have {sorted(self.shards)})")
         return self.shards[shard_id]
 
+    def prefetch_shard(self, shard_id: str, device) -> bool:
+        """Start copying the host CSR shard ``shard_id`` to ``device`` (int64 row pointers, the column indices, fp64
+        values) on a side stream from a background thread, so the copy overlaps the GPU work queued before the
+        shard's consumer runs (the random-effect build after the fixed-effect layout: the copy is a PCIe transfer,
+        the layout build is device work). :meth:`take_prefetched` hands the arrays over. False when there is
+        nothing to do (no GPU, not a host CSR, already started)."""
+        import threading
+        import torch
+        dev = torch.device(device)
+        pre = self.__dict__.setdefault("_prefetch", {})
+        x = self.shards.get(shard_id)
+        if dev.type != "cuda" or shard_id in pre or not isinstance(x, sp.csr_matrix):
+            return False
+        side = torch.cuda.Stream(dev)
+        out = {}
+
+        def run():
+            try:
+                with torch.cuda.device(dev), torch.cuda.stream(side):
+                    out["arrays"] = (torch.from_numpy(x.indptr.astype(np.int64)).to(dev),
+                                     torch.from_numpy(x.indices).to(dev),
+                                     torch.from_numpy(x.data).to(dev, torch.float64))
+                side.synchronize()
+            except BaseException as e:       # surfaced by take_prefetched
+                out["error"] = e
+
+        th = threading.Thread(target=run, name=f"prefetch-{shard_id}", daemon=True)
+        th.start()
+        pre[shard_id] = (x, th, out, side)
+        return True
+
+    def take_prefetched(self, shard_id: str, x) -> Optional[tuple]:
+        """The device arrays ``(indptr int64, indices, values fp64)`` of a shard started by :meth:`prefetch_shard`,
+        if it was started for this very matrix ``x`` (waits for the copy); None otherwise. Hands them over once."""
+        pre = self.__dict__.get("_prefetch", {}).pop(shard_id, None)
+        if pre is None:
+            return None
+        src, th, out, side = pre
+        th.join()
+        if "error" in out:
+            raise out["error"]
+        if src is not x:
+            return None
+        import torch
+        arrays = out["arrays"]
+        for t in arrays:
+            t.record_stream(torch.cuda.current_stream(t.device))     # allocated on the side stream, used here
+        return arrays
+
     def labeled(self, shard_id: str, offsets: Optional[np.ndarray] = None) -> LabeledData:
         return LabeledData(self.shard(shard_id), self.response, self.offsets if offsets is None else offsets,
                            self.weights, self.uids)

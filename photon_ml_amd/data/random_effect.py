@@ -185,6 +185,9 @@ class RandomEffectDataset:
         self.dtype = dtype
         re_type, shard_id = config.random_effect_type, config.feature_shard_id
         x = data.shard(shard_id)
+        # device copy of the shard started by GameData.prefetch_shard (used by the segmented device build below when
+        # every row is active; taken here in any case so an unused copy is released)
+        prefetched = data.take_prefetched(shard_id, x) if hasattr(data, "take_prefetched") else None
         if isinstance(x, DeviceCSR) and not (
                 self.device.type == "cuda" and layout in ("auto", "segmented")
                 and config.projector_type.kind == ProjectorKind.INDEX_MAP and config.features_to_samples_ratio is None):
@@ -288,7 +291,8 @@ class RandomEffectDataset:
         if layout == "segmented" and self.device.type == "cuda":
             # GPU build: projection + entity-sorted block-diagonal layout computed on the device
             with phase("RE dataset: segmented layout"):
-                self._make_segmented_device(x, xa, ea, ent, active_rows, passive_rows, data.response, wts, n_ent)
+                self._make_segmented_device(x, xa, ea, ent, active_rows, passive_rows, data.response, wts, n_ent,
+                                            prefetched=prefetched if xa is x else None)
             self.d_local = self.projection.local_dims()
             return
         # ---- projection
@@ -465,7 +469,7 @@ class RandomEffectDataset:
                                     torch.zeros(len(rows), dtype=torch.float64, device=dev))
         self.d_total = d_total
 
-    def _make_segmented_device(self, x, xa, ea, ent, active_rows, passive_rows, y, wts, n_ent):
+    def _make_segmented_device(self, x, xa, ea, ent, active_rows, passive_rows, y, wts, n_ent, prefetched=None):
         """Device build of the block-diagonal problem (K14 on the GPU): rows sorted by entity (stable), the
         INDEX_MAP projection = sorted unique ``entity * D + feature`` keys of the active (+ passive) non-zeros,
         each non-zero's block column = its key's rank; then the tiled layout is built from the device CSR."""
@@ -477,6 +481,8 @@ class RandomEffectDataset:
             if isinstance(xa, DeviceCSR):        # routed rows already on the device: no host copy
                 ip = xa.indptr.to(dev)
                 x_ind, x_val = xa.indices.to(dev), xa.data.to(dev)
+            elif prefetched is not None:         # copied by GameData.prefetch_shard while the GPU built other layouts
+                ip, x_ind, x_val = prefetched
             else:
                 ip = torch.from_numpy(xa.indptr.astype(np.int64)).to(dev)
                 x_ind, x_val = torch.from_numpy(xa.indices).to(dev), torch.from_numpy(xa.data).to(dev, torch.float64)

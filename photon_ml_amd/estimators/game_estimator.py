@@ -156,6 +156,18 @@ class GameEstimator:
         with Timed("Device runtime warm-up (first kernel launches of the process)"):
             self.runtime_warmup_s = runtime_warmup(dev)
         coords = OrderedDict()
+        # the first random-effect shard built after a fixed-effect coordinate is copied to the device while the GPU
+        # builds the fixed-effect layout (a host CSR shard no fixed effect reads; GPU only)
+        fe_shards = {dc.feature_shard_id for dc in self.coordinate_data_configurations.values()
+                     if not isinstance(dc, RandomEffectDataConfiguration)}
+        seen_fe = False
+        for cid in seq:
+            dc = self.coordinate_data_configurations[cid]
+            if not isinstance(dc, RandomEffectDataConfiguration):
+                seen_fe = True
+            elif seen_fe and dc.feature_shard_id not in fe_shards:
+                data.prefetch_shard(dc.feature_shard_id, dev)
+                break
         for cid in seq:
             dc = self.coordinate_data_configurations[cid]
             oc = first_cfg[cid]
