@@ -55,8 +55,9 @@ class GameData:
         """Start copying the host CSR shard ``shard_id`` to ``device`` (int64 row pointers, the column indices, fp64
         values) on a side stream from a background thread, so the copy overlaps the GPU work queued before the
         shard's consumer runs (the random-effect build after the fixed-effect layout: the copy is a PCIe transfer,
-        the layout build is device work). :meth:`take_prefetched` hands the arrays over. False when there is
-        nothing to do (no GPU, not a host CSR, already started)."""
+        the layout build is device work). The copy starts once the next tiled build has uploaded its own shard
+        (``ops.device.H2D_GATE``), so the two copies do not share the host link. :meth:`take_prefetched` hands the
+        arrays over. False when there is nothing to do (no GPU, not a host CSR, already started)."""
         import threading
         import torch
         dev = torch.device(device)
@@ -66,8 +67,12 @@ class GameData:
             return False
         side = torch.cuda.Stream(dev)
         out = {}
+        from ..ops.device import H2D_GATE
+        gate = H2D_GATE
+        gate.clear()                 # set by the next tiled build's upload (or by take_prefetched)
 
         def run():
+            gate.wait(timeout=30.0)
             try:
                 with torch.cuda.device(dev), torch.cuda.stream(side):
                     out["arrays"] = (torch.from_numpy(x.indptr.astype(np.int64)).to(dev),
@@ -89,6 +94,8 @@ class GameData:
         if pre is None:
             return None
         src, th, out, side = pre
+        from ..ops.device import H2D_GATE
+        H2D_GATE.set()               # no upload to wait for any more: copy now if not yet started
         th.join()
         if "error" in out:
             raise out["error"]

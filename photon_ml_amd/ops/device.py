@@ -17,6 +17,7 @@ from __future__ import annotations
 
 import ctypes
 import os
+import threading
 from dataclasses import dataclass
 from typing import List, Optional, Sequence
 
@@ -29,6 +30,11 @@ from .native import SegChunkDesc, check, require_glm_lib, stream_handle
 from .reference import GLMComputable
 from .tiled import DEFAULT_ITEM_ENTRIES, TLFwdChunk, TLTChunk, tl_supported
 from ..utils.timing import phase, trace_range
+
+# Set after a tiled build's host -> device upload: GameData.prefetch_shard's copy waits for it, so the two copies do
+# not share the host link (concurrent, the fixed-effect upload took 164 -> 472 ms) and the prefetch overlaps the
+# layout build's device work instead
+H2D_GATE = threading.Event()
 
 LAYOUTS = ("auto", "tiled", "segmented")
 
@@ -397,6 +403,7 @@ class DeviceGLMData(GLMComputable):
                 indptr = torch.from_numpy(np.ascontiguousarray(x.indptr, dtype=np.int64)).to(dev)
                 col = torch.from_numpy(np.ascontiguousarray(x.indices)).to(dev).to(torch.int64)
                 val = torch.from_numpy(np.ascontiguousarray(x.data)).to(dev)
+        H2D_GATE.set()          # the host link is free: a prefetched shard (GameData.prefetch_shard) may copy now
         old_of_new = None
         from ..parallel.dist import is_dist
         shared = relabel and is_dist() and not col_windows
