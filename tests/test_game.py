@@ -350,3 +350,40 @@ def test_batched_trsv_host_path(trans):
     torch.testing.assert_close(torch.bmm(M, y.unsqueeze(-1)).squeeze(-1), x, rtol=1e-10, atol=1e-10)
     torch.testing.assert_close(y, torch.bmm(torch.linalg.inv(M), x.unsqueeze(-1)).squeeze(-1), rtol=1e-9,
                                atol=1e-9)
+    out = torch.full_like(x, float("nan"))
+    assert batched_trsv(L, x, trans, out=out) is out and torch.equal(out, y)
+
+
+def test_lazy_glm_data_builds_once_on_first_use():
+    """LazyGLMData (the random-effect pass layout built on first use): no build until an attribute is read, then
+    exactly one build, every later access delegated to the built object."""
+    from photon_ml_amd.data.random_effect import LazyGLMData
+    calls = []
+
+    class Backend:
+        n_rows = 7
+
+        def matvec(self, w):
+            return w * 2
+
+    def build():
+        calls.append(1)
+        return Backend()
+
+    lazy = LazyGLMData(build)
+    assert not lazy.built and calls == []
+    assert lazy.n_rows == 7 and lazy.built and calls == [1]
+    assert lazy.matvec(3) == 6 and calls == [1]
+    with pytest.raises(AttributeError):
+        lazy.no_such_attribute
+    assert calls == [1]
+
+
+def test_prefetch_shard_is_a_no_op_off_the_gpu():
+    """GameData.prefetch_shard copies a host shard to a GPU in the background; on the CPU (or for an unknown /
+    device-resident shard) it does nothing and take_prefetched hands back nothing."""
+    data = generate_game_data(n_rows=200, seed=5)
+    data = data[0] if isinstance(data, tuple) else data
+    sid = next(iter(data.shards))
+    assert data.prefetch_shard(sid, "cpu") is False
+    assert data.take_prefetched(sid, data.shard(sid)) is None
