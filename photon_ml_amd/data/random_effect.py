@@ -497,8 +497,9 @@ class RandomEffectDataset:
         src = torch.repeat_interleave(ip[:-1][order] - nip[:-1], lens, output_size=nnz)
         src += torch.arange(nnz, device=dev)
         del ip
-        col = x_ind[src].to(torch.int64)
-        val = x_val[src]
+        with phase("RE keys: entity-order gather"):
+            col = x_ind[src].to(torch.int64)
+            val = x_val[src]
         del src, x_ind, x_val
         e_row = ea_t[order]
         key = torch.repeat_interleave(e_row, lens, output_size=nnz) * D + col
@@ -514,7 +515,8 @@ class RandomEffectDataset:
             cp = x[passive_rows].tocoo()
             pk = torch.from_numpy(ent[passive_rows][cp.row].astype(np.int64) * D + cp.col.astype(np.int64))
             allk = torch.cat([key, pk.to(dev)])
-        ukeys = torch.unique(allk, sorted=True)
+        with phase("RE keys: unique"):
+            ukeys = torch.unique(allk, sorted=True)
         n_keys_in = int(allk.numel())
         del allk
         # cheap integrity checks of the device build (first / last key, no more keys than entries): a corrupt
@@ -525,7 +527,8 @@ class RandomEffectDataset:
                 raise RuntimeError(f"random-effect projection keys out of range: [{lo_k}, {hi_k}] for {n_ent} "
                                    f"entities x {D} features, {ukeys.numel()} keys from {n_keys_in} entries")
         self.projection = IndexMapProjection.from_sorted_keys(ukeys, n_ent, D)
-        pos = torch.searchsorted(ukeys, key)
+        with phase("RE keys: entry ranks"):
+            pos = torch.searchsorted(ukeys, key)
         del key
         d_total = int(ukeys.numel())
         rows_t = torch.from_numpy(active_rows.astype(np.int64)).to(dev)[order]
