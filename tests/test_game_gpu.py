@@ -504,3 +504,40 @@ def test_lean_streaming_tron_matches_csr_kernel(task, d_user, monkeypatch):
         # differences, amplified along the TRON path as in test_fused_entity_tron_matches_pass_path
         torch.testing.assert_close(tb, ta, rtol=1e-5, atol=1e-6)
     assert abs(a[4] - b[4]) < 0.05
+
+
+def test_row_space_classes_over_two_streams_match_one_stream(monkeypatch):
+    """The opt-in multi-stream class path of the row-space solve (PML_RS_STREAMS > 1: classes dealt to side streams,
+    warm starts / offsets recorded on them, None inputs skipped) gives bitwise the single-stream models and scores,
+    over two updates (a cold and a warm start)."""
+    import scipy.sparse as sp
+    import photon_ml_amd.optimization.row_space as rsm
+    from photon_ml_amd.data.game_data import GameData
+    rng = np.random.default_rng(43)
+    D, rows, cols, vals, ids = 3000, [], [], [], []
+    r = 0
+    sizes = [3, 7, 12, 16, 24, 30, 45, 60] * 8            # several size classes
+    for e, n in enumerate(sizes):
+        pool = rng.choice(D - 1, size=300, replace=False)
+        for _ in range(n):
+            c = np.sort(rng.choice(pool, size=20, replace=False))
+            rows += [r] * 21
+            cols += c.tolist() + [D - 1]
+            vals += rng.normal(size=20).tolist() + [1.0]
+            ids.append(e)
+            r += 1
+    x = sp.csr_matrix((vals, (rows, cols)), shape=(r, D))
+    z = np.asarray(x.sum(axis=1)).ravel() * 0.05
+    y = (rng.random(r) < 1 / (1 + np.exp(-z))).astype(float)
+    data = GameData(y, {"user": x}, {"userId": np.array(ids)})
+    out = {}
+    for k in (1, 2):
+        monkeypatch.setattr(rsm, "RS_STREAMS", k)
+        c, v1, s1, v2, s2 = _re_two_updates(data, "LOGISTIC_REGRESSION", max_iter=30, tol=1e-10)
+        rsb = c._comps[0]
+        assert rsb is not None and len(rsb.classes) > 1
+        if k == 2:
+            assert getattr(rsb, "_streams", None)        # the side streams were used
+        out[k] = (v1, s1, v2, s2)
+    for a, b in zip(out[1], out[2]):
+        assert torch.equal(torch.as_tensor(a), torch.as_tensor(b))
