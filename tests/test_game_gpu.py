@@ -541,3 +541,37 @@ def test_row_space_classes_over_two_streams_match_one_stream(monkeypatch):
         out[k] = (v1, s1, v2, s2)
     for a, b in zip(out[1], out[2]):
         assert torch.equal(torch.as_tensor(a), torch.as_tensor(b))
+
+
+def test_fused_random_effect_update_never_builds_the_pass_layout():
+    """With the fused solvers (row-space + per-entity primal TRON) an update, its scores and the materialised model
+    need no pass over the whole random-effect coordinate: the block-diagonal pass layout (LazyGLMData) stays unbuilt
+    (it is 0.6 s of game5pl's coordinate build); a pass-path consumer (the Hessian diagonal) then builds it once."""
+    import scipy.sparse as sp
+    from photon_ml_amd.data.game_data import GameData
+    from photon_ml_amd.data.random_effect import LazyGLMData
+    from photon_ml_amd.function.losses import loss_for_task
+    rng = np.random.default_rng(47)
+    D, rows, cols, vals, ids = 3000, [], [], [], []
+    r = 0
+    for e, n in enumerate([5, 12, 30, 90, 200, 260] * 6):   # row-space and fused primal entities
+        pool = rng.choice(D - 1, size=300, replace=False)
+        for _ in range(n):
+            c = np.sort(rng.choice(pool, size=20, replace=False))
+            rows += [r] * 21
+            cols += c.tolist() + [D - 1]
+            vals += rng.normal(size=20).tolist() + [1.0]
+            ids.append(e)
+            r += 1
+    x = sp.csr_matrix((vals, (rows, cols)), shape=(r, D))
+    y = (rng.random(r) < 0.4).astype(float)
+    data = GameData(y, {"user": x}, {"userId": np.array(ids)})
+    c, v1, s1, v2, s2 = _re_two_updates(data, "LOGISTIC_REGRESSION", max_iter=20, tol=1e-8)
+    rs, fused, sub = c._comps
+    assert rs is not None and fused is not None and sub is None
+    glm = c.dataset.seg.glm
+    assert isinstance(glm, LazyGLMData) and not glm.built
+    assert np.isfinite(v2).all() and torch.isfinite(s2).all()
+    W = torch.as_tensor(v2, device="cuda")
+    h = c.dataset.seg.hdiag(loss_for_task("LOGISTIC_REGRESSION"), W, 1.0)
+    assert glm.built and torch.isfinite(h).all() and bool((h >= 1.0 - 1e-12).all())
